@@ -1,0 +1,267 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/*.npz by running the REFERENCE model code (/root/reference) on CPU.
+
+Run only in the build container (the reference does not exist on the GPU box):
+    python tools/gen_golden.py
+The reference source is imported, never copied; third-party packages absent from this image are
+replaced by tools/ref_standins.py (restated MONAI-1.3 / mamba-ssm-1.2.0 behaviour).
+
+Each fixture holds data only: state_dict tensors ("sd/<key>"), inputs ("in/<name>"), outputs
+("out/<name>") and gradients of a fixed random cotangent ("grad/<name>"). Large deterministic
+buffers (the Hyena positional embedding, l_max=66000) are stored as checksums ("chk/<key>").
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+REF = "/root/reference/model/models"
+OUT = os.path.join(REPO, "tests", "golden")
+
+sys.path.insert(0, HERE)
+import ref_standins  # noqa: E402
+
+ref_standins.install()
+sys.path.insert(0, REF)
+import backbone_swin as rswin  # noqa: E402
+import backbone_vit as rvit  # noqa: E402
+import hyena as rhyena  # noqa: E402
+import mamba as rmamba  # noqa: E402
+
+BIG = ("filter_fn.pos_emb.z", "filter_fn.pos_emb.t")
+
+
+def np32(t):
+    t = t.detach()
+    return t.numpy().astype(np.float32) if t.is_floating_point() else t.numpy()
+
+
+def dump(name, module=None, **arrays):
+    d = {}
+    if module is not None:
+        for k, v in module.state_dict().items():
+            if any(k.endswith(b) for b in BIG):
+                d[f"chk/{k}"] = np.array([v.double().sum().item(), v.double().abs().sum().item(),
+                                          float(v.numel())])
+            else:
+                d[f"sd/{k}"] = np32(v)
+    for k, v in arrays.items():
+        d[k] = np32(v) if isinstance(v, torch.Tensor) else np.asarray(v)
+    path = os.path.join(OUT, name + ".npz")
+    np.savez_compressed(path, **d)
+    print(f"{path}: {os.path.getsize(path) / 1024:.0f} KiB, {len(d)} arrays")
+
+
+def fwd_bwd(module, *inputs, grads=(), seed=123, **kw):
+    """Run forward, then backward of sum(out * cot) with a seeded N(0,1) cotangent."""
+    ins = [x.clone().requires_grad_(True) for x in inputs]
+    out = module(*ins, **kw)
+    outs = out if isinstance(out, (list, tuple)) else [out]
+    g = torch.Generator().manual_seed(seed)
+    cots = [torch.randn(o.shape, generator=g) for o in outs]
+    loss = sum((o * c).sum() for o, c in zip(outs, cots))
+    module.zero_grad(set_to_none=True)
+    loss.backward()
+    res = {}
+    for i, o in enumerate(outs):
+        res[f"out/{i}"] = o  # cotangent i = seeded randn (tests/golden_util.py:cotangents)
+    for i, x in enumerate(ins):
+        res[f"grad/in{i}"] = x.grad
+    params = dict(module.named_parameters())
+    for p in grads:
+        res[f"grad/{p}"] = params[p].grad
+    return res
+
+
+# ------------------------------------------------------------------------------------------ fixtures
+def sablock(name, hidden, heads, B, L, seed):
+    torch.manual_seed(seed)
+    m = rvit.SABlock(False, False, hidden, heads).eval()
+    x = torch.randn(B, L, hidden)
+    r = fwd_bwd(m, x, grads=("qkv.weight", "out_proj.weight", "out_proj.bias"))
+    dump(name, m, **{"in/x": x, "cfg/heads": heads}, **r)
+
+
+def vit_encoder(name, hidden, heads, mlp, layers, img, patch, B, seed, classification=False,
+                use_hyena=False, use_mamba=False):
+    torch.manual_seed(seed)
+    m = rvit.ViT_with_alt_ops(use_hyena, use_mamba, in_channels=1, img_size=img, patch_size=patch,
+                              hidden_size=hidden, mlp_dim=mlp, num_layers=layers, num_heads=heads,
+                              dropout_rate=0.0, spatial_dims=2, classification=classification).eval()
+    x = torch.rand(B, 1, 1, *img)
+    gnames = ["patch_embedding.patch_embeddings.weight", "patch_embedding.position_embeddings",
+              "blocks.0.norm1.weight"]
+    if not use_hyena and not use_mamba:
+        gnames.append("blocks.0.attn.qkv.weight")
+    r = fwd_bwd(m, x, grads=tuple(gnames))
+    r = {k: v for k, v in r.items() if not k.startswith("grad/in")}
+    dump(name, m, **{"in/x": x, "cfg/heads": heads, "cfg/layers": layers}, **r)
+
+
+def hyena_op(seed):
+    torch.manual_seed(seed)
+    m = rhyena.HyenaOperator(d_model=128, l_max=66000, filter_order=64, num_heads=2, num_blocks=1,
+                             short_filter_order=5, bidrectional=True, dropout=0.0, filter_dropout=0.0,
+                             activation="id").eval()
+    assert m.bidirectional is False
+    x = torch.randn(1, 512, 128)
+    r = fwd_bwd(m, x, grads=("in_proj.weight", "filter_fn.bias", "short_filter.weight",
+                             "filter_fn.implicit_filter.0.weight"))
+    k = m.filter_fn.filter(512)[0].transpose(0, 1)
+    dump("hyena_op", m, **{"in/x": x, "out/k": k}, **r)
+    # kernel-level long conv pin: the reference fftconv_ref on random u, k, D
+    g = torch.Generator().manual_seed(seed + 1)
+    for L, nb in ((1000, 2), (2048, 1)):
+        u = torch.randn(1, nb, 64, 1, L, generator=g)
+        kk = torch.randn(64, L, generator=g) * torch.exp(-torch.linspace(0, 6, L))[None]
+        D = torch.randn(1, 64, 1, generator=g)
+        y = rhyena.fftconv_ref(u, kk, D, dropout_mask=None, gelu=False)
+        dump(f"fftconv_L{L}", None, **{"in/u": u[:, :, :, 0], "in/k": kk, "in/D": D.reshape(64),
+                                       "out/y": y[:, :, :, 0]})
+    # reference behaviour beyond l_max: assert message references a missing attribute
+    try:
+        m(torch.randn(1, 66001, 128))
+        err = "none"
+    except AttributeError as e:
+        err = "AttributeError:" + str(e)
+    except AssertionError as e:
+        err = "AssertionError:" + str(e)
+    dump("hyena_lmax", None, **{"out/err": np.array(err)})
+
+
+def mamba_mixer(seed):
+    torch.manual_seed(seed)
+    m = rmamba.MambaVisionMixer(d_model=128, d_state=8, d_conv=3, expand=1).eval()
+    x = torch.randn(2, 256, 128)
+    r = fwd_bwd(m, x, grads=("A_log", "D", "dt_proj.bias", "x_proj.weight", "in_proj.weight",
+                             "conv1d_x.weight"))
+    dump("mamba_mixer", m, **{"in/x": x}, **r)
+    # kernel-level scan pin (mamba-ssm selective_scan_ref semantics, as called at mamba.py:125-134)
+    g = torch.Generator().manual_seed(seed + 1)
+    b, d, n, L = 2, 32, 8, 384
+    u = torch.randn(b, d, L, generator=g)
+    delta = torch.randn(b, d, L, generator=g) * 0.5
+    A = -torch.exp(torch.randn(d, n, generator=g) * 0.5)
+    Bm = torch.randn(b, n, L, generator=g)
+    Cm = torch.randn(b, n, L, generator=g)
+    D = torch.randn(d, generator=g)
+    db = torch.randn(d, generator=g) * 0.3
+    ins = [t.clone().requires_grad_(True) for t in (u, delta, A, Bm, Cm, D, db)]
+    y = ref_standins.selective_scan_fn(ins[0], ins[1], ins[2], ins[3], ins[4], ins[5], z=None,
+                                       delta_bias=ins[6], delta_softplus=True)
+    cot = torch.randn(y.shape, generator=g)
+    (y * cot).sum().backward()
+    names = ["u", "delta", "A", "B", "C", "D", "delta_bias"]
+    arr = {f"in/{k}": t for k, t in zip(names, (u, delta, A, Bm, Cm, D, db))}
+    arr.update({f"grad/{k}": t.grad for k, t in zip(names, ins)})
+    dump("selective_scan", None, **arr, **{"out/y": y, "cot/y": cot})  # scan cot kept (own generator)
+
+
+def window_attention(seed):
+    torch.manual_seed(seed)
+    ws = (7, 7, 7)
+    m = rswin.WindowAttention(False, False, 64, 2, ws, qkv_bias=True).eval()
+    mask = rswin.compute_mask([7, 7, 14], ws, (3, 3, 3), "cpu")  # nW = 2
+    x = torch.randn(2, 343, 64)
+    r = fwd_bwd(m, x, grads=("relative_position_bias_table", "qkv.weight", "qkv.bias"), mask=mask)
+    r0 = fwd_bwd(m, x, grads=("relative_position_bias_table",), mask=None)
+    extra = {k.replace("out/", "out_nomask/").replace("grad/", "grad_nomask/"): v for k, v in r0.items()}
+    dump("window_attn_3d", m, **{"in/x": x, "in/mask": mask}, **r, **extra)
+
+    torch.manual_seed(seed + 1)
+    m2 = rswin.WindowAttention(False, False, 64, 2, (7, 7), qkv_bias=True).eval()
+    mask2 = rswin.compute_mask([14, 14], (7, 7), (3, 3), "cpu")  # nW = 4
+    x2 = torch.randn(8, 49, 64)
+    r2 = fwd_bwd(m2, x2, grads=("relative_position_bias_table",), mask=mask2)
+    dump("window_attn_2d", m2, **{"in/x": x2, "in/mask": mask2}, **r2)
+
+
+def swin_layer(seed):
+    torch.manual_seed(seed)
+    layer = rswin.BasicLayer(False, False, dim=64, depth=2, num_heads=2, window_size=(7, 7, 7),
+                             drop_path=[0.0, 0.0], qkv_bias=True,
+                             downsample=rswin.PatchMergingV2).eval()
+    x = torch.randn(1, 64, 10, 10, 10)
+    r = fwd_bwd(layer, x, grads=("blocks.1.attn.relative_position_bias_table",))
+    dump("swin_basic_layer", layer, **{"in/x": x}, **r)
+
+
+def swin_index():
+    arr = {}
+    ws, ss = (7, 7, 7), (3, 3, 3)
+    arr["out/rp_index_3d"] = rswin.WindowAttention(False, False, 96, 3, ws).relative_position_index.numpy()
+    arr["out/rp_index_2d"] = rswin.WindowAttention(False, False, 96, 3, (7, 7)).relative_position_index.numpy()
+    for d in (14, 21, 35, 70):
+        dims = [d, d, d]
+        mask = rswin.compute_mask(dims, ws, ss, "cpu").numpy()
+        nz = (mask != 0)
+        assert set(np.unique(mask).tolist()) <= {0.0, -100.0}
+        arr[f"out/mask_sha256_{d}"] = np.array(hashlib.sha256(np.packbits(nz).tobytes()).hexdigest())
+        arr[f"out/mask_shape_{d}"] = np.array(mask.shape)
+        arr[f"out/mask_nnz_{d}"] = np.array(int(nz.sum()))
+        if d <= 21:
+            arr[f"out/mask_bits_{d}"] = np.packbits(nz)
+        # shifted partition as a permutation of voxel ids
+        idx = torch.arange(d * d * d, dtype=torch.float64).reshape(1, d, d, d, 1)
+        sh = torch.roll(idx, shifts=(-3, -3, -3), dims=(1, 2, 3))
+        perm = rswin.window_partition(sh, ws).reshape(-1).long().numpy().astype(np.int32)
+        if d <= 21:
+            arr[f"out/partition_perm_{d}"] = perm
+        arr[f"out/partition_sha256_{d}"] = np.array(hashlib.sha256(perm.tobytes()).hexdigest())
+    for x_size in ((64, 64, 64), (5, 9, 40), (4, 4, 4)):
+        w, s = rswin.get_window_size(x_size, ws, ss)
+        arr[f"out/gws_{'x'.join(map(str, x_size))}"] = np.array(list(w) + list(s))
+    dump("swin_index", None, **arr)
+
+
+def train_step(seed):
+    """One SGD step of a small ViT encoder + mean-pool linear head, MSE loss (CPU, fp32)."""
+    torch.manual_seed(seed)
+    enc = rvit.ViT_with_alt_ops(False, False, in_channels=1, img_size=(16, 16), patch_size=(2, 2),
+                                hidden_size=128, mlp_dim=256, num_layers=2, num_heads=2, dropout_rate=0.0,
+                                spatial_dims=2).eval()
+    head = torch.nn.Linear(128, 3)
+    x = torch.rand(2, 1, 1, 16, 16)
+    y = torch.randn(2, 3)
+    sd0 = {**{f"enc.{k}": v.clone() for k, v in enc.state_dict().items()},
+           **{f"head.{k}": v.clone() for k, v in head.state_dict().items()}}
+    params = list(enc.parameters()) + list(head.parameters())
+    opt = torch.optim.SGD(params, lr=0.1)
+    loss = torch.nn.functional.mse_loss(head(enc(x)[-1].mean(1)), y)
+    loss.backward()
+    opt.step()
+    arr = {"in/x": x, "in/y": y, "out/loss": loss.detach()}
+    for k, v in sd0.items():
+        arr[f"sd/{k}"] = v
+    post = {**{f"enc.{k}": v for k, v in enc.state_dict().items()},
+            **{f"head.{k}": v for k, v in head.state_dict().items()}}
+    for k, v in post.items():
+        arr[f"post_sum/{k}"] = np.array([v.double().sum().item(), v.double().abs().sum().item()])
+    dump("train_step", None, **arr)
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    sablock("sablock_attn_h128", 128, 2, 2, 256, 0)
+    sablock("sablock_attn_h192_l77", 192, 3, 1, 77, 1)
+    vit_encoder("vit_enc_attn", 128, 2, 256, 2, (16, 16), (2, 2), 2, 2)
+    vit_encoder("vit_enc_cls", 128, 2, 256, 1, (8, 8), (2, 2), 2, 3, classification=True)
+    vit_encoder("vit_enc_hyena", 128, 2, 256, 1, (16, 16), (2, 2), 1, 4, use_hyena=True)
+    vit_encoder("vit_enc_mamba", 128, 2, 256, 1, (16, 16), (2, 2), 1, 5, use_mamba=True)
+    hyena_op(6)
+    mamba_mixer(7)
+    window_attention(8)
+    swin_layer(9)
+    swin_index()
+    train_step(10)
+
+
+if __name__ == "__main__":
+    main()

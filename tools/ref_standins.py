@@ -1,0 +1,232 @@
+"""Stand-ins for the third-party packages the reference imports but this image lacks.
+
+TEST INFRASTRUCTURE ONLY (used by tools/gen_golden.py to import the reference model files from
+/root/reference and emit golden vectors). Nothing under long_context_biomedical_imaging_amd/ imports this.
+
+Each class restates the *published behaviour* of the pinned dependency version:
+  - monai==1.3.0  (requirements.txt:5)   PatchEmbeddingBlock, PatchEmbed, MLPBlock, trunc_normal_,
+                                          ensure_tuple_rep, look_up_option, optional_import
+  - timm==0.9.2   (requirements.txt:13)  only names imported by mamba.py:22-23 (unused in forward)
+  - mamba-ssm==1.2.0.post1 (README.md:15) selective_scan_fn -> selective_scan_ref semantics
+    (mamba_ssm/ops/selective_scan_interface.py: per-step recurrence, fp32 math, output in u.dtype)
+"""
+from __future__ import annotations
+
+import math
+import sys
+import types
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+# ---------------------------------------------------------------- monai.utils
+def ensure_tuple_rep(tup, dim):
+    if isinstance(tup, torch.Tensor):
+        tup = tup.detach().cpu().numpy()
+    if isinstance(tup, np.ndarray):
+        tup = tup.tolist()
+    if not isinstance(tup, (list, tuple)):
+        return (tup,) * dim
+    if len(tup) == dim:
+        return tuple(tup)
+    raise ValueError(f"Sequence must have length {dim}, got {len(tup)}.")
+
+
+def look_up_option(opt, supported, default="no_default"):
+    if isinstance(supported, dict) and opt in supported:
+        return supported[opt]
+    if opt in supported:
+        return opt
+    raise ValueError(f"Unsupported option '{opt}'")
+
+
+def optional_import(module, version="", version_checker=None, name="", descriptor="", version_args=None,
+                    allow_namespace_pkg=False, as_type="default"):
+    import importlib
+    mod = importlib.import_module(module)
+    return (getattr(mod, name) if name else mod), True
+
+
+def deprecated_arg(name, since=None, removed=None, msg_suffix="", version_val="", new_name=None, warning_category=None):
+    def deco(f):
+        return f
+    return deco
+
+
+def trunc_normal_(tensor, mean=0.0, std=1.0, a=-2.0, b=2.0):
+    with torch.no_grad():
+        return nn.init.trunc_normal_(tensor, mean=mean, std=std, a=a, b=b)
+
+
+class DropPath(nn.Module):
+    def __init__(self, drop_prob=0.0, scale_by_keep=True):
+        super().__init__()
+        self.drop_prob = drop_prob
+
+    def forward(self, x):
+        return x
+
+
+# ---------------------------------------------------------------- monai.networks.blocks (1.3 semantics)
+class MLPBlock(nn.Module):
+    """monai 1.3 MLPBlock: linear1 -> act (GELU, erf) -> drop1 -> linear2 -> drop2."""
+
+    def __init__(self, hidden_size, mlp_dim, dropout_rate=0.0, act="GELU", dropout_mode="vit"):
+        super().__init__()
+        mlp_dim = mlp_dim or hidden_size
+        self.linear1 = nn.Linear(hidden_size, mlp_dim)
+        self.linear2 = nn.Linear(mlp_dim, hidden_size)
+        self.fn = nn.GELU()
+        self.drop1 = nn.Dropout(dropout_rate)
+        self.drop2 = nn.Dropout(dropout_rate) if dropout_mode == "vit" else self.drop1
+
+    def forward(self, x):
+        x = self.fn(self.linear1(x))
+        x = self.drop1(x)
+        x = self.linear2(x)
+        return self.drop2(x)
+
+
+class PatchEmbeddingBlock(nn.Module):
+    """monai 1.3 PatchEmbeddingBlock with proj_type='conv'."""
+
+    def __init__(self, in_channels, img_size, patch_size, hidden_size, num_heads, proj_type="conv",
+                 pos_embed_type="learnable", dropout_rate=0.0, spatial_dims=3):
+        super().__init__()
+        img_size = ensure_tuple_rep(img_size, spatial_dims)
+        patch_size = ensure_tuple_rep(patch_size, spatial_dims)
+        self.proj_type = proj_type
+        self.pos_embed_type = pos_embed_type
+        self.n_patches = int(np.prod([i // p for i, p in zip(img_size, patch_size)]))
+        conv = nn.Conv2d if spatial_dims == 2 else nn.Conv3d
+        self.patch_embeddings = conv(in_channels, hidden_size, kernel_size=patch_size, stride=patch_size)
+        self.position_embeddings = nn.Parameter(torch.zeros(1, self.n_patches, hidden_size))
+        self.dropout = nn.Dropout(dropout_rate)
+        if pos_embed_type == "learnable":
+            trunc_normal_(self.position_embeddings, mean=0.0, std=0.02, a=-2.0, b=2.0)
+        self.apply(self._init_weights)
+
+    def _init_weights(self, m):
+        if isinstance(m, nn.Linear):
+            trunc_normal_(m.weight, mean=0.0, std=0.02, a=-2.0, b=2.0)
+            if m.bias is not None:
+                nn.init.constant_(m.bias, 0)
+        elif isinstance(m, nn.LayerNorm):
+            nn.init.constant_(m.bias, 0)
+            nn.init.constant_(m.weight, 1.0)
+
+    def forward(self, x):
+        x = self.patch_embeddings(x)
+        x = x.flatten(2).transpose(-1, -2)
+        return self.dropout(x + self.position_embeddings)
+
+
+class PatchEmbed(nn.Module):
+    """monai 1.3 PatchEmbed (swin): right-pad to a patch multiple, then Conv(k=s=patch)."""
+
+    def __init__(self, patch_size=2, in_chans=1, embed_dim=48, norm_layer=nn.LayerNorm, spatial_dims=3):
+        super().__init__()
+        patch_size = ensure_tuple_rep(patch_size, spatial_dims)
+        self.patch_size = patch_size
+        self.embed_dim = embed_dim
+        conv = nn.Conv2d if spatial_dims == 2 else nn.Conv3d
+        self.proj = conv(in_chans, embed_dim, kernel_size=patch_size, stride=patch_size)
+        self.norm = norm_layer(embed_dim) if norm_layer is not None else None
+
+    def forward(self, x):
+        s = x.size()
+        if len(s) == 5:
+            _, _, d, h, w = s
+            if w % self.patch_size[2] != 0:
+                x = F.pad(x, (0, self.patch_size[2] - w % self.patch_size[2]))
+            if h % self.patch_size[1] != 0:
+                x = F.pad(x, (0, 0, 0, self.patch_size[1] - h % self.patch_size[1]))
+            if d % self.patch_size[0] != 0:
+                x = F.pad(x, (0, 0, 0, 0, 0, self.patch_size[0] - d % self.patch_size[0]))
+        else:
+            _, _, h, w = s
+            if w % self.patch_size[1] != 0:
+                x = F.pad(x, (0, self.patch_size[1] - w % self.patch_size[1]))
+            if h % self.patch_size[0] != 0:
+                x = F.pad(x, (0, 0, 0, self.patch_size[0] - h % self.patch_size[0]))
+        x = self.proj(x)
+        if self.norm is not None:
+            raise NotImplementedError("patch_norm is False in the reference (backbone_swin.py:760)")
+        return x
+
+
+class _Unavailable(nn.Module):
+    def __init__(self, *a, **k):
+        raise RuntimeError("MONAI UNETR blocks are not available in this image")
+
+
+# ---------------------------------------------------------------- mamba_ssm selective_scan_ref
+def selective_scan_ref(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_softplus=False,
+                       return_last_state=False):
+    """mamba-ssm 1.2.0.post1 selective_scan_ref, real A, 3-D (variable) B/C."""
+    dtype_in = u.dtype
+    u = u.float()
+    delta = delta.float()
+    if delta_bias is not None:
+        delta = delta + delta_bias[..., None].float()
+    if delta_softplus:
+        delta = F.softplus(delta)
+    batch, dim, dstate = u.shape[0], A.shape[0], A.shape[1]
+    B = B.float()
+    C = C.float()
+    x = A.new_zeros((batch, dim, dstate))
+    ys = []
+    deltaA = torch.exp(torch.einsum("bdl,dn->bdln", delta, A))
+    deltaB_u = torch.einsum("bdl,bnl,bdl->bdln", delta, B, u)
+    last_state = None
+    for i in range(u.shape[2]):
+        x = deltaA[:, :, i] * x + deltaB_u[:, :, i]
+        y = torch.einsum("bdn,bn->bd", x, C[:, :, i])
+        if i == u.shape[2] - 1:
+            last_state = x
+        ys.append(y)
+    y = torch.stack(ys, dim=2)
+    out = y if D is None else y + u * D[:, None]
+    if z is not None:
+        out = out * F.silu(z)
+    out = out.to(dtype=dtype_in)
+    return out if not return_last_state else (out, last_state)
+
+
+def selective_scan_fn(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_softplus=False,
+                      return_last_state=False):
+    return selective_scan_ref(u, delta, A, B, C, D, z, delta_bias, delta_softplus, bool(return_last_state))
+
+
+# ---------------------------------------------------------------- install into sys.modules
+def install():
+    def mod(name, **attrs):
+        m = types.ModuleType(name)
+        m.__dict__.update(attrs)
+        sys.modules[name] = m
+        return m
+
+    utils = dict(ensure_tuple_rep=ensure_tuple_rep, look_up_option=look_up_option,
+                 optional_import=optional_import, deprecated_arg=deprecated_arg)
+    blocks = dict(PatchEmbed=PatchEmbed, MLPBlock=MLPBlock, UnetOutBlock=_Unavailable,
+                  UnetrBasicBlock=_Unavailable, UnetrUpBlock=_Unavailable, UnetrPrUpBlock=_Unavailable)
+    mod("monai")
+    mod("monai.utils", **utils)
+    mod("monai.utils.deprecate_utils", deprecated_arg=deprecated_arg)
+    mod("monai.networks")
+    mod("monai.networks.blocks", **blocks)
+    mod("monai.networks.blocks.patchembedding", PatchEmbeddingBlock=PatchEmbeddingBlock)
+    mod("monai.networks.blocks.mlp", MLPBlock=MLPBlock)
+    mod("monai.networks.blocks.dynunet_block", UnetOutBlock=_Unavailable)
+    mod("monai.networks.layers", DropPath=DropPath, trunc_normal_=trunc_normal_)
+    mod("timm")
+    mod("timm.models")
+    mod("timm.models.layers", trunc_normal_=trunc_normal_, DropPath=DropPath, LayerNorm2d=nn.LayerNorm)
+    mod("timm.models.vision_transformer", Mlp=MLPBlock)
+    mod("mamba_ssm")
+    mod("mamba_ssm.ops")
+    mod("mamba_ssm.ops.selective_scan_interface", selective_scan_fn=selective_scan_fn,
+        selective_scan_ref=selective_scan_ref)
