@@ -1,0 +1,76 @@
+"""ctypes binding of liblci.so (the C-ABI declared in include/lci.h).
+
+There is no fallback: if the library is missing, or a tensor is not on a ROCm device, the op raises.
+`import torch` happens first so that liblci's libamdhip64.so.7 dependency binds to the HIP runtime torch
+already loaded (one runtime, one set of streams).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liblci.so")
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_F = ctypes.c_float
+_L = ctypes.c_longlong
+
+# name -> argtypes (all return int status)
+SIGNATURES = {
+    "lci_attn_fwd": [_P, _P, _P, _I, _I, _I, _I, _F, _P],
+    "lci_attn_bwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P],
+}
+
+_lib = None
+
+
+class LciError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """Load liblci.so and bind every symbol in SIGNATURES (raises if missing)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise LciError(f"{path} not found: build it with `python -m long_context_biomedical_imaging_amd.build_lib`"
+                       " (the HIP path has no CPU fallback)")
+    lib = ctypes.CDLL(path)
+    lib.lci_last_error.restype = ctypes.c_char_p
+    lib.lci_abi_version.restype = ctypes.c_int
+    for name, argt in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argt
+        fn.restype = ctypes.c_int
+    _lib = lib
+    return lib
+
+
+def call(name: str, *args):
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        raise LciError(f"{name} failed (rc={rc}): {lib.lci_last_error().decode()}")
+
+
+def stream_of(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def require_gpu(*ts: torch.Tensor):
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise LciError("liblci ops run on the GPU only (tensor on %s); there is no CPU path" % t.device)
+        if not t.is_contiguous():
+            raise LciError("liblci ops need contiguous tensors")

@@ -1,0 +1,512 @@
+// ViT full self-attention (SABlock, backbone_vit.py:191-203) as flash attention for gfx950.
+//
+// Replaces:  att = softmax(einsum("blxd,blyd->blxy", q, k) * scale); x = einsum("bhxy,bhyd->bhxd", att, v)
+// Layout:    q/k/v are read in place from the packed qkv Linear output (B, L, 3*H*64) bf16, channel
+//            order (qkv, head, d) (backbone_vit.py:168); O is written as (B, L, H*64) = out_rearrange.
+//            The L x L score matrix is never materialised; the forward keeps lse2 = log2(sum exp) per row.
+//
+// Forward:   one workgroup = NW waves x 32 query rows; K/V tiles of 64 keys double-buffered in LDS
+//            (register-staged, issue-early / write-late). Per wave and tile: S^T = K.Q^T with the
+//            query on the MFMA lane (v_mfma_f32_32x32x16_bf16, 8 MFMAs), lane-local online softmax,
+//            O^T += V^T.P^T with P taken straight from the S accumulators (8 MFMAs, V^T via
+//            ds_read_b64_tr_b16).
+// Backward:  (1) delta = rowsum(dO*O); (2) dK/dV kernel: a workgroup owns NW*32 keys (key on the lane),
+//            sweeps query tiles: S, dP recomputed, dV^T += dO^T.P, dK^T += Q^T.dS (32 MFMAs / tile);
+//            (3) dQ kernel: a workgroup owns NW*32 queries, sweeps key tiles: S^T, dP^T, dQ^T += K^T.dS^T.
+//            No atomics: results are bitwise reproducible.
+#include "common.hpp"
+
+namespace lci {
+
+constexpr int DH = 64;        // head dim (ViT-small/base: 384/6, 768/12)
+constexpr int KT = 64;        // keys (or queries) per LDS tile
+constexpr int LD_ROW = 72;    // LDS row stride (elements) for tiles read by rows: 144 B, b128 conflict-free
+constexpr int LD_TR = 96;     // LDS row stride for tiles read only transposed: 192 B, tr_b16 conflict-free
+constexpr float NEG_BIG = -1.0e30f;
+
+struct AttnArgs {
+  const bf16* q; const bf16* k; const bf16* v;    // base pointers of head 0, batch 0
+  const bf16* o; const bf16* dout;                 // bwd only
+  bf16* out;                                       // fwd: O ; bwd dq kernel: dQ
+  bf16* dk; bf16* dv;                              // bwd dkdv kernel
+  float* lse2;                                     // (B, H, L)
+  float* delta;                                    // (B, H, L)
+  long long bs_q, bs_k, bs_v, bs_o, bs_do, bs_out, bs_dk, bs_dv;   // batch strides (elements)
+  int rs_q, rs_k, rs_v, rs_o, rs_do, rs_out, rs_dk, rs_dv;         // token (row) strides (elements)
+  int hs;                                          // head stride (elements) in every tensor (= 64)
+  int H, L;
+  float c;                                         // scale * log2(e)
+  float scale;
+};
+
+// Stage a 64 x 64 bf16 tile (rows row0.., 128 B per row) into registers: NT threads, 16 B per thread-pass.
+template <int NT>
+struct TileRegs {
+  static constexpr int PASSES = (KT * DH * 2) / (NT * 16);
+  u32x4 r[PASSES];
+  __device__ __forceinline__ void load(const bf16* base, int rs, int row0, int L, int tid) {
+#pragma unroll
+    for (int p = 0; p < PASSES; ++p) {
+      const int idx = p * NT + tid;
+      const int row = idx >> 3, ch = idx & 7;
+      const int g = row0 + row;
+      if (g < L) r[p] = *(const u32x4*)(base + (long long)g * rs + ch * 8);
+      else r[p] = u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+  __device__ __forceinline__ void store(bf16* lds, int ld, int tid) const {
+#pragma unroll
+    for (int p = 0; p < PASSES; ++p) {
+      const int idx = p * NT + tid;
+      const int row = idx >> 3, ch = idx & 7;
+      *(u32x4*)(lds + row * ld + ch * 8) = r[p];
+    }
+  }
+};
+
+// ------------------------------------------------------------------------------------------ forward
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
+  constexpr int NT = NW * 64;
+  constexpr int STAGE = KT * LD_ROW + KT * LD_TR;   // K tile (rows) + V tile (transposed reads)
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hh = blockIdx.y, b = blockIdx.z;
+  const int L = a.L;
+  const int q0 = blockIdx.x * (NW * 32) + wave * 32;
+  const int qrow = q0 + (lane & 31);
+  const int half = lane >> 5;
+
+  const bf16* qp = a.q + b * a.bs_q + hh * a.hs;
+  const bf16* kp = a.k + b * a.bs_k + hh * a.hs;
+  const bf16* vp = a.v + b * a.bs_v + hh * a.hs;
+
+  // Q^T as the B operand: lane (query r, half h) holds Q[q][16ks + 8h .. +7]
+  bf16x8 qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    if (qrow < L) qf[ks] = *(const bf16x8*)(qp + (long long)qrow * a.rs_q + ks * 16 + 8 * half);
+    else qf[ks] = bf16x8{};
+  }
+
+  TileRegs<NT> kr, vr;
+  const int nkt = (L + KT - 1) / KT;
+  kr.load(kp, a.rs_k, 0, L, tid);
+  vr.load(vp, a.rs_v, 0, L, tid);
+  kr.store(smem, LD_ROW, tid);
+  vr.store(smem + KT * LD_ROW, LD_TR, tid);
+  __syncthreads();
+
+  f32x16 o0 = {}, o1 = {};
+  float m_run = NEG_BIG, l_run = 0.f;
+  const float c = a.c;
+
+  for (int kt = 0; kt < nkt; ++kt) {
+    const bf16* kl = smem + (kt & 1) * STAGE;
+    const bf16* vl = kl + KT * LD_ROW;
+    if (kt + 1 < nkt) {
+      kr.load(kp, a.rs_k, (kt + 1) * KT, L, tid);
+      vr.load(vp, a.rs_v, (kt + 1) * KT, L, tid);
+    }
+    // S^T tiles: keys 0..31 and 32..63 of this tile (rows), queries on lanes
+    f32x16 s0 = {}, s1 = {};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      s0 = mfma32(frag_row(kl, LD_ROW, 0, ks * 16, lane), qf[ks], s0);
+      s1 = mfma32(frag_row(kl, LD_ROW, 32, ks * 16, lane), qf[ks], s1);
+    }
+    if ((kt + 1) * KT > L) {  // ragged last tile: mask keys >= L
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int key = kt * KT + (i & 3) + 8 * (i >> 2) + 4 * half;
+        if (key >= L) s0[i] = NEG_BIG;
+        if (key + 32 >= L) s1[i] = NEG_BIG;
+      }
+    }
+    float mx = s0[0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) mx = fmaxf(mx, s0[i]);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s1[i]);
+    mx = wave_max_xor32(mx);
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = exp2_fast((m_run - m_new) * c);
+    m_run = m_new;
+    const float mc = m_new * c;
+    float ls = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      s0[i] = exp2_fast(fmaf(s0[i], c, -mc));
+      s1[i] = exp2_fast(fmaf(s1[i], c, -mc));
+      ls += s0[i] + s1[i];
+    }
+    l_run = l_run * alpha + ls;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { o0[i] *= alpha; o1[i] *= alpha; }
+    const bf16x8 p00 = pack8<0>(s0), p01 = pack8<1>(s0), p10 = pack8<0>(s1), p11 = pack8<1>(s1);
+    // O^T[d][q] += V^T[d][key] P^T[key][q]
+    o0 = mfma32(frag_tr<0>(vl, LD_TR, 0, 0, lane), p00, o0);
+    o0 = mfma32(frag_tr<1>(vl, LD_TR, 0, 0, lane), p01, o0);
+    o0 = mfma32(frag_tr<0>(vl, LD_TR, 32, 0, lane), p10, o0);
+    o0 = mfma32(frag_tr<1>(vl, LD_TR, 32, 0, lane), p11, o0);
+    o1 = mfma32(frag_tr<0>(vl, LD_TR, 0, 32, lane), p00, o1);
+    o1 = mfma32(frag_tr<1>(vl, LD_TR, 0, 32, lane), p01, o1);
+    o1 = mfma32(frag_tr<0>(vl, LD_TR, 32, 32, lane), p10, o1);
+    o1 = mfma32(frag_tr<1>(vl, LD_TR, 32, 32, lane), p11, o1);
+    if (kt + 1 < nkt) {
+      bf16* nb = smem + ((kt + 1) & 1) * STAGE;
+      kr.store(nb, LD_ROW, tid);
+      vr.store(nb + KT * LD_ROW, LD_TR, tid);
+    }
+    __syncthreads();
+  }
+
+  const float l_tot = wave_sum_xor32(l_run);
+  const float inv = 1.f / l_tot;
+  if (qrow < L) {
+    bf16* op = a.out + b * a.bs_out + (long long)qrow * a.rs_out + hh * a.hs;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf16x4 w0, w1;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        w0[j] = to_bf16(o0[4 * g + j] * inv);
+        w1[j] = to_bf16(o1[4 * g + j] * inv);
+      }
+      *(bf16x4*)(op + 8 * g + 4 * half) = w0;
+      *(bf16x4*)(op + 32 + 8 * g + 4 * half) = w1;
+    }
+    if (half == 0) a.lse2[((long long)b * a.H + hh) * L + qrow] = m_run * c + __log2f(l_tot);
+  }
+}
+
+// --------------------------------------------------------------------------- backward: delta
+// delta[b,h,q] = sum_d dO[b,q,h,d] * O[b,q,h,d]; 8 threads per (q, h) row, 16 B each.
+__global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnArgs a) {
+  const int tid = threadIdx.x;
+  const int row = blockIdx.x * 32 + (tid >> 3), ch = tid & 7;
+  const int hh = blockIdx.y, b = blockIdx.z;
+  float acc = 0.f;
+  if (row < a.L) {
+    const bf16x8 o = *(const bf16x8*)(a.o + b * a.bs_o + (long long)row * a.rs_o + hh * a.hs + ch * 8);
+    const bf16x8 d = *(const bf16x8*)(a.dout + b * a.bs_do + (long long)row * a.rs_do + hh * a.hs + ch * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += to_f32(o[j]) * to_f32(d[j]);
+  }
+  acc += __shfl_xor(acc, 1);
+  acc += __shfl_xor(acc, 2);
+  acc += __shfl_xor(acc, 4);
+  if (ch == 0 && row < a.L) a.delta[((long long)b * a.H + hh) * a.L + row] = acc;
+}
+
+// ---------------------------------------------------------------------- backward: dK, dV kernel
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv_kernel(AttnArgs a) {
+  constexpr int NT = NW * 64;
+  constexpr int TILE = 2 * KT * LD_ROW;                 // Q tile + dO tile (both read by rows and transposed)
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * TILE];
+  __shared__ __attribute__((aligned(16))) float rowc[2][2][KT];  // [buf][lse2 | delta][query]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hh = blockIdx.y, b = blockIdx.z;
+  const int L = a.L;
+  const int half = lane >> 5;
+  const int key = blockIdx.x * (NW * 32) + wave * 32 + (lane & 31);
+
+  const bf16* qp = a.q + b * a.bs_q + hh * a.hs;
+  const bf16* dop = a.dout + b * a.bs_do + hh * a.hs;
+  const float* lsep = a.lse2 + ((long long)b * a.H + hh) * L;
+  const float* dlp = a.delta + ((long long)b * a.H + hh) * L;
+
+  // K^T and V^T as B operands: lane (key r, half h) holds K[key][16ks+8h..], V[key][16ks+8h..]
+  bf16x8 kf[4], vf[4];
+  {
+    const bf16* kp = a.k + b * a.bs_k + hh * a.hs;
+    const bf16* vp = a.v + b * a.bs_v + hh * a.hs;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      if (key < L) {
+        kf[ks] = *(const bf16x8*)(kp + (long long)key * a.rs_k + ks * 16 + 8 * half);
+        vf[ks] = *(const bf16x8*)(vp + (long long)key * a.rs_v + ks * 16 + 8 * half);
+      } else {
+        kf[ks] = bf16x8{};
+        vf[ks] = bf16x8{};
+      }
+    }
+  }
+
+  TileRegs<NT> qr, dr;
+  const int nqt = (L + KT - 1) / KT;
+  auto stage_rowc = [&](int buf, int qt) {
+    if (tid < 2 * KT) {
+      const int which = tid / KT, qi = tid % KT, q = qt * KT + qi;
+      float v;
+      if (which == 0) v = (q < L) ? lsep[q] : 1.0e30f;  // invalid rows: P = exp2(-huge) = 0
+      else v = (q < L) ? dlp[q] : 0.f;
+      rowc[buf][which][qi] = v;
+    }
+  };
+  qr.load(qp, a.rs_q, 0, L, tid);
+  dr.load(dop, a.rs_do, 0, L, tid);
+  qr.store(smem, LD_ROW, tid);
+  dr.store(smem + KT * LD_ROW, LD_ROW, tid);
+  stage_rowc(0, 0);
+  __syncthreads();
+
+  f32x16 dv0 = {}, dv1 = {}, dk0 = {}, dk1 = {};
+  const float c = a.c;
+  for (int qt = 0; qt < nqt; ++qt) {
+    const int buf = qt & 1;
+    const bf16* ql = smem + buf * TILE;
+    const bf16* dl = ql + KT * LD_ROW;
+    if (qt + 1 < nqt) {
+      qr.load(qp, a.rs_q, (qt + 1) * KT, L, tid);
+      dr.load(dop, a.rs_do, (qt + 1) * KT, L, tid);
+    }
+    // S[q][key] and dP[q][key] for query sub-tiles 0..31 / 32..63; key on the lane
+    f32x16 s0 = {}, s1 = {}, p0 = {}, p1 = {};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      s0 = mfma32(frag_row(ql, LD_ROW, 0, ks * 16, lane), kf[ks], s0);
+      s1 = mfma32(frag_row(ql, LD_ROW, 32, ks * 16, lane), kf[ks], s1);
+      p0 = mfma32(frag_row(dl, LD_ROW, 0, ks * 16, lane), vf[ks], p0);
+      p1 = mfma32(frag_row(dl, LD_ROW, 32, ks * 16, lane), vf[ks], p1);
+    }
+    // P = exp2(S c - lse2[q]); dS = P (dP - delta[q]); q index = (i&3) + 8(i>>2) + 4h (+32)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 la = *(const f32x4*)&rowc[buf][0][8 * g + 4 * half];
+      const f32x4 lb = *(const f32x4*)&rowc[buf][0][32 + 8 * g + 4 * half];
+      const f32x4 da = *(const f32x4*)&rowc[buf][1][8 * g + 4 * half];
+      const f32x4 db = *(const f32x4*)&rowc[buf][1][32 + 8 * g + 4 * half];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i = 4 * g + j;
+        s0[i] = exp2_fast(fmaf(s0[i], c, -la[j]));
+        s1[i] = exp2_fast(fmaf(s1[i], c, -lb[j]));
+        p0[i] = s0[i] * (p0[i] - da[j]);
+        p1[i] = s1[i] * (p1[i] - db[j]);
+      }
+    }
+    const bf16x8 P00 = pack8<0>(s0), P01 = pack8<1>(s0), P10 = pack8<0>(s1), P11 = pack8<1>(s1);
+    const bf16x8 D00 = pack8<0>(p0), D01 = pack8<1>(p0), D10 = pack8<0>(p1), D11 = pack8<1>(p1);
+    // dV^T[d][key] += dO^T[d][q] P[q][key] ; dK^T[d][key] += Q^T[d][q] dS[q][key]
+    dv0 = mfma32(frag_tr<0>(dl, LD_ROW, 0, 0, lane), P00, dv0);
+    dv0 = mfma32(frag_tr<1>(dl, LD_ROW, 0, 0, lane), P01, dv0);
+    dv0 = mfma32(frag_tr<0>(dl, LD_ROW, 32, 0, lane), P10, dv0);
+    dv0 = mfma32(frag_tr<1>(dl, LD_ROW, 32, 0, lane), P11, dv0);
+    dv1 = mfma32(frag_tr<0>(dl, LD_ROW, 0, 32, lane), P00, dv1);
+    dv1 = mfma32(frag_tr<1>(dl, LD_ROW, 0, 32, lane), P01, dv1);
+    dv1 = mfma32(frag_tr<0>(dl, LD_ROW, 32, 32, lane), P10, dv1);
+    dv1 = mfma32(frag_tr<1>(dl, LD_ROW, 32, 32, lane), P11, dv1);
+    dk0 = mfma32(frag_tr<0>(ql, LD_ROW, 0, 0, lane), D00, dk0);
+    dk0 = mfma32(frag_tr<1>(ql, LD_ROW, 0, 0, lane), D01, dk0);
+    dk0 = mfma32(frag_tr<0>(ql, LD_ROW, 32, 0, lane), D10, dk0);
+    dk0 = mfma32(frag_tr<1>(ql, LD_ROW, 32, 0, lane), D11, dk0);
+    dk1 = mfma32(frag_tr<0>(ql, LD_ROW, 0, 32, lane), D00, dk1);
+    dk1 = mfma32(frag_tr<1>(ql, LD_ROW, 0, 32, lane), D01, dk1);
+    dk1 = mfma32(frag_tr<0>(ql, LD_ROW, 32, 32, lane), D10, dk1);
+    dk1 = mfma32(frag_tr<1>(ql, LD_ROW, 32, 32, lane), D11, dk1);
+    if (qt + 1 < nqt) {
+      bf16* nb = smem + (buf ^ 1) * TILE;
+      qr.store(nb, LD_ROW, tid);
+      dr.store(nb + KT * LD_ROW, LD_ROW, tid);
+      stage_rowc(buf ^ 1, qt + 1);
+    }
+    __syncthreads();
+  }
+
+  if (key < L) {
+    bf16* dkp = a.dk + b * a.bs_dk + (long long)key * a.rs_dk + hh * a.hs;
+    bf16* dvp = a.dv + b * a.bs_dv + (long long)key * a.rs_dv + hh * a.hs;
+    const float sc = a.scale;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf16x4 k0, k1, v0, v1;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        k0[j] = to_bf16(dk0[4 * g + j] * sc);
+        k1[j] = to_bf16(dk1[4 * g + j] * sc);
+        v0[j] = to_bf16(dv0[4 * g + j]);
+        v1[j] = to_bf16(dv1[4 * g + j]);
+      }
+      *(bf16x4*)(dkp + 8 * g + 4 * half) = k0;
+      *(bf16x4*)(dkp + 32 + 8 * g + 4 * half) = k1;
+      *(bf16x4*)(dvp + 8 * g + 4 * half) = v0;
+      *(bf16x4*)(dvp + 32 + 8 * g + 4 * half) = v1;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------- backward: dQ kernel
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnArgs a) {
+  constexpr int NT = NW * 64;
+  constexpr int TILE = 2 * KT * LD_ROW;   // K tile (rows + transposed) + V tile (rows)
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * TILE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hh = blockIdx.y, b = blockIdx.z;
+  const int L = a.L;
+  const int half = lane >> 5;
+  const int qrow = blockIdx.x * (NW * 32) + wave * 32 + (lane & 31);
+
+  const bf16* kp = a.k + b * a.bs_k + hh * a.hs;
+  const bf16* vp = a.v + b * a.bs_v + hh * a.hs;
+  bf16x8 qf[4], df[4];
+  float lse2 = 1.0e30f, dlt = 0.f;
+  {
+    const bf16* qp = a.q + b * a.bs_q + hh * a.hs;
+    const bf16* dop = a.dout + b * a.bs_do + hh * a.hs;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      if (qrow < L) {
+        qf[ks] = *(const bf16x8*)(qp + (long long)qrow * a.rs_q + ks * 16 + 8 * half);
+        df[ks] = *(const bf16x8*)(dop + (long long)qrow * a.rs_do + ks * 16 + 8 * half);
+      } else {
+        qf[ks] = bf16x8{};
+        df[ks] = bf16x8{};
+      }
+    }
+    if (qrow < L) {
+      lse2 = a.lse2[((long long)b * a.H + hh) * L + qrow];
+      dlt = a.delta[((long long)b * a.H + hh) * L + qrow];
+    }
+  }
+
+  TileRegs<NT> kr, vr;
+  const int nkt = (L + KT - 1) / KT;
+  kr.load(kp, a.rs_k, 0, L, tid);
+  vr.load(vp, a.rs_v, 0, L, tid);
+  kr.store(smem, LD_ROW, tid);
+  vr.store(smem + KT * LD_ROW, LD_ROW, tid);
+  __syncthreads();
+
+  f32x16 dq0 = {}, dq1 = {};
+  const float c = a.c;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int buf = kt & 1;
+    const bf16* kl = smem + buf * TILE;
+    const bf16* vl = kl + KT * LD_ROW;
+    if (kt + 1 < nkt) {
+      kr.load(kp, a.rs_k, (kt + 1) * KT, L, tid);
+      vr.load(vp, a.rs_v, (kt + 1) * KT, L, tid);
+    }
+    f32x16 s0 = {}, s1 = {}, p0 = {}, p1 = {};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      s0 = mfma32(frag_row(kl, LD_ROW, 0, ks * 16, lane), qf[ks], s0);
+      s1 = mfma32(frag_row(kl, LD_ROW, 32, ks * 16, lane), qf[ks], s1);
+      p0 = mfma32(frag_row(vl, LD_ROW, 0, ks * 16, lane), df[ks], p0);
+      p1 = mfma32(frag_row(vl, LD_ROW, 32, ks * 16, lane), df[ks], p1);
+    }
+    const bool ragged = (kt + 1) * KT > L;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float e0 = exp2_fast(fmaf(s0[i], c, -lse2));
+      float e1 = exp2_fast(fmaf(s1[i], c, -lse2));
+      if (ragged) {
+        const int key = kt * KT + (i & 3) + 8 * (i >> 2) + 4 * half;
+        if (key >= L) e0 = 0.f;
+        if (key + 32 >= L) e1 = 0.f;
+      }
+      s0[i] = e0 * (p0[i] - dlt);
+      s1[i] = e1 * (p1[i] - dlt);
+    }
+    const bf16x8 D00 = pack8<0>(s0), D01 = pack8<1>(s0), D10 = pack8<0>(s1), D11 = pack8<1>(s1);
+    // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
+    dq0 = mfma32(frag_tr<0>(kl, LD_ROW, 0, 0, lane), D00, dq0);
+    dq0 = mfma32(frag_tr<1>(kl, LD_ROW, 0, 0, lane), D01, dq0);
+    dq0 = mfma32(frag_tr<0>(kl, LD_ROW, 32, 0, lane), D10, dq0);
+    dq0 = mfma32(frag_tr<1>(kl, LD_ROW, 32, 0, lane), D11, dq0);
+    dq1 = mfma32(frag_tr<0>(kl, LD_ROW, 0, 32, lane), D00, dq1);
+    dq1 = mfma32(frag_tr<1>(kl, LD_ROW, 0, 32, lane), D01, dq1);
+    dq1 = mfma32(frag_tr<0>(kl, LD_ROW, 32, 32, lane), D10, dq1);
+    dq1 = mfma32(frag_tr<1>(kl, LD_ROW, 32, 32, lane), D11, dq1);
+    if (kt + 1 < nkt) {
+      bf16* nb = smem + (buf ^ 1) * TILE;
+      kr.store(nb, LD_ROW, tid);
+      vr.store(nb + KT * LD_ROW, LD_ROW, tid);
+    }
+    __syncthreads();
+  }
+  if (qrow < L) {
+    bf16* dqp = a.out + b * a.bs_out + (long long)qrow * a.rs_out + hh * a.hs;
+    const float sc = a.scale;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf16x4 w0, w1;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        w0[j] = to_bf16(dq0[4 * g + j] * sc);
+        w1[j] = to_bf16(dq1[4 * g + j] * sc);
+      }
+      *(bf16x4*)(dqp + 8 * g + 4 * half) = w0;
+      *(bf16x4*)(dqp + 32 + 8 * g + 4 * half) = w1;
+    }
+  }
+}
+
+}  // namespace lci
+
+// =============================================================================== C-ABI entry points
+using namespace lci;
+
+static int check_packed(const void* p, int rs) {
+  return ((uintptr_t)p % 16 == 0) && (rs % 8 == 0);
+}
+
+extern "C" int lci_attn_fwd(const void* qkv, void* out, float* lse2, int B, int L, int H, int head_dim,
+                            float scale, void* stream) {
+  LCI_CHECK(head_dim == DH, "lci_attn_fwd: head_dim %d unsupported (only 64)", head_dim);
+  LCI_CHECK(B > 0 && L > 0 && H > 0, "lci_attn_fwd: bad shape B=%d L=%d H=%d", B, L, H);
+  const int rs = 3 * H * DH;
+  LCI_CHECK(check_packed(qkv, rs) && check_packed(out, H * DH), "lci_attn_fwd: misaligned pointers");
+  AttnArgs a{};
+  const bf16* base = (const bf16*)qkv;
+  a.q = base; a.k = base + H * DH; a.v = base + 2 * H * DH;
+  a.out = (bf16*)out; a.lse2 = lse2;
+  a.bs_q = a.bs_k = a.bs_v = (long long)L * rs;
+  a.rs_q = a.rs_k = a.rs_v = rs;
+  a.bs_out = (long long)L * H * DH; a.rs_out = H * DH;
+  a.hs = DH; a.H = H; a.L = L;
+  a.scale = scale; a.c = scale * 1.4426950408889634f;
+  constexpr int NW = 4;
+  dim3 grid((L + NW * 32 - 1) / (NW * 32), H, B);
+  hipLaunchKernelGGL(attn_fwd_kernel<NW>, grid, dim3(NW * 64), 0, (hipStream_t)stream, a);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int lci_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse2,
+                            void* dqkv, float* delta_ws, int B, int L, int H, int head_dim, float scale,
+                            void* stream) {
+  LCI_CHECK(head_dim == DH, "lci_attn_bwd: head_dim %d unsupported (only 64)", head_dim);
+  LCI_CHECK(B > 0 && L > 0 && H > 0, "lci_attn_bwd: bad shape B=%d L=%d H=%d", B, L, H);
+  const int rs = 3 * H * DH;
+  LCI_CHECK(check_packed(qkv, rs) && check_packed(dqkv, rs) && check_packed(out, H * DH) &&
+                check_packed(dout, H * DH), "lci_attn_bwd: misaligned pointers");
+  AttnArgs a{};
+  const bf16* base = (const bf16*)qkv;
+  bf16* dbase = (bf16*)dqkv;
+  a.q = base; a.k = base + H * DH; a.v = base + 2 * H * DH;
+  a.o = (const bf16*)out; a.dout = (const bf16*)dout;
+  a.lse2 = (float*)lse2; a.delta = delta_ws;
+  a.bs_q = a.bs_k = a.bs_v = (long long)L * rs;
+  a.rs_q = a.rs_k = a.rs_v = rs;
+  a.bs_o = a.bs_do = (long long)L * H * DH;
+  a.rs_o = a.rs_do = H * DH;
+  a.out = dbase; a.dk = dbase + H * DH; a.dv = dbase + 2 * H * DH;
+  a.bs_out = a.bs_dk = a.bs_dv = (long long)L * rs;
+  a.rs_out = a.rs_dk = a.rs_dv = rs;
+  a.hs = DH; a.H = H; a.L = L;
+  a.scale = scale; a.c = scale * 1.4426950408889634f;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((L + 31) / 32, H, B), dim3(256), 0, s, a);
+  LCI_LAUNCH_CHECK();
+  constexpr int NW = 4;
+  dim3 grid((L + NW * 32 - 1) / (NW * 32), H, B);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel<NW>, grid, dim3(NW * 64), 0, s, a);
+  LCI_LAUNCH_CHECK();
+  hipLaunchKernelGGL(attn_bwd_dq_kernel<NW>, grid, dim3(NW * 64), 0, s, a);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
