@@ -23,6 +23,9 @@ _L = ctypes.c_longlong
 SIGNATURES = {
     "lci_attn_fwd": [_P, _P, _P, _I, _I, _I, _I, _F, _P],
     "lci_attn_bwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P],
+    "lci_attn_bwd_stage": [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P],
+    "lci_patch_embed_fwd": [_P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P],
+    "lci_patch_embed_bwd": [_P, _I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P, _P, _I, _P],
 }
 
 _lib = None

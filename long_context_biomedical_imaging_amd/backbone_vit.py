@@ -1,0 +1,166 @@
+"""ViT backbone with attention / Hyena / Mamba token mixers — drop-in for
+/root/reference/model/models/backbone_vit.py.
+
+Same public names, constructor signatures, forward shapes, parameter-creation order and state_dict
+keys as the reference (custom_ViT :45-116, SABlock :120-211, TransformerBlock :213-263,
+ViT_with_alt_ops :265-397). The attention core runs the liblci flash-attention HIP kernels
+(kernels.flash_attention); the L x L matrix is never formed, so `save_attn=True` recomputes the
+attention matrix on demand instead of storing it every forward (see SABlock.attention_matrix).
+"""
+from __future__ import annotations
+
+from collections.abc import Sequence
+
+import torch
+import torch.nn as nn
+
+from . import kernels
+from .blocks import MLPBlock, PatchEmbeddingBlock
+from .hyena import HyenaOperator
+from .mamba import MambaVisionMixer
+
+
+def custom_ViT(config, input_feature_channels):
+    """Returns (ViT_with_alt_ops, [hidden_size]*13), sizes as backbone_vit.py:56-89."""
+    v = config.ViT
+    if v.size == "small":
+        hidden_size, mlp_dim, num_layers, num_heads = 384, 1536, 12, 6
+    elif v.size == "base":
+        hidden_size, mlp_dim, num_layers, num_heads = 768, 3072, 12, 12
+    elif v.size == "custom":
+        hidden_size, mlp_dim, num_layers, num_heads = v.hidden_size, v.mlp_dim, v.num_layers, v.num_heads
+    else:
+        raise ValueError(f"Unknown model size {v.size} specified in config.")
+    v.hidden_size, v.mlp_dim, v.num_layers, v.num_heads = hidden_size, mlp_dim, num_layers, num_heads
+
+    if config.time == 1:
+        spatial_dims = 2
+        input_size = [config.height, config.width]
+        mod_patch_size = v.patch_size[1:] if len(v.patch_size) == 3 else v.patch_size
+    else:
+        spatial_dims = 3
+        input_size = [config.time, config.height, config.width]
+        mod_patch_size = v.patch_size
+
+    model = ViT_with_alt_ops(use_hyena=v.use_hyena, use_mamba=v.use_mamba, in_channels=input_feature_channels,
+                             img_size=input_size, patch_size=mod_patch_size, hidden_size=hidden_size,
+                             mlp_dim=mlp_dim, num_layers=num_layers, num_heads=num_heads, dropout_rate=0.0,
+                             spatial_dims=spatial_dims, classification=config.task_type == "class")
+    return model, [hidden_size] * 13
+
+
+class SABlock(nn.Module):
+    """Token mixer: full self-attention (flash, HIP), or HyenaOperator, or MambaVisionMixer."""
+
+    def __init__(self, use_hyena: bool, use_mamba: bool, hidden_size: int, num_heads: int,
+                 dropout_rate: float = 0.0, qkv_bias: bool = False, save_attn: bool = False) -> None:
+        super().__init__()
+        if not (0 <= dropout_rate <= 1):
+            raise ValueError("dropout_rate should be between 0 and 1.")
+        if hidden_size % num_heads != 0:
+            raise ValueError("hidden size should be divisible by num_heads.")
+        self.num_heads = num_heads
+        self.use_hyena = use_hyena
+        self.use_mamba = use_mamba
+        if not use_hyena and not use_mamba:
+            self.drop_output = nn.Dropout(dropout_rate)
+            self.drop_weights = nn.Dropout(dropout_rate)
+            self.head_dim = hidden_size // num_heads
+            self.scale = self.head_dim ** -0.5
+            self.save_attn = save_attn
+            self.att_mat = torch.Tensor()
+            self.qkv = nn.Linear(hidden_size, hidden_size * 3, bias=qkv_bias)
+            self.out_proj = nn.Linear(hidden_size, hidden_size)
+        elif use_hyena and not use_mamba:
+            self.hyena = HyenaOperator(d_model=hidden_size, l_max=66000, filter_order=64, num_heads=num_heads,
+                                       num_blocks=1, short_filter_order=5, bidrectional=True,
+                                       dropout=dropout_rate, filter_dropout=dropout_rate, activation="id")
+        elif not use_hyena and use_mamba:
+            self.mamba = MambaVisionMixer(d_model=hidden_size, d_state=8, d_conv=3, expand=1)
+
+    def forward(self, x):
+        if not self.use_hyena and not self.use_mamba:
+            if self.training and self.drop_weights.p > 0:
+                raise NotImplementedError("attention-weight dropout > 0 is not fused into the flash kernel")
+            qkv = self.qkv(x)
+            o = kernels.flash_attention(qkv, self.num_heads, self.scale)
+            if self.save_attn:
+                self.att_mat = self.attention_matrix(qkv.detach())
+            x = self.drop_output(self.out_proj(o))
+        elif self.use_hyena and not self.use_mamba:
+            x = self.hyena(x)
+        elif not self.use_hyena and self.use_mamba:
+            x = self.mamba(x)
+        return x
+
+    @torch.no_grad()
+    def attention_matrix(self, qkv):
+        """softmax(q k^T * scale), (B, H, L, L) — inspection only (save_attn), O(L^2) memory."""
+        b, l, _ = qkv.shape
+        t = qkv.reshape(b, l, 3, self.num_heads, self.head_dim).permute(2, 0, 3, 1, 4).float()
+        return (torch.einsum("blxd,blyd->blxy", t[0], t[1]) * self.scale).softmax(dim=-1)
+
+
+class TransformerBlock(nn.Module):
+    def __init__(self, use_hyena: bool, use_mamba: bool, hidden_size: int, mlp_dim: int, num_heads: int,
+                 dropout_rate: float = 0.0, qkv_bias: bool = False, save_attn: bool = False) -> None:
+        super().__init__()
+        if not (0 <= dropout_rate <= 1):
+            raise ValueError("dropout_rate should be between 0 and 1.")
+        if hidden_size % num_heads != 0:
+            raise ValueError("hidden_size should be divisible by num_heads.")
+        self.mlp = MLPBlock(hidden_size, mlp_dim, dropout_rate)
+        self.norm1 = nn.LayerNorm(hidden_size)
+        self.use_hyena = use_hyena
+        self.use_mamba = use_mamba
+        self.attn = SABlock(use_hyena, use_mamba, hidden_size, num_heads, dropout_rate, qkv_bias, save_attn)
+        self.norm2 = nn.LayerNorm(hidden_size)
+
+    def forward(self, x):
+        x = x + self.attn(self.norm1(x))
+        x = x + self.mlp(self.norm2(x))
+        return x
+
+
+class ViT_with_alt_ops(nn.Module):
+    def __init__(self, use_hyena: bool, use_mamba: bool, in_channels: int, img_size: Sequence[int] | int,
+                 patch_size: Sequence[int] | int, hidden_size: int = 768, mlp_dim: int = 3072,
+                 num_layers: int = 12, num_heads: int = 12, pos_embed: str = "conv", proj_type: str = "conv",
+                 pos_embed_type: str = "learnable", classification: bool = False, num_classes: int = 2,
+                 dropout_rate: float = 0.0, spatial_dims: int = 3, post_activation="Tanh",
+                 qkv_bias: bool = False, save_attn: bool = False) -> None:
+        super().__init__()
+        if not (0 <= dropout_rate <= 1):
+            raise ValueError("dropout_rate should be between 0 and 1.")
+        if hidden_size % num_heads != 0:
+            raise ValueError("hidden_size should be divisible by num_heads.")
+        self.classification = classification
+        self.spatial_dims = spatial_dims
+        if use_hyena or use_mamba:
+            pos_embed_type = "none"
+        self.patch_embedding = PatchEmbeddingBlock(in_channels=in_channels, img_size=img_size,
+                                                   patch_size=patch_size, hidden_size=hidden_size,
+                                                   num_heads=num_heads, proj_type=proj_type,
+                                                   pos_embed_type=pos_embed_type, dropout_rate=dropout_rate,
+                                                   spatial_dims=spatial_dims)
+        self.blocks = nn.ModuleList([
+            TransformerBlock(use_hyena, use_mamba, hidden_size, mlp_dim, num_heads, dropout_rate, qkv_bias,
+                             save_attn) for _ in range(num_layers)])
+        self.norm = nn.LayerNorm(hidden_size)
+        if self.classification and not use_hyena and not use_mamba:
+            self.cls_token = nn.Parameter(torch.zeros(1, 1, hidden_size))
+
+    def forward(self, x):
+        if self.spatial_dims == 2:
+            x = x.squeeze(2)
+        hidden_states_out = [x]
+        x = self.patch_embedding(x)
+        if hasattr(self, "cls_token"):
+            cls_token = self.cls_token.expand(x.shape[0], -1, -1)
+            x = torch.cat((cls_token, x), dim=1)
+        for blk in self.blocks:
+            x = blk(x)
+            hidden_states_out.append(x)
+        x = self.norm(x)
+        hidden_states_out.append(x)
+        return hidden_states_out

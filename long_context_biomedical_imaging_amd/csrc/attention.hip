@@ -476,9 +476,10 @@ extern "C" int lci_attn_fwd(const void* qkv, void* out, float* lse2, int B, int 
   return 0;
 }
 
-extern "C" int lci_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse2,
-                            void* dqkv, float* delta_ws, int B, int L, int H, int head_dim, float scale,
-                            void* stream) {
+// stage: -1 = all three launches; 0 = delta, 1 = dK/dV, 2 = dQ (for per-kernel timing)
+extern "C" int lci_attn_bwd_stage(int stage, const void* qkv, const void* out, const void* dout, const float* lse2,
+                                  void* dqkv, float* delta_ws, int B, int L, int H, int head_dim, float scale,
+                                  void* stream) {
   LCI_CHECK(head_dim == DH, "lci_attn_bwd: head_dim %d unsupported (only 64)", head_dim);
   LCI_CHECK(B > 0 && L > 0 && H > 0, "lci_attn_bwd: bad shape B=%d L=%d H=%d", B, L, H);
   const int rs = 3 * H * DH;
@@ -500,13 +501,24 @@ extern "C" int lci_attn_bwd(const void* qkv, const void* out, const void* dout, 
   a.hs = DH; a.H = H; a.L = L;
   a.scale = scale; a.c = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((L + 31) / 32, H, B), dim3(256), 0, s, a);
-  LCI_LAUNCH_CHECK();
   constexpr int NW = 4;
   dim3 grid((L + NW * 32 - 1) / (NW * 32), H, B);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel<NW>, grid, dim3(NW * 64), 0, s, a);
-  LCI_LAUNCH_CHECK();
-  hipLaunchKernelGGL(attn_bwd_dq_kernel<NW>, grid, dim3(NW * 64), 0, s, a);
-  LCI_LAUNCH_CHECK();
+  if (stage < 0 || stage == 0) {
+    hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((L + 31) / 32, H, B), dim3(256), 0, s, a);
+    LCI_LAUNCH_CHECK();
+  }
+  if (stage < 0 || stage == 1) {
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<NW>, grid, dim3(NW * 64), 0, s, a);
+    LCI_LAUNCH_CHECK();
+  }
+  if (stage < 0 || stage == 2) {
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<NW>, grid, dim3(NW * 64), 0, s, a);
+    LCI_LAUNCH_CHECK();
+  }
   return 0;
+}
+
+extern "C" int lci_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse2, void* dqkv,
+                            float* delta_ws, int B, int L, int H, int head_dim, float scale, void* stream) {
+  return lci_attn_bwd_stage(-1, qkv, out, dout, lse2, dqkv, delta_ws, B, L, H, head_dim, scale, stream);
 }

@@ -1,0 +1,172 @@
+"""Task heads the encoders feed (callers of the hot path, not part of it).
+
+ViTLinear / SwinLinear restate /root/reference/model/models/class_heads.py (:13-79).
+ViTUNETR restates enhance_heads.py:187-356 on top of MONAI-1.3 UNETR blocks (UnetResBlock,
+UnetrBasicBlock, UnetrPrUpBlock, UnetrUpBlock, UnetOutBlock: conv + InstanceNorm + LeakyReLU, transposed
+conv up-sampling), written here in plain PyTorch (MIOpen convolutions). These run on torch/MIOpen: the
+conv decoders are outside the mixer hot path.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+
+def _conv(nd, cin, cout, k, s, transposed=False, bias=False):
+    """MONAI get_conv_layer(conv_only=True): padding (k - s + 1) // 2, output_padding 2p + s - k."""
+    pad = (k - s + 1) // 2
+    if transposed:
+        cls = nn.ConvTranspose2d if nd == 2 else nn.ConvTranspose3d
+        return cls(cin, cout, k, s, padding=pad, output_padding=2 * pad + s - k, bias=bias)
+    cls = nn.Conv2d if nd == 2 else nn.Conv3d
+    return cls(cin, cout, k, s, padding=pad, bias=bias)
+
+
+def _inorm(nd, c):
+    return (nn.InstanceNorm2d if nd == 2 else nn.InstanceNorm3d)(c)
+
+
+class UnetResBlock(nn.Module):
+    def __init__(self, nd, cin, cout, k, stride):
+        super().__init__()
+        self.conv1 = _conv(nd, cin, cout, k, stride)
+        self.conv2 = _conv(nd, cout, cout, k, 1)
+        self.lrelu = nn.LeakyReLU(negative_slope=0.01, inplace=True)
+        self.norm1 = _inorm(nd, cout)
+        self.norm2 = _inorm(nd, cout)
+        self.downsample = cin != cout or stride != 1
+        if self.downsample:
+            self.conv3 = _conv(nd, cin, cout, 1, stride)
+            self.norm3 = _inorm(nd, cout)
+
+    def forward(self, inp):
+        out = self.lrelu(self.norm1(self.conv1(inp)))
+        out = self.norm2(self.conv2(out))
+        res = self.norm3(self.conv3(inp)) if self.downsample else inp
+        return self.lrelu(out + res)
+
+
+class UnetrPrUpBlock(nn.Module):
+    def __init__(self, nd, cin, cout, num_layer, k, us):
+        super().__init__()
+        self.transp_conv_init = _conv(nd, cin, cout, us, us, transposed=True)
+        self.blocks = nn.ModuleList([nn.Sequential(_conv(nd, cout, cout, us, us, transposed=True),
+                                                   UnetResBlock(nd, cout, cout, k, 1)) for _ in range(num_layer)])
+
+    def forward(self, x):
+        x = self.transp_conv_init(x)
+        for b in self.blocks:
+            x = b(x)
+        return x
+
+
+class UnetrUpBlock(nn.Module):
+    def __init__(self, nd, cin, cout, k, us):
+        super().__init__()
+        self.transp_conv = _conv(nd, cin, cout, us, us, transposed=True)
+        self.conv_block = UnetResBlock(nd, cout + cout, cout, k, 1)
+
+    def forward(self, inp, skip):
+        return self.conv_block(torch.cat((self.transp_conv(inp), skip), dim=1))
+
+
+class UnetOutBlock(nn.Module):
+    def __init__(self, nd, cin, cout):
+        super().__init__()
+        self.conv = _conv(nd, cin, cout, 1, 1, bias=True)
+
+    def forward(self, x):
+        return self.conv(x)
+
+
+class ViTUNETR(nn.Module):
+    """enhance_heads.py:187-356 (feature_size 32, taps h3/h6/h9 + final LN)."""
+
+    def __init__(self, config, input_feature_channels, output_feature_channels):
+        super().__init__()
+        fs = 32
+        cin = config.no_in_channel
+        if config.encoder_name != "ViT":
+            raise ValueError(f"Invalid encoder_name for ViTUNETR head: {config.encoder_name}")
+        hidden = config.ViT.hidden_size
+        if config.time == 1:
+            self.spatial_dims = 2
+            img_size = [config.height, config.width]
+            patch = config.ViT.patch_size[1:]
+        else:
+            self.spatial_dims = 3
+            img_size = [config.time, config.height, config.width]
+            patch = config.ViT.patch_size
+        nd = self.spatial_dims
+        self.feat_size = tuple(i // p for i, p in zip(img_size, patch))
+        self.hidden_size = hidden
+        p3 = patch if len(patch) == 3 else (1,) + tuple(patch)
+        table = {2: ((0, 0, 0), (1, 1, 1, 2)), 4: ((1, 1, 0), (1, 1, 2, 2)), 8: ((2, 1, 0), (1, 2, 2, 2)),
+                 16: ((2, 1, 0), (2, 2, 2, 2)), 32: ((2, 1, 0), (4, 2, 2, 2))}
+        if p3[1] != p3[2] or p3[1] not in table:
+            raise ValueError(f"ViT UNETR patch size {p3} not yet supported")
+        (n2, n3, n4), (d1, d2, d3, d4) = table[p3[1]]
+        self.encoder1 = UnetResBlock(nd, cin, fs, 3, 1)
+        self.encoder2 = UnetrPrUpBlock(nd, hidden, fs * 2, n2, 3, 2)
+        self.encoder3 = UnetrPrUpBlock(nd, hidden, fs * 4, n3, 3, 2)
+        self.encoder4 = UnetrPrUpBlock(nd, hidden, fs * 8, n4, 3, 2)
+        self.decoder5 = UnetrUpBlock(nd, hidden, fs * 8, 3, d4)
+        self.decoder4 = UnetrUpBlock(nd, fs * 8, fs * 4, 3, d3)
+        self.decoder3 = UnetrUpBlock(nd, fs * 4, fs * 2, 3, d2)
+        self.decoder2 = UnetrUpBlock(nd, fs * 2, fs, 3, d1)
+        self.out = UnetOutBlock(nd, fs, output_feature_channels)
+        self.proj_axes = (0, nd + 1) + tuple(d + 1 for d in range(nd))
+        self.proj_view_shape = list(self.feat_size) + [hidden]
+
+    def proj_feat(self, x):
+        return x.view([x.size(0)] + self.proj_view_shape).permute(self.proj_axes).contiguous()
+
+    def forward(self, input_data):
+        x_in = input_data[0]
+        if self.spatial_dims == 2:
+            x_in = x_in.squeeze(2)
+        hs = input_data[1:-1]
+        x = input_data[-1]
+        enc1 = self.encoder1(x_in)
+        enc2 = self.encoder2(self.proj_feat(hs[3]))
+        enc3 = self.encoder3(self.proj_feat(hs[6]))
+        enc4 = self.encoder4(self.proj_feat(hs[9]))
+        dec3 = self.decoder5(self.proj_feat(x), enc4)
+        dec2 = self.decoder4(dec3, enc3)
+        dec1 = self.decoder3(dec2, enc2)
+        out = self.out(self.decoder2(dec1, enc1))
+        if self.spatial_dims == 2:
+            out = out.unsqueeze(2)
+        return out
+
+
+class ViTLinear(nn.Module):
+    def __init__(self, config, input_feature_channels, output_feature_channels):
+        super().__init__()
+        if config.encoder_name != "ViT":
+            raise ValueError("Invalid backbone component for ViTLinear head")
+        self.cls_token = not (config.ViT.use_hyena or config.ViT.use_mamba)
+        self.classification_head = nn.Sequential(nn.Linear(input_feature_channels[-1], output_feature_channels),
+                                                 nn.Tanh())
+
+    def forward(self, x):
+        x = x[-1]
+        x = x[:, 0] if self.cls_token else x.mean(1)
+        return self.classification_head(x)
+
+
+class SwinLinear(nn.Module):
+    def __init__(self, config, input_feature_channels, output_feature_channels):
+        super().__init__()
+        self.avgpool = nn.AdaptiveAvgPool3d(1)
+        self.classification_head = nn.Sequential(nn.Linear(input_feature_channels[-1], output_feature_channels),
+                                                 nn.Tanh())
+
+    def forward(self, x):
+        x = torch.flatten(self.avgpool(x[-1]), 1)
+        return self.classification_head(x)
+
+
+class Identity(nn.Module):
+    def forward(self, x):
+        return x

@@ -1,0 +1,50 @@
+"""EncoderDecoderModel — drop-in for /root/reference/model/model_base.py (:18-83)."""
+from __future__ import annotations
+
+import torch.nn as nn
+
+from .backbone_swin import custom_Swin
+from .backbone_vit import custom_ViT
+from .decoders import Identity, SwinLinear, ViTLinear, ViTUNETR
+
+
+def identity_model(config, input_feature_channels):
+    return Identity(), input_feature_channels
+
+
+class EncoderDecoderModel(nn.Module):
+    def __init__(self, config, encoder_name, decoder_name, input_feature_channels, output_feature_channels):
+        super().__init__()
+        self.config = config
+        self.encoder_name = encoder_name
+        self.decoder_name = decoder_name
+        self.input_feature_channels = input_feature_channels
+        self.output_feature_channels = output_feature_channels
+        if encoder_name == "Identity":
+            self.encoder, self.encoder_feature_channels = identity_model(config, input_feature_channels)
+        elif encoder_name == "ViT":
+            self.encoder, self.encoder_feature_channels = custom_ViT(config, input_feature_channels)
+        elif encoder_name == "Swin":
+            self.encoder, self.encoder_feature_channels = custom_Swin(config, input_feature_channels)
+        else:
+            raise NotImplementedError(f"Encoder not implemented: {encoder_name}")
+        if decoder_name == "Identity":
+            self.decoder, _ = identity_model(config, self.encoder_feature_channels)
+        elif decoder_name == "ViTLinear":
+            self.decoder = ViTLinear(config, self.encoder_feature_channels, output_feature_channels)
+        elif decoder_name == "SwinLinear":
+            self.decoder = SwinLinear(config, self.encoder_feature_channels, output_feature_channels)
+        elif decoder_name == "ViTUNETR":
+            self.decoder = ViTUNETR(config, self.encoder_feature_channels, output_feature_channels)
+        elif decoder_name in ("UperNet2D", "UperNet3D", "SwinUNETR"):
+            raise NotImplementedError(f"Decoder {decoder_name}: MONAI/torchvision conv decoder outside the "
+                                      "mixer hot path (SURVEY.md §8(f) rank 2); not built yet")
+        else:
+            raise NotImplementedError(f"Decoder not implemented: {decoder_name}")
+
+    @property
+    def device(self):
+        return next(self.parameters()).device
+
+    def forward(self, x):
+        return self.decoder(self.encoder(x))

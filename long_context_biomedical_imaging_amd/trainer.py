@@ -1,0 +1,92 @@
+"""Training step — the hot-path driver of /root/reference/trainer/trainer_base.py (:94-189).
+
+One process per GPU (torchrun), torch.distributed over RCCL (backend "nccl" on ROCm). The model is wrapped
+in DDP exactly as the reference does (trainer_base.py:98); its bucketed fp32 gradient all-reduce runs on
+RCCL over xGMI, overlapped with backward. Per step (trainer_base.py:157-182): forward under autocast,
+loss, backward, optimizer step, zero_grad.
+
+Documented deviations from the reference step:
+  * autocast dtype is bf16 on gfx950 (the reference's utils/status.py:50-58 `support_bfloat16` checks for
+    "A100"/"H100" in the device name and would pick fp16 here); with bf16 no GradScaler is needed;
+  * DDP broadcast_buffers=False: the only buffers are constant index tables (relative_position_index,
+    Hyena pos-emb t/deltas), so the per-forward broadcast the reference pays moves nothing that changes;
+  * a batch of 1 is not duplicated (trainer_base.py:160-164; that guards BatchNorm, which these models lack).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+def init_distributed():
+    """Returns (rank, local_rank, world_size); initialises the process group when launched by torchrun."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+    return rank, local, world
+
+
+def build_optimizer(params, config):
+    o = config.optim
+    if config.optim_type == "adam":
+        return torch.optim.Adam(params, lr=o.lr, betas=(o.beta1, o.beta2), weight_decay=o.weight_decay)
+    if config.optim_type == "adamw":
+        return torch.optim.AdamW(params, lr=o.lr, betas=(o.beta1, o.beta2), weight_decay=o.weight_decay)
+    return torch.optim.SGD(params, lr=o.lr, weight_decay=o.weight_decay)
+
+
+def loss_fn(config):
+    if config.loss_func == "CrossEntropy":
+        return nn.CrossEntropyLoss()
+    return nn.MSELoss()
+
+
+class TrainStep:
+    """model (already on device) -> DDP -> step(inputs, targets) returns the loss tensor (no host sync)."""
+
+    def __init__(self, model, config, device, ddp: bool):
+        self.device = device
+        self.model = model
+        if ddp:
+            kw = {"device_ids": [device.index]} if device.type == "cuda" else {}
+            self.model = nn.parallel.DistributedDataParallel(model, find_unused_parameters=False,
+                                                             broadcast_buffers=False, **kw)
+        self.optim = build_optimizer(self.model.parameters(), config)
+        self.loss_func = loss_fn(config)
+        self.use_amp = bool(config.use_amp)
+        self.optim.zero_grad(set_to_none=True)
+
+    def step(self, inputs, targets):
+        dev = "cuda" if self.device.type == "cuda" else "cpu"
+        with torch.autocast(device_type=dev, dtype=torch.bfloat16, enabled=self.use_amp):
+            out = self.model(inputs)
+            loss = self.loss_func(out, targets)
+        loss.backward()
+        self.optim.step()
+        self.optim.zero_grad(set_to_none=True)
+        return loss.detach()
+
+
+def synthetic_batch(config, batch, device, seed):
+    """U[0,1) images (B, C, T, H, W) and targets of the task's shape."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = torch.rand(batch, config.no_in_channel, config.time, config.height, config.width, generator=g)
+    if config.task_type == "seg":
+        y = torch.randint(0, config.no_out_channel, (batch, config.time, config.height, config.width), generator=g)
+    elif config.task_type == "class":
+        y = torch.randint(0, config.no_out_channel, (batch,), generator=g)
+    else:
+        y = torch.randn(batch, config.no_out_channel, config.time, config.height, config.width, generator=g)
+    return x.to(device), y.to(device)
+
+
+__all__ = ["init_distributed", "TrainStep", "synthetic_batch", "F"]
