@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""Summarize a tools/profile_bench.sh run: per-kernel average duration (kernel trace) and HBM traffic
+(PMC passes) for the liblci kernels.
+
+Traffic follows MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are KiB per dispatch; on gfx950
+FETCH_SIZE reports half the bytes of a wide (16 B/lane) coalesced streaming read, so it is doubled.
+Only dispatches after the first `skip_frac` of the run are counted (warm-up includes MIOpen's find phase).
+
+    python tools/summarize_prof.py gpurun_out/prof_r01 > profiles/r01_rocprof_summary.md
+"""
+import csv
+import os
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    for key in ("attn_fwd", "attn_bwd_dkdv", "attn_bwd_dq", "attn_bwd_delta", "patch_embed", "scan", "window",
+                "fftconv", "hyena", "dwconv"):
+        if key in name:
+            return name.split("(")[0].replace("void ", "")
+    return None
+
+
+def load_trace(path):
+    rows = list(csv.DictReader(open(path)))
+    return rows
+
+
+def main():
+    d = sys.argv[1]
+    skip_frac = float(sys.argv[2]) if len(sys.argv) > 2 else 0.5
+    tr = load_trace(os.path.join(d, "trace", "run_kernel_trace.csv"))
+    start = int(len(tr) * skip_frac)
+    dur = defaultdict(list)
+    for r in tr[start:]:
+        n = short(r["Kernel_Name"])
+        if n:
+            dur[n].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+    counters = {}
+    for c in ("fetch", "write"):
+        p = os.path.join(d, c, "run_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        rows = list(csv.DictReader(open(p)))
+        acc = defaultdict(list)
+        for r in rows[int(len(rows) * skip_frac):]:
+            n = short(r["Kernel_Name"])
+            if n:
+                acc[n].append(float(r["Counter_Value"]))
+        counters[c] = acc
+    print(f"# rocprofv3 summary: {d}\n")
+    print(f"Kernel-trace dispatches counted: the last {100 * (1 - skip_frac):.0f}% of the run "
+          f"({len(tr) - start} of {len(tr)} dispatches).\n")
+    print("| kernel | dispatches | avg ms | min ms | max ms | HBM read MB/launch (2x FETCH_SIZE) | HBM write MB/launch |")
+    print("|---|---|---|---|---|---|---|")
+    for n, v in sorted(dur.items(), key=lambda kv: -sum(kv[1])):
+        f = counters.get("fetch", {}).get(n)
+        w = counters.get("write", {}).get(n)
+        fm = f"{2 * sum(f) / len(f) / 1024:.1f}" if f else "n/a"
+        wm = f"{sum(w) / len(w) / 1024:.1f}" if w else "n/a"
+        print(f"| {n} | {len(v)} | {sum(v) / len(v):.3f} | {min(v):.3f} | {max(v):.3f} | {fm} | {wm} |")
+    print("\nrocprofv3 --stats top kernels (whole run, includes warm-up / MIOpen find):\n")
+    st = list(csv.DictReader(open(os.path.join(d, "trace", "run_kernel_stats.csv"))))
+    st.sort(key=lambda r: -float(r["TotalDurationNs"]))
+    print("| kernel | calls | total ms | avg ms | % |")
+    print("|---|---|---|---|---|")
+    for r in st[:12]:
+        print(f"| {r['Name'][:80]} | {r['Calls']} | {float(r['TotalDurationNs']) / 1e6:.1f} | "
+              f"{float(r['AverageNs']) / 1e6:.3f} | {float(r['Percentage']):.1f} |")
+
+
+if __name__ == "__main__":
+    main()
