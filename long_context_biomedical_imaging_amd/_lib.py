@@ -26,6 +26,11 @@ SIGNATURES = {
     "lci_attn_bwd_stage": [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P],
     "lci_patch_embed_fwd": [_P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P],
     "lci_patch_embed_bwd": [_P, _I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P, _P, _I, _P],
+    "lci_selective_scan_fwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
+    "lci_selective_scan_bwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I,
+                               _P, _P, _P, _P, _P],
+    "lci_dwconv_silu_fwd": [_I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    "lci_dwconv_silu_bwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
 }
 
 _lib = None

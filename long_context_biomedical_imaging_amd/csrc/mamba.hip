@@ -1,0 +1,507 @@
+// Mamba mixer kernels for gfx950: selective scan (fwd / bwd) and depthwise conv + SiLU, channels-last.
+//
+// Replaces (MambaVisionMixer.forward, mamba.py:108-139):
+//   x, z = SiLU(conv1d(x|z, k=3, padding='same', groups=C))                             (:118-119)
+//   y = selective_scan_fn(x, dt, A, B, C, D, delta_bias=b, delta_softplus=True)         (:125-134)
+// selective_scan_fn is mamba-ssm 1.2.0.post1's CUDA op; semantics = selective_scan_ref:
+//   dt' = softplus(dt + b);  x_t[n] = exp(dt' A[n]) x_{t-1}[n] + dt' B_t[n] u_t;  y_t = sum_n C_t[n] x_t[n] + D u_t
+//
+// Layout: every activation is channels-last (B, L, C) with a token stride, so the Linear outputs are read in
+// place (B and C are strided column slices of the x_proj output). One wave = 64 channels (lane = channel,
+// 8 fp32 states in registers); B_t / C_t are wave-uniform loads. L is split into chunks of Tc steps:
+//   fwd pass 1 (per chunk, zero init): end state + sum(dt')      fwd pass 2 (per channel/state): carry over chunks
+//   fwd pass 3 (per chunk from the true initial state): y, and x checkpoints every 16 steps for the backward
+//   bwd pass A (per chunk): local adjoint aggregate              bwd pass B: reverse carry over chunks
+//   bwd pass C (per chunk, reverse 16-step sub-blocks recomputed from the checkpoints in registers):
+//       du, d(dt), dA, dD, d(delta_bias), and per-token dB/dC reduced over channels (butterfly + LDS).
+#include "common.hpp"
+
+namespace lci {
+
+constexpr int SCAN_N = 8;     // d_state (the reference always uses 8: backbone_vit.py:184, backbone_swin.py:329)
+constexpr int CKPT = 16;      // backward checkpoint spacing (steps)
+constexpr float LOG2E = 1.4426950408889634f;
+
+struct ScanArgs {
+  const void* u; const void* delta; const void* Bm; const void* Cm; const void* dy;
+  const float* A; const float* D; const float* dbias;
+  void* y; void* du; void* ddelta;
+  float* xend; float* sdt; float* xinit; float* ckpt;   // (B,nch,Dx,N) (B,nch,Dx) (B,nch,Dx,N) (B,nck,Dx,N)
+  float* gl; float* gin;                                // (B,nch,Dx,N) x2
+  float* dBC;                                           // (B, L, 2N) f32
+  float* dA; float* dD; float* ddbias;                  // (Dx,N) (Dx) (Dx), accumulated
+  long long bu, bd, bB, bC, by, bdy, bdu, bdd;          // batch strides (elements)
+  int tu, td, tB, tC, ty, tdy, tdu, tdd;                // token strides (elements)
+  int B, L, Dx, Tc, nch, nck;
+  int write_ckpt;
+};
+
+template <typename T> __device__ __forceinline__ float ldf(const T* p) { return (float)(*p); }
+
+template <typename T>
+__device__ __forceinline__ void ld8(const T* p, float (&v)[SCAN_N]) {
+  if constexpr (sizeof(T) == 2) {
+    const bf16x8 r = *(const bf16x8*)p;
+#pragma unroll
+    for (int n = 0; n < SCAN_N; ++n) v[n] = (float)r[n];
+  } else {
+    const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+#pragma unroll
+    for (int n = 0; n < 4; ++n) { v[n] = a[n]; v[n + 4] = b[n]; }
+  }
+}
+
+// B/C rows are 16-byte aligned only when the token stride keeps them so; fall back to scalar loads.
+template <typename T>
+__device__ __forceinline__ void ld8u(const T* p, float (&v)[SCAN_N], bool aligned) {
+  if (aligned) { ld8(p, v); return; }
+#pragma unroll
+  for (int n = 0; n < SCAN_N; ++n) v[n] = (float)p[n];
+}
+
+__device__ __forceinline__ float softplus(float v) { return v <= 20.f ? log1pf(__expf(v)) : v; }
+
+// ---------------------------------------------------------------------------------- forward chunk pass
+// MODE 0: zero initial state -> xend, sdt. MODE 1: xinit -> y (+ checkpoints).
+template <typename T, int MODE>
+__global__ __launch_bounds__(256) void scan_fwd_kernel(ScanArgs a) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int chunk = blockIdx.x * 4 + wv;
+  const int b = blockIdx.z;
+  const int d = blockIdx.y * 64 + lane;
+  if (chunk >= a.nch) return;
+  const bool valid = d < a.Dx;
+  const int dd = valid ? d : a.Dx - 1;
+  float A2[SCAN_N], x[SCAN_N];
+#pragma unroll
+  for (int n = 0; n < SCAN_N; ++n) A2[n] = a.A[dd * SCAN_N + n] * LOG2E;
+  const float bias = a.dbias ? a.dbias[dd] : 0.f;
+  const float Dd = a.D ? a.D[dd] : 0.f;
+  const long long sidx = (((long long)b * a.nch + chunk) * a.Dx + dd) * SCAN_N;
+#pragma unroll
+  for (int n = 0; n < SCAN_N; ++n) x[n] = MODE ? a.xinit[sidx + n] : 0.f;
+  const T* up = (const T*)a.u + b * a.bu + dd;
+  const T* dp = (const T*)a.delta + b * a.bd + dd;
+  const T* Bp = (const T*)a.Bm + b * a.bB;
+  const T* Cp = (const T*)a.Cm + b * a.bC;
+  T* yp = (T*)a.y + b * a.by + dd;
+  const bool alB = ((a.tB * sizeof(T)) % 16 == 0) && (((uintptr_t)a.Bm) % 16 == 0);
+  const bool alC = ((a.tC * sizeof(T)) % 16 == 0) && (((uintptr_t)a.Cm) % 16 == 0);
+  const int t0 = chunk * a.Tc, t1 = min(a.L, t0 + a.Tc);
+  float sumdt = 0.f;
+  for (int t = t0; t < t1; ++t) {
+    if (MODE == 1 && a.write_ckpt && ((t & (CKPT - 1)) == 0) && valid) {
+      float* cp = a.ckpt + (((long long)b * a.nck + (t / CKPT)) * a.Dx + d) * SCAN_N;
+      *(f32x4*)cp = f32x4{x[0], x[1], x[2], x[3]};
+      *(f32x4*)(cp + 4) = f32x4{x[4], x[5], x[6], x[7]};
+    }
+    const float uf = ldf(up + (long long)t * a.tu);
+    const float dt = softplus(ldf(dp + (long long)t * a.td) + bias);
+    float Bv[SCAN_N];
+    ld8u(Bp + (long long)t * a.tB, Bv, alB);
+    const float dtu = dt * uf;
+#pragma unroll
+    for (int n = 0; n < SCAN_N; ++n) x[n] = fmaf(exp2_fast(dt * A2[n]), x[n], dtu * Bv[n]);
+    if (MODE == 1) {
+      float Cv[SCAN_N];
+      ld8u(Cp + (long long)t * a.tC, Cv, alC);
+      float yv = Dd * uf;
+#pragma unroll
+      for (int n = 0; n < SCAN_N; ++n) yv = fmaf(Cv[n], x[n], yv);
+      if (valid) yp[(long long)t * a.ty] = (T)yv;
+    } else {
+      sumdt += dt;
+    }
+  }
+  if (MODE == 0 && valid) {
+    float* xe = a.xend + sidx;
+    *(f32x4*)xe = f32x4{x[0], x[1], x[2], x[3]};
+    *(f32x4*)(xe + 4) = f32x4{x[4], x[5], x[6], x[7]};
+    a.sdt[((long long)b * a.nch + chunk) * a.Dx + d] = sumdt;
+  }
+}
+
+// carry over chunks: xinit[c] = carry; carry = exp(A sdt[c]) carry + xend[c]   (thread per (b, d, n))
+// REVERSE: gin[c] = carry; carry = gl[c] + exp(A sdt[c]) carry, chunks from last to first.
+template <bool REVERSE>
+__global__ __launch_bounds__(256) void scan_carry_kernel(ScanArgs a) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int total = a.B * a.Dx * SCAN_N;
+  if (i >= total) return;
+  const int n = i % SCAN_N, d = (i / SCAN_N) % a.Dx, b = i / (SCAN_N * a.Dx);
+  const float A2 = a.A[d * SCAN_N + n] * LOG2E;
+  float carry = 0.f;
+  const float* src = REVERSE ? a.gl : a.xend;
+  float* dst = REVERSE ? a.gin : a.xinit;
+  for (int k = 0; k < a.nch; ++k) {
+    const int c = REVERSE ? a.nch - 1 - k : k;
+    const long long ci = ((long long)b * a.nch + c) * a.Dx + d;
+    const float s = a.sdt[ci];
+    const float e = src[ci * SCAN_N + n];
+    dst[ci * SCAN_N + n] = carry;
+    carry = fmaf(exp2_fast(A2 * s), carry, e);
+  }
+}
+
+// ------------------------------------------------------------------------------------- backward pass A
+// local adjoint with zero carry-in from later chunks: Gl = a_{t0} g_{t0}
+template <typename T>
+__global__ __launch_bounds__(256) void scan_bwd_agg_kernel(ScanArgs a) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int chunk = blockIdx.x * 4 + wv;
+  const int b = blockIdx.z;
+  const int d = blockIdx.y * 64 + lane;
+  if (chunk >= a.nch) return;
+  const bool valid = d < a.Dx;
+  const int dd = valid ? d : a.Dx - 1;
+  float A2[SCAN_N], g[SCAN_N];
+#pragma unroll
+  for (int n = 0; n < SCAN_N; ++n) { A2[n] = a.A[dd * SCAN_N + n] * LOG2E; g[n] = 0.f; }
+  const float bias = a.dbias ? a.dbias[dd] : 0.f;
+  const T* dp = (const T*)a.delta + b * a.bd + dd;
+  const T* gyp = (const T*)a.dy + b * a.bdy + dd;
+  const T* Cp = (const T*)a.Cm + b * a.bC;
+  const bool alC = ((a.tC * sizeof(T)) % 16 == 0) && (((uintptr_t)a.Cm) % 16 == 0);
+  const int t0 = chunk * a.Tc, t1 = min(a.L, t0 + a.Tc);
+  for (int t = t1 - 1; t >= t0; --t) {
+    const float dt = softplus(ldf(dp + (long long)t * a.td) + bias);
+    const float gy = valid ? ldf(gyp + (long long)t * a.tdy) : 0.f;
+    float Cv[SCAN_N];
+    ld8u(Cp + (long long)t * a.tC, Cv, alC);
+#pragma unroll
+    for (int n = 0; n < SCAN_N; ++n) g[n] = exp2_fast(dt * A2[n]) * fmaf(Cv[n], gy, g[n]);
+  }
+  if (valid) {
+    float* o = a.gl + (((long long)b * a.nch + chunk) * a.Dx + d) * SCAN_N;
+    *(f32x4*)o = f32x4{g[0], g[1], g[2], g[3]};
+    *(f32x4*)(o + 4) = f32x4{g[4], g[5], g[6], g[7]};
+  }
+}
+
+// reduce 16 values over the 64 lanes of a wave (reduce-scatter butterfly): afterwards lane l holds the
+// total of value index (l >> 2) & 15.
+__device__ __forceinline__ float wave_reduce16(float (&v)[16], int lane) {
+#pragma unroll
+  for (int lvl = 0; lvl < 4; ++lvl) {
+    const int m = 32 >> lvl;
+    const int half = 8 >> lvl;
+    const bool up = (lane & m) != 0;
+#pragma unroll
+    for (int i = 0; i < half; ++i) {
+      const float send = up ? v[i] : v[i + half];
+      const float keep = up ? v[i + half] : v[i];
+      v[i] = keep + __shfl_xor(send, m);
+    }
+  }
+  float r = v[0];
+  r += __shfl_xor(r, 2);
+  r += __shfl_xor(r, 1);
+  return r;
+}
+
+// ------------------------------------------------------------------------------------- backward pass C
+// Workgroup = one (b, chunk), NWV waves cover all channels. Sub-blocks of CKPT steps in reverse.
+template <typename T>
+__global__ __launch_bounds__(256) void scan_bwd_kernel(ScanArgs a) {
+  __shared__ float red[CKPT][2 * SCAN_N];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int chunk = blockIdx.x, b = blockIdx.z;
+  const int d = blockIdx.y * 256 + wv * 64 + lane;
+  const bool valid = d < a.Dx;
+  const int dd = valid ? d : a.Dx - 1;
+  for (int i = threadIdx.x; i < CKPT * 2 * SCAN_N; i += blockDim.x) (&red[0][0])[i] = 0.f;
+  float A1[SCAN_N], A2[SCAN_N], h[SCAN_N], dA[SCAN_N];
+#pragma unroll
+  for (int n = 0; n < SCAN_N; ++n) {
+    A1[n] = a.A[dd * SCAN_N + n];
+    A2[n] = A1[n] * LOG2E;
+    h[n] = valid ? a.gin[(((long long)b * a.nch + chunk) * a.Dx + d) * SCAN_N + n] : 0.f;
+    dA[n] = 0.f;
+  }
+  const float bias = a.dbias ? a.dbias[dd] : 0.f;
+  const float Dd = a.D ? a.D[dd] : 0.f;
+  float dDacc = 0.f, dbacc = 0.f;
+  const T* up = (const T*)a.u + b * a.bu + dd;
+  const T* dp = (const T*)a.delta + b * a.bd + dd;
+  const T* gyp = (const T*)a.dy + b * a.bdy + dd;
+  const T* Bp = (const T*)a.Bm + b * a.bB;
+  const T* Cp = (const T*)a.Cm + b * a.bC;
+  T* dup = (T*)a.du + b * a.bdu + dd;
+  T* ddp = (T*)a.ddelta + b * a.bdd + dd;
+  const bool alB = ((a.tB * sizeof(T)) % 16 == 0) && (((uintptr_t)a.Bm) % 16 == 0);
+  const bool alC = ((a.tC * sizeof(T)) % 16 == 0) && (((uintptr_t)a.Cm) % 16 == 0);
+  const int t0 = chunk * a.Tc, t1 = min(a.L, t0 + a.Tc);
+  const int nsb = (t1 - t0 + CKPT - 1) / CKPT;
+  __syncthreads();
+  for (int sb = nsb - 1; sb >= 0; --sb) {
+    const int s0 = t0 + sb * CKPT;
+    // forward recompute of the sub-block from its checkpoint: xs[i] = x after step s0 + i
+    float xck[SCAN_N], xs[CKPT][SCAN_N];
+    {
+      const float* cp = a.ckpt + (((long long)b * a.nck + s0 / CKPT) * a.Dx + dd) * SCAN_N;
+      const f32x4 c0 = *(const f32x4*)cp, c1 = *(const f32x4*)(cp + 4);
+#pragma unroll
+      for (int n = 0; n < 4; ++n) { xck[n] = c0[n]; xck[n + 4] = c1[n]; }
+    }
+#pragma unroll
+    for (int i = 0; i < CKPT; ++i) {
+      const int t = s0 + i;
+#pragma unroll
+      for (int n = 0; n < SCAN_N; ++n) xs[i][n] = (i == 0) ? xck[n] : xs[i - 1][n];
+      if (t < t1) {
+        const float uf = ldf(up + (long long)t * a.tu);
+        const float dt = softplus(ldf(dp + (long long)t * a.td) + bias);
+        float Bv[SCAN_N];
+        ld8u(Bp + (long long)t * a.tB, Bv, alB);
+        const float dtu = dt * uf;
+#pragma unroll
+        for (int n = 0; n < SCAN_N; ++n) xs[i][n] = fmaf(exp2_fast(dt * A2[n]), xs[i][n], dtu * Bv[n]);
+      }
+    }
+    // reverse sweep
+#pragma unroll
+    for (int i = CKPT - 1; i >= 0; --i) {
+      const int t = s0 + i;
+      if (t < t1) {
+        const float uf = ldf(up + (long long)t * a.tu);
+        const float draw = ldf(dp + (long long)t * a.td) + bias;
+        const float dt = softplus(draw);
+        const float gy = valid ? ldf(gyp + (long long)t * a.tdy) : 0.f;
+        float Bv[SCAN_N], Cv[SCAN_N], v[16];
+        ld8u(Bp + (long long)t * a.tB, Bv, alB);
+        ld8u(Cp + (long long)t * a.tC, Cv, alC);
+        float du = Dd * gy, ddt = 0.f;
+        const float dtu = dt * uf;
+#pragma unroll
+        for (int n = 0; n < SCAN_N; ++n) {
+          const float xp = (i == 0) ? xck[n] : xs[i - 1][n];
+          const float at = exp2_fast(dt * A2[n]);
+          const float gt = fmaf(Cv[n], gy, h[n]);
+          v[SCAN_N + n] = gy * xs[i][n];                  // dC_t partial
+          v[n] = gt * dtu;                                // dB_t partial
+          du = fmaf(gt * dt, Bv[n], du);
+          const float gxa = gt * xp * at;
+          ddt = fmaf(gt, Bv[n] * uf, fmaf(gxa, A1[n], ddt));
+          dA[n] = fmaf(gxa, dt, dA[n]);
+          h[n] = at * gt;
+        }
+        if (!valid) {
+#pragma unroll
+          for (int k = 0; k < 16; ++k) v[k] = 0.f;
+        }
+        const float sg = draw <= 20.f ? 1.f / (1.f + __expf(-draw)) : 1.f;
+        const float ddl = ddt * sg;
+        dDacc = fmaf(gy, uf, dDacc);
+        dbacc += ddl;
+        if (valid) {
+          dup[(long long)t * a.tdu] = (T)du;
+          ddp[(long long)t * a.tdd] = (T)ddl;
+        }
+        const float r = wave_reduce16(v, lane);
+        if ((lane & 3) == 0) atomicAdd(&red[i][lane >> 2], r);
+      }
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < CKPT * 2 * SCAN_N; k += blockDim.x) {
+      const int i = k / (2 * SCAN_N), j = k % (2 * SCAN_N);
+      const int t = s0 + i;
+      if (t < t1) atomicAdd(a.dBC + ((long long)b * a.L + t) * (2 * SCAN_N) + j, red[i][j]);
+      red[i][j] = 0.f;
+    }
+    __syncthreads();
+  }
+  if (valid) {
+#pragma unroll
+    for (int n = 0; n < SCAN_N; ++n) atomicAdd(a.dA + d * SCAN_N + n, dA[n]);
+    atomicAdd(a.dD + d, dDacc);
+    atomicAdd(a.ddbias + d, dbacc);
+  }
+}
+
+// ------------------------------------------------------------------------------ depthwise conv + SiLU
+// in (B, L, 2C) (x | z halves, channels-last), w (C, 3) x2, 'same' padding (1 left, 1 right).
+// out_x (B, L, C) and out_z written at column offset zoff of a (B, L, oz_ts) buffer.
+// A thread owns one channel of the 2C and a run of CONV_T tokens (lanes = consecutive channels: coalesced
+// rows); the 3-tap window slides in registers, weight-gradient partials stay in registers until one atomic.
+constexpr int CONV_K = 3;
+constexpr int CONV_T = 256;
+
+struct ConvArgs {
+  const void* in; const float* wx; const float* bx; const float* wz; const float* bz;
+  void* ox; void* oz;
+  const void* gx; const void* gz;   // bwd: grads of the SiLU outputs
+  void* din;                        // bwd: (B, L, 2C)
+  float* dwx; float* dbx; float* dwz; float* dbz;
+  int B, L, C, in_ts, ox_ts, oz_ts, zoff;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void dwconv_silu_fwd_kernel(ConvArgs a) {
+  const int cc = blockIdx.x * 256 + threadIdx.x;
+  if (cc >= 2 * a.C) return;
+  const int b = blockIdx.z, t0 = blockIdx.y * CONV_T, t1 = min(a.L, t0 + CONV_T);
+  const int half = cc / a.C, c = cc % a.C;
+  const float* w = (half ? a.wz : a.wx) + c * CONV_K;
+  const float* bp = half ? a.bz : a.bx;
+  const float w0 = w[0], w1 = w[1], w2 = w[2], bias = bp ? bp[c] : 0.f;
+  const T* in = (const T*)a.in + (long long)b * a.L * a.in_ts + cc;
+  auto X = [&](int s) -> float { return (s >= 0 && s < a.L) ? (float)in[(long long)s * a.in_ts] : 0.f; };
+  float xm = X(t0 - 1), x0 = X(t0);
+  for (int t = t0; t < t1; ++t) {
+    const float xp = X(t + 1);
+    const float pre = fmaf(w0, xm, fmaf(w1, x0, fmaf(w2, xp, bias)));
+    const float sv = pre / (1.f + __expf(-pre));
+    if (half == 0) ((T*)a.ox)[((long long)b * a.L + t) * a.ox_ts + c] = (T)sv;
+    else ((T*)a.oz)[((long long)b * a.L + t) * a.oz_ts + a.zoff + c] = (T)sv;
+    xm = x0; x0 = xp;
+  }
+}
+
+// g(s) = dout(s) * silu'(pre(s)); din(t) = w0 g(t+1) + w1 g(t) + w2 g(t-1); dw[j] += g(t) x(t+j-1)
+template <typename T>
+__global__ __launch_bounds__(256) void dwconv_silu_bwd_kernel(ConvArgs a) {
+  const int cc = blockIdx.x * 256 + threadIdx.x;
+  if (cc >= 2 * a.C) return;
+  const int b = blockIdx.z, t0 = blockIdx.y * CONV_T, t1 = min(a.L, t0 + CONV_T);
+  const int half = cc / a.C, c = cc % a.C;
+  const float* w = (half ? a.wz : a.wx) + c * CONV_K;
+  const float* bp = half ? a.bz : a.bx;
+  const float w0 = w[0], w1 = w[1], w2 = w[2], bias = bp ? bp[c] : 0.f;
+  const T* in = (const T*)a.in + (long long)b * a.L * a.in_ts + cc;
+  const T* go = half ? (const T*)a.gz + (long long)b * a.L * a.oz_ts + a.zoff + c
+                     : (const T*)a.gx + (long long)b * a.L * a.ox_ts + c;
+  const int gts = half ? a.oz_ts : a.ox_ts;
+  auto X = [&](int s) -> float { return (s >= 0 && s < a.L) ? (float)in[(long long)s * a.in_ts] : 0.f; };
+  auto G = [&](int s, float xm, float x0, float xp) -> float {
+    if (s < 0 || s >= a.L) return 0.f;
+    const float pre = fmaf(w0, xm, fmaf(w1, x0, fmaf(w2, xp, bias)));
+    const float sg = 1.f / (1.f + __expf(-pre));
+    return (float)go[(long long)s * gts] * sg * fmaf(pre, 1.f - sg, 1.f);
+  };
+  // window over x: x(t-2) .. x(t+2); g(t-1), g(t), g(t+1)
+  float xa = X(t0 - 2), xb = X(t0 - 1), xc = X(t0), xd = X(t0 + 1);
+  float gm = G(t0 - 1, xa, xb, xc), g0 = G(t0, xb, xc, xd);
+  float dw0 = 0.f, dw1 = 0.f, dw2 = 0.f, db = 0.f;
+  T* din = (T*)a.din + (long long)b * a.L * a.in_ts + cc;
+  for (int t = t0; t < t1; ++t) {
+    const float xe = X(t + 2);
+    const float gp = G(t + 1, xc, xd, xe);
+    din[(long long)t * a.in_ts] = (T)fmaf(w0, gp, fmaf(w1, g0, w2 * gm));
+    dw0 = fmaf(g0, xb, dw0);
+    dw1 = fmaf(g0, xc, dw1);
+    dw2 = fmaf(g0, xd, dw2);
+    db += g0;
+    xa = xb; xb = xc; xc = xd; xd = xe;
+    gm = g0; g0 = gp;
+  }
+  float* dw = (half ? a.dwz : a.dwx) + c * CONV_K;
+  atomicAdd(dw + 0, dw0);
+  atomicAdd(dw + 1, dw1);
+  atomicAdd(dw + 2, dw2);
+  float* dbp = half ? a.dbz : a.dbx;
+  if (dbp) atomicAdd(dbp + c, db);
+}
+
+}  // namespace lci
+
+using namespace lci;
+
+static int scan_fill(ScanArgs& a, int B, int L, int Dx, int N, int Tc) {
+  LCI_CHECK(N == SCAN_N, "selective_scan: d_state %d unsupported (8)", N);
+  LCI_CHECK(B > 0 && L > 0 && Dx > 0 && Dx <= 1024, "selective_scan: bad shape B=%d L=%d Dx=%d", B, L, Dx);
+  LCI_CHECK(Tc % CKPT == 0 && Tc > 0, "selective_scan: chunk %d must be a multiple of %d", Tc, CKPT);
+  a.B = B; a.L = L; a.Dx = Dx; a.Tc = Tc;
+  a.nch = (L + Tc - 1) / Tc; a.nck = (L + CKPT - 1) / CKPT;
+  return 0;
+}
+
+// strides: array of 16 long long: [bu,tu, bd,td, bB,tB, bC,tC, by,ty, bdy,tdy, bdu,tdu, bdd,tdd] (elements)
+static void scan_strides(ScanArgs& a, const long long* s) {
+  a.bu = s[0]; a.tu = (int)s[1]; a.bd = s[2]; a.td = (int)s[3]; a.bB = s[4]; a.tB = (int)s[5];
+  a.bC = s[6]; a.tC = (int)s[7]; a.by = s[8]; a.ty = (int)s[9]; a.bdy = s[10]; a.tdy = (int)s[11];
+  a.bdu = s[12]; a.tdu = (int)s[13]; a.bdd = s[14]; a.tdd = (int)s[15];
+}
+
+// Workspace (f32): xend, xinit (B*nch*Dx*N each), sdt (B*nch*Dx), ckpt (B*nck*Dx*N) if ckpt != null.
+extern "C" int lci_selective_scan_fwd(int dtype, const void* u, const void* delta, const float* A, const void* Bm,
+                                      const void* Cm, const float* D, const float* delta_bias, void* y,
+                                      const long long* strides, int B, int L, int Dx, int N, int chunk,
+                                      float* xend, float* xinit, float* sdt, float* ckpt, void* stream) {
+  ScanArgs a{};
+  if (scan_fill(a, B, L, Dx, N, chunk)) return 1;
+  scan_strides(a, strides);
+  a.u = u; a.delta = delta; a.A = A; a.Bm = Bm; a.Cm = Cm; a.D = D; a.dbias = delta_bias; a.y = y;
+  a.xend = xend; a.xinit = xinit; a.sdt = sdt; a.ckpt = ckpt; a.write_ckpt = ckpt != nullptr;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((a.nch + 3) / 4, (Dx + 63) / 64, B);
+  const int nthr = B * Dx * SCAN_N;
+  if (dtype == 1) hipLaunchKernelGGL((scan_fwd_kernel<bf16, 0>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((scan_fwd_kernel<float, 0>), grid, dim3(256), 0, s, a);
+  LCI_LAUNCH_CHECK();
+  hipLaunchKernelGGL(scan_carry_kernel<false>, dim3((nthr + 255) / 256), dim3(256), 0, s, a);
+  LCI_LAUNCH_CHECK();
+  if (dtype == 1) hipLaunchKernelGGL((scan_fwd_kernel<bf16, 1>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((scan_fwd_kernel<float, 1>), grid, dim3(256), 0, s, a);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+
+// dA (Dx*N), dD (Dx), ddelta_bias (Dx) and dBC (B, L, 2N) are accumulated (caller zeroes them).
+// Workspace: gl, gin (B*nch*Dx*N each); sdt and ckpt from the forward (same chunk).
+extern "C" int lci_selective_scan_bwd(int dtype, const void* u, const void* delta, const float* A, const void* Bm,
+                                      const void* Cm, const float* D, const float* delta_bias, const void* dy,
+                                      void* du, void* ddelta, float* dBC, float* dA, float* dD, float* ddelta_bias,
+                                      const long long* strides, int B, int L, int Dx, int N, int chunk,
+                                      const float* sdt, const float* ckpt, float* gl, float* gin, void* stream) {
+  ScanArgs a{};
+  if (scan_fill(a, B, L, Dx, N, chunk)) return 1;
+  scan_strides(a, strides);
+  a.u = u; a.delta = delta; a.A = A; a.Bm = Bm; a.Cm = Cm; a.D = D; a.dbias = delta_bias; a.dy = dy;
+  a.du = du; a.ddelta = ddelta; a.dBC = dBC; a.dA = dA; a.dD = dD; a.ddbias = ddelta_bias;
+  a.sdt = (float*)sdt; a.ckpt = (float*)ckpt; a.gl = gl; a.gin = gin;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((a.nch + 3) / 4, (Dx + 63) / 64, B);
+  const int nthr = B * Dx * SCAN_N;
+  if (dtype == 1) hipLaunchKernelGGL((scan_bwd_agg_kernel<bf16>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((scan_bwd_agg_kernel<float>), grid, dim3(256), 0, s, a);
+  LCI_LAUNCH_CHECK();
+  hipLaunchKernelGGL(scan_carry_kernel<true>, dim3((nthr + 255) / 256), dim3(256), 0, s, a);
+  LCI_LAUNCH_CHECK();
+  const int nwv = Dx >= 256 ? 4 : (Dx + 63) / 64;
+  dim3 gridc(a.nch, (Dx + 255) / 256, B);
+  if (dtype == 1) hipLaunchKernelGGL((scan_bwd_kernel<bf16>), gridc, dim3(nwv * 64), 0, s, a);
+  else hipLaunchKernelGGL((scan_bwd_kernel<float>), gridc, dim3(nwv * 64), 0, s, a);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int lci_dwconv_silu_fwd(int dtype, const void* in, const float* wx, const float* bx, const float* wz,
+                                   const float* bz, void* ox, void* oz, int B, int L, int C, int K, int in_ts,
+                                   int ox_ts, int oz_ts, int zoff, void* stream) {
+  LCI_CHECK(K == CONV_K, "dwconv_silu: kernel size %d unsupported (3, as mamba.py d_conv=3)", K);
+  ConvArgs a{};
+  a.in = in; a.wx = wx; a.bx = bx; a.wz = wz; a.bz = bz; a.ox = ox; a.oz = oz;
+  a.B = B; a.L = L; a.C = C; a.in_ts = in_ts; a.ox_ts = ox_ts; a.oz_ts = oz_ts; a.zoff = zoff;
+  dim3 grid((2 * C + 255) / 256, (L + CONV_T - 1) / CONV_T, B);
+  if (dtype == 1) hipLaunchKernelGGL(dwconv_silu_fwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL(dwconv_silu_fwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+
+// dwx/dbx/dwz/dbz accumulated (caller zeroes). din (B, L, 2C) written with token stride in_ts.
+extern "C" int lci_dwconv_silu_bwd(int dtype, const void* in, const float* wx, const float* bx, const float* wz,
+                                   const float* bz, const void* gx, const void* gz, void* din, float* dwx,
+                                   float* dbx, float* dwz, float* dbz, int B, int L, int C, int K, int in_ts,
+                                   int ox_ts, int oz_ts, int zoff, void* stream) {
+  LCI_CHECK(K == CONV_K, "dwconv_silu: kernel size %d unsupported (3, as mamba.py d_conv=3)", K);
+  ConvArgs a{};
+  a.in = in; a.wx = wx; a.bx = bx; a.wz = wz; a.bz = bz; a.gx = gx; a.gz = gz; a.din = din;
+  a.dwx = dwx; a.dbx = dbx; a.dwz = dwz; a.dbz = dbz;
+  a.B = B; a.L = L; a.C = C; a.in_ts = in_ts; a.ox_ts = ox_ts; a.oz_ts = oz_ts; a.zoff = zoff;
+  dim3 grid((2 * C + 255) / 256, (L + CONV_T - 1) / CONV_T, B);
+  if (dtype == 1) hipLaunchKernelGGL(dwconv_silu_bwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL(dwconv_silu_bwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}

@@ -174,3 +174,163 @@ def patch_embed(x, weight, bias, pos, channels_last_tokens: bool):
         if out_dtype not in _DT:
             out_dtype = torch.float32
     return _PatchEmbed.apply(x, weight, bias, pos, channels_last_tokens, out_dtype)
+
+
+# ----------------------------------------------------------------------------------------- mamba
+SCAN_N = 8
+CKPT = 16
+
+
+def _ll_array(vals):
+    import ctypes
+    return (ctypes.c_longlong * len(vals))(*vals)
+
+
+def _scan_chunk(L):
+    """Chunk length: >= 256 steps, at most ~512 chunks per sequence (the carry passes are sequential)."""
+    tc = max(256, -(-L // 512))
+    return -(-tc // CKPT) * CKPT
+
+
+def _bt(t):
+    """(batch stride, token stride) in elements of a (B, L, C)-shaped view with unit channel stride."""
+    assert t.stride(-1) == 1, "channel dimension must be contiguous"
+    return t.stride(0), t.stride(1)
+
+
+class _DWConvSiLUPair(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, xz, wx, bx, wz, bz):
+        B, L, C2 = xz.shape
+        C = C2 // 2
+        xs = torch.empty(B, L, C, device=xz.device, dtype=xz.dtype)
+        yz = torch.empty(B, L, C2, device=xz.device, dtype=xz.dtype)
+        w = [t.float().reshape(C, -1).contiguous() if t is not None else None for t in (wx, bx, wz, bz)]
+        K = w[0].shape[1]
+        KernelTimer.run("dwconv_silu_fwd", 0.0, xz, lambda: _lib.call(
+            "lci_dwconv_silu_fwd", _DT[xz.dtype], xz.data_ptr(), w[0].data_ptr(), _lib.ptr(w[1]), w[2].data_ptr(),
+            _lib.ptr(w[3]), xs.data_ptr(), yz.data_ptr(), B, L, C, K, C2, C, C2, C, _lib.stream_of(xz)))
+        ctx.save_for_backward(xz, *[t for t in w if t is not None])
+        ctx.meta = (bx is not None, bz is not None, wx.shape, wz.shape)
+        return xs, yz
+
+    @staticmethod
+    def backward(ctx, gxs, gyz):
+        xz, *ws = ctx.saved_tensors
+        has_bx, has_bz, wxs, wzs = ctx.meta
+        wx = ws.pop(0)
+        bx = ws.pop(0) if has_bx else None
+        wz = ws.pop(0)
+        bz = ws.pop(0) if has_bz else None
+        B, L, C2 = xz.shape
+        C = C2 // 2
+        K = wx.shape[1]
+        gxs = torch.zeros(B, L, C, device=xz.device, dtype=xz.dtype) if gxs is None else gxs.to(xz.dtype).contiguous()
+        gyz = torch.zeros(B, L, C2, device=xz.device, dtype=xz.dtype) if gyz is None else gyz.to(xz.dtype).contiguous()
+        din = torch.empty_like(xz)
+        f32 = dict(device=xz.device, dtype=torch.float32)
+        dwx, dwz = torch.zeros(C, K, **f32), torch.zeros(C, K, **f32)
+        dbx = torch.zeros(C, **f32) if has_bx else None
+        dbz = torch.zeros(C, **f32) if has_bz else None
+        KernelTimer.run("dwconv_silu_bwd", 0.0, xz, lambda: _lib.call(
+            "lci_dwconv_silu_bwd", _DT[xz.dtype], xz.data_ptr(), wx.data_ptr(), _lib.ptr(bx), wz.data_ptr(),
+            _lib.ptr(bz), gxs.data_ptr(), gyz.data_ptr(), din.data_ptr(), dwx.data_ptr(), _lib.ptr(dbx),
+            dwz.data_ptr(), _lib.ptr(dbz), B, L, C, K, C2, C, C2, C, _lib.stream_of(xz)))
+        return din, dwx.reshape(wxs), dbx, dwz.reshape(wzs), dbz
+
+
+def dwconv_silu_pair(xz, wx, bx, wz, bz):
+    """SiLU(depthwise conv1d(k, 'same')) of both channel halves of the channels-last in_proj output.
+
+    xz (B, L, 2C) -> xs (B, L, C), yz (B, L, 2C) whose second half holds SiLU(conv z) (mamba.py:118-119);
+    the first half of yz is left for the selective scan to fill (the reference's cat([y, z]), :136).
+    """
+    _lib.require_gpu(xz)
+    if xz.dtype not in _DT:
+        xz = xz.float()
+    return _DWConvSiLUPair.apply(xz, wx, bx, wz, bz)
+
+
+class _SelectiveScanCL(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, u, delta, A, Bm, Cm, D, delta_bias, yz):
+        B, L, Dx = u.shape
+        N = A.shape[1]
+        dt = u.dtype
+        tc = _scan_chunk(L)
+        nch = -(-L // tc)
+        nck = -(-L // CKPT)
+        f32 = dict(device=u.device, dtype=torch.float32)
+        xend = torch.empty(B, nch, Dx, N, **f32)
+        xinit = torch.empty(B, nch, Dx, N, **f32)
+        sdt = torch.empty(B, nch, Dx, **f32)
+        need_grad = any(ctx.needs_input_grad)
+        ckpt = torch.empty(B, nck, Dx, N, **f32) if need_grad else None
+        Af, Dv, bv = A.float().contiguous(), D.float().contiguous(), delta_bias.float().contiguous()
+        y = yz[..., :Dx]
+        strides = _ll_array([*_bt(u), *_bt(delta), *_bt(Bm), *_bt(Cm), *_bt(y), 0, 0, 0, 0, 0, 0])
+        KernelTimer.run("selective_scan_fwd", float(B * L), u, lambda: _lib.call(
+            "lci_selective_scan_fwd", _DT[dt], u.data_ptr(), delta.data_ptr(), Af.data_ptr(), Bm.data_ptr(),
+            Cm.data_ptr(), Dv.data_ptr(), bv.data_ptr(), y.data_ptr(), strides, B, L, Dx, N, tc,
+            xend.data_ptr(), xinit.data_ptr(), sdt.data_ptr(), _lib.ptr(ckpt), _lib.stream_of(u)))
+        ctx.mark_dirty(yz)
+        if need_grad:
+            ctx.save_for_backward(u, delta, Af, Bm, Cm, Dv, bv, sdt, ckpt)
+        ctx.tc = tc
+        return yz
+
+    @staticmethod
+    def backward(ctx, gyz):
+        u, delta, Af, Bm, Cm, Dv, bv, sdt, ckpt = ctx.saved_tensors
+        B, L, Dx = u.shape
+        N = Af.shape[1]
+        tc = ctx.tc
+        nch = -(-L // tc)
+        gyz = gyz.to(u.dtype)
+        if gyz.stride(-1) != 1:
+            gyz = gyz.contiguous()
+        dy = gyz[..., :Dx]
+        f32 = dict(device=u.device, dtype=torch.float32)
+        du = torch.empty_like(u)
+        dd = torch.empty(B, L, Dx, device=u.device, dtype=u.dtype)
+        dBC = torch.zeros(B, L, 2 * N, **f32)
+        dA = torch.zeros(Dx, N, **f32)
+        dD = torch.zeros(Dx, **f32)
+        db = torch.zeros(Dx, **f32)
+        gl = torch.empty(B, nch, Dx, N, **f32)
+        gin = torch.empty(B, nch, Dx, N, **f32)
+        strides = _ll_array([*_bt(u), *_bt(delta), *_bt(Bm), *_bt(Cm), 0, 0, *_bt(dy), *_bt(du), *_bt(dd)])
+        KernelTimer.run("selective_scan_bwd", float(B * L), u, lambda: _lib.call(
+            "lci_selective_scan_bwd", _DT[u.dtype], u.data_ptr(), delta.data_ptr(), Af.data_ptr(), Bm.data_ptr(),
+            Cm.data_ptr(), Dv.data_ptr(), bv.data_ptr(), dy.data_ptr(), du.data_ptr(), dd.data_ptr(),
+            dBC.data_ptr(), dA.data_ptr(), dD.data_ptr(), db.data_ptr(), strides, B, L, Dx, N, tc, sdt.data_ptr(),
+            ckpt.data_ptr(), gl.data_ptr(), gin.data_ptr(), _lib.stream_of(u)))
+        gz = gyz.clone()
+        gz[..., :Dx] = 0
+        return (du, dd, dA, dBC[..., :N].to(Bm.dtype), dBC[..., N:].to(Cm.dtype), dD, db, gz)
+
+
+def selective_scan_cl(u, delta, A, Bm, Cm, D, delta_bias, yz):
+    """Channels-last selective scan (mamba-ssm selective_scan_fn semantics with delta_softplus=True).
+
+    u, delta (B, L, Dx); Bm, Cm (B, L, N) views with unit channel stride (e.g. column slices of x_proj's
+    output); A (Dx, N) f32; D, delta_bias (Dx) f32; yz (B, L, 2*Dx): y is written into yz[..., :Dx] in place
+    and yz is returned (the reference's cat([y, z]) target). y dtype = u dtype.
+    """
+    _lib.require_gpu(u, delta, yz)
+    dt = u.dtype
+    if dt not in _DT:
+        raise _lib.LciError("selective_scan: u must be bf16 or f32")
+    u = u.contiguous()
+    delta = delta.to(dt)
+    Bm = Bm.to(dt)
+    Cm = Cm.to(dt)
+    if Bm.stride(-1) != 1:
+        Bm = Bm.contiguous()
+    if Cm.stride(-1) != 1:
+        Cm = Cm.contiguous()
+    if delta.stride(-1) != 1:
+        delta = delta.contiguous()
+    if yz.dtype != dt:
+        raise _lib.LciError("selective_scan: yz dtype must match u")
+    return _SelectiveScanCL.apply(u, delta, A, Bm, Cm, D, delta_bias, yz)
