@@ -29,6 +29,8 @@ SIGNATURES = {
     "lci_selective_scan_fwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "lci_selective_scan_bwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I,
                                _P, _P, _P, _P, _P],
+    "lci_window_attn_fwd": [_P, _P, _P, _P, _P, _P, _P, _F, _P],
+    "lci_window_attn_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P],
     "lci_dwconv_silu_fwd": [_I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "lci_dwconv_silu_bwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
 }
@@ -51,6 +53,8 @@ def load(path: str = LIB_PATH):
     lib = ctypes.CDLL(path)
     lib.lci_last_error.restype = ctypes.c_char_p
     lib.lci_abi_version.restype = ctypes.c_int
+    lib.lci_window_dS_elems.restype = ctypes.c_longlong
+    lib.lci_window_dS_elems.argtypes = [_P]
     for name, argt in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.argtypes = argt

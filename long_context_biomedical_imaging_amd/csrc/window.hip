@@ -1,0 +1,450 @@
+// Swin shifted-window attention for gfx950 (head_dim 32).
+//
+// Replaces WindowAttention.forward (backbone_swin.py:339-359):
+//   attn = (q*scale) k^T + rpb_table[rp_index] (+ mask (-100 across regions)); softmax; (attn v)
+// and, in GRID mode, the index ops around it in SwinTransformerBlock.forward_part1 (:435-487):
+//   F.pad -> torch.roll(-shift) -> window_partition ... window_reverse -> torch.roll(+shift) -> crop,
+// evaluated as address arithmetic on the channels-last qkv grid (B, S0, S1[, S2], 3C): window token n of
+// window w reads source voxel (p + shift) mod Sp (p = padded coordinate); voxels beyond S are the zero padding,
+// whose qkv row is the Linear bias. The -100 mask is recomputed from per-axis region ids exactly as
+// compute_mask builds it (:591-628). WINDOWS mode takes pre-partitioned (Bw, N, 3C) and an optional mask.
+//
+// One workgroup = one (window, head); the whole window's K and V live in LDS; 4 waves x 32-query blocks;
+// S^T = K.Q^T with the query on the MFMA lane, online softmax over 32-key tiles, O^T += V^T.P^T.
+// Backward: phase 1 (query on lane): dP^T, dS^T, dQ^T += K^T dS^T, and dS tiles for d(rpb);
+//           phase 2 (key on lane, Q/dO in LDS): dV^T += dO^T P, dK^T += Q^T dS. Pad-token dK/dV go to the
+//           qkv bias gradient. d(rpb) = sum over windows of dS (separate reduction kernel, no atomics).
+#include "common.hpp"
+
+namespace lci {
+
+constexpr int WHD = 32;          // head dim (Swin: C / heads = 32 at every stage)
+constexpr int WLD = 40;          // LDS row stride (elements, 80 B): b128 row reads conflict-free
+constexpr int WMAXN = 768;       // max tokens per window (LDS: two Npad x 80 B tiles)
+constexpr float WLOG2E = 1.4426950408889634f;
+constexpr float WNEG = -1.0e30f;
+
+struct WinArgs {
+  const bf16* qkv; const float* qkv_bias;  // bias (3C) f32 or null: value of padded tokens
+  const float* rpb;                        // (H, N, Npad) f32, log-domain bias (rpb_table[index])
+  const float* mask;                       // WINDOWS mode: (nW, N, N) f32 or null
+  bf16* out; const bf16* o; const bf16* dout;
+  float* lse2;                             // (Bw, H, N)
+  bf16* dqkv; float* dbias_pad;            // bwd
+  bf16* dS;                                // (Bw, H, nqb, nkt, 64, 16) bf16 tiles or null
+  float* drpb;                             // (H, N, N) f32 (reduction kernel)
+  int mode, nd, S[3], ws[3], sh[3], Sp[3], nwin[3];
+  int Bw, nW, N, Npad, nqb, nkt, C, H, masked;
+  float scale, c;
+};
+
+// token row of window token n (>= 0), -1 for a padded voxel, and its region id (grid mode)
+__device__ __forceinline__ int win_row(const WinArgs& a, int w, int n, int& rid) {
+  rid = 0;
+  if (a.mode == 0) return w * a.N + n;
+  const int b = w / a.nW;
+  int wi = w % a.nW;
+  int widx[3], nidx[3];
+  for (int s = a.nd - 1; s >= 0; --s) { widx[s] = wi % a.nwin[s]; wi /= a.nwin[s]; }
+  int nn = n;
+  for (int s = a.nd - 1; s >= 0; --s) { nidx[s] = nn % a.ws[s]; nn /= a.ws[s]; }
+  long long row = b;
+  bool pad = false;
+  for (int s = 0; s < a.nd; ++s) {
+    const int p = widx[s] * a.ws[s] + nidx[s];
+    int r = 0;
+    if (a.sh[s] > 0) r = p < a.Sp[s] - a.ws[s] ? 0 : (p < a.Sp[s] - a.sh[s] ? 1 : 2);
+    rid = rid * 3 + r;
+    int src = p + a.sh[s];
+    if (src >= a.Sp[s]) src -= a.Sp[s];
+    if (src >= a.S[s]) pad = true;
+    row = row * a.S[s] + src;
+  }
+  return pad ? -1 : (int)row;
+}
+
+// load 8 bf16 (16 B) of token row `row` at channel offset col, or of the bias for padded tokens
+__device__ __forceinline__ bf16x8 win_load8(const WinArgs& a, int row, int col, bool exists) {
+  if (!exists) return bf16x8{};
+  if (row >= 0) return *(const bf16x8*)(a.qkv + (long long)row * 3 * a.C + col);
+  bf16x8 r;
+  if (a.qkv_bias) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = to_bf16(a.qkv_bias[col + j]);
+  } else {
+    r = bf16x8{};
+  }
+  return r;
+}
+
+__device__ __forceinline__ const bf16* out_row_ptr(const WinArgs& a, const bf16* base, int w, int n, int row) {
+  return base + (long long)(a.mode == 0 ? w * a.N + n : row) * a.C;
+}
+
+// log2-domain additive term for (q, key): rpb*log2e + (mask)
+__device__ __forceinline__ float win_mask_term(const WinArgs& a, int w, int q, int k, int rq, int rk) {
+  float t = 0.f;
+  if (a.mode == 1) {
+    if (a.masked && rq != rk) t = -100.f * WLOG2E;
+  } else if (a.mask) {
+    t = a.mask[((long long)(w % a.nW) * a.N + q) * a.N + k] * WLOG2E;
+  }
+  return t;
+}
+
+struct WinLds {
+  bf16* t0; bf16* t1; int* row; int* rid;
+};
+
+__device__ __forceinline__ void win_setup(const WinArgs& a, char* smem, WinLds& L, int w) {
+  L.t0 = (bf16*)smem;
+  L.t1 = L.t0 + a.Npad * WLD;
+  L.row = (int*)(L.t1 + a.Npad * WLD);
+  L.rid = L.row + a.Npad;
+  for (int n = threadIdx.x; n < a.Npad; n += blockDim.x) {
+    int rid = 0;
+    L.row[n] = n < a.N ? win_row(a, w, n, rid) : -2;
+    L.rid[n] = rid;
+  }
+  __syncthreads();
+}
+
+// stage two (Npad x 32) tiles of the window: channel offsets c0, c1 of the token rows (or the bias)
+__device__ __forceinline__ void win_stage(const WinArgs& a, const WinLds& L, int c0, int c1, bool second_is_out,
+                                          const bf16* obase, int w) {
+  for (int idx = threadIdx.x; idx < a.Npad * 4; idx += blockDim.x) {
+    const int n = idx >> 2, ch = idx & 3;
+    const int row = L.row[n];
+    const bool ex = n < a.N;
+    *(bf16x8*)(L.t0 + n * WLD + ch * 8) = win_load8(a, row, c0 + ch * 8, ex);
+    bf16x8 v;
+    if (second_is_out) {
+      v = (ex && row != -1) ? *(const bf16x8*)(out_row_ptr(a, obase, w, n, row) + c1 + ch * 8) : bf16x8{};
+    } else {
+      v = win_load8(a, row, c1 + ch * 8, ex);
+    }
+    *(bf16x8*)(L.t1 + n * WLD + ch * 8) = v;
+  }
+  __syncthreads();
+}
+
+// --------------------------------------------------------------------------------------------- forward
+__global__ __launch_bounds__(256) void win_attn_fwd_kernel(WinArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int w = blockIdx.x, hh = blockIdx.y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5;
+  WinLds L;
+  win_setup(a, smem, L, w);
+  win_stage(a, L, a.C + hh * WHD, 2 * a.C + hh * WHD, false, nullptr, w);   // K -> t0, V -> t1
+  const float c = a.c;
+  const float* rpbh = a.rpb + (long long)hh * a.N * a.Npad;
+  for (int qb = wave; qb < a.nqb; qb += 4) {
+    const int q = qb * 32 + (lane & 31);
+    const bool qv = q < a.N;
+    const int qrow = qv ? L.row[q] : -2;
+    const int rq = qv ? L.rid[q] : 0;
+    bf16x8 qf[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) qf[ks] = win_load8(a, qrow, hh * WHD + ks * 16 + 8 * half, qv);
+    f32x16 o = {};
+    float m = WNEG, l = 0.f;
+    const int qq = qv ? q : 0;
+    for (int kt = 0; kt < a.nkt; ++kt) {
+      f32x16 s = {};
+      s = mfma32(frag_row(L.t0, WLD, kt * 32, 0, lane), qf[0], s);
+      s = mfma32(frag_row(L.t0, WLD, kt * 32, 16, lane), qf[1], s);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int k0 = kt * 32 + 8 * g + 4 * half;
+        const f32x4 rb = *(const f32x4*)(rpbh + (long long)qq * a.Npad + k0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int i = 4 * g + j, k = k0 + j;
+          float v = fmaf(s[i], c, rb[j] * WLOG2E);
+          if (k < a.N) v += win_mask_term(a, w, qq, k, rq, L.rid[k]);
+          else v = WNEG;
+          s[i] = v;
+        }
+      }
+      float mx = s[0];
+#pragma unroll
+      for (int i = 1; i < 16; ++i) mx = fmaxf(mx, s[i]);
+      mx = wave_max_xor32(mx);
+      const float mn = fmaxf(m, mx);
+      const float al = exp2_fast(m - mn);
+      m = mn;
+      float ls = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { s[i] = exp2_fast(s[i] - mn); ls += s[i]; }
+      l = l * al + ls;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) o[i] *= al;
+      o = mfma32(frag_tr<0>(L.t1, WLD, kt * 32, 0, lane), pack8<0>(s), o);
+      o = mfma32(frag_tr<1>(L.t1, WLD, kt * 32, 0, lane), pack8<1>(s), o);
+    }
+    const float lt = wave_sum_xor32(l);
+    const float inv = 1.f / lt;
+    if (qv && qrow != -1) {
+      bf16* op = (bf16*)out_row_ptr(a, a.out, w, q, qrow) + hh * WHD;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = to_bf16(o[4 * g + j] * inv);
+        *(bf16x4*)(op + 8 * g + 4 * half) = v;
+      }
+    }
+    if (qv && half == 0) a.lse2[((long long)w * a.H + hh) * a.N + q] = m + __log2f(lt);
+  }
+}
+
+// -------------------------------------------------------------------------------------------- backward
+__global__ __launch_bounds__(256) void win_attn_bwd_kernel(WinArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int w = blockIdx.x, hh = blockIdx.y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5;
+  WinLds L;
+  win_setup(a, smem, L, w);
+  float* lse_l = (float*)(L.rid + a.Npad);
+  float* dl_l = lse_l + a.Npad;
+  const float c = a.c;
+  const float* rpbh = a.rpb + (long long)hh * a.N * a.Npad;
+  const float* lseg = a.lse2 + ((long long)w * a.H + hh) * a.N;
+
+  // ---------------- phase 1: K, V in LDS; query on the lane -> dQ, dS tiles, delta
+  win_stage(a, L, a.C + hh * WHD, 2 * a.C + hh * WHD, false, nullptr, w);
+  for (int qb = wave; qb < a.nqb; qb += 4) {
+    const int q = qb * 32 + (lane & 31);
+    const bool qv = q < a.N;
+    const int qrow = qv ? L.row[q] : -2;
+    const int rq = qv ? L.rid[q] : 0;
+    const int qq = qv ? q : 0;
+    bf16x8 qf[2], df[2];
+    float dsum = 0.f;
+    const bool has_out = qv && qrow != -1;   // padded queries are cropped: dO = 0
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      qf[ks] = win_load8(a, qrow, hh * WHD + ks * 16 + 8 * half, qv);
+      if (has_out) {
+        df[ks] = *(const bf16x8*)(out_row_ptr(a, a.dout, w, q, qrow) + hh * WHD + ks * 16 + 8 * half);
+        const bf16x8 ov = *(const bf16x8*)(out_row_ptr(a, a.o, w, q, qrow) + hh * WHD + ks * 16 + 8 * half);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dsum = fmaf(to_f32(df[ks][j]), to_f32(ov[j]), dsum);
+      } else {
+        df[ks] = bf16x8{};
+      }
+    }
+    const float delta = wave_sum_xor32(dsum);
+    const float lse = qv ? lseg[q] : 1.0e30f;
+    if (half == 0) {
+      lse_l[q] = lse;
+      dl_l[q] = delta;
+    }
+    f32x16 dq = {};
+    for (int kt = 0; kt < a.nkt; ++kt) {
+      f32x16 s = {}, dp = {};
+      s = mfma32(frag_row(L.t0, WLD, kt * 32, 0, lane), qf[0], s);
+      s = mfma32(frag_row(L.t0, WLD, kt * 32, 16, lane), qf[1], s);
+      dp = mfma32(frag_row(L.t1, WLD, kt * 32, 0, lane), df[0], dp);
+      dp = mfma32(frag_row(L.t1, WLD, kt * 32, 16, lane), df[1], dp);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int k0 = kt * 32 + 8 * g + 4 * half;
+        const f32x4 rb = *(const f32x4*)(rpbh + (long long)qq * a.Npad + k0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int i = 4 * g + j, k = k0 + j;
+          float p = 0.f;
+          if (k < a.N && qv) {
+            const float v = fmaf(s[i], c, rb[j] * WLOG2E) + win_mask_term(a, w, qq, k, rq, L.rid[k]);
+            p = exp2_fast(v - lse);
+          }
+          s[i] = p * (dp[i] - delta);   // dS^T (natural-log units)
+        }
+      }
+      if (a.dS) {
+        bf16* dst = a.dS + ((((long long)w * a.H + hh) * a.nqb + qb) * a.nkt + kt) * 1024 + lane * 16;
+        bf16x8 lo = pack8<0>(s), hi = pack8<1>(s);
+        *(bf16x8*)dst = lo;
+        *(bf16x8*)(dst + 8) = hi;
+      }
+      dq = mfma32(frag_tr<0>(L.t0, WLD, kt * 32, 0, lane), pack8<0>(s), dq);
+      dq = mfma32(frag_tr<1>(L.t0, WLD, kt * 32, 0, lane), pack8<1>(s), dq);
+    }
+    if (qv && qrow >= 0) {
+      bf16* dqp = a.dqkv + (long long)(a.mode == 0 ? w * a.N + q : qrow) * 3 * a.C + hh * WHD;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = to_bf16(dq[4 * g + j] * a.scale);
+        *(bf16x4*)(dqp + 8 * g + 4 * half) = v;
+      }
+    }
+  }
+  for (int n = a.N + threadIdx.x; n < a.Npad; n += blockDim.x) { lse_l[n] = 1.0e30f; dl_l[n] = 0.f; }
+  __syncthreads();
+
+  // ---------------- phase 2: Q, dO in LDS; key on the lane -> dK, dV
+  win_stage(a, L, hh * WHD, hh * WHD, true, a.dout, w);   // Q -> t0, dO -> t1
+  for (int kb = wave; kb < a.nqb; kb += 4) {
+    const int key = kb * 32 + (lane & 31);
+    const bool kv = key < a.N;
+    const int krow = kv ? L.row[key] : -2;
+    const int rk = kv ? L.rid[key] : 0;
+    const int kk = kv ? key : 0;
+    bf16x8 kf[2], vf[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      kf[ks] = win_load8(a, krow, a.C + hh * WHD + ks * 16 + 8 * half, kv);
+      vf[ks] = win_load8(a, krow, 2 * a.C + hh * WHD + ks * 16 + 8 * half, kv);
+    }
+    f32x16 dk = {}, dv = {};
+    for (int qt = 0; qt < a.nkt; ++qt) {
+      f32x16 s = {}, dp = {};
+      s = mfma32(frag_row(L.t0, WLD, qt * 32, 0, lane), kf[0], s);
+      s = mfma32(frag_row(L.t0, WLD, qt * 32, 16, lane), kf[1], s);
+      dp = mfma32(frag_row(L.t1, WLD, qt * 32, 0, lane), vf[0], dp);
+      dp = mfma32(frag_row(L.t1, WLD, qt * 32, 16, lane), vf[1], dp);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int q0 = qt * 32 + 8 * g + 4 * half;
+        const f32x4 lz = *(const f32x4*)(lse_l + q0);
+        const f32x4 dz = *(const f32x4*)(dl_l + q0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int i = 4 * g + j, q = q0 + j;
+          float p = 0.f;
+          if (kv && q < a.N) {
+            const float v = fmaf(s[i], c, rpbh[(long long)q * a.Npad + kk] * WLOG2E) +
+                            win_mask_term(a, w, q, kk, L.rid[q], rk);
+            p = exp2_fast(v - lz[j]);
+          }
+          s[i] = p;
+          dp[i] = p * (dp[i] - dz[j]);
+        }
+      }
+      dv = mfma32(frag_tr<0>(L.t1, WLD, qt * 32, 0, lane), pack8<0>(s), dv);
+      dv = mfma32(frag_tr<1>(L.t1, WLD, qt * 32, 0, lane), pack8<1>(s), dv);
+      dk = mfma32(frag_tr<0>(L.t0, WLD, qt * 32, 0, lane), pack8<0>(dp), dk);
+      dk = mfma32(frag_tr<1>(L.t0, WLD, qt * 32, 0, lane), pack8<1>(dp), dk);
+    }
+    if (kv) {
+      if (krow >= 0) {
+        bf16* base = a.dqkv + (long long)(a.mode == 0 ? w * a.N + key : krow) * 3 * a.C + hh * WHD;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          bf16x4 v0, v1;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v0[j] = to_bf16(dk[4 * g + j] * a.scale);
+            v1[j] = to_bf16(dv[4 * g + j]);
+          }
+          *(bf16x4*)(base + a.C + 8 * g + 4 * half) = v0;
+          *(bf16x4*)(base + 2 * a.C + 8 * g + 4 * half) = v1;
+        }
+      } else if (a.dbias_pad) {   // padded voxel: its k, v are the qkv bias
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int d = 8 * g + 4 * half + j;
+            atomicAdd(a.dbias_pad + a.C + hh * WHD + d, dk[4 * g + j] * a.scale);
+            atomicAdd(a.dbias_pad + 2 * a.C + hh * WHD + d, dv[4 * g + j]);
+          }
+      }
+    }
+  }
+}
+
+// d(rpb)[h][q][k] = sum_w dS[w][h][q][k]  from the (Bw, H, nqb, nkt, 64, 16) tile layout
+__global__ __launch_bounds__(256) void win_rpb_grad_kernel(WinArgs a) {
+  const long long per_w = (long long)a.H * a.nqb * a.nkt * 1024;
+  const long long e = blockIdx.x * 256LL + threadIdx.x;
+  if (e >= per_w) return;
+  float acc = 0.f;
+  for (int w = 0; w < a.Bw; ++w) acc += to_f32(a.dS[w * per_w + e]);
+  const int i = e & 15, lane = (e >> 4) & 63;
+  long long t = e >> 10;
+  const int kt = t % a.nkt; t /= a.nkt;
+  const int qb = t % a.nqb;
+  const int hh = t / a.nqb;
+  const int q = qb * 32 + (lane & 31);
+  const int k = kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+  if (q < a.N && k < a.N) a.drpb[((long long)hh * a.N + q) * a.N + k] = acc;
+}
+
+static int win_fill(WinArgs& a, const int* geo, float scale) {
+  // geo: [mode, nd, S0, S1, S2, ws0, ws1, ws2, sh0, sh1, sh2, Bw_or_B, nW, N, C, H]
+  a.mode = geo[0]; a.nd = geo[1];
+  for (int s = 0; s < 3; ++s) { a.S[s] = geo[2 + s]; a.ws[s] = geo[5 + s]; a.sh[s] = geo[8 + s]; }
+  a.N = geo[13]; a.C = geo[14]; a.H = geo[15];
+  LCI_CHECK(a.C == a.H * WHD, "window_attn: C %d != heads %d * 32", a.C, a.H);
+  LCI_CHECK(a.N > 0 && a.N <= WMAXN, "window_attn: N %d unsupported (<= %d)", a.N, WMAXN);
+  a.masked = 0;
+  if (a.mode == 1) {
+    int nW = 1, N = 1;
+    for (int s = 0; s < a.nd; ++s) {
+      LCI_CHECK(a.ws[s] > 0 && a.S[s] > 0 && a.sh[s] >= 0 && a.sh[s] < a.ws[s], "window_attn: bad geometry");
+      a.Sp[s] = (a.S[s] + a.ws[s] - 1) / a.ws[s] * a.ws[s];
+      a.nwin[s] = a.Sp[s] / a.ws[s];
+      nW *= a.nwin[s]; N *= a.ws[s];
+      if (a.sh[s] > 0) a.masked = 1;
+    }
+    LCI_CHECK(N == a.N, "window_attn: N %d != prod(window) %d", a.N, N);
+    a.nW = nW; a.Bw = geo[11] * nW;
+  } else {
+    a.Bw = geo[11]; a.nW = geo[12] > 0 ? geo[12] : 1;
+  }
+  a.Npad = (a.N + 31) / 32 * 32;
+  a.nqb = a.nkt = a.Npad / 32;
+  a.scale = scale; a.c = scale * WLOG2E;
+  return 0;
+}
+
+static size_t win_lds(const WinArgs& a, bool bwd) {
+  return (size_t)a.Npad * WLD * 2 * 2 + (size_t)a.Npad * 4 * 2 + (bwd ? (size_t)a.Npad * 4 * 2 : 0);
+}
+
+}  // namespace lci
+
+using namespace lci;
+
+extern "C" int lci_window_attn_fwd(const void* qkv, const float* qkv_bias, const float* rpb, const float* mask,
+                                   void* out, float* lse2, const int* geo, float scale, void* stream) {
+  WinArgs a{};
+  if (win_fill(a, geo, scale)) return 1;
+  a.qkv = (const bf16*)qkv; a.qkv_bias = qkv_bias; a.rpb = rpb; a.mask = mask; a.out = (bf16*)out; a.lse2 = lse2;
+  (void)hipFuncSetAttribute((const void*)win_attn_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipLaunchKernelGGL(win_attn_fwd_kernel, dim3(a.Bw, a.H), dim3(256), win_lds(a, false), (hipStream_t)stream, a);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+
+// dbias_pad (3C) accumulated (caller zeroes); dS tiles (Bw*H*nqb*nkt*1024 bf16) optional workspace;
+// drpb (H, N, N) f32 written when dS and drpb are given.
+extern "C" int lci_window_attn_bwd(const void* qkv, const float* qkv_bias, const float* rpb, const float* mask,
+                                   const void* out, const void* dout, const float* lse2, void* dqkv, float* dbias_pad,
+                                   void* dS, float* drpb, const int* geo, float scale, void* stream) {
+  WinArgs a{};
+  if (win_fill(a, geo, scale)) return 1;
+  a.qkv = (const bf16*)qkv; a.qkv_bias = qkv_bias; a.rpb = rpb; a.mask = mask; a.o = (const bf16*)out;
+  a.dout = (const bf16*)dout; a.lse2 = (float*)lse2; a.dqkv = (bf16*)dqkv; a.dbias_pad = dbias_pad;
+  a.dS = (bf16*)dS; a.drpb = drpb;
+  hipStream_t s = (hipStream_t)stream;
+  (void)hipFuncSetAttribute((const void*)win_attn_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipLaunchKernelGGL(win_attn_bwd_kernel, dim3(a.Bw, a.H), dim3(256), win_lds(a, true), s, a);
+  LCI_LAUNCH_CHECK();
+  if (dS && drpb) {
+    const long long per_w = (long long)a.H * a.nqb * a.nkt * 1024;
+    hipLaunchKernelGGL(win_rpb_grad_kernel, dim3((unsigned)((per_w + 255) / 256)), dim3(256), 0, s, a);
+    LCI_LAUNCH_CHECK();
+  }
+  return 0;
+}
+
+extern "C" long long lci_window_dS_elems(const int* geo) {
+  WinArgs a{};
+  if (win_fill(a, geo, 1.f)) return -1;
+  return (long long)a.Bw * a.H * a.nqb * a.nkt * 1024;
+}

@@ -334,3 +334,103 @@ def selective_scan_cl(u, delta, A, Bm, Cm, D, delta_bias, yz):
     if yz.dtype != dt:
         raise _lib.LciError("selective_scan: yz dtype must match u")
     return _SelectiveScanCL.apply(u, delta, A, Bm, Cm, D, delta_bias, yz)
+
+
+# ------------------------------------------------------------------------------------ window attention
+def _i32(vals):
+    import ctypes
+    return (ctypes.c_int * len(vals))(*[int(v) for v in vals])
+
+
+class _WindowAttention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, bias, rpb_p, mask, geo, scale):
+        C = qkv.shape[-1] // 3
+        out = torch.empty(*qkv.shape[:-1], C, device=qkv.device, dtype=torch.bfloat16)
+        g = _i32(geo)
+        N, H = geo[13], geo[15]
+        Bw = geo[11] * (geo[12] if geo[0] == 1 else 1)
+        lse2 = torch.empty(Bw, H, N, device=qkv.device, dtype=torch.float32)
+        bf = bias.float().contiguous() if bias is not None else None
+        mk = mask.float().contiguous() if mask is not None else None
+        KernelTimer.run("window_attn_fwd", 4.0 * Bw * H * N * N * 32, qkv, lambda: _lib.call(
+            "lci_window_attn_fwd", qkv.data_ptr(), _lib.ptr(bf), rpb_p.data_ptr(), _lib.ptr(mk), out.data_ptr(),
+            lse2.data_ptr(), g, float(scale), _lib.stream_of(qkv)))
+        ctx.save_for_backward(qkv, bf, rpb_p, mk, out, lse2)
+        ctx.geo, ctx.scale, ctx.has_bias = geo, scale, bias is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, bf, rpb_p, mk, out, lse2 = ctx.saved_tensors
+        geo, scale = ctx.geo, ctx.scale
+        g = _i32(geo)
+        N, C, H = geo[13], geo[14], geo[15]
+        Bw = lse2.shape[0]
+        dout = dout.to(torch.bfloat16).contiguous()
+        dqkv = torch.empty_like(qkv)
+        f32 = dict(device=qkv.device, dtype=torch.float32)
+        dbias = torch.zeros(3 * C, **f32) if (ctx.has_bias and ctx.needs_input_grad[1]) else None
+        want_rpb = ctx.needs_input_grad[2]
+        dS = drpb = None
+        if want_rpb:
+            n_el = _lib.load().lci_window_dS_elems(g)
+            dS = torch.empty(int(n_el), device=qkv.device, dtype=torch.bfloat16)
+            drpb = torch.empty(H, N, N, **f32)
+        KernelTimer.run("window_attn_bwd", 8.0 * Bw * H * N * N * 32, qkv, lambda: _lib.call(
+            "lci_window_attn_bwd", qkv.data_ptr(), _lib.ptr(bf), rpb_p.data_ptr(), _lib.ptr(mk), out.data_ptr(),
+            dout.data_ptr(), lse2.data_ptr(), dqkv.data_ptr(), _lib.ptr(dbias), _lib.ptr(dS), _lib.ptr(drpb), g,
+            float(scale), _lib.stream_of(qkv)))
+        drpb_p = None
+        if want_rpb:
+            drpb_p = torch.nn.functional.pad(drpb, (0, rpb_p.shape[-1] - N))
+        return dqkv, dbias, drpb_p, None, None, None
+
+
+def _pad_rpb(rpb):
+    H, N, _ = rpb.shape
+    npad = -(-N // 32) * 32
+    return torch.nn.functional.pad(rpb.float(), (0, npad - N)).contiguous()
+
+
+def _win_prep(qkv):
+    dt = qkv.dtype
+    q = qkv if dt == torch.bfloat16 else qkv.to(torch.bfloat16)
+    return q.contiguous(), dt
+
+
+def window_attention_grid(qkv, bias, rpb, num_heads, scale, window_size, shift_size):
+    """Fused pad + roll(-shift) + window_partition + window attention + window_reverse + roll(+shift) + crop.
+
+    qkv: (B, S0, S1[, S2], 3C) = qkv Linear of the LN1 output on the un-padded channels-last grid;
+    bias: the qkv Linear bias (the q/k/v of padded voxels) or None; rpb: (H, N, N) = table[index].
+    Returns (B, S0, S1[, S2], C) — the reference's forward_part1 output before proj (backbone_swin.py:435-487).
+    """
+    _lib.require_gpu(qkv.contiguous())
+    q, dt = _win_prep(qkv)
+    nd = q.dim() - 2
+    S = list(q.shape[1:-1])
+    C = q.shape[-1] // 3
+    N = 1
+    for w in window_size:
+        N *= w
+    ws3 = list(window_size) + [1] * (3 - nd)
+    sh3 = list(shift_size) + [0] * (3 - nd)
+    S3 = S + [1] * (3 - nd)
+    nW = 1
+    for s, w in zip(S, window_size):
+        nW *= -(-s // w)
+    geo = (1, nd, *S3, *ws3, *sh3, q.shape[0], nW, N, C, num_heads)
+    o = _WindowAttention.apply(q, bias, _pad_rpb(rpb), None, geo, scale)
+    return o if dt == torch.bfloat16 else o.to(dt)
+
+
+def window_attention(qkv, rpb, mask, num_heads, scale):
+    """Pre-partitioned windows (WindowAttention.forward signature): qkv (Bw, N, 3C), mask (nW, N, N) or None."""
+    _lib.require_gpu(qkv.contiguous())
+    q, dt = _win_prep(qkv)
+    Bw, N, C3 = q.shape
+    nW = mask.shape[0] if mask is not None else 1
+    geo = (0, 0, 1, 1, 1, 1, 1, 1, 0, 0, 0, Bw, nW, N, C3 // 3, num_heads)
+    o = _WindowAttention.apply(q, None, _pad_rpb(rpb), mask, geo, scale)
+    return o if dt == torch.bfloat16 else o.to(dt)
