@@ -1,0 +1,542 @@
+// Hyena long convolution for gfx950.
+//
+// Replaces fftconv_ref (hyena.py:32-51, gelu=False, no dropout):
+//     y = irfft(rfft(u, n=2L) * rfft(k, n=2L) / 2L, n=2L, norm="forward")[..., :L] + u * D
+// i.e. the causal linear convolution y[t] = sum_{s<=t} k[t-s] u[s] + D u[t], evaluated exactly (fp32) with
+// an FFT of size n = pow2 >= 2L. Two rows that share a filter are packed as one complex sequence
+// z = u_a + i u_b (k is real, so conv(z, k) = conv(u_a, k) + i conv(u_b, k)).
+//
+// Four-step FFT, n = n1 * n2, index m = a*n2 + c, frequency f = k1 + n1*k2:
+//   col pass   (per pair, G columns c):  T[k1][c] = FFT_n1 over a of z[a*n2+c], times W_n^(c k1)
+//   row pass   (per filter j, row k1, looping over that filter's pairs): X[k1][k2] = FFT_n2 over c;
+//              times K_j[k1][k2] (or conj(K_j) for the adjoint); inverse FFT_n2; conj twiddle applied in
+//              the inverse column pass. The backward also accumulates sum_pairs conj(X_vg) X_dy for dk.
+//   inverse col pass: IFFT_n1 over k1 -> z[m]; Re -> row a, Im -> row b, + D * u.
+// Sub-FFTs are radix-2 Stockham in LDS (ping-pong); twiddles come from one W_n table built in f64.
+// hyena_pre / hyena_post: the causal depthwise short conv (k = short_filter_order) and gating around the
+// long conv, reading/writing the channels-last (B, L, C) tensors of in_proj / out_proj directly and
+// transposing through LDS to the channel-major rows the FFT wants.
+#include "common.hpp"
+
+namespace lci {
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x2 cmul(f32x2 a, f32x2 b) { return f32x2{a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
+__device__ __forceinline__ f32x2 cmulc(f32x2 a, f32x2 b) {  // a * conj(b)
+  return f32x2{a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y};
+}
+__device__ __forceinline__ f32x2 conj2(f32x2 a) { return f32x2{a.x, -a.y}; }
+
+struct FftArgs {
+  const float* src; const float* src2;  // rows (R_outer, C, L) f32 channel-major; src2: second input (vg) for dk
+  float* dst;                           // output rows
+  const f32x2* tw;                      // W_n^t, t < n
+  f32x2* S; f32x2* S2;                  // scratch (npairs_total, n) complex
+  f32x2* K;                             // filter spectra (C, n) in [k1][k2] layout (already / n)
+  f32x2* SK;                            // dk scratch (C, n)
+  const float* Dv;                      // (C) or null
+  float* dk; float* dD;                 // (C, L) and (C) outputs (bwd)
+  int L, C, R, P;                       // row length, filters, outer rows per filter, pairs per filter
+  int n, n1, n2, ln1, ln2, G;
+  int mode;                             // row pass: 0 = spectrum of filters, 1 = fwd conv, 2 = bwd (conj + dk)
+  int single;                           // col passes: 1 = the source is the filter (C rows, no pairing)
+};
+
+// radix-2 Stockham FFT of `cnt` sequences of length N (=2^lN) stored [seq][N] in x; result back in x
+// (ping-pong through y). sign -1: forward (W = exp(-2 pi i/N)), +1: inverse (unnormalised).
+__device__ void lds_fft(f32x2* x, f32x2* y, int N, int lN, int cnt, const f32x2* tw, int n, bool inverse) {
+  const int half = N >> 1;
+  const int total = cnt * half;
+  for (int s = 0; s < lN; ++s) {
+    const int Ns = 1 << s;
+    const int tstep = n / (2 * Ns);
+    for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
+      const int sq = idx / half, j = idx - sq * half;
+      const int k = j & (Ns - 1);
+      f32x2 u0 = x[sq * N + j], u1 = x[sq * N + j + half];
+      f32x2 w = tw[k * tstep];
+      if (inverse) w.y = -w.y;
+      u1 = cmul(u1, w);
+      const int d = ((j - k) << 1) + k;
+      y[sq * N + d] = u0 + u1;
+      y[sq * N + d + Ns] = u0 - u1;
+    }
+    __syncthreads();
+    f32x2* t = x; x = y; y = t;
+  }
+  if (lN & 1) {  // result is in y (the original x buffer was swapped an odd number of times): copy back
+    for (int idx = threadIdx.x; idx < cnt * N; idx += blockDim.x) y[idx] = x[idx];
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ int pair_row(const FftArgs& a, int j, int p, int which) {
+  const int ro = 2 * p + which;
+  return ro < a.R ? ro * a.C + j : -1;
+}
+
+// ------------------------------------------------------------------------------------- forward columns
+// grid: (n2 / G, npairs_total or C); block 256. LDS: 2 * G * n1 complex.
+__global__ __launch_bounds__(256) void fft_col_fwd_kernel(FftArgs a) {
+  extern __shared__ __attribute__((aligned(16))) f32x2 lds[];
+  f32x2* x = lds;
+  f32x2* y = lds + a.G * a.n1;
+  const int c0 = blockIdx.x * a.G;
+  const int pid = blockIdx.y;           // pair id (j * P + p) or filter id when single
+  int r0, r1;
+  if (a.single) { r0 = pid; r1 = -1; }
+  else {
+    const int j = pid / a.P, p = pid % a.P;
+    r0 = pair_row(a, j, p, 0);
+    r1 = pair_row(a, j, p, 1);
+  }
+  const float* s = a.src;
+  for (int idx = threadIdx.x; idx < a.G * a.n1; idx += blockDim.x) {
+    const int g = idx % a.G, ai = idx / a.G;
+    const int m = ai * a.n2 + c0 + g;
+    f32x2 v = {0.f, 0.f};
+    if (m < a.L) {
+      v.x = s[(long long)r0 * a.L + m];
+      if (r1 >= 0) v.y = s[(long long)r1 * a.L + m];
+    }
+    x[g * a.n1 + ai] = v;
+  }
+  __syncthreads();
+  lds_fft(x, y, a.n1, a.ln1, a.G, a.tw, a.n, false);
+  f32x2* S = (a.single ? a.SK : a.S) + (long long)pid * a.n;
+  for (int idx = threadIdx.x; idx < a.G * a.n1; idx += blockDim.x) {
+    const int g = idx % a.G, k1 = idx / a.G;
+    const int c = c0 + g;
+    const f32x2 w = a.tw[((long long)c * k1) & (a.n - 1)];
+    S[(long long)k1 * a.n2 + c] = cmul(x[g * a.n1 + k1], w);
+  }
+}
+
+// ------------------------------------------------------------------------------------------ row pass
+// grid: (n1, C); block 256. One (filter j, row k1); loops over the filter's pairs.
+// LDS: x, y (n2 complex each) + kr (n2) + acc (n2).
+__global__ __launch_bounds__(256) void fft_row_kernel(FftArgs a) {
+  extern __shared__ __attribute__((aligned(16))) f32x2 lds[];
+  const int N = a.n2;
+  f32x2* x = lds;
+  f32x2* y = x + N;
+  f32x2* kr = y + N;
+  f32x2* acc = kr + N;
+  f32x2* x2 = acc + N;
+  f32x2* y2 = x2 + N;
+  const int k1 = blockIdx.x, j = blockIdx.y;
+  const float invn = 1.f / (float)a.n;
+  if (a.mode == 0) {  // filter spectrum: K_j[k1][:] = FFT_n2(T[k1][:]) / n
+    f32x2* S = a.SK + (long long)j * a.n + (long long)k1 * N;
+    for (int i = threadIdx.x; i < N; i += blockDim.x) x[i] = S[i];
+    __syncthreads();
+    lds_fft(x, y, N, a.ln2, 1, a.tw, a.n, false);
+    f32x2* K = a.K + (long long)j * a.n + (long long)k1 * N;
+    for (int i = threadIdx.x; i < N; i += blockDim.x) K[i] = x[i] * invn;
+    return;
+  }
+  const f32x2* K = a.K + (long long)j * a.n + (long long)k1 * N;
+  for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    kr[i] = K[i];
+    acc[i] = f32x2{0.f, 0.f};
+  }
+  __syncthreads();
+  for (int p = 0; p < a.P; ++p) {
+    f32x2* S = a.S + ((long long)j * a.P + p) * a.n + (long long)k1 * N;
+    for (int i = threadIdx.x; i < N; i += blockDim.x) x[i] = S[i];
+    if (a.mode == 2 && a.SK) {
+      const f32x2* S2 = a.S2 + ((long long)j * a.P + p) * a.n + (long long)k1 * N;
+      for (int i = threadIdx.x; i < N; i += blockDim.x) x2[i] = S2[i];
+    }
+    __syncthreads();
+    lds_fft(x, y, N, a.ln2, 1, a.tw, a.n, false);
+    if (a.mode == 2 && a.SK) {
+      lds_fft(x2, y2, N, a.ln2, 1, a.tw, a.n, false);
+      for (int i = threadIdx.x; i < N; i += blockDim.x) acc[i] += cmulc(x[i], x2[i]);  // X_dy conj(X_vg)
+    }
+    for (int i = threadIdx.x; i < N; i += blockDim.x) x[i] = (a.mode == 1) ? cmul(x[i], kr[i]) : cmulc(x[i], kr[i]);
+    __syncthreads();
+    lds_fft(x, y, N, a.ln2, 1, a.tw, a.n, true);
+    for (int i = threadIdx.x; i < N; i += blockDim.x) S[i] = x[i];
+    __syncthreads();
+  }
+  if (a.mode == 2 && a.SK) {  // dk spectrum row (unnormalised correlation): inverse row FFT, store
+    for (int i = threadIdx.x; i < N; i += blockDim.x) x[i] = acc[i];
+    __syncthreads();
+    lds_fft(x, y, N, a.ln2, 1, a.tw, a.n, true);
+    f32x2* SK = a.SK + (long long)j * a.n + (long long)k1 * N;
+    for (int i = threadIdx.x; i < N; i += blockDim.x) SK[i] = x[i] * invn;   // correlation needs 1/n
+  }
+}
+
+// ---------------------------------------------------------------------------------- inverse columns
+// grid: (n2 / G, npairs_total or C); out rows (+ D * src); single: dk[j][m] = Re(...) for the filter.
+__global__ __launch_bounds__(256) void fft_col_inv_kernel(FftArgs a) {
+  extern __shared__ __attribute__((aligned(16))) f32x2 lds[];
+  f32x2* x = lds;
+  f32x2* y = lds + a.G * a.n1;
+  const int c0 = blockIdx.x * a.G;
+  const int pid = blockIdx.y;
+  const f32x2* S = (a.single ? a.SK : a.S) + (long long)pid * a.n;
+  for (int idx = threadIdx.x; idx < a.G * a.n1; idx += blockDim.x) {
+    const int g = idx % a.G, k1 = idx / a.G;
+    const int c = c0 + g;
+    f32x2 w = a.tw[((long long)c * k1) & (a.n - 1)];
+    w.y = -w.y;
+    x[g * a.n1 + k1] = cmul(S[(long long)k1 * a.n2 + c], w);
+  }
+  __syncthreads();
+  lds_fft(x, y, a.n1, a.ln1, a.G, a.tw, a.n, true);
+  if (a.single) {
+    for (int idx = threadIdx.x; idx < a.G * a.n1; idx += blockDim.x) {
+      const int g = idx % a.G, ai = idx / a.G;
+      const int m = ai * a.n2 + c0 + g;
+      if (m < a.L) a.dk[(long long)pid * a.L + m] = x[g * a.n1 + ai].x;
+    }
+    return;
+  }
+  const int j = pid / a.P, p = pid % a.P;
+  const int r0 = pair_row(a, j, p, 0), r1 = pair_row(a, j, p, 1);
+  const float Dj = a.Dv ? a.Dv[j] : 0.f;
+  for (int idx = threadIdx.x; idx < a.G * a.n1; idx += blockDim.x) {
+    const int g = idx % a.G, ai = idx / a.G;
+    const int m = ai * a.n2 + c0 + g;
+    if (m < a.L) {
+      const f32x2 v = x[g * a.n1 + ai];
+      a.dst[(long long)r0 * a.L + m] = fmaf(Dj, a.src[(long long)r0 * a.L + m], v.x);
+      if (r1 >= 0) a.dst[(long long)r1 * a.L + m] = fmaf(Dj, a.src[(long long)r1 * a.L + m], v.y);
+    }
+  }
+}
+
+// dD[j] += sum_rows sum_t a[row][t] * b[row][t] over rows of filter j (block partial + atomic)
+__global__ __launch_bounds__(256) void row_dot_kernel(const float* x, const float* y, float* out, int L, int C,
+                                                      int R) {
+  __shared__ float red[256];
+  const int row = blockIdx.x;   // r_outer * C + j
+  const int j = row % C;
+  float acc = 0.f;
+  for (int t = threadIdx.x; t < L; t += 256) acc = fmaf(x[(long long)row * L + t], y[(long long)row * L + t], acc);
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) atomicAdd(out + j, red[0]);
+}
+
+__global__ void twiddle_kernel(f32x2* tw, int n) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= n) return;
+  double s, c;
+  sincospi(-2.0 * (double)t / (double)n, &s, &c);
+  tw[t] = f32x2{(float)c, (float)s};
+}
+
+// ------------------------------------------------------------------------------- short conv + gating
+// z (BB, L, 3D) channels-last; weight (3D, K) f32; bias (3D). For output channel ch = h*hd + jj of D:
+// x1 = conv[h*3hd + jj], x2 = conv[h*3hd + hd + jj], v = conv[h*3hd + 2hd + jj] (hyena.py:321-330).
+// Causal: conv_c(t) = bias[c] + sum_i w[c][i] z[t + i - (K-1)][c].
+struct GateArgs {
+  const void* z; const float* w; const float* bias;
+  float* vg;            // (BB, D, L) f32 channel-major: v * x1
+  void* x2;             // (BB, L, D) channels-last (z dtype)
+  const float* y;       // (BB, D, L) f32 long-conv output (post)
+  void* out;            // (BB, L, D) channels-last (z dtype) = y * x2 (post)
+  const void* dout;     // post bwd: (BB, L, D)
+  float* dy;            // post bwd: (BB, D, L) f32 = dout * x2
+  void* dx2;            // post bwd: (BB, L, D) f32 = dout * y
+  const float* dvg;     // pre bwd: (BB, D, L)
+  const void* gx2;      // pre bwd: dL/dx2 (BB, L, D) (f32)
+  void* dz;             // pre bwd: (BB, L, 3D)
+  float* dw; float* db; // pre bwd: (3D, K), (3D) accumulated
+  int BB, L, D, H, hd, K;
+};
+
+template <typename T>
+__device__ __forceinline__ float conv_at(const GateArgs& a, const T* zb, int t, int c) {
+  float acc = a.bias ? a.bias[c] : 0.f;
+  for (int i = 0; i < a.K; ++i) {
+    const int s = t + i - (a.K - 1);
+    if (s >= 0) acc = fmaf(a.w[c * a.K + i], (float)zb[(long long)s * 3 * a.D + c], acc);
+  }
+  return acc;
+}
+
+// tile: 64 tokens x 64 output channels; grid (ceil(L/64), ceil(D/64), BB); block 256
+template <typename T>
+__global__ __launch_bounds__(256) void hyena_pre_fwd_kernel(GateArgs a) {
+  __shared__ float tile[64][65];
+  const int t0 = blockIdx.x * 64, ch0 = blockIdx.y * 64, bb = blockIdx.z;
+  const T* zb = (const T*)a.z + (long long)bb * a.L * 3 * a.D;
+  for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
+    const int cl = idx & 63, tl = idx >> 6;
+    const int t = t0 + tl, ch = ch0 + cl;
+    float vg = 0.f;
+    if (t < a.L && ch < a.D) {
+      const int h = ch / a.hd, jj = ch % a.hd;
+      const int base = h * 3 * a.hd + jj;
+      const float x1 = conv_at(a, zb, t, base);
+      const float x2 = conv_at(a, zb, t, base + a.hd);
+      const float v = conv_at(a, zb, t, base + 2 * a.hd);
+      vg = v * x1;
+      ((T*)a.x2)[((long long)bb * a.L + t) * a.D + ch] = (T)x2;
+    }
+    tile[cl][tl] = vg;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
+    const int tl = idx & 63, cl = idx >> 6;
+    const int t = t0 + tl, ch = ch0 + cl;
+    if (t < a.L && ch < a.D) a.vg[((long long)bb * a.D + ch) * a.L + t] = tile[cl][tl];
+  }
+}
+
+// out[bb, t, ch] = y[bb, ch, t] * x2[bb, t, ch]
+template <typename T>
+__global__ __launch_bounds__(256) void hyena_post_fwd_kernel(GateArgs a) {
+  __shared__ float tile[64][65];
+  const int t0 = blockIdx.x * 64, ch0 = blockIdx.y * 64, bb = blockIdx.z;
+  for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
+    const int tl = idx & 63, cl = idx >> 6;
+    const int t = t0 + tl, ch = ch0 + cl;
+    tile[cl][tl] = (t < a.L && ch < a.D) ? a.y[((long long)bb * a.D + ch) * a.L + t] : 0.f;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
+    const int cl = idx & 63, tl = idx >> 6;
+    const int t = t0 + tl, ch = ch0 + cl;
+    if (t < a.L && ch < a.D) {
+      const long long o = ((long long)bb * a.L + t) * a.D + ch;
+      ((T*)a.out)[o] = (T)(tile[cl][tl] * (float)((const T*)a.x2)[o]);
+    }
+  }
+}
+
+// dy[bb, ch, t] = dout * x2 ; dx2[bb, t, ch] = dout * y
+template <typename T>
+__global__ __launch_bounds__(256) void hyena_post_bwd_kernel(GateArgs a) {
+  __shared__ float ty[64][65];
+  __shared__ float tg[64][65];
+  const int t0 = blockIdx.x * 64, ch0 = blockIdx.y * 64, bb = blockIdx.z;
+  for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
+    const int tl = idx & 63, cl = idx >> 6;
+    const int t = t0 + tl, ch = ch0 + cl;
+    ty[cl][tl] = (t < a.L && ch < a.D) ? a.y[((long long)bb * a.D + ch) * a.L + t] : 0.f;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
+    const int cl = idx & 63, tl = idx >> 6;
+    const int t = t0 + tl, ch = ch0 + cl;
+    float g = 0.f;
+    if (t < a.L && ch < a.D) {
+      const long long o = ((long long)bb * a.L + t) * a.D + ch;
+      const float go = (float)((const T*)a.dout)[o];
+      g = go * (float)((const T*)a.x2)[o];
+      ((float*)a.dx2)[o] = go * ty[cl][tl];
+    }
+    tg[cl][tl] = g;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
+    const int tl = idx & 63, cl = idx >> 6;
+    const int t = t0 + tl, ch = ch0 + cl;
+    if (t < a.L && ch < a.D) a.dy[((long long)bb * a.D + ch) * a.L + t] = tg[cl][tl];
+  }
+}
+
+// pre bwd: per (token tile, channel tile): dconv for the 3 groups, then the causal conv transpose.
+// dconv_x1 = dvg * v, dconv_v = dvg * x1, dconv_x2 = gx2. dz[s][c] = sum_i w[c][i] dconv_c[s - i + K - 1].
+// One thread per (channel of 3D, token run of 64): sliding window, register partials for dw/db.
+template <typename T>
+__global__ __launch_bounds__(256) void hyena_pre_bwd_kernel(GateArgs a) {
+  const int c = blockIdx.y * 256 + threadIdx.x;   // channel of 3D
+  if (c >= 3 * a.D) return;
+  const int bb = blockIdx.z, t0 = blockIdx.x * 64, t1 = min(a.L, t0 + 64);
+  const int h = c / (3 * a.hd), rem = c % (3 * a.hd), part = rem / a.hd, jj = rem % a.hd;
+  const int ch = h * a.hd + jj;                   // output channel of D
+  const int base = h * 3 * a.hd + jj;
+  const T* zb = (const T*)a.z + (long long)bb * a.L * 3 * a.D;
+  const float* dvg = a.dvg + ((long long)bb * a.D + ch) * a.L;
+  auto dconv = [&](int t) -> float {
+    if (t < 0 || t >= a.L) return 0.f;
+    if (part == 1) return (float)((const float*)a.gx2)[((long long)bb * a.L + t) * a.D + ch];
+    const float other = conv_at(a, zb, t, part == 0 ? base + 2 * a.hd : base);
+    return dvg[t] * other;
+  };
+  float dwl[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float dbl = 0.f;
+  const int K = a.K;
+  for (int s = t0; s < t1; ++s) {
+    // dz[s] = sum_i w[i] dconv[s - i + K - 1]
+    float acc = 0.f;
+    for (int i = 0; i < K; ++i) acc = fmaf(a.w[c * K + i], dconv(s - i + K - 1), acc);
+    ((T*)a.dz)[((long long)bb * a.L + s) * 3 * a.D + c] = (T)acc;
+    // dw[i] += dconv[s] * z[s + i - (K-1)]
+    const float g = dconv(s);
+    dbl += g;
+    for (int i = 0; i < K && i < 8; ++i) {
+      const int q = s + i - (K - 1);
+      if (q >= 0) dwl[i] = fmaf(g, (float)zb[(long long)q * 3 * a.D + c], dwl[i]);
+    }
+  }
+  for (int i = 0; i < K && i < 8; ++i) atomicAdd(a.dw + c * K + i, dwl[i]);
+  if (a.db) atomicAdd(a.db + c, dbl);
+}
+
+static int fft_plan(FftArgs& a, int L) {
+  LCI_CHECK(L > 0 && L <= (1 << 17), "fftconv: L %d unsupported (<= 131072)", L);
+  int e = 1;
+  while ((1 << e) < 2 * L) ++e;
+  a.n = 1 << e;
+  a.ln1 = e < 8 ? e : 8;
+  a.ln2 = e - a.ln1;
+  if (a.ln2 == 0) { a.ln1 = e - 1; a.ln2 = 1; }
+  a.n1 = 1 << a.ln1; a.n2 = 1 << a.ln2;
+  a.G = a.n2 < 16 ? a.n2 : 16;
+  a.L = L;
+  return 0;
+}
+
+}  // namespace lci
+
+using namespace lci;
+
+extern "C" long long lci_fft_size(int L) {
+  FftArgs a{};
+  if (fft_plan(a, L)) return -1;
+  return a.n;
+}
+
+// tw: n complex (f32x2) workspace filled here.
+extern "C" int lci_fft_twiddles(void* tw, int n, void* stream) {
+  hipLaunchKernelGGL(twiddle_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, (f32x2*)tw, n);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+
+static int launch_col(FftArgs& a, bool inv, int nblk_y, hipStream_t s) {
+  const size_t sh = (size_t)2 * a.G * a.n1 * sizeof(f32x2);
+  dim3 grid(a.n2 / a.G, nblk_y);
+  if (inv) hipLaunchKernelGGL(fft_col_inv_kernel, grid, dim3(256), sh, s, a);
+  else hipLaunchKernelGGL(fft_col_fwd_kernel, grid, dim3(256), sh, s, a);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+
+static int launch_row(FftArgs& a, hipStream_t s) {
+  const size_t sh = (size_t)6 * a.n2 * sizeof(f32x2);
+  hipLaunchKernelGGL(fft_row_kernel, dim3(a.n1, a.C), dim3(256), sh, s, a);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+
+// Filter spectra: k (C, L) f32 -> K (C, n) complex in [k1][k2] layout, scaled by 1/n. SK: (C, n) scratch.
+extern "C" int lci_fftconv_spectrum(const float* k, void* K, void* SK, const void* tw, int C, int L, void* stream) {
+  FftArgs a{};
+  if (fft_plan(a, L)) return 1;
+  a.src = k; a.K = (f32x2*)K; a.SK = (f32x2*)SK; a.tw = (const f32x2*)tw; a.C = C; a.single = 1; a.mode = 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (launch_col(a, false, C, s)) return 3;
+  if (launch_row(a, s)) return 3;
+  return 0;
+}
+
+// y = causal_conv(u, k) + D u for rows (R, C, L) f32; filter j = row % C. S: (C * ceil(R/2), n) scratch.
+extern "C" int lci_fftconv_fwd(const float* u, const void* K, const float* Dv, float* y, void* S, const void* tw,
+                               int R, int C, int L, void* stream) {
+  FftArgs a{};
+  if (fft_plan(a, L)) return 1;
+  a.src = u; a.dst = y; a.K = (f32x2*)K; a.S = (f32x2*)S; a.tw = (const f32x2*)tw; a.Dv = Dv;
+  a.R = R; a.C = C; a.P = (R + 1) / 2; a.single = 0; a.mode = 1;
+  hipStream_t s = (hipStream_t)stream;
+  if (launch_col(a, false, C * a.P, s)) return 3;
+  if (launch_row(a, s)) return 3;
+  if (launch_col(a, true, C * a.P, s)) return 3;
+  return 0;
+}
+
+// Adjoint: du = corr(dy, k) + D dy; dk (C, L) = sum_rows corr(dy, u) (overwritten); dD (C) accumulated.
+// S, S2: (C * ceil(R/2), n) scratch; SK: (C, n) scratch.
+extern "C" int lci_fftconv_bwd(const float* dy, const float* u, const void* K, const float* Dv, float* du, float* dk,
+                               float* dD, void* S, void* S2, void* SK, const void* tw, int R, int C, int L,
+                               void* stream) {
+  FftArgs a{};
+  if (fft_plan(a, L)) return 1;
+  a.tw = (const f32x2*)tw; a.K = (f32x2*)K; a.S = (f32x2*)S; a.S2 = (f32x2*)S2; a.SK = dk ? (f32x2*)SK : nullptr;
+  a.R = R; a.C = C; a.P = (R + 1) / 2; a.Dv = Dv; a.dk = dk;
+  hipStream_t s = (hipStream_t)stream;
+  a.single = 0;
+  a.src = dy;
+  if (launch_col(a, false, C * a.P, s)) return 3;            // S <- col FFT of dy pairs
+  if (dk) {
+    FftArgs b = a;
+    b.S = (f32x2*)S2; b.src = u;
+    if (launch_col(b, false, C * a.P, s)) return 3;          // S2 <- col FFT of u pairs
+  }
+  a.mode = 2;
+  if (launch_row(a, s)) return 3;                            // S <- conj(K) products, SK <- dk rows
+  a.src = dy; a.dst = du;
+  if (launch_col(a, true, C * a.P, s)) return 3;             // du = IFFT + D dy
+  if (dk) {
+    FftArgs b = a;
+    b.single = 1;
+    if (launch_col(b, true, C, s)) return 3;                 // dk[j] = Re IFFT(SK_j)
+  }
+  if (dD) {
+    hipLaunchKernelGGL(row_dot_kernel, dim3(R * C), dim3(256), 0, s, dy, u, dD, L, C, R);
+    LCI_LAUNCH_CHECK();
+  }
+  return 0;
+}
+
+extern "C" int lci_hyena_pre_fwd(int dtype, const void* z, const float* w, const float* bias, float* vg, void* x2,
+                                 int BB, int L, int H, int hd, int K, void* stream) {
+  LCI_CHECK(K >= 1 && K <= 8, "hyena_pre: short filter order %d unsupported (<= 8)", K);
+  GateArgs a{};
+  a.z = z; a.w = w; a.bias = bias; a.vg = vg; a.x2 = x2; a.BB = BB; a.L = L; a.H = H; a.hd = hd; a.D = H * hd; a.K = K;
+  dim3 grid((L + 63) / 64, (a.D + 63) / 64, BB);
+  if (dtype == 1) hipLaunchKernelGGL(hyena_pre_fwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL(hyena_pre_fwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int lci_hyena_post_fwd(int dtype, const float* y, const void* x2, void* out, int BB, int L, int D,
+                                  void* stream) {
+  GateArgs a{};
+  a.y = y; a.x2 = (void*)x2; a.out = out; a.BB = BB; a.L = L; a.D = D;
+  dim3 grid((L + 63) / 64, (D + 63) / 64, BB);
+  if (dtype == 1) hipLaunchKernelGGL(hyena_post_fwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL(hyena_post_fwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int lci_hyena_post_bwd(int dtype, const float* y, const void* x2, const void* dout, float* dy, float* dx2,
+                                  int BB, int L, int D, void* stream) {
+  GateArgs a{};
+  a.y = y; a.x2 = (void*)x2; a.dout = dout; a.dy = dy; a.dx2 = dx2; a.BB = BB; a.L = L; a.D = D;
+  dim3 grid((L + 63) / 64, (D + 63) / 64, BB);
+  if (dtype == 1) hipLaunchKernelGGL(hyena_post_bwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL(hyena_post_bwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+
+// dw (3D, K), db (3D) accumulated (caller zeroes). gx2 is f32 (BB, L, D).
+extern "C" int lci_hyena_pre_bwd(int dtype, const void* z, const float* w, const float* bias, const float* dvg,
+                                 const float* gx2, void* dz, float* dw, float* db, int BB, int L, int H, int hd, int K,
+                                 void* stream) {
+  LCI_CHECK(K >= 1 && K <= 8, "hyena_pre: short filter order %d unsupported (<= 8)", K);
+  GateArgs a{};
+  a.z = z; a.w = w; a.bias = bias; a.dvg = dvg; a.gx2 = gx2; a.dz = dz; a.dw = dw; a.db = db;
+  a.BB = BB; a.L = L; a.H = H; a.hd = hd; a.D = H * hd; a.K = K;
+  dim3 grid((L + 63) / 64, (3 * a.D + 255) / 256, BB);
+  if (dtype == 1) hipLaunchKernelGGL(hyena_pre_bwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL(hyena_pre_bwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}

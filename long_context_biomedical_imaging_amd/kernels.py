@@ -434,3 +434,170 @@ def window_attention(qkv, rpb, mask, num_heads, scale):
     geo = (0, 0, 1, 1, 1, 1, 1, 1, 0, 0, 0, Bw, nW, N, C3 // 3, num_heads)
     o = _WindowAttention.apply(q, None, _pad_rpb(rpb), mask, geo, scale)
     return o if dt == torch.bfloat16 else o.to(dt)
+
+
+# ----------------------------------------------------------------------------------------- hyena
+_TW = {}
+
+
+def _twiddles(n, device):
+    key = (n, str(device))
+    t = _TW.get(key)
+    if t is None:
+        t = torch.empty(n, 2, device=device, dtype=torch.float32)
+        _lib.call("lci_fft_twiddles", t.data_ptr(), n, _lib.stream_of(t))
+        _TW[key] = t
+    return t
+
+
+def _fft_n(L):
+    return int(_lib.load().lci_fft_size(int(L)))
+
+
+def _spectrum(k):
+    C, L = k.shape
+    n = _fft_n(L)
+    tw = _twiddles(n, k.device)
+    K = torch.empty(C, n, 2, device=k.device, dtype=torch.float32)
+    SK = torch.empty(C, n, 2, device=k.device, dtype=torch.float32)
+    KernelTimer.run("fftconv_spectrum", 0.0, k, lambda: _lib.call(
+        "lci_fftconv_spectrum", k.data_ptr(), K.data_ptr(), SK.data_ptr(), tw.data_ptr(), C, L, _lib.stream_of(k)))
+    return K
+
+
+class _FFTConv(torch.autograd.Function):
+    """y = causal_conv(u, k) + D u along L for rows (R, C, L) f32; filter = channel index."""
+
+    @staticmethod
+    def forward(ctx, u, k, D):
+        R, C, L = u.shape
+        kf = k.float().contiguous()
+        Dv = D.float().contiguous()
+        K = _spectrum(kf)
+        n = K.shape[1]
+        tw = _twiddles(n, u.device)
+        y = torch.empty_like(u)
+        S = torch.empty(C * ((R + 1) // 2), n, 2, device=u.device, dtype=torch.float32)
+        KernelTimer.run("fftconv_fwd", float(R * C * L), u, lambda: _lib.call(
+            "lci_fftconv_fwd", u.data_ptr(), K.data_ptr(), Dv.data_ptr(), y.data_ptr(), S.data_ptr(), tw.data_ptr(),
+            R, C, L, _lib.stream_of(u)))
+        ctx.save_for_backward(u, K, Dv)
+        ctx.kdtype = k.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        u, K, Dv = ctx.saved_tensors
+        R, C, L = u.shape
+        n = K.shape[1]
+        tw = _twiddles(n, u.device)
+        dy = dy.float().contiguous()
+        du = torch.empty_like(u)
+        want_k = ctx.needs_input_grad[1]
+        want_d = ctx.needs_input_grad[2]
+        dk = torch.empty(C, L, device=u.device, dtype=torch.float32) if want_k else None
+        dD = torch.zeros(C, device=u.device, dtype=torch.float32) if want_d else None
+        P = (R + 1) // 2
+        S = torch.empty(C * P, n, 2, device=u.device, dtype=torch.float32)
+        S2 = torch.empty(C * P, n, 2, device=u.device, dtype=torch.float32) if want_k else None
+        SK = torch.empty(C, n, 2, device=u.device, dtype=torch.float32) if want_k else None
+        KernelTimer.run("fftconv_bwd", float(R * C * L), u, lambda: _lib.call(
+            "lci_fftconv_bwd", dy.data_ptr(), u.data_ptr(), K.data_ptr(), Dv.data_ptr(), du.data_ptr(),
+            _lib.ptr(dk), _lib.ptr(dD), S.data_ptr(), _lib.ptr(S2), _lib.ptr(SK), tw.data_ptr(), R, C, L,
+            _lib.stream_of(u)))
+        return du, (dk.to(ctx.kdtype) if dk is not None else None), dD
+
+
+def fftconv(u, k, D):
+    """fftconv_ref (hyena.py:32-51, gelu=False): u (..., C, L), k (C, L), D (C) -> causal conv + D u, in u.dtype.
+
+    Computed in f32 (the reference casts u to k's f32 dtype for the FFT) with the HIP four-step FFT.
+    """
+    _lib.require_gpu(u.contiguous(), k.contiguous())
+    shp = u.shape
+    C, L = shp[-2], shp[-1]
+    rows = u.float().reshape(-1, C, L).contiguous()
+    y = _FFTConv.apply(rows, k, D)
+    return y.reshape(shp).to(u.dtype)
+
+
+class _HyenaPre(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z, w, b, num_heads):
+        BB, L, C3 = z.shape
+        D = C3 // 3
+        hd = D // num_heads
+        K = w.shape[-1]
+        wf = w.float().reshape(C3, K).contiguous()
+        bf = b.float().contiguous() if b is not None else None
+        vg = torch.empty(BB, D, L, device=z.device, dtype=torch.float32)
+        x2 = torch.empty(BB, L, D, device=z.device, dtype=z.dtype)
+        KernelTimer.run("hyena_pre_fwd", 0.0, z, lambda: _lib.call(
+            "lci_hyena_pre_fwd", _DT[z.dtype], z.data_ptr(), wf.data_ptr(), _lib.ptr(bf), vg.data_ptr(),
+            x2.data_ptr(), BB, L, num_heads, hd, K, _lib.stream_of(z)))
+        ctx.save_for_backward(z, wf, bf)
+        ctx.meta = (num_heads, w.shape, b is not None)
+        return vg, x2
+
+    @staticmethod
+    def backward(ctx, dvg, dx2):
+        z, wf, bf = ctx.saved_tensors
+        num_heads, wshape, has_b = ctx.meta
+        BB, L, C3 = z.shape
+        D = C3 // 3
+        hd = D // num_heads
+        K = wf.shape[1]
+        f32 = dict(device=z.device, dtype=torch.float32)
+        dvg = torch.zeros(BB, D, L, **f32) if dvg is None else dvg.float().contiguous()
+        dx2 = torch.zeros(BB, L, D, **f32) if dx2 is None else dx2.float().contiguous()
+        dz = torch.empty_like(z)
+        dw = torch.zeros(C3, K, **f32)
+        db = torch.zeros(C3, **f32) if has_b else None
+        KernelTimer.run("hyena_pre_bwd", 0.0, z, lambda: _lib.call(
+            "lci_hyena_pre_bwd", _DT[z.dtype], z.data_ptr(), wf.data_ptr(), _lib.ptr(bf), dvg.data_ptr(),
+            dx2.data_ptr(), dz.data_ptr(), dw.data_ptr(), _lib.ptr(db), BB, L, num_heads, hd, K, _lib.stream_of(z)))
+        return dz, dw.reshape(wshape), db, None
+
+
+class _HyenaPost(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y, x2):
+        BB, D, L = y.shape
+        out = torch.empty(BB, L, D, device=y.device, dtype=x2.dtype)
+        KernelTimer.run("hyena_post_fwd", 0.0, y, lambda: _lib.call(
+            "lci_hyena_post_fwd", _DT[x2.dtype], y.data_ptr(), x2.data_ptr(), out.data_ptr(), BB, L, D,
+            _lib.stream_of(y)))
+        ctx.save_for_backward(y, x2)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        y, x2 = ctx.saved_tensors
+        BB, D, L = y.shape
+        dout = dout.to(x2.dtype).contiguous()
+        dy = torch.empty(BB, D, L, device=y.device, dtype=torch.float32)
+        dx2 = torch.empty(BB, L, D, device=y.device, dtype=torch.float32)
+        KernelTimer.run("hyena_post_bwd", 0.0, y, lambda: _lib.call(
+            "lci_hyena_post_bwd", _DT[x2.dtype], y.data_ptr(), x2.data_ptr(), dout.data_ptr(), dy.data_ptr(),
+            dx2.data_ptr(), BB, L, D, _lib.stream_of(y)))
+        return dy, dx2
+
+
+def hyena_pre(z, weight, bias, num_heads):
+    """Causal depthwise short conv of the channels-last in_proj output z (B, L, 3D) + pre-gate (hyena.py:321-333).
+
+    Returns vg = v * x1 as channel-major f32 rows (B, D, L) for the long conv, and x2 channels-last (B, L, D).
+    """
+    _lib.require_gpu(z.contiguous())
+    z = z.contiguous()
+    if z.dtype not in _DT:
+        z = z.float()
+    return _HyenaPre.apply(z, weight, bias, num_heads)
+
+
+def hyena_fftconv_gate(vg, k, bias, x2):
+    """(causal_conv(vg, k) + bias * vg) * x2, returned channels-last (B, L, D) in x2's dtype (hyena.py:343-355)."""
+    BB, D, L = vg.shape
+    hd = k.shape[0]
+    y = _FFTConv.apply(vg.reshape(BB * (D // hd), hd, L), k, bias).reshape(BB, D, L)
+    return _HyenaPost.apply(y, x2)
