@@ -1,15 +1,25 @@
-/* liblci — MI355X (gfx950) kernels for the long-context image-token mixers.
+/* liblci — MI355X (gfx950) kernels for the long-context image-token mixers of
+ * NHLBI/long_context_biomedical_imaging (the reference), exposed as a C ABI.
  *
- * C-ABI boundary: plain device pointers, sizes and a hipStream_t passed as void*. No torch types.
- * Every entry point enqueues on `stream` and returns 0 on success; on failure it returns non-zero and
- * lci_last_error() describes the problem (bad shape/alignment -> 1, HIP API error -> 2, launch -> 3).
- * Memory is owned by the caller: the library never allocates or frees device memory.
- * bf16 = IEEE bfloat16 stored as uint16. Row-major throughout.
+ * Conventions
+ *   - Plain device pointers, sizes and a hipStream_t passed as void*. No torch types.
+ *   - Every entry point enqueues on `stream` and returns 0 on success; non-zero on failure with
+ *     lci_last_error() describing it (1 = bad shape/alignment, 2 = HIP API error, 3 = launch error).
+ *   - Memory is owned by the caller; the library never allocates or frees device memory. Buffers
+ *     documented as "accumulated" must be zeroed by the caller.
+ *   - dtype codes: 0 = f32, 1 = bf16 (IEEE bfloat16 stored as uint16). Row-major throughout.
+ *   - "channels-last" = (B, L, C) with unit channel stride; "channel-major rows" = (rows, L).
  *
- * Reference interfaces replaced (file:line in NHLBI/long_context_biomedical_imaging):
- *   lci_attn_fwd / lci_attn_bwd
- *       SABlock.forward attention core, model/models/backbone_vit.py:191-203
- *       (einsum QK^T * scale -> softmax -> einsum AV; autograd backward of the same)
+ * Reference interfaces replaced (file:line under /root/reference)
+ *   lci_attn_*            SABlock.forward attention core, model/models/backbone_vit.py:191-203
+ *   lci_window_attn_*     WindowAttention.forward, model/models/backbone_swin.py:339-359, and in grid mode the
+ *                         pad/roll/window_partition/window_reverse/crop of SwinTransformerBlock.forward_part1
+ *                         (:435-487) with compute_mask (:591-628)
+ *   lci_selective_scan_*  mamba_ssm selective_scan_fn (mamba-ssm 1.2.0.post1) as called at model/models/mamba.py:125-134
+ *   lci_dwconv_silu_*     MambaVisionMixer depthwise conv1d + SiLU, model/models/mamba.py:118-119
+ *   lci_fftconv_*         fftconv_ref (gelu=False), model/models/hyena.py:32-51 / Filter.forward :201-216
+ *   lci_hyena_pre/post_*  HyenaOperator short filter + gating, model/models/hyena.py:317-355
+ *   lci_patch_embed_*     MONAI-1.3 PatchEmbeddingBlock (backbone_vit.py:351-361) / PatchEmbed (backbone_swin.py:800-806)
  */
 #ifndef LCI_H_
 #define LCI_H_
@@ -21,19 +31,107 @@ extern "C" {
 const char* lci_last_error(void);
 int lci_abi_version(void);
 
-/* Flash attention forward.
- *   qkv  : (B, L, 3*H*head_dim) bf16 — the packed qkv Linear output, channel order (qkv, head, d)
- *          (backbone_vit.py:168 Rearrange "b h (qkv l d) -> qkv b l h d").
- *   out  : (B, L, H*head_dim) bf16 — softmax(q k^T * scale) v in "b l (h d)" order (backbone_vit.py:169).
- *   lse2 : (B, H, L) f32 — log2(sum_y exp(scale q.k_y)) per query row, consumed by lci_attn_bwd.
- *   head_dim must be 64; pointers 16-byte aligned. */
+/* ------------------------------------------------------------------ ViT full self-attention (flash)
+ * qkv : (B, L, 3*H*64) bf16, the packed qkv Linear output, channel order (qkv, head, d)
+ *       (backbone_vit.py:168 Rearrange "b h (qkv l d) -> qkv b l h d").
+ * out : (B, L, H*64) bf16 = softmax(q k^T * scale) v in "b l (h d)" order (backbone_vit.py:169).
+ * lse2: (B, H, L) f32 = log2 sum_y exp(scale q.k_y) per query row (consumed by the backward).
+ * head_dim must be 64; pointers 16-byte aligned. */
 int lci_attn_fwd(const void* qkv, void* out, float* lse2, int B, int L, int H, int head_dim, float scale,
                  void* stream);
-
-/* Flash attention backward: dqkv (B, L, 3*H*head_dim) bf16 receives dQ, dK, dV in the packed layout.
- *   dout: (B, L, H*head_dim) bf16; delta_ws: (B, H, L) f32 workspace. */
+/* dqkv (B, L, 3*H*64) bf16 <- dQ, dK, dV in the packed layout; dout (B, L, H*64) bf16;
+ * delta_ws (B, H, L) f32 workspace. No atomics: bitwise reproducible. */
 int lci_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse2, void* dqkv,
                  float* delta_ws, int B, int L, int H, int head_dim, float scale, void* stream);
+/* Same as lci_attn_bwd, one launch at a time (stage 0 = delta, 1 = dK/dV, 2 = dQ; -1 = all) for timing. */
+int lci_attn_bwd_stage(int stage, const void* qkv, const void* out, const void* dout, const float* lse2,
+                       void* dqkv, float* delta_ws, int B, int L, int H, int head_dim, float scale, void* stream);
+
+/* ------------------------------------------------------------------ Swin window attention (head_dim 32)
+ * geo[16] = {mode, nd, S0, S1, S2, ws0, ws1, ws2, sh0, sh1, sh2, B_or_Bw, nW, N, C, H}
+ *   mode 1 (grid): qkv (B, S0, S1[, S2], 3C) bf16 channels-last on the UN-padded grid; window ws, shift sh;
+ *                  padded voxels take q/k/v = qkv_bias (f32, 3C, may be null = zeros); the -100 region mask
+ *                  is evaluated in-kernel; out (B, S.., C) bf16 is the un-shifted, cropped result.
+ *   mode 0 (windows): qkv (Bw, N, 3C), optional mask (nW, N, N) f32, out (Bw, N, C).
+ * rpb : (H, N, Npad) f32 relative-position bias (rpb_table[rp_index]), Npad = ceil(N/32)*32.
+ * lse2: (Bw, H, N) f32 (Bw = B * prod(ceil(S/ws)) in grid mode). N <= 768. */
+int lci_window_attn_fwd(const void* qkv, const float* qkv_bias, const float* rpb, const float* mask, void* out,
+                        float* lse2, const int* geo, float scale, void* stream);
+/* dqkv (same layout as qkv) <- dQ/dK/dV; dbias_pad (3C, accumulated) <- dK/dV of padded voxels;
+ * dS: optional bf16 workspace of lci_window_dS_elems(geo) elements; drpb (H, N, N) f32 written if dS given. */
+int lci_window_attn_bwd(const void* qkv, const float* qkv_bias, const float* rpb, const float* mask,
+                        const void* out, const void* dout, const float* lse2, void* dqkv, float* dbias_pad,
+                        void* dS, float* drpb, const int* geo, float scale, void* stream);
+long long lci_window_dS_elems(const int* geo);
+
+/* ------------------------------------------------------------------ Mamba selective scan (d_state 8)
+ * Channels-last: u, delta (B, L, Dx); Bm, Cm (B, L, 8) (e.g. column slices of x_proj's output); y (B, L, .).
+ * strides[16] (elements) = {bu,tu, bd,td, bB,tB, bC,tC, by,ty, bdy,tdy, bdu,tdu, bdd,tdd} (batch, token).
+ * A (Dx, 8), D (Dx), delta_bias (Dx) f32. delta' = softplus(delta + delta_bias).
+ * chunk: multiple of 16. Workspaces f32: xend, xinit (B*nch*Dx*8), sdt (B*nch*Dx), nch = ceil(L/chunk);
+ * ckpt (B*ceil(L/16)*Dx*8) or null (needed by the backward). */
+int lci_selective_scan_fwd(int dtype, const void* u, const void* delta, const float* A, const void* Bm,
+                           const void* Cm, const float* D, const float* delta_bias, void* y,
+                           const long long* strides, int B, int L, int Dx, int N, int chunk, float* xend,
+                           float* xinit, float* sdt, float* ckpt, void* stream);
+/* du, ddelta (B, L, Dx) written; dBC (B, L, 16) f32 = [dB | dC], dA (Dx, 8), dD, ddelta_bias accumulated.
+ * sdt / ckpt from the forward with the same chunk; gl, gin: (B*nch*Dx*8) f32 workspaces. */
+int lci_selective_scan_bwd(int dtype, const void* u, const void* delta, const float* A, const void* Bm,
+                           const void* Cm, const float* D, const float* delta_bias, const void* dy, void* du,
+                           void* ddelta, float* dBC, float* dA, float* dD, float* ddelta_bias,
+                           const long long* strides, int B, int L, int Dx, int N, int chunk, const float* sdt,
+                           const float* ckpt, float* gl, float* gin, void* stream);
+
+/* SiLU(depthwise conv1d(k = 3, 'same')) of both channel halves of in (B, L, 2C) (token stride in_ts):
+ * ox (B, L, C) (token stride ox_ts) and oz at column offset zoff of a (B, L, oz_ts) buffer. */
+int lci_dwconv_silu_fwd(int dtype, const void* in, const float* wx, const float* bx, const float* wz,
+                        const float* bz, void* ox, void* oz, int B, int L, int C, int K, int in_ts, int ox_ts,
+                        int oz_ts, int zoff, void* stream);
+/* din (B, L, 2C) written; dwx, dbx, dwz, dbz accumulated. gx / gz: grads of ox / oz (same layouts). */
+int lci_dwconv_silu_bwd(int dtype, const void* in, const float* wx, const float* bx, const float* wz,
+                        const float* bz, const void* gx, const void* gz, void* din, float* dwx, float* dbx,
+                        float* dwz, float* dbz, int B, int L, int C, int K, int in_ts, int ox_ts, int oz_ts,
+                        int zoff, void* stream);
+
+/* ------------------------------------------------------------------ Hyena long convolution (f32)
+ * FFT size n = lci_fft_size(L) = pow2 >= 2L (L <= 131072). tw: n complex f32 (f32x2) from lci_fft_twiddles.
+ * Rows are channel-major f32 (R, C, L); the filter of row r is r % C; k (C, L). */
+long long lci_fft_size(int L);
+int lci_fft_twiddles(void* tw, int n, void* stream);
+/* K (C, n) complex f32 = filter spectra (scaled by 1/n); SK (C, n) complex scratch. */
+int lci_fftconv_spectrum(const float* k, void* K, void* SK, const void* tw, int C, int L, void* stream);
+/* y = causal_conv(u, k) + D u; S: (C*ceil(R/2), n) complex scratch. */
+int lci_fftconv_fwd(const float* u, const void* K, const float* Dv, float* y, void* S, const void* tw, int R,
+                    int C, int L, void* stream);
+/* du = corr(dy, k) + D dy (written); dk (C, L) = sum_rows corr(dy, u) (written, optional); dD accumulated
+ * (optional). S, S2: (C*ceil(R/2), n) complex scratch (S2 only with dk); SK: (C, n) complex scratch. */
+int lci_fftconv_bwd(const float* dy, const float* u, const void* K, const float* Dv, float* du, float* dk,
+                    float* dD, void* S, void* S2, void* SK, const void* tw, int R, int C, int L, void* stream);
+/* z (BB, L, 3D) channels-last in_proj output; causal depthwise conv (w (3D, K), bias (3D)); per head h,
+ * x1/x2/v = conv channels [h*3hd, +hd), [+hd, +2hd), [+2hd, +3hd). vg = v*x1 -> (BB, D, L) f32 rows;
+ * x2 -> (BB, L, D) channels-last (z dtype). */
+int lci_hyena_pre_fwd(int dtype, const void* z, const float* w, const float* bias, float* vg, void* x2, int BB,
+                      int L, int H, int hd, int K, void* stream);
+/* out (BB, L, D) = y (BB, D, L) f32 * x2, channels-last. */
+int lci_hyena_post_fwd(int dtype, const float* y, const void* x2, void* out, int BB, int L, int D, void* stream);
+/* dy (BB, D, L) f32 = dout * x2; dx2 (BB, L, D) f32 = dout * y. */
+int lci_hyena_post_bwd(int dtype, const float* y, const void* x2, const void* dout, float* dy, float* dx2, int BB,
+                       int L, int D, void* stream);
+/* dz (BB, L, 3D) written; dw (3D, K), db (3D) accumulated. gx2: (BB, L, D) f32. */
+int lci_hyena_pre_bwd(int dtype, const void* z, const float* w, const float* bias, const float* dvg,
+                      const float* gx2, void* dz, float* dw, float* db, int BB, int L, int H, int hd, int K,
+                      void* stream);
+
+/* ------------------------------------------------------------------ patch embedding (conv, k = stride = p)
+ * x (B, C, S0, S1[, S2]) (dtype x_dtype), w (D, C*prod(p)) f32, bias (D) / pos (L, D) f32 or null;
+ * channels_last = 1: y (B, L, D) (ViT, + pos); 0: y (B, D, G0, G1[, G2]) (Swin; right zero-pad to p). */
+int lci_patch_embed_fwd(const void* x, int x_dtype, const float* w, const float* bias, const float* pos, void* y,
+                        int y_dtype, int B, int C, int D, int nd, const int* img_size, const int* patch,
+                        int channels_last, void* stream);
+/* dw (D*K), db (D) accumulated; dpos (L, D) written (channels_last only). */
+int lci_patch_embed_bwd(const void* x, int x_dtype, const void* dy, int dy_dtype, float* dw, float* db, float* dpos,
+                        int B, int C, int D, int nd, const int* img_size, const int* patch, int channels_last,
+                        void* stream);
 
 #ifdef __cplusplus
 }
