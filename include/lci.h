@@ -67,20 +67,21 @@ long long lci_window_dS_elems(const int* geo);
 /* ------------------------------------------------------------------ Mamba selective scan (d_state 8)
  * Channels-last: u, delta (B, L, Dx); Bm, Cm (B, L, 8) (e.g. column slices of x_proj's output); y (B, L, .).
  * strides[16] (elements) = {bu,tu, bd,td, bB,tB, bC,tC, by,ty, bdy,tdy, bdu,tdu, bdd,tdd} (batch, token).
- * A (Dx, 8), D (Dx), delta_bias (Dx) f32. delta' = softplus(delta + delta_bias).
+ * A (Dx, 8), D (Dx), delta_bias (Dx) f32 (D, delta_bias may be null). delta' = softplus(delta + delta_bias)
+ * when delta_softplus, else delta + delta_bias.
  * chunk: multiple of 16. Workspaces f32: xend, xinit (B*nch*Dx*8), sdt (B*nch*Dx), nch = ceil(L/chunk);
  * ckpt (B*ceil(L/16)*Dx*8) or null (needed by the backward). */
 int lci_selective_scan_fwd(int dtype, const void* u, const void* delta, const float* A, const void* Bm,
                            const void* Cm, const float* D, const float* delta_bias, void* y,
-                           const long long* strides, int B, int L, int Dx, int N, int chunk, float* xend,
-                           float* xinit, float* sdt, float* ckpt, void* stream);
+                           const long long* strides, int B, int L, int Dx, int N, int chunk, int delta_softplus,
+                           float* xend, float* xinit, float* sdt, float* ckpt, void* stream);
 /* du, ddelta (B, L, Dx) written; dBC (B, L, 16) f32 = [dB | dC], dA (Dx, 8), dD, ddelta_bias accumulated.
  * sdt / ckpt from the forward with the same chunk; gl, gin: (B*nch*Dx*8) f32 workspaces. */
 int lci_selective_scan_bwd(int dtype, const void* u, const void* delta, const float* A, const void* Bm,
                            const void* Cm, const float* D, const float* delta_bias, const void* dy, void* du,
                            void* ddelta, float* dBC, float* dA, float* dD, float* ddelta_bias,
-                           const long long* strides, int B, int L, int Dx, int N, int chunk, const float* sdt,
-                           const float* ckpt, float* gl, float* gin, void* stream);
+                           const long long* strides, int B, int L, int Dx, int N, int chunk, int delta_softplus,
+                           const float* sdt, const float* ckpt, float* gl, float* gin, void* stream);
 
 /* SiLU(depthwise conv1d(k = 3, 'same')) of both channel halves of in (B, L, 2C) (token stride in_ts):
  * ox (B, L, C) (token stride ox_ts) and oz at column offset zoff of a (B, L, oz_ts) buffer. */

@@ -26,9 +26,9 @@ SIGNATURES = {
     "lci_attn_bwd_stage": [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P],
     "lci_patch_embed_fwd": [_P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P],
     "lci_patch_embed_bwd": [_P, _I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P, _P, _I, _P],
-    "lci_selective_scan_fwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
+    "lci_selective_scan_fwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "lci_selective_scan_bwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I,
-                               _P, _P, _P, _P, _P],
+                               _I, _P, _P, _P, _P, _P],
     "lci_window_attn_fwd": [_P, _P, _P, _P, _P, _P, _P, _F, _P],
     "lci_window_attn_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P],
     "lci_fft_twiddles": [_P, _I, _P],

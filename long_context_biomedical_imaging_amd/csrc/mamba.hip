@@ -34,6 +34,7 @@ struct ScanArgs {
   int tu, td, tB, tC, ty, tdy, tdu, tdd;                // token strides (elements)
   int B, L, Dx, Tc, nch, nck;
   int write_ckpt;
+  int softplus;                                         // delta_softplus
 };
 
 template <typename T> __device__ __forceinline__ float ldf(const T* p) { return (float)(*p); }
@@ -59,7 +60,8 @@ __device__ __forceinline__ void ld8u(const T* p, float (&v)[SCAN_N], bool aligne
   for (int n = 0; n < SCAN_N; ++n) v[n] = (float)p[n];
 }
 
-__device__ __forceinline__ float softplus(float v) { return v <= 20.f ? log1pf(__expf(v)) : v; }
+__device__ __forceinline__ float softplus_raw(float v) { return v <= 20.f ? log1pf(__expf(v)) : v; }
+#define softplus(v) (a.softplus ? softplus_raw(v) : (v))
 
 // ---------------------------------------------------------------------------------- forward chunk pass
 // MODE 0: zero initial state -> xend, sdt. MODE 1: xinit -> y (+ checkpoints).
@@ -289,7 +291,7 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(ScanArgs a) {
 #pragma unroll
           for (int k = 0; k < 16; ++k) v[k] = 0.f;
         }
-        const float sg = draw <= 20.f ? 1.f / (1.f + __expf(-draw)) : 1.f;
+        const float sg = (a.softplus && draw <= 20.f) ? 1.f / (1.f + __expf(-draw)) : 1.f;
         const float ddl = ddt * sg;
         dDacc = fmaf(gy, uf, dDacc);
         dbacc += ddl;
@@ -426,9 +428,11 @@ static void scan_strides(ScanArgs& a, const long long* s) {
 extern "C" int lci_selective_scan_fwd(int dtype, const void* u, const void* delta, const float* A, const void* Bm,
                                       const void* Cm, const float* D, const float* delta_bias, void* y,
                                       const long long* strides, int B, int L, int Dx, int N, int chunk,
-                                      float* xend, float* xinit, float* sdt, float* ckpt, void* stream) {
+                                      int delta_softplus, float* xend, float* xinit, float* sdt, float* ckpt,
+                                      void* stream) {
   ScanArgs a{};
   if (scan_fill(a, B, L, Dx, N, chunk)) return 1;
+  a.softplus = delta_softplus;
   scan_strides(a, strides);
   a.u = u; a.delta = delta; a.A = A; a.Bm = Bm; a.Cm = Cm; a.D = D; a.dbias = delta_bias; a.y = y;
   a.xend = xend; a.xinit = xinit; a.sdt = sdt; a.ckpt = ckpt; a.write_ckpt = ckpt != nullptr;
@@ -452,9 +456,11 @@ extern "C" int lci_selective_scan_bwd(int dtype, const void* u, const void* delt
                                       const void* Cm, const float* D, const float* delta_bias, const void* dy,
                                       void* du, void* ddelta, float* dBC, float* dA, float* dD, float* ddelta_bias,
                                       const long long* strides, int B, int L, int Dx, int N, int chunk,
-                                      const float* sdt, const float* ckpt, float* gl, float* gin, void* stream) {
+                                      int delta_softplus, const float* sdt, const float* ckpt, float* gl, float* gin,
+                                      void* stream) {
   ScanArgs a{};
   if (scan_fill(a, B, L, Dx, N, chunk)) return 1;
+  a.softplus = delta_softplus;
   scan_strides(a, strides);
   a.u = u; a.delta = delta; a.A = A; a.Bm = Bm; a.Cm = Cm; a.D = D; a.dbias = delta_bias; a.dy = dy;
   a.du = du; a.ddelta = ddelta; a.dBC = dBC; a.dA = dA; a.dD = dD; a.ddbias = ddelta_bias;

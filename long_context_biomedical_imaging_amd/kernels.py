@@ -253,7 +253,7 @@ def dwconv_silu_pair(xz, wx, bx, wz, bz):
 
 class _SelectiveScanCL(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, u, delta, A, Bm, Cm, D, delta_bias, yz):
+    def forward(ctx, u, delta, A, Bm, Cm, D, delta_bias, yz, softplus=True):
         B, L, Dx = u.shape
         N = A.shape[1]
         dt = u.dtype
@@ -266,21 +266,27 @@ class _SelectiveScanCL(torch.autograd.Function):
         sdt = torch.empty(B, nch, Dx, **f32)
         need_grad = any(ctx.needs_input_grad)
         ckpt = torch.empty(B, nck, Dx, N, **f32) if need_grad else None
-        Af, Dv, bv = A.float().contiguous(), D.float().contiguous(), delta_bias.float().contiguous()
+        Af = A.float().contiguous()
+        Dv = D.float().contiguous() if D is not None else torch.zeros(Dx, **f32)
+        bv = delta_bias.float().contiguous() if delta_bias is not None else torch.zeros(Dx, **f32)
         y = yz[..., :Dx]
         strides = _ll_array([*_bt(u), *_bt(delta), *_bt(Bm), *_bt(Cm), *_bt(y), 0, 0, 0, 0, 0, 0])
         KernelTimer.run("selective_scan_fwd", float(B * L), u, lambda: _lib.call(
             "lci_selective_scan_fwd", _DT[dt], u.data_ptr(), delta.data_ptr(), Af.data_ptr(), Bm.data_ptr(),
-            Cm.data_ptr(), Dv.data_ptr(), bv.data_ptr(), y.data_ptr(), strides, B, L, Dx, N, tc,
+            Cm.data_ptr(), Dv.data_ptr(), bv.data_ptr(), y.data_ptr(), strides, B, L, Dx, N, tc, int(softplus),
             xend.data_ptr(), xinit.data_ptr(), sdt.data_ptr(), _lib.ptr(ckpt), _lib.stream_of(u)))
         ctx.mark_dirty(yz)
         if need_grad:
             ctx.save_for_backward(u, delta, Af, Bm, Cm, Dv, bv, sdt, ckpt)
-        ctx.tc = tc
-        return yz
+        ctx.tc, ctx.softplus = tc, softplus
+        ctx.has_D, ctx.has_b = D is not None, delta_bias is not None
+        # final state x_L = exp(A sum(dt) over the last chunk) xinit_last + xend_last (return_last_state)
+        last = torch.exp(Af[None] * sdt[:, -1, :, None]) * xinit[:, -1] + xend[:, -1]
+        ctx.mark_non_differentiable(last)
+        return yz, last
 
     @staticmethod
-    def backward(ctx, gyz):
+    def backward(ctx, gyz, _glast=None):
         u, delta, Af, Bm, Cm, Dv, bv, sdt, ckpt = ctx.saved_tensors
         B, L, Dx = u.shape
         N = Af.shape[1]
@@ -303,14 +309,15 @@ class _SelectiveScanCL(torch.autograd.Function):
         KernelTimer.run("selective_scan_bwd", float(B * L), u, lambda: _lib.call(
             "lci_selective_scan_bwd", _DT[u.dtype], u.data_ptr(), delta.data_ptr(), Af.data_ptr(), Bm.data_ptr(),
             Cm.data_ptr(), Dv.data_ptr(), bv.data_ptr(), dy.data_ptr(), du.data_ptr(), dd.data_ptr(),
-            dBC.data_ptr(), dA.data_ptr(), dD.data_ptr(), db.data_ptr(), strides, B, L, Dx, N, tc, sdt.data_ptr(),
-            ckpt.data_ptr(), gl.data_ptr(), gin.data_ptr(), _lib.stream_of(u)))
+            dBC.data_ptr(), dA.data_ptr(), dD.data_ptr(), db.data_ptr(), strides, B, L, Dx, N, tc,
+            int(ctx.softplus), sdt.data_ptr(), ckpt.data_ptr(), gl.data_ptr(), gin.data_ptr(), _lib.stream_of(u)))
         gz = gyz.clone()
         gz[..., :Dx] = 0
-        return (du, dd, dA, dBC[..., :N].to(Bm.dtype), dBC[..., N:].to(Cm.dtype), dD, db, gz)
+        return (du, dd, dA, dBC[..., :N].to(Bm.dtype), dBC[..., N:].to(Cm.dtype), dD if ctx.has_D else None,
+                db if ctx.has_b else None, gz, None)
 
 
-def selective_scan_cl(u, delta, A, Bm, Cm, D, delta_bias, yz):
+def selective_scan_cl(u, delta, A, Bm, Cm, D, delta_bias, yz, delta_softplus=True, return_last_state=False):
     """Channels-last selective scan (mamba-ssm selective_scan_fn semantics with delta_softplus=True).
 
     u, delta (B, L, Dx); Bm, Cm (B, L, N) views with unit channel stride (e.g. column slices of x_proj's
@@ -333,7 +340,8 @@ def selective_scan_cl(u, delta, A, Bm, Cm, D, delta_bias, yz):
         delta = delta.contiguous()
     if yz.dtype != dt:
         raise _lib.LciError("selective_scan: yz dtype must match u")
-    return _SelectiveScanCL.apply(u, delta, A, Bm, Cm, D, delta_bias, yz)
+    out, last = _SelectiveScanCL.apply(u, delta, A, Bm, Cm, D, delta_bias, yz, bool(delta_softplus))
+    return (out, last) if return_last_state else out
 
 
 # ------------------------------------------------------------------------------------ window attention

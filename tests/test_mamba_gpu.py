@@ -110,3 +110,27 @@ def test_mamba_mixer_vs_reference(amp):
     assert rel_err(x.grad, g.t("grad/in0")) < (5e-2 if amp else 2e-4)
     for p in ("A_log", "D", "dt_proj.bias", "x_proj.weight", "in_proj.weight", "conv1d_x.weight"):
         assert rel_err(dict(m.named_parameters())[p].grad, g.t(f"grad/{p}")) < (6e-2 if amp else 3e-4), p
+
+
+def test_compat_selective_scan_fn_signature():
+    """mamba-ssm selective_scan_fn signature (channel-major) vs the reference fixture; last state vs oracle loop."""
+    from long_context_biomedical_imaging_amd.compat import selective_scan_fn
+    g = Golden("selective_scan")
+    names = ["u", "delta", "A", "B", "C", "D", "delta_bias"]
+    ins = {n: g.t(f"in/{n}").cuda() for n in names}
+    y, last = selective_scan_fn(ins["u"], ins["delta"], ins["A"], ins["B"], ins["C"], ins["D"], z=None,
+                                delta_bias=ins["delta_bias"], delta_softplus=True, return_last_state=True)
+    assert rel_err(y, g.t("out/y")) < 1e-4
+    u, dl, A, Bm = (g.t(f"in/{n}").double() for n in ("u", "delta", "A", "B"))
+    dt = F.softplus(dl + g.t("in/delta_bias").double()[:, None])
+    x = torch.zeros(u.shape[0], u.shape[1], A.shape[1], dtype=torch.float64)
+    for t in range(u.shape[2]):
+        x = torch.exp(dt[:, :, t, None] * A[None]) * x + (dt[:, :, t] * u[:, :, t])[..., None] * Bm[:, None, :, t]
+    assert rel_err(last, x) < 1e-4
+    dpos = g.t("in/delta").abs() * 0.2 + 0.01   # positive dt without softplus (a stable recurrence)
+    y2 = selective_scan_fn(ins["u"], dpos.cuda(), ins["A"], ins["B"], ins["C"], ins["D"], delta_bias=None,
+                           delta_softplus=False)
+    t6 = [g.t(f"in/{n}").double() for n in names[:6]]
+    t6[1] = dpos.double()
+    yr = oscan.selective_scan(*t6, delta_bias=None, delta_softplus=False)
+    assert rel_err(y2, yr) < 1e-4

@@ -1,0 +1,143 @@
+#!/usr/bin/env python3
+"""Per-kernel benchmark of every liblci hot-path kernel at its BASELINE config size (HIP events, random data).
+
+Prints one JSON line per kernel with the algorithmic work per launch and the roofline fraction:
+  attention   C2/metric: B=2, H=6, L=65536, d=64            FLOPs fwd 4BHL^2d, bwd 8BHL^2d (MFMA bf16)
+  window      C3 stage 1: 128^3 p2 -> 64^3 grid, C=96, H=3, w=7, shift 3   FLOPs 4*Bw*H*N^2*32 (N=343)
+  scan        ViT-mamba 512^2 p2 (L=65536) and C5 256^3 p2 (L=2^21), Dx=192, N=8, bf16
+              bytes/token fwd 2*(3*192+16)=1184, bwd 1984
+  fftconv     ViT-hyena 512^2 p2: rows B*D = 768, L = 65536, f32 in/out: bytes/row-elem 8 fwd, 16 bwd
+  patch embed ViT p2 512^2: image 4 B/px + tokens B*L*384*4 B
+"""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from long_context_biomedical_imaging_amd import kernels  # noqa: E402
+
+MFMA = 2500.0
+HBM = 8000.0
+
+
+def timeit(fn, iters=5):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def emit(name, ms, work, unit, cfg):
+    if unit == "TFLOP/s":
+        ach = work / (ms * 1e-3) / 1e12
+        peak = MFMA
+    else:
+        ach = work / (ms * 1e-3) / 1e9
+        peak = HBM
+    print(json.dumps({"kernel": name, "ms": round(ms, 3), "achieved": round(ach, 1), "unit": unit,
+                      "peak": peak, "frac": round(ach / peak, 4), "work_per_launch": work, "config": cfg}),
+          flush=True)
+
+
+def bench_attention():
+    B, H, L = 2, 6, 65536
+    qkv = torch.randn(B, L, 3 * H * 64, device="cuda").to(torch.bfloat16)
+    dout = torch.randn(B, L, H * 64, device="cuda").to(torch.bfloat16)
+    out, lse = kernels.attn_fwd(qkv, H, 0.125)
+    f = 4.0 * B * H * L * L * 64
+    emit("attn_fwd", timeit(lambda: kernels.attn_fwd(qkv, H, 0.125)), f, "TFLOP/s", f"B{B} H{H} L{L} d64")
+    emit("attn_bwd(3 launches)", timeit(lambda: kernels.attn_bwd(qkv, out, dout, lse, H, 0.125)), 2 * f, "TFLOP/s",
+         f"B{B} H{H} L{L} d64")
+
+
+def bench_window():
+    B, S, C, H, w, sh = 2, 64, 96, 3, 7, 3
+    qkv = torch.randn(B, S, S, S, 3 * C, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    bias = torch.randn(3 * C, device="cuda") * 0.1
+    rpb = torch.randn(H, w ** 3, w ** 3, device="cuda") * 0.1
+    N = w ** 3
+    Bw = B * (-(-S // w)) ** 3
+    f = 4.0 * Bw * H * N * N * 32
+    run = lambda: kernels.window_attention_grid(qkv, bias, rpb, H, 32 ** -0.5, (w, w, w), (sh, sh, sh))  # noqa
+    emit("window_attn_fwd", timeit(lambda: run()), f, "TFLOP/s", f"Swin-tiny stage1 128^3 p2: B{B} 64^3 C{C} H{H} w7 s3")
+    o = run()
+    g = torch.randn_like(o)
+    emit("window_attn_fwd+bwd", timeit(lambda: torch.autograd.grad(run(), qkv, g)), 3 * f, "TFLOP/s",
+         "same, fwd+bwd (rpb grad off)")
+
+
+def bench_scan(L, B=2, Dx=192):
+    u = torch.randn(B, L, Dx, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    dl = (torch.randn(B, L, Dx, device="cuda") * 0.5 - 3).to(torch.bfloat16).requires_grad_(True)
+    A = -torch.rand(Dx, 8, device="cuda") - 0.5
+    xdbl = torch.randn(B, L, 40, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    D = torch.randn(Dx, device="cuda")
+    db = torch.randn(Dx, device="cuda") * 0.1
+
+    def fwd(grad=False):
+        yz = torch.empty(B, L, 2 * Dx, device="cuda", dtype=torch.bfloat16)
+        with torch.set_grad_enabled(grad):
+            return kernels.selective_scan_cl(u, dl, A, xdbl[..., 24:32], xdbl[..., 32:], D, db, yz)
+
+    emit("selective_scan_fwd", timeit(lambda: fwd(False)), 1184.0 * B * L, "GB/s", f"B{B} L{L} Dx{Dx} N8 bf16")
+    y = fwd(True)
+    gy = torch.randn_like(y)
+    kernels.KernelTimer.reset()
+    kernels.KernelTimer.enabled = True
+    for _ in range(3):
+        y = fwd(True)
+        torch.autograd.grad(y, [u, dl, xdbl], gy)
+    kernels.KernelTimer.enabled = False
+    s = kernels.KernelTimer.summary()
+    emit("selective_scan_bwd", s["selective_scan_bwd"]["avg_ms"], 1984.0 * B * L, "GB/s", f"B{B} L{L} Dx{Dx} N8 bf16")
+
+
+def bench_fftconv():
+    B, H, hd, L = 2, 6, 64, 65536
+    u = torch.randn(B * H, hd, L, device="cuda").requires_grad_(True)
+    k = (torch.randn(hd, L, device="cuda") * torch.exp(-torch.linspace(0, 8, L, device="cuda"))).requires_grad_(True)
+    D = torch.randn(hd, device="cuda").requires_grad_(True)
+    rows = B * H * hd
+    emit("fftconv_fwd", timeit(lambda: kernels.fftconv(u, k, D)), 8.0 * rows * L, "GB/s",
+         f"rows {rows} L{L} f32 (ViT-hyena 512^2 p2)")
+    y = kernels.fftconv(u, k, D)
+    g = torch.randn_like(y)
+    emit("fftconv_fwd+bwd", timeit(lambda: torch.autograd.grad(kernels.fftconv(u, k, D), [u, k, D], g)),
+         24.0 * rows * L, "GB/s", "same, fwd+bwd (u, k, D grads)")
+
+
+def bench_patch_embed():
+    B, S, D = 2, 512, 384
+    x = torch.rand(B, 1, S, S, device="cuda")
+    w = (torch.randn(D, 1, 2, 2, device="cuda") * 0.1).requires_grad_(True)
+    b = torch.zeros(D, device="cuda").requires_grad_(True)
+    pos = torch.zeros(1, (S // 2) ** 2, D, device="cuda").requires_grad_(True)
+    byt = 4.0 * B * S * S + 4.0 * B * (S // 2) ** 2 * D + 4.0 * (S // 2) ** 2 * D
+    emit("patch_embed_fwd", timeit(lambda: kernels.patch_embed(x, w, b, pos, True)), byt, "GB/s",
+         "ViT p2 512^2 -> (2, 65536, 384) f32 + pos")
+
+
+def main():
+    which = sys.argv[1:] or ["attention", "window", "scan", "fftconv", "patch"]
+    if "attention" in which:
+        bench_attention()
+    if "window" in which:
+        bench_window()
+    if "scan" in which:
+        bench_scan(65536)
+        bench_scan(1 << 21)
+    if "fftconv" in which:
+        bench_fftconv()
+    if "patch" in which:
+        bench_patch_embed()
+
+
+if __name__ == "__main__":
+    main()
