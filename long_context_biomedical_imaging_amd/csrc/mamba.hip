@@ -19,7 +19,7 @@
 namespace lci {
 
 constexpr int SCAN_N = 8;     // d_state (the reference always uses 8: backbone_vit.py:184, backbone_swin.py:329)
-constexpr int CKPT = 16;      // backward checkpoint spacing (steps)
+constexpr int CKPT = 8;       // backward checkpoint spacing (steps); sub-block states live in registers
 constexpr float LOG2E = 1.4426950408889634f;
 
 struct ScanArgs {
@@ -60,6 +60,21 @@ __device__ __forceinline__ void ld8u(const T* p, float (&v)[SCAN_N], bool aligne
   for (int n = 0; n < SCAN_N; ++n) v[n] = (float)p[n];
 }
 
+// raw B_t / C_t row (8 values): one 16-B load for bf16, two for f32; converted at use
+template <typename T> struct Row8;
+template <> struct Row8<bf16> {
+  bf16x8 v;
+  __device__ __forceinline__ void load(const bf16* p) { v = *(const bf16x8*)p; }
+  __device__ __forceinline__ float operator[](int n) const { return (float)v[n]; }
+};
+template <> struct Row8<float> {
+  f32x4 lo, hi;
+  __device__ __forceinline__ void load(const float* p) { lo = *(const f32x4*)p; hi = *(const f32x4*)(p + 4); }
+  __device__ __forceinline__ float operator[](int n) const { return n < 4 ? lo[n] : hi[n - 4]; }
+};
+
+constexpr int PF = 8;         // timesteps whose loads are issued ahead of the dependent recurrence
+
 __device__ __forceinline__ float softplus_raw(float v) { return v <= 20.f ? log1pf(__expf(v)) : v; }
 #define softplus(v) (a.softplus ? softplus_raw(v) : (v))
 
@@ -87,32 +102,41 @@ __global__ __launch_bounds__(256) void scan_fwd_kernel(ScanArgs a) {
   const T* Bp = (const T*)a.Bm + b * a.bB;
   const T* Cp = (const T*)a.Cm + b * a.bC;
   T* yp = (T*)a.y + b * a.by + dd;
-  const bool alB = ((a.tB * sizeof(T)) % 16 == 0) && (((uintptr_t)a.Bm) % 16 == 0);
-  const bool alC = ((a.tC * sizeof(T)) % 16 == 0) && (((uintptr_t)a.Cm) % 16 == 0);
   const int t0 = chunk * a.Tc, t1 = min(a.L, t0 + a.Tc);
   float sumdt = 0.f;
-  for (int t = t0; t < t1; ++t) {
-    if (MODE == 1 && a.write_ckpt && ((t & (CKPT - 1)) == 0) && valid) {
-      float* cp = a.ckpt + (((long long)b * a.nck + (t / CKPT)) * a.Dx + d) * SCAN_N;
-      *(f32x4*)cp = f32x4{x[0], x[1], x[2], x[3]};
-      *(f32x4*)(cp + 4) = f32x4{x[4], x[5], x[6], x[7]};
+  for (int tb = t0; tb < t1; tb += PF) {
+    float uf[PF], dr[PF];
+    Row8<T> Bv[PF], Cv[PF];
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {        // all loads of the group first (clamped, branch-free)
+      const long long t = min(tb + i, t1 - 1);
+      uf[i] = ldf(up + t * a.tu);
+      dr[i] = ldf(dp + t * a.td);
+      Bv[i].load(Bp + t * a.tB);
+      if (MODE == 1) Cv[i].load(Cp + t * a.tC);
     }
-    const float uf = ldf(up + (long long)t * a.tu);
-    const float dt = softplus(ldf(dp + (long long)t * a.td) + bias);
-    float Bv[SCAN_N];
-    ld8u(Bp + (long long)t * a.tB, Bv, alB);
-    const float dtu = dt * uf;
 #pragma unroll
-    for (int n = 0; n < SCAN_N; ++n) x[n] = fmaf(exp2_fast(dt * A2[n]), x[n], dtu * Bv[n]);
-    if (MODE == 1) {
-      float Cv[SCAN_N];
-      ld8u(Cp + (long long)t * a.tC, Cv, alC);
-      float yv = Dd * uf;
+    for (int i = 0; i < PF; ++i) {
+      const int t = tb + i;
+      if (t < t1) {
+        if (MODE == 1 && a.write_ckpt && ((t & (CKPT - 1)) == 0) && valid) {
+          float* cp = a.ckpt + (((long long)b * a.nck + (t / CKPT)) * a.Dx + d) * SCAN_N;
+          *(f32x4*)cp = f32x4{x[0], x[1], x[2], x[3]};
+          *(f32x4*)(cp + 4) = f32x4{x[4], x[5], x[6], x[7]};
+        }
+        const float dt = softplus(dr[i] + bias);
+        const float dtu = dt * uf[i];
 #pragma unroll
-      for (int n = 0; n < SCAN_N; ++n) yv = fmaf(Cv[n], x[n], yv);
-      if (valid) yp[(long long)t * a.ty] = (T)yv;
-    } else {
-      sumdt += dt;
+        for (int n = 0; n < SCAN_N; ++n) x[n] = fmaf(exp2_fast(dt * A2[n]), x[n], dtu * Bv[i][n]);
+        if (MODE == 1) {
+          float yv = Dd * uf[i];
+#pragma unroll
+          for (int n = 0; n < SCAN_N; ++n) yv = fmaf(Cv[i][n], x[n], yv);
+          if (valid) yp[(long long)t * a.ty] = (T)yv;
+        } else {
+          sumdt += dt;
+        }
+      }
     }
   }
   if (MODE == 0 && valid) {
@@ -135,13 +159,26 @@ __global__ __launch_bounds__(256) void scan_carry_kernel(ScanArgs a) {
   float carry = 0.f;
   const float* src = REVERSE ? a.gl : a.xend;
   float* dst = REVERSE ? a.gin : a.xinit;
-  for (int k = 0; k < a.nch; ++k) {
-    const int c = REVERSE ? a.nch - 1 - k : k;
-    const long long ci = ((long long)b * a.nch + c) * a.Dx + d;
-    const float s = a.sdt[ci];
-    const float e = src[ci * SCAN_N + n];
-    dst[ci * SCAN_N + n] = carry;
-    carry = fmaf(exp2_fast(A2 * s), carry, e);
+  for (int kb = 0; kb < a.nch; kb += PF) {
+    float sv[PF], ev[PF];
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int k = min(kb + i, a.nch - 1);
+      const int c = REVERSE ? a.nch - 1 - k : k;
+      const long long ci = ((long long)b * a.nch + c) * a.Dx + d;
+      sv[i] = a.sdt[ci];
+      ev[i] = src[ci * SCAN_N + n];
+    }
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int k = kb + i;
+      if (k < a.nch) {
+        const int c = REVERSE ? a.nch - 1 - k : k;
+        const long long ci = ((long long)b * a.nch + c) * a.Dx + d;
+        dst[ci * SCAN_N + n] = carry;
+        carry = fmaf(exp2_fast(A2 * sv[i]), carry, ev[i]);
+      }
+    }
   }
 }
 
@@ -163,15 +200,26 @@ __global__ __launch_bounds__(256) void scan_bwd_agg_kernel(ScanArgs a) {
   const T* dp = (const T*)a.delta + b * a.bd + dd;
   const T* gyp = (const T*)a.dy + b * a.bdy + dd;
   const T* Cp = (const T*)a.Cm + b * a.bC;
-  const bool alC = ((a.tC * sizeof(T)) % 16 == 0) && (((uintptr_t)a.Cm) % 16 == 0);
   const int t0 = chunk * a.Tc, t1 = min(a.L, t0 + a.Tc);
-  for (int t = t1 - 1; t >= t0; --t) {
-    const float dt = softplus(ldf(dp + (long long)t * a.td) + bias);
-    const float gy = valid ? ldf(gyp + (long long)t * a.tdy) : 0.f;
-    float Cv[SCAN_N];
-    ld8u(Cp + (long long)t * a.tC, Cv, alC);
+  for (int te = t1 - 1; te >= t0; te -= PF) {
+    float dr[PF], gyv[PF];
+    Row8<T> Cv[PF];
 #pragma unroll
-    for (int n = 0; n < SCAN_N; ++n) g[n] = exp2_fast(dt * A2[n]) * fmaf(Cv[n], gy, g[n]);
+    for (int i = 0; i < PF; ++i) {
+      const long long t = max(te - i, t0);
+      dr[i] = ldf(dp + t * a.td);
+      gyv[i] = ldf(gyp + t * a.tdy);
+      Cv[i].load(Cp + t * a.tC);
+    }
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      if (te - i >= t0) {
+        const float dt = softplus(dr[i] + bias);
+        const float gy = valid ? gyv[i] : 0.f;
+#pragma unroll
+        for (int n = 0; n < SCAN_N; ++n) g[n] = exp2_fast(dt * A2[n]) * fmaf(Cv[i][n], gy, g[n]);
+      }
+    }
   }
   if (valid) {
     float* o = a.gl + (((long long)b * a.nch + chunk) * a.Dx + d) * SCAN_N;
@@ -230,15 +278,14 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(ScanArgs a) {
   const T* Cp = (const T*)a.Cm + b * a.bC;
   T* dup = (T*)a.du + b * a.bdu + dd;
   T* ddp = (T*)a.ddelta + b * a.bdd + dd;
-  const bool alB = ((a.tB * sizeof(T)) % 16 == 0) && (((uintptr_t)a.Bm) % 16 == 0);
-  const bool alC = ((a.tC * sizeof(T)) % 16 == 0) && (((uintptr_t)a.Cm) % 16 == 0);
   const int t0 = chunk * a.Tc, t1 = min(a.L, t0 + a.Tc);
   const int nsb = (t1 - t0 + CKPT - 1) / CKPT;
   __syncthreads();
   for (int sb = nsb - 1; sb >= 0; --sb) {
     const int s0 = t0 + sb * CKPT;
-    // forward recompute of the sub-block from its checkpoint: xs[i] = x after step s0 + i
-    float xck[SCAN_N], xs[CKPT][SCAN_N];
+    // all loads of the sub-block first (clamped addresses, no branches), then the dependent math
+    float xck[SCAN_N], xs[CKPT][SCAN_N], uf[CKPT], dr[CKPT], gyv[CKPT];
+    Row8<T> Bv[CKPT], Cv[CKPT];
     {
       const float* cp = a.ckpt + (((long long)b * a.nck + s0 / CKPT) * a.Dx + dd) * SCAN_N;
       const f32x4 c0 = *(const f32x4*)cp, c1 = *(const f32x4*)(cp + 4);
@@ -247,17 +294,22 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(ScanArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < CKPT; ++i) {
-      const int t = s0 + i;
+      const long long t = min(s0 + i, t1 - 1);
+      uf[i] = ldf(up + t * a.tu);
+      dr[i] = ldf(dp + t * a.td) + bias;
+      gyv[i] = valid ? ldf(gyp + t * a.tdy) : 0.f;
+      Bv[i].load(Bp + t * a.tB);
+      Cv[i].load(Cp + t * a.tC);
+    }
+    // forward recompute of the sub-block from its checkpoint: xs[i] = x after step s0 + i
 #pragma unroll
-      for (int n = 0; n < SCAN_N; ++n) xs[i][n] = (i == 0) ? xck[n] : xs[i - 1][n];
-      if (t < t1) {
-        const float uf = ldf(up + (long long)t * a.tu);
-        const float dt = softplus(ldf(dp + (long long)t * a.td) + bias);
-        float Bv[SCAN_N];
-        ld8u(Bp + (long long)t * a.tB, Bv, alB);
-        const float dtu = dt * uf;
+    for (int i = 0; i < CKPT; ++i) {
+      const float dt = softplus(dr[i]);
+      const float dtu = dt * uf[i];
 #pragma unroll
-        for (int n = 0; n < SCAN_N; ++n) xs[i][n] = fmaf(exp2_fast(dt * A2[n]), xs[i][n], dtu * Bv[n]);
+      for (int n = 0; n < SCAN_N; ++n) {
+        const float xp = (i == 0) ? xck[n] : xs[i - 1][n];
+        xs[i][n] = fmaf(exp2_fast(dt * A2[n]), xp, dtu * Bv[i][n]);
       }
     }
     // reverse sweep
@@ -265,25 +317,22 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(ScanArgs a) {
     for (int i = CKPT - 1; i >= 0; --i) {
       const int t = s0 + i;
       if (t < t1) {
-        const float uf = ldf(up + (long long)t * a.tu);
-        const float draw = ldf(dp + (long long)t * a.td) + bias;
+        const float draw = dr[i];
         const float dt = softplus(draw);
-        const float gy = valid ? ldf(gyp + (long long)t * a.tdy) : 0.f;
-        float Bv[SCAN_N], Cv[SCAN_N], v[16];
-        ld8u(Bp + (long long)t * a.tB, Bv, alB);
-        ld8u(Cp + (long long)t * a.tC, Cv, alC);
+        const float gy = gyv[i];
+        float v[16];
         float du = Dd * gy, ddt = 0.f;
-        const float dtu = dt * uf;
+        const float dtu = dt * uf[i];
 #pragma unroll
         for (int n = 0; n < SCAN_N; ++n) {
           const float xp = (i == 0) ? xck[n] : xs[i - 1][n];
           const float at = exp2_fast(dt * A2[n]);
-          const float gt = fmaf(Cv[n], gy, h[n]);
+          const float gt = fmaf(Cv[i][n], gy, h[n]);
           v[SCAN_N + n] = gy * xs[i][n];                  // dC_t partial
           v[n] = gt * dtu;                                // dB_t partial
-          du = fmaf(gt * dt, Bv[n], du);
+          du = fmaf(gt * dt, Bv[i][n], du);
           const float gxa = gt * xp * at;
-          ddt = fmaf(gt, Bv[n] * uf, fmaf(gxa, A1[n], ddt));
+          ddt = fmaf(gt, Bv[i][n] * uf[i], fmaf(gxa, A1[n], ddt));
           dA[n] = fmaf(gxa, dt, dA[n]);
           h[n] = at * gt;
         }
@@ -293,7 +342,7 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(ScanArgs a) {
         }
         const float sg = (a.softplus && draw <= 20.f) ? 1.f / (1.f + __expf(-draw)) : 1.f;
         const float ddl = ddt * sg;
-        dDacc = fmaf(gy, uf, dDacc);
+        dDacc = fmaf(gy, uf[i], dDacc);
         dbacc += ddl;
         if (valid) {
           dup[(long long)t * a.tdu] = (T)du;
@@ -418,6 +467,13 @@ static int scan_fill(ScanArgs& a, int B, int L, int Dx, int N, int Tc) {
 }
 
 // strides: array of 16 long long: [bu,tu, bd,td, bB,tB, bC,tC, by,ty, bdy,tdy, bdu,tdu, bdd,tdd] (elements)
+static int scan_check_bc(const void* Bm, const void* Cm, long long tB, long long tC, int dtype) {
+  const long long es = dtype == 1 ? 2 : 4;
+  LCI_CHECK(((uintptr_t)Bm) % 16 == 0 && ((uintptr_t)Cm) % 16 == 0 && (tB * es) % 16 == 0 && (tC * es) % 16 == 0,
+            "selective_scan: B/C rows must be 16-byte aligned");
+  return 0;
+}
+
 static void scan_strides(ScanArgs& a, const long long* s) {
   a.bu = s[0]; a.tu = (int)s[1]; a.bd = s[2]; a.td = (int)s[3]; a.bB = s[4]; a.tB = (int)s[5];
   a.bC = s[6]; a.tC = (int)s[7]; a.by = s[8]; a.ty = (int)s[9]; a.bdy = s[10]; a.tdy = (int)s[11];
@@ -434,6 +490,7 @@ extern "C" int lci_selective_scan_fwd(int dtype, const void* u, const void* delt
   if (scan_fill(a, B, L, Dx, N, chunk)) return 1;
   a.softplus = delta_softplus;
   scan_strides(a, strides);
+  if (scan_check_bc(Bm, Cm, strides[5], strides[7], dtype)) return 1;
   a.u = u; a.delta = delta; a.A = A; a.Bm = Bm; a.Cm = Cm; a.D = D; a.dbias = delta_bias; a.y = y;
   a.xend = xend; a.xinit = xinit; a.sdt = sdt; a.ckpt = ckpt; a.write_ckpt = ckpt != nullptr;
   hipStream_t s = (hipStream_t)stream;
@@ -462,6 +519,7 @@ extern "C" int lci_selective_scan_bwd(int dtype, const void* u, const void* delt
   if (scan_fill(a, B, L, Dx, N, chunk)) return 1;
   a.softplus = delta_softplus;
   scan_strides(a, strides);
+  if (scan_check_bc(Bm, Cm, strides[5], strides[7], dtype)) return 1;
   a.u = u; a.delta = delta; a.A = A; a.Bm = Bm; a.Cm = Cm; a.D = D; a.dbias = delta_bias; a.dy = dy;
   a.du = du; a.ddelta = ddelta; a.dBC = dBC; a.dA = dA; a.dD = dD; a.ddbias = ddelta_bias;
   a.sdt = (float*)sdt; a.ckpt = (float*)ckpt; a.gl = gl; a.gin = gin;

@@ -178,7 +178,7 @@ def patch_embed(x, weight, bias, pos, channels_last_tokens: bool):
 
 # ----------------------------------------------------------------------------------------- mamba
 SCAN_N = 8
-CKPT = 16
+CKPT = 8          # = csrc/mamba.hip CKPT (backward checkpoint spacing)
 
 
 def _ll_array(vals):
@@ -186,9 +186,12 @@ def _ll_array(vals):
     return (ctypes.c_longlong * len(vals))(*vals)
 
 
-def _scan_chunk(L):
-    """Chunk length: >= 256 steps, at most ~512 chunks per sequence (the carry passes are sequential)."""
-    tc = max(256, -(-L // 512))
+def _scan_chunk(L, B=1, Dx=64):
+    """Chunk length (multiple of CKPT): enough chunks for ~8K waves in flight (B * ceil(Dx/64) waves per chunk),
+    at least 64 steps per chunk and at most 4096 chunks (the carry passes walk the chunks sequentially)."""
+    waves_per_chunk = B * (-(-Dx // 64))
+    target = max(1, 8192 // waves_per_chunk)
+    tc = max(64, -(-L // target), -(-L // 4096))
     return -(-tc // CKPT) * CKPT
 
 
@@ -257,7 +260,7 @@ class _SelectiveScanCL(torch.autograd.Function):
         B, L, Dx = u.shape
         N = A.shape[1]
         dt = u.dtype
-        tc = _scan_chunk(L)
+        tc = _scan_chunk(L, B, Dx)
         nch = -(-L // tc)
         nck = -(-L // CKPT)
         f32 = dict(device=u.device, dtype=torch.float32)
