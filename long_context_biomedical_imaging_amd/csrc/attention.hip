@@ -129,10 +129,16 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s1[i]);
     mx = wave_max_xor32(mx);
-    const float m_new = fmaxf(m_run, mx);
-    const float alpha = exp2_fast((m_run - m_new) * c);
-    m_run = m_new;
-    const float mc = m_new * c;
+    // Rescale only when some row's running max grew (wave-uniform vote). Exact: otherwise alpha == 1.
+    if (__any(mx > m_run)) {
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha = exp2_fast((m_run - m_new) * c);
+      m_run = m_new;
+      l_run *= alpha;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { o0[i] *= alpha; o1[i] *= alpha; }
+    }
+    const float mc = m_run * c;
     float ls = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -140,9 +146,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
       s1[i] = exp2_fast(fmaf(s1[i], c, -mc));
       ls += s0[i] + s1[i];
     }
-    l_run = l_run * alpha + ls;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) { o0[i] *= alpha; o1[i] *= alpha; }
+    l_run += ls;
     const bf16x8 p00 = pack8<0>(s0), p01 = pack8<1>(s0), p10 = pack8<0>(s1), p11 = pack8<1>(s1);
     // O^T[d][q] += V^T[d][key] P^T[key][q]
     o0 = mfma32(frag_tr<0>(vl, LD_TR, 0, 0, lane), p00, o0);
@@ -201,7 +205,7 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnArgs a) {
 
 // ---------------------------------------------------------------------- backward: dK, dV kernel
 template <int NW>
-__global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv_kernel(AttnArgs a) {
+__global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dkdv_kernel(AttnArgs a) {
   constexpr int NT = NW * 64;
   constexpr int TILE = 2 * KT * LD_ROW;                 // Q tile + dO tile (both read by rows and transposed)
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * TILE];
@@ -262,50 +266,38 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv_kernel(AttnArgs a) {
       qr.load(qp, a.rs_q, (qt + 1) * KT, L, tid);
       dr.load(dop, a.rs_do, (qt + 1) * KT, L, tid);
     }
-    // S[q][key] and dP[q][key] for query sub-tiles 0..31 / 32..63; key on the lane
-    f32x16 s0 = {}, s1 = {}, p0 = {}, p1 = {};
+    // Two 32-query halves per 64-query tile (halves the live S/dP/P/dS registers); key on the lane.
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      s0 = mfma32(frag_row(ql, LD_ROW, 0, ks * 16, lane), kf[ks], s0);
-      s1 = mfma32(frag_row(ql, LD_ROW, 32, ks * 16, lane), kf[ks], s1);
-      p0 = mfma32(frag_row(dl, LD_ROW, 0, ks * 16, lane), vf[ks], p0);
-      p1 = mfma32(frag_row(dl, LD_ROW, 32, ks * 16, lane), vf[ks], p1);
-    }
-    // P = exp2(S c - lse2[q]); dS = P (dP - delta[q]); q index = (i&3) + 8(i>>2) + 4h (+32)
+    for (int qs = 0; qs < 2; ++qs) {
+      f32x16 s = {}, p = {};
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const f32x4 la = *(const f32x4*)&rowc[buf][0][8 * g + 4 * half];
-      const f32x4 lb = *(const f32x4*)&rowc[buf][0][32 + 8 * g + 4 * half];
-      const f32x4 da = *(const f32x4*)&rowc[buf][1][8 * g + 4 * half];
-      const f32x4 db = *(const f32x4*)&rowc[buf][1][32 + 8 * g + 4 * half];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int i = 4 * g + j;
-        s0[i] = exp2_fast(fmaf(s0[i], c, -la[j]));
-        s1[i] = exp2_fast(fmaf(s1[i], c, -lb[j]));
-        p0[i] = s0[i] * (p0[i] - da[j]);
-        p1[i] = s1[i] * (p1[i] - db[j]);
+      for (int ks = 0; ks < 4; ++ks) {
+        s = mfma32(frag_row(ql, LD_ROW, qs * 32, ks * 16, lane), kf[ks], s);
+        p = mfma32(frag_row(dl, LD_ROW, qs * 32, ks * 16, lane), vf[ks], p);
       }
+      // P = exp2(S c - lse2[q]); dS = P (dP - delta[q]); q = qs*32 + (i&3) + 8(i>>2) + 4h
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 la = *(const f32x4*)&rowc[buf][0][qs * 32 + 8 * g + 4 * half];
+        const f32x4 da = *(const f32x4*)&rowc[buf][1][qs * 32 + 8 * g + 4 * half];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int i = 4 * g + j;
+          s[i] = exp2_fast(fmaf(s[i], c, -la[j]));
+          p[i] = s[i] * (p[i] - da[j]);
+        }
+      }
+      const bf16x8 P0 = pack8<0>(s), P1 = pack8<1>(s), D0 = pack8<0>(p), D1 = pack8<1>(p);
+      // dV^T[d][key] += dO^T[d][q] P[q][key] ; dK^T[d][key] += Q^T[d][q] dS[q][key]
+      dv0 = mfma32(frag_tr<0>(dl, LD_ROW, qs * 32, 0, lane), P0, dv0);
+      dv0 = mfma32(frag_tr<1>(dl, LD_ROW, qs * 32, 0, lane), P1, dv0);
+      dv1 = mfma32(frag_tr<0>(dl, LD_ROW, qs * 32, 32, lane), P0, dv1);
+      dv1 = mfma32(frag_tr<1>(dl, LD_ROW, qs * 32, 32, lane), P1, dv1);
+      dk0 = mfma32(frag_tr<0>(ql, LD_ROW, qs * 32, 0, lane), D0, dk0);
+      dk0 = mfma32(frag_tr<1>(ql, LD_ROW, qs * 32, 0, lane), D1, dk0);
+      dk1 = mfma32(frag_tr<0>(ql, LD_ROW, qs * 32, 32, lane), D0, dk1);
+      dk1 = mfma32(frag_tr<1>(ql, LD_ROW, qs * 32, 32, lane), D1, dk1);
     }
-    const bf16x8 P00 = pack8<0>(s0), P01 = pack8<1>(s0), P10 = pack8<0>(s1), P11 = pack8<1>(s1);
-    const bf16x8 D00 = pack8<0>(p0), D01 = pack8<1>(p0), D10 = pack8<0>(p1), D11 = pack8<1>(p1);
-    // dV^T[d][key] += dO^T[d][q] P[q][key] ; dK^T[d][key] += Q^T[d][q] dS[q][key]
-    dv0 = mfma32(frag_tr<0>(dl, LD_ROW, 0, 0, lane), P00, dv0);
-    dv0 = mfma32(frag_tr<1>(dl, LD_ROW, 0, 0, lane), P01, dv0);
-    dv0 = mfma32(frag_tr<0>(dl, LD_ROW, 32, 0, lane), P10, dv0);
-    dv0 = mfma32(frag_tr<1>(dl, LD_ROW, 32, 0, lane), P11, dv0);
-    dv1 = mfma32(frag_tr<0>(dl, LD_ROW, 0, 32, lane), P00, dv1);
-    dv1 = mfma32(frag_tr<1>(dl, LD_ROW, 0, 32, lane), P01, dv1);
-    dv1 = mfma32(frag_tr<0>(dl, LD_ROW, 32, 32, lane), P10, dv1);
-    dv1 = mfma32(frag_tr<1>(dl, LD_ROW, 32, 32, lane), P11, dv1);
-    dk0 = mfma32(frag_tr<0>(ql, LD_ROW, 0, 0, lane), D00, dk0);
-    dk0 = mfma32(frag_tr<1>(ql, LD_ROW, 0, 0, lane), D01, dk0);
-    dk0 = mfma32(frag_tr<0>(ql, LD_ROW, 32, 0, lane), D10, dk0);
-    dk0 = mfma32(frag_tr<1>(ql, LD_ROW, 32, 0, lane), D11, dk0);
-    dk1 = mfma32(frag_tr<0>(ql, LD_ROW, 0, 32, lane), D00, dk1);
-    dk1 = mfma32(frag_tr<1>(ql, LD_ROW, 0, 32, lane), D01, dk1);
-    dk1 = mfma32(frag_tr<0>(ql, LD_ROW, 32, 32, lane), D10, dk1);
-    dk1 = mfma32(frag_tr<1>(ql, LD_ROW, 32, 32, lane), D11, dk1);
     if (qt + 1 < nqt) {
       bf16* nb = smem + (buf ^ 1) * TILE;
       qr.store(nb, LD_ROW, tid);
