@@ -21,6 +21,11 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
          "-munsafe-fp-atomics"]
+# Device code: MFMA accumulators in ordinary VGPRs (gfx950's unified register file) instead of AGPRs, which
+# otherwise cost v_accvgpr_read/write copies around every softmax rescale and lower occupancy.
+DEVICE_FLAGS = ["-Xarch_device", "-mllvm=-amdgpu-mfma-vgpr-form"]
+# Softmax kernels: no NaN-quieting canonicalisation (v_max x,x) in front of every fmaxf on MFMA results.
+FILE_FLAGS = {"attention.hip": ["-fno-honor-nans"], "window.hip": ["-fno-honor-nans"]}
 
 
 def sources():
@@ -35,7 +40,7 @@ def _stale(src, obj):
     if not os.path.exists(obj):
         return True
     t = os.path.getmtime(obj)
-    deps = [src] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".hpp")]
+    deps = [src, os.path.abspath(__file__)] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".hpp")]
     return any(os.path.getmtime(d) > t for d in deps)
 
 
@@ -43,7 +48,8 @@ def _compile(src, force):
     obj = _obj(src)
     if not force and not _stale(src, obj):
         return obj, None
-    cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj]
+    cmd = [HIPCC, *FLAGS, *(DEVICE_FLAGS if src.endswith(".hip") else []), *FILE_FLAGS.get(os.path.basename(src), []),
+           "-c", src, "-o", obj]
     if src.endswith(".cpp"):
         cmd = [HIPCC, "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)

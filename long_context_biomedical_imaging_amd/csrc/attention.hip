@@ -16,6 +16,8 @@
 //            No atomics: results are bitwise reproducible.
 #include "common.hpp"
 
+#include <type_traits>
+
 namespace lci {
 
 constexpr int DH = 64;        // head dim (ViT-small/base: 384/6, 768/12)
@@ -44,13 +46,15 @@ template <int NT>
 struct TileRegs {
   static constexpr int PASSES = (KT * DH * 2) / (NT * 16);
   u32x4 r[PASSES];
+  // GUARD=false: the caller knows rows row0..row0+63 are all < L (full tiles: no exec-masked branches).
+  template <bool GUARD = true>
   __device__ __forceinline__ void load(const bf16* base, int rs, int row0, int L, int tid) {
 #pragma unroll
     for (int p = 0; p < PASSES; ++p) {
       const int idx = p * NT + tid;
       const int row = idx >> 3, ch = idx & 7;
       const int g = row0 + row;
-      if (g < L) r[p] = *(const u32x4*)(base + (long long)g * rs + ch * 8);
+      if (!GUARD || g < L) r[p] = *(const u32x4*)(base + (long long)g * rs + ch * 8);
       else r[p] = u32x4{0u, 0u, 0u, 0u};
     }
   }
@@ -81,12 +85,18 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
   const bf16* kp = a.k + b * a.bs_k + hh * a.hs;
   const bf16* vp = a.v + b * a.bs_v + hh * a.hs;
 
-  // Q^T as the B operand: lane (query r, half h) holds Q[q][16ks + 8h .. +7]
+  // Q^T as the B operand: lane (query r, half h) holds Q[q][16ks + 8h .. +7], prescaled by c = scale*log2(e)
+  // (one bf16 rounding, the same size as the reference's bf16 score rounding under autocast), so the
+  // MFMA chain yields scores directly in the exp2 domain.
+  const float c = a.c;
   bf16x8 qf[4];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
-    if (qrow < L) qf[ks] = *(const bf16x8*)(qp + (long long)qrow * a.rs_q + ks * 16 + 8 * half);
-    else qf[ks] = bf16x8{};
+    bf16x8 t{};
+    if (qrow < L) t = *(const bf16x8*)(qp + (long long)qrow * a.rs_q + ks * 16 + 8 * half);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = to_bf16(to_f32(t[j]) * c);
+    qf[ks] = t;
   }
 
   TileRegs<NT> kr, vr;
@@ -97,25 +107,34 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
   vr.store(smem + KT * LD_ROW, LD_TR, tid);
   __syncthreads();
 
-  f32x16 o0 = {}, o1 = {};
-  float m_run = NEG_BIG, l_run = 0.f;
-  const float c = a.c;
+  // Running max m (exp2 domain) enters the score MFMA chain as its initial accumulator: S' = S - m comes
+  // out of the MFMAs, so the common tile needs no per-score subtract, only exp2 (VALU is this loop's
+  // bound, not the matrix pipe). m starts at 0; the first tile always re-bases.
+  f32x16 o0 = {}, o1 = {}, negm = {};
+  float m_run = 0.f, l_run = 0.f;
 
-  for (int kt = 0; kt < nkt; ++kt) {
+  // Full tiles run without any key-bound code; only the ragged last tile masks (compile-time flag,
+  // otherwise the compiler if-converts the mask into 64 selects per tile).
+  const int nfull = L / KT;
+  auto tile = [&](const int kt, auto ragged) {
     const bf16* kl = smem + (kt & 1) * STAGE;
     const bf16* vl = kl + KT * LD_ROW;
-    if (kt + 1 < nkt) {
+    if (kt + 1 < nfull) {
+      kr.template load<false>(kp, a.rs_k, (kt + 1) * KT, L, tid);
+      vr.template load<false>(vp, a.rs_v, (kt + 1) * KT, L, tid);
+    } else if (kt + 1 < nkt) {
       kr.load(kp, a.rs_k, (kt + 1) * KT, L, tid);
       vr.load(vp, a.rs_v, (kt + 1) * KT, L, tid);
     }
-    // S^T tiles: keys 0..31 and 32..63 of this tile (rows), queries on lanes
-    f32x16 s0 = {}, s1 = {};
+    // S'^T tiles: keys 0..31 and 32..63 of this tile (rows), queries on lanes
+    f32x16 s0 = mfma32(frag_row(kl, LD_ROW, 0, 0, lane), qf[0], negm);
+    f32x16 s1 = mfma32(frag_row(kl, LD_ROW, 32, 0, lane), qf[0], negm);
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
+    for (int ks = 1; ks < 4; ++ks) {
       s0 = mfma32(frag_row(kl, LD_ROW, 0, ks * 16, lane), qf[ks], s0);
       s1 = mfma32(frag_row(kl, LD_ROW, 32, ks * 16, lane), qf[ks], s1);
     }
-    if ((kt + 1) * KT > L) {  // ragged last tile: mask keys >= L
+    if constexpr (decltype(ragged)::value) {  // ragged last tile: mask keys >= L
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int key = kt * KT + (i & 3) + 8 * (i >> 2) + 4 * half;
@@ -123,30 +142,43 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
         if (key + 32 >= L) s1[i] = NEG_BIG;
       }
     }
-    float mx = s0[0];
+    // row max of S' as four independent chains (latency), then across the two lane halves
+    float mq[4] = {fmaxf(s0[0], s0[1]), fmaxf(s0[2], s0[3]), fmaxf(s1[0], s1[1]), fmaxf(s1[2], s1[3])};
 #pragma unroll
-    for (int i = 1; i < 16; ++i) mx = fmaxf(mx, s0[i]);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s1[i]);
-    mx = wave_max_xor32(mx);
-    // Rescale only when some row's running max grew (wave-uniform vote). Exact: otherwise alpha == 1.
-    if (__any(mx > m_run)) {
-      const float m_new = fmaxf(m_run, mx);
-      const float alpha = exp2_fast((m_run - m_new) * c);
-      m_run = m_new;
-      l_run *= alpha;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) { o0[i] *= alpha; o1[i] *= alpha; }
+    for (int i = 4; i < 16; i += 4) {
+      mq[0] = fmaxf(mq[0], fmaxf(s0[i], s0[i + 1]));
+      mq[1] = fmaxf(mq[1], fmaxf(s0[i + 2], s0[i + 3]));
+      mq[2] = fmaxf(mq[2], fmaxf(s1[i], s1[i + 1]));
+      mq[3] = fmaxf(mq[3], fmaxf(s1[i + 2], s1[i + 3]));
     }
-    const float mc = m_run * c;
-    float ls = 0.f;
+    const float mx = wave_max_xor32(fmaxf(fmaxf(mq[0], mq[1]), fmaxf(mq[2], mq[3])));
+    // Re-base only when some row's max grew (wave-uniform vote; exact, since otherwise alpha == 1).
+    if (kt == 0 || __any(mx > 0.f)) {
+      const float d = (kt == 0) ? mx : fmaxf(mx, 0.f);
+      m_run += d;
+      if (kt != 0) {
+        const float alpha = exp2_fast(-d);
+        l_run *= alpha;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { o0[i] *= alpha; o1[i] *= alpha; }
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { s0[i] -= d; s1[i] -= d; negm[i] = -m_run; }
+    }
+    float lq[4];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      s0[i] = exp2_fast(fmaf(s0[i], c, -mc));
-      s1[i] = exp2_fast(fmaf(s1[i], c, -mc));
-      ls += s0[i] + s1[i];
+      s0[i] = exp2_fast(s0[i]);
+      s1[i] = exp2_fast(s1[i]);
+      if (i < 2) {
+        lq[2 * i] = s0[i];
+        lq[2 * i + 1] = s1[i];
+      } else {
+        lq[(i & 1) * 2] += s0[i];
+        lq[(i & 1) * 2 + 1] += s1[i];
+      }
     }
-    l_run += ls;
+    l_run += (lq[0] + lq[1]) + (lq[2] + lq[3]);
     const bf16x8 p00 = pack8<0>(s0), p01 = pack8<1>(s0), p10 = pack8<0>(s1), p11 = pack8<1>(s1);
     // O^T[d][q] += V^T[d][key] P^T[key][q]
     o0 = mfma32(frag_tr<0>(vl, LD_TR, 0, 0, lane), p00, o0);
@@ -163,7 +195,9 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
       vr.store(nb + KT * LD_ROW, LD_TR, tid);
     }
     __syncthreads();
-  }
+  };
+  for (int kt = 0; kt < nfull; ++kt) tile(kt, std::false_type{});
+  if (nfull < nkt) tile(nfull, std::true_type{});
 
   const float l_tot = wave_sum_xor32(l_run);
   const float inv = 1.f / l_tot;
@@ -180,7 +214,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
       *(bf16x4*)(op + 8 * g + 4 * half) = w0;
       *(bf16x4*)(op + 32 + 8 * g + 4 * half) = w1;
     }
-    if (half == 0) a.lse2[((long long)b * a.H + hh) * L + qrow] = m_run * c + __log2f(l_tot);
+    if (half == 0) a.lse2[((long long)b * a.H + hh) * L + qrow] = m_run + __log2f(l_tot);
   }
 }
 
@@ -235,6 +269,8 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dkdv_kernel(AttnArgs a) {
         kf[ks] = bf16x8{};
         vf[ks] = bf16x8{};
       }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) kf[ks][j] = to_bf16(to_f32(kf[ks][j]) * a.c);  // scores in the exp2 domain
     }
   }
 
@@ -243,9 +279,9 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dkdv_kernel(AttnArgs a) {
   auto stage_rowc = [&](int buf, int qt) {
     if (tid < 2 * KT) {
       const int which = tid / KT, qi = tid % KT, q = qt * KT + qi;
-      float v;
-      if (which == 0) v = (q < L) ? lsep[q] : 1.0e30f;  // invalid rows: P = exp2(-huge) = 0
-      else v = (q < L) ? dlp[q] : 0.f;
+      float v;  // stored negated: they are the initial accumulators of the S and dP MFMA chains
+      if (which == 0) v = (q < L) ? -lsep[q] : -1.0e30f;  // invalid rows: P = exp2(-huge) = 0
+      else v = (q < L) ? -dlp[q] : 0.f;
       rowc[buf][which][qi] = v;
     }
   };
@@ -269,23 +305,28 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dkdv_kernel(AttnArgs a) {
     // Two 32-query halves per 64-query tile (halves the live S/dP/P/dS registers); key on the lane.
 #pragma unroll
     for (int qs = 0; qs < 2; ++qs) {
-      f32x16 s = {}, p = {};
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        s = mfma32(frag_row(ql, LD_ROW, qs * 32, ks * 16, lane), kf[ks], s);
-        p = mfma32(frag_row(dl, LD_ROW, qs * 32, ks * 16, lane), vf[ks], p);
-      }
-      // P = exp2(S c - lse2[q]); dS = P (dP - delta[q]); q = qs*32 + (i&3) + 8(i>>2) + 4h
+      // Row constants as the initial accumulators (q = qs*32 + (i&3) + 8(i>>2) + 4h): the chains give
+      // S c - lse2[q] and dP - delta[q] directly; then P = exp2(.), dS = P (dP - delta).
+      f32x16 s, p;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const f32x4 la = *(const f32x4*)&rowc[buf][0][qs * 32 + 8 * g + 4 * half];
         const f32x4 da = *(const f32x4*)&rowc[buf][1][qs * 32 + 8 * g + 4 * half];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int i = 4 * g + j;
-          s[i] = exp2_fast(fmaf(s[i], c, -la[j]));
-          p[i] = s[i] * (p[i] - da[j]);
+          s[4 * g + j] = la[j];
+          p[4 * g + j] = da[j];
         }
+      }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        s = mfma32(frag_row(ql, LD_ROW, qs * 32, ks * 16, lane), kf[ks], s);
+        p = mfma32(frag_row(dl, LD_ROW, qs * 32, ks * 16, lane), vf[ks], p);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        s[i] = exp2_fast(s[i]);
+        p[i] = s[i] * p[i];
       }
       const bf16x8 P0 = pack8<0>(s), P1 = pack8<1>(s), D0 = pack8<0>(p), D1 = pack8<1>(p);
       // dV^T[d][key] += dO^T[d][q] P[q][key] ; dK^T[d][key] += Q^T[d][q] dS[q][key]
@@ -357,6 +398,8 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnArgs a) {
         qf[ks] = bf16x8{};
         df[ks] = bf16x8{};
       }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[ks][j] = to_bf16(to_f32(qf[ks][j]) * a.c);  // scores in the exp2 domain
     }
     if (qrow < L) {
       lse2 = a.lse2[((long long)b * a.H + hh) * L + qrow];
@@ -373,8 +416,11 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnArgs a) {
   __syncthreads();
 
   f32x16 dq0 = {}, dq1 = {};
-  const float c = a.c;
-  for (int kt = 0; kt < nkt; ++kt) {
+  // -lse2 and -delta of this lane's query as the (constant) initial accumulators of the S^T / dP^T chains
+  f32x16 neg_lse, neg_dlt;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { neg_lse[i] = -lse2; neg_dlt[i] = -dlt; }
+  auto tile = [&](const int kt, auto ragged) {
     const int buf = kt & 1;
     const bf16* kl = smem + buf * TILE;
     const bf16* vl = kl + KT * LD_ROW;
@@ -382,26 +428,28 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnArgs a) {
       kr.load(kp, a.rs_k, (kt + 1) * KT, L, tid);
       vr.load(vp, a.rs_v, (kt + 1) * KT, L, tid);
     }
-    f32x16 s0 = {}, s1 = {}, p0 = {}, p1 = {};
+    f32x16 s0 = mfma32(frag_row(kl, LD_ROW, 0, 0, lane), qf[0], neg_lse);
+    f32x16 s1 = mfma32(frag_row(kl, LD_ROW, 32, 0, lane), qf[0], neg_lse);
+    f32x16 p0 = mfma32(frag_row(vl, LD_ROW, 0, 0, lane), df[0], neg_dlt);
+    f32x16 p1 = mfma32(frag_row(vl, LD_ROW, 32, 0, lane), df[0], neg_dlt);
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
+    for (int ks = 1; ks < 4; ++ks) {
       s0 = mfma32(frag_row(kl, LD_ROW, 0, ks * 16, lane), qf[ks], s0);
       s1 = mfma32(frag_row(kl, LD_ROW, 32, ks * 16, lane), qf[ks], s1);
       p0 = mfma32(frag_row(vl, LD_ROW, 0, ks * 16, lane), df[ks], p0);
       p1 = mfma32(frag_row(vl, LD_ROW, 32, ks * 16, lane), df[ks], p1);
     }
-    const bool ragged = (kt + 1) * KT > L;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      float e0 = exp2_fast(fmaf(s0[i], c, -lse2));
-      float e1 = exp2_fast(fmaf(s1[i], c, -lse2));
-      if (ragged) {
+      float e0 = exp2_fast(s0[i]);
+      float e1 = exp2_fast(s1[i]);
+      if constexpr (decltype(ragged)::value) {
         const int key = kt * KT + (i & 3) + 8 * (i >> 2) + 4 * half;
         if (key >= L) e0 = 0.f;
         if (key + 32 >= L) e1 = 0.f;
       }
-      s0[i] = e0 * (p0[i] - dlt);
-      s1[i] = e1 * (p1[i] - dlt);
+      s0[i] = e0 * p0[i];
+      s1[i] = e1 * p1[i];
     }
     const bf16x8 D00 = pack8<0>(s0), D01 = pack8<1>(s0), D10 = pack8<0>(s1), D11 = pack8<1>(s1);
     // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
@@ -419,7 +467,10 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnArgs a) {
       vr.store(nb + KT * LD_ROW, LD_ROW, tid);
     }
     __syncthreads();
-  }
+  };
+  const int nfull = L / KT;
+  for (int kt = 0; kt < nfull; ++kt) tile(kt, std::false_type{});
+  if (nfull < nkt) tile(nfull, std::true_type{});
   if (qrow < L) {
     bf16* dqp = a.out + b * a.bs_out + (long long)qrow * a.rs_out + hh * a.hs;
     const float sc = a.scale;

@@ -66,8 +66,15 @@ __device__ __forceinline__ bf16x8 frag_row(const bf16* tile, int ld, int r0, int
   return *(const bf16x8*)(tile + (r0 + (lane & 31)) * ld + c0 + 8 * (lane >> 5));
 }
 
-__device__ __forceinline__ float wave_max_xor32(float v) { return fmaxf(v, __shfl_xor(v, 32)); }
-__device__ __forceinline__ float wave_sum_xor32(float v) { return v + __shfl_xor(v, 32); }
+// Combine lane l with lane l^32 (the two halves of a 32x32 MFMA column): one v_permlane32_swap, no LDS.
+__device__ __forceinline__ float wave_max_xor32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float wave_sum_xor32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 
 }  // namespace lci
 

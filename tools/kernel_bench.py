@@ -55,6 +55,16 @@ def bench_attention():
     emit("attn_fwd", timeit(lambda: kernels.attn_fwd(qkv, H, 0.125)), f, "TFLOP/s", f"B{B} H{H} L{L} d64")
     emit("attn_bwd(3 launches)", timeit(lambda: kernels.attn_bwd(qkv, out, dout, lse, H, 0.125)), 2 * f, "TFLOP/s",
          f"B{B} H{H} L{L} d64")
+    kernels.KernelTimer.reset()
+    kernels.KernelTimer.enabled = True
+    for _ in range(3):
+        kernels.attn_bwd(qkv, out, dout, lse, H, 0.125)
+    kernels.KernelTimer.enabled = False
+    for name, d in kernels.KernelTimer.summary().items():
+        if d["work_per_call"]:
+            emit(name, d["avg_ms"], d["work_per_call"], "TFLOP/s", f"B{B} H{H} L{L} d64 (MFMA FLOPs of this stage)")
+        else:
+            print(json.dumps({"kernel": name, "ms": round(d["avg_ms"], 3)}), flush=True)
 
 
 def bench_window():
