@@ -29,8 +29,9 @@ SIGNATURES = {
     "lci_selective_scan_fwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "lci_selective_scan_bwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I,
                                _I, _P, _P, _P, _P, _P],
-    "lci_window_attn_fwd": [_P, _P, _P, _P, _P, _P, _P, _F, _P],
-    "lci_window_attn_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P],
+    "lci_window_bias": [_P, _P, _P, _P, _P, _P],
+    "lci_window_attn_fwd": [_P, _P, _P, _I, _P, _P, _P, _F, _P],
+    "lci_window_attn_bwd": [_P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P],
     "lci_fft_twiddles": [_P, _I, _P],
     "lci_fftconv_spectrum": [_P, _P, _P, _P, _I, _I, _P],
     "lci_fftconv_fwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
@@ -63,6 +64,8 @@ def load(path: str = LIB_PATH):
     lib.lci_abi_version.restype = ctypes.c_int
     lib.lci_window_dS_elems.restype = ctypes.c_longlong
     lib.lci_window_dS_elems.argtypes = [_P]
+    lib.lci_window_bias_elems.restype = ctypes.c_longlong
+    lib.lci_window_bias_elems.argtypes = [_P, _I]
     lib.lci_fft_size.restype = ctypes.c_longlong
     lib.lci_fft_size.argtypes = [_I]
     for name, argt in SIGNATURES.items():

@@ -24,8 +24,9 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-re
 # Device code: MFMA accumulators in ordinary VGPRs (gfx950's unified register file) instead of AGPRs, which
 # otherwise cost v_accvgpr_read/write copies around every softmax rescale and lower occupancy.
 DEVICE_FLAGS = ["-Xarch_device", "-mllvm=-amdgpu-mfma-vgpr-form"]
-# Softmax kernels: no NaN-quieting canonicalisation (v_max x,x) in front of every fmaxf on MFMA results.
-FILE_FLAGS = {"attention.hip": ["-fno-honor-nans"], "window.hip": ["-fno-honor-nans"]}
+# Softmax kernels: no NaN-quieting canonicalisation (v_max x,x) in front of every fmaxf on MFMA results;
+# attention: no SLP packing of f32 multiplies into v_pk_mul_f32 (needs aligned pairs -> moves + alignbit).
+FILE_FLAGS = {"attention.hip": ["-fno-honor-nans", "-fno-slp-vectorize"], "window.hip": ["-fno-honor-nans"]}
 
 
 def sources():

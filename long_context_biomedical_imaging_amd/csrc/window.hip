@@ -9,11 +9,17 @@
 // whose qkv row is the Linear bias. The -100 mask is recomputed from per-axis region ids exactly as
 // compute_mask builds it (:591-628). WINDOWS mode takes pre-partitioned (Bw, N, 3C) and an optional mask.
 //
+// Additive logit term: every window of one "type" shares rpb + mask, so lci_window_bias builds, once per call,
+// a log2-domain table bias[type][head][q][k] = (rpb[h][q][k] + mask) * log2(e), -1e30 for padded keys/queries
+// (grid mode: type = which axes the window is the last one on, when shifted -> <= 8 types; windows mode:
+// type = w % nW when a mask is given). The table tile is the INITIAL ACCUMULATOR of the score MFMAs, Q is
+// prescaled by scale*log2(e): the chain yields the full log2-domain logit, no per-element bias/mask VALU.
 // One workgroup = one (window, head); the whole window's K and V live in LDS; 4 waves x 32-query blocks;
-// S^T = K.Q^T with the query on the MFMA lane, online softmax over 32-key tiles, O^T += V^T.P^T.
-// Backward: phase 1 (query on lane): dP^T, dS^T, dQ^T += K^T dS^T, and dS tiles for d(rpb);
-//           phase 2 (key on lane, Q/dO in LDS): dV^T += dO^T P, dK^T += Q^T dS. Pad-token dK/dV go to the
-//           qkv bias gradient. d(rpb) = sum over windows of dS (separate reduction kernel, no atomics).
+// S^T = K.Q^T with the query on the MFMA lane, online softmax (lazy exact rescale) over 32-key tiles,
+// O^T += V^T.P^T.
+// Backward: phase 1 (query on lane): dP^T (initial accumulator -delta), dS^T, dQ^T += K^T dS^T, dS tiles for
+//           d(rpb); phase 2 (key on lane, Q/dO in LDS, transposed table): dV^T += dO^T P, dK^T += Q^T dS.
+//           Pad-token dK/dV go to the qkv bias gradient. d(rpb) = sum over windows of dS (reduction kernel).
 #include "common.hpp"
 
 namespace lci {
@@ -26,15 +32,17 @@ constexpr float WNEG = -1.0e30f;
 
 struct WinArgs {
   const bf16* qkv; const float* qkv_bias;  // bias (3C) f32 or null: value of padded tokens
-  const float* rpb;                        // (H, N, Npad) f32, log-domain bias (rpb_table[index])
-  const float* mask;                       // WINDOWS mode: (nW, N, N) f32 or null
+  const float* rpb;                        // (H, N, N) f32 rpb_table[index] (table builder only)
+  const float* mask;                       // WINDOWS mode: (nW, N, N) f32 or null (table builder only)
+  const float* bias;                       // (T, H, Npad, Npad) log2-domain logit term [q][k]
+  const float* biasT;                      // the same, transposed [k][q] (backward phase 2)
   bf16* out; const bf16* o; const bf16* dout;
   float* lse2;                             // (Bw, H, N)
   bf16* dqkv; float* dbias_pad;            // bwd
   bf16* dS;                                // (Bw, H, nqb, nkt, 64, 16) bf16 tiles or null
   float* drpb;                             // (H, N, N) f32 (reduction kernel)
   int mode, nd, S[3], ws[3], sh[3], Sp[3], nwin[3];
-  int Bw, nW, N, Npad, nqb, nkt, C, H, masked;
+  int Bw, nW, N, Npad, nqb, nkt, C, H, masked, T;
   float scale, c;
 };
 
@@ -81,17 +89,6 @@ __device__ __forceinline__ const bf16* out_row_ptr(const WinArgs& a, const bf16*
   return base + (long long)(a.mode == 0 ? w * a.N + n : row) * a.C;
 }
 
-// log2-domain additive term for (q, key): rpb*log2e + (mask)
-__device__ __forceinline__ float win_mask_term(const WinArgs& a, int w, int q, int k, int rq, int rk) {
-  float t = 0.f;
-  if (a.mode == 1) {
-    if (a.masked && rq != rk) t = -100.f * WLOG2E;
-  } else if (a.mask) {
-    t = a.mask[((long long)(w % a.nW) * a.N + q) * a.N + k] * WLOG2E;
-  }
-  return t;
-}
-
 struct WinLds {
   bf16* t0; bf16* t1; int* row; int* rid;
 };
@@ -128,6 +125,65 @@ __device__ __forceinline__ void win_stage(const WinArgs& a, const WinLds& L, int
   __syncthreads();
 }
 
+// window type (index into the bias table)
+__device__ __forceinline__ int win_type(const WinArgs& a, int w) {
+  if (a.mode == 0) return a.T > 1 ? w % a.nW : 0;
+  if (!a.masked) return 0;
+  int wi = w % a.nW, t = 0;
+  for (int s = a.nd - 1; s >= 0; --s) {
+    const int widx = wi % a.nwin[s];
+    wi /= a.nwin[s];
+    if (a.sh[s] > 0 && widx == a.nwin[s] - 1) t |= 1 << s;
+  }
+  return t;
+}
+
+// compute_mask's region id (backbone_swin.py:591-628) of window token n in a window of type t
+__device__ __forceinline__ int win_region(const WinArgs& a, int t, int n) {
+  int nidx[3] = {0, 0, 0};
+  for (int s = a.nd - 1; s >= 0; --s) { nidx[s] = n % a.ws[s]; n /= a.ws[s]; }
+  int rid = 0;
+  for (int s = 0; s < a.nd; ++s) rid = rid * 3 + (((t >> s) & 1) ? (nidx[s] < a.ws[s] - a.sh[s] ? 1 : 2) : 0);
+  return rid;
+}
+
+__global__ __launch_bounds__(256) void win_bias_kernel(WinArgs a, float* bias, float* biasT) {
+  const long long np2 = (long long)a.Npad * a.Npad;
+  const long long e = blockIdx.x * 256LL + threadIdx.x;
+  if (e >= (long long)a.T * a.H * np2) return;
+  const int k = e % a.Npad, q = (e / a.Npad) % a.Npad;
+  const long long th = e / np2;   // t * H + h
+  const int h = th % a.H, t = th / a.H;
+  float v = WNEG;
+  if (q < a.N && k < a.N) {
+    v = a.rpb[((long long)h * a.N + q) * a.N + k];
+    if (a.mode == 0 && a.mask) v += a.mask[((long long)t * a.N + q) * a.N + k];
+    if (a.mode == 1 && a.masked && win_region(a, t, q) != win_region(a, t, k)) v += -100.f;
+    v *= WLOG2E;
+  }
+  bias[e] = v;
+  if (biasT) biasT[th * np2 + (long long)k * a.Npad + q] = v;
+}
+
+// 16 table values of one 32x32 score tile for this lane: row r (q or key, the lane's), columns
+// c0 + 8g + 4h + j  ->  register 4g + j (the 32x32x16 accumulator layout)
+__device__ __forceinline__ f32x16 win_bias_tile(const float* row, int c0) {
+  f32x16 r;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const f32x4 v = *(const f32x4*)(row + c0 + 8 * g);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[4 * g + j] = v[j];
+  }
+  return r;
+}
+
+__device__ __forceinline__ bf16x8 scaled8(bf16x8 v, float c) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = to_bf16(to_f32(v[j]) * c);
+  return v;
+}
+
 // --------------------------------------------------------------------------------------------- forward
 __global__ __launch_bounds__(256) void win_attn_fwd_kernel(WinArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -137,48 +193,49 @@ __global__ __launch_bounds__(256) void win_attn_fwd_kernel(WinArgs a) {
   win_setup(a, smem, L, w);
   win_stage(a, L, a.C + hh * WHD, 2 * a.C + hh * WHD, false, nullptr, w);   // K -> t0, V -> t1
   const float c = a.c;
-  const float* rpbh = a.rpb + (long long)hh * a.N * a.Npad;
+  const float* bh = a.bias + ((long long)win_type(a, w) * a.H + hh) * a.Npad * a.Npad;
   for (int qb = wave; qb < a.nqb; qb += 4) {
     const int q = qb * 32 + (lane & 31);
     const bool qv = q < a.N;
     const int qrow = qv ? L.row[q] : -2;
-    const int rq = qv ? L.rid[q] : 0;
     bf16x8 qf[2];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) qf[ks] = win_load8(a, qrow, hh * WHD + ks * 16 + 8 * half, qv);
+    for (int ks = 0; ks < 2; ++ks) qf[ks] = scaled8(win_load8(a, qrow, hh * WHD + ks * 16 + 8 * half, qv), c);
+    const float* brow = bh + (long long)q * a.Npad + 4 * half;
     f32x16 o = {};
-    float m = WNEG, l = 0.f;
-    const int qq = qv ? q : 0;
+    float m = 0.f, l = 0.f;
+    f32x16 bn = win_bias_tile(brow, 0);
     for (int kt = 0; kt < a.nkt; ++kt) {
-      f32x16 s = {};
+      f32x16 s = bn;
+      if (kt + 1 < a.nkt) bn = win_bias_tile(brow, (kt + 1) * 32);
       s = mfma32(frag_row(L.t0, WLD, kt * 32, 0, lane), qf[0], s);
       s = mfma32(frag_row(L.t0, WLD, kt * 32, 16, lane), qf[1], s);
+      float m4[4] = {fmaxf(s[0], s[1]), fmaxf(s[2], s[3]), fmaxf(s[4], s[5]), fmaxf(s[6], s[7])};
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int k0 = kt * 32 + 8 * g + 4 * half;
-        const f32x4 rb = *(const f32x4*)(rpbh + (long long)qq * a.Npad + k0);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int i = 4 * g + j, k = k0 + j;
-          float v = fmaf(s[i], c, rb[j] * WLOG2E);
-          if (k < a.N) v += win_mask_term(a, w, qq, k, rq, L.rid[k]);
-          else v = WNEG;
-          s[i] = v;
-        }
+      for (int i = 8; i < 16; i += 4) {
+        m4[0] = fmaxf(m4[0], s[i]);
+        m4[1] = fmaxf(m4[1], s[i + 1]);
+        m4[2] = fmaxf(m4[2], s[i + 2]);
+        m4[3] = fmaxf(m4[3], s[i + 3]);
       }
-      float mx = s[0];
+      const float mx = wave_max_xor32(fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3])));
+      if (kt == 0 || __any(mx > m)) {   // lazy exact rescale (alpha == 1 otherwise)
+        const float mn = kt == 0 ? mx : fmaxf(m, mx);
+        if (kt != 0) {
+          const float al = exp2_fast(m - mn);
+          l *= al;
 #pragma unroll
-      for (int i = 1; i < 16; ++i) mx = fmaxf(mx, s[i]);
-      mx = wave_max_xor32(mx);
-      const float mn = fmaxf(m, mx);
-      const float al = exp2_fast(m - mn);
-      m = mn;
-      float ls = 0.f;
+          for (int i = 0; i < 16; ++i) o[i] *= al;
+        }
+        m = mn;
+      }
+      float l4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int i = 0; i < 16; ++i) { s[i] = exp2_fast(s[i] - mn); ls += s[i]; }
-      l = l * al + ls;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) o[i] *= al;
+      for (int i = 0; i < 16; ++i) {
+        s[i] = exp2_fast(s[i] - m);
+        l4[i & 3] += s[i];
+      }
+      l += (l4[0] + l4[1]) + (l4[2] + l4[3]);
       o = mfma32(frag_tr<0>(L.t1, WLD, kt * 32, 0, lane), pack8<0>(s), o);
       o = mfma32(frag_tr<1>(L.t1, WLD, kt * 32, 0, lane), pack8<1>(s), o);
     }
@@ -206,9 +263,9 @@ __global__ __launch_bounds__(256) void win_attn_bwd_kernel(WinArgs a) {
   WinLds L;
   win_setup(a, smem, L, w);
   float* lse_l = (float*)(L.rid + a.Npad);
-  float* dl_l = lse_l + a.Npad;
+  float* ndl_l = lse_l + a.Npad;   // -delta
   const float c = a.c;
-  const float* rpbh = a.rpb + (long long)hh * a.N * a.Npad;
+  const long long tho = ((long long)win_type(a, w) * a.H + hh) * a.Npad * a.Npad;
   const float* lseg = a.lse2 + ((long long)w * a.H + hh) * a.N;
 
   // ---------------- phase 1: K, V in LDS; query on the lane -> dQ, dS tiles, delta
@@ -217,14 +274,12 @@ __global__ __launch_bounds__(256) void win_attn_bwd_kernel(WinArgs a) {
     const int q = qb * 32 + (lane & 31);
     const bool qv = q < a.N;
     const int qrow = qv ? L.row[q] : -2;
-    const int rq = qv ? L.rid[q] : 0;
-    const int qq = qv ? q : 0;
     bf16x8 qf[2], df[2];
     float dsum = 0.f;
     const bool has_out = qv && qrow != -1;   // padded queries are cropped: dO = 0
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      qf[ks] = win_load8(a, qrow, hh * WHD + ks * 16 + 8 * half, qv);
+      qf[ks] = scaled8(win_load8(a, qrow, hh * WHD + ks * 16 + 8 * half, qv), c);
       if (has_out) {
         df[ks] = *(const bf16x8*)(out_row_ptr(a, a.dout, w, q, qrow) + hh * WHD + ks * 16 + 8 * half);
         const bf16x8 ov = *(const bf16x8*)(out_row_ptr(a, a.o, w, q, qrow) + hh * WHD + ks * 16 + 8 * half);
@@ -235,41 +290,34 @@ __global__ __launch_bounds__(256) void win_attn_bwd_kernel(WinArgs a) {
       }
     }
     const float delta = wave_sum_xor32(dsum);
-    const float lse = qv ? lseg[q] : 1.0e30f;
+    const float lse = qv ? lseg[q] : 0.f;   // invalid lanes: every table entry is -1e30 -> P = 0
     if (half == 0) {
-      lse_l[q] = lse;
-      dl_l[q] = delta;
+      lse_l[q] = qv ? lse : 1.0e30f;
+      ndl_l[q] = -delta;
     }
+    f32x16 ndl;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ndl[i] = -delta;
+    const float* brow = a.bias + tho + (long long)q * a.Npad + 4 * half;
     f32x16 dq = {};
+    f32x16 bn = win_bias_tile(brow, 0);
     for (int kt = 0; kt < a.nkt; ++kt) {
-      f32x16 s = {}, dp = {};
+      f32x16 s = bn;
+      if (kt + 1 < a.nkt) bn = win_bias_tile(brow, (kt + 1) * 32);
       s = mfma32(frag_row(L.t0, WLD, kt * 32, 0, lane), qf[0], s);
       s = mfma32(frag_row(L.t0, WLD, kt * 32, 16, lane), qf[1], s);
-      dp = mfma32(frag_row(L.t1, WLD, kt * 32, 0, lane), df[0], dp);
+      f32x16 dp = mfma32(frag_row(L.t1, WLD, kt * 32, 0, lane), df[0], ndl);
       dp = mfma32(frag_row(L.t1, WLD, kt * 32, 16, lane), df[1], dp);
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int k0 = kt * 32 + 8 * g + 4 * half;
-        const f32x4 rb = *(const f32x4*)(rpbh + (long long)qq * a.Npad + k0);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int i = 4 * g + j, k = k0 + j;
-          float p = 0.f;
-          if (k < a.N && qv) {
-            const float v = fmaf(s[i], c, rb[j] * WLOG2E) + win_mask_term(a, w, qq, k, rq, L.rid[k]);
-            p = exp2_fast(v - lse);
-          }
-          s[i] = p * (dp[i] - delta);   // dS^T (natural-log units)
-        }
-      }
+      for (int i = 0; i < 16; ++i) s[i] = exp2_fast(s[i] - lse) * dp[i];   // dS^T (natural-log units)
+      const bf16x8 lo = pack8<0>(s), hi = pack8<1>(s);
       if (a.dS) {
         bf16* dst = a.dS + ((((long long)w * a.H + hh) * a.nqb + qb) * a.nkt + kt) * 1024 + lane * 16;
-        bf16x8 lo = pack8<0>(s), hi = pack8<1>(s);
         *(bf16x8*)dst = lo;
         *(bf16x8*)(dst + 8) = hi;
       }
-      dq = mfma32(frag_tr<0>(L.t0, WLD, kt * 32, 0, lane), pack8<0>(s), dq);
-      dq = mfma32(frag_tr<1>(L.t0, WLD, kt * 32, 0, lane), pack8<1>(s), dq);
+      dq = mfma32(frag_tr<0>(L.t0, WLD, kt * 32, 0, lane), lo, dq);
+      dq = mfma32(frag_tr<1>(L.t0, WLD, kt * 32, 0, lane), hi, dq);
     }
     if (qv && qrow >= 0) {
       bf16* dqp = a.dqkv + (long long)(a.mode == 0 ? w * a.N + q : qrow) * 3 * a.C + hh * WHD;
@@ -282,7 +330,7 @@ __global__ __launch_bounds__(256) void win_attn_bwd_kernel(WinArgs a) {
       }
     }
   }
-  for (int n = a.N + threadIdx.x; n < a.Npad; n += blockDim.x) { lse_l[n] = 1.0e30f; dl_l[n] = 0.f; }
+  for (int n = a.N + threadIdx.x; n < a.Npad; n += blockDim.x) { lse_l[n] = 1.0e30f; ndl_l[n] = 0.f; }
   __syncthreads();
 
   // ---------------- phase 2: Q, dO in LDS; key on the lane -> dK, dV
@@ -291,38 +339,34 @@ __global__ __launch_bounds__(256) void win_attn_bwd_kernel(WinArgs a) {
     const int key = kb * 32 + (lane & 31);
     const bool kv = key < a.N;
     const int krow = kv ? L.row[key] : -2;
-    const int rk = kv ? L.rid[key] : 0;
-    const int kk = kv ? key : 0;
     bf16x8 kf[2], vf[2];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      kf[ks] = win_load8(a, krow, a.C + hh * WHD + ks * 16 + 8 * half, kv);
+      kf[ks] = scaled8(win_load8(a, krow, a.C + hh * WHD + ks * 16 + 8 * half, kv), c);
       vf[ks] = win_load8(a, krow, 2 * a.C + hh * WHD + ks * 16 + 8 * half, kv);
     }
+    const float* brow = a.biasT + tho + (long long)key * a.Npad + 4 * half;
     f32x16 dk = {}, dv = {};
+    f32x16 bn = win_bias_tile(brow, 0);
     for (int qt = 0; qt < a.nkt; ++qt) {
-      f32x16 s = {}, dp = {};
+      f32x16 s = bn;
+      if (qt + 1 < a.nkt) bn = win_bias_tile(brow, (qt + 1) * 32);
+      f32x16 dp, lz;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {   // row constants of queries qt*32 + 8g + 4h + j
+        const f32x4 l4 = *(const f32x4*)(lse_l + qt * 32 + 8 * g + 4 * half);
+        const f32x4 d4 = *(const f32x4*)(ndl_l + qt * 32 + 8 * g + 4 * half);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { lz[4 * g + j] = l4[j]; dp[4 * g + j] = d4[j]; }
+      }
       s = mfma32(frag_row(L.t0, WLD, qt * 32, 0, lane), kf[0], s);
       s = mfma32(frag_row(L.t0, WLD, qt * 32, 16, lane), kf[1], s);
       dp = mfma32(frag_row(L.t1, WLD, qt * 32, 0, lane), vf[0], dp);
       dp = mfma32(frag_row(L.t1, WLD, qt * 32, 16, lane), vf[1], dp);
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int q0 = qt * 32 + 8 * g + 4 * half;
-        const f32x4 lz = *(const f32x4*)(lse_l + q0);
-        const f32x4 dz = *(const f32x4*)(dl_l + q0);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int i = 4 * g + j, q = q0 + j;
-          float p = 0.f;
-          if (kv && q < a.N) {
-            const float v = fmaf(s[i], c, rpbh[(long long)q * a.Npad + kk] * WLOG2E) +
-                            win_mask_term(a, w, q, kk, L.rid[q], rk);
-            p = exp2_fast(v - lz[j]);
-          }
-          s[i] = p;
-          dp[i] = p * (dp[i] - dz[j]);
-        }
+      for (int i = 0; i < 16; ++i) {
+        s[i] = exp2_fast(s[i] - lz[i]);   // P (query rows, key on lane)
+        dp[i] = s[i] * dp[i];             // dS
       }
       dv = mfma32(frag_tr<0>(L.t1, WLD, qt * 32, 0, lane), pack8<0>(s), dv);
       dv = mfma32(frag_tr<1>(L.t1, WLD, qt * 32, 0, lane), pack8<1>(s), dv);
@@ -393,8 +437,10 @@ static int win_fill(WinArgs& a, const int* geo, float scale) {
     }
     LCI_CHECK(N == a.N, "window_attn: N %d != prod(window) %d", a.N, N);
     a.nW = nW; a.Bw = geo[11] * nW;
+    a.T = a.masked ? (1 << a.nd) : 1;
   } else {
     a.Bw = geo[11]; a.nW = geo[12] > 0 ? geo[12] : 1;
+    a.T = 1;   // lci_window_bias / _elems set T = nW when a mask is given
   }
   a.Npad = (a.N + 31) / 32 * 32;
   a.nqb = a.nkt = a.Npad / 32;
@@ -410,11 +456,32 @@ static size_t win_lds(const WinArgs& a, bool bwd) {
 
 using namespace lci;
 
-extern "C" int lci_window_attn_fwd(const void* qkv, const float* qkv_bias, const float* rpb, const float* mask,
+extern "C" long long lci_window_bias_elems(const int* geo, int has_mask) {
+  WinArgs a{};
+  if (win_fill(a, geo, 1.f)) return -1;
+  if (a.mode == 0 && has_mask) a.T = a.nW;
+  return (long long)a.T * a.H * a.Npad * a.Npad;
+}
+
+extern "C" int lci_window_bias(const float* rpb, const float* mask, float* bias, float* biasT, const int* geo,
+                               void* stream) {
+  WinArgs a{};
+  if (win_fill(a, geo, 1.f)) return 1;
+  a.rpb = rpb; a.mask = mask;
+  if (a.mode == 0 && mask) a.T = a.nW;
+  const long long n = (long long)a.T * a.H * a.Npad * a.Npad;
+  hipLaunchKernelGGL(win_bias_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a,
+                     bias, biasT);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int lci_window_attn_fwd(const void* qkv, const float* qkv_bias, const float* bias, int has_mask,
                                    void* out, float* lse2, const int* geo, float scale, void* stream) {
   WinArgs a{};
   if (win_fill(a, geo, scale)) return 1;
-  a.qkv = (const bf16*)qkv; a.qkv_bias = qkv_bias; a.rpb = rpb; a.mask = mask; a.out = (bf16*)out; a.lse2 = lse2;
+  if (a.mode == 0 && has_mask) a.T = a.nW;
+  a.qkv = (const bf16*)qkv; a.qkv_bias = qkv_bias; a.bias = bias; a.out = (bf16*)out; a.lse2 = lse2;
   (void)hipFuncSetAttribute((const void*)win_attn_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipLaunchKernelGGL(win_attn_fwd_kernel, dim3(a.Bw, a.H), dim3(256), win_lds(a, false), (hipStream_t)stream, a);
   LCI_LAUNCH_CHECK();
@@ -423,12 +490,14 @@ extern "C" int lci_window_attn_fwd(const void* qkv, const float* qkv_bias, const
 
 // dbias_pad (3C) accumulated (caller zeroes); dS tiles (Bw*H*nqb*nkt*1024 bf16) optional workspace;
 // drpb (H, N, N) f32 written when dS and drpb are given.
-extern "C" int lci_window_attn_bwd(const void* qkv, const float* qkv_bias, const float* rpb, const float* mask,
-                                   const void* out, const void* dout, const float* lse2, void* dqkv, float* dbias_pad,
-                                   void* dS, float* drpb, const int* geo, float scale, void* stream) {
+extern "C" int lci_window_attn_bwd(const void* qkv, const float* qkv_bias, const float* bias, const float* biasT,
+                                   int has_mask, const void* out, const void* dout, const float* lse2, void* dqkv,
+                                   float* dbias_pad, void* dS, float* drpb, const int* geo, float scale,
+                                   void* stream) {
   WinArgs a{};
   if (win_fill(a, geo, scale)) return 1;
-  a.qkv = (const bf16*)qkv; a.qkv_bias = qkv_bias; a.rpb = rpb; a.mask = mask; a.o = (const bf16*)out;
+  if (a.mode == 0 && has_mask) a.T = a.nW;
+  a.qkv = (const bf16*)qkv; a.qkv_bias = qkv_bias; a.bias = bias; a.biasT = biasT; a.o = (const bf16*)out;
   a.dout = (const bf16*)dout; a.lse2 = (float*)lse2; a.dqkv = (bf16*)dqkv; a.dbias_pad = dbias_pad;
   a.dS = (bf16*)dS; a.drpb = drpb;
   hipStream_t s = (hipStream_t)stream;

@@ -353,9 +353,23 @@ def _i32(vals):
     return (ctypes.c_int * len(vals))(*[int(v) for v in vals])
 
 
+def _window_bias(rpb, mask, geo, transposed=False):
+    """(T, H, Npad, Npad) log2-domain logit term (and its transpose): rpb + region/explicit mask, padding."""
+    g = _i32(geo)
+    n = int(_lib.load().lci_window_bias_elems(g, int(mask is not None)))
+    if n <= 0:
+        raise _lib.LciError(_lib.load().lci_last_error().decode())
+    f32 = dict(device=rpb.device, dtype=torch.float32)
+    bias = torch.empty(n, **f32)
+    bt = torch.empty(n, **f32) if transposed else None
+    _lib.call("lci_window_bias", rpb.data_ptr(), _lib.ptr(mask), bias.data_ptr(), _lib.ptr(bt), g,
+              _lib.stream_of(rpb))
+    return bias, bt
+
+
 class _WindowAttention(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, bias, rpb_p, mask, geo, scale):
+    def forward(ctx, qkv, bias, rpb, mask, geo, scale):
         C = qkv.shape[-1] // 3
         out = torch.empty(*qkv.shape[:-1], C, device=qkv.device, dtype=torch.bfloat16)
         g = _i32(geo)
@@ -364,16 +378,18 @@ class _WindowAttention(torch.autograd.Function):
         lse2 = torch.empty(Bw, H, N, device=qkv.device, dtype=torch.float32)
         bf = bias.float().contiguous() if bias is not None else None
         mk = mask.float().contiguous() if mask is not None else None
+        rp = rpb.float().contiguous()
+        tab, _ = _window_bias(rp, mk, geo)
         KernelTimer.run("window_attn_fwd", 4.0 * Bw * H * N * N * 32, qkv, lambda: _lib.call(
-            "lci_window_attn_fwd", qkv.data_ptr(), _lib.ptr(bf), rpb_p.data_ptr(), _lib.ptr(mk), out.data_ptr(),
+            "lci_window_attn_fwd", qkv.data_ptr(), _lib.ptr(bf), tab.data_ptr(), int(mk is not None), out.data_ptr(),
             lse2.data_ptr(), g, float(scale), _lib.stream_of(qkv)))
-        ctx.save_for_backward(qkv, bf, rpb_p, mk, out, lse2)
+        ctx.save_for_backward(qkv, bf, rp, mk, out, lse2)
         ctx.geo, ctx.scale, ctx.has_bias = geo, scale, bias is not None
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        qkv, bf, rpb_p, mk, out, lse2 = ctx.saved_tensors
+        qkv, bf, rp, mk, out, lse2 = ctx.saved_tensors
         geo, scale = ctx.geo, ctx.scale
         g = _i32(geo)
         N, C, H = geo[13], geo[14], geo[15]
@@ -388,20 +404,12 @@ class _WindowAttention(torch.autograd.Function):
             n_el = _lib.load().lci_window_dS_elems(g)
             dS = torch.empty(int(n_el), device=qkv.device, dtype=torch.bfloat16)
             drpb = torch.empty(H, N, N, **f32)
+        tab, tabT = _window_bias(rp, mk, geo, transposed=True)
         KernelTimer.run("window_attn_bwd", 8.0 * Bw * H * N * N * 32, qkv, lambda: _lib.call(
-            "lci_window_attn_bwd", qkv.data_ptr(), _lib.ptr(bf), rpb_p.data_ptr(), _lib.ptr(mk), out.data_ptr(),
-            dout.data_ptr(), lse2.data_ptr(), dqkv.data_ptr(), _lib.ptr(dbias), _lib.ptr(dS), _lib.ptr(drpb), g,
-            float(scale), _lib.stream_of(qkv)))
-        drpb_p = None
-        if want_rpb:
-            drpb_p = torch.nn.functional.pad(drpb, (0, rpb_p.shape[-1] - N))
-        return dqkv, dbias, drpb_p, None, None, None
-
-
-def _pad_rpb(rpb):
-    H, N, _ = rpb.shape
-    npad = -(-N // 32) * 32
-    return torch.nn.functional.pad(rpb.float(), (0, npad - N)).contiguous()
+            "lci_window_attn_bwd", qkv.data_ptr(), _lib.ptr(bf), tab.data_ptr(), tabT.data_ptr(), int(mk is not None),
+            out.data_ptr(), dout.data_ptr(), lse2.data_ptr(), dqkv.data_ptr(), _lib.ptr(dbias), _lib.ptr(dS),
+            _lib.ptr(drpb), g, float(scale), _lib.stream_of(qkv)))
+        return dqkv, dbias, drpb, None, None, None
 
 
 def _win_prep(qkv):
@@ -432,7 +440,7 @@ def window_attention_grid(qkv, bias, rpb, num_heads, scale, window_size, shift_s
     for s, w in zip(S, window_size):
         nW *= -(-s // w)
     geo = (1, nd, *S3, *ws3, *sh3, q.shape[0], nW, N, C, num_heads)
-    o = _WindowAttention.apply(q, bias, _pad_rpb(rpb), None, geo, scale)
+    o = _WindowAttention.apply(q, bias, rpb.float(), None, geo, scale)
     return o if dt == torch.bfloat16 else o.to(dt)
 
 
@@ -443,7 +451,7 @@ def window_attention(qkv, rpb, mask, num_heads, scale):
     Bw, N, C3 = q.shape
     nW = mask.shape[0] if mask is not None else 1
     geo = (0, 0, 1, 1, 1, 1, 1, 1, 0, 0, 0, Bw, nW, N, C3 // 3, num_heads)
-    o = _WindowAttention.apply(q, None, _pad_rpb(rpb), mask, geo, scale)
+    o = _WindowAttention.apply(q, None, rpb.float(), mask, geo, scale)
     return o if dt == torch.bfloat16 else o.to(dt)
 
 
