@@ -107,20 +107,46 @@ __device__ __forceinline__ void win_setup(const WinArgs& a, char* smem, WinLds& 
 }
 
 // stage two (Npad x 32) tiles of the window: channel offsets c0, c1 of the token rows (or the bias)
+__device__ __forceinline__ bf16x8 win_stage_src1(const WinArgs& a, const WinLds& L, int n, int ch, int c1,
+                                                 bool second_is_out, const bf16* obase, int w) {
+  const int row = L.row[n];
+  const bool ex = n < a.N;
+  if (second_is_out)
+    return (ex && row != -1) ? *(const bf16x8*)(out_row_ptr(a, obase, w, n, row) + c1 + ch * 8) : bf16x8{};
+  return win_load8(a, row, c1 + ch * 8, ex);
+}
+
+template <int NT>
 __device__ __forceinline__ void win_stage(const WinArgs& a, const WinLds& L, int c0, int c1, bool second_is_out,
                                           const bf16* obase, int w) {
-  for (int idx = threadIdx.x; idx < a.Npad * 4; idx += blockDim.x) {
-    const int n = idx >> 2, ch = idx & 3;
-    const int row = L.row[n];
-    const bool ex = n < a.N;
-    *(bf16x8*)(L.t0 + n * WLD + ch * 8) = win_load8(a, row, c0 + ch * 8, ex);
-    bf16x8 v;
-    if (second_is_out) {
-      v = (ex && row != -1) ? *(const bf16x8*)(out_row_ptr(a, obase, w, n, row) + c1 + ch * 8) : bf16x8{};
-    } else {
-      v = win_load8(a, row, c1 + ch * 8, ex);
+  constexpr int IT = 1536 / NT;   // Npad <= 384 (every Swin window up to 7x7x7): all row loads in flight at once
+  const int items = a.Npad * 4;
+  if (items <= IT * NT) {
+    bf16x8 r0[IT], r1[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int idx = it * NT + threadIdx.x;
+      if (idx < items) {
+        const int n = idx >> 2, ch = idx & 3;
+        r0[it] = win_load8(a, L.row[n], c0 + ch * 8, n < a.N);
+        r1[it] = win_stage_src1(a, L, n, ch, c1, second_is_out, obase, w);
+      }
     }
-    *(bf16x8*)(L.t1 + n * WLD + ch * 8) = v;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int idx = it * NT + threadIdx.x;
+      if (idx < items) {
+        const int n = idx >> 2, ch = idx & 3;
+        *(bf16x8*)(L.t0 + n * WLD + ch * 8) = r0[it];
+        *(bf16x8*)(L.t1 + n * WLD + ch * 8) = r1[it];
+      }
+    }
+  } else {
+    for (int idx = threadIdx.x; idx < items; idx += blockDim.x) {
+      const int n = idx >> 2, ch = idx & 3;
+      *(bf16x8*)(L.t0 + n * WLD + ch * 8) = win_load8(a, L.row[n], c0 + ch * 8, n < a.N);
+      *(bf16x8*)(L.t1 + n * WLD + ch * 8) = win_stage_src1(a, L, n, ch, c1, second_is_out, obase, w);
+    }
   }
   __syncthreads();
 }
@@ -185,29 +211,40 @@ __device__ __forceinline__ bf16x8 scaled8(bf16x8 v, float c) {
 }
 
 // --------------------------------------------------------------------------------------------- forward
-__global__ __launch_bounds__(256) void win_attn_fwd_kernel(WinArgs a) {
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void win_attn_fwd_kernel(WinArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int w = blockIdx.x, hh = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5;
   WinLds L;
   win_setup(a, smem, L, w);
-  win_stage(a, L, a.C + hh * WHD, 2 * a.C + hh * WHD, false, nullptr, w);   // K -> t0, V -> t1
+  win_stage<NW * 64>(a, L, a.C + hh * WHD, 2 * a.C + hh * WHD, false, nullptr, w);   // K -> t0, V -> t1
   const float c = a.c;
   const float* bh = a.bias + ((long long)win_type(a, w) * a.H + hh) * a.Npad * a.Npad;
-  for (int qb = wave; qb < a.nqb; qb += 4) {
+  bf16x8 qn[2];   // next query block's Q, loaded one block ahead
+  auto load_q = [&](int qb) {
     const int q = qb * 32 + (lane & 31);
     const bool qv = q < a.N;
     const int qrow = qv ? L.row[q] : -2;
-    bf16x8 qf[2];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) qf[ks] = scaled8(win_load8(a, qrow, hh * WHD + ks * 16 + 8 * half, qv), c);
+    for (int ks = 0; ks < 2; ++ks) qn[ks] = win_load8(a, qrow, hh * WHD + ks * 16 + 8 * half, qv);
+  };
+  if (wave < a.nqb) load_q(wave);
+  for (int qb = wave; qb < a.nqb; qb += NW) {
+    const int q = qb * 32 + (lane & 31);
+    const bool qv = q < a.N;
+    const int qrow = qv ? L.row[q] : -2;
+    const bf16x8 qf[2] = {scaled8(qn[0], c), scaled8(qn[1], c)};
+    if (qb + NW < a.nqb) load_q(qb + NW);
     const float* brow = bh + (long long)q * a.Npad + 4 * half;
     f32x16 o = {};
     float m = 0.f, l = 0.f;
-    f32x16 bn = win_bias_tile(brow, 0);
+    f32x16 b0 = win_bias_tile(brow, 0), b1;   // table tiles two ahead
+    if (a.nkt > 1) b1 = win_bias_tile(brow, 32);
     for (int kt = 0; kt < a.nkt; ++kt) {
-      f32x16 s = bn;
-      if (kt + 1 < a.nkt) bn = win_bias_tile(brow, (kt + 1) * 32);
+      f32x16 s = b0;
+      b0 = b1;
+      if (kt + 2 < a.nkt) b1 = win_bias_tile(brow, (kt + 2) * 32);
       s = mfma32(frag_row(L.t0, WLD, kt * 32, 0, lane), qf[0], s);
       s = mfma32(frag_row(L.t0, WLD, kt * 32, 16, lane), qf[1], s);
       float m4[4] = {fmaxf(s[0], s[1]), fmaxf(s[2], s[3]), fmaxf(s[4], s[5]), fmaxf(s[6], s[7])};
@@ -269,7 +306,7 @@ __global__ __launch_bounds__(256) void win_attn_bwd_kernel(WinArgs a) {
   const float* lseg = a.lse2 + ((long long)w * a.H + hh) * a.N;
 
   // ---------------- phase 1: K, V in LDS; query on the lane -> dQ, dS tiles, delta
-  win_stage(a, L, a.C + hh * WHD, 2 * a.C + hh * WHD, false, nullptr, w);
+  win_stage<256>(a, L, a.C + hh * WHD, 2 * a.C + hh * WHD, false, nullptr, w);
   for (int qb = wave; qb < a.nqb; qb += 4) {
     const int q = qb * 32 + (lane & 31);
     const bool qv = q < a.N;
@@ -300,10 +337,12 @@ __global__ __launch_bounds__(256) void win_attn_bwd_kernel(WinArgs a) {
     for (int i = 0; i < 16; ++i) ndl[i] = -delta;
     const float* brow = a.bias + tho + (long long)q * a.Npad + 4 * half;
     f32x16 dq = {};
-    f32x16 bn = win_bias_tile(brow, 0);
+    f32x16 b0 = win_bias_tile(brow, 0), b1;
+    if (a.nkt > 1) b1 = win_bias_tile(brow, 32);
     for (int kt = 0; kt < a.nkt; ++kt) {
-      f32x16 s = bn;
-      if (kt + 1 < a.nkt) bn = win_bias_tile(brow, (kt + 1) * 32);
+      f32x16 s = b0;
+      b0 = b1;
+      if (kt + 2 < a.nkt) b1 = win_bias_tile(brow, (kt + 2) * 32);
       s = mfma32(frag_row(L.t0, WLD, kt * 32, 0, lane), qf[0], s);
       s = mfma32(frag_row(L.t0, WLD, kt * 32, 16, lane), qf[1], s);
       f32x16 dp = mfma32(frag_row(L.t1, WLD, kt * 32, 0, lane), df[0], ndl);
@@ -334,7 +373,7 @@ __global__ __launch_bounds__(256) void win_attn_bwd_kernel(WinArgs a) {
   __syncthreads();
 
   // ---------------- phase 2: Q, dO in LDS; key on the lane -> dK, dV
-  win_stage(a, L, hh * WHD, hh * WHD, true, a.dout, w);   // Q -> t0, dO -> t1
+  win_stage<256>(a, L, hh * WHD, hh * WHD, true, a.dout, w);   // Q -> t0, dO -> t1
   for (int kb = wave; kb < a.nqb; kb += 4) {
     const int key = kb * 32 + (lane & 31);
     const bool kv = key < a.N;
@@ -347,10 +386,12 @@ __global__ __launch_bounds__(256) void win_attn_bwd_kernel(WinArgs a) {
     }
     const float* brow = a.biasT + tho + (long long)key * a.Npad + 4 * half;
     f32x16 dk = {}, dv = {};
-    f32x16 bn = win_bias_tile(brow, 0);
+    f32x16 b0 = win_bias_tile(brow, 0), b1;
+    if (a.nkt > 1) b1 = win_bias_tile(brow, 32);
     for (int qt = 0; qt < a.nkt; ++qt) {
-      f32x16 s = bn;
-      if (qt + 1 < a.nkt) bn = win_bias_tile(brow, (qt + 1) * 32);
+      f32x16 s = b0;
+      b0 = b1;
+      if (qt + 2 < a.nkt) b1 = win_bias_tile(brow, (qt + 2) * 32);
       f32x16 dp, lz;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {   // row constants of queries qt*32 + 8g + 4h + j
@@ -482,8 +523,11 @@ extern "C" int lci_window_attn_fwd(const void* qkv, const float* qkv_bias, const
   if (win_fill(a, geo, scale)) return 1;
   if (a.mode == 0 && has_mask) a.T = a.nW;
   a.qkv = (const bf16*)qkv; a.qkv_bias = qkv_bias; a.bias = bias; a.out = (bf16*)out; a.lse2 = lse2;
-  (void)hipFuncSetAttribute((const void*)win_attn_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipLaunchKernelGGL(win_attn_fwd_kernel, dim3(a.Bw, a.H), dim3(256), win_lds(a, false), (hipStream_t)stream, a);
+  constexpr int NW = 8;   // 8 waves share the window's K/V: 4 waves per SIMD at 2 workgroups per CU (LDS-bound)
+  (void)hipFuncSetAttribute((const void*)win_attn_fwd_kernel<NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024);
+  hipLaunchKernelGGL(win_attn_fwd_kernel<NW>, dim3(a.Bw, a.H), dim3(NW * 64), win_lds(a, false), (hipStream_t)stream,
+                     a);
   LCI_LAUNCH_CHECK();
   return 0;
 }
