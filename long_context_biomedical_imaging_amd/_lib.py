@@ -12,7 +12,7 @@ import os
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liblci.so")
+LIB_PATH = os.environ.get("LCI_LIB_PATH", os.path.join(HERE, "liblci.so"))   # override: kernel-variant A/B runs
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int

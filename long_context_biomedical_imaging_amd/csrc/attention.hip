@@ -26,6 +26,12 @@ constexpr int LD_ROW = 72;    // LDS row stride (elements) for tiles read by row
 constexpr int LD_TR = 96;     // LDS row stride for tiles read only transposed: 192 B, tr_b16 conflict-free
 constexpr float NEG_BIG = -1.0e30f;
 
+#ifdef LCI_IGLP   // scheduling-strategy experiments (tools/attn_variants.sh)
+#define LCI_SCHED_HINT() __builtin_amdgcn_iglp_opt(LCI_IGLP)
+#else
+#define LCI_SCHED_HINT()
+#endif
+
 struct AttnArgs {
   const bf16* q; const bf16* k; const bf16* v;    // base pointers of head 0, batch 0
   const bf16* o; const bf16* dout;                 // bwd only
@@ -126,6 +132,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
       kr.load(kp, a.rs_k, (kt + 1) * KT, L, tid);
       vr.load(vp, a.rs_v, (kt + 1) * KT, L, tid);
     }
+    LCI_SCHED_HINT();
     // S'^T tiles: keys 0..31 and 32..63 of this tile (rows), queries on lanes
     f32x16 s0 = mfma32(frag_row(kl, LD_ROW, 0, 0, lane), qf[0], negm);
     f32x16 s1 = mfma32(frag_row(kl, LD_ROW, 32, 0, lane), qf[0], negm);
@@ -239,7 +246,7 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnArgs a) {
 
 // ---------------------------------------------------------------------- backward: dK, dV kernel
 template <int NW>
-__global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dkdv_kernel(AttnArgs a) {
+__global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv_kernel(AttnArgs a) {
   constexpr int NT = NW * 64;
   constexpr int TILE = 2 * KT * LD_ROW;                 // Q tile + dO tile (both read by rows and transposed)
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * TILE];
@@ -302,6 +309,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dkdv_kernel(AttnArgs a) {
       qr.load(qp, a.rs_q, (qt + 1) * KT, L, tid);
       dr.load(dop, a.rs_do, (qt + 1) * KT, L, tid);
     }
+    LCI_SCHED_HINT();
     // Two 32-query halves per 64-query tile (halves the live S/dP/P/dS registers); key on the lane.
 #pragma unroll
     for (int qs = 0; qs < 2; ++qs) {
@@ -428,6 +436,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnArgs a) {
       kr.load(kp, a.rs_k, (kt + 1) * KT, L, tid);
       vr.load(vp, a.rs_v, (kt + 1) * KT, L, tid);
     }
+    LCI_SCHED_HINT();
     f32x16 s0 = mfma32(frag_row(kl, LD_ROW, 0, 0, lane), qf[0], neg_lse);
     f32x16 s1 = mfma32(frag_row(kl, LD_ROW, 32, 0, lane), qf[0], neg_lse);
     f32x16 p0 = mfma32(frag_row(vl, LD_ROW, 0, 0, lane), df[0], neg_dlt);
@@ -544,7 +553,10 @@ extern "C" int lci_attn_bwd_stage(int stage, const void* qkv, const void* out, c
   a.hs = DH; a.H = H; a.L = L;
   a.scale = scale; a.c = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
-  constexpr int NW = 4;
+#ifndef LCI_BWD_NW
+#define LCI_BWD_NW 8   // 8 waves share each staged Q/dO (K/V) tile: -4% dK/dV, -8% dQ vs 4
+#endif
+  constexpr int NW = LCI_BWD_NW;
   dim3 grid((L + NW * 32 - 1) / (NW * 32), H, B);
   if (stage < 0 || stage == 0) {
     hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((L + 31) / 32, H, B), dim3(256), 0, s, a);
