@@ -75,14 +75,52 @@ template <> struct Row8<float> {
 
 constexpr int PF = 8;         // timesteps whose loads are issued ahead of the dependent recurrence
 
-__device__ __forceinline__ float softplus_raw(float v) { return v <= 20.f ? log1pf(__expf(v)) : v; }
-#define softplus(v) (a.softplus ? softplus_raw(v) : (v))
+constexpr float LN2 = 0.6931471805599453f;
+// softplus as F.softplus / mamba-ssm's log1pf(expf(v)) with threshold 20, from one v_exp and one v_log;
+// below e^-9, log(1 + e) = e to f32 precision (and 1 + e would drop e's low bits)
+__device__ __forceinline__ float softplus_fast(float v) {
+  const float e = exp2_fast(v * LOG2E);
+  const float r = e < 1.2e-4f ? e : __builtin_amdgcn_logf(1.f + e) * LN2;
+  return v > 20.f ? v : r;
+}
+#define softplus(v) (a.softplus ? softplus_fast(v) : (v))
+
+constexpr int SB = 64;        // steps per LDS-staged block of B_t / C_t rows (one row per lane)
+constexpr int BCS = 20;       // LDS floats per staged row (B 0..7, C 8..15, pad: 80-B rows)
+
+// Stage the f32 B_t (and C_t) rows of steps tb .. tb+SB-1 into this wave's LDS block, lane i <- step tb+i:
+// B/C are wave-uniform per step, so they are converted once here instead of in every lane at every step.
+template <typename T, bool WITH_C>
+__device__ __forceinline__ void stage_bc(const ScanArgs& a, float* bc, const T* Bp, const T* Cp, int tb, int t1,
+                                         int lane) {
+  const long long t = min(tb + lane, t1 - 1);
+  Row8<T> rb;
+  rb.load(Bp + t * a.tB);
+  float* dst = bc + lane * BCS;
+  *(f32x4*)dst = f32x4{rb[0], rb[1], rb[2], rb[3]};
+  *(f32x4*)(dst + 4) = f32x4{rb[4], rb[5], rb[6], rb[7]};
+  if constexpr (WITH_C) {
+    Row8<T> rc;
+    rc.load(Cp + t * a.tC);
+    *(f32x4*)(dst + 8) = f32x4{rc[0], rc[1], rc[2], rc[3]};
+    *(f32x4*)(dst + 12) = f32x4{rc[4], rc[5], rc[6], rc[7]};
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ void lds_row8(const float* p, float (&v)[SCAN_N]) {
+  const f32x4 lo = *(const f32x4*)p, hi = *(const f32x4*)(p + 4);
+#pragma unroll
+  for (int n = 0; n < 4; ++n) { v[n] = lo[n]; v[n + 4] = hi[n]; }
+}
 
 // ---------------------------------------------------------------------------------- forward chunk pass
 // MODE 0: zero initial state -> xend, sdt. MODE 1: xinit -> y (+ checkpoints).
 template <typename T, int MODE>
 __global__ __launch_bounds__(256) void scan_fwd_kernel(ScanArgs a) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __shared__ __attribute__((aligned(16))) float bcl[4][SB * BCS];
+  // wave index made provably uniform: chunk / step indices then live in SGPRs (scalar address arithmetic)
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int chunk = blockIdx.x * 4 + wv;
   const int b = blockIdx.z;
   const int d = blockIdx.y * 64 + lane;
@@ -97,44 +135,57 @@ __global__ __launch_bounds__(256) void scan_fwd_kernel(ScanArgs a) {
   const long long sidx = (((long long)b * a.nch + chunk) * a.Dx + dd) * SCAN_N;
 #pragma unroll
   for (int n = 0; n < SCAN_N; ++n) x[n] = MODE ? a.xinit[sidx + n] : 0.f;
-  const T* up = (const T*)a.u + b * a.bu + dd;
-  const T* dp = (const T*)a.delta + b * a.bd + dd;
+  // per-step addresses = wave-uniform row base (scalar arithmetic) + this lane's channel offset
+  const T* ub = (const T*)a.u + b * a.bu;
+  const T* db = (const T*)a.delta + b * a.bd;
   const T* Bp = (const T*)a.Bm + b * a.bB;
   const T* Cp = (const T*)a.Cm + b * a.bC;
-  T* yp = (T*)a.y + b * a.by + dd;
+  T* yb = (T*)a.y + b * a.by;
+  float* ckb = a.ckpt + (long long)b * a.nck * a.Dx * SCAN_N;
+  float* bc = bcl[wv];
   const int t0 = chunk * a.Tc, t1 = min(a.L, t0 + a.Tc);
   float sumdt = 0.f;
-  for (int tb = t0; tb < t1; tb += PF) {
-    float uf[PF], dr[PF];
-    Row8<T> Bv[PF], Cv[PF];
+  for (int tsb = t0; tsb < t1; tsb += SB) {
+    stage_bc<T, MODE == 1>(a, bc, Bp, Cp, tsb, t1, lane);
+    const int tse = min(t1, tsb + SB);
+    for (int tb = tsb; tb < tse; tb += PF) {
+      float uf[PF], dr[PF];
 #pragma unroll
-    for (int i = 0; i < PF; ++i) {        // all loads of the group first (clamped, branch-free)
-      const long long t = min(tb + i, t1 - 1);
-      uf[i] = ldf(up + t * a.tu);
-      dr[i] = ldf(dp + t * a.td);
-      Bv[i].load(Bp + t * a.tB);
-      if (MODE == 1) Cv[i].load(Cp + t * a.tC);
-    }
+      for (int i = 0; i < PF; ++i) {        // the group's u / dt loads first (clamped, branch-free)
+        const long long t = min(tb + i, tse - 1);
+        uf[i] = ldf((ub + t * a.tu) + dd);
+        dr[i] = ldf((db + t * a.td) + dd);
+      }
+      const int nvalid = tse - tb;   // >= PF except in a chunk's ragged tail
 #pragma unroll
-    for (int i = 0; i < PF; ++i) {
-      const int t = tb + i;
-      if (t < t1) {
-        if (MODE == 1 && a.write_ckpt && ((t & (CKPT - 1)) == 0) && valid) {
-          float* cp = a.ckpt + (((long long)b * a.nck + (t / CKPT)) * a.Dx + d) * SCAN_N;
-          *(f32x4*)cp = f32x4{x[0], x[1], x[2], x[3]};
-          *(f32x4*)(cp + 4) = f32x4{x[4], x[5], x[6], x[7]};
-        }
-        const float dt = softplus(dr[i] + bias);
-        const float dtu = dt * uf[i];
+      for (int i = 0; i < PF; ++i) {
+        if (i < nvalid) {
+          const int t = tb + i;
+          if (MODE == 1 && a.write_ckpt && ((t & (CKPT - 1)) == 0) && valid) {
+            float* cp = (ckb + (long long)(t / CKPT) * a.Dx * SCAN_N) + d * SCAN_N;
+            *(f32x4*)cp = f32x4{x[0], x[1], x[2], x[3]};
+            *(f32x4*)(cp + 4) = f32x4{x[4], x[5], x[6], x[7]};
+          }
+          const float* row = bc + (t - tsb) * BCS;
+          float Bv[SCAN_N];
+          lds_row8(row, Bv);
+          const float dt = softplus(dr[i] + bias);
+          const float dtu = dt * uf[i];
 #pragma unroll
-        for (int n = 0; n < SCAN_N; ++n) x[n] = fmaf(exp2_fast(dt * A2[n]), x[n], dtu * Bv[i][n]);
-        if (MODE == 1) {
-          float yv = Dd * uf[i];
+          for (int n = 0; n < SCAN_N; ++n) x[n] = fmaf(exp2_fast(dt * A2[n]), x[n], dtu * Bv[n]);
+          if (MODE == 1) {
+            float Cv[SCAN_N];
+            lds_row8(row + 8, Cv);
+            float y0 = Dd * uf[i], y1 = 0.f;
 #pragma unroll
-          for (int n = 0; n < SCAN_N; ++n) yv = fmaf(Cv[i][n], x[n], yv);
-          if (valid) yp[(long long)t * a.ty] = (T)yv;
-        } else {
-          sumdt += dt;
+            for (int n = 0; n < SCAN_N; n += 2) {
+              y0 = fmaf(Cv[n], x[n], y0);
+              y1 = fmaf(Cv[n + 1], x[n + 1], y1);
+            }
+            if (valid) (yb + (long long)t * a.ty)[dd] = (T)(y0 + y1);
+          } else {
+            sumdt += dt;
+          }
         }
       }
     }
@@ -147,38 +198,60 @@ __global__ __launch_bounds__(256) void scan_fwd_kernel(ScanArgs a) {
   }
 }
 
-// carry over chunks: xinit[c] = carry; carry = exp(A sdt[c]) carry + xend[c]   (thread per (b, d, n))
+// carry over chunks: xinit[c] = carry; carry = exp(A sdt[c]) carry + xend[c]
 // REVERSE: gin[c] = carry; carry = gl[c] + exp(A sdt[c]) carry, chunks from last to first.
+// One wave per (b, d): lane = (group g, state n), 8 groups of consecutive chunks. Each lane folds its group
+// with zero carry-in (the group's decay is exp(A * sum sdt)), the 8 group maps are combined across lanes,
+// then each lane replays its group from the true carry-in: 2 * nch/8 sequential steps instead of nch.
 template <bool REVERSE>
-__global__ __launch_bounds__(256) void scan_carry_kernel(ScanArgs a) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  const int total = a.B * a.Dx * SCAN_N;
-  if (i >= total) return;
-  const int n = i % SCAN_N, d = (i / SCAN_N) % a.Dx, b = i / (SCAN_N * a.Dx);
+__global__ __launch_bounds__(64) void scan_carry_kernel(ScanArgs a) {
+  const int lane = threadIdx.x, n = lane & 7, g = lane >> 3;
+  const int d = blockIdx.x, b = blockIdx.y;
   const float A2 = a.A[d * SCAN_N + n] * LOG2E;
-  float carry = 0.f;
   const float* src = REVERSE ? a.gl : a.xend;
   float* dst = REVERSE ? a.gin : a.xinit;
-  for (int kb = 0; kb < a.nch; kb += PF) {
+  const int G = (a.nch + 7) / 8;
+  const int k0 = min(a.nch, g * G), k1 = min(a.nch, k0 + G);
+  auto cidx = [&](int k) -> long long {
+    const int c = REVERSE ? a.nch - 1 - k : k;
+    return ((long long)b * a.nch + c) * a.Dx + d;
+  };
+  float E = 0.f, S = 0.f;
+  for (int kb = k0; kb < k1; kb += PF) {
     float sv[PF], ev[PF];
 #pragma unroll
     for (int i = 0; i < PF; ++i) {
-      const int k = min(kb + i, a.nch - 1);
-      const int c = REVERSE ? a.nch - 1 - k : k;
-      const long long ci = ((long long)b * a.nch + c) * a.Dx + d;
+      const long long ci = cidx(min(kb + i, k1 - 1));
       sv[i] = a.sdt[ci];
       ev[i] = src[ci * SCAN_N + n];
     }
 #pragma unroll
+    for (int i = 0; i < PF; ++i)
+      if (kb + i < k1) {
+        E = fmaf(exp2_fast(A2 * sv[i]), E, ev[i]);
+        S += sv[i];
+      }
+  }
+  float carry = 0.f;
+#pragma unroll
+  for (int gg = 0; gg < 8; ++gg) {
+    const float Sg = __shfl(S, gg * 8 + n), Eg = __shfl(E, gg * 8 + n);
+    if (gg < g) carry = fmaf(exp2_fast(A2 * Sg), carry, Eg);
+  }
+  for (int kb = k0; kb < k1; kb += PF) {
+    float sv[PF], ev[PF];
+#pragma unroll
     for (int i = 0; i < PF; ++i) {
-      const int k = kb + i;
-      if (k < a.nch) {
-        const int c = REVERSE ? a.nch - 1 - k : k;
-        const long long ci = ((long long)b * a.nch + c) * a.Dx + d;
-        dst[ci * SCAN_N + n] = carry;
+      const long long ci = cidx(min(kb + i, k1 - 1));
+      sv[i] = a.sdt[ci];
+      ev[i] = src[ci * SCAN_N + n];
+    }
+#pragma unroll
+    for (int i = 0; i < PF; ++i)
+      if (kb + i < k1) {
+        dst[cidx(kb + i) * SCAN_N + n] = carry;
         carry = fmaf(exp2_fast(A2 * sv[i]), carry, ev[i]);
       }
-    }
   }
 }
 
@@ -228,66 +301,101 @@ __global__ __launch_bounds__(256) void scan_bwd_agg_kernel(ScanArgs a) {
   }
 }
 
-// reduce 16 values over the 64 lanes of a wave (reduce-scatter butterfly): afterwards lane l holds the
-// total of value index (l >> 2) & 15.
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+
+__device__ __forceinline__ float sel_bits(unsigned m, float x, float y) {   // m ? x : y, m all-ones or zero
+  return __uint_as_float((__float_as_uint(x) & m) | (__float_as_uint(y) & ~m));
+}
+
+// Reduce 16 values over the 64 lanes of a wave (reduce-scatter butterfly); afterwards lane l holds the total of
+// value index (l >> 2) & 15. Levels: lanes l / l^32 by v_permlane32_swap and l / l^16 by v_permlane16_swap on
+// value pairs (the swap itself routes each half its kept index: one add per pair, no select), then l / l^8
+// (DPP row_ror:8) and the half-row mirror (DPP), then the quad (DPP quad_perm) -- no LDS round trips.
 __device__ __forceinline__ float wave_reduce16(float (&v)[16], int lane) {
 #pragma unroll
-  for (int lvl = 0; lvl < 4; ++lvl) {
-    const int m = 32 >> lvl;
-    const int half = 8 >> lvl;
-    const bool up = (lane & m) != 0;
-#pragma unroll
-    for (int i = 0; i < half; ++i) {
-      const float send = up ? v[i] : v[i + half];
-      const float keep = up ? v[i + half] : v[i];
-      v[i] = keep + __shfl_xor(send, m);
-    }
+  for (int i = 0; i < 8; ++i) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 8]), false, false);
+    v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
   }
-  float r = v[0];
-  r += __shfl_xor(r, 2);
-  r += __shfl_xor(r, 1);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 4]), false, false);
+    v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  const unsigned up8 = (lane & 8) ? 0xffffffffu : 0u, up4 = (lane & 4) ? 0xffffffffu : 0u;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const float lo = v[i] + dpp<0x128>(v[i]), hi = v[i + 2] + dpp<0x128>(v[i + 2]);   // row_ror:8 = lane ^ 8
+    v[i] = sel_bits(up8, hi, lo);
+  }
+  const float lo = v[0] + dpp<0x141>(v[0]), hi = v[1] + dpp<0x141>(v[1]);             // row_half_mirror
+  float r = sel_bits(up4, hi, lo);
+  r += dpp<0xB1>(r);   // quad_perm [1,0,3,2]
+  r += dpp<0x4E>(r);   // quad_perm [2,3,0,1]
   return r;
 }
 
 // ------------------------------------------------------------------------------------- backward pass C
-// Workgroup = one (b, chunk), NWV waves cover all channels. Sub-blocks of CKPT steps in reverse.
+// Workgroup = one (b, chunk), up to 4 waves cover 256 channels. Sub-blocks of CKPT steps in reverse: the
+// sub-block's states x and decays exp(dt A) are recomputed from its checkpoint into registers, then swept back.
+// B_t / C_t rows go through LDS once per workgroup (8 threads load the next sub-block's rows ahead).
 template <typename T>
 __global__ __launch_bounds__(256) void scan_bwd_kernel(ScanArgs a) {
   __shared__ float red[CKPT][2 * SCAN_N];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __shared__ __attribute__((aligned(16))) float bcs[CKPT][BCS];
+  const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int chunk = blockIdx.x, b = blockIdx.z;
   const int d = blockIdx.y * 256 + wv * 64 + lane;
   const bool valid = d < a.Dx;
   const int dd = valid ? d : a.Dx - 1;
-  for (int i = threadIdx.x; i < CKPT * 2 * SCAN_N; i += blockDim.x) (&red[0][0])[i] = 0.f;
-  float A1[SCAN_N], A2[SCAN_N], h[SCAN_N], dA[SCAN_N];
+  for (int i = tid; i < CKPT * 2 * SCAN_N; i += blockDim.x) (&red[0][0])[i] = 0.f;
+  float A2[SCAN_N], h[SCAN_N], dA[SCAN_N];
 #pragma unroll
   for (int n = 0; n < SCAN_N; ++n) {
-    A1[n] = a.A[dd * SCAN_N + n];
-    A2[n] = A1[n] * LOG2E;
+    A2[n] = a.A[dd * SCAN_N + n] * LOG2E;
     h[n] = valid ? a.gin[(((long long)b * a.nch + chunk) * a.Dx + d) * SCAN_N + n] : 0.f;
     dA[n] = 0.f;
   }
   const float bias = a.dbias ? a.dbias[dd] : 0.f;
   const float Dd = a.D ? a.D[dd] : 0.f;
   float dDacc = 0.f, dbacc = 0.f;
-  const T* up = (const T*)a.u + b * a.bu + dd;
-  const T* dp = (const T*)a.delta + b * a.bd + dd;
-  const T* gyp = (const T*)a.dy + b * a.bdy + dd;
+  const T* ub = (const T*)a.u + b * a.bu;
+  const T* db = (const T*)a.delta + b * a.bd;
+  const T* gb = (const T*)a.dy + b * a.bdy;
   const T* Bp = (const T*)a.Bm + b * a.bB;
   const T* Cp = (const T*)a.Cm + b * a.bC;
-  T* dup = (T*)a.du + b * a.bdu + dd;
-  T* ddp = (T*)a.ddelta + b * a.bdd + dd;
+  T* dub = (T*)a.du + b * a.bdu;
+  T* ddb = (T*)a.ddelta + b * a.bdd;
+  const float* ckb = a.ckpt + (long long)b * a.nck * a.Dx * SCAN_N;
   const int t0 = chunk * a.Tc, t1 = min(a.L, t0 + a.Tc);
   const int nsb = (t1 - t0 + CKPT - 1) / CKPT;
-  __syncthreads();
+  float rbc[2 * SCAN_N];   // threads < CKPT: rows of step (next sub-block start + tid)
+  auto load_rows = [&](int s0) {
+    if (tid < CKPT) {
+      const long long t = min(s0 + tid, t1 - 1);
+      Row8<T> rb, rc;
+      rb.load(Bp + t * a.tB);
+      rc.load(Cp + t * a.tC);
+#pragma unroll
+      for (int n = 0; n < SCAN_N; ++n) { rbc[n] = rb[n]; rbc[SCAN_N + n] = rc[n]; }
+    }
+  };
+  load_rows(t0 + (nsb - 1) * CKPT);
   for (int sb = nsb - 1; sb >= 0; --sb) {
     const int s0 = t0 + sb * CKPT;
-    // all loads of the sub-block first (clamped addresses, no branches), then the dependent math
-    float xck[SCAN_N], xs[CKPT][SCAN_N], uf[CKPT], dr[CKPT], gyv[CKPT];
-    Row8<T> Bv[CKPT], Cv[CKPT];
+    if (tid < CKPT) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        *(f32x4*)&bcs[tid][4 * k] = f32x4{rbc[4 * k], rbc[4 * k + 1], rbc[4 * k + 2], rbc[4 * k + 3]};
+    }
+    if (sb > 0) load_rows(s0 - CKPT);
+    // per-lane loads of the sub-block (clamped addresses, no branches)
+    float xck[SCAN_N], uf[CKPT], dr[CKPT], gyv[CKPT];
     {
-      const float* cp = a.ckpt + (((long long)b * a.nck + s0 / CKPT) * a.Dx + dd) * SCAN_N;
+      const float* cp = (ckb + (long long)(s0 / CKPT) * a.Dx * SCAN_N) + dd * SCAN_N;
       const f32x4 c0 = *(const f32x4*)cp, c1 = *(const f32x4*)(cp + 4);
 #pragma unroll
       for (int n = 0; n < 4; ++n) { xck[n] = c0[n]; xck[n + 4] = c1[n]; }
@@ -295,21 +403,23 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(ScanArgs a) {
 #pragma unroll
     for (int i = 0; i < CKPT; ++i) {
       const long long t = min(s0 + i, t1 - 1);
-      uf[i] = ldf(up + t * a.tu);
-      dr[i] = ldf(dp + t * a.td) + bias;
-      gyv[i] = valid ? ldf(gyp + t * a.tdy) : 0.f;
-      Bv[i].load(Bp + t * a.tB);
-      Cv[i].load(Cp + t * a.tC);
+      uf[i] = ldf((ub + t * a.tu) + dd);
+      dr[i] = ldf((db + t * a.td) + dd) + bias;
+      gyv[i] = valid ? ldf((gb + t * a.tdy) + dd) : 0.f;
     }
-    // forward recompute of the sub-block from its checkpoint: xs[i] = x after step s0 + i
+    __syncthreads();   // rows visible; previous sub-block's dB/dC flush done
+    // forward recompute from the checkpoint: xs[i] = x after step s0 + i, at[i] = exp(dt A)
+    float xs[CKPT][SCAN_N], at[CKPT][SCAN_N], dts[CKPT];
 #pragma unroll
     for (int i = 0; i < CKPT; ++i) {
-      const float dt = softplus(dr[i]);
-      const float dtu = dt * uf[i];
+      float Bv[SCAN_N];
+      lds_row8(&bcs[i][0], Bv);
+      dts[i] = softplus(dr[i]);
+      const float dtu = dts[i] * uf[i];
 #pragma unroll
       for (int n = 0; n < SCAN_N; ++n) {
-        const float xp = (i == 0) ? xck[n] : xs[i - 1][n];
-        xs[i][n] = fmaf(exp2_fast(dt * A2[n]), xp, dtu * Bv[i][n]);
+        at[i][n] = exp2_fast(dts[i] * A2[n]);
+        xs[i][n] = fmaf(at[i][n], (i == 0) ? xck[n] : xs[i - 1][n], dtu * Bv[n]);
       }
     }
     // reverse sweep
@@ -317,49 +427,47 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(ScanArgs a) {
     for (int i = CKPT - 1; i >= 0; --i) {
       const int t = s0 + i;
       if (t < t1) {
-        const float draw = dr[i];
-        const float dt = softplus(draw);
-        const float gy = gyv[i];
-        float v[16];
-        float du = Dd * gy, ddt = 0.f;
+        float Bv[SCAN_N], Cv[SCAN_N];
+        lds_row8(&bcs[i][0], Bv);
+        lds_row8(&bcs[i][SCAN_N], Cv);
+        const float dt = dts[i], gy = gyv[i];   // gy = 0 on padding lanes: their dC partials vanish
         const float dtu = dt * uf[i];
+        const float dtuv = valid ? dtu : 0.f;    // ... and dB partials
+        float v[16];
+        float sgB = 0.f, sA = 0.f;   // sum_n g_n B_n, sum_n g_n (a_n x_{t-1,n}) A2_n
 #pragma unroll
         for (int n = 0; n < SCAN_N; ++n) {
-          const float xp = (i == 0) ? xck[n] : xs[i - 1][n];
-          const float at = exp2_fast(dt * A2[n]);
-          const float gt = fmaf(Cv[i][n], gy, h[n]);
-          v[SCAN_N + n] = gy * xs[i][n];                  // dC_t partial
-          v[n] = gt * dtu;                                // dB_t partial
-          du = fmaf(gt * dt, Bv[i][n], du);
-          const float gxa = gt * xp * at;
-          ddt = fmaf(gt, Bv[i][n] * uf[i], fmaf(gxa, A1[n], ddt));
+          const float gt = fmaf(Cv[n], gy, h[n]);
+          v[SCAN_N + n] = gy * xs[i][n];                   // dC_t partial
+          v[n] = gt * dtuv;                                // dB_t partial
+          sgB = fmaf(gt, Bv[n], sgB);
+          const float gxa = gt * fmaf(-dtu, Bv[n], xs[i][n]);   // g * a * x_{t-1} = g (x_t - dt u B)
+          sA = fmaf(gxa, A2[n], sA);
           dA[n] = fmaf(gxa, dt, dA[n]);
-          h[n] = at * gt;
+          h[n] = at[i][n] * gt;
         }
-        if (!valid) {
-#pragma unroll
-          for (int k = 0; k < 16; ++k) v[k] = 0.f;
-        }
-        const float sg = (a.softplus && draw <= 20.f) ? 1.f / (1.f + __expf(-draw)) : 1.f;
+        const float du = fmaf(dt, sgB, Dd * gy);
+        const float ddt = fmaf(uf[i], sgB, sA * LN2);
+        const float draw = dr[i];
+        const float sg = (a.softplus && draw <= 20.f) ? 1.f / (1.f + exp2_fast(-draw * LOG2E)) : 1.f;
         const float ddl = ddt * sg;
         dDacc = fmaf(gy, uf[i], dDacc);
         dbacc += ddl;
         if (valid) {
-          dup[(long long)t * a.tdu] = (T)du;
-          ddp[(long long)t * a.tdd] = (T)ddl;
+          (dub + (long long)t * a.tdu)[dd] = (T)du;
+          (ddb + (long long)t * a.tdd)[dd] = (T)ddl;
         }
         const float r = wave_reduce16(v, lane);
         if ((lane & 3) == 0) atomicAdd(&red[i][lane >> 2], r);
       }
     }
     __syncthreads();
-    for (int k = threadIdx.x; k < CKPT * 2 * SCAN_N; k += blockDim.x) {
+    for (int k = tid; k < CKPT * 2 * SCAN_N; k += blockDim.x) {
       const int i = k / (2 * SCAN_N), j = k % (2 * SCAN_N);
       const int t = s0 + i;
       if (t < t1) atomicAdd(a.dBC + ((long long)b * a.L + t) * (2 * SCAN_N) + j, red[i][j]);
       red[i][j] = 0.f;
     }
-    __syncthreads();
   }
   if (valid) {
 #pragma unroll
@@ -495,11 +603,10 @@ extern "C" int lci_selective_scan_fwd(int dtype, const void* u, const void* delt
   a.xend = xend; a.xinit = xinit; a.sdt = sdt; a.ckpt = ckpt; a.write_ckpt = ckpt != nullptr;
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((a.nch + 3) / 4, (Dx + 63) / 64, B);
-  const int nthr = B * Dx * SCAN_N;
   if (dtype == 1) hipLaunchKernelGGL((scan_fwd_kernel<bf16, 0>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((scan_fwd_kernel<float, 0>), grid, dim3(256), 0, s, a);
   LCI_LAUNCH_CHECK();
-  hipLaunchKernelGGL(scan_carry_kernel<false>, dim3((nthr + 255) / 256), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(scan_carry_kernel<false>, dim3(Dx, B), dim3(64), 0, s, a);
   LCI_LAUNCH_CHECK();
   if (dtype == 1) hipLaunchKernelGGL((scan_fwd_kernel<bf16, 1>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((scan_fwd_kernel<float, 1>), grid, dim3(256), 0, s, a);
@@ -525,11 +632,10 @@ extern "C" int lci_selective_scan_bwd(int dtype, const void* u, const void* delt
   a.sdt = (float*)sdt; a.ckpt = (float*)ckpt; a.gl = gl; a.gin = gin;
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((a.nch + 3) / 4, (Dx + 63) / 64, B);
-  const int nthr = B * Dx * SCAN_N;
   if (dtype == 1) hipLaunchKernelGGL((scan_bwd_agg_kernel<bf16>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((scan_bwd_agg_kernel<float>), grid, dim3(256), 0, s, a);
   LCI_LAUNCH_CHECK();
-  hipLaunchKernelGGL(scan_carry_kernel<true>, dim3((nthr + 255) / 256), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(scan_carry_kernel<true>, dim3(Dx, B), dim3(64), 0, s, a);
   LCI_LAUNCH_CHECK();
   const int nwv = Dx >= 256 ? 4 : (Dx + 63) / 64;
   dim3 gridc(a.nch, (Dx + 255) / 256, B);
