@@ -259,7 +259,8 @@ __global__ __launch_bounds__(64) void scan_carry_kernel(ScanArgs a) {
 // local adjoint with zero carry-in from later chunks: Gl = a_{t0} g_{t0}
 template <typename T>
 __global__ __launch_bounds__(256) void scan_bwd_agg_kernel(ScanArgs a) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __shared__ __attribute__((aligned(16))) float bcl[4][SB * BCS];
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int chunk = blockIdx.x * 4 + wv;
   const int b = blockIdx.z;
   const int d = blockIdx.y * 64 + lane;
@@ -270,29 +271,44 @@ __global__ __launch_bounds__(256) void scan_bwd_agg_kernel(ScanArgs a) {
 #pragma unroll
   for (int n = 0; n < SCAN_N; ++n) { A2[n] = a.A[dd * SCAN_N + n] * LOG2E; g[n] = 0.f; }
   const float bias = a.dbias ? a.dbias[dd] : 0.f;
-  const T* dp = (const T*)a.delta + b * a.bd + dd;
-  const T* gyp = (const T*)a.dy + b * a.bdy + dd;
+  const T* db = (const T*)a.delta + b * a.bd;
+  const T* gb = (const T*)a.dy + b * a.bdy;
   const T* Cp = (const T*)a.Cm + b * a.bC;
+  float* bc = bcl[wv];
   const int t0 = chunk * a.Tc, t1 = min(a.L, t0 + a.Tc);
-  for (int te = t1 - 1; te >= t0; te -= PF) {
-    float dr[PF], gyv[PF];
-    Row8<T> Cv[PF];
-#pragma unroll
-    for (int i = 0; i < PF; ++i) {
-      const long long t = max(te - i, t0);
-      dr[i] = ldf(dp + t * a.td);
-      gyv[i] = ldf(gyp + t * a.tdy);
-      Cv[i].load(Cp + t * a.tC);
+  // staging blocks of SB steps from the chunk's end; C_t rows go to LDS slots 8..15 (stage_bc's C slot)
+  for (int tsb = t0 + ((t1 - 1 - t0) / SB) * SB; tsb >= t0; tsb -= SB) {
+    {
+      const long long t = min(tsb + lane, t1 - 1);
+      Row8<T> rc;
+      rc.load(Cp + t * a.tC);
+      float* dst = bc + lane * BCS;
+      *(f32x4*)(dst + 8) = f32x4{rc[0], rc[1], rc[2], rc[3]};
+      *(f32x4*)(dst + 12) = f32x4{rc[4], rc[5], rc[6], rc[7]};
+      __builtin_amdgcn_wave_barrier();
     }
+    const int tse = min(t1, tsb + SB);
+    for (int te = tse - 1; te >= tsb; te -= PF) {
+      float dr[PF], gyv[PF];
 #pragma unroll
-    for (int i = 0; i < PF; ++i) {
-      if (te - i >= t0) {
-        const float dt = softplus(dr[i] + bias);
-        const float gy = valid ? gyv[i] : 0.f;
+      for (int i = 0; i < PF; ++i) {
+        const long long t = max(te - i, tsb);
+        dr[i] = ldf((db + t * a.td) + dd);
+        gyv[i] = ldf((gb + t * a.tdy) + dd);
+      }
 #pragma unroll
-        for (int n = 0; n < SCAN_N; ++n) g[n] = exp2_fast(dt * A2[n]) * fmaf(Cv[i][n], gy, g[n]);
+      for (int i = 0; i < PF; ++i) {
+        if (te - i >= tsb) {
+          float Cv[SCAN_N];
+          lds_row8(bc + (te - i - tsb) * BCS + 8, Cv);
+          const float dt = softplus(dr[i] + bias);
+          const float gy = valid ? gyv[i] : 0.f;
+#pragma unroll
+          for (int n = 0; n < SCAN_N; ++n) g[n] = exp2_fast(dt * A2[n]) * fmaf(Cv[n], gy, g[n]);
+        }
       }
     }
+    __builtin_amdgcn_wave_barrier();
   }
   if (valid) {
     float* o = a.gl + (((long long)b * a.nch + chunk) * a.Dx + d) * SCAN_N;
@@ -341,17 +357,18 @@ __device__ __forceinline__ float wave_reduce16(float (&v)[16], int lane) {
 // ------------------------------------------------------------------------------------- backward pass C
 // Workgroup = one (b, chunk), up to 4 waves cover 256 channels. Sub-blocks of CKPT steps in reverse: the
 // sub-block's states x and decays exp(dt A) are recomputed from its checkpoint into registers, then swept back.
-// B_t / C_t rows go through LDS once per workgroup (8 threads load the next sub-block's rows ahead).
+// B_t / C_t rows and the per-token dB/dC partial sums go through LDS in blocks of SB steps (two workgroup
+// barriers per SB steps); each lane's u / dt / dy / checkpoint loads are issued one sub-block ahead.
 template <typename T>
 __global__ __launch_bounds__(256) void scan_bwd_kernel(ScanArgs a) {
-  __shared__ float red[CKPT][2 * SCAN_N];
-  __shared__ __attribute__((aligned(16))) float bcs[CKPT][BCS];
+  __shared__ float red[SB][2 * SCAN_N];
+  __shared__ __attribute__((aligned(16))) float bcs[SB][BCS];
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int chunk = blockIdx.x, b = blockIdx.z;
   const int d = blockIdx.y * 256 + wv * 64 + lane;
   const bool valid = d < a.Dx;
   const int dd = valid ? d : a.Dx - 1;
-  for (int i = tid; i < CKPT * 2 * SCAN_N; i += blockDim.x) (&red[0][0])[i] = 0.f;
+  for (int i = tid; i < SB * 2 * SCAN_N; i += blockDim.x) (&red[0][0])[i] = 0.f;
   float A2[SCAN_N], h[SCAN_N], dA[SCAN_N];
 #pragma unroll
   for (int n = 0; n < SCAN_N; ++n) {
@@ -372,49 +389,65 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(ScanArgs a) {
   const float* ckb = a.ckpt + (long long)b * a.nck * a.Dx * SCAN_N;
   const int t0 = chunk * a.Tc, t1 = min(a.L, t0 + a.Tc);
   const int nsb = (t1 - t0 + CKPT - 1) / CKPT;
-  float rbc[2 * SCAN_N];   // threads < CKPT: rows of step (next sub-block start + tid)
-  auto load_rows = [&](int s0) {
-    if (tid < CKPT) {
-      const long long t = min(s0 + tid, t1 - 1);
-      Row8<T> rb, rc;
-      rb.load(Bp + t * a.tB);
-      rc.load(Cp + t * a.tC);
+  // per-lane operands of one sub-block, loaded a sub-block ahead
+  float nck[SCAN_N], nu[CKPT], nd[CKPT], ng[CKPT];
+  auto load_lane = [&](int s0) {
+    const float* cp = (ckb + (long long)(s0 / CKPT) * a.Dx * SCAN_N) + dd * SCAN_N;
+    const f32x4 c0 = *(const f32x4*)cp, c1 = *(const f32x4*)(cp + 4);
 #pragma unroll
-      for (int n = 0; n < SCAN_N; ++n) { rbc[n] = rb[n]; rbc[SCAN_N + n] = rc[n]; }
-    }
-  };
-  load_rows(t0 + (nsb - 1) * CKPT);
-  for (int sb = nsb - 1; sb >= 0; --sb) {
-    const int s0 = t0 + sb * CKPT;
-    if (tid < CKPT) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        *(f32x4*)&bcs[tid][4 * k] = f32x4{rbc[4 * k], rbc[4 * k + 1], rbc[4 * k + 2], rbc[4 * k + 3]};
-    }
-    if (sb > 0) load_rows(s0 - CKPT);
-    // per-lane loads of the sub-block (clamped addresses, no branches)
-    float xck[SCAN_N], uf[CKPT], dr[CKPT], gyv[CKPT];
-    {
-      const float* cp = (ckb + (long long)(s0 / CKPT) * a.Dx * SCAN_N) + dd * SCAN_N;
-      const f32x4 c0 = *(const f32x4*)cp, c1 = *(const f32x4*)(cp + 4);
-#pragma unroll
-      for (int n = 0; n < 4; ++n) { xck[n] = c0[n]; xck[n + 4] = c1[n]; }
-    }
+    for (int n = 0; n < 4; ++n) { nck[n] = c0[n]; nck[n + 4] = c1[n]; }
 #pragma unroll
     for (int i = 0; i < CKPT; ++i) {
       const long long t = min(s0 + i, t1 - 1);
-      uf[i] = ldf((ub + t * a.tu) + dd);
-      dr[i] = ldf((db + t * a.td) + dd) + bias;
-      gyv[i] = valid ? ldf((gb + t * a.tdy) + dd) : 0.f;
+      nu[i] = ldf((ub + t * a.tu) + dd);
+      nd[i] = ldf((db + t * a.td) + dd);
+      ng[i] = ldf((gb + t * a.tdy) + dd);
     }
-    __syncthreads();   // rows visible; previous sub-block's dB/dC flush done
+  };
+  load_lane(t0 + (nsb - 1) * CKPT);
+  int blk0 = -1;   // first step of the staged block
+  for (int sb = nsb - 1; sb >= 0; --sb) {
+    const int s0 = t0 + sb * CKPT;
+    if (blk0 < 0 || s0 < blk0) {   // new staging block [blk0, blk0 + SB) holding s0 (uniform branch)
+      if (blk0 >= 0) {             // flush the finished block's dB/dC sums
+        __syncthreads();
+        for (int k = tid; k < SB * 2 * SCAN_N; k += blockDim.x) {
+          const int i = k / (2 * SCAN_N), j = k % (2 * SCAN_N);
+          const int t = blk0 + i;
+          if (t < t1) atomicAdd(a.dBC + ((long long)b * a.L + t) * (2 * SCAN_N) + j, red[i][j]);
+          red[i][j] = 0.f;
+        }
+      }
+      blk0 = t0 + ((s0 - t0) / SB) * SB;
+      if (tid < SB) {
+        const long long t = min(blk0 + tid, t1 - 1);
+        Row8<T> rb, rc;
+        rb.load(Bp + t * a.tB);
+        rc.load(Cp + t * a.tC);
+        *(f32x4*)&bcs[tid][0] = f32x4{rb[0], rb[1], rb[2], rb[3]};
+        *(f32x4*)&bcs[tid][4] = f32x4{rb[4], rb[5], rb[6], rb[7]};
+        *(f32x4*)&bcs[tid][8] = f32x4{rc[0], rc[1], rc[2], rc[3]};
+        *(f32x4*)&bcs[tid][12] = f32x4{rc[4], rc[5], rc[6], rc[7]};
+      }
+      __syncthreads();
+    }
+    float xck[SCAN_N], uf[CKPT], gyv[CKPT], dts[CKPT];
+#pragma unroll
+    for (int n = 0; n < SCAN_N; ++n) xck[n] = nck[n];
+#pragma unroll
+    for (int i = 0; i < CKPT; ++i) {
+      uf[i] = nu[i];
+      gyv[i] = valid ? ng[i] : 0.f;
+      dts[i] = softplus(nd[i] + bias);
+    }
+    if (sb > 0) load_lane(s0 - CKPT);
+    const float* rows = &bcs[s0 - blk0][0];
     // forward recompute from the checkpoint: xs[i] = x after step s0 + i, at[i] = exp(dt A)
-    float xs[CKPT][SCAN_N], at[CKPT][SCAN_N], dts[CKPT];
+    float xs[CKPT][SCAN_N], at[CKPT][SCAN_N];
 #pragma unroll
     for (int i = 0; i < CKPT; ++i) {
       float Bv[SCAN_N];
-      lds_row8(&bcs[i][0], Bv);
-      dts[i] = softplus(dr[i]);
+      lds_row8(rows + i * BCS, Bv);
       const float dtu = dts[i] * uf[i];
 #pragma unroll
       for (int n = 0; n < SCAN_N; ++n) {
@@ -428,8 +461,8 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(ScanArgs a) {
       const int t = s0 + i;
       if (t < t1) {
         float Bv[SCAN_N], Cv[SCAN_N];
-        lds_row8(&bcs[i][0], Bv);
-        lds_row8(&bcs[i][SCAN_N], Cv);
+        lds_row8(rows + i * BCS, Bv);
+        lds_row8(rows + i * BCS + SCAN_N, Cv);
         const float dt = dts[i], gy = gyv[i];   // gy = 0 on padding lanes: their dC partials vanish
         const float dtu = dt * uf[i];
         const float dtuv = valid ? dtu : 0.f;    // ... and dB partials
@@ -448,8 +481,8 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(ScanArgs a) {
         }
         const float du = fmaf(dt, sgB, Dd * gy);
         const float ddt = fmaf(uf[i], sgB, sA * LN2);
-        const float draw = dr[i];
-        const float sg = (a.softplus && draw <= 20.f) ? 1.f / (1.f + exp2_fast(-draw * LOG2E)) : 1.f;
+        // d softplus / dx = sigmoid(x) = 1 - exp(-softplus(x))  (1 above the threshold 20)
+        const float sg = a.softplus ? 1.f - exp2_fast(-dt * LOG2E) : 1.f;
         const float ddl = ddt * sg;
         dDacc = fmaf(gy, uf[i], dDacc);
         dbacc += ddl;
@@ -458,16 +491,15 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(ScanArgs a) {
           (ddb + (long long)t * a.tdd)[dd] = (T)ddl;
         }
         const float r = wave_reduce16(v, lane);
-        if ((lane & 3) == 0) atomicAdd(&red[i][lane >> 2], r);
+        if ((lane & 3) == 0) atomicAdd(&red[t - blk0][lane >> 2], r);
       }
     }
-    __syncthreads();
-    for (int k = tid; k < CKPT * 2 * SCAN_N; k += blockDim.x) {
-      const int i = k / (2 * SCAN_N), j = k % (2 * SCAN_N);
-      const int t = s0 + i;
-      if (t < t1) atomicAdd(a.dBC + ((long long)b * a.L + t) * (2 * SCAN_N) + j, red[i][j]);
-      red[i][j] = 0.f;
-    }
+  }
+  __syncthreads();
+  for (int k = tid; k < SB * 2 * SCAN_N; k += blockDim.x) {
+    const int i = k / (2 * SCAN_N), j = k % (2 * SCAN_N);
+    const int t = blk0 + i;
+    if (t < t1) atomicAdd(a.dBC + ((long long)b * a.L + t) * (2 * SCAN_N) + j, red[i][j]);
   }
   if (valid) {
 #pragma unroll
