@@ -43,32 +43,83 @@ struct FftArgs {
   int single;                           // col passes: 1 = the source is the filter (C rows, no pairing)
 };
 
-// radix-2 Stockham FFT of `cnt` sequences of length N (=2^lN) stored [seq][N] in x; result back in x
-// (ping-pong through y). sign -1: forward (W = exp(-2 pi i/N)), +1: inverse (unnormalised).
-__device__ void lds_fft(f32x2* x, f32x2* y, int N, int lN, int cnt, const f32x2* tw, int n, bool inverse) {
-  const int half = N >> 1;
-  const int total = cnt * half;
-  for (int s = 0; s < lN; ++s) {
-    const int Ns = 1 << s;
-    const int tstep = n / (2 * Ns);
-    for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
-      const int sq = idx / half, j = idx - sq * half;
-      const int k = j & (Ns - 1);
-      f32x2 u0 = x[sq * N + j], u1 = x[sq * N + j + half];
-      f32x2 w = tw[k * tstep];
-      if (inverse) w.y = -w.y;
-      u1 = cmul(u1, w);
-      const int d = ((j - k) << 1) + k;
-      y[sq * N + d] = u0 + u1;
-      y[sq * N + d + Ns] = u0 - u1;
+// ------------------------------------------------------------------- sub-FFTs: radix-8/4/2 Stockham in LDS
+// Each pass: a thread takes one radix-R butterfly (R points strided N/R apart) into registers, applies the
+// twiddles W_{Ns R}^{m r} (from the LDS table twl[t] = W_N^t), does the R-point DFT in registers and writes the
+// R outputs Ns apart (Stockham auto-sort). N = 512 is three radix-8 passes (3 LDS round trips, 3 barriers).
+template <bool INV> __device__ __forceinline__ f32x2 mul_mi(f32x2 v) {   // v * (-i) forward, v * (+i) inverse
+  return INV ? f32x2{-v.y, v.x} : f32x2{v.y, -v.x};
+}
+
+template <int R, bool INV> __device__ __forceinline__ void dft(f32x2 (&v)[R]) {
+  if constexpr (R == 2) {
+    const f32x2 a = v[0], b = v[1];
+    v[0] = a + b; v[1] = a - b;
+  } else if constexpr (R == 4) {
+    const f32x2 t0 = v[0] + v[2], t1 = v[0] - v[2], t2 = v[1] + v[3], t3 = mul_mi<INV>(v[1] - v[3]);
+    v[0] = t0 + t2; v[2] = t0 - t2; v[1] = t1 + t3; v[3] = t1 - t3;
+  } else {
+    constexpr float H = 0.70710678118654752f;
+    const f32x2 t0 = v[0] + v[4], t1 = v[0] - v[4], t2 = v[2] + v[6], t3 = mul_mi<INV>(v[2] - v[6]);
+    const f32x2 t4 = v[1] + v[5], t5 = v[1] - v[5], t6 = v[3] + v[7], t7 = mul_mi<INV>(v[3] - v[7]);
+    const f32x2 e0 = t0 + t2, e2 = t0 - t2, e1 = t1 + t3, e3 = t1 - t3;   // DFT4 of the even points
+    f32x2 o0 = t4 + t6, o2 = t4 - t6, o1 = t5 + t7, o3 = t5 - t7;         // DFT4 of the odd points
+    // o_k *= W8^k (forward W8 = (1 - i)/sqrt2; inverse conjugate)
+    o1 = INV ? f32x2{(o1.x - o1.y) * H, (o1.x + o1.y) * H} : f32x2{(o1.x + o1.y) * H, (o1.y - o1.x) * H};
+    o2 = mul_mi<INV>(o2);
+    o3 = INV ? f32x2{-(o3.x + o3.y) * H, (o3.x - o3.y) * H} : f32x2{(o3.y - o3.x) * H, -(o3.x + o3.y) * H};
+    v[0] = e0 + o0; v[4] = e0 - o0;
+    v[1] = e1 + o1; v[5] = e1 - o1;
+    v[2] = e2 + o2; v[6] = e2 - o2;
+    v[3] = e3 + o3; v[7] = e3 - o3;
+  }
+}
+
+template <int R, bool INV>
+__device__ __forceinline__ void stockham_pass(const f32x2* x, f32x2* y, int N, int Ns, int cnt, const f32x2* twl,
+                                              int ld) {
+  const int nb = N / R;
+  const int tstep = N / (Ns * R);
+  for (int idx = threadIdx.x; idx < cnt * nb; idx += blockDim.x) {
+    const int sq = idx / nb, j = idx - sq * nb;
+    const int m = j & (Ns - 1);
+    const f32x2* xs = x + sq * ld;
+    f32x2 v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = xs[j + r * nb];
+    if (Ns > 1) {
+#pragma unroll
+      for (int r = 1; r < R; ++r) {
+        f32x2 w = twl[(m * r * tstep) & (N - 1)];
+        if (INV) w.y = -w.y;
+        v[r] = cmul(v[r], w);
+      }
     }
+    dft<R, INV>(v);
+    f32x2* ys = y + sq * ld + (j - m) * R + m;
+#pragma unroll
+    for (int r = 0; r < R; ++r) ys[r * Ns] = v[r];
+  }
+}
+
+// FFT of `cnt` sequences of length N = 2^lN stored ld apart in x (ping-pong through y); returns the buffer
+// holding the result. twl: W_N^t for t < N (LDS). Unnormalised inverse when INV.
+template <bool INV>
+__device__ f32x2* lds_fft(f32x2* x, f32x2* y, int N, int lN, int cnt, const f32x2* twl, int ld) {
+  int Ns = 1, left = lN;
+  while (left > 0) {
+    if (left >= 3 && left != 4) { stockham_pass<8, INV>(x, y, N, Ns, cnt, twl, ld); Ns *= 8; left -= 3; }
+    else if (left >= 2) { stockham_pass<4, INV>(x, y, N, Ns, cnt, twl, ld); Ns *= 4; left -= 2; }
+    else { stockham_pass<2, INV>(x, y, N, Ns, cnt, twl, ld); Ns *= 2; left -= 1; }
     __syncthreads();
     f32x2* t = x; x = y; y = t;
   }
-  if (lN & 1) {  // result is in y (the original x buffer was swapped an odd number of times): copy back
-    for (int idx = threadIdx.x; idx < cnt * N; idx += blockDim.x) y[idx] = x[idx];
-    __syncthreads();
-  }
+  return x;
+}
+
+// twl[t] = W_N^t = W_n^(t n / N), t < N, from the f64-built table
+__device__ __forceinline__ void load_twl(f32x2* twl, const f32x2* tw, int N, int n) {
+  for (int t = threadIdx.x; t < N; t += blockDim.x) twl[t] = tw[(long long)t * (n / N)];
 }
 
 __device__ __forceinline__ int pair_row(const FftArgs& a, int j, int p, int which) {
@@ -80,8 +131,11 @@ __device__ __forceinline__ int pair_row(const FftArgs& a, int j, int p, int whic
 // grid: (n2 / G, npairs_total or C); block 256. LDS: 2 * G * n1 complex.
 __global__ __launch_bounds__(256) void fft_col_fwd_kernel(FftArgs a) {
   extern __shared__ __attribute__((aligned(16))) f32x2 lds[];
+  const int ld = a.n1 + 1;   // padded column stride: the G columns' transposing accesses hit distinct banks
   f32x2* x = lds;
-  f32x2* y = lds + a.G * a.n1;
+  f32x2* y = lds + a.G * ld;
+  f32x2* twl = y + a.G * ld;
+  load_twl(twl, a.tw, a.n1, a.n);
   const int c0 = blockIdx.x * a.G;
   const int pid = blockIdx.y;           // pair id (j * P + p) or filter id when single
   int r0, r1;
@@ -100,40 +154,47 @@ __global__ __launch_bounds__(256) void fft_col_fwd_kernel(FftArgs a) {
       v.x = s[(long long)r0 * a.L + m];
       if (r1 >= 0) v.y = s[(long long)r1 * a.L + m];
     }
-    x[g * a.n1 + ai] = v;
+    x[g * ld + ai] = v;
   }
   __syncthreads();
-  lds_fft(x, y, a.n1, a.ln1, a.G, a.tw, a.n, false);
+  x = lds_fft<false>(x, y, a.n1, a.ln1, a.G, twl, ld);
   f32x2* S = (a.single ? a.SK : a.S) + (long long)pid * a.n;
   for (int idx = threadIdx.x; idx < a.G * a.n1; idx += blockDim.x) {
     const int g = idx % a.G, k1 = idx / a.G;
     const int c = c0 + g;
     const f32x2 w = a.tw[((long long)c * k1) & (a.n - 1)];
-    S[(long long)k1 * a.n2 + c] = cmul(x[g * a.n1 + k1], w);
+    S[(long long)k1 * a.n2 + c] = cmul(x[g * ld + k1], w);
   }
 }
 
 // ------------------------------------------------------------------------------------------ row pass
-// grid: (n1, C); block 256. One (filter j, row k1); loops over the filter's pairs.
-// LDS: x, y (n2 complex each) + kr (n2) + acc (n2).
+// grid: (n1, C); block 256. One (filter j, row k1); the filter's pairs go through in batches of PB sequences
+// (one radix-8 butterfly per thread per pass). LDS: 2 PB n2 (+ 2 PB n2 for the bwd's second operand)
+// + kr + acc + twl (n2 complex each).
+constexpr int ROW_PB = 4;
+
 __global__ __launch_bounds__(256) void fft_row_kernel(FftArgs a) {
   extern __shared__ __attribute__((aligned(16))) f32x2 lds[];
   const int N = a.n2;
-  f32x2* x = lds;
-  f32x2* y = x + N;
-  f32x2* kr = y + N;
+  const bool two = a.mode == 2 && a.SK;           // bwd with filter gradient: also FFT the vg rows
+  const int PB = two ? ROW_PB / 2 : ROW_PB;
+  f32x2* x = lds;                                 // PB * N
+  f32x2* y = x + PB * N;                          // PB * N
+  f32x2* x2 = y + PB * N;                         // PB * N (two)
+  f32x2* y2 = x2 + (two ? PB * N : 0);            // PB * N (two)
+  f32x2* kr = y2 + (two ? PB * N : 0);
   f32x2* acc = kr + N;
-  f32x2* x2 = acc + N;
-  f32x2* y2 = x2 + N;
+  f32x2* twl = acc + N;
   const int k1 = blockIdx.x, j = blockIdx.y;
   const float invn = 1.f / (float)a.n;
+  load_twl(twl, a.tw, N, a.n);
   if (a.mode == 0) {  // filter spectrum: K_j[k1][:] = FFT_n2(T[k1][:]) / n
     f32x2* S = a.SK + (long long)j * a.n + (long long)k1 * N;
     for (int i = threadIdx.x; i < N; i += blockDim.x) x[i] = S[i];
     __syncthreads();
-    lds_fft(x, y, N, a.ln2, 1, a.tw, a.n, false);
+    f32x2* r = lds_fft<false>(x, y, N, a.ln2, 1, twl, N);
     f32x2* K = a.K + (long long)j * a.n + (long long)k1 * N;
-    for (int i = threadIdx.x; i < N; i += blockDim.x) K[i] = x[i] * invn;
+    for (int i = threadIdx.x; i < N; i += blockDim.x) K[i] = r[i] * invn;
     return;
   }
   const f32x2* K = a.K + (long long)j * a.n + (long long)k1 * N;
@@ -141,32 +202,44 @@ __global__ __launch_bounds__(256) void fft_row_kernel(FftArgs a) {
     kr[i] = K[i];
     acc[i] = f32x2{0.f, 0.f};
   }
-  __syncthreads();
-  for (int p = 0; p < a.P; ++p) {
-    f32x2* S = a.S + ((long long)j * a.P + p) * a.n + (long long)k1 * N;
-    for (int i = threadIdx.x; i < N; i += blockDim.x) x[i] = S[i];
-    if (a.mode == 2 && a.SK) {
-      const f32x2* S2 = a.S2 + ((long long)j * a.P + p) * a.n + (long long)k1 * N;
-      for (int i = threadIdx.x; i < N; i += blockDim.x) x2[i] = S2[i];
+  for (int p0 = 0; p0 < a.P; p0 += PB) {
+    const int cnt = min(PB, a.P - p0);
+    for (int i = threadIdx.x; i < cnt * N; i += blockDim.x) {
+      const int q = i / N, e = i - q * N;
+      const long long off = ((long long)j * a.P + p0 + q) * a.n + (long long)k1 * N + e;
+      x[i] = a.S[off];
+      if (two) x2[i] = a.S2[off];
     }
     __syncthreads();
-    lds_fft(x, y, N, a.ln2, 1, a.tw, a.n, false);
-    if (a.mode == 2 && a.SK) {
-      lds_fft(x2, y2, N, a.ln2, 1, a.tw, a.n, false);
-      for (int i = threadIdx.x; i < N; i += blockDim.x) acc[i] += cmulc(x[i], x2[i]);  // X_dy conj(X_vg)
+    f32x2* fx = lds_fft<false>(x, y, N, a.ln2, cnt, twl, N);
+    f32x2* gx = fx == x ? y : x;
+    if (two) {
+      f32x2* fx2 = lds_fft<false>(x2, y2, N, a.ln2, cnt, twl, N);
+      for (int i = threadIdx.x; i < N; i += blockDim.x) {
+        f32x2 s = acc[i];
+        for (int q = 0; q < cnt; ++q) s += cmulc(fx[q * N + i], fx2[q * N + i]);   // X_dy conj(X_vg)
+        acc[i] = s;
+      }
+      __syncthreads();   // fx is overwritten in place below
     }
-    for (int i = threadIdx.x; i < N; i += blockDim.x) x[i] = (a.mode == 1) ? cmul(x[i], kr[i]) : cmulc(x[i], kr[i]);
+    for (int i = threadIdx.x; i < cnt * N; i += blockDim.x) {
+      const int e = i % N;
+      fx[i] = (a.mode == 1) ? cmul(fx[i], kr[e]) : cmulc(fx[i], kr[e]);
+    }
     __syncthreads();
-    lds_fft(x, y, N, a.ln2, 1, a.tw, a.n, true);
-    for (int i = threadIdx.x; i < N; i += blockDim.x) S[i] = x[i];
+    f32x2* rx = lds_fft<true>(fx, gx, N, a.ln2, cnt, twl, N);
+    for (int i = threadIdx.x; i < cnt * N; i += blockDim.x) {
+      const int q = i / N, e = i - q * N;
+      a.S[((long long)j * a.P + p0 + q) * a.n + (long long)k1 * N + e] = rx[i];
+    }
     __syncthreads();
   }
-  if (a.mode == 2 && a.SK) {  // dk spectrum row (unnormalised correlation): inverse row FFT, store
+  if (two) {  // dk spectrum row (unnormalised correlation): inverse row FFT, store
     for (int i = threadIdx.x; i < N; i += blockDim.x) x[i] = acc[i];
     __syncthreads();
-    lds_fft(x, y, N, a.ln2, 1, a.tw, a.n, true);
+    f32x2* r = lds_fft<true>(x, y, N, a.ln2, 1, twl, N);
     f32x2* SK = a.SK + (long long)j * a.n + (long long)k1 * N;
-    for (int i = threadIdx.x; i < N; i += blockDim.x) SK[i] = x[i] * invn;   // correlation needs 1/n
+    for (int i = threadIdx.x; i < N; i += blockDim.x) SK[i] = r[i] * invn;   // correlation needs 1/n
   }
 }
 
@@ -174,8 +247,11 @@ __global__ __launch_bounds__(256) void fft_row_kernel(FftArgs a) {
 // grid: (n2 / G, npairs_total or C); out rows (+ D * src); single: dk[j][m] = Re(...) for the filter.
 __global__ __launch_bounds__(256) void fft_col_inv_kernel(FftArgs a) {
   extern __shared__ __attribute__((aligned(16))) f32x2 lds[];
+  const int ld = a.n1 + 1;   // padded column stride: the G columns' transposing accesses hit distinct banks
   f32x2* x = lds;
-  f32x2* y = lds + a.G * a.n1;
+  f32x2* y = lds + a.G * ld;
+  f32x2* twl = y + a.G * ld;
+  load_twl(twl, a.tw, a.n1, a.n);
   const int c0 = blockIdx.x * a.G;
   const int pid = blockIdx.y;
   const f32x2* S = (a.single ? a.SK : a.S) + (long long)pid * a.n;
@@ -184,15 +260,15 @@ __global__ __launch_bounds__(256) void fft_col_inv_kernel(FftArgs a) {
     const int c = c0 + g;
     f32x2 w = a.tw[((long long)c * k1) & (a.n - 1)];
     w.y = -w.y;
-    x[g * a.n1 + k1] = cmul(S[(long long)k1 * a.n2 + c], w);
+    x[g * ld + k1] = cmul(S[(long long)k1 * a.n2 + c], w);
   }
   __syncthreads();
-  lds_fft(x, y, a.n1, a.ln1, a.G, a.tw, a.n, true);
+  x = lds_fft<true>(x, y, a.n1, a.ln1, a.G, twl, ld);
   if (a.single) {
     for (int idx = threadIdx.x; idx < a.G * a.n1; idx += blockDim.x) {
       const int g = idx % a.G, ai = idx / a.G;
       const int m = ai * a.n2 + c0 + g;
-      if (m < a.L) a.dk[(long long)pid * a.L + m] = x[g * a.n1 + ai].x;
+      if (m < a.L) a.dk[(long long)pid * a.L + m] = x[g * ld + ai].x;
     }
     return;
   }
@@ -203,7 +279,7 @@ __global__ __launch_bounds__(256) void fft_col_inv_kernel(FftArgs a) {
     const int g = idx % a.G, ai = idx / a.G;
     const int m = ai * a.n2 + c0 + g;
     if (m < a.L) {
-      const f32x2 v = x[g * a.n1 + ai];
+      const f32x2 v = x[g * ld + ai];
       a.dst[(long long)r0 * a.L + m] = fmaf(Dj, a.src[(long long)r0 * a.L + m], v.x);
       if (r1 >= 0) a.dst[(long long)r1 * a.L + m] = fmaf(Dj, a.src[(long long)r1 * a.L + m], v.y);
     }
@@ -418,7 +494,9 @@ extern "C" int lci_fft_twiddles(void* tw, int n, void* stream) {
 }
 
 static int launch_col(FftArgs& a, bool inv, int nblk_y, hipStream_t s) {
-  const size_t sh = (size_t)2 * a.G * a.n1 * sizeof(f32x2);
+  const size_t sh = ((size_t)2 * a.G * (a.n1 + 1) + a.n1) * sizeof(f32x2);
+  (void)hipFuncSetAttribute((const void*)(inv ? fft_col_inv_kernel : fft_col_fwd_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   dim3 grid(a.n2 / a.G, nblk_y);
   if (inv) hipLaunchKernelGGL(fft_col_inv_kernel, grid, dim3(256), sh, s, a);
   else hipLaunchKernelGGL(fft_col_fwd_kernel, grid, dim3(256), sh, s, a);
@@ -427,7 +505,8 @@ static int launch_col(FftArgs& a, bool inv, int nblk_y, hipStream_t s) {
 }
 
 static int launch_row(FftArgs& a, hipStream_t s) {
-  const size_t sh = (size_t)6 * a.n2 * sizeof(f32x2);
+  const size_t sh = ((size_t)2 * ROW_PB + 3) * a.n2 * sizeof(f32x2);   // x, y (+ x2, y2 at PB/2) + kr, acc, twl
+  (void)hipFuncSetAttribute((const void*)fft_row_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipLaunchKernelGGL(fft_row_kernel, dim3(a.n1, a.C), dim3(256), sh, s, a);
   LCI_LAUNCH_CHECK();
   return 0;
