@@ -18,6 +18,8 @@
 // transposing through LDS to the channel-major rows the FFT wants.
 #include "common.hpp"
 
+#include <cstdlib>
+
 namespace lci {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -122,6 +124,8 @@ __device__ __forceinline__ void load_twl(f32x2* twl, const f32x2* tw, int N, int
   for (int t = threadIdx.x; t < N; t += blockDim.x) twl[t] = tw[(long long)t * (n / N)];
 }
 
+constexpr int UB = 8;   // global loads in flight per thread in the staging loops
+
 __device__ __forceinline__ int pair_row(const FftArgs& a, int j, int p, int which) {
   const int ro = 2 * p + which;
   return ro < a.R ? ro * a.C + j : -1;
@@ -146,34 +150,54 @@ __global__ __launch_bounds__(256) void fft_col_fwd_kernel(FftArgs a) {
     r1 = pair_row(a, j, p, 1);
   }
   const float* s = a.src;
-  for (int idx = threadIdx.x; idx < a.G * a.n1; idx += blockDim.x) {
-    const int g = idx % a.G, ai = idx / a.G;
-    const int m = ai * a.n2 + c0 + g;
-    f32x2 v = {0.f, 0.f};
-    if (m < a.L) {
-      v.x = s[(long long)r0 * a.L + m];
-      if (r1 >= 0) v.y = s[(long long)r1 * a.L + m];
+  const int total = a.G * a.n1;
+  // UB items per thread in flight: all of a batch's global loads issue before any LDS store
+  for (int base = 0; base < total; base += UB * blockDim.x) {
+    f32x2 v[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int idx = base + u * blockDim.x + threadIdx.x;
+      const int g = idx % a.G, ai = idx / a.G;
+      const int m = ai * a.n2 + c0 + g;
+      v[u] = f32x2{0.f, 0.f};
+      if (idx < total && m < a.L) {
+        v[u].x = s[(long long)r0 * a.L + m];
+        if (r1 >= 0) v[u].y = s[(long long)r1 * a.L + m];
+      }
     }
-    x[g * ld + ai] = v;
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int idx = base + u * blockDim.x + threadIdx.x;
+      if (idx < total) x[(idx % a.G) * ld + idx / a.G] = v[u];
+    }
   }
   __syncthreads();
   x = lds_fft<false>(x, y, a.n1, a.ln1, a.G, twl, ld);
   f32x2* S = (a.single ? a.SK : a.S) + (long long)pid * a.n;
-  for (int idx = threadIdx.x; idx < a.G * a.n1; idx += blockDim.x) {
-    const int g = idx % a.G, k1 = idx / a.G;
-    const int c = c0 + g;
-    const f32x2 w = a.tw[((long long)c * k1) & (a.n - 1)];
-    S[(long long)k1 * a.n2 + c] = cmul(x[g * ld + k1], w);
+  for (int base = 0; base < total; base += UB * blockDim.x) {
+    f32x2 w[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int idx = base + u * blockDim.x + threadIdx.x;
+      const int g = idx % a.G, k1 = idx / a.G;
+      w[u] = idx < total ? a.tw[((long long)(c0 + g) * k1) & (a.n - 1)] : f32x2{0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int idx = base + u * blockDim.x + threadIdx.x;
+      const int g = idx % a.G, k1 = idx / a.G;
+      if (idx < total) S[(long long)k1 * a.n2 + c0 + g] = cmul(x[g * ld + k1], w[u]);
+    }
   }
 }
 
 // ------------------------------------------------------------------------------------------ row pass
-// grid: (n1, C); block 256. One (filter j, row k1); the filter's pairs go through in batches of PB sequences
+// grid: (n1, C); block 512. One (filter j, row k1); the filter's pairs go through in batches of PB sequences
 // (one radix-8 butterfly per thread per pass). LDS: 2 PB n2 (+ 2 PB n2 for the bwd's second operand)
 // + kr + acc + twl (n2 complex each).
 constexpr int ROW_PB = 4;
 
-__global__ __launch_bounds__(256) void fft_row_kernel(FftArgs a) {
+__global__ __launch_bounds__(512) void fft_row_kernel(FftArgs a) {
   extern __shared__ __attribute__((aligned(16))) f32x2 lds[];
   const int N = a.n2;
   const bool two = a.mode == 2 && a.SK;           // bwd with filter gradient: also FFT the vg rows
@@ -204,11 +228,26 @@ __global__ __launch_bounds__(256) void fft_row_kernel(FftArgs a) {
   }
   for (int p0 = 0; p0 < a.P; p0 += PB) {
     const int cnt = min(PB, a.P - p0);
-    for (int i = threadIdx.x; i < cnt * N; i += blockDim.x) {
-      const int q = i / N, e = i - q * N;
-      const long long off = ((long long)j * a.P + p0 + q) * a.n + (long long)k1 * N + e;
-      x[i] = a.S[off];
-      if (two) x2[i] = a.S2[off];
+    for (int base = 0; base < cnt * N; base += UB * blockDim.x) {
+      f32x2 v[UB], v2[UB];
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const int i = base + u * blockDim.x + threadIdx.x;
+        const int q = i / N, e = i - q * N;
+        const long long off = ((long long)j * a.P + p0 + q) * a.n + (long long)k1 * N + e;
+        if (i < cnt * N) {
+          v[u] = a.S[off];
+          if (two) v2[u] = a.S2[off];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const int i = base + u * blockDim.x + threadIdx.x;
+        if (i < cnt * N) {
+          x[i] = v[u];
+          if (two) x2[i] = v2[u];
+        }
+      }
     }
     __syncthreads();
     f32x2* fx = lds_fft<false>(x, y, N, a.ln2, cnt, twl, N);
@@ -255,12 +294,23 @@ __global__ __launch_bounds__(256) void fft_col_inv_kernel(FftArgs a) {
   const int c0 = blockIdx.x * a.G;
   const int pid = blockIdx.y;
   const f32x2* S = (a.single ? a.SK : a.S) + (long long)pid * a.n;
-  for (int idx = threadIdx.x; idx < a.G * a.n1; idx += blockDim.x) {
-    const int g = idx % a.G, k1 = idx / a.G;
-    const int c = c0 + g;
-    f32x2 w = a.tw[((long long)c * k1) & (a.n - 1)];
-    w.y = -w.y;
-    x[g * ld + k1] = cmul(S[(long long)k1 * a.n2 + c], w);
+  const int total = a.G * a.n1;
+  for (int base = 0; base < total; base += UB * blockDim.x) {
+    f32x2 v[UB], w[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int idx = base + u * blockDim.x + threadIdx.x;
+      const int g = idx % a.G, k1 = idx / a.G;
+      if (idx < total) {
+        w[u] = a.tw[((long long)(c0 + g) * k1) & (a.n - 1)];
+        v[u] = S[(long long)k1 * a.n2 + c0 + g];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int idx = base + u * blockDim.x + threadIdx.x;
+      if (idx < total) x[(idx % a.G) * ld + idx / a.G] = cmulc(v[u], w[u]);
+    }
   }
   __syncthreads();
   x = lds_fft<true>(x, y, a.n1, a.ln1, a.G, twl, ld);
@@ -275,13 +325,28 @@ __global__ __launch_bounds__(256) void fft_col_inv_kernel(FftArgs a) {
   const int j = pid / a.P, p = pid % a.P;
   const int r0 = pair_row(a, j, p, 0), r1 = pair_row(a, j, p, 1);
   const float Dj = a.Dv ? a.Dv[j] : 0.f;
-  for (int idx = threadIdx.x; idx < a.G * a.n1; idx += blockDim.x) {
-    const int g = idx % a.G, ai = idx / a.G;
-    const int m = ai * a.n2 + c0 + g;
-    if (m < a.L) {
-      const f32x2 v = x[g * ld + ai];
-      a.dst[(long long)r0 * a.L + m] = fmaf(Dj, a.src[(long long)r0 * a.L + m], v.x);
-      if (r1 >= 0) a.dst[(long long)r1 * a.L + m] = fmaf(Dj, a.src[(long long)r1 * a.L + m], v.y);
+  for (int base = 0; base < total; base += UB * blockDim.x) {
+    float s0[UB], s1[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int idx = base + u * blockDim.x + threadIdx.x;
+      const int m = (idx / a.G) * a.n2 + c0 + idx % a.G;
+      s0[u] = s1[u] = 0.f;
+      if (idx < total && m < a.L) {
+        s0[u] = a.src[(long long)r0 * a.L + m];
+        if (r1 >= 0) s1[u] = a.src[(long long)r1 * a.L + m];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int idx = base + u * blockDim.x + threadIdx.x;
+      const int g = idx % a.G, ai = idx / a.G;
+      const int m = ai * a.n2 + c0 + g;
+      if (idx < total && m < a.L) {
+        const f32x2 v = x[g * ld + ai];
+        a.dst[(long long)r0 * a.L + m] = fmaf(Dj, s0[u], v.x);
+        if (r1 >= 0) a.dst[(long long)r1 * a.L + m] = fmaf(Dj, s1[u], v.y);
+      }
     }
   }
 }
@@ -467,11 +532,16 @@ static int fft_plan(FftArgs& a, int L) {
   int e = 1;
   while ((1 << e) < 2 * L) ++e;
   a.n = 1 << e;
-  a.ln1 = e < 8 ? e : 8;
+  // n1 = 256-point column FFTs over G = 8 adjacent columns, n2 = n / 256 row FFTs (512 at L = 65536): the best
+  // of the (n1, G) sweep in tools/fft_sweep.sh (wider column groups cost more in LDS occupancy than they save)
+  // tuning knobs for A/B runs: LCI_FFT_LN1 (log2 n1), LCI_FFT_G (columns per column-pass workgroup)
+  static const int env_ln1 = getenv("LCI_FFT_LN1") ? atoi(getenv("LCI_FFT_LN1")) : 8;
+  static const int env_g = getenv("LCI_FFT_G") ? atoi(getenv("LCI_FFT_G")) : 8;
+  a.ln1 = e < env_ln1 ? e : env_ln1;
   a.ln2 = e - a.ln1;
   if (a.ln2 == 0) { a.ln1 = e - 1; a.ln2 = 1; }
   a.n1 = 1 << a.ln1; a.n2 = 1 << a.ln2;
-  a.G = a.n2 < 16 ? a.n2 : 16;
+  a.G = a.n2 < env_g ? a.n2 : env_g;
   a.L = L;
   return 0;
 }
@@ -507,7 +577,8 @@ static int launch_col(FftArgs& a, bool inv, int nblk_y, hipStream_t s) {
 static int launch_row(FftArgs& a, hipStream_t s) {
   const size_t sh = ((size_t)2 * ROW_PB + 3) * a.n2 * sizeof(f32x2);   // x, y (+ x2, y2 at PB/2) + kr, acc, twl
   (void)hipFuncSetAttribute((const void*)fft_row_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipLaunchKernelGGL(fft_row_kernel, dim3(a.n1, a.C), dim3(256), sh, s, a);
+  const int thr = a.n2 >= 1024 ? 512 : 256;
+  hipLaunchKernelGGL(fft_row_kernel, dim3(a.n1, a.C), dim3(thr), sh, s, a);
   LCI_LAUNCH_CHECK();
   return 0;
 }
