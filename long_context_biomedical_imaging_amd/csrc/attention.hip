@@ -24,6 +24,22 @@ constexpr int DH = 64;        // head dim (ViT-small/base: 384/6, 768/12)
 constexpr int KT = 64;        // keys (or queries) per LDS tile
 constexpr int LD_ROW = 72;    // LDS row stride (elements) for tiles read by rows: 144 B, b128 conflict-free
 constexpr int LD_TR = 96;     // LDS row stride for tiles read only transposed: 192 B, tr_b16 conflict-free
+// Tiles read BOTH by rows (ds_read_b128) and transposed (ds_read_b64_tr_b16): no plain stride is conflict-free
+// for both (144 B: 2-way on tr; 192 B: 4-way on b128). 192-B rows with the 16-B chunk index XORed by
+// (row >> 2) & 3 are conflict-free for both (exhaustive check over the lane groups of MI355X_MICROARCH.md).
+constexpr int LD_SW = 96;
+__device__ __forceinline__ int swz(int row, int col) {   // col: element index; 8-element chunks stay whole
+  return row * LD_SW + ((((col >> 3) ^ ((row >> 2) & 3)) << 3) | (col & 7));
+}
+__device__ __forceinline__ bf16x8 frag_row_sw(const bf16* tile, int r0, int c0, int lane) {
+  return *(const bf16x8*)(tile + swz(r0 + (lane & 31), c0 + 8 * (lane >> 5)));
+}
+template <int S>
+__device__ __forceinline__ bf16x8 frag_tr_sw(const bf16* tile, int r0, int c0, int lane) {
+  const int row = r0 + 16 * S + 4 * (lane >> 5) + ((lane & 15) >> 2);
+  const int col = c0 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+  return cat44(lds_tr4(tile + swz(row, col)), lds_tr4(tile + swz(row + 8, col)));
+}
 constexpr float NEG_BIG = -1.0e30f;
 
 #ifdef LCI_IGLP   // scheduling-strategy experiments (tools/attn_variants.sh)
@@ -62,6 +78,14 @@ struct TileRegs {
       const int g = row0 + row;
       if (!GUARD || g < L) r[p] = *(const u32x4*)(base + (long long)g * rs + ch * 8);
       else r[p] = u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+  __device__ __forceinline__ void store_sw(bf16* lds, int tid) const {   // swizzled LD_SW layout
+#pragma unroll
+    for (int p = 0; p < PASSES; ++p) {
+      const int idx = p * NT + tid;
+      const int row = idx >> 3, ch = idx & 7;
+      *(u32x4*)(lds + swz(row, ch * 8)) = r[p];
     }
   }
   __device__ __forceinline__ void store(bf16* lds, int ld, int tid) const {
@@ -118,6 +142,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
   // bound, not the matrix pipe). m starts at 0; the first tile always re-bases.
   f32x16 o0 = {}, o1 = {}, negm = {};
   float m_run = 0.f, l_run = 0.f;
+
 
   // Full tiles run without any key-bound code; only the ragged last tile masks (compile-time flag,
   // otherwise the compiler if-converts the mask into 64 selects per tile).
@@ -187,6 +212,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
     }
     l_run += (lq[0] + lq[1]) + (lq[2] + lq[3]);
     const bf16x8 p00 = pack8<0>(s0), p01 = pack8<1>(s0), p10 = pack8<0>(s1), p11 = pack8<1>(s1);
+
     // O^T[d][q] += V^T[d][key] P^T[key][q]
     o0 = mfma32(frag_tr<0>(vl, LD_TR, 0, 0, lane), p00, o0);
     o0 = mfma32(frag_tr<1>(vl, LD_TR, 0, 0, lane), p01, o0);
@@ -248,7 +274,7 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnArgs a) {
 template <int NW>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv_kernel(AttnArgs a) {
   constexpr int NT = NW * 64;
-  constexpr int TILE = 2 * KT * LD_ROW;                 // Q tile + dO tile (both read by rows and transposed)
+  constexpr int TILE = 2 * KT * LD_SW;                  // Q tile + dO tile (both read by rows and transposed)
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * TILE];
   __shared__ __attribute__((aligned(16))) float rowc[2][2][KT];  // [buf][lse2 | delta][query]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -294,8 +320,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv_kernel(AttnArgs
   };
   qr.load(qp, a.rs_q, 0, L, tid);
   dr.load(dop, a.rs_do, 0, L, tid);
-  qr.store(smem, LD_ROW, tid);
-  dr.store(smem + KT * LD_ROW, LD_ROW, tid);
+  qr.store_sw(smem, tid);
+  dr.store_sw(smem + KT * LD_SW, tid);
   stage_rowc(0, 0);
   __syncthreads();
 
@@ -304,7 +330,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv_kernel(AttnArgs
   for (int qt = 0; qt < nqt; ++qt) {
     const int buf = qt & 1;
     const bf16* ql = smem + buf * TILE;
-    const bf16* dl = ql + KT * LD_ROW;
+    const bf16* dl = ql + KT * LD_SW;
     if (qt + 1 < nqt) {
       qr.load(qp, a.rs_q, (qt + 1) * KT, L, tid);
       dr.load(dop, a.rs_do, (qt + 1) * KT, L, tid);
@@ -328,8 +354,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv_kernel(AttnArgs
       }
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        s = mfma32(frag_row(ql, LD_ROW, qs * 32, ks * 16, lane), kf[ks], s);
-        p = mfma32(frag_row(dl, LD_ROW, qs * 32, ks * 16, lane), vf[ks], p);
+        s = mfma32(frag_row_sw(ql, qs * 32, ks * 16, lane), kf[ks], s);
+        p = mfma32(frag_row_sw(dl, qs * 32, ks * 16, lane), vf[ks], p);
       }
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -338,19 +364,19 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv_kernel(AttnArgs
       }
       const bf16x8 P0 = pack8<0>(s), P1 = pack8<1>(s), D0 = pack8<0>(p), D1 = pack8<1>(p);
       // dV^T[d][key] += dO^T[d][q] P[q][key] ; dK^T[d][key] += Q^T[d][q] dS[q][key]
-      dv0 = mfma32(frag_tr<0>(dl, LD_ROW, qs * 32, 0, lane), P0, dv0);
-      dv0 = mfma32(frag_tr<1>(dl, LD_ROW, qs * 32, 0, lane), P1, dv0);
-      dv1 = mfma32(frag_tr<0>(dl, LD_ROW, qs * 32, 32, lane), P0, dv1);
-      dv1 = mfma32(frag_tr<1>(dl, LD_ROW, qs * 32, 32, lane), P1, dv1);
-      dk0 = mfma32(frag_tr<0>(ql, LD_ROW, qs * 32, 0, lane), D0, dk0);
-      dk0 = mfma32(frag_tr<1>(ql, LD_ROW, qs * 32, 0, lane), D1, dk0);
-      dk1 = mfma32(frag_tr<0>(ql, LD_ROW, qs * 32, 32, lane), D0, dk1);
-      dk1 = mfma32(frag_tr<1>(ql, LD_ROW, qs * 32, 32, lane), D1, dk1);
+      dv0 = mfma32(frag_tr_sw<0>(dl, qs * 32, 0, lane), P0, dv0);
+      dv0 = mfma32(frag_tr_sw<1>(dl, qs * 32, 0, lane), P1, dv0);
+      dv1 = mfma32(frag_tr_sw<0>(dl, qs * 32, 32, lane), P0, dv1);
+      dv1 = mfma32(frag_tr_sw<1>(dl, qs * 32, 32, lane), P1, dv1);
+      dk0 = mfma32(frag_tr_sw<0>(ql, qs * 32, 0, lane), D0, dk0);
+      dk0 = mfma32(frag_tr_sw<1>(ql, qs * 32, 0, lane), D1, dk0);
+      dk1 = mfma32(frag_tr_sw<0>(ql, qs * 32, 32, lane), D0, dk1);
+      dk1 = mfma32(frag_tr_sw<1>(ql, qs * 32, 32, lane), D1, dk1);
     }
     if (qt + 1 < nqt) {
       bf16* nb = smem + (buf ^ 1) * TILE;
-      qr.store(nb, LD_ROW, tid);
-      dr.store(nb + KT * LD_ROW, LD_ROW, tid);
+      qr.store_sw(nb, tid);
+      dr.store_sw(nb + KT * LD_SW, tid);
       stage_rowc(buf ^ 1, qt + 1);
     }
     __syncthreads();
