@@ -85,6 +85,20 @@ def cpu_baseline(budget_s: float = 20.0):
                       f"both extrapolated linearly to the full layer, x12 layers"}
 
 
+def profiled_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed PMC profile of this bench (profiles/traffic.json, written
+    by tools/summarize_prof.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes), or None."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        prof = json.load(f)
+    for name, d in prof.get("kernels", {}).items():
+        if kernel + "_kernel" in name or name.endswith(kernel):
+            return int(d["read_bytes"] + d["write_bytes"])
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -152,7 +166,8 @@ def main():
                        "global_batch": world * args.batch, "seq_len": L, "parallelism": f"ddp{world}",
                        "per_gpu_batch": args.batch, "optimizer": cfg.optim_type, "loss": cfg.loss_func},
             "roofline": {"kernel": dom, "bound": "mfma", "achieved": round(ach, 1), "peak": MFMA_BF16_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(ach / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
+                         "unit": "TFLOP/s", "frac": round(ach / MFMA_BF16_PEAK_TFLOPS, 4),
+                         "traffic": profiled_traffic(dom), "traffic_source": "profiles/traffic.json",
                          "work_per_launch": dd["work_per_call"], "avg_launch_ms": round(dd["avg_ms"], 3)},
             "kernels": kern,
             "loss": round(loss_v, 5),

@@ -7,6 +7,7 @@ FETCH_SIZE reports half the bytes of a wide (16 B/lane) coalesced streaming read
 Only dispatches after the first `skip_frac` of the run are counted (warm-up includes MIOpen's find phase).
 
     python tools/summarize_prof.py gpurun_out/prof_r01 > profiles/r01_rocprof_summary.md
+    python tools/summarize_prof.py gpurun_out/prof_r01 0.5 profiles/traffic.json   # + per-kernel HBM bytes
 """
 import csv
 import os
@@ -49,6 +50,17 @@ def main():
             if n:
                 acc[n].append(float(r["Counter_Value"]))
         counters[c] = acc
+    if len(sys.argv) > 3:   # per-kernel HBM bytes per launch as JSON (bench.py's roofline.traffic)
+        import json
+        out = {}
+        for n in dur:
+            f = counters.get("fetch", {}).get(n)
+            w = counters.get("write", {}).get(n)
+            if f and w:
+                out[n] = {"read_bytes": 2.0 * sum(f) / len(f) * 1024, "write_bytes": sum(w) / len(w) * 1024,
+                          "avg_ms": sum(dur[n]) / len(dur[n])}
+        json.dump({"source": d, "note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB -> bytes, per launch",
+                   "kernels": out}, open(sys.argv[3], "w"), indent=1)
     print(f"# rocprofv3 summary: {d}\n")
     print(f"Kernel-trace dispatches counted: the last {100 * (1 - skip_frac):.0f}% of the run "
           f"({len(tr) - start} of {len(tr)} dispatches).\n")
