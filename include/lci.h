@@ -36,9 +36,12 @@ int lci_abi_version(void);
  *       (backbone_vit.py:168 Rearrange "b h (qkv l d) -> qkv b l h d").
  * out : (B, L, H*64) bf16 = softmax(q k^T * scale) v in "b l (h d)" order (backbone_vit.py:169).
  * lse2: (B, H, L) f32 = log2 sum_y exp(scale q.k_y) per query row (consumed by the backward).
+ * knorm_ws: lci_attn_fwd_ws_bytes(B, L, H) bytes of device memory (per-64-key-tile bounds max ||k||,
+ *       written and read by this call; they let the forward skip the row max on provably safe tiles).
  * head_dim must be 64; pointers 16-byte aligned. */
-int lci_attn_fwd(const void* qkv, void* out, float* lse2, int B, int L, int H, int head_dim, float scale,
-                 void* stream);
+int lci_attn_fwd(const void* qkv, void* out, float* lse2, float* knorm_ws, int B, int L, int H, int head_dim,
+                 float scale, void* stream);
+long long lci_attn_fwd_ws_bytes(int B, int L, int H);
 /* dqkv (B, L, 3*H*64) bf16 <- dQ, dK, dV in the packed layout; dout (B, L, H*64) bf16;
  * delta_ws (B, H, L) f32 workspace. No atomics: bitwise reproducible. */
 int lci_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse2, void* dqkv,

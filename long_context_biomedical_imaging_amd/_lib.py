@@ -21,7 +21,7 @@ _L = ctypes.c_longlong
 
 # name -> argtypes (all return int status)
 SIGNATURES = {
-    "lci_attn_fwd": [_P, _P, _P, _I, _I, _I, _I, _F, _P],
+    "lci_attn_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _F, _P],
     "lci_attn_bwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P],
     "lci_attn_bwd_stage": [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P],
     "lci_patch_embed_fwd": [_P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P],
@@ -66,6 +66,8 @@ def load(path: str = LIB_PATH):
     lib.lci_window_dS_elems.argtypes = [_P]
     lib.lci_window_bias_elems.restype = ctypes.c_longlong
     lib.lci_window_bias_elems.argtypes = [_P, _I]
+    lib.lci_attn_fwd_ws_bytes.restype = ctypes.c_longlong
+    lib.lci_attn_fwd_ws_bytes.argtypes = [_I, _I, _I]
     lib.lci_fft_size.restype = ctypes.c_longlong
     lib.lci_fft_size.argtypes = [_I]
     for name, argt in SIGNATURES.items():

@@ -13,4 +13,4 @@ void set_error(const char* fmt, ...) {
 }  // namespace lci
 
 extern "C" const char* lci_last_error(void) { return lci::g_err; }
-extern "C" int lci_abi_version(void) { return 1; }
+extern "C" int lci_abi_version(void) { return 2; }

@@ -251,6 +251,286 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------ forward, v2
+// Per-64-key-tile bound on |k|: knorm[b][h][t] = max_{key in tile t} ||k_key||_2 (f32 of the bf16 keys).
+// One wave per tile, lane = key. Used by the forward's max-free fast path (below).
+__global__ __launch_bounds__(256) void attn_key_norm_kernel(AttnArgs a, float* knorm, int nkt) {
+  const int lane = threadIdx.x & 63, t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int hh = blockIdx.y, b = blockIdx.z;
+  if (t >= nkt) return;
+  const int key = t * KT + lane;
+  float ss = 0.f;
+  if (key < a.L) {
+    const bf16* kp = a.k + b * a.bs_k + (long long)key * a.rs_k + hh * a.hs;
+#pragma unroll
+    for (int c = 0; c < DH / 8; ++c) {
+      const bf16x8 v = *(const bf16x8*)(kp + 8 * c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += to_f32(v[j]) * to_f32(v[j]);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) ss = fmaxf(ss, __shfl_xor(ss, off));
+  if (lane == 0) knorm[((long long)b * a.H + hh) * nkt + t] = sqrtf(ss);
+}
+
+// Forward v2: one workgroup = 8 waves x 32 query rows (256 queries share every staged K/V tile: half the LDS
+// write traffic per MFMA of a 4-wave group), 2 waves per SIMD.
+//  * K/V tiles arrive by buffer loads (scalar tile offset, no per-tile address VALU; rows >= L read as zero)
+//    two tiles ahead into alternating register sets, and are written into a 3-slot LDS ring one tile ahead:
+//    one barrier per tile.
+//  * Software pipeline per wave: while the exp2/pack/row-sum of tile j runs on the VALU, the MFMAs of tile j+1's
+//    scores S_{j+1} = K_{j+1} Q~^T are in flight; then O^T += V_j^T P_j^T.
+//  * Max-free softmax: p = exp2(s~ - m) against a reference m that is only moved when it must be. A tile is
+//    "safe" when every row's bound ||q~|| * max||k|| - m <= 64 (q~ = c q, bf16; knorm per tile from
+//    attn_key_norm_kernel): then p <= 2^64, which f32 sums and bf16 P carry exactly as well as p <= 1, and
+//    the tile needs no row max at all. Unsafe tiles (and the first) take the exact path: row max, lazy
+//    re-base of m (alpha = exp2(-d) on O and l). The result is the same softmax; only the reference point
+//    of the exponent differs.
+#ifndef LCI_SB
+#define LCI_SB() __builtin_amdgcn_sched_barrier(0)
+#endif
+constexpr int FW_NW = 8;
+constexpr int FSLOT = KT * LD_ROW + KT * LD_TR;   // one ring slot: K tile (rows) + V tile (transposed reads)
+constexpr float SAFE_EXP2 = 64.f;
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ u32x4 bload16(rsrc_t r, int voff, int soff) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+}
+
+__global__ __launch_bounds__(FW_NW * 64, 1) void attn_fwd2_kernel(AttnArgs a, const float* knorm) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[3 * FSLOT];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hh = blockIdx.y, b = blockIdx.z;
+  const int L = a.L;
+  const int qrow = blockIdx.x * (FW_NW * 32) + wave * 32 + (lane & 31);
+  const int half = lane >> 5;
+  const int nkt = (L + KT - 1) / KT, nfull = L / KT;
+
+  // staging: thread -> (row, 16-B chunk) of a 64 x 128 B tile; one K and one V chunk per thread per tile
+  const int srow = tid >> 3, sch = tid & 7;
+  const int rs2 = a.rs_k * 2;
+  const uint32_t nbytes = (uint32_t)(L - 1) * (uint32_t)rs2 + DH * 2;
+  const rsrc_t rk = make_rsrc(a.k + b * a.bs_k + hh * a.hs, nbytes);
+  const rsrc_t rv = make_rsrc(a.v + b * a.bs_v + hh * a.hs, nbytes);
+  const int voff = srow * rs2 + sch * 16;
+  const int st_k = srow * LD_ROW + sch * 8, st_v = KT * LD_ROW + srow * LD_TR + sch * 8;
+  const float* kn = knorm + ((long long)b * a.H + hh) * nkt;
+
+  const float c = a.c;
+  bf16x8 qf[4];
+  float qss = 0.f;
+  {
+    const bf16* qp = a.q + b * a.bs_q + hh * a.hs;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      bf16x8 t{};
+      if (qrow < L) t = *(const bf16x8*)(qp + (long long)qrow * a.rs_q + ks * 16 + 8 * half);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        t[j] = to_bf16(to_f32(t[j]) * c);
+        qss += to_f32(t[j]) * to_f32(t[j]);
+      }
+      qf[ks] = t;
+    }
+  }
+  const float qn = sqrtf(wave_sum_xor32(qss));   // ||q~|| of this lane's row
+
+  // per-lane LDS fragment bases; a ring slot adds a wave-uniform element offset, fragments add immediates
+  const bf16* kfrag = smem + (lane & 31) * LD_ROW + 8 * half;
+  const bf16* vfrag = smem + KT * LD_ROW + (4 * half + ((lane & 15) >> 2)) * LD_TR + 16 * ((lane >> 4) & 1) +
+                      4 * (lane & 3);
+  auto kf = [&](int slot, int r0, int c0) { return *(const bf16x8*)(kfrag + slot + r0 * LD_ROW + c0); };
+  auto vf = [&](int slot, int r0, int s, int c0) {
+    const bf16* p = vfrag + slot + (r0 + 16 * s) * LD_TR + c0;
+    return cat44(lds_tr4(p), lds_tr4(p + 8 * LD_TR));
+  };
+
+  // prologue: tiles 0 and 1 into ring slots 0 and 1
+  {
+    const u32x4 k0 = bload16(rk, voff, 0), v0 = bload16(rv, voff, 0);
+    const u32x4 k1 = bload16(rk, voff, KT * rs2), v1 = bload16(rv, voff, KT * rs2);
+    *(u32x4*)(smem + st_k) = k0;
+    *(u32x4*)(smem + st_v) = v0;
+    *(u32x4*)(smem + FSLOT + st_k) = k1;   // beyond L: zeros, never read
+    *(u32x4*)(smem + FSLOT + st_v) = v1;
+  }
+  __syncthreads();
+
+  f32x16 o0 = {}, o1 = {}, negm = {};
+  float m_run = 0.f, l_run = 0.f;
+
+  auto mask_ragged = [&](int kt, f32x16& t0, f32x16& t1) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int key = kt * KT + (i & 3) + 8 * (i >> 2) + 4 * half;
+      if (key >= L) t0[i] = NEG_BIG;
+      if (key + 32 >= L) t1[i] = NEG_BIG;
+    }
+  };
+  // exact path: row max of the tile (relative to m), lazy re-base when it grew (always on the first tile)
+  auto exact = [&](f32x16& t0, f32x16& t1, bool first) {
+    float mq[4] = {fmaxf(t0[0], t0[1]), fmaxf(t0[2], t0[3]), fmaxf(t1[0], t1[1]), fmaxf(t1[2], t1[3])};
+#pragma unroll
+    for (int i = 4; i < 16; i += 4) {
+      mq[0] = fmaxf(mq[0], fmaxf(t0[i], t0[i + 1]));
+      mq[1] = fmaxf(mq[1], fmaxf(t0[i + 2], t0[i + 3]));
+      mq[2] = fmaxf(mq[2], fmaxf(t1[i], t1[i + 1]));
+      mq[3] = fmaxf(mq[3], fmaxf(t1[i + 2], t1[i + 3]));
+    }
+    const float mx = wave_max_xor32(fmaxf(fmaxf(mq[0], mq[1]), fmaxf(mq[2], mq[3])));
+    if (first || __any(mx > 0.f)) {
+      const float d = first ? mx : fmaxf(mx, 0.f);
+      m_run += d;
+      if (!first) {
+        const float alpha = exp2_fast(-d);
+        l_run *= alpha;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { o0[i] *= alpha; o1[i] *= alpha; }
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { t0[i] -= d; t1[i] -= d; negm[i] = -m_run; }
+    }
+  };
+
+  // S_0
+  f32x16 x0, x1;
+  x0 = mfma32(kf(0, 0, 0), qf[0], negm);
+  x1 = mfma32(kf(0, 32, 0), qf[0], negm);
+#pragma unroll
+  for (int ks = 1; ks < 4; ++ks) {
+    x0 = mfma32(kf(0, 0, ks * 16), qf[ks], x0);
+    x1 = mfma32(kf(0, 32, ks * 16), qf[ks], x1);
+  }
+  if (nfull == 0) mask_ragged(0, x0, x1);
+  exact(x0, x1, true);
+
+  // Ring slots (element offsets) of tiles j, j+1, j+2; rotated every tile.
+  int slA = 0, slB = FSLOT, slC = 2 * FSLOT;
+  // One tile j. Entry: S_j in (x0, x1). Exit (NEXT): S_{j+1} in (x0, x1) - the score MFMAs of the next tile
+  // write the registers of this tile's scores once these have been exponentiated, packed and summed.
+  auto iter = [&](const int j, auto next) -> bool {
+    constexpr bool NEXT = decltype(next)::value;
+    // tile j+2 -> registers now, -> LDS slot C at the end (beyond the last tile the range check gives zeros)
+    const u32x4 kw = bload16(rk, voff, (j + 2) * KT * rs2);
+    const u32x4 vw = bload16(rv, voff, (j + 2) * KT * rs2);
+    const float knext = NEXT ? kn[j + 1] : 0.f;
+    float lq[4];
+    bf16x8 vq[8], kq[8];
+    // (1) exp2 of keys 0-31 half 0, pack p00; V fragments for the first PV MFMAs
+    vq[0] = vf(slA, 0, 0, 0);
+    vq[1] = vf(slA, 0, 0, 32);
+    vq[2] = vf(slA, 0, 1, 0);
+    vq[3] = vf(slA, 0, 1, 32);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x0[i] = exp2_fast(x0[i]);
+    const bf16x8 p00 = pack8<0>(x0);
+    lq[0] = (x0[0] + x0[1]) + (x0[2] + x0[3]);
+    lq[1] = (x0[4] + x0[5]) + (x0[6] + x0[7]);
+    LCI_SB();
+    // (2) PV with p00, exp2 of x0[8..15]
+    o0 = mfma32(vq[0], p00, o0);
+    o1 = mfma32(vq[1], p00, o1);
+    vq[4] = vf(slA, 32, 0, 0);
+    vq[5] = vf(slA, 32, 0, 32);
+#pragma unroll
+    for (int i = 8; i < 16; ++i) x0[i] = exp2_fast(x0[i]);
+    const bf16x8 p01 = pack8<1>(x0);
+    lq[0] += (x0[8] + x0[9]) + (x0[10] + x0[11]);
+    lq[1] += (x0[12] + x0[13]) + (x0[14] + x0[15]);
+    if constexpr (NEXT) {
+      kq[0] = kf(slB, 0, 0);
+      kq[1] = kf(slB, 0, 16);
+    }
+    LCI_SB();
+    // (3) PV with p01, exp2 of x1[0..7]
+    o0 = mfma32(vq[2], p01, o0);
+    o1 = mfma32(vq[3], p01, o1);
+    vq[6] = vf(slA, 32, 1, 0);
+    vq[7] = vf(slA, 32, 1, 32);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x1[i] = exp2_fast(x1[i]);
+    const bf16x8 p10 = pack8<0>(x1);
+    lq[2] = (x1[0] + x1[1]) + (x1[2] + x1[3]);
+    lq[3] = (x1[4] + x1[5]) + (x1[6] + x1[7]);
+    if constexpr (NEXT) {
+      kq[2] = kf(slB, 0, 32);
+      kq[3] = kf(slB, 0, 48);
+    }
+    LCI_SB();
+    // (4) scores S_{j+1} keys 0..31 into x0, exp2 of x1[8..15]
+    if constexpr (NEXT) {
+      x0 = mfma32(kq[0], qf[0], negm);
+      x0 = mfma32(kq[1], qf[1], x0);
+      kq[4] = kf(slB, 32, 0);
+      kq[5] = kf(slB, 32, 16);
+    }
+#pragma unroll
+    for (int i = 8; i < 16; ++i) x1[i] = exp2_fast(x1[i]);
+    const bf16x8 p11 = pack8<1>(x1);
+    lq[2] += (x1[8] + x1[9]) + (x1[10] + x1[11]);
+    lq[3] += (x1[12] + x1[13]) + (x1[14] + x1[15]);
+    l_run += (lq[0] + lq[1]) + (lq[2] + lq[3]);
+    LCI_SB();
+    // (5) rest of the PV MFMAs and of the scores
+    if constexpr (NEXT) {
+      x0 = mfma32(kq[2], qf[2], x0);
+      kq[6] = kf(slB, 32, 32);
+      kq[7] = kf(slB, 32, 48);
+    }
+    o0 = mfma32(vq[4], p10, o0);
+    o1 = mfma32(vq[5], p10, o1);
+    if constexpr (NEXT) x0 = mfma32(kq[3], qf[3], x0);
+    o0 = mfma32(vq[6], p11, o0);
+    o1 = mfma32(vq[7], p11, o1);
+    if constexpr (NEXT) {
+      x1 = mfma32(kq[4], qf[0], negm);
+      x1 = mfma32(kq[5], qf[1], x1);
+      x1 = mfma32(kq[6], qf[2], x1);
+      x1 = mfma32(kq[7], qf[3], x1);
+    }
+    *(u32x4*)(smem + slC + st_k) = kw;
+    *(u32x4*)(smem + slC + st_v) = vw;
+    __syncthreads();
+    const int t = slA; slA = slB; slB = slC; slC = t;
+    if constexpr (NEXT) return (j + 1 == nfull) | !__all(qn * knext - m_run <= SAFE_EXP2);
+    return false;
+  };
+  using T = std::true_type;
+  using F = std::false_type;
+  // a ragged or unsafe next tile takes the exact path (in place)
+  int j = 0;
+  for (; j + 1 < nkt; ++j) {
+    if (iter(j, T{})) [[unlikely]] {
+      if (j + 1 == nfull) mask_ragged(j + 1, x0, x1);
+      exact(x0, x1, false);
+    }
+  }
+  iter(j, F{});
+
+  const float l_tot = wave_sum_xor32(l_run);
+  const float inv = 1.f / l_tot;
+  if (qrow < L) {
+    bf16* op = a.out + b * a.bs_out + (long long)qrow * a.rs_out + hh * a.hs;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf16x4 w0, w1;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        w0[j] = to_bf16(o0[4 * g + j] * inv);
+        w1[j] = to_bf16(o1[4 * g + j] * inv);
+      }
+      *(bf16x4*)(op + 8 * g + 4 * half) = w0;
+      *(bf16x4*)(op + 32 + 8 * g + 4 * half) = w1;
+    }
+    if (half == 0) a.lse2[((long long)b * a.H + hh) * L + qrow] = m_run + __log2f(l_tot);
+  }
+}
+
 // --------------------------------------------------------------------------- backward: delta
 // delta[b,h,q] = sum_d dO[b,q,h,d] * O[b,q,h,d]; 8 threads per (q, h) row, 16 B each.
 __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnArgs a) {
@@ -532,12 +812,17 @@ static int check_packed(const void* p, int rs) {
   return ((uintptr_t)p % 16 == 0) && (rs % 8 == 0);
 }
 
-extern "C" int lci_attn_fwd(const void* qkv, void* out, float* lse2, int B, int L, int H, int head_dim,
-                            float scale, void* stream) {
+extern "C" long long lci_attn_fwd_ws_bytes(int B, int L, int H) {
+  return (long long)B * H * ((L + KT - 1) / KT) * sizeof(float);
+}
+
+extern "C" int lci_attn_fwd(const void* qkv, void* out, float* lse2, float* knorm_ws, int B, int L, int H,
+                            int head_dim, float scale, void* stream) {
   LCI_CHECK(head_dim == DH, "lci_attn_fwd: head_dim %d unsupported (only 64)", head_dim);
   LCI_CHECK(B > 0 && L > 0 && H > 0, "lci_attn_fwd: bad shape B=%d L=%d H=%d", B, L, H);
   const int rs = 3 * H * DH;
   LCI_CHECK(check_packed(qkv, rs) && check_packed(out, H * DH), "lci_attn_fwd: misaligned pointers");
+  LCI_CHECK((long long)(L + 4 * KT) * rs * 2 < (1ll << 31), "lci_attn_fwd: L=%d too long for 32-bit buffer offsets", L);
   AttnArgs a{};
   const bf16* base = (const bf16*)qkv;
   a.q = base; a.k = base + H * DH; a.v = base + 2 * H * DH;
@@ -547,9 +832,20 @@ extern "C" int lci_attn_fwd(const void* qkv, void* out, float* lse2, int B, int 
   a.bs_out = (long long)L * H * DH; a.rs_out = H * DH;
   a.hs = DH; a.H = H; a.L = L;
   a.scale = scale; a.c = scale * 1.4426950408889634f;
+  hipStream_t s = (hipStream_t)stream;
+#ifdef LCI_FWD_V1
+  (void)knorm_ws;
   constexpr int NW = 4;
   dim3 grid((L + NW * 32 - 1) / (NW * 32), H, B);
-  hipLaunchKernelGGL(attn_fwd_kernel<NW>, grid, dim3(NW * 64), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(attn_fwd_kernel<NW>, grid, dim3(NW * 64), 0, s, a);
+#else
+  LCI_CHECK(knorm_ws != nullptr, "lci_attn_fwd: knorm_ws (lci_attn_fwd_ws_bytes) is required");
+  const int nkt = (L + KT - 1) / KT;
+  hipLaunchKernelGGL(attn_key_norm_kernel, dim3((nkt + 3) / 4, H, B), dim3(256), 0, s, a, knorm_ws, nkt);
+  LCI_LAUNCH_CHECK();
+  dim3 grid((L + FW_NW * 32 - 1) / (FW_NW * 32), H, B);
+  hipLaunchKernelGGL(attn_fwd2_kernel, grid, dim3(FW_NW * 64), 0, s, a, (const float*)knorm_ws);
+#endif
   LCI_LAUNCH_CHECK();
   return 0;
 }

@@ -54,9 +54,11 @@ def attn_fwd(qkv: torch.Tensor, num_heads: int, scale: float):
         raise _lib.LciError("attn_fwd expects bf16 qkv")
     out = torch.empty(B, L, num_heads * dh, device=qkv.device, dtype=torch.bfloat16)
     lse2 = torch.empty(B, num_heads, L, device=qkv.device, dtype=torch.float32)
+    ws = torch.empty(_lib.load().lci_attn_fwd_ws_bytes(B, L, num_heads) // 4, device=qkv.device,
+                     dtype=torch.float32)
     KernelTimer.run("attn_fwd", 4.0 * B * num_heads * L * L * dh, qkv, lambda: _lib.call(
-        "lci_attn_fwd", qkv.data_ptr(), out.data_ptr(), lse2.data_ptr(), B, L, num_heads, dh, float(scale),
-        _lib.stream_of(qkv)))
+        "lci_attn_fwd", qkv.data_ptr(), out.data_ptr(), lse2.data_ptr(), ws.data_ptr(), B, L, num_heads, dh,
+        float(scale), _lib.stream_of(qkv)))
     return out, lse2
 
 

@@ -112,3 +112,37 @@ def test_attention_long_rows_subset():
     o, _ = oatt.attention_core(q[:, :, rows], k, v, 64 ** -0.5)
     ref = o.permute(0, 2, 1, 3).reshape(B, len(rows), -1)
     _check(out.cpu()[:, rows], ref, "O rows L16384")
+
+
+@pytest.mark.parametrize("L", [63, 64, 65, 127, 128, 129, 255, 256, 257, 320, 513])
+def test_attention_forward_tile_edges(L):
+    """Ragged key tiles and partial 256-query workgroups around every tile/workgroup boundary."""
+    from long_context_biomedical_imaging_amd import kernels
+    qkv = _qkv(1, L, 2, 1000 + L)
+    out, lse2 = kernels.attn_fwd(qkv.cuda(), 2, 64 ** -0.5)
+    ref, lse = _oracle(qkv, 2)
+    _check(out, ref, f"O L{L}")
+    assert (lse2.cpu() / 1.4426950408889634 - lse).abs().max().item() < 1e-3 * max(1.0, lse.abs().max().item())
+
+
+def test_attention_forward_unsafe_and_growing_tiles():
+    """Exercise both forward paths: keys whose norm grows along the sequence (the stale exponent reference of
+    the max-free fast path carries p up to 2^64) and isolated huge-norm keys late in the sweep (the tile bound
+    fails, so those tiles take the exact row-max path and re-base O and l)."""
+    from long_context_biomedical_imaging_amd import kernels
+    B, L, H = 1, 3000, 2
+    g = torch.Generator().manual_seed(21)
+    qkv = torch.randn(B, L, 3 * H * 64, generator=g)
+    C = H * 64
+    ramp = torch.linspace(0.5, 3.0, L).view(1, L, 1)
+    qkv[..., C:2 * C] *= ramp                                   # growing key norms
+    qkv[:, 2100, C:2 * C] = 40.0 * qkv[:, 7, 0:C] / qkv[:, 7, 0:C].norm(dim=-1, keepdim=True).clamp_min(1e-3)
+    qkv[:, 2900, C:2 * C] *= 25.0                               # an outlier key near the end
+    qkv = qkv.to(torch.bfloat16)
+    out, lse2 = kernels.attn_fwd(qkv.cuda(), H, 64 ** -0.5)
+    ref, lse = _oracle(qkv, H)
+    # scores reach ~60 here: the max error is bounded by the reference's own autocast deviation (peaky test)
+    ac = _reference_autocast_attention(qkv, H, 64 ** -0.5)
+    err, err_ref = (out.float().cpu() - ref).abs().max().item(), (ac - ref).abs().max().item()
+    assert rel_err(out, ref) <= 1e-2 and err <= err_ref, f"O unsafe/growing: {err:.3e} vs autocast {err_ref:.3e}"
+    assert (lse2.cpu() / 1.4426950408889634 - lse).abs().max().item() < 1e-3 * max(1.0, lse.abs().max().item())
