@@ -5,15 +5,16 @@
 //            order (qkv, head, d) (backbone_vit.py:168); O is written as (B, L, H*64) = out_rearrange.
 //            The L x L score matrix is never materialised; the forward keeps lse2 = log2(sum exp) per row.
 //
-// Forward:   one workgroup = NW waves x 32 query rows; K/V tiles of 64 keys double-buffered in LDS
-//            (register-staged, issue-early / write-late). Per wave and tile: S^T = K.Q^T with the
-//            query on the MFMA lane (v_mfma_f32_32x32x16_bf16, 8 MFMAs), lane-local online softmax,
-//            O^T += V^T.P^T with P taken straight from the S accumulators (8 MFMAs, V^T via
-//            ds_read_b64_tr_b16).
+// Forward:   attn_key_norm_kernel (per-64-key-tile max ||k||) + attn_fwd2_kernel: one workgroup = 8 waves x 32
+//            query rows; K/V tiles of 64 keys by buffer loads into a 3-slot LDS ring. Per wave and tile:
+//            S^T = K.Q~^T with the query on the MFMA lane (v_mfma_f32_32x32x16_bf16, 8 MFMAs), lane-local
+//            max-free softmax on tiles the key-norm bound proves safe (exact row max otherwise), O^T += V^T.P^T
+//            with P taken straight from the S accumulators (8 MFMAs, V^T via ds_read_b64_tr_b16); the next
+//            tile's scores are computed in place while this tile's exp2 runs.
 // Backward:  (1) delta = rowsum(dO*O); (2) dK/dV kernel: a workgroup owns NW*32 keys (key on the lane),
 //            sweeps query tiles: S, dP recomputed, dV^T += dO^T.P, dK^T += Q^T.dS (32 MFMAs / tile);
-//            (3) dQ kernel: a workgroup owns NW*32 queries, sweeps key tiles: S^T, dP^T, dQ^T += K^T.dS^T.
-//            No atomics: results are bitwise reproducible.
+//            (3) dQ kernel (v2, pipelined like the forward): a workgroup owns 256 queries, sweeps key tiles:
+//            S^T, dP^T, dQ^T += K^T.dS^T. No atomics: results are bitwise reproducible.
 #include "common.hpp"
 
 #include <type_traits>
@@ -97,159 +98,6 @@ struct TileRegs {
     }
   }
 };
-
-// ------------------------------------------------------------------------------------------ forward
-template <int NW>
-__global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
-  constexpr int NT = NW * 64;
-  constexpr int STAGE = KT * LD_ROW + KT * LD_TR;   // K tile (rows) + V tile (transposed reads)
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * STAGE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int hh = blockIdx.y, b = blockIdx.z;
-  const int L = a.L;
-  const int q0 = blockIdx.x * (NW * 32) + wave * 32;
-  const int qrow = q0 + (lane & 31);
-  const int half = lane >> 5;
-
-  const bf16* qp = a.q + b * a.bs_q + hh * a.hs;
-  const bf16* kp = a.k + b * a.bs_k + hh * a.hs;
-  const bf16* vp = a.v + b * a.bs_v + hh * a.hs;
-
-  // Q^T as the B operand: lane (query r, half h) holds Q[q][16ks + 8h .. +7], prescaled by c = scale*log2(e)
-  // (one bf16 rounding, the same size as the reference's bf16 score rounding under autocast), so the
-  // MFMA chain yields scores directly in the exp2 domain.
-  const float c = a.c;
-  bf16x8 qf[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    bf16x8 t{};
-    if (qrow < L) t = *(const bf16x8*)(qp + (long long)qrow * a.rs_q + ks * 16 + 8 * half);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) t[j] = to_bf16(to_f32(t[j]) * c);
-    qf[ks] = t;
-  }
-
-  TileRegs<NT> kr, vr;
-  const int nkt = (L + KT - 1) / KT;
-  kr.load(kp, a.rs_k, 0, L, tid);
-  vr.load(vp, a.rs_v, 0, L, tid);
-  kr.store(smem, LD_ROW, tid);
-  vr.store(smem + KT * LD_ROW, LD_TR, tid);
-  __syncthreads();
-
-  // Running max m (exp2 domain) enters the score MFMA chain as its initial accumulator: S' = S - m comes
-  // out of the MFMAs, so the common tile needs no per-score subtract, only exp2 (VALU is this loop's
-  // bound, not the matrix pipe). m starts at 0; the first tile always re-bases.
-  f32x16 o0 = {}, o1 = {}, negm = {};
-  float m_run = 0.f, l_run = 0.f;
-
-
-  // Full tiles run without any key-bound code; only the ragged last tile masks (compile-time flag,
-  // otherwise the compiler if-converts the mask into 64 selects per tile).
-  const int nfull = L / KT;
-  auto tile = [&](const int kt, auto ragged) {
-    const bf16* kl = smem + (kt & 1) * STAGE;
-    const bf16* vl = kl + KT * LD_ROW;
-    if (kt + 1 < nfull) {
-      kr.template load<false>(kp, a.rs_k, (kt + 1) * KT, L, tid);
-      vr.template load<false>(vp, a.rs_v, (kt + 1) * KT, L, tid);
-    } else if (kt + 1 < nkt) {
-      kr.load(kp, a.rs_k, (kt + 1) * KT, L, tid);
-      vr.load(vp, a.rs_v, (kt + 1) * KT, L, tid);
-    }
-    LCI_SCHED_HINT();
-    // S'^T tiles: keys 0..31 and 32..63 of this tile (rows), queries on lanes
-    f32x16 s0 = mfma32(frag_row(kl, LD_ROW, 0, 0, lane), qf[0], negm);
-    f32x16 s1 = mfma32(frag_row(kl, LD_ROW, 32, 0, lane), qf[0], negm);
-#pragma unroll
-    for (int ks = 1; ks < 4; ++ks) {
-      s0 = mfma32(frag_row(kl, LD_ROW, 0, ks * 16, lane), qf[ks], s0);
-      s1 = mfma32(frag_row(kl, LD_ROW, 32, ks * 16, lane), qf[ks], s1);
-    }
-    if constexpr (decltype(ragged)::value) {  // ragged last tile: mask keys >= L
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int key = kt * KT + (i & 3) + 8 * (i >> 2) + 4 * half;
-        if (key >= L) s0[i] = NEG_BIG;
-        if (key + 32 >= L) s1[i] = NEG_BIG;
-      }
-    }
-    // row max of S' as four independent chains (latency), then across the two lane halves
-    float mq[4] = {fmaxf(s0[0], s0[1]), fmaxf(s0[2], s0[3]), fmaxf(s1[0], s1[1]), fmaxf(s1[2], s1[3])};
-#pragma unroll
-    for (int i = 4; i < 16; i += 4) {
-      mq[0] = fmaxf(mq[0], fmaxf(s0[i], s0[i + 1]));
-      mq[1] = fmaxf(mq[1], fmaxf(s0[i + 2], s0[i + 3]));
-      mq[2] = fmaxf(mq[2], fmaxf(s1[i], s1[i + 1]));
-      mq[3] = fmaxf(mq[3], fmaxf(s1[i + 2], s1[i + 3]));
-    }
-    const float mx = wave_max_xor32(fmaxf(fmaxf(mq[0], mq[1]), fmaxf(mq[2], mq[3])));
-    // Re-base only when some row's max grew (wave-uniform vote; exact, since otherwise alpha == 1).
-    if (kt == 0 || __any(mx > 0.f)) {
-      const float d = (kt == 0) ? mx : fmaxf(mx, 0.f);
-      m_run += d;
-      if (kt != 0) {
-        const float alpha = exp2_fast(-d);
-        l_run *= alpha;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) { o0[i] *= alpha; o1[i] *= alpha; }
-      }
-#pragma unroll
-      for (int i = 0; i < 16; ++i) { s0[i] -= d; s1[i] -= d; negm[i] = -m_run; }
-    }
-    float lq[4];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      s0[i] = exp2_fast(s0[i]);
-      s1[i] = exp2_fast(s1[i]);
-      if (i < 2) {
-        lq[2 * i] = s0[i];
-        lq[2 * i + 1] = s1[i];
-      } else {
-        lq[(i & 1) * 2] += s0[i];
-        lq[(i & 1) * 2 + 1] += s1[i];
-      }
-    }
-    l_run += (lq[0] + lq[1]) + (lq[2] + lq[3]);
-    const bf16x8 p00 = pack8<0>(s0), p01 = pack8<1>(s0), p10 = pack8<0>(s1), p11 = pack8<1>(s1);
-
-    // O^T[d][q] += V^T[d][key] P^T[key][q]
-    o0 = mfma32(frag_tr<0>(vl, LD_TR, 0, 0, lane), p00, o0);
-    o0 = mfma32(frag_tr<1>(vl, LD_TR, 0, 0, lane), p01, o0);
-    o0 = mfma32(frag_tr<0>(vl, LD_TR, 32, 0, lane), p10, o0);
-    o0 = mfma32(frag_tr<1>(vl, LD_TR, 32, 0, lane), p11, o0);
-    o1 = mfma32(frag_tr<0>(vl, LD_TR, 0, 32, lane), p00, o1);
-    o1 = mfma32(frag_tr<1>(vl, LD_TR, 0, 32, lane), p01, o1);
-    o1 = mfma32(frag_tr<0>(vl, LD_TR, 32, 32, lane), p10, o1);
-    o1 = mfma32(frag_tr<1>(vl, LD_TR, 32, 32, lane), p11, o1);
-    if (kt + 1 < nkt) {
-      bf16* nb = smem + ((kt + 1) & 1) * STAGE;
-      kr.store(nb, LD_ROW, tid);
-      vr.store(nb + KT * LD_ROW, LD_TR, tid);
-    }
-    __syncthreads();
-  };
-  for (int kt = 0; kt < nfull; ++kt) tile(kt, std::false_type{});
-  if (nfull < nkt) tile(nfull, std::true_type{});
-
-  const float l_tot = wave_sum_xor32(l_run);
-  const float inv = 1.f / l_tot;
-  if (qrow < L) {
-    bf16* op = a.out + b * a.bs_out + (long long)qrow * a.rs_out + hh * a.hs;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      bf16x4 w0, w1;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        w0[j] = to_bf16(o0[4 * g + j] * inv);
-        w1[j] = to_bf16(o1[4 * g + j] * inv);
-      }
-      *(bf16x4*)(op + 8 * g + 4 * half) = w0;
-      *(bf16x4*)(op + 32 + 8 * g + 4 * half) = w1;
-    }
-    if (half == 0) a.lse2[((long long)b * a.H + hh) * L + qrow] = m_run + __log2f(l_tot);
-  }
-}
 
 // ------------------------------------------------------------------------------ forward, v2
 // Per-64-key-tile bound on |k|: knorm[b][h][t] = max_{key in tile t} ||k_key||_2 (f32 of the bf16 keys).
@@ -344,8 +192,8 @@ __global__ __launch_bounds__(FW_NW * 64, 1) void attn_fwd2_kernel(AttnArgs a, co
   const bf16* kfrag = smem + (lane & 31) * LD_ROW + 8 * half;
   const bf16* vfrag = smem + KT * LD_ROW + (4 * half + ((lane & 15) >> 2)) * LD_TR + 16 * ((lane >> 4) & 1) +
                       4 * (lane & 3);
-  auto kf = [&](int slot, int r0, int c0) { return *(const bf16x8*)(kfrag + slot + r0 * LD_ROW + c0); };
-  auto vf = [&](int slot, int r0, int s, int c0) {
+  auto kf = [&](int slot, int r0, int c0) __attribute__((always_inline)) { return *(const bf16x8*)(kfrag + slot + r0 * LD_ROW + c0); };
+  auto vf = [&](int slot, int r0, int s, int c0) __attribute__((always_inline)) {
     const bf16* p = vfrag + slot + (r0 + 16 * s) * LD_TR + c0;
     return cat44(lds_tr4(p), lds_tr4(p + 8 * LD_TR));
   };
@@ -364,7 +212,7 @@ __global__ __launch_bounds__(FW_NW * 64, 1) void attn_fwd2_kernel(AttnArgs a, co
   f32x16 o0 = {}, o1 = {}, negm = {};
   float m_run = 0.f, l_run = 0.f;
 
-  auto mask_ragged = [&](int kt, f32x16& t0, f32x16& t1) {
+  auto mask_ragged = [&](int kt, f32x16& t0, f32x16& t1) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int key = kt * KT + (i & 3) + 8 * (i >> 2) + 4 * half;
@@ -373,7 +221,7 @@ __global__ __launch_bounds__(FW_NW * 64, 1) void attn_fwd2_kernel(AttnArgs a, co
     }
   };
   // exact path: row max of the tile (relative to m), lazy re-base when it grew (always on the first tile)
-  auto exact = [&](f32x16& t0, f32x16& t1, bool first) {
+  auto exact = [&](f32x16& t0, f32x16& t1, bool first) __attribute__((always_inline)) {
     float mq[4] = {fmaxf(t0[0], t0[1]), fmaxf(t0[2], t0[3]), fmaxf(t1[0], t1[1]), fmaxf(t1[2], t1[3])};
 #pragma unroll
     for (int i = 4; i < 16; i += 4) {
@@ -413,7 +261,7 @@ __global__ __launch_bounds__(FW_NW * 64, 1) void attn_fwd2_kernel(AttnArgs a, co
   int slA = 0, slB = FSLOT, slC = 2 * FSLOT;
   // One tile j. Entry: S_j in (x0, x1). Exit (NEXT): S_{j+1} in (x0, x1) - the score MFMAs of the next tile
   // write the registers of this tile's scores once these have been exponentiated, packed and summed.
-  auto iter = [&](const int j, auto next) -> bool {
+  auto iter = [&](const int j, auto next) __attribute__((always_inline)) -> bool {
     constexpr bool NEXT = decltype(next)::value;
     // tile j+2 -> registers now, -> LDS slot C at the end (beyond the last tile the range check gives zeros)
     const u32x4 kw = bload16(rk, voff, (j + 2) * KT * rs2);
@@ -556,7 +404,9 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv_kernel(AttnArgs
   constexpr int NT = NW * 64;
   constexpr int TILE = 2 * KT * LD_SW;                  // Q tile + dO tile (both read by rows and transposed)
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * TILE];
+#ifdef LCI_DKDV_ROWC
   __shared__ __attribute__((aligned(16))) float rowc[2][2][KT];  // [buf][lse2 | delta][query]
+#endif
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int hh = blockIdx.y, b = blockIdx.z;
   const int L = a.L;
@@ -589,7 +439,29 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv_kernel(AttnArgs
 
   TileRegs<NT> qr, dr;
   const int nqt = (L + KT - 1) / KT;
-  auto stage_rowc = [&](int buf, int qt) {
+#ifndef LCI_DKDV_ROWC
+  // Row constants as an extra k-step of the S and dP chains: columns 64..79 of each staged Q (dO) row hold
+  // -lse2 (-delta) split into three bf16 terms (hi + mid + lo carries ~24 bits), and the matching B fragment is
+  // 1 in rows 0..2. The chains then yield S c - lse2 and dP - delta with no per-lane row-constant loads
+  // (those were a third of this kernel's LDS read cycles) and no accumulator initialisation moves.
+  auto stage_rowc = [&](int buf, int qt) __attribute__((always_inline)) {
+    if (tid < 2 * KT) {
+      const int which = tid / KT, qi = tid % KT, q = qt * KT + qi;
+      float v;
+      if (which == 0) v = (q < L) ? -lsep[q] : -1.0e30f;  // invalid rows: P = exp2(-huge) = 0
+      else v = (q < L) ? -dlp[q] : 0.f;
+      const bf16 hi = to_bf16(v), mid = to_bf16(v - to_f32(hi)), lo = to_bf16(v - to_f32(hi) - to_f32(mid));
+      bf16x8 e{};
+      e[0] = hi; e[1] = mid; e[2] = lo;
+      bf16* row = smem + buf * TILE + which * KT * LD_SW;
+      *(bf16x8*)(row + swz(qi, 64)) = e;
+      *(bf16x8*)(row + swz(qi, 72)) = bf16x8{};
+    }
+  };
+  bf16x8 onef{};
+  if (half == 0) { onef[0] = to_bf16(1.f); onef[1] = onef[0]; onef[2] = onef[0]; }
+#else
+  auto stage_rowc = [&](int buf, int qt) __attribute__((always_inline)) {
     if (tid < 2 * KT) {
       const int which = tid / KT, qi = tid % KT, q = qt * KT + qi;
       float v;  // stored negated: they are the initial accumulators of the S and dP MFMA chains
@@ -598,6 +470,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv_kernel(AttnArgs
       rowc[buf][which][qi] = v;
     }
   };
+#endif
   qr.load(qp, a.rs_q, 0, L, tid);
   dr.load(dop, a.rs_do, 0, L, tid);
   qr.store_sw(smem, tid);
@@ -622,6 +495,10 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv_kernel(AttnArgs
       // Row constants as the initial accumulators (q = qs*32 + (i&3) + 8(i>>2) + 4h): the chains give
       // S c - lse2[q] and dP - delta[q] directly; then P = exp2(.), dS = P (dP - delta).
       f32x16 s, p;
+#ifndef LCI_DKDV_ROWC
+      s = mfma32(frag_row_sw(ql, qs * 32, 64, lane), onef, f32x16{});
+      p = mfma32(frag_row_sw(dl, qs * 32, 64, lane), onef, f32x16{});
+#else
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const f32x4 la = *(const f32x4*)&rowc[buf][0][qs * 32 + 8 * g + 4 * half];
@@ -632,6 +509,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv_kernel(AttnArgs
           p[4 * g + j] = da[j];
         }
       }
+#endif
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         s = mfma32(frag_row_sw(ql, qs * 32, ks * 16, lane), kf[ks], s);
@@ -684,20 +562,26 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv_kernel(AttnArgs
   }
 }
 
-// ---------------------------------------------------------------------------- backward: dQ kernel
-template <int NW>
-__global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnArgs a) {
-  constexpr int NT = NW * 64;
-  constexpr int TILE = 2 * KT * LD_ROW;   // K tile (rows + transposed) + V tile (rows)
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * TILE];
+// ---------------------------------------------------------------------- backward: dQ kernel, v2
+// Work split of attn_bwd_dq_kernel (8 waves x 32 queries on the lane, key tiles of 64), restructured like the
+// v2 forward: buffer-load staging into a 3-slot LDS ring (K tile swizzled: read by rows for S^T and transposed
+// for dQ), one barrier per tile, and the next tile's S^T / dP^T chains written in place into the accumulators
+// of the current tile as soon as its exp2 / dS / packing has consumed them:
+//   A: VALU on keys 0-31 of tile j (s0, p0) -> dS packs
+//   B: S^T, dP^T chains of keys 0-31 of tile j+1 + dQ MFMAs of keys 0-31 of tile j  ||  VALU on keys 32-63
+//   C: chains of keys 32-63 of tile j+1 + dQ MFMAs of keys 32-63 of tile j
+// Key rows >= L read as zero and are masked (P = 0) on the ragged last tile only.
+constexpr int QSLOT = KT * LD_SW + KT * LD_ROW;   // K tile (swizzled rows) + V tile (rows)
+
+__global__ __launch_bounds__(FW_NW * 64, 1) void attn_bwd_dq2_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[3 * QSLOT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int hh = blockIdx.y, b = blockIdx.z;
   const int L = a.L;
   const int half = lane >> 5;
-  const int qrow = blockIdx.x * (NW * 32) + wave * 32 + (lane & 31);
+  const int qrow = blockIdx.x * (FW_NW * 32) + wave * 32 + (lane & 31);
+  const int nkt = (L + KT - 1) / KT, nfull = L / KT;
 
-  const bf16* kp = a.k + b * a.bs_k + hh * a.hs;
-  const bf16* vp = a.v + b * a.bs_v + hh * a.hs;
   bf16x8 qf[4], df[4];
   float lse2 = 1.0e30f, dlt = 0.f;
   {
@@ -720,72 +604,91 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnArgs a) {
       dlt = a.delta[((long long)b * a.H + hh) * L + qrow];
     }
   }
-
-  TileRegs<NT> kr, vr;
-  const int nkt = (L + KT - 1) / KT;
-  kr.load(kp, a.rs_k, 0, L, tid);
-  vr.load(vp, a.rs_v, 0, L, tid);
-  kr.store(smem, LD_ROW, tid);
-  vr.store(smem + KT * LD_ROW, LD_ROW, tid);
-  __syncthreads();
-
-  f32x16 dq0 = {}, dq1 = {};
-  // -lse2 and -delta of this lane's query as the (constant) initial accumulators of the S^T / dP^T chains
   f32x16 neg_lse, neg_dlt;
 #pragma unroll
   for (int i = 0; i < 16; ++i) { neg_lse[i] = -lse2; neg_dlt[i] = -dlt; }
-  auto tile = [&](const int kt, auto ragged) {
-    const int buf = kt & 1;
-    const bf16* kl = smem + buf * TILE;
-    const bf16* vl = kl + KT * LD_ROW;
-    if (kt + 1 < nkt) {
-      kr.load(kp, a.rs_k, (kt + 1) * KT, L, tid);
-      vr.load(vp, a.rs_v, (kt + 1) * KT, L, tid);
-    }
-    LCI_SCHED_HINT();
-    f32x16 s0 = mfma32(frag_row(kl, LD_ROW, 0, 0, lane), qf[0], neg_lse);
-    f32x16 s1 = mfma32(frag_row(kl, LD_ROW, 32, 0, lane), qf[0], neg_lse);
-    f32x16 p0 = mfma32(frag_row(vl, LD_ROW, 0, 0, lane), df[0], neg_dlt);
-    f32x16 p1 = mfma32(frag_row(vl, LD_ROW, 32, 0, lane), df[0], neg_dlt);
+
+  const int srow = tid >> 3, sch = tid & 7;
+  const int rs2 = a.rs_k * 2;
+  const uint32_t nbytes = (uint32_t)(L - 1) * (uint32_t)rs2 + DH * 2;
+  const rsrc_t rk = make_rsrc(a.k + b * a.bs_k + hh * a.hs, nbytes);
+  const rsrc_t rv = make_rsrc(a.v + b * a.bs_v + hh * a.hs, nbytes);
+  const int voff = srow * rs2 + sch * 16;
+  const int st_k = swz(srow, sch * 8), st_v = KT * LD_SW + srow * LD_ROW + sch * 8;
+
+  {
+    const u32x4 k0 = bload16(rk, voff, 0), v0 = bload16(rv, voff, 0);
+    const u32x4 k1 = bload16(rk, voff, KT * rs2), v1 = bload16(rv, voff, KT * rs2);
+    *(u32x4*)(smem + st_k) = k0;
+    *(u32x4*)(smem + st_v) = v0;
+    *(u32x4*)(smem + QSLOT + st_k) = k1;
+    *(u32x4*)(smem + QSLOT + st_v) = v1;
+  }
+  __syncthreads();
+
+  f32x16 s0, s1, p0, p1, dq0 = {}, dq1 = {};
+  // chains of keys kb*32..+31 of the tile in `slot`
+  auto chains = [&](int slot, int kb, f32x16& sx, f32x16& px) __attribute__((always_inline)) {
+    const bf16* kl = smem + slot * QSLOT;
+    const bf16* vl = kl + KT * LD_SW;
+    sx = mfma32(frag_row_sw(kl, kb * 32, 0, lane), qf[0], neg_lse);
+    px = mfma32(frag_row(vl, LD_ROW, kb * 32, 0, lane), df[0], neg_dlt);
 #pragma unroll
     for (int ks = 1; ks < 4; ++ks) {
-      s0 = mfma32(frag_row(kl, LD_ROW, 0, ks * 16, lane), qf[ks], s0);
-      s1 = mfma32(frag_row(kl, LD_ROW, 32, ks * 16, lane), qf[ks], s1);
-      p0 = mfma32(frag_row(vl, LD_ROW, 0, ks * 16, lane), df[ks], p0);
-      p1 = mfma32(frag_row(vl, LD_ROW, 32, ks * 16, lane), df[ks], p1);
+      sx = mfma32(frag_row_sw(kl, kb * 32, ks * 16, lane), qf[ks], sx);
+      px = mfma32(frag_row(vl, LD_ROW, kb * 32, ks * 16, lane), df[ks], px);
     }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      float e0 = exp2_fast(s0[i]);
-      float e1 = exp2_fast(s1[i]);
-      if constexpr (decltype(ragged)::value) {
-        const int key = kt * KT + (i & 3) + 8 * (i >> 2) + 4 * half;
-        if (key >= L) e0 = 0.f;
-        if (key + 32 >= L) e1 = 0.f;
-      }
-      s0[i] = e0 * p0[i];
-      s1[i] = e1 * p1[i];
-    }
-    const bf16x8 D00 = pack8<0>(s0), D01 = pack8<1>(s0), D10 = pack8<0>(s1), D11 = pack8<1>(s1);
-    // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
-    dq0 = mfma32(frag_tr<0>(kl, LD_ROW, 0, 0, lane), D00, dq0);
-    dq0 = mfma32(frag_tr<1>(kl, LD_ROW, 0, 0, lane), D01, dq0);
-    dq0 = mfma32(frag_tr<0>(kl, LD_ROW, 32, 0, lane), D10, dq0);
-    dq0 = mfma32(frag_tr<1>(kl, LD_ROW, 32, 0, lane), D11, dq0);
-    dq1 = mfma32(frag_tr<0>(kl, LD_ROW, 0, 32, lane), D00, dq1);
-    dq1 = mfma32(frag_tr<1>(kl, LD_ROW, 0, 32, lane), D01, dq1);
-    dq1 = mfma32(frag_tr<0>(kl, LD_ROW, 32, 32, lane), D10, dq1);
-    dq1 = mfma32(frag_tr<1>(kl, LD_ROW, 32, 32, lane), D11, dq1);
-    if (kt + 1 < nkt) {
-      bf16* nb = smem + (buf ^ 1) * TILE;
-      kr.store(nb, LD_ROW, tid);
-      vr.store(nb + KT * LD_ROW, LD_ROW, tid);
-    }
-    __syncthreads();
   };
-  const int nfull = L / KT;
-  for (int kt = 0; kt < nfull; ++kt) tile(kt, std::false_type{});
-  if (nfull < nkt) tile(nfull, std::true_type{});
+  auto mask_ragged = [&](int kt, f32x16& sx, int kb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (kt * KT + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * half >= L) sx[i] = -1.0e30f;
+  };
+  // dS^T = P^T (dP^T - delta), packed as the B operands of dQ^T += K^T dS^T
+  auto grad = [&](f32x16& sx, f32x16& px, bf16x8& d0, bf16x8& d1) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sx[i] = exp2_fast(sx[i]) * px[i];
+    d0 = pack8<0>(sx);
+    d1 = pack8<1>(sx);
+  };
+  auto dq_mfma = [&](int slot, int kb, const bf16x8& d0, const bf16x8& d1) __attribute__((always_inline)) {
+    const bf16* kl = smem + slot * QSLOT;
+    dq0 = mfma32(frag_tr_sw<0>(kl, kb * 32, 0, lane), d0, dq0);
+    dq1 = mfma32(frag_tr_sw<0>(kl, kb * 32, 32, lane), d0, dq1);
+    dq0 = mfma32(frag_tr_sw<1>(kl, kb * 32, 0, lane), d1, dq0);
+    dq1 = mfma32(frag_tr_sw<1>(kl, kb * 32, 32, lane), d1, dq1);
+  };
+
+  chains(0, 0, s0, p0);
+  chains(0, 1, s1, p1);
+  if (nfull == 0) { mask_ragged(0, s0, 0); mask_ragged(0, s1, 1); }
+  int slA = 0, slB = 1, slC = 2;   // ring slots of tiles j, j+1, j+2
+  auto iter = [&](const int j, auto next) __attribute__((always_inline)) {
+    constexpr bool NEXT = decltype(next)::value;
+    const u32x4 kw = bload16(rk, voff, (j + 2) * KT * rs2);
+    const u32x4 vw = bload16(rv, voff, (j + 2) * KT * rs2);
+    bf16x8 a0, a1, c0, c1;
+    grad(s0, p0, a0, a1);                              // A
+    LCI_SB();
+    if constexpr (NEXT) chains(slB, 0, s0, p0);       // B
+    dq_mfma(slA, 0, a0, a1);
+    grad(s1, p1, c0, c1);
+    LCI_SB();
+    if constexpr (NEXT) chains(slB, 1, s1, p1);       // C
+    dq_mfma(slA, 1, c0, c1);
+    LCI_SB();
+    *(u32x4*)(smem + slC * QSLOT + st_k) = kw;
+    *(u32x4*)(smem + slC * QSLOT + st_v) = vw;
+    __syncthreads();
+    const int t = slA; slA = slB; slB = slC; slC = t;
+    if constexpr (NEXT) {
+      if (j + 1 == nfull) [[unlikely]] { mask_ragged(j + 1, s0, 0); mask_ragged(j + 1, s1, 1); }
+    }
+  };
+  int j = 0;
+  for (; j + 1 < nkt; ++j) iter(j, std::true_type{});
+  iter(j, std::false_type{});
+
   if (qrow < L) {
     bf16* dqp = a.out + b * a.bs_out + (long long)qrow * a.rs_out + hh * a.hs;
     const float sc = a.scale;
@@ -793,9 +696,9 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(AttnArgs a) {
     for (int g = 0; g < 4; ++g) {
       bf16x4 w0, w1;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        w0[j] = to_bf16(dq0[4 * g + j] * sc);
-        w1[j] = to_bf16(dq1[4 * g + j] * sc);
+      for (int jj = 0; jj < 4; ++jj) {
+        w0[jj] = to_bf16(dq0[4 * g + jj] * sc);
+        w1[jj] = to_bf16(dq1[4 * g + jj] * sc);
       }
       *(bf16x4*)(dqp + 8 * g + 4 * half) = w0;
       *(bf16x4*)(dqp + 32 + 8 * g + 4 * half) = w1;
@@ -833,19 +736,12 @@ extern "C" int lci_attn_fwd(const void* qkv, void* out, float* lse2, float* knor
   a.hs = DH; a.H = H; a.L = L;
   a.scale = scale; a.c = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
-#ifdef LCI_FWD_V1
-  (void)knorm_ws;
-  constexpr int NW = 4;
-  dim3 grid((L + NW * 32 - 1) / (NW * 32), H, B);
-  hipLaunchKernelGGL(attn_fwd_kernel<NW>, grid, dim3(NW * 64), 0, s, a);
-#else
   LCI_CHECK(knorm_ws != nullptr, "lci_attn_fwd: knorm_ws (lci_attn_fwd_ws_bytes) is required");
   const int nkt = (L + KT - 1) / KT;
   hipLaunchKernelGGL(attn_key_norm_kernel, dim3((nkt + 3) / 4, H, B), dim3(256), 0, s, a, knorm_ws, nkt);
   LCI_LAUNCH_CHECK();
   dim3 grid((L + FW_NW * 32 - 1) / (FW_NW * 32), H, B);
   hipLaunchKernelGGL(attn_fwd2_kernel, grid, dim3(FW_NW * 64), 0, s, a, (const float*)knorm_ws);
-#endif
   LCI_LAUNCH_CHECK();
   return 0;
 }
@@ -889,7 +785,8 @@ extern "C" int lci_attn_bwd_stage(int stage, const void* qkv, const void* out, c
     LCI_LAUNCH_CHECK();
   }
   if (stage < 0 || stage == 2) {
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<NW>, grid, dim3(NW * 64), 0, s, a);
+    hipLaunchKernelGGL(attn_bwd_dq2_kernel, dim3((L + FW_NW * 32 - 1) / (FW_NW * 32), H, B), dim3(FW_NW * 64), 0, s,
+                       a);
     LCI_LAUNCH_CHECK();
   }
   return 0;
