@@ -58,16 +58,16 @@ int lci_attn_bwd_stage(int stage, const void* qkv, const void* out, const void* 
  *                  is the un-shifted, cropped result.
  *   mode 0 (windows): qkv (Bw, N, 3C), optional mask (nW, N, N) f32 (has_mask), out (Bw, N, C).
  * Bias table: lci_window_bias(rpb (H, N, N) f32 = rpb_table[rp_index], mask or null) writes
- *   bias (T, H, Npad, Npad) f32 = (rpb + mask) * log2(e), -1e30 at padded rows/columns (Npad = ceil(N/32)*32,
+ *   bias (T, H, Npad, Npad) bf16 = (rpb + mask) * log2(e), -1e30 at padded rows/columns (Npad = ceil(N/32)*32,
  *   T = lci_window_bias_elems(geo, has_mask) / (H Npad^2): window types), and its transpose biasT (or null).
  * lse2: (Bw, H, N) f32 (Bw = B * prod(ceil(S/ws)) in grid mode). N <= 768. */
 long long lci_window_bias_elems(const int* geo, int has_mask);
-int lci_window_bias(const float* rpb, const float* mask, float* bias, float* biasT, const int* geo, void* stream);
-int lci_window_attn_fwd(const void* qkv, const float* qkv_bias, const float* bias, int has_mask, void* out,
+int lci_window_bias(const float* rpb, const float* mask, void* bias, void* biasT, const int* geo, void* stream);
+int lci_window_attn_fwd(const void* qkv, const float* qkv_bias, const void* bias, int has_mask, void* out,
                         float* lse2, const int* geo, float scale, void* stream);
 /* dqkv (same layout as qkv) <- dQ/dK/dV; dbias_pad (3C, accumulated) <- dK/dV of padded voxels;
  * dS: optional bf16 workspace of lci_window_dS_elems(geo) elements; drpb (H, N, N) f32 written if dS given. */
-int lci_window_attn_bwd(const void* qkv, const float* qkv_bias, const float* bias, const float* biasT, int has_mask,
+int lci_window_attn_bwd(const void* qkv, const float* qkv_bias, const void* bias, const void* biasT, int has_mask,
                         const void* out, const void* dout, const float* lse2, void* dqkv, float* dbias_pad,
                         void* dS, float* drpb, const int* geo, float scale, void* stream);
 long long lci_window_dS_elems(const int* geo);

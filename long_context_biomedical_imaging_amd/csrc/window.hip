@@ -10,7 +10,7 @@
 // compute_mask builds it (:591-628). WINDOWS mode takes pre-partitioned (Bw, N, 3C) and an optional mask.
 //
 // Additive logit term: every window of one "type" shares rpb + mask, so lci_window_bias builds, once per call,
-// a log2-domain table bias[type][head][q][k] = (rpb[h][q][k] + mask) * log2(e), -1e30 for padded keys/queries
+// a log2-domain bf16 table bias[type][head][q][k] = (rpb[h][q][k] + mask) * log2(e), -1e30 for padded keys/queries
 // (grid mode: type = which axes the window is the last one on, when shifted -> <= 8 types; windows mode:
 // type = w % nW when a mask is given). The table tile is the INITIAL ACCUMULATOR of the score MFMAs, Q is
 // prescaled by scale*log2(e): the chain yields the full log2-domain logit, no per-element bias/mask VALU.
@@ -34,8 +34,8 @@ struct WinArgs {
   const bf16* qkv; const float* qkv_bias;  // bias (3C) f32 or null: value of padded tokens
   const float* rpb;                        // (H, N, N) f32 rpb_table[index] (table builder only)
   const float* mask;                       // WINDOWS mode: (nW, N, N) f32 or null (table builder only)
-  const float* bias;                       // (T, H, Npad, Npad) log2-domain logit term [q][k]
-  const float* biasT;                      // the same, transposed [k][q] (backward phase 2)
+  const bf16* bias;                        // (T, H, Npad, Npad) log2-domain logit term [q][k], bf16
+  const bf16* biasT;                       // the same, transposed [k][q] (backward phase 2)
   bf16* out; const bf16* o; const bf16* dout;
   float* lse2;                             // (Bw, H, N)
   bf16* dqkv; float* dbias_pad;            // bwd
@@ -173,7 +173,7 @@ __device__ __forceinline__ int win_region(const WinArgs& a, int t, int n) {
   return rid;
 }
 
-__global__ __launch_bounds__(256) void win_bias_kernel(WinArgs a, float* bias, float* biasT) {
+__global__ __launch_bounds__(256) void win_bias_kernel(WinArgs a, bf16* bias, bf16* biasT) {
   const long long np2 = (long long)a.Npad * a.Npad;
   const long long e = blockIdx.x * 256LL + threadIdx.x;
   if (e >= (long long)a.T * a.H * np2) return;
@@ -187,19 +187,23 @@ __global__ __launch_bounds__(256) void win_bias_kernel(WinArgs a, float* bias, f
     if (a.mode == 1 && a.masked && win_region(a, t, q) != win_region(a, t, k)) v += -100.f;
     v *= WLOG2E;
   }
-  bias[e] = v;
-  if (biasT) biasT[th * np2 + (long long)k * a.Npad + q] = v;
+  bias[e] = to_bf16(v);
+  if (biasT) biasT[th * np2 + (long long)k * a.Npad + q] = to_bf16(v);
 }
 
 // 16 table values of one 32x32 score tile for this lane: row r (q or key, the lane's), columns
-// c0 + 8g + 4h + j  ->  register 4g + j (the 32x32x16 accumulator layout)
-__device__ __forceinline__ f32x16 win_bias_tile(const float* row, int c0) {
+// c0 + 8g + 4h + j  ->  register 4g + j (the 32x32x16 accumulator layout). The table is bf16 (|rpb| ~ 0.02 and
+// the -100 mask lose nothing that matters at bf16 score precision): half the bytes of an f32 table, and the
+// tables of one head (all window types) stay L2-resident while that head's windows run.
+__device__ __forceinline__ f32x16 win_bias_tile(const bf16* row, int c0) {
   f32x16 r;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
-    const f32x4 v = *(const f32x4*)(row + c0 + 8 * g);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) r[4 * g + j] = v[j];
+    const u32x2 v = *(const u32x2*)(row + c0 + 8 * g);
+    r[4 * g + 0] = __uint_as_float(v[0] << 16);
+    r[4 * g + 1] = __uint_as_float(v[0] & 0xffff0000u);
+    r[4 * g + 2] = __uint_as_float(v[1] << 16);
+    r[4 * g + 3] = __uint_as_float(v[1] & 0xffff0000u);
   }
   return r;
 }
@@ -220,7 +224,7 @@ __global__ __launch_bounds__(NW * 64) void win_attn_fwd_kernel(WinArgs a) {
   win_setup(a, smem, L, w);
   win_stage<NW * 64>(a, L, a.C + hh * WHD, 2 * a.C + hh * WHD, false, nullptr, w);   // K -> t0, V -> t1
   const float c = a.c;
-  const float* bh = a.bias + ((long long)win_type(a, w) * a.H + hh) * a.Npad * a.Npad;
+  const bf16* bh = a.bias + ((long long)win_type(a, w) * a.H + hh) * a.Npad * a.Npad;
   bf16x8 qn[2];   // next query block's Q, loaded one block ahead
   auto load_q = [&](int qb) {
     const int q = qb * 32 + (lane & 31);
@@ -236,7 +240,7 @@ __global__ __launch_bounds__(NW * 64) void win_attn_fwd_kernel(WinArgs a) {
     const int qrow = qv ? L.row[q] : -2;
     const bf16x8 qf[2] = {scaled8(qn[0], c), scaled8(qn[1], c)};
     if (qb + NW < a.nqb) load_q(qb + NW);
-    const float* brow = bh + (long long)q * a.Npad + 4 * half;
+    const bf16* brow = bh + (long long)q * a.Npad + 4 * half;
     f32x16 o = {};
     float m = 0.f, l = 0.f;
     f32x16 b0 = win_bias_tile(brow, 0), b1;   // table tiles two ahead
@@ -335,7 +339,7 @@ __global__ __launch_bounds__(256) void win_attn_bwd_kernel(WinArgs a) {
     f32x16 ndl;
 #pragma unroll
     for (int i = 0; i < 16; ++i) ndl[i] = -delta;
-    const float* brow = a.bias + tho + (long long)q * a.Npad + 4 * half;
+    const bf16* brow = a.bias + tho + (long long)q * a.Npad + 4 * half;
     f32x16 dq = {};
     f32x16 b0 = win_bias_tile(brow, 0), b1;
     if (a.nkt > 1) b1 = win_bias_tile(brow, 32);
@@ -384,7 +388,7 @@ __global__ __launch_bounds__(256) void win_attn_bwd_kernel(WinArgs a) {
       kf[ks] = scaled8(win_load8(a, krow, a.C + hh * WHD + ks * 16 + 8 * half, kv), c);
       vf[ks] = win_load8(a, krow, 2 * a.C + hh * WHD + ks * 16 + 8 * half, kv);
     }
-    const float* brow = a.biasT + tho + (long long)key * a.Npad + 4 * half;
+    const bf16* brow = a.biasT + tho + (long long)key * a.Npad + 4 * half;
     f32x16 dk = {}, dv = {};
     f32x16 b0 = win_bias_tile(brow, 0), b1;
     if (a.nkt > 1) b1 = win_bias_tile(brow, 32);
@@ -504,7 +508,7 @@ extern "C" long long lci_window_bias_elems(const int* geo, int has_mask) {
   return (long long)a.T * a.H * a.Npad * a.Npad;
 }
 
-extern "C" int lci_window_bias(const float* rpb, const float* mask, float* bias, float* biasT, const int* geo,
+extern "C" int lci_window_bias(const float* rpb, const float* mask, void* bias, void* biasT, const int* geo,
                                void* stream) {
   WinArgs a{};
   if (win_fill(a, geo, 1.f)) return 1;
@@ -512,17 +516,17 @@ extern "C" int lci_window_bias(const float* rpb, const float* mask, float* bias,
   if (a.mode == 0 && mask) a.T = a.nW;
   const long long n = (long long)a.T * a.H * a.Npad * a.Npad;
   hipLaunchKernelGGL(win_bias_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a,
-                     bias, biasT);
+                     (bf16*)bias, (bf16*)biasT);
   LCI_LAUNCH_CHECK();
   return 0;
 }
 
-extern "C" int lci_window_attn_fwd(const void* qkv, const float* qkv_bias, const float* bias, int has_mask,
+extern "C" int lci_window_attn_fwd(const void* qkv, const float* qkv_bias, const void* bias, int has_mask,
                                    void* out, float* lse2, const int* geo, float scale, void* stream) {
   WinArgs a{};
   if (win_fill(a, geo, scale)) return 1;
   if (a.mode == 0 && has_mask) a.T = a.nW;
-  a.qkv = (const bf16*)qkv; a.qkv_bias = qkv_bias; a.bias = bias; a.out = (bf16*)out; a.lse2 = lse2;
+  a.qkv = (const bf16*)qkv; a.qkv_bias = qkv_bias; a.bias = (const bf16*)bias; a.out = (bf16*)out; a.lse2 = lse2;
   constexpr int NW = 8;   // 8 waves share the window's K/V: 4 waves per SIMD at 2 workgroups per CU (LDS-bound)
   (void)hipFuncSetAttribute((const void*)win_attn_fwd_kernel<NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             160 * 1024);
@@ -534,14 +538,14 @@ extern "C" int lci_window_attn_fwd(const void* qkv, const float* qkv_bias, const
 
 // dbias_pad (3C) accumulated (caller zeroes); dS tiles (Bw*H*nqb*nkt*1024 bf16) optional workspace;
 // drpb (H, N, N) f32 written when dS and drpb are given.
-extern "C" int lci_window_attn_bwd(const void* qkv, const float* qkv_bias, const float* bias, const float* biasT,
+extern "C" int lci_window_attn_bwd(const void* qkv, const float* qkv_bias, const void* bias, const void* biasT,
                                    int has_mask, const void* out, const void* dout, const float* lse2, void* dqkv,
                                    float* dbias_pad, void* dS, float* drpb, const int* geo, float scale,
                                    void* stream) {
   WinArgs a{};
   if (win_fill(a, geo, scale)) return 1;
   if (a.mode == 0 && has_mask) a.T = a.nW;
-  a.qkv = (const bf16*)qkv; a.qkv_bias = qkv_bias; a.bias = bias; a.biasT = biasT; a.o = (const bf16*)out;
+  a.qkv = (const bf16*)qkv; a.qkv_bias = qkv_bias; a.bias = (const bf16*)bias; a.biasT = (const bf16*)biasT; a.o = (const bf16*)out;
   a.dout = (const bf16*)dout; a.lse2 = (float*)lse2; a.dqkv = (bf16*)dqkv; a.dbias_pad = dbias_pad;
   a.dS = (bf16*)dS; a.drpb = drpb;
   hipStream_t s = (hipStream_t)stream;

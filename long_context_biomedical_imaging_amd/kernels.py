@@ -361,9 +361,9 @@ def _window_bias(rpb, mask, geo, transposed=False):
     n = int(_lib.load().lci_window_bias_elems(g, int(mask is not None)))
     if n <= 0:
         raise _lib.LciError(_lib.load().lci_last_error().decode())
-    f32 = dict(device=rpb.device, dtype=torch.float32)
-    bias = torch.empty(n, **f32)
-    bt = torch.empty(n, **f32) if transposed else None
+    b16 = dict(device=rpb.device, dtype=torch.bfloat16)
+    bias = torch.empty(n, **b16)
+    bt = torch.empty(n, **b16) if transposed else None
     _lib.call("lci_window_bias", rpb.data_ptr(), _lib.ptr(mask), bias.data_ptr(), _lib.ptr(bt), g,
               _lib.stream_of(rpb))
     return bias, bt
