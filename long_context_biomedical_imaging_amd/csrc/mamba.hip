@@ -39,6 +39,40 @@ struct ScanArgs {
 
 template <typename T> __device__ __forceinline__ float ldf(const T* p) { return (float)(*p); }
 
+// One channel column of a channels-last (B, L, ·) tensor addressed through a buffer resource: the lane's channel
+// byte offset is the VGPR offset, the token offset t * stride is a wave-uniform SGPR offset, so per-step loads and
+// stores need no 64-bit address VALU. Lanes past Dx get an out-of-range offset: their loads read 0 and their
+// stores are dropped by the range check (no exec-mask branches).
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+template <typename T>
+struct Col {
+  rsrc_t r;
+  int voff, ts;   // bytes
+  // the host checks L * tstride * sizeof(T) < 2^31 (scan_fill)
+  __device__ __forceinline__ Col(const void* base, int L, int tstride, int Dx, int d, bool valid) {
+    const int bytes = ((L - 1) * tstride + Dx) * (int)sizeof(T);
+    r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
+    voff = valid ? d * (int)sizeof(T) : 0x7fffffff;
+    ts = tstride * (int)sizeof(T);
+  }
+  __device__ __forceinline__ float ld(int t) const {
+    if constexpr (sizeof(T) == 2) {
+      const uint32_t v = __builtin_amdgcn_raw_buffer_load_b16(r, voff, t * ts, 0);
+      return __uint_as_float(v << 16);
+    } else {
+      return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, t * ts, 0));
+    }
+  }
+  __device__ __forceinline__ void st(int t, float v) const {
+    if constexpr (sizeof(T) == 2) {
+      const bf16 h = to_bf16(v);
+      __builtin_amdgcn_raw_buffer_store_b16(*(const uint16_t*)&h, r, voff, t * ts, 0);
+    } else {
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff, t * ts, 0);
+    }
+  }
+};
+
 template <typename T>
 __device__ __forceinline__ void ld8(const T* p, float (&v)[SCAN_N]) {
   if constexpr (sizeof(T) == 2) {
@@ -136,11 +170,11 @@ __global__ __launch_bounds__(256) void scan_fwd_kernel(ScanArgs a) {
 #pragma unroll
   for (int n = 0; n < SCAN_N; ++n) x[n] = MODE ? a.xinit[sidx + n] : 0.f;
   // per-step addresses = wave-uniform row base (scalar arithmetic) + this lane's channel offset
-  const T* ub = (const T*)a.u + b * a.bu;
-  const T* db = (const T*)a.delta + b * a.bd;
+  const Col<T> ucol((const T*)a.u + b * a.bu, a.L, a.tu, a.Dx, d, valid);
+  const Col<T> dcol((const T*)a.delta + b * a.bd, a.L, a.td, a.Dx, d, valid);
+  const Col<T> ycol((T*)a.y + b * a.by, a.L, a.ty, a.Dx, d, valid);
   const T* Bp = (const T*)a.Bm + b * a.bB;
   const T* Cp = (const T*)a.Cm + b * a.bC;
-  T* yb = (T*)a.y + b * a.by;
   float* ckb = a.ckpt + (long long)b * a.nck * a.Dx * SCAN_N;
   float* bc = bcl[wv];
   const int t0 = chunk * a.Tc, t1 = min(a.L, t0 + a.Tc);
@@ -152,9 +186,9 @@ __global__ __launch_bounds__(256) void scan_fwd_kernel(ScanArgs a) {
       float uf[PF], dr[PF];
 #pragma unroll
       for (int i = 0; i < PF; ++i) {        // the group's u / dt loads first (clamped, branch-free)
-        const long long t = min(tb + i, tse - 1);
-        uf[i] = ldf((ub + t * a.tu) + dd);
-        dr[i] = ldf((db + t * a.td) + dd);
+        const int t = min(tb + i, tse - 1);
+        uf[i] = ucol.ld(t);
+        dr[i] = dcol.ld(t);
       }
       const int nvalid = tse - tb;   // >= PF except in a chunk's ragged tail
 #pragma unroll
@@ -182,7 +216,7 @@ __global__ __launch_bounds__(256) void scan_fwd_kernel(ScanArgs a) {
               y0 = fmaf(Cv[n], x[n], y0);
               y1 = fmaf(Cv[n + 1], x[n + 1], y1);
             }
-            if (valid) (yb + (long long)t * a.ty)[dd] = (T)(y0 + y1);
+            ycol.st(t, y0 + y1);
           } else {
             sumdt += dt;
           }
@@ -271,8 +305,8 @@ __global__ __launch_bounds__(256) void scan_bwd_agg_kernel(ScanArgs a) {
 #pragma unroll
   for (int n = 0; n < SCAN_N; ++n) { A2[n] = a.A[dd * SCAN_N + n] * LOG2E; g[n] = 0.f; }
   const float bias = a.dbias ? a.dbias[dd] : 0.f;
-  const T* db = (const T*)a.delta + b * a.bd;
-  const T* gb = (const T*)a.dy + b * a.bdy;
+  const Col<T> dcol((const T*)a.delta + b * a.bd, a.L, a.td, a.Dx, d, valid);
+  const Col<T> gcol((const T*)a.dy + b * a.bdy, a.L, a.tdy, a.Dx, d, valid);
   const T* Cp = (const T*)a.Cm + b * a.bC;
   float* bc = bcl[wv];
   const int t0 = chunk * a.Tc, t1 = min(a.L, t0 + a.Tc);
@@ -292,9 +326,9 @@ __global__ __launch_bounds__(256) void scan_bwd_agg_kernel(ScanArgs a) {
       float dr[PF], gyv[PF];
 #pragma unroll
       for (int i = 0; i < PF; ++i) {
-        const long long t = max(te - i, tsb);
-        dr[i] = ldf((db + t * a.td) + dd);
-        gyv[i] = ldf((gb + t * a.tdy) + dd);
+        const int t = max(te - i, tsb);
+        dr[i] = dcol.ld(t);
+        gyv[i] = gcol.ld(t);
       }
 #pragma unroll
       for (int i = 0; i < PF; ++i) {
@@ -614,10 +648,15 @@ static int scan_check_bc(const void* Bm, const void* Cm, long long tB, long long
   return 0;
 }
 
-static void scan_strides(ScanArgs& a, const long long* s) {
+static int scan_strides(ScanArgs& a, const long long* s, int dtype) {
   a.bu = s[0]; a.tu = (int)s[1]; a.bd = s[2]; a.td = (int)s[3]; a.bB = s[4]; a.tB = (int)s[5];
   a.bC = s[6]; a.tC = (int)s[7]; a.by = s[8]; a.ty = (int)s[9]; a.bdy = s[10]; a.tdy = (int)s[11];
   a.bdu = s[12]; a.tdu = (int)s[13]; a.bdd = s[14]; a.tdd = (int)s[15];
+  // per-sample column tensors are addressed with 32-bit buffer offsets (Col): (L + 1) rows of token stride
+  for (int i = 1; i < 16; i += 2)
+    LCI_CHECK((long long)(a.L + 1) * s[i] * (dtype == 1 ? 2 : 4) < (1ll << 31),
+              "selective_scan: L=%d x token stride %lld too large for 32-bit buffer offsets", a.L, s[i]);
+  return 0;
 }
 
 // Workspace (f32): xend, xinit (B*nch*Dx*N each), sdt (B*nch*Dx), ckpt (B*nck*Dx*N) if ckpt != null.
@@ -629,7 +668,7 @@ extern "C" int lci_selective_scan_fwd(int dtype, const void* u, const void* delt
   ScanArgs a{};
   if (scan_fill(a, B, L, Dx, N, chunk)) return 1;
   a.softplus = delta_softplus;
-  scan_strides(a, strides);
+  if (scan_strides(a, strides, dtype)) return 1;
   if (scan_check_bc(Bm, Cm, strides[5], strides[7], dtype)) return 1;
   a.u = u; a.delta = delta; a.A = A; a.Bm = Bm; a.Cm = Cm; a.D = D; a.dbias = delta_bias; a.y = y;
   a.xend = xend; a.xinit = xinit; a.sdt = sdt; a.ckpt = ckpt; a.write_ckpt = ckpt != nullptr;
@@ -657,7 +696,7 @@ extern "C" int lci_selective_scan_bwd(int dtype, const void* u, const void* delt
   ScanArgs a{};
   if (scan_fill(a, B, L, Dx, N, chunk)) return 1;
   a.softplus = delta_softplus;
-  scan_strides(a, strides);
+  if (scan_strides(a, strides, dtype)) return 1;
   if (scan_check_bc(Bm, Cm, strides[5], strides[7], dtype)) return 1;
   a.u = u; a.delta = delta; a.A = A; a.Bm = Bm; a.Cm = Cm; a.D = D; a.dbias = delta_bias; a.dy = dy;
   a.du = du; a.ddelta = ddelta; a.dBC = dBC; a.dA = dA; a.dD = dD; a.ddbias = ddelta_bias;
