@@ -13,6 +13,7 @@ from collections.abc import Sequence
 
 import torch
 import torch.nn as nn
+import torch.utils.checkpoint
 
 from . import kernels
 from .blocks import MLPBlock, PatchEmbeddingBlock
@@ -147,6 +148,9 @@ class ViT_with_alt_ops(nn.Module):
             TransformerBlock(use_hyena, use_mamba, hidden_size, mlp_dim, num_heads, dropout_rate, qkv_bias,
                              save_attn) for _ in range(num_layers)])
         self.norm = nn.LayerNorm(hidden_size)
+        # Not a reference option: per-block activation checkpointing (recompute each block's forward in the
+        # backward) for token counts whose saved activations exceed one GPU (256^3 p2: ~35 GB per block).
+        self.checkpoint_blocks = False
         if self.classification and not use_hyena and not use_mamba:
             self.cls_token = nn.Parameter(torch.zeros(1, 1, hidden_size))
 
@@ -159,7 +163,10 @@ class ViT_with_alt_ops(nn.Module):
             cls_token = self.cls_token.expand(x.shape[0], -1, -1)
             x = torch.cat((cls_token, x), dim=1)
         for blk in self.blocks:
-            x = blk(x)
+            if self.checkpoint_blocks and self.training and torch.is_grad_enabled():
+                x = torch.utils.checkpoint.checkpoint(blk, x, use_reentrant=False)
+            else:
+                x = blk(x)
             hidden_states_out.append(x)
         x = self.norm(x)
         hidden_states_out.append(x)

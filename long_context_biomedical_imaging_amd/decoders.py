@@ -10,14 +10,22 @@ from __future__ import annotations
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 
 def _conv(nd, cin, cout, k, s, transposed=False, bias=False):
-    """MONAI get_conv_layer(conv_only=True): padding (k - s + 1) // 2, output_padding 2p + s - k."""
-    pad = (k - s + 1) // 2
+    """MONAI get_conv_layer(conv_only=True): padding (k - s + 1) // 2, output_padding 2p + s - k (per axis)."""
+    if isinstance(k, (tuple, list)) or isinstance(s, (tuple, list)):
+        k = tuple(k) if isinstance(k, (tuple, list)) else (k,) * nd
+        s = tuple(s) if isinstance(s, (tuple, list)) else (s,) * nd
+        pad = tuple((a - b + 1) // 2 for a, b in zip(k, s))
+        opad = tuple(2 * p + b - a for p, a, b in zip(pad, k, s))
+    else:
+        pad = (k - s + 1) // 2
+        opad = 2 * pad + s - k
     if transposed:
         cls = nn.ConvTranspose2d if nd == 2 else nn.ConvTranspose3d
-        return cls(cin, cout, k, s, padding=pad, output_padding=2 * pad + s - k, bias=bias)
+        return cls(cin, cout, k, s, padding=pad, output_padding=opad, bias=bias)
     cls = nn.Conv2d if nd == 2 else nn.Conv3d
     return cls(cin, cout, k, s, padding=pad, bias=bias)
 
@@ -77,6 +85,67 @@ class UnetOutBlock(nn.Module):
 
     def forward(self, x):
         return self.conv(x)
+
+
+class UnetrBasicBlock(nn.Module):
+    """MONAI UnetrBasicBlock(res_block=True): one UnetResBlock under `.layer`."""
+
+    def __init__(self, nd, cin, cout, k, stride):
+        super().__init__()
+        self.layer = UnetResBlock(nd, cin, cout, k, stride)
+
+    def forward(self, x):
+        return self.layer(x)
+
+
+class SwinUNETR(nn.Module):
+    """enhance_heads.py:30-184: UNETR-style decoder over the five Swin stage taps (features [96, 192, 384, 768,
+    1536] for Swin-tiny) and the input image; instance-norm residual conv blocks, transposed-conv up-sampling, the
+    last up-sampling by the patch size."""
+
+    def __init__(self, config, input_feature_channels, output_feature_channels):
+        super().__init__()
+        f = input_feature_channels
+        if f[0] % 12 != 0:
+            raise ValueError("Features should be divisible by 12 to use current UNETR config.")
+        if config.encoder_name != "Swin":
+            raise ValueError(f"Invalid backbone component for SwinUNETR head: {config.encoder_name}")
+        cin = config.no_in_channel
+        if config.time == 1:
+            nd, self.spatial_dims, up = 2, 2, 2
+            patch = tuple(config.Swin.patch_size[1:])
+        else:
+            nd, self.spatial_dims, up = 3, 3, (2, 2, 2)
+            patch = tuple(config.Swin.patch_size)
+        self.encoder1 = UnetrBasicBlock(nd, cin, f[0], 3, 1)
+        self.encoder2 = UnetrBasicBlock(nd, f[0], f[0], 3, 1)
+        self.encoder3 = UnetrBasicBlock(nd, f[1], f[1], 3, 1)
+        self.encoder4 = UnetrBasicBlock(nd, f[2], f[2], 3, 1)
+        self.encoder10 = UnetrBasicBlock(nd, f[4], f[4], 3, 1)
+        self.decoder5 = UnetrUpBlock(nd, f[4], f[3], 3, up)
+        self.decoder4 = UnetrUpBlock(nd, f[3], f[2], 3, up)
+        self.decoder3 = UnetrUpBlock(nd, f[2], f[1], 3, up)
+        self.decoder2 = UnetrUpBlock(nd, f[1], f[0], 3, up)
+        self.decoder1 = UnetrUpBlock(nd, f[0], f[0], 3, patch)
+        self.out = UnetOutBlock(nd, f[0], output_feature_channels)
+
+    def forward(self, input_data):
+        if self.spatial_dims == 2:
+            input_data = [i.squeeze(2) for i in input_data]
+        x_in, feats = input_data[0], input_data[1:]
+        enc0 = self.encoder1(x_in)
+        enc1 = self.encoder2(feats[0])
+        enc2 = self.encoder3(feats[1])
+        enc3 = self.encoder4(feats[2])
+        dec4 = self.encoder10(feats[4])
+        dec3 = self.decoder5(dec4, feats[3])
+        dec2 = self.decoder4(dec3, enc3)
+        dec1 = self.decoder3(dec2, enc2)
+        dec0 = self.decoder2(dec1, enc1)
+        out = self.out(self.decoder1(dec0, enc0))
+        if self.spatial_dims == 2:
+            out = out.unsqueeze(2)
+        return out
 
 
 class ViTUNETR(nn.Module):

@@ -5,7 +5,7 @@ import torch.nn as nn
 
 from .backbone_swin import custom_Swin
 from .backbone_vit import custom_ViT
-from .decoders import Identity, SwinLinear, ViTLinear, ViTUNETR
+from .decoders import Identity, SwinLinear, SwinUNETR, ViTLinear, ViTUNETR
 
 
 def identity_model(config, input_feature_channels):
@@ -36,7 +36,9 @@ class EncoderDecoderModel(nn.Module):
             self.decoder = SwinLinear(config, self.encoder_feature_channels, output_feature_channels)
         elif decoder_name == "ViTUNETR":
             self.decoder = ViTUNETR(config, self.encoder_feature_channels, output_feature_channels)
-        elif decoder_name in ("UperNet2D", "UperNet3D", "SwinUNETR"):
+        elif decoder_name == "SwinUNETR":
+            self.decoder = SwinUNETR(config, self.encoder_feature_channels, output_feature_channels)
+        elif decoder_name in ("UperNet2D", "UperNet3D"):
             raise NotImplementedError(f"Decoder {decoder_name}: MONAI/torchvision conv decoder outside the "
                                       "mixer hot path (SURVEY.md §8(f) rank 2); not built yet")
         else:

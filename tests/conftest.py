@@ -6,6 +6,9 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+# MIOpen's default find mode benchmarks every solver on a conv shape's first call (70-120 s per 3-D shape on
+# a fresh box, tools/conv3d_probe.py); the decoder-head tests only need a working solver
+os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
 TESTS = os.path.dirname(os.path.abspath(__file__))
 if TESTS not in sys.path:
     sys.path.insert(0, TESTS)

@@ -88,3 +88,23 @@ def test_product_path_has_no_cpu_fallback():
     m = backbone_vit.SABlock(False, False, 128, 2)
     with pytest.raises(RuntimeError):
         m(torch.randn(1, 16, 128))
+
+
+def test_swin_unetr_head_construction():
+    """SwinUNETR head over Swin-tiny's feature channels [96, 192, 384, 768, 1536] (enhance_heads.py:30-184):
+    block structure and the reference's argument checks."""
+    import pytest
+    from long_context_biomedical_imaging_amd import config as lconfig
+    from long_context_biomedical_imaging_amd.decoders import SwinUNETR
+    cfg = lconfig.parse_config(["--encoder_name", "Swin", "--decoder_name", "SwinUNETR", "--height", "64",
+                                "--width", "64", "--time", "64", "--Swin.patch_size", "2", "2", "2"])
+    h = SwinUNETR(cfg, [96, 192, 384, 768, 1536], 2)
+    assert h.encoder10.layer.conv1.weight.shape == (1536, 1536, 3, 3, 3)
+    assert h.decoder5.transp_conv.weight.shape == (1536, 768, 2, 2, 2)
+    assert h.decoder1.transp_conv.weight.shape == (96, 96, 2, 2, 2)
+    assert h.out.conv.weight.shape == (2, 96, 1, 1, 1)
+    with pytest.raises(ValueError):
+        SwinUNETR(cfg, [100, 192, 384, 768, 1536], 2)
+    cfg.encoder_name = "ViT"
+    with pytest.raises(ValueError):
+        SwinUNETR(cfg, [96, 192, 384, 768, 1536], 2)
