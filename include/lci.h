@@ -19,6 +19,7 @@
  *   lci_dwconv_silu_*     MambaVisionMixer depthwise conv1d + SiLU, model/models/mamba.py:118-119
  *   lci_fftconv_*         fftconv_ref (gelu=False), model/models/hyena.py:32-51 / Filter.forward :201-216
  *   lci_hyena_pre/post_*  HyenaOperator short filter + gating, model/models/hyena.py:317-355
+ *   lci_conv3_fwd         MONAI-1.3 UnetResBlock 3x3(x3) convs of the ViTUNETR / SwinUNETR heads, enhance_heads.py:30-356
  *   lci_patch_embed_*     MONAI-1.3 PatchEmbeddingBlock (backbone_vit.py:351-361) / PatchEmbed (backbone_swin.py:800-806)
  */
 #ifndef LCI_H_
@@ -71,6 +72,22 @@ int lci_window_attn_bwd(const void* qkv, const float* qkv_bias, const void* bias
                         const void* out, const void* dout, const float* lse2, void* dqkv, float* dbias_pad,
                         void* dS, float* drpb, const int* geo, float scale, void* stream);
 long long lci_window_dS_elems(const int* geo);
+
+/* ------------------------------------------------------------------ decoder-head 3x3(x3) convolution
+ * Replaces the kernel-3 stride-1 convs of MONAI-1.3 UnetResBlock (get_conv_layer conv_only, bias=False) in the
+ * ViTUNETR / SwinUNETR heads (model/models/enhance_heads.py:30-356).
+ * x (B, D, H, W, Cin) bf16 channels-last; w (Cout, KD*9, Cin) bf16 (tap order kd, kh, kw); y (B, D, H, W, Cout)
+ * bf16 = sum over taps/channels of x[p + (kd-1, kh-1, kw-1)] w (zero outside the volume), f32 accumulation.
+ * KD = 3 (3-D) or 1 (2-D, D = 1). Cout % 32 == 0. The input gradient is the same call on dy with
+ * w'[c, t, n] = w[n, c, KD*9-1-t]. */
+int lci_conv3_fwd(const void* x, const void* w, void* y, int B, int D, int H, int W, int Cin, int Cout, int KD,
+                  void* stream);
+/* Weight gradient: part (lci_conv3_wgrad_splits(B*D*H*W) * 4, KD*9, Cout, Cin) f32 <- per-(voxel split, wave)
+ * partial sums of dy[p, n] * x[p + off(tap), c]; dW[n, c, tap] = sum over the first axis (caller). x (.., Cin),
+ * dy (.., Cout) bf16 channels-last; Cin, Cout multiples of 32. Deterministic (no atomics). */
+long long lci_conv3_wgrad_splits(long long V);
+int lci_conv3_wgrad(const void* x, const void* dy, float* part, int B, int D, int H, int W, int Cin, int Cout,
+                    int KD, void* stream);
 
 /* ------------------------------------------------------------------ Mamba selective scan (d_state 8)
  * Channels-last: u, delta (B, L, Dx); Bm, Cm (B, L, 8) (e.g. column slices of x_proj's output); y (B, L, .).

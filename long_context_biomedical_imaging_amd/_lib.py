@@ -41,6 +41,8 @@ SIGNATURES = {
     "lci_hyena_post_bwd": [_I, _P, _P, _P, _P, _P, _I, _I, _I, _P],
     "lci_hyena_pre_bwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "lci_dwconv_silu_fwd": [_I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    "lci_conv3_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
+    "lci_conv3_wgrad": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "lci_dwconv_silu_bwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
 }
 
@@ -68,6 +70,8 @@ def load(path: str = LIB_PATH):
     lib.lci_window_bias_elems.argtypes = [_P, _I]
     lib.lci_attn_fwd_ws_bytes.restype = ctypes.c_longlong
     lib.lci_attn_fwd_ws_bytes.argtypes = [_I, _I, _I]
+    lib.lci_conv3_wgrad_splits.restype = ctypes.c_longlong
+    lib.lci_conv3_wgrad_splits.argtypes = [ctypes.c_longlong]
     lib.lci_fft_size.restype = ctypes.c_longlong
     lib.lci_fft_size.argtypes = [_I]
     for name, argt in SIGNATURES.items():

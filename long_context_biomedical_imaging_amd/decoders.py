@@ -3,14 +3,88 @@
 ViTLinear / SwinLinear restate /root/reference/model/models/class_heads.py (:13-79).
 ViTUNETR restates enhance_heads.py:187-356 on top of MONAI-1.3 UNETR blocks (UnetResBlock,
 UnetrBasicBlock, UnetrPrUpBlock, UnetrUpBlock, UnetOutBlock: conv + InstanceNorm + LeakyReLU, transposed
-conv up-sampling), written here in plain PyTorch (MIOpen convolutions). These run on torch/MIOpen: the
-conv decoders are outside the mixer hot path.
+conv up-sampling); SwinUNETR restates enhance_heads.py:30-184. SURVEY.md §8(f) rank 2.
+
+The convolutions keep the nn.Conv / nn.ConvTranspose parameters (names, shapes, seeded init) but not their
+MIOpen kernels, which at 128^3 spend 70-120 s in solver search per shape and then run a 96->96 3x3x3 conv
+fwd+bwd in ~390 ms (tools/conv3d_probe.py), and which refuse 256^3 inputs (32-bit size limit):
+  - 3x3(x3) stride-1 convs: the HIP implicit-GEMM kernel (csrc/conv.hip, kernels.conv3), channels-last;
+  - transposed convs with kernel == stride (the up-sampling): one GEMM (V x Cin).(Cin x Cout*k^nd) and an
+    interleaving copy, i.e. exactly the non-overlapping scatter they compute;
+  - 1x1 convs: one GEMM over channels-last voxels.
 """
 from __future__ import annotations
+
+import os
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from . import kernels
+
+# A/B switch for the 2-D heads (the headline ViTUNETR at 512^2): HIP conv3 vs torch/MIOpen
+HIP_CONV_2D = os.environ.get("LCI_HIP_CONV_2D", "1") != "0"
+
+
+class Conv3x3(nn.Conv3d):
+    """nn.Conv3d(cin, cout, 3, 1, padding=1, bias=False) computed by the HIP conv3 kernel."""
+
+    def forward(self, x):
+        return kernels.conv3(x, self.weight)
+
+
+class Conv3x3_2d(nn.Conv2d):
+    """nn.Conv2d(cin, cout, 3, 1, padding=1, bias=False) computed by the HIP conv3 kernel (D = 1)."""
+
+    def forward(self, x):
+        if not HIP_CONV_2D:
+            return super().forward(x)
+        return kernels.conv3(x, self.weight)
+
+
+def _pointwise(x, weight, bias):
+    """1x1 conv as a GEMM over channels-last voxels; result (B, Cout, *S) with channels-last strides."""
+    y = F.linear(x.movedim(1, -1), weight.reshape(weight.shape[0], weight.shape[1]), bias)
+    return y.movedim(-1, 1)
+
+
+class Conv1x1(nn.Conv3d):
+    def forward(self, x):
+        return _pointwise(x, self.weight, self.bias)
+
+
+class Conv1x1_2d(nn.Conv2d):
+    def forward(self, x):
+        return _pointwise(x, self.weight, self.bias)
+
+
+def _up_gemm(x, weight, bias, k):
+    """ConvTranspose with kernel == stride: y[.., s*k + i, ..] = sum_c x[.., s, .., c] w[c, :, i..]."""
+    nd = x.dim() - 2
+    B, Cin = x.shape[:2]
+    S = x.shape[2:]
+    Cout = weight.shape[1]
+    y = torch.matmul(x.movedim(1, -1).reshape(-1, Cin), weight.reshape(Cin, -1))      # (V, Cout * prod(k))
+    y = y.view(B, *S, Cout, *k)
+    if nd == 3:
+        y = y.permute(0, 1, 5, 2, 6, 3, 7, 4)
+    else:
+        y = y.permute(0, 1, 4, 2, 5, 3)
+    y = y.reshape(B, *(s * kk for s, kk in zip(S, k)), Cout)
+    if bias is not None:
+        y = y + bias
+    return y.movedim(-1, 1)
+
+
+class ConvUp(nn.ConvTranspose3d):
+    def forward(self, x):
+        return _up_gemm(x, self.weight, self.bias, self.kernel_size)
+
+
+class ConvUp_2d(nn.ConvTranspose2d):
+    def forward(self, x):
+        return _up_gemm(x, self.weight, self.bias, self.kernel_size)
 
 
 def _conv(nd, cin, cout, k, s, transposed=False, bias=False):
@@ -23,10 +97,20 @@ def _conv(nd, cin, cout, k, s, transposed=False, bias=False):
     else:
         pad = (k - s + 1) // 2
         opad = 2 * pad + s - k
+    kt = k if isinstance(k, tuple) else (k,) * nd
+    st = s if isinstance(s, tuple) else (s,) * nd
     if transposed:
-        cls = nn.ConvTranspose2d if nd == 2 else nn.ConvTranspose3d
+        if kt == st:
+            cls = ConvUp_2d if nd == 2 else ConvUp
+        else:
+            cls = nn.ConvTranspose2d if nd == 2 else nn.ConvTranspose3d
         return cls(cin, cout, k, s, padding=pad, output_padding=opad, bias=bias)
-    cls = nn.Conv2d if nd == 2 else nn.Conv3d
+    if all(a == 3 for a in kt) and all(b == 1 for b in st) and not bias and cout % 32 == 0:
+        cls = Conv3x3_2d if nd == 2 else Conv3x3
+    elif all(a == 1 for a in kt) and all(b == 1 for b in st):
+        cls = Conv1x1_2d if nd == 2 else Conv1x1
+    else:
+        cls = nn.Conv2d if nd == 2 else nn.Conv3d
     return cls(cin, cout, k, s, padding=pad, bias=bias)
 
 

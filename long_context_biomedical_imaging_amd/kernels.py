@@ -32,11 +32,15 @@ class KernelTimer:
         torch.cuda.synchronize()
         out = {}
         for name, e0, e1, work in cls.records:
-            d = out.setdefault(name, {"calls": 0, "total_ms": 0.0, "work_per_call": work})
+            d = out.setdefault(name, {"calls": 0, "total_ms": 0.0, "total_work": 0.0})
             d["calls"] += 1
             d["total_ms"] += e0.elapsed_time(e1)
+            d["total_work"] += work
         for d in out.values():
             d["avg_ms"] = d["total_ms"] / d["calls"]
+            # mean work per launch: with avg_ms, gives the time-weighted rate total_work / total_ms even when
+            # one name covers launches of different shapes (window attention per stage, decoder convs)
+            d["work_per_call"] = d["total_work"] / d["calls"]
         return out
 
     @classmethod
@@ -622,3 +626,124 @@ def hyena_fftconv_gate(vg, k, bias, x2):
     hd = k.shape[0]
     y = _FFTConv.apply(vg.reshape(BB * (D // hd), hd, L), k, bias).reshape(BB, D, L)
     return _HyenaPost.apply(y, x2)
+
+
+# ------------------------------------------------------------------- decoder-head 3x3(x3) convolution
+def conv3_cl(x_cl: torch.Tensor, w_packed: torch.Tensor, kd: int) -> torch.Tensor:
+    """x_cl (B, D, H, W, Cin) bf16 channels-last, w_packed (Cout, kd*9, Cin) bf16 -> (B, D, H, W, Cout) bf16."""
+    _lib.require_gpu(x_cl, w_packed)
+    B, D, H, W, Cin = x_cl.shape
+    Cout = w_packed.shape[0]
+    y = torch.empty(B, D, H, W, Cout, device=x_cl.device, dtype=torch.bfloat16)
+    KernelTimer.run("conv3", 2.0 * B * D * H * W * Cout * Cin * kd * 9, x_cl, lambda: _lib.call(
+        "lci_conv3_fwd", x_cl.data_ptr(), w_packed.data_ptr(), y.data_ptr(), B, D, H, W, Cin, Cout, kd,
+        _lib.stream_of(x_cl)))
+    return y
+
+
+def _to_cl(x: torch.Tensor, nd: int) -> torch.Tensor:
+    """(B, C, [D,] H, W) any layout/dtype -> (B, D, H, W, C) bf16 contiguous (D = 1 for 2-D): one copy at most."""
+    if nd == 2:
+        x = x.unsqueeze(2)
+    return x.permute(0, 2, 3, 4, 1).to(torch.bfloat16).contiguous()
+
+
+def _from_cl(y: torch.Tensor, nd: int) -> torch.Tensor:
+    """(B, D, H, W, C) -> (B, C, [D,] H, W) view (channels-last strides)."""
+    y = y.permute(0, 4, 1, 2, 3)
+    return y.squeeze(2) if nd == 2 else y
+
+
+def _conv3_wgrad(x_cl: torch.Tensor, dy_cl: torch.Tensor, kd: int) -> torch.Tensor:
+    """dW (Cout, Cin, [3,] 3, 3) f32 = sum_p x[p + off(tap)] (x) dy[p], as kd*9 GEMMs over flat-shifted rows.
+
+    Both volumes are zero-padded by one voxel per convolved axis and flattened to rows; for tap offset o the
+    rows p in [s, Np - s) of dy_pad pair with rows p + o of x_pad (border rows of dy_pad are zero, so rows whose
+    neighbour wraps into another line / sample contribute nothing). Each tap is one (Cin x n) . (n x Cout)
+    GEMM with f32 output (hipBLASLt, bf16 inputs, f32 accumulation).
+    """
+    B, D, H, W, Cin = x_cl.shape
+    Cout = dy_cl.shape[-1]
+    pz = 1 if kd == 3 else 0
+    xp = torch.nn.functional.pad(x_cl, (0, 0, 1, 1, 1, 1, pz, pz))
+    dp = torch.nn.functional.pad(dy_cl, (0, 0, 1, 1, 1, 1, pz, pz))
+    Pd, Ph, Pw = D + 2 * pz, H + 2, W + 2
+    X = xp.view(-1, Cin)
+    Y = dp.view(-1, Cout)
+    s = pz * Ph * Pw + Pw + 1
+    n = X.shape[0] - 2 * s
+    G = torch.empty(kd * 9, Cin, Cout, device=x_cl.device, dtype=torch.float32)
+    Ys = Y[s:s + n]
+    t = 0
+    for a in range(kd):
+        for b in range(3):
+            for c in range(3):
+                o = ((a - 1) if kd == 3 else 0) * Ph * Pw + (b - 1) * Pw + (c - 1)
+                if X.is_cuda:
+                    G[t] = torch.mm(X[s + o:s + o + n].t(), Ys, out_dtype=torch.float32)
+                else:   # host check of the row-shift algebra (tests); the HIP conv itself has no CPU path
+                    G[t] = X[s + o:s + o + n].t().float() @ Ys.float()
+                t += 1
+    dw = G.permute(2, 1, 0)                                       # (Cout, Cin, taps)
+    return dw.reshape(Cout, Cin, *((3, 3, 3) if kd == 3 else (3, 3)))
+
+
+def conv3_wgrad_cl(x_cl: torch.Tensor, dy_cl: torch.Tensor, kd: int) -> torch.Tensor:
+    """dW (Cout, Cin, [3,] 3, 3) f32 by the HIP split-voxel kernel (per-split partials summed here).
+    Cin is zero-padded to a multiple of 32 (the 1-channel image of encoder1) and sliced off again."""
+    _lib.require_gpu(x_cl, dy_cl)
+    B, D, H, W, Cin = x_cl.shape
+    Cout = dy_cl.shape[-1]
+    cp = -(-Cin // 32) * 32
+    xp = x_cl if cp == Cin else torch.nn.functional.pad(x_cl, (0, cp - Cin))
+    lib = _lib.load()
+    ns = lib.lci_conv3_wgrad_splits(B * D * H * W)
+    part = torch.empty(ns * 4, kd * 9, Cout, cp, device=x_cl.device, dtype=torch.float32)
+    KernelTimer.run("conv3_wgrad", 2.0 * B * D * H * W * Cout * Cin * kd * 9, x_cl, lambda: _lib.call(
+        "lci_conv3_wgrad", xp.data_ptr(), dy_cl.data_ptr(), part.data_ptr(), B, D, H, W, cp, Cout, kd,
+        _lib.stream_of(x_cl)))
+    g = part.sum(0)[..., :Cin]                                    # (taps, Cout, Cin)
+    return g.permute(1, 2, 0).reshape(Cout, Cin, *((3, 3, 3) if kd == 3 else (3, 3)))
+
+
+class _Conv3(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, nd):
+        kd = 3 if nd == 3 else 1
+        Cout, Cin = weight.shape[:2]
+        x_cl = _to_cl(x, nd)
+        wp = weight.to(torch.bfloat16).permute(0, *range(2, 2 + nd), 1).reshape(Cout, kd * 9, Cin).contiguous()
+        y = conv3_cl(x_cl, wp, kd)
+        ctx.save_for_backward(x_cl, weight)
+        ctx.nd = nd
+        return _from_cl(y, nd)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x_cl, weight = ctx.saved_tensors
+        nd = ctx.nd
+        kd = 3 if nd == 3 else 1
+        Cout, Cin = weight.shape[:2]
+        dy_cl = _to_cl(dy, nd)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            sp = tuple(range(2, 2 + nd))
+            wd = weight.to(torch.bfloat16).flip(sp).permute(1, *sp, 0).reshape(Cin, kd * 9, Cout)
+            cp = -(-Cin // 32) * 32                      # the kernel's Cout multiple: zero rows, sliced off
+            if cp != Cin:
+                wd = torch.cat([wd, wd.new_zeros(cp - Cin, kd * 9, Cout)])
+            dx = conv3_cl(dy_cl, wd.contiguous(), kd)
+            dx = _from_cl(dx if cp == Cin else dx[..., :Cin], nd)
+        if ctx.needs_input_grad[1]:
+            dw = conv3_wgrad_cl(x_cl, dy_cl, kd).to(weight.dtype)
+        return dx, dw, None
+
+
+def conv3(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """Conv{2,3}d(kernel 3, stride 1, padding 1, no bias) in bf16 MFMA with f32 accumulation (the dtype
+    autocast gives the reference's conv). x (B, Cin, [D,] H, W) -> (B, Cout, [D,] H, W) bf16, channels-last
+    strides. Needs Cout % 32 == 0."""
+    _lib.require_gpu(weight)
+    if not x.is_cuda:
+        raise _lib.LciError("conv3 runs on the GPU only; there is no CPU path")
+    return _Conv3.apply(x, weight, weight.dim() - 2)

@@ -1,0 +1,53 @@
+"""GPU parity of the decoder-head 3x3(x3) convolution (csrc/conv.hip) against torch's fp32 convolution on the
+same bf16-rounded operands (MONAI-1.3 get_conv_layer(kernel 3, stride 1, bias=False) = Conv(padding=1)).
+
+Tolerance: rel-L2 <= 1e-2 on y and dx (bf16 output rounding), <= 1e-2 on dW (f32 output of bf16 GEMMs).
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from golden_util import rel_err
+from long_context_biomedical_imaging_amd import kernels
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("B,S,Cin,Cout", [
+    (2, (9, 10, 11), 32, 32),      # ragged volume, NT=1
+    (1, (16, 16, 16), 96, 96),     # Swin-tiny stage-1 channels, NT=3
+    (1, (7, 12, 5), 192, 96),      # UnetrUpBlock conv1 (2C -> C)
+    (2, (6, 6, 6), 64, 128),       # NT=4
+    (1, (8, 9, 10), 1, 96),        # encoder1 on the image: generic (Cin % 16 != 0) path
+    (2, (1, 33, 47), 64, 32),      # 2-D (D = 1, 9 taps)
+    (1, (1, 20, 24), 3, 64),       # 2-D generic
+])
+def test_conv3_parity(B, S, Cin, Cout):
+    torch.manual_seed(0)
+    nd = 2 if S[0] == 1 else 3
+    shp = S[1:] if nd == 2 else S
+    x = torch.randn(B, Cin, *shp).bfloat16().float()
+    w = (torch.randn(Cout, Cin, *(3,) * nd) / (Cin * 27) ** 0.5).bfloat16().float()
+    dy = torch.randn(B, Cout, *shp).bfloat16().float()
+    conv = F.conv3d if nd == 3 else F.conv2d
+    xr, wr = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    yr = conv(xr, wr, padding=1)
+    yr.backward(dy)
+    xc = x.cuda().requires_grad_(True)
+    wc = w.cuda().requires_grad_(True)
+    y = kernels.conv3(xc, wc)
+    assert y.shape == yr.shape and y.dtype == torch.bfloat16
+    assert rel_err(y.float(), yr) < 1e-2
+    y.backward(dy.cuda().bfloat16())
+    assert rel_err(xc.grad.float(), xr.grad) < 1e-2
+    assert rel_err(wc.grad, wr.grad) < 1e-2
+
+
+def test_conv3_large_vs_miopen():
+    """Swin-tiny decoder1 shape at 64^3 (96 -> 96): against torch's (MIOpen) bf16 conv on the GPU."""
+    torch.manual_seed(1)
+    x = torch.randn(1, 96, 64, 64, 64, device="cuda").bfloat16()
+    w = (torch.randn(96, 96, 3, 3, 3, device="cuda") / (96 * 27) ** 0.5)
+    y = kernels.conv3(x, w)
+    yr = F.conv3d(x.float(), w.bfloat16().float(), padding=1)
+    assert rel_err(y.float(), yr) < 1e-2

@@ -10,10 +10,16 @@ import time
 import torch
 import torch.nn as nn
 
+import os
+import sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from long_context_biomedical_imaging_amd import decoders  # noqa: E402
+
 ap = argparse.ArgumentParser()
 ap.add_argument("--layout", default="ncdhw", choices=["ncdhw", "ndhwc"])
 ap.add_argument("--size", type=int, default=128)
 ap.add_argument("--only", default="")
+ap.add_argument("--hip", action="store_true", help="the repo's decoder convs (HIP conv3 / GEMM forms)")
 args = ap.parse_args()
 S = args.size
 dev = torch.device("cuda")
@@ -36,7 +42,14 @@ print(f"layout={args.layout} S={S}", flush=True)
 for name, ctor, shape in cases:
     if args.only and args.only not in name:
         continue
-    m = ctor().to(dev).to(memory_format=mf)
+    m = ctor()
+    if args.hip and isinstance(m, (nn.Conv3d, nn.ConvTranspose3d)):
+        k, st = m.kernel_size, m.stride
+        hm = decoders._conv(3, m.in_channels, m.out_channels, k, st,
+                            transposed=isinstance(m, nn.ConvTranspose3d), bias=m.bias is not None)
+        hm.load_state_dict(m.state_dict())
+        m = hm
+    m = m.to(dev).to(memory_format=mf)
     x = torch.randn(shape, device=dev).to(memory_format=mf).requires_grad_(True)
     times = []
     for it in range(3):
