@@ -10,7 +10,9 @@ backward (DDP gradient all-reduce over RCCL), Adam step — on synthetic U[0,1) 
 Throughput = (world * B * L) tokens / step time (max over ranks).
 
 Also reported (rank 0): `roofline` of the dominant liblci kernel (HIP events over the timed region),
-per-kernel breakdown, and `cpu_baseline` = the CPU oracle's forward on a bounded sample (N = 1 only).
+per-kernel breakdown, `cpu_baseline` = the CPU oracle's forward on a bounded sample (N = 1 only), and
+`secondary.swin_p2_128` = the same harness on BASELINE configs[2] (Swin-tiny + SwinUNETR, 128^3 patch 2, one
+volume per GPU), which north_star also names. `--workload` runs one of the other configs on its own.
 """
 from __future__ import annotations
 
@@ -131,43 +133,31 @@ def profiled_traffic(kernel: str):
     return None
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=None, help="images per GPU (default 2; 1 for the 3-D configs)")
-    ap.add_argument("--workload", default="vit_p2_512", choices=sorted(WORKLOADS))
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=20.0)
-    args = ap.parse_args()
-
-    if args.batch is None:
-        args.batch = 2 if args.workload in ("vit_p2_512", "vit_hyena_p2_512") else 1
-    if args.workload in ("swin_p2_128", "vit_mamba_p2_256"):
-        # the 3-D decoders' MIOpen convolutions: heuristic solver choice instead of a minutes-long exhaustive find
+def run_workload(workload, batch, steps, warmup, rank, world, device):
+    """Build the workload's model, run `warmup` untimed and `steps` timed training steps (barrier + sync on both
+    sides, max over ranks). Returns the bench dict on rank 0 (None elsewhere); frees the model."""
+    if workload in ("swin_p2_128", "vit_mamba_p2_256"):
+        # any 3-D conv left on MIOpen (none in these heads today): heuristic solver instead of a minutes-long find
         os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
-    rank, local, world = init_distributed()
-    device = torch.device("cuda", local)
-    torch.cuda.set_device(device)
-    cfg = lconfig.parse_config(WORKLOADS[args.workload] + ["--batch_size", str(args.batch)])
+    cfg = lconfig.parse_config(WORKLOADS[workload] + ["--batch_size", str(batch)])
     torch.manual_seed(0)
     model = EncoderDecoderModel(cfg, cfg.encoder_name, cfg.decoder_name, cfg.no_in_channel,
                                 cfg.no_out_channel).to(device)
-    ckpt = args.workload == "vit_mamba_p2_256"
+    ckpt = workload == "vit_mamba_p2_256"
     if ckpt:
         model.encoder.checkpoint_blocks = True   # ~35 GB of saved activations per block at 2^21 tokens
     trainer = TrainStep(model, cfg, device, ddp=world > 1)
-    x, y = synthetic_batch(cfg, args.batch, device, seed=1234 + rank)
+    x, y = synthetic_batch(cfg, batch, device, seed=1234 + rank)
     L = (model.encoder.patch_embedding.n_patches if hasattr(model.encoder, "patch_embedding")
          else cfg.time * cfg.height * cfg.width // 8)
 
-    for i in range(args.warmup):
+    for i in range(warmup):
         tw = time.perf_counter()
         trainer.step(x, y)
         torch.cuda.synchronize()
         if rank == 0:
-            print(f"[bench] warmup step {i}: {time.perf_counter() - tw:.2f} s", file=sys.stderr, flush=True)
+            print(f"[bench] {workload} warmup step {i}: {time.perf_counter() - tw:.2f} s", file=sys.stderr,
+                  flush=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -175,7 +165,7 @@ def main():
     kernels.KernelTimer.reset()
     kernels.KernelTimer.enabled = True
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         loss = trainer.step(x, y)
     torch.cuda.synchronize()
     if world > 1:
@@ -184,47 +174,83 @@ def main():
     elapsed = time.perf_counter() - t0
     kernels.KernelTimer.enabled = False
     ksum = kernels.KernelTimer.summary()
+    kernels.KernelTimer.reset()
     t = torch.tensor([elapsed], device=device, dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = t.item()
     loss_v = float(loss.item())
+    del trainer, model, x, y, loss
+    torch.cuda.empty_cache()
+    if rank != 0:
+        return None
 
+    ms = 1000.0 * elapsed / steps
+    tokens = world * batch * L * steps
+    kern = {}
+    for name, d in ksum.items():
+        kern[name] = {"calls_per_step": d["calls"] / steps, "avg_ms": round(d["avg_ms"], 3),
+                      "ms_per_step": round(d["total_ms"] / steps, 2)}
+        if d["work_per_call"]:
+            b, pu = ROOF.get(name, ("mfma", 1.0))
+            rate = d["work_per_call"] * pu / (d["avg_ms"] * 1e-3)
+            kern[name]["tflops" if b == "mfma" else "gbs"] = round(rate / (1e12 if b == "mfma" else 1e9), 1)
+    dom = max((n for n in ksum if ksum[n]["work_per_call"]), key=lambda n: ksum[n]["total_ms"])
+    dd = ksum[dom]
+    bound, per_unit = ROOF.get(dom, ("mfma", 1.0))
+    work = dd["work_per_call"] * per_unit
+    if bound == "mfma":
+        ach, peak, unit = work / (dd["avg_ms"] * 1e-3) / 1e12, MFMA_BF16_PEAK_TFLOPS, "TFLOP/s"
+    else:
+        ach, peak, unit = work / (dd["avg_ms"] * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s"
+    return {
+        "metric": WORKLOAD_NAMES[workload][0],
+        "value": round(tokens / elapsed, 1), "unit": "image-tokens/s", "n_gpus": world, "steps": steps,
+        "warmup": warmup, "ms_per_step": round(ms, 2), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16", "data": "synthetic U[0,1) images, random-init weights",
+        "config": {"workload": WORKLOAD_NAMES[workload][1],
+                   "global_batch": world * batch, "seq_len": L, "parallelism": f"ddp{world}",
+                   "per_gpu_batch": batch, "optimizer": cfg.optim_type, "loss": cfg.loss_func,
+                   "activation_checkpointing": "per encoder block" if ckpt else "none"},
+        "roofline": {"kernel": dom, "bound": bound, "achieved": round(ach, 1), "peak": peak,
+                     "unit": unit, "frac": round(ach / peak, 4),
+                     "traffic": profiled_traffic(dom), "traffic_source": "profiles/traffic.json",
+                     "work_per_launch": work, "avg_launch_ms": round(dd["avg_ms"], 3)},
+        "kernels": kern,
+        "loss": round(loss_v, 5),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=None, help="images per GPU (default 2; 1 for the 3-D configs)")
+    ap.add_argument("--workload", default="vit_p2_512", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the Swin 128^3 line that the default (ViT 512^2) run also reports")
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    args = ap.parse_args()
+
+    if args.batch is None:
+        args.batch = 2 if args.workload in ("vit_p2_512", "vit_hyena_p2_512") else 1
+    rank, local, world = init_distributed()
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    res = run_workload(args.workload, args.batch, args.steps, args.warmup, rank, world, device)
+    if args.workload == "vit_p2_512" and not args.no_secondary:
+        # north_star also asks for tokens/s on 128^3 patch-2 volumes (BASELINE configs[2], Swin + SwinUNETR):
+        # same DDP harness, 1 volume per GPU, same steps (at most 10), reported under "secondary"
+        try:
+            sec = run_workload("swin_p2_128", 1, min(args.steps, 10), 2, rank, world, device)
+        except Exception as e:   # never lose the headline line to the secondary workload
+            sec = {"error": f"{type(e).__name__}: {e}"}
+        if rank == 0:
+            keep = ("metric", "value", "unit", "ms_per_step", "steps", "warmup", "config", "roofline", "kernels")
+            res["secondary"] = {"swin_p2_128": {k: sec[k] for k in keep if k in sec} if "error" not in sec else sec}
     if rank == 0:
-        ms = 1000.0 * elapsed / args.steps
-        tokens = world * args.batch * L * args.steps
-        kern = {}
-        for name, d in ksum.items():
-            kern[name] = {"calls_per_step": d["calls"] / args.steps, "avg_ms": round(d["avg_ms"], 3),
-                          "ms_per_step": round(d["total_ms"] / args.steps, 2)}
-            if d["work_per_call"]:
-                b, pu = ROOF.get(name, ("mfma", 1.0))
-                rate = d["work_per_call"] * pu / (d["avg_ms"] * 1e-3)
-                kern[name]["tflops" if b == "mfma" else "gbs"] = round(rate / (1e12 if b == "mfma" else 1e9), 1)
-        dom = max((n for n in ksum if ksum[n]["work_per_call"]), key=lambda n: ksum[n]["total_ms"])
-        dd = ksum[dom]
-        bound, per_unit = ROOF.get(dom, ("mfma", 1.0))
-        work = dd["work_per_call"] * per_unit
-        if bound == "mfma":
-            ach, peak, unit = work / (dd["avg_ms"] * 1e-3) / 1e12, MFMA_BF16_PEAK_TFLOPS, "TFLOP/s"
-        else:
-            ach, peak, unit = work / (dd["avg_ms"] * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s"
-        res = {
-            "metric": WORKLOAD_NAMES[args.workload][0],
-            "value": round(tokens / elapsed, 1), "unit": "image-tokens/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms, 2), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "bf16", "data": "synthetic U[0,1) images, random-init weights",
-            "config": {"workload": WORKLOAD_NAMES[args.workload][1],
-                       "global_batch": world * args.batch, "seq_len": L, "parallelism": f"ddp{world}",
-                       "per_gpu_batch": args.batch, "optimizer": cfg.optim_type, "loss": cfg.loss_func,
-                       "activation_checkpointing": "per encoder block" if ckpt else "none"},
-            "roofline": {"kernel": dom, "bound": bound, "achieved": round(ach, 1), "peak": peak,
-                         "unit": unit, "frac": round(ach / peak, 4),
-                         "traffic": profiled_traffic(dom), "traffic_source": "profiles/traffic.json",
-                         "work_per_launch": work, "avg_launch_ms": round(dd["avg_ms"], 3)},
-            "kernels": kern,
-            "loss": round(loss_v, 5),
-        }
         if world == 1 and not args.no_cpu_baseline and args.workload == "vit_p2_512":
             res["cpu_baseline"] = cpu_baseline(args.cpu_budget)
         print(json.dumps(res), flush=True)

@@ -82,10 +82,10 @@ long long lci_window_dS_elems(const int* geo);
  * w'[c, t, n] = w[n, c, KD*9-1-t]. */
 int lci_conv3_fwd(const void* x, const void* w, void* y, int B, int D, int H, int W, int Cin, int Cout, int KD,
                   void* stream);
-/* Weight gradient: part (lci_conv3_wgrad_splits(B*D*H*W) * 4, KD*9, Cout, Cin) f32 <- per-(voxel split, wave)
+/* Weight gradient: part (lci_conv3_wgrad_splits(B*D*H*W, Cin, Cout, KD) * 4, KD*9, Cout, Cin) f32 <- per-(voxel split, wave)
  * partial sums of dy[p, n] * x[p + off(tap), c]; dW[n, c, tap] = sum over the first axis (caller). x (.., Cin),
  * dy (.., Cout) bf16 channels-last; Cin, Cout multiples of 32. Deterministic (no atomics). */
-long long lci_conv3_wgrad_splits(long long V);
+long long lci_conv3_wgrad_splits(long long V, int Cin, int Cout, int KD);
 int lci_conv3_wgrad(const void* x, const void* dy, float* part, int B, int D, int H, int W, int Cin, int Cout,
                     int KD, void* stream);
 

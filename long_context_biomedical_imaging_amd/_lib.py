@@ -71,7 +71,7 @@ def load(path: str = LIB_PATH):
     lib.lci_attn_fwd_ws_bytes.restype = ctypes.c_longlong
     lib.lci_attn_fwd_ws_bytes.argtypes = [_I, _I, _I]
     lib.lci_conv3_wgrad_splits.restype = ctypes.c_longlong
-    lib.lci_conv3_wgrad_splits.argtypes = [ctypes.c_longlong]
+    lib.lci_conv3_wgrad_splits.argtypes = [ctypes.c_longlong, _I, _I, _I]
     lib.lci_fft_size.restype = ctypes.c_longlong
     lib.lci_fft_size.argtypes = [_I]
     for name, argt in SIGNATURES.items():

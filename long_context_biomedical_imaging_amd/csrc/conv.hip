@@ -32,21 +32,21 @@ __device__ __forceinline__ bf16x8 zero8() {
   return z;
 }
 
-// Vector path: Cin % 16 == 0. NT = 32-channel output blocks per wave.
-template <int NT>
+// Vector path: Cin % 16 == 0. NT = 32-channel output blocks per wave, MV = 32-voxel blocks per wave.
+template <int NT, int MV>
 __global__ __launch_bounds__(256) void conv3_fwd_kernel(ConvArgs a) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 31, h = lane >> 5;
-  const long long v0 = ((long long)blockIdx.x * 4 + wave) * 64;
+  const long long v0 = ((long long)blockIdx.x * 4 + wave) * 32 * MV;
   const int n0 = blockIdx.y * 32 * NT;
   const int T = a.KD * 9;
   const int HW = a.H * a.W;
-  // voxel coordinates of this lane's two B-operand columns (voxels v0 + r, v0 + 32 + r)
-  int zc[2], yc[2], xc[2];
-  long long vb[2];
-  bool inb[2];
+  // voxel coordinates of this lane's B-operand columns (voxels v0 + 32m + r)
+  int zc[MV], yc[MV], xc[MV];
+  long long vb[MV];
+  bool inb[MV];
 #pragma unroll
-  for (int m = 0; m < 2; ++m) {
+  for (int m = 0; m < MV; ++m) {
     const long long v = v0 + 32 * m + r;
     inb[m] = v < a.V;
     const long long vv = inb[m] ? v : 0;
@@ -56,9 +56,9 @@ __global__ __launch_bounds__(256) void conv3_fwd_kernel(ConvArgs a) {
     yc[m] = rem / a.W; xc[m] = rem - yc[m] * a.W;
     vb[m] = vv;
   }
-  f32x16 acc[2][NT];
+  f32x16 acc[MV][NT];
 #pragma unroll
-  for (int m = 0; m < 2; ++m)
+  for (int m = 0; m < MV; ++m)
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -70,10 +70,10 @@ __global__ __launch_bounds__(256) void conv3_fwd_kernel(ConvArgs a) {
 
   for (int tap = 0; tap < T; ++tap) {
     const int dz = (a.KD == 3 ? tap / 9 : 1) - 1, dy = (tap / 3) % 3 - 1, dx = tap % 3 - 1;
-    const bf16* px[2];
-    bool ok[2];
+    const bf16* px[MV];
+    bool ok[MV];
 #pragma unroll
-    for (int m = 0; m < 2; ++m) {
+    for (int m = 0; m < MV; ++m) {
       const int z = zc[m] + dz, y = yc[m] + dy, xx = xc[m] + dx;
       ok[m] = inb[m] && (unsigned)z < (unsigned)a.D && (unsigned)y < (unsigned)a.H && (unsigned)xx < (unsigned)a.W;
       const long long nb = vb[m] + (long long)dz * HW + dy * a.W + dx;
@@ -82,9 +82,9 @@ __global__ __launch_bounds__(256) void conv3_fwd_kernel(ConvArgs a) {
     const long long wt = (long long)tap * a.Cin;
 #pragma unroll 2
     for (int c = 0; c < a.Cin; c += 16) {
-      bf16x8 xb[2], wa[NT];
+      bf16x8 xb[MV], wa[NT];
 #pragma unroll
-      for (int m = 0; m < 2; ++m) {
+      for (int m = 0; m < MV; ++m) {
         xb[m] = *(const bf16x8*)(px[m] + c);
         if (!ok[m]) xb[m] = zero8();
       }
@@ -93,12 +93,12 @@ __global__ __launch_bounds__(256) void conv3_fwd_kernel(ConvArgs a) {
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int m = 0; m < 2; ++m) acc[m][t] = mfma32(wa[t], xb[m], acc[m][t]);
+        for (int m = 0; m < MV; ++m) acc[m][t] = mfma32(wa[t], xb[m], acc[m][t]);
     }
   }
   // acc[m][t] reg i: output channel n0 + 32t + (i&3) + 8(i>>2) + 4h, voxel v0 + 32m + r
 #pragma unroll
-  for (int m = 0; m < 2; ++m) {
+  for (int m = 0; m < MV; ++m) {
     if (!inb[m]) continue;
     bf16* yp = a.y + vb[m] * a.Cout + n0 + 4 * h;
 #pragma unroll
@@ -295,12 +295,14 @@ static int tile3(int c) { return (c / 32) % 3 == 0 ? 3 : ((c / 32) % 2 == 0 ? 2 
 
 template <int NT>
 static int launch(const ConvArgs& a, hipStream_t st) {
-  const long long nblk = (a.V + 255) / 256;
-  dim3 grid((unsigned)nblk, a.Cout / (32 * NT));
-  if (a.Cin % 16 == 0)
-    hipLaunchKernelGGL(conv3_fwd_kernel<NT>, grid, dim3(256), 0, st, a);
-  else
+  constexpr int MV = NT <= 2 ? 4 : 2;   // narrow outputs: more voxels per wave to reuse the weight fragments
+  if (a.Cin % 16 == 0) {
+    dim3 grid((unsigned)((a.V + 128 * MV - 1) / (128 * MV)), a.Cout / (32 * NT));
+    hipLaunchKernelGGL((conv3_fwd_kernel<NT, MV>), grid, dim3(256), 0, st, a);
+  } else {
+    dim3 grid((unsigned)((a.V + 255) / 256), a.Cout / (32 * NT));
     hipLaunchKernelGGL(conv3_fwd_generic_kernel<NT>, grid, dim3(256), 0, st, a);
+  }
   LCI_LAUNCH_CHECK();
   return 0;
 }
@@ -329,7 +331,14 @@ extern "C" int lci_conv3_fwd(const void* x, const void* w, void* y, int B, int D
   return launch<1>(a, st);
 }
 
-extern "C" long long lci_conv3_wgrad_splits(long long V) { return (V + 32767) / 32768; }
+// Voxel splits: up to 32768 voxels per workgroup, fewer (>= 1024) when that leaves under ~2048 workgroups
+// (small 2-D volumes, few channel tiles), so the grid still fills the 256 CUs.
+extern "C" long long lci_conv3_wgrad_splits(long long V, int Cin, int Cout, int KD) {
+  const long long tiles = (long long)KD * 9 * (Cout / (32 * tile3(Cout))) * (Cin / (32 * tile3(Cin)));
+  long long lv = 32768;
+  while (lv > 1024 && ((V + lv - 1) / lv) * tiles < 2048) lv >>= 1;
+  return (V + lv - 1) / lv;
+}
 
 extern "C" int lci_conv3_wgrad(const void* x, const void* dy, float* part, int B, int D, int H, int W, int Cin,
                                int Cout, int KD, void* stream) {
@@ -342,9 +351,9 @@ extern "C" int lci_conv3_wgrad(const void* x, const void* dy, float* part, int B
   WgradArgs a;
   a.x = (const bf16*)x; a.dy = (const bf16*)dy; a.part = part;
   a.V = (long long)B * D * H * W;
-  a.Lv = 32768;
   a.D = D; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.KD = KD;
-  const long long ns = lci_conv3_wgrad_splits(a.V);
+  const long long ns = lci_conv3_wgrad_splits(a.V, Cin, Cout, KD);
+  a.Lv = (a.V + ns - 1) / ns;
   LCI_CHECK(ns < 65536, "conv3_wgrad: volume too large");
   hipStream_t st = (hipStream_t)stream;
   const int mt = tile3(Cout), nt = tile3(Cin);

@@ -432,15 +432,26 @@ __global__ __launch_bounds__(256) void win_attn_bwd_kernel(WinArgs a) {
           *(bf16x4*)(base + a.C + 8 * g + 4 * half) = v0;
           *(bf16x4*)(base + 2 * a.C + 8 * g + 4 * half) = v1;
         }
-      } else if (a.dbias_pad) {   // padded voxel: its k, v are the qkv bias
+      }
+    }
+    // padded voxels: their k, v are the qkv bias. All padded keys of the wave target the same 2 x 32 words,
+    // so sum over the 32 key lanes of each half first (one atomic per word per wave instead of one per key:
+    // per-key atomics serialised on 192 addresses cost ~37 ms at Swin-tiny stage 1, 128^3)
+    const bool padk = kv && krow < 0 && a.dbias_pad != nullptr;
+    if (__any(padk)) {
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
+      for (int i = 0; i < 16; ++i) {
+        float sk = padk ? dk[i] * a.scale : 0.f, sv = padk ? dv[i] : 0.f;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int d = 8 * g + 4 * half + j;
-            atomicAdd(a.dbias_pad + a.C + hh * WHD + d, dk[4 * g + j] * a.scale);
-            atomicAdd(a.dbias_pad + 2 * a.C + hh * WHD + d, dv[4 * g + j]);
-          }
+        for (int o = 16; o >= 1; o >>= 1) {
+          sk += __shfl_xor(sk, o);
+          sv += __shfl_xor(sv, o);
+        }
+        if ((lane & 31) == 0) {
+          const int d = 8 * (i >> 2) + 4 * half + (i & 3);
+          atomicAdd(a.dbias_pad + a.C + hh * WHD + d, sk);
+          atomicAdd(a.dbias_pad + 2 * a.C + hh * WHD + d, sv);
+        }
       }
     }
   }
