@@ -15,6 +15,10 @@
 // Neighbour reuse (27 taps read the same voxels) is served by L1/L2: the volume is swept in voxel order.
 #include "common.hpp"
 
+#ifndef LCI_CONV_MV_WIDE
+#define LCI_CONV_MV_WIDE 4   // 32-voxel blocks per wave for NT >= 3 (A/B: tools/conv_variants.sh)
+#endif
+
 namespace lci {
 
 struct ConvArgs {
@@ -192,7 +196,10 @@ __global__ __launch_bounds__(256) void conv3_fwd_generic_kernel(ConvArgs a) {
 // ds_read_b64_tr_b16. Grid x = tap (fastest: the 27 workgroups of one voxel range share it in L2),
 // y = voxel split, z = (n tile, c tile). Plain stores of per-wave partials (no atomics, deterministic); the
 // caller sums them.
-constexpr int WG_ROWS = 128, WG_LD = 96;
+constexpr int WG_ROWS = 128;
+// LDS row stride (elements) of a 32*M-channel tile: 64 / 160 / 192-B rows keep the four rows of a transposed
+// read in disjoint bank windows (a 128-B stride would pair them up)
+__host__ __device__ constexpr int wg_ld(int M) { return M == 1 ? 32 : (M == 2 ? 80 : 96); }
 
 struct WgradArgs {
   const bf16* x;    // (B, D, H, W, Cin)
@@ -204,8 +211,10 @@ struct WgradArgs {
 
 template <int MT, int NT>
 __global__ __launch_bounds__(256) void conv3_wgrad_kernel(WgradArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16 sdy[WG_ROWS * WG_LD];
-  __shared__ __attribute__((aligned(16))) bf16 sx[WG_ROWS * WG_LD];
+  // two LDS buffers: tile j+1 is loaded into registers during tile j's MFMAs and stored to the other buffer
+  constexpr int LDY = wg_ld(MT), LDX = wg_ld(NT);
+  __shared__ __attribute__((aligned(16))) bf16 sdy[2][WG_ROWS * LDY];
+  __shared__ __attribute__((aligned(16))) bf16 sx[2][WG_ROWS * LDX];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
   const int tap = blockIdx.x, split = blockIdx.y;
   const int nct = a.Cin / (32 * NT);
@@ -225,22 +234,20 @@ __global__ __launch_bounds__(256) void conv3_wgrad_kernel(WgradArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[m][n][i] = 0.f;
 
-  for (long long v0 = vs; v0 < ve; v0 += WG_ROWS) {
-    // dy tile: 128 rows x 4*MT 16-B chunks
+  u32x4 rdy[2 * MT], rx[2 * NT];
+  auto load = [&](long long v0) {
 #pragma unroll
-    for (int i = 0; i < 2 * MT; ++i) {
+    for (int i = 0; i < 2 * MT; ++i) {   // dy tile: 128 rows x 4*MT 16-B chunks
       const int c = tid + 256 * i, row = c / (4 * MT), ch = c % (4 * MT);
       const long long v = v0 + row;
-      u32x4 val = {0u, 0u, 0u, 0u};
-      if (v < ve) val = *(const u32x4*)(a.dy + v * a.Cout + n0 + 8 * ch);
-      *(u32x4*)(sdy + row * WG_LD + 8 * ch) = val;
+      rdy[i] = u32x4{0u, 0u, 0u, 0u};
+      if (v < ve) rdy[i] = *(const u32x4*)(a.dy + v * a.Cout + n0 + 8 * ch);
     }
-    // shifted x tile: row p holds x[p + off] (zero outside the volume)
 #pragma unroll
-    for (int i = 0; i < 2 * NT; ++i) {
+    for (int i = 0; i < 2 * NT; ++i) {   // shifted x tile: row p holds x[p + off] (zero outside the volume)
       const int c = tid + 256 * i, row = c / (4 * NT), ch = c % (4 * NT);
       const long long v = v0 + row;
-      u32x4 val = {0u, 0u, 0u, 0u};
+      rx[i] = u32x4{0u, 0u, 0u, 0u};
       if (v < ve) {
         int rem = (int)(v % DHW);
         const int z = rem / HW;
@@ -248,26 +255,49 @@ __global__ __launch_bounds__(256) void conv3_wgrad_kernel(WgradArgs a) {
         const int y = rem / a.W, xx = rem - y * a.W;
         if ((unsigned)(z + dz) < (unsigned)a.D && (unsigned)(y + dyy) < (unsigned)a.H &&
             (unsigned)(xx + dx) < (unsigned)a.W)
-          val = *(const u32x4*)(a.x + (v + off) * a.Cin + c0 + 8 * ch);
+          rx[i] = *(const u32x4*)(a.x + (v + off) * a.Cin + c0 + 8 * ch);
       }
-      *(u32x4*)(sx + row * WG_LD + 8 * ch) = val;
     }
-    __syncthreads();
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2 * MT; ++i) {
+      const int c = tid + 256 * i, row = c / (4 * MT), ch = c % (4 * MT);
+      *(u32x4*)(&sdy[buf][row * LDY + 8 * ch]) = rdy[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 2 * NT; ++i) {
+      const int c = tid + 256 * i, row = c / (4 * NT), ch = c % (4 * NT);
+      *(u32x4*)(&sx[buf][row * LDX + 8 * ch]) = rx[i];
+    }
+  };
+
+  load(vs);
+  store(0);
+  __syncthreads();
+  int buf = 0;
+  for (long long v0 = vs; v0 < ve; v0 += WG_ROWS) {
+    const bool more = v0 + WG_ROWS < ve;
+    if (more) load(v0 + WG_ROWS);
+    const bf16* tdy = sdy[buf];
+    const bf16* tx = sx[buf];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       bf16x8 fa[MT], fb[NT];
 #pragma unroll
       for (int m = 0; m < MT; ++m)
-        fa[m] = s ? frag_tr<1>(sdy, WG_LD, 32 * wave, 32 * m, lane) : frag_tr<0>(sdy, WG_LD, 32 * wave, 32 * m, lane);
+        fa[m] = s ? frag_tr<1>(tdy, LDY, 32 * wave, 32 * m, lane) : frag_tr<0>(tdy, LDY, 32 * wave, 32 * m, lane);
 #pragma unroll
       for (int n = 0; n < NT; ++n)
-        fb[n] = s ? frag_tr<1>(sx, WG_LD, 32 * wave, 32 * n, lane) : frag_tr<0>(sx, WG_LD, 32 * wave, 32 * n, lane);
+        fb[n] = s ? frag_tr<1>(tx, LDX, 32 * wave, 32 * n, lane) : frag_tr<0>(tx, LDX, 32 * wave, 32 * n, lane);
 #pragma unroll
       for (int m = 0; m < MT; ++m)
 #pragma unroll
         for (int n = 0; n < NT; ++n) acc[m][n] = mfma32(fa[m], fb[n], acc[m][n]);
     }
+    if (more) store(buf ^ 1);
     __syncthreads();
+    buf ^= 1;
   }
   // acc[m][n] reg i: n-index n0 + 32m + (i&3) + 8(i>>2) + 4h, c-index c0 + 32n + (lane&31)
   const int h = lane >> 5;
@@ -295,7 +325,7 @@ static int tile3(int c) { return (c / 32) % 3 == 0 ? 3 : ((c / 32) % 2 == 0 ? 2 
 
 template <int NT>
 static int launch(const ConvArgs& a, hipStream_t st) {
-  constexpr int MV = NT <= 2 ? 4 : 2;   // narrow outputs: more voxels per wave to reuse the weight fragments
+  constexpr int MV = NT <= 2 ? 4 : LCI_CONV_MV_WIDE;   // narrow outputs: more voxels per wave
   if (a.Cin % 16 == 0) {
     dim3 grid((unsigned)((a.V + 128 * MV - 1) / (128 * MV)), a.Cout / (32 * NT));
     hipLaunchKernelGGL((conv3_fwd_kernel<NT, MV>), grid, dim3(256), 0, st, a);

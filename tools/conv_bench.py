@@ -18,6 +18,9 @@ SETS = {
     # Swin-tiny + SwinUNETR at 128^3 patch 2
     "c3": [((128, 128, 128), 96, 96), ((128, 128, 128), 192, 96), ((64, 64, 64), 96, 96), ((64, 64, 64), 192, 96),
            ((32, 32, 32), 192, 192), ((32, 32, 32), 384, 192), ((16, 16, 16), 384, 384)],
+    # A/B mix of tile widths (NT = 1..4) at 128^3
+    "mix": [((128, 128, 128), 96, 96), ((128, 128, 128), 192, 96), ((128, 128, 128), 256, 128),
+            ((128, 128, 128), 512, 256), ((128, 128, 128), 64, 64), ((128, 128, 128), 64, 32)],
     # ViT + ViTUNETR at 256^3 patch 2: the whole decoder runs at full resolution (enhance_heads.py:221-224)
     "c5": [((256, 256, 256), 512, 256), ((256, 256, 256), 256, 256), ((256, 256, 256), 256, 128),
            ((256, 256, 256), 128, 128), ((256, 256, 256), 128, 64), ((256, 256, 256), 64, 64),
@@ -48,7 +51,7 @@ def main():
     ap.add_argument("--only", default="")
     args = ap.parse_args()
     hold = [torch.empty(1 << 30, dtype=torch.uint8, device="cuda") for _ in range(int(args.fill))]
-    names = list(SETS) if args.set == "all" else args.set.split(",")
+    names = ["c3", "c5", "2d"] if args.set == "all" else args.set.split(",")
     dev = torch.device("cuda")
     for sname in names:
         for S, cin, cout in SETS[sname]:
