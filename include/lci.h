@@ -20,6 +20,7 @@
  *   lci_fftconv_*         fftconv_ref (gelu=False), model/models/hyena.py:32-51 / Filter.forward :201-216
  *   lci_hyena_pre/post_*  HyenaOperator short filter + gating, model/models/hyena.py:317-355
  *   lci_conv3_fwd         MONAI-1.3 UnetResBlock 3x3(x3) convs of the ViTUNETR / SwinUNETR heads, enhance_heads.py:30-356
+ *   lci_inorm_*           MONAI-1.3 UnetResBlock InstanceNorm (+ LeakyReLU) of the same heads
  *   lci_patch_embed_*     MONAI-1.3 PatchEmbeddingBlock (backbone_vit.py:351-361) / PatchEmbed (backbone_swin.py:800-806)
  */
 #ifndef LCI_H_
@@ -88,6 +89,19 @@ int lci_conv3_fwd(const void* x, const void* w, void* y, int B, int D, int H, in
 long long lci_conv3_wgrad_splits(long long V, int Cin, int Cout, int KD);
 int lci_conv3_wgrad(const void* x, const void* dy, float* part, int B, int D, int H, int W, int Cin, int Cout,
                     int KD, void* stream);
+
+/* ------------------------------------------------------------------ decoder-head instance norm (+ LeakyReLU)
+ * Replaces MONAI-1.3 UnetResBlock norm1+lrelu / norm2 / norm3 (InstanceNorm, affine=False, eps 1e-5) in the UNETR
+ * heads (enhance_heads.py:30-356), channels-last. x, dz, out: (B, V, C) bf16, C % 8 == 0, C <= 2048.
+ * reduce: part (B, lci_inorm_chunks(V, B), 2, C) f32 <- per-chunk sums of (x, x^2) when dz is null, else of
+ *   (dn, dn*n) with n = (x - mean) * rstd, dn = dz * (act && n < 0 ? slope : 1); stats (B, 2, C) = mean, rstd.
+ * apply: dz null -> out = act ? lrelu(n) : n;  else out = dx = rstd * (dn - coef0 - n * coef1), coef (B, 2, C)
+ *   = voxel means of (dn, dn*n). The caller combines the partial sums (in f64) between the two calls. */
+int lci_inorm_chunks(long long V, int B);
+int lci_inorm_reduce(const void* x, const void* dz, const float* stats, float* part, long long V, int B, int C,
+                     int act, float slope, void* stream);
+int lci_inorm_apply(const void* x, const void* dz, const float* stats, const float* coef, void* out, long long V,
+                    int B, int C, int act, float slope, void* stream);
 
 /* ------------------------------------------------------------------ Mamba selective scan (d_state 8)
  * Channels-last: u, delta (B, L, Dx); Bm, Cm (B, L, 8) (e.g. column slices of x_proj's output); y (B, L, .).

@@ -1,0 +1,173 @@
+// Instance normalisation (+ LeakyReLU) over channels-last volumes, for the UNETR decoder heads.
+//
+// Replaces MONAI-1.3 UnetResBlock's norm1 + lrelu, norm2 and norm3 (InstanceNorm{2,3}d(C), affine=False,
+// eps 1e-5, biased variance; LeakyReLU(0.01)) in ViTUNETR / SwinUNETR (model/models/enhance_heads.py:30-356),
+// without the NCDHW round trips torch's instance_norm needs (it runs batch_norm on a contiguous (1, B*C, ...)
+// view): x stays (B, V, C) bf16 channels-last between the HIP convolutions.
+//   forward : n = (x - mean[b,c]) * rstd[b,c];  z = act ? lrelu(n) : n
+//   backward: dn = dz * (act && n < 0 ? slope : 1);  dx = rstd * (dn - mean_V(dn) - n * mean_V(dn * n))
+// Two passes each way: a reduction (per-(b, c) partial sums over voxel chunks, combined in f64 by the caller)
+// and an elementwise pass. All HBM-bound: a thread moves 8 channels (16 B) per voxel.
+#include "common.hpp"
+
+namespace lci {
+
+struct NormArgs {
+  const bf16* x;       // (B, V, C)
+  const bf16* dz;      // bwd: (B, V, C)
+  bf16* out;           // fwd: z; bwd: dx
+  const float* stats;  // (B, 2, C): mean, rstd
+  const float* coef;   // bwd: (B, 2, C): mean_V(dn), mean_V(dn * n)
+  float* part;         // (B, nchunk, 2, C) partial sums
+  long long V, chunk;
+  int C, nchunk, act;
+  float slope;
+};
+
+__device__ __forceinline__ void load8(const bf16* p, float* f) {
+  const bf16x8 v = *(const bf16x8*)p;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = to_f32(v[j]);
+}
+
+// BWD = false: sums of x and x^2.  BWD = true: sums of dn and dn * n.
+template <bool BWD>
+__global__ __launch_bounds__(256) void inorm_reduce_kernel(NormArgs a) {
+  __shared__ float red[2][2048];
+  const int G = a.C >> 3, rows = 256 / G;
+  const int tid = threadIdx.x, g = tid % G, r = tid / G;
+  const int b = blockIdx.y, chunk = blockIdx.x;
+  const long long v0 = chunk * a.chunk, v1 = min(a.V, v0 + a.chunk);
+  float s1[8], s2[8], mu[8], rs[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+  if (BWD && r < rows) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      mu[j] = a.stats[(long long)b * 2 * a.C + 8 * g + j];
+      rs[j] = a.stats[(long long)b * 2 * a.C + a.C + 8 * g + j];
+    }
+  }
+  if (r < rows) {
+    const long long base = (long long)b * a.V * a.C + 8 * g;
+    for (long long v = v0 + r; v < v1; v += rows) {
+      float x[8];
+      load8(a.x + base + v * a.C, x);
+      if (!BWD) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { s1[j] += x[j]; s2[j] += x[j] * x[j]; }
+      } else {
+        float d[8];
+        load8(a.dz + base + v * a.C, d);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float n = (x[j] - mu[j]) * rs[j];
+          const float dn = (a.act && n < 0.f) ? d[j] * a.slope : d[j];
+          s1[j] += dn;
+          s2[j] += dn * n;
+        }
+      }
+    }
+  }
+  // combine the `rows` voxel lanes of each channel through LDS
+  for (int c = tid; c < rows * a.C; c += 256) { red[0][c] = 0.f; red[1][c] = 0.f; }
+  __syncthreads();
+  if (r < rows) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { red[0][r * a.C + 8 * g + j] = s1[j]; red[1][r * a.C + 8 * g + j] = s2[j]; }
+  }
+  __syncthreads();
+  for (int c = tid; c < a.C; c += 256) {
+    float t1 = 0.f, t2 = 0.f;
+    for (int q = 0; q < rows; ++q) { t1 += red[0][q * a.C + c]; t2 += red[1][q * a.C + c]; }
+    float* p = a.part + ((long long)b * a.nchunk + chunk) * 2 * a.C;
+    p[c] = t1;
+    p[a.C + c] = t2;
+  }
+}
+
+template <bool BWD>
+__global__ __launch_bounds__(256) void inorm_apply_kernel(NormArgs a) {
+  const int G = a.C >> 3;
+  const long long e = blockIdx.x * 256LL + threadIdx.x;   // 8-channel group index over (B, V, G)
+  const int b = blockIdx.y;
+  if (e >= a.V * G) return;
+  const int g = (int)(e % G);
+  const long long off = (long long)b * a.V * a.C + e * 8;
+  const float* st = a.stats + (long long)b * 2 * a.C + 8 * g;
+  float x[8];
+  load8(a.x + off, x);
+  bf16x8 o;
+  if (!BWD) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float n = (x[j] - st[j]) * st[a.C + j];
+      if (a.act && n < 0.f) n *= a.slope;
+      o[j] = to_bf16(n);
+    }
+  } else {
+    float d[8];
+    load8(a.dz + off, d);
+    const float* cf = a.coef + (long long)b * 2 * a.C + 8 * g;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float rs = st[a.C + j];
+      const float n = (x[j] - st[j]) * rs;
+      const float dn = (a.act && n < 0.f) ? d[j] * a.slope : d[j];
+      o[j] = to_bf16(rs * (dn - cf[j] - n * cf[a.C + j]));
+    }
+  }
+  *(bf16x8*)(a.out + off) = o;
+}
+
+}  // namespace lci
+
+using namespace lci;
+
+// Voxel chunks per sample for the reduction: ~2048 workgroups in total, at least 256 voxels per chunk.
+extern "C" int lci_inorm_chunks(long long V, int B) {
+  long long n = (2048 + B - 1) / B;
+  if (n > (V + 255) / 256) n = (V + 255) / 256;
+  return (int)(n < 1 ? 1 : n);
+}
+
+static int norm_check(long long V, int B, int C, const void* x) {
+  LCI_CHECK(V > 0 && B > 0 && C > 0 && C % 8 == 0 && C <= 2048, "inorm: bad shape (C %% 8 == 0, C <= 2048)");
+  LCI_CHECK(((uintptr_t)x & 15) == 0, "inorm: misaligned input");
+  return 0;
+}
+
+extern "C" int lci_inorm_reduce(const void* x, const void* dz, const float* stats, float* part, long long V, int B,
+                                int C, int act, float slope, void* stream) {
+  if (norm_check(V, B, C, x)) return 1;
+  NormArgs a = {};
+  a.x = (const bf16*)x; a.dz = (const bf16*)dz; a.stats = stats; a.part = part;
+  a.V = V; a.C = C; a.act = act; a.slope = slope;
+  a.nchunk = lci_inorm_chunks(V, B);
+  a.chunk = (V + a.nchunk - 1) / a.nchunk;
+  dim3 grid(a.nchunk, B);
+  if (dz)
+    hipLaunchKernelGGL(inorm_reduce_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(inorm_reduce_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int lci_inorm_apply(const void* x, const void* dz, const float* stats, const float* coef, void* out,
+                               long long V, int B, int C, int act, float slope, void* stream) {
+  if (norm_check(V, B, C, x)) return 1;
+  LCI_CHECK(((uintptr_t)out & 15) == 0 && (!dz || ((uintptr_t)dz & 15) == 0), "inorm: misaligned buffers");
+  NormArgs a = {};
+  a.x = (const bf16*)x; a.dz = (const bf16*)dz; a.stats = stats; a.coef = coef; a.out = (bf16*)out;
+  a.V = V; a.C = C; a.act = act; a.slope = slope;
+  const long long groups = V * (C / 8);
+  LCI_CHECK((groups + 255) / 256 < (1LL << 31), "inorm: volume too large");
+  dim3 grid((unsigned)((groups + 255) / 256), B);
+  if (dz)
+    hipLaunchKernelGGL(inorm_apply_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(inorm_apply_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}

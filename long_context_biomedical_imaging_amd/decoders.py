@@ -131,7 +131,16 @@ class UnetResBlock(nn.Module):
             self.conv3 = _conv(nd, cin, cout, 1, stride)
             self.norm3 = _inorm(nd, cout)
 
+        # channels-last HIP path: the convs are the HIP conv3 / GEMM forms and the instance norms (+ LeakyReLU)
+        # the lci_inorm kernels, so the block never round-trips through NCDHW (2-D: only with HIP_CONV_2D)
+        self.fused = isinstance(self.conv1, (Conv3x3, Conv3x3_2d)) and cout % 8 == 0 and (nd == 3 or HIP_CONV_2D)
+
     def forward(self, inp):
+        if self.fused and inp.is_cuda:
+            out = kernels.instance_norm_act(self.conv1(inp), True)
+            out = kernels.instance_norm_act(self.conv2(out), False)
+            res = kernels.instance_norm_act(self.conv3(inp), False) if self.downsample else inp
+            return F.leaky_relu(out + res, 0.01)
         out = self.lrelu(self.norm1(self.conv1(inp)))
         out = self.norm2(self.conv2(out))
         res = self.norm3(self.conv3(inp)) if self.downsample else inp

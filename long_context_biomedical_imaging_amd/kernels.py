@@ -747,3 +747,63 @@ def conv3(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     if not x.is_cuda:
         raise _lib.LciError("conv3 runs on the GPU only; there is no CPU path")
     return _Conv3.apply(x, weight, weight.dim() - 2)
+
+
+# ------------------------------------------------------- decoder-head instance norm (+ LeakyReLU), channels-last
+INORM_EPS = 1e-5
+LRELU_SLOPE = 0.01
+
+
+def _inorm_sums(x_cl, dz_cl, stats, act):
+    """(B, 2, C) f64 sums over voxels: (x, x^2) forward, (dn, dn * n) backward."""
+    B, V, C = x_cl.shape
+    lib = _lib.load()
+    nch = lib.lci_inorm_chunks(V, B)
+    part = torch.empty(B, nch, 2, C, device=x_cl.device, dtype=torch.float32)
+    _lib.call("lci_inorm_reduce", x_cl.data_ptr(), _lib.ptr(dz_cl), _lib.ptr(stats), part.data_ptr(), V, B, C,
+              int(act), LRELU_SLOPE, _lib.stream_of(x_cl))
+    return part.double().sum(1)
+
+
+class _InstanceNormAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x_cl, act):
+        B, V, C = x_cl.shape
+        s = _inorm_sums(x_cl, None, None, act) / V
+        mean = s[:, 0]
+        rstd = torch.rsqrt((s[:, 1] - mean * mean).clamp_min(0.0) + INORM_EPS)
+        stats = torch.stack([mean, rstd], 1).float().contiguous()
+        z = torch.empty_like(x_cl)
+        KernelTimer.run("inorm_fwd", 0.0, x_cl, lambda: _lib.call(
+            "lci_inorm_apply", x_cl.data_ptr(), None, stats.data_ptr(), None, z.data_ptr(), V, B, C, int(act),
+            LRELU_SLOPE, _lib.stream_of(x_cl)))
+        ctx.save_for_backward(x_cl, stats)
+        ctx.act = act
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        x_cl, stats = ctx.saved_tensors
+        B, V, C = x_cl.shape
+        dz = dz.to(torch.bfloat16).contiguous()
+        coef = (_inorm_sums(x_cl, dz, stats, ctx.act) / V).float().contiguous()
+        dx = torch.empty_like(x_cl)
+        KernelTimer.run("inorm_bwd", 0.0, x_cl, lambda: _lib.call(
+            "lci_inorm_apply", x_cl.data_ptr(), dz.data_ptr(), stats.data_ptr(), coef.data_ptr(), dx.data_ptr(),
+            V, B, C, int(ctx.act), LRELU_SLOPE, _lib.stream_of(x_cl)))
+        return dx, None
+
+
+def instance_norm_act(x: torch.Tensor, act: bool) -> torch.Tensor:
+    """InstanceNorm{2,3}d(C) (affine=False, eps 1e-5) [+ LeakyReLU(0.01)] of a bf16 (B, C, *S) tensor, computed
+    channels-last by the HIP kernels; returns (B, C, *S) bf16 with channels-last strides."""
+    if not x.is_cuda:
+        raise _lib.LciError("instance_norm_act runs on the GPU only; there is no CPU path")
+    B, C = x.shape[:2]
+    S = x.shape[2:]
+    x_cl = x.movedim(1, -1).reshape(B, -1, C)
+    if x_cl.dtype != torch.bfloat16:
+        x_cl = x_cl.to(torch.bfloat16)
+    x_cl = x_cl.contiguous()
+    z = _InstanceNormAct.apply(x_cl, act)
+    return z.view(B, *S, C).movedim(-1, 1)

@@ -51,3 +51,24 @@ def test_conv3_large_vs_miopen():
     y = kernels.conv3(x, w)
     yr = F.conv3d(x.float(), w.bfloat16().float(), padding=1)
     assert rel_err(y.float(), yr) < 1e-2
+
+
+@pytest.mark.parametrize("shape", [(2, 96, 9, 10, 11), (1, 64, 33, 47), (1, 1536, 3, 3, 3), (2, 32, 40, 3, 5)])
+@pytest.mark.parametrize("act", [True, False])
+def test_instance_norm_act_parity(shape, act):
+    """lci_inorm (channels-last) vs torch InstanceNorm (affine=False, eps 1e-5) [+ LeakyReLU(0.01)] in fp32 on
+    the same bf16 input; rel-L2 <= 1e-2 (bf16 output) forward, <= 2e-2 input gradient."""
+    torch.manual_seed(0)
+    x = (torch.randn(shape) * 3 + 0.5).bfloat16().float()
+    dz = torch.randn(shape).bfloat16().float()
+    xr = x.clone().requires_grad_(True)
+    zr = F.instance_norm(xr, eps=1e-5)
+    if act:
+        zr = F.leaky_relu(zr, 0.01)
+    zr.backward(dz)
+    xc = x.cuda().bfloat16().requires_grad_(True)
+    z = kernels.instance_norm_act(xc, act)
+    assert z.shape == zr.shape and z.dtype == torch.bfloat16
+    assert rel_err(z.float(), zr) < 1e-2
+    z.backward(dz.cuda().bfloat16())
+    assert rel_err(xc.grad.float(), xr.grad) < 2e-2
