@@ -23,8 +23,9 @@ import torch.nn.functional as F
 
 from . import kernels
 
-# A/B switch for the 2-D heads (the headline ViTUNETR at 512^2): HIP conv3 vs torch/MIOpen
-HIP_CONV_2D = os.environ.get("LCI_HIP_CONV_2D", "0") == "1"
+# A/B switch for the 2-D heads (the headline ViTUNETR at 512^2): HIP conv3 + inorm (default; same step time as
+# MIOpen at 512^2, without its ~2 min first-call solver search) vs torch/MIOpen (LCI_HIP_CONV_2D=0)
+HIP_CONV_2D = os.environ.get("LCI_HIP_CONV_2D", "1") != "0"
 
 
 class Conv3x3(nn.Conv3d):
