@@ -494,18 +494,31 @@ __global__ __launch_bounds__(256) void hyena_post_bwd_kernel(GateArgs a) {
 template <typename T>
 __global__ __launch_bounds__(256) void hyena_pre_bwd_kernel(GateArgs a) {
   const int c = blockIdx.y * 256 + threadIdx.x;   // channel of 3D
-  if (c >= 3 * a.D) return;
   const int bb = blockIdx.z, t0 = blockIdx.x * 64, t1 = min(a.L, t0 + 64);
   const int h = c / (3 * a.hd), rem = c % (3 * a.hd), part = rem / a.hd, jj = rem % a.hd;
   const int ch = h * a.hd + jj;                   // output channel of D
   const int base = h * 3 * a.hd + jj;
   const T* zb = (const T*)a.z + (long long)bb * a.L * 3 * a.D;
-  const float* dvg = a.dvg + ((long long)bb * a.D + ch) * a.L;
+  // dvg is channel-major (BB, D, L): a thread per channel reading it directly strides by L across the wave
+  // (uncoalesced, ~9x slower overall), so the workgroup first stages the rows of its heads' channels for
+  // tokens [t0, t0 + 64 + K - 1) through LDS with token-contiguous loads.
+  extern __shared__ float sdvg[];                 // [256 threads][64 + K - 1] (row of the thread's channel)
+  __shared__ int chrow[256];
+  const int tw = 64 + a.K - 1;
+  chrow[threadIdx.x] = (c < 3 * a.D && part != 1) ? ch : -1;   // the x2 part (1) does not read dvg
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < 256 * tw; idx += 256) {
+    const int rr = idx / tw, tt = idx - rr * tw, t = t0 + tt, cr = chrow[rr];
+    sdvg[idx] = (cr >= 0 && t < a.L) ? a.dvg[((long long)bb * a.D + cr) * a.L + t] : 0.f;
+  }
+  __syncthreads();
+  if (c >= 3 * a.D) return;
+  const float* dvl = sdvg + threadIdx.x * tw - t0;
   auto dconv = [&](int t) -> float {
     if (t < 0 || t >= a.L) return 0.f;
     if (part == 1) return (float)((const float*)a.gx2)[((long long)bb * a.L + t) * a.D + ch];
     const float other = conv_at(a, zb, t, part == 0 ? base + 2 * a.hd : base);
-    return dvg[t] * other;
+    return dvl[t] * other;
   };
   float dwl[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float dbl = 0.f;
@@ -524,6 +537,75 @@ __global__ __launch_bounds__(256) void hyena_pre_bwd_kernel(GateArgs a) {
     }
   }
   for (int i = 0; i < K && i < 8; ++i) atomicAdd(a.dw + c * K + i, dwl[i]);
+  if (a.db) atomicAdd(a.db + c, dbl);
+}
+
+// Same result as hyena_pre_bwd_kernel for a compile-time filter order KC: each dconv(t), each short-conv value
+// and each z element is produced once per thread and kept in register rings (the generic kernel recomputes
+// dconv K + 1 times per token, each with a K-tap conv: ~16 loads per token-channel instead of 2).
+template <typename T, int KC>
+__global__ __launch_bounds__(256) void hyena_pre_bwd_ring_kernel(GateArgs a) {
+  const int c = blockIdx.y * 256 + threadIdx.x;   // channel of 3D
+  const int bb = blockIdx.z, t0 = blockIdx.x * 64, t1 = min(a.L, t0 + 64);
+  const int h = c / (3 * a.hd), rem = c % (3 * a.hd), part = rem / a.hd, jj = rem % a.hd;
+  const int ch = h * a.hd + jj;
+  const int base = h * 3 * a.hd + jj;
+  const T* zb = (const T*)a.z + (long long)bb * a.L * 3 * a.D;
+  constexpr int TW = 64 + KC;
+  extern __shared__ float sdvg[];                 // [256 threads][TW]: dvg row of the thread's channel
+  __shared__ int chrow[256];
+  chrow[threadIdx.x] = (c < 3 * a.D && part != 1) ? ch : -1;
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < 256 * TW; idx += 256) {
+    const int rr = idx / TW, tt = idx - rr * TW, t = t0 + tt, cr = chrow[rr];
+    sdvg[idx] = (cr >= 0 && t < a.L) ? a.dvg[((long long)bb * a.D + cr) * a.L + t] : 0.f;
+  }
+  __syncthreads();
+  if (c >= 3 * a.D) return;
+  const float* dvl = sdvg + threadIdx.x * TW - t0;
+  const int oc = part == 0 ? base + 2 * a.hd : base;   // the other gate factor's channel (parts 0, 2)
+  float wc[KC], wo[KC];
+#pragma unroll
+  for (int i = 0; i < KC; ++i) { wc[i] = a.w[c * KC + i]; wo[i] = a.w[oc * KC + i]; }
+  const float bo = a.bias ? a.bias[oc] : 0.f;
+  auto zl = [&](int t, int cc) -> float { return (t >= 0 && t < a.L) ? (float)zb[(long long)t * 3 * a.D + cc] : 0.f; };
+  float zo[KC];   // z[t - KC + 1 .. t][oc] for the newest dconv position t
+  float zs[KC];   // z[s - KC + 1 .. s][c]
+  float dcw[KC];  // dconv(s .. s + KC - 1)
+#pragma unroll
+  for (int i = 0; i < KC; ++i) { zo[i] = zl(t0 - KC + i, oc); zs[i] = zl(t0 - KC + 1 + i, c); }
+  auto dconv_push = [&](int t) -> float {   // advance zo to position t, return dconv(t)
+#pragma unroll
+    for (int i = 0; i < KC - 1; ++i) zo[i] = zo[i + 1];
+    zo[KC - 1] = zl(t, oc);
+    if (t < 0 || t >= a.L) return 0.f;
+    if (part == 1) return (float)((const float*)a.gx2)[((long long)bb * a.L + t) * a.D + ch];
+    float conv = bo;
+#pragma unroll
+    for (int i = 0; i < KC; ++i) conv = fmaf(wo[i], zo[i], conv);
+    return dvl[t] * conv;
+  };
+#pragma unroll
+  for (int j = 0; j < KC; ++j) dcw[j] = dconv_push(t0 + j);
+  float dwl[KC], dbl = 0.f;
+#pragma unroll
+  for (int i = 0; i < KC; ++i) dwl[i] = 0.f;
+  for (int s = t0; s < t1; ++s) {
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < KC; ++i) acc = fmaf(wc[i], dcw[KC - 1 - i], acc);
+    ((T*)a.dz)[((long long)bb * a.L + s) * 3 * a.D + c] = (T)acc;
+    const float g = dcw[0];
+    dbl += g;
+#pragma unroll
+    for (int i = 0; i < KC; ++i) dwl[i] = fmaf(g, zs[i], dwl[i]);
+#pragma unroll
+    for (int i = 0; i < KC - 1; ++i) { dcw[i] = dcw[i + 1]; zs[i] = zs[i + 1]; }
+    zs[KC - 1] = zl(s + 1, c);
+    dcw[KC - 1] = (s + KC < t0 + TW) ? dconv_push(s + KC) : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < KC; ++i) atomicAdd(a.dw + c * KC + i, dwl[i]);
   if (a.db) atomicAdd(a.db + c, dbl);
 }
 
@@ -685,8 +767,26 @@ extern "C" int lci_hyena_pre_bwd(int dtype, const void* z, const float* w, const
   a.z = z; a.w = w; a.bias = bias; a.dvg = dvg; a.gx2 = gx2; a.dz = dz; a.dw = dw; a.db = db;
   a.BB = BB; a.L = L; a.H = H; a.hd = hd; a.D = H * hd; a.K = K;
   dim3 grid((L + 63) / 64, (3 * a.D + 255) / 256, BB);
-  if (dtype == 1) hipLaunchKernelGGL(hyena_pre_bwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, a);
-  else hipLaunchKernelGGL(hyena_pre_bwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  {   // register-ring kernel for every supported order (the reference's models use short_filter_order = 5)
+    const size_t lds = (size_t)256 * (64 + K) * sizeof(float);
+#define LCI_PRE_BWD(KK)                                                                                          \
+  case KK:                                                                                                     \
+    if (dtype == 1)                                                                                            \
+      hipLaunchKernelGGL((hyena_pre_bwd_ring_kernel<bf16, KK>), grid, dim3(256), lds, (hipStream_t)stream, a); \
+    else                                                                                                       \
+      hipLaunchKernelGGL((hyena_pre_bwd_ring_kernel<float, KK>), grid, dim3(256), lds, (hipStream_t)stream, a); \
+    LCI_LAUNCH_CHECK();                                                                                        \
+    return 0;
+    switch (K) {
+      LCI_PRE_BWD(1) LCI_PRE_BWD(2) LCI_PRE_BWD(3) LCI_PRE_BWD(4) LCI_PRE_BWD(5) LCI_PRE_BWD(6) LCI_PRE_BWD(7)
+      LCI_PRE_BWD(8)
+      default: break;
+    }
+#undef LCI_PRE_BWD
+  }
+  const size_t lds = (size_t)256 * (64 + K - 1) * sizeof(float);
+  if (dtype == 1) hipLaunchKernelGGL(hyena_pre_bwd_kernel<bf16>, grid, dim3(256), lds, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL(hyena_pre_bwd_kernel<float>, grid, dim3(256), lds, (hipStream_t)stream, a);
   LCI_LAUNCH_CHECK();
   return 0;
 }
