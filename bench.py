@@ -237,7 +237,7 @@ def main():
     if args.batch is None:
         args.batch = 2 if args.workload in ("vit_p2_512", "vit_hyena_p2_512") else 1
     rank, local, world = init_distributed()
-    device = torch.device("cuda", local)
+    device = torch.device("cuda", local % torch.cuda.device_count())   # % : gloo rehearsals on one GPU
     torch.cuda.set_device(device)
     res = run_workload(args.workload, args.batch, args.steps, args.warmup, rank, world, device)
     if args.workload == "vit_p2_512" and not args.no_secondary:

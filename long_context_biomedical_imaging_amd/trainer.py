@@ -28,7 +28,8 @@ def init_distributed():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and not dist.is_initialized():
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # LCI_DIST_BACKEND=gloo: rehearse N ranks on fewer GPUs (gloo moves CUDA tensors through the host)
+        backend = os.environ.get("LCI_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
