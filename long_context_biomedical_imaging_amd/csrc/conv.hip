@@ -13,6 +13,8 @@
 // fragments, and issues 2*NT v_mfma_f32_32x32x16_bf16. With W as the A operand, a lane's accumulators hold 4
 // consecutive output channels per register quad, so the bf16 results go out as 8-byte stores.
 // Neighbour reuse (27 taps read the same voxels) is served by L1/L2: the volume is swept in voxel order.
+#include <stdlib.h>
+
 #include "common.hpp"
 
 #ifndef LCI_CONV_MV_WIDE
@@ -105,6 +107,111 @@ __global__ __launch_bounds__(256) void conv3_fwd_kernel(ConvArgs a) {
   for (int m = 0; m < MV; ++m) {
     if (!inb[m]) continue;
     bf16* yp = a.y + vb[m] * a.Cout + n0 + 4 * h;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        bf16x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = to_bf16(acc[m][t][4 * q + j]);
+        *(bf16x4*)(yp + 32 * t + 8 * q) = o;
+      }
+  }
+}
+
+// LDS-staged variant (Cin % 32 == 0): a workgroup owns 4*32*MV consecutive voxels. For each (dz, dy) tap
+// group and 32-channel chunk it stages the contiguous source rows [v0 + off(dz,dy) - 1, ... + 4*32*MV + 1) of x
+// (so the three dx taps read the same LDS rows at offsets 0, 1, 2) and the three taps' weight slabs, with
+// coalesced 16-B loads; fragments then come from LDS (80-B rows). Replaces 3 global fragment loads per voxel
+// block and tap by one staged row set, and shares the weight fragments across the 4 waves.
+constexpr int CLD = 40;   // LDS row stride (elements): 32 channels + 8 pad = 80 B
+
+template <int NT, int MV>
+__global__ __launch_bounds__(256) void conv3_fwd_lds_kernel(ConvArgs a) {
+  constexpr int WV = 4 * 32 * MV;                 // voxels per workgroup
+  constexpr int XR = WV + 2;                      // staged rows (dx halo)
+  __shared__ __attribute__((aligned(16))) bf16 sX[XR * CLD];
+  __shared__ __attribute__((aligned(16))) bf16 sW[3 * 32 * NT * CLD];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+  const int r = lane & 31, h = lane >> 5;
+  const long long vg0 = (long long)blockIdx.x * WV;
+  const int n0 = blockIdx.y * 32 * NT;
+  const int T = a.KD * 9;
+  const int HW = a.H * a.W;
+  int zc[MV], yc[MV], xc[MV];
+  bool inb[MV];
+#pragma unroll
+  for (int m = 0; m < MV; ++m) {
+    const long long v = vg0 + wave * 32 * MV + 32 * m + r;
+    inb[m] = v < a.V;
+    const long long vv = inb[m] ? v : 0;
+    const long long s = vv / ((long long)a.D * HW);
+    int rem = (int)(vv - s * (long long)a.D * HW);
+    zc[m] = rem / HW; rem -= zc[m] * HW;
+    yc[m] = rem / a.W; xc[m] = rem - yc[m] * a.W;
+  }
+  f32x16 acc[MV][NT];
+#pragma unroll
+  for (int m = 0; m < MV; ++m)
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[m][t][i] = 0.f;
+
+  const int ngroups = a.KD * 3;
+  for (int grp = 0; grp < ngroups; ++grp) {
+    const int dz = (a.KD == 3 ? grp / 3 : 1) - 1, dy = grp % 3 - 1;
+    const long long src0 = vg0 + (long long)dz * HW + (long long)dy * a.W - 1;   // source row of LDS row 0
+    bool okzy[MV];
+#pragma unroll
+    for (int m = 0; m < MV; ++m)
+      okzy[m] = inb[m] && (unsigned)(zc[m] + dz) < (unsigned)a.D && (unsigned)(yc[m] + dy) < (unsigned)a.H;
+    for (int c0 = 0; c0 < a.Cin; c0 += 32) {
+      __syncthreads();
+      for (int q = tid; q < XR * 4; q += 256) {
+        const int row = q >> 2, ch = q & 3;
+        const long long u = src0 + row;
+        u32x4 val = {0u, 0u, 0u, 0u};
+        if (u >= 0 && u < a.V) val = *(const u32x4*)(a.x + u * a.Cin + c0 + 8 * ch);
+        *(u32x4*)(sX + row * CLD + 8 * ch) = val;
+      }
+      for (int q = tid; q < 3 * 32 * NT * 4; q += 256) {
+        const int row = q >> 2, ch = q & 3;                 // row = dx * 32NT + n
+        const int dxi = row / (32 * NT), n = row - dxi * 32 * NT;
+        const int tap = grp * 3 + dxi;
+        *(u32x4*)(sW + row * CLD + 8 * ch) =
+            *(const u32x4*)(a.w + ((long long)(n0 + n) * T + tap) * a.Cin + c0 + 8 * ch);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int dxi = 0; dxi < 3; ++dxi) {
+        bool ok[MV];
+#pragma unroll
+        for (int m = 0; m < MV; ++m) ok[m] = okzy[m] && (unsigned)(xc[m] + dxi - 1) < (unsigned)a.W;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          bf16x8 wa[NT], xb[MV];
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+            wa[t] = *(const bf16x8*)(sW + (dxi * 32 * NT + 32 * t + r) * CLD + 16 * ks + 8 * h);
+#pragma unroll
+          for (int m = 0; m < MV; ++m) {
+            xb[m] = *(const bf16x8*)(sX + (wave * 32 * MV + 32 * m + r + dxi) * CLD + 16 * ks + 8 * h);
+            if (!ok[m]) xb[m] = zero8();
+          }
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int m = 0; m < MV; ++m) acc[m][t] = mfma32(wa[t], xb[m], acc[m][t]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < MV; ++m) {
+    if (!inb[m]) continue;
+    const long long v = vg0 + wave * 32 * MV + 32 * m + r;
+    bf16* yp = a.y + v * a.Cout + n0 + 4 * h;
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -323,10 +430,19 @@ static int launch_wgrad(const WgradArgs& a, int nsplit, hipStream_t st) {
 
 static int tile3(int c) { return (c / 32) % 3 == 0 ? 3 : ((c / 32) % 2 == 0 ? 2 : 1); }
 
+static bool lci_conv_lds() {   // LCI_CONV_LDS=0: the direct-load kernel (A/B)
+  static const bool on = !getenv("LCI_CONV_LDS") || atoi(getenv("LCI_CONV_LDS")) != 0;
+  return on;
+}
+
 template <int NT>
 static int launch(const ConvArgs& a, hipStream_t st) {
   constexpr int MV = NT <= 2 ? 4 : LCI_CONV_MV_WIDE;   // narrow outputs: more voxels per wave
-  if (a.Cin % 16 == 0) {
+  if (a.Cin % 32 == 0 && lci_conv_lds()) {
+    constexpr int ML = NT == 4 ? 2 : 4;
+    dim3 grid((unsigned)((a.V + 128 * ML - 1) / (128 * ML)), a.Cout / (32 * NT));
+    hipLaunchKernelGGL((conv3_fwd_lds_kernel<NT, ML>), grid, dim3(256), 0, st, a);
+  } else if (a.Cin % 16 == 0) {
     dim3 grid((unsigned)((a.V + 128 * MV - 1) / (128 * MV)), a.Cout / (32 * NT));
     hipLaunchKernelGGL((conv3_fwd_kernel<NT, MV>), grid, dim3(256), 0, st, a);
   } else {
