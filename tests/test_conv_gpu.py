@@ -72,3 +72,55 @@ def test_instance_norm_act_parity(shape, act):
     assert rel_err(z.float(), zr) < 1e-2
     z.backward(dz.cuda().bfloat16())
     assert rel_err(xc.grad.float(), xr.grad) < 2e-2
+
+
+def _ref_resblock(blk, x):
+    """MONAI-1.3 UnetResBlock forward in plain torch ops on the module's own weights (moved to x's device):
+    conv-norm-lrelu-conv-norm (+ conv3-norm3 residual) -> add -> lrelu. On CPU in fp32 it is the oracle; on the
+    GPU under autocast it is the reference's own bf16 path (MIOpen convs, torch instance_norm)."""
+    nd = x.dim() - 2
+    conv = F.conv3d if nd == 3 else F.conv2d
+    dev = x.device
+    w = lambda m: m.weight if m.weight.device == dev else m.weight.detach().float().to(dev)   # noqa: E731
+    out = F.leaky_relu(F.instance_norm(conv(x, w(blk.conv1), padding=1), eps=1e-5), 0.01)
+    out = F.instance_norm(conv(out, w(blk.conv2), padding=1), eps=1e-5)
+    res = F.instance_norm(conv(x, w(blk.conv3)), eps=1e-5) if blk.downsample else x
+    return F.leaky_relu(out + res, 0.01)
+
+
+@pytest.mark.parametrize("nd,S,cin,cout", [(3, (12, 10, 14), 64, 32), (3, (8, 8, 8), 96, 96), (2, (40, 36), 128, 64)])
+def test_unet_resblock_fused_vs_torch(nd, S, cin, cout):
+    """Decoder block on the HIP conv + inorm kernels (channels-last) vs the fp32 torch restatement on the same
+    weights and bf16-rounded input. Bound: no worse than 1.5x the error of the reference's own bf16 autocast path
+    (torch/MIOpen on the GPU) against the same fp32 oracle, and <= 3e-2 on the output."""
+    from long_context_biomedical_imaging_amd.decoders import UnetResBlock
+    torch.manual_seed(0)
+    blk = UnetResBlock(nd, cin, cout, 3, 1).cuda()
+    assert blk.fused
+    x = torch.randn(2, cin, *S).bfloat16().float()
+    dy = torch.randn(2, cout, *S)
+    xr = x.clone().requires_grad_(True)
+    yr = _ref_resblock(blk, xr)                       # fp32 CPU oracle
+    yr.backward(dy)
+    xt = x.cuda().requires_grad_(True)                # reference's bf16 autocast path on the GPU
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        yt = _ref_resblock(blk, xt)
+    yt.float().backward(dy.cuda())
+    gt = blk.conv1.weight.grad.float().cpu()
+    blk.zero_grad(set_to_none=True)
+    xc = x.cuda().requires_grad_(True)                # this repo's fused HIP path
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = blk(xc)
+    assert y.shape == yr.shape
+    y.float().backward(dy.cuda())
+    e_y, e_yt = rel_err(y.float(), yr), rel_err(yt.float(), yr)
+    e_dx, e_dxt = rel_err(xc.grad.float(), xr.grad), rel_err(xt.grad.float(), xr.grad)
+    assert e_y < 3e-2 and e_y <= max(1.5 * e_yt, 1e-2), (e_y, e_yt)
+    assert e_dx <= max(1.5 * e_dxt, 1e-2), (e_dx, e_dxt)
+    # conv1 weight gradient against an fp32 CPU replay with conv1.weight as the leaf (same relative bound)
+    g = blk.conv1.weight.grad.float().cpu()
+    wr = torch.nn.Parameter(blk.conv1.weight.detach().float().cpu())
+    blk.conv1.weight = wr
+    _ref_resblock(blk, x.clone()).backward(dy)
+    e_g, e_gt = rel_err(g, wr.grad), rel_err(gt, wr.grad)
+    assert e_g <= max(1.5 * e_gt, 1e-2), (e_g, e_gt)
