@@ -420,6 +420,119 @@ __global__ __launch_bounds__(256) void conv3_wgrad_kernel(WgradArgs a) {
       }
 }
 
+// Three-tap weight gradient: one workgroup computes the three dx taps of a (dz, dy) tap group for a 32*MT x 32
+// (n, c) tile. Voxels are enumerated in a "gapped" row space, one zero row after every W-voxel line, so that the
+// x neighbour of dy row g for tap dx is simply staged row g + dx: it falls on a zero gap row exactly when x + dx
+// leaves [0, W). The dy tile is staged once per step and its fragments feed all three taps; the x tile is 130
+// rows (1-row halo each side). Staging per tap drops 3x versus conv3_wgrad_kernel.
+template <int MT>
+__global__ __launch_bounds__(256) void conv3_wgrad3_kernel(WgradArgs a) {
+  constexpr int LDY = wg_ld(MT), LDX = wg_ld(1), XR = WG_ROWS + 2;
+  __shared__ __attribute__((aligned(16))) bf16 sdy[2][WG_ROWS * LDY];
+  __shared__ __attribute__((aligned(16))) bf16 sx[2][(XR + 6) * LDX];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+  const int grp = blockIdx.x, split = blockIdx.y;
+  const int nct = a.Cin / 32;
+  const int n0 = (blockIdx.z / nct) * 32 * MT, c0 = (blockIdx.z % nct) * 32;
+  const int T = a.KD * 9;
+  const int dz = (a.KD == 3 ? grp / 3 : 1) - 1, dyy = grp % 3 - 1;
+  const int HW = a.H * a.W, W1 = a.W + 1;
+  const long long lines = a.V / a.W, R = lines * W1;
+  const long long shift = (long long)dz * HW + (long long)dyy * a.W;
+  const long long gs = (long long)split * a.Lv, ge = min(R, gs + a.Lv);
+
+  f32x16 acc[3][MT];
+#pragma unroll
+  for (int d = 0; d < 3; ++d)
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[d][m][i] = 0.f;
+
+  u32x4 rdy[2 * MT], rx[3];
+  // Row -> (line, x) without per-element 64-bit division: one (uniform) division per step for the tile's first
+  // gapped row, then a 32-bit quotient by W + 1 and a carry of (y, z) per element.
+  auto load = [&](long long g0) {
+    const long long gb = g0 - 1;                        // x tile row 0
+    long long lb = (gb >= 0 ? gb : gb - W1 + 1) / W1;   // floor division (gb may be -1)
+    const int xb = (int)(gb - lb * W1);
+    const int yb = (int)(((lb % a.H) + a.H) % a.H);
+    const int zb = (int)((((lb >= 0 ? lb : lb - a.H + 1) / a.H) % a.D + a.D) % a.D);
+#pragma unroll
+    for (int i = 0; i < 2 * MT; ++i) {   // dy rows g0 .. g0 + 127 (zero on gaps / past the split)
+      const int c = tid + 256 * i, row = c / (4 * MT), ch = c % (4 * MT);
+      rdy[i] = u32x4{0u, 0u, 0u, 0u};
+      if (g0 + row < ge) {
+        const int t = xb + 1 + row, q = t / W1, xx = t - q * W1;
+        if (xx < a.W) rdy[i] = *(const u32x4*)(a.dy + ((lb + q) * a.W + xx) * a.Cout + n0 + 8 * ch);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {        // x rows g0 - 1 .. g0 + 128, shifted by (dz, dy); zero on gaps / outside
+      const int c = tid + 256 * i, row = c >> 2, ch = c & 3;
+      rx[i] = u32x4{0u, 0u, 0u, 0u};
+      if (row < XR && gb + row >= 0 && gb + row < R) {
+        const int t = xb + row, q = t / W1, xx = t - q * W1;
+        int yl = yb + q, zl = zb;
+        while (yl >= a.H) { yl -= a.H; if (++zl == a.D) zl = 0; }
+        if (xx < a.W && (unsigned)(zl + dz) < (unsigned)a.D && (unsigned)(yl + dyy) < (unsigned)a.H)
+          rx[i] = *(const u32x4*)(a.x + ((lb + q) * a.W + xx + shift) * a.Cin + c0 + 8 * ch);
+      }
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2 * MT; ++i) {
+      const int c = tid + 256 * i, row = c / (4 * MT), ch = c % (4 * MT);
+      *(u32x4*)(&sdy[buf][row * LDY + 8 * ch]) = rdy[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int c = tid + 256 * i, row = c >> 2, ch = c & 3;
+      if (row < XR) *(u32x4*)(&sx[buf][row * LDX + 8 * ch]) = rx[i];
+    }
+  };
+
+  load(gs);
+  store(0);
+  __syncthreads();
+  int buf = 0;
+  for (long long g0 = gs; g0 < ge; g0 += WG_ROWS) {
+    const bool more = g0 + WG_ROWS < ge;
+    if (more) load(g0 + WG_ROWS);
+    const bf16* tdy = sdy[buf];
+    const bf16* tx = sx[buf];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 fa[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        fa[m] = s ? frag_tr<1>(tdy, LDY, 32 * wave, 32 * m, lane) : frag_tr<0>(tdy, LDY, 32 * wave, 32 * m, lane);
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        const bf16x8 fb = s ? frag_tr<1>(tx, LDX, 32 * wave + d, 0, lane) : frag_tr<0>(tx, LDX, 32 * wave + d, 0, lane);
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[d][m] = mfma32(fa[m], fb, acc[d][m]);
+      }
+    }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  const int h = lane >> 5;
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    float* out = a.part + ((long long)(split * 4 + wave) * T + grp * 3 + d) * a.Cout * a.Cin;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = n0 + 32 * m + (i & 3) + 8 * (i >> 2) + 4 * h;
+        out[(long long)row * a.Cin + c0 + (lane & 31)] = acc[d][m][i];
+      }
+  }
+}
+
 template <int MT, int NT>
 static int launch_wgrad(const WgradArgs& a, int nsplit, hipStream_t st) {
   dim3 grid(a.KD * 9, nsplit, (a.Cout / (32 * MT)) * (a.Cin / (32 * NT)));
@@ -502,6 +615,19 @@ extern "C" int lci_conv3_wgrad(const void* x, const void* dy, float* part, int B
   a.Lv = (a.V + ns - 1) / ns;
   LCI_CHECK(ns < 65536, "conv3_wgrad: volume too large");
   hipStream_t st = (hipStream_t)stream;
+  static const bool wg3 = !getenv("LCI_WGRAD3") || atoi(getenv("LCI_WGRAD3")) != 0;   // A/B switch
+  if (wg3) {
+    const long long R = (a.V / W) * (W + 1);
+    a.Lv = (R + ns - 1) / ns;
+    static const int mt_env = getenv("LCI_WGRAD3_MT") ? atoi(getenv("LCI_WGRAD3_MT")) : 0;   // A/B override
+    const int mt = (mt_env > 0 && (Cout / 32) % mt_env == 0) ? mt_env : tile3(Cout);
+    dim3 grid(KD * 3, (unsigned)ns, (Cout / (32 * mt)) * (Cin / 32));
+    if (mt == 3) hipLaunchKernelGGL(conv3_wgrad3_kernel<3>, grid, dim3(256), 0, st, a);
+    else if (mt == 2) hipLaunchKernelGGL(conv3_wgrad3_kernel<2>, grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(conv3_wgrad3_kernel<1>, grid, dim3(256), 0, st, a);
+    LCI_LAUNCH_CHECK();
+    return 0;
+  }
   const int mt = tile3(Cout), nt = tile3(Cin);
 #define LCI_WG(M, N) if (mt == M && nt == N) return launch_wgrad<M, N>(a, (int)ns, st);
   LCI_WG(3, 3) LCI_WG(3, 2) LCI_WG(3, 1) LCI_WG(2, 3) LCI_WG(2, 2) LCI_WG(2, 1) LCI_WG(1, 3) LCI_WG(1, 2)
