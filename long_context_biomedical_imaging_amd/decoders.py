@@ -26,12 +26,17 @@ from . import kernels
 # A/B switch for the 2-D heads (the headline ViTUNETR at 512^2): HIP conv3 + inorm (default; same step time as
 # MIOpen at 512^2, without its ~2 min first-call solver search) vs torch/MIOpen (LCI_HIP_CONV_2D=0)
 HIP_CONV_2D = os.environ.get("LCI_HIP_CONV_2D", "1") != "0"
+# 3-D: HIP always in the product (MIOpen 3-D is ~40x slower here and refuses 256^3); the switch exists so the
+# parity tests can run the same modules through torch's fp32 / bf16 convolutions as references
+HIP_CONV_3D = os.environ.get("LCI_HIP_CONV_3D", "1") != "0"
 
 
 class Conv3x3(nn.Conv3d):
     """nn.Conv3d(cin, cout, 3, 1, padding=1, bias=False) computed by the HIP conv3 kernel."""
 
     def forward(self, x):
+        if not HIP_CONV_3D:
+            return super().forward(x)
         return kernels.conv3(x, self.weight)
 
 
@@ -134,10 +139,10 @@ class UnetResBlock(nn.Module):
 
         # channels-last HIP path: the convs are the HIP conv3 / GEMM forms and the instance norms (+ LeakyReLU)
         # the lci_inorm kernels, so the block never round-trips through NCDHW (2-D: only with HIP_CONV_2D)
-        self.fused = isinstance(self.conv1, (Conv3x3, Conv3x3_2d)) and cout % 8 == 0 and (nd == 3 or HIP_CONV_2D)
+        self.fused = isinstance(self.conv1, (Conv3x3, Conv3x3_2d)) and cout % 8 == 0
 
     def forward(self, inp):
-        if self.fused and inp.is_cuda:
+        if self.fused and inp.is_cuda and (HIP_CONV_3D if inp.dim() == 5 else HIP_CONV_2D):
             out = kernels.instance_norm_act(self.conv1(inp), True)
             out = kernels.instance_norm_act(self.conv2(out), False)
             res = kernels.instance_norm_act(self.conv3(inp), False) if self.downsample else inp
@@ -333,3 +338,186 @@ class SwinLinear(nn.Module):
 class Identity(nn.Module):
     def forward(self, x):
         return x
+
+
+# ----------------------------------------------------------------------------------------- UperNet heads
+# The UperNet convs return standard-layout tensors: BatchNorm / interpolate follow them, and torch's ROCm
+# batch_norm crashed (SIGSEGV) on channels-last views of 1x1-pixel pyramid maps.
+class ConvK3(nn.Conv3d):
+    """nn.Conv3d(cin, cout, 3, padding=1[, bias]) on the HIP conv3 kernel (any cout, optional bias)."""
+
+    def forward(self, x):
+        if not HIP_CONV_3D:
+            return super().forward(x)
+        return kernels.conv3(x, self.weight, self.bias).contiguous()
+
+
+class ConvK3_2d(nn.Conv2d):
+    def forward(self, x):
+        if not HIP_CONV_2D:
+            return super().forward(x)
+        return kernels.conv3(x, self.weight, self.bias).contiguous()
+
+
+class ConvPoint(nn.Conv3d):
+    """nn.Conv3d(cin, cout, 1, padding=p[, bias]) as one GEMM over channels-last voxels (zero border first)."""
+
+    def forward(self, x):
+        p = self.padding[0]
+        if p:
+            x = F.pad(x, (p,) * 6)
+        return _pointwise(x, self.weight, self.bias).contiguous()
+
+
+class ConvPoint_2d(nn.Conv2d):
+    def forward(self, x):
+        p = self.padding[0]
+        if p:
+            x = F.pad(x, (p,) * 4)
+        return _pointwise(x, self.weight, self.bias).contiguous()
+
+
+def _k3(nd, cin, cout, bias=True):
+    return (ConvK3_2d if nd == 2 else ConvK3)(cin, cout, kernel_size=3, padding=1, bias=bias)
+
+
+def _k1(nd, cin, cout, bias=True, padding=0):
+    return (ConvPoint_2d if nd == 2 else ConvPoint)(cin, cout, kernel_size=1, padding=padding, bias=bias)
+
+
+class BatchNorm2d(nn.BatchNorm2d):
+    """BatchNorm in f32 whatever the input dtype (output f32). Under bf16 autocast torch's ROCm batch_norm
+    segfaults on the 1x1-pixel maps of the PSP pyramid (bin 1); computing the statistics in f32 avoids that and
+    is at least as accurate as the reference's bf16 batch_norm. Same parameters/buffers as nn.BatchNorm2d."""
+
+    def forward(self, x):
+        return super().forward(x.float())
+
+
+class BatchNorm3d(nn.BatchNorm3d):
+    def forward(self, x):
+        return super().forward(x.float())
+
+
+def _bn(nd, c):
+    return (BatchNorm2d if nd == 2 else BatchNorm3d)(c)
+
+
+class PSPModule(nn.Module):
+    """seg_heads.py:18-47 (2-D) / :153-182 (3-D): adaptive-average-pool pyramid (bins 1, 2, 4, 6) -> 1x1 conv ->
+    BN -> ReLU, (bi|tri)linear up-sampling (align_corners=True), concat, and a 1x1 bottleneck conv whose
+    padding=1 grows the map by one voxel per side (kept: the FPN re-samples it), BN, ReLU, Dropout(0.1)."""
+
+    def __init__(self, nd, in_channels, bin_sizes=(1, 2, 4, 6)):
+        super().__init__()
+        self.nd = nd
+        out_channels = in_channels // len(bin_sizes)
+        pool = nn.AdaptiveAvgPool2d if nd == 2 else nn.AdaptiveAvgPool3d
+        self.stages = nn.ModuleList([nn.Sequential(pool(output_size=b), _k1(nd, in_channels, out_channels, False),
+                                                   _bn(nd, out_channels), nn.ReLU(inplace=True))
+                                     for b in bin_sizes])
+        self.bottleneck = nn.Sequential(
+            _k1(nd, in_channels + out_channels * len(bin_sizes), in_channels, bias=False, padding=1),
+            _bn(nd, in_channels), nn.ReLU(inplace=True), (nn.Dropout2d if nd == 2 else nn.Dropout3d)(0.1))
+
+    def forward(self, features):
+        size = features.shape[2:]
+        mode = "bilinear" if self.nd == 2 else "trilinear"
+        pyramids = [features] + [F.interpolate(stage(features), size=size, mode=mode, align_corners=True)
+                                 for stage in self.stages]
+        return self.bottleneck(torch.cat(pyramids, dim=1))
+
+
+class FPN_fuse(nn.Module):
+    """seg_heads.py:52-76 / :187-211: lateral 1x1 convs, top-down up-and-add, ONE 3x3 smoothing conv shared by
+    the three levels (the reference lists the same module three times), up-sample all to the finest level,
+    concat, 3x3 conv -> BN -> ReLU."""
+
+    def __init__(self, nd, feature_channels, fpn_out):
+        super().__init__()
+        assert feature_channels[0] == fpn_out
+        self.nd = nd
+        self.conv1x1 = nn.ModuleList([_k1(nd, c, fpn_out) for c in feature_channels[1:]])
+        self.smooth_conv = nn.ModuleList([_k3(nd, fpn_out, fpn_out)] * (len(feature_channels) - 1))
+        self.conv_fusion = nn.Sequential(_k3(nd, len(feature_channels) * fpn_out, fpn_out, bias=False),
+                                         _bn(nd, fpn_out), nn.ReLU(inplace=True))
+
+    def forward(self, features):
+        mode = "bilinear" if self.nd == 2 else "trilinear"
+        features = list(features)
+        features[1:] = [c(f) for f, c in zip(features[1:], self.conv1x1)]
+        up_add = lambda x, y: F.interpolate(x, size=y.shape[2:], mode=mode, align_corners=True) + y  # noqa: E731
+        P = [up_add(features[i], features[i - 1]) for i in reversed(range(1, len(features)))]
+        P = [sc(x) for sc, x in zip(self.smooth_conv, P)]
+        P = list(reversed(P))
+        P.append(features[-1])
+        size = P[0].shape[2:]
+        P[1:] = [F.interpolate(f, size=size, mode=mode, align_corners=True) for f in P[1:]]
+        return self.conv_fusion(torch.cat(P, dim=1))
+
+
+class _UperNet(nn.Module):
+    def __init__(self, nd, config, input_feature_channels, output_feature_channels):
+        super().__init__()
+        if config.encoder_name == "Swin":
+            self.upernet_feature_channels = [-4, -3, -2, -1]
+        elif config.encoder_name == "ViT":
+            self.upernet_feature_channels = [4, 7, 10, -1]
+        else:
+            raise ValueError(f"encoder_name {config.encoder_name} not recognized or comaptible with UperNet3D")
+        chans = [input_feature_channels[c] for c in self.upernet_feature_channels]
+        self.nd = nd
+        self.encoder_name = config.encoder_name
+        self.fpn_out = chans[0]
+        self.input_size = (config.height, config.width) if nd == 2 else (config.time, config.height, config.width)
+        self.PPN = PSPModule(nd, chans[-1])
+        self.FPN = FPN_fuse(nd, chans, self.fpn_out)
+        self.head = _k3(nd, self.fpn_out, output_feature_channels)
+        if config.encoder_name == "ViT":
+            patch = list(config.ViT.patch_size[1:]) if nd == 2 else list(config.ViT.patch_size)
+            self.feat_size = tuple(i // p for i, p in zip(self.input_size, patch))
+            self.proj_axes = (0, nd + 1) + tuple(d + 1 for d in range(nd))
+
+    def _reshape_vit_output(self, x):
+        x = x.view([x.size(0)] + list(self.feat_size) + [x.shape[-1]])
+        return x.permute(self.proj_axes).contiguous()
+
+    def freeze_bn(self):
+        for module in self.modules():
+            if isinstance(module, (nn.BatchNorm2d, nn.BatchNorm3d)):
+                module.eval()
+
+
+class UperNet2D(_UperNet):
+    """seg_heads.py:79-147: UperNet on the ViT token taps h4/h7/h10/final or the last four Swin stages (time axis
+    dropped), bilinear up-sampling to the image size (align_corners=False), 3x3 head, time axis re-inserted."""
+
+    def __init__(self, config, input_feature_channels, output_feature_channels):
+        super().__init__(2, config, input_feature_channels, output_feature_channels)
+
+    def forward(self, features):
+        features = [features[c] for c in self.upernet_feature_channels]
+        if self.encoder_name == "ViT":
+            features = [self._reshape_vit_output(f) for f in features]
+        else:
+            features = [f[:, :, 0, :, :] for f in features]
+        features[-1] = self.PPN(features[-1])
+        x = self.FPN(features)
+        x = F.interpolate(x, size=self.input_size, mode="bilinear")
+        return torch.unsqueeze(self.head(x), 2)
+
+
+class UperNet3D(_UperNet):
+    """seg_heads.py:214-277: the 3-D UperNet (trilinear), optional output_size."""
+
+    def __init__(self, config, input_feature_channels, output_feature_channels):
+        super().__init__(3, config, input_feature_channels, output_feature_channels)
+
+    def forward(self, features, output_size=None):
+        features = [features[c] for c in self.upernet_feature_channels]
+        if self.encoder_name == "ViT":
+            features = [self._reshape_vit_output(f) for f in features]
+        features[-1] = self.PPN(features[-1])
+        x = self.FPN(features)
+        x = F.interpolate(x, size=self.input_size if output_size is None else output_size, mode="trilinear")
+        return self.head(x)

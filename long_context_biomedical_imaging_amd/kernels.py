@@ -739,14 +739,22 @@ class _Conv3(torch.autograd.Function):
         return dx, dw, None
 
 
-def conv3(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
-    """Conv{2,3}d(kernel 3, stride 1, padding 1, no bias) in bf16 MFMA with f32 accumulation (the dtype
-    autocast gives the reference's conv). x (B, Cin, [D,] H, W) -> (B, Cout, [D,] H, W) bf16, channels-last
-    strides. Needs Cout % 32 == 0."""
+def conv3(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
+    """Conv{2,3}d(kernel 3, stride 1, padding 1) in bf16 MFMA with f32 accumulation (the dtype autocast gives
+    the reference's conv). x (B, Cin, [D,] H, W) -> (B, Cout, [D,] H, W) bf16, channels-last strides.
+    Cout not a multiple of 32 (a head's class count) runs on zero-padded weight rows and is sliced back."""
     _lib.require_gpu(weight)
     if not x.is_cuda:
         raise _lib.LciError("conv3 runs on the GPU only; there is no CPU path")
-    return _Conv3.apply(x, weight, weight.dim() - 2)
+    cout = weight.shape[0]
+    cp = -(-cout // 32) * 32
+    w = weight if cp == cout else torch.cat([weight, weight.new_zeros(cp - cout, *weight.shape[1:])])
+    y = _Conv3.apply(x, w, weight.dim() - 2)
+    if cp != cout:
+        y = y[:, :cout]
+    if bias is not None:
+        y = y + bias.to(y.dtype).view(1, -1, *([1] * (y.dim() - 2)))
+    return y
 
 
 # ------------------------------------------------------- decoder-head instance norm (+ LeakyReLU), channels-last

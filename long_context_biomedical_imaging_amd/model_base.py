@@ -5,7 +5,7 @@ import torch.nn as nn
 
 from .backbone_swin import custom_Swin
 from .backbone_vit import custom_ViT
-from .decoders import Identity, SwinLinear, SwinUNETR, ViTLinear, ViTUNETR
+from .decoders import Identity, SwinLinear, SwinUNETR, UperNet2D, UperNet3D, ViTLinear, ViTUNETR
 
 
 def identity_model(config, input_feature_channels):
@@ -38,9 +38,10 @@ class EncoderDecoderModel(nn.Module):
             self.decoder = ViTUNETR(config, self.encoder_feature_channels, output_feature_channels)
         elif decoder_name == "SwinUNETR":
             self.decoder = SwinUNETR(config, self.encoder_feature_channels, output_feature_channels)
-        elif decoder_name in ("UperNet2D", "UperNet3D"):
-            raise NotImplementedError(f"Decoder {decoder_name}: MONAI/torchvision conv decoder outside the "
-                                      "mixer hot path (SURVEY.md §8(f) rank 2); not built yet")
+        elif decoder_name == "UperNet2D":
+            self.decoder = UperNet2D(config, self.encoder_feature_channels, output_feature_channels)
+        elif decoder_name == "UperNet3D":
+            self.decoder = UperNet3D(config, self.encoder_feature_channels, output_feature_channels)
         else:
             raise NotImplementedError(f"Decoder not implemented: {decoder_name}")
 

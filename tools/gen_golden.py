@@ -33,6 +33,7 @@ import backbone_swin as rswin  # noqa: E402
 import backbone_vit as rvit  # noqa: E402
 import hyena as rhyena  # noqa: E402
 import mamba as rmamba  # noqa: E402
+import seg_heads as rseg  # noqa: E402
 
 BIG = ("filter_fn.pos_emb.z", "filter_fn.pos_emb.t")
 
@@ -246,6 +247,57 @@ def train_step(seed):
     dump("train_step", None, **arr)
 
 
+class _Cfg:
+    """The config fields UperNet2D/3D read (seg_heads.py:96-117, 248-269)."""
+
+    def __init__(self, encoder_name, time, height, width, patch):
+        self.encoder_name, self.time, self.height, self.width = encoder_name, time, height, width
+        self.ViT = type("V", (), {"patch_size": patch})()
+
+
+def upernet(name, nd, encoder, seed):
+    """UperNet2D/3D (seg_heads.py:79-277) in training mode (BatchNorm batch statistics) with the PSP dropout set
+    to p = 0, fed a Swin-like (5 stage taps + image) or ViT-like (13 token taps + image) feature list."""
+    torch.manual_seed(seed)
+    if encoder == "Swin":
+        chans = [1, 8, 16, 32, 64, 128]
+        S = (8, 16, 16) if nd == 3 else (1, 32, 32)
+        shapes = [(2, 1) + S] + [(2, c) + tuple(max(1, s // 2 ** (i + 1)) if (nd == 3 or k > 0) else 1
+                                            for k, s in enumerate(S)) for i, c in enumerate(chans[1:])]
+        cfg = _Cfg("Swin", S[0], S[1], S[2], None)
+    else:
+        chans = [1] + [32] * 13
+        S = (8, 16, 16) if nd == 3 else (1, 32, 32)
+        patch = (2, 4, 4) if nd == 3 else (1, 4, 4)
+        L = 1
+        for s, p in zip(S, patch):
+            L *= s // p
+        shapes = [(2, 1) + S] + [(2, L, 32)] * 13
+        cfg = _Cfg("ViT", S[0], S[1], S[2], patch)
+    cls = rseg.UperNet3D if nd == 3 else rseg.UperNet2D
+    m = cls(cfg, chans, 3).train()
+    m.PPN.bottleneck[3].p = 0.0
+    feats = [torch.randn(s) for s in shapes]
+    idx = [c % len(feats) for c in m.upernet_feature_channels]
+    ins = [f.clone().requires_grad_(True) if i in idx else f for i, f in enumerate(feats)]
+    sd0 = {k: v.clone() for k, v in m.state_dict().items()}
+    out = m(list(ins))
+    cot = torch.randn(out.shape, generator=torch.Generator().manual_seed(123))
+    m.zero_grad(set_to_none=True)
+    (out * cot).sum().backward()
+    arr = {f"in/f{i}": f for i, f in enumerate(feats)}
+    arr["out/0"] = out
+    for i in idx:
+        arr[f"grad/f{i}"] = ins[i].grad
+    params = dict(m.named_parameters())
+    for p in ("head.weight", "FPN.conv_fusion.0.weight", "FPN.smooth_conv.0.weight", "PPN.bottleneck.0.weight",
+              "PPN.stages.0.1.weight"):
+        arr[f"grad/{p}"] = params[p].grad
+    for k, v in sd0.items():
+        arr[f"sd/{k}"] = v
+    dump(name, None, **arr)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(min(8, os.cpu_count() or 1))
@@ -261,6 +313,10 @@ def main():
     swin_layer(9)
     swin_index()
     train_step(10)
+    upernet("upernet2d_swin", 2, "Swin", 11)
+    upernet("upernet2d_vit", 2, "ViT", 12)
+    upernet("upernet3d_swin", 3, "Swin", 13)
+    upernet("upernet3d_vit", 3, "ViT", 14)
 
 
 if __name__ == "__main__":

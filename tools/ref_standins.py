@@ -7,6 +7,7 @@ Each class restates the *published behaviour* of the pinned dependency version:
   - monai==1.3.0  (requirements.txt:5)   PatchEmbeddingBlock, PatchEmbed, MLPBlock, trunc_normal_,
                                           ensure_tuple_rep, look_up_option, optional_import
   - timm==0.9.2   (requirements.txt:13)  only names imported by mamba.py:22-23 (unused in forward)
+  - torchvision==0.16.1 (README.md:12)  imported by seg_heads.py, unused: an empty module
   - mamba-ssm==1.2.0.post1 (README.md:15) selective_scan_fn -> selective_scan_ref semantics
     (mamba_ssm/ops/selective_scan_interface.py: per-step recurrence, fp32 math, output in u.dtype)
 """
@@ -226,6 +227,7 @@ def install():
     mod("timm.models")
     mod("timm.models.layers", trunc_normal_=trunc_normal_, DropPath=DropPath, LayerNorm2d=nn.LayerNorm)
     mod("timm.models.vision_transformer", Mlp=MLPBlock)
+    mod("torchvision")   # seg_heads.py:11 imports it but its UperNet code never uses it (torchvision 0.16.1)
     mod("mamba_ssm")
     mod("mamba_ssm.ops")
     mod("mamba_ssm.ops.selective_scan_interface", selective_scan_fn=selective_scan_fn,
