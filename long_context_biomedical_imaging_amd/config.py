@@ -56,6 +56,12 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--no_in_channel", type=int, default=1)
     p.add_argument("--no_out_channel", type=int, default=2)
     p.add_argument("--batch_size", type=int, default=2)
+    # general_parser.py:31-32, 70-72 (data.NumpyDataset)
+    p.add_argument("--data_dir", type=str, default="data")
+    p.add_argument("--split_csv_path", type=lambda v: None if v in (None, "None", "none") else v, default=None)
+    p.add_argument("--affine_aug", type=str_to_bool, default=True)
+    p.add_argument("--brightness_aug", type=str_to_bool, default=True)
+    p.add_argument("--gaussian_blur_aug", type=str_to_bool, default=True)
     p.add_argument("--use_amp", action="store_true")
     p.add_argument("--ddp", action="store_true")
     p.add_argument("--optim_type", type=str, default="adam", choices=["adam", "adamw", "sgd"])
