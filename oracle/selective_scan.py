@@ -25,16 +25,17 @@ def selective_scan(u, delta, A, B, C, D=None, delta_bias=None, delta_softplus=Tr
     size of the exp(delta A) temporaries at large L).
     """
     dtype_in = u.dtype
-    u = u.float()
-    delta = delta.float()
+    ct = torch.promote_types(u.dtype, torch.float32)   # f32 math as mamba-ssm; f64 inputs stay f64 (gradcheck)
+    u = u.to(ct)
+    delta = delta.to(ct)
     if delta_bias is not None:
-        delta = delta + delta_bias[..., None].float()
+        delta = delta + delta_bias[..., None].to(ct)
     if delta_softplus:
         delta = F.softplus(delta)
     b, d, L = u.shape
-    A = A.float()
-    B = B.float()
-    C = C.float()
+    A = A.to(ct)
+    B = B.to(ct)
+    C = C.to(ct)
     x = A.new_zeros((b, d, A.shape[1]))
     chunk = chunk or L
     ys = []
@@ -47,7 +48,7 @@ def selective_scan(u, delta, A, B, C, D=None, delta_bias=None, delta_softplus=Tr
             ys.append(torch.einsum("bdn,bn->bd", x, C[:, :, s + i]))
     y = torch.stack(ys, dim=2)
     if D is not None:
-        y = y + u * D[:, None].float()
+        y = y + u * D[:, None].to(ct)
     return y.to(dtype_in)
 
 

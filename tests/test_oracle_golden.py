@@ -187,3 +187,25 @@ def test_patch_embed_vit_block():
                                     sd["patch_embedding.patch_embeddings.bias"],
                                     sd["patch_embedding.position_embeddings"])
     assert y.shape == (2, 64, 128)
+
+
+def test_oracle_gradients_fp64_gradcheck():
+    """the CPU restatements' autograd gradients (which the GPU backward kernels are checked
+    against) are verified by finite differences in fp64."""
+    from torch.autograd import gradcheck
+    from oracle import attention as oatt
+    from oracle import hyena as ohy
+    from oracle import selective_scan as oss
+    from oracle import window as owin
+    g = torch.Generator().manual_seed(0)
+    r = lambda *s: torch.randn(*s, generator=g, dtype=torch.float64).requires_grad_(True)   # noqa: E731
+    q, k, v = r(1, 2, 5, 4), r(1, 2, 5, 4), r(1, 2, 5, 4)
+    assert gradcheck(lambda a, b, c: oatt.attention_core(a, b, c, 0.5), (q, k, v))
+    rpb, mask = r(2, 5, 5), torch.zeros(1, 5, 5, dtype=torch.float64)
+    mask[0, 0, 3:] = -100.0
+    assert gradcheck(lambda a, b, c, p: owin.window_attention_core(a, b, c, p, mask, 0.5), (q, k, v, rpb))
+    u, dt, A = r(1, 3, 6), r(1, 3, 6), (-torch.rand(3, 2, generator=g, dtype=torch.float64)).requires_grad_(True)
+    B, C, D, db = r(1, 2, 6), r(1, 2, 6), r(3), r(3)
+    assert gradcheck(lambda *a: oss.selective_scan(*a, delta_softplus=True), (u, dt, A, B, C, D, db))
+    uu, kk, dd = r(2, 3, 8), r(3, 8), r(3)
+    assert gradcheck(ohy.fftconv, (uu, kk, dd))
