@@ -108,3 +108,33 @@ def test_swin_unetr_head_construction():
     cfg.encoder_name = "ViT"
     with pytest.raises(ValueError):
         SwinUNETR(cfg, [96, 192, 384, 768, 1536], 2)
+
+
+def test_checkpoint_roundtrip_and_ddp_prefix(tmp_path):
+    """model_utils.save_model / load_model (model/model_utils.py:13-77): round trip with optimizer state, config
+    stored as plain data (weights_only load), and the `module.` prefix reconciled both ways."""
+    import torch
+    from long_context_biomedical_imaging_amd import config as lconfig
+    from long_context_biomedical_imaging_amd.model_base import EncoderDecoderModel
+    from long_context_biomedical_imaging_amd.model_utils import load_model, save_model
+    cfg = lconfig.parse_config(["--encoder_name", "ViT", "--decoder_name", "ViTLinear", "--task_type", "class",
+                                "--height", "32", "--width", "32", "--ViT.patch_size", "1", "8", "8"])
+    torch.manual_seed(0)
+    a = EncoderDecoderModel(cfg, "ViT", "ViTLinear", 1, 3)
+    opt = torch.optim.Adam(a.parameters())
+    path = save_model(cfg, a, save_dir=str(tmp_path), epoch=3, optim=opt)
+    torch.manual_seed(1)
+    b = EncoderDecoderModel(cfg, "ViT", "ViTLinear", 1, 3)
+    load_model(b, path)
+    for (k, x), (_, y) in zip(a.state_dict().items(), b.state_dict().items()):
+        assert torch.equal(x, y), k
+    saved = torch.load(path, weights_only=True)
+    assert saved["epoch"] == 3 and saved["config"]["encoder_name"] == "ViT" and "optim_state" in saved
+    wrapped = torch.nn.Module()
+    wrapped.module = EncoderDecoderModel(cfg, "ViT", "ViTLinear", 1, 3)      # DDP-style keys
+    load_model(wrapped, path)
+    assert torch.equal(wrapped.module.encoder.blocks[0].attn.qkv.weight, a.encoder.blocks[0].attn.qkv.weight)
+    p2 = save_model(cfg, wrapped, save_dir=str(tmp_path), save_filename="ddp")
+    c = EncoderDecoderModel(cfg, "ViT", "ViTLinear", 1, 3)
+    load_model(c, p2)
+    assert torch.equal(c.encoder.norm.weight, a.encoder.norm.weight)
