@@ -32,7 +32,8 @@ sys.path.insert(0, ROOT)
 from long_context_biomedical_imaging_amd import config as lconfig  # noqa: E402
 from long_context_biomedical_imaging_amd import kernels  # noqa: E402
 from long_context_biomedical_imaging_amd.model_base import EncoderDecoderModel  # noqa: E402
-from long_context_biomedical_imaging_amd.trainer import TrainStep, init_distributed, synthetic_batch  # noqa: E402
+from long_context_biomedical_imaging_amd.trainer import (TrainStep, init_distributed, synthetic_batch,  # noqa: E402
+                                                         use_tuned_gemms)
 
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # dense bf16, MI355X_MICROARCH.md chip table
 HBM_PEAK_GBS = 8000.0
@@ -239,6 +240,7 @@ def main():
     rank, local, world = init_distributed()
     device = torch.device("cuda", local % torch.cuda.device_count())   # % : gloo rehearsals on one GPU
     torch.cuda.set_device(device)
+    tuned = use_tuned_gemms()
     res = run_workload(args.workload, args.batch, args.steps, args.warmup, rank, world, device)
     if args.workload == "vit_p2_512" and not args.no_secondary:
         # north_star also asks for tokens/s on 128^3 patch-2 volumes (BASELINE configs[2], Swin + SwinUNETR):
@@ -251,6 +253,7 @@ def main():
             keep = ("metric", "value", "unit", "ms_per_step", "steps", "warmup", "config", "roofline", "kernels")
             res["secondary"] = {"swin_p2_128": {k: sec[k] for k in keep if k in sec} if "error" not in sec else sec}
     if rank == 0:
+        res["config"]["tuned_gemms"] = tuned
         if world == 1 and not args.no_cpu_baseline and args.workload == "vit_p2_512":
             res["cpu_baseline"] = cpu_baseline(args.cpu_budget)
         print(json.dumps(res), flush=True)

@@ -36,6 +36,27 @@ def init_distributed():
     return rank, local, world
 
 
+TUNED_GEMMS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tunableop_gfx950.csv")
+
+
+def use_tuned_gemms(path: str = TUNED_GEMMS) -> bool:
+    """Route torch's Linear / matmul GEMMs through PyTorch-ROCm TunableOp with the solutions recorded for this
+    package's shapes on MI355X (hipBLASLt / rocBLAS solution ids, written by a tuning run of bench.py with
+    PYTORCH_TUNABLEOP_ENABLED=1; e.g. the ViT-small qkv projection at L = 65536: 0.58 -> 0.15 ms). Tuning itself
+    stays off (it costs ~2 min per workload on first use); shapes absent from the file keep the default
+    heuristics, and a file recorded under another PyTorch / ROCm / hipBLASLt / arch is rejected by TunableOp's
+    validators. LCI_TUNED_GEMMS=0 disables. Returns whether the table is active."""
+    if os.environ.get("LCI_TUNED_GEMMS", "1") == "0" or not os.path.exists(path) or not torch.cuda.is_available():
+        return False
+    import torch.cuda.tunable as tunable
+    tunable.enable(True)
+    tunable.tuning_enable(False)
+    # anything TunableOp writes at exit goes to the temp dir, never over the shipped table
+    import tempfile
+    tunable.set_filename(os.path.join(tempfile.gettempdir(), f"lci_tunableop_{os.getpid()}.csv"))
+    return bool(tunable.read_file(path))
+
+
 def build_optimizer(params, config):
     o = config.optim
     if config.optim_type == "adam":
