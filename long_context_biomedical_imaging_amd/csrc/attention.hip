@@ -399,19 +399,19 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnArgs a) {
 }
 
 // ---------------------------------------------------------------------- backward: dK, dV kernel
-template <int NW>
-__global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv_kernel(AttnArgs a) {
+// KB key blocks of 32 per wave (key on the MFMA lane). With KB = 2 every Q / dO fragment read from LDS (row
+// fragments of the S and dP chains, transposed fragments of the dV / dK products) feeds two key blocks: half the
+// LDS read cycles per MFMA, at one wave per SIMD (the second key block's chains are the in-wave ILP).
+template <int NW, int KB>
+__global__ __launch_bounds__(NW * 64, (KB == 1 ? 8 / NW : 4 / NW)) void attn_bwd_dkdv_kernel(AttnArgs a) {
   constexpr int NT = NW * 64;
   constexpr int TILE = 2 * KT * LD_SW;                  // Q tile + dO tile (both read by rows and transposed)
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * TILE];
-#ifdef LCI_DKDV_ROWC
-  __shared__ __attribute__((aligned(16))) float rowc[2][2][KT];  // [buf][lse2 | delta][query]
-#endif
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int hh = blockIdx.y, b = blockIdx.z;
   const int L = a.L;
   const int half = lane >> 5;
-  const int key = blockIdx.x * (NW * 32) + wave * 32 + (lane & 31);
+  const int key0 = blockIdx.x * (NW * 32 * KB) + wave * (32 * KB) + (lane & 31);
 
   const bf16* qp = a.q + b * a.bs_q + hh * a.hs;
   const bf16* dop = a.dout + b * a.bs_do + hh * a.hs;
@@ -419,27 +419,30 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv_kernel(AttnArgs
   const float* dlp = a.delta + ((long long)b * a.H + hh) * L;
 
   // K^T and V^T as B operands: lane (key r, half h) holds K[key][16ks+8h..], V[key][16ks+8h..]
-  bf16x8 kf[4], vf[4];
+  bf16x8 kf[KB][4], vf[KB][4];
   {
     const bf16* kp = a.k + b * a.bs_k + hh * a.hs;
     const bf16* vp = a.v + b * a.bs_v + hh * a.hs;
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      if (key < L) {
-        kf[ks] = *(const bf16x8*)(kp + (long long)key * a.rs_k + ks * 16 + 8 * half);
-        vf[ks] = *(const bf16x8*)(vp + (long long)key * a.rs_v + ks * 16 + 8 * half);
-      } else {
-        kf[ks] = bf16x8{};
-        vf[ks] = bf16x8{};
-      }
+    for (int kb = 0; kb < KB; ++kb) {
+      const int key = key0 + 32 * kb;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) kf[ks][j] = to_bf16(to_f32(kf[ks][j]) * a.c);  // scores in the exp2 domain
+      for (int ks = 0; ks < 4; ++ks) {
+        if (key < L) {
+          kf[kb][ks] = *(const bf16x8*)(kp + (long long)key * a.rs_k + ks * 16 + 8 * half);
+          vf[kb][ks] = *(const bf16x8*)(vp + (long long)key * a.rs_v + ks * 16 + 8 * half);
+        } else {
+          kf[kb][ks] = bf16x8{};
+          vf[kb][ks] = bf16x8{};
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) kf[kb][ks][j] = to_bf16(to_f32(kf[kb][ks][j]) * a.c);  // exp2-domain scores
+      }
     }
   }
 
   TileRegs<NT> qr, dr;
   const int nqt = (L + KT - 1) / KT;
-#ifndef LCI_DKDV_ROWC
   // Row constants as an extra k-step of the S and dP chains: columns 64..79 of each staged Q (dO) row hold
   // -lse2 (-delta) split into three bf16 terms (hi + mid + lo carries ~24 bits), and the matching B fragment is
   // 1 in rows 0..2. The chains then yield S c - lse2 and dP - delta with no per-lane row-constant loads
@@ -460,17 +463,6 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv_kernel(AttnArgs
   };
   bf16x8 onef{};
   if (half == 0) { onef[0] = to_bf16(1.f); onef[1] = onef[0]; onef[2] = onef[0]; }
-#else
-  auto stage_rowc = [&](int buf, int qt) __attribute__((always_inline)) {
-    if (tid < 2 * KT) {
-      const int which = tid / KT, qi = tid % KT, q = qt * KT + qi;
-      float v;  // stored negated: they are the initial accumulators of the S and dP MFMA chains
-      if (which == 0) v = (q < L) ? -lsep[q] : -1.0e30f;  // invalid rows: P = exp2(-huge) = 0
-      else v = (q < L) ? -dlp[q] : 0.f;
-      rowc[buf][which][qi] = v;
-    }
-  };
-#endif
   qr.load(qp, a.rs_q, 0, L, tid);
   dr.load(dop, a.rs_do, 0, L, tid);
   qr.store_sw(smem, tid);
@@ -478,8 +470,9 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv_kernel(AttnArgs
   stage_rowc(0, 0);
   __syncthreads();
 
-  f32x16 dv0 = {}, dv1 = {}, dk0 = {}, dk1 = {};
-  const float c = a.c;
+  f32x16 dv0[KB], dv1[KB], dk0[KB], dk1[KB];
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) dv0[kb] = dv1[kb] = dk0[kb] = dk1[kb] = f32x16{};
   for (int qt = 0; qt < nqt; ++qt) {
     const int buf = qt & 1;
     const bf16* ql = smem + buf * TILE;
@@ -492,44 +485,49 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv_kernel(AttnArgs
     // Two 32-query halves per 64-query tile (halves the live S/dP/P/dS registers); key on the lane.
 #pragma unroll
     for (int qs = 0; qs < 2; ++qs) {
-      // Row constants as the initial accumulators (q = qs*32 + (i&3) + 8(i>>2) + 4h): the chains give
-      // S c - lse2[q] and dP - delta[q] directly; then P = exp2(.), dS = P (dP - delta).
-      f32x16 s, p;
-#ifndef LCI_DKDV_ROWC
-      s = mfma32(frag_row_sw(ql, qs * 32, 64, lane), onef, f32x16{});
-      p = mfma32(frag_row_sw(dl, qs * 32, 64, lane), onef, f32x16{});
-#else
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 la = *(const f32x4*)&rowc[buf][0][qs * 32 + 8 * g + 4 * half];
-        const f32x4 da = *(const f32x4*)&rowc[buf][1][qs * 32 + 8 * g + 4 * half];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          s[4 * g + j] = la[j];
-          p[4 * g + j] = da[j];
-        }
-      }
-#endif
+      // Row constants enter as the extra k-step: the chains give S c - lse2[q] and dP - delta[q] directly;
+      // then P = exp2(.), dS = P (dP - delta).
+      bf16x8 qa[5], da[5];
+      qa[4] = frag_row_sw(ql, qs * 32, 64, lane);
+      da[4] = frag_row_sw(dl, qs * 32, 64, lane);
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        s = mfma32(frag_row_sw(ql, qs * 32, ks * 16, lane), kf[ks], s);
-        p = mfma32(frag_row_sw(dl, qs * 32, ks * 16, lane), vf[ks], p);
+        qa[ks] = frag_row_sw(ql, qs * 32, ks * 16, lane);
+        da[ks] = frag_row_sw(dl, qs * 32, ks * 16, lane);
       }
+      f32x16 s[KB], p[KB];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        s[i] = exp2_fast(s[i]);
-        p[i] = s[i] * p[i];
+      for (int kb = 0; kb < KB; ++kb) {
+        s[kb] = mfma32(qa[4], onef, f32x16{});
+        p[kb] = mfma32(da[4], onef, f32x16{});
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          s[kb] = mfma32(qa[ks], kf[kb][ks], s[kb]);
+          p[kb] = mfma32(da[ks], vf[kb][ks], p[kb]);
+        }
       }
-      const bf16x8 P0 = pack8<0>(s), P1 = pack8<1>(s), D0 = pack8<0>(p), D1 = pack8<1>(p);
-      // dV^T[d][key] += dO^T[d][q] P[q][key] ; dK^T[d][key] += Q^T[d][q] dS[q][key]
-      dv0 = mfma32(frag_tr_sw<0>(dl, qs * 32, 0, lane), P0, dv0);
-      dv0 = mfma32(frag_tr_sw<1>(dl, qs * 32, 0, lane), P1, dv0);
-      dv1 = mfma32(frag_tr_sw<0>(dl, qs * 32, 32, lane), P0, dv1);
-      dv1 = mfma32(frag_tr_sw<1>(dl, qs * 32, 32, lane), P1, dv1);
-      dk0 = mfma32(frag_tr_sw<0>(ql, qs * 32, 0, lane), D0, dk0);
-      dk0 = mfma32(frag_tr_sw<1>(ql, qs * 32, 0, lane), D1, dk0);
-      dk1 = mfma32(frag_tr_sw<0>(ql, qs * 32, 32, lane), D0, dk1);
-      dk1 = mfma32(frag_tr_sw<1>(ql, qs * 32, 32, lane), D1, dk1);
+      const bf16x8 tdo00 = frag_tr_sw<0>(dl, qs * 32, 0, lane), tdo10 = frag_tr_sw<1>(dl, qs * 32, 0, lane);
+      const bf16x8 tdo01 = frag_tr_sw<0>(dl, qs * 32, 32, lane), tdo11 = frag_tr_sw<1>(dl, qs * 32, 32, lane);
+      const bf16x8 tq00 = frag_tr_sw<0>(ql, qs * 32, 0, lane), tq10 = frag_tr_sw<1>(ql, qs * 32, 0, lane);
+      const bf16x8 tq01 = frag_tr_sw<0>(ql, qs * 32, 32, lane), tq11 = frag_tr_sw<1>(ql, qs * 32, 32, lane);
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          s[kb][i] = exp2_fast(s[kb][i]);
+          p[kb][i] = s[kb][i] * p[kb][i];
+        }
+        const bf16x8 P0 = pack8<0>(s[kb]), P1 = pack8<1>(s[kb]), D0 = pack8<0>(p[kb]), D1 = pack8<1>(p[kb]);
+        // dV^T[d][key] += dO^T[d][q] P[q][key] ; dK^T[d][key] += Q^T[d][q] dS[q][key]
+        dv0[kb] = mfma32(tdo00, P0, dv0[kb]);
+        dv0[kb] = mfma32(tdo10, P1, dv0[kb]);
+        dv1[kb] = mfma32(tdo01, P0, dv1[kb]);
+        dv1[kb] = mfma32(tdo11, P1, dv1[kb]);
+        dk0[kb] = mfma32(tq00, D0, dk0[kb]);
+        dk0[kb] = mfma32(tq10, D1, dk0[kb]);
+        dk1[kb] = mfma32(tq01, D0, dk1[kb]);
+        dk1[kb] = mfma32(tq11, D1, dk1[kb]);
+      }
     }
     if (qt + 1 < nqt) {
       bf16* nb = smem + (buf ^ 1) * TILE;
@@ -540,24 +538,28 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv_kernel(AttnArgs
     __syncthreads();
   }
 
-  if (key < L) {
-    bf16* dkp = a.dk + b * a.bs_dk + (long long)key * a.rs_dk + hh * a.hs;
-    bf16* dvp = a.dv + b * a.bs_dv + (long long)key * a.rs_dv + hh * a.hs;
-    const float sc = a.scale;
+  const float sc = a.scale;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      bf16x4 k0, k1, v0, v1;
+  for (int kb = 0; kb < KB; ++kb) {
+    const int key = key0 + 32 * kb;
+    if (key < L) {
+      bf16* dkp = a.dk + b * a.bs_dk + (long long)key * a.rs_dk + hh * a.hs;
+      bf16* dvp = a.dv + b * a.bs_dv + (long long)key * a.rs_dv + hh * a.hs;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        k0[j] = to_bf16(dk0[4 * g + j] * sc);
-        k1[j] = to_bf16(dk1[4 * g + j] * sc);
-        v0[j] = to_bf16(dv0[4 * g + j]);
-        v1[j] = to_bf16(dv1[4 * g + j]);
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 k0, k1, v0, v1;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          k0[j] = to_bf16(dk0[kb][4 * g + j] * sc);
+          k1[j] = to_bf16(dk1[kb][4 * g + j] * sc);
+          v0[j] = to_bf16(dv0[kb][4 * g + j]);
+          v1[j] = to_bf16(dv1[kb][4 * g + j]);
+        }
+        *(bf16x4*)(dkp + 8 * g + 4 * half) = k0;
+        *(bf16x4*)(dkp + 32 + 8 * g + 4 * half) = k1;
+        *(bf16x4*)(dvp + 8 * g + 4 * half) = v0;
+        *(bf16x4*)(dvp + 32 + 8 * g + 4 * half) = v1;
       }
-      *(bf16x4*)(dkp + 8 * g + 4 * half) = k0;
-      *(bf16x4*)(dkp + 32 + 8 * g + 4 * half) = k1;
-      *(bf16x4*)(dvp + 8 * g + 4 * half) = v0;
-      *(bf16x4*)(dvp + 32 + 8 * g + 4 * half) = v1;
     }
   }
 }
@@ -774,14 +776,18 @@ extern "C" int lci_attn_bwd_stage(int stage, const void* qkv, const void* out, c
 #ifndef LCI_BWD_NW
 #define LCI_BWD_NW 8   // 8 waves share each staged Q/dO (K/V) tile: -4% dK/dV, -8% dQ vs 4
 #endif
-  constexpr int NW = LCI_BWD_NW;
-  dim3 grid((L + NW * 32 - 1) / (NW * 32), H, B);
+#ifndef LCI_DKDV_KB
+#define LCI_DKDV_KB 1
+#endif
+  constexpr int KB = LCI_DKDV_KB;
+  constexpr int NW = KB == 1 ? LCI_BWD_NW : 4;   // KB = 2: one wave per SIMD
+  dim3 grid((L + NW * 32 * KB - 1) / (NW * 32 * KB), H, B);
   if (stage < 0 || stage == 0) {
     hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((L + 31) / 32, H, B), dim3(256), 0, s, a);
     LCI_LAUNCH_CHECK();
   }
   if (stage < 0 || stage == 1) {
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<NW>, grid, dim3(NW * 64), 0, s, a);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<NW, KB>), grid, dim3(NW * 64), 0, s, a);
     LCI_LAUNCH_CHECK();
   }
   if (stage < 0 || stage == 2) {
