@@ -40,7 +40,9 @@ HBM_PEAK_GBS = 8000.0
 # kernels whose roofline is HBM: algorithmic bytes per unit of KernelTimer work (scan units are
 # tokens at Dx = 192, N = 8, bf16 I/O; FFT-conv units are row-elements, f32 in/out). Others: MFMA FLOPs.
 ROOF = {"selective_scan_fwd": ("hbm", 1184.0), "selective_scan_bwd": ("hbm", 1984.0),
-        "fftconv_fwd": ("hbm", 8.0), "fftconv_bwd": ("hbm", 16.0)}
+        "fftconv_fwd": ("hbm", 8.0), "fftconv_bwd": ("hbm", 16.0),
+        # LayerNorm work is counted in bytes already (f32 x in, bf16 y out; bwd + bf16 dy in, f32 dx out)
+        "ln_fwd": ("hbm", 1.0), "ln_bwd": ("hbm", 1.0)}
 
 WORKLOADS = {
     # metric config (BASELINE.json `metric`, configs[1] shape at patch 2): ViT-small, patch 2, 512x512 -> L = 65536

@@ -22,6 +22,8 @@
  *   lci_conv3_fwd         MONAI-1.3 UnetResBlock 3x3(x3) convs of the ViTUNETR / SwinUNETR heads, enhance_heads.py:30-356
  *   lci_inorm_*           MONAI-1.3 UnetResBlock InstanceNorm (+ LeakyReLU) of the same heads
  *   lci_patch_embed_*     MONAI-1.3 PatchEmbeddingBlock (backbone_vit.py:351-361) / PatchEmbed (backbone_swin.py:800-806)
+ *   lci_layernorm_*       TransformerBlock norm1 / norm2 (nn.LayerNorm, backbone_vit.py:253-263) + the autocast cast
+ *                         of its output to the next Linear's bf16 operand
  */
 #ifndef LCI_H_
 #define LCI_H_
@@ -172,6 +174,19 @@ int lci_patch_embed_fwd(const void* x, int x_dtype, const float* w, const float*
 int lci_patch_embed_bwd(const void* x, int x_dtype, const void* dy, int dy_dtype, float* dw, float* db, float* dpos,
                         int B, int C, int D, int nd, const int* img_size, const int* patch, int channels_last,
                         void* stream);
+
+/* ------------------------------------------------------------------ transformer-block LayerNorm
+ * x (rows, C) f32 residual stream, C % 4 == 0, C <= 1024; gamma, beta (C) f32; eps as nn.LayerNorm's.
+ * fwd: y (rows, C) = bf16 when bf16_out (the value autocast would hand the next Linear) else f32;
+ *      mean, rstd (rows) f32 (biased variance, as torch).
+ * bwd: dy (rows, C) bf16 when bf16_dy else f32; dx (rows, C) f32 written; part (lci_layernorm_bwd_blocks(rows),
+ *      2, C) f32 written with per-workgroup partial sums of (dy * n, dy), n = (x - mean) * rstd: the caller sums
+ *      them over the first axis for dgamma, dbeta. */
+int lci_layernorm_bwd_blocks(long long rows);
+int lci_layernorm_fwd(const float* x, const float* gamma, const float* beta, void* y, int bf16_out, float* mean,
+                      float* rstd, long long rows, int C, float eps, void* stream);
+int lci_layernorm_bwd(const float* x, const void* dy, int bf16_dy, const float* gamma, const float* mean,
+                      const float* rstd, float* dx, float* part, long long rows, int C, void* stream);
 
 #ifdef __cplusplus
 }

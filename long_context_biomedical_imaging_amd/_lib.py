@@ -45,6 +45,8 @@ SIGNATURES = {
     "lci_conv3_wgrad": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "lci_inorm_reduce": [_P, _P, _P, _P, _L, _I, _I, _I, _F, _P],
     "lci_inorm_apply": [_P, _P, _P, _P, _P, _L, _I, _I, _I, _F, _P],
+    "lci_layernorm_fwd": [_P, _P, _P, _P, _I, _P, _P, _L, _I, _F, _P],
+    "lci_layernorm_bwd": [_P, _P, _I, _P, _P, _P, _P, _P, _L, _I, _P],
     "lci_dwconv_silu_bwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
 }
 
@@ -76,6 +78,8 @@ def load(path: str = LIB_PATH):
     lib.lci_conv3_wgrad_splits.argtypes = [ctypes.c_longlong, _I, _I, _I]
     lib.lci_inorm_chunks.restype = ctypes.c_int
     lib.lci_inorm_chunks.argtypes = [ctypes.c_longlong, _I]
+    lib.lci_layernorm_bwd_blocks.restype = ctypes.c_int
+    lib.lci_layernorm_bwd_blocks.argtypes = [ctypes.c_longlong]
     lib.lci_fft_size.restype = ctypes.c_longlong
     lib.lci_fft_size.argtypes = [_I]
     for name, argt in SIGNATURES.items():

@@ -102,6 +102,17 @@ class SABlock(nn.Module):
         return (torch.einsum("blxd,blyd->blxy", t[0], t[1]) * self.scale).softmax(dim=-1)
 
 
+class TokenLayerNorm(nn.LayerNorm):
+    """nn.LayerNorm (same parameters, state_dict keys and init) for TransformerBlock's norm1 / norm2
+    (backbone_vit.py:253-263) on the HIP LayerNorm kernels. Under bf16 autocast the output is the bf16 operand the
+    following Linear would cast it to (the same rounding of the same f32 result), so the f32 intermediate and the
+    cast kernels drop out; outside autocast it returns f32 as nn.LayerNorm does. GPU only."""
+
+    def forward(self, x):
+        bf16_out = torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+        return kernels.layer_norm(x, self.weight, self.bias, self.eps, bf16_out)
+
+
 class TransformerBlock(nn.Module):
     def __init__(self, use_hyena: bool, use_mamba: bool, hidden_size: int, mlp_dim: int, num_heads: int,
                  dropout_rate: float = 0.0, qkv_bias: bool = False, save_attn: bool = False) -> None:
@@ -111,11 +122,11 @@ class TransformerBlock(nn.Module):
         if hidden_size % num_heads != 0:
             raise ValueError("hidden_size should be divisible by num_heads.")
         self.mlp = MLPBlock(hidden_size, mlp_dim, dropout_rate)
-        self.norm1 = nn.LayerNorm(hidden_size)
+        self.norm1 = TokenLayerNorm(hidden_size)
         self.use_hyena = use_hyena
         self.use_mamba = use_mamba
         self.attn = SABlock(use_hyena, use_mamba, hidden_size, num_heads, dropout_rate, qkv_bias, save_attn)
-        self.norm2 = nn.LayerNorm(hidden_size)
+        self.norm2 = TokenLayerNorm(hidden_size)
 
     def forward(self, x):
         x = x + self.attn(self.norm1(x))

@@ -815,3 +815,48 @@ def instance_norm_act(x: torch.Tensor, act: bool) -> torch.Tensor:
     x_cl = x_cl.contiguous()
     z = _InstanceNormAct.apply(x_cl, act)
     return z.view(B, *S, C).movedim(-1, 1)
+
+
+# ------------------------------------------------------------------ transformer-block LayerNorm (+ autocast cast)
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps, bf16_out):
+        C = x.shape[-1]
+        x2 = x.reshape(-1, C)
+        rows = x2.shape[0]
+        y = torch.empty(x.shape, device=x.device, dtype=torch.bfloat16 if bf16_out else torch.float32)
+        mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        KernelTimer.run("ln_fwd", rows * C * (4 + y.element_size()), x, lambda: _lib.call(
+            "lci_layernorm_fwd", x2.data_ptr(), weight.data_ptr(), bias.data_ptr(), y.data_ptr(), int(bf16_out),
+            mean.data_ptr(), rstd.data_ptr(), rows, C, float(eps), _lib.stream_of(x)))
+        ctx.save_for_backward(x2, weight, mean, rstd)
+        ctx.shape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight, mean, rstd = ctx.saved_tensors
+        rows, C = x2.shape
+        bf = dy.dtype == torch.bfloat16
+        dy = (dy if bf else dy.float()).contiguous()
+        dx = torch.empty(rows, C, device=x2.device, dtype=torch.float32)
+        nblk = _lib.load().lci_layernorm_bwd_blocks(rows)
+        part = torch.empty(nblk, 2, C, device=x2.device, dtype=torch.float32)
+        KernelTimer.run("ln_bwd", rows * C * (8 + dy.element_size()), x2, lambda: _lib.call(
+            "lci_layernorm_bwd", x2.data_ptr(), dy.data_ptr(), int(bf), weight.data_ptr(), mean.data_ptr(),
+            rstd.data_ptr(), dx.data_ptr(), part.data_ptr(), rows, C, _lib.stream_of(x2)))
+        s = part.sum(0)
+        return dx.view(ctx.shape), s[0], s[1], None, None
+
+
+def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float, bf16_out: bool):
+    """nn.LayerNorm over the last dim of an f32 tensor; bf16_out returns the bf16 rounding of the f32 result
+    (what autocast hands the next Linear). HIP kernels only."""
+    _lib.require_gpu(weight, bias)
+    if not x.is_cuda:
+        raise _lib.LciError("layer_norm runs on the GPU only; there is no CPU path")
+    if weight.dtype != torch.float32 or bias.dtype != torch.float32:
+        raise _lib.LciError("layer_norm expects f32 affine parameters")
+    x = x.float().contiguous()
+    return _LayerNorm.apply(x, weight, bias, eps, bf16_out)

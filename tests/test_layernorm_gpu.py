@@ -1,0 +1,66 @@
+"""HIP LayerNorm of TransformerBlock (backbone_vit.py:253-263) against torch's fp32 layer_norm.
+
+f32 output: rel-L2 <= 1e-6 and max |err| <= 1e-5. bf16 output (the autocast operand of the next Linear): each
+element is the bf16 rounding of the fp32 result, so it may differ from torch's rounding only where the two f32
+values straddle a rounding boundary: |err| <= 1 bf16 ulp of the reference + 1e-5 (the f32 absolute error where
+y = n gamma + beta cancels to near zero) everywhere, >= 99.5 % bit-equal.
+Gradients (dx, dgamma, dbeta) vs torch autograd in fp64 on the same cotangent: rel-L2 <= 1e-5.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from golden_util import rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("rows,C", [(1, 384), (4099, 384), (513, 192), (257, 768), (130, 1024), (77, 100),
+                                    (2 * 65536, 384)])
+@pytest.mark.parametrize("bf16", [False, True])
+def test_layernorm_vs_torch(rows, C, bf16):
+    from long_context_biomedical_imaging_amd import kernels
+    torch.manual_seed(rows + C)
+    x = (torch.randn(rows, C) * 3 + 0.5).cuda()
+    w = (1 + 0.1 * torch.randn(C)).cuda()
+    b = (0.1 * torch.randn(C)).cuda()
+    xr, wr, br = [t.double().requires_grad_(True) for t in (x, w, b)]
+    ref = F.layer_norm(xr, (C,), wr, br, 1e-5)
+    xc, wc, bc = [t.clone().requires_grad_(True) for t in (x, w, b)]
+    y = kernels.layer_norm(xc, wc, bc, 1e-5, bf16)
+    if bf16:
+        assert y.dtype == torch.bfloat16
+        r32 = ref.detach().float()
+        exact = (y == r32.to(torch.bfloat16)).float().mean().item()
+        ulp = r32.abs().clamp_min(1e-30) * 2.0 ** -7
+        assert ((y.float() - r32).abs() <= ulp + 1e-5).all()
+        assert exact >= 0.995, exact
+    else:
+        assert y.dtype == torch.float32
+        assert rel_err(y, ref) < 1e-6
+        assert (y.double() - ref.detach()).abs().max().item() < 1e-5
+    dy = torch.randn(rows, C).cuda().to(y.dtype)
+    y.backward(dy)
+    ref.backward(dy.double())
+    assert rel_err(xc.grad, xr.grad) < 1e-5
+    assert rel_err(wc.grad, wr.grad) < 1e-5
+    assert rel_err(bc.grad, br.grad) < 1e-5
+
+
+def test_token_layernorm_module_autocast():
+    """TransformerBlock's norm under bf16 autocast hands the Linear the bf16 operand; outside autocast f32."""
+    from long_context_biomedical_imaging_amd import backbone_vit
+    torch.manual_seed(0)
+    m = backbone_vit.TokenLayerNorm(384).cuda()
+    ref = torch.nn.LayerNorm(384).cuda()
+    ref.load_state_dict(m.state_dict())
+    x = torch.randn(2, 1000, 384, device="cuda")
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m(x)
+        lin = torch.nn.Linear(384, 8).cuda()
+        r = ref(x)
+        assert y.dtype == torch.bfloat16 and r.dtype == torch.float32
+        assert torch.allclose(lin(y).float(), lin(r).float(), atol=0, rtol=0) or \
+            rel_err(lin(y), lin(r)) < 1e-3
+    y32 = m(x)
+    assert y32.dtype == torch.float32 and rel_err(y32, ref(x)) < 1e-6
