@@ -22,7 +22,8 @@
  *   lci_conv3_fwd         MONAI-1.3 UnetResBlock 3x3(x3) convs of the ViTUNETR / SwinUNETR heads, enhance_heads.py:30-356
  *   lci_inorm_*           MONAI-1.3 UnetResBlock InstanceNorm (+ LeakyReLU) of the same heads
  *   lci_patch_embed_*     MONAI-1.3 PatchEmbeddingBlock (backbone_vit.py:351-361) / PatchEmbed (backbone_swin.py:800-806)
- *   lci_layernorm_*       TransformerBlock norm1 / norm2 (nn.LayerNorm, backbone_vit.py:253-263) + the autocast cast
+ *   lci_layernorm_*       TransformerBlock / SwinTransformerBlock norm1, norm2 (nn.LayerNorm, backbone_vit.py:250-262,
+ *                         backbone_swin.py:418,431) + the autocast cast
  *                         of its output to the next Linear's bf16 operand
  */
 #ifndef LCI_H_

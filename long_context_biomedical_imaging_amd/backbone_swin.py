@@ -26,7 +26,7 @@ import torch.nn.functional as F
 
 from . import kernels
 from .blocks import MLPBlock as Mlp
-from .blocks import PatchEmbed, trunc_normal_
+from .blocks import PatchEmbed, TokenLayerNorm, trunc_normal_
 from .hyena import HyenaOperator
 from .mamba import MambaVisionMixer
 
@@ -185,6 +185,8 @@ class SwinTransformerBlock(nn.Module):
         self.shift_size = shift_size
         self.mlp_ratio = mlp_ratio
         self.use_checkpoint = use_checkpoint
+        if norm_layer is nn.LayerNorm:   # same parameters and init, HIP kernels (bf16 autocast operand out)
+            norm_layer = TokenLayerNorm
         self.norm1 = norm_layer(dim)
         self.attn = WindowAttention(use_hyena, use_mamba, dim, window_size=self.window_size, num_heads=num_heads,
                                     qkv_bias=qkv_bias, attn_drop=attn_drop, proj_drop=drop)

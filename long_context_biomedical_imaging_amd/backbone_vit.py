@@ -16,7 +16,7 @@ import torch.nn as nn
 import torch.utils.checkpoint
 
 from . import kernels
-from .blocks import MLPBlock, PatchEmbeddingBlock
+from .blocks import MLPBlock, PatchEmbeddingBlock, TokenLayerNorm
 from .hyena import HyenaOperator
 from .mamba import MambaVisionMixer
 
@@ -100,17 +100,6 @@ class SABlock(nn.Module):
         b, l, _ = qkv.shape
         t = qkv.reshape(b, l, 3, self.num_heads, self.head_dim).permute(2, 0, 3, 1, 4).float()
         return (torch.einsum("blxd,blyd->blxy", t[0], t[1]) * self.scale).softmax(dim=-1)
-
-
-class TokenLayerNorm(nn.LayerNorm):
-    """nn.LayerNorm (same parameters, state_dict keys and init) for TransformerBlock's norm1 / norm2
-    (backbone_vit.py:253-263) on the HIP LayerNorm kernels. Under bf16 autocast the output is the bf16 operand the
-    following Linear would cast it to (the same rounding of the same f32 result), so the f32 intermediate and the
-    cast kernels drop out; outside autocast it returns f32 as nn.LayerNorm does. GPU only."""
-
-    def forward(self, x):
-        bf16_out = torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
-        return kernels.layer_norm(x, self.weight, self.bias, self.eps, bf16_out)
 
 
 class TransformerBlock(nn.Module):

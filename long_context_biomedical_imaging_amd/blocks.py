@@ -5,7 +5,8 @@ checkpoints load and seeded initialisation reproduces the reference's weights:
   MLPBlock            backbone_vit.py:249 / backbone_swin.py:433  (linear1 -> GELU(erf) -> linear2)
   PatchEmbeddingBlock backbone_vit.py:351-361  (conv k=s=p -> flatten/transpose -> + position_embeddings)
   PatchEmbed          backbone_swin.py:800-806 (right pad to a patch multiple -> conv k=s=p)
-The patch-embedding forward runs the HIP patch-embed kernels (kernels.patch_embed_*).
+The patch-embedding forward runs the HIP patch-embed kernels (kernels.patch_embed_*); TokenLayerNorm (an
+nn.LayerNorm) runs the HIP LayerNorm kernels (kernels.layer_norm).
 """
 from __future__ import annotations
 
@@ -29,6 +30,18 @@ def ensure_tuple_rep(tup, dim):
 def trunc_normal_(tensor, mean=0.0, std=1.0, a=-2.0, b=2.0):
     with torch.no_grad():
         return nn.init.trunc_normal_(tensor, mean=mean, std=std, a=a, b=b)
+
+
+class TokenLayerNorm(nn.LayerNorm):
+    """nn.LayerNorm (same parameters, state_dict keys and init) for the token blocks' norm1 / norm2
+    (TransformerBlock backbone_vit.py:250,256,261-262; SwinTransformerBlock backbone_swin.py:418,431) on the HIP
+    LayerNorm kernels. Under bf16 autocast the output is the bf16 operand the following Linear would cast it to
+    (the same rounding of the same f32 result), so the f32 intermediate and the cast kernels drop out; outside
+    autocast it returns f32 as nn.LayerNorm does. GPU only."""
+
+    def forward(self, x):
+        bf16_out = torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+        return kernels.layer_norm(x, self.weight, self.bias, self.eps, bf16_out)
 
 
 class MLPBlock(nn.Module):

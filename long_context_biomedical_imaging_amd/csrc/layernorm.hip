@@ -1,6 +1,7 @@
 // LayerNorm of the transformer blocks' residual stream, with the autocast cast folded into the output.
 //
-// Replaces TransformerBlock's norm1 / norm2 (nn.LayerNorm(hidden), eps 1e-5, backbone_vit.py:253-263) as
+// Replaces TransformerBlock / SwinTransformerBlock norm1, norm2 (nn.LayerNorm, eps 1e-5, backbone_vit.py:250-262,
+// backbone_swin.py:418,431) as
 // executed under the trainer's bf16 autocast (trainer_base.py:167): torch runs layer_norm in f32 (an autocast
 // f32 op), writes the f32 result, and the next Linear (qkv / in_proj / mlp.linear1) reads it back to cast it
 // to bf16. Here the forward writes the bf16 operand directly (the same RNE rounding of the same f32 value), and
