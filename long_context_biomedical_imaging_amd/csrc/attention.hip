@@ -43,7 +43,12 @@ __device__ __forceinline__ bf16x8 frag_tr_sw(const bf16* tile, int r0, int c0, i
 }
 constexpr float NEG_BIG = -1.0e30f;
 
-#ifdef LCI_IGLP   // scheduling-strategy experiments (tools/attn_variants.sh)
+// dK/dV loop scheduling strategy: iglp_opt(3) (MFMA / exp interleave) measured 23.66 -> 23.11 ms on one box
+// (profiles/r01_attn_dkdv_iglp_ab.jsonl); 0-2 were slower. -DLCI_IGLP=-1 builds without the hint.
+#ifndef LCI_IGLP
+#define LCI_IGLP 3
+#endif
+#if LCI_IGLP >= 0
 #define LCI_SCHED_HINT() __builtin_amdgcn_iglp_opt(LCI_IGLP)
 #else
 #define LCI_SCHED_HINT()

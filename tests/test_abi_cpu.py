@@ -22,7 +22,8 @@ def test_header_declares_entry_points():
     d = _declared()
     for must in ("lci_attn_fwd", "lci_attn_bwd", "lci_window_attn_fwd", "lci_window_attn_bwd",
                  "lci_selective_scan_fwd", "lci_selective_scan_bwd", "lci_fftconv_fwd", "lci_fftconv_bwd",
-                 "lci_patch_embed_fwd", "lci_patch_embed_bwd", "lci_hyena_pre_fwd", "lci_dwconv_silu_fwd"):
+                 "lci_patch_embed_fwd", "lci_patch_embed_bwd", "lci_hyena_pre_fwd", "lci_dwconv_silu_fwd",
+                 "lci_layernorm_fwd", "lci_layernorm_bwd", "lci_conv3_fwd", "lci_inorm_apply"):
         assert must in d, must
 
 
