@@ -21,6 +21,18 @@
 #define LCI_CONV_MV_WIDE 4   // 32-voxel blocks per wave for NT >= 3 (A/B: tools/conv_variants.sh)
 #endif
 
+// scheduling-strategy hooks for A/B runs (tools/conv_variants.sh): iglp_opt(N) on the fwd / wgrad main loops
+#ifdef LCI_CONV_IGLP
+#define LCI_CONV_SCHED() __builtin_amdgcn_iglp_opt(LCI_CONV_IGLP)
+#else
+#define LCI_CONV_SCHED()
+#endif
+#ifdef LCI_WGRAD_IGLP
+#define LCI_WGRAD_SCHED() __builtin_amdgcn_iglp_opt(LCI_WGRAD_IGLP)
+#else
+#define LCI_WGRAD_SCHED()
+#endif
+
 namespace lci {
 
 struct ConvArgs {
@@ -183,6 +195,7 @@ __global__ __launch_bounds__(256) void conv3_fwd_lds_kernel(ConvArgs a) {
             *(const u32x4*)(a.w + ((long long)(n0 + n) * T + tap) * a.Cin + c0 + 8 * ch);
       }
       __syncthreads();
+      LCI_CONV_SCHED();
 #pragma unroll
       for (int dxi = 0; dxi < 3; ++dxi) {
         bool ok[MV];
@@ -500,6 +513,7 @@ __global__ __launch_bounds__(256) void conv3_wgrad3_kernel(WgradArgs a) {
   for (long long g0 = gs; g0 < ge; g0 += WG_ROWS) {
     const bool more = g0 + WG_ROWS < ge;
     if (more) load(g0 + WG_ROWS);
+    LCI_WGRAD_SCHED();
     const bf16* tdy = sdy[buf];
     const bf16* tx = sx[buf];
 #pragma unroll
