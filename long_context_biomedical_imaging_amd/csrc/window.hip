@@ -22,6 +22,18 @@
 //           Pad-token dK/dV go to the qkv bias gradient. d(rpb) = sum over windows of dS (reduction kernel).
 #include "common.hpp"
 
+// scheduling-strategy hooks for A/B runs (tools/attn_variants.sh): iglp_opt(N) on the fwd / bwd tile loops
+#ifdef LCI_WIN_IGLP_FWD
+#define LCI_WIN_FWD_SCHED() __builtin_amdgcn_iglp_opt(LCI_WIN_IGLP_FWD)
+#else
+#define LCI_WIN_FWD_SCHED()
+#endif
+#ifdef LCI_WIN_IGLP_BWD
+#define LCI_WIN_BWD_SCHED() __builtin_amdgcn_iglp_opt(LCI_WIN_IGLP_BWD)
+#else
+#define LCI_WIN_BWD_SCHED()
+#endif
+
 namespace lci {
 
 constexpr int WHD = 32;          // head dim (Swin: C / heads = 32 at every stage)
@@ -246,6 +258,7 @@ __global__ __launch_bounds__(NW * 64) void win_attn_fwd_kernel(WinArgs a) {
     f32x16 b0 = win_bias_tile(brow, 0), b1;   // table tiles two ahead
     if (a.nkt > 1) b1 = win_bias_tile(brow, 32);
     for (int kt = 0; kt < a.nkt; ++kt) {
+      LCI_WIN_FWD_SCHED();
       f32x16 s = b0;
       b0 = b1;
       if (kt + 2 < a.nkt) b1 = win_bias_tile(brow, (kt + 2) * 32);
@@ -344,6 +357,7 @@ __global__ __launch_bounds__(256) void win_attn_bwd_kernel(WinArgs a) {
     f32x16 b0 = win_bias_tile(brow, 0), b1;
     if (a.nkt > 1) b1 = win_bias_tile(brow, 32);
     for (int kt = 0; kt < a.nkt; ++kt) {
+      LCI_WIN_BWD_SCHED();
       f32x16 s = b0;
       b0 = b1;
       if (kt + 2 < a.nkt) b1 = win_bias_tile(brow, (kt + 2) * 32);
@@ -393,6 +407,7 @@ __global__ __launch_bounds__(256) void win_attn_bwd_kernel(WinArgs a) {
     f32x16 b0 = win_bias_tile(brow, 0), b1;
     if (a.nkt > 1) b1 = win_bias_tile(brow, 32);
     for (int qt = 0; qt < a.nkt; ++qt) {
+      LCI_WIN_BWD_SCHED();
       f32x16 s = b0;
       b0 = b1;
       if (qt + 2 < a.nkt) b1 = win_bias_tile(brow, (qt + 2) * 32);

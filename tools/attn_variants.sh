@@ -1,5 +1,5 @@
 #!/bin/bash
-# Build liblci variants of attention.hip with extra defines into build_variants/ (run here, before gpurun),
+# Build liblci variants of attention.hip / window.hip with extra defines into build_variants/ (run here, before gpurun),
 # or time them on the GPU box:  bash tools/attn_variants.sh build "v1:-DLCI_IGLP=0" ... ; bash tools/attn_variants.sh run
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
@@ -13,7 +13,7 @@ if [ "$1" = build ]; then
     for f in $ROOT/long_context_biomedical_imaging_amd/csrc/*.hip $ROOT/long_context_biomedical_imaging_amd/csrc/*.cpp; do
       b=$(basename $f)
       extra=""
-      case $b in attention.hip) extra="-fno-honor-nans -fno-slp-vectorize $defs";; window.hip) extra="-fno-honor-nans";; esac
+      case $b in attention.hip) extra="-fno-honor-nans -fno-slp-vectorize $defs";; window.hip) extra="-fno-honor-nans $defs";; esac
       if [ "${b##*.}" = hip ]; then
         /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result -munsafe-fp-atomics \
           -Xarch_device -mllvm=-amdgpu-mfma-vgpr-form $extra -c $f -o $OUT/$name.$b.o &
@@ -27,8 +27,9 @@ if [ "$1" = build ]; then
     echo "built $OUT/liblci_$name.so ($defs)"
   done
 elif [ "$1" = run ]; then
+  which=${2:-attention}   # kernel_bench.py section: attention | window | ...
   for so in $OUT/liblci_*.so; do
     echo "== $(basename $so)"
-    LCI_LIB_PATH=$so timeout -k 10 200 python $ROOT/tools/kernel_bench.py attention
+    LCI_LIB_PATH=$so timeout -k 10 200 python $ROOT/tools/kernel_bench.py $which
   done
 fi
