@@ -180,14 +180,16 @@ int lci_patch_embed_bwd(const void* x, int x_dtype, const void* dy, int dy_dtype
  * x (rows, C) f32 residual stream, C % 4 == 0, C <= 1024; gamma, beta (C) f32; eps as nn.LayerNorm's.
  * fwd: y (rows, C) = bf16 when bf16_out (the value autocast would hand the next Linear) else f32;
  *      mean, rstd (rows) f32 (biased variance, as torch).
- * bwd: dy (rows, C) bf16 when bf16_dy else f32; dx (rows, C) f32 written; part (lci_layernorm_bwd_blocks(rows),
+ * bwd: dy (rows, C) bf16 when bf16_dy else f32; dx (rows, C) f32 written (+ dres (rows, C) f32, the residual
+ *      path's gradient, when not null); part (lci_layernorm_bwd_blocks(rows),
  *      2, C) f32 written with per-workgroup partial sums of (dy * n, dy), n = (x - mean) * rstd: the caller sums
  *      them over the first axis for dgamma, dbeta. */
 int lci_layernorm_bwd_blocks(long long rows);
 int lci_layernorm_fwd(const float* x, const float* gamma, const float* beta, void* y, int bf16_out, float* mean,
                       float* rstd, long long rows, int C, float eps, void* stream);
 int lci_layernorm_bwd(const float* x, const void* dy, int bf16_dy, const float* gamma, const float* mean,
-                      const float* rstd, float* dx, float* part, long long rows, int C, void* stream);
+                      const float* rstd, const float* dres, float* dx, float* part, long long rows, int C,
+                      void* stream);
 
 #ifdef __cplusplus
 }

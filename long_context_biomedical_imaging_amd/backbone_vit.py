@@ -118,8 +118,12 @@ class TransformerBlock(nn.Module):
         self.norm2 = TokenLayerNorm(hidden_size)
 
     def forward(self, x):
-        x = x + self.attn(self.norm1(x))
-        x = x + self.mlp(self.norm2(x))
+        # x + attn(norm1(x)); x + mlp(norm2(x)) (backbone_vit.py:261-262), the residual gradient of each added
+        # inside the LayerNorm backward kernel
+        h, y = self.norm1.forward_residual(x)
+        x = h + self.attn(y)
+        h, y = self.norm2.forward_residual(x)
+        x = h + self.mlp(y)
         return x
 
 

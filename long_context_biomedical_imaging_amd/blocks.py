@@ -39,9 +39,17 @@ class TokenLayerNorm(nn.LayerNorm):
     (the same rounding of the same f32 result), so the f32 intermediate and the cast kernels drop out; outside
     autocast it returns f32 as nn.LayerNorm does. GPU only."""
 
+    @staticmethod
+    def _bf16_out():
+        return torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+
     def forward(self, x):
-        bf16_out = torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
-        return kernels.layer_norm(x, self.weight, self.bias, self.eps, bf16_out)
+        return kernels.layer_norm(x, self.weight, self.bias, self.eps, self._bf16_out())
+
+    def forward_residual(self, x):
+        """(x, self(x)) for a residual block x + f(self(x)); the backward adds the residual gradient inside the
+        LayerNorm kernel (one pass over the residual stream fewer)."""
+        return kernels.residual_layer_norm(x, self.weight, self.bias, self.eps, self._bf16_out())
 
 
 class MLPBlock(nn.Module):

@@ -6,9 +6,11 @@
 // f32 op), writes the f32 result, and the next Linear (qkv / in_proj / mlp.linear1) reads it back to cast it
 // to bf16. Here the forward writes the bf16 operand directly (the same RNE rounding of the same f32 value), and
 // the backward reads the bf16 cotangent the Linear produces, so neither cast kernel nor the f32 intermediate
-// exists. Math (f32, per row of C):
+// exists. With dres the backward also adds the residual path's gradient (x feeds both the LN and the residual
+// add of the block), so autograd's separate accumulation pass over the residual stream disappears.
+// Math (f32, per row of C):
 //   forward : mean = sum(x)/C, var = sum((x-mean)^2)/C, rstd = 1/sqrt(var+eps), y = (x-mean) rstd gamma + beta
-//   backward: n = (x-mean) rstd, g = dy gamma, dx = rstd (g - mean_C(g) - n mean_C(g n));
+//   backward: n = (x-mean) rstd, g = dy gamma, dx = [dres +] rstd (g - mean_C(g) - n mean_C(g n));
 //             dgamma = sum_rows dy n, dbeta = sum_rows dy (per-workgroup partials, summed by the caller)
 // One wave per row: lane l holds the 16-B column groups 4l + 256k (k < NV), so a row is NV coalesced
 // 1-KB wave loads. HBM-bound: forward 4C + 2C bytes per row (f32 in, bf16 out), backward 4C + 2C + 4C.
@@ -23,6 +25,7 @@ struct LnArgs {
   void* y;              // fwd: (rows, C) bf16 or f32
   const void* dy;       // bwd: (rows, C) bf16 or f32
   float* dx;            // bwd: (rows, C) f32
+  const float* dres;    // bwd: (rows, C) f32 residual-path gradient added into dx, or null
   float* mean;          // (rows)
   float* rstd;          // (rows)
   float* part;          // bwd: (gridDim.x, 2, C) partial dgamma, dbeta
@@ -143,9 +146,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnArgs a) {
     for (int k = 0; k < NV; ++k) {
       const int c = 4 * lane + 256 * k;
       if (c < C) {
-        f32x4 o;
+        f32x4 o = a.dres ? *(const f32x4*)(a.dres + row * C + c) : f32x4{};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = rstd * (g[k][j] - m1 - n[k][j] * m2);
+        for (int j = 0; j < 4; ++j) o[j] += rstd * (g[k][j] - m1 - n[k][j] * m2);
         *(f32x4*)(a.dx + row * C + c) = o;
       }
     }
@@ -205,9 +208,12 @@ extern "C" int lci_layernorm_fwd(const float* x, const float* gamma, const float
 }
 
 extern "C" int lci_layernorm_bwd(const float* x, const void* dy, int bf16_dy, const float* gamma, const float* mean,
-                                 const float* rstd, float* dx, float* part, long long rows, int C, void* stream) {
+                                 const float* rstd, const float* dres, float* dx, float* part, long long rows, int C,
+                                 void* stream) {
   if (ln_check(rows, C, x)) return 1;
+  LCI_CHECK(!dres || ((uintptr_t)dres & 15) == 0, "layernorm: misaligned residual gradient");
   LnArgs a = {};
+  a.dres = dres;
   a.x = x; a.dy = dy; a.gamma = gamma; a.mean = const_cast<float*>(mean); a.rstd = const_cast<float*>(rstd);
   a.dx = dx; a.part = part;
   a.rows = rows; a.C = C; a.bf16_io = bf16_dy;

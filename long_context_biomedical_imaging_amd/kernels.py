@@ -818,18 +818,40 @@ def instance_norm_act(x: torch.Tensor, act: bool) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------ transformer-block LayerNorm (+ autocast cast)
+def _ln_fwd(x, weight, bias, eps, bf16_out):
+    C = x.shape[-1]
+    x2 = x.reshape(-1, C)
+    rows = x2.shape[0]
+    y = torch.empty(x.shape, device=x.device, dtype=torch.bfloat16 if bf16_out else torch.float32)
+    mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+    rstd = torch.empty_like(mean)
+    KernelTimer.run("ln_fwd", rows * C * (4 + y.element_size()), x, lambda: _lib.call(
+        "lci_layernorm_fwd", x2.data_ptr(), weight.data_ptr(), bias.data_ptr(), y.data_ptr(), int(bf16_out),
+        mean.data_ptr(), rstd.data_ptr(), rows, C, float(eps), _lib.stream_of(x)))
+    return y, x2, mean, rstd
+
+
+def _ln_bwd(x2, weight, mean, rstd, dy, dres, shape):
+    rows, C = x2.shape
+    bf = dy.dtype == torch.bfloat16
+    dy = (dy if bf else dy.float()).contiguous()
+    if dres is not None:
+        dres = dres.float().contiguous()
+    dx = torch.empty(rows, C, device=x2.device, dtype=torch.float32)
+    nblk = _lib.load().lci_layernorm_bwd_blocks(rows)
+    part = torch.empty(nblk, 2, C, device=x2.device, dtype=torch.float32)
+    KernelTimer.run("ln_bwd", rows * C * (8 + dy.element_size() + (4 if dres is not None else 0)), x2,
+                    lambda: _lib.call("lci_layernorm_bwd", x2.data_ptr(), dy.data_ptr(), int(bf), weight.data_ptr(),
+                                      mean.data_ptr(), rstd.data_ptr(), _lib.ptr(dres), dx.data_ptr(),
+                                      part.data_ptr(), rows, C, _lib.stream_of(x2)))
+    s = part.sum(0)
+    return dx.view(shape), s[0], s[1]
+
+
 class _LayerNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, eps, bf16_out):
-        C = x.shape[-1]
-        x2 = x.reshape(-1, C)
-        rows = x2.shape[0]
-        y = torch.empty(x.shape, device=x.device, dtype=torch.bfloat16 if bf16_out else torch.float32)
-        mean = torch.empty(rows, device=x.device, dtype=torch.float32)
-        rstd = torch.empty_like(mean)
-        KernelTimer.run("ln_fwd", rows * C * (4 + y.element_size()), x, lambda: _lib.call(
-            "lci_layernorm_fwd", x2.data_ptr(), weight.data_ptr(), bias.data_ptr(), y.data_ptr(), int(bf16_out),
-            mean.data_ptr(), rstd.data_ptr(), rows, C, float(eps), _lib.stream_of(x)))
+        y, x2, mean, rstd = _ln_fwd(x, weight, bias, eps, bf16_out)
         ctx.save_for_backward(x2, weight, mean, rstd)
         ctx.shape = x.shape
         return y
@@ -837,26 +859,47 @@ class _LayerNorm(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x2, weight, mean, rstd = ctx.saved_tensors
-        rows, C = x2.shape
-        bf = dy.dtype == torch.bfloat16
-        dy = (dy if bf else dy.float()).contiguous()
-        dx = torch.empty(rows, C, device=x2.device, dtype=torch.float32)
-        nblk = _lib.load().lci_layernorm_bwd_blocks(rows)
-        part = torch.empty(nblk, 2, C, device=x2.device, dtype=torch.float32)
-        KernelTimer.run("ln_bwd", rows * C * (8 + dy.element_size()), x2, lambda: _lib.call(
-            "lci_layernorm_bwd", x2.data_ptr(), dy.data_ptr(), int(bf), weight.data_ptr(), mean.data_ptr(),
-            rstd.data_ptr(), dx.data_ptr(), part.data_ptr(), rows, C, _lib.stream_of(x2)))
-        s = part.sum(0)
-        return dx.view(ctx.shape), s[0], s[1], None, None
+        dx, dw, db = _ln_bwd(x2, weight, mean, rstd, dy, None, ctx.shape)
+        return dx, dw, db, None, None
 
 
-def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float, bf16_out: bool):
-    """nn.LayerNorm over the last dim of an f32 tensor; bf16_out returns the bf16 rounding of the f32 result
-    (what autocast hands the next Linear). HIP kernels only."""
+class _ResidualLayerNorm(torch.autograd.Function):
+    """(h, y) = (x, LN(x)) for a block `x + f(LN(x))`: the backward adds the residual path's gradient dh into
+    the LN input gradient inside the HIP kernel, instead of autograd accumulating the two in a separate pass."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps, bf16_out):
+        y, x2, mean, rstd = _ln_fwd(x, weight, bias, eps, bf16_out)
+        ctx.save_for_backward(x2, weight, mean, rstd)
+        ctx.shape = x.shape
+        return x.view_as(x), y
+
+    @staticmethod
+    def backward(ctx, dh, dy):
+        x2, weight, mean, rstd = ctx.saved_tensors
+        if dy is None:
+            return dh, None, None, None, None
+        dx, dw, db = _ln_bwd(x2, weight, mean, rstd, dy, dh, ctx.shape)
+        return dx, dw, db, None, None
+
+
+def _ln_checks(x, weight, bias):
     _lib.require_gpu(weight, bias)
     if not x.is_cuda:
         raise _lib.LciError("layer_norm runs on the GPU only; there is no CPU path")
     if weight.dtype != torch.float32 or bias.dtype != torch.float32:
         raise _lib.LciError("layer_norm expects f32 affine parameters")
-    x = x.float().contiguous()
+    return x.float().contiguous()
+
+
+def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float, bf16_out: bool):
+    """nn.LayerNorm over the last dim of an f32 tensor; bf16_out returns the bf16 rounding of the f32 result
+    (what autocast hands the next Linear). HIP kernels only."""
+    x = _ln_checks(x, weight, bias)
     return _LayerNorm.apply(x, weight, bias, eps, bf16_out)
+
+
+def residual_layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float, bf16_out: bool):
+    """(x, layer_norm(x)) with the residual gradient fused into the LN backward (see _ResidualLayerNorm)."""
+    x = _ln_checks(x, weight, bias)
+    return _ResidualLayerNorm.apply(x, weight, bias, eps, bf16_out)
