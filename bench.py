@@ -13,6 +13,8 @@ Also reported (rank 0): `roofline` of the dominant liblci kernel (HIP events ove
 per-kernel breakdown, `cpu_baseline` = the CPU oracle's forward on a bounded sample (N = 1 only), and
 `secondary.swin_p2_128` = the same harness on BASELINE configs[2] (Swin-tiny + SwinUNETR, 128^3 patch 2, one
 volume per GPU), which north_star also names. `--workload` runs one of the other configs on its own.
+`--no-kernel-timer` drops the per-launch HIP events (for rocprofv3 PMC passes: the profiler serialises
+dispatches and the extra event packets are not needed there); the line then has no `roofline`/`kernels`.
 """
 from __future__ import annotations
 
@@ -80,21 +82,31 @@ WORKLOAD_NAMES = {
 }
 
 
+def cpu_threads():
+    """Host threads for the CPU baseline: every core in this process's affinity mask, capped by OMP_NUM_THREADS
+    when the launcher sets it (the GPU box exposes the whole machine's CPUs but allots 16 per GPU and sets
+    OMP_NUM_THREADS accordingly)."""
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return min(n, int(omp)) if omp.isdigit() and int(omp) > 0 else n
+
+
 def cpu_baseline(budget_s: float = 20.0):
     """Oracle (CPU restatement) forward of the same encoder, bounded sample, extrapolated per token.
 
-    One 12-layer ViT-small layer at L = 65536 is: LN + qkv + out_proj + MLP over all tokens (timed on a
-    4096-token slice, scaled x16) + attention (timed on `rows` query rows per head against all 65536 keys,
-    scaled to all rows; rows are independent and equal work). tokens/s = L / (12 * t_layer).
+    SURVEY.md §8(d): the attention of one layer at L = 65536 is computed in query-row chunks of 4096 (per-row
+    softmax is exact, 6.4 GB of f32 scores per chunk for the 6 heads); chunks are timed until the budget is
+    spent and the per-chunk time is scaled to the 16 chunks of a layer. LN + qkv + out_proj + MLP are timed on
+    one 4096-token chunk and scaled the same way. tokens/s = L / (12 * t_layer).
     """
     from oracle import attention as oatt
-    ncores = min(16, len(os.sched_getaffinity(0)))
+    ncores = cpu_threads()
     torch.set_num_threads(ncores)
-    L, D, H, dh, MLP = 65536, 384, 6, 64, 1536
+    L, D, H, dh, MLP, CH = 65536, 384, 6, 64, 1536, 4096
     g = torch.Generator().manual_seed(0)
     w = {k: torch.randn(s, generator=g) * 0.02 for k, s in
          {"qkv": (3 * D, D), "out": (D, D), "l1": (MLP, D), "l2": (D, MLP)}.items()}
-    x = torch.randn(1, 4096, D, generator=g)
+    x = torch.randn(1, CH, D, generator=g)
     F = torch.nn.functional
     t0 = time.perf_counter()
     h = F.layer_norm(x, (D,))
@@ -102,24 +114,24 @@ def cpu_baseline(budget_s: float = 20.0):
     o = F.linear(qkv[..., :D], w["out"])
     h2 = F.layer_norm(x + o, (D,))
     _ = F.linear(F.gelu(F.linear(h2, w["l1"])), w["l2"])
-    t_lin = (time.perf_counter() - t0) * (L / 4096)
-    q = torch.randn(1, H, 1, dh, generator=g)
+    t_lin = (time.perf_counter() - t0) * (L / CH)
     k = torch.randn(1, H, L, dh, generator=g)
     v = torch.randn(1, H, L, dh, generator=g)
-    rows, t_att, done = 256, 0.0, 0
+    t_att, done = 0.0, 0
     t_start = time.perf_counter()
-    while time.perf_counter() - t_start < budget_s * 0.8 and done < L:
-        qs = q.expand(1, H, rows, dh).contiguous()
+    while done < L and (done == 0 or time.perf_counter() - t_start < budget_s * 0.8):
+        q = torch.randn(1, H, CH, dh, generator=g)
         t1 = time.perf_counter()
-        oatt.attention_core(qs, k, v, dh ** -0.5)
+        oatt.attention_core(q, k, v, dh ** -0.5)
         t_att += time.perf_counter() - t1
-        done += rows
+        done += CH
     t_layer = t_lin + t_att * (L / done)
     return {"value": round(L / (12 * t_layer), 1), "unit": "image-tokens/s (fwd only, fp32)", "cores": ncores,
             "kind": "port",
-            "sample": f"oracle ViT-small encoder forward at L=65536, B=1: per layer, attention timed on {done} of "
-                      f"65536 query rows per head (all keys) and the Linear/LN/MLP work on a 4096-token slice, "
-                      f"both extrapolated linearly to the full layer, x12 layers"}
+            "sample": f"oracle ViT-small encoder forward at L=65536, B=1: per layer, attention over all 65536 keys "
+                      f"in query-row chunks of {CH} (all 6 heads), {done // CH} of the layer's {L // CH} chunks "
+                      f"timed, plus LN/Linear/MLP on one {CH}-token chunk; both scaled linearly to the full layer, "
+                      f"x12 layers; {ncores} threads (affinity mask capped by OMP_NUM_THREADS)"}
 
 
 def profiled_traffic(kernel: str):
@@ -136,13 +148,13 @@ def profiled_traffic(kernel: str):
     return None
 
 
-def run_workload(workload, batch, steps, warmup, rank, world, device):
+def run_workload(workload, batch, steps, warmup, rank, world, device, kernel_timer=True, cfg_extra=()):
     """Build the workload's model, run `warmup` untimed and `steps` timed training steps (barrier + sync on both
     sides, max over ranks). Returns the bench dict on rank 0 (None elsewhere); frees the model."""
     if workload in ("swin_p2_128", "vit_mamba_p2_256"):
         # any 3-D conv left on MIOpen (none in these heads today): heuristic solver instead of a minutes-long find
         os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
-    cfg = lconfig.parse_config(WORKLOADS[workload] + ["--batch_size", str(batch)])
+    cfg = lconfig.parse_config(WORKLOADS[workload] + ["--batch_size", str(batch)] + list(cfg_extra))
     torch.manual_seed(0)
     model = EncoderDecoderModel(cfg, cfg.encoder_name, cfg.decoder_name, cfg.no_in_channel,
                                 cfg.no_out_channel).to(device)
@@ -166,7 +178,7 @@ def run_workload(workload, batch, steps, warmup, rank, world, device):
         dist.barrier()
     torch.cuda.synchronize()
     kernels.KernelTimer.reset()
-    kernels.KernelTimer.enabled = True
+    kernels.KernelTimer.enabled = kernel_timer
     t0 = time.perf_counter()
     for _ in range(steps):
         loss = trainer.step(x, y)
@@ -198,14 +210,20 @@ def run_workload(workload, batch, steps, warmup, rank, world, device):
             b, pu = ROOF.get(name, ("mfma", 1.0))
             rate = d["work_per_call"] * pu / (d["avg_ms"] * 1e-3)
             kern[name]["tflops" if b == "mfma" else "gbs"] = round(rate / (1e12 if b == "mfma" else 1e9), 1)
-    dom = max((n for n in ksum if ksum[n]["work_per_call"]), key=lambda n: ksum[n]["total_ms"])
-    dd = ksum[dom]
-    bound, per_unit = ROOF.get(dom, ("mfma", 1.0))
-    work = dd["work_per_call"] * per_unit
-    if bound == "mfma":
-        ach, peak, unit = work / (dd["avg_ms"] * 1e-3) / 1e12, MFMA_BF16_PEAK_TFLOPS, "TFLOP/s"
-    else:
-        ach, peak, unit = work / (dd["avg_ms"] * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s"
+    roof = None
+    if ksum:
+        dom = max((n for n in ksum if ksum[n]["work_per_call"]), key=lambda n: ksum[n]["total_ms"])
+        dd = ksum[dom]
+        bound, per_unit = ROOF.get(dom, ("mfma", 1.0))
+        work = dd["work_per_call"] * per_unit
+        if bound == "mfma":
+            ach, peak, unit = work / (dd["avg_ms"] * 1e-3) / 1e12, MFMA_BF16_PEAK_TFLOPS, "TFLOP/s"
+        else:
+            ach, peak, unit = work / (dd["avg_ms"] * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s"
+        roof = {"kernel": dom, "bound": bound, "achieved": round(ach, 1), "peak": peak,
+                "unit": unit, "frac": round(ach / peak, 4),
+                "traffic": profiled_traffic(dom), "traffic_source": "profiles/traffic.json",
+                "work_per_launch": work, "avg_launch_ms": round(dd["avg_ms"], 3)}
     return {
         "metric": WORKLOAD_NAMES[workload][0],
         "value": round(tokens / elapsed, 1), "unit": "image-tokens/s", "n_gpus": world, "steps": steps,
@@ -215,10 +233,7 @@ def run_workload(workload, batch, steps, warmup, rank, world, device):
                    "global_batch": world * batch, "seq_len": L, "parallelism": f"ddp{world}",
                    "per_gpu_batch": batch, "optimizer": cfg.optim_type, "loss": cfg.loss_func,
                    "activation_checkpointing": "per encoder block" if ckpt else "none"},
-        "roofline": {"kernel": dom, "bound": bound, "achieved": round(ach, 1), "peak": peak,
-                     "unit": unit, "frac": round(ach / peak, 4),
-                     "traffic": profiled_traffic(dom), "traffic_source": "profiles/traffic.json",
-                     "work_per_launch": work, "avg_launch_ms": round(dd["avg_ms"], 3)},
+        "roofline": roof,
         "kernels": kern,
         "loss": round(loss_v, 5),
     }
@@ -235,6 +250,8 @@ def main():
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the Swin 128^3 line that the default (ViT 512^2) run also reports")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--no-kernel-timer", action="store_true",
+                    help="no per-launch HIP events (rocprofv3 PMC passes); the line then carries no roofline")
     args = ap.parse_args()
 
     if args.batch is None:
@@ -243,12 +260,14 @@ def main():
     device = torch.device("cuda", local % torch.cuda.device_count())   # % : gloo rehearsals on one GPU
     torch.cuda.set_device(device)
     tuned = use_tuned_gemms()
-    res = run_workload(args.workload, args.batch, args.steps, args.warmup, rank, world, device)
+    res = run_workload(args.workload, args.batch, args.steps, args.warmup, rank, world, device,
+                       kernel_timer=not args.no_kernel_timer)
     if args.workload == "vit_p2_512" and not args.no_secondary:
         # north_star also asks for tokens/s on 128^3 patch-2 volumes (BASELINE configs[2], Swin + SwinUNETR):
         # same DDP harness, 1 volume per GPU, same steps (at most 10), reported under "secondary"
         try:
-            sec = run_workload("swin_p2_128", 1, min(args.steps, 10), 2, rank, world, device)
+            sec = run_workload("swin_p2_128", 1, min(args.steps, 10), 2, rank, world, device,
+                               kernel_timer=not args.no_kernel_timer)
         except Exception as e:   # never lose the headline line to the secondary workload
             sec = {"error": f"{type(e).__name__}: {e}"}
         if rank == 0:

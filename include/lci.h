@@ -33,8 +33,13 @@
 extern "C" {
 #endif
 
+/* Bumped whenever an entry point's argument list changes (3: lci_layernorm_bwd gained dres). */
+#define LCI_ABI_VERSION 3
 const char* lci_last_error(void);
 int lci_abi_version(void);
+/* sha256 prefix of the sources the library was built from (build_lib.source_hash); the Python binding refuses a
+ * library whose hash differs from the sources beside it. */
+const char* lci_build_hash(void);
 
 /* ------------------------------------------------------------------ ViT full self-attention (flash)
  * qkv : (B, L, 3*H*64) bf16, the packed qkv Linear output, channel order (qkv, head, d)
@@ -177,7 +182,8 @@ int lci_patch_embed_bwd(const void* x, int x_dtype, const void* dy, int dy_dtype
                         void* stream);
 
 /* ------------------------------------------------------------------ transformer-block LayerNorm
- * x (rows, C) f32 residual stream, C % 4 == 0, C <= 1024; gamma, beta (C) f32; eps as nn.LayerNorm's.
+ * x (rows, C) f32 residual stream, C % 4 == 0, C <= 2048; gamma, beta (C) f32; eps as nn.LayerNorm's.
+ * Pointers 16-byte aligned (8 for bf16 y / dy).
  * fwd: y (rows, C) = bf16 when bf16_out (the value autocast would hand the next Linear) else f32;
  *      mean, rstd (rows) f32 (biased variance, as torch).
  * bwd: dy (rows, C) bf16 when bf16_dy else f32; dx (rows, C) f32 written (+ dres (rows, C) f32, the residual

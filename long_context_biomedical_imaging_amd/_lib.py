@@ -12,7 +12,9 @@ import os
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("LCI_LIB_PATH", os.path.join(HERE, "liblci.so"))   # override: kernel-variant A/B runs
+DEFAULT_LIB = os.path.join(HERE, "liblci.so")
+LIB_PATH = os.environ.get("LCI_LIB_PATH", DEFAULT_LIB)   # override: kernel-variant A/B runs (no staleness check)
+ABI_VERSION = 3   # include/lci.h LCI_ABI_VERSION
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -68,6 +70,16 @@ def load(path: str = LIB_PATH):
     lib = ctypes.CDLL(path)
     lib.lci_last_error.restype = ctypes.c_char_p
     lib.lci_abi_version.restype = ctypes.c_int
+    lib.lci_build_hash.restype = ctypes.c_char_p
+    if lib.lci_abi_version() != ABI_VERSION:
+        raise LciError(f"{path}: ABI version {lib.lci_abi_version()} != {ABI_VERSION} expected by this binding; "
+                       "rebuild with `python -m long_context_biomedical_imaging_amd.build_lib`")
+    if path == DEFAULT_LIB and os.path.isdir(os.path.join(HERE, "csrc")):
+        from . import build_lib
+        want, got = build_lib.source_hash(), lib.lci_build_hash().decode()
+        if want != got:
+            raise LciError(f"{path} is stale: built from sources {got}, the sources beside it hash to {want}; "
+                           "rebuild with `python -m long_context_biomedical_imaging_amd.build_lib`")
     lib.lci_window_dS_elems.restype = ctypes.c_longlong
     lib.lci_window_dS_elems.argtypes = [_P]
     lib.lci_window_bias_elems.restype = ctypes.c_longlong

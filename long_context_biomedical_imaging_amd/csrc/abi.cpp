@@ -1,6 +1,12 @@
-// Host-side C-ABI plumbing for liblci: error reporting and version query.
+// Host-side C-ABI plumbing for liblci: error reporting, ABI version and build hash.
 #include <stdarg.h>
 #include <stdio.h>
+
+#include "lci.h"
+
+#ifndef LCI_BUILD_HASH
+#define LCI_BUILD_HASH "unknown"
+#endif
 
 namespace lci {
 static thread_local char g_err[1024] = {0};
@@ -13,4 +19,5 @@ void set_error(const char* fmt, ...) {
 }  // namespace lci
 
 extern "C" const char* lci_last_error(void) { return lci::g_err; }
-extern "C" int lci_abi_version(void) { return 2; }
+extern "C" int lci_abi_version(void) { return LCI_ABI_VERSION; }
+extern "C" const char* lci_build_hash(void) { return LCI_BUILD_HASH; }

@@ -18,6 +18,8 @@
 
 namespace lci {
 
+constexpr int LN_MAX_C = 2048;   // NV = C / 256 column groups per lane, up to 8 (Swin-large stage 4: C = 1536)
+
 struct LnArgs {
   const float* x;       // (rows, C) f32
   const float* gamma;   // (C)
@@ -103,7 +105,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnArgs a) {
 
 template <int NV>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(LnArgs a) {
-  __shared__ float red[4][2][1024];
+  __shared__ float red[4][2][NV * 256];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int C = a.C;
   const bool bf = a.bf16_io;
@@ -172,10 +174,22 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnArgs a) {
 
 static int ln_check(long long rows, int C, const void* x) {
   LCI_CHECK(x != nullptr, "layernorm: null input");
-  LCI_CHECK(rows >= 0 && C > 0 && C % 4 == 0 && C <= 1024, "layernorm: need C % 4 == 0 and C <= 1024");
+  LCI_CHECK(rows >= 0 && C > 0 && C % 4 == 0 && C <= LN_MAX_C, "layernorm: need C %% 4 == 0 and C <= %d", LN_MAX_C);
   LCI_CHECK(((uintptr_t)x & 15) == 0, "layernorm: misaligned input");
   return 0;
 }
+
+#define LN_SWITCH(KERNEL, NV, GRID, S, A)                                            \
+  switch (NV) {                                                                      \
+    case 1: hipLaunchKernelGGL(KERNEL<1>, GRID, dim3(256), 0, S, A); break;          \
+    case 2: hipLaunchKernelGGL(KERNEL<2>, GRID, dim3(256), 0, S, A); break;          \
+    case 3: hipLaunchKernelGGL(KERNEL<3>, GRID, dim3(256), 0, S, A); break;          \
+    case 4: hipLaunchKernelGGL(KERNEL<4>, GRID, dim3(256), 0, S, A); break;          \
+    case 5: hipLaunchKernelGGL(KERNEL<5>, GRID, dim3(256), 0, S, A); break;          \
+    case 6: hipLaunchKernelGGL(KERNEL<6>, GRID, dim3(256), 0, S, A); break;          \
+    case 7: hipLaunchKernelGGL(KERNEL<7>, GRID, dim3(256), 0, S, A); break;          \
+    default: hipLaunchKernelGGL(KERNEL<8>, GRID, dim3(256), 0, S, A); break;         \
+  }
 
 }  // namespace lci
 
@@ -189,6 +203,8 @@ extern "C" int lci_layernorm_bwd_blocks(long long rows) {
 extern "C" int lci_layernorm_fwd(const float* x, const float* gamma, const float* beta, void* y, int bf16_out,
                                  float* mean, float* rstd, long long rows, int C, float eps, void* stream) {
   if (ln_check(rows, C, x)) return 1;
+  LCI_CHECK(((uintptr_t)gamma & 15) == 0 && ((uintptr_t)beta & 15) == 0 &&
+            ((uintptr_t)y & (bf16_out ? 7 : 15)) == 0, "layernorm: misaligned gamma/beta/output");
   if (rows == 0) return 0;
   LnArgs a = {};
   a.x = x; a.gamma = gamma; a.beta = beta; a.y = y; a.mean = mean; a.rstd = rstd;
@@ -197,12 +213,7 @@ extern "C" int lci_layernorm_fwd(const float* x, const float* gamma, const float
   LCI_CHECK(nb < (1LL << 31), "layernorm: too many rows");
   const int NV = (C + 255) / 256;
   hipStream_t s = (hipStream_t)stream;
-  switch (NV) {
-    case 1: hipLaunchKernelGGL(ln_fwd_kernel<1>, dim3((unsigned)nb), dim3(256), 0, s, a); break;
-    case 2: hipLaunchKernelGGL(ln_fwd_kernel<2>, dim3((unsigned)nb), dim3(256), 0, s, a); break;
-    case 3: hipLaunchKernelGGL(ln_fwd_kernel<3>, dim3((unsigned)nb), dim3(256), 0, s, a); break;
-    default: hipLaunchKernelGGL(ln_fwd_kernel<4>, dim3((unsigned)nb), dim3(256), 0, s, a); break;
-  }
+  LN_SWITCH(ln_fwd_kernel, NV, dim3((unsigned)nb), s, a);
   LCI_LAUNCH_CHECK();
   return 0;
 }
@@ -212,6 +223,8 @@ extern "C" int lci_layernorm_bwd(const float* x, const void* dy, int bf16_dy, co
                                  void* stream) {
   if (ln_check(rows, C, x)) return 1;
   LCI_CHECK(!dres || ((uintptr_t)dres & 15) == 0, "layernorm: misaligned residual gradient");
+  LCI_CHECK(((uintptr_t)dy & (bf16_dy ? 7 : 15)) == 0 && ((uintptr_t)gamma & 15) == 0 &&
+            ((uintptr_t)dx & 15) == 0, "layernorm: misaligned dy/gamma/dx");
   LnArgs a = {};
   a.dres = dres;
   a.x = x; a.dy = dy; a.gamma = gamma; a.mean = const_cast<float*>(mean); a.rstd = const_cast<float*>(rstd);
@@ -220,12 +233,7 @@ extern "C" int lci_layernorm_bwd(const float* x, const void* dy, int bf16_dy, co
   const int nb = lci_layernorm_bwd_blocks(rows);
   const int NV = (C + 255) / 256;
   hipStream_t s = (hipStream_t)stream;
-  switch (NV) {
-    case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, dim3(nb), dim3(256), 0, s, a); break;
-    case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, dim3(nb), dim3(256), 0, s, a); break;
-    case 3: hipLaunchKernelGGL(ln_bwd_kernel<3>, dim3(nb), dim3(256), 0, s, a); break;
-    default: hipLaunchKernelGGL(ln_bwd_kernel<4>, dim3(nb), dim3(256), 0, s, a); break;
-  }
+  LN_SWITCH(ln_bwd_kernel, NV, dim3(nb), s, a);
   LCI_LAUNCH_CHECK();
   return 0;
 }

@@ -835,8 +835,12 @@ def _ln_bwd(x2, weight, mean, rstd, dy, dres, shape):
     rows, C = x2.shape
     bf = dy.dtype == torch.bfloat16
     dy = (dy if bf else dy.float()).contiguous()
+    if dy.data_ptr() % 16:   # a contiguous view at a storage offset: the kernel's vector loads need 8/16-B rows
+        dy = dy.clone()
     if dres is not None:
         dres = dres.float().contiguous()
+        if dres.data_ptr() % 16:
+            dres = dres.clone()
     dx = torch.empty(rows, C, device=x2.device, dtype=torch.float32)
     nblk = _lib.load().lci_layernorm_bwd_blocks(rows)
     part = torch.empty(nblk, 2, C, device=x2.device, dtype=torch.float32)
@@ -872,12 +876,13 @@ class _ResidualLayerNorm(torch.autograd.Function):
         y, x2, mean, rstd = _ln_fwd(x, weight, bias, eps, bf16_out)
         ctx.save_for_backward(x2, weight, mean, rstd)
         ctx.shape = x.shape
+        ctx.set_materialize_grads(False)   # an unused output arrives as None, not as a zeros tensor
         return x.view_as(x), y
 
     @staticmethod
     def backward(ctx, dh, dy):
         x2, weight, mean, rstd = ctx.saved_tensors
-        if dy is None:
+        if dy is None:   # LN output unused: the residual gradient passes straight through
             return dh, None, None, None, None
         dx, dw, db = _ln_bwd(x2, weight, mean, rstd, dy, dh, ctx.shape)
         return dx, dw, db, None, None
@@ -892,14 +897,33 @@ def _ln_checks(x, weight, bias):
     return x.float().contiguous()
 
 
+LN_MAX_C = 2048   # csrc/layernorm.hip LN_MAX_C
+
+
+def ln_kernel_supports(C: int) -> bool:
+    """The HIP LayerNorm covers C % 4 == 0, C <= 2048 (every ViT / Swin preset of the reference: ViT 384-1024,
+    Swin stages up to 1536). Other widths (custom sizes only) run torch's own GPU layer_norm."""
+    return C % 4 == 0 and C <= LN_MAX_C
+
+
+def _torch_ln(x, weight, bias, eps, bf16_out):
+    y = torch.nn.functional.layer_norm(x, (x.shape[-1],), weight, bias, eps)
+    return y.to(torch.bfloat16) if bf16_out else y
+
+
 def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float, bf16_out: bool):
     """nn.LayerNorm over the last dim of an f32 tensor; bf16_out returns the bf16 rounding of the f32 result
-    (what autocast hands the next Linear). HIP kernels only."""
+    (what autocast hands the next Linear). HIP kernels (GPU tensors only; widths outside ln_kernel_supports run
+    torch's GPU layer_norm)."""
     x = _ln_checks(x, weight, bias)
+    if not ln_kernel_supports(x.shape[-1]):
+        return _torch_ln(x, weight, bias, eps, bf16_out)
     return _LayerNorm.apply(x, weight, bias, eps, bf16_out)
 
 
 def residual_layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float, bf16_out: bool):
     """(x, layer_norm(x)) with the residual gradient fused into the LN backward (see _ResidualLayerNorm)."""
     x = _ln_checks(x, weight, bias)
+    if not ln_kernel_supports(x.shape[-1]):
+        return x, _torch_ln(x, weight, bias, eps, bf16_out)
     return _ResidualLayerNorm.apply(x, weight, bias, eps, bf16_out)

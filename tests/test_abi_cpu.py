@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
     lib = ctypes.CDLL(_lib.LIB_PATH)
     for name in _declared():
         assert hasattr(lib, name), f"{name} declared in include/lci.h but not exported"
-    assert _lib.load().lci_abi_version() == 2
+    assert _lib.load().lci_abi_version() == _lib.ABI_VERSION == 3
 
 
 def test_python_binding_arity_matches_header():
@@ -43,3 +43,15 @@ def test_python_binding_arity_matches_header():
     for name, argt in _lib.SIGNATURES.items():
         assert name in d, f"{name} bound in Python but not declared"
         assert len(argt) == len(d[name]), f"{name}: python {len(argt)} args, header {len(d[name])}"
+
+
+def test_integration_doc_stubs_match_header():
+    """Every `lib.<name>.argtypes = [...]` in INTEGRATION.md declares the header's argument count."""
+    d = _declared()
+    txt = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    stubs = re.findall(r"lib\.(lci_\w+)\.argtypes\s*=\s*\[([^\]]*)\]", txt)
+    assert stubs, "INTEGRATION.md has no ctypes stub"
+    for name, args in stubs:
+        assert name in d, f"INTEGRATION.md binds {name}, not declared in include/lci.h"
+        n = len([a for a in args.split(",") if a.strip()])
+        assert n == len(d[name]), f"INTEGRATION.md {name}: {n} args, header {len(d[name])}"

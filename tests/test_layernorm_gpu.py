@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("rows,C", [(1, 384), (4099, 384), (513, 192), (257, 768), (130, 1024), (77, 100),
-                                    (2 * 65536, 384)])
+                                    (2 * 65536, 384), (97, 1536), (33, 2048), (41, 1030), (19, 2052), (25, 6)])
 @pytest.mark.parametrize("bf16", [False, True])
 def test_layernorm_vs_torch(rows, C, bf16):
     from long_context_biomedical_imaging_amd import kernels
@@ -89,3 +89,40 @@ def test_residual_layernorm_fused_gradient(bf16):
     assert rel_err(xc.grad, xr.grad) < tol
     assert rel_err(wc.grad, wr.grad) < tol
     assert rel_err(bc.grad, br.grad) < tol
+
+
+def test_residual_layernorm_unused_output_and_offset_cotangent():
+    """LN output unused: the residual gradient passes through unchanged (no LN backward over zeros). A bf16
+    cotangent that is a contiguous view at an odd storage offset is realigned before the kernel's vector loads."""
+    from long_context_biomedical_imaging_amd import kernels
+    torch.manual_seed(3)
+    rows, C = 257, 384
+    x = torch.randn(rows, C, device="cuda", requires_grad=True)
+    w, b = torch.ones(C, device="cuda"), torch.zeros(C, device="cuda")
+    h, _y = kernels.residual_layer_norm(x, w, b, 1e-5, True)
+    g = torch.randn(rows, C, device="cuda")
+    h.backward(g)
+    assert torch.equal(x.grad, g)
+    xr = x.detach().double().requires_grad_(True)
+    ref = F.layer_norm(xr, (C,), w.double(), b.double(), 1e-5)
+    big = torch.randn(rows * C + 1, device="cuda").to(torch.bfloat16)
+    dy = big[1:].view(rows, C)          # contiguous, 2-byte offset
+    assert dy.data_ptr() % 8 != 0
+    x2 = x.detach().clone().requires_grad_(True)
+    y2 = kernels.layer_norm(x2, w, b, 1e-5, True)
+    y2.backward(dy)
+    ref.backward(dy.double())
+    assert rel_err(x2.grad, xr.grad) < 1e-5
+
+
+def test_swin_large_stage4_block():
+    """The Swin 'large' preset's last stage has C = 192 * 8 = 1536 channels (> the 1024 the first LayerNorm
+    kernel handled): a SwinTransformerBlock of that width runs fwd + bwd on the HIP LayerNorm."""
+    from long_context_biomedical_imaging_amd import backbone_swin
+    torch.manual_seed(0)
+    blk = backbone_swin.SwinTransformerBlock(False, False, 1536, 48, (7, 7, 7), (0, 0, 0)).cuda()
+    x = torch.randn(1, 4, 4, 4, 1536, device="cuda", requires_grad=True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = blk(x, None)
+    y.float().square().mean().backward()
+    assert y.shape == x.shape and torch.isfinite(x.grad).all()
