@@ -81,6 +81,12 @@ int lci_window_attn_bwd(const void* qkv, const float* qkv_bias, const void* bias
                         const void* out, const void* dout, const float* lse2, void* dqkv, float* dbias_pad,
                         void* dS, float* drpb, const int* geo, float scale, void* stream);
 long long lci_window_dS_elems(const int* geo);
+/* Index maps of the grid mode (test/inspection entry; same device functions as the kernels), per window w < Bw and
+ * window token n < N, int32 (Bw, N): src_row = token row (b, s0, s1[, s2]) flattened that the window token reads
+ * and the output scatters to, -1 for a padded voxel (F.pad + roll(-shift) + window_partition, and their inverse);
+ * region = compute_mask region id (3 slices per shifted axis) of the token within its window type, rid = the same
+ * derived from the padded coordinate; wtype (Bw) = the bias-table type of each window. */
+int lci_window_index_map(const int* geo, int* src_row, int* region, int* rid, int* wtype, void* stream);
 
 /* ------------------------------------------------------------------ decoder-head 3x3(x3) convolution
  * Replaces the kernel-3 stride-1 convs of MONAI-1.3 UnetResBlock (get_conv_layer conv_only, bias=False) in the

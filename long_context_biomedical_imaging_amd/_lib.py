@@ -34,6 +34,7 @@ SIGNATURES = {
     "lci_window_bias": [_P, _P, _P, _P, _P, _P],
     "lci_window_attn_fwd": [_P, _P, _P, _I, _P, _P, _P, _F, _P],
     "lci_window_attn_bwd": [_P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P],
+    "lci_window_index_map": [_P, _P, _P, _P, _P, _P],
     "lci_fft_twiddles": [_P, _I, _P],
     "lci_fftconv_spectrum": [_P, _P, _P, _P, _I, _I, _P],
     "lci_fftconv_fwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P],

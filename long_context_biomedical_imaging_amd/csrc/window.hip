@@ -489,6 +489,23 @@ __global__ __launch_bounds__(256) void win_rpb_grad_kernel(WinArgs a) {
   if (q < a.N && k < a.N) a.drpb[((long long)hh * a.N + q) * a.N + k] = acc;
 }
 
+// Index-map export (tests): for every window w and window token n, the source token row win_row() reads and the
+// output scatters to (-1 = padded voxel), the region id win_row() derives on the padded grid, and the window type
+// win_type() selects the bias table with, plus win_region() of the token under that type -- the same __device__
+// functions the attention kernels and the table builder call.
+__global__ __launch_bounds__(256) void win_index_map_kernel(WinArgs a, int* src_row, int* region, int* rid_out,
+                                                            int* wtype) {
+  const long long e = blockIdx.x * 256LL + threadIdx.x;
+  if (e >= (long long)a.Bw * a.N) return;
+  const int w = (int)(e / a.N), n = (int)(e % a.N);
+  int rid = 0;
+  src_row[e] = win_row(a, w, n, rid);
+  const int t = win_type(a, w);
+  region[e] = win_region(a, t, n);
+  rid_out[e] = rid;
+  if (n == 0) wtype[w] = t;
+}
+
 static int win_fill(WinArgs& a, const int* geo, float scale) {
   // geo: [mode, nd, S0, S1, S2, ws0, ws1, ws2, sh0, sh1, sh2, Bw_or_B, nW, N, C, H]
   a.mode = geo[0]; a.nd = geo[1];
@@ -590,4 +607,15 @@ extern "C" long long lci_window_dS_elems(const int* geo) {
   WinArgs a{};
   if (win_fill(a, geo, 1.f)) return -1;
   return (long long)a.Bw * a.H * a.nqb * a.nkt * 1024;
+}
+
+extern "C" int lci_window_index_map(const int* geo, int* src_row, int* region, int* rid, int* wtype, void* stream) {
+  WinArgs a{};
+  if (win_fill(a, geo, 1.f)) return 1;
+  LCI_CHECK(src_row && region && rid && wtype, "window_index_map: null output");
+  const long long n = (long long)a.Bw * a.N;
+  hipLaunchKernelGGL(win_index_map_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a,
+                     src_row, region, rid, wtype);
+  LCI_LAUNCH_CHECK();
+  return 0;
 }

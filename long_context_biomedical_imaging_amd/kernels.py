@@ -424,6 +424,41 @@ def _win_prep(qkv):
     return q.contiguous(), dt
 
 
+def grid_geo(B, S, window_size, shift_size, C, num_heads):
+    """geo[16] of the grid mode (include/lci.h) for a (B, *S, .) channels-last grid."""
+    S = list(S)
+    nd = len(S)
+    N = 1
+    for w in window_size:
+        N *= w
+    nW = 1
+    for s, w in zip(S, window_size):
+        nW *= -(-s // w)
+    return (1, nd, *(S + [1] * (3 - nd)), *(list(window_size) + [1] * (3 - nd)),
+            *(list(shift_size) + [0] * (3 - nd)), B, nW, N, C, num_heads)
+
+
+def window_index_map(B, S, window_size, shift_size, device="cuda"):
+    """The grid mode's index maps as the kernels compute them (lci_window_index_map): int32 src_row, region, rid
+    (B*nW, N) and wtype (B*nW,) on `device`. See include/lci.h."""
+    geo = grid_geo(B, S, window_size, shift_size, 32, 1)
+    Bw, N = geo[11] * geo[12], geo[13]
+    i32 = dict(device=device, dtype=torch.int32)
+    src, reg, rid = (torch.empty(Bw, N, **i32) for _ in range(3))
+    wt = torch.empty(Bw, **i32)
+    _lib.call("lci_window_index_map", _i32(geo), src.data_ptr(), reg.data_ptr(), rid.data_ptr(), wt.data_ptr(),
+              torch.cuda.current_stream(torch.device(device)).cuda_stream)
+    return src, reg, rid, wt
+
+
+def window_bias_table(rpb, B, S, window_size, shift_size, num_heads):
+    """The (T, H, Npad, Npad) bf16 logit table lci_window_bias builds for the grid mode from rpb (H, N, N)."""
+    geo = grid_geo(B, S, window_size, shift_size, 32 * num_heads, num_heads)
+    tab, _ = _window_bias(rpb.float().contiguous(), None, geo)
+    npad = -(-geo[13] // 32) * 32
+    return tab.view(-1, num_heads, npad, npad)
+
+
 def window_attention_grid(qkv, bias, rpb, num_heads, scale, window_size, shift_size):
     """Fused pad + roll(-shift) + window_partition + window attention + window_reverse + roll(+shift) + crop.
 
@@ -433,19 +468,7 @@ def window_attention_grid(qkv, bias, rpb, num_heads, scale, window_size, shift_s
     """
     _lib.require_gpu(qkv.contiguous())
     q, dt = _win_prep(qkv)
-    nd = q.dim() - 2
-    S = list(q.shape[1:-1])
-    C = q.shape[-1] // 3
-    N = 1
-    for w in window_size:
-        N *= w
-    ws3 = list(window_size) + [1] * (3 - nd)
-    sh3 = list(shift_size) + [0] * (3 - nd)
-    S3 = S + [1] * (3 - nd)
-    nW = 1
-    for s, w in zip(S, window_size):
-        nW *= -(-s // w)
-    geo = (1, nd, *S3, *ws3, *sh3, q.shape[0], nW, N, C, num_heads)
+    geo = grid_geo(q.shape[0], q.shape[1:-1], window_size, shift_size, q.shape[-1] // 3, num_heads)
     o = _WindowAttention.apply(q, bias, rpb.float(), None, geo, scale)
     return o if dt == torch.bfloat16 else o.to(dt)
 

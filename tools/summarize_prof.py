@@ -8,6 +8,13 @@ Only dispatches after the first `skip_frac` of the run are counted (warm-up incl
 
     python tools/summarize_prof.py gpurun_out/prof_r01 > profiles/r01_rocprof_summary.md
     python tools/summarize_prof.py gpurun_out/prof_r01 0.5 profiles/traffic.json   # + per-kernel HBM bytes
+
+Directory layouts: tools/profile_bench.sh (trace/, fetch/, write/) or tools/gpu_round.sh (trace/, pmc_FETCH_SIZE/,
+pmc_WRITE_SIZE/, pmc_SQ_WAVES/). The SQ pass gives, per kernel (MI355X_MICROARCH.md §rocprofv3 PMC slots,
+per-instruction constants): cycles = GRBM_GUI_ACTIVE / 8 (summed over the 8 XCDs), MFMA busy =
+SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x cycles), VALU busy = 4 SQ_ACTIVE_INST_VALU (quad-cycles) / (1024 x cycles),
+executed MFMA FLOP = SQ_INSTS_MFMA x 32768 (v_mfma_f32_32x32x16_bf16; other shapes make this an upper bound),
+effective clock = cycles / duration.
 """
 import csv
 import os
@@ -28,6 +35,38 @@ def load_trace(path):
     return rows
 
 
+def sq_summary(d, skip_frac):
+    p = os.path.join(d, "pmc_SQ_WAVES", "run_counter_collection.csv")
+    if not os.path.exists(p):
+        return None
+    rows = list(csv.DictReader(open(p)))
+    per = defaultdict(lambda: defaultdict(float))
+    for r in rows:
+        per[(r["Dispatch_Id"], r["Kernel_Name"])][r["Counter_Name"]] += float(r["Counter_Value"])
+        per[(r["Dispatch_Id"], r["Kernel_Name"])]["_ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    keys = sorted(per, key=lambda k: int(k[0]))
+    acc = defaultdict(lambda: defaultdict(float))
+    for k in keys[int(len(keys) * skip_frac):]:
+        n = short(k[1])
+        if not n:
+            continue
+        c = per[k]
+        cyc = c["GRBM_GUI_ACTIVE"] / 8
+        a = acc[n]
+        a["n"] += 1
+        a["ns"] += c["_ns"]
+        a["cyc"] += cyc
+        a["mfma"] += c["SQ_VALU_MFMA_BUSY_CYCLES"]
+        a["valu"] += 4 * c["SQ_ACTIVE_INST_VALU"]
+        a["flop"] += 32768 * c["SQ_INSTS_MFMA"]
+    out = {}
+    for n, a in acc.items():
+        out[n] = {"n": int(a["n"]), "ms": a["ns"] / a["n"] / 1e6, "clock": a["cyc"] / a["ns"],
+                  "mfma": a["mfma"] / (1024 * a["cyc"]), "valu": a["valu"] / (1024 * a["cyc"]),
+                  "flop": a["flop"] / a["n"]}
+    return out
+
+
 def main():
     d = sys.argv[1]
     skip_frac = float(sys.argv[2]) if len(sys.argv) > 2 else 0.5
@@ -41,6 +80,8 @@ def main():
     counters = {}
     for c in ("fetch", "write"):
         p = os.path.join(d, c, "run_counter_collection.csv")
+        if not os.path.exists(p):
+            p = os.path.join(d, "pmc_" + {"fetch": "FETCH_SIZE", "write": "WRITE_SIZE"}[c], "run_counter_collection.csv")
         if not os.path.exists(p):
             continue
         rows = list(csv.DictReader(open(p)))
@@ -72,6 +113,14 @@ def main():
         fm = f"{2 * sum(f) / len(f) / 1024:.1f}" if f else "n/a"
         wm = f"{sum(w) / len(w) / 1024:.1f}" if w else "n/a"
         print(f"| {n} | {len(v)} | {sum(v) / len(v):.3f} | {min(v):.3f} | {max(v):.3f} | {fm} | {wm} |")
+    sq = sq_summary(d, skip_frac)
+    if sq:
+        print("\nSQ counter pass (MFMA / VALU busy per SIMD-cycle, executed MFMA FLOP per launch, effective clock):\n")
+        print("| kernel | dispatches | avg ms | clock GHz | MFMA busy | VALU busy | executed TFLOP/launch | executed TFLOP/s |")
+        print("|---|---|---|---|---|---|---|---|")
+        for n, v in sorted(sq.items(), key=lambda kv: -kv[1]["ms"] * kv[1]["n"]):
+            print(f"| {n} | {v['n']} | {v['ms']:.3f} | {v['clock']:.2f} | {v['mfma']:.3f} | {v['valu']:.3f} | "
+                  f"{v['flop'] / 1e12:.2f} | {v['flop'] / v['ms'] / 1e9:.0f} |")
     print("\nrocprofv3 --stats top kernels (whole run, includes warm-up / MIOpen find):\n")
     st = list(csv.DictReader(open(os.path.join(d, "trace", "run_kernel_stats.csv"))))
     st.sort(key=lambda r: -float(r["TotalDurationNs"]))
