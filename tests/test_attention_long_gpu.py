@@ -1,0 +1,118 @@
+"""Flash attention at the C2 and metric sequence lengths (SABlock core, backbone_vit.py:191-203).
+
+- Backward at L = 16384 (C2, 512^2 patch 4), B = 1, H = 6: dQ on a query-row subset and dK / dV on a key subset
+  against exact CPU values built from the full-row logsumexp (fp32 chunked pass over all 16384 x 16384 scores
+  for lse, O and delta = dO.O; the subsets' P, dP, dS then in fp64). The rows/keys straddle every tile and
+  workgroup boundary of the dQ (256 queries) and dK/dV (256 keys, 32 per wave) kernels.
+- Forward at L = 65536 (the metric), B = 2, H = 6, on a row subset, with a few huge-norm keys late in the
+  sequence (the max-free fast path's tile bound fails there and the exact row-max path must re-base O and l).
+Tolerances as tests/test_attention_gpu.py (bf16 I/O, f32 softmax): O rel-L2 <= 1e-2 (at L = 65536: the larger of
+1e-2 and the reference's own autocast deviation on the same rows, plus <= 3e-3 from an emulation of the kernel's
+own roundings); grads rel-L2 <= 2e-2, max |err| <= 3e-2 max|ref| + 2e-3.
+"""
+import pytest
+import torch
+
+from golden_util import rel_err
+from oracle import attention as oatt
+
+pytestmark = pytest.mark.gpu
+
+SCALE = 64 ** -0.5
+LOG2E = 1.4426950408889634
+
+
+def _check(a, b, what, rel=1e-2, absf=2e-2):
+    a, b = a.double().cpu(), b.double().cpu()
+    re = rel_err(a, b)
+    mx = (a - b).abs().max().item()
+    assert re <= rel, f"{what}: rel L2 err {re:.3e}"
+    assert mx <= absf * b.abs().max().item() + 2e-3, f"{what}: max err {mx:.3e} (max|ref| {b.abs().max():.3e})"
+
+
+def _subset(L):
+    base = [0, 1, 31, 32, 33, 63, 64, 127, 128, 255, 256, 257, 511, 512, 4095, 4096, L // 2 - 1, L // 2,
+            L - 257, L - 256, L - 33, L - 32, L - 2, L - 1]
+    g = torch.Generator().manual_seed(L)
+    extra = torch.randint(0, L, (24,), generator=g).tolist()
+    return torch.tensor(sorted(set(base + extra)))
+
+
+def test_attention_backward_L16384_subsets():
+    from long_context_biomedical_imaging_amd import kernels
+    B, L, H = 1, 16384, 6
+    g = torch.Generator().manual_seed(16384)
+    qkv = torch.randn(B, L, 3 * H * 64, generator=g).to(torch.bfloat16)
+    dout = torch.randn(B, L, H * 64, generator=g).to(torch.bfloat16)
+    x = qkv.cuda().requires_grad_(True)
+    out = kernels.flash_attention(x, H, SCALE)
+    out.backward(dout.cuda())
+    dq_gpu, dk_gpu, dv_gpu = (x.grad[..., i * H * 64:(i + 1) * H * 64].float().cpu().view(B, L, H, 64).permute(0, 2, 1, 3)
+                              for i in range(3))
+    o_gpu = out.detach().float().cpu()
+    del x, out
+    torch.cuda.empty_cache()
+
+    q, k, v = oatt.split_qkv(qkv.float(), H)                     # (B, H, L, 64) f32 (bf16 values, exact)
+    do = dout.float().view(B, L, H, 64).permute(0, 2, 1, 3)
+    o, lse = oatt.attention_core(q, k, v, SCALE, q_chunk=2048)    # all rows: O and natural-log lse
+    _check(o_gpu, o.permute(0, 2, 1, 3).reshape(B, L, -1), "O L16384")
+    delta = (do.double() * o.double()).sum(-1)                   # (B, H, L) = sum_j P_ij dP_ij
+    qd, kd, vd, dod, lsed = q.double(), k.double(), v.double(), do.double(), lse.double()
+
+    rows = _subset(L)
+    s = torch.einsum("bhid,bhjd->bhij", qd[:, :, rows], kd) * SCALE
+    p = torch.exp(s - lsed[:, :, rows, None])
+    dp = torch.einsum("bhid,bhjd->bhij", dod[:, :, rows], vd)
+    ds = p * (dp - delta[:, :, rows, None])
+    dq_ref = torch.einsum("bhij,bhjd->bhid", ds, kd) * SCALE
+    _check(dq_gpu[:, :, rows], dq_ref, "dQ rows L16384", rel=2e-2, absf=3e-2)
+
+    keys = _subset(L)
+    s = torch.einsum("bhid,bhjd->bhij", qd, kd[:, :, keys]) * SCALE          # (B, H, L, |keys|)
+    p = torch.exp(s - lsed[..., None])
+    dv_ref = torch.einsum("bhij,bhid->bhjd", p, dod)
+    dp = torch.einsum("bhid,bhjd->bhij", dod, vd[:, :, keys])
+    ds = p * (dp - delta[..., None])
+    dk_ref = torch.einsum("bhij,bhid->bhjd", ds, qd) * SCALE
+    _check(dv_gpu[:, :, keys], dv_ref, "dV keys L16384", rel=2e-2, absf=3e-2)
+    _check(dk_gpu[:, :, keys], dk_ref, "dK keys L16384", rel=2e-2, absf=3e-2)
+
+
+def test_attention_forward_L65536_rows_with_late_outlier_keys():
+    from long_context_biomedical_imaging_amd import kernels
+    B, L, H = 2, 65536, 6
+    C = H * 64
+    g = torch.Generator().manual_seed(65536)
+    qkv = torch.randn(B, L, 3 * C, generator=g)
+    # huge-norm keys late in the sweep: 4x the typical key norm (scores up to ~4 sigma larger)
+    for b, pos in ((0, 60001), (0, 65535), (1, 40000), (1, 65500)):
+        qkv[b, pos, C:2 * C] *= 4.0
+    qkv = qkv.to(torch.bfloat16)
+    out, lse2 = kernels.attn_fwd(qkv.cuda(), H, SCALE)
+    out, lse2 = out.float().cpu(), lse2.cpu()
+    rows = _subset(L)
+    q, k, v = oatt.split_qkv(qkv.float(), H)
+    qd, kd, vd = q[:, :, rows].double(), k.double(), v.double()
+    s = torch.einsum("bhid,bhjd->bhij", qd, kd) * SCALE
+    lse = torch.logsumexp(s, -1)
+    o = torch.einsum("bhij,bhjd->bhid", torch.softmax(s, -1), vd)
+    ref = o.permute(0, 2, 1, 3).reshape(B, len(rows), C)
+    # the kernel rounds q * scale * log2(e) to bf16 once (the reference's autocast path rounds the scores
+    # themselves); emulate exactly that to bound the error the rounding alone explains
+    qe = (q[:, :, rows] * (SCALE * LOG2E)).to(torch.bfloat16).double()
+    se = torch.einsum("bhid,bhjd->bhij", qe, kd)
+    pe = torch.exp2(se - se.max(-1, keepdim=True).values)
+    emu = (torch.einsum("bhij,bhjd->bhid", pe.to(torch.bfloat16).double(), vd) / pe.sum(-1, keepdim=True))
+    emu = emu.permute(0, 2, 1, 3).reshape(B, len(rows), C)
+    # the reference's own autocast GPU path on the same rows (backbone_vit.py:191-201: bf16 einsum output, bf16
+    # `* scale`, f32 softmax rounded to bf16 before the AV einsum): with 65536 keys and diffuse attention, rounding
+    # P to bf16 (both paths do) alone costs ~1e-2 rel-L2 on O, so the bound is max(1e-2, the reference's deviation)
+    sa = torch.einsum("bhid,bhjd->bhij", q[:, :, rows], k).to(torch.bfloat16)
+    pa = (sa * SCALE).to(torch.bfloat16).float().softmax(-1).to(torch.bfloat16).double()
+    ac = torch.einsum("bhij,bhjd->bhid", pa, vd).permute(0, 2, 1, 3).reshape(B, len(rows), C)
+    got = out[:, rows]
+    _check(got, ref, "O rows L65536", rel=max(1e-2, rel_err(ac, ref)))
+    assert rel_err(got, emu) <= 3e-3, f"kernel vs its own rounding emulation: {rel_err(got, emu):.3e}"
+    lse_got = lse2[:, :, rows].double() / LOG2E
+    assert (lse_got - lse).abs().max().item() < 1e-3 * max(1.0, lse.abs().max().item())

@@ -209,3 +209,30 @@ def test_oracle_gradients_fp64_gradcheck():
     assert gradcheck(lambda *a: oss.selective_scan(*a, delta_softplus=True), (u, dt, A, B, C, D, db))
     uu, kk, dd = r(2, 3, 8), r(3, 8), r(3)
     assert gradcheck(ohy.fftconv, (uu, kk, dd))
+
+
+def test_scan_c_oracle_matches_python_restatement():
+    """oracle/scan_ref.c (fp64 per-step loop, used for the L = 2^21 GPU check) == oracle/selective_scan.py
+    (pinned by the reference fixture) on the same inputs: output and all seven gradients, fp64."""
+    from oracle import scan_c
+    from oracle import selective_scan as oss
+    torch.manual_seed(11)
+    L, d, n = 777, 16, 8
+    u = torch.randn(1, d, L)
+    delta = torch.randn(1, d, L) * 0.5 - 1.0
+    delta[0, 3, 100] = 25.0   # softplus threshold branch
+    A = -torch.exp(torch.randn(d, n) * 0.3)
+    Bm, Cm = torch.randn(1, n, L), torch.randn(1, n, L)
+    D, db = torch.randn(d), torch.randn(d) * 0.1
+    dy = torch.randn(1, d, L)
+    ins = [t.double().requires_grad_(True) for t in (u, delta, A, Bm, Cm, D, db)]
+    yr = oss.selective_scan(*ins[:6], delta_bias=ins[6], delta_softplus=True)
+    (yr * dy.double()).sum().backward()
+    cl = lambda t: t[0].T.numpy()  # noqa: E731  (1, c, L) -> (L, c)
+    y = scan_c.scan_fwd(cl(u), cl(delta), A.numpy(), cl(Bm), cl(Cm), D.numpy(), db.numpy())
+    assert np.abs(y - cl(yr.detach())).max() < 1e-10 * max(1.0, np.abs(y).max())
+    du, dd, dA, dD, ddb, dB, dC = scan_c.scan_bwd(cl(u), cl(delta), A.numpy(), cl(Bm), cl(Cm), D.numpy(),
+                                                   db.numpy(), cl(dy))
+    for mine, ref in ((du, cl(ins[0].grad)), (dd, cl(ins[1].grad)), (dA, ins[2].grad.numpy()), (dB, cl(ins[3].grad)),
+                      (dC, cl(ins[4].grad)), (dD, ins[5].grad.numpy()), (ddb, ins[6].grad.numpy())):
+        assert np.abs(mine - ref).max() < 1e-9 * max(1.0, np.abs(ref).max())

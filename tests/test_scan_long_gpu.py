@@ -1,0 +1,77 @@
+"""Selective scan at the C5 sequence length (L = 2^21 = 256^3 / 8 tokens, Dx = 192, N = 8; mamba.py:125-134).
+
+The GPU scan runs the whole sequence in thousands of chunks with the two-level carry (fwd and bwd); the
+reference is oracle/scan_ref.c, an fp64 per-step restatement of mamba-ssm's `selective_scan_ref` (cross-checked
+against the fixture-pinned Python restatement in tests/test_oracle_golden.py), run on the host cores.
+- bf16 I/O (the C5 autocast dtype) at L = 2^21, forward + all seven gradients, on the same bf16-rounded inputs:
+  rel-L2 <= 2e-2 on y and 3e-2 on the gradients (bf16 outputs; dB/dC sum 192 channels of bf16-rounded terms).
+- f32 I/O at L = 2^20 (the f32 y/z buffer of 2^21 tokens exceeds the kernel's 32-bit buffer offsets, which it
+  reports as an error), forward + all seven gradients: rel-L2 <= 2e-4 (f32 arithmetic over 2^20 steps vs f64).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import scan_c
+
+pytestmark = pytest.mark.gpu
+
+L, DX, N = 1 << 21, 192, 8
+
+
+def _inputs(seed, Lr):
+    g = torch.Generator().manual_seed(seed)
+    u = torch.randn(1, Lr, DX, generator=g)
+    delta = torch.randn(1, Lr, DX, generator=g) * 0.5 - 1.0
+    A = -torch.exp(torch.randn(DX, N, generator=g) * 0.3)
+    BC = torch.randn(1, Lr, 2 * N, generator=g)
+    D = torch.randn(DX, generator=g)
+    db = torch.randn(DX, generator=g) * 0.1
+    return u, delta, A, BC, D, db
+
+
+def _rel(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+
+
+def _run(dtype, Lr, seed):
+    from long_context_biomedical_imaging_amd import kernels
+    u, delta, A, BC, D, db = _inputs(seed, Lr)
+    g = torch.Generator().manual_seed(seed + 1)
+    dy = torch.randn(1, Lr, DX, generator=g).to(dtype)
+    q = lambda t: t.to(dtype)  # noqa: E731
+    uc = q(u).cuda().requires_grad_(True)
+    dc = q(delta).cuda().requires_grad_(True)
+    Ac = A.cuda().requires_grad_(True)
+    BCc = q(BC).cuda().requires_grad_(True)
+    Dc = D.cuda().requires_grad_(True)
+    bc = db.cuda().requires_grad_(True)
+    yz = torch.zeros(1, Lr, 2 * DX, device="cuda", dtype=dtype)
+    out = kernels.selective_scan_cl(uc, dc, Ac, BCc[..., :N], BCc[..., N:], Dc, bc, yz)
+    (out[..., :DX].float() * dy.cuda().float()).sum().backward()
+    y = out[0, :, :DX].detach().float().cpu().numpy()
+    grads = {"u": uc.grad[0].float().cpu().numpy(), "delta": dc.grad[0].float().cpu().numpy(),
+             "A": Ac.grad.cpu().numpy(), "B": BCc.grad[0, :, :N].float().cpu().numpy(),
+             "C": BCc.grad[0, :, N:].float().cpu().numpy(), "D": Dc.grad.cpu().numpy(),
+             "delta_bias": bc.grad.cpu().numpy()}
+    del uc, dc, BCc, yz, out
+    torch.cuda.empty_cache()
+    f = lambda t: q(t).float().numpy()  # noqa: E731  (the reference sees the same rounded inputs)
+    args = (f(u[0]), f(delta[0]), A.numpy(), f(BC[0, :, :N]), f(BC[0, :, N:]), D.numpy(), db.numpy())
+    yr = scan_c.scan_fwd(*args)
+    ref = dict(zip(("u", "delta", "A", "D", "delta_bias", "B", "C"), scan_c.scan_bwd(*args, f(dy[0]))))
+    return y, yr, grads, ref
+
+
+@pytest.mark.parametrize("dtype,Lr,tol_y,tol_g", [(torch.bfloat16, L, 2e-2, 3e-2), (torch.float32, L // 2, 2e-4, 2e-4)])
+def test_scan_full_length_fwd_bwd(dtype, Lr, tol_y, tol_g):
+    y, yr, grads, ref = _run(dtype, Lr, 0 if dtype == torch.float32 else 2)
+    assert _rel(y, yr) < tol_y, f"y rel {_rel(y, yr):.3e}"
+    assert _rel(y[-4096:], yr[-4096:]) < tol_y, "y over the last 4096 tokens (after ~L steps of carries)"
+    for name, r in ref.items():
+        e = _rel(grads[name], r)
+        assert e < tol_g, f"d{name} rel {e:.3e}"
+    e = _rel(grads["u"][:4096], ref["u"][:4096])   # the first tokens: reverse carry over the whole sequence
+    assert e < tol_g, f"du over the first 4096 tokens: {e:.3e}"

@@ -1,0 +1,154 @@
+"""Bit-exact GPU check of the Swin grid-mode index maps (north_star: "bit-exact for window index/shift ops").
+
+The window kernels never materialise the padded / rolled / partitioned grid: each window token's source voxel is
+address arithmetic (`win_row`), the region id of compute_mask is recomputed per window type (`win_type`,
+`win_region`), and the -100 mask lives in the bias table built by lci_window_bias. `lci_window_index_map` exports
+the maps from the *same* __device__ functions, and `window_bias_table` returns the table the kernels read. They
+are compared integer-for-integer with
+  - the reference's own outputs: the `swin_index` goldens (sha256 of the shifted window_partition permutation
+    and of compute_mask's nonzero pattern at 14^3, 21^3, 35^3, 70^3, generated from backbone_swin.py by
+    tools/gen_golden.py), and
+  - the oracle restatement of F.pad -> torch.roll(-shift) -> window_partition (backbone_swin.py:135-165,
+    435-487) and compute_mask (:591-628) on padded, 2-D, batched and window-collapse geometries, including the
+    C3 stage-1 grid (64^3 padded to 70^3, 1000 windows, 8 window types).
+Plus one grid-mode forward at the true C3 stage-1 shape (64^3, C = 96, 3 heads, shift 3, B = 1) vs the oracle.
+"""
+import hashlib
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from golden_util import Golden, rel_err
+from oracle import window as ow
+
+pytestmark = pytest.mark.gpu
+
+LOG2E = 1.4426950408889634
+
+
+def _ref_src(B, S, ws, sh):
+    """Reference index map: the voxel row each window token reads (-1 = zero padding), by the reference's own
+    sequence of tensor ops applied to an index grid."""
+    idx = torch.arange(B * math.prod(S), dtype=torch.float64).reshape(B, *S, 1)
+    pads = [(w - s % w) % w for s, w in zip(S, ws)]
+    padarg = []
+    for p in reversed(pads):
+        padarg += [0, p]
+    x = F.pad(idx, [0, 0] + padarg, value=-1.0)
+    if any(v > 0 for v in sh):
+        x = torch.roll(x, shifts=tuple(-v for v in sh), dims=tuple(range(1, len(S) + 1)))
+    return ow.window_partition(x, tuple(ws)).reshape(-1, math.prod(ws)).long()
+
+
+def _ref_mask(S, ws, sh):
+    """compute_mask on the padded dims (nW, N, N) != 0, or None when unshifted."""
+    if not any(v > 0 for v in sh):
+        return None
+    return ow.compute_mask(ow.padded_dims(tuple(S), ws), ws, sh) != 0
+
+
+def _kernel_maps(B, S, ws, sh):
+    from long_context_biomedical_imaging_amd import kernels
+    src, reg, rid, wt = kernels.window_index_map(B, S, ws, sh)
+    torch.cuda.synchronize()
+    return src.long().cpu(), reg.long().cpu(), rid.long().cpu(), wt.long().cpu()
+
+
+@pytest.mark.parametrize("d", [14, 21, 35, 70])
+def test_index_maps_vs_reference_goldens(d):
+    """Unpadded cubes with shift 3: the kernel's partition permutation and mask hash to the reference's."""
+    g = Golden("swin_index")
+    src, reg, rid, wt = _kernel_maps(1, (d, d, d), (7, 7, 7), (3, 3, 3))
+    perm = src.reshape(-1).numpy().astype(np.int32)
+    assert hashlib.sha256(perm.tobytes()).hexdigest() == str(g.z[f"out/partition_sha256_{d}"])
+    nz = (reg[:, :, None] != reg[:, None, :]).numpy()
+    assert list(nz.shape) == list(g.z[f"out/mask_shape_{d}"])
+    assert int(nz.sum()) == int(g.z[f"out/mask_nnz_{d}"])
+    assert hashlib.sha256(np.packbits(nz).tobytes()).hexdigest() == str(g.z[f"out/mask_sha256_{d}"])
+    assert torch.equal(rid, reg)
+
+
+GEOMS = [
+    (1, (64, 64, 64), (7, 7, 7), (3, 3, 3)),    # C3 stage 1: 64 -> 70, 1000 windows, 8 types
+    (1, (32, 32, 32), (7, 7, 7), (3, 3, 3)),    # C3 stage 2: 32 -> 35
+    (2, (16, 16, 16), (7, 7, 7), (3, 3, 3)),    # C3 stage 3: 16 -> 21, batch 2
+    (1, (8, 8, 8), (7, 7, 7), (3, 3, 3)),       # C3 stage 4: 8 -> 14
+    (2, (10, 10, 10), (7, 7, 7), (0, 0, 0)),    # unshifted block, padded
+    (1, (5, 9, 40), (5, 7, 7), (0, 3, 3)),      # get_window_size collapse on the first axis (window = dim, no shift)
+    (1, (8, 8, 8), (4, 4, 4), (2, 2, 2)),       # window 4 (project scripts)
+    (2, (9, 20), (7, 7), (3, 3)),               # 2-D
+    (1, (256, 256), (7, 7), (3, 3)),            # 2-D at 512^2 patch 2 (256 -> 259)
+]
+
+
+@pytest.mark.parametrize("B,S,ws,sh", GEOMS)
+def test_index_maps_vs_reference_ops(B, S, ws, sh):
+    src, reg, rid, wt = _kernel_maps(B, S, ws, sh)
+    ref = _ref_src(B, S, ws, sh)
+    assert src.shape == ref.shape
+    assert torch.equal(src, ref), f"{int((src != ref).sum())} mismatched window-token rows"
+    mask = _ref_mask(S, ws, sh)
+    nW = src.shape[0] // B
+    if mask is None:
+        assert (reg == 0).all() and (rid == 0).all() and (wt == 0).all()
+        return
+    mine = reg[:, :, None] != reg[:, None, :]
+    for b in range(B):
+        assert torch.equal(mine[b * nW:(b + 1) * nW], mask), "region-id mask != compute_mask"
+    assert torch.equal(rid, reg)
+
+
+@pytest.mark.parametrize("B,S,ws,sh", [g for g in GEOMS if any(v > 0 for v in g[3])])
+def test_bias_table_mask_bit_exact(B, S, ws, sh):
+    """The table the kernels add to the logits: with rpb = 0 every entry is exactly bf16(-100 log2 e) where
+    compute_mask has -100, exactly 0 where it has 0, and -1e30 on padded rows/columns; window w uses the table
+    of its type wtype[w]."""
+    from long_context_biomedical_imaging_amd import kernels
+    N = math.prod(ws)
+    tab = kernels.window_bias_table(torch.zeros(1, N, N, device="cuda"), B, S, ws, sh, 1).cpu()
+    _, _, _, wt = _kernel_maps(B, S, ws, sh)
+    mask = _ref_mask(S, ws, sh)
+    nW = mask.shape[0]
+    m100 = torch.tensor(-100.0 * LOG2E).to(torch.bfloat16)
+    t = tab[:, 0].float()
+    assert (t[:, N:, :] < -1e29).all() and (t[:, :N, N:] < -1e29).all()   # bf16(-1e30) on padded rows / columns
+    core = tab[:, 0, :N, :N]
+    vals = set(core.float().unique().tolist())
+    assert vals <= {0.0, m100.float().item()}, vals
+    for w in range(nW):
+        assert torch.equal(core[wt[w]] != 0, mask[w]), f"window {w} type {int(wt[w])}"
+
+
+def test_c3_stage1_grid_forward_vs_oracle():
+    """Grid-mode window attention at the C3 stage-1 shape (64^3 tokens, C = 96, 3 heads, window 7, shift 3,
+    padded to 70^3) against the oracle's explicit pad/roll/partition path, B = 1. bf16 MFMA: rel-L2 <= 2e-2,
+    plus every window-token row compared: no row may be an outlier (a mis-mapped token would stand out at
+    O(1) relative error where bf16 rounding gives <= 5e-2)."""
+    from long_context_biomedical_imaging_amd import backbone_swin
+    torch.manual_seed(5)
+    blk = backbone_swin.SwinTransformerBlock(False, False, 96, 3, (7, 7, 7), (3, 3, 3), qkv_bias=True)
+    with torch.no_grad():
+        blk.attn.relative_position_bias_table.normal_(0, 0.5)
+        blk.attn.qkv.bias.normal_(0, 0.5)
+    blk = blk.cuda()
+    x = torch.randn(1, 64, 64, 64, 96)
+    with torch.no_grad():
+        out = blk.forward_part1(x.cuda(), None).float().cpu()
+        a = blk.attn
+        sd = {k: (v.detach().float() if v.is_floating_point() else v).cpu() for k, v in blk.state_dict().items()}
+
+        def attn_fn(win, mask):
+            return ow.window_attention(win, mask, sd["attn.qkv.weight"], sd["attn.qkv.bias"], sd["attn.proj.weight"],
+                                       sd["attn.proj.bias"], sd["attn.relative_position_bias_table"],
+                                       sd["attn.relative_position_index"], a.num_heads)
+
+        mask = ow.compute_mask(ow.padded_dims((64, 64, 64), (7, 7, 7)), (7, 7, 7), (3, 3, 3)).float()
+        ref = ow.swin_part1(x, sd["norm1.weight"], sd["norm1.bias"], (7, 7, 7), (3, 3, 3), attn_fn, mask)
+    assert out.shape == ref.shape == (1, 64, 64, 64, 96)
+    assert rel_err(out, ref) < 2e-2
+    rn = ref.reshape(-1, 96).norm(dim=1)
+    row_err = (out - ref).reshape(-1, 96).norm(dim=1) / rn.clamp_min(0.1 * rn.mean().item())
+    assert row_err.max().item() < 0.1, f"worst token row rel err {row_err.max().item():.3g}"
