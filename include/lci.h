@@ -148,7 +148,7 @@ int lci_dwconv_silu_bwd(int dtype, const void* in, const float* wx, const float*
                         int zoff, void* stream);
 
 /* ------------------------------------------------------------------ Hyena long convolution (f32)
- * FFT size n = lci_fft_size(L) = pow2 >= 2L (L <= 131072). tw: n complex f32 (f32x2) from lci_fft_twiddles.
+ * FFT size n = lci_fft_size(L) = pow2 >= 2L (L <= 262144). tw: n complex f32 (f32x2) from lci_fft_twiddles.
  * Rows are channel-major f32 (R, C, L); the filter of row r is r % C; k (C, L). */
 long long lci_fft_size(int L);
 int lci_fft_twiddles(void* tw, int n, void* stream);

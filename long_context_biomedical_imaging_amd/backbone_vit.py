@@ -46,15 +46,24 @@ def custom_ViT(config, input_feature_channels):
     model = ViT_with_alt_ops(use_hyena=v.use_hyena, use_mamba=v.use_mamba, in_channels=input_feature_channels,
                              img_size=input_size, patch_size=mod_patch_size, hidden_size=hidden_size,
                              mlp_dim=mlp_dim, num_layers=num_layers, num_heads=num_heads, dropout_rate=0.0,
-                             spatial_dims=spatial_dims, classification=config.task_type == "class")
+                             spatial_dims=spatial_dims, classification=config.task_type == "class",
+                             hyena_l_max=getattr(v, "hyena_l_max", HYENA_L_MAX))
     return model, [hidden_size] * 13
+
+
+# The reference hard-codes HyenaOperator(l_max=66000) (backbone_vit.py:172), so any sequence longer than 66000
+# tokens raises (hyena.py:314) -- among them BASELINE configs[3] (1024^2 patch 2, L = 262144). `hyena_l_max`
+# (config --ViT.hyena_l_max, default 66000 = the reference) is an opt-in deviation that sizes the implicit
+# filter (and its positional-embedding Parameter, (1, l_max, 3)) for longer sequences.
+HYENA_L_MAX = 66000
 
 
 class SABlock(nn.Module):
     """Token mixer: full self-attention (flash, HIP), or HyenaOperator, or MambaVisionMixer."""
 
     def __init__(self, use_hyena: bool, use_mamba: bool, hidden_size: int, num_heads: int,
-                 dropout_rate: float = 0.0, qkv_bias: bool = False, save_attn: bool = False) -> None:
+                 dropout_rate: float = 0.0, qkv_bias: bool = False, save_attn: bool = False, *,
+                 hyena_l_max: int = HYENA_L_MAX) -> None:
         super().__init__()
         if not (0 <= dropout_rate <= 1):
             raise ValueError("dropout_rate should be between 0 and 1.")
@@ -73,7 +82,7 @@ class SABlock(nn.Module):
             self.qkv = nn.Linear(hidden_size, hidden_size * 3, bias=qkv_bias)
             self.out_proj = nn.Linear(hidden_size, hidden_size)
         elif use_hyena and not use_mamba:
-            self.hyena = HyenaOperator(d_model=hidden_size, l_max=66000, filter_order=64, num_heads=num_heads,
+            self.hyena = HyenaOperator(d_model=hidden_size, l_max=hyena_l_max, filter_order=64, num_heads=num_heads,
                                        num_blocks=1, short_filter_order=5, bidrectional=True,
                                        dropout=dropout_rate, filter_dropout=dropout_rate, activation="id")
         elif not use_hyena and use_mamba:
@@ -104,7 +113,8 @@ class SABlock(nn.Module):
 
 class TransformerBlock(nn.Module):
     def __init__(self, use_hyena: bool, use_mamba: bool, hidden_size: int, mlp_dim: int, num_heads: int,
-                 dropout_rate: float = 0.0, qkv_bias: bool = False, save_attn: bool = False) -> None:
+                 dropout_rate: float = 0.0, qkv_bias: bool = False, save_attn: bool = False, *,
+                 hyena_l_max: int = HYENA_L_MAX) -> None:
         super().__init__()
         if not (0 <= dropout_rate <= 1):
             raise ValueError("dropout_rate should be between 0 and 1.")
@@ -114,7 +124,8 @@ class TransformerBlock(nn.Module):
         self.norm1 = TokenLayerNorm(hidden_size)
         self.use_hyena = use_hyena
         self.use_mamba = use_mamba
-        self.attn = SABlock(use_hyena, use_mamba, hidden_size, num_heads, dropout_rate, qkv_bias, save_attn)
+        self.attn = SABlock(use_hyena, use_mamba, hidden_size, num_heads, dropout_rate, qkv_bias, save_attn,
+                            hyena_l_max=hyena_l_max)
         self.norm2 = TokenLayerNorm(hidden_size)
 
     def forward(self, x):
@@ -133,7 +144,7 @@ class ViT_with_alt_ops(nn.Module):
                  num_layers: int = 12, num_heads: int = 12, pos_embed: str = "conv", proj_type: str = "conv",
                  pos_embed_type: str = "learnable", classification: bool = False, num_classes: int = 2,
                  dropout_rate: float = 0.0, spatial_dims: int = 3, post_activation="Tanh",
-                 qkv_bias: bool = False, save_attn: bool = False) -> None:
+                 qkv_bias: bool = False, save_attn: bool = False, *, hyena_l_max: int = HYENA_L_MAX) -> None:
         super().__init__()
         if not (0 <= dropout_rate <= 1):
             raise ValueError("dropout_rate should be between 0 and 1.")
@@ -150,7 +161,7 @@ class ViT_with_alt_ops(nn.Module):
                                                    spatial_dims=spatial_dims)
         self.blocks = nn.ModuleList([
             TransformerBlock(use_hyena, use_mamba, hidden_size, mlp_dim, num_heads, dropout_rate, qkv_bias,
-                             save_attn) for _ in range(num_layers)])
+                             save_attn, hyena_l_max=hyena_l_max) for _ in range(num_layers)])
         self.norm = nn.LayerNorm(hidden_size)
         # Not a reference option: per-block activation checkpointing (recompute each block's forward in the
         # backward) for token counts whose saved activations exceed one GPU (256^3 p2: ~35 GB per block).

@@ -78,6 +78,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--ViT.num_heads", type=int, default=12)
     p.add_argument("--ViT.use_hyena", type=str_to_bool, default=False)
     p.add_argument("--ViT.use_mamba", type=str_to_bool, default=False)
+    # not a reference flag: opt-in Hyena filter length (the reference hard-codes 66000, backbone_vit.py:172, and
+    # raises for longer sequences, hyena.py:314); needed for configs[3] (1024^2 patch 2, L = 262144)
+    p.add_argument("--ViT.hyena_l_max", type=int, default=66000)
     # model_parser.py:39-47
     p.add_argument("--Swin.size", type=str, default="tiny", choices=["unetr", "tiny", "small", "base", "large", "custom"])
     p.add_argument("--Swin.patch_size", nargs="+", type=int, default=[2, 2, 2])

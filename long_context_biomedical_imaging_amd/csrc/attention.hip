@@ -54,6 +54,20 @@ constexpr float NEG_BIG = -1.0e30f;
 #define LCI_SCHED_HINT()
 #endif
 
+// Static priority for waves 4-7 (the arbitration losers of an 8-wave workgroup; MI355X_MICROARCH.md "Two waves
+// per SIMD" item 4): -DLCI_PRIO_YOUNG=1 sets s_setprio 1 on them once, before the main loop.
+#ifndef LCI_PRIO_YOUNG
+#define LCI_PRIO_YOUNG 0
+#endif
+__device__ __forceinline__ void prio_young(int wave) {
+  if (LCI_PRIO_YOUNG && wave >= 4) __builtin_amdgcn_s_setprio(1);
+}
+// dK/dV row constants: 0 = extra MFMA k-step on bf16 hi/mid/lo splits staged in the Q/dO rows (default);
+// 1 = f32 -lse2 / -delta staged in a side LDS array, subtracted on the VALU (2 fewer MFMAs of 18 per half-tile)
+#ifndef LCI_DKDV_ROWC_VALU
+#define LCI_DKDV_ROWC_VALU 0
+#endif
+
 struct AttnArgs {
   const bf16* q; const bf16* k; const bf16* v;    // base pointers of head 0, batch 0
   const bf16* o; const bf16* dout;                 // bwd only
@@ -216,6 +230,7 @@ __global__ __launch_bounds__(FW_NW * 64, 1) void attn_fwd2_kernel(AttnArgs a, co
 
   f32x16 o0 = {}, o1 = {}, negm = {};
   float m_run = 0.f, l_run = 0.f;
+  prio_young(wave);
 
   auto mask_ragged = [&](int kt, f32x16& t0, f32x16& t1) __attribute__((always_inline)) {
 #pragma unroll
@@ -452,7 +467,15 @@ __global__ __launch_bounds__(NW * 64, (KB == 1 ? 8 / NW : 4 / NW)) void attn_bwd
   // -lse2 (-delta) split into three bf16 terms (hi + mid + lo carries ~24 bits), and the matching B fragment is
   // 1 in rows 0..2. The chains then yield S c - lse2 and dP - delta with no per-lane row-constant loads
   // (those were a third of this kernel's LDS read cycles) and no accumulator initialisation moves.
+  __shared__ __attribute__((aligned(16))) float rowc[2][2][KT];   // ROWC_VALU: [buf][lse2 | delta][query]
   auto stage_rowc = [&](int buf, int qt) __attribute__((always_inline)) {
+    if constexpr (LCI_DKDV_ROWC_VALU) {
+      if (tid < 2 * KT) {
+        const int which = tid / KT, qi = tid % KT, q = qt * KT + qi;
+        rowc[buf][which][qi] = which == 0 ? ((q < L) ? lsep[q] : 1.0e30f) : ((q < L) ? dlp[q] : 0.f);
+      }
+      return;
+    }
     if (tid < 2 * KT) {
       const int which = tid / KT, qi = tid % KT, q = qt * KT + qi;
       float v;
@@ -478,6 +501,7 @@ __global__ __launch_bounds__(NW * 64, (KB == 1 ? 8 / NW : 4 / NW)) void attn_bwd
   f32x16 dv0[KB], dv1[KB], dk0[KB], dk1[KB];
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb) dv0[kb] = dv1[kb] = dk0[kb] = dk1[kb] = f32x16{};
+  prio_young(wave);
   for (int qt = 0; qt < nqt; ++qt) {
     const int buf = qt & 1;
     const bf16* ql = smem + buf * TILE;
@@ -493,8 +517,10 @@ __global__ __launch_bounds__(NW * 64, (KB == 1 ? 8 / NW : 4 / NW)) void attn_bwd
       // Row constants enter as the extra k-step: the chains give S c - lse2[q] and dP - delta[q] directly;
       // then P = exp2(.), dS = P (dP - delta).
       bf16x8 qa[5], da[5];
-      qa[4] = frag_row_sw(ql, qs * 32, 64, lane);
-      da[4] = frag_row_sw(dl, qs * 32, 64, lane);
+      if constexpr (!LCI_DKDV_ROWC_VALU) {
+        qa[4] = frag_row_sw(ql, qs * 32, 64, lane);
+        da[4] = frag_row_sw(dl, qs * 32, 64, lane);
+      }
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         qa[ks] = frag_row_sw(ql, qs * 32, ks * 16, lane);
@@ -503,12 +529,35 @@ __global__ __launch_bounds__(NW * 64, (KB == 1 ? 8 / NW : 4 / NW)) void attn_bwd
       f32x16 s[KB], p[KB];
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
-        s[kb] = mfma32(qa[4], onef, f32x16{});
-        p[kb] = mfma32(da[4], onef, f32x16{});
+        if constexpr (LCI_DKDV_ROWC_VALU) {
+          s[kb] = mfma32(qa[0], kf[kb][0], f32x16{});
+          p[kb] = mfma32(da[0], vf[kb][0], f32x16{});
+        } else {
+          s[kb] = mfma32(qa[4], onef, f32x16{});
+          p[kb] = mfma32(da[4], onef, f32x16{});
+          s[kb] = mfma32(qa[0], kf[kb][0], s[kb]);
+          p[kb] = mfma32(da[0], vf[kb][0], p[kb]);
+        }
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
+        for (int ks = 1; ks < 4; ++ks) {
           s[kb] = mfma32(qa[ks], kf[kb][ks], s[kb]);
           p[kb] = mfma32(da[ks], vf[kb][ks], p[kb]);
+        }
+      }
+      if constexpr (LCI_DKDV_ROWC_VALU) {
+        // query of accumulator register i of this lane: qs*32 + 8(i>>2) + 4*half + (i&3): 4 contiguous per group
+        const float* rl = &rowc[buf][0][qs * 32 + 4 * half];
+        const float* rd = &rowc[buf][1][qs * 32 + 4 * half];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 l4 = *(const f32x4*)(rl + 8 * g), d4 = *(const f32x4*)(rd + 8 * g);
+#pragma unroll
+          for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              s[kb][4 * g + jj] -= l4[jj];
+              p[kb][4 * g + jj] -= d4[jj];
+            }
         }
       }
       const bf16x8 tdo00 = frag_tr_sw<0>(dl, qs * 32, 0, lane), tdo10 = frag_tr_sw<1>(dl, qs * 32, 0, lane);
@@ -634,6 +683,7 @@ __global__ __launch_bounds__(FW_NW * 64, 1) void attn_bwd_dq2_kernel(AttnArgs a)
   __syncthreads();
 
   f32x16 s0, s1, p0, p1, dq0 = {}, dq1 = {};
+  prio_young(wave);
   // chains of keys kb*32..+31 of the tile in `slot`
   auto chains = [&](int slot, int kb, f32x16& sx, f32x16& px) __attribute__((always_inline)) {
     const bf16* kl = smem + slot * QSLOT;

@@ -610,7 +610,7 @@ __global__ __launch_bounds__(256) void hyena_pre_bwd_ring_kernel(GateArgs a) {
 }
 
 static int fft_plan(FftArgs& a, int L) {
-  LCI_CHECK(L > 0 && L <= (1 << 17), "fftconv: L %d unsupported (<= 131072)", L);
+  LCI_CHECK(L > 0 && L <= (1 << 18), "fftconv: L %d unsupported (<= 262144)", L);
   int e = 1;
   while ((1 << e) < 2 * L) ++e;
   a.n = 1 << e;
@@ -620,6 +620,8 @@ static int fft_plan(FftArgs& a, int L) {
   static const int env_ln1 = getenv("LCI_FFT_LN1") ? atoi(getenv("LCI_FFT_LN1")) : 8;
   static const int env_g = getenv("LCI_FFT_G") ? atoi(getenv("LCI_FFT_G")) : 8;
   a.ln1 = e < env_ln1 ? e : env_ln1;
+  // the row pass keeps ~11 n2-point complex rows in LDS: n2 <= 1024 (n = 2^19 at L = 262144: n1 = 512, n2 = 1024)
+  if (e - a.ln1 > 10) a.ln1 = e - 10;
   a.ln2 = e - a.ln1;
   if (a.ln2 == 0) { a.ln1 = e - 1; a.ln2 = 1; }
   a.n1 = 1 << a.ln1; a.n2 = 1 << a.ln2;

@@ -18,7 +18,7 @@ if [ "$1" = build ]; then
         /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result -munsafe-fp-atomics \
           -Xarch_device -mllvm=-amdgpu-mfma-vgpr-form $extra -c $f -o $OUT/$name.$b.o &
       else
-        /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -c $f -o $OUT/$name.$b.o &
+        /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -I $ROOT/include -c $f -o $OUT/$name.$b.o &
       fi
       objs="$objs $OUT/$name.$b.o"
     done
