@@ -18,6 +18,7 @@
 // transposing through LDS to the channel-major rows the FFT wants.
 #include "common.hpp"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace lci {
@@ -609,6 +610,192 @@ __global__ __launch_bounds__(256) void hyena_pre_bwd_ring_kernel(GateArgs a) {
   if (a.db) atomicAdd(a.db + c, dbl);
 }
 
+// ------------------------------------------------------------- short conv + gating, register-ring kernels
+// One lane = one output channel ch of D (64 per workgroup), waves split the tokens: each wave runs HY_TW
+// consecutive tokens with the causal short-conv taps of its three gate channels (x1, x2, v = conv channels base,
+// base + hd, base + 2 hd, hyena.py:321-330) in register rings, so every z element is loaded once per wave
+// (+ K - 1 halo tokens), 8 tokens' loads in flight; the channel-major f32 rows (vg / dvg, what the FFT passes
+// read) go through an LDS tile so both sides of the transpose are coalesced.
+constexpr int HY_TT = 128;   // tokens per workgroup tile
+constexpr int HY_TW = 32;    // tokens per wave
+constexpr int HY_PF = 8;     // tokens whose loads are issued together
+
+template <typename T>
+__device__ __forceinline__ float zld(const T* zb, long long t, int L, int D3, int c) {
+  return (t >= 0 && t < L) ? (float)zb[t * D3 + c] : 0.f;
+}
+
+template <typename T, int KC>
+__global__ __launch_bounds__(256) void hyena_pre_fwd2_kernel(GateArgs a) {
+  __shared__ float vgt[64][HY_TT + 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int t0 = blockIdx.x * HY_TT, ch0 = blockIdx.y * 64, bb = blockIdx.z;
+  const int ch = ch0 + lane, L = a.L, D3 = 3 * a.D;
+  const bool valid = ch < a.D;
+  const int chc = valid ? ch : a.D - 1;
+  const int h = chc / a.hd, jj = chc - h * a.hd;
+  const int c1 = h * 3 * a.hd + jj, c2 = c1 + a.hd, c3 = c1 + 2 * a.hd;
+  const T* zb = (const T*)a.z + (long long)bb * L * D3;
+  float w1[KC], w2[KC], w3[KC];
+#pragma unroll
+  for (int i = 0; i < KC; ++i) { w1[i] = a.w[c1 * KC + i]; w2[i] = a.w[c2 * KC + i]; w3[i] = a.w[c3 * KC + i]; }
+  const float b1 = a.bias ? a.bias[c1] : 0.f, b2 = a.bias ? a.bias[c2] : 0.f, b3 = a.bias ? a.bias[c3] : 0.f;
+  const int ts = t0 + wave * HY_TW, te = min(L, ts + HY_TW);
+  float r1[KC], r2[KC], r3[KC];   // z[t - KC + 1 .. t] of the three channels
+#pragma unroll
+  for (int i = 1; i < KC; ++i) {
+    r1[i] = zld(zb, ts - KC + i, L, D3, c1);
+    r2[i] = zld(zb, ts - KC + i, L, D3, c2);
+    r3[i] = zld(zb, ts - KC + i, L, D3, c3);
+  }
+  T* x2p = (T*)a.x2 + (long long)bb * L * a.D + ch;
+#pragma unroll
+  for (int g = 0; g < HY_TW; g += HY_PF) {
+    float n1[HY_PF], n2[HY_PF], n3[HY_PF];
+#pragma unroll
+    for (int u = 0; u < HY_PF; ++u) {
+      const long long t = ts + g + u;
+      n1[u] = zld(zb, t, L, D3, c1);
+      n2[u] = zld(zb, t, L, D3, c2);
+      n3[u] = zld(zb, t, L, D3, c3);
+    }
+#pragma unroll
+    for (int u = 0; u < HY_PF; ++u) {
+      const int t = ts + g + u;
+#pragma unroll
+      for (int i = 0; i < KC - 1; ++i) { r1[i] = r1[i + 1]; r2[i] = r2[i + 1]; r3[i] = r3[i + 1]; }
+      r1[KC - 1] = n1[u]; r2[KC - 1] = n2[u]; r3[KC - 1] = n3[u];
+      float x1 = b1, x2 = b2, v = b3;
+#pragma unroll
+      for (int i = 0; i < KC; ++i) { x1 = fmaf(w1[i], r1[i], x1); x2 = fmaf(w2[i], r2[i], x2); v = fmaf(w3[i], r3[i], v); }
+      if (t < te) {
+        if (valid) x2p[(long long)t * a.D] = (T)x2;
+        vgt[lane][t - t0] = v * x1;
+      }
+    }
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < 64 * HY_TT; idx += 256) {
+    const int row = idx / HY_TT, col = idx - row * HY_TT;
+    const int t = t0 + col, c = ch0 + row;
+    if (c < a.D && t < L) a.vg[((long long)bb * a.D + c) * L + t] = vgt[row][col];
+  }
+}
+
+// dconv_x1 = dvg * v, dconv_v = dvg * x1, dconv_x2 = gx2; dz[s][c] = sum_i w[c][i] dconv_c[s + K - 1 - i];
+// dw[c][i] += sum_s dconv_c[s] z[s + i - (K - 1)][c]; db[c] += sum_s dconv_c[s]. Workgroups stride over token
+// tiles (so the dw/db partials are reduced over the waves and tiles in registers / LDS first and each workgroup
+// adds them once: a few hundred float atomics per address instead of one per 64-token run).
+template <typename T, int KC>
+__global__ __launch_bounds__(256) void hyena_pre_bwd2_kernel(GateArgs a) {
+  constexpr int W = HY_TT + KC - 1;            // dvg tile width: the tile's tokens + the K - 1 lookahead
+  constexpr int NR = 2 * KC - 1;               // z ring: taps of the conv at tn and of dw at s = tn - K + 1
+  constexpr int NIT = HY_TW + KC - 1;          // iterations per wave run (tn = s0 .. s1 + K - 2)
+  constexpr int NA = 3 * (KC + 1);             // dw (3 x K) + db (3) per channel
+  __shared__ float dvt[64][W | 1];
+  __shared__ float red[4][NA][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ch0 = blockIdx.y * 64, bb = blockIdx.z;
+  const int ch = ch0 + lane, L = a.L, D3 = 3 * a.D;
+  const bool valid = ch < a.D;
+  const int chc = valid ? ch : a.D - 1;
+  const int h = chc / a.hd, jj = chc - h * a.hd;
+  const int c1 = h * 3 * a.hd + jj, c2 = c1 + a.hd, c3 = c1 + 2 * a.hd;
+  const T* zb = (const T*)a.z + (long long)bb * L * D3;
+  const float* gx2 = (const float*)a.gx2 + (long long)bb * L * a.D + chc;
+  T* dzb = (T*)a.dz + (long long)bb * L * D3;
+  float w1[KC], w2[KC], w3[KC];
+#pragma unroll
+  for (int i = 0; i < KC; ++i) { w1[i] = a.w[c1 * KC + i]; w2[i] = a.w[c2 * KC + i]; w3[i] = a.w[c3 * KC + i]; }
+  const float b1 = a.bias ? a.bias[c1] : 0.f, b3 = a.bias ? a.bias[c3] : 0.f;
+  float acc[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) acc[i] = 0.f;
+  const int ntiles = (L + HY_TT - 1) / HY_TT;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int t0 = tile * HY_TT;
+    for (int idx = threadIdx.x; idx < 64 * W; idx += 256) {
+      const int row = idx / W, col = idx - row * W;
+      const int t = t0 + col, c = ch0 + row;
+      dvt[row][col] = (c < a.D && t < L) ? a.dvg[((long long)bb * a.D + c) * L + t] : 0.f;
+    }
+    __syncthreads();
+    const int s0 = t0 + wave * HY_TW, s1 = min(L, s0 + HY_TW);
+    float z1[NR], z2[NR], z3[NR], d1[KC], d2[KC], d3[KC];
+#pragma unroll
+    for (int j = 1; j < NR; ++j) {
+      z1[j] = zld(zb, s0 - NR + j, L, D3, c1);
+      z2[j] = zld(zb, s0 - NR + j, L, D3, c2);
+      z3[j] = zld(zb, s0 - NR + j, L, D3, c3);
+    }
+#pragma unroll
+    for (int i = 0; i < KC; ++i) d1[i] = d2[i] = d3[i] = 0.f;
+#pragma unroll
+    for (int g = 0; g < NIT; g += HY_PF) {
+      float n1[HY_PF], n2[HY_PF], n3[HY_PF], ng[HY_PF];
+#pragma unroll
+      for (int u = 0; u < HY_PF; ++u) {
+        const int tn = s0 + g + u;
+        n1[u] = zld(zb, tn, L, D3, c1);
+        n2[u] = zld(zb, tn, L, D3, c2);
+        n3[u] = zld(zb, tn, L, D3, c3);
+        ng[u] = (tn < L && g + u < NIT) ? gx2[(long long)tn * a.D] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < HY_PF; ++u) {
+        if (g + u < NIT) {
+          const int tn = s0 + g + u;
+#pragma unroll
+          for (int j = 0; j < NR - 1; ++j) { z1[j] = z1[j + 1]; z2[j] = z2[j + 1]; z3[j] = z3[j + 1]; }
+          z1[NR - 1] = n1[u]; z2[NR - 1] = n2[u]; z3[NR - 1] = n3[u];
+          float x1 = b1, v = b3;
+#pragma unroll
+          for (int i = 0; i < KC; ++i) { x1 = fmaf(w1[i], z1[KC - 1 + i], x1); v = fmaf(w3[i], z3[KC - 1 + i], v); }
+          const float dv = tn < L ? dvt[lane][tn - t0] : 0.f;
+#pragma unroll
+          for (int i = 0; i < KC - 1; ++i) { d1[i] = d1[i + 1]; d2[i] = d2[i + 1]; d3[i] = d3[i + 1]; }
+          d1[KC - 1] = dv * v; d2[KC - 1] = ng[u]; d3[KC - 1] = dv * x1;
+          const int s = tn - (KC - 1);
+          if (s >= s0 && s < s1) {
+            float o1 = 0.f, o2 = 0.f, o3 = 0.f;
+#pragma unroll
+            for (int i = 0; i < KC; ++i) {
+              o1 = fmaf(w1[i], d1[KC - 1 - i], o1);
+              o2 = fmaf(w2[i], d2[KC - 1 - i], o2);
+              o3 = fmaf(w3[i], d3[KC - 1 - i], o3);
+            }
+            if (valid) {
+              T* dzr = dzb + (long long)s * D3;
+              dzr[c1] = (T)o1; dzr[c2] = (T)o2; dzr[c3] = (T)o3;
+            }
+#pragma unroll
+            for (int i = 0; i < KC; ++i) {
+              acc[i] = fmaf(d1[0], z1[i], acc[i]);
+              acc[KC + 1 + i] = fmaf(d2[0], z2[i], acc[KC + 1 + i]);
+              acc[2 * KC + 2 + i] = fmaf(d3[0], z3[i], acc[2 * KC + 2 + i]);
+            }
+            acc[KC] += d1[0]; acc[2 * KC + 1] += d2[0]; acc[3 * KC + 2] += d3[0];
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < NA; ++i) red[wave][i][lane] = acc[i];
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < NA * 64; idx += 256) {
+    const int i = idx / 64, l = idx - i * 64, c = ch0 + l;
+    if (c >= a.D) continue;
+    const float sum = (red[0][i][l] + red[1][i][l]) + (red[2][i][l] + red[3][i][l]);
+    const int hh = c / a.hd, jc = c - hh * a.hd;
+    const int grp = i / (KC + 1), k = i - grp * (KC + 1);
+    const int cc = hh * 3 * a.hd + grp * a.hd + jc;
+    if (k < KC) atomicAdd(a.dw + cc * KC + k, sum);
+    else if (a.db) atomicAdd(a.db + cc, sum);
+  }
+}
+
 static int fft_plan(FftArgs& a, int L) {
   LCI_CHECK(L > 0 && L <= (1 << 18), "fftconv: L %d unsupported (<= 262144)", L);
   int e = 1;
@@ -731,6 +918,25 @@ extern "C" int lci_hyena_pre_fwd(int dtype, const void* z, const float* w, const
   LCI_CHECK(K >= 1 && K <= 8, "hyena_pre: short filter order %d unsupported (<= 8)", K);
   GateArgs a{};
   a.z = z; a.w = w; a.bias = bias; a.vg = vg; a.x2 = x2; a.BB = BB; a.L = L; a.H = H; a.hd = hd; a.D = H * hd; a.K = K;
+  {   // register-ring kernels (every order the C-ABI accepts)
+    dim3 grid2((L + HY_TT - 1) / HY_TT, (a.D + 63) / 64, BB);
+#define LCI_PRE_FWD(KK)                                                                                         \
+  case KK:                                                                                                    \
+    if (dtype == 1)                                                                                           \
+      hipLaunchKernelGGL((hyena_pre_fwd2_kernel<bf16, KK>), grid2, dim3(256), 0, (hipStream_t)stream, a);     \
+    else                                                                                                      \
+      hipLaunchKernelGGL((hyena_pre_fwd2_kernel<float, KK>), grid2, dim3(256), 0, (hipStream_t)stream, a);    \
+    LCI_LAUNCH_CHECK();                                                                                       \
+    return 0;
+    if (!getenv("LCI_HYENA_PRE_V1")) {
+      switch (K) {
+        LCI_PRE_FWD(1) LCI_PRE_FWD(2) LCI_PRE_FWD(3) LCI_PRE_FWD(4) LCI_PRE_FWD(5) LCI_PRE_FWD(6) LCI_PRE_FWD(7)
+        LCI_PRE_FWD(8)
+        default: break;
+      }
+    }
+#undef LCI_PRE_FWD
+  }
   dim3 grid((L + 63) / 64, (a.D + 63) / 64, BB);
   if (dtype == 1) hipLaunchKernelGGL(hyena_pre_fwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, a);
   else hipLaunchKernelGGL(hyena_pre_fwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, a);
@@ -768,6 +974,25 @@ extern "C" int lci_hyena_pre_bwd(int dtype, const void* z, const float* w, const
   GateArgs a{};
   a.z = z; a.w = w; a.bias = bias; a.dvg = dvg; a.gx2 = gx2; a.dz = dz; a.dw = dw; a.db = db;
   a.BB = BB; a.L = L; a.H = H; a.hd = hd; a.D = H * hd; a.K = K;
+  if (!getenv("LCI_HYENA_PRE_V1")) {   // one lane per output channel, token tiles strided over ~8 workgroups/CU
+    const int ntiles = (L + HY_TT - 1) / HY_TT, ncy = (a.D + 63) / 64;
+    const int gx = std::max(1, std::min(ntiles, 2048 / std::max(1, ncy * BB)));
+    dim3 grid2(gx, ncy, BB);
+#define LCI_PRE_BWD2(KK)                                                                                        \
+  case KK:                                                                                                    \
+    if (dtype == 1)                                                                                           \
+      hipLaunchKernelGGL((hyena_pre_bwd2_kernel<bf16, KK>), grid2, dim3(256), 0, (hipStream_t)stream, a);     \
+    else                                                                                                      \
+      hipLaunchKernelGGL((hyena_pre_bwd2_kernel<float, KK>), grid2, dim3(256), 0, (hipStream_t)stream, a);    \
+    LCI_LAUNCH_CHECK();                                                                                       \
+    return 0;
+    switch (K) {
+      LCI_PRE_BWD2(1) LCI_PRE_BWD2(2) LCI_PRE_BWD2(3) LCI_PRE_BWD2(4) LCI_PRE_BWD2(5) LCI_PRE_BWD2(6)
+      LCI_PRE_BWD2(7) LCI_PRE_BWD2(8)
+      default: break;
+    }
+#undef LCI_PRE_BWD2
+  }
   dim3 grid((L + 63) / 64, (3 * a.D + 255) / 256, BB);
   {   // register-ring kernel for every supported order (the reference's models use short_filter_order = 5)
     const size_t lds = (size_t)256 * (64 + K) * sizeof(float);

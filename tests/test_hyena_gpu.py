@@ -140,3 +140,37 @@ def test_fftconv_c4_length_subset():
     assert rel_err(uc.grad, du) < 1e-4
     assert rel_err(kc.grad, dk) < 1e-4
     assert rel_err(Dc.grad, dD) < 1e-4
+
+
+@pytest.mark.parametrize("BB,L,H,hd,K,dtype", [(2, 1000, 6, 64, 5, torch.float32), (1, 4099, 2, 32, 3, torch.float32),
+                                              (2, 777, 6, 64, 5, torch.bfloat16), (1, 300, 1, 64, 8, torch.float32),
+                                              (1, 129, 3, 64, 1, torch.float32)])
+def test_hyena_short_conv_gate_vs_torch(BB, L, H, hd, K, dtype):
+    """hyena_pre (register-ring kernels) vs a torch fp64 restatement of hyena.py:317-333 (causal depthwise conv1d,
+    split x1 / x2 / v per head, v * x1): forward and the gradients of z, weight and bias. Ragged token tiles,
+    head dims 32 / 64, filter orders 1-8."""
+    from long_context_biomedical_imaging_amd import kernels
+    torch.manual_seed(L + K)
+    D = H * hd
+    z = torch.randn(BB, L, 3 * D).to(dtype)
+    w = torch.randn(3 * D, 1, K) * 0.5
+    b = torch.randn(3 * D) * 0.1
+    zc, wc, bc = (t.cuda().requires_grad_(True) for t in (z, w, b))
+    vg, x2 = kernels.hyena_pre(zc, wc, bc, H)
+    gv, g2 = torch.randn(BB, D, L), torch.randn(BB, L, D)
+    (vg * gv.cuda()).sum().add_((x2.float() * g2.cuda()).sum()).backward()
+    zr, wr, br = (t.double().requires_grad_(True) for t in (z.float(), w, b))
+    conv = torch.nn.functional.conv1d(zr.transpose(1, 2), wr, br, padding=K - 1, groups=3 * D)[..., :L]
+    conv = conv.view(BB, H, 3, hd, L)
+    x1r, x2r, vr = conv[:, :, 0].reshape(BB, D, L), conv[:, :, 1].reshape(BB, D, L), conv[:, :, 2].reshape(BB, D, L)
+    vgr = vr * x1r
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert rel_err(vg, vgr) < tol
+    assert rel_err(x2.float(), x2r.transpose(1, 2)) < tol
+    ((vgr * gv.double()).sum() + (x2r.transpose(1, 2) * g2.double()).sum()).backward()
+    assert rel_err(zc.grad.float(), zr.grad) < max(tol, 1e-5)
+    # bf16: autograd hands the kernel the x2 cotangent rounded to bf16 (x2 is bf16), so dw / db of the x2
+    # channels carry that rounding (~2^-9 relative)
+    tw = 1e-4 if dtype == torch.float32 else 1e-2
+    assert rel_err(wc.grad, wr.grad) < tw
+    assert rel_err(bc.grad, br.grad) < tw
