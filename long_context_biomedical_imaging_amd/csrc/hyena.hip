@@ -352,6 +352,187 @@ __global__ __launch_bounds__(256) void fft_col_inv_kernel(FftArgs a) {
   }
 }
 
+// --------------------------------------------------------------- column passes, wide column groups (v2)
+// GW = 8192 / n1 adjacent columns per workgroup (32 at n1 = 256, 16 at n1 = 512): every global row segment is
+// GW contiguous f32 (128 B / 64 B) and every spectrum segment GW complex (256 B / 128 B), where the v1 kernels'
+// 8 columns gave 32-B / 64-B segments. The column FFTs run in place in ONE LDS buffer: each radix pass reads all
+// of its butterflies into registers, barriers, then writes (Stockham order), so the buffer is half the v1 ping-pong.
+constexpr int CW_ELEMS = 8192;   // GW * n1 complex per workgroup
+
+template <int R, bool INV>
+__device__ __forceinline__ void stockham_inplace(f32x2* x, int N, int Ns, const f32x2* twl, int ld) {
+  constexpr int PER = CW_ELEMS / R / 256;   // butterflies per thread
+  const int nb = N / R;
+  const int tstep = N / (Ns * R);
+  f32x2 v[PER][R];
+  int pos[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int idx = k * 256 + threadIdx.x;
+    const int sq = idx / nb, j = idx - sq * nb;
+    const int m = j & (Ns - 1);
+    const f32x2* xs = x + sq * ld;
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[k][r] = xs[j + r * nb];
+    if (Ns > 1) {
+#pragma unroll
+      for (int r = 1; r < R; ++r) {
+        f32x2 w = twl[(m * r * tstep) & (N - 1)];
+        if (INV) w.y = -w.y;
+        v[k][r] = cmul(v[k][r], w);
+      }
+    }
+    dft<R, INV>(v[k]);
+    pos[k] = sq * ld + (j - m) * R + m;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < PER; ++k)
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[pos[k] + r * Ns] = v[k][r];
+  __syncthreads();
+}
+
+template <bool INV>
+__device__ __forceinline__ void lds_fft_inplace(f32x2* x, int N, int lN, const f32x2* twl, int ld) {
+  int Ns = 1, left = lN;
+  while (left > 0) {
+    if (left >= 3 && left != 4) { stockham_inplace<8, INV>(x, N, Ns, twl, ld); Ns *= 8; left -= 3; }
+    else if (left >= 2) { stockham_inplace<4, INV>(x, N, Ns, twl, ld); Ns *= 4; left -= 2; }
+    else { stockham_inplace<2, INV>(x, N, Ns, twl, ld); Ns *= 2; left -= 1; }
+  }
+}
+
+// grid (n2 / GW, npairs_total or C); block 256. Same math as fft_col_fwd_kernel.
+template <int GW>
+__global__ __launch_bounds__(256) void fft_colw_fwd_kernel(FftArgs a) {
+  extern __shared__ __attribute__((aligned(16))) f32x2 lds[];
+  const int ld = a.n1 + 1;
+  f32x2* x = lds;
+  f32x2* twl = x + GW * ld;
+  load_twl(twl, a.tw, a.n1, a.n);
+  const int c0 = blockIdx.x * GW;
+  const int pid = blockIdx.y;
+  int r0, r1;
+  if (a.single) { r0 = pid; r1 = -1; }
+  else {
+    const int j = pid / a.P, p = pid % a.P;
+    r0 = pair_row(a, j, p, 0);
+    r1 = pair_row(a, j, p, 1);
+  }
+  const float* s0 = a.src + (long long)r0 * a.L;
+  const float* s1 = r1 >= 0 ? a.src + (long long)r1 * a.L : nullptr;
+  for (int base = 0; base < CW_ELEMS; base += UB * 256) {
+    f32x2 v[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int idx = base + u * 256 + threadIdx.x;
+      const int g = idx % GW, ai = idx / GW;
+      const int m = ai * a.n2 + c0 + g;
+      v[u] = f32x2{0.f, 0.f};
+      if (m < a.L) {
+        v[u].x = s0[m];
+        if (s1) v[u].y = s1[m];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int idx = base + u * 256 + threadIdx.x;
+      x[(idx % GW) * ld + idx / GW] = v[u];
+    }
+  }
+  __syncthreads();
+  lds_fft_inplace<false>(x, a.n1, a.ln1, twl, ld);
+  f32x2* S = (a.single ? a.SK : a.S) + (long long)pid * a.n;
+  for (int base = 0; base < CW_ELEMS; base += UB * 256) {
+    f32x2 w[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int idx = base + u * 256 + threadIdx.x;
+      const int g = idx % GW, k1 = idx / GW;
+      w[u] = a.tw[((long long)(c0 + g) * k1) & (a.n - 1)];
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int idx = base + u * 256 + threadIdx.x;
+      const int g = idx % GW, k1 = idx / GW;
+      S[(long long)k1 * a.n2 + c0 + g] = cmul(x[g * ld + k1], w[u]);
+    }
+  }
+}
+
+// grid (n2 / GW, npairs_total or C); same math as fft_col_inv_kernel.
+template <int GW>
+__global__ __launch_bounds__(256) void fft_colw_inv_kernel(FftArgs a) {
+  extern __shared__ __attribute__((aligned(16))) f32x2 lds[];
+  const int ld = a.n1 + 1;
+  f32x2* x = lds;
+  f32x2* twl = x + GW * ld;
+  load_twl(twl, a.tw, a.n1, a.n);
+  const int c0 = blockIdx.x * GW;
+  const int pid = blockIdx.y;
+  const f32x2* S = (a.single ? a.SK : a.S) + (long long)pid * a.n;
+  for (int base = 0; base < CW_ELEMS; base += UB * 256) {
+    f32x2 v[UB], w[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int idx = base + u * 256 + threadIdx.x;
+      const int g = idx % GW, k1 = idx / GW;
+      w[u] = a.tw[((long long)(c0 + g) * k1) & (a.n - 1)];
+      v[u] = S[(long long)k1 * a.n2 + c0 + g];
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int idx = base + u * 256 + threadIdx.x;
+      x[(idx % GW) * ld + idx / GW] = cmulc(v[u], w[u]);
+    }
+  }
+  __syncthreads();
+  lds_fft_inplace<true>(x, a.n1, a.ln1, twl, ld);
+  // only a < ceil(L / n2) rows of the column carry outputs (m < L); the rest is the discarded wrap half
+  const int na = (a.L - c0 + a.n2 - 1) / a.n2;
+  if (a.single) {
+    for (int idx = threadIdx.x; idx < GW * na; idx += 256) {
+      const int g = idx % GW, ai = idx / GW;
+      const int m = ai * a.n2 + c0 + g;
+      if (m < a.L) a.dk[(long long)pid * a.L + m] = x[g * ld + ai].x;
+    }
+    return;
+  }
+  const int j = pid / a.P, p = pid % a.P;
+  const int r0 = pair_row(a, j, p, 0), r1 = pair_row(a, j, p, 1);
+  const float Dj = a.Dv ? a.Dv[j] : 0.f;
+  const float* s0 = a.src + (long long)r0 * a.L;
+  const float* s1 = r1 >= 0 ? a.src + (long long)r1 * a.L : nullptr;
+  float* d0 = a.dst + (long long)r0 * a.L;
+  float* d1 = r1 >= 0 ? a.dst + (long long)r1 * a.L : nullptr;
+  const int total = GW * na;
+  for (int base = 0; base < total; base += UB * 256) {
+    float u0[UB], u1[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int idx = base + u * 256 + threadIdx.x;
+      const int m = (idx / GW) * a.n2 + c0 + idx % GW;
+      u0[u] = u1[u] = 0.f;
+      if (idx < total && m < a.L) {
+        u0[u] = s0[m];
+        if (s1) u1[u] = s1[m];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int idx = base + u * 256 + threadIdx.x;
+      const int g = idx % GW, ai = idx / GW;
+      const int m = ai * a.n2 + c0 + g;
+      if (idx < total && m < a.L) {
+        const f32x2 v = x[g * ld + ai];
+        d0[m] = fmaf(Dj, u0[u], v.x);
+        if (d1) d1[m] = fmaf(Dj, u1[u], v.y);
+      }
+    }
+  }
+}
+
 // dD[j] += sum_rows sum_t a[row][t] * b[row][t] over rows of filter j (block partial + atomic)
 __global__ __launch_bounds__(256) void row_dot_kernel(const float* x, const float* y, float* out, int L, int C,
                                                       int R) {
@@ -835,6 +1016,20 @@ extern "C" int lci_fft_twiddles(void* tw, int n, void* stream) {
 }
 
 static int launch_col(FftArgs& a, bool inv, int nblk_y, hipStream_t s) {
+  const int gw = CW_ELEMS / a.n1;
+  if ((gw == 16 || gw == 32) && a.n2 % gw == 0 && !getenv("LCI_FFT_COL_V1")) {
+    const size_t sh = ((size_t)gw * (a.n1 + 1) + a.n1) * sizeof(f32x2);
+    dim3 grid(a.n2 / gw, nblk_y);
+#define LCI_COLW(GW)                                                                                       \
+    (void)hipFuncSetAttribute((const void*)(inv ? fft_colw_inv_kernel<GW> : fft_colw_fwd_kernel<GW>),      \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                   \
+    if (inv) hipLaunchKernelGGL(fft_colw_inv_kernel<GW>, grid, dim3(256), sh, s, a);                     \
+    else hipLaunchKernelGGL(fft_colw_fwd_kernel<GW>, grid, dim3(256), sh, s, a);
+    if (gw == 32) { LCI_COLW(32) } else { LCI_COLW(16) }
+#undef LCI_COLW
+    LCI_LAUNCH_CHECK();
+    return 0;
+  }
   const size_t sh = ((size_t)2 * a.G * (a.n1 + 1) + a.n1) * sizeof(f32x2);
   (void)hipFuncSetAttribute((const void*)(inv ? fft_col_inv_kernel : fft_col_fwd_kernel),
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
