@@ -158,6 +158,42 @@ def profiled_traffic(kernel: str):
     return None
 
 
+def _sync(device):
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+
+
+def timed_steps(step, steps, warmup, world, device, rank, label="", on_start=None):
+    """The contract's timing: `warmup` untimed steps, then exactly `steps` timed steps bracketed by a barrier and a
+    device synchronize on both sides; returns (max elapsed seconds over ranks, last step's return value).
+    Device-agnostic (CUDA/RCCL on the GPU box; CPU/gloo in the multi-process rehearsal test)."""
+    for i in range(warmup):
+        tw = time.perf_counter()
+        step()
+        _sync(device)
+        if rank == 0 and label:
+            print(f"[bench] {label} warmup step {i}: {time.perf_counter() - tw:.2f} s", file=sys.stderr, flush=True)
+    _sync(device)
+    if world > 1:
+        dist.barrier()
+    _sync(device)
+    if on_start is not None:
+        on_start()
+    t0 = time.perf_counter()
+    out = None
+    for _ in range(steps):
+        out = step()
+    _sync(device)
+    if world > 1:
+        dist.barrier()
+    _sync(device)
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.item(), out
+
+
 def run_workload(workload, batch, steps, warmup, rank, world, device, kernel_timer=True, cfg_extra=()):
     """Build the workload's model, run `warmup` untimed and `steps` timed training steps (barrier + sync on both
     sides, max over ranks). Returns the bench dict on rank 0 (None elsewhere); frees the model."""
@@ -176,34 +212,15 @@ def run_workload(workload, batch, steps, warmup, rank, world, device, kernel_tim
     L = (model.encoder.patch_embedding.n_patches if hasattr(model.encoder, "patch_embedding")
          else cfg.time * cfg.height * cfg.width // 8)
 
-    for i in range(warmup):
-        tw = time.perf_counter()
-        trainer.step(x, y)
-        torch.cuda.synchronize()
-        if rank == 0:
-            print(f"[bench] {workload} warmup step {i}: {time.perf_counter() - tw:.2f} s", file=sys.stderr,
-                  flush=True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    kernels.KernelTimer.reset()
-    kernels.KernelTimer.enabled = kernel_timer
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        loss = trainer.step(x, y)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    def on_timed_start():
+        kernels.KernelTimer.reset()
+        kernels.KernelTimer.enabled = kernel_timer
+
+    elapsed, loss = timed_steps(lambda: trainer.step(x, y), steps, warmup, world, device, rank,
+                                label=workload, on_start=on_timed_start)
     kernels.KernelTimer.enabled = False
-    ksum = kernels.KernelTimer.summary()
+    ksum = kernels.KernelTimer.summary() if device.type == "cuda" else {}
     kernels.KernelTimer.reset()
-    t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = t.item()
     loss_v = float(loss.item())
     del trainer, model, x, y, loss
     torch.cuda.empty_cache()

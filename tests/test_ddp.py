@@ -111,3 +111,52 @@ def test_ddp_two_ranks_gpu_kernels():
         assert p.exitcode == 0
     for a, b in zip(res[0], res[1]):
         assert (a == b).all()
+
+
+def _bench_worker(rank, world, port, q):
+    """One rank of bench.py's timing harness (timed_steps) around a DDP step on CPU/gloo: rank 1 is made slower,
+    so the reported time must be the max over ranks, and the weights must stay identical across ranks."""
+    import time
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import bench
+    from long_context_biomedical_imaging_amd.trainer import TrainStep, init_distributed
+    r, local, w = init_distributed()          # the harness's own rendezvous path (gloo without a GPU)
+    assert (r, w) == (rank, world) and dist.is_initialized()
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.GELU(), torch.nn.Linear(16, 4))
+    ts = TrainStep(model, _cfg(), torch.device("cpu"), ddp=True)
+    g = torch.Generator().manual_seed(100 + rank)
+    x, y = torch.randn(4, 8, generator=g), torch.randn(4, 4, generator=g)
+
+    def step():
+        if rank == 1:
+            time.sleep(0.05)
+        return ts.step(x, y)
+
+    t0 = time.perf_counter()
+    elapsed, loss = bench.timed_steps(step, 4, 1, world, torch.device("cpu"), rank)
+    mine = time.perf_counter() - t0
+    q.put((rank, elapsed, mine, float(loss), [p.detach().numpy().copy() for p in model.parameters()]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_harness_two_ranks_cpu_gloo():
+    """bench.py's N > 1 path rehearsed on CPU (world size 2, gloo): barrier-bracketed timing, max over ranks,
+    DDP gradient all-reduce keeping the replicas identical."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: (e, m, l, w) for r, e, m, l, w in (q.get(timeout=180) for _ in range(2))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    e0, e1 = res[0][0], res[1][0]
+    assert e0 == e1, "every rank reports the same (max) time"
+    assert e0 >= 4 * 0.05, "the slow rank's 4 timed steps bound the reported time"
+    for a, b in zip(res[0][3], res[1][3]):
+        assert (a == b).all()
