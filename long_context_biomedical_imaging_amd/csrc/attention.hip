@@ -155,7 +155,11 @@ __global__ __launch_bounds__(256) void attn_key_norm_kernel(AttnArgs a, float* k
 //    re-base of m (alpha = exp2(-d) on O and l). The result is the same softmax; only the reference point
 //    of the exponent differs.
 #ifndef LCI_SB
+#if defined(LCI_SB_OFF) && LCI_SB_OFF
+#define LCI_SB()
+#else
 #define LCI_SB() __builtin_amdgcn_sched_barrier(0)
+#endif
 #endif
 constexpr int FW_NW = 8;
 constexpr int FSLOT = KT * LD_ROW + KT * LD_TR;   // one ring slot: K tile (rows) + V tile (transposed reads)
@@ -722,6 +726,9 @@ __global__ __launch_bounds__(FW_NW * 64, 1) void attn_bwd_dq2_kernel(AttnArgs a)
   int slA = 0, slB = 1, slC = 2;   // ring slots of tiles j, j+1, j+2
   auto iter = [&](const int j, auto next) __attribute__((always_inline)) {
     constexpr bool NEXT = decltype(next)::value;
+#ifdef LCI_DQ_IGLP
+    __builtin_amdgcn_iglp_opt(LCI_DQ_IGLP);
+#endif
     const u32x4 kw = bload16(rk, voff, (j + 2) * KT * rs2);
     const u32x4 vw = bload16(rv, voff, (j + 2) * KT * rs2);
     bf16x8 a0, a1, c0, c1;
