@@ -194,19 +194,23 @@ def timed_steps(step, steps, warmup, world, device, rank, label="", on_start=Non
     return t.item(), out
 
 
-def run_workload(workload, batch, steps, warmup, rank, world, device, kernel_timer=True, cfg_extra=()):
+def run_workload(workload, batch, steps, warmup, rank, world, device, kernel_timer=True, cfg_extra=(),
+                 ckpt_blocks=None):
     """Build the workload's model, run `warmup` untimed and `steps` timed training steps (barrier + sync on both
     sides, max over ranks). Returns the bench dict on rank 0 (None elsewhere); frees the model."""
     if workload in ("swin_p2_128", "vit_mamba_p2_256"):
         # any 3-D conv left on MIOpen (none in these heads today): heuristic solver instead of a minutes-long find
         os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
     cfg = lconfig.parse_config(WORKLOADS[workload] + ["--batch_size", str(batch)] + list(cfg_extra))
+    if device.type == "cuda":
+        torch.cuda.empty_cache()
+        torch.cuda.reset_peak_memory_stats(device)
     torch.manual_seed(0)
     model = EncoderDecoderModel(cfg, cfg.encoder_name, cfg.decoder_name, cfg.no_in_channel,
                                 cfg.no_out_channel).to(device)
-    ckpt = workload == "vit_mamba_p2_256"
+    ckpt = ckpt_blocks if ckpt_blocks is not None else (12 if workload == "vit_mamba_p2_256" else 0)
     if ckpt:
-        model.encoder.checkpoint_blocks = True   # ~35 GB of saved activations per block at 2^21 tokens
+        model.encoder.checkpoint_blocks = ckpt   # ~35 GB of saved activations per block at 2^21 tokens
     trainer = TrainStep(model, cfg, device, ddp=world > 1)
     x, y = synthetic_batch(cfg, batch, device, seed=1234 + rank)
     L = (model.encoder.patch_embedding.n_patches if hasattr(model.encoder, "patch_embedding")
@@ -222,6 +226,8 @@ def run_workload(workload, batch, steps, warmup, rank, world, device, kernel_tim
     ksum = kernels.KernelTimer.summary() if device.type == "cuda" else {}
     kernels.KernelTimer.reset()
     loss_v = float(loss.item())
+    model_blocks = list(model.encoder.blocks) if hasattr(model.encoder, "blocks") else []
+    peak_mem = torch.cuda.max_memory_allocated(device) if device.type == "cuda" else 0
     del trainer, model, x, y, loss
     torch.cuda.empty_cache()
     if rank != 0:
@@ -259,7 +265,9 @@ def run_workload(workload, batch, steps, warmup, rank, world, device, kernel_tim
         "config": {"workload": WORKLOAD_NAMES[workload][1],
                    "global_batch": world * batch, "seq_len": L, "parallelism": f"ddp{world}",
                    "per_gpu_batch": batch, "optimizer": cfg.optim_type, "loss": cfg.loss_func,
-                   "activation_checkpointing": "per encoder block" if ckpt else "none"},
+                   "activation_checkpointing": f"first {ckpt} of {len(model_blocks)} encoder blocks" if ckpt
+                   else "none"},
+        "peak_memory_gb": round(peak_mem / 2 ** 30, 1),
         "roofline": roof,
         "kernels": kern,
         "loss": round(loss_v, 5),
@@ -277,6 +285,8 @@ def main():
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the Swin 128^3 line that the default (ViT 512^2) run also reports")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--ckpt-blocks", type=int, default=None,
+                    help="checkpoint the first K encoder blocks (default: all 12 for vit_mamba_p2_256, else none)")
     ap.add_argument("--no-kernel-timer", action="store_true",
                     help="no per-launch HIP events (rocprofv3 PMC passes); the line then carries no roofline")
     args = ap.parse_args()
@@ -288,7 +298,7 @@ def main():
     torch.cuda.set_device(device)
     tuned = use_tuned_gemms()
     res = run_workload(args.workload, args.batch, args.steps, args.warmup, rank, world, device,
-                       kernel_timer=not args.no_kernel_timer)
+                       kernel_timer=not args.no_kernel_timer, ckpt_blocks=args.ckpt_blocks)
     if args.workload == "vit_p2_512" and not args.no_secondary:
         # north_star also asks for tokens/s on 128^3 patch-2 volumes (BASELINE configs[2], Swin + SwinUNETR):
         # same DDP harness, 1 volume per GPU, same steps (at most 10), reported under "secondary"

@@ -165,6 +165,8 @@ class ViT_with_alt_ops(nn.Module):
         self.norm = nn.LayerNorm(hidden_size)
         # Not a reference option: per-block activation checkpointing (recompute each block's forward in the
         # backward) for token counts whose saved activations exceed one GPU (256^3 p2: ~35 GB per block).
+        # True = every block; an int k = the first k blocks only (the rest keep their activations: less recompute
+        # where the memory allows it).
         self.checkpoint_blocks = False
         if self.classification and not use_hyena and not use_mamba:
             self.cls_token = nn.Parameter(torch.zeros(1, 1, hidden_size))
@@ -177,8 +179,9 @@ class ViT_with_alt_ops(nn.Module):
         if hasattr(self, "cls_token"):
             cls_token = self.cls_token.expand(x.shape[0], -1, -1)
             x = torch.cat((cls_token, x), dim=1)
-        for blk in self.blocks:
-            if self.checkpoint_blocks and self.training and torch.is_grad_enabled():
+        nck = len(self.blocks) if self.checkpoint_blocks is True else int(self.checkpoint_blocks or 0)
+        for i, blk in enumerate(self.blocks):
+            if i < nck and self.training and torch.is_grad_enabled():
                 x = torch.utils.checkpoint.checkpoint(blk, x, use_reentrant=False)
             else:
                 x = blk(x)
