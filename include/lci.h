@@ -33,8 +33,9 @@
 extern "C" {
 #endif
 
-/* Bumped whenever an entry point's argument list changes (3: lci_layernorm_bwd gained dres). */
-#define LCI_ABI_VERSION 3
+/* Bumped whenever an entry point's argument list or buffer contract changes (3: lci_layernorm_bwd gained dres;
+ * 4: lci_conv3_wgrad writes one partial per voxel split instead of one per split and wave). */
+#define LCI_ABI_VERSION 4
 const char* lci_last_error(void);
 int lci_abi_version(void);
 /* sha256 prefix of the sources the library was built from (build_lib.source_hash); the Python binding refuses a
@@ -97,7 +98,7 @@ int lci_window_index_map(const int* geo, int* src_row, int* region, int* rid, in
  * w'[c, t, n] = w[n, c, KD*9-1-t]. */
 int lci_conv3_fwd(const void* x, const void* w, void* y, int B, int D, int H, int W, int Cin, int Cout, int KD,
                   void* stream);
-/* Weight gradient: part (lci_conv3_wgrad_splits(B*D*H*W, Cin, Cout, KD) * 4, KD*9, Cout, Cin) f32 <- per-(voxel split, wave)
+/* Weight gradient: part (lci_conv3_wgrad_splits(B*D*H*W, Cin, Cout, KD), KD*9, Cout, Cin) f32 <- per-voxel-split
  * partial sums of dy[p, n] * x[p + off(tap), c]; dW[n, c, tap] = sum over the first axis (caller). x (.., Cin),
  * dy (.., Cout) bf16 channels-last; Cin, Cout multiples of 32. Deterministic (no atomics). */
 long long lci_conv3_wgrad_splits(long long V, int Cin, int Cout, int KD);

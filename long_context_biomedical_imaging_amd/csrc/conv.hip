@@ -41,7 +41,26 @@ struct ConvArgs {
   bf16* y;          // (B, D, H, W, Cout)
   long long V;      // B * D * H * W
   int D, H, W, Cin, Cout, KD;
+  int nvb, ntile, order;   // LDS kernel: voxel blocks, Cout tiles, work order of the 1-D grid (conv_work)
 };
+
+// (voxel block, Cout tile) of workgroup b for the LDS-staged forward. order 0: voxel block fastest over the plain
+// launch order (consecutive voxel blocks land on different XCDs); order 1: every XCD (workgroup b -> XCD b % 8,
+// observed round-robin, not relied on for correctness) takes a contiguous range of voxel blocks with the Cout
+// tiles fastest, so the workgroups staging the same x rows (and the +-W row shifts of the dy = +-1 taps) share
+// that XCD's L2; order 2: contiguous voxel-block ranges per XCD, Cout tile slowest.
+__device__ __forceinline__ bool conv_work(const ConvArgs& a, long long& vb, int& nt) {
+  long long w = blockIdx.x;
+  const long long nb = (long long)a.nvb * a.ntile;
+  if (a.order != 0) {
+    const long long per = (nb + 7) / 8;
+    w = (long long)(blockIdx.x % 8) * per + blockIdx.x / 8;
+  }
+  if (w >= nb) return false;
+  if (a.order == 1) { nt = (int)(w % a.ntile); vb = w / a.ntile; }
+  else { vb = w % a.nvb; nt = (int)(w / a.nvb); }
+  return true;
+}
 
 __device__ __forceinline__ bf16x8 zero8() {
   bf16x8 z;
@@ -146,8 +165,11 @@ __global__ __launch_bounds__(256) void conv3_fwd_lds_kernel(ConvArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 sW[3 * 32 * NT * CLD];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
   const int r = lane & 31, h = lane >> 5;
-  const long long vg0 = (long long)blockIdx.x * WV;
-  const int n0 = blockIdx.y * 32 * NT;
+  long long vblk;
+  int ntl;
+  if (!conv_work(a, vblk, ntl)) return;   // 1-D grid padding (uniform per workgroup, before any barrier)
+  const long long vg0 = vblk * WV;
+  const int n0 = ntl * 32 * NT;
   const int T = a.KD * 9;
   const int HW = a.H * a.W;
   int zc[MV], yc[MV], xc[MV];
@@ -309,150 +331,105 @@ __global__ __launch_bounds__(256) void conv3_fwd_generic_kernel(ConvArgs a) {
   }
 }
 
-// Weight gradient, split over voxels: part[s, w, tap, n, c] = sum over this workgroup's voxels p (rows of
-// wave w) of dy[p, n] * x[p + off(tap), c]. Both operands have the voxel as the reduction index, which is the
-// slow axis of a channels-last tensor, so 128-voxel tiles of dy and of the tap-shifted x are staged row-major
-// in LDS (192-B rows: conflict-free for the transposed reads) and read back as MFMA fragments with
-// ds_read_b64_tr_b16. Grid x = tap (fastest: the 27 workgroups of one voxel range share it in L2),
-// y = voxel split, z = (n tile, c tile). Plain stores of per-wave partials (no atomics, deterministic); the
-// caller sums them.
+// Weight gradient: dW[n, c, tap] = sum_p dy[p, n] x[p + off(tap), c]. Both operands have the voxel as the reduction
+// index, which is the slow axis of a channels-last tensor, so 128-voxel tiles of dy and of the shifted x are staged
+// row-major in LDS and read back as MFMA fragments with ds_read_b64_tr_b16 (64 / 160 / 192-B rows keep the four
+// rows of a transposed read in disjoint bank windows). One workgroup computes the three dx taps of a (dz, dy) tap
+// group for a 32*MT x 32 (n, c) tile over one voxel split. Voxels are enumerated in a "gapped" row space, one zero
+// row after every W-voxel line, so that the x neighbour of dy row g for tap dx is simply staged row g + dx: it
+// falls on a zero gap row exactly when x + dx leaves [0, W), with no per-element masks; the dy fragments feed all
+// three taps.
+//  * Row indexing is incremental: every thread stages the same rows of each 128-row step, so their (line, x, y, z)
+//    advance by one add and one carry per step (the previous version spent about half of its VALU issue on a
+//    32-bit division and a carry loop per element and step).
+//  * The 4 waves' partial sums are reduced in LDS at the end: one (T, Cout, Cin) partial per voxel split (the
+//    caller sums the splits), with splits of up to 2^17 rows -- ~16x less partial-sum traffic than one partial per
+//    wave of 2^15-row splits.
+// Double-buffered: the next step's rows are loaded into registers during this step's MFMAs. Deterministic.
 constexpr int WG_ROWS = 128;
-// LDS row stride (elements) of a 32*M-channel tile: 64 / 160 / 192-B rows keep the four rows of a transposed
-// read in disjoint bank windows (a 128-B stride would pair them up)
 __host__ __device__ constexpr int wg_ld(int M) { return M == 1 ? 32 : (M == 2 ? 80 : 96); }
 
 struct WgradArgs {
   const bf16* x;    // (B, D, H, W, Cin)
   const bf16* dy;   // (B, D, H, W, Cout)
-  float* part;      // (nsplit * 4, T, Cout, Cin)
+  float* part;      // (nsplit, T, Cout, Cin)
   long long V, Lv;
   int D, H, W, Cin, Cout, KD;
+  int ns, nb, order;   // work decode of the 1-D grid (see wgrad_work)
 };
 
-template <int MT, int NT>
-__global__ __launch_bounds__(256) void conv3_wgrad_kernel(WgradArgs a) {
-  // two LDS buffers: tile j+1 is loaded into registers during tile j's MFMAs and stored to the other buffer
-  constexpr int LDY = wg_ld(MT), LDX = wg_ld(NT);
-  __shared__ __attribute__((aligned(16))) bf16 sdy[2][WG_ROWS * LDY];
-  __shared__ __attribute__((aligned(16))) bf16 sx[2][WG_ROWS * LDX];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
-  const int tap = blockIdx.x, split = blockIdx.y;
-  const int nct = a.Cin / (32 * NT);
-  const int n0 = (blockIdx.z / nct) * 32 * MT, c0 = (blockIdx.z % nct) * 32 * NT;
-  const int T = a.KD * 9;
-  const int dz = (a.KD == 3 ? tap / 9 : 1) - 1, dyy = (tap / 3) % 3 - 1, dx = tap % 3 - 1;
-  const int HW = a.H * a.W;
-  const long long DHW = (long long)a.D * HW;
-  const long long off = (long long)dz * HW + dyy * a.W + dx;
-  const long long vs = (long long)split * a.Lv, ve = min(a.V, vs + a.Lv);
-
-  f32x16 acc[MT][NT];
-#pragma unroll
-  for (int m = 0; m < MT; ++m)
-#pragma unroll
-    for (int n = 0; n < NT; ++n)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[m][n][i] = 0.f;
-
-  u32x4 rdy[2 * MT], rx[2 * NT];
-  auto load = [&](long long v0) {
-#pragma unroll
-    for (int i = 0; i < 2 * MT; ++i) {   // dy tile: 128 rows x 4*MT 16-B chunks
-      const int c = tid + 256 * i, row = c / (4 * MT), ch = c % (4 * MT);
-      const long long v = v0 + row;
-      rdy[i] = u32x4{0u, 0u, 0u, 0u};
-      if (v < ve) rdy[i] = *(const u32x4*)(a.dy + v * a.Cout + n0 + 8 * ch);
-    }
-#pragma unroll
-    for (int i = 0; i < 2 * NT; ++i) {   // shifted x tile: row p holds x[p + off] (zero outside the volume)
-      const int c = tid + 256 * i, row = c / (4 * NT), ch = c % (4 * NT);
-      const long long v = v0 + row;
-      rx[i] = u32x4{0u, 0u, 0u, 0u};
-      if (v < ve) {
-        int rem = (int)(v % DHW);
-        const int z = rem / HW;
-        rem -= z * HW;
-        const int y = rem / a.W, xx = rem - y * a.W;
-        if ((unsigned)(z + dz) < (unsigned)a.D && (unsigned)(y + dyy) < (unsigned)a.H &&
-            (unsigned)(xx + dx) < (unsigned)a.W)
-          rx[i] = *(const u32x4*)(a.x + (v + off) * a.Cin + c0 + 8 * ch);
-      }
-    }
-  };
-  auto store = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < 2 * MT; ++i) {
-      const int c = tid + 256 * i, row = c / (4 * MT), ch = c % (4 * MT);
-      *(u32x4*)(&sdy[buf][row * LDY + 8 * ch]) = rdy[i];
-    }
-#pragma unroll
-    for (int i = 0; i < 2 * NT; ++i) {
-      const int c = tid + 256 * i, row = c / (4 * NT), ch = c % (4 * NT);
-      *(u32x4*)(&sx[buf][row * LDX + 8 * ch]) = rx[i];
-    }
-  };
-
-  load(vs);
-  store(0);
-  __syncthreads();
-  int buf = 0;
-  for (long long v0 = vs; v0 < ve; v0 += WG_ROWS) {
-    const bool more = v0 + WG_ROWS < ve;
-    if (more) load(v0 + WG_ROWS);
-    const bf16* tdy = sdy[buf];
-    const bf16* tx = sx[buf];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 fa[MT], fb[NT];
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-        fa[m] = s ? frag_tr<1>(tdy, LDY, 32 * wave, 32 * m, lane) : frag_tr<0>(tdy, LDY, 32 * wave, 32 * m, lane);
-#pragma unroll
-      for (int n = 0; n < NT; ++n)
-        fb[n] = s ? frag_tr<1>(tx, LDX, 32 * wave, 32 * n, lane) : frag_tr<0>(tx, LDX, 32 * wave, 32 * n, lane);
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int n = 0; n < NT; ++n) acc[m][n] = mfma32(fa[m], fb[n], acc[m][n]);
-    }
-    if (more) store(buf ^ 1);
-    __syncthreads();
-    buf ^= 1;
+// Work item of workgroup b. The dispatcher places workgroup b on XCD b % 8 (observed round-robin; nothing here
+// depends on it for correctness), and each XCD has its own 4 MB L2, so `order` 1/2 give every XCD a contiguous
+// range of work items: the workgroups resident on one XCD at a time then share rows -- order 1: same (split,
+// n tile), all tap groups / c tiles (the dy rows are common); order 2: same (split, tap group, c tile), all n
+// tiles (the shifted x rows are common). order 0: tap group fastest over the plain launch order.
+struct WgradWork { int grp, split, n0, c0; bool valid; };
+__device__ __forceinline__ WgradWork wgrad_work(const WgradArgs& a, int MT) {
+  const int b = blockIdx.x;
+  const int G = a.KD * 3, NT = a.Cout / (32 * MT), NC = a.Cin / 32;
+  long long w = b;
+  if (a.order != 0) {
+    const long long per = ((long long)a.nb + 7) / 8;
+    w = (long long)(b % 8) * per + b / 8;
   }
-  // acc[m][n] reg i: n-index n0 + 32m + (i&3) + 8(i>>2) + 4h, c-index c0 + 32n + (lane&31)
-  const int h = lane >> 5;
-  float* out = a.part + ((long long)(split * 4 + wave) * T + tap) * a.Cout * a.Cin;
-#pragma unroll
-  for (int m = 0; m < MT; ++m)
-#pragma unroll
-    for (int n = 0; n < NT; ++n)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int row = n0 + 32 * m + (i & 3) + 8 * (i >> 2) + 4 * h;
-        out[(long long)row * a.Cin + c0 + 32 * n + (lane & 31)] = acc[m][n][i];
-      }
+  WgradWork r{};
+  r.valid = w < a.nb;
+  if (!r.valid) return r;
+  int g, sp, nt, ct;
+  if (a.order == 0) {
+    g = (int)(w % G); long long q = w / G; sp = (int)(q % a.ns); q /= a.ns; nt = (int)(q / NC); ct = (int)(q % NC);
+  } else if (a.order == 1) {
+    ct = (int)(w % NC); long long q = w / NC; g = (int)(q % G); q /= G; nt = (int)(q % NT); sp = (int)(q / NT);
+  } else {
+    nt = (int)(w % NT); long long q = w / NT; ct = (int)(q % NC); q /= NC; g = (int)(q % G); sp = (int)(q / G);
+  }
+  r.grp = g; r.split = sp; r.n0 = nt * 32 * MT; r.c0 = ct * 32;
+  return r;
 }
 
-// Three-tap weight gradient: one workgroup computes the three dx taps of a (dz, dy) tap group for a 32*MT x 32
-// (n, c) tile. Voxels are enumerated in a "gapped" row space, one zero row after every W-voxel line, so that the
-// x neighbour of dy row g for tap dx is simply staged row g + dx: it falls on a zero gap row exactly when x + dx
-// leaves [0, W). The dy tile is staged once per step and its fragments feed all three taps; the x tile is 130
-// rows (1-row halo each side). Staging per tap drops 3x versus conv3_wgrad_kernel.
+// gapped row G -> line L = floor(G / (W + 1)), position X in the line, and (y, z) of the line
+struct GRow {
+  int L, X, y, z;
+  __device__ __forceinline__ void init(long long G, int W1, int H, int D) {
+    long long l = G >= 0 ? G / W1 : -((-G + W1 - 1) / W1);
+    L = (int)l;
+    X = (int)(G - l * W1);
+    long long yy = l % H;
+    if (yy < 0) yy += H;
+    y = (int)yy;
+    long long zq = l >= 0 ? l / H : -((-l + H - 1) / H);
+    long long zz = zq % D;
+    if (zz < 0) zz += D;
+    z = (int)zz;
+  }
+  // G += 128: q128 = 128 / W1, r128 = 128 % W1
+  __device__ __forceinline__ void advance(int q128, int r128, int W1, int H, int D) {
+    X += r128;
+    int dl = q128;
+    if (X >= W1) { X -= W1; ++dl; }
+    L += dl;
+    y += dl;
+    while (y >= H) { y -= H; if (++z == D) z = 0; }
+  }
+};
+
 template <int MT>
-__global__ __launch_bounds__(256) void conv3_wgrad3_kernel(WgradArgs a) {
+__global__ __launch_bounds__(256) void conv3_wgrad4_kernel(WgradArgs a) {
   constexpr int LDY = wg_ld(MT), LDX = wg_ld(1), XR = WG_ROWS + 2;
+  constexpr int NDY = 2 * MT, NXS = 3;
   __shared__ __attribute__((aligned(16))) bf16 sdy[2][WG_ROWS * LDY];
   __shared__ __attribute__((aligned(16))) bf16 sx[2][(XR + 6) * LDX];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
-  const int grp = blockIdx.x, split = blockIdx.y;
-  const int nct = a.Cin / 32;
-  const int n0 = (blockIdx.z / nct) * 32 * MT, c0 = (blockIdx.z % nct) * 32;
+  const WgradWork wk = wgrad_work(a, MT);
+  if (!wk.valid) return;   // padding of the 1-D grid to a multiple of 8 (uniform per workgroup, before any barrier)
+  const int grp = wk.grp, split = wk.split, n0 = wk.n0, c0 = wk.c0;
   const int T = a.KD * 9;
   const int dz = (a.KD == 3 ? grp / 3 : 1) - 1, dyy = grp % 3 - 1;
   const int HW = a.H * a.W, W1 = a.W + 1;
   const long long lines = a.V / a.W, R = lines * W1;
   const long long shift = (long long)dz * HW + (long long)dyy * a.W;
   const long long gs = (long long)split * a.Lv, ge = min(R, gs + a.Lv);
+  const int q128 = WG_ROWS / W1, r128 = WG_ROWS % W1;
 
   f32x16 acc[3][MT];
 #pragma unroll
@@ -462,48 +439,48 @@ __global__ __launch_bounds__(256) void conv3_wgrad3_kernel(WgradArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[d][m][i] = 0.f;
 
-  u32x4 rdy[2 * MT], rx[3];
-  // Row -> (line, x) without per-element 64-bit division: one (uniform) division per step for the tile's first
-  // gapped row, then a 32-bit quotient by W + 1 and a carry of (y, z) per element.
+  // this thread's staging slots: fixed rows of every step
+  int rdy[NDY], cdy[NDY], rxs[NXS], cxs[NXS];
+  GRow gdy[NDY], gx[NXS];
+#pragma unroll
+  for (int i = 0; i < NDY; ++i) {
+    const int c = tid + 256 * i;
+    rdy[i] = c / (4 * MT); cdy[i] = c % (4 * MT);
+    gdy[i].init(gs + rdy[i], W1, a.H, a.D);
+  }
+#pragma unroll
+  for (int i = 0; i < NXS; ++i) {
+    const int c = tid + 256 * i;
+    rxs[i] = c >> 2; cxs[i] = c & 3;
+    gx[i].init(gs - 1 + rxs[i], W1, a.H, a.D);
+  }
+  u32x4 vdy[NDY], vx[NXS];
   auto load = [&](long long g0) {
-    const long long gb = g0 - 1;                        // x tile row 0
-    long long lb = (gb >= 0 ? gb : gb - W1 + 1) / W1;   // floor division (gb may be -1)
-    const int xb = (int)(gb - lb * W1);
-    const int yb = (int)(((lb % a.H) + a.H) % a.H);
-    const int zb = (int)((((lb >= 0 ? lb : lb - a.H + 1) / a.H) % a.D + a.D) % a.D);
 #pragma unroll
-    for (int i = 0; i < 2 * MT; ++i) {   // dy rows g0 .. g0 + 127 (zero on gaps / past the split)
-      const int c = tid + 256 * i, row = c / (4 * MT), ch = c % (4 * MT);
-      rdy[i] = u32x4{0u, 0u, 0u, 0u};
-      if (g0 + row < ge) {
-        const int t = xb + 1 + row, q = t / W1, xx = t - q * W1;
-        if (xx < a.W) rdy[i] = *(const u32x4*)(a.dy + ((lb + q) * a.W + xx) * a.Cout + n0 + 8 * ch);
-      }
+    for (int i = 0; i < NDY; ++i) {
+      vdy[i] = u32x4{0u, 0u, 0u, 0u};
+      if (g0 + rdy[i] < ge && gdy[i].X < a.W)
+        vdy[i] = *(const u32x4*)(a.dy + ((long long)gdy[i].L * a.W + gdy[i].X) * a.Cout + n0 + 8 * cdy[i]);
     }
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {        // x rows g0 - 1 .. g0 + 128, shifted by (dz, dy); zero on gaps / outside
-      const int c = tid + 256 * i, row = c >> 2, ch = c & 3;
-      rx[i] = u32x4{0u, 0u, 0u, 0u};
-      if (row < XR && gb + row >= 0 && gb + row < R) {
-        const int t = xb + row, q = t / W1, xx = t - q * W1;
-        int yl = yb + q, zl = zb;
-        while (yl >= a.H) { yl -= a.H; if (++zl == a.D) zl = 0; }
-        if (xx < a.W && (unsigned)(zl + dz) < (unsigned)a.D && (unsigned)(yl + dyy) < (unsigned)a.H)
-          rx[i] = *(const u32x4*)(a.x + ((lb + q) * a.W + xx + shift) * a.Cin + c0 + 8 * ch);
-      }
+    for (int i = 0; i < NXS; ++i) {
+      vx[i] = u32x4{0u, 0u, 0u, 0u};
+      const long long G = g0 - 1 + rxs[i];
+      if (rxs[i] < XR && G >= 0 && G < R && gx[i].X < a.W && (unsigned)(gx[i].z + dz) < (unsigned)a.D &&
+          (unsigned)(gx[i].y + dyy) < (unsigned)a.H)
+        vx[i] = *(const u32x4*)(a.x + ((long long)gx[i].L * a.W + gx[i].X + shift) * a.Cin + c0 + 8 * cxs[i]);
     }
+#pragma unroll
+    for (int i = 0; i < NDY; ++i) gdy[i].advance(q128, r128, W1, a.H, a.D);
+#pragma unroll
+    for (int i = 0; i < NXS; ++i) gx[i].advance(q128, r128, W1, a.H, a.D);
   };
   auto store = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 2 * MT; ++i) {
-      const int c = tid + 256 * i, row = c / (4 * MT), ch = c % (4 * MT);
-      *(u32x4*)(&sdy[buf][row * LDY + 8 * ch]) = rdy[i];
-    }
+    for (int i = 0; i < NDY; ++i) *(u32x4*)(&sdy[buf][rdy[i] * LDY + 8 * cdy[i]]) = vdy[i];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const int c = tid + 256 * i, row = c >> 2, ch = c & 3;
-      if (row < XR) *(u32x4*)(&sx[buf][row * LDX + 8 * ch]) = rx[i];
-    }
+    for (int i = 0; i < NXS; ++i)
+      if (rxs[i] < XR) *(u32x4*)(&sx[buf][rxs[i] * LDX + 8 * cxs[i]]) = vx[i];
   };
 
   load(gs);
@@ -533,29 +510,29 @@ __global__ __launch_bounds__(256) void conv3_wgrad3_kernel(WgradArgs a) {
     __syncthreads();
     buf ^= 1;
   }
+  // reduce the 4 waves' partials through LDS (the staging buffers are free now), one tap at a time
+  float* red = (float*)&sdy[0][0];   // [wave][m][i][lane]: 4 * 16 MT * 64 floats <= sizeof(sdy)
   const int h = lane >> 5;
+  (void)h;
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
-    float* out = a.part + ((long long)(split * 4 + wave) * T + grp * 3 + d) * a.Cout * a.Cin;
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int row = n0 + 32 * m + (i & 3) + 8 * (i >> 2) + 4 * h;
-        out[(long long)row * a.Cin + c0 + (lane & 31)] = acc[d][m][i];
-      }
+      for (int i = 0; i < 16; ++i) red[((wave * MT + m) * 16 + i) * 64 + lane] = acc[d][m][i];
+    __syncthreads();
+    float* out = a.part + ((long long)split * T + grp * 3 + d) * a.Cout * a.Cin;
+    for (int idx = tid; idx < MT * 16 * 64; idx += 256) {
+      const int l = idx & 63, i = (idx >> 6) & 15, m = idx >> 10;
+      const float v = (red[((0 * MT + m) * 16 + i) * 64 + l] + red[((1 * MT + m) * 16 + i) * 64 + l]) +
+                      (red[((2 * MT + m) * 16 + i) * 64 + l] + red[((3 * MT + m) * 16 + i) * 64 + l]);
+      const int row = n0 + 32 * m + (i & 3) + 8 * (i >> 2) + 4 * (l >> 5);
+      out[(long long)row * a.Cin + c0 + (l & 31)] = v;
+    }
+    __syncthreads();
   }
 }
 
-template <int MT, int NT>
-static int launch_wgrad(const WgradArgs& a, int nsplit, hipStream_t st) {
-  dim3 grid(a.KD * 9, nsplit, (a.Cout / (32 * MT)) * (a.Cin / (32 * NT)));
-  hipLaunchKernelGGL((conv3_wgrad_kernel<MT, NT>), grid, dim3(256), 0, st, a);
-  LCI_LAUNCH_CHECK();
-  return 0;
-}
-
-static int tile3(int c) { return (c / 32) % 3 == 0 ? 3 : ((c / 32) % 2 == 0 ? 2 : 1); }
 
 static bool lci_conv_lds() {   // LCI_CONV_LDS=0: the direct-load kernel (A/B)
   static const bool on = !getenv("LCI_CONV_LDS") || atoi(getenv("LCI_CONV_LDS")) != 0;
@@ -567,8 +544,16 @@ static int launch(const ConvArgs& a, hipStream_t st) {
   constexpr int MV = NT <= 2 ? 4 : LCI_CONV_MV_WIDE;   // narrow outputs: more voxels per wave
   if (a.Cin % 32 == 0 && lci_conv_lds()) {
     constexpr int ML = NT == 4 ? 2 : 4;
-    dim3 grid((unsigned)((a.V + 128 * ML - 1) / (128 * ML)), a.Cout / (32 * NT));
-    hipLaunchKernelGGL((conv3_fwd_lds_kernel<NT, ML>), grid, dim3(256), 0, st, a);
+    // measured (tools/conv_bench.py, C3/C5 shapes): order 1 gains up to 12 % from Cout >= 96 (512->256 at 256^3:
+    // 164 -> 146 ms) and loses up to 15 % on the 1-2 tile Cout = 32 / 64 convs, which keep order 0
+    static const int order_env = getenv("LCI_CONV_ORDER") ? atoi(getenv("LCI_CONV_ORDER")) : -1;
+    ConvArgs b = a;
+    b.nvb = (int)((a.V + 128 * ML - 1) / (128 * ML));
+    b.ntile = a.Cout / (32 * NT);
+    b.order = order_env >= 0 ? order_env : (a.Cout >= 96 ? 1 : 0);
+    const long long nb = (long long)b.nvb * b.ntile;
+    dim3 grid((unsigned)(b.order ? (nb + 7) / 8 * 8 : nb));
+    hipLaunchKernelGGL((conv3_fwd_lds_kernel<NT, ML>), grid, dim3(256), 0, st, b);
   } else if (a.Cin % 16 == 0) {
     dim3 grid((unsigned)((a.V + 128 * MV - 1) / (128 * MV)), a.Cout / (32 * NT));
     hipLaunchKernelGGL((conv3_fwd_kernel<NT, MV>), grid, dim3(256), 0, st, a);
@@ -604,11 +589,11 @@ extern "C" int lci_conv3_fwd(const void* x, const void* w, void* y, int B, int D
   return launch<1>(a, st);
 }
 
-// Voxel splits: up to 32768 voxels per workgroup, fewer (>= 1024) when that leaves under ~2048 workgroups
+// Voxel (gapped-row) splits: up to 2^17 rows per workgroup, fewer (>= 1024) when that leaves under ~2048 workgroups
 // (small 2-D volumes, few channel tiles), so the grid still fills the 256 CUs.
 extern "C" long long lci_conv3_wgrad_splits(long long V, int Cin, int Cout, int KD) {
-  const long long tiles = (long long)KD * 9 * (Cout / (32 * tile3(Cout))) * (Cin / (32 * tile3(Cin)));
-  long long lv = 32768;
+  const long long tiles = (long long)KD * 3 * (Cout / (32 * ((Cout / 32) % 2 == 0 ? 2 : 1))) * (Cin / 32);
+  long long lv = 1 << 17;
   while (lv > 1024 && ((V + lv - 1) / lv) * tiles < 2048) lv >>= 1;
   return (V + lv - 1) / lv;
 }
@@ -625,27 +610,27 @@ extern "C" int lci_conv3_wgrad(const void* x, const void* dy, float* part, int B
   a.x = (const bf16*)x; a.dy = (const bf16*)dy; a.part = part;
   a.V = (long long)B * D * H * W;
   a.D = D; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.KD = KD;
+  LCI_CHECK(a.V / W < (1LL << 31), "conv3_wgrad: volume too large");
   const long long ns = lci_conv3_wgrad_splits(a.V, Cin, Cout, KD);
-  a.Lv = (a.V + ns - 1) / ns;
   LCI_CHECK(ns < 65536, "conv3_wgrad: volume too large");
+  const long long R = (a.V / W) * (W + 1);
+  a.Lv = (R + ns - 1) / ns;
+  a.Lv = (a.Lv + WG_ROWS - 1) / WG_ROWS * WG_ROWS;   // splits start on a step boundary
   hipStream_t st = (hipStream_t)stream;
-  static const bool wg3 = !getenv("LCI_WGRAD3") || atoi(getenv("LCI_WGRAD3")) != 0;   // A/B switch
-  if (wg3) {
-    const long long R = (a.V / W) * (W + 1);
-    a.Lv = (R + ns - 1) / ns;
-    static const int mt_env = getenv("LCI_WGRAD3_MT") ? atoi(getenv("LCI_WGRAD3_MT")) : 0;   // A/B override
-    const int mt = (mt_env > 0 && (Cout / 32) % mt_env == 0) ? mt_env : tile3(Cout);
-    dim3 grid(KD * 3, (unsigned)ns, (Cout / (32 * mt)) * (Cin / 32));
-    if (mt == 3) hipLaunchKernelGGL(conv3_wgrad3_kernel<3>, grid, dim3(256), 0, st, a);
-    else if (mt == 2) hipLaunchKernelGGL(conv3_wgrad3_kernel<2>, grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(conv3_wgrad3_kernel<1>, grid, dim3(256), 0, st, a);
-    LCI_LAUNCH_CHECK();
-    return 0;
-  }
-  const int mt = tile3(Cout), nt = tile3(Cin);
-#define LCI_WG(M, N) if (mt == M && nt == N) return launch_wgrad<M, N>(a, (int)ns, st);
-  LCI_WG(3, 3) LCI_WG(3, 2) LCI_WG(3, 1) LCI_WG(2, 3) LCI_WG(2, 2) LCI_WG(2, 1) LCI_WG(1, 3) LCI_WG(1, 2)
-  LCI_WG(1, 1)
-#undef LCI_WG
-  LCI_CHECK(false, "conv3_wgrad: no tile for Cin %d Cout %d", Cin, Cout);
+  // 32*MT output channels per workgroup: 2 where Cout allows (2 waves per SIMD), else 1. MT = 3 (256 registers, one
+  // wave per SIMD) measured 1.2-1.4x slower than MT = 1 on the Cout = 96 / 192 C3 shapes. LCI_WGRAD3_MT: A/B override
+  static const int mt_env = getenv("LCI_WGRAD3_MT") ? atoi(getenv("LCI_WGRAD3_MT")) : 0;
+  const int mt = (mt_env > 0 && (Cout / 32) % mt_env == 0) ? mt_env : ((Cout / 32) % 2 == 0 ? 2 : 1);
+  a.ns = (int)ns;
+  const long long nb = (long long)KD * 3 * ns * (Cout / (32 * mt)) * (Cin / 32);
+  LCI_CHECK(nb < (1LL << 30), "conv3_wgrad: too many workgroups");
+  a.nb = (int)nb;
+  static const int order_env = getenv("LCI_WGRAD_ORDER") ? atoi(getenv("LCI_WGRAD_ORDER")) : 1;
+  a.order = order_env;
+  dim3 grid((unsigned)(a.order ? (nb + 7) / 8 * 8 : nb));
+  if (mt == 3) hipLaunchKernelGGL(conv3_wgrad4_kernel<3>, grid, dim3(256), 0, st, a);
+  else if (mt == 2) hipLaunchKernelGGL(conv3_wgrad4_kernel<2>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(conv3_wgrad4_kernel<1>, grid, dim3(256), 0, st, a);
+  LCI_LAUNCH_CHECK();
+  return 0;
 }

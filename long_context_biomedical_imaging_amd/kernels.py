@@ -721,7 +721,7 @@ def conv3_wgrad_cl(x_cl: torch.Tensor, dy_cl: torch.Tensor, kd: int) -> torch.Te
     xp = x_cl if cp == Cin else torch.nn.functional.pad(x_cl, (0, cp - Cin))
     lib = _lib.load()
     ns = lib.lci_conv3_wgrad_splits(B * D * H * W, cp, Cout, kd)
-    part = torch.empty(ns * 4, kd * 9, Cout, cp, device=x_cl.device, dtype=torch.float32)
+    part = torch.empty(ns, kd * 9, Cout, cp, device=x_cl.device, dtype=torch.float32)
     KernelTimer.run("conv3_wgrad", 2.0 * B * D * H * W * Cout * Cin * kd * 9, x_cl, lambda: _lib.call(
         "lci_conv3_wgrad", xp.data_ptr(), dy_cl.data_ptr(), part.data_ptr(), B, D, H, W, cp, Cout, kd,
         _lib.stream_of(x_cl)))

@@ -49,6 +49,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--fill", type=float, default=0.0, help="GB of device memory to hold in 1-GB blocks first")
     ap.add_argument("--only", default="")
+    ap.add_argument("--passes", default="fwd,dgrad,wgrad")
     args = ap.parse_args()
     hold = [torch.empty(1 << 30, dtype=torch.uint8, device="cuda") for _ in range(int(args.fill))]
     names = ["c3", "c5", "2d"] if args.set == "all" else args.set.split(",")
@@ -67,6 +68,8 @@ def main():
             for pas, fn in (("fwd", lambda: kernels.conv3_cl(x, w, kd)),
                             ("dgrad", lambda: kernels.conv3_cl(dy, wd, kd)),
                             ("wgrad", lambda: kernels.conv3_wgrad_cl(x, dy, kd))):
+                if pas not in args.passes.split(","):
+                    continue
                 ms = timeit(fn, args.reps if V < 4_000_000 else 2)
                 print(json.dumps({"fill": args.fill, "set": sname, "S": S, "cin": cin, "cout": cout, "pass": pas, "ms": round(ms, 3),
                                   "tflops": round(fl / ms / 1e9, 1)}), flush=True)
