@@ -671,16 +671,16 @@ __global__ __launch_bounds__(256) void conv3_wgrad4_kernel(WgradArgs a) {
 }
 
 
-// Weight gradient v5: the workgroup output tile grows to 64*WN output x 32*WC input channels (x 3 dx taps), split
-// among WN*WC waves (wave (wn, wc) owns n blocks 2wn, 2wn+1 and c block wc over ALL 128 rows of a step), so every
-// staged dy / x byte feeds WC / 2WN x more MFMAs than in v4 (at (WN, WC) = (2, 4): 193 FLOP per staged byte vs 64)
-// and no cross-wave reduction is needed. The staged tiles are kept as separate 32-channel LDS blocks with 64-B
+// Weight gradient v5: the workgroup output tile grows to 32*MB*WN output x 32*WC input channels (x 3 dx taps),
+// split among WN*WC waves (wave (wn, wc) owns n blocks MB wn .. MB wn + MB - 1 and c block wc over ALL 128 rows of
+// a step), so every staged dy / x byte feeds many more MFMAs than in v4 (at (MB, WN, WC) = (2, 2, 4): 193 FLOP
+// per staged byte vs 64) and no cross-wave reduction is needed. The staged tiles are kept as separate 32-channel LDS blocks with 64-B
 // rows (conflict-free transposed reads), double-buffered with the same incremental gapped-row indexing as v4.
-template <int WN, int WC>
+template <int MB, int WN, int WC>
 __global__ __launch_bounds__(64 * WN * WC) void conv3_wgrad5_kernel(WgradArgs a) {
   constexpr int NTH = 64 * WN * WC;
   constexpr int XR = WG_ROWS + 2;
-  constexpr int NB_DY = 2 * WN, NB_X = WC;                      // 32-channel blocks staged per step
+  constexpr int NB_DY = MB * WN, NB_X = WC;                     // 32-channel blocks staged per step
   constexpr int DYBLK = WG_ROWS * 32, XBLK = (XR + 6) * 32;     // elements per LDS block
   constexpr int BUF = NB_DY * DYBLK + NB_X * XBLK;
   constexpr int NDY = (WG_ROWS * NB_DY * 4 + NTH - 1) / NTH;    // 16-B chunks per thread per step
@@ -689,7 +689,7 @@ __global__ __launch_bounds__(64 * WN * WC) void conv3_wgrad5_kernel(WgradArgs a)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
   const int wn = wave / WC, wc = wave % WC;
   // work decode (XCD-contiguous, as wgrad_work order 1, for a 64WN x 32WC tile)
-  const int G = a.KD * 3, NT = a.Cout / (64 * WN), NC = a.Cin / (32 * WC);
+  const int G = a.KD * 3, NT = a.Cout / (32 * MB * WN), NC = a.Cin / (32 * WC);
   long long w = blockIdx.x;
   {
     const long long per = ((long long)a.nb + 7) / 8;
@@ -701,7 +701,7 @@ __global__ __launch_bounds__(64 * WN * WC) void conv3_wgrad5_kernel(WgradArgs a)
   const int grp = (int)(q % G);
   q /= G;
   const int nt = (int)(q % NT), split = (int)(q / NT);
-  const int n0 = nt * 64 * WN, c0 = ct * 32 * WC;
+  const int n0 = nt * 32 * MB * WN, c0 = ct * 32 * WC;
   const int T = a.KD * 9;
   const int dz = (a.KD == 3 ? grp / 3 : 1) - 1, dyy = grp % 3 - 1;
   const int HW = a.H * a.W, W1 = a.W + 1;
@@ -710,11 +710,11 @@ __global__ __launch_bounds__(64 * WN * WC) void conv3_wgrad5_kernel(WgradArgs a)
   const long long gs = (long long)split * a.Lv, ge = min(R, gs + a.Lv);
   const int q128 = WG_ROWS / W1, r128 = WG_ROWS % W1;
 
-  f32x16 acc[3][2];
+  f32x16 acc[3][MB];
 #pragma unroll
   for (int d = 0; d < 3; ++d)
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+    for (int m = 0; m < MB; ++m)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[d][m][i] = 0.f;
 
@@ -773,20 +773,29 @@ __global__ __launch_bounds__(64 * WN * WC) void conv3_wgrad5_kernel(WgradArgs a)
     const bool more = g0 + WG_ROWS < ge;
     if (more) load(g0 + WG_ROWS);
     LCI_WGRAD_SCHED();
-    const bf16* tdy0 = wsm + buf * BUF + (2 * wn) * DYBLK;
-    const bf16* tdy1 = tdy0 + DYBLK;
+    const bf16* tdy0 = wsm + buf * BUF + (MB * wn) * DYBLK;
     const bf16* tx = wsm + buf * BUF + NB_DY * DYBLK + wc * XBLK;
 #pragma unroll
     for (int r0 = 0; r0 < WG_ROWS; r0 += 32) {
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub) {
-        const bf16x8 fa0 = sub ? frag_tr<1>(tdy0, 32, r0, 0, lane) : frag_tr<0>(tdy0, 32, r0, 0, lane);
-        const bf16x8 fa1 = sub ? frag_tr<1>(tdy1, 32, r0, 0, lane) : frag_tr<0>(tdy1, 32, r0, 0, lane);
+        if constexpr (MB == 2) {
+          const bf16* tdy1 = tdy0 + DYBLK;
+          const bf16x8 fa0 = sub ? frag_tr<1>(tdy0, 32, r0, 0, lane) : frag_tr<0>(tdy0, 32, r0, 0, lane);
+          const bf16x8 fa1 = sub ? frag_tr<1>(tdy1, 32, r0, 0, lane) : frag_tr<0>(tdy1, 32, r0, 0, lane);
 #pragma unroll
-        for (int d = 0; d < 3; ++d) {
-          const bf16x8 fb = sub ? frag_tr<1>(tx, 32, r0 + d, 0, lane) : frag_tr<0>(tx, 32, r0 + d, 0, lane);
-          acc[d][0] = mfma32(fa0, fb, acc[d][0]);
-          acc[d][1] = mfma32(fa1, fb, acc[d][1]);
+          for (int d = 0; d < 3; ++d) {
+            const bf16x8 fb = sub ? frag_tr<1>(tx, 32, r0 + d, 0, lane) : frag_tr<0>(tx, 32, r0 + d, 0, lane);
+            acc[d][0] = mfma32(fa0, fb, acc[d][0]);
+            acc[d][MB - 1] = mfma32(fa1, fb, acc[d][MB - 1]);
+          }
+        } else {
+          const bf16x8 fa0 = sub ? frag_tr<1>(tdy0, 32, r0, 0, lane) : frag_tr<0>(tdy0, 32, r0, 0, lane);
+#pragma unroll
+          for (int d = 0; d < 3; ++d) {
+            const bf16x8 fb = sub ? frag_tr<1>(tx, 32, r0 + d, 0, lane) : frag_tr<0>(tx, 32, r0 + d, 0, lane);
+            acc[d][0] = mfma32(fa0, fb, acc[d][0]);
+          }
         }
       }
     }
@@ -794,44 +803,45 @@ __global__ __launch_bounds__(64 * WN * WC) void conv3_wgrad5_kernel(WgradArgs a)
     __syncthreads();
     buf ^= 1;
   }
-  // acc[d][m] reg i: n = n0 + 64 wn + 32 m + (i&3) + 8(i>>2) + 4h, c = c0 + 32 wc + (lane & 31)
+  // acc[d][m] reg i: n = n0 + 32 (MB wn + m) + (i&3) + 8(i>>2) + 4h, c = c0 + 32 wc + (lane & 31)
   const int h = lane >> 5;
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
     float* out = a.part + ((long long)split * T + grp * 3 + d) * a.Cout * a.Cin;
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+    for (int m = 0; m < MB; ++m)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int row = n0 + 64 * wn + 32 * m + (i & 3) + 8 * (i >> 2) + 4 * h;
+        const int row = n0 + 32 * (MB * wn + m) + (i & 3) + 8 * (i >> 2) + 4 * h;
         out[(long long)row * a.Cin + c0 + 32 * wc + (lane & 31)] = acc[d][m][i];
       }
   }
 }
 
-template <int WN, int WC>
+template <int MB, int WN, int WC>
 static int launch_wgrad5(WgradArgs a, hipStream_t st) {
   constexpr int XR = WG_ROWS + 2;
-  const size_t sh = (size_t)2 * (2 * WN * WG_ROWS * 32 + WC * (XR + 6) * 32) * sizeof(bf16);
-  const long long nb = (long long)a.KD * 3 * a.ns * (a.Cout / (64 * WN)) * (a.Cin / (32 * WC));
+  const size_t sh = (size_t)2 * (MB * WN * WG_ROWS * 32 + WC * (XR + 6) * 32) * sizeof(bf16);
+  const long long nb = (long long)a.KD * 3 * a.ns * (a.Cout / (32 * MB * WN)) * (a.Cin / (32 * WC));
   LCI_CHECK(nb < (1LL << 30), "conv3_wgrad: too many workgroups");
   a.nb = (int)nb;
-  (void)hipFuncSetAttribute((const void*)conv3_wgrad5_kernel<WN, WC>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024);
-  hipLaunchKernelGGL((conv3_wgrad5_kernel<WN, WC>), dim3((unsigned)((nb + 7) / 8 * 8)), dim3(64 * WN * WC), sh, st, a);
+  (void)hipFuncSetAttribute((const void*)conv3_wgrad5_kernel<MB, WN, WC>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipLaunchKernelGGL((conv3_wgrad5_kernel<MB, WN, WC>), dim3((unsigned)((nb + 7) / 8 * 8)), dim3(64 * WN * WC), sh,
+                     st, a);
   LCI_LAUNCH_CHECK();
   return 0;
 }
 
-// (WN, WC) for the v5 weight gradient, or (0, 0) when the v4 kernel handles the shape (Cout = 32)
-// (WN, WC) for the v5 weight gradient, or (0, 0) when the v4 kernel handles the shape: v5 needs >= 4 waves per
-// workgroup (with fewer threads each one stages so many rows that its row state alone fills the register file)
-static void wgrad5_tile(int Cin, int Cout, int& wn, int& wc) {
-  // measured (tools/conv_bench.py): WN = 2 tiles 1.6-1.8x over v4 (C5 512->256: 228 -> 128 ms); the 4-wave
-  // (1, 4) tile was 5-10 % slower than v4 (one workgroup of 4 waves per CU), so v5 runs for Cout % 128 == 0 only
-  wn = Cout % 128 == 0 ? 2 : 0;
-  wc = Cin % 128 == 0 ? 4 : (Cin % 64 == 0 ? 2 : 1);
-  if (wn * wc < 4) wn = wc = 0;
+// (MB, WN, WC) of the v5 weight gradient, or MB = 0 when the v4 kernel handles the shape. Measured
+// (tools/conv_bench.py): the 8-wave (2, 2, 4) tile 1.6-1.8x over v4 (C5 512->256: 228 -> 128 ms); a 4-wave
+// (1, 1, 4) tile was 5-10 % slower than v4, so v5 needs >= 6 waves: Cout % 128 -> (2, 2, 4 or 2); the Swin
+// channel counts (Cout % 96) -> (1, 3, 3 or 2) (9-wave workgroups cannot hold MB = 2 without spilling).
+static void wgrad5_tile(int Cin, int Cout, int& mb, int& wn, int& wc) {
+  mb = wn = wc = 0;
+  if (Cout % 128 == 0) { mb = 2; wn = 2; wc = Cin % 128 == 0 ? 4 : (Cin % 64 == 0 ? 2 : 0); }
+  else if (Cout % 96 == 0) { mb = 1; wn = 3; wc = Cin % 96 == 0 ? 3 : (Cin % 64 == 0 ? 2 : 0); }
+  if (wc == 0) mb = wn = 0;
 }
 
 static bool lci_conv_lds() {   // LCI_CONV_LDS=0: the direct-load kernel (A/B)
@@ -905,9 +915,9 @@ extern "C" int lci_conv3_fwd(const void* x, const void* w, void* y, int B, int D
 // Voxel (gapped-row) splits: up to 2^17 rows per workgroup, fewer (>= 1024) when that leaves under ~2048 workgroups
 // (small 2-D volumes, few channel tiles), so the grid still fills the 256 CUs.
 extern "C" long long lci_conv3_wgrad_splits(long long V, int Cin, int Cout, int KD) {
-  int wn, wc;
-  wgrad5_tile(Cin, Cout, wn, wc);
-  const long long tiles = wn ? (long long)KD * 3 * (Cout / (64 * wn)) * (Cin / (32 * wc))
+  int mb, wn, wc;
+  wgrad5_tile(Cin, Cout, mb, wn, wc);
+  const long long tiles = mb ? (long long)KD * 3 * (Cout / (32 * mb * wn)) * (Cin / (32 * wc))
                              : (long long)KD * 3 * (Cout / (32 * ((Cout / 32) % 2 == 0 ? 2 : 1))) * (Cin / 32);
   long long lv = 1 << 17;
   while (lv > 1024 && ((V + lv - 1) / lv) * tiles < 2048) lv >>= 1;
@@ -935,11 +945,11 @@ extern "C" int lci_conv3_wgrad(const void* x, const void* dy, float* part, int B
   hipStream_t st = (hipStream_t)stream;
   a.ns = (int)ns;
   static const int v5_env = getenv("LCI_WGRAD_V5") ? atoi(getenv("LCI_WGRAD_V5")) : 1;
-  int wn, wc;
-  wgrad5_tile(Cin, Cout, wn, wc);
-  if (v5_env && wn) {
-#define LCI_W5(N, C) if (wn == N && wc == C) return launch_wgrad5<N, C>(a, st);
-    LCI_W5(2, 4) LCI_W5(2, 2)
+  int mb, wn, wc;
+  wgrad5_tile(Cin, Cout, mb, wn, wc);
+  if (v5_env && mb) {
+#define LCI_W5(M, N, C) if (mb == M && wn == N && wc == C) return launch_wgrad5<M, N, C>(a, st);
+    LCI_W5(2, 2, 4) LCI_W5(2, 2, 2) LCI_W5(1, 3, 3) LCI_W5(1, 3, 2)
 #undef LCI_W5
   }
   // 32*MT output channels per workgroup: 2 where Cout allows (2 waves per SIMD), else 1. MT = 3 (256 registers, one
