@@ -58,11 +58,18 @@ def use_tuned_gemms(path: str = TUNED_GEMMS) -> bool:
 
 
 def build_optimizer(params, config):
+    """The reference's optimizers (trainer_base.py; same hyper-parameters). On the GPU Adam / AdamW use torch's
+    fused single-kernel implementation (same update rule; the default multi-tensor version launched ~150 kernels per
+    step for the SwinUNETR parameter list, 6.4 ms per C3 step)."""
     o = config.optim
+    params = list(params)
+    fused = all(p.is_cuda for p in params) and os.environ.get("LCI_FUSED_ADAM", "1") != "0"
     if config.optim_type == "adam":
-        return torch.optim.Adam(params, lr=o.lr, betas=(o.beta1, o.beta2), weight_decay=o.weight_decay)
+        return torch.optim.Adam(params, lr=o.lr, betas=(o.beta1, o.beta2), weight_decay=o.weight_decay,
+                                fused=fused or None)
     if config.optim_type == "adamw":
-        return torch.optim.AdamW(params, lr=o.lr, betas=(o.beta1, o.beta2), weight_decay=o.weight_decay)
+        return torch.optim.AdamW(params, lr=o.lr, betas=(o.beta1, o.beta2), weight_decay=o.weight_decay,
+                                 fused=fused or None)
     return torch.optim.SGD(params, lr=o.lr, weight_decay=o.weight_decay)
 
 

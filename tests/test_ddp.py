@@ -118,7 +118,7 @@ def _bench_worker(rank, world, port, q):
     so the reported time must be the max over ranks, and the weights must stay identical across ranks."""
     import time
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
+                      LOCAL_RANK=str(rank), LCI_DIST_BACKEND="gloo")   # CPU ranks even on a GPU box
     import bench
     from long_context_biomedical_imaging_amd.trainer import TrainStep, init_distributed
     r, local, w = init_distributed()          # the harness's own rendezvous path (gloo without a GPU)
