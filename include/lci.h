@@ -25,6 +25,9 @@
  *   lci_layernorm_*       TransformerBlock / SwinTransformerBlock norm1, norm2 (nn.LayerNorm, backbone_vit.py:250-262,
  *                         backbone_swin.py:418,431) + the autocast cast
  *                         of its output to the next Linear's bf16 operand
+ *   lci_linear_wgrad      the weight / bias gradient GEMM of the token-wise nn.Linear layers (SABlock qkv / out_proj
+ *                         backbone_vit.py:166-167, MONAI MLPBlock linear1/2, MambaVisionMixer in/x/dt/out_proj
+ *                         mamba.py:60-64,90, HyenaOperator in/out_proj hyena.py:278-279, Swin qkv/proj/mlp)
  */
 #ifndef LCI_H_
 #define LCI_H_
@@ -34,8 +37,8 @@ extern "C" {
 #endif
 
 /* Bumped whenever an entry point's argument list or buffer contract changes (3: lci_layernorm_bwd gained dres;
- * 4: lci_conv3_wgrad writes one partial per voxel split instead of one per split and wave). */
-#define LCI_ABI_VERSION 4
+ * 4: lci_conv3_wgrad writes one partial per voxel split instead of one per split and wave; 5: lci_linear_wgrad). */
+#define LCI_ABI_VERSION 5
 const char* lci_last_error(void);
 int lci_abi_version(void);
 /* sha256 prefix of the sources the library was built from (build_lib.source_hash); the Python binding refuses a
@@ -203,6 +206,16 @@ int lci_layernorm_fwd(const float* x, const float* gamma, const float* beta, voi
 int lci_layernorm_bwd(const float* x, const void* dy, int bf16_dy, const float* gamma, const float* mean,
                       const float* rstd, const float* dres, float* dx, float* part, long long rows, int C,
                       void* stream);
+
+/* ------------------------------------------------------------------ token-wise Linear: weight / bias gradient
+ * dy (M, ldy) bf16 row-major (columns [0, N) used), x (M, ldx) bf16 row-major (columns [0, K) used): the layer's
+ * output gradient and (autocast) input. part (ns, N, K) f32 <- per-token-split partial sums of dy^T x and, when
+ * dbpart is not null, dbpart (ns, N) f32 <- partial column sums of dy; ns = lci_linear_wgrad_splits(M, N, K)
+ * (0: shape not supported). dW / db = sums over the first axis (caller). N, K, ldy, ldx multiples of 8, pointers
+ * 16-byte aligned. Deterministic (no atomics). */
+long long lci_linear_wgrad_splits(long long M, int N, int K);
+int lci_linear_wgrad(const void* dy, long long ldy, const void* x, long long ldx, long long M, int N, int K,
+                     float* part, float* dbpart, void* stream);
 
 #ifdef __cplusplus
 }

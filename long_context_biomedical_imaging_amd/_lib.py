@@ -14,7 +14,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_LIB = os.path.join(HERE, "liblci.so")
 LIB_PATH = os.environ.get("LCI_LIB_PATH", DEFAULT_LIB)   # override: kernel-variant A/B runs (no staleness check)
-ABI_VERSION = 4   # include/lci.h LCI_ABI_VERSION
+ABI_VERSION = 5   # include/lci.h LCI_ABI_VERSION
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -51,6 +51,7 @@ SIGNATURES = {
     "lci_layernorm_fwd": [_P, _P, _P, _P, _I, _P, _P, _L, _I, _F, _P],
     "lci_layernorm_bwd": [_P, _P, _I, _P, _P, _P, _P, _P, _P, _L, _I, _P],
     "lci_dwconv_silu_bwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    "lci_linear_wgrad": [_P, _L, _P, _L, _L, _I, _I, _P, _P, _P],
 }
 
 _lib = None
@@ -89,6 +90,8 @@ def load(path: str = LIB_PATH):
     lib.lci_attn_fwd_ws_bytes.argtypes = [_I, _I, _I]
     lib.lci_conv3_wgrad_splits.restype = ctypes.c_longlong
     lib.lci_conv3_wgrad_splits.argtypes = [ctypes.c_longlong, _I, _I, _I]
+    lib.lci_linear_wgrad_splits.restype = ctypes.c_longlong
+    lib.lci_linear_wgrad_splits.argtypes = [ctypes.c_longlong, _I, _I]
     lib.lci_inorm_chunks.restype = ctypes.c_int
     lib.lci_inorm_chunks.argtypes = [ctypes.c_longlong, _I]
     lib.lci_layernorm_bwd_blocks.restype = ctypes.c_int

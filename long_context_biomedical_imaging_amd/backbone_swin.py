@@ -26,7 +26,7 @@ import torch.nn.functional as F
 
 from . import kernels
 from .blocks import MLPBlock as Mlp
-from .blocks import PatchEmbed, TokenLayerNorm, trunc_normal_
+from .blocks import PatchEmbed, TokenLayerNorm, TokenLinear, trunc_normal_
 from .hyena import HyenaOperator
 from .mamba import MambaVisionMixer
 
@@ -144,9 +144,9 @@ class WindowAttention(nn.Module):
             n_tab = int(np.prod([2 * w - 1 for w in window_size]))
             self.relative_position_bias_table = nn.Parameter(torch.zeros(n_tab, num_heads))
             self.register_buffer("relative_position_index", relative_position_index(window_size))
-            self.qkv = nn.Linear(dim, dim * 3, bias=qkv_bias)
+            self.qkv = TokenLinear(dim, dim * 3, bias=qkv_bias)
             self.attn_drop = nn.Dropout(attn_drop)
-            self.proj = nn.Linear(dim, dim)
+            self.proj = TokenLinear(dim, dim)
             self.proj_drop = nn.Dropout(proj_drop)
             trunc_normal_(self.relative_position_bias_table, std=0.02)
             self.softmax = nn.Softmax(dim=-1)
@@ -263,10 +263,10 @@ class PatchMergingV2(nn.Module):
         super().__init__()
         self.dim = dim
         if spatial_dims == 3:
-            self.reduction = nn.Linear(8 * dim, 2 * dim, bias=False)
+            self.reduction = TokenLinear(8 * dim, 2 * dim, bias=False)
             self.norm = norm_layer(8 * dim)
         elif spatial_dims == 2:
-            self.reduction = nn.Linear(4 * dim, 2 * dim, bias=False)
+            self.reduction = TokenLinear(4 * dim, 2 * dim, bias=False)
             self.norm = norm_layer(4 * dim)
 
     def forward(self, x):

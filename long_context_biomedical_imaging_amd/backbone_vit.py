@@ -16,7 +16,7 @@ import torch.nn as nn
 import torch.utils.checkpoint
 
 from . import kernels
-from .blocks import MLPBlock, PatchEmbeddingBlock, TokenLayerNorm
+from .blocks import MLPBlock, PatchEmbeddingBlock, TokenLayerNorm, TokenLinear
 from .hyena import HyenaOperator
 from .mamba import MambaVisionMixer
 
@@ -79,8 +79,8 @@ class SABlock(nn.Module):
             self.scale = self.head_dim ** -0.5
             self.save_attn = save_attn
             self.att_mat = torch.Tensor()
-            self.qkv = nn.Linear(hidden_size, hidden_size * 3, bias=qkv_bias)
-            self.out_proj = nn.Linear(hidden_size, hidden_size)
+            self.qkv = TokenLinear(hidden_size, hidden_size * 3, bias=qkv_bias)
+            self.out_proj = TokenLinear(hidden_size, hidden_size)
         elif use_hyena and not use_mamba:
             self.hyena = HyenaOperator(d_model=hidden_size, l_max=hyena_l_max, filter_order=64, num_heads=num_heads,
                                        num_blocks=1, short_filter_order=5, bidrectional=True,

@@ -6,7 +6,8 @@ checkpoints load and seeded initialisation reproduces the reference's weights:
   PatchEmbeddingBlock backbone_vit.py:351-361  (conv k=s=p -> flatten/transpose -> + position_embeddings)
   PatchEmbed          backbone_swin.py:800-806 (right pad to a patch multiple -> conv k=s=p)
 The patch-embedding forward runs the HIP patch-embed kernels (kernels.patch_embed_*); TokenLayerNorm (an
-nn.LayerNorm) runs the HIP LayerNorm kernels (kernels.layer_norm).
+nn.LayerNorm) runs the HIP LayerNorm kernels (kernels.layer_norm); TokenLinear (an nn.Linear) takes its weight / bias
+gradient from the HIP split-token GEMM (kernels.linear, lci_linear_wgrad).
 """
 from __future__ import annotations
 
@@ -52,6 +53,17 @@ class TokenLayerNorm(nn.LayerNorm):
         return kernels.residual_layer_norm(x, self.weight, self.bias, self.eps, self._bf16_out())
 
 
+class TokenLinear(nn.Linear):
+    """nn.Linear (same parameters, state_dict keys and seeded init) for the token-wise projections. On the GPU the
+    forward and data gradient are the autocast GEMMs torch would run (hipBLASLt); the weight and bias gradients,
+    a reduction over all B*L tokens into a small N x K output, run on lci_linear_wgrad (kernels.linear)."""
+
+    def forward(self, x):
+        if x.is_cuda:
+            return kernels.linear(x, self.weight, self.bias)
+        return super().forward(x)
+
+
 class MLPBlock(nn.Module):
     def __init__(self, hidden_size: int, mlp_dim: int, dropout_rate: float = 0.0, act="GELU",
                  dropout_mode="vit") -> None:
@@ -59,8 +71,8 @@ class MLPBlock(nn.Module):
         if not (0 <= dropout_rate <= 1):
             raise ValueError("dropout_rate should be between 0 and 1.")
         mlp_dim = mlp_dim or hidden_size
-        self.linear1 = nn.Linear(hidden_size, mlp_dim)
-        self.linear2 = nn.Linear(mlp_dim, hidden_size)
+        self.linear1 = TokenLinear(hidden_size, mlp_dim)
+        self.linear2 = TokenLinear(mlp_dim, hidden_size)
         if act != "GELU":
             raise NotImplementedError(f"act={act}: only GELU is used by the reference")
         self.fn = nn.GELU()

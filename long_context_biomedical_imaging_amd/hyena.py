@@ -23,6 +23,7 @@ import torch.nn as nn
 from pydantic import validate_call
 
 from . import kernels
+from .blocks import TokenLinear
 
 
 class OptimModule(nn.Module):
@@ -159,8 +160,8 @@ class HyenaOperator(nn.Module):
         self.outer_mixing = outer_mixing
         self.return_state = return_state
         self.dropout = nn.Dropout(dropout)
-        self.in_proj = nn.Linear(self.d_model, self.NUM_PROJECTIONS * self.d_model)
-        self.out_proj = nn.Linear(self.d_model, self.d_model)
+        self.in_proj = TokenLinear(self.d_model, self.NUM_PROJECTIONS * self.d_model)
+        self.out_proj = TokenLinear(self.d_model, self.d_model)
         self.bidirectional = bidirectional
         total_width = self.d_model * self.NUM_PROJECTIONS
         self.short_filter = nn.Conv1d(in_channels=total_width, out_channels=total_width,

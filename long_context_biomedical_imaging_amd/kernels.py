@@ -950,3 +950,76 @@ def residual_layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tenso
     if not ln_kernel_supports(x.shape[-1]):
         return x, _torch_ln(x, weight, bias, eps, bf16_out)
     return _ResidualLayerNorm.apply(x, weight, bias, eps, bf16_out)
+
+
+# ------------------------------------------------------------------------------------- token-wise Linear
+def linear_wgrad_supported(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
+    """Whether lci_linear_wgrad takes (dy2 (M, N), x2 (M, K)): bf16 CUDA row-major views with unit column stride,
+    N, K and the row strides multiples of 8, 16-byte aligned, and a tile that fits (N, K)."""
+    if not (dy2.is_cuda and x2.is_cuda and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16):
+        return False
+    (M, N), K = dy2.shape, x2.shape[1]
+    if dy2.stride(1) != 1 or x2.stride(1) != 1 or N % 8 or K % 8 or dy2.stride(0) % 8 or x2.stride(0) % 8:
+        return False
+    if dy2.data_ptr() % 16 or x2.data_ptr() % 16 or M == 0:
+        return False
+    return _lib.load().lci_linear_wgrad_splits(M, N, K) > 0
+
+
+def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor, bias: bool):
+    """dW (N, K) f32 = dy2^T x2 and db (N) f32 = column sums of dy2 (or None), by the HIP split-token kernel
+    (per-split partials summed here)."""
+    (M, N), K = dy2.shape, x2.shape[1]
+    lib = _lib.load()
+    ns = lib.lci_linear_wgrad_splits(M, N, K)
+    if ns <= 0:
+        raise _lib.LciError(f"linear_wgrad: unsupported shape N={N}, K={K}")
+    part = torch.empty(ns, N, K, device=dy2.device, dtype=torch.float32)
+    dbp = torch.empty(ns, N, device=dy2.device, dtype=torch.float32) if bias else None
+    KernelTimer.run("linear_wgrad", 2.0 * M * N * K, dy2, lambda: _lib.call(
+        "lci_linear_wgrad", dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), M, N, K, part.data_ptr(),
+        _lib.ptr(dbp), _lib.stream_of(dy2)))
+    return part.sum(0), (dbp.sum(0) if bias else None)
+
+
+class _Linear(torch.autograd.Function):
+    """y = x W^T + b with autocast's casts done here (x, W, b -> the autocast dtype, exactly what F.linear under
+    autocast computes: hipBLASLt forward and data gradient); the weight / bias gradient runs on lci_linear_wgrad
+    (f32 result, returned to the f32 parameters without the bf16 rounding the autocast GEMM would apply)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        if torch.is_autocast_enabled("cuda"):
+            dt = torch.get_autocast_dtype("cuda")
+            xc, wc = x.to(dt), weight.to(dt)
+            bc = bias.to(dt) if bias is not None else None
+        else:
+            xc, wc, bc = x, weight, bias
+        with torch.autocast("cuda", enabled=False):
+            y = torch.nn.functional.linear(xc, wc, bc)
+        ctx.save_for_backward(xc, wc)
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, wc = ctx.saved_tensors
+        N, K = wc.shape
+        dy2 = dy.reshape(-1, N)
+        if dy2.stride(1) != 1:
+            dy2 = dy2.contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = (dy2 @ wc).view(*dy.shape[:-1], K)
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            x2 = xc.reshape(-1, K)
+            if linear_wgrad_supported(dy2, x2):
+                dw, db = linear_wgrad(dy2, x2, ctx.has_bias)
+            else:
+                dw = (dy2.t() @ x2).float()
+                db = dy2.float().sum(0) if ctx.has_bias else None
+        return dx, dw, db
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None) -> torch.Tensor:
+    return _Linear.apply(x, weight, bias)

@@ -18,6 +18,7 @@ import torch
 import torch.nn as nn
 
 from . import kernels
+from .blocks import TokenLinear
 
 
 class MambaVisionMixer(nn.Module):
@@ -34,9 +35,9 @@ class MambaVisionMixer(nn.Module):
         self.dt_rank = math.ceil(self.d_model / 16) if dt_rank == "auto" else dt_rank
         self.use_fast_path = use_fast_path
         self.layer_idx = layer_idx
-        self.in_proj = nn.Linear(self.d_model, self.d_inner, bias=bias, **factory_kwargs)
-        self.x_proj = nn.Linear(self.d_inner // 2, self.dt_rank + self.d_state * 2, bias=False, **factory_kwargs)
-        self.dt_proj = nn.Linear(self.dt_rank, self.d_inner // 2, bias=True, **factory_kwargs)
+        self.in_proj = TokenLinear(self.d_model, self.d_inner, bias=bias, **factory_kwargs)
+        self.x_proj = TokenLinear(self.d_inner // 2, self.dt_rank + self.d_state * 2, bias=False, **factory_kwargs)
+        self.dt_proj = TokenLinear(self.dt_rank, self.d_inner // 2, bias=True, **factory_kwargs)
         dt_init_std = self.dt_rank ** -0.5 * dt_scale
         if dt_init == "constant":
             nn.init.constant_(self.dt_proj.weight, dt_init_std)
@@ -56,7 +57,7 @@ class MambaVisionMixer(nn.Module):
         self.A_log._no_weight_decay = True
         self.D = nn.Parameter(torch.ones(self.d_inner // 2, device=device))
         self.D._no_weight_decay = True
-        self.out_proj = nn.Linear(self.d_inner, self.d_model, bias=bias, **factory_kwargs)
+        self.out_proj = TokenLinear(self.d_inner, self.d_model, bias=bias, **factory_kwargs)
         self.conv1d_x = nn.Conv1d(in_channels=self.d_inner // 2, out_channels=self.d_inner // 2,
                                   bias=conv_bias // 2, kernel_size=d_conv, groups=self.d_inner // 2,
                                   **factory_kwargs)

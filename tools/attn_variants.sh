@@ -13,7 +13,7 @@ if [ "$1" = build ]; then
     for f in $ROOT/long_context_biomedical_imaging_amd/csrc/*.hip $ROOT/long_context_biomedical_imaging_amd/csrc/*.cpp; do
       b=$(basename $f)
       extra=""
-      case $b in attention.hip) extra="-fno-honor-nans -fno-slp-vectorize $defs";; window.hip) extra="-fno-honor-nans $defs";; esac
+      case $b in attention.hip) extra="-fno-honor-nans -fno-slp-vectorize $defs";; window.hip) extra="-fno-honor-nans $defs";; *.hip) extra="$defs";; esac
       if [ "${b##*.}" = hip ]; then
         /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result -munsafe-fp-atomics \
           -Xarch_device -mllvm=-amdgpu-mfma-vgpr-form $extra -c $f -o $OUT/$name.$b.o &

@@ -138,8 +138,26 @@ def bench_patch_embed():
          "ViT p2 512^2 -> (2, 65536, 384) f32 + pos")
 
 
+def bench_linear():
+    """Linear weight gradient dW = dY^T X (+ db) at the ViT (M = 131072) and C5 (M = 2^21) token counts: the HIP
+    split-token kernel vs torch's hipBLASLt GEMM of the same bf16 operands."""
+    shapes = {"qkv": (1152, 384), "proj": (384, 384), "fc1": (1536, 384), "fc2": (384, 1536),
+              "m_x": (40, 192), "m_dt": (192, 24), "swin_qkv96": (288, 96), "swin_fc2_96": (96, 384)}
+    for M in (131072, 1 << 21):
+        for name, (N, K) in shapes.items():
+            dy = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+            x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+            f = 2.0 * M * N * K
+            if kernels.linear_wgrad_supported(dy, x):
+                emit(f"linear_wgrad {name}", timeit(lambda: kernels.linear_wgrad(dy, x, True)), f, "TFLOP/s",
+                     f"M{M} N{N} K{K} (+db, split partials summed)")
+            emit(f"torch dy^T x {name}", timeit(lambda: dy.t() @ x), f, "TFLOP/s", f"M{M} N{N} K{K}")
+            del dy, x
+            torch.cuda.empty_cache()
+
+
 def main():
-    which = sys.argv[1:] or ["attention", "window", "scan", "fftconv", "patch"]
+    which = sys.argv[1:] or ["attention", "window", "scan", "fftconv", "patch", "linear"]
     if "attention" in which:
         bench_attention()
     if "window" in which:
@@ -151,6 +169,8 @@ def main():
         bench_fftconv()
     if "patch" in which:
         bench_patch_embed()
+    if "linear" in which:
+        bench_linear()
 
 
 if __name__ == "__main__":
