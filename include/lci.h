@@ -25,7 +25,8 @@
  *   lci_layernorm_*       TransformerBlock / SwinTransformerBlock norm1, norm2 (nn.LayerNorm, backbone_vit.py:250-262,
  *                         backbone_swin.py:418,431) + the autocast cast
  *                         of its output to the next Linear's bf16 operand
- *   lci_linear_wgrad      the weight / bias gradient GEMM of the token-wise nn.Linear layers (SABlock qkv / out_proj
+ *   lci_linear_*          the token-wise nn.Linear GEMMs: MLPBlock linear1 + GELU + linear2 with fused epilogues
+ *                         (backbone_vit.py:249, MONAI MLPBlock) and the weight / bias gradient of (SABlock qkv / out_proj
  *                         backbone_vit.py:166-167, MONAI MLPBlock linear1/2, MambaVisionMixer in/x/dt/out_proj
  *                         mamba.py:60-64,90, HyenaOperator in/out_proj hyena.py:278-279, Swin qkv/proj/mlp)
  */
@@ -216,6 +217,16 @@ int lci_layernorm_bwd(const float* x, const void* dy, int bf16_dy, const float* 
 long long lci_linear_wgrad_splits(long long M, int N, int K);
 int lci_linear_wgrad(const void* dy, long long ldy, const void* x, long long ldx, long long M, int N, int K,
                      float* part, float* dbpart, void* stream);
+/* y (M, ldy) bf16 = epilogue(x (M, ldx) bf16 . w^T), w (N, K) bf16 contiguous, f32 accumulation:
+ *   epilogue 0: y = bf16(acc + bias)            (bias (N) bf16 or null; nn.Linear under autocast)
+ *   epilogue 1: aux = pre = bf16(acc + bias), y = bf16(gelu(pre))    (MLPBlock linear1 + GELU, exact erf)
+ *   epilogue 2: y = bf16(bf16(acc) * gelu'(aux))  (linear2's data gradient through GELU; aux = saved pre)
+ * The data gradient of a Linear is the same call with the transposed weight. Supported when
+ * lci_linear_fwd_supported(N, K): N % 128 == 0 or N % 96 == 0, K % 8 == 0; ldx % 8, ldy / ldaux % 4 == 0,
+ * x / w 16-byte aligned, y / aux / bias 8-byte aligned. */
+int lci_linear_fwd_supported(int N, int K);
+int lci_linear_fwd(int epilogue, const void* x, long long ldx, const void* w, const void* bias, void* y,
+                   long long ldy, void* aux, long long ldaux, long long M, int N, int K, void* stream);
 
 #ifdef __cplusplus
 }

@@ -52,6 +52,7 @@ SIGNATURES = {
     "lci_layernorm_bwd": [_P, _P, _I, _P, _P, _P, _P, _P, _P, _L, _I, _P],
     "lci_dwconv_silu_bwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "lci_linear_wgrad": [_P, _L, _P, _L, _L, _I, _I, _P, _P, _P],
+    "lci_linear_fwd": [_I, _P, _L, _P, _P, _P, _L, _P, _L, _L, _I, _I, _P],
 }
 
 _lib = None
@@ -92,6 +93,8 @@ def load(path: str = LIB_PATH):
     lib.lci_conv3_wgrad_splits.argtypes = [ctypes.c_longlong, _I, _I, _I]
     lib.lci_linear_wgrad_splits.restype = ctypes.c_longlong
     lib.lci_linear_wgrad_splits.argtypes = [ctypes.c_longlong, _I, _I]
+    lib.lci_linear_fwd_supported.restype = ctypes.c_int
+    lib.lci_linear_fwd_supported.argtypes = [_I, _I]
     lib.lci_inorm_chunks.restype = ctypes.c_int
     lib.lci_inorm_chunks.argtypes = [ctypes.c_longlong, _I]
     lib.lci_layernorm_bwd_blocks.restype = ctypes.c_int

@@ -11,6 +11,7 @@ gradient from the HIP split-token GEMM (kernels.linear, lci_linear_wgrad).
 """
 from __future__ import annotations
 
+import os
 from collections.abc import Sequence
 
 import numpy as np
@@ -64,6 +65,12 @@ class TokenLinear(nn.Linear):
         return super().forward(x)
 
 
+# MLPBlock on the fused-epilogue HIP GEMMs (lci_linear_fwd): opt-in (LCI_FUSED_MLP=1). Parity-tested, but measured
+# slower than hipBLASLt + torch's GELU kernels on MI355X today (tools/kernel_bench.py mlp), so the
+# default keeps the TokenLinear path (hipBLASLt forward / data gradient, HIP weight gradient).
+FUSED_MLP = os.environ.get("LCI_FUSED_MLP", "0") == "1"
+
+
 class MLPBlock(nn.Module):
     def __init__(self, hidden_size: int, mlp_dim: int, dropout_rate: float = 0.0, act="GELU",
                  dropout_mode="vit") -> None:
@@ -85,6 +92,11 @@ class MLPBlock(nn.Module):
             raise ValueError(f"dropout_mode {dropout_mode}")
 
     def forward(self, x):
+        D, H = self.linear1.in_features, self.linear1.out_features
+        if (FUSED_MLP and self.drop1.p == 0 and self.drop2.p == 0 and self.linear1.bias is not None
+                and kernels.mlp_supported(x, D, H)):
+            # fused HIP path (kernels.mlp): GEMM epilogues carry bias + GELU forward and GELU' backward
+            return kernels.mlp(x, self.linear1.weight, self.linear1.bias, self.linear2.weight, self.linear2.bias)
         x = self.drop1(self.fn(self.linear1(x)))
         return self.drop2(self.linear2(x))
 

@@ -82,3 +82,68 @@ def test_token_linear_matches_autocast_linear(N, K, bias):
     assert ((dw1 - dw0).abs() <= 2 ** -8 * dw0.abs() + 1e-5 * (g2.t() @ x2)).all()
     if bias:
         assert ((db1 - db0).abs() <= 2 ** -8 * db0.abs() + 1e-5 * g2.sum(0)).all()
+
+
+def _ulp_close(a, b, ulps=1):
+    """|a - b| <= ulps bf16 ulps of max(|a|, |b|) (elementwise), plus a tiny absolute floor."""
+    a, b = a.double(), b.double()
+    tol = ulps * 2.0 ** -7 * torch.maximum(a.abs(), b.abs()) + 1e-30
+    return ((a - b).abs() <= tol)
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 1536, 384), (4099, 384, 1536), (333, 1152, 384), (2500, 288, 96),
+                                   (1234, 96, 384), (65, 384, 384)])
+def test_linear_fwd_epilogues_vs_reference(M, N, K):
+    from long_context_biomedical_imaging_amd import kernels
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N)
+    x = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).to(torch.bfloat16)
+    b = torch.randn(N, device="cuda", generator=g).to(torch.bfloat16)
+    acc = x.double() @ w.double().t()
+    bound = x.double().abs() @ w.double().abs().t()
+    # plain: bf16(acc + b) -- within half an ulp of the exact value plus f32 reassociation
+    y = kernels.linear_fwd(x, w, b, kernels.LF_PLAIN)
+    exact = acc + b.double()
+    assert ((y.double() - exact).abs() <= 2.0 ** -8 * exact.abs() + 1e-5 * bound + 1e-6).all()
+    # GELU: pre as plain; act = bf16(gelu(pre)) exactly as torch's GELU of the same bf16 pre-activation
+    act, pre = kernels.linear_fwd(x, w, b, kernels.LF_GELU)
+    assert torch.equal(pre, y)
+    ref_act = torch.nn.functional.gelu(pre.float()).to(torch.bfloat16)
+    assert _ulp_close(act, ref_act).all()
+    # dGELU (linear2's data gradient through GELU): x = dY (M, K), w = W2^T (N, K), aux = pre (M, N);
+    # reference = torch's gelu_backward of bf16(dY . W2) and the same bf16 pre-activation
+    dy = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    w2t = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).to(torch.bfloat16)
+    d_pre = kernels.linear_fwd(dy, w2t, None, kernels.LF_DGELU, aux=pre)
+    d_act = (dy.double() @ w2t.double().t()).to(torch.bfloat16)
+    ref = torch.ops.aten.gelu_backward(d_act, pre)
+    close = _ulp_close(d_pre, ref, ulps=2) | ((d_pre.double() - ref.double()).abs() <= 1e-5 * (
+        dy.double().abs() @ w2t.double().abs().t()))
+    assert close.all(), f"{(~close).sum().item()} mismatches"
+
+
+@pytest.mark.parametrize("D,H,M", [(384, 1536, 3000), (96, 384, 4099), (192, 768, 65)])
+def test_mlp_block_fused_matches_module_path(D, H, M):
+    """blocks.MLPBlock under bf16 autocast: the fused HIP path vs the same module run op by op (torch GEMMs +
+    nn.GELU), same weights: outputs and all five gradients."""
+    from long_context_biomedical_imaging_amd import blocks, kernels
+    torch.manual_seed(D + H)
+    mod = blocks.MLPBlock(D, H).cuda()
+    x = torch.randn(2, M, D, device="cuda")
+    gy = torch.randn(2, M, D, device="cuda").to(torch.bfloat16)
+    res = []
+    for fused in (True, False):
+        mod.zero_grad()
+        xi = x.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            if fused:
+                assert kernels.mlp_supported(xi, D, H)
+                y = kernels.mlp(xi, mod.linear1.weight, mod.linear1.bias, mod.linear2.weight, mod.linear2.bias)
+            else:
+                y = mod.linear2(mod.fn(torch.nn.functional.linear(xi, mod.linear1.weight, mod.linear1.bias)))
+        y.backward(gy)
+        res.append([y.detach().float(), xi.grad] + [p.grad.clone() for p in mod.parameters()])
+    names = ["y", "dx", "dW1", "db1", "dW2", "db2"]
+    for n, a, b in zip(names, res[0], res[1]):
+        e = ((a.double() - b.double()).norm() / b.double().norm()).item()
+        assert e < 1e-2, f"{n}: rel-L2 {e:.3e}"

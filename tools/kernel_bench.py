@@ -156,8 +156,40 @@ def bench_linear():
             torch.cuda.empty_cache()
 
 
+def bench_mlp():
+    """MLPBlock GEMMs at the ViT (M = 131072) and C5 (M = 2^21) token counts: HIP fused-epilogue GEMMs vs torch
+    (hipBLASLt addmm + GELU / matmul + gelu_backward) on the same bf16 operands."""
+    D, H = 384, 1536
+    for M in (131072, 1 << 21):
+        x = torch.randn(M, D, device="cuda").to(torch.bfloat16)
+        w1 = (torch.randn(H, D, device="cuda") * 0.05).to(torch.bfloat16)
+        b1 = torch.randn(H, device="cuda").to(torch.bfloat16)
+        w2 = (torch.randn(D, H, device="cuda") * 0.05).to(torch.bfloat16)
+        b2 = torch.randn(D, device="cuda").to(torch.bfloat16)
+        f = 2.0 * M * D * H
+        cfg = f"M{M} D{D} H{H}"
+        act, pre = kernels.linear_fwd(x, w1, b1, kernels.LF_GELU)
+        emit("hip fc1+bias+gelu", timeit(lambda: kernels.linear_fwd(x, w1, b1, kernels.LF_GELU)), f, "TFLOP/s", cfg)
+        emit("torch fc1 addmm+gelu", timeit(lambda: torch.nn.functional.gelu(torch.nn.functional.linear(x, w1, b1))),
+             f, "TFLOP/s", cfg)
+        emit("hip fc2+bias", timeit(lambda: kernels.linear_fwd(act, w2, b2)), f, "TFLOP/s", cfg)
+        emit("torch fc2 addmm", timeit(lambda: torch.nn.functional.linear(act, w2, b2)), f, "TFLOP/s", cfg)
+        dy = torch.randn(M, D, device="cuda").to(torch.bfloat16)
+        w2t = w2.t().contiguous()
+        emit("hip fc2 dgrad+gelu'", timeit(lambda: kernels.linear_fwd(dy, w2t, None, kernels.LF_DGELU, aux=pre)), f,
+             "TFLOP/s", cfg)
+        emit("torch fc2 dgrad+gelu_backward", timeit(lambda: torch.ops.aten.gelu_backward(dy @ w2, pre)), f,
+             "TFLOP/s", cfg)
+        dp = torch.randn(M, H, device="cuda").to(torch.bfloat16)
+        w1t = w1.t().contiguous()
+        emit("hip fc1 dgrad", timeit(lambda: kernels.linear_fwd(dp, w1t, None)), f, "TFLOP/s", cfg)
+        emit("torch fc1 dgrad", timeit(lambda: dp @ w1), f, "TFLOP/s", cfg)
+        del x, act, pre, dy, dp
+        torch.cuda.empty_cache()
+
+
 def main():
-    which = sys.argv[1:] or ["attention", "window", "scan", "fftconv", "patch", "linear"]
+    which = sys.argv[1:] or ["attention", "window", "scan", "fftconv", "patch", "linear", "mlp"]
     if "attention" in which:
         bench_attention()
     if "window" in which:
@@ -171,6 +203,8 @@ def main():
         bench_patch_embed()
     if "linear" in which:
         bench_linear()
+    if "mlp" in which:
+        bench_mlp()
 
 
 if __name__ == "__main__":
