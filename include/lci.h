@@ -225,6 +225,15 @@ int lci_linear_wgrad(const void* dy, long long ldy, const void* x, long long ldx
  * lci_linear_fwd_supported(N, K): N % 128 == 0 or N % 96 == 0, K % 8 == 0; ldx % 8, ldy / ldaux % 4 == 0,
  * x / w 16-byte aligned, y / aux / bias 8-byte aligned. */
 int lci_linear_fwd_supported(int N, int K);
+/* Narrow outputs (the UNETR heads' 1x1 conv to 1-8 channels, over channels-last voxel rows): y (M, N) bf16 =
+ * x (M, ldx) . w^T + bias, w (N, K) bf16, bias (N) bf16 or null; N <= 8, K <= 256, K % 8 == 0.
+ * bwd (N <= 4): dx (M, K) bf16 = dy . w (optional); part ((N K + N), lci_linear_small_threads()) f32 <- per-thread
+ * partial sums of dy^T x (row-major N x K) and of dy; dW, db = sums over the last axis (caller). */
+int lci_linear_small_threads(void);
+int lci_linear_small_fwd(const void* x, long long ldx, const void* w, const void* bias, void* y, long long M, int N,
+                         int K, void* stream);
+int lci_linear_small_bwd(const void* x, long long ldx, const void* w, const void* dy, void* dx, float* part,
+                         long long M, int N, int K, void* stream);
 int lci_linear_fwd(int epilogue, const void* x, long long ldx, const void* w, const void* bias, void* y,
                    long long ldy, void* aux, long long ldaux, long long M, int N, int K, void* stream);
 

@@ -53,6 +53,8 @@ SIGNATURES = {
     "lci_dwconv_silu_bwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "lci_linear_wgrad": [_P, _L, _P, _L, _L, _I, _I, _P, _P, _P],
     "lci_linear_fwd": [_I, _P, _L, _P, _P, _P, _L, _P, _L, _L, _I, _I, _P],
+    "lci_linear_small_fwd": [_P, _L, _P, _P, _P, _L, _I, _I, _P],
+    "lci_linear_small_bwd": [_P, _L, _P, _P, _P, _P, _L, _I, _I, _P],
 }
 
 _lib = None
@@ -95,6 +97,8 @@ def load(path: str = LIB_PATH):
     lib.lci_linear_wgrad_splits.argtypes = [ctypes.c_longlong, _I, _I]
     lib.lci_linear_fwd_supported.restype = ctypes.c_int
     lib.lci_linear_fwd_supported.argtypes = [_I, _I]
+    lib.lci_linear_small_threads.restype = ctypes.c_int
+    lib.lci_linear_small_threads.argtypes = []
     lib.lci_inorm_chunks.restype = ctypes.c_int
     lib.lci_inorm_chunks.argtypes = [ctypes.c_longlong, _I]
     lib.lci_layernorm_bwd_blocks.restype = ctypes.c_int

@@ -478,6 +478,94 @@ static int lf_dispatch(const LinFwdArgs& a, hipStream_t st) {
   return launch_lf<4, 3, 2, 1, EPI>(a, st);               // 2 waves of 128 tokens x 96 features
 }
 
+
+// ------------------------------------------------------------------------- narrow outputs (the heads' 1x1 convs)
+// y (M, N) = x (M, K) . w^T + b for N <= 8: UnetOutBlock's 1x1 conv to the class / output channels (MONAI-1.3
+// get_conv_layer(kernel_size=1, bias=True), enhance_heads.py:30-356) over every voxel, as channels-last rows.
+// hipBLASLt runs these 2-column GEMMs with 16-32-wide tiles at ~1% of the HBM rate (C3: 3 ms forward, 3 ms backward
+// per step); they are pure streams: one thread per row, the weights in LDS as f32.
+constexpr int LS_MAXN = 8, LS_MAXK = 256, LS_THREADS = 65536;   // backward: fixed grid-stride thread count
+
+__global__ __launch_bounds__(256) void linear_small_fwd_kernel(const bf16* __restrict__ x, long long ldx,
+                                                                const bf16* __restrict__ w,
+                                                                const bf16* __restrict__ b, bf16* __restrict__ y,
+                                                                long long M, int N, int K) {
+  __shared__ float sw[LS_MAXN * LS_MAXK];
+  for (int i = threadIdx.x; i < N * K; i += 256) sw[i] = to_f32(w[i]);
+  __syncthreads();
+  for (long long m = (long long)blockIdx.x * 256 + threadIdx.x; m < M; m += (long long)gridDim.x * 256) {
+    float acc[LS_MAXN];
+#pragma unroll
+    for (int o = 0; o < LS_MAXN; ++o) acc[o] = 0.f;
+    const bf16* xr = x + m * ldx;
+    for (int c = 0; c < K; c += 8) {
+      const bf16x8 v = *(const bf16x8*)(xr + c);
+#pragma unroll
+      for (int o = 0; o < LS_MAXN; ++o) {
+        if (o >= N) break;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[o] += to_f32(v[j]) * sw[o * K + c + j];
+      }
+    }
+    for (int o = 0; o < N; ++o) y[m * N + o] = to_bf16(acc[o] + (b ? to_f32(b[o]) : 0.f));
+  }
+}
+
+// dx (M, K) = dy . w (optional); part ((N K + N), LS_THREADS) f32 = per-thread partial sums of dy^T x and of dy
+template <int N>
+__global__ __launch_bounds__(256) void linear_small_bwd_kernel(const bf16* __restrict__ x, long long ldx,
+                                                                const bf16* __restrict__ w,
+                                                                const bf16* __restrict__ dy, bf16* __restrict__ dx,
+                                                                float* __restrict__ part, long long M, int K) {
+  __shared__ float sw[N * LS_MAXK];
+  for (int i = threadIdx.x; i < N * K; i += 256) sw[i] = to_f32(w[i]);
+  __syncthreads();
+  const int t = blockIdx.x * 256 + threadIdx.x;   // < LS_THREADS
+  constexpr int KC = N <= 2 ? 64 : 32;             // K handled in register chunks (N KC partials per thread)
+  for (int c0 = 0; c0 < K; c0 += KC) {
+    const int kc = min(KC, K - c0);
+    float gw[N][KC], gb[N];
+#pragma unroll
+    for (int o = 0; o < N; ++o) {
+      gb[o] = 0.f;
+#pragma unroll
+      for (int j = 0; j < KC; ++j) gw[o][j] = 0.f;
+    }
+    for (long long m = t; m < M; m += LS_THREADS) {
+      float d[N];
+#pragma unroll
+      for (int o = 0; o < N; ++o) { d[o] = to_f32(dy[m * N + o]); gb[o] += d[o]; }
+      const bf16* xr = x + m * ldx + c0;
+#pragma unroll
+      for (int c = 0; c < KC; c += 8) {
+        if (c >= kc) break;
+        const bf16x8 v = *(const bf16x8*)(xr + c);
+        bf16x8 o8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float s = 0.f;
+#pragma unroll
+          for (int o = 0; o < N; ++o) {
+            gw[o][c + j] += d[o] * to_f32(v[j]);
+            s += d[o] * sw[o * K + c0 + c + j];
+          }
+          o8[j] = to_bf16(s);
+        }
+        if (dx) *(bf16x8*)(dx + m * K + c0 + c) = o8;
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < N; ++o)
+#pragma unroll
+      for (int j = 0; j < KC; ++j)
+        if (j < kc) part[(long long)(o * K + c0 + j) * LS_THREADS + t] = gw[o][j];
+    if (c0 == 0) {
+#pragma unroll
+      for (int o = 0; o < N; ++o) part[(long long)(N * K + o) * LS_THREADS + t] = gb[o];
+    }
+  }
+}
+
 }  // namespace lci
 
 using namespace lci;
@@ -540,4 +628,35 @@ extern "C" int lci_linear_fwd(int epilogue, const void* x, long long ldx, const 
   if (epilogue == LF_GELU) return lf_dispatch<LF_GELU>(a, st);
   if (epilogue == LF_DGELU) return lf_dispatch<LF_DGELU>(a, st);
   return lf_dispatch<LF_PLAIN>(a, st);
+}
+
+extern "C" int lci_linear_small_threads(void) { return LS_THREADS; }
+
+extern "C" int lci_linear_small_fwd(const void* x, long long ldx, const void* w, const void* bias, void* y,
+                                    long long M, int N, int K, void* stream) {
+  LCI_CHECK(M > 0 && N >= 1 && N <= LS_MAXN && K > 0 && K <= LS_MAXK && K % 8 == 0 && ldx % 8 == 0 && ldx >= K,
+            "linear_small_fwd: unsupported shape M = %lld, N = %d, K = %d", M, N, K);
+  LCI_CHECK(((uintptr_t)x & 15) == 0, "linear_small_fwd: misaligned x");
+  const long long blocks = std::min((M + 255) / 256, 8192LL);
+  hipLaunchKernelGGL(linear_small_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16*)x, ldx, (const bf16*)w, (const bf16*)bias, (bf16*)y, M, N, K);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int lci_linear_small_bwd(const void* x, long long ldx, const void* w, const void* dy, void* dx,
+                                    float* part, long long M, int N, int K, void* stream) {
+  LCI_CHECK(M > 0 && N >= 1 && N <= 4 && K > 0 && K <= LS_MAXK && K % 8 == 0 && ldx % 8 == 0 && ldx >= K,
+            "linear_small_bwd: unsupported shape M = %lld, N = %d, K = %d", M, N, K);
+  LCI_CHECK(((uintptr_t)x & 15) == 0 && ((uintptr_t)dx & 15) == 0, "linear_small_bwd: misaligned x / dx");
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 g(LS_THREADS / 256), blk(256);
+  const bf16 *xp = (const bf16*)x, *wp = (const bf16*)w, *dyp = (const bf16*)dy;
+  bf16* dxp = (bf16*)dx;
+  if (N == 1) hipLaunchKernelGGL(linear_small_bwd_kernel<1>, g, blk, 0, st, xp, ldx, wp, dyp, dxp, part, M, K);
+  else if (N == 2) hipLaunchKernelGGL(linear_small_bwd_kernel<2>, g, blk, 0, st, xp, ldx, wp, dyp, dxp, part, M, K);
+  else if (N == 3) hipLaunchKernelGGL(linear_small_bwd_kernel<3>, g, blk, 0, st, xp, ldx, wp, dyp, dxp, part, M, K);
+  else hipLaunchKernelGGL(linear_small_bwd_kernel<4>, g, blk, 0, st, xp, ldx, wp, dyp, dxp, part, M, K);
+  LCI_LAUNCH_CHECK();
+  return 0;
 }

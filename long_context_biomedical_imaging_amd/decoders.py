@@ -50,8 +50,20 @@ class Conv3x3_2d(nn.Conv2d):
 
 
 def _pointwise(x, weight, bias):
-    """1x1 conv as a GEMM over channels-last voxels; result (B, Cout, *S) with channels-last strides."""
-    y = F.linear(x.movedim(1, -1), weight.reshape(weight.shape[0], weight.shape[1]), bias)
+    """1x1 conv as a GEMM over channels-last voxels; result (B, Cout, *S) with channels-last strides. Narrow outputs
+    (the heads' Conv to 1-4 classes / channels) under bf16 autocast run on lci_linear_small_* (kernels.pointwise_small):
+    a 2-column GEMM is a pure stream that hipBLASLt runs with tiny tiles far below the HBM rate."""
+    xl = x.movedim(1, -1)
+    Cout, Cin = weight.shape[0], weight.shape[1]
+    if (x.is_cuda and Cout <= 4 and torch.is_autocast_enabled("cuda")
+            and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+        x2 = xl.to(torch.bfloat16).reshape(-1, Cin)
+        if kernels.pointwise_small_supported(x2, Cout):
+            y = kernels.pointwise_small(x2, weight, bias)
+            return y.view(*xl.shape[:-1], Cout).movedim(-1, 1)
+    if x.is_cuda:   # hipBLASLt forward / data gradient, HIP weight gradient (kernels.linear, as TokenLinear)
+        return kernels.linear(xl, weight.reshape(Cout, Cin), bias).movedim(-1, 1)
+    y = F.linear(xl, weight.reshape(Cout, Cin), bias)
     return y.movedim(-1, 1)
 
 

@@ -1013,10 +1013,14 @@ class _Linear(torch.autograd.Function):
             dx = (dy2 @ wc).view(*dy.shape[:-1], K)
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             x2 = xc.reshape(-1, K)
+            if K % 8 and x2.dtype == torch.bfloat16 and x2.is_cuda:
+                # few input channels (the 1-channel image into a head's 1x1 residual conv): zero-pad to 8 columns
+                x2 = torch.nn.functional.pad(x2, (0, 8 - K % 8))
             if linear_wgrad_supported(dy2, x2):
                 dw, db = linear_wgrad(dy2, x2, ctx.has_bias)
+                dw = dw[:, :K]
             else:
-                dw = (dy2.t() @ x2).float()
+                dw = (dy2.t() @ x2).float()[:, :K]
                 db = dy2.float().sum(0) if ctx.has_bias else None
         return dx, dw, db
 
@@ -1093,3 +1097,49 @@ def mlp_supported(x: torch.Tensor, D: int, H: int) -> bool:
 
 def mlp(x, w1, b1, w2, b2):
     return _MLP.apply(x, w1, b1, w2, b2)
+
+
+def pointwise_small_supported(x2: torch.Tensor, N: int) -> bool:
+    """lci_linear_small_*: x2 (M, K) bf16 CUDA rows (unit column stride, 16-B aligned), N <= 4, K % 8, K <= 256."""
+    K = x2.shape[1]
+    return (x2.is_cuda and x2.dtype == torch.bfloat16 and 1 <= N <= 4 and K % 8 == 0 and K <= 256
+            and x2.stride(1) == 1 and x2.stride(0) % 8 == 0 and x2.data_ptr() % 16 == 0 and x2.shape[0] > 0)
+
+
+class _PointwiseSmall(torch.autograd.Function):
+    """x2 (M, K) bf16 . w^T + b for N <= 4 output channels (autocast casts done here, as F.linear would)."""
+
+    @staticmethod
+    def forward(ctx, x2, weight, bias):
+        M, K = x2.shape
+        N = weight.shape[0]
+        wc = weight.reshape(N, K).to(torch.bfloat16).contiguous()
+        bc = bias.to(torch.bfloat16) if bias is not None else None
+        y = torch.empty(M, N, device=x2.device, dtype=torch.bfloat16)
+        KernelTimer.run("pointwise_small_fwd", 0, x2, lambda: _lib.call(
+            "lci_linear_small_fwd", x2.data_ptr(), x2.stride(0), wc.data_ptr(), _lib.ptr(bc), y.data_ptr(), M, N, K,
+            _lib.stream_of(x2)))
+        ctx.save_for_backward(x2, wc)
+        ctx.has_bias, ctx.wshape = bias is not None, weight.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, wc = ctx.saved_tensors
+        M, K = x2.shape
+        N = wc.shape[0]
+        dy = dy.to(torch.bfloat16).contiguous()
+        nt = _lib.load().lci_linear_small_threads()
+        part = torch.empty(N * K + N, nt, device=x2.device, dtype=torch.float32)
+        dx = torch.empty(M, K, device=x2.device, dtype=torch.bfloat16) if ctx.needs_input_grad[0] else None
+        KernelTimer.run("pointwise_small_bwd", 0, x2, lambda: _lib.call(
+            "lci_linear_small_bwd", x2.data_ptr(), x2.stride(0), wc.data_ptr(), dy.data_ptr(), _lib.ptr(dx),
+            part.data_ptr(), M, N, K, _lib.stream_of(x2)))
+        g = part.sum(1)
+        dw = g[:N * K].view(N, K).reshape(ctx.wshape)
+        db = g[N * K:] if ctx.has_bias else None
+        return dx, dw, db
+
+
+def pointwise_small(x2: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None) -> torch.Tensor:
+    return _PointwiseSmall.apply(x2, weight, bias)

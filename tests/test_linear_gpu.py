@@ -147,3 +147,49 @@ def test_mlp_block_fused_matches_module_path(D, H, M):
     for n, a, b in zip(names, res[0], res[1]):
         e = ((a.double() - b.double()).norm() / b.double().norm()).item()
         assert e < 1e-2, f"{n}: rel-L2 {e:.3e}"
+
+
+@pytest.mark.parametrize("M,N,K", [(2 * 64 ** 3, 2, 48), (524288, 2, 16), (1000, 1, 24), (777, 4, 256), (99, 3, 64)])
+def test_pointwise_small_vs_autocast_linear(M, N, K):
+    """The UNETR heads' 1x1 conv to N <= 4 channels (decoders._pointwise) vs F.linear under bf16 autocast."""
+    from long_context_biomedical_imaging_amd import kernels
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    x = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", generator=g) * K ** -0.5
+    b = torch.randn(N, device="cuda", generator=g)
+    gy = torch.randn(M, N, device="cuda", generator=g).to(torch.bfloat16)
+    outs = []
+    for hip in (True, False):
+        xi, wi, bi = x.clone().requires_grad_(True), w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = kernels.pointwise_small(xi, wi, bi) if hip else torch.nn.functional.linear(xi, wi, bi)
+        y.backward(gy)
+        outs.append((y.detach(), xi.grad, wi.grad, bi.grad))
+    for name, a, r in zip(("y", "dx", "dW", "db"), outs[0], outs[1]):
+        assert a.dtype == r.dtype and a.shape == r.shape, name
+        e = ((a.double() - r.double()).norm() / r.double().norm()).item()
+        assert e < 5e-3, f"{name}: rel-L2 {e:.3e}"   # bf16 outputs / dW, db rounded to bf16 by the reference
+
+
+@pytest.mark.parametrize("Cin,Cout", [(1, 96), (192, 96), (3, 32)])
+def test_decoder_pointwise_conv_grads(Cin, Cout):
+    """decoders.Conv1x1 (UnetResBlock's 1x1 residual conv) on kernels.linear: forward and input gradient equal to
+    the same 1x1 conv as F.linear under autocast (torch's GEMMs), weight / bias gradients within its bf16 rounding (incl. Cin = 1, zero-padded to 8 for
+    the HIP weight gradient)."""
+    from long_context_biomedical_imaging_amd import decoders
+    torch.manual_seed(Cin)
+    conv = decoders.Conv1x1(Cin, Cout, 1, 1, bias=True).cuda()
+    x = torch.randn(1, Cin, 24, 20, 16, device="cuda").to(memory_format=torch.channels_last_3d)
+    outs = []
+    for hip in (True, False):
+        conv.zero_grad()
+        xi = x.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = conv(xi) if hip else torch.nn.functional.linear(
+                xi.movedim(1, -1), conv.weight.reshape(Cout, Cin), conv.bias).movedim(-1, 1)
+        gy = torch.randn(y.shape, device="cuda", generator=torch.Generator(device="cuda").manual_seed(5)).to(y.dtype)
+        y.backward(gy)
+        outs.append((y.detach().float(), xi.grad.float(), conv.weight.grad.clone(), conv.bias.grad.clone()))
+    for name, a, r in zip(("y", "dx", "dW", "db"), outs[0], outs[1]):
+        e = ((a.double() - r.double()).norm() / r.double().norm()).item()
+        assert e < 1e-2, f"{name}: rel-L2 {e:.3e}"
