@@ -222,8 +222,8 @@ int lci_linear_wgrad(const void* dy, long long ldy, const void* x, long long ldx
  *   epilogue 1: aux = pre = bf16(acc + bias), y = bf16(gelu(pre))    (MLPBlock linear1 + GELU, exact erf)
  *   epilogue 2: y = bf16(bf16(acc) * gelu'(aux))  (linear2's data gradient through GELU; aux = saved pre)
  * The data gradient of a Linear is the same call with the transposed weight. Supported when
- * lci_linear_fwd_supported(N, K): N % 128 == 0 or N % 96 == 0, K % 8 == 0; ldx % 8, ldy / ldaux % 4 == 0,
- * x / w 16-byte aligned, y / aux / bias 8-byte aligned. */
+ * lci_linear_fwd_supported(N, K): N % 128 == 0 or N % 96 == 0, K % 8 == 0; row strides % 8 == 0,
+ * x / w / y / aux 16-byte aligned, bias 8-byte aligned. */
 int lci_linear_fwd_supported(int N, int K);
 /* Narrow outputs (the UNETR heads' 1x1 conv to 1-8 channels, over channels-last voxel rows): y (M, N) bf16 =
  * x (M, ldx) . w^T + bias, w (N, K) bf16, bias (N) bf16 or null; N <= 8, K <= 256, K % 8 == 0.

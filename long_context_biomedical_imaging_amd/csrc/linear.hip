@@ -402,46 +402,55 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void linear_fwd_kernel(LinFwdArgs 
         for (int j = 0; j < MB; ++j) acc[i][j] = mfma32(fw[i], fx[j], acc[i][j]);
     }
   }
-  // acc[i][j] reg e: feature n0 + 32 (NB wn + i) + (e&3) + 8(e>>2) + 4h, token m0 + 32 (MB wm + j) + (lane & 31)
+  // Epilogue through LDS: the accumulators (+ bias, rounded to bf16: the pre-activation for LF_GELU, the bf16 GEMM
+  // output for LF_DGELU) go to a [TM][TN + 8] tile in the freed ring, then the workgroup streams whole rows: every
+  // global access (y, and aux for the GELU forms) is a 16-B piece of a contiguous 2 TN-byte row segment.
+  // acc[i][j] reg e: feature 32 (NB wn + i) + (e&3) + 8(e>>2) + 4h, token 32 (MB wm + j) + (lane & 31) of the tile
+  constexpr int TLD = TN + 8;
+  static_assert(TM * TLD <= NBUF * SLOT, "epilogue tile must fit the ring");
+  __syncthreads();   // every wave is done reading the ring
+  bf16* tile = lsm;
 #pragma unroll
-  for (int j = 0; j < MB; ++j) {
-    const long long m = m0 + 32 * (MB * wm + j) + r;
-    if (m >= a.M) continue;
+  for (int j = 0; j < MB; ++j)
 #pragma unroll
     for (int i = 0; i < NB; ++i)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int n = n0 + 32 * (NB * wn + i) + 8 * g + 4 * h;
-        if (n >= a.N) continue;
+        const int nl = 32 * (NB * wn + i) + 8 * g + 4 * h;
         float v[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = acc[i][j][4 * g + q];
-        bf16x4 o;
-        if constexpr (EPI == LF_DGELU) {
-          const bf16x4 p = *(const bf16x4*)(a.aux + m * a.ldaux + n);
+        if (EPI != LF_DGELU && a.bias && n0 + nl < a.N) {
+          const bf16x4 bb = *(const bf16x4*)(a.bias + n0 + nl);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) o[q] = to_bf16(to_f32(to_bf16(v[q])) * gelu_erf_grad(to_f32(p[q])));
-        } else {
-          if (a.bias) {
-            const bf16x4 b = *(const bf16x4*)(a.bias + n);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) v[q] += to_f32(b[q]);
-          }
-          if constexpr (EPI == LF_GELU) {
-            bf16x4 pre;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              pre[q] = to_bf16(v[q]);
-              o[q] = to_bf16(gelu_erf(to_f32(pre[q])));
-            }
-            *(bf16x4*)(a.aux + m * a.ldaux + n) = pre;
-          } else {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) o[q] = to_bf16(v[q]);
-          }
+          for (int q = 0; q < 4; ++q) v[q] += to_f32(bb[q]);
         }
-        *(bf16x4*)(a.y + m * a.ldy + n) = o;
+        bf16x4 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = to_bf16(v[q]);
+        *(bf16x4*)(tile + (32 * (MB * wm + j) + r) * TLD + nl) = o;
       }
+  __syncthreads();
+  constexpr int CPR = TN / 8;                       // 16-B chunks per tile row
+  for (int c = threadIdx.x; c < TM * CPR; c += 64 * NW) {
+    const int row = c / CPR, col = 8 * (c - row * CPR);
+    const long long m = m0 + row;
+    const int n = n0 + col;
+    if (m >= a.M || n >= a.N) continue;
+    const bf16x8 t = *(const bf16x8*)(tile + row * TLD + col);
+    bf16x8 o;
+    if constexpr (EPI == LF_PLAIN) {
+      o = t;
+    } else if constexpr (EPI == LF_GELU) {
+      *(bf16x8*)(a.aux + m * a.ldaux + n) = t;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] = to_bf16(gelu_erf(to_f32(t[q])));
+    } else {
+      const bf16x8 p = *(const bf16x8*)(a.aux + m * a.ldaux + n);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] = to_bf16(to_f32(t[q]) * gelu_erf_grad(to_f32(p[q])));
+    }
+    *(bf16x8*)(a.y + m * a.ldy + n) = o;
   }
 }
 
@@ -617,10 +626,10 @@ extern "C" int lci_linear_fwd(int epilogue, const void* x, long long ldx, const 
                               long long ldy, void* aux, long long ldaux, long long M, int N, int K, void* stream) {
   LCI_CHECK(M > 0 && lci_linear_fwd_supported(N, K), "linear_fwd: unsupported shape N = %d, K = %d", N, K);
   LCI_CHECK(epilogue >= LF_PLAIN && epilogue <= LF_DGELU, "linear_fwd: bad epilogue %d", epilogue);
-  LCI_CHECK(ldx % 8 == 0 && ldy % 4 == 0 && ldx >= K && ldy >= N && (epilogue == LF_PLAIN || (aux && ldaux % 4 == 0)),
+  LCI_CHECK(ldx % 8 == 0 && ldy % 8 == 0 && ldx >= K && ldy >= N && (epilogue == LF_PLAIN || (aux && ldaux % 8 == 0)),
             "linear_fwd: bad row strides");
-  LCI_CHECK(((uintptr_t)x & 15) == 0 && ((uintptr_t)w & 15) == 0 && ((uintptr_t)y & 7) == 0 &&
-            ((uintptr_t)aux & 7) == 0 && ((uintptr_t)bias & 7) == 0, "linear_fwd: misaligned pointers");
+  LCI_CHECK(((uintptr_t)x & 15) == 0 && ((uintptr_t)w & 15) == 0 && ((uintptr_t)y & 15) == 0 &&
+            ((uintptr_t)aux & 15) == 0 && ((uintptr_t)bias & 7) == 0, "linear_fwd: misaligned pointers");
   LinFwdArgs a{};
   a.x = (const bf16*)x; a.w = (const bf16*)w; a.bias = (const bf16*)bias; a.y = (bf16*)y; a.aux = (bf16*)aux;
   a.M = M; a.ldx = ldx; a.ldy = ldy; a.ldaux = ldaux; a.N = N; a.K = K;

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--ckpt", type=int, default=0)
     ap.add_argument("--rows", type=int, default=45)
+    ap.add_argument("--stack", default="", help="comma-separated op names: print their time grouped by Python stack")
     args = ap.parse_args()
     extra = []
     if args.size:
@@ -42,12 +43,20 @@ def main():
         ts.step(x, y)
     torch.cuda.synchronize()
     from torch.profiler import ProfilerActivity, profile
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True,
+                 with_stack=bool(args.stack)) as prof:
         ts.step(x, y)
         torch.cuda.synchronize()
     ka = prof.key_averages(group_by_input_shape=True)
     print(ka.table(sort_by="self_cuda_time_total", row_limit=args.rows, max_name_column_width=40,
                    max_shapes_column_width=90))
+    if args.stack:
+        want = set(args.stack.split(","))
+        for e in sorted(prof.key_averages(group_by_stack_n=6), key=lambda e: -e.self_device_time_total):
+            if e.key in want and e.self_device_time_total > 0:
+                print(f"{e.key} {e.self_device_time_total / 1e3:.2f} ms x{e.count}")
+                for fr in e.stack[:6]:
+                    print("     ", fr)
 
 
 if __name__ == "__main__":
