@@ -141,6 +141,8 @@ def bench_patch_embed():
 def bench_linear():
     """Linear weight gradient dW = dY^T X (+ db) at the ViT (M = 131072) and C5 (M = 2^21) token counts: the HIP
     split-token kernel vs torch's hipBLASLt GEMM of the same bf16 operands."""
+    from long_context_biomedical_imaging_amd.trainer import use_tuned_gemms
+    print(json.dumps({"tuned_gemm_table": use_tuned_gemms()}), flush=True)   # torch's side as the product runs it
     shapes = {"qkv": (1152, 384), "proj": (384, 384), "fc1": (1536, 384), "fc2": (384, 1536),
               "m_x": (40, 192), "m_dt": (192, 24), "swin_qkv96": (288, 96), "swin_fc2_96": (96, 384)}
     for M in (131072, 1 << 21):
