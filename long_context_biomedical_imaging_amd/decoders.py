@@ -49,6 +49,9 @@ class Conv3x3_2d(nn.Conv2d):
         return kernels.conv3(x, self.weight)
 
 
+_CL = {2: torch.channels_last, 3: torch.channels_last_3d}   # dense channels-last layout per spatial rank
+
+
 def _pointwise(x, weight, bias):
     """1x1 conv as a GEMM over channels-last voxels; result (B, Cout, *S) with channels-last strides. Narrow outputs
     (the heads' Conv to 1-4 classes / channels) under bf16 autocast run on lci_linear_small_* (kernels.pointwise_small):
@@ -299,7 +302,10 @@ class ViTUNETR(nn.Module):
         self.proj_view_shape = list(self.feat_size) + [hidden]
 
     def proj_feat(self, x):
-        return x.view([x.size(0)] + self.proj_view_shape).permute(self.proj_axes).contiguous()
+        # the (B, L, C) tokens are already the channels-last (B, *S, C) volume: return the (B, C, *S) permuted view
+        # (channels-last strides, which the HIP convs consume in place) instead of the reference's NCDHW copy
+        return x.view([x.size(0)] + self.proj_view_shape).permute(self.proj_axes).contiguous(
+            memory_format=_CL[self.spatial_dims])
 
     def forward(self, input_data):
         x_in = input_data[0]
@@ -492,7 +498,7 @@ class _UperNet(nn.Module):
 
     def _reshape_vit_output(self, x):
         x = x.view([x.size(0)] + list(self.feat_size) + [x.shape[-1]])
-        return x.permute(self.proj_axes).contiguous()
+        return x.permute(self.proj_axes).contiguous()   # NCHW: UperNet's BatchNorm / pooling / interpolation paths
 
     def freeze_bn(self):
         for module in self.modules():
