@@ -193,3 +193,38 @@ def test_decoder_pointwise_conv_grads(Cin, Cout):
     for name, a, r in zip(("y", "dx", "dW", "db"), outs[0], outs[1]):
         e = ((a.double() - r.double()).norm() / r.double().norm()).item()
         assert e < 1e-2, f"{name}: rel-L2 {e:.3e}"
+
+
+@pytest.mark.parametrize("nd,Cin,Cout,k", [(3, 96, 64, (2, 2, 2)), (3, 384, 128, (2, 2, 2)), (2, 64, 32, (2, 2))])
+def test_conv_up_gemm_grads(nd, Cin, Cout, k):
+    """decoders.ConvUp (kernel == stride transposed conv as one GEMM on kernels.linear, tap-major columns, bias in
+    the GEMM) under bf16 autocast vs the fp32 transposed convolution on the same (bf16-representable) data."""
+    from long_context_biomedical_imaging_amd import decoders
+    torch.manual_seed(Cin + Cout)
+    ct = (torch.nn.ConvTranspose3d if nd == 3 else torch.nn.ConvTranspose2d)(Cin, Cout, k, k, bias=True).cuda()
+    with torch.no_grad():
+        ct.weight.copy_(ct.weight.to(torch.bfloat16).float())
+        ct.bias.copy_(ct.bias.to(torch.bfloat16).float())
+    shape = (1, Cin, 10, 12, 6) if nd == 3 else (2, Cin, 20, 14)
+    mf = torch.channels_last_3d if nd == 3 else torch.channels_last
+    x = torch.randn(shape, device="cuda").to(torch.bfloat16).float().to(memory_format=mf)
+    gshape = (shape[0], Cout) + tuple(s * kk for s, kk in zip(shape[2:], k))
+    gy = torch.randn(gshape, device="cuda").to(torch.bfloat16)
+    res = []
+    for hip in (True, False):
+        ct.zero_grad()
+        xi = x.clone().requires_grad_(True)
+        if hip:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = decoders._up_gemm(xi, ct.weight, ct.bias, k)
+            y.backward(gy)
+        else:   # fp32 reference: the same math as torch's transposed conv (tests/test_conv_cpu.py pins it to it)
+            w2 = ct.weight.reshape(Cin, -1)
+            yy = (xi.movedim(1, -1).reshape(-1, Cin) @ w2).view(shape[0], *shape[2:], Cout, *k)
+            yy = yy.permute(0, 1, 5, 2, 6, 3, 7, 4) if nd == 3 else yy.permute(0, 1, 4, 2, 5, 3)
+            y = (yy.reshape(shape[0], *gshape[2:], Cout) + ct.bias).movedim(-1, 1)
+            y.backward(gy.float())
+        res.append((y.detach().float(), xi.grad.float(), ct.weight.grad.clone(), ct.bias.grad.clone()))
+    for name, a, r in zip(("y", "dx", "dW", "db"), res[0], res[1]):
+        e = ((a.double() - r.double()).norm() / r.double().norm()).item()
+        assert e < 1e-2, f"{name}: rel-L2 {e:.3e}"
