@@ -19,6 +19,8 @@
  *   lci_dwconv_silu_*     MambaVisionMixer depthwise conv1d + SiLU, model/models/mamba.py:118-119
  *   lci_fftconv_*         fftconv_ref (gelu=False), model/models/hyena.py:32-51 / Filter.forward :201-216
  *   lci_hyena_pre/post_*  HyenaOperator short filter + gating, model/models/hyena.py:317-355
+ *   lci_hyena_filter_*    Filter.filter (implicit-filter MLP z -> Linear/Sin x3 -> Linear, ExponentialModulation),
+ *                         model/models/hyena.py:54-117,190-199, called at :343
  *   lci_conv3_fwd         MONAI-1.3 UnetResBlock 3x3(x3) convs of the ViTUNETR / SwinUNETR heads, enhance_heads.py:30-356
  *   lci_inorm_*           MONAI-1.3 UnetResBlock InstanceNorm (+ LeakyReLU) of the same heads
  *   lci_patch_embed_*     MONAI-1.3 PatchEmbeddingBlock (backbone_vit.py:351-361) / PatchEmbed (backbone_swin.py:800-806)
@@ -38,8 +40,9 @@ extern "C" {
 #endif
 
 /* Bumped whenever an entry point's argument list or buffer contract changes (3: lci_layernorm_bwd gained dres;
- * 4: lci_conv3_wgrad writes one partial per voxel split instead of one per split and wave; 5: lci_linear_wgrad). */
-#define LCI_ABI_VERSION 5
+ * 4: lci_conv3_wgrad writes one partial per voxel split instead of one per split and wave; 5: lci_linear_wgrad;
+ * 6: lci_hyena_filter). */
+#define LCI_ABI_VERSION 6
 const char* lci_last_error(void);
 int lci_abi_version(void);
 /* sha256 prefix of the sources the library was built from (build_lib.source_hash); the Python binding refuses a
@@ -180,6 +183,25 @@ int lci_hyena_post_bwd(int dtype, const float* y, const void* x2, const void* do
 int lci_hyena_pre_bwd(int dtype, const void* z, const float* w, const float* bias, const float* dvg,
                       const float* gx2, void* dz, float* dw, float* db, int BB, int L, int H, int hd, int K,
                       void* stream);
+
+/* ------------------------------------------------------------------ Hyena implicit filter (order = D = 64)
+ * prep: the f32 parameters W1 (64, E), b1, freq (64), W2, b2, W3, b3 (64x64, 64), W4 (64, 64), deltas (64) ->
+ * img (lci_hyena_filter_img_elems() bf16, 16-B aligned: MFMA weight fragments) and vec (320 f32).
+ * fwd: z (L, E) f32 rows, t (L) f32 -> k (64, L) f32 = modulated filter, bf16-autocast rounding.
+ * bwd: dk (64, L) f32 -> dh, s3, da3, s2, da2, s1 (L, 64) bf16 with permuted feature columns (feature of column c:
+ * 32(c>>4>>1) + 16((c>>4)&1) + 8((c&7)>>2) + 4((c>>3)&1) + (c&3)) for the three 64x64 weight gradients,
+ * dz (L, E) f32 (written), part (lci_hyena_filter_partials(L, E) f32: per-wave [2 + E][64] sums of
+ * db1, dfreq, dW1[:, e] over positions, indexed by feature; the caller sums them). 1 <= E <= 8. */
+long long lci_hyena_filter_img_elems(void);
+long long lci_hyena_filter_partials(int L, int E);
+int lci_hyena_filter_prep(const float* W1, const float* b1, const float* freq, const float* W2, const float* b2,
+                          const float* W3, const float* b3, const float* W4, const float* deltas, int E, void* img,
+                          float* vec, void* stream);
+int lci_hyena_filter_fwd(const float* z, const float* t, const void* img, const float* vec, int E, int L, float shift,
+                         float* k, void* stream);
+int lci_hyena_filter_bwd(const float* z, const float* t, const void* img, const float* vec, int E, int L, float shift,
+                         const float* dk, void* dh, void* s3, void* da3, void* s2, void* da2, void* s1, float* dz,
+                         float* part, void* stream);
 
 /* ------------------------------------------------------------------ patch embedding (conv, k = stride = p)
  * x (B, C, S0, S1[, S2]) (dtype x_dtype), w (D, C*prod(p)) f32, bias (D) / pos (L, D) f32 or null;

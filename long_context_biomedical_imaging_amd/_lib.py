@@ -14,7 +14,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_LIB = os.path.join(HERE, "liblci.so")
 LIB_PATH = os.environ.get("LCI_LIB_PATH", DEFAULT_LIB)   # override: kernel-variant A/B runs (no staleness check)
-ABI_VERSION = 5   # include/lci.h LCI_ABI_VERSION
+ABI_VERSION = 6   # include/lci.h LCI_ABI_VERSION
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -55,6 +55,9 @@ SIGNATURES = {
     "lci_linear_fwd": [_I, _P, _L, _P, _P, _P, _L, _P, _L, _L, _I, _I, _P],
     "lci_linear_small_fwd": [_P, _L, _P, _P, _P, _L, _I, _I, _P],
     "lci_linear_small_bwd": [_P, _L, _P, _P, _P, _P, _L, _I, _I, _P],
+    "lci_hyena_filter_prep": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P],
+    "lci_hyena_filter_fwd": [_P, _P, _P, _P, _I, _I, _F, _P, _P],
+    "lci_hyena_filter_bwd": [_P, _P, _P, _P, _I, _I, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
 }
 
 _lib = None
@@ -103,6 +106,10 @@ def load(path: str = LIB_PATH):
     lib.lci_inorm_chunks.argtypes = [ctypes.c_longlong, _I]
     lib.lci_layernorm_bwd_blocks.restype = ctypes.c_int
     lib.lci_layernorm_bwd_blocks.argtypes = [ctypes.c_longlong]
+    lib.lci_hyena_filter_img_elems.restype = ctypes.c_longlong
+    lib.lci_hyena_filter_img_elems.argtypes = []
+    lib.lci_hyena_filter_partials.restype = ctypes.c_longlong
+    lib.lci_hyena_filter_partials.argtypes = [_I, _I]
     lib.lci_fft_size.restype = ctypes.c_longlong
     lib.lci_fft_size.argtypes = [_I]
     for name, argt in SIGNATURES.items():

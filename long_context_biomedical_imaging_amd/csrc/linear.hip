@@ -231,8 +231,9 @@ struct LwTile { int mb, cb, wn, wc; };
 // 128 x 384 as 4 waves of 128 x 96 (one wave per SIMD, 12 accumulators: 7 LDS fragments per 12 MFMAs),
 // 128 x 384 as 6 waves of 64 x 128 (6 fragments per 8 MFMAs), 128 x 192 (6 waves), 128 x 128 (4),
 // 64 x 192 (3: x_proj 40 x 192), 192 x 32 (3: dt_proj 192 x 24), 96 x 96 (3: Swin C = 96 projections)
+// The last tile (64 x 64, the Hyena filter's layers) is only taken when no other tile fits within 2x padding.
 static const LwTile kLwTiles[] = {{4, 3, 1, 4}, {2, 4, 2, 3}, {2, 2, 2, 3}, {2, 2, 2, 2},
-                                  {2, 2, 1, 3}, {2, 1, 3, 1}, {1, 3, 3, 1}};
+                                  {2, 2, 1, 3}, {2, 1, 3, 1}, {1, 3, 3, 1}, {1, 1, 2, 2}};
 constexpr int kLwNTiles = (int)(sizeof(kLwTiles) / sizeof(kLwTiles[0]));
 
 // The first tile with the least padded work (LCI_LW_TILE=i forces tile i for A/B runs); -1 if every tile more than
@@ -247,6 +248,7 @@ static int lw_pick(int N, int K) {
     const double padded = (double)((N + tn - 1) / tn * tn) * ((K + tk - 1) / tk * tk);
     const double waste = padded / ((double)N * K);
     if (t == force && waste <= 2.0) return t;
+    if (t == kLwNTiles - 1 && best >= 0) break;
     if (waste <= 2.0 && (best < 0 || waste < bw - 1e-9)) { best = t; bw = waste; }
   }
   return best;
@@ -615,6 +617,7 @@ extern "C" int lci_linear_wgrad(const void* dy, long long ldy, const void* x, lo
 #define LCI_LW(A, B, C, D) \
   if (c.mb == A && c.cb == B && c.wn == C && c.wc == D) return launch_lw<A, B, C, D>(a, st);
   LCI_LW(4, 3, 1, 4) LCI_LW(2, 4, 2, 3) LCI_LW(2, 2, 2, 3) LCI_LW(2, 2, 2, 2) LCI_LW(2, 2, 1, 3) LCI_LW(2, 1, 3, 1) LCI_LW(1, 3, 3, 1)
+  LCI_LW(1, 1, 2, 2)
 #undef LCI_LW
   LCI_CHECK(false, "linear_wgrad: tile not instantiated");
   return 1;

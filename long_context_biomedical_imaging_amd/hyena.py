@@ -8,7 +8,7 @@ Forward data flow (HIP kernels in kernels.hyena_*):
   in_proj (B, L, 3D) channels-last
   -> hyena_pre: causal depthwise conv k=short_filter_order over L + pre-gate v*x1, written channel-major
      f32 for the long convolution, plus x2 (post-gate operand)
-  -> implicit filter k (64, L) (small MLP, torch)
+  -> implicit filter k (64, L): kernels.hyena_filter (MLP + sin + modulation fused, bf16-autocast numerics)
   -> hyena_fftconv: y = causal_conv(v*x1, k) + D (v*x1), times x2, written channels-last for out_proj.
 The reference's causal long conv (fftconv_ref, n = 2L FFT) is evaluated exactly as a linear convolution
 (block-partitioned FFT on the GPU), bidirectional stays False as in the reference (the `bidrectional`
@@ -17,6 +17,7 @@ kwarg is swallowed by **filter_args, backbone_vit.py:177).
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -123,10 +124,44 @@ class Filter(OptimModule):
             h = h / torch.norm(h, dim=-1, p=1, keepdim=True)
         return h
 
+    def fused_filter_ok(self, L) -> bool:
+        """Whether filter_k(L) runs the fused HIP implicit filter: the reference's default MLP (emb_dim <= 8,
+        order = d_model = 64, num_inner_mlps = 2, one shared trainable Sin), modulation on with fixed deltas, no
+        normalisation, on the GPU under bf16 autocast (LCI_FUSED_FILTER=0 turns it off)."""
+        f = self.implicit_filter
+        z = self.pos_emb.z
+        if os.environ.get("LCI_FUSED_FILTER", "1") == "0" or not z.is_cuda:
+            return False
+        if not (torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+            return False
+        if len(f) != 7 or self.d_model != 64 or not self.modulate or self.normalized or L > z.shape[1]:
+            return False
+        lins, acts = [f[i] for i in (0, 2, 4, 6)], [f[i] for i in (1, 3, 5)]
+        if not all(isinstance(m, nn.Linear) for m in lins) or not all(a is acts[0] for a in acts):
+            return False
+        if not isinstance(acts[0], Sin) or not isinstance(acts[0].freq, nn.Parameter):
+            return False
+        shapes = [tuple(m.weight.shape) for m in lins]
+        if shapes != [(64, self.emb_dim), (64, 64), (64, 64), (64, 64)] or self.emb_dim > 8:
+            return False
+        if lins[3].bias is not None or any(m.bias is None for m in lins[:3]):
+            return False
+        return isinstance(self.modulation.deltas, torch.Tensor) and \
+            not isinstance(self.modulation.deltas, nn.Parameter)
+
+    def filter_k(self, L):
+        """The modulated filter as (d_model, L) = filter(L)[0].transpose(0, 1) (hyena.py:343-345)."""
+        if self.fused_filter_ok(L):
+            f = self.implicit_filter
+            return kernels.hyena_filter(self.pos_emb.z, f[0].weight, f[0].bias, f[1].freq, f[2].weight, f[2].bias,
+                                        f[4].weight, f[4].bias, f[6].weight, self.pos_emb.t, self.modulation.deltas,
+                                        self.modulation.shift, L)
+        return self.filter(L)[0].transpose(0, 1)
+
     def forward(self, x, L, k=None, bias=None, *args, **kwargs):
         """Long convolution of x (B, H, C, L) channel-major with k (C, L) plus bias*x (fftconv_ref)."""
         if k is None:
-            k = self.filter(L)[0].transpose(0, 1)
+            k = self.filter_k(L)
         k = k[0] if type(k) is tuple else k
         if bias is None:
             bias = self.bias
@@ -186,7 +221,7 @@ class HyenaOperator(nn.Module):
             raise NotImplementedError("Hyena dropout > 0 is not fused")
         z = self.in_proj(u)                                                    # (B, L, 3D)
         v, x2 = kernels.hyena_pre(z, self.short_filter.weight, self.short_filter.bias, self.num_heads)
-        k = self.filter_fn.filter(l)[0].transpose(0, 1)                        # (head_dim, L)
+        k = self.filter_fn.filter_k(l)                                         # (head_dim, L)
         bias = self.filter_fn.bias if self.filter_fn.use_bias else 0 * self.filter_fn.bias
         y = kernels.hyena_fftconv_gate(v, k, bias, x2)                         # (B, L, D) channels-last
         y = self.out_proj(y)

@@ -651,6 +651,86 @@ def hyena_fftconv_gate(vg, k, bias, x2):
     return _HyenaPost.apply(y, x2)
 
 
+def _hf_feature_of_column():
+    """Feature index of each permuted column of the filter backward's (L, 64) tensors (include/lci.h)."""
+    c = torch.arange(64)
+    t, h, j = c >> 4, (c >> 3) & 1, c & 7
+    return 32 * (t >> 1) + 16 * (t & 1) + 8 * (j >> 2) + 4 * h + (j & 3)
+
+
+_HF_INV = {}
+
+
+def _hf_inv(device):
+    """inv[f] = permuted column holding feature f."""
+    inv = _HF_INV.get(str(device))
+    if inv is None:
+        inv = torch.argsort(_hf_feature_of_column()).to(device)
+        _HF_INV[str(device)] = inv
+    return inv
+
+
+class _HyenaFilter(torch.autograd.Function):
+    """k (64, L) f32 = Filter.filter(L)[0].T under bf16 autocast (hyena.py:54-117,190-199), fused on the GPU.
+
+    Forward and the data-gradient chain are one HIP kernel each (lci_hyena_filter_fwd / _bwd: MFMA layers, sin,
+    modulation, dz, dfreq, db1, dW1); the three 64x64 weight gradients run on lci_linear_wgrad over the bf16
+    activations / gradients the backward kernel writes. Weight and bias gradients are returned in f32 without
+    autocast's bf16 rounding of the GEMM output (as kernels._Linear does); data gradients keep it.
+    """
+
+    @staticmethod
+    def forward(ctx, z, W1, b1, freq, W2, b2, W3, b3, W4, t, deltas, shift, L):
+        E = z.shape[-1]
+        dev = z.device
+        lib = _lib.load()
+        img = torch.empty(int(lib.lci_hyena_filter_img_elems()), device=dev, dtype=torch.bfloat16)
+        vec = torch.empty(5 * 64, device=dev, dtype=torch.float32)
+        ps = [p.detach().float().contiguous() for p in (W1, b1, freq, W2, b2, W3, b3, W4, deltas)]
+        st = _lib.stream_of(z)
+        _lib.call("lci_hyena_filter_prep", *[p.data_ptr() for p in ps], E, img.data_ptr(), vec.data_ptr(), st)
+        k = torch.empty(64, L, device=dev, dtype=torch.float32)
+        KernelTimer.run("hyena_filter_fwd", 0.0, z, lambda: _lib.call(
+            "lci_hyena_filter_fwd", z.data_ptr(), t.data_ptr(), img.data_ptr(), vec.data_ptr(), E, L, float(shift),
+            k.data_ptr(), st))
+        ctx.save_for_backward(z, t, img, vec)
+        ctx.meta = (float(shift), L)
+        return k
+
+    @staticmethod
+    def backward(ctx, dk):
+        z, t, img, vec = ctx.saved_tensors
+        shift, L = ctx.meta
+        E = z.shape[-1]
+        dev = z.device
+        lib = _lib.load()
+        dk = dk.float().contiguous()
+        bufs = torch.empty(6, L, 64, device=dev, dtype=torch.bfloat16)
+        dh, s3, da3, s2, da2, s1 = bufs.unbind(0)
+        dz = torch.zeros_like(z)
+        part = torch.empty(int(lib.lci_hyena_filter_partials(L, E)), device=dev, dtype=torch.float32)
+        KernelTimer.run("hyena_filter_bwd", 0.0, z, lambda: _lib.call(
+            "lci_hyena_filter_bwd", z.data_ptr(), t.data_ptr(), img.data_ptr(), vec.data_ptr(), E, L, shift,
+            dk.data_ptr(), dh.data_ptr(), s3.data_ptr(), da3.data_ptr(), s2.data_ptr(), da2.data_ptr(),
+            s1.data_ptr(), dz.data_ptr(), part.data_ptr(), _lib.stream_of(z)))
+        sums = part.view(-1, 2 + E, 64).sum(0)
+        inv = _hf_inv(dev)
+        dW4, _ = linear_wgrad(dh, s3, False)
+        dW3, db3 = linear_wgrad(da3, s2, True)
+        dW2, db2 = linear_wgrad(da2, s1, True)
+        unp = lambda w: w[inv][:, inv]   # noqa: E731
+        return (dz, sums[2:].t().contiguous(), sums[0], sums[1].view(1, 64), unp(dW2), db2[inv], unp(dW3),
+                db3[inv], unp(dW4), None, None, None, None)
+
+
+def hyena_filter(z, W1, b1, freq, W2, b2, W3, b3, W4, t, deltas, shift, L):
+    """Modulated implicit filter k (64, L) f32 (Filter.filter(L)[0].transpose(0, 1), hyena.py:190-199) for the
+    default MLP (emb_dim E <= 8, order = d_model = 64, one shared Sin): z (1, >=L, E) f32 parameter rows, t (1, >=L, 1)
+    positions, deltas (1, 1, 64) buffer. bf16-autocast numerics (see _HyenaFilter)."""
+    _lib.require_gpu(z, t)
+    return _HyenaFilter.apply(z, W1, b1, freq, W2, b2, W3, b3, W4, t, deltas, shift, int(L))
+
+
 # ------------------------------------------------------------------- decoder-head 3x3(x3) convolution
 def conv3_cl(x_cl: torch.Tensor, w_packed: torch.Tensor, kd: int) -> torch.Tensor:
     """x_cl (B, D, H, W, Cin) bf16 channels-last, w_packed (Cout, kd*9, Cin) bf16 -> (B, D, H, W, Cout) bf16."""
