@@ -19,6 +19,7 @@
 #include "common.hpp"
 
 #include <algorithm>
+#include <initializer_list>
 #include <cstdlib>
 
 namespace lci {
@@ -998,6 +999,271 @@ static int fft_plan(FftArgs& a, int L) {
   return 0;
 }
 
+
+// ------------------------------------------- short conv + gating, LDS-staged 16-byte global accesses (v3)
+// Same math as the register-ring kernels above; every global access is a 16-byte vector (8 bf16 / 4 f32) of
+// one row: the channels-last rows (z, x2, dz, out, dout, dx2, gx2) and the channel-major f32 rows (vg, dvg, y, dy)
+// are staged through LDS tiles of 64 tokens x 64 output channels, and the per-channel arithmetic reads LDS with
+// lane = channel. The narrow (2-byte-per-lane) global accesses of the v2 kernels held them to 1-3 TB/s.
+// Preconditions (checked by the launcher, else v2 runs): bf16 activations, hd % 8 == 0, D % 8 == 0, L % 4 == 0.
+constexpr int HG_TT = 64;            // tokens per tile
+constexpr int HG_S = HG_TT + 1;      // odd row stride (f32) of the channel-major LDS tiles
+
+__device__ __forceinline__ int hg_zcol(int ch, int g, int hd) {   // z channel of gate g (x1, x2, v) of channel ch
+  const int h = ch / hd;
+  return h * 3 * hd + g * hd + (ch - h * hd);
+}
+
+// ty[r][tl] <- rows (channels ch0 + r) x tokens [t0, t0 + 64) of a channel-major f32 tensor
+__device__ __forceinline__ void hg_stage_cm(float* ty, const float* src, int bb, int ch0, int t0, int D, int L) {
+  for (int i = threadIdx.x; i < 64 * (HG_TT / 4); i += 256) {
+    const int r = i / (HG_TT / 4), c4 = (i - r * (HG_TT / 4)) * 4, ch = ch0 + r, t = t0 + c4;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (ch < D && t < L) v = *(const f32x4*)(src + ((long long)bb * D + ch) * L + t);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ty[r * HG_S + c4 + j] = v[j];
+  }
+}
+
+// dst rows (channel-major) <- ty
+__device__ __forceinline__ void hg_store_cm(float* dst, const float* ty, int bb, int ch0, int t0, int D, int L) {
+  for (int i = threadIdx.x; i < 64 * (HG_TT / 4); i += 256) {
+    const int r = i / (HG_TT / 4), c4 = (i - r * (HG_TT / 4)) * 4, ch = ch0 + r, t = t0 + c4;
+    if (ch >= D || t >= L) continue;
+    f32x4 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = ty[r * HG_S + c4 + j];
+    *(f32x4*)(dst + ((long long)bb * D + ch) * L + t) = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void hyena_post_fwd3_kernel(GateArgs a) {
+  __shared__ float ty[64 * HG_S];
+  const int t0 = blockIdx.x * HG_TT, ch0 = blockIdx.y * 64, bb = blockIdx.z, L = a.L, D = a.D;
+  hg_stage_cm(ty, a.y, bb, ch0, t0, D, L);
+  __syncthreads();
+  for (int i = threadIdx.x; i < HG_TT * 8; i += 256) {
+    const int q = i & 7, tl = i >> 3, t = t0 + tl, ch = ch0 + 8 * q;
+    if (t >= L || ch >= D) continue;
+    const long long o = ((long long)bb * L + t) * D + ch;
+    const bf16x8 xv = *(const bf16x8*)((const bf16*)a.x2 + o);
+    bf16x8 ov;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ov[j] = (bf16)(ty[(8 * q + j) * HG_S + tl] * (float)xv[j]);
+    *(bf16x8*)((bf16*)a.out + o) = ov;
+  }
+}
+
+__global__ __launch_bounds__(256) void hyena_post_bwd3_kernel(GateArgs a) {
+  __shared__ float ty[64 * HG_S];
+  __shared__ float tg[64 * HG_S];
+  const int t0 = blockIdx.x * HG_TT, ch0 = blockIdx.y * 64, bb = blockIdx.z, L = a.L, D = a.D;
+  hg_stage_cm(ty, a.y, bb, ch0, t0, D, L);
+  __syncthreads();
+  for (int i = threadIdx.x; i < HG_TT * 8; i += 256) {
+    const int q = i & 7, tl = i >> 3, t = t0 + tl, ch = ch0 + 8 * q;
+    if (t >= L || ch >= D) continue;
+    const long long o = ((long long)bb * L + t) * D + ch;
+    const bf16x8 gv = *(const bf16x8*)((const bf16*)a.dout + o);
+    const bf16x8 xv = *(const bf16x8*)((const bf16*)a.x2 + o);
+    f32x4 d0, d1;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float go = (float)gv[j];
+      tg[(8 * q + j) * HG_S + tl] = go * (float)xv[j];
+      const float dx = go * ty[(8 * q + j) * HG_S + tl];
+      if (j < 4) d0[j] = dx; else d1[j - 4] = dx;
+    }
+    *(f32x4*)((float*)a.dx2 + o) = d0;
+    *(f32x4*)((float*)a.dx2 + o + 4) = d1;
+  }
+  __syncthreads();
+  hg_store_cm(a.dy, tg, bb, ch0, t0, D, L);
+}
+
+// z tile rows r <- tokens t0 - HALO + r (zero outside [0, L)), the three gate channel runs of ch0 .. ch0 + 63.
+__device__ __forceinline__ void hg_stage_z(bf16* zt, const bf16* zb, int rows, int t0, int halo, int ch0, int D,
+                                           int L, int hd) {
+  for (int i = threadIdx.x; i < rows * 24; i += 256) {
+    const int r = i / 24, k = i - r * 24, g = k >> 3, q = k & 7;
+    const int t = t0 - halo + r, ch = ch0 + 8 * q;
+    bf16x8 v = {};
+    if (t >= 0 && t < L && ch < D) v = *(const bf16x8*)(zb + (long long)t * 3 * D + hg_zcol(ch, g, hd));
+    *(bf16x8*)(zt + r * 192 + g * 64 + 8 * q) = v;
+  }
+}
+
+template <int KC>
+__global__ __launch_bounds__(256) void hyena_pre_fwd3_kernel(GateArgs a) {
+  constexpr int ZR = HG_TT + KC - 1;
+  __shared__ __attribute__((aligned(16))) bf16 zt[ZR * 192];
+  __shared__ __attribute__((aligned(16))) bf16 x2t[HG_TT * 64];
+  __shared__ float vgt[64 * HG_S];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int t0 = blockIdx.x * HG_TT, ch0 = blockIdx.y * 64, bb = blockIdx.z, L = a.L, D = a.D;
+  hg_stage_z(zt, (const bf16*)a.z + (long long)bb * L * 3 * D, ZR, t0, KC - 1, ch0, D, L, a.hd);
+  const int chc = min(ch0 + lane, D - 1);
+  const int c1 = hg_zcol(chc, 0, a.hd), c2 = c1 + a.hd, c3 = c1 + 2 * a.hd;
+  float w1[KC], w2[KC], w3[KC];
+#pragma unroll
+  for (int i = 0; i < KC; ++i) { w1[i] = a.w[c1 * KC + i]; w2[i] = a.w[c2 * KC + i]; w3[i] = a.w[c3 * KC + i]; }
+  const float b1 = a.bias ? a.bias[c1] : 0.f, b2 = a.bias ? a.bias[c2] : 0.f, b3 = a.bias ? a.bias[c3] : 0.f;
+  __syncthreads();
+  const int sl0 = wave * (HG_TT / 4);
+  auto zr = [&](int row, int g) -> float { return (float)zt[row * 192 + g * 64 + lane]; };
+  float r1[KC], r2[KC], r3[KC];   // rows sl .. sl + KC - 1 = tokens s - KC + 1 .. s
+#pragma unroll
+  for (int i = 1; i < KC; ++i) { r1[i] = zr(sl0 + i - 1, 0); r2[i] = zr(sl0 + i - 1, 1); r3[i] = zr(sl0 + i - 1, 2); }
+#pragma unroll
+  for (int u = 0; u < HG_TT / 4; ++u) {
+    const int sl = sl0 + u;
+#pragma unroll
+    for (int i = 0; i < KC - 1; ++i) { r1[i] = r1[i + 1]; r2[i] = r2[i + 1]; r3[i] = r3[i + 1]; }
+    r1[KC - 1] = zr(sl + KC - 1, 0); r2[KC - 1] = zr(sl + KC - 1, 1); r3[KC - 1] = zr(sl + KC - 1, 2);
+    float x1 = b1, x2 = b2, v = b3;
+#pragma unroll
+    for (int i = 0; i < KC; ++i) { x1 = fmaf(w1[i], r1[i], x1); x2 = fmaf(w2[i], r2[i], x2); v = fmaf(w3[i], r3[i], v); }
+    x2t[sl * 64 + lane] = (bf16)x2;
+    vgt[lane * HG_S + sl] = v * x1;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < HG_TT * 8; i += 256) {
+    const int q = i & 7, tl = i >> 3, t = t0 + tl, ch = ch0 + 8 * q;
+    if (t < L && ch < D)
+      *(bf16x8*)((bf16*)a.x2 + ((long long)bb * L + t) * D + ch) = *(const bf16x8*)(x2t + tl * 64 + 8 * q);
+  }
+  hg_store_cm(a.vg, vgt, bb, ch0, t0, D, L);
+}
+
+// dz / dw / db of the short conv + gates (see hyena_pre_bwd2_kernel), token tiles strided over a persistent grid.
+template <int KC>
+__global__ __launch_bounds__(256) void hyena_pre_bwd3_kernel(GateArgs a) {
+  constexpr int ZR = HG_TT + 2 * KC - 2;        // z rows: tokens t0 - KC + 1 .. t0 + TT + KC - 2
+  constexpr int W = HG_TT + KC - 1;             // dconv tokens t0 .. t0 + TT + KC - 2
+  constexpr int WS = W | 1;                     // odd stride of the dvg tile
+  constexpr int W4 = (W + 3) / 4;
+  constexpr int NR = 2 * KC - 1;
+  constexpr int TW = HG_TT / 4;                 // output tokens per wave
+  constexpr int NIT = TW + KC - 1;
+  constexpr int NA = 3 * (KC + 1);
+  static_assert(4 * NA * 64 * 4 <= ZR * 192 * 2, "reduction scratch must fit the z tile");
+  __shared__ __attribute__((aligned(16))) bf16 zt[ZR * 192];    // z rows, then dz rows, then the dw/db reduction
+  __shared__ float dvt[64 * WS];
+  __shared__ __attribute__((aligned(16))) float gxt[W4 * 4 * 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ch0 = blockIdx.y * 64, bb = blockIdx.z, L = a.L, D = a.D, D3 = 3 * D;
+  const int ch = ch0 + lane, chc = min(ch, D - 1);
+  const int c1 = hg_zcol(chc, 0, a.hd), c2 = c1 + a.hd, c3 = c1 + 2 * a.hd;
+  const bf16* zb = (const bf16*)a.z + (long long)bb * L * D3;
+  const float* gx2 = (const float*)a.gx2 + (long long)bb * L * D;
+  bf16* dzb = (bf16*)a.dz + (long long)bb * L * D3;
+  float w1[KC], w2[KC], w3[KC];
+#pragma unroll
+  for (int i = 0; i < KC; ++i) { w1[i] = a.w[c1 * KC + i]; w2[i] = a.w[c2 * KC + i]; w3[i] = a.w[c3 * KC + i]; }
+  const float b1 = a.bias ? a.bias[c1] : 0.f, b3 = a.bias ? a.bias[c3] : 0.f;
+  float acc[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) acc[i] = 0.f;
+  const int ntiles = (L + HG_TT - 1) / HG_TT;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int t0 = tile * HG_TT;
+    hg_stage_z(zt, zb, ZR, t0, KC - 1, ch0, D, L, a.hd);
+    for (int i = threadIdx.x; i < 64 * W4; i += 256) {          // dvg rows, tokens t0 .. t0 + W - 1
+      const int r = i / W4, c4 = (i - r * W4) * 4, c = ch0 + r, t = t0 + c4;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (c < D && t < L) v = *(const f32x4*)(a.dvg + ((long long)bb * D + c) * L + t);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (c4 + j < W) dvt[r * WS + c4 + j] = v[j];
+    }
+    for (int i = threadIdx.x; i < W4 * 4 * 16; i += 256) {      // gx2 rows (tokens), 64 channels
+      const int r = i >> 4, c4 = (i & 15) * 4, t = t0 + r, c = ch0 + c4;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (t < L && c < D) v = *(const f32x4*)(gx2 + (long long)t * D + c);
+      *(f32x4*)(gxt + r * 64 + c4) = v;
+    }
+    __syncthreads();
+    const int sl0 = wave * TW, s0 = t0 + sl0;
+    auto zr = [&](int row, int g) -> float { return row >= 0 ? (float)zt[row * 192 + g * 64 + lane] : 0.f; };
+    float z1[NR], z2[NR], z3[NR], d1[KC], d2[KC], d3[KC], o1[TW], o2[TW], o3[TW];
+#pragma unroll
+    for (int j = 1; j < NR; ++j) {   // ring entry j <-> token s0 - NR + j (row sl0 - NR + j + KC - 1)
+      z1[j] = zr(sl0 - NR + j + KC - 1, 0); z2[j] = zr(sl0 - NR + j + KC - 1, 1); z3[j] = zr(sl0 - NR + j + KC - 1, 2);
+    }
+#pragma unroll
+    for (int i = 0; i < KC; ++i) d1[i] = d2[i] = d3[i] = 0.f;
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int tn = s0 + k, tl = sl0 + k;    // tl < W
+#pragma unroll
+      for (int j = 0; j < NR - 1; ++j) { z1[j] = z1[j + 1]; z2[j] = z2[j + 1]; z3[j] = z3[j + 1]; }
+      z1[NR - 1] = zr(tl + KC - 1, 0); z2[NR - 1] = zr(tl + KC - 1, 1); z3[NR - 1] = zr(tl + KC - 1, 2);
+      float x1 = b1, v = b3;
+#pragma unroll
+      for (int i = 0; i < KC; ++i) { x1 = fmaf(w1[i], z1[KC - 1 + i], x1); v = fmaf(w3[i], z3[KC - 1 + i], v); }
+      const bool in = tn < L;
+      const float dv = in ? dvt[lane * WS + tl] : 0.f;
+#pragma unroll
+      for (int i = 0; i < KC - 1; ++i) { d1[i] = d1[i + 1]; d2[i] = d2[i + 1]; d3[i] = d3[i + 1]; }
+      d1[KC - 1] = dv * v; d2[KC - 1] = in ? gxt[tl * 64 + lane] : 0.f; d3[KC - 1] = dv * x1;
+      if (k >= KC - 1) {
+        const int u = k - (KC - 1), s = s0 + u;
+        float p1 = 0.f, p2 = 0.f, p3 = 0.f;
+#pragma unroll
+        for (int i = 0; i < KC; ++i) {
+          p1 = fmaf(w1[i], d1[KC - 1 - i], p1);
+          p2 = fmaf(w2[i], d2[KC - 1 - i], p2);
+          p3 = fmaf(w3[i], d3[KC - 1 - i], p3);
+        }
+        o1[u] = p1; o2[u] = p2; o3[u] = p3;
+        if (s < L) {
+#pragma unroll
+          for (int i = 0; i < KC; ++i) {
+            acc[i] = fmaf(d1[0], z1[i], acc[i]);
+            acc[KC + 1 + i] = fmaf(d2[0], z2[i], acc[KC + 1 + i]);
+            acc[2 * KC + 2 + i] = fmaf(d3[0], z3[i], acc[2 * KC + 2 + i]);
+          }
+          acc[KC] += d1[0]; acc[2 * KC + 1] += d2[0]; acc[3 * KC + 2] += d3[0];
+        }
+      }
+    }
+    __syncthreads();                                   // every wave is done with the z / dvg / gx2 tiles
+#pragma unroll
+    for (int u = 0; u < TW; ++u) {
+      bf16* row = zt + (sl0 + u) * 192 + lane;
+      row[0] = (bf16)o1[u]; row[64] = (bf16)o2[u]; row[128] = (bf16)o3[u];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < HG_TT * 24; i += 256) {
+      const int r = i / 24, k = i - r * 24, g = k >> 3, q = k & 7, t = t0 + r, c = ch0 + 8 * q;
+      if (t < L && c < D)
+        *(bf16x8*)(dzb + (long long)t * D3 + hg_zcol(c, g, a.hd)) = *(const bf16x8*)(zt + r * 192 + g * 64 + 8 * q);
+    }
+    __syncthreads();
+  }
+  float* red = (float*)zt;                           // [4 waves][NA][64]
+#pragma unroll
+  for (int i = 0; i < NA; ++i) red[(wave * NA + i) * 64 + lane] = acc[i];
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < NA * 64; idx += 256) {
+    const int i = idx / 64, l = idx - i * 64, c = ch0 + l;
+    if (c >= D) continue;
+    const float sum = (red[i * 64 + l] + red[(NA + i) * 64 + l]) + (red[(2 * NA + i) * 64 + l] + red[(3 * NA + i) * 64 + l]);
+    const int grp = i / (KC + 1), k = i - grp * (KC + 1);
+    const int cc = hg_zcol(c, grp, a.hd);
+    if (k < KC) atomicAdd(a.dw + cc * KC + k, sum);
+    else if (a.db) atomicAdd(a.db + cc, sum);
+  }
+}
+
+// Whether the v3 kernels take this call (LCI_HYENA_GLUE_V2=1 forces the v2 kernels).
+static bool hg_v3_ok(const GateArgs& a, int dtype, std::initializer_list<const void*> ptrs) {
+  static const bool off = getenv("LCI_HYENA_GLUE_V2") != nullptr;
+  if (off || dtype != 1 || a.hd % 8 || a.D % 8 || a.L % 4) return false;
+  for (const void* p : ptrs)
+    if (p && ((uintptr_t)p & 15)) return false;
+  return true;
+}
 }  // namespace lci
 
 using namespace lci;
@@ -1113,6 +1379,17 @@ extern "C" int lci_hyena_pre_fwd(int dtype, const void* z, const float* w, const
   LCI_CHECK(K >= 1 && K <= 8, "hyena_pre: short filter order %d unsupported (<= 8)", K);
   GateArgs a{};
   a.z = z; a.w = w; a.bias = bias; a.vg = vg; a.x2 = x2; a.BB = BB; a.L = L; a.H = H; a.hd = hd; a.D = H * hd; a.K = K;
+  if (hg_v3_ok(a, dtype, {z, vg, x2})) {
+    dim3 grid3((L + HG_TT - 1) / HG_TT, (a.D + 63) / 64, BB);
+#define LCI_PRE_FWD3(KK) \
+  case KK: hipLaunchKernelGGL(hyena_pre_fwd3_kernel<KK>, grid3, dim3(256), 0, (hipStream_t)stream, a); LCI_LAUNCH_CHECK(); return 0;
+    switch (K) {
+      LCI_PRE_FWD3(1) LCI_PRE_FWD3(2) LCI_PRE_FWD3(3) LCI_PRE_FWD3(4) LCI_PRE_FWD3(5) LCI_PRE_FWD3(6) LCI_PRE_FWD3(7)
+      LCI_PRE_FWD3(8)
+      default: break;
+    }
+#undef LCI_PRE_FWD3
+  }
   {   // register-ring kernels (every order the C-ABI accepts)
     dim3 grid2((L + HY_TT - 1) / HY_TT, (a.D + 63) / 64, BB);
 #define LCI_PRE_FWD(KK)                                                                                         \
@@ -1142,8 +1419,13 @@ extern "C" int lci_hyena_pre_fwd(int dtype, const void* z, const float* w, const
 extern "C" int lci_hyena_post_fwd(int dtype, const float* y, const void* x2, void* out, int BB, int L, int D,
                                   void* stream) {
   GateArgs a{};
-  a.y = y; a.x2 = (void*)x2; a.out = out; a.BB = BB; a.L = L; a.D = D;
+  a.y = y; a.x2 = (void*)x2; a.out = out; a.BB = BB; a.L = L; a.D = D; a.hd = 8;
   dim3 grid((L + 63) / 64, (D + 63) / 64, BB);
+  if (hg_v3_ok(a, dtype, {y, x2, out})) {
+    hipLaunchKernelGGL(hyena_post_fwd3_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
+    LCI_LAUNCH_CHECK();
+    return 0;
+  }
   if (dtype == 1) hipLaunchKernelGGL(hyena_post_fwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, a);
   else hipLaunchKernelGGL(hyena_post_fwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, a);
   LCI_LAUNCH_CHECK();
@@ -1153,8 +1435,13 @@ extern "C" int lci_hyena_post_fwd(int dtype, const float* y, const void* x2, voi
 extern "C" int lci_hyena_post_bwd(int dtype, const float* y, const void* x2, const void* dout, float* dy, float* dx2,
                                   int BB, int L, int D, void* stream) {
   GateArgs a{};
-  a.y = y; a.x2 = (void*)x2; a.dout = dout; a.dy = dy; a.dx2 = dx2; a.BB = BB; a.L = L; a.D = D;
+  a.y = y; a.x2 = (void*)x2; a.dout = dout; a.dy = dy; a.dx2 = dx2; a.BB = BB; a.L = L; a.D = D; a.hd = 8;
   dim3 grid((L + 63) / 64, (D + 63) / 64, BB);
+  if (hg_v3_ok(a, dtype, {y, x2, dout, dy, dx2})) {
+    hipLaunchKernelGGL(hyena_post_bwd3_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
+    LCI_LAUNCH_CHECK();
+    return 0;
+  }
   if (dtype == 1) hipLaunchKernelGGL(hyena_post_bwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, a);
   else hipLaunchKernelGGL(hyena_post_bwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, a);
   LCI_LAUNCH_CHECK();
@@ -1169,6 +1456,19 @@ extern "C" int lci_hyena_pre_bwd(int dtype, const void* z, const float* w, const
   GateArgs a{};
   a.z = z; a.w = w; a.bias = bias; a.dvg = dvg; a.gx2 = gx2; a.dz = dz; a.dw = dw; a.db = db;
   a.BB = BB; a.L = L; a.H = H; a.hd = hd; a.D = H * hd; a.K = K;
+  if (hg_v3_ok(a, dtype, {z, dvg, gx2, dz})) {   // persistent: ~2 workgroups per CU stride over the token tiles
+    const int ntiles = (L + HG_TT - 1) / HG_TT, ncy = (a.D + 63) / 64;
+    const int gx = std::max(1, std::min(ntiles, 512 / std::max(1, ncy * BB)));
+    dim3 grid3(gx, ncy, BB);
+#define LCI_PRE_BWD3(KK) \
+  case KK: hipLaunchKernelGGL(hyena_pre_bwd3_kernel<KK>, grid3, dim3(256), 0, (hipStream_t)stream, a); LCI_LAUNCH_CHECK(); return 0;
+    switch (K) {
+      LCI_PRE_BWD3(1) LCI_PRE_BWD3(2) LCI_PRE_BWD3(3) LCI_PRE_BWD3(4) LCI_PRE_BWD3(5) LCI_PRE_BWD3(6) LCI_PRE_BWD3(7)
+      LCI_PRE_BWD3(8)
+      default: break;
+    }
+#undef LCI_PRE_BWD3
+  }
   if (!getenv("LCI_HYENA_PRE_V1")) {   // one lane per output channel, token tiles strided over ~8 workgroups/CU
     const int ntiles = (L + HY_TT - 1) / HY_TT, ncy = (a.D + 63) / 64;
     const int gx = std::max(1, std::min(ntiles, 2048 / std::max(1, ncy * BB)));
