@@ -45,6 +45,8 @@ struct FftArgs {
   int n, n1, n2, ln1, ln2, G;
   int mode;                             // row pass: 0 = spectrum of filters, 1 = fwd conv, 2 = bwd (conj + dk)
   int single;                           // col passes: 1 = the source is the filter (C rows, no pairing)
+  int pid0;                             // first pair (col passes) / filter (row pass) of this launch's chunk
+  int pb;                               // row pass: sequences per LDS batch (ROW_PB, LCI_FFT_ROW_PB)
 };
 
 // ------------------------------------------------------------------- sub-FFTs: radix-8/4/2 Stockham in LDS
@@ -143,7 +145,7 @@ __global__ __launch_bounds__(256) void fft_col_fwd_kernel(FftArgs a) {
   f32x2* twl = y + a.G * ld;
   load_twl(twl, a.tw, a.n1, a.n);
   const int c0 = blockIdx.x * a.G;
-  const int pid = blockIdx.y;           // pair id (j * P + p) or filter id when single
+  const int pid = a.pid0 + blockIdx.y;  // pair id (j * P + p) or filter id when single
   int r0, r1;
   if (a.single) { r0 = pid; r1 = -1; }
   else {
@@ -203,7 +205,7 @@ __global__ __launch_bounds__(512) void fft_row_kernel(FftArgs a) {
   extern __shared__ __attribute__((aligned(16))) f32x2 lds[];
   const int N = a.n2;
   const bool two = a.mode == 2 && a.SK;           // bwd with filter gradient: also FFT the vg rows
-  const int PB = two ? ROW_PB / 2 : ROW_PB;
+  const int PB = two ? a.pb / 2 : a.pb;
   f32x2* x = lds;                                 // PB * N
   f32x2* y = x + PB * N;                          // PB * N
   f32x2* x2 = y + PB * N;                         // PB * N (two)
@@ -211,7 +213,7 @@ __global__ __launch_bounds__(512) void fft_row_kernel(FftArgs a) {
   f32x2* kr = y2 + (two ? PB * N : 0);
   f32x2* acc = kr + N;
   f32x2* twl = acc + N;
-  const int k1 = blockIdx.x, j = blockIdx.y;
+  const int k1 = blockIdx.x, j = a.pid0 + blockIdx.y;
   const float invn = 1.f / (float)a.n;
   load_twl(twl, a.tw, N, a.n);
   if (a.mode == 0) {  // filter spectrum: K_j[k1][:] = FFT_n2(T[k1][:]) / n
@@ -294,7 +296,7 @@ __global__ __launch_bounds__(256) void fft_col_inv_kernel(FftArgs a) {
   f32x2* twl = y + a.G * ld;
   load_twl(twl, a.tw, a.n1, a.n);
   const int c0 = blockIdx.x * a.G;
-  const int pid = blockIdx.y;
+  const int pid = a.pid0 + blockIdx.y;
   const f32x2* S = (a.single ? a.SK : a.S) + (long long)pid * a.n;
   const int total = a.G * a.n1;
   for (int base = 0; base < total; base += UB * blockDim.x) {
@@ -404,6 +406,34 @@ __device__ __forceinline__ void lds_fft_inplace(f32x2* x, int N, int lN, const f
   }
 }
 
+// Inter-pass twiddles W_n^e, e < n = 2^ln, as the product of three LDS tables (W_n^e0, W_n^(e1 2^l0),
+// W_n^(e2 2^(l0+l1)), copied from the f64-built table): two complex multiplies and three LDS reads instead of one
+// random 8-byte gather from the n-entry global table per element (a cache line per lane).
+struct Tw3 {
+  const f32x2* t;   // [2^l0 | 2^l1 | 2^l2]
+  int l0, l1;
+};
+__host__ __device__ constexpr int tw3_entries(int ln) {
+  return (1 << ((ln + 2) / 3)) + (1 << ((ln + 1) / 3)) + (1 << (ln / 3));
+}
+__device__ __forceinline__ Tw3 load_tw3(f32x2* t, const f32x2* tw, int ln) {
+  const int l0 = (ln + 2) / 3, l1 = (ln + 1) / 3, l2 = ln / 3;
+  const int n0 = 1 << l0, n1 = 1 << l1, n2 = 1 << l2;
+  for (int i = threadIdx.x; i < n0 + n1 + n2; i += blockDim.x) {
+    long long e;
+    if (i < n0) e = i;
+    else if (i < n0 + n1) e = (long long)(i - n0) << l0;
+    else e = (long long)(i - n0 - n1) << (l0 + l1);
+    t[i] = tw[e];
+  }
+  return Tw3{t, l0, l1};
+}
+__device__ __forceinline__ f32x2 tw3(const Tw3& w, long long e) {
+  const int e0 = (int)(e & ((1 << w.l0) - 1)), e1 = (int)((e >> w.l0) & ((1 << w.l1) - 1));
+  const int e2 = (int)(e >> (w.l0 + w.l1));
+  return cmul(cmul(w.t[e0], w.t[(1 << w.l0) + e1]), w.t[(1 << w.l0) + (1 << w.l1) + e2]);
+}
+
 // grid (n2 / GW, npairs_total or C); block 256. Same math as fft_col_fwd_kernel.
 template <int GW>
 __global__ __launch_bounds__(256) void fft_colw_fwd_kernel(FftArgs a) {
@@ -412,8 +442,9 @@ __global__ __launch_bounds__(256) void fft_colw_fwd_kernel(FftArgs a) {
   f32x2* x = lds;
   f32x2* twl = x + GW * ld;
   load_twl(twl, a.tw, a.n1, a.n);
+  const Tw3 tw3t = load_tw3(twl + a.n1, a.tw, a.ln1 + a.ln2);
   const int c0 = blockIdx.x * GW;
-  const int pid = blockIdx.y;
+  const int pid = a.pid0 + blockIdx.y;
   int r0, r1;
   if (a.single) { r0 = pid; r1 = -1; }
   else {
@@ -445,20 +476,9 @@ __global__ __launch_bounds__(256) void fft_colw_fwd_kernel(FftArgs a) {
   __syncthreads();
   lds_fft_inplace<false>(x, a.n1, a.ln1, twl, ld);
   f32x2* S = (a.single ? a.SK : a.S) + (long long)pid * a.n;
-  for (int base = 0; base < CW_ELEMS; base += UB * 256) {
-    f32x2 w[UB];
-#pragma unroll
-    for (int u = 0; u < UB; ++u) {
-      const int idx = base + u * 256 + threadIdx.x;
-      const int g = idx % GW, k1 = idx / GW;
-      w[u] = a.tw[((long long)(c0 + g) * k1) & (a.n - 1)];
-    }
-#pragma unroll
-    for (int u = 0; u < UB; ++u) {
-      const int idx = base + u * 256 + threadIdx.x;
-      const int g = idx % GW, k1 = idx / GW;
-      S[(long long)k1 * a.n2 + c0 + g] = cmul(x[g * ld + k1], w[u]);
-    }
+  for (int idx = threadIdx.x; idx < CW_ELEMS; idx += 256) {
+    const int g = idx % GW, k1 = idx / GW;
+    S[(long long)k1 * a.n2 + c0 + g] = cmul(x[g * ld + k1], tw3(tw3t, ((long long)(c0 + g) * k1) & (a.n - 1)));
   }
 }
 
@@ -470,22 +490,24 @@ __global__ __launch_bounds__(256) void fft_colw_inv_kernel(FftArgs a) {
   f32x2* x = lds;
   f32x2* twl = x + GW * ld;
   load_twl(twl, a.tw, a.n1, a.n);
+  const Tw3 tw3t = load_tw3(twl + a.n1, a.tw, a.ln1 + a.ln2);
   const int c0 = blockIdx.x * GW;
-  const int pid = blockIdx.y;
+  const int pid = a.pid0 + blockIdx.y;
   const f32x2* S = (a.single ? a.SK : a.S) + (long long)pid * a.n;
+  __syncthreads();   // the twiddle tables are read below
   for (int base = 0; base < CW_ELEMS; base += UB * 256) {
-    f32x2 v[UB], w[UB];
+    f32x2 v[UB];
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
       const int idx = base + u * 256 + threadIdx.x;
       const int g = idx % GW, k1 = idx / GW;
-      w[u] = a.tw[((long long)(c0 + g) * k1) & (a.n - 1)];
       v[u] = S[(long long)k1 * a.n2 + c0 + g];
     }
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
       const int idx = base + u * 256 + threadIdx.x;
-      x[(idx % GW) * ld + idx / GW] = cmulc(v[u], w[u]);
+      const int g = idx % GW, k1 = idx / GW;
+      x[g * ld + k1] = cmulc(v[u], tw3(tw3t, ((long long)(c0 + g) * k1) & (a.n - 1)));
     }
   }
   __syncthreads();
@@ -1284,7 +1306,7 @@ extern "C" int lci_fft_twiddles(void* tw, int n, void* stream) {
 static int launch_col(FftArgs& a, bool inv, int nblk_y, hipStream_t s) {
   const int gw = CW_ELEMS / a.n1;
   if ((gw == 16 || gw == 32) && a.n2 % gw == 0 && !getenv("LCI_FFT_COL_V1")) {
-    const size_t sh = ((size_t)gw * (a.n1 + 1) + a.n1) * sizeof(f32x2);
+    const size_t sh = ((size_t)gw * (a.n1 + 1) + a.n1 + tw3_entries(a.ln1 + a.ln2)) * sizeof(f32x2);
     dim3 grid(a.n2 / gw, nblk_y);
 #define LCI_COLW(GW)                                                                                       \
     (void)hipFuncSetAttribute((const void*)(inv ? fft_colw_inv_kernel<GW> : fft_colw_fwd_kernel<GW>),      \
@@ -1306,13 +1328,25 @@ static int launch_col(FftArgs& a, bool inv, int nblk_y, hipStream_t s) {
   return 0;
 }
 
-static int launch_row(FftArgs& a, hipStream_t s) {
-  const size_t sh = ((size_t)2 * ROW_PB + 3) * a.n2 * sizeof(f32x2);   // x, y (+ x2, y2 at PB/2) + kr, acc, twl
+static int launch_row(FftArgs& a, int nfilt, hipStream_t s) {
+  static const int env_pb = getenv("LCI_FFT_ROW_PB") ? atoi(getenv("LCI_FFT_ROW_PB")) : ROW_PB;
+  a.pb = std::max(2, std::min(16, env_pb)) & ~1;
+  const size_t sh = ((size_t)2 * a.pb + 3) * a.n2 * sizeof(f32x2);   // x, y (+ x2, y2 at PB/2) + kr, acc, twl
+  LCI_CHECK(sh <= 160 * 1024, "fft row pass: %zu bytes of LDS", sh);
   (void)hipFuncSetAttribute((const void*)fft_row_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   const int thr = a.n2 >= 1024 ? 512 : 256;
-  hipLaunchKernelGGL(fft_row_kernel, dim3(a.n1, a.C), dim3(thr), sh, s, a);
+  hipLaunchKernelGGL(fft_row_kernel, dim3(a.n1, nfilt), dim3(thr), sh, s, a);
   LCI_LAUNCH_CHECK();
   return 0;
+}
+
+// Filters per launch chunk: the passes of one chunk run back to back so its spectra scratch (bytes_per_filter
+// each) stays resident in the Infinity Cache between the column and row passes (LCI_FFT_CHUNK_MB, 0 = one chunk).
+static int fft_chunk(int C, long long bytes_per_filter) {
+  static const long long mb = getenv("LCI_FFT_CHUNK_MB") ? atoll(getenv("LCI_FFT_CHUNK_MB")) : 0;
+  if (mb <= 0) return C;
+  const long long jc = (mb << 20) / std::max(1LL, bytes_per_filter);
+  return (int)std::max(1LL, std::min((long long)C, jc));
 }
 
 // Filter spectra: k (C, L) f32 -> K (C, n) complex in [k1][k2] layout, scaled by 1/n. SK: (C, n) scratch.
@@ -1321,8 +1355,13 @@ extern "C" int lci_fftconv_spectrum(const float* k, void* K, void* SK, const voi
   if (fft_plan(a, L)) return 1;
   a.src = k; a.K = (f32x2*)K; a.SK = (f32x2*)SK; a.tw = (const f32x2*)tw; a.C = C; a.single = 1; a.mode = 0;
   hipStream_t s = (hipStream_t)stream;
-  if (launch_col(a, false, C, s)) return 3;
-  if (launch_row(a, s)) return 3;
+  const int jc = fft_chunk(C, (long long)a.n * 8);
+  for (int j0 = 0; j0 < C; j0 += jc) {
+    const int nj = std::min(jc, C - j0);
+    a.pid0 = j0;
+    if (launch_col(a, false, nj, s)) return 3;
+    if (launch_row(a, nj, s)) return 3;
+  }
   return 0;
 }
 
@@ -1334,9 +1373,16 @@ extern "C" int lci_fftconv_fwd(const float* u, const void* K, const float* Dv, f
   a.src = u; a.dst = y; a.K = (f32x2*)K; a.S = (f32x2*)S; a.tw = (const f32x2*)tw; a.Dv = Dv;
   a.R = R; a.C = C; a.P = (R + 1) / 2; a.single = 0; a.mode = 1;
   hipStream_t s = (hipStream_t)stream;
-  if (launch_col(a, false, C * a.P, s)) return 3;
-  if (launch_row(a, s)) return 3;
-  if (launch_col(a, true, C * a.P, s)) return 3;
+  const int jc = fft_chunk(C, (long long)a.P * a.n * 8);
+  for (int j0 = 0; j0 < C; j0 += jc) {
+    const int nj = std::min(jc, C - j0);
+    a.pid0 = j0 * a.P;
+    if (launch_col(a, false, nj * a.P, s)) return 3;
+    a.pid0 = j0;
+    if (launch_row(a, nj, s)) return 3;
+    a.pid0 = j0 * a.P;
+    if (launch_col(a, true, nj * a.P, s)) return 3;
+  }
   return 0;
 }
 
@@ -1350,22 +1396,31 @@ extern "C" int lci_fftconv_bwd(const float* dy, const float* u, const void* K, c
   a.tw = (const f32x2*)tw; a.K = (f32x2*)K; a.S = (f32x2*)S; a.S2 = (f32x2*)S2; a.SK = dk ? (f32x2*)SK : nullptr;
   a.R = R; a.C = C; a.P = (R + 1) / 2; a.Dv = Dv; a.dk = dk;
   hipStream_t s = (hipStream_t)stream;
-  a.single = 0;
-  a.src = dy;
-  if (launch_col(a, false, C * a.P, s)) return 3;            // S <- col FFT of dy pairs
-  if (dk) {
-    FftArgs b = a;
-    b.S = (f32x2*)S2; b.src = u;
-    if (launch_col(b, false, C * a.P, s)) return 3;          // S2 <- col FFT of u pairs
-  }
-  a.mode = 2;
-  if (launch_row(a, s)) return 3;                            // S <- conj(K) products, SK <- dk rows
-  a.src = dy; a.dst = du;
-  if (launch_col(a, true, C * a.P, s)) return 3;             // du = IFFT + D dy
-  if (dk) {
-    FftArgs b = a;
-    b.single = 1;
-    if (launch_col(b, true, C, s)) return 3;                 // dk[j] = Re IFFT(SK_j)
+  const int jc = fft_chunk(C, (long long)a.P * a.n * 8 * (dk ? 2 : 1));
+  for (int j0 = 0; j0 < C; j0 += jc) {
+    const int nj = std::min(jc, C - j0);
+    FftArgs c = a;
+    c.single = 0;
+    c.src = dy;
+    c.pid0 = j0 * a.P;
+    if (launch_col(c, false, nj * a.P, s)) return 3;         // S <- col FFT of dy pairs
+    if (dk) {
+      FftArgs b = c;
+      b.S = (f32x2*)S2; b.src = u;
+      if (launch_col(b, false, nj * a.P, s)) return 3;       // S2 <- col FFT of u pairs
+    }
+    c.mode = 2;
+    c.pid0 = j0;
+    if (launch_row(c, nj, s)) return 3;                      // S <- conj(K) products, SK <- dk rows
+    c.src = dy; c.dst = du;
+    c.pid0 = j0 * a.P;
+    if (launch_col(c, true, nj * a.P, s)) return 3;          // du = IFFT + D dy
+    if (dk) {
+      FftArgs b = c;
+      b.single = 1;
+      b.pid0 = j0;
+      if (launch_col(b, true, nj, s)) return 3;              // dk[j] = Re IFFT(SK_j)
+    }
   }
   if (dD) {
     hipLaunchKernelGGL(row_dot_kernel, dim3(R * C), dim3(256), 0, s, dy, u, dD, L, C, R);
