@@ -286,6 +286,121 @@ __global__ __launch_bounds__(512) void fft_row_kernel(FftArgs a) {
   }
 }
 
+// --------------------------------------------------------------------- row pass, n2 = 512, one wave per row
+// The 512-point row FFTs run in registers, one sequence per wave (8 points per lane) as 8 x 8 x 8: lane L holds
+// x[L + 64 r]; a radix-8 DFT over r, twiddle W_512^(L k), an LDS transpose, a radix-8 DFT, twiddle W_64, a second
+// transpose and a third radix-8 DFT leave X[L + 64 m] in the same lane layout, so the spectrum product and the
+// inverse transform follow without a reordering, and the only synchronisation is within the wave (the LDS pass
+// kernel above runs 3 workgroup-barrier passes per transform). Waves of a workgroup take different pairs of the
+// same (filter, row k1); the backward's filter-gradient sum over pairs is reduced across the waves at the end.
+constexpr int R5_S1 = 72;    // transpose-1 row stride (complex): the column reads of a half-wave hit distinct banks
+constexpr int R5_S2 = 9;     // transpose-2 row stride
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <bool INV>
+__device__ __forceinline__ f32x2 tw_at(const f32x2* twl, int t) {
+  f32x2 w = twl[t & 511];
+  if (INV) w.y = -w.y;
+  return w;
+}
+
+// v[r] = x[L + 64 r] in, X[L + 64 r] out (unnormalised inverse when INV). buf: this wave's 8 * R5_S1 complex.
+template <bool INV>
+__device__ __forceinline__ void fft512_wave(f32x2 (&v)[8], f32x2* buf, const f32x2* twl, int L) {
+  dft<8, INV>(v);                                        // over r -> k (frequency mod 8)
+#pragma unroll
+  for (int k = 1; k < 8; ++k) v[k] = cmul(v[k], tw_at<INV>(twl, L * k));
+#pragma unroll
+  for (int k = 0; k < 8; ++k) buf[k * R5_S1 + L] = v[k];
+  wave_lds_sync();
+  const int la = L & 7, kk = L >> 3;                    // lane = (la, k): the 8 values l = la + 8 lb
+#pragma unroll
+  for (int lb = 0; lb < 8; ++lb) v[lb] = buf[kk * R5_S1 + la + 8 * lb];
+  wave_lds_sync();
+  dft<8, INV>(v);                                        // over lb -> m1
+#pragma unroll
+  for (int m = 1; m < 8; ++m) v[m] = cmul(v[m], tw_at<INV>(twl, 8 * la * m));
+#pragma unroll
+  for (int m = 0; m < 8; ++m) buf[(kk + 8 * m) * R5_S2 + la] = v[m];
+  wave_lds_sync();
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v[q] = buf[L * R5_S2 + q];   // lane L = k + 8 m1: the 8 values over la
+  wave_lds_sync();
+  dft<8, INV>(v);                                        // over la -> m2: X[k + 8 m1 + 64 m2] = X[L + 64 m2]
+}
+
+// grid (n1, filters of the chunk); block 64 * nw (waves split the filter's pairs). Same math as fft_row_kernel.
+__global__ __launch_bounds__(256) void fft_row512_kernel(FftArgs a) {
+  __shared__ f32x2 twl[512];
+  __shared__ f32x2 wbuf[4][8 * R5_S1];
+  const int L = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int k1 = blockIdx.x, j = a.pid0 + blockIdx.y;
+  const float invn = 1.f / (float)a.n;
+  load_twl(twl, a.tw, 512, a.n);
+  __syncthreads();
+  f32x2* buf = wbuf[w];
+  const long long row = (long long)k1 * 512 + L;
+  if (a.mode == 0) {   // filter spectrum: K_j[k1][:] = FFT_512(T[k1][:]) / n  (one wave)
+    if (w != 0) return;
+    f32x2 v[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = a.SK[(long long)j * a.n + row + 64 * r];
+    fft512_wave<false>(v, buf, twl, L);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) a.K[(long long)j * a.n + row + 64 * r] = v[r] * invn;
+    return;
+  }
+  f32x2 kr[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) kr[r] = a.K[(long long)j * a.n + row + 64 * r];
+  const bool two = a.mode == 2 && a.SK;
+  f32x2 acc[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) acc[r] = f32x2{0.f, 0.f};
+  for (int p = w; p < a.P; p += nw) {
+    const long long off = ((long long)j * a.P + p) * a.n + row;
+    f32x2 v[8], v2[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      v[r] = a.S[off + 64 * r];
+      if (two) v2[r] = a.S2[off + 64 * r];
+    }
+    fft512_wave<false>(v, buf, twl, L);
+    if (two) {
+      fft512_wave<false>(v2, buf, twl, L);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) acc[r] += cmulc(v[r], v2[r]);   // X_dy conj(X_vg)
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = a.mode == 1 ? cmul(v[r], kr[r]) : cmulc(v[r], kr[r]);
+    fft512_wave<true>(v, buf, twl, L);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) a.S[off + 64 * r] = v[r];
+  }
+  if (!two) return;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 8; ++r) wbuf[w][L + 64 * r] = acc[r];
+  __syncthreads();
+  if (w != 0) return;
+  f32x2 v[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    f32x2 t = wbuf[0][L + 64 * r];
+    for (int q = 1; q < nw; ++q) t += wbuf[q][L + 64 * r];
+    v[r] = t;
+  }
+  wave_lds_sync();
+  fft512_wave<true>(v, buf, twl, L);                     // dk spectrum row (unnormalised correlation)
+#pragma unroll
+  for (int r = 0; r < 8; ++r) a.SK[(long long)j * a.n + row + 64 * r] = v[r] * invn;
+}
+
 // ---------------------------------------------------------------------------------- inverse columns
 // grid: (n2 / G, npairs_total or C); out rows (+ D * src); single: dk[j][m] = Re(...) for the filter.
 __global__ __launch_bounds__(256) void fft_col_inv_kernel(FftArgs a) {
@@ -1015,6 +1130,9 @@ static int fft_plan(FftArgs& a, int L) {
   if (e - a.ln1 > 10) a.ln1 = e - 10;
   a.ln2 = e - a.ln1;
   if (a.ln2 == 0) { a.ln1 = e - 1; a.ln2 = 1; }
+  // n = 2^17 .. 2^19: 512-point rows on fft_row512_kernel, n1 = 256 .. 1024 columns on the wide column kernel
+  static const bool row512 = !getenv("LCI_FFT_ROW_V1") && !getenv("LCI_FFT_LN1");
+  if (row512 && e >= 17 && e <= 19) { a.ln2 = 9; a.ln1 = e - 9; }
   a.n1 = 1 << a.ln1; a.n2 = 1 << a.ln2;
   a.G = a.n2 < env_g ? a.n2 : env_g;
   a.L = L;
@@ -1305,7 +1423,7 @@ extern "C" int lci_fft_twiddles(void* tw, int n, void* stream) {
 
 static int launch_col(FftArgs& a, bool inv, int nblk_y, hipStream_t s) {
   const int gw = CW_ELEMS / a.n1;
-  if ((gw == 16 || gw == 32) && a.n2 % gw == 0 && !getenv("LCI_FFT_COL_V1")) {
+  if ((gw == 8 || gw == 16 || gw == 32) && a.n2 % gw == 0 && !getenv("LCI_FFT_COL_V1")) {
     const size_t sh = ((size_t)gw * (a.n1 + 1) + a.n1 + tw3_entries(a.ln1 + a.ln2)) * sizeof(f32x2);
     dim3 grid(a.n2 / gw, nblk_y);
 #define LCI_COLW(GW)                                                                                       \
@@ -1313,7 +1431,7 @@ static int launch_col(FftArgs& a, bool inv, int nblk_y, hipStream_t s) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                   \
     if (inv) hipLaunchKernelGGL(fft_colw_inv_kernel<GW>, grid, dim3(256), sh, s, a);                     \
     else hipLaunchKernelGGL(fft_colw_fwd_kernel<GW>, grid, dim3(256), sh, s, a);
-    if (gw == 32) { LCI_COLW(32) } else { LCI_COLW(16) }
+    if (gw == 32) { LCI_COLW(32) } else if (gw == 16) { LCI_COLW(16) } else { LCI_COLW(8) }
 #undef LCI_COLW
     LCI_LAUNCH_CHECK();
     return 0;
@@ -1329,6 +1447,15 @@ static int launch_col(FftArgs& a, bool inv, int nblk_y, hipStream_t s) {
 }
 
 static int launch_row(FftArgs& a, int nfilt, hipStream_t s) {
+  if (a.n2 == 512 && !getenv("LCI_FFT_ROW_V1")) {
+    int nw = 1;   // waves per workgroup: the largest divisor of the pair count up to 4 (balanced waves)
+    for (int q = 4; q >= 1; --q)
+      if (a.P % q == 0) { nw = q; break; }
+    if (a.mode == 0) nw = 1;
+    hipLaunchKernelGGL(fft_row512_kernel, dim3(a.n1, nfilt), dim3(64 * nw), 0, s, a);
+    LCI_LAUNCH_CHECK();
+    return 0;
+  }
   static const int env_pb = getenv("LCI_FFT_ROW_PB") ? atoi(getenv("LCI_FFT_ROW_PB")) : ROW_PB;
   a.pb = std::max(2, std::min(16, env_pb)) & ~1;
   const size_t sh = ((size_t)2 * a.pb + 3) * a.n2 * sizeof(f32x2);   // x, y (+ x2, y2 at PB/2) + kr, acc, twl
