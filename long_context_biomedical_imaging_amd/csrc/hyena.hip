@@ -569,31 +569,61 @@ __global__ __launch_bounds__(256) void fft_colw_fwd_kernel(FftArgs a) {
   }
   const float* s0 = a.src + (long long)r0 * a.L;
   const float* s1 = r1 >= 0 ? a.src + (long long)r1 * a.L : nullptr;
-  for (int base = 0; base < CW_ELEMS; base += UB * 256) {
-    f32x2 v[UB];
+  if ((a.L & 3) == 0) {   // 16-byte loads of 4 adjacent columns (rows are 16-B aligned, chunks all in or out)
+    constexpr int NQ = CW_ELEMS / 4;
+    for (int base = 0; base < NQ; base += UB * 256) {
+      f32x4 v0[UB], v1[UB];
 #pragma unroll
-    for (int u = 0; u < UB; ++u) {
-      const int idx = base + u * 256 + threadIdx.x;
-      const int g = idx % GW, ai = idx / GW;
-      const int m = ai * a.n2 + c0 + g;
-      v[u] = f32x2{0.f, 0.f};
-      if (m < a.L) {
-        v[u].x = s0[m];
-        if (s1) v[u].y = s1[m];
+      for (int u = 0; u < UB; ++u) {
+        const int idx = base + u * 256 + threadIdx.x;
+        const int g = (idx % (GW / 4)) * 4, ai = idx / (GW / 4);
+        const int m = ai * a.n2 + c0 + g;
+        v0[u] = v1[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (idx < NQ && m < a.L) {
+          v0[u] = *(const f32x4*)(s0 + m);
+          if (s1) v1[u] = *(const f32x4*)(s1 + m);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const int idx = base + u * 256 + threadIdx.x;
+        const int g = (idx % (GW / 4)) * 4, ai = idx / (GW / 4);
+        if (idx < NQ) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) x[(g + q) * ld + ai] = f32x2{v0[u][q], v1[u][q]};
+        }
       }
     }
+  } else {
+    for (int base = 0; base < CW_ELEMS; base += UB * 256) {
+      f32x2 v[UB];
 #pragma unroll
-    for (int u = 0; u < UB; ++u) {
-      const int idx = base + u * 256 + threadIdx.x;
-      x[(idx % GW) * ld + idx / GW] = v[u];
+      for (int u = 0; u < UB; ++u) {
+        const int idx = base + u * 256 + threadIdx.x;
+        const int g = idx % GW, ai = idx / GW;
+        const int m = ai * a.n2 + c0 + g;
+        v[u] = f32x2{0.f, 0.f};
+        if (m < a.L) {
+          v[u].x = s0[m];
+          if (s1) v[u].y = s1[m];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const int idx = base + u * 256 + threadIdx.x;
+        x[(idx % GW) * ld + idx / GW] = v[u];
+      }
     }
   }
   __syncthreads();
   lds_fft_inplace<false>(x, a.n1, a.ln1, twl, ld);
   f32x2* S = (a.single ? a.SK : a.S) + (long long)pid * a.n;
-  for (int idx = threadIdx.x; idx < CW_ELEMS; idx += 256) {
-    const int g = idx % GW, k1 = idx / GW;
-    S[(long long)k1 * a.n2 + c0 + g] = cmul(x[g * ld + k1], tw3(tw3t, ((long long)(c0 + g) * k1) & (a.n - 1)));
+  for (int idx = threadIdx.x; idx < CW_ELEMS / 2; idx += 256) {   // 16-byte stores of 2 adjacent columns
+    const int g = (idx % (GW / 2)) * 2, k1 = idx / (GW / 2);
+    const long long e = (long long)(c0 + g) * k1;
+    const f32x2 p0 = cmul(x[g * ld + k1], tw3(tw3t, e & (a.n - 1)));
+    const f32x2 p1 = cmul(x[(g + 1) * ld + k1], tw3(tw3t, (e + k1) & (a.n - 1)));
+    *(f32x4*)(S + (long long)k1 * a.n2 + c0 + g) = f32x4{p0.x, p0.y, p1.x, p1.y};
   }
 }
 
@@ -610,19 +640,24 @@ __global__ __launch_bounds__(256) void fft_colw_inv_kernel(FftArgs a) {
   const int pid = a.pid0 + blockIdx.y;
   const f32x2* S = (a.single ? a.SK : a.S) + (long long)pid * a.n;
   __syncthreads();   // the twiddle tables are read below
-  for (int base = 0; base < CW_ELEMS; base += UB * 256) {
-    f32x2 v[UB];
+  constexpr int NH = CW_ELEMS / 2;   // 16-byte loads of 2 adjacent columns
+  for (int base = 0; base < NH; base += UB * 256) {
+    f32x4 v[UB];
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
       const int idx = base + u * 256 + threadIdx.x;
-      const int g = idx % GW, k1 = idx / GW;
-      v[u] = S[(long long)k1 * a.n2 + c0 + g];
+      const int g = (idx % (GW / 2)) * 2, k1 = idx / (GW / 2);
+      if (idx < NH) v[u] = *(const f32x4*)(S + (long long)k1 * a.n2 + c0 + g);
     }
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
       const int idx = base + u * 256 + threadIdx.x;
-      const int g = idx % GW, k1 = idx / GW;
-      x[g * ld + k1] = cmulc(v[u], tw3(tw3t, ((long long)(c0 + g) * k1) & (a.n - 1)));
+      const int g = (idx % (GW / 2)) * 2, k1 = idx / (GW / 2);
+      if (idx < NH) {
+        const long long e = (long long)(c0 + g) * k1;
+        x[g * ld + k1] = cmulc(f32x2{v[u][0], v[u][1]}, tw3(tw3t, e & (a.n - 1)));
+        x[(g + 1) * ld + k1] = cmulc(f32x2{v[u][2], v[u][3]}, tw3(tw3t, (e + k1) & (a.n - 1)));
+      }
     }
   }
   __syncthreads();
@@ -644,6 +679,40 @@ __global__ __launch_bounds__(256) void fft_colw_inv_kernel(FftArgs a) {
   const float* s1 = r1 >= 0 ? a.src + (long long)r1 * a.L : nullptr;
   float* d0 = a.dst + (long long)r0 * a.L;
   float* d1 = r1 >= 0 ? a.dst + (long long)r1 * a.L : nullptr;
+  if ((a.L & 3) == 0) {   // 16-byte loads / stores of 4 adjacent columns
+    const int totq = (GW / 4) * na;
+    for (int base = 0; base < totq; base += UB * 256) {
+      f32x4 u0[UB], u1[UB];
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const int idx = base + u * 256 + threadIdx.x;
+        const int m = (idx / (GW / 4)) * a.n2 + c0 + (idx % (GW / 4)) * 4;
+        u0[u] = u1[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (idx < totq && m < a.L && a.Dv) {
+          u0[u] = *(const f32x4*)(s0 + m);
+          if (s1) u1[u] = *(const f32x4*)(s1 + m);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const int idx = base + u * 256 + threadIdx.x;
+        const int g = (idx % (GW / 4)) * 4, ai = idx / (GW / 4);
+        const int m = ai * a.n2 + c0 + g;
+        if (idx < totq && m < a.L) {
+          f32x4 o0, o1;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const f32x2 v = x[(g + q) * ld + ai];
+            o0[q] = fmaf(Dj, u0[u][q], v.x);
+            o1[q] = fmaf(Dj, u1[u][q], v.y);
+          }
+          *(f32x4*)(d0 + m) = o0;
+          if (d1) *(f32x4*)(d1 + m) = o1;
+        }
+      }
+    }
+    return;
+  }
   const int total = GW * na;
   for (int base = 0; base < total; base += UB * 256) {
     float u0[UB], u1[UB];
