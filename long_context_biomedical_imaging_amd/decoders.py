@@ -430,6 +430,74 @@ def _bn(nd, c):
     return (BatchNorm2d if nd == 2 else BatchNorm3d)(c)
 
 
+# The PSP pyramid's adaptive average pooling (to 1-6 bins) and its align_corners bilinear / trilinear up-sampling
+# back to the feature size are separable linear maps along each spatial axis. Applied as small matrices (f32,
+# autocast off, so the arithmetic stays f32 as in torch's kernels) they become batched GEMMs whose backward is a
+# GEMM too: torch's upsample backward scatters every output pixel into the 1-36 pooled pixels with atomics
+# (13.7 ms per stage at 512^2 x 96 channels, C4) and its adaptive-pool backward takes ~10 ms per stage.
+SEPARABLE_PSP = os.environ.get("LCI_SEPARABLE_PSP", "1") != "0"
+_SEP_CACHE = {}
+
+
+def _lin_interp_matrix(out_size, in_size, device):
+    """(out, in) f32 weights of 1-D linear interpolation with align_corners=True, computed as torch's
+    upsample kernels do (scale = (in - 1) / (out - 1) in f32, src = scale * i, i0 = floor, lambda = src - i0)."""
+    key = ("lin", out_size, in_size, str(device))
+    m = _SEP_CACHE.get(key)
+    if m is None:
+        scale = torch.tensor((in_size - 1) / (out_size - 1) if out_size > 1 else 0.0, dtype=torch.float32)
+        src = scale * torch.arange(out_size, dtype=torch.float32)
+        i0 = src.floor().to(torch.long).clamp(max=in_size - 1)
+        lam1 = src - i0.to(torch.float32)
+        i1 = torch.clamp(i0 + 1, max=in_size - 1)
+        m = torch.zeros(out_size, in_size, dtype=torch.float32)
+        rows = torch.arange(out_size)
+        m.index_put_((rows, i0), 1.0 - lam1, accumulate=True)
+        m.index_put_((rows, i1), lam1, accumulate=True)
+        m = m.to(device)
+        _SEP_CACHE[key] = m
+    return m
+
+
+def _avg_pool_matrix(out_size, in_size, device):
+    """(out, in) f32 weights of adaptive average pooling: bin i averages [floor(i in / out), ceil((i+1) in / out))."""
+    key = ("pool", out_size, in_size, str(device))
+    m = _SEP_CACHE.get(key)
+    if m is None:
+        m = torch.zeros(out_size, in_size, dtype=torch.float32)
+        for i in range(out_size):
+            a, b = (i * in_size) // out_size, -((-(i + 1) * in_size) // out_size)
+            m[i, a:b] = 1.0 / (b - a)
+        m = m.to(device)
+        _SEP_CACHE[key] = m
+    return m
+
+
+def _separable(x, mats):
+    """Apply mats[k] (out_k, in_k) along spatial axis k of x (N, C, *S), last axis first; f32 result."""
+    nd = len(mats)
+    with torch.autocast(x.device.type, enabled=False):
+        y = x.float() @ mats[-1].t()                              # (N, C, ..., W_out)
+        if nd >= 2:
+            y = mats[-2] @ y                                      # (N, C, [D,] H_out, W_out)
+        if nd == 3:
+            n, c, d, h, w = y.shape
+            y = (mats[0] @ y.reshape(n * c, d, h * w)).reshape(n, c, mats[0].shape[0], h, w)
+    return y
+
+
+def adaptive_avg_pool(x, bins):
+    """nn.AdaptiveAvgPool{2,3}d(bins)(x) as separable GEMMs (x's dtype out)."""
+    mats = [_avg_pool_matrix(bins, s, x.device) for s in x.shape[2:]]
+    return _separable(x, mats).to(x.dtype)
+
+
+def upsample_align_corners(x, size):
+    """F.interpolate(x, size, mode=(bi|tri)linear, align_corners=True) as separable GEMMs (f32 out)."""
+    mats = [_lin_interp_matrix(o, i, x.device) for o, i in zip(size, x.shape[2:])]
+    return _separable(x, mats)
+
+
 class PSPModule(nn.Module):
     """seg_heads.py:18-47 (2-D) / :153-182 (3-D): adaptive-average-pool pyramid (bins 1, 2, 4, 6) -> 1x1 conv ->
     BN -> ReLU, (bi|tri)linear up-sampling (align_corners=True), concat, and a 1x1 bottleneck conv whose
@@ -450,8 +518,17 @@ class PSPModule(nn.Module):
     def forward(self, features):
         size = features.shape[2:]
         mode = "bilinear" if self.nd == 2 else "trilinear"
-        pyramids = [features] + [F.interpolate(stage(features), size=size, mode=mode, align_corners=True)
-                                 for stage in self.stages]
+        if SEPARABLE_PSP and features.is_cuda:
+            pyramids = [features]
+            for stage in self.stages:
+                y = adaptive_avg_pool(features, stage[0].output_size)
+                for m in list(stage)[1:]:
+                    y = m(y)
+                up = upsample_align_corners(y, size)
+                pyramids.append(up if up.dtype == y.dtype else up.to(y.dtype))
+        else:
+            pyramids = [features] + [F.interpolate(stage(features), size=size, mode=mode, align_corners=True)
+                                     for stage in self.stages]
         return self.bottleneck(torch.cat(pyramids, dim=1))
 
 

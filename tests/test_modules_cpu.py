@@ -138,3 +138,24 @@ def test_checkpoint_roundtrip_and_ddp_prefix(tmp_path):
     c = EncoderDecoderModel(cfg, "ViT", "ViTLinear", 1, 3)
     load_model(c, p2)
     assert torch.equal(c.encoder.norm.weight, a.encoder.norm.weight)
+
+
+def test_separable_psp_ops_match_torch():
+    """decoders.adaptive_avg_pool / upsample_align_corners (the PSP pyramid as separable GEMMs, used on the GPU)
+    equal nn.AdaptiveAvgPool / F.interpolate(align_corners=True) to f32 rounding, values and gradients."""
+    import torch.nn.functional as F
+    from long_context_biomedical_imaging_amd import decoders
+    torch.manual_seed(0)
+    for nd, shape in ((2, (2, 5, 37, 29)), (3, (1, 3, 9, 11, 13))):
+        mode = "bilinear" if nd == 2 else "trilinear"
+        pool_cls = torch.nn.AdaptiveAvgPool2d if nd == 2 else torch.nn.AdaptiveAvgPool3d
+        for b in (1, 2, 4, 6):
+            x = torch.randn(*shape, requires_grad=True)
+            x2 = x.detach().clone().requires_grad_(True)
+            ref = F.interpolate(pool_cls(b)(x), size=shape[2:], mode=mode, align_corners=True)
+            got = decoders.upsample_align_corners(decoders.adaptive_avg_pool(x2, b), shape[2:])
+            assert torch.allclose(got, ref, atol=1e-6, rtol=1e-5)
+            g = torch.randn_like(ref)
+            ref.backward(g)
+            got.backward(g)
+            assert torch.allclose(x2.grad, x.grad, atol=1e-6, rtol=1e-5)
