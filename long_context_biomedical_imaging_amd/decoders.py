@@ -532,6 +532,21 @@ class PSPModule(nn.Module):
         return self.bottleneck(torch.cat(pyramids, dim=1))
 
 
+_INTERP_DTYPE = {}
+
+
+def _interp_dtype(x, mode):
+    """The dtype F.interpolate(x, mode=mode) returns in the current autocast state (probed once on a 2x2 map)."""
+    dev = x.device.type
+    key = (x.dtype, mode, dev, torch.is_autocast_enabled(dev), torch.get_autocast_dtype(dev))
+    dt = _INTERP_DTYPE.get(key)
+    if dt is None:
+        probe = x.new_zeros((1, 1) + (2,) * (x.dim() - 2))
+        dt = F.interpolate(probe, size=(2,) * (x.dim() - 2), mode=mode, align_corners=True).dtype
+        _INTERP_DTYPE[key] = dt
+    return dt
+
+
 class FPN_fuse(nn.Module):
     """seg_heads.py:52-76 / :187-211: lateral 1x1 convs, top-down up-and-add, ONE 3x3 smoothing conv shared by
     the three levels (the reference lists the same module three times), up-sample all to the finest level,
@@ -550,13 +565,19 @@ class FPN_fuse(nn.Module):
         mode = "bilinear" if self.nd == 2 else "trilinear"
         features = list(features)
         features[1:] = [c(f) for f, c in zip(features[1:], self.conv1x1)]
-        up_add = lambda x, y: F.interpolate(x, size=y.shape[2:], mode=mode, align_corners=True) + y  # noqa: E731
-        P = [up_add(features[i], features[i - 1]) for i in reversed(range(1, len(features)))]
+        # align_corners=True re-sampling to the same size is the identity (src = dst, weights 1 / 0): skipped for
+        # the ViT taps, which all share one grid (torch still runs an interpolation kernel and an atomic backward)
+        def resize(x, size):
+            if tuple(x.shape[2:]) == tuple(size):
+                return x.to(_interp_dtype(x, mode))
+            return F.interpolate(x, size=size, mode=mode, align_corners=True)
+
+        P = [resize(features[i], features[i - 1].shape[2:]) + features[i - 1] for i in reversed(range(1, len(features)))]
         P = [sc(x) for sc, x in zip(self.smooth_conv, P)]
         P = list(reversed(P))
         P.append(features[-1])
         size = P[0].shape[2:]
-        P[1:] = [F.interpolate(f, size=size, mode=mode, align_corners=True) for f in P[1:]]
+        P[1:] = [resize(f, size) for f in P[1:]]
         return self.conv_fusion(torch.cat(P, dim=1))
 
 
