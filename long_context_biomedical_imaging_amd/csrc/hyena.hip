@@ -477,9 +477,9 @@ __global__ __launch_bounds__(256) void fft_col_inv_kernel(FftArgs a) {
 // of its butterflies into registers, barriers, then writes (Stockham order), so the buffer is half the v1 ping-pong.
 constexpr int CW_ELEMS = 8192;   // GW * n1 complex per workgroup
 
-template <int R, bool INV>
+template <int R, bool INV, int CW>
 __device__ __forceinline__ void stockham_inplace(f32x2* x, int N, int Ns, const f32x2* twl, int ld) {
-  constexpr int PER = CW_ELEMS / R / 256;   // butterflies per thread
+  constexpr int PER = CW / R / 256;   // butterflies per thread
   const int nb = N / R;
   const int tstep = N / (Ns * R);
   f32x2 v[PER][R];
@@ -511,13 +511,13 @@ __device__ __forceinline__ void stockham_inplace(f32x2* x, int N, int Ns, const 
   __syncthreads();
 }
 
-template <bool INV>
+template <bool INV, int CW>
 __device__ __forceinline__ void lds_fft_inplace(f32x2* x, int N, int lN, const f32x2* twl, int ld) {
   int Ns = 1, left = lN;
   while (left > 0) {
-    if (left >= 3 && left != 4) { stockham_inplace<8, INV>(x, N, Ns, twl, ld); Ns *= 8; left -= 3; }
-    else if (left >= 2) { stockham_inplace<4, INV>(x, N, Ns, twl, ld); Ns *= 4; left -= 2; }
-    else { stockham_inplace<2, INV>(x, N, Ns, twl, ld); Ns *= 2; left -= 1; }
+    if (left >= 3 && left != 4) { stockham_inplace<8, INV, CW>(x, N, Ns, twl, ld); Ns *= 8; left -= 3; }
+    else if (left >= 2) { stockham_inplace<4, INV, CW>(x, N, Ns, twl, ld); Ns *= 4; left -= 2; }
+    else { stockham_inplace<2, INV, CW>(x, N, Ns, twl, ld); Ns *= 2; left -= 1; }
   }
 }
 
@@ -550,7 +550,7 @@ __device__ __forceinline__ f32x2 tw3(const Tw3& w, long long e) {
 }
 
 // grid (n2 / GW, npairs_total or C); block 256. Same math as fft_col_fwd_kernel.
-template <int GW>
+template <int GW, int CW>
 __global__ __launch_bounds__(256) void fft_colw_fwd_kernel(FftArgs a) {
   extern __shared__ __attribute__((aligned(16))) f32x2 lds[];
   const int ld = a.n1 + 1;
@@ -570,7 +570,7 @@ __global__ __launch_bounds__(256) void fft_colw_fwd_kernel(FftArgs a) {
   const float* s0 = a.src + (long long)r0 * a.L;
   const float* s1 = r1 >= 0 ? a.src + (long long)r1 * a.L : nullptr;
   if ((a.L & 3) == 0) {   // 16-byte loads of 4 adjacent columns (rows are 16-B aligned, chunks all in or out)
-    constexpr int NQ = CW_ELEMS / 4;
+    constexpr int NQ = CW / 4;
     for (int base = 0; base < NQ; base += UB * 256) {
       f32x4 v0[UB], v1[UB];
 #pragma unroll
@@ -595,7 +595,7 @@ __global__ __launch_bounds__(256) void fft_colw_fwd_kernel(FftArgs a) {
       }
     }
   } else {
-    for (int base = 0; base < CW_ELEMS; base += UB * 256) {
+    for (int base = 0; base < CW; base += UB * 256) {
       f32x2 v[UB];
 #pragma unroll
       for (int u = 0; u < UB; ++u) {
@@ -616,9 +616,9 @@ __global__ __launch_bounds__(256) void fft_colw_fwd_kernel(FftArgs a) {
     }
   }
   __syncthreads();
-  lds_fft_inplace<false>(x, a.n1, a.ln1, twl, ld);
+  lds_fft_inplace<false, CW>(x, a.n1, a.ln1, twl, ld);
   f32x2* S = (a.single ? a.SK : a.S) + (long long)pid * a.n;
-  for (int idx = threadIdx.x; idx < CW_ELEMS / 2; idx += 256) {   // 16-byte stores of 2 adjacent columns
+  for (int idx = threadIdx.x; idx < CW / 2; idx += 256) {   // 16-byte stores of 2 adjacent columns
     const int g = (idx % (GW / 2)) * 2, k1 = idx / (GW / 2);
     const long long e = (long long)(c0 + g) * k1;
     const f32x2 p0 = cmul(x[g * ld + k1], tw3(tw3t, e & (a.n - 1)));
@@ -628,7 +628,7 @@ __global__ __launch_bounds__(256) void fft_colw_fwd_kernel(FftArgs a) {
 }
 
 // grid (n2 / GW, npairs_total or C); same math as fft_col_inv_kernel.
-template <int GW>
+template <int GW, int CW>
 __global__ __launch_bounds__(256) void fft_colw_inv_kernel(FftArgs a) {
   extern __shared__ __attribute__((aligned(16))) f32x2 lds[];
   const int ld = a.n1 + 1;
@@ -640,7 +640,7 @@ __global__ __launch_bounds__(256) void fft_colw_inv_kernel(FftArgs a) {
   const int pid = a.pid0 + blockIdx.y;
   const f32x2* S = (a.single ? a.SK : a.S) + (long long)pid * a.n;
   __syncthreads();   // the twiddle tables are read below
-  constexpr int NH = CW_ELEMS / 2;   // 16-byte loads of 2 adjacent columns
+  constexpr int NH = CW / 2;   // 16-byte loads of 2 adjacent columns
   for (int base = 0; base < NH; base += UB * 256) {
     f32x4 v[UB];
 #pragma unroll
@@ -661,7 +661,7 @@ __global__ __launch_bounds__(256) void fft_colw_inv_kernel(FftArgs a) {
     }
   }
   __syncthreads();
-  lds_fft_inplace<true>(x, a.n1, a.ln1, twl, ld);
+  lds_fft_inplace<true, CW>(x, a.n1, a.ln1, twl, ld);
   // only a < ceil(L / n2) rows of the column carry outputs (m < L); the rest is the discarded wrap half
   const int na = (a.L - c0 + a.n2 - 1) / a.n2;
   if (a.single) {
@@ -1491,16 +1491,25 @@ extern "C" int lci_fft_twiddles(void* tw, int n, void* stream) {
 }
 
 static int launch_col(FftArgs& a, bool inv, int nblk_y, hipStream_t s) {
-  const int gw = CW_ELEMS / a.n1;
-  if ((gw == 8 || gw == 16 || gw == 32) && a.n2 % gw == 0 && !getenv("LCI_FFT_COL_V1")) {
+  // complex elements per workgroup: 4096 (half the round-1 tile: ~130 instead of ~245 VGPRs, 4 workgroups per CU)
+  static const int cw = getenv("LCI_FFT_CW") ? atoi(getenv("LCI_FFT_CW")) : CW_ELEMS / 2;
+  const int gw = cw / a.n1;
+  if ((cw == 8192 || cw == 4096) && (gw == 4 || gw == 8 || gw == 16 || gw == 32) && a.n2 % gw == 0 &&
+      !getenv("LCI_FFT_COL_V1")) {
     const size_t sh = ((size_t)gw * (a.n1 + 1) + a.n1 + tw3_entries(a.ln1 + a.ln2)) * sizeof(f32x2);
     dim3 grid(a.n2 / gw, nblk_y);
-#define LCI_COLW(GW)                                                                                       \
-    (void)hipFuncSetAttribute((const void*)(inv ? fft_colw_inv_kernel<GW> : fft_colw_fwd_kernel<GW>),      \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                   \
-    if (inv) hipLaunchKernelGGL(fft_colw_inv_kernel<GW>, grid, dim3(256), sh, s, a);                     \
-    else hipLaunchKernelGGL(fft_colw_fwd_kernel<GW>, grid, dim3(256), sh, s, a);
-    if (gw == 32) { LCI_COLW(32) } else if (gw == 16) { LCI_COLW(16) } else { LCI_COLW(8) }
+#define LCI_COLW(GW, CW)                                                                                           \
+    (void)hipFuncSetAttribute((const void*)(inv ? fft_colw_inv_kernel<GW, CW> : fft_colw_fwd_kernel<GW, CW>),      \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                           \
+    if (inv) hipLaunchKernelGGL((fft_colw_inv_kernel<GW, CW>), grid, dim3(256), sh, s, a);                       \
+    else hipLaunchKernelGGL((fft_colw_fwd_kernel<GW, CW>), grid, dim3(256), sh, s, a);
+    if (cw == 8192) {
+      if (gw == 32) { LCI_COLW(32, 8192) } else if (gw == 16) { LCI_COLW(16, 8192) } else if (gw == 8) { LCI_COLW(8, 8192) }
+      else return 1;
+    } else {
+      if (gw == 16) { LCI_COLW(16, 4096) } else if (gw == 8) { LCI_COLW(8, 4096) } else if (gw == 4) { LCI_COLW(4, 4096) }
+      else return 1;
+    }
 #undef LCI_COLW
     LCI_LAUNCH_CHECK();
     return 0;
