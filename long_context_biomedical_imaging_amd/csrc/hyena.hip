@@ -1491,8 +1491,11 @@ extern "C" int lci_fft_twiddles(void* tw, int n, void* stream) {
 }
 
 static int launch_col(FftArgs& a, bool inv, int nblk_y, hipStream_t s) {
-  // complex elements per workgroup: 4096 (half the round-1 tile: ~130 instead of ~245 VGPRs, 4 workgroups per CU)
-  static const int cw = getenv("LCI_FFT_CW") ? atoi(getenv("LCI_FFT_CW")) : CW_ELEMS / 2;
+  // complex elements per workgroup: 4096 (~130 instead of ~245 VGPRs, 4 workgroups per CU) while that still gives
+  // >= 8 columns (32-B row segments); 8192 for n1 = 1024 (C4: 4096 would load 16-B row segments, measured 24 ms/step
+  // slower)
+  static const int env_cw = getenv("LCI_FFT_CW") ? atoi(getenv("LCI_FFT_CW")) : 0;
+  const int cw = env_cw ? env_cw : (a.n1 <= 512 ? CW_ELEMS / 2 : CW_ELEMS);
   const int gw = cw / a.n1;
   if ((cw == 8192 || cw == 4096) && (gw == 4 || gw == 8 || gw == 16 || gw == 32) && a.n2 % gw == 0 &&
       !getenv("LCI_FFT_COL_V1")) {
