@@ -19,6 +19,8 @@
  *   lci_dwconv_silu_*     MambaVisionMixer depthwise conv1d + SiLU, model/models/mamba.py:118-119
  *   lci_fftconv_*         fftconv_ref (gelu=False), model/models/hyena.py:32-51 / Filter.forward :201-216
  *   lci_hyena_pre/post_*  HyenaOperator short filter + gating, model/models/hyena.py:317-355
+ *   lci_upsample2x_*      UperNet2D.forward's final bilinear re-sampling (align_corners=False, 2x), model/models/
+ *                         seg_heads.py:138, into the head conv's channels-last bf16 operand
  *   lci_hyena_filter_*    Filter.filter (implicit-filter MLP z -> Linear/Sin x3 -> Linear, ExponentialModulation),
  *                         model/models/hyena.py:54-117,190-199, called at :343
  *   lci_conv3_fwd         MONAI-1.3 UnetResBlock 3x3(x3) convs of the ViTUNETR / SwinUNETR heads, enhance_heads.py:30-356
@@ -41,8 +43,8 @@ extern "C" {
 
 /* Bumped whenever an entry point's argument list or buffer contract changes (3: lci_layernorm_bwd gained dres;
  * 4: lci_conv3_wgrad writes one partial per voxel split instead of one per split and wave; 5: lci_linear_wgrad;
- * 6: lci_hyena_filter). */
-#define LCI_ABI_VERSION 6
+ * 6: lci_hyena_filter; 7: lci_upsample2x). */
+#define LCI_ABI_VERSION 7
 const char* lci_last_error(void);
 int lci_abi_version(void);
 /* sha256 prefix of the sources the library was built from (build_lib.source_hash); the Python binding refuses a
@@ -192,6 +194,12 @@ int lci_hyena_pre_bwd(int dtype, const void* z, const float* w, const float* bia
  * 32(c>>4>>1) + 16((c>>4)&1) + 8((c&7)>>2) + 4((c>>3)&1) + (c&3)) for the three 64x64 weight gradients,
  * dz (L, E) f32 (written), part (lci_hyena_filter_partials(L, E) f32: per-wave [2 + E][64] sums of
  * db1, dfreq, dW1[:, e] over positions, indexed by feature; the caller sums them). 1 <= E <= 8. */
+/* ------------------------------------------------------------------ bilinear 2x up-sampling (align_corners=False)
+ * fwd: x (B, C, H, W) f32 -> y (B, 2H, 2W, C) bf16 channels-last (16-B aligned); bwd: dy (B, 2H, 2W, C) bf16
+ * channels-last -> dx (B, C, H, W) f32 (written). C % 8 == 0. */
+int lci_upsample2x_fwd(const float* x, void* y, int B, int C, int H, int W, void* stream);
+int lci_upsample2x_bwd(const void* dy, float* dx, int B, int C, int H, int W, void* stream);
+
 long long lci_hyena_filter_img_elems(void);
 long long lci_hyena_filter_partials(int L, int E);
 int lci_hyena_filter_prep(const float* W1, const float* b1, const float* freq, const float* W2, const float* b2,

@@ -628,7 +628,12 @@ class UperNet2D(_UperNet):
             features = [f[:, :, 0, :, :] for f in features]
         features[-1] = self.PPN(features[-1])
         x = self.FPN(features)
-        x = F.interpolate(x, size=self.input_size, mode="bilinear")
+        if (HIP_CONV_2D and isinstance(self.head, ConvK3_2d) and kernels.upsample2x_supported(x, self.input_size)
+                and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+            # the head conv computes in bf16 from a channels-last operand: up-sample straight into it
+            x = kernels.upsample2x_bilinear_cl(x)
+        else:
+            x = F.interpolate(x, size=self.input_size, mode="bilinear")
         return torch.unsqueeze(self.head(x), 2)
 
 

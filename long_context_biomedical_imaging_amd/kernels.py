@@ -731,6 +731,42 @@ def hyena_filter(z, W1, b1, freq, W2, b2, W3, b3, W4, t, deltas, shift, L):
     return _HyenaFilter.apply(z, W1, b1, freq, W2, b2, W3, b3, W4, t, deltas, shift, int(L))
 
 
+class _Upsample2x(torch.autograd.Function):
+    """F.interpolate(x, size=2x, mode="bilinear") (align_corners=False) returned as the bf16 channels-last operand of
+    the next conv (what that conv's autocast cast produces), adjoint by gather (lci_upsample2x_fwd / _bwd)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        B, C, H, W = x.shape
+        xf = x.float().contiguous()
+        y = torch.empty(B, 2 * H, 2 * W, C, device=x.device, dtype=torch.bfloat16)
+        KernelTimer.run("upsample2x_fwd", 0.0, x, lambda: _lib.call(
+            "lci_upsample2x_fwd", xf.data_ptr(), y.data_ptr(), B, C, H, W, _lib.stream_of(x)))
+        ctx.shape = (B, C, H, W)
+        ctx.xdtype = x.dtype
+        return y.permute(0, 3, 1, 2)                      # (B, C, 2H, 2W), channels-last strides
+
+    @staticmethod
+    def backward(ctx, dy):
+        B, C, H, W = ctx.shape
+        g = dy.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
+        dx = torch.empty(B, C, H, W, device=dy.device, dtype=torch.float32)
+        KernelTimer.run("upsample2x_bwd", 0.0, dy, lambda: _lib.call(
+            "lci_upsample2x_bwd", g.data_ptr(), dx.data_ptr(), B, C, H, W, _lib.stream_of(dy)))
+        return dx.to(ctx.xdtype)
+
+
+def upsample2x_supported(x: torch.Tensor, size) -> bool:
+    return (x.is_cuda and x.dim() == 4 and tuple(size) == (2 * x.shape[2], 2 * x.shape[3]) and x.shape[1] % 8 == 0
+            and x.dtype in (torch.float32, torch.bfloat16))
+
+
+def upsample2x_bilinear_cl(x: torch.Tensor) -> torch.Tensor:
+    """Bilinear 2x up-sampling, align_corners=False (seg_heads.py:138), as bf16 with channels-last strides."""
+    _lib.require_gpu(x.contiguous())
+    return _Upsample2x.apply(x)
+
+
 # ------------------------------------------------------------------- decoder-head 3x3(x3) convolution
 def conv3_cl(x_cl: torch.Tensor, w_packed: torch.Tensor, kd: int) -> torch.Tensor:
     """x_cl (B, D, H, W, Cin) bf16 channels-last, w_packed (Cout, kd*9, Cin) bf16 -> (B, D, H, W, Cout) bf16."""

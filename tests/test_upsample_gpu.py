@@ -1,0 +1,54 @@
+"""lci_upsample2x (UperNet2D's final bilinear 2x re-sampling, seg_heads.py:138, align_corners=False) vs torch.
+
+Forward: the kernel evaluates torch's upsample_bilinear2d expression in f32 and rounds to bf16 (the head conv's
+autocast cast): compared with bf16(F.interpolate(x)) — equal up to one bf16 ulp where the f32 contraction order
+differs (plus 1e-6 max|x| absolute for cancelling sums near zero). Backward: the deterministic gather vs torch's autograd of F.interpolate on the same bf16 cotangent
+(rel-L2 <= 1e-6).
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from golden_util import rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("B,C,H,W", [(2, 64, 17, 23), (1, 384, 64, 64), (1, 8, 1, 5), (2, 136, 40, 33), (1, 96, 96, 7)])
+def test_upsample2x_vs_torch(B, C, H, W):
+    from long_context_biomedical_imaging_amd import kernels
+    torch.manual_seed(B * 1000 + C + H + W)
+    x = torch.randn(B, C, H, W, device="cuda")
+    assert kernels.upsample2x_supported(x, (2 * H, 2 * W))
+    xr = x.clone().requires_grad_(True)
+    ref = F.interpolate(xr, size=(2 * H, 2 * W), mode="bilinear")
+    xc = x.clone().requires_grad_(True)
+    y = kernels.upsample2x_bilinear_cl(xc)
+    assert y.shape == ref.shape and y.dtype == torch.bfloat16
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    diff = (y.float() - ref.detach().to(torch.bfloat16).float()).abs()
+    # one bf16 ulp, plus the f32 contraction difference (fma vs mul+add) on cancelling sums of O(1) inputs
+    ulp = ref.detach().abs() * 2.0 ** -7 + 1e-6 * x.abs().max()
+    assert bool((diff <= ulp).all()), diff.max().item()
+    g = torch.randn_like(ref).to(torch.bfloat16)
+    ref.backward(g.float())
+    y.backward(g)
+    assert rel_err(xc.grad, xr.grad) < 1e-6
+
+
+def test_upernet2d_head_path_matches_interpolate(monkeypatch):
+    """UperNet2D.forward under autocast: the fused up-sampling into the head conv vs F.interpolate + the same conv."""
+    from long_context_biomedical_imaging_amd import decoders, kernels
+    torch.manual_seed(0)
+    head = decoders.ConvK3_2d(64, 2, kernel_size=3, padding=1).cuda()
+    x = torch.randn(1, 64, 48, 40, device="cuda")
+    outs = []
+    for fused in (False, True):
+        xi = x.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            u = kernels.upsample2x_bilinear_cl(xi) if fused else F.interpolate(xi, size=(96, 80), mode="bilinear")
+            o = head(u)
+        o.float().pow(2).sum().backward()
+        outs.append((o.float(), xi.grad.clone()))
+    assert rel_err(outs[1][0], outs[0][0]) < 1e-3
+    assert rel_err(outs[1][1], outs[0][1]) < 1e-2
