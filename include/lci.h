@@ -29,6 +29,7 @@
  *   lci_layernorm_*       TransformerBlock / SwinTransformerBlock norm1, norm2 (nn.LayerNorm, backbone_vit.py:250-262,
  *                         backbone_swin.py:418,431) + the autocast cast
  *                         of its output to the next Linear's bf16 operand
+ *   lci_gelu_*            MONAI MLPBlock's nn.GELU() between linear1 and linear2 (backbone_vit.py:249) under autocast
  *   lci_linear_*          the token-wise nn.Linear GEMMs: MLPBlock linear1 + GELU + linear2 with fused epilogues
  *                         (backbone_vit.py:249, MONAI MLPBlock) and the weight / bias gradient of (SABlock qkv / out_proj
  *                         backbone_vit.py:166-167, MONAI MLPBlock linear1/2, MambaVisionMixer in/x/dt/out_proj
@@ -43,8 +44,8 @@ extern "C" {
 
 /* Bumped whenever an entry point's argument list or buffer contract changes (3: lci_layernorm_bwd gained dres;
  * 4: lci_conv3_wgrad writes one partial per voxel split instead of one per split and wave; 5: lci_linear_wgrad;
- * 6: lci_hyena_filter; 7: lci_upsample2x). */
-#define LCI_ABI_VERSION 7
+ * 6: lci_hyena_filter; 7: lci_upsample2x; 8: lci_gelu). */
+#define LCI_ABI_VERSION 8
 const char* lci_last_error(void);
 int lci_abi_version(void);
 /* sha256 prefix of the sources the library was built from (build_lib.source_hash); the Python binding refuses a
@@ -264,6 +265,9 @@ int lci_linear_small_fwd(const void* x, long long ldx, const void* w, const void
                          int K, void* stream);
 int lci_linear_small_bwd(const void* x, long long ldx, const void* w, const void* dy, void* dx, float* part,
                          long long M, int N, int K, void* stream);
+/* GELU (erf) of n bf16 elements (n % 8 == 0, 16-B aligned): y = gelu(x); dx = dy * gelu'(x). */
+int lci_gelu_fwd(const void* x, void* y, long long n, void* stream);
+int lci_gelu_bwd(const void* x, const void* dy, void* dx, long long n, void* stream);
 int lci_linear_fwd(int epilogue, const void* x, long long ldx, const void* w, const void* bias, void* y,
                    long long ldy, void* aux, long long ldaux, long long M, int N, int K, void* stream);
 

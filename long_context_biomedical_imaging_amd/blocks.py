@@ -97,8 +97,9 @@ class MLPBlock(nn.Module):
                 and kernels.mlp_supported(x, D, H)):
             # fused HIP path (kernels.mlp): GEMM epilogues carry bias + GELU forward and GELU' backward
             return kernels.mlp(x, self.linear1.weight, self.linear1.bias, self.linear2.weight, self.linear2.bias)
-        x = self.drop1(self.fn(self.linear1(x)))
-        return self.drop2(self.linear2(x))
+        h = self.linear1(x)
+        h = kernels.gelu(h) if kernels.gelu_supported(h) else self.fn(h)
+        return self.drop2(self.linear2(self.drop1(h)))
 
 
 class PatchEmbeddingBlock(nn.Module):

@@ -731,6 +731,37 @@ def hyena_filter(z, W1, b1, freq, W2, b2, W3, b3, W4, t, deltas, shift, L):
     return _HyenaFilter.apply(z, W1, b1, freq, W2, b2, W3, b3, W4, t, deltas, shift, int(L))
 
 
+class _GELU(torch.autograd.Function):
+    """nn.GELU() (erf) on a contiguous bf16 tensor: lci_gelu_fwd / _bwd, torch's arithmetic, bf16 results."""
+
+    @staticmethod
+    def forward(ctx, x):
+        y = torch.empty_like(x)
+        KernelTimer.run("gelu_fwd", 0.0, x, lambda: _lib.call(
+            "lci_gelu_fwd", x.data_ptr(), y.data_ptr(), x.numel(), _lib.stream_of(x)))
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dy = dy.to(torch.bfloat16).contiguous()
+        dx = torch.empty_like(x)
+        KernelTimer.run("gelu_bwd", 0.0, x, lambda: _lib.call(
+            "lci_gelu_bwd", x.data_ptr(), dy.data_ptr(), dx.data_ptr(), x.numel(), _lib.stream_of(x)))
+        return dx
+
+
+def gelu_supported(x: torch.Tensor) -> bool:
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and x.numel() % 8 == 0 and x.numel() > 0
+            and x.data_ptr() % 16 == 0)
+
+
+def gelu(x: torch.Tensor) -> torch.Tensor:
+    """F.gelu(x) (approximate='none') for contiguous bf16 CUDA tensors on the HIP kernels."""
+    return _GELU.apply(x)
+
+
 class _Upsample2x(torch.autograd.Function):
     """F.interpolate(x, size=2x, mode="bilinear") (align_corners=False) returned as the bf16 channels-last operand of
     the next conv (what that conv's autocast cast produces), adjoint by gather (lci_upsample2x_fwd / _bwd)."""

@@ -228,3 +228,50 @@ def test_conv_up_gemm_grads(nd, Cin, Cout, k):
     for name, a, r in zip(("y", "dx", "dW", "db"), res[0], res[1]):
         e = ((a.double() - r.double()).norm() / r.double().norm()).item()
         assert e < 1e-2, f"{name}: rel-L2 {e:.3e}"
+
+
+def test_gelu_kernel_matches_torch_bf16():
+    """lci_gelu_fwd / _bwd vs torch's bf16 GELU (approximate='none') and its autograd: torch's f32 opmath
+    expression with the same erff / expf, so the bf16 results agree bitwise (one bf16 ulp allowed where the f32
+    contraction order could round differently)."""
+    from long_context_biomedical_imaging_amd import kernels
+    torch.manual_seed(0)
+    x = torch.randn(3, 1000, 1536, device="cuda") * 3
+    x.view(-1)[:8] = torch.tensor([0.0, -0.0, 1e-30, -1e-30, 20.0, -20.0, 6.5, -6.5])
+    x = x.to(torch.bfloat16)
+    assert kernels.gelu_supported(x)
+    xr = x.clone().requires_grad_(True)
+    ref = torch.nn.functional.gelu(xr)
+    xc = x.clone().requires_grad_(True)
+    y = kernels.gelu(xc)
+    ulp = ref.detach().float().abs() * 2.0 ** -7 + 1e-30
+    assert bool(((y.float() - ref.detach().float()).abs() <= ulp).all())
+    assert (y == ref).float().mean().item() > 0.999
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    y.backward(g)
+    ulp = xr.grad.float().abs() * 2.0 ** -7 + 1e-30
+    assert bool(((xc.grad.float() - xr.grad.float()).abs() <= ulp).all())
+    assert (xc.grad == xr.grad).float().mean().item() > 0.999
+
+
+def test_gelu_kernel_exhaustive_bf16():
+    """Every finite bf16 input (|x| < 1e4): the HIP GELU (forward, and backward with a unit cotangent) within one bf16
+    ulp of torch's and bitwise equal for > 99.5 % of the inputs."""
+    from long_context_biomedical_imaging_amd import kernels
+    bits = torch.arange(0, 65536, dtype=torch.int32).to(torch.int16)
+    x = bits.view(torch.bfloat16).cuda()
+    x = x[torch.isfinite(x.float()) & (x.float().abs() < 1e4)].contiguous()
+    x = x[: x.numel() // 8 * 8].contiguous()
+    ref = torch.nn.functional.gelu(x)
+    y = kernels.gelu(x)
+    d = (y.float() - ref.float()).abs()
+    assert bool((d <= ref.float().abs() * 2.0 ** -7 + 1e-37).all())
+    assert (y != ref).float().mean().item() < 5e-3
+    xr = x.clone().requires_grad_(True)
+    torch.nn.functional.gelu(xr).backward(torch.ones_like(x))
+    xc = x.clone().requires_grad_(True)
+    kernels.gelu(xc).backward(torch.ones_like(x))
+    d = (xc.grad.float() - xr.grad.float()).abs()
+    assert bool((d <= xr.grad.float().abs() * 2.0 ** -7 + 1e-37).all())
+    assert (xc.grad != xr.grad).float().mean().item() < 5e-3
