@@ -44,8 +44,9 @@ extern "C" {
 
 /* Bumped whenever an entry point's argument list or buffer contract changes (3: lci_layernorm_bwd gained dres;
  * 4: lci_conv3_wgrad writes one partial per voxel split instead of one per split and wave; 5: lci_linear_wgrad;
- * 6: lci_hyena_filter; 7: lci_upsample2x; 8: lci_gelu). */
-#define LCI_ABI_VERSION 8
+ * 6: lci_hyena_filter; 7: lci_upsample2x; 8: lci_gelu;
+ * 9: lci_layernorm_add_fwd). */
+#define LCI_ABI_VERSION 9
 const char* lci_last_error(void);
 int lci_abi_version(void);
 /* sha256 prefix of the sources the library was built from (build_lib.source_hash); the Python binding refuses a
@@ -235,6 +236,11 @@ int lci_patch_embed_bwd(const void* x, int x_dtype, const void* dy, int dy_dtype
 int lci_layernorm_bwd_blocks(long long rows);
 int lci_layernorm_fwd(const float* x, const float* gamma, const float* beta, void* y, int bf16_out, float* mean,
                       float* rstd, long long rows, int C, float eps, void* stream);
+/* xsum = h + add (f32; add bf16 if add_bf16 else f32), y = LayerNorm(xsum) as lci_layernorm_fwd (mean / rstd of xsum):
+ * the block's mid residual add fused into norm2; the backward is lci_layernorm_bwd on xsum. */
+int lci_layernorm_add_fwd(const float* h, const void* add, int add_bf16, float* xsum, const float* gamma,
+                          const float* beta, void* y, int bf16_out, float* mean, float* rstd, long long rows, int C,
+                          float eps, void* stream);
 int lci_layernorm_bwd(const float* x, const void* dy, int bf16_dy, const float* gamma, const float* mean,
                       const float* rstd, const float* dres, float* dx, float* part, long long rows, int C,
                       void* stream);

@@ -132,8 +132,7 @@ class TransformerBlock(nn.Module):
         # x + attn(norm1(x)); x + mlp(norm2(x)) (backbone_vit.py:261-262), the residual gradient of each added
         # inside the LayerNorm backward kernel
         h, y = self.norm1.forward_residual(x)
-        x = h + self.attn(y)
-        h, y = self.norm2.forward_residual(x)
+        h, y = self.norm2.forward_residual_add(h, self.attn(y))   # x + attn(.) summed inside the norm2 kernel
         x = h + self.mlp(y)
         return x
 

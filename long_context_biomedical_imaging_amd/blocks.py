@@ -48,6 +48,10 @@ class TokenLayerNorm(nn.LayerNorm):
     def forward(self, x):
         return kernels.layer_norm(x, self.weight, self.bias, self.eps, self._bf16_out())
 
+    def forward_residual_add(self, h, a):
+        """(h + a, self(h + a)) with the residual add inside the LayerNorm forward kernel."""
+        return kernels.add_residual_layer_norm(h, a, self.weight, self.bias, self.eps, self._bf16_out())
+
     def forward_residual(self, x):
         """(x, self(x)) for a residual block x + f(self(x)); the backward adds the residual gradient inside the
         LayerNorm kernel (one pass over the residual stream fewer)."""

@@ -31,6 +31,9 @@ struct LnArgs {
   float* mean;          // (rows)
   float* rstd;          // (rows)
   float* part;          // bwd: (gridDim.x, 2, C) partial dgamma, dbeta
+  const void* add;      // fwd: (rows, C) bf16 or f32 branch output added to x first (x + add is normalised), or null
+  float* xsum;          // fwd with add: (rows, C) f32 x + add, the next residual stream
+  int add_bf16;
   long long rows;
   int C, bf16_io;
   float eps;
@@ -63,6 +66,12 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnArgs a) {
   for (int k = 0; k < NV; ++k) {
     const int c = 4 * lane + 256 * k;
     v[k] = c < C ? *(const f32x4*)(xr + c) : f32x4{};
+    if (a.add && c < C) {   // residual add of the block's branch output (the f32 sum torch's add produces)
+      const f32x4 t = ld_io4(a.add, row * C + c, a.add_bf16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[k][j] += t[j];
+      *(f32x4*)(a.xsum + row * C + c) = v[k];
+    }
     s += (v[k][0] + v[k][1]) + (v[k][2] + v[k][3]);
   }
   const float mean = wave_sum(s) / C;
@@ -208,6 +217,29 @@ extern "C" int lci_layernorm_fwd(const float* x, const float* gamma, const float
   if (rows == 0) return 0;
   LnArgs a = {};
   a.x = x; a.gamma = gamma; a.beta = beta; a.y = y; a.mean = mean; a.rstd = rstd;
+  a.rows = rows; a.C = C; a.bf16_io = bf16_out; a.eps = eps;
+  const long long nb = (rows + 3) / 4;
+  LCI_CHECK(nb < (1LL << 31), "layernorm: too many rows");
+  const int NV = (C + 255) / 256;
+  hipStream_t s = (hipStream_t)stream;
+  LN_SWITCH(ln_fwd_kernel, NV, dim3((unsigned)nb), s, a);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+
+// xsum = h + add (f32; add bf16 or f32), y = LayerNorm(xsum): the mid-block residual add fused into norm2.
+extern "C" int lci_layernorm_add_fwd(const float* h, const void* add, int add_bf16, float* xsum, const float* gamma,
+                                     const float* beta, void* y, int bf16_out, float* mean, float* rstd, long long rows,
+                                     int C, float eps, void* stream) {
+  if (ln_check(rows, C, h)) return 1;
+  LCI_CHECK(add && xsum && ((uintptr_t)add & (add_bf16 ? 7 : 15)) == 0 && ((uintptr_t)xsum & 15) == 0,
+            "layernorm_add: misaligned or missing branch / sum");
+  LCI_CHECK(((uintptr_t)gamma & 15) == 0 && ((uintptr_t)beta & 15) == 0 &&
+            ((uintptr_t)y & (bf16_out ? 7 : 15)) == 0, "layernorm: misaligned gamma/beta/output");
+  if (rows == 0) return 0;
+  LnArgs a = {};
+  a.x = h; a.add = add; a.add_bf16 = add_bf16; a.xsum = xsum;
+  a.gamma = gamma; a.beta = beta; a.y = y; a.mean = mean; a.rstd = rstd;
   a.rows = rows; a.C = C; a.bf16_io = bf16_out; a.eps = eps;
   const long long nb = (rows + 3) / 4;
   LCI_CHECK(nb < (1LL << 31), "layernorm: too many rows");

@@ -1058,6 +1058,57 @@ class _ResidualLayerNorm(torch.autograd.Function):
         return dx, dw, db, None, None
 
 
+class _AddResidualLayerNorm(torch.autograd.Function):
+    """(x, y) = (h + a, LN(h + a)) for the middle of a block `h + a -> norm2 -> ...`: the residual add runs inside
+    the LN forward kernel (no separate add pass), the backward is the residual LN backward on x (dh = dx,
+    da = dx in a's dtype)."""
+
+    @staticmethod
+    def forward(ctx, h, a, weight, bias, eps, bf16_out):
+        C = h.shape[-1]
+        h2 = h.reshape(-1, C)
+        a2 = a.reshape(-1, C)
+        rows = h2.shape[0]
+        xsum = torch.empty(rows, C, device=h.device, dtype=torch.float32)
+        y = torch.empty(h.shape, device=h.device, dtype=torch.bfloat16 if bf16_out else torch.float32)
+        mean = torch.empty(rows, device=h.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        KernelTimer.run("ln_add_fwd", rows * C * (8 + a.element_size() + y.element_size()), h, lambda: _lib.call(
+            "lci_layernorm_add_fwd", h2.data_ptr(), a2.data_ptr(), int(a.dtype == torch.bfloat16), xsum.data_ptr(),
+            weight.data_ptr(), bias.data_ptr(), y.data_ptr(), int(bf16_out), mean.data_ptr(), rstd.data_ptr(), rows,
+            C, float(eps), _lib.stream_of(h)))
+        ctx.save_for_backward(xsum, weight, mean, rstd)
+        ctx.shape = h.shape
+        ctx.adtype = a.dtype
+        ctx.set_materialize_grads(False)
+        return xsum.view(h.shape), y
+
+    @staticmethod
+    def backward(ctx, dx_out, dy):
+        xsum, weight, mean, rstd = ctx.saved_tensors
+        if dy is None:
+            dx, dw, db = dx_out, None, None
+        else:
+            dx, dw, db = _ln_bwd(xsum, weight, mean, rstd, dy, dx_out, ctx.shape)
+        if dx is None:
+            return None, None, None, None, None, None
+        return dx, dx.to(ctx.adtype), dw, db, None, None
+
+
+def add_residual_layer_norm(h, a, weight, bias, eps, bf16_out):
+    """(h + a, layer_norm(h + a)) with the add inside the HIP LN forward; h f32, a bf16 / f32 of h's shape."""
+    h = _ln_checks(h, weight, bias)
+    ok = (ln_kernel_supports(h.shape[-1]) and a.shape == h.shape and a.dtype in (torch.bfloat16, torch.float32)
+          and a.is_cuda)
+    if ok:
+        a = a.contiguous()
+        ok = a.data_ptr() % 16 == 0
+    if not ok:
+        x = h + a
+        return residual_layer_norm(x, weight, bias, eps, bf16_out)
+    return _AddResidualLayerNorm.apply(h, a, weight, bias, eps, bf16_out)
+
+
 def _ln_checks(x, weight, bias):
     _lib.require_gpu(weight, bias)
     if not x.is_cuda:

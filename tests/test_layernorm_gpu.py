@@ -126,3 +126,33 @@ def test_swin_large_stage4_block():
         y = blk(x, None)
     y.float().square().mean().backward()
     assert y.shape == x.shape and torch.isfinite(x.grad).all()
+
+
+@pytest.mark.parametrize("adtype", [torch.float32, torch.bfloat16])
+def test_add_residual_layernorm(adtype):
+    """(x, y) = add_residual_layer_norm(h, a): x = h + a computed in the LN forward kernel (bitwise torch's f32
+    add), y = LN(x) as layer_norm; gradients of h, a, gamma, beta on a block (h + a) + f(LN(h + a)) against fp64
+    torch autograd (rel-L2 <= 1e-5), a's gradient in a's dtype."""
+    from long_context_biomedical_imaging_amd import kernels
+    torch.manual_seed(11)
+    rows, C = 2051, 384
+    h = (torch.randn(rows, C) * 2).cuda()
+    a = torch.randn(rows, C).cuda().to(adtype)
+    w = (1 + 0.1 * torch.randn(C)).cuda()
+    b = (0.1 * torch.randn(C)).cuda()
+    P = (torch.randn(C, C) / C ** 0.5).cuda()
+    cot = torch.randn(rows, C).cuda()
+    hr, ar, wr, br = [t.double().requires_grad_(True) for t in (h, a.float(), w, b)]
+    xr = hr + ar
+    yr = F.layer_norm(xr, (C,), wr, br, 1e-5)
+    (((xr + yr @ P.double()) * cot.double()).sum()).backward()
+    hc, ac, wc, bc = [t.clone().requires_grad_(True) for t in (h, a, w, b)]
+    x, y = kernels.add_residual_layer_norm(hc, ac, wc, bc, 1e-5, False)
+    assert torch.equal(x, h + a)
+    assert rel_err(y, F.layer_norm(h + a, (C,), w, b, 1e-5)) < 1e-6
+    (((x + y @ P) * cot).sum()).backward()
+    assert ac.grad.dtype == adtype
+    assert rel_err(hc.grad, hr.grad) < 1e-5
+    assert rel_err(ac.grad, ar.grad) < (1e-5 if adtype == torch.float32 else 1e-2)
+    assert rel_err(wc.grad, wr.grad) < 1e-5
+    assert rel_err(bc.grad, br.grad) < 1e-5
