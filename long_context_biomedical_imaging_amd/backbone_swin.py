@@ -250,6 +250,11 @@ class SwinTransformerBlock(nn.Module):
             x = torch.utils.checkpoint.checkpoint(self.forward_part1, x, mask_matrix, use_reentrant=False)
         else:
             x = self.forward_part1(x, mask_matrix)
+        if (not self.use_checkpoint and isinstance(self.drop_path, nn.Identity) and x.is_cuda
+                and isinstance(self.norm2, TokenLayerNorm)):
+            # shortcut + attention summed inside the norm2 LayerNorm kernel (one pass over the stream fewer)
+            x, y = self.norm2.forward_residual_add(shortcut, x)
+            return x + self.mlp(y)
         x = shortcut + self.drop_path(x)
         if self.use_checkpoint:
             x = x + torch.utils.checkpoint.checkpoint(self.forward_part2, x, use_reentrant=False)
