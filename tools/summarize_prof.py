@@ -24,7 +24,7 @@ from collections import defaultdict
 
 def short(name):
     for key in ("attn_fwd", "attn_bwd_dkdv", "attn_bwd_dq", "attn_bwd_delta", "patch_embed", "scan", "window", "fft_",
-                "fftconv", "hyena", "dwconv", "conv3", "inorm", "ln_fwd", "ln_bwd", "linear_"):
+                "fftconv", "hyena", "dwconv", "conv3", "inorm", "ln_fwd", "ln_bwd", "linear_", "gelu_", "upsample2x", "hf_"):
         if key in name:
             return name.split("(")[0].replace("void ", "")
     return None
