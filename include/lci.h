@@ -45,8 +45,8 @@ extern "C" {
 /* Bumped whenever an entry point's argument list or buffer contract changes (3: lci_layernorm_bwd gained dres;
  * 4: lci_conv3_wgrad writes one partial per voxel split instead of one per split and wave; 5: lci_linear_wgrad;
  * 6: lci_hyena_filter; 7: lci_upsample2x; 8: lci_gelu;
- * 9: lci_layernorm_add_fwd). */
-#define LCI_ABI_VERSION 9
+ * 9: lci_layernorm_add_fwd; 10: lci_upsample2x_nhwc). */
+#define LCI_ABI_VERSION 10
 const char* lci_last_error(void);
 int lci_abi_version(void);
 /* sha256 prefix of the sources the library was built from (build_lib.source_hash); the Python binding refuses a
@@ -201,6 +201,9 @@ int lci_hyena_pre_bwd(int dtype, const void* z, const float* w, const float* bia
  * channels-last -> dx (B, C, H, W) f32 (written). C % 8 == 0. */
 int lci_upsample2x_fwd(const float* x, void* y, int B, int C, int H, int W, void* stream);
 int lci_upsample2x_bwd(const void* dy, float* dx, int B, int C, int H, int W, void* stream);
+/* the same for a channels-last input map: x (B, H, W, C) f32 -> y (B, 2H, 2W, C) bf16; dy -> dx (B, H, W, C) f32 */
+int lci_upsample2x_nhwc_fwd(const float* x, void* y, int B, int C, int H, int W, void* stream);
+int lci_upsample2x_nhwc_bwd(const void* dy, float* dx, int B, int C, int H, int W, void* stream);
 
 long long lci_hyena_filter_img_elems(void);
 long long lci_hyena_filter_partials(int L, int E);

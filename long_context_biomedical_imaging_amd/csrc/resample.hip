@@ -12,6 +12,8 @@
 // with contiguous 16-byte (channels-last) or row-coalesced (NCHW) vectors.
 #include "common.hpp"
 
+#include <algorithm>
+
 namespace lci {
 
 struct UpArgs {
@@ -121,6 +123,79 @@ __global__ __launch_bounds__(256) void upsample2x_bwd_kernel(UpArgs a) {
   }
 }
 
+
+// Channels-last (NHWC) variants, for a channels-last input map: x (B, H, W, C) f32 -> y (B, 2H, 2W, C) bf16, and
+// dy (B, 2H, 2W, C) bf16 -> dx (B, H, W, C) f32. One thread per (pixel, 8-channel chunk): the chunks of a pixel
+// are consecutive threads, so every tap is a contiguous 32-byte (f32) or 16-byte (bf16) access.
+__global__ __launch_bounds__(256) void upsample2x_nhwc_fwd_kernel(UpArgs a) {
+  const int C8 = a.C / 8, W2 = 2 * a.W, H2 = 2 * a.H;
+  const long long total = (long long)a.B * H2 * W2 * C8;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int q = (int)(i % C8);
+    long long p = i / C8;
+    const int ox = (int)(p % W2);
+    p /= W2;
+    const int oy = (int)(p % H2), b = (int)(p / H2);
+    int h0, h1, w0, w1;
+    float hl0, hl1, wl0, wl1;
+    up_taps(oy, a.H, h0, h1, hl0, hl1);
+    up_taps(ox, a.W, w0, w1, wl0, wl1);
+    const float* base = a.x + (long long)b * a.H * a.W * a.C + 8 * q;
+    const float* p00 = base + ((long long)h0 * a.W + w0) * a.C;
+    const float* p01 = base + ((long long)h0 * a.W + w1) * a.C;
+    const float* p10 = base + ((long long)h1 * a.W + w0) * a.C;
+    const float* p11 = base + ((long long)h1 * a.W + w1) * a.C;
+    bf16x8 v;
+#pragma unroll
+    for (int hv = 0; hv < 2; ++hv) {
+      const f32x4 x00 = *(const f32x4*)(p00 + 4 * hv), x01 = *(const f32x4*)(p01 + 4 * hv);
+      const f32x4 x10 = *(const f32x4*)(p10 + 4 * hv), x11 = *(const f32x4*)(p11 + 4 * hv);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        v[4 * hv + k] = (bf16)(hl0 * (wl0 * x00[k] + wl1 * x01[k]) + hl1 * (wl0 * x10[k] + wl1 * x11[k]));
+    }
+    *(bf16x8*)(a.y + (((long long)b * H2 + oy) * W2 + ox) * a.C + 8 * q) = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void upsample2x_nhwc_bwd_kernel(UpArgs a) {
+  const int C8 = a.C / 8, W2 = 2 * a.W, H2 = 2 * a.H;
+  const long long total = (long long)a.B * a.H * a.W * C8;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int q = (int)(i % C8);
+    long long p = i / C8;
+    const int ix = (int)(p % a.W);
+    p /= a.W;
+    const int iy = (int)(p % a.H), b = (int)(p / a.H);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ty = 0; ty < 4; ++ty) {
+      const int oy = 2 * iy - 1 + ty;
+      if (oy < 0 || oy >= H2) continue;
+      const float wy = up_weight(oy, a.H, iy);
+      if (wy == 0.f) continue;
+#pragma unroll
+      for (int tx = 0; tx < 4; ++tx) {
+        const int ox = 2 * ix - 1 + tx;
+        if (ox < 0 || ox >= W2) continue;
+        const float w = wy * up_weight(ox, a.W, ix);
+        if (w == 0.f) continue;
+        const bf16x8 g = *(const bf16x8*)(a.dy + (((long long)b * H2 + oy) * W2 + ox) * a.C + 8 * q);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] = fmaf(w, (float)g[k], acc[k]);
+      }
+    }
+    float* o = a.dx + (((long long)b * a.H + iy) * a.W + ix) * a.C + 8 * q;
+    *(f32x4*)o = f32x4{acc[0], acc[1], acc[2], acc[3]};
+    *(f32x4*)(o + 4) = f32x4{acc[4], acc[5], acc[6], acc[7]};
+  }
+}
+
+static unsigned up_grid(long long items) {
+  const long long want = (items + 255) / 256;
+  return (unsigned)std::max(1LL, std::min(want, 256LL * 64));
+}
+
 }  // namespace lci
 
 using namespace lci;
@@ -143,6 +218,29 @@ extern "C" int lci_upsample2x_bwd(const void* dy, float* dx, int B, int C, int H
   a.dy = (const bf16*)dy; a.dx = dx; a.B = B; a.C = C; a.H = H; a.W = W;
   dim3 grid((W + UP_JB - 1) / UP_JB, H, B * ((C + UP_CB - 1) / UP_CB));
   hipLaunchKernelGGL(upsample2x_bwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+
+// Channels-last variants: x (B, H, W, C) f32 -> y (B, 2H, 2W, C) bf16; dy (B, 2H, 2W, C) bf16 -> dx (B, H, W, C) f32.
+extern "C" int lci_upsample2x_nhwc_fwd(const float* x, void* y, int B, int C, int H, int W, void* stream) {
+  LCI_CHECK(B > 0 && C > 0 && H > 0 && W > 0 && C % 8 == 0, "upsample2x: bad shape B=%d C=%d H=%d W=%d", B, C, H, W);
+  LCI_CHECK(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0, "upsample2x: pointers must be 16-byte aligned");
+  UpArgs a{};
+  a.x = x; a.y = (bf16*)y; a.B = B; a.C = C; a.H = H; a.W = W;
+  hipLaunchKernelGGL(upsample2x_nhwc_fwd_kernel, dim3(up_grid((long long)B * 4 * H * W * (C / 8))), dim3(256), 0,
+                     (hipStream_t)stream, a);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int lci_upsample2x_nhwc_bwd(const void* dy, float* dx, int B, int C, int H, int W, void* stream) {
+  LCI_CHECK(B > 0 && C > 0 && H > 0 && W > 0 && C % 8 == 0, "upsample2x: bad shape B=%d C=%d H=%d W=%d", B, C, H, W);
+  LCI_CHECK(((uintptr_t)dy & 15) == 0 && ((uintptr_t)dx & 15) == 0, "upsample2x: pointers must be 16-byte aligned");
+  UpArgs a{};
+  a.dy = (const bf16*)dy; a.dx = dx; a.B = B; a.C = C; a.H = H; a.W = W;
+  hipLaunchKernelGGL(upsample2x_nhwc_bwd_kernel, dim3(up_grid((long long)B * H * W * (C / 8))), dim3(256), 0,
+                     (hipStream_t)stream, a);
   LCI_LAUNCH_CHECK();
   return 0;
 }

@@ -383,7 +383,8 @@ class ConvK3_2d(nn.Conv2d):
     def forward(self, x):
         if not HIP_CONV_2D:
             return super().forward(x)
-        return kernels.conv3(x, self.weight, self.bias).contiguous()
+        y = kernels.conv3(x, self.weight, self.bias)
+        return y if _is_cl(x) else y.contiguous()   # channels-last in -> channels-last out (UPERNET_CL)
 
 
 class ConvPoint(nn.Conv3d):
@@ -399,6 +400,14 @@ class ConvPoint(nn.Conv3d):
 class ConvPoint_2d(nn.Conv2d):
     def forward(self, x):
         p = self.padding[0]
+        if _is_cl(x):   # channels-last map (UPERNET_CL): the GEMM reads it in place, the zero border goes on after
+            if p and self.bias is not None:
+                x = F.pad(x.permute(0, 2, 3, 1), (0, 0, p, p, p, p)).permute(0, 3, 1, 2)
+                p = 0
+            y = _pointwise(x, self.weight, self.bias)
+            if p:   # no bias: the border of a 1x1 conv of a zero-padded map is zero
+                y = F.pad(y.permute(0, 2, 3, 1), (0, 0, p, p, p, p)).permute(0, 3, 1, 2)
+            return y
         if p:
             x = F.pad(x, (p,) * 4)
         return _pointwise(x, self.weight, self.bias).contiguous()
@@ -437,6 +446,44 @@ def _bn(nd, c):
 # (13.7 ms per stage at 512^2 x 96 channels, C4) and its adaptive-pool backward takes ~10 ms per stage.
 SEPARABLE_PSP = os.environ.get("LCI_SEPARABLE_PSP", "1") != "0"
 _SEP_CACHE = {}
+
+# UperNet2D on ViT taps keeps the big maps channels-last end to end (the token taps already are): no NCHW copies of
+# the 512^2 x 384-1536 maps at C4. The PSP's pooled 1-36 pixel maps stay NCHW (torch's ROCm batch_norm crashed on
+# channels-last views of 1x1 maps).
+UPERNET_CL = os.environ.get("LCI_UPERNET_CL", "1") != "0"
+
+
+def _is_cl(x):
+    """A 4-D map in channels-last memory that is not also plain-contiguous (and big enough to matter)."""
+    return (UPERNET_CL and x.dim() == 4 and x.shape[2] * x.shape[3] > 64 and not x.is_contiguous()
+            and x.is_contiguous(memory_format=torch.channels_last))
+
+
+def _cat_channels(ts):
+    """torch.cat(ts, dim=1); channels-last maps are concatenated as NHWC (one channels-last result, no copies)."""
+    if all(_is_cl(t) for t in ts):
+        return torch.cat([t.permute(0, 2, 3, 1) for t in ts], dim=-1).permute(0, 3, 1, 2)
+    return torch.cat(ts, dim=1)
+
+
+def _pool_cl(x, bins):
+    """adaptive average pooling of a channels-last (B, C, H, W) map: GEMMs over the NHWC layout, NCHW result."""
+    B, C, H, W = x.shape
+    ah, aw = _avg_pool_matrix(bins, H, x.device), _avg_pool_matrix(bins, W, x.device)
+    with torch.autocast(x.device.type, enabled=False):
+        t = ah @ x.float().permute(0, 2, 3, 1).reshape(B, H, W * C)           # (B, b, W C)
+        t = aw @ t.reshape(B * bins, W, C)                                     # (B b, b, C)
+    return t.reshape(B, bins, bins, C).permute(0, 3, 1, 2).contiguous().to(x.dtype)
+
+
+def _up_cl(y, size):
+    """align_corners=True up-sampling of a small NCHW map into a channels-last (B, C, H, W) f32 map."""
+    B, C, bh, bw = y.shape
+    uh, uw = _lin_interp_matrix(size[0], bh, y.device), _lin_interp_matrix(size[1], bw, y.device)
+    with torch.autocast(y.device.type, enabled=False):
+        t = uw @ y.float().permute(0, 2, 3, 1).reshape(B * bh, bw, C)          # (B bh, W, C)
+        t = uh @ t.reshape(B, bh, size[1] * C)                                 # (B, H, W C)
+    return t.reshape(B, size[0], size[1], C).permute(0, 3, 1, 2)
 
 
 def _lin_interp_matrix(out_size, in_size, device):
@@ -518,6 +565,15 @@ class PSPModule(nn.Module):
     def forward(self, features):
         size = features.shape[2:]
         mode = "bilinear" if self.nd == 2 else "trilinear"
+        if SEPARABLE_PSP and features.is_cuda and self.nd == 2 and _is_cl(features):
+            pyramids = [features]
+            for stage in self.stages:
+                y = _pool_cl(features, stage[0].output_size)
+                for m in list(stage)[1:]:
+                    y = m(y)
+                up = _up_cl(y, size)
+                pyramids.append(up if up.dtype == y.dtype else up.to(y.dtype))
+            return self.bottleneck(_cat_channels(pyramids))
         if SEPARABLE_PSP and features.is_cuda:
             pyramids = [features]
             for stage in self.stages:
@@ -578,7 +634,7 @@ class FPN_fuse(nn.Module):
         P.append(features[-1])
         size = P[0].shape[2:]
         P[1:] = [resize(f, size) for f in P[1:]]
-        return self.conv_fusion(torch.cat(P, dim=1))
+        return self.conv_fusion(_cat_channels(P))
 
 
 class _UperNet(nn.Module):
@@ -604,8 +660,10 @@ class _UperNet(nn.Module):
             self.proj_axes = (0, nd + 1) + tuple(d + 1 for d in range(nd))
 
     def _reshape_vit_output(self, x):
-        x = x.view([x.size(0)] + list(self.feat_size) + [x.shape[-1]])
-        return x.permute(self.proj_axes).contiguous()   # NCHW: UperNet's BatchNorm / pooling / interpolation paths
+        x = x.view([x.size(0)] + list(self.feat_size) + [x.shape[-1]]).permute(self.proj_axes)
+        if self.nd == 2 and UPERNET_CL and x.is_cuda:
+            return x   # the token taps are channels-last already (see UPERNET_CL)
+        return x.contiguous()   # NCHW: UperNet's BatchNorm / pooling / interpolation paths
 
     def freeze_bn(self):
         for module in self.modules():

@@ -769,18 +769,30 @@ class _Upsample2x(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x):
         B, C, H, W = x.shape
-        xf = x.float().contiguous()
+        nhwc = x.dim() == 4 and not x.is_contiguous() and x.is_contiguous(memory_format=torch.channels_last)
         y = torch.empty(B, 2 * H, 2 * W, C, device=x.device, dtype=torch.bfloat16)
-        KernelTimer.run("upsample2x_fwd", 0.0, x, lambda: _lib.call(
-            "lci_upsample2x_fwd", xf.data_ptr(), y.data_ptr(), B, C, H, W, _lib.stream_of(x)))
+        if nhwc:   # channels-last input map: read it in place
+            xf = x.float().permute(0, 2, 3, 1).contiguous()
+            KernelTimer.run("upsample2x_fwd", 0.0, x, lambda: _lib.call(
+                "lci_upsample2x_nhwc_fwd", xf.data_ptr(), y.data_ptr(), B, C, H, W, _lib.stream_of(x)))
+        else:
+            xf = x.float().contiguous()
+            KernelTimer.run("upsample2x_fwd", 0.0, x, lambda: _lib.call(
+                "lci_upsample2x_fwd", xf.data_ptr(), y.data_ptr(), B, C, H, W, _lib.stream_of(x)))
         ctx.shape = (B, C, H, W)
         ctx.xdtype = x.dtype
+        ctx.nhwc = nhwc
         return y.permute(0, 3, 1, 2)                      # (B, C, 2H, 2W), channels-last strides
 
     @staticmethod
     def backward(ctx, dy):
         B, C, H, W = ctx.shape
         g = dy.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
+        if ctx.nhwc:
+            dx = torch.empty(B, H, W, C, device=dy.device, dtype=torch.float32)
+            KernelTimer.run("upsample2x_bwd", 0.0, dy, lambda: _lib.call(
+                "lci_upsample2x_nhwc_bwd", g.data_ptr(), dx.data_ptr(), B, C, H, W, _lib.stream_of(dy)))
+            return dx.permute(0, 3, 1, 2).to(ctx.xdtype)
         dx = torch.empty(B, C, H, W, device=dy.device, dtype=torch.float32)
         KernelTimer.run("upsample2x_bwd", 0.0, dy, lambda: _lib.call(
             "lci_upsample2x_bwd", g.data_ptr(), dx.data_ptr(), B, C, H, W, _lib.stream_of(dy)))
@@ -794,7 +806,8 @@ def upsample2x_supported(x: torch.Tensor, size) -> bool:
 
 def upsample2x_bilinear_cl(x: torch.Tensor) -> torch.Tensor:
     """Bilinear 2x up-sampling, align_corners=False (seg_heads.py:138), as bf16 with channels-last strides."""
-    _lib.require_gpu(x.contiguous())
+    if not x.is_cuda:
+        raise _lib.LciError("upsample2x runs on the GPU only; there is no CPU path")
     return _Upsample2x.apply(x)
 
 

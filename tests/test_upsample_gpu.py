@@ -36,6 +36,23 @@ def test_upsample2x_vs_torch(B, C, H, W):
     assert rel_err(xc.grad, xr.grad) < 1e-6
 
 
+@pytest.mark.parametrize("B,C,H,W", [(2, 64, 17, 23), (1, 384, 64, 64)])
+def test_upsample2x_channels_last_input(B, C, H, W):
+    """A channels-last input map takes the NHWC kernels (lci_upsample2x_nhwc_*): same results as the NCHW path."""
+    from long_context_biomedical_imaging_amd import kernels
+    torch.manual_seed(C + H)
+    x = torch.randn(B, C, H, W, device="cuda")
+    g = torch.randn(B, C, 2 * H, 2 * W, device="cuda").to(torch.bfloat16)
+    outs = []
+    for cl in (False, True):
+        xi = (x.contiguous(memory_format=torch.channels_last) if cl else x.clone()).requires_grad_(True)
+        y = kernels.upsample2x_bilinear_cl(xi)
+        y.backward(g)
+        outs.append((y.float(), xi.grad.float()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert rel_err(outs[1][1], outs[0][1]) < 1e-6
+
+
 def test_upernet2d_head_path_matches_interpolate(monkeypatch):
     """UperNet2D.forward under autocast: the fused up-sampling into the head conv vs F.interpolate + the same conv."""
     from long_context_biomedical_imaging_amd import decoders, kernels
