@@ -681,18 +681,26 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv16_kernel(AttnAr
 
   TileRegs<NT> qr, dr;
   const int nqt = (L + KT - 1) / KT;
-  auto stage_rowc = [&](int buf, int qt) __attribute__((always_inline)) {
+  // Row constants of a query tile: thread tid < 128 owns one (-lse2 | -delta, query) entry. Loaded into a register
+  // at the top of the previous tile's iteration with the Q / dO tiles, written to LDS at its end: a load issued at
+  // the end would put a full memory latency in front of every tile's barrier.
+  // The load is unconditional (clamped index) so no exec-masked join makes the compiler wait for it early; the
+  // out-of-range substitutions happen at the LDS write.
+  const float* rcp = (tid / KT) == 1 ? dlp : lsep;
+  auto load_rowc = [&](int qt) __attribute__((always_inline)) -> float {
+    return rcp[min(qt * KT + tid % KT, L - 1)];
+  };
+  auto stage_rowc = [&](int buf, int qt, float v) __attribute__((always_inline)) {
     if (tid < 2 * KT) {
-      const int which = tid / KT, qi = tid % KT, q = qt * KT + qi;
-      rowc[buf][which][qi] = which == 0 ? ((q < L) ? -lsep[q] : -1.0e30f)   // invalid rows: P = 0
-                                        : ((q < L) ? -dlp[q] : 0.f);
+      const bool ok = qt * KT + tid % KT < L;
+      rowc[buf][tid / KT][tid % KT] = ok ? -v : (tid < KT ? -1.0e30f : 0.f);   // invalid rows: P = 0
     }
   };
   qr.load(qp, a.rs_q, 0, L, tid);
   dr.load(dop, a.rs_do, 0, L, tid);
   qr.store_sw(smem, tid);
   dr.store_sw(smem + KT * LD_SW, tid);
-  stage_rowc(0, 0);
+  stage_rowc(0, 0, load_rowc(0));
   __syncthreads();
 
   f32x4 dv[4][2], dk[4][2];   // [d block][key block]: lane holds rows d = 16db + 4g + i, column key c16
@@ -704,9 +712,11 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv16_kernel(AttnAr
     const int buf = qt & 1;
     const bf16* ql = smem + buf * TILE;
     const bf16* dl = ql + KT * LD_SW;
+    float rc_next = 0.f;
     if (qt + 1 < nqt) {
       qr.load(qp, a.rs_q, (qt + 1) * KT, L, tid);
       dr.load(dop, a.rs_do, (qt + 1) * KT, L, tid);
+      rc_next = load_rowc(qt + 1);
     }
 #if LCI_D16_IGLP >= 0
     __builtin_amdgcn_iglp_opt(LCI_D16_IGLP);
@@ -769,7 +779,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv16_kernel(AttnAr
       bf16* nb = smem + (buf ^ 1) * TILE;
       qr.store_sw(nb, tid);
       dr.store_sw(nb + KT * LD_SW, tid);
-      stage_rowc(buf ^ 1, qt + 1);
+      stage_rowc(buf ^ 1, qt + 1, rc_next);
     }
     __syncthreads();
   }
