@@ -46,7 +46,7 @@ extern "C" {
  * 4: lci_conv3_wgrad writes one partial per voxel split instead of one per split and wave; 5: lci_linear_wgrad;
  * 6: lci_hyena_filter; 7: lci_upsample2x; 8: lci_gelu;
  * 9: lci_layernorm_add_fwd; 10: lci_upsample2x_nhwc). */
-#define LCI_ABI_VERSION 10
+#define LCI_ABI_VERSION 11
 const char* lci_last_error(void);
 int lci_abi_version(void);
 /* sha256 prefix of the sources the library was built from (build_lib.source_hash); the Python binding refuses a
@@ -166,13 +166,16 @@ long long lci_fft_size(int L);
 int lci_fft_twiddles(void* tw, int n, void* stream);
 /* K (C, n) complex f32 = filter spectra (scaled by 1/n); SK (C, n) complex scratch. */
 int lci_fftconv_spectrum(const float* k, void* K, void* SK, const void* tw, int C, int L, void* stream);
-/* y = causal_conv(u, k) + D u; S: (C*ceil(R/2), n) complex scratch. */
-int lci_fftconv_fwd(const float* u, const void* K, const float* Dv, float* y, void* S, const void* tw, int R,
-                    int C, int L, void* stream);
+/* y = causal_conv(u, k) + D u; S: (C*ceil(R/2), n) complex scratch. Su (optional, same shape): receives the
+ * column spectra of u, left intact for lci_fftconv_bwd (ABI 11). */
+int lci_fftconv_fwd(const float* u, const void* K, const float* Dv, float* y, void* S, void* Su, const void* tw,
+                    int R, int C, int L, void* stream);
 /* du = corr(dy, k) + D dy (written); dk (C, L) = sum_rows corr(dy, u) (written, optional); dD accumulated
- * (optional). S, S2: (C*ceil(R/2), n) complex scratch (S2 only with dk); SK: (C, n) complex scratch. */
+ * (optional). S, S2: (C*ceil(R/2), n) complex scratch (S2 only with dk and no Su); Su: the forward's kept
+ * column spectra of u (optional: skips their recomputation); SK: (C, n) complex scratch. */
 int lci_fftconv_bwd(const float* dy, const float* u, const void* K, const float* Dv, float* du, float* dk,
-                    float* dD, void* S, void* S2, void* SK, const void* tw, int R, int C, int L, void* stream);
+                    float* dD, void* S, void* S2, const void* Su, void* SK, const void* tw, int R, int C, int L,
+                    void* stream);
 /* z (BB, L, 3D) channels-last in_proj output; causal depthwise conv (w (3D, K), bias (3D)); per head h,
  * x1/x2/v = conv channels [h*3hd, +hd), [+hd, +2hd), [+2hd, +3hd). vg = v*x1 -> (BB, D, L) f32 rows;
  * x2 -> (BB, L, D) channels-last (z dtype). */

@@ -37,6 +37,7 @@ struct FftArgs {
   float* dst;                           // output rows
   const f32x2* tw;                      // W_n^t, t < n
   f32x2* S; f32x2* S2;                  // scratch (npairs_total, n) complex
+  f32x2* So;                            // row pass output when not in place (forward with a kept input spectrum)
   f32x2* K;                             // filter spectra (C, n) in [k1][k2] layout (already / n)
   f32x2* SK;                            // dk scratch (C, n)
   const float* Dv;                      // (C) or null
@@ -273,7 +274,7 @@ __global__ __launch_bounds__(512) void fft_row_kernel(FftArgs a) {
     f32x2* rx = lds_fft<true>(fx, gx, N, a.ln2, cnt, twl, N);
     for (int i = threadIdx.x; i < cnt * N; i += blockDim.x) {
       const int q = i / N, e = i - q * N;
-      a.S[((long long)j * a.P + p0 + q) * a.n + (long long)k1 * N + e] = rx[i];
+      (a.So ? a.So : a.S)[((long long)j * a.P + p0 + q) * a.n + (long long)k1 * N + e] = rx[i];
     }
     __syncthreads();
   }
@@ -359,6 +360,7 @@ __global__ __launch_bounds__(256) void fft_row512_kernel(FftArgs a) {
 #pragma unroll
   for (int r = 0; r < 8; ++r) kr[r] = a.K[(long long)j * a.n + row + 64 * r];
   const bool two = a.mode == 2 && a.SK;
+  f32x2* so = a.So ? a.So : a.S;
   f32x2 acc[8];
 #pragma unroll
   for (int r = 0; r < 8; ++r) acc[r] = f32x2{0.f, 0.f};
@@ -380,7 +382,7 @@ __global__ __launch_bounds__(256) void fft_row512_kernel(FftArgs a) {
     for (int r = 0; r < 8; ++r) v[r] = a.mode == 1 ? cmul(v[r], kr[r]) : cmulc(v[r], kr[r]);
     fft512_wave<true>(v, buf, twl, L);
 #pragma unroll
-    for (int r = 0; r < 8; ++r) a.S[off + 64 * r] = v[r];
+    for (int r = 0; r < 8; ++r) so[off + 64 * r] = v[r];
   }
   if (!two) return;
   __syncthreads();
@@ -1574,20 +1576,26 @@ extern "C" int lci_fftconv_spectrum(const float* k, void* K, void* SK, const voi
 }
 
 // y = causal_conv(u, k) + D u for rows (R, C, L) f32; filter j = row % C. S: (C * ceil(R/2), n) scratch.
-extern "C" int lci_fftconv_fwd(const float* u, const void* K, const float* Dv, float* y, void* S, const void* tw,
-                               int R, int C, int L, void* stream) {
+// Su (optional, same shape as S): receives the column spectra of u and is left intact (the row pass writes its
+// products to S), so the backward's filter gradient reuses it instead of recomputing the column FFT of u.
+extern "C" int lci_fftconv_fwd(const float* u, const void* K, const float* Dv, float* y, void* S, void* Su,
+                               const void* tw, int R, int C, int L, void* stream) {
   FftArgs a{};
   if (fft_plan(a, L)) return 1;
-  a.src = u; a.dst = y; a.K = (f32x2*)K; a.S = (f32x2*)S; a.tw = (const f32x2*)tw; a.Dv = Dv;
+  a.src = u; a.dst = y; a.K = (f32x2*)K; a.tw = (const f32x2*)tw; a.Dv = Dv;
   a.R = R; a.C = C; a.P = (R + 1) / 2; a.single = 0; a.mode = 1;
   hipStream_t s = (hipStream_t)stream;
   const int jc = fft_chunk(C, (long long)a.P * a.n * 8);
   for (int j0 = 0; j0 < C; j0 += jc) {
     const int nj = std::min(jc, C - j0);
     a.pid0 = j0 * a.P;
+    a.S = (f32x2*)(Su ? Su : S);
     if (launch_col(a, false, nj * a.P, s)) return 3;
     a.pid0 = j0;
+    a.So = Su ? (f32x2*)S : nullptr;
     if (launch_row(a, nj, s)) return 3;
+    a.So = nullptr;
+    a.S = (f32x2*)S;
     a.pid0 = j0 * a.P;
     if (launch_col(a, true, nj * a.P, s)) return 3;
   }
@@ -1595,13 +1603,15 @@ extern "C" int lci_fftconv_fwd(const float* u, const void* K, const float* Dv, f
 }
 
 // Adjoint: du = corr(dy, k) + D dy; dk (C, L) = sum_rows corr(dy, u) (overwritten); dD (C) accumulated.
-// S, S2: (C * ceil(R/2), n) scratch; SK: (C, n) scratch.
+// S, S2: (C * ceil(R/2), n) scratch; SK: (C, n) scratch. Su: the forward's kept column spectra of u, or null (then
+// S2 receives them here).
 extern "C" int lci_fftconv_bwd(const float* dy, const float* u, const void* K, const float* Dv, float* du, float* dk,
-                               float* dD, void* S, void* S2, void* SK, const void* tw, int R, int C, int L,
-                               void* stream) {
+                               float* dD, void* S, void* S2, const void* Su, void* SK, const void* tw, int R, int C,
+                               int L, void* stream) {
   FftArgs a{};
   if (fft_plan(a, L)) return 1;
-  a.tw = (const f32x2*)tw; a.K = (f32x2*)K; a.S = (f32x2*)S; a.S2 = (f32x2*)S2; a.SK = dk ? (f32x2*)SK : nullptr;
+  a.tw = (const f32x2*)tw; a.K = (f32x2*)K; a.S = (f32x2*)S; a.S2 = (f32x2*)(Su ? Su : S2);
+  a.SK = dk ? (f32x2*)SK : nullptr;
   a.R = R; a.C = C; a.P = (R + 1) / 2; a.Dv = Dv; a.dk = dk;
   hipStream_t s = (hipStream_t)stream;
   const int jc = fft_chunk(C, (long long)a.P * a.n * 8 * (dk ? 2 : 1));
@@ -1612,7 +1622,7 @@ extern "C" int lci_fftconv_bwd(const float* dy, const float* u, const void* K, c
     c.src = dy;
     c.pid0 = j0 * a.P;
     if (launch_col(c, false, nj * a.P, s)) return 3;         // S <- col FFT of dy pairs
-    if (dk) {
+    if (dk && !Su) {
       FftArgs b = c;
       b.S = (f32x2*)S2; b.src = u;
       if (launch_col(b, false, nj * a.P, s)) return 3;       // S2 <- col FFT of u pairs

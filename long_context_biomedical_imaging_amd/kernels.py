@@ -1,6 +1,8 @@
 """torch.autograd wrappers over the liblci C-ABI. Each op runs the HIP kernels; none has a CPU path."""
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib
@@ -513,6 +515,9 @@ def _spectrum(k):
     return K
 
 
+_KEEP_U_SPECTRUM = os.environ.get("LCI_FFT_KEEP_SPECTRUM", "1") != "0"
+
+
 class _FFTConv(torch.autograd.Function):
     """y = causal_conv(u, k) + D u along L for rows (R, C, L) f32; filter = channel index."""
 
@@ -526,16 +531,19 @@ class _FFTConv(torch.autograd.Function):
         tw = _twiddles(n, u.device)
         y = torch.empty_like(u)
         S = torch.empty(C * ((R + 1) // 2), n, 2, device=u.device, dtype=torch.float32)
+        # column spectra of u kept for the filter gradient (one column pass fewer in the backward), when k needs one
+        Su = torch.empty_like(S) if (ctx.needs_input_grad[1] and _KEEP_U_SPECTRUM) else None
         KernelTimer.run("fftconv_fwd", float(R * C * L), u, lambda: _lib.call(
-            "lci_fftconv_fwd", u.data_ptr(), K.data_ptr(), Dv.data_ptr(), y.data_ptr(), S.data_ptr(), tw.data_ptr(),
-            R, C, L, _lib.stream_of(u)))
-        ctx.save_for_backward(u, K, Dv)
+            "lci_fftconv_fwd", u.data_ptr(), K.data_ptr(), Dv.data_ptr(), y.data_ptr(), S.data_ptr(), _lib.ptr(Su),
+            tw.data_ptr(), R, C, L, _lib.stream_of(u)))
+        del S
+        ctx.save_for_backward(u, K, Dv, Su)
         ctx.kdtype = k.dtype
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        u, K, Dv = ctx.saved_tensors
+        u, K, Dv, Su = ctx.saved_tensors
         R, C, L = u.shape
         n = K.shape[1]
         tw = _twiddles(n, u.device)
@@ -547,12 +555,12 @@ class _FFTConv(torch.autograd.Function):
         dD = torch.zeros(C, device=u.device, dtype=torch.float32) if want_d else None
         P = (R + 1) // 2
         S = torch.empty(C * P, n, 2, device=u.device, dtype=torch.float32)
-        S2 = torch.empty(C * P, n, 2, device=u.device, dtype=torch.float32) if want_k else None
+        S2 = torch.empty(C * P, n, 2, device=u.device, dtype=torch.float32) if (want_k and Su is None) else None
         SK = torch.empty(C, n, 2, device=u.device, dtype=torch.float32) if want_k else None
         KernelTimer.run("fftconv_bwd", float(R * C * L), u, lambda: _lib.call(
             "lci_fftconv_bwd", dy.data_ptr(), u.data_ptr(), K.data_ptr(), Dv.data_ptr(), du.data_ptr(),
-            _lib.ptr(dk), _lib.ptr(dD), S.data_ptr(), _lib.ptr(S2), _lib.ptr(SK), tw.data_ptr(), R, C, L,
-            _lib.stream_of(u)))
+            _lib.ptr(dk), _lib.ptr(dD), S.data_ptr(), _lib.ptr(S2), _lib.ptr(Su if want_k else None), _lib.ptr(SK),
+            tw.data_ptr(), R, C, L, _lib.stream_of(u)))
         return du, (dk.to(ctx.kdtype) if dk is not None else None), dD
 
 

@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
     lib = ctypes.CDLL(_lib.LIB_PATH)
     for name in _declared():
         assert hasattr(lib, name), f"{name} declared in include/lci.h but not exported"
-    assert _lib.load().lci_abi_version() == _lib.ABI_VERSION == 10
+    assert _lib.load().lci_abi_version() == _lib.ABI_VERSION == 11
 
 
 def test_python_binding_arity_matches_header():
