@@ -742,21 +742,40 @@ __global__ __launch_bounds__(256) void fft_colw_inv_kernel(FftArgs a) {
   }
 }
 
-// dD[j] += sum_rows sum_t a[row][t] * b[row][t] over rows of filter j (block partial + atomic)
+// dD[j] += sum_rows sum_t a[row][t] * b[row][t] over rows of filter j (block partial + one atomic per block).
+// grid (rows, splits): a block takes a contiguous span of its row; 16-byte loads when the rows allow them.
+constexpr int RD_SPAN = 16384;   // elements per block
 __global__ __launch_bounds__(256) void row_dot_kernel(const float* x, const float* y, float* out, int L, int C,
-                                                      int R) {
-  __shared__ float red[256];
+                                                      int vec) {
+  __shared__ float red[4];
   const int row = blockIdx.x;   // r_outer * C + j
   const int j = row % C;
+  const long long base = (long long)row * L;
+  const int t0 = blockIdx.y * RD_SPAN, t1 = min(L, t0 + RD_SPAN);
   float acc = 0.f;
-  for (int t = threadIdx.x; t < L; t += 256) acc = fmaf(x[(long long)row * L + t], y[(long long)row * L + t], acc);
-  red[threadIdx.x] = acc;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-    __syncthreads();
+  if (vec) {   // L % 4 == 0 and 16-byte aligned rows
+    const f32x4* xv = (const f32x4*)(x + base);
+    const f32x4* yv = (const f32x4*)(y + base);
+    int i = t0 / 4 + threadIdx.x;
+    for (; i + 768 < t1 / 4; i += 1024) {
+      const f32x4 a0 = xv[i], a1 = xv[i + 256], a2 = xv[i + 512], a3 = xv[i + 768];
+      const f32x4 b0 = yv[i], b1 = yv[i + 256], b2 = yv[i + 512], b3 = yv[i + 768];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc += (a0[q] * b0[q] + a1[q] * b1[q]) + (a2[q] * b2[q] + a3[q] * b3[q]);
+    }
+    for (; i < t1 / 4; i += 256) {
+      const f32x4 a0 = xv[i], b0 = yv[i];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc = fmaf(a0[q], b0[q], acc);
+    }
+  } else {
+    for (int t = t0 + threadIdx.x; t < t1; t += 256) acc = fmaf(x[base + t], y[base + t], acc);
   }
-  if (threadIdx.x == 0) atomicAdd(out + j, red[0]);
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out + j, (red[0] + red[1]) + (red[2] + red[3]));
 }
 
 __global__ void twiddle_kernel(f32x2* tw, int n) {
@@ -1641,7 +1660,9 @@ extern "C" int lci_fftconv_bwd(const float* dy, const float* u, const void* K, c
     }
   }
   if (dD) {
-    hipLaunchKernelGGL(row_dot_kernel, dim3(R * C), dim3(256), 0, s, dy, u, dD, L, C, R);
+    const int vec = (L % 4 == 0) && ((uintptr_t)dy & 15) == 0 && ((uintptr_t)u & 15) == 0;
+    hipLaunchKernelGGL(row_dot_kernel, dim3(R * C, (L + RD_SPAN - 1) / RD_SPAN), dim3(256), 0, s, dy, u, dD, L, C,
+                       vec);
     LCI_LAUNCH_CHECK();
   }
   return 0;
