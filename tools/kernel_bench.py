@@ -81,6 +81,9 @@ def bench_window():
     g = torch.randn_like(o)
     emit("window_attn_fwd+bwd", timeit(lambda: torch.autograd.grad(run(), qkv, g)), 3 * f, "TFLOP/s",
          "same, fwd+bwd (rpb grad off)")
+    rpb.requires_grad_(True)
+    emit("window_attn_fwd+bwd+drpb", timeit(lambda: torch.autograd.grad(run(), [qkv, rpb], g)), 3 * f, "TFLOP/s",
+         "same, fwd+bwd with the rpb gradient (dS tiles + window reduction)")
 
 
 def bench_scan(L, B=2, Dx=192):

@@ -13,7 +13,7 @@ Directory layouts: tools/profile_bench.sh (trace/, fetch/, write/) or tools/gpu_
 pmc_WRITE_SIZE/, pmc_SQ_WAVES/). The SQ pass gives, per kernel (MI355X_MICROARCH.md §rocprofv3 PMC slots,
 per-instruction constants): cycles = GRBM_GUI_ACTIVE / 8 (summed over the 8 XCDs), MFMA busy =
 SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x cycles), VALU busy = 4 SQ_ACTIVE_INST_VALU (quad-cycles) / (1024 x cycles),
-executed MFMA FLOP = SQ_INSTS_MFMA x 32768 (v_mfma_f32_32x32x16_bf16; other shapes make this an upper bound),
+executed MFMA FLOP = SQ_INSTS_MFMA x 32768 (v_mfma_f32_32x32x16_bf16; x 16384 for the 16x16x32 attention kernels),
 effective clock = cycles / duration.
 """
 import csv
@@ -58,7 +58,8 @@ def sq_summary(d, skip_frac):
         a["cyc"] += cyc
         a["mfma"] += c["SQ_VALU_MFMA_BUSY_CYCLES"]
         a["valu"] += 4 * c["SQ_ACTIVE_INST_VALU"]
-        a["flop"] += 32768 * c["SQ_INSTS_MFMA"]
+        # FLOP per MFMA instruction: 16x16x32 kernels (the *16 attention kernels) 16384, 32x32x16 32768
+        a["flop"] += (16384 if ("dkdv16" in k[1] or "dq16" in k[1] or "fwd16" in k[1]) else 32768) * c["SQ_INSTS_MFMA"]
     out = {}
     for n, a in acc.items():
         out[n] = {"n": int(a["n"]), "ms": a["ns"] / a["n"] / 1e6, "clock": a["cyc"] / a["ns"],
