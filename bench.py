@@ -153,7 +153,7 @@ def profiled_traffic(kernel: str):
     with open(path) as f:
         prof = json.load(f)
     for name, d in prof.get("kernels", {}).items():
-        if re.search(re.escape(kernel) + r"2?_kernel", name) or name.endswith(kernel):
+        if re.search(re.escape(kernel) + r"\d*_kernel", name) or name.endswith(kernel):
             return int(d["read_bytes"] + d["write_bytes"])
     return None
 
