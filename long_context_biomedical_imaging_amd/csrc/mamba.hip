@@ -162,7 +162,43 @@ __device__ __forceinline__ void lds_row8(const float* p, float (&v)[SCAN_N]) {
 
 // ---------------------------------------------------------------------------------- forward chunk pass
 // MODE 0: zero initial state -> xend, sdt. MODE 1: xinit -> y (+ checkpoints).
+// PFN: software-pipelined loads. Each group's u / dt loads are issued one group ahead and the next staging
+// block's B / C rows one block ahead (held in registers, written to LDS after the block). On gfx950 vmcnt counts
+// stores too, so without this the wait for a group's loads also waits for the previous group's y / checkpoint
+// stores, and the B / C staging load latency is exposed once per SB steps.
 template <typename T, int MODE>
+__device__ __forceinline__ void scan_fwd_step(const ScanArgs& a, float (&x)[SCAN_N], const float (&A2)[SCAN_N],
+                                              float bias, float Dd, float uv, float drv, const float* row, int t,
+                                              bool valid, int d, float* ckb, const Col<T>& ycol, float& sumdt) {
+  if (MODE == 1 && a.write_ckpt && ((t & (CKPT - 1)) == 0) && valid) {
+    float* cp = (ckb + (long long)(t / CKPT) * a.Dx * SCAN_N) + d * SCAN_N;
+    *(f32x4*)cp = f32x4{x[0], x[1], x[2], x[3]};
+    *(f32x4*)(cp + 4) = f32x4{x[4], x[5], x[6], x[7]};
+  }
+  float Bv[SCAN_N];
+  lds_row8(row, Bv);
+  const float dt = softplus(drv + bias);
+  const float dtu = dt * uv;
+  float e[SCAN_N];
+  decay8(dt, A2, e);
+#pragma unroll
+  for (int n = 0; n < SCAN_N; ++n) x[n] = fmaf(e[n], x[n], dtu * Bv[n]);
+  if (MODE == 1) {
+    float Cv[SCAN_N];
+    lds_row8(row + 8, Cv);
+    float y0 = Dd * uv, y1 = 0.f;
+#pragma unroll
+    for (int n = 0; n < SCAN_N; n += 2) {
+      y0 = fmaf(Cv[n], x[n], y0);
+      y1 = fmaf(Cv[n + 1], x[n + 1], y1);
+    }
+    ycol.st(t, y0 + y1);
+  } else {
+    sumdt += dt;
+  }
+}
+
+template <typename T, int MODE, bool PFN>
 __global__ __launch_bounds__(256) void scan_fwd_kernel(ScanArgs a) {
   __shared__ __attribute__((aligned(16))) float bcl[4][SB * BCS];
   // wave index made provably uniform: chunk / step indices then live in SGPRs (scalar address arithmetic)
@@ -191,51 +227,78 @@ __global__ __launch_bounds__(256) void scan_fwd_kernel(ScanArgs a) {
   float* bc = bcl[wv];
   const int t0 = chunk * a.Tc, t1 = min(a.L, t0 + a.Tc);
   float sumdt = 0.f;
-  for (int tsb = t0; tsb < t1; tsb += SB) {
-    stage_bc<T, MODE == 1>(a, bc, Bp, Cp, tsb, t1, lane);
-    const int tse = min(t1, tsb + SB);
-    for (int tb = tsb; tb < tse; tb += PF) {
-      float uf[PF], dr[PF];
+  if constexpr (!PFN) {
+    for (int tsb = t0; tsb < t1; tsb += SB) {
+      stage_bc<T, MODE == 1>(a, bc, Bp, Cp, tsb, t1, lane);
+      const int tse = min(t1, tsb + SB);
+      for (int tb = tsb; tb < tse; tb += PF) {
+        float uf[PF], dr[PF];
 #pragma unroll
-      for (int i = 0; i < PF; ++i) {        // the group's u / dt loads first (clamped, branch-free)
-        const int t = min(tb + i, tse - 1);
+        for (int i = 0; i < PF; ++i) {        // the group's u / dt loads first (clamped, branch-free)
+          const int t = min(tb + i, tse - 1);
+          uf[i] = ucol.ld(t);
+          dr[i] = dcol.ld(t);
+        }
+        const int nvalid = tse - tb;   // >= PF except in a chunk's ragged tail
+#pragma unroll
+        for (int i = 0; i < PF; ++i)
+          if (i < nvalid)
+            scan_fwd_step<T, MODE>(a, x, A2, bias, Dd, uf[i], dr[i], bc + (tb + i - tsb) * BCS, tb + i, valid, d,
+                                   ckb, ycol, sumdt);
+      }
+    }
+  } else {
+    // two register sets for the u / dt groups (even / odd group of the chunk) and one for the next B / C rows
+    float ua[PF], da[PF], ub[PF], db[PF];
+    auto load_group = [&](int tb, float (&uf)[PF], float (&dr)[PF]) {
+#pragma unroll
+      for (int i = 0; i < PF; ++i) {
+        const int t = min(tb + i, t1 - 1);   // clamped, branch-free; past the chunk end the values are unused
         uf[i] = ucol.ld(t);
         dr[i] = dcol.ld(t);
       }
-      const int nvalid = tse - tb;   // >= PF except in a chunk's ragged tail
+    };
+    auto run_group = [&](int tb, int tsb, const float (&uf)[PF], const float (&dr)[PF]) {
+      const int nvalid = t1 - tb;
 #pragma unroll
-      for (int i = 0; i < PF; ++i) {
-        if (i < nvalid) {
-          const int t = tb + i;
-          if (MODE == 1 && a.write_ckpt && ((t & (CKPT - 1)) == 0) && valid) {
-            float* cp = (ckb + (long long)(t / CKPT) * a.Dx * SCAN_N) + d * SCAN_N;
-            *(f32x4*)cp = f32x4{x[0], x[1], x[2], x[3]};
-            *(f32x4*)(cp + 4) = f32x4{x[4], x[5], x[6], x[7]};
-          }
-          const float* row = bc + (t - tsb) * BCS;
-          float Bv[SCAN_N];
-          lds_row8(row, Bv);
-          const float dt = softplus(dr[i] + bias);
-          const float dtu = dt * uf[i];
-          float e[SCAN_N];
-          decay8(dt, A2, e);
-#pragma unroll
-          for (int n = 0; n < SCAN_N; ++n) x[n] = fmaf(e[n], x[n], dtu * Bv[n]);
-          if (MODE == 1) {
-            float Cv[SCAN_N];
-            lds_row8(row + 8, Cv);
-            float y0 = Dd * uf[i], y1 = 0.f;
-#pragma unroll
-            for (int n = 0; n < SCAN_N; n += 2) {
-              y0 = fmaf(Cv[n], x[n], y0);
-              y1 = fmaf(Cv[n + 1], x[n + 1], y1);
-            }
-            ycol.st(t, y0 + y1);
-          } else {
-            sumdt += dt;
-          }
+      for (int i = 0; i < PF; ++i)
+        if (i < nvalid)
+          scan_fwd_step<T, MODE>(a, x, A2, bias, Dd, uf[i], dr[i], bc + (tb + i - tsb) * BCS, tb + i, valid, d,
+                                 ckb, ycol, sumdt);
+    };
+    Row8<T> rb, rc;
+    auto load_rows = [&](int tsb) {
+      const long long t = min(tsb + lane, t1 - 1);
+      rb.load(Bp + t * a.tB);
+      if constexpr (MODE == 1) rc.load(Cp + t * a.tC);
+    };
+    auto store_rows = [&]() {
+      float* dst = bc + lane * BCS;
+      *(f32x4*)dst = f32x4{rb[0], rb[1], rb[2], rb[3]};
+      *(f32x4*)(dst + 4) = f32x4{rb[4], rb[5], rb[6], rb[7]};
+      if constexpr (MODE == 1) {
+        *(f32x4*)(dst + 8) = f32x4{rc[0], rc[1], rc[2], rc[3]};
+        *(f32x4*)(dst + 12) = f32x4{rc[4], rc[5], rc[6], rc[7]};
+      }
+      __builtin_amdgcn_wave_barrier();
+    };
+    load_rows(t0);
+    load_group(t0, ua, da);
+    store_rows();
+    for (int tsb = t0; tsb < t1; tsb += SB) {
+      const int tse = min(t1, tsb + SB);
+      if (tse < t1) load_rows(tse);           // next block's rows, written to LDS after this block's steps
+      // SB / PF = 8 groups per block (even count): the two register sets alternate without copies
+      for (int tb = tsb; tb < tse; tb += 2 * PF) {
+        load_group(tb + PF, ub, db);
+        run_group(tb, tsb, ua, da);
+        if (tb + PF < tse) {
+          load_group(tb + 2 * PF, ua, da);
+          run_group(tb + PF, tsb, ub, db);
         }
       }
+      __builtin_amdgcn_wave_barrier();        // this block's LDS row reads precede the overwrite (wave-local)
+      if (tse < t1) store_rows();
     }
   }
   if (MODE == 0 && valid) {
@@ -690,13 +753,23 @@ extern "C" int lci_selective_scan_fwd(int dtype, const void* u, const void* delt
   a.xend = xend; a.xinit = xinit; a.sdt = sdt; a.ckpt = ckpt; a.write_ckpt = ckpt != nullptr;
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((a.nch + 3) / 4, (Dx + 63) / 64, B);
-  if (dtype == 1) hipLaunchKernelGGL((scan_fwd_kernel<bf16, 0>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((scan_fwd_kernel<float, 0>), grid, dim3(256), 0, s, a);
+  // LCI_SCAN_PF=0: the forward passes without the software-pipelined loads (A/B hook)
+  static const bool pf = !getenv("LCI_SCAN_PF") || atoi(getenv("LCI_SCAN_PF")) != 0;
+  auto chunk_pass = [&](auto mode) {
+    constexpr int M = decltype(mode)::value;
+    if (dtype == 1) {
+      if (pf) hipLaunchKernelGGL((scan_fwd_kernel<bf16, M, true>), grid, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((scan_fwd_kernel<bf16, M, false>), grid, dim3(256), 0, s, a);
+    } else {
+      if (pf) hipLaunchKernelGGL((scan_fwd_kernel<float, M, true>), grid, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((scan_fwd_kernel<float, M, false>), grid, dim3(256), 0, s, a);
+    }
+  };
+  chunk_pass(std::integral_constant<int, 0>{});
   LCI_LAUNCH_CHECK();
   hipLaunchKernelGGL(scan_carry_kernel<false>, dim3(Dx, B), dim3(64), 0, s, a);
   LCI_LAUNCH_CHECK();
-  if (dtype == 1) hipLaunchKernelGGL((scan_fwd_kernel<bf16, 1>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((scan_fwd_kernel<float, 1>), grid, dim3(256), 0, s, a);
+  chunk_pass(std::integral_constant<int, 1>{});
   LCI_LAUNCH_CHECK();
   return 0;
 }

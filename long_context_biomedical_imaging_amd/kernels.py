@@ -198,7 +198,7 @@ def _scan_chunk(L, B=1, Dx=64):
     """Chunk length (multiple of CKPT): enough chunks for ~8K waves in flight (B * ceil(Dx/64) waves per chunk),
     at least 64 steps per chunk and at most 4096 chunks (the carry passes walk the chunks sequentially)."""
     waves_per_chunk = B * (-(-Dx // 64))
-    target = max(1, 8192 // waves_per_chunk)
+    target = max(1, int(os.environ.get("LCI_SCAN_WAVES", 8192)) // waves_per_chunk)
     tc = max(64, -(-L // target), -(-L // 4096))
     return -(-tc // CKPT) * CKPT
 

@@ -112,6 +112,9 @@ def bench_scan(L, B=2, Dx=192):
     kernels.KernelTimer.enabled = False
     if timed:
         s = kernels.KernelTimer.summary()
+        if "selective_scan_fwd" in s:
+            emit("selective_scan_fwd(+ckpt)", s["selective_scan_fwd"]["avg_ms"], 1184.0 * B * L, "GB/s",
+                 f"B{B} L{L} Dx{Dx} N8 bf16, training forward (writes the backward's state checkpoints)")
         emit("selective_scan_bwd", s["selective_scan_bwd"]["avg_ms"], 1984.0 * B * L, "GB/s",
              f"B{B} L{L} Dx{Dx} N8 bf16")
 
