@@ -478,7 +478,7 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(ScanArgs a) {
   __shared__ __attribute__((aligned(16))) float bcs[SB][BCS];
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int chunk = blockIdx.x, b = blockIdx.z;
-  const int d = blockIdx.y * 256 + wv * 64 + lane;
+  const int d = blockIdx.y * blockDim.x + wv * 64 + lane;
   const bool valid = d < a.Dx;
   const int dd = valid ? d : a.Dx - 1;
   for (int i = tid; i < SB * 2 * SCAN_N; i += blockDim.x) (&red[0][0])[i] = 0.f;
@@ -797,8 +797,15 @@ extern "C" int lci_selective_scan_bwd(int dtype, const void* u, const void* delt
   LCI_LAUNCH_CHECK();
   hipLaunchKernelGGL(scan_carry_kernel<true>, dim3(Dx, B), dim3(64), 0, s, a);
   LCI_LAUNCH_CHECK();
-  const int nwv = Dx >= 256 ? 4 : (Dx + 63) / 64;
-  dim3 gridc(a.nch, (Dx + 255) / 256, B);
+  // waves per workgroup (channel blocks of 64 sharing one chunk's B/C staging and dB/dC sums): at 254 VGPRs
+  // (2 waves per SIMD) 3-wave groups leave 2 of a CU's 8 wave slots empty and two SIMDs with one wave each, so
+  // long chunks run one wave per workgroup (L=2^21: 7.8 -> 6.6 ms); short chunks keep the shared staging, whose
+  // per-token dB/dC flush (one set of global atomics per workgroup and token) dominates there (L=65536, Tc=64:
+  // 0.60 ms at 4 waves vs 0.80 at 1). LCI_SCAN_BWD_WAVES overrides.
+  static const int wenv = getenv("LCI_SCAN_BWD_WAVES") ? atoi(getenv("LCI_SCAN_BWD_WAVES")) : 0;
+  const int wmax = wenv > 0 ? wenv : (a.Tc >= 512 ? 1 : 4);
+  const int nwv = std::max(1, std::min(std::min(wmax, 4), (Dx + 63) / 64));
+  dim3 gridc(a.nch, (Dx + nwv * 64 - 1) / (nwv * 64), B);
   if (dtype == 1) hipLaunchKernelGGL((scan_bwd_kernel<bf16>), gridc, dim3(nwv * 64), 0, s, a);
   else hipLaunchKernelGGL((scan_bwd_kernel<float>), gridc, dim3(nwv * 64), 0, s, a);
   LCI_LAUNCH_CHECK();
