@@ -71,27 +71,37 @@ def test_selective_scan_chunked_long(L, d, dtype, tol):
         assert rel_err(grads[name], r.grad) < 5 * tol, name
 
 
-def test_dwconv_silu_pair():
+@pytest.mark.parametrize("dtype,L,C,bias", [(torch.float32, 700, 96, False), (torch.float32, 257, 96, True),
+                                             (torch.bfloat16, 1000, 192, True), (torch.bfloat16, 513, 40, False)])
+def test_dwconv_silu_pair(dtype, L, C, bias):
+    """mamba.py:118-119 conv1d(k=3, 'same', groups=C) + SiLU on both halves (16-byte vector kernels when C % V == 0:
+    V = 4 f32 / 8 bf16; C=40 bf16 takes the scalar kernels), runs across the 256-token run boundary."""
     from long_context_biomedical_imaging_amd import kernels
     torch.manual_seed(0)
-    B, L, C = 2, 700, 96
-    xz = torch.randn(B, L, 2 * C)
+    B = 2
+    xz = torch.randn(B, L, 2 * C).to(dtype).float()
     wx, wz = torch.randn(C, 1, 3), torch.randn(C, 1, 3)
-    x = xz.cuda().requires_grad_(True)
+    bx, bz = (torch.randn(C), torch.randn(C)) if bias else (None, None)
+    x = xz.to(dtype).cuda().requires_grad_(True)
     wxc, wzc = wx.cuda().requires_grad_(True), wz.cuda().requires_grad_(True)
-    xs, yz = kernels.dwconv_silu_pair(x, wxc, None, wzc, None)
+    bxc, bzc = (bx.cuda().requires_grad_(True), bz.cuda().requires_grad_(True)) if bias else (None, None)
+    xs, yz = kernels.dwconv_silu_pair(x, wxc, bxc, wzc, bzc)
     xr = xz.clone().requires_grad_(True)
     wxr, wzr = wx.clone().requires_grad_(True), wz.clone().requires_grad_(True)
+    bxr, bzr = (bx.clone().requires_grad_(True), bz.clone().requires_grad_(True)) if bias else (None, None)
     xx, zz = xr.transpose(1, 2).chunk(2, dim=1)
-    rx = F.silu(F.conv1d(xx, wxr, None, padding="same", groups=C)).transpose(1, 2)
-    rz = F.silu(F.conv1d(zz, wzr, None, padding="same", groups=C)).transpose(1, 2)
-    assert rel_err(xs, rx) < 1e-5 and rel_err(yz[..., C:], rz) < 1e-5
-    cx, cz = torch.randn(B, L, C), torch.randn(B, L, C)
+    rx = F.silu(F.conv1d(xx, wxr, bxr, padding="same", groups=C)).transpose(1, 2)
+    rz = F.silu(F.conv1d(zz, wzr, bzr, padding="same", groups=C)).transpose(1, 2)
+    tol = 1e-5 if dtype == torch.float32 else 8e-3   # bf16 outputs: one rounding (2^-9 relative)
+    assert rel_err(xs.float(), rx) < tol and rel_err(yz[..., C:].float(), rz) < tol
+    cx, cz = torch.randn(B, L, C).to(dtype).float(), torch.randn(B, L, C).to(dtype).float()
     gyz = torch.cat([torch.zeros(B, L, C), cz], -1)
-    torch.autograd.backward([xs, yz], [cx.cuda(), gyz.cuda()])
+    torch.autograd.backward([xs, yz], [cx.to(dtype).cuda(), gyz.to(dtype).cuda()])
     torch.autograd.backward([rx, rz], [cx, cz])
-    assert rel_err(x.grad, xr.grad) < 1e-5
-    assert rel_err(wxc.grad, wxr.grad) < 1e-4 and rel_err(wzc.grad, wzr.grad) < 1e-4
+    assert rel_err(x.grad.float(), xr.grad) < tol
+    assert rel_err(wxc.grad, wxr.grad) < 10 * tol and rel_err(wzc.grad, wzr.grad) < 10 * tol
+    if bias:
+        assert rel_err(bxc.grad, bxr.grad) < 10 * tol and rel_err(bzc.grad, bzr.grad) < 10 * tol
 
 
 @pytest.mark.parametrize("amp", [False, True])

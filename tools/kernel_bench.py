@@ -119,6 +119,24 @@ def bench_scan(L, B=2, Dx=192):
              f"B{B} L{L} Dx{Dx} N8 bf16")
 
 
+def bench_dwconv(L=1 << 21, B=1, C=192):
+    """Mamba depthwise conv + SiLU pair (mamba.py:118-119) at the C5 shape: in (B, L, 2C) bf16; fwd reads 2C and
+    writes 2C values per token (4 B each way per channel at bf16), bwd reads in + dout and writes din."""
+    xz = torch.randn(B, L, 2 * C, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    wx, wz = torch.randn(C, 1, 3, device="cuda"), torch.randn(C, 1, 3, device="cuda")
+    bx, bz = torch.randn(C, device="cuda"), torch.randn(C, device="cuda")
+    for t in (wx, wz, bx, bz):
+        t.requires_grad_(True)
+    fb = 2.0 * 2 * C * B * L * 2
+    emit("dwconv_silu_fwd", timeit(lambda: kernels.dwconv_silu_pair(xz, wx, bx, wz, bz)), fb, "GB/s",
+         f"B{B} L{L} 2C{2 * C} bf16")
+    xs, yz = kernels.dwconv_silu_pair(xz, wx, bx, wz, bz)
+    gx, gz = torch.randn_like(xs), torch.randn_like(yz)
+    emit("dwconv_silu_fwd+bwd", timeit(lambda: torch.autograd.grad(kernels.dwconv_silu_pair(xz, wx, bx, wz, bz),
+                                                                     [xz, wx, wz], [gx, gz])),
+         fb + 3.0 * 2 * C * B * L * 2, "GB/s", f"B{B} L{L} 2C{2 * C} bf16 (bwd: in + dout read, din written)")
+
+
 def bench_fftconv():
     B, H, hd, L = 2, 6, 64, 65536
     u = torch.randn(B * H, hd, L, device="cuda").requires_grad_(True)
@@ -205,6 +223,8 @@ def main():
     if "scan" in which:
         bench_scan(65536)
         bench_scan(1 << 21)
+    if "dwconv" in which:
+        bench_dwconv()
     if "fftconv" in which:
         bench_fftconv()
     if "patch" in which:
