@@ -712,46 +712,36 @@ __global__ __launch_bounds__(256) void dwconv_silu_bwd_kernel(ConvArgs a) {
 // accesses are 16 bytes per lane instead of 2. Rows are loaded CONV_U tokens ahead of their use.
 constexpr int CONV_U = 4;
 
-template <typename T> struct Vec16;
-template <> struct Vec16<bf16> {
-  static constexpr int V = 8;
-  typedef bf16x8 raw;
-  static __device__ __forceinline__ void unpack(const raw& r, float (&f)[8]) {
+// V channels of one token row as a T vector of V lanes (16 B: 8 bf16 / 4 f32; 8 B: 4 bf16)
+template <typename T, int V>
+struct VecN {
+  typedef T raw __attribute__((ext_vector_type(V)));
+  static __device__ __forceinline__ void unpack(const raw& r, float (&f)[V]) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) f[i] = (float)r[i];
+    for (int i = 0; i < V; ++i) f[i] = (float)r[i];
   }
-  static __device__ __forceinline__ raw pack(const float (&f)[8]) {
+  static __device__ __forceinline__ raw pack(const float (&f)[V]) {
     raw r;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) r[i] = to_bf16(f[i]);
+    for (int i = 0; i < V; ++i) r[i] = (T)f[i];
     return r;
   }
 };
-template <> struct Vec16<float> {
-  static constexpr int V = 4;
-  typedef f32x4 raw;
-  static __device__ __forceinline__ void unpack(const raw& r, float (&f)[4]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) f[i] = r[i];
-  }
-  static __device__ __forceinline__ raw pack(const float (&f)[4]) { return raw{f[0], f[1], f[2], f[3]}; }
-};
 
-template <typename T>
+template <typename T, int V, int TR = CONV_T>
 struct ConvVecCtx {
-  static constexpr int V = Vec16<T>::V;
-  typedef typename Vec16<T>::raw raw;
+  typedef typename VecN<T, V>::raw raw;
   int b, t0, t1, c, cc0;
   bool zhalf, ok;
   __device__ __forceinline__ ConvVecCtx(const ConvArgs& a) {
     const int G = 2 * a.C / V;                      // vectors per token row
     const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     const int run = (int)(idx / G), g = (int)(idx % G);
-    const int nrun = (a.L + CONV_T - 1) / CONV_T;
+    const int nrun = (a.L + TR - 1) / TR;
     b = blockIdx.z;
     ok = run < nrun;
-    t0 = run * CONV_T;
-    t1 = min(a.L, t0 + CONV_T);
+    t0 = run * TR;
+    t1 = min(a.L, t0 + TR);
     cc0 = g * V;
     zhalf = cc0 >= a.C;
     c = zhalf ? cc0 - a.C : cc0;
@@ -764,11 +754,11 @@ struct ConvVecCtx {
   }
 };
 
-template <typename T>
+template <typename T, int V>
 __global__ __launch_bounds__(256) void dwconv_silu_fwd_vec_kernel(ConvArgs a) {
-  const ConvVecCtx<T> ctx(a);
-  constexpr int V = ConvVecCtx<T>::V;
-  typedef typename ConvVecCtx<T>::raw raw;
+  const ConvVecCtx<T, V> ctx(a);
+  typedef VecN<T, V> Vec;
+  typedef typename Vec::raw raw;
   if (!ctx.ok) return;
   const float* w = (ctx.zhalf ? a.wz : a.wx) + ctx.c * CONV_K;
   const float* bp = ctx.zhalf ? a.bz : a.bx;
@@ -782,8 +772,8 @@ __global__ __launch_bounds__(256) void dwconv_silu_fwd_vec_kernel(ConvArgs a) {
                     : (T*)a.ox + (long long)ctx.b * a.L * a.ox_ts + ctx.c;
   const int ots = ctx.zhalf ? a.oz_ts : a.ox_ts;
   float xm[V], x0[V];
-  Vec16<T>::unpack(ctx.in_row(a, ctx.t0 - 1), xm);
-  Vec16<T>::unpack(ctx.in_row(a, ctx.t0), x0);
+  Vec::unpack(ctx.in_row(a, ctx.t0 - 1), xm);
+  Vec::unpack(ctx.in_row(a, ctx.t0), x0);
   for (int tb = ctx.t0; tb < ctx.t1; tb += CONV_U) {
     raw nx[CONV_U];
 #pragma unroll
@@ -791,23 +781,27 @@ __global__ __launch_bounds__(256) void dwconv_silu_fwd_vec_kernel(ConvArgs a) {
 #pragma unroll
     for (int u = 0; u < CONV_U; ++u) {
       float xp[V], y[V];
-      Vec16<T>::unpack(nx[u], xp);
+      Vec::unpack(nx[u], xp);
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         const float pre = fmaf(w0[v], xm[v], fmaf(w1[v], x0[v], fmaf(w2[v], xp[v], bias[v])));
         y[v] = pre / (1.f + __expf(-pre));
         xm[v] = x0[v]; x0[v] = xp[v];
       }
-      if (tb + u < ctx.t1) *(raw*)(op + (long long)(tb + u) * ots) = Vec16<T>::pack(y);
+      if (tb + u < ctx.t1) *(raw*)(op + (long long)(tb + u) * ots) = Vec::pack(y);
     }
   }
 }
 
-template <typename T>
+// Runs of CONV_TB tokens: each run ends in 4 V float atomics onto the (C, 3) weight / (C) bias gradients, and the
+// L2 serialises atomics to one address, so the run count (not the bytes) bounded the backward at 256-token runs.
+constexpr int CONV_TB = 1024;
+
+template <typename T, int V>
 __global__ __launch_bounds__(256) void dwconv_silu_bwd_vec_kernel(ConvArgs a) {
-  const ConvVecCtx<T> ctx(a);
-  constexpr int V = ConvVecCtx<T>::V;
-  typedef typename ConvVecCtx<T>::raw raw;
+  const ConvVecCtx<T, V, CONV_TB> ctx(a);
+  typedef VecN<T, V> Vec;
+  typedef typename Vec::raw raw;
   if (!ctx.ok) return;
   const float* w = (ctx.zhalf ? a.wz : a.wx) + ctx.c * CONV_K;
   const float* bp = ctx.zhalf ? a.bz : a.bx;
@@ -828,7 +822,7 @@ __global__ __launch_bounds__(256) void dwconv_silu_bwd_vec_kernel(ConvArgs a) {
   // g(s) = dout(s) silu'(pre(s)) from x(s-1..s+1); zero outside [0, L) (dout row is zero there)
   auto G = [&](const float (&xm)[V], const float (&x0)[V], const float (&xp)[V], const raw& gr, float (&g)[V]) {
     float gf[V];
-    Vec16<T>::unpack(gr, gf);
+    Vec::unpack(gr, gf);
 #pragma unroll
     for (int v = 0; v < V; ++v) {
       const float pre = fmaf(w0[v], xm[v], fmaf(w1[v], x0[v], fmaf(w2[v], xp[v], bias[v])));
@@ -838,10 +832,10 @@ __global__ __launch_bounds__(256) void dwconv_silu_bwd_vec_kernel(ConvArgs a) {
   };
   const int t0 = ctx.t0;
   float xa[V], xb[V], xc[V], xd[V], gm[V], g0[V];
-  Vec16<T>::unpack(ctx.in_row(a, t0 - 2), xa);
-  Vec16<T>::unpack(ctx.in_row(a, t0 - 1), xb);
-  Vec16<T>::unpack(ctx.in_row(a, t0), xc);
-  Vec16<T>::unpack(ctx.in_row(a, t0 + 1), xd);
+  Vec::unpack(ctx.in_row(a, t0 - 2), xa);
+  Vec::unpack(ctx.in_row(a, t0 - 1), xb);
+  Vec::unpack(ctx.in_row(a, t0), xc);
+  Vec::unpack(ctx.in_row(a, t0 + 1), xd);
   G(xa, xb, xc, go_row(t0 - 1), gm);
   G(xb, xc, xd, go_row(t0), g0);
   float dw0[V], dw1[V], dw2[V], db[V];
@@ -860,7 +854,7 @@ __global__ __launch_bounds__(256) void dwconv_silu_bwd_vec_kernel(ConvArgs a) {
       const int t = tb + u;
       if (t < ctx.t1) {
         float xe[V], gp[V], o[V];
-        Vec16<T>::unpack(nx[u], xe);
+        Vec::unpack(nx[u], xe);
         G(xc, xd, xe, ng[u], gp);
 #pragma unroll
         for (int v = 0; v < V; ++v) {
@@ -872,7 +866,7 @@ __global__ __launch_bounds__(256) void dwconv_silu_bwd_vec_kernel(ConvArgs a) {
           xa[v] = xb[v]; xb[v] = xc[v]; xc[v] = xd[v]; xd[v] = xe[v];
           gm[v] = g0[v]; g0[v] = gp[v];
         }
-        *(raw*)(din + (long long)t * a.in_ts) = Vec16<T>::pack(o);
+        *(raw*)(din + (long long)t * a.in_ts) = Vec::pack(o);
       }
     }
   }
@@ -995,20 +989,20 @@ extern "C" int lci_selective_scan_bwd(int dtype, const void* u, const void* delt
 
 // The 16-byte vector kernels need C a multiple of the vector width and 16-byte aligned rows of every operand;
 // LCI_DWCONV_VEC=0 forces the scalar kernels (A/B hook).
-static bool dwconv_vec_ok(int dtype, int C, const void* const* ptrs, int np, const int* tss, int nts, int zoff) {
+static bool dwconv_vec_ok(int dtype, int V, int C, const void* const* ptrs, int np, const int* tss, int nts,
+                          int zoff) {
   static const bool on = !getenv("LCI_DWCONV_VEC") || atoi(getenv("LCI_DWCONV_VEC")) != 0;
-  const int es = dtype == 1 ? 2 : 4, V = 16 / es;
+  const int vb = V * (dtype == 1 ? 2 : 4);   // vector bytes
   if (!on || C % V || zoff % V) return false;
   for (int i = 0; i < np; ++i)
-    if (ptrs[i] && ((uintptr_t)ptrs[i] & 15)) return false;
+    if (ptrs[i] && ((uintptr_t)ptrs[i] % vb)) return false;
   for (int i = 0; i < nts; ++i)
     if (tss[i] % V) return false;
   return true;
 }
 
-static dim3 dwconv_vec_grid(int dtype, int B, int L, int C) {
-  const int V = dtype == 1 ? 8 : 4;
-  const long long threads = (long long)((L + CONV_T - 1) / CONV_T) * (2 * C / V);
+static dim3 dwconv_vec_grid(int V, int B, int L, int C, int TR = CONV_T) {
+  const long long threads = (long long)((L + TR - 1) / TR) * (2 * C / V);
   return dim3((unsigned)((threads + 255) / 256), 1, B);
 }
 
@@ -1021,10 +1015,10 @@ extern "C" int lci_dwconv_silu_fwd(int dtype, const void* in, const float* wx, c
   a.B = B; a.L = L; a.C = C; a.in_ts = in_ts; a.ox_ts = ox_ts; a.oz_ts = oz_ts; a.zoff = zoff;
   const void* vp[] = {in, ox, oz};
   const int vt[] = {in_ts, ox_ts, oz_ts};
-  if (dwconv_vec_ok(dtype, C, vp, 3, vt, 3, zoff)) {
-    const dim3 gv = dwconv_vec_grid(dtype, B, L, C);
-    if (dtype == 1) hipLaunchKernelGGL(dwconv_silu_fwd_vec_kernel<bf16>, gv, dim3(256), 0, (hipStream_t)stream, a);
-    else hipLaunchKernelGGL(dwconv_silu_fwd_vec_kernel<float>, gv, dim3(256), 0, (hipStream_t)stream, a);
+  if (dwconv_vec_ok(dtype, dtype == 1 ? 8 : 4, C, vp, 3, vt, 3, zoff)) {
+    const dim3 gv = dwconv_vec_grid(dtype == 1 ? 8 : 4, B, L, C);
+    if (dtype == 1) hipLaunchKernelGGL((dwconv_silu_fwd_vec_kernel<bf16, 8>), gv, dim3(256), 0, (hipStream_t)stream, a);
+    else hipLaunchKernelGGL((dwconv_silu_fwd_vec_kernel<float, 4>), gv, dim3(256), 0, (hipStream_t)stream, a);
     LCI_LAUNCH_CHECK();
     return 0;
   }
@@ -1045,15 +1039,18 @@ extern "C" int lci_dwconv_silu_bwd(int dtype, const void* in, const float* wx, c
   a.in = in; a.wx = wx; a.bx = bx; a.wz = wz; a.bz = bz; a.gx = gx; a.gz = gz; a.din = din;
   a.dwx = dwx; a.dbx = dbx; a.dwz = dwz; a.dbz = dbz;
   a.B = B; a.L = L; a.C = C; a.in_ts = in_ts; a.ox_ts = ox_ts; a.oz_ts = oz_ts; a.zoff = zoff;
-  // the vector backward holds 16 channels' windows (182 VGPRs at bf16, 2 waves per SIMD) and measured slower than
-  // the scalar one (3.5 vs 2.6 ms at B=1, L=2^21, 2C=384): opt-in (LCI_DWCONV_VEC_BWD=1)
-  static const bool vec_bwd = getenv("LCI_DWCONV_VEC_BWD") && atoi(getenv("LCI_DWCONV_VEC_BWD")) != 0;
+  // backward: 4 channels per thread (8-byte bf16 / 16-byte f32 vectors). The 8-channel bf16 version holds 16
+  // windows' state in 182 VGPRs (2 waves per SIMD) and measured slower than the scalar kernels (3.5 vs 2.6 ms at
+  // B=1, L=2^21, 2C=384). LCI_DWCONV_BWD_V = 0 (scalar) / 4 / 8 overrides.
+  static const int bwd_v = getenv("LCI_DWCONV_BWD_V") ? atoi(getenv("LCI_DWCONV_BWD_V")) : 4;
   const void* vp[] = {in, gx, gz, din};
   const int vt[] = {in_ts, ox_ts, oz_ts};
-  if (vec_bwd && dwconv_vec_ok(dtype, C, vp, 4, vt, 3, zoff)) {
-    const dim3 gv = dwconv_vec_grid(dtype, B, L, C);
-    if (dtype == 1) hipLaunchKernelGGL(dwconv_silu_bwd_vec_kernel<bf16>, gv, dim3(256), 0, (hipStream_t)stream, a);
-    else hipLaunchKernelGGL(dwconv_silu_bwd_vec_kernel<float>, gv, dim3(256), 0, (hipStream_t)stream, a);
+  const int V = dtype == 1 ? bwd_v : std::min(bwd_v, 4);
+  if (V > 0 && dwconv_vec_ok(dtype, V, C, vp, 4, vt, 3, zoff)) {
+    const dim3 gv = dwconv_vec_grid(V, B, L, C, CONV_TB);
+    if (dtype != 1) hipLaunchKernelGGL((dwconv_silu_bwd_vec_kernel<float, 4>), gv, dim3(256), 0, (hipStream_t)stream, a);
+    else if (V == 8) hipLaunchKernelGGL((dwconv_silu_bwd_vec_kernel<bf16, 8>), gv, dim3(256), 0, (hipStream_t)stream, a);
+    else hipLaunchKernelGGL((dwconv_silu_bwd_vec_kernel<bf16, 4>), gv, dim3(256), 0, (hipStream_t)stream, a);
     LCI_LAUNCH_CHECK();
     return 0;
   }

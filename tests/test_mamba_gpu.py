@@ -72,10 +72,10 @@ def test_selective_scan_chunked_long(L, d, dtype, tol):
 
 
 @pytest.mark.parametrize("dtype,L,C,bias", [(torch.float32, 700, 96, False), (torch.float32, 257, 96, True),
-                                             (torch.bfloat16, 1000, 192, True), (torch.bfloat16, 513, 40, False)])
+                                             (torch.bfloat16, 1000, 192, True), (torch.bfloat16, 513, 36, False)])
 def test_dwconv_silu_pair(dtype, L, C, bias):
-    """mamba.py:118-119 conv1d(k=3, 'same', groups=C) + SiLU on both halves (16-byte vector kernels when C % V == 0:
-    V = 4 f32 / 8 bf16; C=40 bf16 takes the scalar kernels), runs across the 256-token run boundary."""
+    """mamba.py:118-119 conv1d(k=3, 'same', groups=C) + SiLU on both halves: vector forward when C % V == 0 (V = 4 f32 /
+    8 bf16; C=36 bf16 takes the scalar forward), 4-channel vector backward; runs across the 256-token boundary."""
     from long_context_biomedical_imaging_amd import kernels
     torch.manual_seed(0)
     B = 2
