@@ -472,7 +472,9 @@ __device__ __forceinline__ float wave_reduce16(float (&v)[16], int lane) {
 // sub-block's states x and decays exp(dt A) are recomputed from its checkpoint into registers, then swept back.
 // B_t / C_t rows and the per-token dB/dC partial sums go through LDS in blocks of SB steps (two workgroup
 // barriers per SB steps); each lane's u / dt / dy / checkpoint loads are issued one sub-block ahead.
-template <typename T>
+// PARTIALS: per-(b, chunk) dA / dD / d(delta_bias) partials into the lane's own gin entry (read at the start) and
+// its dead gl entry, summed by scan_param_reduce_kernel, instead of B * nch float atomics per address.
+template <typename T, bool PARTIALS>
 __global__ __launch_bounds__(256) void scan_bwd_kernel(ScanArgs a) {
   __shared__ float red[SB][2 * SCAN_N];
   __shared__ __attribute__((aligned(16))) float bcs[SB][BCS];
@@ -614,12 +616,43 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(ScanArgs a) {
     const int t = blk0 + i;
     if (t < t1) atomicAdd(a.dBC + ((long long)b * a.L + t) * (2 * SCAN_N) + j, red[i][j]);
   }
-  if (valid) {
+  if constexpr (PARTIALS) {
+    if (!valid) return;
+    const long long o = (((long long)b * a.nch + chunk) * a.Dx + d) * SCAN_N;
+    *(f32x4*)(a.gin + o) = f32x4{dA[0], dA[1], dA[2], dA[3]};
+    *(f32x4*)(a.gin + o + 4) = f32x4{dA[4], dA[5], dA[6], dA[7]};
+    a.gl[o] = dDacc;
+    a.gl[o + 1] = dbacc;
+  } else if (valid) {
 #pragma unroll
     for (int n = 0; n < SCAN_N; ++n) atomicAdd(a.dA + d * SCAN_N + n, dA[n]);
     atomicAdd(a.dD + d, dDacc);
     atomicAdd(a.ddbias + d, dbacc);
   }
+}
+
+// Sum of the per-(b, chunk) parameter-gradient partials: thread = (channel d, value q) with q < 8 the dA states and
+// q = 8 / 9 dD / d(delta_bias); blockIdx.y takes a stride-gridDim.y subset of the (b, chunk) rows, one atomic per
+// thread at the end (gridDim.y atomics per address instead of B * nch from the scan kernel's waves).
+constexpr int SCAN_NP = SCAN_N + 2;
+__global__ __launch_bounds__(256) void scan_param_reduce_kernel(ScanArgs a) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.Dx * SCAN_NP) return;
+  const int d = i / SCAN_NP, q = i % SCAN_NP;
+  const float* src = q < SCAN_N ? a.gin + q : a.gl + (q - SCAN_N);
+  const int rows = a.B * a.nch;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int r = blockIdx.y;
+  const int st = gridDim.y;
+  for (; r + 3 * st < rows; r += 4 * st) {
+    s0 += src[((long long)r * a.Dx + d) * SCAN_N];
+    s1 += src[((long long)(r + st) * a.Dx + d) * SCAN_N];
+    s2 += src[((long long)(r + 2 * st) * a.Dx + d) * SCAN_N];
+    s3 += src[((long long)(r + 3 * st) * a.Dx + d) * SCAN_N];
+  }
+  for (; r < rows; r += st) s0 += src[((long long)r * a.Dx + d) * SCAN_N];
+  float* dst = q < SCAN_N ? a.dA + d * SCAN_N + q : (q == SCAN_N ? a.dD + d : a.ddbias + d);
+  atomicAdd(dst, (s0 + s1) + (s2 + s3));
 }
 
 // ------------------------------------------------------------------------------ depthwise conv + SiLU
@@ -981,9 +1014,25 @@ extern "C" int lci_selective_scan_bwd(int dtype, const void* u, const void* delt
   const int wmax = wenv > 0 ? wenv : (a.Tc >= 512 ? 1 : 4);
   const int nwv = std::max(1, std::min(std::min(wmax, 4), (Dx + 63) / 64));
   dim3 gridc(a.nch, (Dx + nwv * 64 - 1) / (nwv * 64), B);
-  if (dtype == 1) hipLaunchKernelGGL((scan_bwd_kernel<bf16>), gridc, dim3(nwv * 64), 0, s, a);
-  else hipLaunchKernelGGL((scan_bwd_kernel<float>), gridc, dim3(nwv * 64), 0, s, a);
+  // parameter gradients: the B * nch float atomics per address from the waves' ends serialise in L2 (the dwconv
+  // backward's lesson): short chunks write partials and sum them in one more launch (L=65536: 0.60 -> 0.42 ms).
+  // Long chunks keep the atomics: there the partials build of the kernel measured slower (8.6 vs 6.9 ms at L=2^21,
+  // a main-loop schedule change at 256 VGPRs). LCI_SCAN_PARAM_PARTIALS = 0 / 1 overrides.
+  static const int penv = getenv("LCI_SCAN_PARAM_PARTIALS") ? atoi(getenv("LCI_SCAN_PARAM_PARTIALS")) : -1;
+  const bool partials = penv >= 0 ? penv != 0 : a.Tc < 512;
+  if (partials) {
+    if (dtype == 1) hipLaunchKernelGGL((scan_bwd_kernel<bf16, true>), gridc, dim3(nwv * 64), 0, s, a);
+    else hipLaunchKernelGGL((scan_bwd_kernel<float, true>), gridc, dim3(nwv * 64), 0, s, a);
+  } else {
+    if (dtype == 1) hipLaunchKernelGGL((scan_bwd_kernel<bf16, false>), gridc, dim3(nwv * 64), 0, s, a);
+    else hipLaunchKernelGGL((scan_bwd_kernel<float, false>), gridc, dim3(nwv * 64), 0, s, a);
+  }
   LCI_LAUNCH_CHECK();
+  if (partials) {
+    const int ny = std::max(1, std::min(64, (B * a.nch) / 16));
+    hipLaunchKernelGGL(scan_param_reduce_kernel, dim3((Dx * SCAN_NP + 255) / 256, ny), dim3(256), 0, s, a);
+    LCI_LAUNCH_CHECK();
+  }
   return 0;
 }
 
