@@ -125,7 +125,11 @@ class _TableGather(torch.autograd.Function):
     def backward(ctx, g):
         (idx,) = ctx.saved_tensors
         gt = torch.zeros(ctx.rows, g.shape[-1], device=g.device, dtype=g.dtype)
-        gt.index_add_(0, idx, g)
+        if torch.are_deterministic_algorithms_enabled():
+            # fixed-order sum (autograd's sorted index backward); index_add_ below uses float atomics
+            gt.index_put_((idx,), g, accumulate=True)
+        else:
+            gt.index_add_(0, idx, g)
         return gt, None
 
 

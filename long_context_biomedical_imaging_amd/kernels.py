@@ -754,6 +754,8 @@ class _GELU(torch.autograd.Function):
     def backward(ctx, dy):
         (x,) = ctx.saved_tensors
         dy = dy.to(torch.bfloat16).contiguous()
+        if dy.data_ptr() % 16:          # a contiguous view at a storage offset: the kernel needs 16-byte vectors
+            dy = dy.clone()
         dx = torch.empty_like(x)
         KernelTimer.run("gelu_bwd", 0.0, x, lambda: _lib.call(
             "lci_gelu_bwd", x.data_ptr(), dy.data_ptr(), dx.data_ptr(), x.numel(), _lib.stream_of(x)))

@@ -12,6 +12,7 @@ cross-checked against that restatement in tests/test_oracle_golden.py. Only test
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import os
 import subprocess
 
@@ -23,18 +24,32 @@ LIB = os.path.join(HERE, "_build", "libscan_ref.so")
 _lib = None
 
 
+_CMD = ["gcc", "-O2", "-fopenmp", "-fPIC", "-shared", SRC, "-o", LIB, "-lm"]
+
+
+def _key() -> str:
+    """Staleness key: sha256 of scan_ref.c + the compile line (copied trees have unreliable mtimes)."""
+    h = hashlib.sha256(open(SRC, "rb").read())
+    h.update(" ".join(_CMD).encode())
+    return h.hexdigest()
+
+
 def build(force: bool = False) -> str:
-    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(SRC):
+    key_path = LIB + ".key"
+    key = _key()
+    stale = not os.path.exists(LIB) or not os.path.exists(key_path) or open(key_path).read().strip() != key
+    if force or stale:
         os.makedirs(os.path.dirname(LIB), exist_ok=True)
-        subprocess.run(["gcc", "-O2", "-fopenmp", "-fPIC", "-shared", SRC, "-o", LIB, "-lm"], check=True)
+        subprocess.run(_CMD, check=True)
+        with open(key_path, "w") as f:
+            f.write(key)
     return LIB
 
 
 def _load():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB):
-            build()
+        build()
         _lib = ctypes.CDLL(LIB)
         _lib.scan_ref_fwd.restype = ctypes.c_int
         _lib.scan_ref_bwd.restype = ctypes.c_int

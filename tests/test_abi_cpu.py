@@ -18,6 +18,24 @@ def _declared():
             for name, args in decls}
 
 
+def _header_abi_version() -> int:
+    m = re.search(r"#define\s+LCI_ABI_VERSION\s+(\d+)", open(HDR).read())
+    assert m, "include/lci.h defines no LCI_ABI_VERSION"
+    return int(m.group(1))
+
+
+def test_abi_version_constants_agree():
+    """include/lci.h, the Python binding and every `lci_abi_version() == N` literal in INTEGRATION.md agree."""
+    from long_context_biomedical_imaging_amd import _lib
+    v = _header_abi_version()
+    assert _lib.ABI_VERSION == v
+    txt = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    lits = re.findall(r"lci_abi_version\(\)\s*==\s*(\d+)", txt)
+    assert lits, "INTEGRATION.md stub checks no ABI version"
+    for n in lits:
+        assert int(n) == v, f"INTEGRATION.md asserts ABI {n}, include/lci.h defines {v}"
+
+
 def test_header_declares_entry_points():
     d = _declared()
     for must in ("lci_attn_fwd", "lci_attn_bwd", "lci_window_attn_fwd", "lci_window_attn_bwd",
@@ -34,7 +52,7 @@ def test_library_exports_every_declared_symbol():
     lib = ctypes.CDLL(_lib.LIB_PATH)
     for name in _declared():
         assert hasattr(lib, name), f"{name} declared in include/lci.h but not exported"
-    assert _lib.load().lci_abi_version() == _lib.ABI_VERSION == 11
+    assert _lib.load().lci_abi_version() == _lib.ABI_VERSION == _header_abi_version()
 
 
 def test_python_binding_arity_matches_header():
