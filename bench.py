@@ -39,9 +39,10 @@ from long_context_biomedical_imaging_amd.trainer import (TrainStep, init_distrib
 
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # dense bf16, MI355X_MICROARCH.md chip table
 HBM_PEAK_GBS = 8000.0
-# kernels whose roofline is HBM: algorithmic bytes per unit of KernelTimer work (scan units are
-# tokens at Dx = 192, N = 8, bf16 I/O; FFT-conv units are row-elements, f32 in/out). Others: MFMA FLOPs.
-ROOF = {"selective_scan_fwd": ("hbm", 1184.0), "selective_scan_bwd": ("hbm", 1984.0),
+# kernels whose roofline is HBM: algorithmic bytes per unit of KernelTimer work (the scan's work is
+# its algorithmic bytes already — 1184 / 1984 B per token at Dx = 192, N = 8, bf16 I/O; FFT-conv units are
+# row-elements, f32 in/out). Others: MFMA FLOPs.
+ROOF = {"selective_scan_fwd": ("hbm", 1.0), "selective_scan_bwd": ("hbm", 1.0),
         "fftconv_fwd": ("hbm", 8.0), "fftconv_bwd": ("hbm", 16.0),
         # LayerNorm work is counted in bytes already (f32 x in, bf16 y out; bwd + bf16 dy in, f32 dx out)
         "ln_fwd": ("hbm", 1.0), "ln_bwd": ("hbm", 1.0)}
@@ -76,8 +77,30 @@ WORKLOADS = {
                           "--no_in_channel", "1", "--no_out_channel", "1", "--ViT.size", "small",
                           "--ViT.patch_size", "1", "2", "2", "--ViT.use_hyena", "True",
                           "--ViT.hyena_l_max", "262144", "--use_amp"],
+    # configs[1] (C2): ViT-small + ViTUNETR 2-D segmentation, 512x512, patch 4 -> L = 16384, full attention
+    "vit_p4_512": ["--encoder_name", "ViT", "--decoder_name", "ViTUNETR", "--task_type", "seg",
+                   "--height", "512", "--width", "512", "--time", "1", "--no_in_channel", "1",
+                   "--no_out_channel", "2", "--ViT.size", "small", "--ViT.patch_size", "1", "4", "4",
+                   "--use_amp"],
+    # the reference's project recipes (projects/run_*.sh): Swin-tiny patch 2 with Mamba / Hyena inside the windows
+    # (shift 0, backbone_swin.py:674) + UperNet3D segmentation, here on a 128^3 volume (64^3 = 262144 tokens);
+    # window 4 as run_abct.sh (Mamba), window 8 as run_cmr.sh (Hyena)
+    "swin_mamba_p2_128": ["--encoder_name", "Swin", "--decoder_name", "UperNet3D", "--task_type", "seg",
+                          "--height", "128", "--width", "128", "--time", "128", "--no_in_channel", "1",
+                          "--no_out_channel", "2", "--Swin.size", "tiny", "--Swin.patch_size", "2", "2", "2",
+                          "--Swin.window_size", "4", "4", "4", "--Swin.use_mamba", "True", "--use_amp"],
+    "swin_hyena_p2_128": ["--encoder_name", "Swin", "--decoder_name", "UperNet3D", "--task_type", "seg",
+                          "--height", "128", "--width", "128", "--time", "128", "--no_in_channel", "1",
+                          "--no_out_channel", "2", "--Swin.size", "tiny", "--Swin.patch_size", "2", "2", "2",
+                          "--Swin.window_size", "8", "8", "8", "--Swin.use_hyena", "True", "--use_amp"],
 }
 WORKLOAD_NAMES = {
+    "vit_p4_512": ("image-tokens/sec fwd+bwd, ViT patch=4 512^2 (L=16384)",
+                   "ViT-small p4 512x512 2-D seg (ViTUNETR head), full attention (BASELINE configs[1])"),
+    "swin_mamba_p2_128": ("image-tokens/sec fwd+bwd, Swin-Mamba patch=2 128^3 (L=262144), window 4",
+                          "Swin-tiny p2 128^3 3-D seg (UperNet3D head), Mamba inside 4^3 windows (run_abct.sh recipe)"),
+    "swin_hyena_p2_128": ("image-tokens/sec fwd+bwd, Swin-Hyena patch=2 128^3 (L=262144), window 8",
+                          "Swin-tiny p2 128^3 3-D seg (UperNet3D head), Hyena inside 8^3 windows (run_cmr.sh recipe)"),
     "vit_p2_512": ("image-tokens/sec fwd+bwd, ViT patch=2 512^2 (L=65536), 1/2/4/8 MI355X",
                    "ViT-small p2 512x512 2-D seg (ViTUNETR head), full attention"),
     "swin_p2_128": ("image-tokens/sec fwd+bwd, Swin patch=2 128^3 (L=262144), window 7",
@@ -198,7 +221,7 @@ def run_workload(workload, batch, steps, warmup, rank, world, device, kernel_tim
                  ckpt_blocks=None):
     """Build the workload's model, run `warmup` untimed and `steps` timed training steps (barrier + sync on both
     sides, max over ranks). Returns the bench dict on rank 0 (None elsewhere); frees the model."""
-    if workload in ("swin_p2_128", "vit_mamba_p2_256"):
+    if workload in ("swin_p2_128", "vit_mamba_p2_256", "swin_mamba_p2_128", "swin_hyena_p2_128"):
         # any 3-D conv left on MIOpen (none in these heads today): heuristic solver instead of a minutes-long find
         os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
     cfg = lconfig.parse_config(WORKLOADS[workload] + ["--batch_size", str(batch)] + list(cfg_extra))
@@ -292,7 +315,7 @@ def main():
     args = ap.parse_args()
 
     if args.batch is None:
-        args.batch = 2 if args.workload in ("vit_p2_512", "vit_hyena_p2_512", "vit_hyena_p2_1024") else 1
+        args.batch = 2 if args.workload in ("vit_p2_512", "vit_p4_512", "vit_hyena_p2_512", "vit_hyena_p2_1024") else 1
     rank, local, world = init_distributed()
     device = torch.device("cuda", local % torch.cuda.device_count())   # % : gloo rehearsals on one GPU
     torch.cuda.set_device(device)

@@ -64,11 +64,14 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--gaussian_blur_aug", type=str_to_bool, default=True)
     p.add_argument("--use_amp", action="store_true")
     p.add_argument("--ddp", action="store_true")
-    p.add_argument("--optim_type", type=str, default="adam", choices=["adam", "adamw", "sgd"])
+    p.add_argument("--optim_type", type=str, default="adam", choices=["adam", "adamw", "sgd", "nadam"])
     p.add_argument("--optim.lr", type=float, default=1e-4)
     p.add_argument("--optim.weight_decay", type=float, default=0.0)
     p.add_argument("--optim.beta1", type=float, default=0.90)
     p.add_argument("--optim.beta2", type=float, default=0.95)
+    # general_parser.py:109-110 (trainer_base.py:168-176)
+    p.add_argument("--clip_grad_norm", type=float, default=0.0)
+    p.add_argument("--iters_to_accumulate", type=int, default=1)
     # model_parser.py:29-37
     p.add_argument("--ViT.size", type=str, default="small", choices=["small", "base", "custom"])
     p.add_argument("--ViT.patch_size", nargs="+", type=int, default=[16, 16, 16])

@@ -282,7 +282,8 @@ class _SelectiveScanCL(torch.autograd.Function):
         bv = delta_bias.float().contiguous() if delta_bias is not None else torch.zeros(Dx, **f32)
         y = yz[..., :Dx]
         strides = _ll_array([*_bt(u), *_bt(delta), *_bt(Bm), *_bt(Cm), *_bt(y), 0, 0, 0, 0, 0, 0])
-        KernelTimer.run("selective_scan_fwd", float(B * L), u, lambda: _lib.call(
+        es = u.element_size()   # algorithmic bytes: read u, delta, B, C; write y
+        KernelTimer.run("selective_scan_fwd", float(B * L * (3 * Dx + 2 * N) * es), u, lambda: _lib.call(
             "lci_selective_scan_fwd", _DT[dt], u.data_ptr(), delta.data_ptr(), Af.data_ptr(), Bm.data_ptr(),
             Cm.data_ptr(), Dv.data_ptr(), bv.data_ptr(), y.data_ptr(), strides, B, L, Dx, N, tc, int(softplus),
             xend.data_ptr(), xinit.data_ptr(), sdt.data_ptr(), _lib.ptr(ckpt), _lib.stream_of(u)))
@@ -317,7 +318,8 @@ class _SelectiveScanCL(torch.autograd.Function):
         gl = torch.empty(B, nch, Dx, N, **f32)
         gin = torch.empty(B, nch, Dx, N, **f32)
         strides = _ll_array([*_bt(u), *_bt(delta), *_bt(Bm), *_bt(Cm), 0, 0, *_bt(dy), *_bt(du), *_bt(dd)])
-        KernelTimer.run("selective_scan_bwd", float(B * L), u, lambda: _lib.call(
+        es = u.element_size()   # read u, delta, dy, B, C; write du, ddelta, dB, dC
+        KernelTimer.run("selective_scan_bwd", float(B * L * (5 * Dx + 4 * N) * es), u, lambda: _lib.call(
             "lci_selective_scan_bwd", _DT[u.dtype], u.data_ptr(), delta.data_ptr(), Af.data_ptr(), Bm.data_ptr(),
             Cm.data_ptr(), Dv.data_ptr(), bv.data_ptr(), dy.data_ptr(), du.data_ptr(), dd.data_ptr(),
             dBC.data_ptr(), dA.data_ptr(), dD.data_ptr(), db.data_ptr(), strides, B, L, Dx, N, tc,

@@ -70,7 +70,11 @@ def build_optimizer(params, config):
     if config.optim_type == "adamw":
         return torch.optim.AdamW(params, lr=o.lr, betas=(o.beta1, o.beta2), weight_decay=o.weight_decay,
                                  fused=fused or None)
-    return torch.optim.SGD(params, lr=o.lr, weight_decay=o.weight_decay)
+    if config.optim_type == "nadam":
+        return torch.optim.NAdam(params, lr=o.lr, betas=(o.beta1, o.beta2), weight_decay=o.weight_decay)
+    if config.optim_type == "sgd":   # optim_base.py:90-91: momentum 0.9
+        return torch.optim.SGD(params, lr=o.lr, momentum=0.9, weight_decay=o.weight_decay)
+    raise NotImplementedError(f"Optimizer not implemented: {config.optim_type}")
 
 
 def loss_fn(config):
@@ -92,16 +96,23 @@ class TrainStep:
         self.optim = build_optimizer(self.model.parameters(), config)
         self.loss_func = loss_fn(config)
         self.use_amp = bool(config.use_amp)
+        self.clip = float(getattr(config, "clip_grad_norm", 0.0) or 0.0)
+        self.accum = max(1, int(getattr(config, "iters_to_accumulate", 1) or 1))
         self.optim.zero_grad(set_to_none=True)
 
-    def step(self, inputs, targets):
+    def step(self, inputs, targets, update: bool = True):
+        """trainer_base.py:166-182: autocast forward + loss / iters_to_accumulate, backward, then (when `update`,
+        i.e. at the end of an accumulation window) optional grad-norm clip, optimizer step and zero_grad."""
         dev = "cuda" if self.device.type == "cuda" else "cpu"
         with torch.autocast(device_type=dev, dtype=torch.bfloat16, enabled=self.use_amp):
             out = self.model(inputs)
-            loss = self.loss_func(out, targets)
+            loss = self.loss_func(out, targets) / self.accum
         loss.backward()
-        self.optim.step()
-        self.optim.zero_grad(set_to_none=True)
+        if update:
+            if self.clip > 0:
+                nn.utils.clip_grad_norm_(self.model.parameters(), self.clip)
+            self.optim.step()
+            self.optim.zero_grad(set_to_none=True)
         return loss.detach()
 
 

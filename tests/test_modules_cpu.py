@@ -63,6 +63,34 @@ def test_swin_init_matches_reference():
     _same_sd(layer, Golden("swin_basic_layer"))
 
 
+@pytest.mark.parametrize("name,seed", [("swin_hyena_w7", 20), ("swin_mamba_w7", 21), ("swin_hyena_w4", 22),
+                                       ("swin_mamba_w4", 23), ("swin_hyena_w8", 24), ("swin_mamba_w8", 25),
+                                       ("swin_mamba_w4_2d", 26), ("swin_hyena_w8_2d", 27)])
+def test_swin_alt_layer_init_matches_reference(name, seed):
+    """BasicLayer with Hyena / Mamba in the windows: seed-identical state_dict incl. the Hyena positional
+    embedding (checksummed) against the reference's (tools/gen_golden.py:swin_alt_layer)."""
+    g = Golden(name)
+    hy = bool(g.scalar("cfg/hyena"))
+    ws = tuple(int(v) for v in g.z["cfg/window"])
+    torch.manual_seed(seed)
+    down = backbone_swin.PatchMergingV2 if int(g.scalar("cfg/downsample")) else None
+    layer = backbone_swin.BasicLayer(hy, not hy, dim=96, depth=2, num_heads=3, window_size=ws,
+                                     drop_path=[0.0, 0.0], qkv_bias=True, downsample=down)
+    _same_sd(layer, g)
+
+
+def test_vit_cls_c1_init_matches_reference():
+    """BASELINE configs[0] model (EncoderDecoderModel(ViT small, 64^2 patch 16, ViTLinear)): every tensor of the
+    seeded state_dict against the reference's checksums (tools/gen_golden.py:vit_cls_c1)."""
+    g = Golden("vit_cls_c1")
+    cfg = config.parse_config(["--encoder_name", "ViT", "--ViT.size", "small", "--ViT.patch_size", "16",
+                               "--height", "64", "--width", "64", "--task_type", "class",
+                               "--decoder_name", "ViTLinear"])
+    torch.manual_seed(15)
+    m = model_base.EncoderDecoderModel(cfg, "ViT", "ViTLinear", 1, 4)
+    _same_sd(m, g)
+
+
 def test_flag_surface_and_factories():
     cfg = config.parse_config(["--encoder_name", "ViT", "--ViT.size", "small", "--ViT.patch_size", "2",
                                "--height", "64", "--width", "64", "--task_type", "class",

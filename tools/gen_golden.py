@@ -31,6 +31,7 @@ ref_standins.install()
 sys.path.insert(0, REF)
 import backbone_swin as rswin  # noqa: E402
 import backbone_vit as rvit  # noqa: E402
+import class_heads as rcls  # noqa: E402
 import hyena as rhyena  # noqa: E402
 import mamba as rmamba  # noqa: E402
 import seg_heads as rseg  # noqa: E402
@@ -193,6 +194,115 @@ def swin_layer(seed):
     dump("swin_basic_layer", layer, **{"in/x": x}, **r)
 
 
+# Swin-tiny with Hyena / Mamba inside the windows: what every reference project script trains
+# (projects/run_*.sh: --Swin.size tiny, patch 2, window 4 or 8, use_hyena xor use_mamba; shift forced to 0 at
+# backbone_swin.py:674). Stage-1 shapes: dim 96, 3 heads (Hyena head_dim 32), Mamba d_inner 96 -> Dx 48.
+SWIN_ALT = [
+    # name, use_hyena, use_mamba, batch, grid, window
+    ("swin_hyena_w7", True, False, 1, (10, 10, 10), (7, 7, 7)),     # pad 10 -> 14, N = 343 (configs[2] window)
+    ("swin_mamba_w7", False, True, 1, (10, 10, 10), (7, 7, 7)),
+    ("swin_hyena_w4", True, False, 2, (8, 6, 10), (4, 4, 4)),       # run_cmr/abct-style window 4, ragged pad
+    ("swin_mamba_w4", False, True, 2, (8, 6, 10), (4, 4, 4)),
+    ("swin_hyena_w8", True, False, 1, (8, 9, 12), (8, 8, 8)),       # window 8, N = 512, pad 9 -> 16, 12 -> 16
+    ("swin_mamba_w8", False, True, 1, (8, 9, 12), (8, 8, 8)),
+    ("swin_mamba_w4_2d", False, True, 2, (18, 14), (4, 4)),         # run_micro: 2-D, window 4, N = 16
+    ("swin_hyena_w8_2d", True, False, 2, (12, 20), (8, 8)),         # run_vessel/ptx-style 2-D window 8
+]
+
+
+def swin_alt_layer(name, use_hyena, use_mamba, B, grid, ws, seed):
+    """BasicLayer(use_hyena | use_mamba, dim 96, depth 2, 3 heads) + PatchMergingV2, fp32 CPU fwd/bwd."""
+    torch.manual_seed(seed)
+    down = rswin.PatchMergingV2 if name.endswith("_w7") else None   # merging pinned once per mixer (size)
+    layer = rswin.BasicLayer(use_hyena, use_mamba, dim=96, depth=2, num_heads=3, window_size=ws,
+                             drop_path=[0.0, 0.0], qkv_bias=True, downsample=down).eval()
+    x = torch.randn(B, 96, *grid)
+    if use_hyena:
+        gn = ("blocks.0.attn.hyena.in_proj.weight", "blocks.1.attn.hyena.short_filter.weight",
+              "blocks.0.attn.hyena.filter_fn.bias", "blocks.1.attn.hyena.filter_fn.implicit_filter.0.weight",
+              "blocks.1.attn.hyena.out_proj.weight", "blocks.0.norm1.weight")
+    else:
+        gn = ("blocks.0.attn.mamba.in_proj.weight", "blocks.1.attn.mamba.A_log", "blocks.1.attn.mamba.D",
+              "blocks.0.attn.mamba.dt_proj.bias", "blocks.1.attn.mamba.x_proj.weight",
+              "blocks.0.attn.mamba.conv1d_z.weight", "blocks.1.attn.mamba.out_proj.weight", "blocks.0.norm1.weight")
+    if down is not None:
+        gn = gn + ("downsample.reduction.weight",)
+    r = fwd_bwd(layer, x, grads=gn)
+    dump(name, layer, **{"in/x": x, "cfg/window": np.array(ws), "cfg/hyena": int(use_hyena),
+                         "cfg/downsample": int(down is not None)}, **r)
+
+
+class _Ns:
+    """The config fields custom_ViT / ViTLinear read (backbone_vit.py:45-116, class_heads.py:13-49)."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+class _EncDec(torch.nn.Module):
+    """EncoderDecoderModel's structure (model_base.py:23-83: encoder built first, then decoder; same keys)."""
+
+    def __init__(self, enc, dec):
+        super().__init__()
+        self.encoder, self.decoder = enc, dec
+
+    def forward(self, x):
+        return self.decoder(self.encoder(x))
+
+
+def _vit_cls_model(size, img, patch, n_cls, **vit):
+    cfg = _Ns(ViT=_Ns(size=size, patch_size=list(patch), use_hyena=False, use_mamba=False, **vit),
+              time=1, height=img[0], width=img[1], task_type="class", encoder_name="ViT")
+    enc, ch = rvit.custom_ViT(cfg, 1)
+    dec = rcls.ViTLinear(cfg, ch, n_cls)
+    return _EncDec(enc, dec)
+
+
+def vit_cls_c1(seed):
+    """BASELINE configs[0]: ViT-small + ViTLinear classification, 64x64 2-D, patch 16 (L = 16 + cls token).
+    ViT-small's 21.7M weights are not stored: the state_dict is pinned by per-tensor checksums (this package's
+    modules reproduce the seeded init bit-for-bit; tests/test_modules_cpu.py), outputs and selected gradients."""
+    torch.manual_seed(seed)
+    m = _vit_cls_model("small", (64, 64), (16, 16, 16), 4).eval()
+    x = torch.rand(2, 1, 1, 64, 64)
+    gn = ("decoder.classification_head.0.weight", "decoder.classification_head.0.bias", "encoder.cls_token",
+          "encoder.patch_embedding.patch_embeddings.weight", "encoder.patch_embedding.position_embeddings",
+          "encoder.norm.weight", "encoder.blocks.11.mlp.linear2.bias", "encoder.blocks.0.attn.out_proj.weight")
+    r = fwd_bwd(m, x, grads=gn)
+    r = {k: v for k, v in r.items() if not k.startswith("grad/in")}
+    arr = {"in/x": x}
+    for k, v in m.state_dict().items():
+        arr[f"chk/{k}"] = np.array([v.double().sum().item(), v.double().abs().sum().item(), float(v.numel())])
+    for k, v in m.named_parameters():
+        arr[f"gsum/{k}"] = np.array([v.grad.double().sum().item(), v.grad.double().abs().sum().item()])
+    dump("vit_cls_c1", None, **arr, **r)
+
+
+def train_step_product(seed):
+    """Two steps of the reference's training loop (trainer_base.py:166-182, use_amp off, iters_to_accumulate 1, no
+    clipping) with its SGD (optim_base.py:90-91: momentum 0.9, lr 0.1) and CrossEntropy loss on a small ViT +
+    ViTLinear (cls token) classifier, fp32 on CPU. Every weight is stored before and after, element by element."""
+    torch.manual_seed(seed)
+    m = _vit_cls_model("custom", (16, 16), (2, 2, 2), 3, hidden_size=128, mlp_dim=256, num_layers=2, num_heads=2)
+    m.train()
+    g = torch.Generator().manual_seed(seed + 1)
+    xs = [torch.rand(2, 1, 1, 16, 16, generator=g) for _ in range(2)]
+    ys = [torch.randint(0, 3, (2,), generator=g) for _ in range(2)]
+    arr = {f"sd/{k}": v.clone() for k, v in m.state_dict().items()}
+    opt = torch.optim.SGD([{"params": list(m.parameters()), "lr": 0.1, "weight_decay": 0.0}], lr=0.1, momentum=0.9,
+                          weight_decay=0.0)
+    loss_f = torch.nn.CrossEntropyLoss()
+    for i, (x, y) in enumerate(zip(xs, ys)):
+        loss = loss_f(m(x), y)
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        arr[f"in/x{i}"], arr[f"in/y{i}"], arr[f"out/loss{i}"] = x, y, loss.detach()
+    for k, v in m.state_dict().items():
+        arr[f"post/{k}"] = v
+    dump("train_step_product", None, **arr)
+
+
 def swin_index():
     arr = {}
     ws, ss = (7, 7, 7), (3, 3, 3)
@@ -298,8 +408,21 @@ def upernet(name, nd, encoder, seed):
     dump(name, None, **arr)
 
 
-def main():
+def main(only=None):
     os.makedirs(OUT, exist_ok=True)
+    if only:                       # python tools/gen_golden.py swin_alt vit_cls_c1 train_step_product
+        torch.set_num_threads(min(8, os.cpu_count() or 1))
+        for name in only:
+            if name == "swin_alt":
+                for i, cfg in enumerate(SWIN_ALT):
+                    swin_alt_layer(*cfg, seed=20 + i)
+            elif name == "vit_cls_c1":
+                vit_cls_c1(15)
+            elif name == "train_step_product":
+                train_step_product(16)
+            else:
+                raise SystemExit(f"unknown fixture group {name}")
+        return
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     sablock("sablock_attn_h128", 128, 2, 2, 256, 0)
     sablock("sablock_attn_h192_l77", 192, 3, 1, 77, 1)
@@ -313,6 +436,10 @@ def main():
     swin_layer(9)
     swin_index()
     train_step(10)
+    train_step_product(16)
+    vit_cls_c1(15)
+    for i, cfg in enumerate(SWIN_ALT):
+        swin_alt_layer(*cfg, seed=20 + i)
     upernet("upernet2d_swin", 2, "Swin", 11)
     upernet("upernet2d_vit", 2, "ViT", 12)
     upernet("upernet3d_swin", 3, "Swin", 13)
@@ -320,4 +447,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])
