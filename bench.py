@@ -315,7 +315,9 @@ def main():
     args = ap.parse_args()
 
     if args.batch is None:
-        args.batch = 2 if args.workload in ("vit_p2_512", "vit_p4_512", "vit_hyena_p2_512", "vit_hyena_p2_1024") else 1
+        # 2 images per GPU, except the 3-D ViTUNETR / SwinUNETR configs (1 volume); the UperNet heads' BatchNorm needs
+        # 2 samples in training (the reference duplicates a batch of 1, trainer_base.py:160-164; run_abct.sh uses 2)
+        args.batch = 1 if args.workload in ("swin_p2_128", "vit_mamba_p2_256") else 2
     rank, local, world = init_distributed()
     device = torch.device("cuda", local % torch.cuda.device_count())   # % : gloo rehearsals on one GPU
     torch.cuda.set_device(device)

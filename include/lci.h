@@ -21,6 +21,8 @@
  *   lci_hyena_pre/post_*  HyenaOperator short filter + gating, model/models/hyena.py:317-355
  *   lci_upsample2x_*      UperNet2D.forward's final bilinear re-sampling (align_corners=False, 2x), model/models/
  *                         seg_heads.py:138, into the head conv's channels-last bf16 operand
+ *   lci_upsample3d_cl_fwd UperNet3D.forward's final trilinear re-sampling (seg_heads.py:273), same fusion;
+ *   lci_resample1d_adj    its adjoint (deterministic gather), one axis at a time
  *   lci_hyena_filter_*    Filter.filter (implicit-filter MLP z -> Linear/Sin x3 -> Linear, ExponentialModulation),
  *                         model/models/hyena.py:54-117,190-199, called at :343
  *   lci_conv3_fwd         MONAI-1.3 UnetResBlock 3x3(x3) convs of the ViTUNETR / SwinUNETR heads, enhance_heads.py:30-356
@@ -45,8 +47,9 @@ extern "C" {
 /* Bumped whenever an entry point's argument list or buffer contract changes (3: lci_layernorm_bwd gained dres;
  * 4: lci_conv3_wgrad writes one partial per voxel split instead of one per split and wave; 5: lci_linear_wgrad;
  * 6: lci_hyena_filter; 7: lci_upsample2x; 8: lci_gelu;
- * 9: lci_layernorm_add_fwd; 10: lci_upsample2x_nhwc). */
-#define LCI_ABI_VERSION 11
+ * 9: lci_layernorm_add_fwd; 10: lci_upsample2x_nhwc; 11: lci_fftconv Su; 12: lci_upsample3d_cl_fwd,
+ * lci_resample1d_adj and the round-3 entry points below). */
+#define LCI_ABI_VERSION 12
 const char* lci_last_error(void);
 int lci_abi_version(void);
 /* sha256 prefix of the sources the library was built from (build_lib.source_hash); the Python binding refuses a
@@ -207,6 +210,16 @@ int lci_upsample2x_bwd(const void* dy, float* dx, int B, int C, int H, int W, vo
 /* the same for a channels-last input map: x (B, H, W, C) f32 -> y (B, 2H, 2W, C) bf16; dy -> dx (B, H, W, C) f32 */
 int lci_upsample2x_nhwc_fwd(const float* x, void* y, int B, int C, int H, int W, void* stream);
 int lci_upsample2x_nhwc_bwd(const void* dy, float* dx, int B, int C, int H, int W, void* stream);
+/* ------------------------------------------------------------------ trilinear up-sampling (align_corners=False)
+ * UperNet3D.forward's final F.interpolate(x, size=input_size, mode="trilinear") (seg_heads.py:273) into the head
+ * conv's channels-last bf16 operand: x (B, D, H, W, C) f32 channels-last -> y (B, OD, OH, OW, C) bf16, any output
+ * size (scale in/out per axis, torch's arithmetic). Its adjoint, one axis at a time: lci_resample1d_adj maps
+ * dy (outer, n_out, inner) (bf16 if dy_bf16, else f32) to dx (outer, n_in, inner) f32 (written), deterministic.
+ * C % 8 == 0, inner % 8 == 0, 16-byte aligned. */
+int lci_upsample3d_cl_fwd(const float* x, void* y, int B, int C, int D, int H, int W, int OD, int OH, int OW,
+                          void* stream);
+int lci_resample1d_adj(const void* dy, int dy_bf16, float* dx, long long outer, int n_out, int n_in, long long inner,
+                       void* stream);
 
 long long lci_hyena_filter_img_elems(void);
 long long lci_hyena_filter_partials(int L, int E);

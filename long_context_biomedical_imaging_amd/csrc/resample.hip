@@ -191,6 +191,117 @@ __global__ __launch_bounds__(256) void upsample2x_nhwc_bwd_kernel(UpArgs a) {
   }
 }
 
+// ------------------------------------------------------------- trilinear up-sampling (align_corners=False)
+// UperNet3D.forward's last re-sampling (seg_heads.py:273, F.interpolate(x, size=input_size, mode="trilinear")) into
+// the head conv's channels-last bf16 operand, for any output size (scale = in / out per axis, as torch's
+// area_pixel_compute_scale with no scale factor). Forward: one thread per (output voxel, 8-channel chunk), torch's
+// upsample_trilinear3d expression in f32, rounded to bf16 (the conv's autocast cast). Backward: the adjoint applied
+// one axis at a time (resample1d_adj_kernel), each a deterministic gather over the <= 2 ceil(out / in) + 2 outputs
+// that touch an input sample — the fused 3-D gather would re-read every output 8 times.
+struct Up3Args {
+  const float* x; bf16* y;
+  int B, C, D, H, W, OD, OH, OW;
+  float sd, sh, sw;                 // in / out per axis
+};
+
+// torch: src = scale * (o + 0.5) - 0.5, clamped at 0 (area_pixel_compute_source_index, linear modes), products
+// kept unfused so that the taps match torch's for any scale
+__device__ __forceinline__ void lin_taps(int o, int n, float scale, int& i0, int& i1, float& l0, float& l1) {
+  float src = __fsub_rn(__fmul_rn(scale, __fadd_rn((float)o, 0.5f)), 0.5f);
+  src = src < 0.f ? 0.f : src;
+  i0 = (int)src;
+  i1 = i0 + (i0 < n - 1 ? 1 : 0);
+  l1 = __fsub_rn(src, (float)i0);
+  l0 = __fsub_rn(1.f, l1);
+}
+
+__global__ __launch_bounds__(256) void upsample3d_cl_fwd_kernel(Up3Args a) {
+  const int C8 = a.C / 8;
+  const long long total = (long long)a.B * a.OD * a.OH * a.OW * C8;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int q = (int)(i % C8);
+    long long p = i / C8;
+    const int ox = (int)(p % a.OW);
+    p /= a.OW;
+    const int oy = (int)(p % a.OH);
+    p /= a.OH;
+    const int oz = (int)(p % a.OD), b = (int)(p / a.OD);
+    int d0, d1, h0, h1, w0, w1;
+    float dl0, dl1, hl0, hl1, wl0, wl1;
+    lin_taps(oz, a.D, a.sd, d0, d1, dl0, dl1);
+    lin_taps(oy, a.H, a.sh, h0, h1, hl0, hl1);
+    lin_taps(ox, a.W, a.sw, w0, w1, wl0, wl1);
+    const float* base = a.x + (long long)b * a.D * a.H * a.W * a.C + 8 * q;
+    auto at = [&](int d, int h, int w) { return base + (((long long)d * a.H + h) * a.W + w) * a.C; };
+    const float* p000 = at(d0, h0, w0); const float* p001 = at(d0, h0, w1);
+    const float* p010 = at(d0, h1, w0); const float* p011 = at(d0, h1, w1);
+    const float* p100 = at(d1, h0, w0); const float* p101 = at(d1, h0, w1);
+    const float* p110 = at(d1, h1, w0); const float* p111 = at(d1, h1, w1);
+    bf16x8 v;
+#pragma unroll
+    for (int hv = 0; hv < 2; ++hv) {
+      const f32x4 x000 = *(const f32x4*)(p000 + 4 * hv), x001 = *(const f32x4*)(p001 + 4 * hv);
+      const f32x4 x010 = *(const f32x4*)(p010 + 4 * hv), x011 = *(const f32x4*)(p011 + 4 * hv);
+      const f32x4 x100 = *(const f32x4*)(p100 + 4 * hv), x101 = *(const f32x4*)(p101 + 4 * hv);
+      const f32x4 x110 = *(const f32x4*)(p110 + 4 * hv), x111 = *(const f32x4*)(p111 + 4 * hv);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        v[4 * hv + k] = (bf16)(dl0 * (hl0 * (wl0 * x000[k] + wl1 * x001[k]) + hl1 * (wl0 * x010[k] + wl1 * x011[k])) +
+                               dl1 * (hl0 * (wl0 * x100[k] + wl1 * x101[k]) + hl1 * (wl0 * x110[k] + wl1 * x111[k])));
+    }
+    *(bf16x8*)(a.y + ((((long long)b * a.OD + oz) * a.OH + oy) * a.OW + ox) * a.C + 8 * q) = v;
+  }
+}
+
+// Adjoint of 1-D linear interpolation (align_corners=False, scale = n_in / n_out) along the middle axis of
+// dy (outer, n_out, inner) -> dx (outer, n_in, inner) f32 (written): dx[., i, .] = sum_o w(o, i) dy[., o, .] over
+// the outputs o whose taps include i, in increasing o. inner % 8 == 0; one thread per (outer, i, 8-element chunk).
+struct Adj1Args {
+  const void* dy; float* dx;
+  long long outer, inner;
+  int n_out, n_in, dy_bf16;
+  float scale;
+};
+
+__global__ __launch_bounds__(256) void resample1d_adj_kernel(Adj1Args a) {
+  const long long I8 = a.inner / 8;
+  const long long total = a.outer * a.n_in * I8;
+  const float r = 1.f / a.scale;    // outputs per input sample
+  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+    const long long q = t % I8;
+    long long p = t / I8;
+    const int i = (int)(p % a.n_in);
+    const long long ou = p / a.n_in;
+    // outputs whose source coordinate lies in (i - 1, i + 1]; one extra on each side covers the f32 rounding
+    const int lo = max(0, (int)floorf(((float)i - 1.f + 0.5f) * r - 0.5f) - 1);
+    const int hi = min(a.n_out - 1, (int)ceilf(((float)i + 1.f + 0.5f) * r - 0.5f) + 1);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int o = lo; o <= hi; ++o) {
+      int i0, i1;
+      float l0, l1;
+      lin_taps(o, a.n_in, a.scale, i0, i1, l0, l1);
+      const float w = (i0 == i ? l0 : 0.f) + (i1 == i ? l1 : 0.f);
+      if (w == 0.f) continue;
+      const long long off = (ou * a.n_out + o) * a.inner + 8 * q;
+      if (a.dy_bf16) {
+        const bf16x8 g = *(const bf16x8*)((const bf16*)a.dy + off);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] = fmaf(w, (float)g[k], acc[k]);
+      } else {
+        const f32x4 g0 = *(const f32x4*)((const float*)a.dy + off), g1 = *(const f32x4*)((const float*)a.dy + off + 4);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          acc[k] = fmaf(w, g0[k], acc[k]);
+          acc[4 + k] = fmaf(w, g1[k], acc[4 + k]);
+        }
+      }
+    }
+    float* o = a.dx + (ou * a.n_in + i) * a.inner + 8 * q;
+    *(f32x4*)o = f32x4{acc[0], acc[1], acc[2], acc[3]};
+    *(f32x4*)(o + 4) = f32x4{acc[4], acc[5], acc[6], acc[7]};
+  }
+}
+
 static unsigned up_grid(long long items) {
   const long long want = (items + 255) / 256;
   return (unsigned)std::max(1LL, std::min(want, 256LL * 64));
@@ -240,6 +351,37 @@ extern "C" int lci_upsample2x_nhwc_bwd(const void* dy, float* dx, int B, int C, 
   UpArgs a{};
   a.dy = (const bf16*)dy; a.dx = dx; a.B = B; a.C = C; a.H = H; a.W = W;
   hipLaunchKernelGGL(upsample2x_nhwc_bwd_kernel, dim3(up_grid((long long)B * H * W * (C / 8))), dim3(256), 0,
+                     (hipStream_t)stream, a);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+
+// Trilinear (align_corners=False) to any size: x (B, D, H, W, C) f32 channels-last -> y (B, OD, OH, OW, C) bf16.
+extern "C" int lci_upsample3d_cl_fwd(const float* x, void* y, int B, int C, int D, int H, int W, int OD, int OH, int OW,
+                                     void* stream) {
+  LCI_CHECK(B > 0 && C > 0 && D > 0 && H > 0 && W > 0 && OD > 0 && OH > 0 && OW > 0 && C % 8 == 0,
+            "upsample3d: bad shape B=%d C=%d in %dx%dx%d out %dx%dx%d", B, C, D, H, W, OD, OH, OW);
+  LCI_CHECK(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0, "upsample3d: pointers must be 16-byte aligned");
+  Up3Args a{};
+  a.x = x; a.y = (bf16*)y; a.B = B; a.C = C; a.D = D; a.H = H; a.W = W; a.OD = OD; a.OH = OH; a.OW = OW;
+  a.sd = (float)D / (float)OD; a.sh = (float)H / (float)OH; a.sw = (float)W / (float)OW;
+  hipLaunchKernelGGL(upsample3d_cl_fwd_kernel, dim3(up_grid((long long)B * OD * OH * OW * (C / 8))), dim3(256), 0,
+                     (hipStream_t)stream, a);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+
+// Adjoint of linear interpolation along one axis: dy (outer, n_out, inner) (bf16 if dy_bf16 else f32) ->
+// dx (outer, n_in, inner) f32, scale = n_in / n_out (align_corners=False). inner % 8 == 0, 16-byte aligned.
+extern "C" int lci_resample1d_adj(const void* dy, int dy_bf16, float* dx, long long outer, int n_out, int n_in,
+                                  long long inner, void* stream) {
+  LCI_CHECK(outer > 0 && n_out > 0 && n_in > 0 && inner > 0 && inner % 8 == 0,
+            "resample1d_adj: bad shape outer=%lld n_out=%d n_in=%d inner=%lld", outer, n_out, n_in, inner);
+  LCI_CHECK(((uintptr_t)dy & 15) == 0 && ((uintptr_t)dx & 15) == 0, "resample1d_adj: pointers must be 16-byte aligned");
+  Adj1Args a{};
+  a.dy = dy; a.dx = dx; a.outer = outer; a.inner = inner; a.n_out = n_out; a.n_in = n_in; a.dy_bf16 = dy_bf16;
+  a.scale = (float)n_in / (float)n_out;
+  hipLaunchKernelGGL(resample1d_adj_kernel, dim3(up_grid(outer * n_in * (inner / 8))), dim3(256), 0,
                      (hipStream_t)stream, a);
   LCI_LAUNCH_CHECK();
   return 0;

@@ -626,6 +626,9 @@ class FPN_fuse(nn.Module):
         def resize(x, size):
             if tuple(x.shape[2:]) == tuple(size):
                 return x.to(_interp_dtype(x, mode))
+            if SEPARABLE_PSP and x.is_cuda and not _is_cl(x):
+                # separable GEMMs (f32, as torch's kernel) whose backward is a GEMM, not an atomic scatter
+                return upsample_align_corners(x, size).to(_interp_dtype(x, mode))
             return F.interpolate(x, size=size, mode=mode, align_corners=True)
 
         P = [resize(features[i], features[i - 1].shape[2:]) + features[i - 1] for i in reversed(range(1, len(features)))]
@@ -707,5 +710,11 @@ class UperNet3D(_UperNet):
             features = [self._reshape_vit_output(f) for f in features]
         features[-1] = self.PPN(features[-1])
         x = self.FPN(features)
-        x = F.interpolate(x, size=self.input_size if output_size is None else output_size, mode="trilinear")
+        size = self.input_size if output_size is None else output_size
+        if (HIP_CONV_3D and isinstance(self.head, ConvK3) and kernels.upsample3d_supported(x, size)
+                and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+            # the head conv computes in bf16 from a channels-last operand: up-sample straight into it
+            x = kernels.upsample3d_trilinear_cl(x, size)
+        else:
+            x = F.interpolate(x, size=size, mode="trilinear")
         return self.head(x)

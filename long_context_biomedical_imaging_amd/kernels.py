@@ -823,6 +823,57 @@ def upsample2x_bilinear_cl(x: torch.Tensor) -> torch.Tensor:
     return _Upsample2x.apply(x)
 
 
+class _Upsample3d(torch.autograd.Function):
+    """F.interpolate(x, size, mode="trilinear") (align_corners=False) returned as the bf16 channels-last operand of the
+    next conv (lci_upsample3d_cl_fwd); the adjoint one axis at a time (lci_resample1d_adj, deterministic gathers)
+    instead of torch's atomic scatter (upsample_trilinear3d_backward: 136 ms per Swin-UperNet3D step at 128^3)."""
+
+    @staticmethod
+    def forward(ctx, x, size):
+        B, C, D, H, W = x.shape
+        OD, OH, OW = size
+        xf = x.float().permute(0, 2, 3, 4, 1).contiguous()
+        y = torch.empty(B, OD, OH, OW, C, device=x.device, dtype=torch.bfloat16)
+        KernelTimer.run("upsample3d_fwd", 0.0, x, lambda: _lib.call(
+            "lci_upsample3d_cl_fwd", xf.data_ptr(), y.data_ptr(), B, C, D, H, W, OD, OH, OW, _lib.stream_of(x)))
+        ctx.shape, ctx.xdtype = (B, C, D, H, W, OD, OH, OW), x.dtype
+        return y.permute(0, 4, 1, 2, 3)                   # (B, C, OD, OH, OW), channels-last strides
+
+    @staticmethod
+    def backward(ctx, dy):
+        B, C, D, H, W, OD, OH, OW = ctx.shape
+        g = dy.permute(0, 2, 3, 4, 1)
+        if g.dtype not in (torch.bfloat16, torch.float32):
+            g = g.float()
+        g = g.contiguous()
+        f32 = dict(device=dy.device, dtype=torch.float32)
+        st = _lib.stream_of(dy)
+
+        def adj(src, outer, n_out, n_in, inner):
+            out = torch.empty(outer * n_in * inner, **f32)
+            KernelTimer.run("upsample3d_bwd", 0.0, dy, lambda: _lib.call(
+                "lci_resample1d_adj", src.data_ptr(), int(src.dtype == torch.bfloat16), out.data_ptr(), outer, n_out,
+                n_in, inner, st))
+            return out
+
+        t = adj(g, B, OD, D, OH * OW * C)                       # (B, D, OH, OW, C)
+        t = adj(t, B * D, OH, H, OW * C)                        # (B, D, H, OW, C)
+        t = adj(t, B * D * H, OW, W, C)                         # (B, D, H, W, C)
+        return t.view(B, D, H, W, C).permute(0, 4, 1, 2, 3).to(ctx.xdtype), None
+
+
+def upsample3d_supported(x: torch.Tensor, size) -> bool:
+    return (x.is_cuda and x.dim() == 5 and len(size) == 3 and x.shape[1] % 8 == 0
+            and x.dtype in (torch.float32, torch.bfloat16))
+
+
+def upsample3d_trilinear_cl(x: torch.Tensor, size) -> torch.Tensor:
+    """Trilinear up-sampling to `size`, align_corners=False (seg_heads.py:273), as bf16 with channels-last strides."""
+    if not x.is_cuda:
+        raise _lib.LciError("upsample3d runs on the GPU only; there is no CPU path")
+    return _Upsample3d.apply(x, tuple(int(s) for s in size))
+
+
 # ------------------------------------------------------------------- decoder-head 3x3(x3) convolution
 def conv3_cl(x_cl: torch.Tensor, w_packed: torch.Tensor, kd: int) -> torch.Tensor:
     """x_cl (B, D, H, W, Cin) bf16 channels-last, w_packed (Cout, kd*9, Cin) bf16 -> (B, D, H, W, Cout) bf16."""

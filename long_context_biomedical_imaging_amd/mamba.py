@@ -72,10 +72,22 @@ class MambaVisionMixer(nn.Module):
         xs, yz = kernels.dwconv_silu_pair(xz, self.conv1d_x.weight, self.conv1d_x.bias,
                                           self.conv1d_z.weight, self.conv1d_z.bias)
         A = -torch.exp(self.A_log.float())
-        x_dbl = self.x_proj(xs)                                            # (B, L, dt_rank + 2N)
-        dt = self.dt_proj(x_dbl[..., : self.dt_rank])                      # (B, L, Dx), bias added once
-        N = self.d_state
-        Bm = x_dbl[..., self.dt_rank: self.dt_rank + N]
-        Cm = x_dbl[..., self.dt_rank + N:]
+        N, R = self.d_state, self.dt_rank
+        es = 2 if torch.is_autocast_enabled("cuda") else xs.element_size()
+        if (R * es) % 16 or ((R + 2 * N) * es) % 16 or (N * es) % 16:
+            # the scan reads B / C rows with 16-byte vectors: when dt_rank breaks their alignment (Swin stages,
+            # d_model 96 / 192 -> dt_rank 6 / 12) the same projection is computed with its output columns
+            # reordered to [B | C | dt | 0-pad to 8] (the weight rows permuted, gradients flow back through cat)
+            pad = (-(R + 2 * N)) % 8
+            W = self.x_proj.weight
+            w = torch.cat([W[R:], W[:R]] + ([W.new_zeros(pad, W.shape[1])] if pad else []), 0)
+            x_dbl = kernels.linear(xs, w, None)                            # (B, L, 2N + R + pad)
+            Bm, Cm = x_dbl[..., :N], x_dbl[..., N:2 * N]
+            dt = self.dt_proj(x_dbl[..., 2 * N:2 * N + R])
+        else:
+            x_dbl = self.x_proj(xs)                                        # (B, L, dt_rank + 2N)
+            dt = self.dt_proj(x_dbl[..., :R])                              # (B, L, Dx), bias added once
+            Bm = x_dbl[..., R: R + N]
+            Cm = x_dbl[..., R + N:]
         y = kernels.selective_scan_cl(xs, dt, A, Bm, Cm, self.D.float(), self.dt_proj.bias.float(), yz)
         return self.out_proj(y)

@@ -69,3 +69,29 @@ def test_upernet2d_head_path_matches_interpolate(monkeypatch):
         outs.append((o.float(), xi.grad.clone()))
     assert rel_err(outs[1][0], outs[0][0]) < 1e-3
     assert rel_err(outs[1][1], outs[0][1]) < 1e-2
+
+
+@pytest.mark.parametrize("B,C,inp,out", [(1, 192, (8, 8, 8), (32, 32, 32)), (2, 16, (4, 5, 6), (9, 10, 12)),
+                                         (2, 8, (3, 1, 7), (12, 4, 7)), (1, 64, (16, 16, 16), (64, 64, 64))])
+def test_upsample3d_vs_torch(B, C, inp, out):
+    """lci_upsample3d_cl_fwd / lci_resample1d_adj (UperNet3D's final trilinear re-sampling, seg_heads.py:273): forward
+    within one bf16 ulp of bf16(F.interpolate(x, mode="trilinear")) (torch's f32 expression, rounded as the head
+    conv's autocast cast), backward vs torch's autograd on the same bf16 cotangent (rel-L2 <= 1e-6), integer and
+    non-integer scales, a size-1 axis."""
+    from long_context_biomedical_imaging_amd import kernels
+    torch.manual_seed(B * 100 + C + sum(inp))
+    x = torch.randn(B, C, *inp, device="cuda")
+    assert kernels.upsample3d_supported(x, out)
+    xr = x.clone().requires_grad_(True)
+    ref = F.interpolate(xr, size=out, mode="trilinear")
+    xc = x.clone().requires_grad_(True)
+    y = kernels.upsample3d_trilinear_cl(xc, out)
+    assert y.shape == ref.shape and y.dtype == torch.bfloat16
+    assert y.permute(0, 2, 3, 4, 1).is_contiguous()
+    diff = (y.float() - ref.detach().to(torch.bfloat16).float()).abs()
+    ulp = ref.detach().abs() * 2.0 ** -7 + 1e-6 * x.abs().max()
+    assert bool((diff <= ulp).all()), diff.max().item()
+    g = torch.randn_like(ref).to(torch.bfloat16)
+    ref.backward(g.float())
+    y.backward(g)
+    assert rel_err(xc.grad, xr.grad) < 1e-6
