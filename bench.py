@@ -45,7 +45,10 @@ HBM_PEAK_GBS = 8000.0
 ROOF = {"selective_scan_fwd": ("hbm", 1.0), "selective_scan_bwd": ("hbm", 1.0),
         "fftconv_fwd": ("hbm", 8.0), "fftconv_bwd": ("hbm", 16.0),
         # LayerNorm work is counted in bytes already (f32 x in, bf16 y out; bwd + bf16 dy in, f32 dx out)
-        "ln_fwd": ("hbm", 1.0), "ln_bwd": ("hbm", 1.0)}
+        "ln_fwd": ("hbm", 1.0), "ln_bwd": ("hbm", 1.0),
+        # direct (Toeplitz) long conv of Swin-window rows: FLOPs on the f32-input MFMA (157.3 TF dense)
+        "direct_conv_fwd": ("mfma_f32", 1.0), "direct_conv_bwd": ("mfma_f32", 1.0), "direct_conv_dk": ("mfma_f32", 1.0)}
+MFMA_F32_PEAK_TFLOPS = 157.3     # v_mfma_f32_32x32x2_f32, MI355X_MICROARCH.md chip table
 
 WORKLOADS = {
     # metric config (BASELINE.json `metric`, configs[1] shape at patch 2): ViT-small, patch 2, 512x512 -> L = 65536
@@ -265,15 +268,18 @@ def run_workload(workload, batch, steps, warmup, rank, world, device, kernel_tim
         if d["work_per_call"]:
             b, pu = ROOF.get(name, ("mfma", 1.0))
             rate = d["work_per_call"] * pu / (d["avg_ms"] * 1e-3)
-            kern[name]["tflops" if b == "mfma" else "gbs"] = round(rate / (1e12 if b == "mfma" else 1e9), 1)
+            kern[name]["tflops" if b.startswith("mfma") else "gbs"] = round(rate / (1e12 if b.startswith("mfma")
+                                                                                   else 1e9), 1)
     roof = None
     if ksum:
         dom = max((n for n in ksum if ksum[n]["work_per_call"]), key=lambda n: ksum[n]["total_ms"])
         dd = ksum[dom]
         bound, per_unit = ROOF.get(dom, ("mfma", 1.0))
         work = dd["work_per_call"] * per_unit
-        if bound == "mfma":
-            ach, peak, unit = work / (dd["avg_ms"] * 1e-3) / 1e12, MFMA_BF16_PEAK_TFLOPS, "TFLOP/s"
+        if bound.startswith("mfma"):
+            peak = MFMA_F32_PEAK_TFLOPS if bound == "mfma_f32" else MFMA_BF16_PEAK_TFLOPS
+            ach, unit = work / (dd["avg_ms"] * 1e-3) / 1e12, "TFLOP/s"
+            bound = "mfma"
         else:
             ach, peak, unit = work / (dd["avg_ms"] * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s"
         roof = {"kernel": dom, "bound": bound, "achieved": round(ach, 1), "peak": peak,

@@ -18,6 +18,7 @@
  *   lci_selective_scan_*  mamba_ssm selective_scan_fn (mamba-ssm 1.2.0.post1) as called at model/models/mamba.py:125-134
  *   lci_dwconv_silu_*     MambaVisionMixer depthwise conv1d + SiLU, model/models/mamba.py:118-119
  *   lci_fftconv_*         fftconv_ref (gelu=False), model/models/hyena.py:32-51 / Filter.forward :201-216
+ *   lci_direct_conv_*     the same long convolution for Swin-window rows (L <= 512, backbone_swin.py:361-362)
  *   lci_hyena_pre/post_*  HyenaOperator short filter + gating, model/models/hyena.py:317-355
  *   lci_upsample2x_*      UperNet2D.forward's final bilinear re-sampling (align_corners=False, 2x), model/models/
  *                         seg_heads.py:138, into the head conv's channels-last bf16 operand
@@ -179,6 +180,17 @@ int lci_fftconv_fwd(const float* u, const void* K, const float* Dv, float* y, vo
 int lci_fftconv_bwd(const float* dy, const float* u, const void* K, const float* Dv, float* du, float* dk,
                     float* dD, void* S, void* S2, const void* Su, void* SK, const void* tw, int R, int C, int L,
                     void* stream);
+/* Direct causal long convolution for short rows (L <= lci_direct_conv_max_len(): the Swin-window sequences of
+ * backbone_swin.py:361-362), exact f32 products on the f32 MFMA instead of an FFT. u, y (R, C, L) f32 channel-major
+ * rows (filter of row r*C + c is c), k (C, L), D (C) f32 or null.
+ * fwd: adjoint = 0: y = causal_conv(u, k) + D u;  adjoint = 1: y = corr(u, k) + D u, i.e. du from dy (written).
+ * dk: part (lci_direct_conv_dk_splits(R, C, L), C, L) f32 <- per-row-split sums of dy[r][t] u[r][t - tau]
+ *     (written); dk = sum over the first axis, dD[c] = dk[c][0] (caller). Deterministic. */
+int lci_direct_conv_max_len(void);
+int lci_direct_conv_fwd(const float* u, const float* k, const float* D, float* y, int R, int C, int L, int adjoint,
+                        void* stream);
+int lci_direct_conv_dk_splits(int R, int C, int L);
+int lci_direct_conv_dk(const float* dy, const float* u, float* part, int R, int C, int L, void* stream);
 /* z (BB, L, 3D) channels-last in_proj output; causal depthwise conv (w (3D, K), bias (3D)); per head h,
  * x1/x2/v = conv channels [h*3hd, +hd), [+hd, +2hd), [+2hd, +3hd). vg = v*x1 -> (BB, D, L) f32 rows;
  * x2 -> (BB, L, D) channels-last (z dtype). */

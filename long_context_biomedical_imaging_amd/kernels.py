@@ -566,6 +566,63 @@ class _FFTConv(torch.autograd.Function):
         return du, (dk.to(ctx.kdtype) if dk is not None else None), dD
 
 
+_DIRECT_MAX = None
+
+
+def direct_conv_max_len() -> int:
+    """Longest row on the direct (Toeplitz, f32 MFMA) long-conv path; LCI_DIRECT_CONV=0 forces the FFT path."""
+    global _DIRECT_MAX
+    if _DIRECT_MAX is None:
+        _DIRECT_MAX = int(_lib.load().lci_direct_conv_max_len()) if os.environ.get("LCI_DIRECT_CONV", "1") != "0" else 0
+    return _DIRECT_MAX
+
+
+class _DirectConv(torch.autograd.Function):
+    """y = causal_conv(u, k) + D u for short rows (R, C, L) f32 (Swin windows): lci_direct_conv_fwd / _dk."""
+
+    @staticmethod
+    def forward(ctx, u, k, D):
+        R, C, L = u.shape
+        kf = k.float().contiguous()
+        Dv = D.float().contiguous()
+        y = torch.empty_like(u)
+        fl = float(R * C) * L * (L + 1)     # algorithmic FLOPs: 2 per multiply-add of the causal (triangular) sum
+        KernelTimer.run("direct_conv_fwd", fl, u, lambda: _lib.call(
+            "lci_direct_conv_fwd", u.data_ptr(), kf.data_ptr(), Dv.data_ptr(), y.data_ptr(), R, C, L, 0,
+            _lib.stream_of(u)))
+        ctx.save_for_backward(u, kf, Dv)
+        ctx.kdtype = k.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        u, kf, Dv = ctx.saved_tensors
+        R, C, L = u.shape
+        dy = dy.float().contiguous()
+        du = torch.empty_like(u)
+        fl = float(R * C) * L * (L + 1)
+        KernelTimer.run("direct_conv_bwd", fl, u, lambda: _lib.call(
+            "lci_direct_conv_fwd", dy.data_ptr(), kf.data_ptr(), Dv.data_ptr(), du.data_ptr(), R, C, L, 1,
+            _lib.stream_of(u)))
+        dk = dD = None
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            ns = int(_lib.load().lci_direct_conv_dk_splits(R, C, L))
+            part = torch.empty(ns, C, L, device=u.device, dtype=torch.float32)
+            KernelTimer.run("direct_conv_dk", fl, u, lambda: _lib.call(
+                "lci_direct_conv_dk", dy.data_ptr(), u.data_ptr(), part.data_ptr(), R, C, L, _lib.stream_of(u)))
+            g = part.sum(0)
+            dk = g.to(ctx.kdtype) if ctx.needs_input_grad[1] else None
+            dD = g[:, 0].clone() if ctx.needs_input_grad[2] else None
+        return du, dk, dD
+
+
+def _long_conv(rows, k, D):
+    """The long-conv autograd op for channel-major f32 rows (R, C, L): direct for short rows, FFT otherwise."""
+    if rows.shape[-1] <= direct_conv_max_len():
+        return _DirectConv.apply(rows, k, D)
+    return _FFTConv.apply(rows, k, D)
+
+
 def fftconv(u, k, D):
     """fftconv_ref (hyena.py:32-51, gelu=False): u (..., C, L), k (C, L), D (C) -> causal conv + D u, in u.dtype.
 
@@ -575,7 +632,7 @@ def fftconv(u, k, D):
     shp = u.shape
     C, L = shp[-2], shp[-1]
     rows = u.float().reshape(-1, C, L).contiguous()
-    y = _FFTConv.apply(rows, k, D)
+    y = _long_conv(rows, k, D)
     return y.reshape(shp).to(u.dtype)
 
 
@@ -657,7 +714,7 @@ def hyena_fftconv_gate(vg, k, bias, x2):
     """(causal_conv(vg, k) + bias * vg) * x2, returned channels-last (B, L, D) in x2's dtype (hyena.py:343-355)."""
     BB, D, L = vg.shape
     hd = k.shape[0]
-    y = _FFTConv.apply(vg.reshape(BB * (D // hd), hd, L), k, bias).reshape(BB, D, L)
+    y = _long_conv(vg.reshape(BB * (D // hd), hd, L), k, bias).reshape(BB, D, L)
     return _HyenaPost.apply(y, x2)
 
 

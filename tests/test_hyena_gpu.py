@@ -203,3 +203,35 @@ def test_hyena_short_conv_gate_vs_torch(BB, L, H, hd, K, dtype):
     tw = 1e-4 if dtype == torch.float32 else 1e-2
     assert rel_err(wc.grad, wr.grad) < tw
     assert rel_err(bc.grad, br.grad) < tw
+
+
+@pytest.mark.parametrize("R,C,L", [(3072, 32, 512), (40, 32, 343), (7, 3, 64), (33, 32, 16), (5, 8, 49),
+                                   (64, 64, 100), (2, 4, 1), (9, 5, 511)])
+def test_direct_long_conv_vs_oracle(R, C, L):
+    """The direct (Toeplitz, f32 MFMA) long conv taken for Swin-window rows (L <= 512; backbone_swin.py:361-362): y,
+    du, dk and dD against fp64 autograd of the oracle's fftconv (hyena.py:32-51 semantics) at the f32 bounds of the
+    FFT path (2e-5 outputs, 1e-4 gradients), plus the FFT path itself on the same rows (LCI_DIRECT_CONV=0)."""
+    from long_context_biomedical_imaging_amd import kernels
+    assert L <= kernels.direct_conv_max_len()
+    torch.manual_seed(R + C + L)
+    u = torch.randn(R, C, L)
+    k = torch.randn(C, L) * torch.exp(-torch.linspace(0, 4, L))[None]
+    D = torch.randn(C)
+    uc, kc, Dc = (t.cuda().requires_grad_(True) for t in (u, k, D))
+    y = kernels._DirectConv.apply(uc, kc, Dc)
+    ur, kr, Dr = (t.double().requires_grad_(True) for t in (u, k, D))
+    ref = oh.fftconv(ur[None], kr, Dr)[0] if R * C * L <= 2 ** 22 else None
+    if ref is None:   # large case: direct fp64 sums on a row subset
+        rows = torch.tensor([0, 1, R // 2, R - 1])
+        ref_rows = oh.fftconv(u[rows].double()[None], k.double(), D.double())[0]
+        assert rel_err(y[rows], ref_rows) < 2e-5
+    else:
+        assert rel_err(y, ref) < 2e-5
+        cot = torch.randn(R, C, L)
+        y.backward(cot.cuda())
+        (ref * cot.double()).sum().backward()
+        assert rel_err(uc.grad, ur.grad) < 1e-4
+        assert rel_err(kc.grad, kr.grad) < 1e-4
+        assert rel_err(Dc.grad, Dr.grad) < 1e-4
+    yf = kernels._FFTConv.apply(u.cuda(), k.cuda(), D.cuda())
+    assert rel_err(y, yf) < 2e-5
