@@ -104,6 +104,13 @@ long long lci_window_dS_elems(const int* geo);
  * derived from the padded coordinate; wtype (Bw) = the bias-table type of each window. */
 int lci_window_index_map(const int* geo, int* src_row, int* region, int* rid, int* wtype, void* stream);
 
+/* Grid-mode window partition for the Hyena / Mamba mixers inside Swin windows (backbone_swin.py:445-487, 361-365):
+ * scatter = 0: win (Bw, N, C) <- grid (B, S0, S1[, S2], C): F.pad (zeros) -> roll(-shift) -> window_partition;
+ * scatter = 1: grid <- win for the non-padded tokens: window_reverse -> roll(+shift) -> crop. Rows of C elements of
+ * elem_bytes (2 or 4) bytes, C * elem_bytes % 16 == 0, 16-byte aligned; geo as above (mode 1, C in geo[14]). The
+ * index map is win_row(), the one the attention kernels and lci_window_index_map use. */
+int lci_window_gather(const void* src, void* dst, int elem_bytes, const int* geo, int scatter, void* stream);
+
 /* ------------------------------------------------------------------ decoder-head 3x3(x3) convolution
  * Replaces the kernel-3 stride-1 convs of MONAI-1.3 UnetResBlock (get_conv_layer conv_only, bias=False) in the
  * ViTUNETR / SwinUNETR heads (model/models/enhance_heads.py:30-356).

@@ -65,6 +65,7 @@ SIGNATURES = {
     "lci_upsample3d_cl_fwd": [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "lci_resample1d_adj": [_P, _I, _P, _L, _I, _I, _L, _P],
     "lci_direct_conv_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _P],
+    "lci_window_gather": [_P, _P, _I, _P, _I, _P],
     "lci_direct_conv_dk": [_P, _P, _P, _I, _I, _I, _P],
     "lci_hyena_filter_prep": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P],
     "lci_hyena_filter_fwd": [_P, _P, _P, _P, _I, _I, _F, _P, _P],

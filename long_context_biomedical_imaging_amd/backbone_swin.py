@@ -227,7 +227,13 @@ class SwinTransformerBlock(nn.Module):
         window_size, shift_size = get_window_size(dims_sp, self.window_size, self.shift_size)
         if not self.attn.use_hyena and not self.attn.use_mamba:
             return self.attn.forward_grid(x, window_size, shift_size)
-        # Hyena / Mamba inside windows (shift is always 0 there, backbone_swin.py:674): explicit partition
+        if any(i > 0 for i in shift_size):
+            raise NotImplementedError("shifted windows with hyena/mamba do not occur in the reference")
+        if x.is_cuda and kernels.window_gather_supported(x):
+            # Hyena / Mamba inside windows (shift 0, backbone_swin.py:674): F.pad + window_partition as one gather,
+            # window_reverse + crop as one scatter (lci_window_gather)
+            xw = kernels.window_partition_grid(x, window_size, shift_size)
+            return kernels.window_reverse_grid(self.attn(xw, mask=None), x.shape, window_size, shift_size)
         c = x.shape[-1]
         pads = [(window_size[i] - s % window_size[i]) % window_size[i] for i, s in enumerate(dims_sp)]
         padarg = []

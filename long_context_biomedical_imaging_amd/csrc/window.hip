@@ -22,6 +22,8 @@
 //           Pad-token dK/dV go to the qkv bias gradient. d(rpb) = sum over windows of dS (reduction kernel).
 #include "common.hpp"
 
+#include <algorithm>
+
 // scheduling-strategy hooks for A/B runs (tools/attn_variants.sh): iglp_opt(N) on the fwd / bwd tile loops
 #ifdef LCI_WIN_IGLP_FWD
 #define LCI_WIN_FWD_SCHED() __builtin_amdgcn_iglp_opt(LCI_WIN_IGLP_FWD)
@@ -529,6 +531,30 @@ __global__ __launch_bounds__(256) void win_index_map_kernel(WinArgs a, int* src_
   if (n == 0) wtype[w] = t;
 }
 
+// Window gather / scatter for the Hyena / Mamba mixers inside Swin windows (backbone_swin.py:445-487 with
+// WindowAttention :361-365): F.pad -> roll(-shift) -> window_partition as one gather of 16-byte row chunks
+// (padded voxels read as zeros: the reference pads the LayerNorm output with zeros), window_reverse -> roll(+shift)
+// -> crop as the inverse scatter. Both use win_row(), so the maps are the ones the attention kernels use (and
+// lci_window_index_map exports). One thread per (window token, 16-byte chunk); rows of C * elem_bytes bytes.
+__global__ __launch_bounds__(256) void win_gather_kernel(WinArgs a, const char* src, char* dst, int row_bytes,
+                                                         int scatter) {
+  const int nch = row_bytes / 16;
+  const long long total = (long long)a.Bw * a.N * nch;
+  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const int ch = (int)(e % nch);
+    const long long wn = e / nch;
+    const int w = (int)(wn / a.N), n = (int)(wn % a.N);
+    int rid;
+    const int row = win_row(a, w, n, rid);
+    char* wp = (scatter ? (char*)src : dst) + wn * row_bytes + 16 * ch;   // window-token row
+    if (scatter) {
+      if (row >= 0) *(u32x4*)(dst + (long long)row * row_bytes + 16 * ch) = *(const u32x4*)wp;
+    } else {
+      *(u32x4*)wp = row >= 0 ? *(const u32x4*)(src + (long long)row * row_bytes + 16 * ch) : u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+}
+
 static int win_fill(WinArgs& a, const int* geo, float scale) {
   // geo: [mode, nd, S0, S1, S2, ws0, ws1, ws2, sh0, sh1, sh2, Bw_or_B, nW, N, C, H]
   a.mode = geo[0]; a.nd = geo[1];
@@ -639,6 +665,29 @@ extern "C" int lci_window_index_map(const int* geo, int* src_row, int* region, i
   const long long n = (long long)a.Bw * a.N;
   hipLaunchKernelGGL(win_index_map_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a,
                      src_row, region, rid, wtype);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+
+// Grid-mode window gather (scatter = 0): win (Bw, N, C) <- grid (B, S0, S1[, S2], C) with zero rows for padded
+// voxels; scatter (= 1): grid <- win for every non-padded window token (each grid row written exactly once).
+// elem_bytes 2 or 4; C * elem_bytes % 16 == 0; geo as lci_window_attn_fwd (mode 1; its C / H fields unused).
+extern "C" int lci_window_gather(const void* src, void* dst, int elem_bytes, const int* geo, int scatter,
+                                 void* stream) {
+  LCI_CHECK(geo[0] == 1, "window_gather: grid mode only");
+  int g[16];
+  for (int i = 0; i < 16; ++i) g[i] = geo[i];
+  const int C = geo[14];
+  LCI_CHECK(C > 0 && (elem_bytes == 2 || elem_bytes == 4) && (C * elem_bytes) % 16 == 0,
+            "window_gather: C %d x %d bytes must be a multiple of 16", C, elem_bytes);
+  LCI_CHECK(((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0, "window_gather: pointers must be 16-byte aligned");
+  g[14] = WHD; g[15] = 1;   // win_fill's head-dim check does not apply to a plain gather
+  WinArgs a{};
+  if (win_fill(a, g, 1.f)) return 1;
+  const long long n = (long long)a.Bw * a.N * (C * elem_bytes / 16);
+  const unsigned blocks = (unsigned)std::min<long long>((n + 255) / 256, 65536LL);
+  hipLaunchKernelGGL(win_gather_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a, (const char*)src,
+                     (char*)dst, C * elem_bytes, scatter);
   LCI_LAUNCH_CHECK();
   return 0;
 }

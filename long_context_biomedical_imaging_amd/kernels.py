@@ -477,6 +477,67 @@ def window_attention_grid(qkv, bias, rpb, num_heads, scale, window_size, shift_s
     return o if dt == torch.bfloat16 else o.to(dt)
 
 
+def _win_move(src, dst, geo, scatter):
+    _lib.call("lci_window_gather", src.data_ptr(), dst.data_ptr(), src.element_size(), _i32(geo), int(scatter),
+              _lib.stream_of(src))
+
+
+class _WindowGather(torch.autograd.Function):
+    """grid (B, *S, C) -> windows (B*nW, N, C): F.pad + roll(-shift) + window_partition; adjoint = the scatter."""
+
+    @staticmethod
+    def forward(ctx, x, geo):
+        B, C = x.shape[0], x.shape[-1]
+        x = x.contiguous()
+        win = torch.empty(B * geo[12], geo[13], C, device=x.device, dtype=x.dtype)
+        KernelTimer.run("window_gather", 0.0, x, lambda: _win_move(x, win, geo, False))
+        ctx.geo, ctx.shape = geo, x.shape
+        return win
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        dx = torch.empty(ctx.shape, device=g.device, dtype=g.dtype)
+        KernelTimer.run("window_scatter", 0.0, g, lambda: _win_move(g, dx, ctx.geo, True))
+        return dx, None
+
+
+class _WindowScatter(torch.autograd.Function):
+    """windows (B*nW, N, C) -> grid (B, *S, C): window_reverse + roll(+shift) + crop; adjoint = the gather."""
+
+    @staticmethod
+    def forward(ctx, win, geo, shape):
+        win = win.contiguous()
+        out = torch.empty(shape, device=win.device, dtype=win.dtype)
+        KernelTimer.run("window_scatter", 0.0, win, lambda: _win_move(win, out, geo, True))
+        ctx.geo, ctx.wshape = geo, win.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        dw = torch.empty(ctx.wshape, device=g.device, dtype=g.dtype)
+        KernelTimer.run("window_gather", 0.0, g, lambda: _win_move(g, dw, ctx.geo, False))
+        return dw, None, None
+
+
+def window_gather_supported(x: torch.Tensor) -> bool:
+    return x.is_cuda and x.dtype in (torch.float32, torch.bfloat16) and (x.shape[-1] * x.element_size()) % 16 == 0
+
+
+def window_partition_grid(x, window_size, shift_size):
+    """x (B, S0, S1[, S2], C) channels-last -> (B * nW, N, C) windows, zero rows for the padding (the reference's
+    F.pad of the LayerNorm output, roll(-shift) and window_partition, backbone_swin.py:445-465)."""
+    geo = grid_geo(x.shape[0], x.shape[1:-1], window_size, shift_size, x.shape[-1], 1)
+    return _WindowGather.apply(x, geo)
+
+
+def window_reverse_grid(win, grid_shape, window_size, shift_size):
+    """(B * nW, N, C) windows -> (B, S0, S1[, S2], C): window_reverse, roll(+shift) and the crop (:469-487)."""
+    geo = grid_geo(grid_shape[0], grid_shape[1:-1], window_size, shift_size, grid_shape[-1], 1)
+    return _WindowScatter.apply(win, geo, tuple(grid_shape))
+
+
 def window_attention(qkv, rpb, mask, num_heads, scale):
     """Pre-partitioned windows (WindowAttention.forward signature): qkv (Bw, N, 3C), mask (nW, N, N) or None."""
     _lib.require_gpu(qkv.contiguous())

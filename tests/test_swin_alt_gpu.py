@@ -12,6 +12,7 @@ bounds the single-mixer autocast tests use (tests/test_mamba_gpu.py, tests/test_
 """
 import pytest
 import torch
+import torch.nn.functional as F
 
 from golden_util import Golden, cotangents, rel_err
 
@@ -57,3 +58,35 @@ def test_swin_alt_layer_vs_reference(name, amp):
     for p in _grad_names(g):
         e = rel_err(params[p].grad, g.t(f"grad/{p}"))
         assert e < (6e-2 if amp else 1e-3), f"{p}: rel err {e:.3e}"
+
+
+@pytest.mark.parametrize("B,dims,ws,dtype", [(2, (10, 10, 10), (7, 7, 7), torch.bfloat16),
+                                             (1, (8, 6, 10), (4, 4, 4), torch.float32),
+                                             (2, (5, 9, 40), (5, 7, 7), torch.bfloat16),   # collapsed window axis
+                                             (2, (18, 14), (4, 4), torch.float32),
+                                             (1, (64, 64, 64), (4, 4, 4), torch.bfloat16)])
+def test_window_gather_scatter_bit_exact(B, dims, ws, dtype):
+    """lci_window_gather (the Hyena / Mamba window path) against the reference op sequence, bit for bit: F.pad of
+    the LayerNorm output with zeros + window_partition (backbone_swin.py:445-465) and window_reverse + crop
+    (:469-487); both directions of both autograd ops (each one's adjoint is the other)."""
+    from long_context_biomedical_imaging_amd import kernels
+    from oracle import window as ow
+    C = 96
+    g = torch.Generator().manual_seed(B * 7 + sum(dims))
+    x = torch.randn(B, *dims, C, generator=g).to(dtype)
+    pads = [(w - s % w) % w for s, w in zip(dims, ws)]
+    padarg = []
+    for p in reversed(pads):
+        padarg += [0, p]
+    xp = F.pad(x, [0, 0] + padarg)
+    ref = ow.window_partition(xp, ws)
+    xc = x.cuda().requires_grad_(True)
+    win = kernels.window_partition_grid(xc, ws, (0,) * len(ws))
+    assert win.shape == ref.shape and torch.equal(win.cpu(), ref)
+    back = kernels.window_reverse_grid(win, x.shape, ws, (0,) * len(ws))
+    assert torch.equal(back.cpu(), x)
+    cot = torch.randn(ref.shape, generator=g).to(dtype)
+    rev = ow.window_reverse(cot, ws, [B, *xp.shape[1:-1]])
+    crop = rev[tuple([slice(None)] + [slice(0, s) for s in dims])]
+    win.backward(cot.cuda())
+    assert torch.equal(xc.grad.cpu(), crop)
