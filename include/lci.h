@@ -164,11 +164,13 @@ int lci_selective_scan_bwd(int dtype, const void* u, const void* delta, const fl
 int lci_dwconv_silu_fwd(int dtype, const void* in, const float* wx, const float* bx, const float* wz,
                         const float* bz, void* ox, void* oz, int B, int L, int C, int K, int in_ts, int ox_ts,
                         int oz_ts, int zoff, void* stream);
-/* din (B, L, 2C) written; dwx, dbx, dwz, dbz accumulated. gx / gz: grads of ox / oz (same layouts). */
+/* din (B, L, 2C) written. gx / gz: grads of ox / oz (same layouts). part (lci_dwconv_silu_bwd_part_rows(B, L), 2C, 4)
+ * f32 written with per-(sequence, 256-token run) sums of (dw0, dw1, dw2, db) per channel (x half first); the caller
+ * sums the first axis (deterministic; ABI 12 replaced the accumulated dwx/dbx/dwz/dbz float atomics). */
+long long lci_dwconv_silu_bwd_part_rows(int B, int L);
 int lci_dwconv_silu_bwd(int dtype, const void* in, const float* wx, const float* bx, const float* wz,
-                        const float* bz, const void* gx, const void* gz, void* din, float* dwx, float* dbx,
-                        float* dwz, float* dbz, int B, int L, int C, int K, int in_ts, int ox_ts, int oz_ts,
-                        int zoff, void* stream);
+                        const float* bz, const void* gx, const void* gz, void* din, float* part, int B, int L, int C,
+                        int K, int in_ts, int ox_ts, int oz_ts, int zoff, void* stream);
 
 /* ------------------------------------------------------------------ Hyena long convolution (f32)
  * FFT size n = lci_fft_size(L) = pow2 >= 2L (L <= 262144). tw: n complex f32 (f32x2) from lci_fft_twiddles.

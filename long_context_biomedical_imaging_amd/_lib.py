@@ -51,7 +51,7 @@ SIGNATURES = {
     "lci_layernorm_fwd": [_P, _P, _P, _P, _I, _P, _P, _L, _I, _F, _P],
     "lci_layernorm_add_fwd": [_P, _P, _I, _P, _P, _P, _P, _I, _P, _P, _L, _I, _F, _P],
     "lci_layernorm_bwd": [_P, _P, _I, _P, _P, _P, _P, _P, _P, _L, _I, _P],
-    "lci_dwconv_silu_bwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    "lci_dwconv_silu_bwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "lci_linear_wgrad": [_P, _L, _P, _L, _L, _I, _I, _P, _P, _P],
     "lci_linear_fwd": [_I, _P, _L, _P, _P, _P, _L, _P, _L, _L, _I, _I, _P],
     "lci_linear_small_fwd": [_P, _L, _P, _P, _P, _L, _I, _I, _P],
@@ -124,6 +124,12 @@ def load(path: str = LIB_PATH):
     lib.lci_hyena_filter_partials.argtypes = [_I, _I]
     lib.lci_fft_size.restype = ctypes.c_longlong
     lib.lci_fft_size.argtypes = [_I]
+    lib.lci_dwconv_silu_bwd_part_rows.restype = ctypes.c_longlong
+    lib.lci_dwconv_silu_bwd_part_rows.argtypes = [_I, _I]
+    lib.lci_direct_conv_max_len.restype = ctypes.c_int
+    lib.lci_direct_conv_max_len.argtypes = []
+    lib.lci_direct_conv_dk_splits.restype = ctypes.c_int
+    lib.lci_direct_conv_dk_splits.argtypes = [_I, _I, _I]
     for name, argt in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.argtypes = argt

@@ -668,7 +668,7 @@ struct ConvArgs {
   void* ox; void* oz;
   const void* gx; const void* gz;   // bwd: grads of the SiLU outputs
   void* din;                        // bwd: (B, L, 2C)
-  float* dwx; float* dbx; float* dwz; float* dbz;
+  float* part;                      // bwd: (B * ceil(L / CONV_T), 2C, 4) f32 per-run sums of (dw0, dw1, dw2, db)
   int B, L, C, in_ts, ox_ts, oz_ts, zoff;
 };
 
@@ -731,12 +731,9 @@ __global__ __launch_bounds__(256) void dwconv_silu_bwd_kernel(ConvArgs a) {
     xa = xb; xb = xc; xc = xd; xd = xe;
     gm = g0; g0 = gp;
   }
-  float* dw = (half ? a.dwz : a.dwx) + c * CONV_K;
-  atomicAdd(dw + 0, dw0);
-  atomicAdd(dw + 1, dw1);
-  atomicAdd(dw + 2, dw2);
-  float* dbp = half ? a.dbz : a.dbx;
-  if (dbp) atomicAdd(dbp + c, db);
+  const int nrun = (a.L + CONV_T - 1) / CONV_T;
+  float* pp = a.part + (((long long)b * nrun + blockIdx.y) * 2 * a.C + cc) * 4;
+  *(f32x4*)pp = f32x4{dw0, dw1, dw2, db};
 }
 
 // ---------------------------------------------------------------- depthwise conv + SiLU, 16-byte vector path
@@ -826,9 +823,11 @@ __global__ __launch_bounds__(256) void dwconv_silu_fwd_vec_kernel(ConvArgs a) {
   }
 }
 
-// Runs of CONV_TB tokens: each run ends in 4 V float atomics onto the (C, 3) weight / (C) bias gradients, and the
-// L2 serialises atomics to one address, so the run count (not the bytes) bounded the backward at 256-token runs.
-constexpr int CONV_TB = 1024;
+// Weight / bias gradients: every (sequence, run of CONV_T tokens, channel) writes its (dw0, dw1, dw2, db) partial
+// sums to a workspace the caller reduces (deterministic). The float atomics this replaced were serialised by the L2
+// per address: at the Swin-window shapes (8192 sequences of 64 tokens) 2 * 10^5 threads x 16 atomics onto 384
+// addresses took 0.5 ms per call, and they had forced 1024-token runs (a short grid) at long L.
+constexpr int CONV_TB = CONV_T;
 
 template <typename T, int V>
 __global__ __launch_bounds__(256) void dwconv_silu_bwd_vec_kernel(ConvArgs a) {
@@ -903,15 +902,10 @@ __global__ __launch_bounds__(256) void dwconv_silu_bwd_vec_kernel(ConvArgs a) {
       }
     }
   }
-  float* dw = (ctx.zhalf ? a.dwz : a.dwx) + ctx.c * CONV_K;
-  float* dbp = ctx.zhalf ? a.dbz : a.dbx;
+  const int nrun = (a.L + CONV_TB - 1) / CONV_TB;
+  float* pp = a.part + (((long long)ctx.b * nrun + ctx.t0 / CONV_TB) * 2 * a.C + ctx.cc0) * 4;
 #pragma unroll
-  for (int v = 0; v < V; ++v) {
-    atomicAdd(dw + v * CONV_K + 0, dw0[v]);
-    atomicAdd(dw + v * CONV_K + 1, dw1[v]);
-    atomicAdd(dw + v * CONV_K + 2, dw2[v]);
-    if (dbp) atomicAdd(dbp + ctx.c + v, db[v]);
-  }
+  for (int v = 0; v < V; ++v) *(f32x4*)(pp + 4 * v) = f32x4{dw0[v], dw1[v], dw2[v], db[v]};
 }
 
 }  // namespace lci
@@ -1078,15 +1072,20 @@ extern "C" int lci_dwconv_silu_fwd(int dtype, const void* in, const float* wx, c
   return 0;
 }
 
-// dwx/dbx/dwz/dbz accumulated (caller zeroes). din (B, L, 2C) written with token stride in_ts.
+extern "C" long long lci_dwconv_silu_bwd_part_rows(int B, int L) {
+  return (long long)B * ((L + CONV_T - 1) / CONV_T);
+}
+
+// din (B, L, 2C) written with token stride in_ts; part (lci_dwconv_silu_bwd_part_rows(B, L), 2C, 4) f32 written:
+// per-run sums of (dw0, dw1, dw2, db) of channel cc (x half: cc < C), summed over the first axis by the caller.
 extern "C" int lci_dwconv_silu_bwd(int dtype, const void* in, const float* wx, const float* bx, const float* wz,
-                                   const float* bz, const void* gx, const void* gz, void* din, float* dwx,
-                                   float* dbx, float* dwz, float* dbz, int B, int L, int C, int K, int in_ts,
-                                   int ox_ts, int oz_ts, int zoff, void* stream) {
+                                   const float* bz, const void* gx, const void* gz, void* din, float* part, int B,
+                                   int L, int C, int K, int in_ts, int ox_ts, int oz_ts, int zoff, void* stream) {
   LCI_CHECK(K == CONV_K, "dwconv_silu: kernel size %d unsupported (3, as mamba.py d_conv=3)", K);
+  LCI_CHECK(part && ((uintptr_t)part & 15) == 0, "dwconv_silu: part workspace must be 16-byte aligned");
   ConvArgs a{};
   a.in = in; a.wx = wx; a.bx = bx; a.wz = wz; a.bz = bz; a.gx = gx; a.gz = gz; a.din = din;
-  a.dwx = dwx; a.dbx = dbx; a.dwz = dwz; a.dbz = dbz;
+  a.part = part;
   a.B = B; a.L = L; a.C = C; a.in_ts = in_ts; a.ox_ts = ox_ts; a.oz_ts = oz_ts; a.zoff = zoff;
   // backward: 4 channels per thread (8-byte bf16 / 16-byte f32 vectors). The 8-channel bf16 version holds 16
   // windows' state in 182 VGPRs (2 waves per SIMD) and measured slower than the scalar kernels (3.5 vs 2.6 ms at

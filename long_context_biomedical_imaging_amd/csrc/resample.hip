@@ -215,42 +215,38 @@ __device__ __forceinline__ void lin_taps(int o, int n, float scale, int& i0, int
   l0 = __fsub_rn(1.f, l1);
 }
 
+// grid (ceil(OW * C/8 / 256), OH, B * OD): one output row (b, oz, oy) per block row, so the depth / height taps are
+// block-uniform and the per-thread index math is 32-bit (ox, 8-channel chunk q).
 __global__ __launch_bounds__(256) void upsample3d_cl_fwd_kernel(Up3Args a) {
   const int C8 = a.C / 8;
-  const long long total = (long long)a.B * a.OD * a.OH * a.OW * C8;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int q = (int)(i % C8);
-    long long p = i / C8;
-    const int ox = (int)(p % a.OW);
-    p /= a.OW;
-    const int oy = (int)(p % a.OH);
-    p /= a.OH;
-    const int oz = (int)(p % a.OD), b = (int)(p / a.OD);
-    int d0, d1, h0, h1, w0, w1;
-    float dl0, dl1, hl0, hl1, wl0, wl1;
-    lin_taps(oz, a.D, a.sd, d0, d1, dl0, dl1);
-    lin_taps(oy, a.H, a.sh, h0, h1, hl0, hl1);
-    lin_taps(ox, a.W, a.sw, w0, w1, wl0, wl1);
-    const float* base = a.x + (long long)b * a.D * a.H * a.W * a.C + 8 * q;
-    auto at = [&](int d, int h, int w) { return base + (((long long)d * a.H + h) * a.W + w) * a.C; };
-    const float* p000 = at(d0, h0, w0); const float* p001 = at(d0, h0, w1);
-    const float* p010 = at(d0, h1, w0); const float* p011 = at(d0, h1, w1);
-    const float* p100 = at(d1, h0, w0); const float* p101 = at(d1, h0, w1);
-    const float* p110 = at(d1, h1, w0); const float* p111 = at(d1, h1, w1);
-    bf16x8 v;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.OW * C8) return;
+  const int ox = i / C8, q = i - ox * C8;
+  const int oy = blockIdx.y, oz = blockIdx.z % a.OD, b = blockIdx.z / a.OD;
+  int d0, d1, h0, h1, w0, w1;
+  float dl0, dl1, hl0, hl1, wl0, wl1;
+  lin_taps(oz, a.D, a.sd, d0, d1, dl0, dl1);
+  lin_taps(oy, a.H, a.sh, h0, h1, hl0, hl1);
+  lin_taps(ox, a.W, a.sw, w0, w1, wl0, wl1);
+  const float* base = a.x + (long long)b * a.D * a.H * a.W * a.C + 8 * q;
+  auto at = [&](int d, int h, int w) { return base + (((long long)d * a.H + h) * a.W + w) * a.C; };
+  const float* p000 = at(d0, h0, w0); const float* p001 = at(d0, h0, w1);
+  const float* p010 = at(d0, h1, w0); const float* p011 = at(d0, h1, w1);
+  const float* p100 = at(d1, h0, w0); const float* p101 = at(d1, h0, w1);
+  const float* p110 = at(d1, h1, w0); const float* p111 = at(d1, h1, w1);
+  bf16x8 v;
 #pragma unroll
-    for (int hv = 0; hv < 2; ++hv) {
-      const f32x4 x000 = *(const f32x4*)(p000 + 4 * hv), x001 = *(const f32x4*)(p001 + 4 * hv);
-      const f32x4 x010 = *(const f32x4*)(p010 + 4 * hv), x011 = *(const f32x4*)(p011 + 4 * hv);
-      const f32x4 x100 = *(const f32x4*)(p100 + 4 * hv), x101 = *(const f32x4*)(p101 + 4 * hv);
-      const f32x4 x110 = *(const f32x4*)(p110 + 4 * hv), x111 = *(const f32x4*)(p111 + 4 * hv);
+  for (int hv = 0; hv < 2; ++hv) {
+    const f32x4 x000 = *(const f32x4*)(p000 + 4 * hv), x001 = *(const f32x4*)(p001 + 4 * hv);
+    const f32x4 x010 = *(const f32x4*)(p010 + 4 * hv), x011 = *(const f32x4*)(p011 + 4 * hv);
+    const f32x4 x100 = *(const f32x4*)(p100 + 4 * hv), x101 = *(const f32x4*)(p101 + 4 * hv);
+    const f32x4 x110 = *(const f32x4*)(p110 + 4 * hv), x111 = *(const f32x4*)(p111 + 4 * hv);
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        v[4 * hv + k] = (bf16)(dl0 * (hl0 * (wl0 * x000[k] + wl1 * x001[k]) + hl1 * (wl0 * x010[k] + wl1 * x011[k])) +
-                               dl1 * (hl0 * (wl0 * x100[k] + wl1 * x101[k]) + hl1 * (wl0 * x110[k] + wl1 * x111[k])));
-    }
-    *(bf16x8*)(a.y + ((((long long)b * a.OD + oz) * a.OH + oy) * a.OW + ox) * a.C + 8 * q) = v;
+    for (int k = 0; k < 4; ++k)
+      v[4 * hv + k] = (bf16)(dl0 * (hl0 * (wl0 * x000[k] + wl1 * x001[k]) + hl1 * (wl0 * x010[k] + wl1 * x011[k])) +
+                             dl1 * (hl0 * (wl0 * x100[k] + wl1 * x101[k]) + hl1 * (wl0 * x110[k] + wl1 * x111[k])));
   }
+  *(bf16x8*)(a.y + ((((long long)b * a.OD + oz) * a.OH + oy) * a.OW + ox) * a.C + 8 * q) = v;
 }
 
 // Adjoint of 1-D linear interpolation (align_corners=False, scale = n_in / n_out) along the middle axis of
@@ -365,7 +361,8 @@ extern "C" int lci_upsample3d_cl_fwd(const float* x, void* y, int B, int C, int 
   Up3Args a{};
   a.x = x; a.y = (bf16*)y; a.B = B; a.C = C; a.D = D; a.H = H; a.W = W; a.OD = OD; a.OH = OH; a.OW = OW;
   a.sd = (float)D / (float)OD; a.sh = (float)H / (float)OH; a.sw = (float)W / (float)OW;
-  hipLaunchKernelGGL(upsample3d_cl_fwd_kernel, dim3(up_grid((long long)B * OD * OH * OW * (C / 8))), dim3(256), 0,
+  LCI_CHECK((long long)B * OD <= 65535 && OH <= 65535, "upsample3d: output too large for the grid");
+  hipLaunchKernelGGL(upsample3d_cl_fwd_kernel, dim3((OW * (C / 8) + 255) / 256, OH, B * OD), dim3(256), 0,
                      (hipStream_t)stream, a);
   LCI_LAUNCH_CHECK();
   return 0;

@@ -239,14 +239,16 @@ class _DWConvSiLUPair(torch.autograd.Function):
         gxs = torch.zeros(B, L, C, device=xz.device, dtype=xz.dtype) if gxs is None else gxs.to(xz.dtype).contiguous()
         gyz = torch.zeros(B, L, C2, device=xz.device, dtype=xz.dtype) if gyz is None else gyz.to(xz.dtype).contiguous()
         din = torch.empty_like(xz)
-        f32 = dict(device=xz.device, dtype=torch.float32)
-        dwx, dwz = torch.zeros(C, K, **f32), torch.zeros(C, K, **f32)
-        dbx = torch.zeros(C, **f32) if has_bx else None
-        dbz = torch.zeros(C, **f32) if has_bz else None
+        rows = int(_lib.load().lci_dwconv_silu_bwd_part_rows(B, L))
+        part = torch.empty(rows, 2 * C, 4, device=xz.device, dtype=torch.float32)
         KernelTimer.run("dwconv_silu_bwd", 0.0, xz, lambda: _lib.call(
             "lci_dwconv_silu_bwd", _DT[xz.dtype], xz.data_ptr(), wx.data_ptr(), _lib.ptr(bx), wz.data_ptr(),
-            _lib.ptr(bz), gxs.data_ptr(), gyz.data_ptr(), din.data_ptr(), dwx.data_ptr(), _lib.ptr(dbx),
-            dwz.data_ptr(), _lib.ptr(dbz), B, L, C, K, C2, C, C2, C, _lib.stream_of(xz)))
+            _lib.ptr(bz), gxs.data_ptr(), gyz.data_ptr(), din.data_ptr(), part.data_ptr(), B, L, C, K, C2, C, C2, C,
+            _lib.stream_of(xz)))
+        g = part.sum(0)                      # (2C, 4): dw0, dw1, dw2, db per channel (deterministic order)
+        dwx, dwz = g[:C, :K].contiguous(), g[C:, :K].contiguous()
+        dbx = g[:C, 3].contiguous() if has_bx else None
+        dbz = g[C:, 3].contiguous() if has_bz else None
         return din, dwx.reshape(wxs), dbx, dwz.reshape(wzs), dbz
 
 
