@@ -109,6 +109,9 @@ def test_flag_surface_and_factories():
         model_base.EncoderDecoderModel(cfg, "Foo", "ViTLinear", 1, 2)
     with pytest.raises(ValueError):
         backbone_vit.SABlock(False, False, 100, 3)
+    with pytest.raises(ValueError, match="head_dim 32"):      # custom preset split the kernels do not cover
+        backbone_vit.SABlock(False, False, 192, 6)
+    backbone_vit.SABlock(True, False, 192, 6)                 # Hyena / Mamba mixers take any head split
 
 
 def test_product_path_has_no_cpu_fallback():
