@@ -193,8 +193,10 @@ int lci_fftconv_bwd(const float* dy, const float* u, const void* K, const float*
  * backbone_swin.py:361-362), exact f32 products on the f32 MFMA instead of an FFT. u, y (R, C, L) f32 channel-major
  * rows (filter of row r*C + c is c), k (C, L), D (C) f32 or null.
  * fwd: adjoint = 0: y = causal_conv(u, k) + D u;  adjoint = 1: y = corr(u, k) + D u, i.e. du from dy (written).
- * dk: part (lci_direct_conv_dk_splits(R, C, L), C, L) f32 <- per-row-split sums of dy[r][t] u[r][t - tau]
- *     (written); dk = sum over the first axis, dD[c] = dk[c][0] (caller). Deterministic. */
+ * dk: part (lci_direct_conv_dk_splits(R, C, L), C, ceil(L / 32), 64) f32 <- per-row-split diagonal-band sums of
+ *     G = dy^T u (band d, slot e + 31: sum over rows and t - s = 32 d + e of dy[r][t] u[r][s], e in [-31, 31])
+ *     (written); dk[32 d + e] = sum over splits of band[d][e + 31] + band[d + 1][e - 1] for e in [0, 32),
+ *     dD[c] = dk[c][0] (caller). Deterministic. */
 int lci_direct_conv_max_len(void);
 int lci_direct_conv_fwd(const float* u, const float* k, const float* D, float* y, int R, int C, int L, int adjoint,
                         void* stream);

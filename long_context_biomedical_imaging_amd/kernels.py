@@ -670,10 +670,14 @@ class _DirectConv(torch.autograd.Function):
         dk = dD = None
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
             ns = int(_lib.load().lci_direct_conv_dk_splits(R, C, L))
-            part = torch.empty(ns, C, L, device=u.device, dtype=torch.float32)
+            nt = -(-L // 32)
+            part = torch.empty(ns, C, nt, 64, device=u.device, dtype=torch.float32)
             KernelTimer.run("direct_conv_dk", fl, u, lambda: _lib.call(
                 "lci_direct_conv_dk", dy.data_ptr(), u.data_ptr(), part.data_ptr(), R, C, L, _lib.stream_of(u)))
-            g = part.sum(0)
+            band = part.sum(0)                                     # (C, nt, 64): diagonal sums per band
+            g = band[:, :, 31:63].clone()                          # lag 32 d + e from band d
+            g[:, :-1, 1:] += band[:, 1:, 0:31]                     # ... and from band d + 1 (slot e - 1)
+            g = g.reshape(C, nt * 32)[:, :L]
             dk = g.to(ctx.kdtype) if ctx.needs_input_grad[1] else None
             dD = g[:, 0].clone() if ctx.needs_input_grad[2] else None
         return du, dk, dD

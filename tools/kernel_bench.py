@@ -151,6 +151,25 @@ def bench_fftconv():
          24.0 * rows * L, "GB/s", "same, fwd+bwd (u, k, D grads)")
 
 
+def bench_direct_conv():
+    """Direct (Toeplitz, f32 MFMA) long conv at the Swin-Hyena window shapes (128^3 p2, B=2: stage 1-4 at window 8,
+    window 7 and window 4 stage 1). FLOPs = R C L (L + 1) per launch (fwd, adjoint and filter gradient alike)."""
+    for R, C, L, tag in ((3072, 32, 512, "w8 stage1"), (768, 32, 512, "w8 stage2"), (192, 32, 512, "w8 stage3"),
+                         (48, 32, 512, "w8 stage4"), (6000, 32, 343, "w7 stage1"), (24576, 32, 64, "w4 stage1")):
+        u = torch.randn(R, C, L, device="cuda").requires_grad_(True)
+        k = (torch.randn(C, L, device="cuda") * 0.1).requires_grad_(True)
+        D = torch.randn(C, device="cuda").requires_grad_(True)
+        fl = float(R * C) * L * (L + 1)
+        y = kernels._DirectConv.apply(u, k, D)
+        g = torch.randn_like(y)
+        t_f = timeit(lambda: kernels._DirectConv.apply(u, k, D))
+        t_fb = timeit(lambda: torch.autograd.grad(kernels._DirectConv.apply(u, k, D), [u, k, D], g))
+        for name, ms, w in (("direct_conv_fwd", t_f, fl), ("direct_conv_fwd+bwd", t_fb, 3 * fl)):
+            print(json.dumps({"kernel": name, "ms": round(ms, 4), "achieved": round(w / (ms * 1e-3) / 1e12, 1),
+                              "unit": "TFLOP/s", "peak": 157.3, "frac": round(w / (ms * 1e-3) / 1e12 / 157.3, 3),
+                              "config": f"R{R} C{C} L{L} ({tag})"}), flush=True)
+
+
 def bench_patch_embed():
     B, S, D = 2, 512, 384
     x = torch.rand(B, 1, S, S, device="cuda")
@@ -227,6 +246,8 @@ def main():
         bench_dwconv()
     if "fftconv" in which:
         bench_fftconv()
+    if "dconv" in which:
+        bench_direct_conv()
     if "patch" in which:
         bench_patch_embed()
     if "linear" in which:
