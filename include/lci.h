@@ -17,6 +17,7 @@
  *                         (:435-487) with compute_mask (:591-628)
  *   lci_selective_scan_*  mamba_ssm selective_scan_fn (mamba-ssm 1.2.0.post1) as called at model/models/mamba.py:125-134
  *   lci_dwconv_silu_*     MambaVisionMixer depthwise conv1d + SiLU, model/models/mamba.py:118-119
+ *   lci_mamba_proj_*      MambaVisionMixer x_proj -> (dt, B, C) split -> dt_proj, model/models/mamba.py:120-124
  *   lci_fftconv_*         fftconv_ref (gelu=False), model/models/hyena.py:32-51 / Filter.forward :201-216
  *   lci_direct_conv_*     the same long convolution for Swin-window rows (L <= 512, backbone_swin.py:361-362)
  *   lci_hyena_pre/post_*  HyenaOperator short filter + gating, model/models/hyena.py:317-355
@@ -171,6 +172,24 @@ long long lci_dwconv_silu_bwd_part_rows(int B, int L);
 int lci_dwconv_silu_bwd(int dtype, const void* in, const float* wx, const float* bx, const float* wz,
                         const float* bz, const void* gx, const void* gz, void* din, float* part, int B, int L, int C,
                         int K, int in_ts, int ox_ts, int oz_ts, int zoff, void* stream);
+
+/* MambaVisionMixer x_proj -> split -> dt_proj (mamba.py:120-124) fused, bf16 autocast numerics. Per token:
+ * x_dbl = bf16(xs Wx^T) (R + 2N columns), dt = bf16(x_dbl[:R] Wdt^T + bias), bc = x_dbl[R:] (B | C), dtl = x_dbl[:R].
+ * Weight images (bf16, built by the caller; dims = lci_mamba_proj_dims -> {Dxp, nb1, ks2, nb3, ks4}):
+ *   w1 (nb1*32, Dx) = Wx zero-padded; w2p (Dxp, ks2*16): w2p[d][16 s + 8 h + j] = Wdt[d][32 (s >> 1) + 16 (s & 1)
+ *   + (j & 3) + 8 (j >> 2) + 4 h] (zero past R / Dx); w2t (nb3*32, Dx) = Wdt^T zero-padded; w1t (Dxp, ks4*16):
+ *   w1t[d][r] = Wx[r][d] (zero past R + 2N / Dx). bias (Dx) f32.
+ * fwd: xs (M, Dx) bf16 (token stride ts_x) -> dt (M, Dx) (stride ts_dt), bc (M, 2N) contiguous, dtl (M, ld_dtl).
+ * bwd: ddt (M, Dx), dbc (M, 2N) bf16 -> dxs = bf16(d x_dbl Wx) (+ du when not null), dxdbl (M, ld_dxdbl) = d x_dbl
+ *   with d x_dbl = [bf16(ddt Wdt) | dbc]; the weight gradients are lci_linear_wgrad calls on (dxdbl, xs) and
+ *   (ddt, dtl). Dx % 16 == 0, 2N % 8 == 0, R + 2N <= 64; 16-byte aligned rows (dt / dxs / du 8). */
+int lci_mamba_proj_dims(int Dx, int R, int N2, int* dims);
+int lci_mamba_proj_fwd(const void* xs, long long ts_x, const void* w1, const void* w2p, const float* bias, void* dt,
+                       long long ts_dt, void* bc, void* dtl, int ld_dtl, long long M, int Dx, int R, int N2,
+                       void* stream);
+int lci_mamba_proj_bwd(const void* ddt, long long ts_ddt, const void* dbc, const void* w2t, const void* w1t,
+                       const void* du, long long ts_du, void* dxs, long long ts_dxs, void* dxdbl, int ld_dxdbl,
+                       long long M, int Dx, int R, int N2, void* stream);
 
 /* ------------------------------------------------------------------ Hyena long convolution (f32)
  * FFT size n = lci_fft_size(L) = pow2 >= 2L (L <= 262144). tw: n complex f32 (f32x2) from lci_fft_twiddles.

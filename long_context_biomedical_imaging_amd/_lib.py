@@ -66,6 +66,9 @@ SIGNATURES = {
     "lci_resample1d_adj": [_P, _I, _P, _L, _I, _I, _L, _P],
     "lci_direct_conv_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _P],
     "lci_window_gather": [_P, _P, _I, _P, _I, _P],
+    "lci_mamba_proj_dims": [_I, _I, _I, _P],
+    "lci_mamba_proj_fwd": [_P, _L, _P, _P, _P, _P, _L, _P, _P, _I, _L, _I, _I, _I, _P],
+    "lci_mamba_proj_bwd": [_P, _L, _P, _P, _P, _P, _L, _P, _L, _P, _I, _L, _I, _I, _I, _P],
     "lci_direct_conv_dk": [_P, _P, _P, _I, _I, _I, _P],
     "lci_hyena_filter_prep": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P],
     "lci_hyena_filter_fwd": [_P, _P, _P, _P, _I, _I, _F, _P, _P],

@@ -269,6 +269,9 @@ class _SelectiveScanCL(torch.autograd.Function):
     def forward(ctx, u, delta, A, Bm, Cm, D, delta_bias, yz, softplus=True):
         B, L, Dx = u.shape
         N = A.shape[1]
+        ctx.bc_joint = Cm is None            # Bm = [B | C] in one (B, L, 2N) tensor: one gradient for both
+        if ctx.bc_joint:
+            Bm, Cm = Bm[..., :N], Bm[..., N:]
         dt = u.dtype
         tc = _scan_chunk(L, B, Dx)
         nch = -(-L // tc)
@@ -326,10 +329,14 @@ class _SelectiveScanCL(torch.autograd.Function):
             Cm.data_ptr(), Dv.data_ptr(), bv.data_ptr(), dy.data_ptr(), du.data_ptr(), dd.data_ptr(),
             dBC.data_ptr(), dA.data_ptr(), dD.data_ptr(), db.data_ptr(), strides, B, L, Dx, N, tc,
             int(ctx.softplus), sdt.data_ptr(), ckpt.data_ptr(), gl.data_ptr(), gin.data_ptr(), _lib.stream_of(u)))
-        gz = gyz.clone()
-        gz[..., :Dx] = 0
+        # grad of yz: its first half was overwritten by y (zero gradient there), its second half is the SiLU(conv z)
+        # operand of the out_proj input. yz's only producer / consumer pair is dwconv_silu_pair -> this op, and
+        # _DWConvSiLUPair.backward reads only the z half (column offset C): pass gyz through as is instead of a
+        # clone + zero of the x half (a full (B, L, 2 Dx) copy, 0.6 ms per C5 layer).
+        if ctx.bc_joint:   # autograd casts the f32 sums to the input's bf16 (what .to(Bm.dtype) did)
+            return du, dd, dA, dBC, None, dD if ctx.has_D else None, db if ctx.has_b else None, gyz, None
         return (du, dd, dA, dBC[..., :N].to(Bm.dtype), dBC[..., N:].to(Cm.dtype), dD if ctx.has_D else None,
-                db if ctx.has_b else None, gz, None)
+                db if ctx.has_b else None, gyz, None)
 
 
 def selective_scan_cl(u, delta, A, Bm, Cm, D, delta_bias, yz, delta_softplus=True, return_last_state=False):
@@ -346,17 +353,126 @@ def selective_scan_cl(u, delta, A, Bm, Cm, D, delta_bias, yz, delta_softplus=Tru
     u = u.contiguous()
     delta = delta.to(dt)
     Bm = Bm.to(dt)
-    Cm = Cm.to(dt)
     if Bm.stride(-1) != 1:
         Bm = Bm.contiguous()
-    if Cm.stride(-1) != 1:
-        Cm = Cm.contiguous()
+    if Cm is not None:       # Cm None: Bm is the joint (B, L, 2N) [B | C] tensor
+        Cm = Cm.to(dt)
+        if Cm.stride(-1) != 1:
+            Cm = Cm.contiguous()
     if delta.stride(-1) != 1:
         delta = delta.contiguous()
     if yz.dtype != dt:
         raise _lib.LciError("selective_scan: yz dtype must match u")
     out, last = _SelectiveScanCL.apply(u, delta, A, Bm, Cm, D, delta_bias, yz, bool(delta_softplus))
     return (out, last) if return_last_state else out
+
+
+# --------------------------------------------------------------------- Mamba x_proj -> split -> dt_proj
+_MP_IDX = {}
+
+
+def _mp_dims(Dx, R, N2):
+    import ctypes
+    d = (ctypes.c_int * 5)()
+    _lib.call("lci_mamba_proj_dims", Dx, R, N2, d)
+    return tuple(int(v) for v in d)
+
+
+def _mp_slot_rows(ks2, device):
+    """x_dbl row feeding k-slot 16 s + 8 h + j of dt_proj's MFMA (the accumulator-pack order; include/lci.h)."""
+    key = (ks2, str(device))
+    t = _MP_IDX.get(key)
+    if t is None:
+        rows = []
+        for sl in range(16 * ks2):
+            st, k = sl // 16, sl % 16
+            h, j = k >> 3, k & 7
+            rows.append(32 * (st >> 1) + 16 * (st & 1) + (j & 3) + 8 * (j >> 2) + 4 * h)
+        t = torch.tensor(rows, device=device)
+        _MP_IDX[key] = t
+    return t
+
+
+def _mp_images(Wx, Wdt, R, N2):
+    """bf16 weight images of lci_mamba_proj_fwd / _bwd from the f32 parameters (include/lci.h)."""
+    RN, Dx = Wx.shape
+    Dxp, nb1, ks2, nb3, ks4 = _mp_dims(Dx, R, N2)
+    dev = Wx.device
+    wx = Wx.detach().to(torch.bfloat16)
+    wd = Wdt.detach().to(torch.bfloat16)
+    w1 = torch.zeros(nb1 * 32, Dx, device=dev, dtype=torch.bfloat16)
+    w1[:RN] = wx
+    rows = _mp_slot_rows(ks2, dev)
+    wdp = torch.zeros(Dxp, 32 * max(nb1, 2), device=dev, dtype=torch.bfloat16)
+    wdp[:Dx, :R] = wd
+    w2p = wdp[:, rows].contiguous()
+    w2t = torch.zeros(nb3 * 32, Dx, device=dev, dtype=torch.bfloat16)
+    w2t[:R] = wd.t()
+    w1t = torch.zeros(Dxp, ks4 * 16, device=dev, dtype=torch.bfloat16)
+    w1t[:Dx, :RN] = wx.t()
+    return w1, w2p, w2t, w1t
+
+
+class _MambaProj(torch.autograd.Function):
+    """x_dbl = x_proj(xs); dt_low, B|C = split; dt = dt_proj(dt_low) (mamba.py:120-124) under bf16 autocast, in one
+    HIP pass per direction (lci_mamba_proj_fwd / _bwd); weight gradients on lci_linear_wgrad."""
+
+    @staticmethod
+    def forward(ctx, xs, Wx, Wdt, bias, R, N2):
+        Bb, L, Dx = xs.shape
+        M = Bb * L
+        w1, w2p, w2t, w1t = _mp_images(Wx, Wdt, R, N2)
+        bf = bias.detach().to(torch.bfloat16).float().contiguous()
+        b16 = dict(device=xs.device, dtype=torch.bfloat16)
+        dt = torch.empty(Bb, L, Dx, **b16)
+        bc = torch.empty(Bb, L, N2, **b16)
+        ldl = -(-R // 8) * 8
+        dtl = torch.empty(Bb, L, ldl, **b16)
+        KernelTimer.run("mamba_proj_fwd", 0.0, xs, lambda: _lib.call(
+            "lci_mamba_proj_fwd", xs.data_ptr(), Dx, w1.data_ptr(), w2p.data_ptr(), bf.data_ptr(), dt.data_ptr(), Dx,
+            bc.data_ptr(), dtl.data_ptr(), ldl, M, Dx, R, N2, _lib.stream_of(xs)))
+        ctx.save_for_backward(xs, dtl, w2t, w1t)
+        ctx.meta = (R, N2, Wx.shape, Wdt.shape)
+        return dt, bc
+
+    @staticmethod
+    def backward(ctx, gdt, gbc):
+        xs, dtl, w2t, w1t = ctx.saved_tensors
+        R, N2, wxs, wds = ctx.meta
+        Bb, L, Dx = xs.shape
+        M = Bb * L
+        b16 = dict(device=xs.device, dtype=torch.bfloat16)
+        gdt = torch.zeros(Bb, L, Dx, **b16) if gdt is None else gdt.to(torch.bfloat16).contiguous()
+        gbc = torch.zeros(Bb, L, N2, **b16) if gbc is None else gbc.to(torch.bfloat16).contiguous()
+        ldx = -(-(R + N2) // 8) * 8
+        dxs = torch.empty(Bb, L, Dx, **b16)
+        dxdbl = torch.empty(Bb, L, ldx, **b16)
+        KernelTimer.run("mamba_proj_bwd", 0.0, xs, lambda: _lib.call(
+            "lci_mamba_proj_bwd", gdt.data_ptr(), Dx, gbc.data_ptr(), w2t.data_ptr(), w1t.data_ptr(), None, 0,
+            dxs.data_ptr(), Dx, dxdbl.data_ptr(), ldx, M, Dx, R, N2, _lib.stream_of(xs)))
+        dW, _ = linear_wgrad(dxdbl.view(M, ldx), xs.reshape(M, Dx), False)
+        dWd, db = linear_wgrad(gdt.view(M, Dx), dtl.view(M, -1), True)
+        return dxs, dW[:R + N2].reshape(wxs), dWd[:, :R].reshape(wds), db, None, None
+
+
+def mamba_proj_supported(xs: torch.Tensor, Dx: int, R: int, N2: int) -> bool:
+    """The fused projection runs under bf16 autocast on contiguous bf16 rows of the shapes it tiles."""
+    if os.environ.get("LCI_MAMBA_PROJ", "1") == "0" or not xs.is_cuda:
+        return False
+    if not (torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+        return False
+    if xs.dtype != torch.bfloat16 or not xs.is_contiguous() or xs.data_ptr() % 16:
+        return False
+    if Dx % 16 or N2 % 8 or R + N2 > 64 or Dx > 1024:
+        return False
+    ldl, ldx = -(-R // 8) * 8, -(-(R + N2) // 8) * 8
+    M = xs.numel() // Dx
+    return (_lib.load().lci_linear_wgrad_splits(M, ldx, Dx) > 0 and _lib.load().lci_linear_wgrad_splits(M, Dx, ldl) > 0)
+
+
+def mamba_proj(xs, Wx, Wdt, bias, R, N2):
+    """(dt (B, L, Dx) bf16, bc (B, L, 2N) bf16 = [B | C]) of MambaVisionMixer's x_proj / dt_proj (mamba.py:120-124)."""
+    return _MambaProj.apply(xs, Wx, Wdt, bias, R, N2)
 
 
 # ------------------------------------------------------------------------------------ window attention

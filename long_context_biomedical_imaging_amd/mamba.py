@@ -7,6 +7,10 @@ reads u = x, delta = dt_proj(dt) and B, C as strided views of the x_proj output 
 first half of the out_proj input buffer whose second half already holds SiLU(conv(z)) — the reference's
 `torch.cat([y, z], dim=1)` (mamba.py:136) without a copy.
 
+Under bf16 autocast x_proj -> (dt, B, C) split -> dt_proj (mamba.py:120-124) run as one HIP pass per direction
+(kernels.mamba_proj, lci_mamba_proj_fwd / _bwd): x_dbl never goes to HBM, dt and an aligned [B | C] tensor are
+written once and the scan reads them in place; the fp32 (no-autocast) path keeps the two Linear layers.
+
 Reference quirk kept: the dt_proj bias is applied twice (dt_proj(dt) adds it; selective_scan_fn adds it
 again as delta_bias, mamba.py:120-134), so the effective delta = softplus(W dt + 2 b).
 """
@@ -74,6 +78,13 @@ class MambaVisionMixer(nn.Module):
         A = -torch.exp(self.A_log.float())
         N, R = self.d_state, self.dt_rank
         es = 2 if torch.is_autocast_enabled("cuda") else xs.element_size()
+        Dx = self.d_inner // 2
+        if kernels.mamba_proj_supported(xs, Dx, R, 2 * N) and self.dt_proj.bias is not None:
+            # bf16 autocast: x_proj -> split -> dt_proj in one HIP pass (lci_mamba_proj_fwd); [B | C] as one aligned
+            # (B, L, 2N) tensor the scan reads in place
+            dt, bc = kernels.mamba_proj(xs, self.x_proj.weight, self.dt_proj.weight, self.dt_proj.bias, R, 2 * N)
+            y = kernels.selective_scan_cl(xs, dt, A, bc, None, self.D.float(), self.dt_proj.bias.float(), yz)
+            return self.out_proj(y)
         if (R * es) % 16 or ((R + 2 * N) * es) % 16 or (N * es) % 16:
             # the scan reads B / C rows with 16-byte vectors: when dt_rank breaks their alignment (Swin stages,
             # d_model 96 / 192 -> dt_rank 6 / 12) the same projection is computed with its output columns
