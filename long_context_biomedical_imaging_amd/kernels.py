@@ -450,9 +450,16 @@ class _MambaProj(torch.autograd.Function):
         KernelTimer.run("mamba_proj_bwd", 0.0, xs, lambda: _lib.call(
             "lci_mamba_proj_bwd", gdt.data_ptr(), Dx, gbc.data_ptr(), w2t.data_ptr(), w1t.data_ptr(), None, 0,
             dxs.data_ptr(), Dx, dxdbl.data_ptr(), ldx, M, Dx, R, N2, _lib.stream_of(xs)))
-        dW, _ = linear_wgrad(dxdbl.view(M, ldx), xs.reshape(M, Dx), False)
-        dWd, db = linear_wgrad(gdt.view(M, Dx), dtl.view(M, -1), True)
+        dW, _ = _wgrad_any(dxdbl.view(M, ldx), xs.reshape(M, Dx), False)
+        dWd, db = _wgrad_any(gdt.view(M, Dx), dtl.view(M, -1), True)
         return dxs, dW[:R + N2].reshape(wxs), dWd[:, :R].reshape(wds), db, None, None
+
+
+def _wgrad_any(dy2, x2, bias):
+    """dW = dy2^T x2 (f32) and db: the HIP split-token kernel where its tiles fit, else the GEMM (narrow shapes)."""
+    if linear_wgrad_supported(dy2, x2):
+        return linear_wgrad(dy2, x2, bias)
+    return (dy2.t() @ x2).float(), (dy2.float().sum(0) if bias else None)
 
 
 def mamba_proj_supported(xs: torch.Tensor, Dx: int, R: int, N2: int) -> bool:
@@ -463,11 +470,7 @@ def mamba_proj_supported(xs: torch.Tensor, Dx: int, R: int, N2: int) -> bool:
         return False
     if xs.dtype != torch.bfloat16 or not xs.is_contiguous() or xs.data_ptr() % 16:
         return False
-    if Dx % 16 or N2 % 8 or R + N2 > 64 or Dx > 1024:
-        return False
-    ldl, ldx = -(-R // 8) * 8, -(-(R + N2) // 8) * 8
-    M = xs.numel() // Dx
-    return (_lib.load().lci_linear_wgrad_splits(M, ldx, Dx) > 0 and _lib.load().lci_linear_wgrad_splits(M, Dx, ldl) > 0)
+    return not (Dx % 16 or N2 % 8 or R + N2 > 64 or Dx > 1024)
 
 
 def mamba_proj(xs, Wx, Wdt, bias, R, N2):
