@@ -55,11 +55,42 @@ __device__ __forceinline__ bf16x8 tok_frag(const bf16* base, long long ts, long 
   return tok < M ? ld16(base + tok * ts + col) : bf16x8{};
 }
 
+// A wave's 32 token rows of a (M, Dx) tensor with token stride == Dx are one contiguous block: stage it into the
+// wave's LDS tile [token][Dx + 8] with 16-byte loads in memory order (coalesced), rows past M as zeros.
+__device__ __forceinline__ void tile_in(const bf16* g, long long t0, long long M, int Dx, bf16* t, int lane) {
+  const int cpr = Dx / 8, total = MP_TOK * cpr;
+  for (int c = lane; c < total; c += 64) {
+    const int tk = c / cpr, col = 8 * (c - tk * cpr);
+    const long long tok = t0 + tk;
+    *(bf16x8*)(t + tk * (Dx + 8) + col) = tok < M ? ld16(g + tok * Dx + col) : bf16x8{};
+  }
+}
+// ... and back: 16-byte stores in memory order, optionally adding a second (M, Dx) tensor (bf16 + bf16 in f32)
+__device__ __forceinline__ void tile_out(bf16* g, long long t0, long long M, int Dx, const bf16* t, int lane,
+                                         const bf16* add) {
+  const int cpr = Dx / 8, total = MP_TOK * cpr;
+  for (int c = lane; c < total; c += 64) {
+    const int tk = c / cpr, col = 8 * (c - tk * cpr);
+    const long long tok = t0 + tk;
+    if (tok >= M) break;
+    bf16x8 v = *(const bf16x8*)(t + tk * (Dx + 8) + col);
+    if (add) {
+      const bf16x8 u = ld16(add + tok * Dx + col);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = to_bf16(to_f32(v[j]) + to_f32(u[j]));
+    }
+    *(bf16x8*)(g + tok * Dx + col) = v;
+  }
+}
+
 __global__ __launch_bounds__(256) void mamba_proj_fwd_kernel(MpArgs a) {
   extern __shared__ __attribute__((aligned(16))) bf16 xdl[];   // [wave][token][rows_lds]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, n = lane & 31, h = lane >> 5;
   const long long t0 = ((long long)blockIdx.x * MP_WAVES + wave) * MP_TOK, tok = t0 + n;
   bf16* xw = xdl + wave * MP_TOK * a.rows_lds;
+  bf16* tw = xdl + MP_WAVES * MP_TOK * a.rows_lds + wave * MP_TOK * (a.Dxp + 8);   // xs tile, then the dt tile
+  tile_in(a.xs, t0, a.M, a.Dx, tw, lane);
+  __builtin_amdgcn_wave_barrier();
   // GEMM1: x_dbl^T block b (rows 32 b ..) over K = Dx
   f32x16 acc1[2] = {f32x16{}, f32x16{}};
 #pragma unroll
@@ -67,7 +98,7 @@ __global__ __launch_bounds__(256) void mamba_proj_fwd_kernel(MpArgs a) {
     if (b >= a.nb1) break;
     f32x16 acc{};
     for (int k0 = 0; k0 < a.Dx; k0 += 16) {
-      const bf16x8 bx = tok_frag(a.xs, a.ts_x, tok, a.M, k0 + 8 * h);
+      const bf16x8 bx = *(const bf16x8*)(tw + n * (a.Dx + 8) + k0 + 8 * h);
       const bf16x8 aw = ld16(a.w1 + (long long)(32 * b + n) * a.Dx + k0 + 8 * h);
       acc = mfma32(aw, bx, acc);
     }
@@ -110,19 +141,19 @@ __global__ __launch_bounds__(256) void mamba_proj_fwd_kernel(MpArgs a) {
       const bf16x8 aw = ld16(a.w2p + (long long)(32 * db + n) * (a.ks2 * 16) + 16 * s + 8 * h);
       acc = mfma32(aw, bx, acc);
     }
-    if (tok < a.M) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = 32 * db + 8 * g + 4 * h;
-        if (d < a.Dx) {
-          bf16x4 v;
+    for (int g = 0; g < 4; ++g) {
+      const int d = 32 * db + 8 * g + 4 * h;
+      if (d < a.Dx) {
+        bf16x4 v;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = to_bf16(acc[4 * g + j]);
-          *(bf16x4*)(a.dt + tok * a.ts_dt + d) = v;
-        }
+        for (int j = 0; j < 4; ++j) v[j] = to_bf16(acc[4 * g + j]);
+        *(bf16x4*)(tw + n * (a.Dx + 8) + d) = v;
       }
     }
   }
+  __builtin_amdgcn_wave_barrier();
+  tile_out(a.dt, t0, a.M, a.Dx, tw, lane, nullptr);
 }
 
 __global__ __launch_bounds__(256) void mamba_proj_bwd_kernel(MpArgs a) {
@@ -130,12 +161,15 @@ __global__ __launch_bounds__(256) void mamba_proj_bwd_kernel(MpArgs a) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, n = lane & 31, h = lane >> 5;
   const long long t0 = ((long long)blockIdx.x * MP_WAVES + wave) * MP_TOK, tok = t0 + n;
   bf16* xw = xdl + wave * MP_TOK * a.rows_lds;
+  bf16* tw = xdl + MP_WAVES * MP_TOK * a.rows_lds + wave * MP_TOK * (a.Dxp + 8);   // ddt tile, then the dxs tile
   const int RN = a.R + a.N2;
+  tile_in(a.ddt, t0, a.M, a.Dx, tw, lane);
+  __builtin_amdgcn_wave_barrier();
   // GEMM3: d dt_low^T block b = Wdt^T . ddt^T over K = Dx
   for (int b = 0; b < a.nb3; ++b) {
     f32x16 acc{};
     for (int k0 = 0; k0 < a.Dx; k0 += 16) {
-      const bf16x8 bx = tok_frag(a.ddt, a.ts_ddt, tok, a.M, k0 + 8 * h);
+      const bf16x8 bx = *(const bf16x8*)(tw + n * (a.Dx + 8) + k0 + 8 * h);
       const bf16x8 aw = ld16(a.w2t + (long long)(32 * b + n) * a.Dx + k0 + 8 * h);
       acc = mfma32(aw, bx, acc);
     }
@@ -170,26 +204,20 @@ __global__ __launch_bounds__(256) void mamba_proj_bwd_kernel(MpArgs a) {
       const bf16x8 aw = ld16(a.w1t + (long long)(32 * db + n) * (a.ks4 * 16) + 16 * s + 8 * h);
       acc = mfma32(aw, bx, acc);
     }
-    if (tok < a.M) {
+    // the data-gradient GEMM's output is bf16 (autocast); the scan's du is added to it in tile_out
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = 32 * db + 8 * g + 4 * h;
-        if (d < a.Dx) {
-          float e[4] = {acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]};
-          if (a.du) {
-            const bf16x4 u = *(const bf16x4*)(a.du + tok * a.ts_du + d);
-            // the data-gradient GEMM's output is bf16 (autocast) before autograd adds the scan's du
+    for (int g = 0; g < 4; ++g) {
+      const int d = 32 * db + 8 * g + 4 * h;
+      if (d < a.Dx) {
+        bf16x4 v;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) e[j] = to_f32(to_bf16(e[j])) + to_f32(u[j]);
-          }
-          bf16x4 v;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = to_bf16(e[j]);
-          *(bf16x4*)(a.dxs + tok * a.ts_dxs + d) = v;
-        }
+        for (int j = 0; j < 4; ++j) v[j] = to_bf16(acc[4 * g + j]);
+        *(bf16x4*)(tw + n * (a.Dx + 8) + d) = v;
       }
     }
   }
+  __builtin_amdgcn_wave_barrier();
+  tile_out(a.dxs, t0, a.M, a.Dx, tw, lane, a.du);
 }
 
 static int mp_fill(MpArgs& a, long long M, int Dx, int R, int N2) {
@@ -225,13 +253,13 @@ extern "C" int lci_mamba_proj_fwd(const void* xs, long long ts_x, const void* w1
                                   int R, int N2, void* stream) {
   MpArgs a{};
   if (mp_fill(a, M, Dx, R, N2)) return 1;
-  LCI_CHECK(ld_dtl % 8 == 0 && ld_dtl >= R && ts_x % 8 == 0 && ts_dt % 4 == 0, "mamba_proj_fwd: bad strides");
+  LCI_CHECK(ld_dtl % 8 == 0 && ld_dtl >= R && ts_x == Dx && ts_dt == Dx, "mamba_proj_fwd: xs / dt must be (M, Dx) rows");
   LCI_CHECK(((uintptr_t)xs | (uintptr_t)w1 | (uintptr_t)w2p | (uintptr_t)bc | (uintptr_t)dtl) % 16 == 0 &&
-            (uintptr_t)dt % 8 == 0, "mamba_proj_fwd: pointers must be 16-byte aligned (dt 8)");
+            (uintptr_t)dt % 16 == 0, "mamba_proj_fwd: pointers must be 16-byte aligned");
   a.xs = (const bf16*)xs; a.ts_x = ts_x; a.w1 = (const bf16*)w1; a.w2p = (const bf16*)w2p; a.bias = bias;
   a.dt = (bf16*)dt; a.ts_dt = ts_dt; a.bc = (bf16*)bc; a.dtl = (bf16*)dtl; a.ld_dtl = ld_dtl;
   const long long blocks = (M + MP_WAVES * MP_TOK - 1) / (MP_WAVES * MP_TOK);
-  const size_t lds = (size_t)MP_WAVES * MP_TOK * a.rows_lds * sizeof(bf16);
+  const size_t lds = (size_t)MP_WAVES * MP_TOK * (a.rows_lds + a.Dxp + 8) * sizeof(bf16);
   hipLaunchKernelGGL(mamba_proj_fwd_kernel, dim3((unsigned)blocks), dim3(256), lds, (hipStream_t)stream, a);
   LCI_LAUNCH_CHECK();
   return 0;
@@ -242,16 +270,16 @@ extern "C" int lci_mamba_proj_bwd(const void* ddt, long long ts_ddt, const void*
                                   void* dxdbl, int ld_dxdbl, long long M, int Dx, int R, int N2, void* stream) {
   MpArgs a{};
   if (mp_fill(a, M, Dx, R, N2)) return 1;
-  LCI_CHECK(ld_dxdbl % 8 == 0 && ld_dxdbl >= R + N2 && ld_dxdbl <= a.rows_lds && ts_ddt % 8 == 0 &&
-            ts_dxs % 4 == 0 && (!du || ts_du % 4 == 0), "mamba_proj_bwd: bad strides");
+  LCI_CHECK(ld_dxdbl % 8 == 0 && ld_dxdbl >= R + N2 && ld_dxdbl <= a.rows_lds && ts_ddt == Dx && ts_dxs == Dx &&
+            (!du || ts_du == Dx), "mamba_proj_bwd: ddt / dxs / du must be (M, Dx) rows");
   LCI_CHECK(((uintptr_t)ddt | (uintptr_t)w2t | (uintptr_t)w1t | (uintptr_t)dxdbl) % 16 == 0 &&
-            ((uintptr_t)dxs | (uintptr_t)du) % 8 == 0 && (uintptr_t)dbc % 2 == 0,
-            "mamba_proj_bwd: pointers must be 16-byte aligned (dxs / du 8)");
+            ((uintptr_t)dxs | (uintptr_t)du) % 16 == 0 && (uintptr_t)dbc % 2 == 0,
+            "mamba_proj_bwd: pointers must be 16-byte aligned");
   a.ddt = (const bf16*)ddt; a.ts_ddt = ts_ddt; a.dbc = (const bf16*)dbc; a.w2t = (const bf16*)w2t; a.w1t = (const bf16*)w1t;
   a.du = (const bf16*)du; a.ts_du = ts_du; a.dxs = (bf16*)dxs; a.ts_dxs = ts_dxs; a.dxdbl = (bf16*)dxdbl;
   a.ld_dxdbl = ld_dxdbl;
   const long long blocks = (M + MP_WAVES * MP_TOK - 1) / (MP_WAVES * MP_TOK);
-  const size_t lds = (size_t)MP_WAVES * MP_TOK * a.rows_lds * sizeof(bf16);
+  const size_t lds = (size_t)MP_WAVES * MP_TOK * (a.rows_lds + a.Dxp + 8) * sizeof(bf16);
   hipLaunchKernelGGL(mamba_proj_bwd_kernel, dim3((unsigned)blocks), dim3(256), lds, (hipStream_t)stream, a);
   LCI_LAUNCH_CHECK();
   return 0;
