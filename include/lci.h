@@ -86,7 +86,8 @@ int lci_attn_bwd_stage(int stage, const void* qkv, const void* out, const void* 
  *   mode 0 (windows): qkv (Bw, N, 3C), optional mask (nW, N, N) f32 (has_mask), out (Bw, N, C).
  * Bias table: lci_window_bias(rpb (H, N, N) f32 = rpb_table[rp_index], mask or null) writes
  *   bias (T, H, Npad, Npad) bf16 = (rpb + mask) * log2(e), -1e30 at padded rows/columns (Npad = ceil(N/32)*32,
- *   T = lci_window_bias_elems(geo, has_mask) / (H Npad^2): window types), and its transpose biasT (or null).
+ *   T = lci_window_bias_elems(geo, has_mask) / (H Npad^2): window types), and its transpose biasT; either (not
+ *   both) may be null; both 8-byte aligned.
  * lse2: (Bw, H, N) f32 (Bw = B * prod(ceil(S/ws)) in grid mode). N <= 768. */
 long long lci_window_bias_elems(const int* geo, int has_mask);
 int lci_window_bias(const float* rpb, const float* mask, void* bias, void* biasT, const int* geo, void* stream);

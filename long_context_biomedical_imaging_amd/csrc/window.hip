@@ -23,6 +23,7 @@
 #include "common.hpp"
 
 #include <algorithm>
+#include <stdlib.h>
 
 // scheduling-strategy hooks for A/B runs (tools/attn_variants.sh): iglp_opt(N) on the fwd / bwd tile loops
 #ifdef LCI_WIN_IGLP_FWD
@@ -187,22 +188,52 @@ __device__ __forceinline__ int win_region(const WinArgs& a, int t, int n) {
   return rid;
 }
 
+// One workgroup = a 32 (q) x 32 (k) tile of one (type, head). The region ids of the tile's 32 queries and 32 keys
+// are computed once into LDS; a thread evaluates 4 consecutive keys of one query and writes them as one 8-byte
+// chunk of a bias row; the transposed tile goes through LDS so biasT rows are written the same way. (The first
+// version, one thread per element with two region evaluations each and 2-byte strided biasT stores, took 26-188 us
+// per shifted call at the C3 stages.)
+constexpr int WBT_LD = 36;   // LDS row stride of the transposed tile (elements): 8-byte aligned rows
 __global__ __launch_bounds__(256) void win_bias_kernel(WinArgs a, bf16* bias, bf16* biasT) {
-  const long long np2 = (long long)a.Npad * a.Npad;
-  const long long e = blockIdx.x * 256LL + threadIdx.x;
-  if (e >= (long long)a.T * a.H * np2) return;
-  const int k = e % a.Npad, q = (e / a.Npad) % a.Npad;
-  const long long th = e / np2;   // t * H + h
+  __shared__ int rq[32], rk[32];
+  __shared__ __attribute__((aligned(8))) bf16 sT[32 * WBT_LD];
+  const int nt = a.Npad / 32;
+  int b = blockIdx.x;
+  const int kt = b % nt;
+  b /= nt;
+  const int qt = b % nt, th = b / nt;   // th = t * H + h
   const int h = th % a.H, t = th / a.H;
-  float v = WNEG;
-  if (q < a.N && k < a.N) {
-    v = a.rpb[((long long)h * a.N + q) * a.N + k];
-    if (a.mode == 0 && a.mask) v += a.mask[((long long)t * a.N + q) * a.N + k];
-    if (a.mode == 1 && a.masked && win_region(a, t, q) != win_region(a, t, k)) v += -100.f;
-    v *= WLOG2E;
+  const int tid = threadIdx.x;
+  const bool regions = a.mode == 1 && a.masked;
+  if (tid < 64) {
+    const int n = (tid < 32 ? qt : kt) * 32 + (tid & 31);
+    const int r = (regions && n < a.N) ? win_region(a, t, n) : 0;
+    if (tid < 32) rq[tid] = r; else rk[tid - 32] = r;
   }
-  bias[e] = to_bf16(v);
-  if (biasT) biasT[th * np2 + (long long)k * a.Npad + q] = to_bf16(v);
+  __syncthreads();
+  const int ql = tid >> 3, kl = (tid & 7) * 4;
+  const int q = qt * 32 + ql;
+  const long long np = a.Npad;
+  bf16x4 v4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int k = kt * 32 + kl + j;
+    float v = WNEG;
+    if (q < a.N && k < a.N) {
+      v = a.rpb[((long long)h * a.N + q) * a.N + k];
+      if (a.mode == 0 && a.mask) v += a.mask[((long long)t * a.N + q) * a.N + k];
+      if (regions && rq[ql] != rk[kl + j]) v += -100.f;
+      v *= WLOG2E;
+    }
+    v4[j] = to_bf16(v);
+    sT[(kl + j) * WBT_LD + ql] = v4[j];
+  }
+  if (bias) *(bf16x4*)(bias + ((long long)th * np + q) * np + kt * 32 + kl) = v4;
+  if (biasT) {   // uniform per launch
+    __syncthreads();
+    const int kr = tid >> 3, qc = (tid & 7) * 4;
+    *(bf16x4*)(biasT + ((long long)th * np + kt * 32 + kr) * np + qt * 32 + qc) = *(const bf16x4*)(sT + kr * WBT_LD + qc);
+  }
 }
 
 // 16 table values of one 32x32 score tile for this lane: row r (q or key, the lane's), columns
@@ -312,7 +343,8 @@ __global__ __launch_bounds__(NW * 64) void win_attn_fwd_kernel(WinArgs a) {
 }
 
 // -------------------------------------------------------------------------------------------- backward
-__global__ __launch_bounds__(256) void win_attn_bwd_kernel(WinArgs a) {
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void win_attn_bwd_kernel(WinArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int w = blockIdx.x, hh = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5;
@@ -325,8 +357,8 @@ __global__ __launch_bounds__(256) void win_attn_bwd_kernel(WinArgs a) {
   const float* lseg = a.lse2 + ((long long)w * a.H + hh) * a.N;
 
   // ---------------- phase 1: K, V in LDS; query on the lane -> dQ, dS tiles, delta
-  win_stage<256>(a, L, a.C + hh * WHD, 2 * a.C + hh * WHD, false, nullptr, w);
-  for (int qb = wave; qb < a.nqb; qb += 4) {
+  win_stage<NW * 64>(a, L, a.C + hh * WHD, 2 * a.C + hh * WHD, false, nullptr, w);
+  for (int qb = wave; qb < a.nqb; qb += NW) {
     const int q = qb * 32 + (lane & 31);
     const bool qv = q < a.N;
     const int qrow = qv ? L.row[q] : -2;
@@ -393,8 +425,8 @@ __global__ __launch_bounds__(256) void win_attn_bwd_kernel(WinArgs a) {
   __syncthreads();
 
   // ---------------- phase 2: Q, dO in LDS; key on the lane -> dK, dV
-  win_stage<256>(a, L, hh * WHD, hh * WHD, true, a.dout, w);   // Q -> t0, dO -> t1
-  for (int kb = wave; kb < a.nqb; kb += 4) {
+  win_stage<NW * 64>(a, L, hh * WHD, hh * WHD, true, a.dout, w);   // Q -> t0, dO -> t1
+  for (int kb = wave; kb < a.nqb; kb += NW) {
     const int key = kb * 32 + (lane & 31);
     const bool kv = key < a.N;
     const int krow = kv ? L.row[key] : -2;
@@ -606,9 +638,12 @@ extern "C" int lci_window_bias(const float* rpb, const float* mask, void* bias, 
   if (win_fill(a, geo, 1.f)) return 1;
   a.rpb = rpb; a.mask = mask;
   if (a.mode == 0 && mask) a.T = a.nW;
-  const long long n = (long long)a.T * a.H * a.Npad * a.Npad;
-  hipLaunchKernelGGL(win_bias_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a,
-                     (bf16*)bias, (bf16*)biasT);
+  LCI_CHECK(bias || biasT, "window_bias: no output");
+  LCI_CHECK(((uintptr_t)bias & 7) == 0 && ((uintptr_t)biasT & 7) == 0, "window_bias: tables must be 8-byte aligned");
+  const long long nt = a.Npad / 32, n = (long long)a.T * a.H * nt * nt;
+  LCI_CHECK(n < (1LL << 31), "window_bias: table too large");
+  hipLaunchKernelGGL(win_bias_kernel, dim3((unsigned)n), dim3(256), 0, (hipStream_t)stream, a, (bf16*)bias,
+                     (bf16*)biasT);
   LCI_LAUNCH_CHECK();
   return 0;
 }
@@ -641,8 +676,17 @@ extern "C" int lci_window_attn_bwd(const void* qkv, const float* qkv_bias, const
   a.dout = (const bf16*)dout; a.lse2 = (float*)lse2; a.dqkv = (bf16*)dqkv; a.dbias_pad = dbias_pad;
   a.dS = (bf16*)dS; a.drpb = drpb;
   hipStream_t s = (hipStream_t)stream;
-  (void)hipFuncSetAttribute((const void*)win_attn_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipLaunchKernelGGL(win_attn_bwd_kernel, dim3(a.Bw, a.H), dim3(256), win_lds(a, true), s, a);
+  // waves per (window, head) workgroup (LCI_WIN_BWD_WAVES: A/B override)
+  static const int nw_env = getenv("LCI_WIN_BWD_WAVES") ? atoi(getenv("LCI_WIN_BWD_WAVES")) : 4;
+  if (nw_env == 8) {
+    (void)hipFuncSetAttribute((const void*)win_attn_bwd_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    hipLaunchKernelGGL(win_attn_bwd_kernel<8>, dim3(a.Bw, a.H), dim3(512), win_lds(a, true), s, a);
+  } else {
+    (void)hipFuncSetAttribute((const void*)win_attn_bwd_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    hipLaunchKernelGGL(win_attn_bwd_kernel<4>, dim3(a.Bw, a.H), dim3(256), win_lds(a, true), s, a);
+  }
   LCI_LAUNCH_CHECK();
   if (dS && drpb) {
     const long long per_w = (long long)a.H * a.nqb * a.nkt * 1024;

@@ -484,16 +484,16 @@ def _i32(vals):
     return (ctypes.c_int * len(vals))(*[int(v) for v in vals])
 
 
-def _window_bias(rpb, mask, geo, transposed=False):
-    """(T, H, Npad, Npad) log2-domain logit term (and its transpose): rpb + region/explicit mask, padding."""
+def _window_bias(rpb, mask, geo, transposed=False, plain=True):
+    """(T, H, Npad, Npad) log2-domain logit term and / or its transpose: rpb + region/explicit mask, padding."""
     g = _i32(geo)
     n = int(_lib.load().lci_window_bias_elems(g, int(mask is not None)))
     if n <= 0:
         raise _lib.LciError(_lib.load().lci_last_error().decode())
     b16 = dict(device=rpb.device, dtype=torch.bfloat16)
-    bias = torch.empty(n, **b16)
+    bias = torch.empty(n, **b16) if plain else None
     bt = torch.empty(n, **b16) if transposed else None
-    _lib.call("lci_window_bias", rpb.data_ptr(), _lib.ptr(mask), bias.data_ptr(), _lib.ptr(bt), g,
+    _lib.call("lci_window_bias", rpb.data_ptr(), _lib.ptr(mask), _lib.ptr(bias), _lib.ptr(bt), g,
               _lib.stream_of(rpb))
     return bias, bt
 
@@ -514,13 +514,13 @@ class _WindowAttention(torch.autograd.Function):
         KernelTimer.run("window_attn_fwd", 4.0 * Bw * H * N * N * 32, qkv, lambda: _lib.call(
             "lci_window_attn_fwd", qkv.data_ptr(), _lib.ptr(bf), tab.data_ptr(), int(mk is not None), out.data_ptr(),
             lse2.data_ptr(), g, float(scale), _lib.stream_of(qkv)))
-        ctx.save_for_backward(qkv, bf, rp, mk, out, lse2)
+        ctx.save_for_backward(qkv, bf, rp, mk, out, lse2, tab)   # the backward reuses the table
         ctx.geo, ctx.scale, ctx.has_bias = geo, scale, bias is not None
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        qkv, bf, rp, mk, out, lse2 = ctx.saved_tensors
+        qkv, bf, rp, mk, out, lse2, tab = ctx.saved_tensors
         geo, scale = ctx.geo, ctx.scale
         g = _i32(geo)
         N, C, H = geo[13], geo[14], geo[15]
@@ -535,7 +535,7 @@ class _WindowAttention(torch.autograd.Function):
             n_el = _lib.load().lci_window_dS_elems(g)
             dS = torch.empty(int(n_el), device=qkv.device, dtype=torch.bfloat16)
             drpb = torch.empty(H, N, N, **f32)
-        tab, tabT = _window_bias(rp, mk, geo, transposed=True)
+        _, tabT = _window_bias(rp, mk, geo, transposed=True, plain=False)
         KernelTimer.run("window_attn_bwd", 8.0 * Bw * H * N * N * 32, qkv, lambda: _lib.call(
             "lci_window_attn_bwd", qkv.data_ptr(), _lib.ptr(bf), tab.data_ptr(), tabT.data_ptr(), int(mk is not None),
             out.data_ptr(), dout.data_ptr(), lse2.data_ptr(), dqkv.data_ptr(), _lib.ptr(dbias), _lib.ptr(dS),

@@ -86,6 +86,31 @@ def bench_window():
          "same, fwd+bwd with the rpb gradient (dS tiles + window reduction)")
 
 
+def bench_window_stages():
+    """Window attention at every Swin-tiny stage of C3 (128^3 p2, B = 1, window 7): fwd, bwd without / with the
+    rpb gradient, per stage and shift (the block pairs run shift 0 then 3)."""
+    for S, C, H in ((64, 96, 3), (32, 192, 6), (16, 384, 12), (8, 768, 24)):
+        w, B = 7, 1
+        N = w ** 3
+        Bw = B * (-(-S // w)) ** 3
+        f = 4.0 * Bw * H * N * N * 32
+        for sh in (0, 3):
+            qkv = torch.randn(B, S, S, S, 3 * C, device="cuda").to(torch.bfloat16).requires_grad_(True)
+            bias = torch.randn(3 * C, device="cuda") * 0.1
+            rpb = torch.randn(H, N, N, device="cuda") * 0.1
+            run = lambda: kernels.window_attention_grid(qkv, bias, rpb, H, 32 ** -0.5, (w, w, w), (sh, sh, sh))  # noqa
+            cfg = f"S{S} C{C} H{H} Bw{Bw} w7 s{sh}"
+            tf = timeit(lambda: run(), iters=10)
+            emit("window_attn_fwd", tf, f, "TFLOP/s", cfg)
+            o = run()
+            g = torch.randn_like(o)
+            tb = timeit(lambda: torch.autograd.grad(run(), qkv, g), iters=10) - tf
+            emit("window_attn_bwd", tb, 2 * f, "TFLOP/s", cfg + " (bwd = fwd+bwd - fwd, rpb grad off)")
+            rpb.requires_grad_(True)
+            tr = timeit(lambda: torch.autograd.grad(run(), [qkv, rpb], g), iters=10) - tf
+            emit("window_attn_bwd+drpb", tr, 2 * f, "TFLOP/s", cfg + " (with the rpb gradient)")
+
+
 def bench_scan(L, B=2, Dx=192):
     u = torch.randn(B, L, Dx, device="cuda").to(torch.bfloat16).requires_grad_(True)
     dl = (torch.randn(B, L, Dx, device="cuda") * 0.5 - 3).to(torch.bfloat16).requires_grad_(True)
@@ -239,6 +264,8 @@ def main():
         bench_attention()
     if "window" in which:
         bench_window()
+    if "wstages" in which:
+        bench_window_stages()
     if "scan" in which:
         bench_scan(65536)
         bench_scan(1 << 21)
