@@ -396,6 +396,145 @@ __global__ __launch_bounds__(512) void conv3_fwd_lds2_kernel(ConvArgs a) {
   }
 }
 
+// LDS-staged forward v3 (Cin % 32 == 0): the v2 staging (512 voxels x 32*NT output channels per workgroup, slab =
+// one (tap group, 32-channel chunk), register double-buffered, one barrier per slab) with 4 waves of 128 voxels
+// (ML = 4 blocks of 32) instead of 8 waves of 64: a wave's tile is 4 x NT accumulators (up to 256 registers: the
+// accumulator file at one wave per SIMD), so every LDS fragment feeds NT or 4 MFMAs and a k-step reads NT + 4
+// fragments for 4 NT MFMAs (v2: NT + 2 for 2 NT). At NT = 4 that is 0.5 instead of 0.75 KB of LDS reads per MFMA,
+// which kept v2's LDS pipe as busy as its MFMA pipe.
+template <int NT, int ML>
+__global__ __launch_bounds__(256) void conv3_fwd_lds3_kernel(ConvArgs a) {
+  constexpr int NWV = 4;
+  constexpr int WV = NWV * 32 * ML;            // voxels per workgroup
+  constexpr int XR = WV + 2;                   // staged rows (dx halo)
+  constexpr int XBUF = XR * CLD, WBUF = 3 * 32 * NT * CLD;
+  constexpr int NXS = (XR * 4 + 255) / 256, NWS = (3 * 32 * NT * 4 + 255) / 256;
+  extern __shared__ __attribute__((aligned(16))) bf16 smem3[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+  const int r = lane & 31, h = lane >> 5;
+  long long vblk;
+  int ntl;
+  if (!conv_work(a, vblk, ntl)) return;   // 1-D grid padding (uniform per workgroup, before any barrier)
+  const long long vg0 = vblk * WV;
+  const int n0 = ntl * 32 * NT;
+  const int T = a.KD * 9;
+  const int HW = a.H * a.W;
+  int zc[ML], yc[ML], xc[ML];
+  bool inb[ML];
+#pragma unroll
+  for (int m = 0; m < ML; ++m) {
+    const long long v = vg0 + wave * 32 * ML + 32 * m + r;
+    inb[m] = v < a.V;
+    const long long vv = inb[m] ? v : 0;
+    const long long s = vv / ((long long)a.D * HW);
+    int rem = (int)(vv - s * (long long)a.D * HW);
+    zc[m] = rem / HW; rem -= zc[m] * HW;
+    yc[m] = rem / a.W; xc[m] = rem - yc[m] * a.W;
+  }
+  f32x16 acc[ML][NT];
+#pragma unroll
+  for (int m = 0; m < ML; ++m)
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[m][t][i] = 0.f;
+
+  const int nchunk = a.Cin / 32, nslab = a.KD * 3 * nchunk;
+  u32x4 vx[NXS], vw[NWS];
+  auto load = [&](int sl) {
+    const int grp = sl / nchunk, c0 = (sl - grp * nchunk) * 32;
+    const int dz = (a.KD == 3 ? grp / 3 : 1) - 1, dy = grp % 3 - 1;
+    const long long src0 = vg0 + (long long)dz * HW + (long long)dy * a.W - 1;
+#pragma unroll
+    for (int i = 0; i < NXS; ++i) {
+      const int q = tid + 256 * i, row = q >> 2, ch = q & 3;
+      const long long u = src0 + row;
+      vx[i] = u32x4{0u, 0u, 0u, 0u};
+      if (q < XR * 4 && u >= 0 && u < a.V) vx[i] = *(const u32x4*)(a.x + u * a.Cin + c0 + 8 * ch);
+    }
+#pragma unroll
+    for (int i = 0; i < NWS; ++i) {
+      const int q = tid + 256 * i, row = q >> 2, ch = q & 3;   // row = dx * 32NT + n
+      vw[i] = u32x4{0u, 0u, 0u, 0u};
+      if (q < 3 * 32 * NT * 4) {
+        const int dxi = row / (32 * NT), n = row - dxi * 32 * NT;
+        vw[i] = *(const u32x4*)(a.w + ((long long)(n0 + n) * T + grp * 3 + dxi) * a.Cin + c0 + 8 * ch);
+      }
+    }
+  };
+  auto store = [&](int buf) {
+    bf16* sX = smem3 + buf * (XBUF + WBUF);
+    bf16* sW = sX + XBUF;
+#pragma unroll
+    for (int i = 0; i < NXS; ++i) {
+      const int q = tid + 256 * i, row = q >> 2, ch = q & 3;
+      if (q < XR * 4) *(u32x4*)(sX + row * CLD + 8 * ch) = vx[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NWS; ++i) {
+      const int q = tid + 256 * i, row = q >> 2, ch = q & 3;
+      if (q < 3 * 32 * NT * 4) *(u32x4*)(sW + row * CLD + 8 * ch) = vw[i];
+    }
+  };
+  load(0);
+  store(0);
+  __syncthreads();
+  int buf = 0;
+  for (int sl = 0; sl < nslab; ++sl) {
+    const bool more = sl + 1 < nslab;
+    if (more) load(sl + 1);
+    LCI_CONV_SCHED();
+    const int grp = sl / nchunk;
+    const int dz = (a.KD == 3 ? grp / 3 : 1) - 1, dy = grp % 3 - 1;
+    bool okzy[ML];
+#pragma unroll
+    for (int m = 0; m < ML; ++m)
+      okzy[m] = inb[m] && (unsigned)(zc[m] + dz) < (unsigned)a.D && (unsigned)(yc[m] + dy) < (unsigned)a.H;
+    const bf16* sX = smem3 + buf * (XBUF + WBUF);
+    const bf16* sW = sX + XBUF;
+#pragma unroll
+    for (int dxi = 0; dxi < 3; ++dxi) {
+      bool ok[ML];
+#pragma unroll
+      for (int m = 0; m < ML; ++m) ok[m] = okzy[m] && (unsigned)(xc[m] + dxi - 1) < (unsigned)a.W;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 wa[NT], xb[ML];
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          wa[t] = *(const bf16x8*)(sW + (dxi * 32 * NT + 32 * t + r) * CLD + 16 * ks + 8 * h);
+#pragma unroll
+        for (int m = 0; m < ML; ++m) {
+          xb[m] = *(const bf16x8*)(sX + (wave * 32 * ML + 32 * m + r + dxi) * CLD + 16 * ks + 8 * h);
+          if (!ok[m]) xb[m] = zero8();
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int m = 0; m < ML; ++m) acc[m][t] = mfma32(wa[t], xb[m], acc[m][t]);
+      }
+    }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+#pragma unroll
+  for (int m = 0; m < ML; ++m) {
+    if (!inb[m]) continue;
+    const long long v = vg0 + wave * 32 * ML + 32 * m + r;
+    bf16* yp = a.y + v * a.Cout + n0 + 4 * h;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        bf16x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = to_bf16(acc[m][t][4 * q + j]);
+        *(bf16x4*)(yp + 32 * t + 8 * q) = o;
+      }
+  }
+}
+
 // Generic path (any Cin, e.g. the 1-channel image into encoder1): K = T * Cin flattened and zero-padded to
 // 16; each lane gathers its 8 k-values element by element. Only used for tiny Cin, where K is small.
 template <int NT>
@@ -849,11 +988,33 @@ static bool lci_conv_lds() {   // LCI_CONV_LDS=0: the direct-load kernel (A/B)
   return on;
 }
 
+template <int NT, int ML3>
+static int launch_v3(const ConvArgs& a, hipStream_t st) {
+  static const int order_env = getenv("LCI_CONV_ORDER") ? atoi(getenv("LCI_CONV_ORDER")) : -1;
+  ConvArgs b = a;
+  b.nvb = (int)((a.V + 128 * ML3 - 1) / (128 * ML3));
+  b.ntile = a.Cout / (32 * NT);
+  b.order = order_env >= 0 ? order_env : (a.Cout >= 96 ? 1 : 0);
+  const long long nb = (long long)b.nvb * b.ntile;
+  const size_t sh = (size_t)2 * ((128 * ML3 + 2) * CLD + 3 * 32 * NT * CLD) * sizeof(bf16);
+  (void)hipFuncSetAttribute((const void*)conv3_fwd_lds3_kernel<NT, ML3>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024);
+  dim3 grid((unsigned)(b.order ? (nb + 7) / 8 * 8 : nb));
+  hipLaunchKernelGGL((conv3_fwd_lds3_kernel<NT, ML3>), grid, dim3(256), sh, st, b);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+
 template <int NT>
 static int launch(const ConvArgs& a, hipStream_t st) {
   constexpr int MV = NT <= 2 ? 4 : LCI_CONV_MV_WIDE;   // narrow outputs: more voxels per wave
   static const int v2_env = getenv("LCI_CONV_V2") ? atoi(getenv("LCI_CONV_V2")) : 1;
-  if (a.Cin % 32 == 0 && lci_conv_lds() && v2_env) {
+  static const int v3_env = getenv("LCI_CONV_V3") ? atoi(getenv("LCI_CONV_V3")) : 0;
+  if (a.Cin % 32 == 0 && lci_conv_lds() && v3_env) {
+    // 32-voxel blocks per wave: 4, or 3 for NT = 4 (LCI_CONV_V3=3: A/B of 192 vs 256 accumulator registers)
+    if (NT == 4 && v3_env == 3) return launch_v3<NT, 3>(a, st);
+    return launch_v3<NT, 4>(a, st);
+  } else if (a.Cin % 32 == 0 && lci_conv_lds() && v2_env) {
     static const int order_env = getenv("LCI_CONV_ORDER") ? atoi(getenv("LCI_CONV_ORDER")) : -1;
     ConvArgs b = a;
     b.nvb = (int)((a.V + 511) / 512);
