@@ -50,8 +50,9 @@ extern "C" {
  * 4: lci_conv3_wgrad writes one partial per voxel split instead of one per split and wave; 5: lci_linear_wgrad;
  * 6: lci_hyena_filter; 7: lci_upsample2x; 8: lci_gelu;
  * 9: lci_layernorm_add_fwd; 10: lci_upsample2x_nhwc; 11: lci_fftconv Su; 12: lci_upsample3d_cl_fwd,
- * lci_resample1d_adj and the round-3 entry points below). */
-#define LCI_ABI_VERSION 12
+ * lci_resample1d_adj and the round-3 entry points below; 13: lci_conv3_fwd_split, lci_window_bias with either
+ * table optional). */
+#define LCI_ABI_VERSION 13
 const char* lci_last_error(void);
 int lci_abi_version(void);
 /* sha256 prefix of the sources the library was built from (build_lib.source_hash); the Python binding refuses a
@@ -122,6 +123,13 @@ int lci_window_gather(const void* src, void* dst, int elem_bytes, const int* geo
  * w'[c, t, n] = w[n, c, KD*9-1-t]. */
 int lci_conv3_fwd(const void* x, const void* w, void* y, int B, int D, int H, int W, int Cin, int Cout, int KD,
                   void* stream);
+/* Split-K form for small volumes (few 512-voxel tiles): part (nsplit, B*D*H*W, Cout) f32 workspace holds the
+ * partial sums of contiguous ranges of the (tap group, 32-channel chunk) slabs, summed in split order into y
+ * (deterministic). nsplit = lci_conv3_fwd_splits(B*D*H*W, Cin, Cout, KD) (1: use lci_conv3_fwd); Cin % 32 == 0;
+ * y and part 16-byte aligned. */
+int lci_conv3_fwd_splits(long long V, int Cin, int Cout, int KD);
+int lci_conv3_fwd_split(const void* x, const void* w, void* y, float* part, int nsplit, int B, int D, int H, int W,
+                        int Cin, int Cout, int KD, void* stream);
 /* Weight gradient: part (lci_conv3_wgrad_splits(B*D*H*W, Cin, Cout, KD), KD*9, Cout, Cin) f32 <- per-voxel-split
  * partial sums of dy[p, n] * x[p + off(tap), c]; dW[n, c, tap] = sum over the first axis (caller). x (.., Cin),
  * dy (.., Cout) bf16 channels-last; Cin, Cout multiples of 32. Deterministic (no atomics). */

@@ -14,7 +14,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_LIB = os.path.join(HERE, "liblci.so")
 LIB_PATH = os.environ.get("LCI_LIB_PATH", DEFAULT_LIB)   # override: kernel-variant A/B runs (no staleness check)
-ABI_VERSION = 12   # include/lci.h LCI_ABI_VERSION
+ABI_VERSION = 13   # include/lci.h LCI_ABI_VERSION
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -45,6 +45,7 @@ SIGNATURES = {
     "lci_hyena_pre_bwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "lci_dwconv_silu_fwd": [_I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "lci_conv3_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
+    "lci_conv3_fwd_split": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "lci_conv3_wgrad": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "lci_inorm_reduce": [_P, _P, _P, _P, _L, _I, _I, _I, _F, _P],
     "lci_inorm_apply": [_P, _P, _P, _P, _P, _L, _I, _I, _I, _F, _P],
@@ -109,6 +110,8 @@ def load(path: str = LIB_PATH):
     lib.lci_window_bias_elems.argtypes = [_P, _I]
     lib.lci_attn_fwd_ws_bytes.restype = ctypes.c_longlong
     lib.lci_attn_fwd_ws_bytes.argtypes = [_I, _I, _I]
+    lib.lci_conv3_fwd_splits.restype = ctypes.c_int
+    lib.lci_conv3_fwd_splits.argtypes = [ctypes.c_longlong, _I, _I, _I]
     lib.lci_conv3_wgrad_splits.restype = ctypes.c_longlong
     lib.lci_conv3_wgrad_splits.argtypes = [ctypes.c_longlong, _I, _I, _I]
     lib.lci_linear_wgrad_splits.restype = ctypes.c_longlong

@@ -15,6 +15,8 @@
 // Neighbour reuse (27 taps read the same voxels) is served by L1/L2: the volume is swept in voxel order.
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "common.hpp"
 
 #ifndef LCI_CONV_MV_WIDE
@@ -42,6 +44,8 @@ struct ConvArgs {
   long long V;      // B * D * H * W
   int D, H, W, Cin, Cout, KD;
   int nvb, ntile, order;   // LDS kernel: voxel blocks, Cout tiles, work order of the 1-D grid (conv_work)
+  int nsplit;              // v2 kernel: reduction (slab) splits; > 1: f32 partials to part, summed by conv3_sum_kernel
+  float* part;             // (nsplit, V, Cout) f32 when nsplit > 1
 };
 
 // (voxel block, Cout tile) of workgroup b for the LDS-staged forward. order 0: voxel block fastest over the plain
@@ -49,9 +53,17 @@ struct ConvArgs {
 // observed round-robin, not relied on for correctness) takes a contiguous range of voxel blocks with the Cout
 // tiles fastest, so the workgroups staging the same x rows (and the +-W row shifts of the dy = +-1 taps) share
 // that XCD's L2; order 2: contiguous voxel-block ranges per XCD, Cout tile slowest.
-__device__ __forceinline__ bool conv_work(const ConvArgs& a, long long& vb, int& nt) {
+__device__ __forceinline__ bool conv_work(const ConvArgs& a, long long& vb, int& nt, int* split = nullptr) {
   long long w = blockIdx.x;
   const long long nb = (long long)a.nvb * a.ntile;
+  if (split) {   // split-K launch: the split is the slowest index, plain order inside a split
+    *split = (int)(w / nb);
+    if (*split >= a.nsplit) return false;
+    w -= (long long)*split * nb;
+    vb = w % a.nvb;
+    nt = (int)(w / a.nvb);
+    return true;
+  }
   if (a.order != 0) {
     const long long per = (nb + 7) / 8;
     w = (long long)(blockIdx.x % 8) * per + blockIdx.x / 8;
@@ -263,7 +275,7 @@ __global__ __launch_bounds__(256) void conv3_fwd_lds_kernel(ConvArgs a) {
 // (the staged weight slab is shared by twice the voxels of v1), and the staging is double-buffered: the next
 // (tap group, 32-channel chunk) slab is loaded into registers while this one's 48 MFMAs per wave run, then written
 // to the other LDS buffer -- one barrier per slab instead of two around an exposed global-load wait.
-template <int NT>
+template <int NT, bool SPLIT>
 __global__ __launch_bounds__(512) void conv3_fwd_lds2_kernel(ConvArgs a) {
   constexpr int ML = 2, NWV = 8;
   constexpr int WV = NWV * 32 * ML;            // 512 voxels
@@ -274,12 +286,14 @@ __global__ __launch_bounds__(512) void conv3_fwd_lds2_kernel(ConvArgs a) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
   const int r = lane & 31, h = lane >> 5;
   long long vblk;
-  int ntl;
-  if (!conv_work(a, vblk, ntl)) return;   // 1-D grid padding (uniform per workgroup, before any barrier)
+  int ntl, split = 0;
+  if (!conv_work(a, vblk, ntl, SPLIT ? &split : nullptr)) return;   // grid padding (uniform, before any barrier)
   const long long vg0 = vblk * WV;
   const int n0 = ntl * 32 * NT;
   const int T = a.KD * 9;
   const int HW = a.H * a.W;
+  // a wave whose 64 voxels all lie past V (small volumes: V < 512) stages but skips its MFMAs
+  const bool live = vg0 + wave * 32 * ML < a.V;
   int zc[ML], yc[ML], xc[ML];
   bool inb[ML];
 #pragma unroll
@@ -300,7 +314,10 @@ __global__ __launch_bounds__(512) void conv3_fwd_lds2_kernel(ConvArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[m][t][i] = 0.f;
 
-  const int nchunk = a.Cin / 32, nslab = a.KD * 3 * nchunk;
+  const int nchunk = a.Cin / 32, nslab_all = a.KD * 3 * nchunk;
+  // this workgroup's slab range (split-K: contiguous ranges of the (tap group, channel chunk) slabs)
+  const int sl0 = SPLIT ? (int)((long long)nslab_all * split / a.nsplit) : 0;
+  const int sl1 = SPLIT ? (int)((long long)nslab_all * (split + 1) / a.nsplit) : nslab_all;
   u32x4 vx[NXS], vw[NWS];
   auto load = [&](int sl) {
     const int grp = sl / nchunk, c0 = (sl - grp * nchunk) * 32;
@@ -337,12 +354,12 @@ __global__ __launch_bounds__(512) void conv3_fwd_lds2_kernel(ConvArgs a) {
       if (q < 3 * 32 * NT * 4) *(u32x4*)(sW + row * CLD + 8 * ch) = vw[i];
     }
   };
-  load(0);
+  load(sl0);
   store(0);
   __syncthreads();
   int buf = 0;
-  for (int sl = 0; sl < nslab; ++sl) {
-    const bool more = sl + 1 < nslab;
+  for (int sl = sl0; sl < sl1; ++sl) {
+    const bool more = sl + 1 < sl1;
     if (more) load(sl + 1);
     LCI_CONV_SCHED();
     const int grp = sl / nchunk;
@@ -354,7 +371,7 @@ __global__ __launch_bounds__(512) void conv3_fwd_lds2_kernel(ConvArgs a) {
     const bf16* sX = smem2 + buf * (XBUF + WBUF);
     const bf16* sW = sX + XBUF;
 #pragma unroll
-    for (int dxi = 0; dxi < 3; ++dxi) {
+    for (int dxi = 0; dxi < 3 && live; ++dxi) {
       bool ok[ML];
 #pragma unroll
       for (int m = 0; m < ML; ++m) ok[m] = okzy[m] && (unsigned)(xc[m] + dxi - 1) < (unsigned)a.W;
@@ -378,6 +395,24 @@ __global__ __launch_bounds__(512) void conv3_fwd_lds2_kernel(ConvArgs a) {
     if (more) store(buf ^ 1);
     __syncthreads();
     buf ^= 1;
+  }
+  if (SPLIT) {   // f32 partial of this slab range: 16-B stores of 4 consecutive output channels
+#pragma unroll
+    for (int m = 0; m < ML; ++m) {
+      if (!inb[m]) continue;
+      const long long v = vg0 + wave * 32 * ML + 32 * m + r;
+      float* pp = a.part + ((long long)split * a.V + v) * a.Cout + n0 + 4 * h;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          f32x4 o;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = acc[m][t][4 * q + j];
+          *(f32x4*)(pp + 32 * t + 8 * q) = o;
+        }
+    }
+    return;
   }
 #pragma unroll
   for (int m = 0; m < ML; ++m) {
@@ -396,142 +431,21 @@ __global__ __launch_bounds__(512) void conv3_fwd_lds2_kernel(ConvArgs a) {
   }
 }
 
-// LDS-staged forward v3 (Cin % 32 == 0): the v2 staging (512 voxels x 32*NT output channels per workgroup, slab =
-// one (tap group, 32-channel chunk), register double-buffered, one barrier per slab) with 4 waves of 128 voxels
-// (ML = 4 blocks of 32) instead of 8 waves of 64: a wave's tile is 4 x NT accumulators (up to 256 registers: the
-// accumulator file at one wave per SIMD), so every LDS fragment feeds NT or 4 MFMAs and a k-step reads NT + 4
-// fragments for 4 NT MFMAs (v2: NT + 2 for 2 NT). At NT = 4 that is 0.5 instead of 0.75 KB of LDS reads per MFMA,
-// which kept v2's LDS pipe as busy as its MFMA pipe.
-template <int NT, int ML>
-__global__ __launch_bounds__(256) void conv3_fwd_lds3_kernel(ConvArgs a) {
-  constexpr int NWV = 4;
-  constexpr int WV = NWV * 32 * ML;            // voxels per workgroup
-  constexpr int XR = WV + 2;                   // staged rows (dx halo)
-  constexpr int XBUF = XR * CLD, WBUF = 3 * 32 * NT * CLD;
-  constexpr int NXS = (XR * 4 + 255) / 256, NWS = (3 * 32 * NT * 4 + 255) / 256;
-  extern __shared__ __attribute__((aligned(16))) bf16 smem3[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
-  const int r = lane & 31, h = lane >> 5;
-  long long vblk;
-  int ntl;
-  if (!conv_work(a, vblk, ntl)) return;   // 1-D grid padding (uniform per workgroup, before any barrier)
-  const long long vg0 = vblk * WV;
-  const int n0 = ntl * 32 * NT;
-  const int T = a.KD * 9;
-  const int HW = a.H * a.W;
-  int zc[ML], yc[ML], xc[ML];
-  bool inb[ML];
-#pragma unroll
-  for (int m = 0; m < ML; ++m) {
-    const long long v = vg0 + wave * 32 * ML + 32 * m + r;
-    inb[m] = v < a.V;
-    const long long vv = inb[m] ? v : 0;
-    const long long s = vv / ((long long)a.D * HW);
-    int rem = (int)(vv - s * (long long)a.D * HW);
-    zc[m] = rem / HW; rem -= zc[m] * HW;
-    yc[m] = rem / a.W; xc[m] = rem - yc[m] * a.W;
-  }
-  f32x16 acc[ML][NT];
-#pragma unroll
-  for (int m = 0; m < ML; ++m)
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[m][t][i] = 0.f;
-
-  const int nchunk = a.Cin / 32, nslab = a.KD * 3 * nchunk;
-  u32x4 vx[NXS], vw[NWS];
-  auto load = [&](int sl) {
-    const int grp = sl / nchunk, c0 = (sl - grp * nchunk) * 32;
-    const int dz = (a.KD == 3 ? grp / 3 : 1) - 1, dy = grp % 3 - 1;
-    const long long src0 = vg0 + (long long)dz * HW + (long long)dy * a.W - 1;
-#pragma unroll
-    for (int i = 0; i < NXS; ++i) {
-      const int q = tid + 256 * i, row = q >> 2, ch = q & 3;
-      const long long u = src0 + row;
-      vx[i] = u32x4{0u, 0u, 0u, 0u};
-      if (q < XR * 4 && u >= 0 && u < a.V) vx[i] = *(const u32x4*)(a.x + u * a.Cin + c0 + 8 * ch);
+// Split-K reduction: y = bf16(sum over splits of part), the splits added in order (deterministic). n8 = V Cout / 8.
+__global__ __launch_bounds__(256) void conv3_sum_kernel(const float* __restrict__ part, bf16* __restrict__ y,
+                                                        long long n8, int nsplit) {
+  const long long stride = (long long)gridDim.x * 256;
+  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n8; e += stride) {
+    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+    for (int sp = 0; sp < nsplit; ++sp) {
+      const float* p = part + (long long)sp * n8 * 8 + e * 8;
+      a0 += *(const f32x4*)p;
+      a1 += *(const f32x4*)(p + 4);
     }
+    bf16x8 o;
 #pragma unroll
-    for (int i = 0; i < NWS; ++i) {
-      const int q = tid + 256 * i, row = q >> 2, ch = q & 3;   // row = dx * 32NT + n
-      vw[i] = u32x4{0u, 0u, 0u, 0u};
-      if (q < 3 * 32 * NT * 4) {
-        const int dxi = row / (32 * NT), n = row - dxi * 32 * NT;
-        vw[i] = *(const u32x4*)(a.w + ((long long)(n0 + n) * T + grp * 3 + dxi) * a.Cin + c0 + 8 * ch);
-      }
-    }
-  };
-  auto store = [&](int buf) {
-    bf16* sX = smem3 + buf * (XBUF + WBUF);
-    bf16* sW = sX + XBUF;
-#pragma unroll
-    for (int i = 0; i < NXS; ++i) {
-      const int q = tid + 256 * i, row = q >> 2, ch = q & 3;
-      if (q < XR * 4) *(u32x4*)(sX + row * CLD + 8 * ch) = vx[i];
-    }
-#pragma unroll
-    for (int i = 0; i < NWS; ++i) {
-      const int q = tid + 256 * i, row = q >> 2, ch = q & 3;
-      if (q < 3 * 32 * NT * 4) *(u32x4*)(sW + row * CLD + 8 * ch) = vw[i];
-    }
-  };
-  load(0);
-  store(0);
-  __syncthreads();
-  int buf = 0;
-  for (int sl = 0; sl < nslab; ++sl) {
-    const bool more = sl + 1 < nslab;
-    if (more) load(sl + 1);
-    LCI_CONV_SCHED();
-    const int grp = sl / nchunk;
-    const int dz = (a.KD == 3 ? grp / 3 : 1) - 1, dy = grp % 3 - 1;
-    bool okzy[ML];
-#pragma unroll
-    for (int m = 0; m < ML; ++m)
-      okzy[m] = inb[m] && (unsigned)(zc[m] + dz) < (unsigned)a.D && (unsigned)(yc[m] + dy) < (unsigned)a.H;
-    const bf16* sX = smem3 + buf * (XBUF + WBUF);
-    const bf16* sW = sX + XBUF;
-#pragma unroll
-    for (int dxi = 0; dxi < 3; ++dxi) {
-      bool ok[ML];
-#pragma unroll
-      for (int m = 0; m < ML; ++m) ok[m] = okzy[m] && (unsigned)(xc[m] + dxi - 1) < (unsigned)a.W;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 wa[NT], xb[ML];
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-          wa[t] = *(const bf16x8*)(sW + (dxi * 32 * NT + 32 * t + r) * CLD + 16 * ks + 8 * h);
-#pragma unroll
-        for (int m = 0; m < ML; ++m) {
-          xb[m] = *(const bf16x8*)(sX + (wave * 32 * ML + 32 * m + r + dxi) * CLD + 16 * ks + 8 * h);
-          if (!ok[m]) xb[m] = zero8();
-        }
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-          for (int m = 0; m < ML; ++m) acc[m][t] = mfma32(wa[t], xb[m], acc[m][t]);
-      }
-    }
-    if (more) store(buf ^ 1);
-    __syncthreads();
-    buf ^= 1;
-  }
-#pragma unroll
-  for (int m = 0; m < ML; ++m) {
-    if (!inb[m]) continue;
-    const long long v = vg0 + wave * 32 * ML + 32 * m + r;
-    bf16* yp = a.y + v * a.Cout + n0 + 4 * h;
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        bf16x4 o;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = to_bf16(acc[m][t][4 * q + j]);
-        *(bf16x4*)(yp + 32 * t + 8 * q) = o;
-      }
+    for (int j = 0; j < 4; ++j) { o[j] = to_bf16(a0[j]); o[4 + j] = to_bf16(a1[j]); }
+    *(bf16x8*)(y + e * 8) = o;
   }
 }
 
@@ -988,33 +902,11 @@ static bool lci_conv_lds() {   // LCI_CONV_LDS=0: the direct-load kernel (A/B)
   return on;
 }
 
-template <int NT, int ML3>
-static int launch_v3(const ConvArgs& a, hipStream_t st) {
-  static const int order_env = getenv("LCI_CONV_ORDER") ? atoi(getenv("LCI_CONV_ORDER")) : -1;
-  ConvArgs b = a;
-  b.nvb = (int)((a.V + 128 * ML3 - 1) / (128 * ML3));
-  b.ntile = a.Cout / (32 * NT);
-  b.order = order_env >= 0 ? order_env : (a.Cout >= 96 ? 1 : 0);
-  const long long nb = (long long)b.nvb * b.ntile;
-  const size_t sh = (size_t)2 * ((128 * ML3 + 2) * CLD + 3 * 32 * NT * CLD) * sizeof(bf16);
-  (void)hipFuncSetAttribute((const void*)conv3_fwd_lds3_kernel<NT, ML3>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024);
-  dim3 grid((unsigned)(b.order ? (nb + 7) / 8 * 8 : nb));
-  hipLaunchKernelGGL((conv3_fwd_lds3_kernel<NT, ML3>), grid, dim3(256), sh, st, b);
-  LCI_LAUNCH_CHECK();
-  return 0;
-}
-
 template <int NT>
 static int launch(const ConvArgs& a, hipStream_t st) {
   constexpr int MV = NT <= 2 ? 4 : LCI_CONV_MV_WIDE;   // narrow outputs: more voxels per wave
   static const int v2_env = getenv("LCI_CONV_V2") ? atoi(getenv("LCI_CONV_V2")) : 1;
-  static const int v3_env = getenv("LCI_CONV_V3") ? atoi(getenv("LCI_CONV_V3")) : 0;
-  if (a.Cin % 32 == 0 && lci_conv_lds() && v3_env) {
-    // 32-voxel blocks per wave: 4, or 3 for NT = 4 (LCI_CONV_V3=3: A/B of 192 vs 256 accumulator registers)
-    if (NT == 4 && v3_env == 3) return launch_v3<NT, 3>(a, st);
-    return launch_v3<NT, 4>(a, st);
-  } else if (a.Cin % 32 == 0 && lci_conv_lds() && v2_env) {
+  if (a.Cin % 32 == 0 && lci_conv_lds() && v2_env) {
     static const int order_env = getenv("LCI_CONV_ORDER") ? atoi(getenv("LCI_CONV_ORDER")) : -1;
     ConvArgs b = a;
     b.nvb = (int)((a.V + 511) / 512);
@@ -1022,10 +914,22 @@ static int launch(const ConvArgs& a, hipStream_t st) {
     b.order = order_env >= 0 ? order_env : (a.Cout >= 96 ? 1 : 0);
     const long long nb = (long long)b.nvb * b.ntile;
     const size_t sh = (size_t)2 * (514 * CLD + 3 * 32 * NT * CLD) * sizeof(bf16);
-    (void)hipFuncSetAttribute((const void*)conv3_fwd_lds2_kernel<NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    dim3 grid((unsigned)(b.order ? (nb + 7) / 8 * 8 : nb));
-    hipLaunchKernelGGL((conv3_fwd_lds2_kernel<NT>), grid, dim3(512), sh, st, b);
+    if (a.nsplit > 1) {
+      LCI_CHECK(a.part != nullptr, "conv3: split-K needs the partial workspace");
+      LCI_CHECK(nb * a.nsplit < (1LL << 31), "conv3: too many workgroups");
+      (void)hipFuncSetAttribute((const void*)conv3_fwd_lds2_kernel<NT, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      hipLaunchKernelGGL((conv3_fwd_lds2_kernel<NT, true>), dim3((unsigned)(nb * a.nsplit)), dim3(512), sh, st, b);
+      LCI_LAUNCH_CHECK();
+      const long long n8 = a.V * a.Cout / 8;
+      hipLaunchKernelGGL(conv3_sum_kernel, dim3((unsigned)std::min<long long>((n8 + 255) / 256, 8192)), dim3(256), 0,
+                         st, (const float*)a.part, a.y, n8, a.nsplit);
+    } else {
+      (void)hipFuncSetAttribute((const void*)conv3_fwd_lds2_kernel<NT, false>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      dim3 grid((unsigned)(b.order ? (nb + 7) / 8 * 8 : nb));
+      hipLaunchKernelGGL((conv3_fwd_lds2_kernel<NT, false>), grid, dim3(512), sh, st, b);
+    }
   } else if (a.Cin % 32 == 0 && lci_conv_lds()) {
     constexpr int ML = NT == 4 ? 2 : 4;
     // measured (tools/conv_bench.py, C3/C5 shapes): order 1 gains up to 12 % from Cout >= 96 (512->256 at 256^3:
@@ -1053,24 +957,59 @@ static int launch(const ConvArgs& a, hipStream_t st) {
 
 using namespace lci;
 
-extern "C" int lci_conv3_fwd(const void* x, const void* w, void* y, int B, int D, int H, int W, int Cin, int Cout,
-                             int KD, void* stream) {
+// Output-channel tile of the forward kernels (32 NT channels), shared by the launch and the split heuristic.
+static int conv3_nt(int Cout) {
+  const int nb = Cout / 32;
+  return nb % 3 == 0 ? 3 : (nb % 4 == 0 ? 4 : (nb % 2 == 0 ? 2 : 1));
+}
+
+static int conv3_fwd_impl(const void* x, const void* w, void* y, float* part, int nsplit, int B, int D, int H, int W,
+                          int Cin, int Cout, int KD, void* stream) {
   LCI_CHECK(B > 0 && D > 0 && H > 0 && W > 0 && Cin > 0, "conv3: bad shape");
   LCI_CHECK(KD == 3 || (KD == 1 && D == 1), "conv3: KD must be 3, or 1 with D == 1 (2-D)");
   LCI_CHECK(Cout % 32 == 0, "conv3: Cout (%d) must be a multiple of 32", Cout);
-  LCI_CHECK(((uintptr_t)x & 15) == 0 && ((uintptr_t)w & 15) == 0 && ((uintptr_t)y & 7) == 0,
-            "conv3: misaligned pointers");
-  ConvArgs a;
+  LCI_CHECK(((uintptr_t)x & 15) == 0 && ((uintptr_t)w & 15) == 0 && ((uintptr_t)y & (nsplit > 1 ? 15 : 7)) == 0 &&
+                ((uintptr_t)part & 15) == 0, "conv3: misaligned pointers");
+  LCI_CHECK(nsplit >= 1 && (nsplit == 1 || Cin % 32 == 0), "conv3: split-K needs Cin %% 32 == 0");
+  ConvArgs a{};
   a.x = (const bf16*)x; a.w = (const bf16*)w; a.y = (bf16*)y;
   a.V = (long long)B * D * H * W;
   a.D = D; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.KD = KD;
+  a.nsplit = nsplit; a.part = part;
   LCI_CHECK((a.V + 255) / 256 < (1LL << 31), "conv3: volume too large");
   hipStream_t st = (hipStream_t)stream;
-  const int nb = Cout / 32;
-  if (nb % 3 == 0) return launch<3>(a, st);
-  if (nb % 4 == 0) return launch<4>(a, st);
-  if (nb % 2 == 0) return launch<2>(a, st);
-  return launch<1>(a, st);
+  switch (conv3_nt(Cout)) {
+    case 3: return launch<3>(a, st);
+    case 4: return launch<4>(a, st);
+    case 2: return launch<2>(a, st);
+    default: return launch<1>(a, st);
+  }
+}
+
+extern "C" int lci_conv3_fwd(const void* x, const void* w, void* y, int B, int D, int H, int W, int Cin, int Cout,
+                             int KD, void* stream) {
+  return conv3_fwd_impl(x, w, y, nullptr, 1, B, D, H, W, Cin, Cout, KD, stream);
+}
+
+// Split-K for small volumes: under 256 workgroups of 512 voxels x 32 NT channels (the 4^3 - 32^3 stages of the
+// SwinUNETR head: 16-128 workgroups on 256 CUs) the (tap group, channel chunk) slabs are split into ranges whose f32
+// partials a second pass sums: ~512 workgroups, at most 100 MB of partials, at least 2 slabs per range.
+extern "C" int lci_conv3_fwd_splits(long long V, int Cin, int Cout, int KD) {
+  if (V <= 0 || Cin % 32 || Cout % 32 || (KD != 1 && KD != 3)) return 1;
+  if (getenv("LCI_CONV_SPLITK") && atoi(getenv("LCI_CONV_SPLITK")) == 0) return 1;
+  const long long nb = (V + 511) / 512 * (Cout / (32 * conv3_nt(Cout)));
+  if (nb >= 256) return 1;
+  const long long nslab = (long long)KD * 3 * (Cin / 32);
+  long long s = (512 + nb - 1) / nb;
+  s = std::min(s, nslab / 2);
+  s = std::min(s, 64LL);
+  while (s > 1 && s * V * Cout * 4 > (100LL << 20)) --s;
+  return (int)std::max(s, 1LL);
+}
+
+extern "C" int lci_conv3_fwd_split(const void* x, const void* w, void* y, float* part, int nsplit, int B, int D, int H,
+                                   int W, int Cin, int Cout, int KD, void* stream) {
+  return conv3_fwd_impl(x, w, y, part, nsplit, B, D, H, W, Cin, Cout, KD, stream);
 }
 
 // Voxel (gapped-row) splits: up to 2^17 rows per workgroup, fewer (>= 1024) when that leaves under ~2048 workgroups

@@ -1124,7 +1124,15 @@ def conv3_cl(x_cl: torch.Tensor, w_packed: torch.Tensor, kd: int) -> torch.Tenso
     B, D, H, W, Cin = x_cl.shape
     Cout = w_packed.shape[0]
     y = torch.empty(B, D, H, W, Cout, device=x_cl.device, dtype=torch.bfloat16)
-    KernelTimer.run("conv3", 2.0 * B * D * H * W * Cout * Cin * kd * 9, x_cl, lambda: _lib.call(
+    V = B * D * H * W
+    ns = int(_lib.load().lci_conv3_fwd_splits(V, Cin, Cout, kd))
+    if ns > 1:   # small volume: split-K with f32 partials (lci_conv3_fwd_split)
+        part = torch.empty(ns, V, Cout, device=x_cl.device, dtype=torch.float32)
+        KernelTimer.run("conv3", 2.0 * V * Cout * Cin * kd * 9, x_cl, lambda: _lib.call(
+            "lci_conv3_fwd_split", x_cl.data_ptr(), w_packed.data_ptr(), y.data_ptr(), part.data_ptr(), ns, B, D, H,
+            W, Cin, Cout, kd, _lib.stream_of(x_cl)))
+        return y
+    KernelTimer.run("conv3", 2.0 * V * Cout * Cin * kd * 9, x_cl, lambda: _lib.call(
         "lci_conv3_fwd", x_cl.data_ptr(), w_packed.data_ptr(), y.data_ptr(), B, D, H, W, Cin, Cout, kd,
         _lib.stream_of(x_cl)))
     return y
@@ -1499,6 +1507,21 @@ def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor, bias: bool):
     return part.sum(0), (dbp.sum(0) if bias else None)
 
 
+def _wgrad_tiny_k(dy2: torch.Tensor, x2: torch.Tensor, bias: bool):
+    """dW (N, K) f32 = dy2^T x2 for K <= 4 input channels (the 1-channel image into a head's 1x1 residual conv, 2·10^6
+    voxel rows at C3): lci_linear_small_bwd with the roles swapped (its "x" = dy2 (M, N <= 256), its "dy" = x2
+    (M, K)) streams dy2 once; the K-padded GEMM hipBLASLt ran instead took 1.5 ms for this 96 x 8 output."""
+    (M, N), K = dy2.shape, x2.shape[1]
+    nt = _lib.load().lci_linear_small_threads()
+    part = torch.empty(K * N + K, nt, device=dy2.device, dtype=torch.float32)
+    w_unused = torch.zeros(K, N, device=dy2.device, dtype=torch.bfloat16)   # read only for dx, which is not asked
+    KernelTimer.run("linear_wgrad_tiny", 2.0 * M * N * K, dy2, lambda: _lib.call(
+        "lci_linear_small_bwd", dy2.data_ptr(), dy2.stride(0), w_unused.data_ptr(), x2.data_ptr(), None,
+        part.data_ptr(), M, K, N, _lib.stream_of(dy2)))
+    dw = part[:K * N].sum(1).view(K, N).t()
+    return dw, (dy2.float().sum(0) if bias else None)
+
+
 class _Linear(torch.autograd.Function):
     """y = x W^T + b with autocast's casts done here (x, W, b -> the autocast dtype, exactly what F.linear under
     autocast computes: hipBLASLt forward and data gradient); the weight / bias gradient runs on lci_linear_wgrad
@@ -1530,6 +1553,9 @@ class _Linear(torch.autograd.Function):
             dx = (dy2 @ wc).view(*dy.shape[:-1], K)
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             x2 = xc.reshape(-1, K)
+            if K <= 4 and x2.dtype == torch.bfloat16 and pointwise_small_supported(dy2, K):
+                dw, db = _wgrad_tiny_k(dy2, x2.contiguous(), ctx.has_bias)
+                return dx, dw, db
             if K % 8 and x2.dtype == torch.bfloat16 and x2.is_cuda:
                 # few input channels (the 1-channel image into a head's 1x1 residual conv): zero-pad to 8 columns
                 x2 = torch.nn.functional.pad(x2, (0, 8 - K % 8))

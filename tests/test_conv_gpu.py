@@ -43,6 +43,34 @@ def test_conv3_parity(B, S, Cin, Cout):
     assert rel_err(wc.grad, wr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("S,Cin,Cout", [((4, 4, 4), 768, 768), ((8, 8, 8), 384, 192), ((3, 5, 4), 256, 128)])
+def test_conv3_split_k_small_volumes(S, Cin, Cout):
+    """Small volumes (the 4^3 - 16^3 SwinUNETR stages) take the split-K form (lci_conv3_fwd_split: f32 partials of
+    slab ranges, summed in split order): forward, data and weight gradients vs the fp32 conv on the host, and the
+    split forward vs the unsplit kernel (LCI_CONV_SPLITK=0) within bf16 output rounding."""
+    import os
+    torch.manual_seed(2)
+    assert kernels._lib.load().lci_conv3_fwd_splits(S[0] * S[1] * S[2], Cin, Cout, 3) > 1
+    x = torch.randn(1, Cin, *S).bfloat16().float()
+    w = (torch.randn(Cout, Cin, 3, 3, 3) / (Cin * 27) ** 0.5).bfloat16().float()
+    dy = torch.randn(1, Cout, *S).bfloat16().float()
+    xr, wr = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    yr = F.conv3d(xr, wr, padding=1)
+    yr.backward(dy)
+    xc, wc = x.cuda().requires_grad_(True), w.cuda().requires_grad_(True)
+    y = kernels.conv3(xc, wc)
+    assert rel_err(y.float(), yr) < 1e-2
+    y.backward(dy.cuda().bfloat16())
+    assert rel_err(xc.grad.float(), xr.grad) < 1e-2
+    assert rel_err(wc.grad, wr.grad) < 1e-2
+    os.environ["LCI_CONV_SPLITK"] = "0"
+    try:
+        y1 = kernels.conv3(x.cuda(), w.cuda())
+    finally:
+        del os.environ["LCI_CONV_SPLITK"]
+    assert rel_err(y.float(), y1.float()) < 4e-3
+
+
 def test_conv3_large_vs_miopen():
     """Swin-tiny decoder1 shape at 64^3 (96 -> 96): against torch's (MIOpen) bf16 conv on the GPU."""
     torch.manual_seed(1)

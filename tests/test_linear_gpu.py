@@ -171,11 +171,11 @@ def test_pointwise_small_vs_autocast_linear(M, N, K):
         assert e < 5e-3, f"{name}: rel-L2 {e:.3e}"   # bf16 outputs / dW, db rounded to bf16 by the reference
 
 
-@pytest.mark.parametrize("Cin,Cout", [(1, 96), (192, 96), (3, 32)])
+@pytest.mark.parametrize("Cin,Cout", [(1, 96), (192, 96), (3, 32), (2, 48), (6, 32)])
 def test_decoder_pointwise_conv_grads(Cin, Cout):
     """decoders.Conv1x1 (UnetResBlock's 1x1 residual conv) on kernels.linear: forward and input gradient equal to
-    the same 1x1 conv as F.linear under autocast (torch's GEMMs), weight / bias gradients within its bf16 rounding (incl. Cin = 1, zero-padded to 8 for
-    the HIP weight gradient)."""
+    the same 1x1 conv as F.linear under autocast (torch's GEMMs), weight / bias gradients within its bf16 rounding
+    (Cin <= 4: the swapped-role lci_linear_small_bwd weight gradient; Cin = 6: zero-padded to 8 columns)."""
     from long_context_biomedical_imaging_amd import decoders
     torch.manual_seed(Cin)
     conv = decoders.Conv1x1(Cin, Cout, 1, 1, bias=True).cuda()

@@ -122,6 +122,37 @@ def test_bias_table_mask_bit_exact(B, S, ws, sh):
         assert torch.equal(core[wt[w]] != 0, mask[w]), f"window {w} type {int(wt[w])}"
 
 
+@pytest.mark.parametrize("B,S,ws,sh", [((1), (9, 10, 8), (4, 4, 4), (2, 2, 2)), (2, (16, 16, 16), (7, 7, 7), (3, 3, 3)),
+                                       (1, (12, 12), (8, 8), (0, 0))])
+def test_bias_table_values_and_transpose(B, S, ws, sh):
+    """lci_window_bias against a host evaluation of its definition, bf16((rpb + mask) log2 e) with -1e30 padding,
+    for random rpb (incl. N not a multiple of 32); the transposed table built alone (the backward's call) is the
+    exact transpose of the plain one (the forward's)."""
+    from long_context_biomedical_imaging_amd import kernels
+    torch.manual_seed(3)
+    H = 2
+    N = math.prod(ws)
+    rpb = torch.randn(H, N, N, device="cuda")
+    geo = kernels.grid_geo(B, S, ws, sh, 32 * H, H)
+    tab, _ = kernels._window_bias(rpb, None, geo)
+    _, tabT = kernels._window_bias(rpb, None, geo, transposed=True, plain=False)
+    npad = -(-N // 32) * 32
+    tab = tab.view(-1, H, npad, npad).cpu()
+    tabT = tabT.view(-1, H, npad, npad).cpu()
+    assert torch.equal(tabT, tab.transpose(-1, -2))
+    if any(v > 0 for v in sh):
+        _, reg, _, wt = _kernel_maps(B, S, ws, sh)
+        reg, wt = reg.cpu(), wt.cpu()
+    else:
+        reg, wt = torch.zeros(1, N, dtype=torch.int32), torch.zeros(1, dtype=torch.int32)
+    for t in range(tab.shape[0]):
+        w = int((wt == t).nonzero()[0, 0])
+        m = torch.where(reg[w][:, None] != reg[w][None, :], -100.0, 0.0)
+        want = ((rpb.cpu() + m) * LOG2E).to(torch.bfloat16)
+        assert torch.equal(tab[t, :, :N, :N], want), f"type {t}"
+        assert (tab[t, :, N:, :].float() < -1e29).all() and (tab[t, :, :N, N:].float() < -1e29).all()
+
+
 def test_c3_stage1_grid_forward_vs_oracle():
     """Grid-mode window attention at the C3 stage-1 shape (64^3 tokens, C = 96, 3 heads, window 7, shift 3,
     padded to 70^3) against the oracle's explicit pad/roll/partition path, B = 1. bf16 MFMA: rel-L2 <= 2e-2,
