@@ -50,8 +50,8 @@ extern "C" {
  * 4: lci_conv3_wgrad writes one partial per voxel split instead of one per split and wave; 5: lci_linear_wgrad;
  * 6: lci_hyena_filter; 7: lci_upsample2x; 8: lci_gelu;
  * 9: lci_layernorm_add_fwd; 10: lci_upsample2x_nhwc; 11: lci_fftconv Su; 12: lci_upsample3d_cl_fwd,
- * lci_resample1d_adj and the round-3 entry points below; 13: lci_conv3_fwd_split, lci_window_bias with either
- * table optional). */
+ * lci_resample1d_adj and the round-3 entry points below; 13: lci_conv3_fwd_split, lci_conv3_pack_weight,
+ * lci_window_bias with either table optional). */
 #define LCI_ABI_VERSION 13
 const char* lci_last_error(void);
 int lci_abi_version(void);
@@ -128,6 +128,10 @@ int lci_conv3_fwd(const void* x, const void* w, void* y, int B, int D, int H, in
  * (deterministic). nsplit = lci_conv3_fwd_splits(B*D*H*W, Cin, Cout, KD) (1: use lci_conv3_fwd); Cin % 32 == 0;
  * y and part 16-byte aligned. */
 int lci_conv3_fwd_splits(long long V, int Cin, int Cout, int KD);
+/* The kernels' weight operands from the f32 parameter w (Cout, Cin, KD*3*3) (nn.Conv layout), one pass:
+ * mode 0: (Cout, T, Cin) bf16 for lci_conv3_fwd; mode 1: (Cin_pad, T, Cout) bf16 = w[n][c][T-1-t] (the flipped,
+ * transposed weight of the data gradient), rows c >= Cin zero. */
+int lci_conv3_pack_weight(const float* w, void* out, int Cout, int Cin, int KD, int mode, int Cin_pad, void* stream);
 int lci_conv3_fwd_split(const void* x, const void* w, void* y, float* part, int nsplit, int B, int D, int H, int W,
                         int Cin, int Cout, int KD, void* stream);
 /* Weight gradient: part (lci_conv3_wgrad_splits(B*D*H*W, Cin, Cout, KD), KD*9, Cout, Cin) f32 <- per-voxel-split

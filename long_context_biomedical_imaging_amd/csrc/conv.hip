@@ -449,6 +449,36 @@ __global__ __launch_bounds__(256) void conv3_sum_kernel(const float* __restrict_
   }
 }
 
+// Weight packing, one pass from the f32 parameter w (Cout, Cin, T) (T = KD * 9 taps, PyTorch's layout):
+//   mode 0 (forward):       out (Cout, T, Cin) bf16 = w[n][c][t]
+//   mode 1 (data gradient): out (Cin_pad, T, Cout) bf16 = w[n][c][T - 1 - t], rows c >= Cin zero
+// A workgroup transposes one 64-wide block of the contiguous (c, t) or (n, t) rows through LDS, so both the f32
+// reads and the bf16 writes are whole rows (autocast cast + permute [+ flip] were 2-3 separate torch copies:
+// 1.4 ms per C3 step at the 1536-channel convs of the 4^3 / 8^3 stages).
+__global__ __launch_bounds__(256) void conv3_pack_kernel(const float* __restrict__ w, bf16* __restrict__ out,
+                                                         int Cout, int Cin, int Cin_pad, int T, int mode) {
+  __shared__ float s[64 * 28];
+  const int tid = threadIdx.x;
+  const int row = blockIdx.x;              // mode 0: n; mode 1: c (< Cin_pad)
+  const int j0 = blockIdx.y * 64;          // mode 0: c block; mode 1: n block
+  const int J = mode == 0 ? Cin : Cout;    // extent of the blocked index
+  for (int e = tid; e < 64 * T; e += 256) {
+    const int jj = e / T, t = e - jj * T, j = j0 + jj;
+    float v = 0.f;
+    if (j < J) {
+      if (mode == 0) v = w[((long long)row * Cin + j) * T + t];
+      else if (row < Cin) v = w[((long long)j * Cin + row) * T + (T - 1 - t)];
+    }
+    s[jj * 28 + t] = v;
+  }
+  __syncthreads();
+  const int Jo = mode == 0 ? Cin : Cout;   // contiguous output extent
+  for (int e = tid; e < 64 * T; e += 256) {
+    const int t = e / 64, jj = e - t * 64, j = j0 + jj;
+    if (j < Jo) out[((long long)row * T + t) * Jo + j] = to_bf16(s[jj * 28 + t]);
+  }
+}
+
 // Generic path (any Cin, e.g. the 1-channel image into encoder1): K = T * Cin flattened and zero-padded to
 // 16; each lane gathers its 8 k-values element by element. Only used for tiny Cin, where K is small.
 template <int NT>
@@ -1010,6 +1040,18 @@ extern "C" int lci_conv3_fwd_splits(long long V, int Cin, int Cout, int KD) {
 extern "C" int lci_conv3_fwd_split(const void* x, const void* w, void* y, float* part, int nsplit, int B, int D, int H,
                                    int W, int Cin, int Cout, int KD, void* stream) {
   return conv3_fwd_impl(x, w, y, part, nsplit, B, D, H, W, Cin, Cout, KD, stream);
+}
+
+extern "C" int lci_conv3_pack_weight(const float* w, void* out, int Cout, int Cin, int KD, int mode, int Cin_pad,
+                                     void* stream) {
+  LCI_CHECK(Cout > 0 && Cin > 0 && (KD == 1 || KD == 3) && (mode == 0 || mode == 1), "conv3_pack: bad arguments");
+  LCI_CHECK(mode == 0 || Cin_pad >= Cin, "conv3_pack: Cin_pad (%d) < Cin (%d)", Cin_pad, Cin);
+  const int T = KD * 9;
+  const int rows = mode == 0 ? Cout : Cin_pad, J = mode == 0 ? Cin : Cout;
+  hipLaunchKernelGGL(conv3_pack_kernel, dim3((unsigned)rows, (unsigned)((J + 63) / 64)), dim3(256), 0,
+                     (hipStream_t)stream, w, (bf16*)out, Cout, Cin, mode == 0 ? Cin : Cin_pad, T, mode);
+  LCI_LAUNCH_CHECK();
+  return 0;
 }
 
 // Voxel (gapped-row) splits: up to 2^17 rows per workgroup, fewer (>= 1024) when that leaves under ~2048 workgroups

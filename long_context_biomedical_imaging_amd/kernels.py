@@ -1191,6 +1191,18 @@ def conv3_wgrad_cl(x_cl: torch.Tensor, dy_cl: torch.Tensor, kd: int) -> torch.Te
     _lib.require_gpu(x_cl, dy_cl)
     B, D, H, W, Cin = x_cl.shape
     Cout = dy_cl.shape[-1]
+    if Cin <= 2:
+        # the image into encoder1 (Cin = 1): padding Cin to 32 left 31/32 of the kernel's MFMAs on zeros (0.77 ms at
+        # 128^3); as a GEMM over the (V, taps*Cin) im2col rows it is the token-wise weight gradient instead
+        T = kd * 9
+        pz = 1 if kd == 3 else 0
+        xp = torch.nn.functional.pad(x_cl, (0, 0, 1, 1, 1, 1, pz, pz))
+        cols = [xp[:, a:a + D, b:b + H, c:c + W, :] for a in range(kd) for b in range(3) for c in range(3)]
+        K = -(-(T * Cin) // 32) * 32
+        im = torch.zeros(B * D * H * W, K, device=x_cl.device, dtype=torch.bfloat16)
+        im[:, :T * Cin].view(B, D, H, W, Cin, T).copy_(torch.stack(cols, -1))   # column c * T + tap
+        dw, _ = _wgrad_any(dy_cl.reshape(-1, Cout), im, False)                  # (Cout, K) f32
+        return dw[:, :T * Cin].reshape(Cout, Cin, *((3, 3, 3) if kd == 3 else (3, 3)))
     cp = -(-Cin // 32) * 32
     xp = x_cl if cp == Cin else torch.nn.functional.pad(x_cl, (0, cp - Cin))
     lib = _lib.load()
@@ -1203,13 +1215,34 @@ def conv3_wgrad_cl(x_cl: torch.Tensor, dy_cl: torch.Tensor, kd: int) -> torch.Te
     return g.permute(1, 2, 0).reshape(Cout, Cin, *((3, 3, 3) if kd == 3 else (3, 3)))
 
 
+def _conv3_pack(weight: torch.Tensor, kd: int, mode: int, cin_pad: int) -> torch.Tensor:
+    """bf16 kernel operand of a Conv{2,3}d weight (Cout, Cin, [3,] 3, 3): mode 0 (Cout, T, Cin) for the forward,
+    mode 1 (cin_pad, T, Cout) flipped + transposed for the data gradient (lci_conv3_pack_weight on f32 weights)."""
+    Cout, Cin = weight.shape[:2]
+    T = kd * 9
+    if weight.dtype == torch.float32 and weight.is_cuda:
+        w = weight.detach().contiguous()
+        out = torch.empty((Cout, T, Cin) if mode == 0 else (cin_pad, T, Cout), device=w.device, dtype=torch.bfloat16)
+        _lib.call("lci_conv3_pack_weight", w.data_ptr(), out.data_ptr(), Cout, Cin, kd, mode, cin_pad,
+                  _lib.stream_of(w))
+        return out
+    nd = weight.dim() - 2
+    sp = tuple(range(2, 2 + nd))
+    if mode == 0:
+        return weight.to(torch.bfloat16).permute(0, *sp, 1).reshape(Cout, T, Cin).contiguous()
+    wd = weight.to(torch.bfloat16).flip(sp).permute(1, *sp, 0).reshape(Cin, T, Cout)
+    if cin_pad != Cin:
+        wd = torch.cat([wd, wd.new_zeros(cin_pad - Cin, T, Cout)])
+    return wd.contiguous()
+
+
 class _Conv3(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, nd):
         kd = 3 if nd == 3 else 1
         Cout, Cin = weight.shape[:2]
         x_cl = _to_cl(x, nd)
-        wp = weight.to(torch.bfloat16).permute(0, *range(2, 2 + nd), 1).reshape(Cout, kd * 9, Cin).contiguous()
+        wp = _conv3_pack(weight, kd, 0, Cin)
         y = conv3_cl(x_cl, wp, kd)
         ctx.save_for_backward(x_cl, weight)
         ctx.nd = nd
@@ -1224,12 +1257,9 @@ class _Conv3(torch.autograd.Function):
         dy_cl = _to_cl(dy, nd)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            sp = tuple(range(2, 2 + nd))
-            wd = weight.to(torch.bfloat16).flip(sp).permute(1, *sp, 0).reshape(Cin, kd * 9, Cout)
             cp = -(-Cin // 32) * 32                      # the kernel's Cout multiple: zero rows, sliced off
-            if cp != Cin:
-                wd = torch.cat([wd, wd.new_zeros(cp - Cin, kd * 9, Cout)])
-            dx = conv3_cl(dy_cl, wd.contiguous(), kd)
+            wd = _conv3_pack(weight, kd, 1, cp)
+            dx = conv3_cl(dy_cl, wd, kd)
             dx = _from_cl(dx if cp == Cin else dx[..., :Cin], nd)
         if ctx.needs_input_grad[1]:
             dw = conv3_wgrad_cl(x_cl, dy_cl, kd).to(weight.dtype)

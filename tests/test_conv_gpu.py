@@ -21,6 +21,8 @@ pytestmark = pytest.mark.gpu
     (1, (8, 9, 10), 1, 96),        # encoder1 on the image: generic (Cin % 16 != 0) path
     (2, (1, 33, 47), 64, 32),      # 2-D (D = 1, 9 taps)
     (1, (1, 20, 24), 3, 64),       # 2-D generic
+    (2, (1, 17, 19), 1, 32),       # 2-D Cin = 1: weight gradient as the im2col GEMM
+    (1, (5, 6, 7), 2, 64),         # 3-D Cin = 2: the same
 ])
 def test_conv3_parity(B, S, Cin, Cout):
     torch.manual_seed(0)
@@ -152,3 +154,19 @@ def test_unet_resblock_fused_vs_torch(nd, S, cin, cout):
     _ref_resblock(blk, x.clone()).backward(dy)
     e_g, e_gt = rel_err(g, wr.grad), rel_err(gt, wr.grad)
     assert e_g <= max(1.5 * e_gt, 1e-2), (e_g, e_gt)
+
+
+@pytest.mark.parametrize("Cout,Cin,nd", [(96, 192, 3), (64, 1, 3), (32, 3, 2), (130, 70, 3)])
+def test_conv3_weight_pack(Cout, Cin, nd):
+    """lci_conv3_pack_weight: the forward operand (Cout, T, Cin) and the flipped, transposed data-gradient operand
+    (Cin_pad, T, Cout) equal the torch expressions they replace, bit for bit (one bf16 rounding of the f32 weight)."""
+    torch.manual_seed(4)
+    kd = 3 if nd == 3 else 1
+    w = torch.randn(Cout, Cin, *(3,) * nd, device="cuda")
+    sp = tuple(range(2, 2 + nd))
+    ref0 = w.to(torch.bfloat16).permute(0, *sp, 1).reshape(Cout, kd * 9, Cin)
+    assert torch.equal(kernels._conv3_pack(w, kd, 0, Cin), ref0)
+    cp = -(-Cin // 32) * 32
+    ref1 = w.to(torch.bfloat16).flip(sp).permute(1, *sp, 0).reshape(Cin, kd * 9, Cout)
+    ref1 = torch.cat([ref1, ref1.new_zeros(cp - Cin, kd * 9, Cout)])
+    assert torch.equal(kernels._conv3_pack(w, kd, 1, cp), ref1)
