@@ -51,7 +51,7 @@ extern "C" {
  * 6: lci_hyena_filter; 7: lci_upsample2x; 8: lci_gelu;
  * 9: lci_layernorm_add_fwd; 10: lci_upsample2x_nhwc; 11: lci_fftconv Su; 12: lci_upsample3d_cl_fwd,
  * lci_resample1d_adj and the round-3 entry points below; 13: lci_conv3_fwd_split, lci_conv3_pack_weight,
- * lci_window_bias with either table optional). */
+ * lci_inorm_apply_res, lci_window_bias with either table optional). */
 #define LCI_ABI_VERSION 13
 const char* lci_last_error(void);
 int lci_abi_version(void);
@@ -153,6 +153,11 @@ int lci_inorm_reduce(const void* x, const void* dz, const float* stats, float* p
                      int act, float slope, void* stream);
 int lci_inorm_apply(const void* x, const void* dz, const float* stats, const float* coef, void* out, long long V,
                     int B, int C, int act, float slope, void* stream);
+/* UnetResBlock's tail, lrelu(norm2(x) + r), in one pass with the unfused bf16 roundings: out (B, V, C) bf16 =
+ * bf16(lrelu(bf16(bf16(n) + r))), n = (x - mean) * rstd from stats; r = bf16(norm(y; stats_y)) (the norm3 residual)
+ * when stats_y is given, else y (a bf16 block input). */
+int lci_inorm_apply_res(const void* x, const float* stats, const void* y, const float* stats_y, void* out,
+                        long long V, int B, int C, float slope, void* stream);
 
 /* ------------------------------------------------------------------ Mamba selective scan (d_state 8)
  * Channels-last: u, delta (B, L, Dx); Bm, Cm (B, L, 8) (e.g. column slices of x_proj's output); y (B, L, .).

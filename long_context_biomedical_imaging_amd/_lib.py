@@ -50,6 +50,7 @@ SIGNATURES = {
     "lci_conv3_wgrad": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "lci_inorm_reduce": [_P, _P, _P, _P, _L, _I, _I, _I, _F, _P],
     "lci_inorm_apply": [_P, _P, _P, _P, _P, _L, _I, _I, _I, _F, _P],
+    "lci_inorm_apply_res": [_P, _P, _P, _P, _P, _L, _I, _I, _F, _P],
     "lci_layernorm_fwd": [_P, _P, _P, _P, _I, _P, _P, _L, _I, _F, _P],
     "lci_layernorm_add_fwd": [_P, _P, _I, _P, _P, _P, _P, _I, _P, _P, _L, _I, _F, _P],
     "lci_layernorm_bwd": [_P, _P, _I, _P, _P, _P, _P, _P, _P, _L, _I, _P],

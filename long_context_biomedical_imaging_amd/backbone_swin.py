@@ -419,13 +419,15 @@ class SwinTransformer_with_alt_ops(nn.Module):
         hidden_states_out = [x]
         x0 = self.pos_drop(self.patch_embed(x))
         hidden_states_out += [self.proj_out(x0, normalize)]
-        x1 = self.layers1[0](x0.contiguous())
+        # the reference's x.contiguous() between stages (backbone_swin.py:891-906) is a pure layout copy: the
+        # stages exchange channels-last views here, so each BasicLayer's b c ... -> b ... c permute is free
+        x1 = self.layers1[0](x0)
         hidden_states_out += [self.proj_out(x1, normalize)]
-        x2 = self.layers2[0](x1.contiguous())
+        x2 = self.layers2[0](x1)
         hidden_states_out += [self.proj_out(x2, normalize)]
-        x3 = self.layers3[0](x2.contiguous())
+        x3 = self.layers3[0](x2)
         hidden_states_out += [self.proj_out(x3, normalize)]
-        x4 = self.layers4[0](x3.contiguous())
+        x4 = self.layers4[0](x3)
         hidden_states_out += [self.proj_out(x4, normalize)]
         if self.spatial_dims == 2:
             hidden_states_out = [t.unsqueeze(2) for t in hidden_states_out]

@@ -120,6 +120,33 @@ __global__ __launch_bounds__(256) void inorm_apply_kernel(NormArgs a) {
   *(bf16x8*)(a.out + off) = o;
 }
 
+// UnetResBlock's tail in one pass: out = lrelu(bf16(bf16(norm(x)) + r)), r = bf16(norm(y; stats_y)) (the norm3 /
+// conv3 residual) or y itself (a bf16 block input), with torch's bf16 roundings of the unfused
+// instance_norm -> add -> leaky_relu sequence (each op rounds its output to bf16).
+__global__ __launch_bounds__(256) void inorm_res_kernel(NormArgs a, const bf16* __restrict__ y,
+                                                       const float* __restrict__ stats_y) {
+  const int G = a.C >> 3;
+  const long long e = blockIdx.x * 256LL + threadIdx.x;
+  const int b = blockIdx.y;
+  if (e >= a.V * G) return;
+  const int g = (int)(e % G);
+  const long long off = (long long)b * a.V * a.C + e * 8;
+  const float* st = a.stats + (long long)b * 2 * a.C + 8 * g;
+  float x[8], r[8];
+  load8(a.x + off, x);
+  load8(y + off, r);
+  const float* sy = stats_y ? stats_y + (long long)b * 2 * a.C + 8 * g : nullptr;
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float n = to_f32(to_bf16((x[j] - st[j]) * st[a.C + j]));
+    const float rr = sy ? to_f32(to_bf16((r[j] - sy[j]) * sy[a.C + j])) : r[j];
+    const float sum = to_f32(to_bf16(n + rr));
+    o[j] = to_bf16(sum > 0.f ? sum : sum * a.slope);
+  }
+  *(bf16x8*)(a.out + off) = o;
+}
+
 }  // namespace lci
 
 using namespace lci;
@@ -168,6 +195,21 @@ extern "C" int lci_inorm_apply(const void* x, const void* dz, const float* stats
     hipLaunchKernelGGL(inorm_apply_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, a);
   else
     hipLaunchKernelGGL(inorm_apply_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int lci_inorm_apply_res(const void* x, const float* stats, const void* y, const float* stats_y, void* out,
+                                   long long V, int B, int C, float slope, void* stream) {
+  if (norm_check(V, B, C, x)) return 1;
+  LCI_CHECK(((uintptr_t)out & 15) == 0 && ((uintptr_t)y & 15) == 0, "inorm: misaligned buffers");
+  NormArgs a = {};
+  a.x = (const bf16*)x; a.stats = stats; a.out = (bf16*)out;
+  a.V = V; a.C = C; a.slope = slope;
+  const long long groups = V * (C / 8);
+  LCI_CHECK((groups + 255) / 256 < (1LL << 31), "inorm: volume too large");
+  hipLaunchKernelGGL(inorm_res_kernel, dim3((unsigned)((groups + 255) / 256), B), dim3(256), 0, (hipStream_t)stream,
+                     a, (const bf16*)y, stats_y);
   LCI_LAUNCH_CHECK();
   return 0;
 }

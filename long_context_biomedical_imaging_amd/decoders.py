@@ -168,9 +168,14 @@ class UnetResBlock(nn.Module):
     def forward(self, inp):
         if self.fused and inp.is_cuda and (HIP_CONV_3D if inp.dim() == 5 else HIP_CONV_2D):
             out = kernels.instance_norm_act(self.conv1(inp), True)
-            out = kernels.instance_norm_act(self.conv2(out), False)
-            res = kernels.instance_norm_act(self.conv3(inp), False) if self.downsample else inp
-            return F.leaky_relu(out + res, 0.01)
+            c2 = self.conv2(out)
+            r = self.conv3(inp) if self.downsample else inp
+            # norm2 (+ norm3) + residual add + LeakyReLU in one pass where the operands are bf16 channels-last
+            z = kernels.inorm_add_lrelu(c2, r, self.downsample)
+            if z is not None:
+                return z
+            res = kernels.instance_norm_act(r, False) if self.downsample else r
+            return F.leaky_relu(kernels.instance_norm_act(c2, False) + res, 0.01)
         out = self.lrelu(self.norm1(self.conv1(inp)))
         out = self.norm2(self.conv2(out))
         res = self.norm3(self.conv3(inp)) if self.downsample else inp

@@ -1300,14 +1300,32 @@ def _inorm_sums(x_cl, dz_cl, stats, act):
     return part.double().sum(1)
 
 
+def _inorm_stats(x_cl, act):
+    """(B, 2, C) f32 mean, rstd of a (B, V, C) bf16 tensor over its voxels."""
+    V = x_cl.shape[1]
+    s = _inorm_sums(x_cl, None, None, act) / V
+    mean = s[:, 0]
+    rstd = torch.rsqrt((s[:, 1] - mean * mean).clamp_min(0.0) + INORM_EPS)
+    return torch.stack([mean, rstd], 1).float().contiguous()
+
+
+def _inorm_bwd(x_cl, stats, dz, act):
+    """dx of z = [lrelu](norm(x)) for the upstream gradient dz (B, V, C)."""
+    B, V, C = x_cl.shape
+    dz = dz.to(torch.bfloat16).contiguous()
+    coef = (_inorm_sums(x_cl, dz, stats, act) / V).float().contiguous()
+    dx = torch.empty_like(x_cl)
+    KernelTimer.run("inorm_bwd", 0.0, x_cl, lambda: _lib.call(
+        "lci_inorm_apply", x_cl.data_ptr(), dz.data_ptr(), stats.data_ptr(), coef.data_ptr(), dx.data_ptr(),
+        V, B, C, int(act), LRELU_SLOPE, _lib.stream_of(x_cl)))
+    return dx
+
+
 class _InstanceNormAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x_cl, act):
         B, V, C = x_cl.shape
-        s = _inorm_sums(x_cl, None, None, act) / V
-        mean = s[:, 0]
-        rstd = torch.rsqrt((s[:, 1] - mean * mean).clamp_min(0.0) + INORM_EPS)
-        stats = torch.stack([mean, rstd], 1).float().contiguous()
+        stats = _inorm_stats(x_cl, act)
         z = torch.empty_like(x_cl)
         KernelTimer.run("inorm_fwd", 0.0, x_cl, lambda: _lib.call(
             "lci_inorm_apply", x_cl.data_ptr(), None, stats.data_ptr(), None, z.data_ptr(), V, B, C, int(act),
@@ -1319,14 +1337,55 @@ class _InstanceNormAct(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dz):
         x_cl, stats = ctx.saved_tensors
+        return _inorm_bwd(x_cl, stats, dz, ctx.act), None
+
+
+class _InormAddLrelu(torch.autograd.Function):
+    """lrelu(norm(x) + r) with r = norm(y) (pre_norm) or y, one pass forward (lci_inorm_apply_res); backward: the
+    LeakyReLU mask from the saved output, then the instance-norm backward of each normalised input."""
+
+    @staticmethod
+    def forward(ctx, x_cl, y_cl, pre_norm):
         B, V, C = x_cl.shape
-        dz = dz.to(torch.bfloat16).contiguous()
-        coef = (_inorm_sums(x_cl, dz, stats, ctx.act) / V).float().contiguous()
-        dx = torch.empty_like(x_cl)
-        KernelTimer.run("inorm_bwd", 0.0, x_cl, lambda: _lib.call(
-            "lci_inorm_apply", x_cl.data_ptr(), dz.data_ptr(), stats.data_ptr(), coef.data_ptr(), dx.data_ptr(),
-            V, B, C, int(ctx.act), LRELU_SLOPE, _lib.stream_of(x_cl)))
-        return dx, None
+        sx = _inorm_stats(x_cl, False)
+        sy = _inorm_stats(y_cl, False) if pre_norm else None
+        out = torch.empty_like(x_cl)
+        KernelTimer.run("inorm_fwd", 0.0, x_cl, lambda: _lib.call(
+            "lci_inorm_apply_res", x_cl.data_ptr(), sx.data_ptr(), y_cl.data_ptr(), _lib.ptr(sy), out.data_ptr(),
+            V, B, C, LRELU_SLOPE, _lib.stream_of(x_cl)))
+        ctx.save_for_backward(x_cl, sx, y_cl if pre_norm else None, sy, out)
+        ctx.pre_norm = pre_norm
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x_cl, sx, y_cl, sy, out = ctx.saved_tensors
+        gs = torch.ops.aten.leaky_relu_backward(g.to(torch.bfloat16), out, LRELU_SLOPE, True)
+        dx = _inorm_bwd(x_cl, sx, gs, False)
+        dy = _inorm_bwd(y_cl, sy, gs, False) if ctx.pre_norm else gs
+        return dx, dy, None
+
+
+def _as_cl(x: torch.Tensor):
+    """(B, C, *S) -> (B, V, C) view when x is bf16 with dense channels-last strides, else None."""
+    B, C = x.shape[:2]
+    if x.dtype != torch.bfloat16:
+        return None
+    x_cl = x.movedim(1, -1).reshape(B, -1, C)
+    return x_cl if x_cl.is_contiguous() else None
+
+
+def inorm_add_lrelu(x: torch.Tensor, r: torch.Tensor, r_pre_norm: bool) -> torch.Tensor | None:
+    """UnetResBlock's tail lrelu(norm2(x) + r) (r = norm3(r) when r_pre_norm, else r as is) for bf16 channels-last
+    (B, C, *S) tensors in one pass; None when the operands do not qualify (the caller keeps the unfused ops)."""
+    if not x.is_cuda or x.shape != r.shape or x.shape[1] % 8 or x.shape[1] > 2048:
+        return None
+    xc, rc = _as_cl(x), _as_cl(r)
+    if xc is None or rc is None or xc.data_ptr() % 16 or rc.data_ptr() % 16:
+        return None
+    B, C = x.shape[:2]
+    z = _InormAddLrelu.apply(xc, rc, r_pre_norm)
+    return z.view(B, *x.shape[2:], C).movedim(-1, 1)
 
 
 def instance_norm_act(x: torch.Tensor, act: bool) -> torch.Tensor:

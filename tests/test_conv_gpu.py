@@ -170,3 +170,28 @@ def test_conv3_weight_pack(Cout, Cin, nd):
     ref1 = w.to(torch.bfloat16).flip(sp).permute(1, *sp, 0).reshape(Cin, kd * 9, Cout)
     ref1 = torch.cat([ref1, ref1.new_zeros(cp - Cin, kd * 9, Cout)])
     assert torch.equal(kernels._conv3_pack(w, kd, 1, cp), ref1)
+
+
+@pytest.mark.parametrize("nd,S,cin,cout", [(3, (12, 10, 14), 64, 32), (3, (8, 8, 8), 96, 96), (2, (40, 36), 128, 64)])
+def test_unet_resblock_fused_tail_bit_exact(nd, S, cin, cout, monkeypatch):
+    """lci_inorm_apply_res (norm2 [+ norm3] + residual add + LeakyReLU in one pass) against the unfused kernel +
+    torch sequence it replaces: same bf16 roundings, so output and every gradient are bitwise equal (downsample
+    residual = norm3(conv3(x)); identity residual = the bf16 channels-last block input)."""
+    from long_context_biomedical_imaging_amd.decoders import UnetResBlock
+    torch.manual_seed(3)
+    blk = UnetResBlock(nd, cin, cout, 3, 1).cuda()
+    x = torch.randn(2, cin, *S, device="cuda").bfloat16()
+    x = x.to(memory_format=torch.channels_last_3d if nd == 3 else torch.channels_last)
+    dy = torch.randn(2, cout, *S, device="cuda").bfloat16()
+    outs = []
+    for fused in (True, False):
+        if not fused:
+            monkeypatch.setattr(kernels, "inorm_add_lrelu", lambda *a: None)
+        blk.zero_grad(set_to_none=True)
+        xi = x.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = blk(xi)
+        y.backward(dy)
+        outs.append((y.detach(), xi.grad, blk.conv1.weight.grad, blk.conv2.weight.grad))
+    for name, a, b in zip(("y", "dx", "dW1", "dW2"), outs[0], outs[1]):
+        assert torch.equal(a, b), name

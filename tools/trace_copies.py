@@ -20,27 +20,34 @@ args = list(bench.WORKLOADS[wl])
 for k in ("--height", "--width"):
     if k in args:
         args[args.index(k) + 1] = size
-cfg = lconfig.parse_config(args + ["--batch_size", "2"])
+BATCH = int(os.environ.get("TRACE_BATCH", "2"))
+cfg = lconfig.parse_config(args + ["--batch_size", str(BATCH)])
 dev = torch.device("cuda", 0)
 torch.manual_seed(0)
 model = EncoderDecoderModel(cfg, cfg.encoder_name, cfg.decoder_name, cfg.no_in_channel, cfg.no_out_channel).to(dev)
 ts = TrainStep(model, cfg, dev, ddp=False)
-x, y = bench.synthetic_batch(cfg, 2, dev, seed=0)
+x, y = bench.synthetic_batch(cfg, BATCH, dev, seed=0)
 ts.step(x, y)
 torch.cuda.synchronize()
-with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU], record_shapes=True, with_stack=True) as p:
+acts = [torch.profiler.ProfilerActivity.CPU, torch.profiler.ProfilerActivity.CUDA]
+with torch.profiler.profile(activities=acts, record_shapes=True, with_stack=True) as p:
     ts.step(x, y)
     torch.cuda.synchronize()
-MIN_NUMEL = 1 << 20
+NAMES = set((os.environ.get("TRACE_OPS") or "aten::copy_,aten::clone,aten::contiguous").split(","))
+MIN_NUMEL = int(os.environ.get("TRACE_MIN_NUMEL", 1 << 20))
 agg = collections.Counter()
+tm = collections.Counter()
 for ev in p.events():
-    if ev.name in ("aten::copy_", "aten::clone", "aten::contiguous") and ev.input_shapes and ev.input_shapes[0]:
+    if ev.name in NAMES and ev.input_shapes and ev.input_shapes[0]:
         n = 1
         for d in ev.input_shapes[0]:
             n *= d
         if n < MIN_NUMEL:
             continue
         st = [s for s in (ev.stack or []) if "site-packages" not in s and "torch/" not in s][:5]
-        agg[(ev.name, str(ev.input_shapes[:2]), " <- ".join(st))] += 1
-for (name, shp, st), c in agg.most_common(40):
-    print(f"{c:4d} {name} {shp} | {st}", flush=True)
+        key = (ev.name, str(ev.input_shapes[:2]), " <- ".join(st))
+        agg[key] += 1
+        tm[key] += ev.device_time_total
+for key, t in tm.most_common(50):
+    name, shp, st = key
+    print(f"{t / 1e3:8.3f} ms {agg[key]:4d} {name} {shp} | {st}", flush=True)
