@@ -30,6 +30,14 @@ __device__ __forceinline__ void load8(const bf16* p, float* f) {
   for (int j = 0; j < 8; ++j) f[j] = to_f32(v[j]);
 }
 
+// mean / rstd of 8 consecutive channels (st: the (2, C) stats row of one sample; 32-byte aligned: C % 8 == 0)
+__device__ __forceinline__ void load_stats(const float* st, int C, float* mu, float* rs) {
+  const f32x4 m0 = *(const f32x4*)st, m1 = *(const f32x4*)(st + 4);
+  const f32x4 r0 = *(const f32x4*)(st + C), r1 = *(const f32x4*)(st + C + 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { mu[j] = m0[j]; mu[4 + j] = m1[j]; rs[j] = r0[j]; rs[4 + j] = r1[j]; }
+}
+
 // BWD = false: sums of x and x^2.  BWD = true: sums of dn and dn * n.
 template <bool BWD>
 __global__ __launch_bounds__(256) void inorm_reduce_kernel(NormArgs a) {
@@ -123,6 +131,7 @@ __global__ __launch_bounds__(256) void inorm_apply_kernel(NormArgs a) {
 // UnetResBlock's tail in one pass: out = lrelu(bf16(bf16(norm(x)) + r)), r = bf16(norm(y; stats_y)) (the norm3 /
 // conv3 residual) or y itself (a bf16 block input), with torch's bf16 roundings of the unfused
 // instance_norm -> add -> leaky_relu sequence (each op rounds its output to bf16).
+template <bool PRE>
 __global__ __launch_bounds__(256) void inorm_res_kernel(NormArgs a, const bf16* __restrict__ y,
                                                        const float* __restrict__ stats_y) {
   const int G = a.C >> 3;
@@ -131,16 +140,16 @@ __global__ __launch_bounds__(256) void inorm_res_kernel(NormArgs a, const bf16* 
   if (e >= a.V * G) return;
   const int g = (int)(e % G);
   const long long off = (long long)b * a.V * a.C + e * 8;
-  const float* st = a.stats + (long long)b * 2 * a.C + 8 * g;
-  float x[8], r[8];
+  float x[8], r[8], mu[8], rs[8], muy[8], rsy[8];
   load8(a.x + off, x);
   load8(y + off, r);
-  const float* sy = stats_y ? stats_y + (long long)b * 2 * a.C + 8 * g : nullptr;
+  load_stats(a.stats + (long long)b * 2 * a.C + 8 * g, a.C, mu, rs);   // 8 consecutive channels: f32x4 loads
+  if (PRE) load_stats(stats_y + (long long)b * 2 * a.C + 8 * g, a.C, muy, rsy);
   bf16x8 o;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const float n = to_f32(to_bf16((x[j] - st[j]) * st[a.C + j]));
-    const float rr = sy ? to_f32(to_bf16((r[j] - sy[j]) * sy[a.C + j])) : r[j];
+    const float n = to_f32(to_bf16((x[j] - mu[j]) * rs[j]));
+    const float rr = PRE ? to_f32(to_bf16((r[j] - muy[j]) * rsy[j])) : r[j];
     const float sum = to_f32(to_bf16(n + rr));
     o[j] = to_bf16(sum > 0.f ? sum : sum * a.slope);
   }
@@ -208,8 +217,12 @@ extern "C" int lci_inorm_apply_res(const void* x, const float* stats, const void
   a.V = V; a.C = C; a.slope = slope;
   const long long groups = V * (C / 8);
   LCI_CHECK((groups + 255) / 256 < (1LL << 31), "inorm: volume too large");
-  hipLaunchKernelGGL(inorm_res_kernel, dim3((unsigned)((groups + 255) / 256), B), dim3(256), 0, (hipStream_t)stream,
-                     a, (const bf16*)y, stats_y);
+  LCI_CHECK(((uintptr_t)stats & 15) == 0 && ((uintptr_t)stats_y & 15) == 0, "inorm: misaligned stats");
+  const dim3 grid((unsigned)((groups + 255) / 256), B);
+  if (stats_y)
+    hipLaunchKernelGGL(inorm_res_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, a, (const bf16*)y, stats_y);
+  else
+    hipLaunchKernelGGL(inorm_res_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, a, (const bf16*)y, stats_y);
   LCI_LAUNCH_CHECK();
   return 0;
 }

@@ -1211,7 +1211,7 @@ def conv3_wgrad_cl(x_cl: torch.Tensor, dy_cl: torch.Tensor, kd: int) -> torch.Te
     KernelTimer.run("conv3_wgrad", 2.0 * B * D * H * W * Cout * Cin * kd * 9, x_cl, lambda: _lib.call(
         "lci_conv3_wgrad", xp.data_ptr(), dy_cl.data_ptr(), part.data_ptr(), B, D, H, W, cp, Cout, kd,
         _lib.stream_of(x_cl)))
-    g = part.sum(0)[..., :Cin]                                    # (taps, Cout, Cin)
+    g = (part[0] if ns == 1 else part.sum(0))[..., :Cin]         # (taps, Cout, Cin)
     return g.permute(1, 2, 0).reshape(Cout, Cin, *((3, 3, 3) if kd == 3 else (3, 3)))
 
 

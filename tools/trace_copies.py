@@ -25,6 +25,8 @@ cfg = lconfig.parse_config(args + ["--batch_size", str(BATCH)])
 dev = torch.device("cuda", 0)
 torch.manual_seed(0)
 model = EncoderDecoderModel(cfg, cfg.encoder_name, cfg.decoder_name, cfg.no_in_channel, cfg.no_out_channel).to(dev)
+if os.environ.get("TRACE_CKPT"):
+    model.encoder.checkpoint_blocks = int(os.environ["TRACE_CKPT"])   # per-block activation checkpointing (C5)
 ts = TrainStep(model, cfg, dev, ddp=False)
 x, y = bench.synthetic_batch(cfg, BATCH, dev, seed=0)
 ts.step(x, y)
