@@ -51,7 +51,7 @@ extern "C" {
  * 6: lci_hyena_filter; 7: lci_upsample2x; 8: lci_gelu;
  * 9: lci_layernorm_add_fwd; 10: lci_upsample2x_nhwc; 11: lci_fftconv Su; 12: lci_upsample3d_cl_fwd,
  * lci_resample1d_adj and the round-3 entry points below; 13: lci_conv3_fwd_split, lci_conv3_pack_weight,
- * lci_inorm_apply_res, lci_window_bias with either table optional). */
+ * lci_inorm_apply_res, lci_convup_interleave, lci_window_bias with either table optional). */
 #define LCI_ABI_VERSION 13
 const char* lci_last_error(void);
 int lci_abi_version(void);
@@ -132,6 +132,13 @@ int lci_conv3_fwd_splits(long long V, int Cin, int Cout, int KD);
  * mode 0: (Cout, T, Cin) bf16 for lci_conv3_fwd; mode 1: (Cin_pad, T, Cout) bf16 = w[n][c][T-1-t] (the flipped,
  * transposed weight of the data gradient), rows c >= Cin zero. */
 int lci_conv3_pack_weight(const float* w, void* out, int Cout, int Cin, int KD, int mode, int Cin_pad, void* stream);
+/* Transposed conv with kernel == stride (the UNETR heads' up-sampling, MONAI get_conv_layer(is_transposed=True),
+ * enhance_heads.py:30-356) runs as one GEMM Y (B*D*H*W, taps*C) bf16 (columns tap-major, tap = (a*kh + b)*kw + c);
+ * this moves Y to the channels-last output (B, D*kd, H*kh, W*kw, ld) (rows of ld >= C channels, the C written at the
+ * row start: ld = 2C writes the first half of a channel concatenation) and, adjoint = 1, gathers the output-grid
+ * rows back to Y's layout. C, ld multiples of 8; 16-byte aligned pointers. */
+int lci_convup_interleave(const void* src, void* dst, int B, int D, int H, int W, int kd, int kh, int kw, int C, int ld,
+                          int adjoint, void* stream);
 int lci_conv3_fwd_split(const void* x, const void* w, void* y, float* part, int nsplit, int B, int D, int H, int W,
                         int Cin, int Cout, int KD, void* stream);
 /* Weight gradient: part (lci_conv3_wgrad_splits(B*D*H*W, Cin, Cout, KD), KD*9, Cout, Cin) f32 <- per-voxel-split

@@ -47,6 +47,7 @@ SIGNATURES = {
     "lci_conv3_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "lci_conv3_fwd_split": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "lci_conv3_pack_weight": [_P, _P, _I, _I, _I, _I, _I, _P],
+    "lci_convup_interleave": [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "lci_conv3_wgrad": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "lci_inorm_reduce": [_P, _P, _P, _P, _L, _I, _I, _I, _F, _P],
     "lci_inorm_apply": [_P, _P, _P, _P, _P, _L, _I, _I, _I, _F, _P],

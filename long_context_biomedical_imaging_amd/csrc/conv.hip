@@ -479,6 +479,36 @@ __global__ __launch_bounds__(256) void conv3_pack_kernel(const float* __restrict
   }
 }
 
+// Transposed-conv (kernel == stride) interleave: the up-sampling GEMM's rows Y (B*D*H*W, taps*C) (tap-major columns)
+// moved to the channels-last output grid (B, D*kd, H*kh, W*kw) whose rows have `ld` channels (ld = C, or 2C when the
+// result is written straight into the first half of UnetrUpBlock's torch.cat buffer); adjoint: the output-grid rows
+// gathered back to Y's layout. One thread per (input voxel, tap, 16-byte chunk): both sides are whole 2C-byte rows.
+__global__ __launch_bounds__(256) void convup_interleave_kernel(const bf16* __restrict__ src, bf16* __restrict__ dst,
+                                                                long long n, int D, int H, int W, int kd, int kh,
+                                                                int kw, int C, int ld, int adjoint) {
+  const int CC = C >> 3;                       // 16-byte chunks per row
+  const int taps = kd * kh * kw;
+  const long long stride = (long long)gridDim.x * 256;
+  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n; e += stride) {
+    const int ch = (int)(e % CC);
+    long long q = e / CC;
+    const int t = (int)(q % taps);
+    const long long v = q / taps;              // input voxel (b, z, y, x)
+    const int x = (int)(v % W);
+    long long r = v / W;
+    const int y = (int)(r % H);
+    r /= H;
+    const int z = (int)(r % D);
+    const long long b = r / D;
+    const int a = t / (kh * kw), bb = (t / kw) % kh, c = t % kw;
+    const long long o = (((b * D + z) * kd + a) * ((long long)H * kh) + (long long)y * kh + bb) * ((long long)W * kw) +
+                        (long long)x * kw + c;    // output voxel
+    const long long yoff = (v * taps + t) * C + 8 * ch, ooff = o * ld + 8 * ch;
+    if (adjoint) *(u32x4*)(dst + yoff) = *(const u32x4*)(src + ooff);
+    else *(u32x4*)(dst + ooff) = *(const u32x4*)(src + yoff);
+  }
+}
+
 // Generic path (any Cin, e.g. the 1-channel image into encoder1): K = T * Cin flattened and zero-padded to
 // 16; each lane gathers its 8 k-values element by element. Only used for tiny Cin, where K is small.
 template <int NT>
@@ -1050,6 +1080,18 @@ extern "C" int lci_conv3_pack_weight(const float* w, void* out, int Cout, int Ci
   const int rows = mode == 0 ? Cout : Cin_pad, J = mode == 0 ? Cin : Cout;
   hipLaunchKernelGGL(conv3_pack_kernel, dim3((unsigned)rows, (unsigned)((J + 63) / 64)), dim3(256), 0,
                      (hipStream_t)stream, w, (bf16*)out, Cout, Cin, mode == 0 ? Cin : Cin_pad, T, mode);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int lci_convup_interleave(const void* src, void* dst, int B, int D, int H, int W, int kd, int kh, int kw,
+                                     int C, int ld, int adjoint, void* stream) {
+  LCI_CHECK(B > 0 && D > 0 && H > 0 && W > 0 && kd > 0 && kh > 0 && kw > 0 && C > 0 && C % 8 == 0 && ld >= C &&
+                ld % 8 == 0, "convup_interleave: bad shape (C, ld multiples of 8)");
+  LCI_CHECK(((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0, "convup_interleave: pointers must be 16-byte aligned");
+  const long long n = (long long)B * D * H * W * kd * kh * kw * (C / 8);
+  hipLaunchKernelGGL(convup_interleave_kernel, dim3((unsigned)std::min<long long>((n + 255) / 256, 65536)), dim3(256),
+                     0, (hipStream_t)stream, (const bf16*)src, (bf16*)dst, n, D, H, W, kd, kh, kw, C, ld, adjoint);
   LCI_LAUNCH_CHECK();
   return 0;
 }

@@ -80,7 +80,7 @@ class Conv1x1_2d(nn.Conv2d):
         return _pointwise(x, self.weight, self.bias)
 
 
-def _up_gemm(x, weight, bias, k):
+def _up_gemm(x, weight, bias, k, skip=None):
     """ConvTranspose with kernel == stride: y[.., s*k + i, ..] = sum_c x[.., s, .., c] w[c, :, i..].
 
     One GEMM (V x Cin) . (Cin x prod(k) Cout) with the weight columns ordered (tap, Cout) and the bias added per
@@ -98,23 +98,29 @@ def _up_gemm(x, weight, bias, k):
     bt = bias.repeat(taps) if bias is not None else None
     x2 = x.movedim(1, -1).reshape(-1, Cin)
     y = kernels.linear(x2, wt, bt) if x.is_cuda else F.linear(x2, wt, bt)         # (V, taps * Cout)
+    sk = skip.movedim(1, -1) if skip is not None else None
+    if kernels.convup_interleave_supported(y, Cout, sk):
+        # HIP interleave straight to the channels-last grid (and into the cat buffer with the skip, UnetrUpBlock)
+        return kernels.convup_interleave(y, B, S, k, Cout, sk).movedim(-1, 1)
     y = y.view(B, *S, *k, Cout)
     if nd == 3:
         y = y.permute(0, 1, 4, 2, 5, 3, 6, 7)
     else:
         y = y.permute(0, 1, 3, 2, 4, 5)
     y = y.reshape(B, *(s * kk for s, kk in zip(S, k)), Cout)
-    return y.movedim(-1, 1)
+    y = y.movedim(-1, 1)
+    return torch.cat((y, skip), dim=1) if skip is not None else y
 
 
 class ConvUp(nn.ConvTranspose3d):
-    def forward(self, x):
-        return _up_gemm(x, self.weight, self.bias, self.kernel_size)
+    def forward(self, x, skip=None):
+        """skip given: torch.cat((self(x), skip), dim=1) (UnetrUpBlock) produced in one pass."""
+        return _up_gemm(x, self.weight, self.bias, self.kernel_size, skip)
 
 
 class ConvUp_2d(nn.ConvTranspose2d):
-    def forward(self, x):
-        return _up_gemm(x, self.weight, self.bias, self.kernel_size)
+    def forward(self, x, skip=None):
+        return _up_gemm(x, self.weight, self.bias, self.kernel_size, skip)
 
 
 def _conv(nd, cin, cout, k, s, transposed=False, bias=False):
@@ -203,6 +209,8 @@ class UnetrUpBlock(nn.Module):
         self.conv_block = UnetResBlock(nd, cout + cout, cout, k, 1)
 
     def forward(self, inp, skip):
+        if isinstance(self.transp_conv, (ConvUp, ConvUp_2d)):
+            return self.conv_block(self.transp_conv(inp, skip))   # up-sampling + cat in one pass
         return self.conv_block(torch.cat((self.transp_conv(inp), skip), dim=1))
 
 

@@ -1117,6 +1117,55 @@ def upsample3d_trilinear_cl(x: torch.Tensor, size) -> torch.Tensor:
     return _Upsample3d.apply(x, tuple(int(s) for s in size))
 
 
+# ------------------------------------------------------- transposed-conv (kernel == stride) output interleave
+class _ConvUpInterleave(torch.autograd.Function):
+    """Y (V, taps*C) bf16 -> channels-last (B, D*kd, H*kh, W*kw, C) [cat with `skip` (B, .., Cs) along channels];
+    adjoint: the same rows gathered back (lci_convup_interleave)."""
+
+    @staticmethod
+    def forward(ctx, y2, skip, geo):
+        B, D, H, W, kd, kh, kw, C = geo
+        Cs = skip.shape[-1] if skip is not None else 0
+        out = torch.empty(B, D * kd, H * kh, W * kw, C + Cs, device=y2.device, dtype=torch.bfloat16)
+        KernelTimer.run("convup_interleave", 0.0, y2, lambda: _lib.call(
+            "lci_convup_interleave", y2.data_ptr(), out.data_ptr(), B, D, H, W, kd, kh, kw, C, C + Cs, 0,
+            _lib.stream_of(y2)))
+        if skip is not None:
+            out[..., C:].copy_(skip)
+        ctx.geo, ctx.Cs = geo, Cs
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        B, D, H, W, kd, kh, kw, C = ctx.geo
+        g = g.to(torch.bfloat16).contiguous()
+        dy = torch.empty(B * D * H * W, kd * kh * kw * C, device=g.device, dtype=torch.bfloat16)
+        KernelTimer.run("convup_interleave", 0.0, g, lambda: _lib.call(
+            "lci_convup_interleave", g.data_ptr(), dy.data_ptr(), B, D, H, W, kd, kh, kw, C, C + ctx.Cs, 1,
+            _lib.stream_of(g)))
+        return dy, (g[..., C:] if ctx.Cs else None), None
+
+
+def convup_interleave_supported(y2: torch.Tensor, C: int, skip: torch.Tensor | None = None) -> bool:
+    ok = (y2.is_cuda and y2.dtype == torch.bfloat16 and y2.is_contiguous() and y2.data_ptr() % 16 == 0
+          and C % 8 == 0)
+    if skip is not None:
+        ok = ok and skip.dtype == torch.bfloat16 and skip.shape[-1] % 8 == 0
+    return ok
+
+
+def convup_interleave(y2: torch.Tensor, B: int, S, k, C: int, skip: torch.Tensor | None = None) -> torch.Tensor:
+    """The up-sampling GEMM output y2 (B*prod(S), prod(k)*C) as the channels-last grid (B, *(S*k), C [+ Cs]); with
+    skip (B, *(S*k), Cs) channels-last, torch.cat((up, skip), channels) in the same pass (UnetrUpBlock)."""
+    S3 = list(S) + [1] * (3 - len(S))
+    k3 = list(k) + [1] * (3 - len(k))
+    if len(S) == 2:   # 2-D: (H, W) -> D = 1
+        S3, k3 = [1] + list(S), [1] + list(k)
+    geo = (B, *S3, *k3, C)
+    out = _ConvUpInterleave.apply(y2, skip, geo)
+    return out.view(B, *(s * kk for s, kk in zip(S, k)), -1)
+
+
 # ------------------------------------------------------------------- decoder-head 3x3(x3) convolution
 def conv3_cl(x_cl: torch.Tensor, w_packed: torch.Tensor, kd: int) -> torch.Tensor:
     """x_cl (B, D, H, W, Cin) bf16 channels-last, w_packed (Cout, kd*9, Cin) bf16 -> (B, D, H, W, Cout) bf16."""

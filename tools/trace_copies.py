@@ -47,6 +47,12 @@ for ev in p.events():
         if n < MIN_NUMEL:
             continue
         st = [s for s in (ev.stack or []) if "site-packages" not in s and "torch/" not in s][:5]
+        if not st:   # no Python frames recorded (ROCm builds): the enclosing ops instead
+            par, up = ev.cpu_parent, []
+            while par is not None and len(up) < 4:
+                up.append(par.name)
+                par = par.cpu_parent
+            st = up
         key = (ev.name, str(ev.input_shapes[:2]), " <- ".join(st))
         agg[key] += 1
         tm[key] += ev.device_time_total
