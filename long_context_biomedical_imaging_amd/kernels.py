@@ -1159,8 +1159,10 @@ def convup_interleave(y2: torch.Tensor, B: int, S, k, C: int, skip: torch.Tensor
     skip (B, *(S*k), Cs) channels-last, torch.cat((up, skip), channels) in the same pass (UnetrUpBlock)."""
     S3 = list(S) + [1] * (3 - len(S))
     k3 = list(k) + [1] * (3 - len(k))
-    if len(S) == 2:   # 2-D: (H, W) -> D = 1
+    if len(S) == 2:   # 2-D: (H, W) -> D = 1 (the skip too, as a view, so its gradient keeps its 4-D shape)
         S3, k3 = [1] + list(S), [1] + list(k)
+        if skip is not None:
+            skip = skip.unsqueeze(1)
     geo = (B, *S3, *k3, C)
     out = _ConvUpInterleave.apply(y2, skip, geo)
     return out.view(B, *(s * kk for s, kk in zip(S, k)), -1)

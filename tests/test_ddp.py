@@ -160,3 +160,61 @@ def test_bench_harness_two_ranks_cpu_gloo():
     assert e0 >= 4 * 0.05, "the slow rank's 4 timed steps bound the reported time"
     for a, b in zip(res[0][3], res[1][3]):
         assert (a == b).all()
+
+
+def _rccl_worker(port, q):
+    """One rank on backend "nccl" (= RCCL on ROCm): the DDP gradient all-reduce and bench.timed_steps' barrier /
+    MAX all-reduce run through RCCL itself (world size 1: a one-GPU box cannot host two RCCL ranks)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    import bench
+    from long_context_biomedical_imaging_amd import backbone_vit
+    from long_context_biomedical_imaging_amd.trainer import TrainStep
+    t = torch.arange(1024, device=dev, dtype=torch.float32)
+    dist.all_reduce(t)
+    ok_ar = bool(torch.equal(t, torch.arange(1024, device=dev, dtype=torch.float32)))
+    res = []
+    for ddp in (True, False):
+        torch.manual_seed(0)
+        model = torch.nn.Sequential(backbone_vit.TransformerBlock(False, False, 128, 256, 2),
+                                    backbone_vit.TransformerBlock(False, True, 128, 256, 2)).to(dev)
+        cfg = _cfg()
+        cfg.use_amp = True
+        ts = TrainStep(model, cfg, dev, ddp=ddp)
+        g = torch.Generator().manual_seed(7)
+        x = torch.randn(2, 300, 128, generator=g).to(dev)
+        y = torch.randn(2, 300, 128, generator=g).to(dev)
+        if ddp:
+            elapsed, loss = bench.timed_steps(lambda: ts.step(x, y), 2, 1, 1, dev, 0)
+            dist.barrier()                                     # the harness's N > 1 collectives, on RCCL
+            tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            elapsed = tt.item()
+        else:
+            for _ in range(3):
+                loss = ts.step(x, y)
+        torch.cuda.synchronize()
+        res.append([p.detach().float().cpu().numpy().copy() for p in model.parameters()])
+    q.put((ok_ar, float(loss), float(elapsed), res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_ddp_rccl_backend_gpu():
+    """The N > 1 launch path's collective backend executed on the GPU: DDP over RCCL (world size 1) takes 3 SGD
+    steps (1 warm-up + 2 timed by bench.timed_steps) and must land on the same weights as the same 3 steps without
+    DDP (the all-reduce of one rank is the identity; every kernel on this path is deterministic)."""
+    import numpy as np
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    ok_ar, loss, elapsed, (w_ddp, w_ref) = q.get(timeout=300)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    assert ok_ar and loss == loss and elapsed > 0
+    for a, b in zip(w_ddp, w_ref):
+        np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-7)
