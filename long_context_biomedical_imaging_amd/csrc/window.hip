@@ -17,8 +17,10 @@
 // One workgroup = one (window, head); the whole window's K and V live in LDS; 4 waves x 32-query blocks;
 // S^T = K.Q^T with the query on the MFMA lane, online softmax (lazy exact rescale) over 32-key tiles,
 // O^T += V^T.P^T.
-// Backward: phase 1 (query on lane): dP^T (initial accumulator -delta), dS^T, dQ^T += K^T dS^T, dS tiles for
-//           d(rpb); phase 2 (key on lane, Q/dO in LDS, transposed table): dV^T += dO^T P, dK^T += Q^T dS.
+// Backward (windows of <= 12 key blocks, win_attn_bwd1_kernel): single phase, one wave per key block, query tiles
+//           in a rotation with dQ accumulated in LDS (see the kernel). Larger windows, two phases: phase 1 (query on
+//           lane): dP^T (initial accumulator -delta), dS^T, dQ^T += K^T dS^T, dS tiles for d(rpb); phase 2 (key on
+//           lane, Q/dO in LDS, transposed table): dV^T += dO^T P, dK^T += Q^T dS.
 //           Pad-token dK/dV go to the qkv bias gradient. d(rpb) = sum over windows of dS (reduction kernel).
 #include "common.hpp"
 
@@ -58,6 +60,8 @@ struct WinArgs {
   float* drpb;                             // (H, N, N) f32 (reduction kernel)
   int mode, nd, S[3], ws[3], sh[3], Sp[3], nwin[3];
   int Bw, nW, N, Npad, nqb, nkt, C, H, masked, T;
+  int dS_kl;                               // dS tiles in the key-on-lane layout (win_attn_bwd1_kernel)
+  int bwd1_cnt;                            // win_attn_bwd1_kernel: per-tile dQ order counters instead of a barrier
   float scale, c;
 };
 
@@ -166,6 +170,35 @@ __device__ __forceinline__ void win_stage(const WinArgs& a, const WinLds& L, int
   __syncthreads();
 }
 
+// Runtime-width variant (blockDim.x threads, e.g. one wave per 32-token block): up to 4 row chunks per thread in
+// flight before the LDS writes.
+__device__ __forceinline__ void win_stage_rt(const WinArgs& a, const WinLds& L, int c0, int c1, bool second_is_out,
+                                             const bf16* obase, int w) {
+  const int items = a.Npad * 4, NT = blockDim.x;
+  for (int base = 0; base < items; base += 4 * NT) {
+    bf16x8 r0[4], r1[4];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int idx = base + it * NT + threadIdx.x;
+      if (idx < items) {
+        const int n = idx >> 2, ch = idx & 3;
+        r0[it] = win_load8(a, L.row[n], c0 + ch * 8, n < a.N);
+        r1[it] = win_stage_src1(a, L, n, ch, c1, second_is_out, obase, w);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int idx = base + it * NT + threadIdx.x;
+      if (idx < items) {
+        const int n = idx >> 2, ch = idx & 3;
+        *(bf16x8*)(L.t0 + n * WLD + ch * 8) = r0[it];
+        *(bf16x8*)(L.t1 + n * WLD + ch * 8) = r1[it];
+      }
+    }
+  }
+  __syncthreads();
+}
+
 // window type (index into the bias table)
 __device__ __forceinline__ int win_type(const WinArgs& a, int w) {
   if (a.mode == 0) return a.T > 1 ? w % a.nW : 0;
@@ -242,6 +275,10 @@ __global__ __launch_bounds__(256) void win_bias_kernel(WinArgs a, bf16* bias, bf
 // tables of one head (all window types) stay L2-resident while that head's windows run.
 __device__ __forceinline__ f32x16 win_bias_tile(const bf16* row, int c0) {
   f32x16 r;
+#ifdef LCI_WIN_DIAG_NOBIAS   // timing diagnostic only (wrong results): no table reads
+  for (int i = 0; i < 16; ++i) r[i] = 0.f;
+  return r;
+#endif
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const u32x2 v = *(const u32x2*)(row + c0 + 8 * g);
@@ -260,14 +297,17 @@ __device__ __forceinline__ bf16x8 scaled8(bf16x8 v, float c) {
 }
 
 // --------------------------------------------------------------------------------------------- forward
+// NW = 0: one wave per 32-query block (blockDim.x = nqb * 64 <= 1024), no block left over for a second pass
 template <int NW>
-__global__ __launch_bounds__(NW * 64) void win_attn_fwd_kernel(WinArgs a) {
+__global__ __launch_bounds__(NW ? NW * 64 : 1024) void win_attn_fwd_kernel(WinArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int w = blockIdx.x, hh = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5;
+  const int nw = NW ? NW : (int)(blockDim.x >> 6);
   WinLds L;
   win_setup(a, smem, L, w);
-  win_stage<NW * 64>(a, L, a.C + hh * WHD, 2 * a.C + hh * WHD, false, nullptr, w);   // K -> t0, V -> t1
+  if constexpr (NW != 0) win_stage<NW * 64>(a, L, a.C + hh * WHD, 2 * a.C + hh * WHD, false, nullptr, w);   // K, V
+  else win_stage_rt(a, L, a.C + hh * WHD, 2 * a.C + hh * WHD, false, nullptr, w);
   const float c = a.c;
   const bf16* bh = a.bias + ((long long)win_type(a, w) * a.H + hh) * a.Npad * a.Npad;
   bf16x8 qn[2];   // next query block's Q, loaded one block ahead
@@ -279,12 +319,12 @@ __global__ __launch_bounds__(NW * 64) void win_attn_fwd_kernel(WinArgs a) {
     for (int ks = 0; ks < 2; ++ks) qn[ks] = win_load8(a, qrow, hh * WHD + ks * 16 + 8 * half, qv);
   };
   if (wave < a.nqb) load_q(wave);
-  for (int qb = wave; qb < a.nqb; qb += NW) {
+  for (int qb = wave; qb < a.nqb; qb += nw) {
     const int q = qb * 32 + (lane & 31);
     const bool qv = q < a.N;
     const int qrow = qv ? L.row[q] : -2;
     const bf16x8 qf[2] = {scaled8(qn[0], c), scaled8(qn[1], c)};
-    if (qb + NW < a.nqb) load_q(qb + NW);
+    if (qb + nw < a.nqb) load_q(qb + nw);
     const bf16* brow = bh + (long long)q * a.Npad + 4 * half;
     f32x16 o = {};
     float m = 0.f, l = 0.f;
@@ -506,6 +546,253 @@ __global__ __launch_bounds__(NW * 64) void win_attn_bwd_kernel(WinArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------- backward, single phase
+// The two-phase kernel above computes S, dP and the exponentials twice per (query, key) tile (14 MFMAs and 32 exp2
+// per 32 x 32 tile pair) and loads K, V, Q, dO, O rows from global memory inside its loops. Here one wave per key
+// block (NW = nkb <= 12 waves: every 7^3 window) keeps its K / V fragments in registers and takes the query tiles in
+// a rotation, qt = (kb + t) mod nkb at step t, so at every step the waves work on distinct query tiles: per tile
+// S, dP (bias^T table tile and -delta as initial accumulators), P, dS, dV^T += dO^T P, dK^T += Q^T dS (10 MFMAs with
+// dQ, 16 exp2), and dQ^T += K^T dS^T with dS transposed through a per-wave LDS scratch tile, added into an f32 dQ
+// accumulator in LDS that this wave owns for the step (one barrier per step; the summation order is fixed by the
+// rotation: deterministic). Q / dO are staged once; delta = rowsum(dO * O) is computed at staging.
+constexpr int DQLD = 36;   // f32 row stride of the LDS dQ accumulator: the b128 RMW of 16 query rows is conflict-free
+constexpr int WBWD1_MAXW = 12;
+__global__ __launch_bounds__(WBWD1_MAXW * 64) void win_attn_bwd1_kernel(WinArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int w = blockIdx.x, hh = blockIdx.y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5;
+  const int nkb = a.nkt, NT = blockDim.x;
+  WinLds L;
+  win_setup(a, smem, L, w);                                  // t0, t1, row, rid
+  float* lse_l = (float*)(L.rid + a.Npad);                   // -lse2
+  float* ndl_l = lse_l + a.Npad;                             // -delta
+  float* dq_l = ndl_l + a.Npad;                              // (Npad, DQLD) f32
+  bf16* scr = (bf16*)(dq_l + a.Npad * DQLD) + wave * 32 * WLD;   // this wave's 32 x 32 transpose tile
+  const float c = a.c;
+
+  // Q -> t0, dO -> t1 (padded / cropped queries: dO = 0): Npad * 4 16-byte chunks = exactly 2 per thread,
+  // all four loads in flight before the LDS writes
+  {
+    bf16x8 r0[2], r1[2];
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int idx = it * NT + threadIdx.x, n = idx >> 2, ch = idx & 3;
+      r0[it] = win_load8(a, L.row[n], hh * WHD + ch * 8, n < a.N);
+      r1[it] = win_stage_src1(a, L, n, ch, hh * WHD, true, a.dout, w);
+    }
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int idx = it * NT + threadIdx.x, n = idx >> 2, ch = idx & 3;
+      *(bf16x8*)(L.t0 + n * WLD + ch * 8) = r0[it];
+      *(bf16x8*)(L.t1 + n * WLD + ch * 8) = r1[it];
+    }
+    __syncthreads();
+  }
+  // row constants: lse2 and -delta = -rowsum(dO * O), 4 threads per query row (8 channels each); dQ zeroed
+  const float* lseg = a.lse2 + ((long long)w * a.H + hh) * a.N;
+  for (int it = threadIdx.x; it < a.Npad * 4; it += NT) {   // Npad * 4 is a multiple of 64: whole waves
+    const int n = it >> 2, ch = it & 3;
+    const int row = L.row[n];
+    float dsum = 0.f;
+    if (n < a.N && row != -1) {
+      const bf16x8 ov = *(const bf16x8*)(out_row_ptr(a, a.o, w, n, row) + hh * WHD + ch * 8);
+      const bf16x8 dv8 = *(const bf16x8*)(L.t1 + n * WLD + ch * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dsum = fmaf(to_f32(dv8[j]), to_f32(ov[j]), dsum);
+    }
+    dsum += __shfl_xor(dsum, 1);
+    dsum += __shfl_xor(dsum, 2);
+    if (ch == 0) {
+      lse_l[n] = n < a.N ? -lseg[n] : -1.0e30f;   // -lse2 (the S chain's initial accumulator); padded rows: P = 0
+      ndl_l[n] = -dsum;
+    }
+  }
+  for (int i = threadIdx.x; i < a.Npad * DQLD / 4; i += NT) ((f32x4*)dq_l)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int* cnt = (int*)((bf16*)(dq_l + a.Npad * DQLD) + nkb * 32 * WLD);   // dQ contributions added per query tile
+  if (threadIdx.x < nkb) cnt[threadIdx.x] = 0;
+
+  // this wave's key block: K (prescaled into the exp2 domain) / V as B operands, raw K^T as the dQ A operand
+  const int kb = wave;
+  const int key = kb * 32 + (lane & 31);
+  const bool kv = key < a.N;
+  const int krow = kv ? L.row[key] : -2;
+  bf16x8 kf[2], vf[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const bf16x8 kr = win_load8(a, krow, a.C + hh * WHD + ks * 16 + 8 * half, kv);
+    *(bf16x8*)(scr + (lane & 31) * WLD + ks * 16 + 8 * half) = kr;
+    kf[ks] = scaled8(kr, c);
+    vf[ks] = win_load8(a, krow, 2 * a.C + hh * WHD + ks * 16 + 8 * half, kv);
+  }
+  __syncthreads();   // staging, row constants, dQ zero, K scratch
+  const bf16x8 kt0 = frag_tr<0>(scr, WLD, 0, 0, lane), kt1 = frag_tr<1>(scr, WLD, 0, 0, lane);
+  __builtin_amdgcn_wave_barrier();   // K^T read before the scratch takes dS tiles
+
+  const long long tho = ((long long)win_type(a, w) * a.H + hh) * a.Npad * a.Npad;
+  // bias^T (the log2-domain rpb + mask table) enters the S chain through two MFMAs with an identity A operand:
+  // k index 8h + j of k-step u <-> query 16u + 8h + j, A[q][k] = (query(k) == q), B[k][key] = biasT[key][query(k)]
+  // (16-byte loads, no unpacking); -lse2 and -delta are the S / dP chains' initial accumulators (LDS reads), so
+  // P = exp2(S) with no per-element bias, subtract or unpack VALU.
+  const bf16* brow = a.biasT + tho + (long long)key * a.Npad + 8 * half;
+  bf16x8 ident[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ident[u][j] = to_bf16(16 * u + 8 * half + j == (lane & 31) ? 1.f : 0.f);
+  auto load_bias = [&](int tile, bf16x8 (&bt)[2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) bt[u] = *(const bf16x8*)(brow + tile * 32 + 16 * u);
+  };
+  // S and dP - delta of query tile `tile` (16 x f32 each, query rows, key on the lane)
+  auto chains = [&](int tile, const bf16x8 (&bt)[2], f32x16& sx, f32x16& px) __attribute__((always_inline)) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {   // queries tile*32 + 8g + 4h + j
+      const f32x4 l4 = *(const f32x4*)(lse_l + tile * 32 + 8 * g + 4 * half);
+      const f32x4 d4 = *(const f32x4*)(ndl_l + tile * 32 + 8 * g + 4 * half);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { sx[4 * g + j] = l4[j]; px[4 * g + j] = d4[j]; }
+    }
+    sx = mfma32(ident[0], bt[0], sx);
+    sx = mfma32(ident[1], bt[1], sx);
+    sx = mfma32(frag_row(L.t0, WLD, tile * 32, 0, lane), kf[0], sx);
+    sx = mfma32(frag_row(L.t0, WLD, tile * 32, 16, lane), kf[1], sx);
+    px = mfma32(frag_row(L.t1, WLD, tile * 32, 0, lane), vf[0], px);
+    px = mfma32(frag_row(L.t1, WLD, tile * 32, 16, lane), vf[1], px);
+  };
+  f32x16 dk = {}, dv = {};
+  // The dQ partial of step t is added into the LDS accumulator in step t + 1's interval (every wave delays by one
+  // step, so the tiles touched in one interval are still distinct), and step t + 1's S / dP chains are issued before
+  // step t's barrier: their MFMA latency and the RMW's LDS latency overlap the barrier wait. Steps are separated by a
+  // raw s_barrier behind lgkmcnt(0) only: the bias prefetch and the dS stores stay in flight across it (a
+  // __syncthreads would drain them every step).
+  auto dq_rmw = [&](int tile, const f32x16& part) __attribute__((always_inline)) {
+    float* dqrow = dq_l + (tile * 32 + (lane & 31)) * DQLD + 4 * half;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {   // d = 8g + 4h + j
+      f32x4 v = *(f32x4*)(dqrow + 8 * g);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] += part[4 * g + j];
+      *(f32x4*)(dqrow + 8 * g) = v;
+    }
+  };
+  auto step_barrier = [&]() __attribute__((always_inline)) {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(15 | (3 << 14) | (7 << 4));   // lgkmcnt(0): this wave's LDS accesses are done
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  // Counter mode (default): tile q receives its contributions in step order -- at step t from wave (q - t) mod nkb
+  // -- so the wave holding step t's partial waits until cnt[q] == t, adds, and publishes t + 1. (wave, step) waits
+  // only on (wave + 1, step - 1): no cycle, and the waves drift apart instead of meeting at a barrier every step.
+  auto dq_rmw_ordered = [&](int tile, int order, const f32x16& part) __attribute__((always_inline)) {
+    int spins = 0;
+    while (__hip_atomic_load(cnt + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != order) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1 << 24)) break;   // bound: a logic error must not hang the GPU
+    }
+    asm volatile("" ::: "memory");
+    dq_rmw(tile, part);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(15 | (3 << 14) | (7 << 4));   // lgkmcnt(0): the RMW's LDS writes are done
+    if (lane == 0) __hip_atomic_store(cnt + tile, order + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  int qt = kb;
+  bf16x8 bt[2];
+  load_bias(qt, bt);
+  f32x16 s, dp;
+  chains(qt, bt, s, dp);
+  if (nkb > 1) load_bias(qt + 1 == nkb ? 0 : qt + 1, bt);
+  f32x16 dq_prev = {};
+  int qt_prev = -1;
+  for (int t = 0; t < nkb; ++t) {
+    LCI_WIN_BWD_SCHED();
+    const int qn = qt + 1 == nkb ? 0 : qt + 1;
+    if (t > 0) {   // the previous step's tile
+      if (a.bwd1_cnt) dq_rmw_ordered(qt_prev, t - 1, dq_prev);
+      else dq_rmw(qt_prev, dq_prev);   // this wave's in this interval
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      s[i] = exp2_fast(s[i]);   // P (query rows, key on lane)
+      dp[i] = s[i] * dp[i];     // dS
+    }
+    const bf16x8 p0 = pack8<0>(s), p1 = pack8<1>(s), d0 = pack8<0>(dp), d1 = pack8<1>(dp);
+    dv = mfma32(frag_tr<0>(L.t1, WLD, qt * 32, 0, lane), p0, dv);
+    dv = mfma32(frag_tr<1>(L.t1, WLD, qt * 32, 0, lane), p1, dv);
+    dk = mfma32(frag_tr<0>(L.t0, WLD, qt * 32, 0, lane), d0, dk);
+    dk = mfma32(frag_tr<1>(L.t0, WLD, qt * 32, 0, lane), d1, dk);
+    if (a.dS) {   // tile (qt, kb) in the key-on-lane layout (win_rpb_grad_kernel, dS_kl)
+      bf16* dst = a.dS + ((((long long)w * a.H + hh) * a.nqb + qt) * a.nkt + kb) * 1024 + lane * 16;
+      *(bf16x8*)dst = d0;
+      *(bf16x8*)(dst + 8) = d1;
+    }
+    // dS^T through the scratch tile [key][query]: register r of this lane is query (r&3) + 8(r>>2) + 4h
+    bf16* srow = scr + (lane & 31) * WLD + 4 * half;
+    *(bf16x4*)(srow + 0) = bf16x4{d0[0], d0[1], d0[2], d0[3]};
+    *(bf16x4*)(srow + 8) = bf16x4{d0[4], d0[5], d0[6], d0[7]};
+    *(bf16x4*)(srow + 16) = bf16x4{d1[0], d1[1], d1[2], d1[3]};
+    *(bf16x4*)(srow + 24) = bf16x4{d1[4], d1[5], d1[6], d1[7]};
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    dq_prev = mfma32(kt0, frag_tr<0>(scr, WLD, 0, 0, lane), f32x16{});
+    dq_prev = mfma32(kt1, frag_tr<1>(scr, WLD, 0, 0, lane), dq_prev);   // dQ^T[d][query], query on the lane
+    qt_prev = qt;
+    qt = qn;
+    if (t + 1 < nkb) {
+      chains(qt, bt, s, dp);                                 // next step's chains, ahead of the barrier
+      if (t + 2 < nkb) load_bias(qt + 1 == nkb ? 0 : qt + 1, bt);
+    }
+    if (!a.bwd1_cnt) step_barrier();   // next interval: the RMW of this step's tile
+  }
+  if (a.bwd1_cnt) dq_rmw_ordered(qt_prev, nkb - 1, dq_prev);
+  else dq_rmw(qt_prev, dq_prev);
+  __syncthreads();
+  if (kv && krow >= 0) {
+    bf16* base = a.dqkv + (long long)(a.mode == 0 ? w * a.N + key : krow) * 3 * a.C + hh * WHD;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf16x4 v0, v1;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v0[j] = to_bf16(dk[4 * g + j] * a.scale);
+        v1[j] = to_bf16(dv[4 * g + j]);
+      }
+      *(bf16x4*)(base + a.C + 8 * g + 4 * half) = v0;
+      *(bf16x4*)(base + 2 * a.C + 8 * g + 4 * half) = v1;
+    }
+  }
+  // padded voxels: their k, v are the qkv bias (one atomic per word per wave, as in the two-phase kernel)
+  const bool padk = kv && krow < 0 && a.dbias_pad != nullptr;
+  if (__any(padk)) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float sk = padk ? dk[i] * a.scale : 0.f, sv = padk ? dv[i] : 0.f;
+#pragma unroll
+      for (int o = 16; o >= 1; o >>= 1) {
+        sk += __shfl_xor(sk, o);
+        sv += __shfl_xor(sv, o);
+      }
+      if ((lane & 31) == 0) {
+        const int d = 8 * (i >> 2) + 4 * half + (i & 3);
+        atomicAdd(a.dbias_pad + a.C + hh * WHD + d, sk);
+        atomicAdd(a.dbias_pad + 2 * a.C + hh * WHD + d, sv);
+      }
+    }
+  }
+  // dQ rows (the loop's last barrier ordered every RMW): 16-byte chunks of 8 channels, scaled, bf16
+  for (int it = threadIdx.x; it < a.N * 4; it += NT) {
+    const int n = it >> 2, ch = it & 3;
+    const int row = L.row[n];
+    if (row < 0) continue;   // padded voxel: cropped (its dO, hence dS and dQ, are zero)
+    const f32x4 lo = *(const f32x4*)(dq_l + n * DQLD + ch * 8), hi = *(const f32x4*)(dq_l + n * DQLD + ch * 8 + 4);
+    bf16x8 o8;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { o8[j] = to_bf16(lo[j] * a.scale); o8[j + 4] = to_bf16(hi[j] * a.scale); }
+    *(bf16x8*)(a.dqkv + (long long)(a.mode == 0 ? w * a.N + n : row) * 3 * a.C + hh * WHD + ch * 8) = o8;
+  }
+}
+
 // d(rpb)[h][q][k] = sum_w dS[w][h][q][k]  from the (Bw, H, nqb, nkt, 64, 16) tile layout. A thread owns 8
 // consecutive tile elements (one 16-byte load per window) and sums the windows in a fixed order, 8 loads in flight
 // (the v1 kernel read 2 bytes per lane per window with one load in flight). Deterministic.
@@ -540,8 +827,9 @@ __global__ __launch_bounds__(128) void win_rpb_grad_kernel(WinArgs a) {
     const int kt = t % a.nkt; t /= a.nkt;
     const int qb = t % a.nqb;
     const int hh = t / a.nqb;
-    const int q = qb * 32 + (lane & 31);
-    const int k = kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+    const int r_in = (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);   // accumulator row of element i
+    const int q = qb * 32 + (a.dS_kl ? r_in : (lane & 31));
+    const int k = kt * 32 + (a.dS_kl ? (lane & 31) : r_in);
     if (q < a.N && k < a.N) a.drpb[((long long)hh * a.N + q) * a.N + k] = acc[j];
   }
 }
@@ -654,11 +942,22 @@ extern "C" int lci_window_attn_fwd(const void* qkv, const float* qkv_bias, const
   if (win_fill(a, geo, scale)) return 1;
   if (a.mode == 0 && has_mask) a.T = a.nW;
   a.qkv = (const bf16*)qkv; a.qkv_bias = qkv_bias; a.bias = (const bf16*)bias; a.out = (bf16*)out; a.lse2 = lse2;
-  constexpr int NW = 8;   // 8 waves share the window's K/V: 4 waves per SIMD at 2 workgroups per CU (LDS-bound)
-  (void)hipFuncSetAttribute((const void*)win_attn_fwd_kernel<NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024);
-  hipLaunchKernelGGL(win_attn_fwd_kernel<NW>, dim3(a.Bw, a.H), dim3(NW * 64), win_lds(a, false), (hipStream_t)stream,
-                     a);
+  // 8 waves sharing the window's K/V (LCI_WIN_FWD_NW=0: one wave per query block when the window has <= 16 of
+  // them -- no wave idle in a second pass, but at 114 VGPRs one 11-wave workgroup per CU instead of two 8-wave ones:
+  // stage 1 of C3 0.21-0.23 vs 0.18-0.19 ms, not the default)
+  static const int fwd_nw = getenv("LCI_WIN_FWD_NW") ? atoi(getenv("LCI_WIN_FWD_NW")) : 8;
+  if (fwd_nw == 0 && a.nqb <= 16) {
+    (void)hipFuncSetAttribute((const void*)win_attn_fwd_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    hipLaunchKernelGGL(win_attn_fwd_kernel<0>, dim3(a.Bw, a.H), dim3(a.nqb * 64), win_lds(a, false),
+                       (hipStream_t)stream, a);
+  } else {
+    constexpr int NW = 8;
+    (void)hipFuncSetAttribute((const void*)win_attn_fwd_kernel<NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    hipLaunchKernelGGL(win_attn_fwd_kernel<NW>, dim3(a.Bw, a.H), dim3(NW * 64), win_lds(a, false),
+                       (hipStream_t)stream, a);
+  }
   LCI_LAUNCH_CHECK();
   return 0;
 }
@@ -676,9 +975,21 @@ extern "C" int lci_window_attn_bwd(const void* qkv, const float* qkv_bias, const
   a.dout = (const bf16*)dout; a.lse2 = (float*)lse2; a.dqkv = (bf16*)dqkv; a.dbias_pad = dbias_pad;
   a.dS = (bf16*)dS; a.drpb = drpb;
   hipStream_t s = (hipStream_t)stream;
-  // waves per (window, head) workgroup (LCI_WIN_BWD_WAVES: A/B override)
+  // single-phase kernel for windows of <= 12 key blocks (every 7^3 / 7^2 / 4^3 window; LCI_WIN_BWD1=0: the
+  // two-phase kernel, A/B hook); waves per (window, head) workgroup of the two-phase kernel: LCI_WIN_BWD_WAVES
+  static const int bwd1_env = getenv("LCI_WIN_BWD1") ? atoi(getenv("LCI_WIN_BWD1")) : 1;
   static const int nw_env = getenv("LCI_WIN_BWD_WAVES") ? atoi(getenv("LCI_WIN_BWD_WAVES")) : 4;
-  if (nw_env == 8) {
+  if (bwd1_env && a.nkt <= WBWD1_MAXW) {
+    a.dS_kl = 1;
+    static const int cnt_env = getenv("LCI_WIN_BWD1_CNT") ? atoi(getenv("LCI_WIN_BWD1_CNT")) : 1;
+    a.bwd1_cnt = cnt_env;
+    const size_t lds = (size_t)a.Npad * WLD * 2 * 2 + (size_t)a.Npad * 4 * 4 + (size_t)a.Npad * DQLD * 4 +
+                       (size_t)a.nkt * 32 * WLD * 2 + 64;
+    LCI_CHECK(lds <= 160 * 1024, "window_attn_bwd: %zu B of LDS", lds);
+    (void)hipFuncSetAttribute((const void*)win_attn_bwd1_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    hipLaunchKernelGGL(win_attn_bwd1_kernel, dim3(a.Bw, a.H), dim3(a.nkt * 64), lds, s, a);
+  } else if (nw_env == 8) {
     (void)hipFuncSetAttribute((const void*)win_attn_bwd_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     hipLaunchKernelGGL(win_attn_bwd_kernel<8>, dim3(a.Bw, a.H), dim3(512), win_lds(a, true), s, a);
