@@ -309,7 +309,15 @@ __global__ __launch_bounds__(NW ? NW * 64 : 1024) void win_attn_fwd_kernel(WinAr
   if constexpr (NW != 0) win_stage<NW * 64>(a, L, a.C + hh * WHD, 2 * a.C + hh * WHD, false, nullptr, w);   // K, V
   else win_stage_rt(a, L, a.C + hh * WHD, 2 * a.C + hh * WHD, false, nullptr, w);
   const float c = a.c;
-  const bf16* bh = a.bias + ((long long)win_type(a, w) * a.H + hh) * a.Npad * a.Npad;
+  // bias (rpb + mask, log2 domain) from the key-major table biasT, added by two MFMAs with an identity B operand:
+  // k index 8h + j of k-step u <-> query 16u + 8h + j, A[key][k] = biasT[key][query(k)] (16-byte row loads, no
+  // unpacking), B[k][q] = (query(k) == q). The backward reads the same table.
+  const bf16* bT = a.biasT + ((long long)win_type(a, w) * a.H + hh) * a.Npad * a.Npad;
+  bf16x8 ident[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ident[u][j] = to_bf16(16 * u + 8 * half + j == (lane & 31) ? 1.f : 0.f);
   bf16x8 qn[2];   // next query block's Q, loaded one block ahead
   auto load_q = [&](int qb) {
     const int q = qb * 32 + (lane & 31);
@@ -325,16 +333,24 @@ __global__ __launch_bounds__(NW ? NW * 64 : 1024) void win_attn_fwd_kernel(WinAr
     const int qrow = qv ? L.row[q] : -2;
     const bf16x8 qf[2] = {scaled8(qn[0], c), scaled8(qn[1], c)};
     if (qb + nw < a.nqb) load_q(qb + nw);
-    const bf16* brow = bh + (long long)q * a.Npad + 4 * half;
+    const bf16* brow = bT + (long long)(lane & 31) * a.Npad + qb * 32 + 8 * half;   // + key tile * 32 rows
+    const long long kstride = 32LL * a.Npad;
+    auto ld_bias = [&](int kt, bf16x8 (&bt)[2]) __attribute__((always_inline)) {
+      bt[0] = *(const bf16x8*)(brow + kt * kstride);
+      bt[1] = *(const bf16x8*)(brow + kt * kstride + 16);
+    };
     f32x16 o = {};
     float m = 0.f, l = 0.f;
-    f32x16 b0 = win_bias_tile(brow, 0), b1;   // table tiles two ahead
-    if (a.nkt > 1) b1 = win_bias_tile(brow, 32);
+    bf16x8 b0[2], b1[2];   // table tiles two ahead
+    ld_bias(0, b0);
+    if (a.nkt > 1) ld_bias(1, b1);
     for (int kt = 0; kt < a.nkt; ++kt) {
       LCI_WIN_FWD_SCHED();
-      f32x16 s = b0;
-      b0 = b1;
-      if (kt + 2 < a.nkt) b1 = win_bias_tile(brow, (kt + 2) * 32);
+      f32x16 s = mfma32(b0[0], ident[0], f32x16{});
+      s = mfma32(b0[1], ident[1], s);
+      b0[0] = b1[0];
+      b0[1] = b1[1];
+      if (kt + 2 < a.nkt) ld_bias(kt + 2, b1);
       s = mfma32(frag_row(L.t0, WLD, kt * 32, 0, lane), qf[0], s);
       s = mfma32(frag_row(L.t0, WLD, kt * 32, 16, lane), qf[1], s);
       float m4[4] = {fmaxf(s[0], s[1]), fmaxf(s[2], s[3]), fmaxf(s[4], s[5]), fmaxf(s[6], s[7])};
@@ -936,12 +952,13 @@ extern "C" int lci_window_bias(const float* rpb, const float* mask, void* bias, 
   return 0;
 }
 
-extern "C" int lci_window_attn_fwd(const void* qkv, const float* qkv_bias, const void* bias, int has_mask,
+extern "C" int lci_window_attn_fwd(const void* qkv, const float* qkv_bias, const void* biasT, int has_mask,
                                    void* out, float* lse2, const int* geo, float scale, void* stream) {
   WinArgs a{};
   if (win_fill(a, geo, scale)) return 1;
   if (a.mode == 0 && has_mask) a.T = a.nW;
-  a.qkv = (const bf16*)qkv; a.qkv_bias = qkv_bias; a.bias = (const bf16*)bias; a.out = (bf16*)out; a.lse2 = lse2;
+  LCI_CHECK(biasT && ((uintptr_t)biasT & 15) == 0, "window_attn_fwd: biasT must be a 16-byte aligned table");
+  a.qkv = (const bf16*)qkv; a.qkv_bias = qkv_bias; a.biasT = (const bf16*)biasT; a.out = (bf16*)out; a.lse2 = lse2;
   // 8 waves sharing the window's K/V (LCI_WIN_FWD_NW=0: one wave per query block when the window has <= 16 of
   // them -- no wave idle in a second pass, but at 114 VGPRs one 11-wave workgroup per CU instead of two 8-wave ones:
   // stage 1 of C3 0.21-0.23 vs 0.18-0.19 ms, not the default)
@@ -979,6 +996,7 @@ extern "C" int lci_window_attn_bwd(const void* qkv, const float* qkv_bias, const
   // two-phase kernel, A/B hook); waves per (window, head) workgroup of the two-phase kernel: LCI_WIN_BWD_WAVES
   static const int bwd1_env = getenv("LCI_WIN_BWD1") ? atoi(getenv("LCI_WIN_BWD1")) : 1;
   static const int nw_env = getenv("LCI_WIN_BWD_WAVES") ? atoi(getenv("LCI_WIN_BWD_WAVES")) : 4;
+  LCI_CHECK(biasT && ((uintptr_t)biasT & 15) == 0, "window_attn_bwd: biasT must be a 16-byte aligned table");
   if (bwd1_env && a.nkt <= WBWD1_MAXW) {
     a.dS_kl = 1;
     static const int cnt_env = getenv("LCI_WIN_BWD1_CNT") ? atoi(getenv("LCI_WIN_BWD1_CNT")) : 1;
@@ -989,6 +1007,9 @@ extern "C" int lci_window_attn_bwd(const void* qkv, const float* qkv_bias, const
     (void)hipFuncSetAttribute((const void*)win_attn_bwd1_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     hipLaunchKernelGGL(win_attn_bwd1_kernel, dim3(a.Bw, a.H), dim3(a.nkt * 64), lds, s, a);
+  } else if (!bias) {
+    LCI_CHECK(false, "window_attn_bwd: the two-phase kernel (N > %d or LCI_WIN_BWD1=0) needs the plain table too",
+              WBWD1_MAXW * 32);
   } else if (nw_env == 8) {
     (void)hipFuncSetAttribute((const void*)win_attn_bwd_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);

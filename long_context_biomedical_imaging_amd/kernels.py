@@ -510,17 +510,17 @@ class _WindowAttention(torch.autograd.Function):
         bf = bias.float().contiguous() if bias is not None else None
         mk = mask.float().contiguous() if mask is not None else None
         rp = rpb.float().contiguous()
-        tab, _ = _window_bias(rp, mk, geo)
+        _, tabT = _window_bias(rp, mk, geo, transposed=True, plain=False)   # the key-major table only
         KernelTimer.run("window_attn_fwd", 4.0 * Bw * H * N * N * 32, qkv, lambda: _lib.call(
-            "lci_window_attn_fwd", qkv.data_ptr(), _lib.ptr(bf), tab.data_ptr(), int(mk is not None), out.data_ptr(),
+            "lci_window_attn_fwd", qkv.data_ptr(), _lib.ptr(bf), tabT.data_ptr(), int(mk is not None), out.data_ptr(),
             lse2.data_ptr(), g, float(scale), _lib.stream_of(qkv)))
-        ctx.save_for_backward(qkv, bf, rp, mk, out, lse2, tab)   # the backward reuses the table
+        ctx.save_for_backward(qkv, bf, rp, mk, out, lse2, tabT)   # the backward reuses the table
         ctx.geo, ctx.scale, ctx.has_bias = geo, scale, bias is not None
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        qkv, bf, rp, mk, out, lse2, tab = ctx.saved_tensors
+        qkv, bf, rp, mk, out, lse2, tabT = ctx.saved_tensors
         geo, scale = ctx.geo, ctx.scale
         g = _i32(geo)
         N, C, H = geo[13], geo[14], geo[15]
@@ -535,9 +535,12 @@ class _WindowAttention(torch.autograd.Function):
             n_el = _lib.load().lci_window_dS_elems(g)
             dS = torch.empty(int(n_el), device=qkv.device, dtype=torch.bfloat16)
             drpb = torch.empty(H, N, N, **f32)
-        _, tabT = _window_bias(rp, mk, geo, transposed=True, plain=False)
+        # the plain (query-major) table only for the two-phase kernel: windows of more than 12 key blocks
+        tab = None
+        if -(-N // 32) > 12 or os.environ.get("LCI_WIN_BWD1", "1") == "0":
+            tab, _ = _window_bias(rp, mk, geo)
         KernelTimer.run("window_attn_bwd", 8.0 * Bw * H * N * N * 32, qkv, lambda: _lib.call(
-            "lci_window_attn_bwd", qkv.data_ptr(), _lib.ptr(bf), tab.data_ptr(), tabT.data_ptr(), int(mk is not None),
+            "lci_window_attn_bwd", qkv.data_ptr(), _lib.ptr(bf), _lib.ptr(tab), tabT.data_ptr(), int(mk is not None),
             out.data_ptr(), dout.data_ptr(), lse2.data_ptr(), dqkv.data_ptr(), _lib.ptr(dbias), _lib.ptr(dS),
             _lib.ptr(drpb), g, float(scale), _lib.stream_of(qkv)))
         return dqkv, dbias, drpb, None, None, None

@@ -54,6 +54,7 @@ def _oracle_part1(blk, x, ws_cfg, ss_cfg):
     ((5, 9, 40), (7, 7, 7), (3, 3, 3), 64, 2),     # dims <= window collapse (get_window_size)
     ((9, 20), (7, 7), (3, 3), 64, 2),              # 2-D
     ((16, 16), (8, 8), (0, 0), 96, 3),             # 2-D, window 8, unshifted
+    ((12, 12, 12), (8, 8, 8), (4, 4, 4), 64, 2),   # N = 512 > 384: the two-phase backward kernel, shifted
 ])
 def test_swin_part1_grid_vs_oracle(dims, ws, shift, C, heads):
     from long_context_biomedical_imaging_amd import backbone_swin
