@@ -116,6 +116,46 @@ class TrainStep:
         return loss.detach()
 
 
+class GraphedStep:
+    """A TrainStep captured once into a HIP graph and replayed (HIP graphs instead of a tracing compiler).
+
+    The step (autocast forward, loss, backward, optimizer step, zero_grad) on static input/target buffers is warmed
+    up on a side stream, then captured; `step(x, y)` copies the batch into the static buffers (skipped when they
+    are the same tensors) and replays the graph. Every liblci launch goes to torch's current stream, so the
+    kernels are captured as graph nodes; the per-op host work of the Python modules and autograd (~2000 launches
+    per Swin-tiny step) is paid once at capture. Single process only (no DDP: its all-reduce hooks are not part
+    of the capture here); the optimizer runs with capturable=True (fused Adam / AdamW keep their step on device).
+    """
+
+    def __init__(self, trainer: "TrainStep", inputs, targets, warmup: int = 2):
+        if not isinstance(trainer.model, nn.Module) or isinstance(trainer.model, nn.parallel.DistributedDataParallel):
+            raise ValueError("GraphedStep: single-process TrainStep only")
+        for g in trainer.optim.param_groups:
+            if "capturable" in g:
+                g["capturable"] = True
+        self.trainer = trainer
+        self.inputs, self.targets = inputs, targets
+        side = torch.cuda.Stream(device=inputs.device)
+        side.wait_stream(torch.cuda.current_stream(inputs.device))
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                trainer.step(inputs, targets)
+        torch.cuda.current_stream(inputs.device).wait_stream(side)
+        torch.cuda.synchronize(inputs.device)
+        self.graph = torch.cuda.CUDAGraph()
+        # relaxed: the kernels' one-time launch attributes (hipFuncSetAttribute) are legal during the capture
+        with torch.cuda.graph(self.graph, capture_error_mode="relaxed"):
+            self.loss = trainer.step(inputs, targets)
+
+    def step(self, inputs=None, targets=None):
+        if inputs is not None and inputs is not self.inputs:
+            self.inputs.copy_(inputs)
+        if targets is not None and targets is not self.targets:
+            self.targets.copy_(targets)
+        self.graph.replay()
+        return self.loss
+
+
 def synthetic_batch(config, batch, device, seed):
     """U[0,1) images (B, C, T, H, W) and targets of the task's shape."""
     g = torch.Generator(device="cpu").manual_seed(seed)
