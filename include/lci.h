@@ -52,8 +52,9 @@ extern "C" {
  * 9: lci_layernorm_add_fwd; 10: lci_upsample2x_nhwc; 11: lci_fftconv Su; 12: lci_upsample3d_cl_fwd,
  * lci_resample1d_adj and the round-3 entry points below; 13: lci_conv3_fwd_split, lci_conv3_pack_weight,
  * lci_inorm_apply_res, lci_convup_interleave, lci_window_bias with either table optional; 14: lci_window_attn_fwd
- * takes the transposed table biasT, lci_window_attn_bwd's plain table only for windows of N > 384). */
-#define LCI_ABI_VERSION 14
+ * takes the transposed table biasT, lci_window_attn_bwd's plain table only for windows of N > 384; 15:
+ * lci_window_attn_bwd pad_ws). */
+#define LCI_ABI_VERSION 15
 const char* lci_last_error(void);
 int lci_abi_version(void);
 /* sha256 prefix of the sources the library was built from (build_lib.source_hash); the Python binding refuses a
@@ -96,14 +97,16 @@ int lci_window_bias(const float* rpb, const float* mask, void* bias, void* biasT
 /* biasT: the transposed (key-major) table, 16-byte aligned. */
 int lci_window_attn_fwd(const void* qkv, const float* qkv_bias, const void* biasT, int has_mask, void* out,
                         float* lse2, const int* geo, float scale, void* stream);
-/* dqkv (same layout as qkv) <- dQ/dK/dV; dbias_pad (3C, accumulated) <- dK/dV of padded voxels;
+/* dqkv (same layout as qkv) <- dQ/dK/dV; dbias_pad (3C, accumulated) <- dK/dV of padded voxels, with pad_ws an f32
+ * workspace of lci_window_pad_ws_elems(geo) elements (per-window partials, summed in a fixed order);
  * dS: optional bf16 workspace of lci_window_dS_elems(geo) elements; drpb (H, N, N) f32 written if dS given.
  * biasT required (16-byte aligned); bias (plain table) only read for windows of N > 384 (two-phase kernel), may be
  * null otherwise. */
 int lci_window_attn_bwd(const void* qkv, const float* qkv_bias, const void* bias, const void* biasT, int has_mask,
                         const void* out, const void* dout, const float* lse2, void* dqkv, float* dbias_pad,
-                        void* dS, float* drpb, const int* geo, float scale, void* stream);
+                        float* pad_ws, void* dS, float* drpb, const int* geo, float scale, void* stream);
 long long lci_window_dS_elems(const int* geo);
+long long lci_window_pad_ws_elems(const int* geo);
 /* Index maps of the grid mode (test/inspection entry; same device functions as the kernels), per window w < Bw and
  * window token n < N, int32 (Bw, N): src_row = token row (b, s0, s1[, s2]) flattened that the window token reads
  * and the output scatters to, -1 for a padded voxel (F.pad + roll(-shift) + window_partition, and their inverse);

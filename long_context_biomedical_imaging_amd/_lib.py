@@ -14,7 +14,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_LIB = os.path.join(HERE, "liblci.so")
 LIB_PATH = os.environ.get("LCI_LIB_PATH", DEFAULT_LIB)   # override: kernel-variant A/B runs (no staleness check)
-ABI_VERSION = 14   # include/lci.h LCI_ABI_VERSION
+ABI_VERSION = 15   # include/lci.h LCI_ABI_VERSION
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -33,7 +33,7 @@ SIGNATURES = {
                                _I, _P, _P, _P, _P, _P],
     "lci_window_bias": [_P, _P, _P, _P, _P, _P],
     "lci_window_attn_fwd": [_P, _P, _P, _I, _P, _P, _P, _F, _P],
-    "lci_window_attn_bwd": [_P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P],
+    "lci_window_attn_bwd": [_P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P],
     "lci_window_index_map": [_P, _P, _P, _P, _P, _P],
     "lci_fft_twiddles": [_P, _I, _P],
     "lci_fftconv_spectrum": [_P, _P, _P, _P, _I, _I, _P],
@@ -109,6 +109,8 @@ def load(path: str = LIB_PATH):
                            "rebuild with `python -m long_context_biomedical_imaging_amd.build_lib`")
     lib.lci_window_dS_elems.restype = ctypes.c_longlong
     lib.lci_window_dS_elems.argtypes = [_P]
+    lib.lci_window_pad_ws_elems.restype = ctypes.c_longlong
+    lib.lci_window_pad_ws_elems.argtypes = [_P]
     lib.lci_window_bias_elems.restype = ctypes.c_longlong
     lib.lci_window_bias_elems.argtypes = [_P, _I]
     lib.lci_attn_fwd_ws_bytes.restype = ctypes.c_longlong

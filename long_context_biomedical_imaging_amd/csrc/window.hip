@@ -56,6 +56,7 @@ struct WinArgs {
   bf16* out; const bf16* o; const bf16* dout;
   float* lse2;                             // (Bw, H, N)
   bf16* dqkv; float* dbias_pad;            // bwd
+  float* pad_ws;                           // bwd1: (Bw, H, 64) per-workgroup pad-key dK | dV sums, or null
   bf16* dS;                                // (Bw, H, nqb, nkt, 64, 16) bf16 tiles or null
   float* drpb;                             // (H, N, N) f32 (reduction kernel)
   int mode, nd, S[3], ws[3], sh[3], Sp[3], nwin[3];
@@ -779,8 +780,34 @@ __global__ __launch_bounds__(WBWD1_MAXW * 64) void win_attn_bwd1_kernel(WinArgs 
     }
   }
   // padded voxels: their k, v are the qkv bias (one atomic per word per wave, as in the two-phase kernel)
+  // padded voxels: their k, v are the qkv bias. Sum each wave's padded keys over its 32 key lanes, then the waves in
+  // wave order through LDS (the scratch tiles are dead): one (k | v) x 32 partial per workgroup into pad_ws, summed
+  // over windows by win_pad_reduce_kernel -- deterministic, and no float atomics onto the same 192 addresses from
+  // every boundary window (in the model those serialised at the memory side: 3x the kernel time at C3 stage 1)
   const bool padk = kv && krow < 0 && a.dbias_pad != nullptr;
-  if (__any(padk)) {
+  if (a.pad_ws != nullptr) {
+    float* pw = (float*)(scr);   // this wave's 64 floats
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float sk = padk ? dk[i] * a.scale : 0.f, sv = padk ? dv[i] : 0.f;
+#pragma unroll
+      for (int o = 16; o >= 1; o >>= 1) {
+        sk += __shfl_xor(sk, o);
+        sv += __shfl_xor(sv, o);
+      }
+      if ((lane & 31) == 0) {
+        const int d = 8 * (i >> 2) + 4 * half + (i & 3);
+        pw[d] = sk;
+        pw[32 + d] = sv;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      float acc = 0.f;
+      for (int v = 0; v < nkb; ++v) acc += ((const float*)(scr - wave * 32 * WLD + v * 32 * WLD))[threadIdx.x];
+      a.pad_ws[((long long)w * a.H + hh) * 64 + threadIdx.x] = acc;
+    }
+  } else if (__any(padk)) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       float sk = padk ? dk[i] * a.scale : 0.f, sv = padk ? dv[i] : 0.f;
@@ -807,6 +834,22 @@ __global__ __launch_bounds__(WBWD1_MAXW * 64) void win_attn_bwd1_kernel(WinArgs 
     for (int j = 0; j < 4; ++j) { o8[j] = to_bf16(lo[j] * a.scale); o8[j + 4] = to_bf16(hi[j] * a.scale); }
     *(bf16x8*)(a.dqkv + (long long)(a.mode == 0 ? w * a.N + n : row) * 3 * a.C + hh * WHD + ch * 8) = o8;
   }
+}
+
+// dbias_pad[C | 2C + h*32 + d] += sum_w pad_ws[w][h][k|v, d]: one workgroup per (head, value), windows split over
+// 256 threads and summed in a fixed tree order (deterministic).
+__global__ __launch_bounds__(256) void win_pad_reduce_kernel(WinArgs a) {
+  __shared__ float red[256];
+  const int hh = blockIdx.x >> 6, t = blockIdx.x & 63;
+  float acc = 0.f;
+  for (int w = threadIdx.x; w < a.Bw; w += 256) acc += a.pad_ws[((long long)w * a.H + hh) * 64 + t];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o >= 1; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) a.dbias_pad[(t < 32 ? a.C : 2 * a.C) + hh * WHD + (t & 31)] += red[0];
 }
 
 // d(rpb)[h][q][k] = sum_w dS[w][h][q][k]  from the (Bw, H, nqb, nkt, 64, 16) tile layout. A thread owns 8
@@ -979,17 +1022,20 @@ extern "C" int lci_window_attn_fwd(const void* qkv, const float* qkv_bias, const
   return 0;
 }
 
-// dbias_pad (3C) accumulated (caller zeroes); dS tiles (Bw*H*nqb*nkt*1024 bf16) optional workspace;
+// dbias_pad (3C) accumulated (caller zeroes); pad_ws (lci_window_pad_ws_elems f32) required with dbias_pad;
+// dS tiles (Bw*H*nqb*nkt*1024 bf16) optional workspace;
 // drpb (H, N, N) f32 written when dS and drpb are given.
 extern "C" int lci_window_attn_bwd(const void* qkv, const float* qkv_bias, const void* bias, const void* biasT,
                                    int has_mask, const void* out, const void* dout, const float* lse2, void* dqkv,
-                                   float* dbias_pad, void* dS, float* drpb, const int* geo, float scale,
+                                   float* dbias_pad, float* pad_ws, void* dS, float* drpb, const int* geo,
+                                   float scale,
                                    void* stream) {
   WinArgs a{};
   if (win_fill(a, geo, scale)) return 1;
   if (a.mode == 0 && has_mask) a.T = a.nW;
   a.qkv = (const bf16*)qkv; a.qkv_bias = qkv_bias; a.bias = (const bf16*)bias; a.biasT = (const bf16*)biasT; a.o = (const bf16*)out;
   a.dout = (const bf16*)dout; a.lse2 = (float*)lse2; a.dqkv = (bf16*)dqkv; a.dbias_pad = dbias_pad;
+  LCI_CHECK(!dbias_pad || pad_ws, "window_attn_bwd: dbias_pad needs the pad_ws workspace");
   a.dS = (bf16*)dS; a.drpb = drpb;
   hipStream_t s = (hipStream_t)stream;
   // single-phase kernel for windows of <= 12 key blocks (every 7^3 / 7^2 / 4^3 window; LCI_WIN_BWD1=0: the
@@ -1006,7 +1052,10 @@ extern "C" int lci_window_attn_bwd(const void* qkv, const float* qkv_bias, const
     LCI_CHECK(lds <= 160 * 1024, "window_attn_bwd: %zu B of LDS", lds);
     (void)hipFuncSetAttribute((const void*)win_attn_bwd1_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
+    a.pad_ws = dbias_pad ? pad_ws : nullptr;
     hipLaunchKernelGGL(win_attn_bwd1_kernel, dim3(a.Bw, a.H), dim3(a.nkt * 64), lds, s, a);
+    LCI_LAUNCH_CHECK();
+    if (dbias_pad) hipLaunchKernelGGL(win_pad_reduce_kernel, dim3(a.H * 64), dim3(256), 0, s, a);
   } else if (!bias) {
     LCI_CHECK(false, "window_attn_bwd: the two-phase kernel (N > %d or LCI_WIN_BWD1=0) needs the plain table too",
               WBWD1_MAXW * 32);
@@ -1026,6 +1075,12 @@ extern "C" int lci_window_attn_bwd(const void* qkv, const float* qkv_bias, const
     LCI_LAUNCH_CHECK();
   }
   return 0;
+}
+
+extern "C" long long lci_window_pad_ws_elems(const int* geo) {
+  WinArgs a{};
+  if (win_fill(a, geo, 1.f)) return -1;
+  return (long long)a.Bw * a.H * 64;
 }
 
 extern "C" long long lci_window_dS_elems(const int* geo) {

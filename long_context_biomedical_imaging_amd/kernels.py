@@ -529,6 +529,7 @@ class _WindowAttention(torch.autograd.Function):
         dqkv = torch.empty_like(qkv)
         f32 = dict(device=qkv.device, dtype=torch.float32)
         dbias = torch.zeros(3 * C, **f32) if (ctx.has_bias and ctx.needs_input_grad[1]) else None
+        pad_ws = torch.empty(int(_lib.load().lci_window_pad_ws_elems(g)), **f32) if dbias is not None else None
         want_rpb = ctx.needs_input_grad[2]
         dS = drpb = None
         if want_rpb:
@@ -541,7 +542,8 @@ class _WindowAttention(torch.autograd.Function):
             tab, _ = _window_bias(rp, mk, geo)
         KernelTimer.run("window_attn_bwd", 8.0 * Bw * H * N * N * 32, qkv, lambda: _lib.call(
             "lci_window_attn_bwd", qkv.data_ptr(), _lib.ptr(bf), _lib.ptr(tab), tabT.data_ptr(), int(mk is not None),
-            out.data_ptr(), dout.data_ptr(), lse2.data_ptr(), dqkv.data_ptr(), _lib.ptr(dbias), _lib.ptr(dS),
+            out.data_ptr(), dout.data_ptr(), lse2.data_ptr(), dqkv.data_ptr(), _lib.ptr(dbias), _lib.ptr(pad_ws),
+            _lib.ptr(dS),
             _lib.ptr(drpb), g, float(scale), _lib.stream_of(qkv)))
         return dqkv, dbias, drpb, None, None, None
 

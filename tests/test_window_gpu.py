@@ -35,6 +35,8 @@ def test_window_attention_module_vs_reference(name, ws, use_mask):
 def _oracle_part1(blk, x, ws_cfg, ss_cfg):
     a = blk.attn
     sd = {k: (v.detach().double() if v.is_floating_point() else v).cpu() for k, v in blk.state_dict().items()}
+    sd["attn.qkv.bias"].requires_grad_(True)   # the padded voxels' k / v are this bias: its gradient is checked
+    _oracle_part1.qkv_bias = sd["attn.qkv.bias"]
 
     def attn_fn(win, mask):
         return ow.window_attention(win, mask, sd["attn.qkv.weight"], sd["attn.qkv.bias"], sd["attn.proj.weight"],
@@ -75,6 +77,7 @@ def test_swin_part1_grid_vs_oracle(dims, ws, shift, C, heads):
     out.float().backward(cot.cuda())
     ref.backward(cot.double())
     assert rel_err(xc.grad, xr.grad) < 5e-2, "dx"
+    assert rel_err(blk.attn.qkv.bias.grad, _oracle_part1.qkv_bias.grad) < 5e-2, "d(qkv bias), incl. padded voxels"
 
 
 def test_swin_basic_layer_vs_reference():
