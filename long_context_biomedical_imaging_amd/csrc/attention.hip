@@ -166,13 +166,6 @@ constexpr int FW_NW = 8;
 constexpr int FSLOT = KT * LD_ROW + KT * LD_TR;   // one ring slot: K tile (rows) + V tile (transposed reads)
 constexpr float SAFE_EXP2 = 64.f;
 
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
-__device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
-}
-__device__ __forceinline__ u32x4 bload16(rsrc_t r, int voff, int soff) {
-  return __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
-}
 
 __global__ __launch_bounds__(FW_NW * 64, 1) void attn_fwd2_kernel(AttnArgs a, const float* knorm) {
   __shared__ __attribute__((aligned(16))) bf16 smem[3 * FSLOT];

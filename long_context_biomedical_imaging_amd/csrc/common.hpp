@@ -66,6 +66,16 @@ __device__ __forceinline__ bf16x8 frag_row(const bf16* tile, int ld, int r0, int
   return *(const bf16x8*)(tile + (r0 + (lane & 31)) * ld + c0 + 8 * (lane >> 5));
 }
 
+// Buffer resource over `bytes` bytes from `base` (raw, range-checked: a load whose offset + size exceeds `bytes`
+// returns zeros) and a 16-byte load through it (per-lane 32-bit offset + wave-uniform offset).
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ u32x4 bload16(rsrc_t r, int voff, int soff) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+}
+
 // Combine lane l with lane l^32 (the two halves of a 32x32 MFMA column): one v_permlane32_swap, no LDS.
 __device__ __forceinline__ float wave_max_xor32(float v) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);

@@ -319,26 +319,36 @@ __global__ __launch_bounds__(512) void conv3_fwd_lds2_kernel(ConvArgs a) {
   const int sl0 = SPLIT ? (int)((long long)nslab_all * split / a.nsplit) : 0;
   const int sl1 = SPLIT ? (int)((long long)nslab_all * (split + 1) / a.nsplit) : nslab_all;
   u32x4 vx[NXS], vw[NWS];
+  // x rows through a buffer resource based at the slab's first in-range row (wave-uniform 64-bit arithmetic on the
+  // scalar unit): per-lane offsets are 32-bit, rows before the volume give a negative offset and rows past it one
+  // beyond num_records, both of which the range check reads as zero (no 64-bit address VALU, no branch per load)
+  const int rowb = a.Cin * 2;
+  int xoff[NXS], woff[NWS];
+#pragma unroll
+  for (int i = 0; i < NXS; ++i) {
+    const int q = tid + 512 * i, row = q >> 2, ch = q & 3;
+    xoff[i] = q < XR * 4 ? row * rowb + 16 * ch : 0x7fffffff;   // past XR: out of range, reads 0 (not stored)
+  }
+#pragma unroll
+  for (int i = 0; i < NWS; ++i) {
+    const int q = tid + 512 * i, row = q >> 2, ch = q & 3;   // row = dx * 32NT + n
+    const int dxi = row / (32 * NT), n = row - dxi * 32 * NT;
+    woff[i] = q < 3 * 32 * NT * 4 ? ((n0 + n) * T + dxi) * rowb + 16 * ch : 0x7fffffff;
+  }
+  const rsrc_t rw = make_rsrc(a.w, (uint32_t)((long long)a.Cout * T * rowb));
   auto load = [&](int sl) {
     const int grp = sl / nchunk, c0 = (sl - grp * nchunk) * 32;
     const int dz = (a.KD == 3 ? grp / 3 : 1) - 1, dy = grp % 3 - 1;
     const long long src0 = vg0 + (long long)dz * HW + (long long)dy * a.W - 1;
+    const long long b0 = src0 < 0 ? 0 : src0;
+    const long long left = (a.V - b0) * rowb;
+    const rsrc_t rx = make_rsrc(a.x + b0 * a.Cin + c0, left <= 0 ? 0u : (left > 0x7fffffffLL ? 0x7fffffffu : (uint32_t)left));
+    const int sh = (int)(src0 - b0) * rowb;   // <= 0: rows before the volume
 #pragma unroll
-    for (int i = 0; i < NXS; ++i) {
-      const int q = tid + 512 * i, row = q >> 2, ch = q & 3;
-      const long long u = src0 + row;
-      vx[i] = u32x4{0u, 0u, 0u, 0u};
-      if (q < XR * 4 && u >= 0 && u < a.V) vx[i] = *(const u32x4*)(a.x + u * a.Cin + c0 + 8 * ch);
-    }
+    for (int i = 0; i < NXS; ++i) vx[i] = bload16(rx, xoff[i] == 0x7fffffff ? xoff[i] : xoff[i] + sh, 0);
+    const int wg = (grp * 3 * a.Cin + c0) * 2;
 #pragma unroll
-    for (int i = 0; i < NWS; ++i) {
-      const int q = tid + 512 * i, row = q >> 2, ch = q & 3;   // row = dx * 32NT + n
-      vw[i] = u32x4{0u, 0u, 0u, 0u};
-      if (q < 3 * 32 * NT * 4) {
-        const int dxi = row / (32 * NT), n = row - dxi * 32 * NT;
-        vw[i] = *(const u32x4*)(a.w + ((long long)(n0 + n) * T + grp * 3 + dxi) * a.Cin + c0 + 8 * ch);
-      }
-    }
+    for (int i = 0; i < NWS; ++i) vw[i] = bload16(rw, woff[i] == 0x7fffffff ? woff[i] : woff[i] + wg, 0);
   };
   auto store = [&](int buf) {
     bf16* sX = smem2 + buf * (XBUF + WBUF);
