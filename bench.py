@@ -240,7 +240,9 @@ def run_workload(workload, batch, steps, warmup, rank, world, device, kernel_tim
     if use_graph is None:   # host-bound workloads (many small ops per step); LCI_GRAPH=0/1 overrides
         env = os.environ.get("LCI_GRAPH", "")
         use_graph = env == "1" or (env != "0" and workload in GRAPHED)
-    ckpt = ckpt_blocks if ckpt_blocks is not None else (12 if workload == "vit_mamba_p2_256" else 0)
+    # C5: the first 10 of 12 encoder blocks re-run their forward in the backward (~24 GB of saved activations per
+    # un-checkpointed block at 2^21 tokens; 10 -> 230 GB peak of 288, 12 -> 182 GB; 1770 vs 1819 ms per step)
+    ckpt = ckpt_blocks if ckpt_blocks is not None else (10 if workload == "vit_mamba_p2_256" else 0)
     if ckpt:
         model.encoder.checkpoint_blocks = ckpt   # ~35 GB of saved activations per block at 2^21 tokens
     trainer = TrainStep(model, cfg, device, ddp=world > 1)
@@ -343,7 +345,7 @@ def main():
                     help="skip the Swin 128^3 line that the default (ViT 512^2) run also reports")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--ckpt-blocks", type=int, default=None,
-                    help="checkpoint the first K encoder blocks (default: all 12 for vit_mamba_p2_256, else none)")
+                    help="checkpoint the first K encoder blocks (default: 10 of 12 for vit_mamba_p2_256, else none)")
     ap.add_argument("--no-kernel-timer", action="store_true",
                     help="no per-launch HIP events (rocprofv3 PMC passes); the line then carries no roofline")
     args = ap.parse_args()
