@@ -271,6 +271,10 @@ def run_workload(workload, batch, steps, warmup, rank, world, device, kernel_tim
         kernels.KernelTimer.reset()
         kernels.KernelTimer.enabled = kernel_timer
         for _ in range(2):
+            # a ~0.1 s device-side spin first, so the host has queued the whole step before the GPU reaches it: the
+            # per-launch events then bracket kernel time only, not the GPU idling while the host enqueues (these
+            # steps are host-paced when eager; without it small kernels read 2-3x their rocprofv3 durations)
+            torch.cuda._sleep(250_000_000)
             trainer.step(x, y)
         nk = 2
     else:
