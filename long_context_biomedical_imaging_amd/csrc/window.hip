@@ -276,10 +276,6 @@ __global__ __launch_bounds__(256) void win_bias_kernel(WinArgs a, bf16* bias, bf
 // tables of one head (all window types) stay L2-resident while that head's windows run.
 __device__ __forceinline__ f32x16 win_bias_tile(const bf16* row, int c0) {
   f32x16 r;
-#ifdef LCI_WIN_DIAG_NOBIAS   // timing diagnostic only (wrong results): no table reads
-  for (int i = 0; i < 16; ++i) r[i] = 0.f;
-  return r;
-#endif
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const u32x2 v = *(const u32x2*)(row + c0 + 8 * g);
