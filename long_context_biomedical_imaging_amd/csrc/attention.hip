@@ -33,6 +33,15 @@ constexpr int LD_SW = 96;
 __device__ __forceinline__ int swz(int row, int col) {   // col: element index; 8-element chunks stay whole
   return row * LD_SW + ((((col >> 3) ^ ((row >> 2) & 3)) << 3) | (col & 7));
 }
+// The dK/dV kernel on v_mfma_f32_16x16x32_bf16 reads its Q / dO tiles with the 16x16x32 lane maps (b128 rows: row =
+// lane & 15, chunk = lane >> 4; transposed: 4 rows x 16 columns per 16 lanes), for which the swizzle above leaves
+// 2-way conflicts (PMC: 2.2 extra LDS cycles per LDS instruction, 13 % of the wave cycles stalled on LDS issue).
+// 128-byte rows with the chunk XORed by 2 * ((row >> 1) & 3) are conflict-free for both reads and for the 16-byte
+// staging writes (exhaustive check over the MI355X_MICROARCH.md lane groups), and need no padding.
+constexpr int LD_D16 = 64;
+__device__ __forceinline__ int swz16(int row, int col) {
+  return row * LD_D16 + ((((col >> 3) ^ (((row >> 1) & 3) << 1)) << 3) | (col & 7));
+}
 __device__ __forceinline__ bf16x8 frag_row_sw(const bf16* tile, int r0, int c0, int lane) {
   return *(const bf16x8*)(tile + swz(r0 + (lane & 31), c0 + 8 * (lane >> 5)));
 }
@@ -107,6 +116,14 @@ struct TileRegs {
       const int idx = p * NT + tid;
       const int row = idx >> 3, ch = idx & 7;
       *(u32x4*)(lds + swz(row, ch * 8)) = r[p];
+    }
+  }
+  __device__ __forceinline__ void store_sw16(bf16* lds, int tid) const {   // swz16 layout (dK/dV16 tiles)
+#pragma unroll
+    for (int p = 0; p < PASSES; ++p) {
+      const int idx = p * NT + tid;
+      const int row = idx >> 3, ch = idx & 7;
+      *(u32x4*)(lds + swz16(row, ch * 8)) = r[p];
     }
   }
   __device__ __forceinline__ void store(bf16* lds, int ld, int tid) const {
@@ -635,7 +652,7 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
 template <int NW>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv16_kernel(AttnArgs a) {
   constexpr int NT = NW * 64;
-  constexpr int TILE = 2 * KT * LD_SW;                  // Q tile + dO tile (read by rows and transposed)
+  constexpr int TILE = 2 * KT * LD_D16;                 // Q tile + dO tile (read by rows and transposed)
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * TILE];
   __shared__ __attribute__((aligned(16))) float rowc[2][2][KT];   // [buf][-lse2 | -delta][query]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -691,8 +708,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv16_kernel(AttnAr
   };
   qr.load(qp, a.rs_q, 0, L, tid);
   dr.load(dop, a.rs_do, 0, L, tid);
-  qr.store_sw(smem, tid);
-  dr.store_sw(smem + KT * LD_SW, tid);
+  qr.store_sw16(smem, tid);
+  dr.store_sw16(smem + KT * LD_D16, tid);
   stage_rowc(0, 0, load_rowc(0));
   __syncthreads();
 
@@ -704,7 +721,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv16_kernel(AttnAr
   for (int qt = 0; qt < nqt; ++qt) {
     const int buf = qt & 1;
     const bf16* ql = smem + buf * TILE;
-    const bf16* dl = ql + KT * LD_SW;
+    const bf16* dl = ql + KT * LD_D16;
     float rc_next = 0.f;
     if (qt + 1 < nqt) {
       qr.load(qp, a.rs_q, (qt + 1) * KT, L, tid);
@@ -725,8 +742,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv16_kernel(AttnAr
         nd[qb] = *(const f32x4*)&rowc[buf][1][q0 + 16 * qb + 4 * g];
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-          qa[qb][ks] = *(const bf16x8*)(ql + swz(q0 + 16 * qb + c16, 32 * ks + 8 * g));
-          da[qb][ks] = *(const bf16x8*)(dl + swz(q0 + 16 * qb + c16, 32 * ks + 8 * g));
+          qa[qb][ks] = *(const bf16x8*)(ql + swz16(q0 + 16 * qb + c16, 32 * ks + 8 * g));
+          da[qb][ks] = *(const bf16x8*)(dl + swz16(q0 + 16 * qb + c16, 32 * ks + 8 * g));
         }
       }
       f32x4 s[2][2], p[2][2];   // [query block][key block]
@@ -746,8 +763,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv16_kernel(AttnAr
 #pragma unroll
         for (int db = 0; db < 4; ++db) {
           const int col = 16 * db + 4 * (lane & 3);
-          tdo[db] = cat44(lds_tr4(dl + swz(r, col)), lds_tr4(dl + swz(r + 16, col)));
-          tq[db] = cat44(lds_tr4(ql + swz(r, col)), lds_tr4(ql + swz(r + 16, col)));
+          tdo[db] = cat44(lds_tr4(dl + swz16(r, col)), lds_tr4(dl + swz16(r + 16, col)));
+          tq[db] = cat44(lds_tr4(ql + swz16(r, col)), lds_tr4(ql + swz16(r + 16, col)));
         }
       }
 #pragma unroll
@@ -770,8 +787,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv16_kernel(AttnAr
     }
     if (qt + 1 < nqt) {
       bf16* nb = smem + (buf ^ 1) * TILE;
-      qr.store_sw(nb, tid);
-      dr.store_sw(nb + KT * LD_SW, tid);
+      qr.store_sw16(nb, tid);
+      dr.store_sw16(nb + KT * LD_D16, tid);
       stage_rowc(buf ^ 1, qt + 1, rc_next);
     }
     __syncthreads();

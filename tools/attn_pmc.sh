@@ -1,0 +1,16 @@
+#!/bin/bash
+# Wave-cycle accounting of the attention kernels (kernel_bench attention section): two SQ passes, one per run.
+# Usage (GPU box): bash tools/attn_pmc.sh <tag>
+TAG=${1:-apmc}
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp LCI_NO_KTIMER=1
+cd /tmp
+i=0
+for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" \
+           "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE"; do
+  i=$((i+1))
+  timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d $OUT/pmc$i -o run -- python3 $ROOT/tools/kernel_bench.py attention > $OUT/pmc$i.log 2>&1 || exit 1
+done
+echo "attn_pmc $TAG done"
