@@ -168,6 +168,11 @@ __global__ __launch_bounds__(256) void conv3_fwd_kernel(ConvArgs a) {
 // coalesced 16-B loads; fragments then come from LDS (80-B rows). Replaces 3 global fragment loads per voxel
 // block and tap by one staged row set, and shares the weight fragments across the 4 waves.
 constexpr int CLD = 40;   // LDS row stride (elements): 32 channels + 8 pad = 80 B
+// v2 kernel rows: 64 B (no pad) with the 16-byte chunk XORed by (row >> 2) & 3 -- conflict-free for the MFMA fragment
+// reads (b128, lane = row, chunk = 2 ks + h) AND for the 16-byte staging writes, which the 80-B rows left at 8 extra
+// LDS cycles per write (exhaustive bank check, tools/lds_swizzle_check.py patterns)
+constexpr int CLD2 = 32;
+__device__ __forceinline__ int cpos2(int row, int chunk) { return row * CLD2 + ((chunk ^ ((row >> 2) & 3)) << 3); }
 
 template <int NT, int MV>
 __global__ __launch_bounds__(256) void conv3_fwd_lds_kernel(ConvArgs a) {
@@ -280,7 +285,7 @@ __global__ __launch_bounds__(512) void conv3_fwd_lds2_kernel(ConvArgs a) {
   constexpr int ML = 2, NWV = 8;
   constexpr int WV = NWV * 32 * ML;            // 512 voxels
   constexpr int XR = WV + 2;                   // staged rows (dx halo)
-  constexpr int XBUF = XR * CLD, WBUF = 3 * 32 * NT * CLD;
+  constexpr int XBUF = XR * CLD2, WBUF = 3 * 32 * NT * CLD2;
   constexpr int NXS = (XR * 4 + 511) / 512, NWS = (3 * 32 * NT * 4 + 511) / 512;
   extern __shared__ __attribute__((aligned(16))) bf16 smem2[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
@@ -356,12 +361,12 @@ __global__ __launch_bounds__(512) void conv3_fwd_lds2_kernel(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < NXS; ++i) {
       const int q = tid + 512 * i, row = q >> 2, ch = q & 3;
-      if (q < XR * 4) *(u32x4*)(sX + row * CLD + 8 * ch) = vx[i];
+      if (q < XR * 4) *(u32x4*)(sX + cpos2(row, ch)) = vx[i];
     }
 #pragma unroll
     for (int i = 0; i < NWS; ++i) {
       const int q = tid + 512 * i, row = q >> 2, ch = q & 3;
-      if (q < 3 * 32 * NT * 4) *(u32x4*)(sW + row * CLD + 8 * ch) = vw[i];
+      if (q < 3 * 32 * NT * 4) *(u32x4*)(sW + cpos2(row, ch)) = vw[i];
     }
   };
   load(sl0);
@@ -390,10 +395,10 @@ __global__ __launch_bounds__(512) void conv3_fwd_lds2_kernel(ConvArgs a) {
         bf16x8 wa[NT], xb[ML];
 #pragma unroll
         for (int t = 0; t < NT; ++t)
-          wa[t] = *(const bf16x8*)(sW + (dxi * 32 * NT + 32 * t + r) * CLD + 16 * ks + 8 * h);
+          wa[t] = *(const bf16x8*)(sW + cpos2(dxi * 32 * NT + 32 * t + r, 2 * ks + h));
 #pragma unroll
         for (int m = 0; m < ML; ++m) {
-          xb[m] = *(const bf16x8*)(sX + (wave * 32 * ML + 32 * m + r + dxi) * CLD + 16 * ks + 8 * h);
+          xb[m] = *(const bf16x8*)(sX + cpos2(wave * 32 * ML + 32 * m + r + dxi, 2 * ks + h));
           if (!ok[m]) xb[m] = zero8();
         }
 #pragma unroll
@@ -983,7 +988,7 @@ static int launch(const ConvArgs& a, hipStream_t st) {
     b.ntile = a.Cout / (32 * NT);
     b.order = order_env >= 0 ? order_env : (a.Cout >= 96 ? 1 : 0);
     const long long nb = (long long)b.nvb * b.ntile;
-    const size_t sh = (size_t)2 * (514 * CLD + 3 * 32 * NT * CLD) * sizeof(bf16);
+    const size_t sh = (size_t)2 * (514 * CLD2 + 3 * 32 * NT * CLD2) * sizeof(bf16);
     if (a.nsplit > 1) {
       LCI_CHECK(a.part != nullptr, "conv3: split-K needs the partial workspace");
       LCI_CHECK(nb * a.nsplit < (1LL << 31), "conv3: too many workgroups");
