@@ -144,6 +144,12 @@ class WindowAttention(nn.Module):
             self.window_size = window_size
             self.num_heads = num_heads
             head_dim = dim // num_heads
+            if head_dim > kernels.WIN_HEAD_DIM:
+                # csrc/window.hip is built for head_dim 32 (every Swin preset: 96/3 ... 768/24); smaller custom
+                # splits run zero-padded to 32 (kernels.pad_heads, exact), larger ones fail here, not mid-step
+                raise ValueError(f"window attention head_dim {head_dim} (dim {dim} / num_heads {num_heads}) is not "
+                                 f"supported: the HIP window kernels take head_dim <= {kernels.WIN_HEAD_DIM} "
+                                 f"(DESIGN.md §7)")
             self.scale = head_dim ** -0.5
             n_tab = int(np.prod([2 * w - 1 for w in window_size]))
             self.relative_position_bias_table = nn.Parameter(torch.zeros(n_tab, num_heads))

@@ -79,13 +79,13 @@ class SABlock(nn.Module):
             self.drop_output = nn.Dropout(dropout_rate)
             self.drop_weights = nn.Dropout(dropout_rate)
             self.head_dim = hidden_size // num_heads
-            if self.head_dim != ATTN_HEAD_DIM:
+            if self.head_dim > ATTN_HEAD_DIM:
                 # the flash-attention kernels are built for head_dim 64 (every reference preset: small 384/6, base
-                # 768/12); the reference's `custom` preset (backbone_vit.py:78-86) accepts any split, which this
-                # package does not compute (no CPU or torch-math fallback): fail at construction, not mid-step
+                # 768/12); the reference's `custom` preset (backbone_vit.py:78-86) accepts any split: smaller head
+                # dims run zero-padded to 64 (kernels.pad_heads, exact), larger ones fail here, not mid-step
                 raise ValueError(f"attention head_dim {self.head_dim} (hidden_size {hidden_size} / num_heads "
-                                 f"{num_heads}) is not supported: the HIP flash-attention kernels need head_dim "
-                                 f"{ATTN_HEAD_DIM} (DESIGN.md §7)")
+                                 f"{num_heads}) is not supported: the HIP flash-attention kernels take head_dim "
+                                 f"<= {ATTN_HEAD_DIM} (DESIGN.md §7)")
             self.scale = self.head_dim ** -0.5
             self.save_attn = save_attn
             self.att_mat = torch.Tensor()

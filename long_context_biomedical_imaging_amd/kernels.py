@@ -102,15 +102,50 @@ class _FlashAttention(torch.autograd.Function):
         return attn_bwd(qkv, out, dout, lse2, ctx.num_heads, ctx.scale), None, None
 
 
+ATTN_HEAD_DIM = 64   # csrc/attention.hip DH
+WIN_HEAD_DIM = 32    # csrc/window.hip WHD
+
+
+def pad_heads(x: torch.Tensor, parts: int, num_heads: int, to: int) -> torch.Tensor:
+    """(..., parts*H*hd) -> (..., parts*H*to): every head's channels zero-padded from hd to `to` (hd <= to).
+
+    Lets the fixed-head-dim kernels run the reference's `custom` splits with a smaller head dim exactly: zero
+    q / k channels add nothing to q.k, zero v channels give zero output channels (sliced off by unpad_heads), and
+    F.pad's adjoint drops the padded channels' gradients. The softmax scale stays the caller's hd ** -0.5.
+    """
+    lead = x.shape[:-1]
+    hd = x.shape[-1] // (parts * num_heads)
+    return torch.nn.functional.pad(x.reshape(*lead, parts, num_heads, hd), (0, to - hd)).reshape(
+        *lead, parts * num_heads * to)
+
+
+def unpad_heads(o: torch.Tensor, num_heads: int, hd: int) -> torch.Tensor:
+    """(..., H*to) -> (..., H*hd): the first hd channels of every head."""
+    lead = o.shape[:-1]
+    return o.reshape(*lead, num_heads, o.shape[-1] // num_heads)[..., :hd].reshape(*lead, num_heads * hd)
+
+
+def _check_head_dim(hd: int, limit: int, what: str) -> None:
+    if hd > limit:
+        raise ValueError(f"{what} head_dim {hd} is not supported: the HIP kernels take head_dim <= {limit} "
+                         f"(smaller splits run zero-padded to {limit}; DESIGN.md §7)")
+
+
 def flash_attention(qkv: torch.Tensor, num_heads: int, scale: float) -> torch.Tensor:
     """softmax(q k^T * scale) v for the packed qkv projection (B, L, 3*H*dh) -> (B, L, H*dh).
 
     Computes in bf16 MFMA with f32 accumulation and f32 softmax. A non-bf16 qkv (no autocast) is cast to
-    bf16 for the kernel and the result cast back.
+    bf16 for the kernel and the result cast back. dh < 64 runs zero-padded to the kernels' 64 (pad_heads).
     """
+    hd = qkv.shape[-1] // (3 * num_heads)
+    _check_head_dim(hd, ATTN_HEAD_DIM, "attention")
     dt = qkv.dtype
     q = qkv if dt == torch.bfloat16 else qkv.to(torch.bfloat16)
+    if hd < ATTN_HEAD_DIM:
+        q = pad_heads(q, 3, num_heads, ATTN_HEAD_DIM)
     o = _FlashAttention.apply(q.contiguous(), num_heads, scale)
+    if hd < ATTN_HEAD_DIM:
+        o = unpad_heads(o, num_heads, hd)
     return o if dt == torch.bfloat16 else o.to(dt)
 
 
@@ -598,8 +633,15 @@ def window_attention_grid(qkv, bias, rpb, num_heads, scale, window_size, shift_s
     """
     _lib.require_gpu(qkv.contiguous())
     q, dt = _win_prep(qkv)
+    hd = q.shape[-1] // (3 * num_heads)
+    _check_head_dim(hd, WIN_HEAD_DIM, "window attention")
+    if hd < WIN_HEAD_DIM:   # custom Swin splits: zero-padded heads (pad_heads), the padded voxels' bias likewise
+        q = pad_heads(q, 3, num_heads, WIN_HEAD_DIM).contiguous()
+        bias = None if bias is None else pad_heads(bias, 3, num_heads, WIN_HEAD_DIM)
     geo = grid_geo(q.shape[0], q.shape[1:-1], window_size, shift_size, q.shape[-1] // 3, num_heads)
     o = _WindowAttention.apply(q, bias, rpb.float(), None, geo, scale)
+    if hd < WIN_HEAD_DIM:
+        o = unpad_heads(o, num_heads, hd)
     return o if dt == torch.bfloat16 else o.to(dt)
 
 
@@ -668,10 +710,16 @@ def window_attention(qkv, rpb, mask, num_heads, scale):
     """Pre-partitioned windows (WindowAttention.forward signature): qkv (Bw, N, 3C), mask (nW, N, N) or None."""
     _lib.require_gpu(qkv.contiguous())
     q, dt = _win_prep(qkv)
+    hd = q.shape[-1] // (3 * num_heads)
+    _check_head_dim(hd, WIN_HEAD_DIM, "window attention")
+    if hd < WIN_HEAD_DIM:
+        q = pad_heads(q, 3, num_heads, WIN_HEAD_DIM).contiguous()
     Bw, N, C3 = q.shape
     nW = mask.shape[0] if mask is not None else 1
     geo = (0, 0, 1, 1, 1, 1, 1, 1, 0, 0, 0, Bw, nW, N, C3 // 3, num_heads)
     o = _WindowAttention.apply(q, None, rpb.float(), mask, geo, scale)
+    if hd < WIN_HEAD_DIM:
+        o = unpad_heads(o, num_heads, hd)
     return o if dt == torch.bfloat16 else o.to(dt)
 
 

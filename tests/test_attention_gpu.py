@@ -156,3 +156,32 @@ def test_attention_forward_unsafe_and_growing_tiles():
     assert rel_err(out, emu) <= 3e-3, "kernel deviates from the emulation of its own rounding"
     lse_emu = (s.max(-1).values + torch.log2(p.sum(-1))) / 1.4426950408889634
     assert (lse2.cpu() / 1.4426950408889634 - lse_emu).abs().max().item() < 1e-4 * max(1.0, lse.abs().max().item())
+
+
+@pytest.mark.parametrize("hidden,H,L,amp", [(192, 6, 77, True), (192, 4, 300, True), (96, 3, 129, False),
+                                            (320, 5, 64, True)])
+def test_sablock_custom_head_dim(hidden, H, L, amp):
+    """The reference's `custom` ViT preset (backbone_vit.py:78-86) with head_dim 32 / 48 / 64 splits: SABlock runs
+    the smaller heads zero-padded to the kernels' 64 (kernels.pad_heads). Output and input / weight gradients vs
+    the oracle's fp64 SABlock attention (oracle.attention.sablock_attention); bf16 attention core either way."""
+    from long_context_biomedical_imaging_amd import backbone_vit
+    torch.manual_seed(3)
+    m = backbone_vit.SABlock(False, False, hidden, H, qkv_bias=True)
+    with torch.no_grad():
+        m.qkv.bias.normal_(0, 0.2)
+    m = m.cuda()
+    x = torch.randn(2, L, hidden)
+    xc = x.cuda().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+        out = m(xc)
+    sd = {k: v.detach().double().cpu().requires_grad_(True) for k, v in m.state_dict().items()}
+    xr = x.double().requires_grad_(True)
+    ref = oatt.sablock_attention(xr, sd["qkv.weight"], sd["qkv.bias"], sd["out_proj.weight"], sd["out_proj.bias"], H)
+    assert out.shape == ref.shape
+    assert rel_err(out, ref) < 2e-2, "output"
+    cot = torch.randn(ref.shape)
+    out.float().backward(cot.cuda())
+    ref.backward(cot.double())
+    assert rel_err(xc.grad, xr.grad) < 5e-2, "dx"
+    assert rel_err(m.qkv.weight.grad, sd["qkv.weight"].grad) < 5e-2, "d(qkv weight)"
+    assert rel_err(m.qkv.bias.grad, sd["qkv.bias"].grad) < 5e-2, "d(qkv bias)"

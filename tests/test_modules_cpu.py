@@ -109,8 +109,12 @@ def test_flag_surface_and_factories():
         model_base.EncoderDecoderModel(cfg, "Foo", "ViTLinear", 1, 2)
     with pytest.raises(ValueError):
         backbone_vit.SABlock(False, False, 100, 3)
-    with pytest.raises(ValueError, match="head_dim 32"):      # custom preset split the kernels do not cover
-        backbone_vit.SABlock(False, False, 192, 6)
+    backbone_vit.SABlock(False, False, 192, 6)                # custom head_dim 32: zero-padded to the kernels' 64
+    with pytest.raises(ValueError, match="head_dim 128"):     # custom split above the kernels' head dim
+        backbone_vit.SABlock(False, False, 1024, 8)
+    backbone_swin.WindowAttention(False, False, 48, 3, (7, 7, 7))   # head_dim 16: zero-padded to 32
+    with pytest.raises(ValueError, match="head_dim 64"):
+        backbone_swin.WindowAttention(False, False, 128, 2, (7, 7, 7))
     backbone_vit.SABlock(True, False, 192, 6)                 # Hyena / Mamba mixers take any head split
 
 
@@ -190,3 +194,25 @@ def test_separable_psp_ops_match_torch():
             ref.backward(g)
             got.backward(g)
             assert torch.allclose(x2.grad, x.grad, atol=1e-6, rtol=1e-5)
+
+
+def test_head_padding_is_exact():
+    """kernels.pad_heads / unpad_heads (custom head splits below the kernels' head dim): attention over the padded
+    heads equals attention over the original ones (fp64 torch math, the oracle's attention_core), and the pad's
+    adjoint returns exactly the original channels' gradients."""
+    from long_context_biomedical_imaging_amd import kernels
+    from oracle import attention as oatt
+    torch.manual_seed(0)
+    B, L, H, hd = 2, 37, 3, 24
+    qkv = torch.randn(B, L, 3 * H * hd, dtype=torch.float64, requires_grad=True)
+    ref, _ = oatt.attention_core(*oatt.split_qkv(qkv, H), hd ** -0.5)
+    ref = ref.permute(0, 2, 1, 3).reshape(B, L, H * hd)
+    qp = kernels.pad_heads(qkv, 3, H, 64)
+    assert qp.shape == (B, L, 3 * H * 64)
+    op, _ = oatt.attention_core(*oatt.split_qkv(qp, H), hd ** -0.5)
+    op = kernels.unpad_heads(op.permute(0, 2, 1, 3).reshape(B, L, H * 64), H, hd)
+    assert torch.allclose(op, ref, rtol=0, atol=1e-12)
+    g = torch.randn_like(ref)
+    (gr,) = torch.autograd.grad(ref, qkv, g)
+    (gp,) = torch.autograd.grad(op, qkv, g)
+    assert torch.allclose(gp, gr, rtol=0, atol=1e-12)

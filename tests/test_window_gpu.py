@@ -57,6 +57,8 @@ def _oracle_part1(blk, x, ws_cfg, ss_cfg):
     ((9, 20), (7, 7), (3, 3), 64, 2),              # 2-D
     ((16, 16), (8, 8), (0, 0), 96, 3),             # 2-D, window 8, unshifted
     ((12, 12, 12), (8, 8, 8), (4, 4, 4), 64, 2),   # N = 512 > 384: the two-phase backward kernel, shifted
+    ((10, 10, 10), (7, 7, 7), (3, 3, 3), 48, 3),   # custom split, head_dim 16: heads zero-padded to 32
+    ((9, 20), (7, 7), (3, 3), 48, 2),              # custom split, head_dim 24, 2-D
 ])
 def test_swin_part1_grid_vs_oracle(dims, ws, shift, C, heads):
     from long_context_biomedical_imaging_amd import backbone_swin
