@@ -280,7 +280,9 @@ __global__ __launch_bounds__(256) void conv3_fwd_lds_kernel(ConvArgs a) {
 // (the staged weight slab is shared by twice the voxels of v1), and the staging is double-buffered: the next
 // (tap group, 32-channel chunk) slab is loaded into registers while this one's 48 MFMAs per wave run, then written
 // to the other LDS buffer -- one barrier per slab instead of two around an exposed global-load wait.
-template <int NT, bool SPLIT>
+// PF2 = true: the slab loads are issued two slabs ahead into alternating register sets (A / B, the loop unrolled by
+// two), so each load has two slabs of MFMAs (~6k cycles per SIMD) to land before its LDS store instead of one.
+template <int NT, bool SPLIT, bool PF2 = false>
 __global__ __launch_bounds__(512) void conv3_fwd_lds2_kernel(ConvArgs a) {
   constexpr int ML = 2, NWV = 8;
   constexpr int WV = NWV * 32 * ML;            // 512 voxels
@@ -323,7 +325,7 @@ __global__ __launch_bounds__(512) void conv3_fwd_lds2_kernel(ConvArgs a) {
   // this workgroup's slab range (split-K: contiguous ranges of the (tap group, channel chunk) slabs)
   const int sl0 = SPLIT ? (int)((long long)nslab_all * split / a.nsplit) : 0;
   const int sl1 = SPLIT ? (int)((long long)nslab_all * (split + 1) / a.nsplit) : nslab_all;
-  u32x4 vx[NXS], vw[NWS];
+  u32x4 vxA[NXS], vwA[NWS], vxB[NXS], vwB[NWS];
   // x rows through a buffer resource based at the slab's first in-range row (wave-uniform 64-bit arithmetic on the
   // scalar unit): per-lane offsets are 32-bit, rows before the volume give a negative offset and rows past it one
   // beyond num_records, both of which the range check reads as zero (no 64-bit address VALU, no branch per load)
@@ -341,7 +343,7 @@ __global__ __launch_bounds__(512) void conv3_fwd_lds2_kernel(ConvArgs a) {
     woff[i] = q < 3 * 32 * NT * 4 ? ((n0 + n) * T + dxi) * rowb + 16 * ch : 0x7fffffff;
   }
   const rsrc_t rw = make_rsrc(a.w, (uint32_t)((long long)a.Cout * T * rowb));
-  auto load = [&](int sl) {
+  auto load = [&](int sl, u32x4 (&vx)[NXS], u32x4 (&vw)[NWS]) __attribute__((always_inline)) {
     const int grp = sl / nchunk, c0 = (sl - grp * nchunk) * 32;
     const int dz = (a.KD == 3 ? grp / 3 : 1) - 1, dy = grp % 3 - 1;
     const long long src0 = vg0 + (long long)dz * HW + (long long)dy * a.W - 1;
@@ -355,7 +357,7 @@ __global__ __launch_bounds__(512) void conv3_fwd_lds2_kernel(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < NWS; ++i) vw[i] = bload16(rw, woff[i] == 0x7fffffff ? woff[i] : woff[i] + wg, 0);
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, const u32x4 (&vx)[NXS], const u32x4 (&vw)[NWS]) __attribute__((always_inline)) {
     bf16* sX = smem2 + buf * (XBUF + WBUF);
     bf16* sW = sX + XBUF;
 #pragma unroll
@@ -369,13 +371,7 @@ __global__ __launch_bounds__(512) void conv3_fwd_lds2_kernel(ConvArgs a) {
       if (q < 3 * 32 * NT * 4) *(u32x4*)(sW + cpos2(row, ch)) = vw[i];
     }
   };
-  load(sl0);
-  store(0);
-  __syncthreads();
-  int buf = 0;
-  for (int sl = sl0; sl < sl1; ++sl) {
-    const bool more = sl + 1 < sl1;
-    if (more) load(sl + 1);
+  auto compute = [&](int sl, int buf) __attribute__((always_inline)) {
     LCI_CONV_SCHED();
     const int grp = sl / nchunk;
     const int dz = (a.KD == 3 ? grp / 3 : 1) - 1, dy = grp % 3 - 1;
@@ -407,9 +403,36 @@ __global__ __launch_bounds__(512) void conv3_fwd_lds2_kernel(ConvArgs a) {
           for (int m = 0; m < ML; ++m) acc[m][t] = mfma32(wa[t], xb[m], acc[m][t]);
       }
     }
-    if (more) store(buf ^ 1);
+  };
+  load(sl0, vxA, vwA);
+  store(0, vxA, vwA);
+  int buf = 0;
+  if constexpr (PF2) {
+    if (sl0 + 1 < sl1) load(sl0 + 1, vxA, vwA);
     __syncthreads();
-    buf ^= 1;
+    for (int sl = sl0; sl < sl1; sl += 2) {   // entry: set A holds slab sl + 1 (in flight)
+      if (sl + 2 < sl1) load(sl + 2, vxB, vwB);
+      compute(sl, buf);
+      if (sl + 1 < sl1) store(buf ^ 1, vxA, vwA);
+      __syncthreads();
+      buf ^= 1;
+      if (sl + 1 >= sl1) break;               // uniform over the workgroup
+      if (sl + 3 < sl1) load(sl + 3, vxA, vwA);
+      compute(sl + 1, buf);
+      if (sl + 2 < sl1) store(buf ^ 1, vxB, vwB);
+      __syncthreads();
+      buf ^= 1;
+    }
+  } else {
+    __syncthreads();
+    for (int sl = sl0; sl < sl1; ++sl) {
+      const bool more = sl + 1 < sl1;
+      if (more) load(sl + 1, vxA, vwA);
+      compute(sl, buf);
+      if (more) store(buf ^ 1, vxA, vwA);
+      __syncthreads();
+      buf ^= 1;
+    }
   }
   if (SPLIT) {   // f32 partial of this slab range: 16-B stores of 4 consecutive output channels
 #pragma unroll
@@ -1000,10 +1023,19 @@ static int launch(const ConvArgs& a, hipStream_t st) {
       hipLaunchKernelGGL(conv3_sum_kernel, dim3((unsigned)std::min<long long>((n8 + 255) / 256, 8192)), dim3(256), 0,
                          st, (const float*)a.part, a.y, n8, a.nsplit);
     } else {
-      (void)hipFuncSetAttribute((const void*)conv3_fwd_lds2_kernel<NT, false>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      // two-slab-ahead prefetch for the wide tiles (NT >= 3: 1-6 % at the C3 / C5 shapes); NT <= 2 keeps one slab
+      // (PF2 there: 15-20 % slower at Cout = 32, profiles/r03_conv_pf2_ab.txt). LCI_CONV_PF2=0/1 forces it (A/B).
+      static const int pf2_env = getenv("LCI_CONV_PF2") ? atoi(getenv("LCI_CONV_PF2")) : -1;
       dim3 grid((unsigned)(b.order ? (nb + 7) / 8 * 8 : nb));
-      hipLaunchKernelGGL((conv3_fwd_lds2_kernel<NT, false>), grid, dim3(512), sh, st, b);
+      if (pf2_env > 0 || (pf2_env < 0 && NT >= 3)) {
+        (void)hipFuncSetAttribute((const void*)conv3_fwd_lds2_kernel<NT, false, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipLaunchKernelGGL((conv3_fwd_lds2_kernel<NT, false, true>), grid, dim3(512), sh, st, b);
+      } else {
+        (void)hipFuncSetAttribute((const void*)conv3_fwd_lds2_kernel<NT, false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipLaunchKernelGGL((conv3_fwd_lds2_kernel<NT, false>), grid, dim3(512), sh, st, b);
+      }
     }
   } else if (a.Cin % 32 == 0 && lci_conv_lds()) {
     constexpr int ML = NT == 4 ? 2 : 4;
