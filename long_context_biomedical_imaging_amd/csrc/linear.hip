@@ -623,7 +623,20 @@ extern "C" long long lci_linear_wgrad_splits(long long M, int N, int K) {
   const long long tiles = (long long)((N + 32 * c.mb * c.wn - 1) / (32 * c.mb * c.wn)) *
                           ((K + 32 * c.cb * c.wc - 1) / (32 * c.cb * c.wc));
   long long ns = (target + tiles - 1) / tiles;
-  ns = std::min(ns, (M + 2047) / 2048);
+  // rows per split: at least 2048, or down to 512 while the f32 partials (ns N K 4 B, summed by the caller) stay
+  // within 32 MiB or a quarter of the operand bytes read (M (N + K) 2 B) -- the narrow Swin-width gradients (N x K =
+  // 96 x 288 over 2^18 tokens: 3 tiles, 128 splits at 2048 rows; 576 x 192 over 2^15) were short of workgroups (C3
+  // linear_wgrad 3.54 -> 2.45 ms per step at 512 rows, profiles/r03_lw_minrows_ab.txt); the wide ViT / Mamba shapes
+  // keep their split counts. LCI_LW_MINROWS=n: a fixed minimum (A/B).
+  static const long long minrows = getenv("LCI_LW_MINROWS") ? atoll(getenv("LCI_LW_MINROWS")) : 0;
+  long long cap;
+  if (minrows > 0) {
+    cap = (M + minrows - 1) / minrows;
+  } else {
+    const long long budget = std::max(32LL << 20, M * (N + K) / 2);   // partial bytes
+    cap = std::max((M + 2047) / 2048, std::min((M + 511) / 512, budget / (4LL * N * K)));
+  }
+  ns = std::min(ns, cap);
   return std::max(ns, 1LL);
 }
 
