@@ -1,8 +1,12 @@
 #!/usr/bin/env python3
 """Headline benchmark: image-tokens/s fwd+bwd, ViT patch=2 at 512^2 (L = 65 536), 1..8 MI355X.
 
-    python bench.py [--gpus N --steps K --warmup W]                (N = 1)
-    torchrun --nproc-per-node N bench.py --gpus N ...               (N > 1; RCCL DDP)
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...               (the driver's N > 1 launch; RCCL DDP)
+
+`python bench.py --gpus N` with N > 1 outside torchrun starts the N ranks itself (torch.distributed.run as a child
+process, 127.0.0.1 rendezvous) before this process touches the GPU, and exits with its code; every rank checks
+that the process group really has N ranks and the line reports `rccl_world` (the collective's world size).
 
 A step = one DDP training step of the reference's segmentation model (trainer_base.py:157-182):
 EncoderDecoderModel(ViT-small, p2, 512x512, 2-D) + ViTUNETR decoder, bf16 autocast, CrossEntropy loss,
@@ -22,6 +26,8 @@ import argparse
 import json
 import os
 import re
+import socket
+import subprocess
 import sys
 import time
 
@@ -96,6 +102,9 @@ WORKLOADS = {
                           "--height", "128", "--width", "128", "--time", "128", "--no_in_channel", "1",
                           "--no_out_channel", "2", "--Swin.size", "tiny", "--Swin.patch_size", "2", "2", "2",
                           "--Swin.window_size", "8", "8", "8", "--Swin.use_hyena", "True", "--use_amp"],
+    # not a metric: a torch-only model (no HIP kernels), so the N-rank launch path itself can be rehearsed on CPU /
+    # gloo (tests/test_ddp.py::test_bench_gpus2_launch_cpu)
+    "rehearsal": ["--task_type", "enhance", "--loss_func", "MSE", "--optim_type", "adam"],
 }
 WORKLOAD_NAMES = {
     "vit_p4_512": ("image-tokens/sec fwd+bwd, ViT patch=4 512^2 (L=16384)",
@@ -112,6 +121,8 @@ WORKLOAD_NAMES = {
                          "ViT-small p2 256^3 3-D seg (ViTUNETR head), Mamba selective-scan mixer"),
     "vit_hyena_p2_512": ("image-tokens/sec fwd+bwd, ViT-Hyena patch=2 512^2 (L=65536)",
                          "ViT-small p2 512x512 2-D seg (ViTUNETR head), Hyena FFT long-conv mixer"),
+    "rehearsal": ("harness rehearsal (not a metric)",
+                  "torch-only 2-layer MLP: rehearses the N-rank launch, barriers and max-over-ranks timing on CPU / gloo"),
     "vit_hyena_p2_1024": ("image-tokens/sec fwd+bwd, ViT-Hyena patch=2 1024^2 (L=262144), UperNet2D denoising",
                           "ViT-small p2 1024x1024 2-D enhance (UperNet2D head, MSE), Hyena FFT long-conv mixer, "
                           "hyena_l_max 262144 (opt-in; the reference raises above 66000)"),
@@ -170,18 +181,27 @@ def cpu_baseline(budget_s: float = 20.0):
                       f"x12 layers; {ncores} threads (affinity mask capped by OMP_NUM_THREADS)"}
 
 
+# KernelTimer name -> the liblci kernel(s) it launches (rocprofv3 names carry variant suffixes / template args)
+TRAFFIC_KERNELS = {"conv3": r"conv3_fwd\w*_kernel", "conv3_wgrad": r"conv3_wgrad\w*_kernel",
+                   "attn_bwd_dkdv": r"attn_bwd_dkdv\w*_kernel", "attn_bwd_dq": r"attn_bwd_dq\w*_kernel",
+                   "attn_fwd": r"attn_fwd\w*_kernel"}
+
+
 def profiled_traffic(kernel: str):
     """HBM bytes per launch of `kernel` from the committed PMC profile of this bench (profiles/traffic.json, written
-    by tools/summarize_prof.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes), or None."""
+    by tools/summarize_prof.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes), or None. A timer name
+    that covers several kernel variants (the conv3 shapes) gets the launch-weighted mean over them."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
         prof = json.load(f)
-    for name, d in prof.get("kernels", {}).items():
-        if re.search(re.escape(kernel) + r"\d*_kernel", name) or name.endswith(kernel):
-            return int(d["read_bytes"] + d["write_bytes"])
-    return None
+    pat = TRAFFIC_KERNELS.get(kernel, re.escape(kernel) + r"\w*_kernel")
+    hits = [d for name, d in prof.get("kernels", {}).items() if re.search(pat, name) or name.endswith(kernel)]
+    if not hits:
+        return None
+    n = [d.get("launches", 1) for d in hits]
+    return int(sum(k * (d["read_bytes"] + d["write_bytes"]) for k, d in zip(n, hits)) / sum(n))
 
 
 def _sync(device):
@@ -235,8 +255,11 @@ def run_workload(workload, batch, steps, warmup, rank, world, device, kernel_tim
         torch.cuda.empty_cache()
         torch.cuda.reset_peak_memory_stats(device)
     torch.manual_seed(0)
-    model = EncoderDecoderModel(cfg, cfg.encoder_name, cfg.decoder_name, cfg.no_in_channel,
-                                cfg.no_out_channel).to(device)
+    if workload == "rehearsal":
+        model = torch.nn.Sequential(torch.nn.Linear(64, 256), torch.nn.GELU(), torch.nn.Linear(256, 64)).to(device)
+    else:
+        model = EncoderDecoderModel(cfg, cfg.encoder_name, cfg.decoder_name, cfg.no_in_channel,
+                                    cfg.no_out_channel).to(device)
     if use_graph is None:   # host-bound workloads (many small ops per step); LCI_GRAPH=0/1 overrides
         env = os.environ.get("LCI_GRAPH", "")
         use_graph = env == "1" or (env != "0" and workload in GRAPHED)
@@ -246,9 +269,14 @@ def run_workload(workload, batch, steps, warmup, rank, world, device, kernel_tim
     if ckpt:
         model.encoder.checkpoint_blocks = ckpt   # ~35 GB of saved activations per block at 2^21 tokens
     trainer = TrainStep(model, cfg, device, ddp=world > 1)
-    x, y = synthetic_batch(cfg, batch, device, seed=1234 + rank)
-    L = (model.encoder.patch_embedding.n_patches if hasattr(model.encoder, "patch_embedding")
-         else cfg.time * cfg.height * cfg.width // 8)
+    if workload == "rehearsal":
+        g = torch.Generator().manual_seed(1234 + rank)
+        L = 4096
+        x, y = torch.randn(batch, L, 64, generator=g).to(device), torch.randn(batch, L, 64, generator=g).to(device)
+    else:
+        x, y = synthetic_batch(cfg, batch, device, seed=1234 + rank)
+        L = (model.encoder.patch_embedding.n_patches if hasattr(model.encoder, "patch_embedding")
+             else cfg.time * cfg.height * cfg.width // 8)
 
     def on_timed_start():
         kernels.KernelTimer.reset()
@@ -264,10 +292,15 @@ def run_workload(workload, batch, steps, warmup, rank, world, device, kernel_tim
             print(f"[bench] {workload}: graph capture failed ({type(e).__name__}: {e}); eager steps",
                   file=sys.stderr, flush=True)
             graphed = False
+    eager_ms = None
     if graphed:
         elapsed, loss = timed_steps(gstep.step, steps, warmup, world, device, rank, label=workload)
         del gstep
         torch.cuda.synchronize(device)
+        # the same step eager (N > 1 runs are eager: DDP's all-reduce hooks are not captured), so a scaling ratio
+        # against this N = 1 line can compare like with like
+        e_el, _ = timed_steps(lambda: trainer.step(x, y), min(steps, 5), 1, world, device, rank)
+        eager_ms = round(1000.0 * e_el / min(steps, 5), 2)
         kernels.KernelTimer.reset()
         kernels.KernelTimer.enabled = kernel_timer
         for _ in range(2):
@@ -285,10 +318,12 @@ def run_workload(workload, batch, steps, warmup, rank, world, device, kernel_tim
     ksum = kernels.KernelTimer.summary() if device.type == "cuda" else {}
     kernels.KernelTimer.reset()
     loss_v = float(loss.item())
-    model_blocks = list(model.encoder.blocks) if hasattr(model.encoder, "blocks") else []
+    enc = getattr(model, "encoder", None)
+    model_blocks = list(enc.blocks) if hasattr(enc, "blocks") else []
     peak_mem = torch.cuda.max_memory_allocated(device) if device.type == "cuda" else 0
     del trainer, model, x, y, loss
-    torch.cuda.empty_cache()
+    if device.type == "cuda":
+        torch.cuda.empty_cache()
     if rank != 0:
         return None
 
@@ -324,12 +359,14 @@ def run_workload(workload, batch, steps, warmup, rank, world, device, kernel_tim
         "value": round(tokens / elapsed, 1), "unit": "image-tokens/s", "n_gpus": world, "steps": steps,
         "warmup": warmup, "ms_per_step": round(ms, 2), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "bf16", "data": "synthetic U[0,1) images, random-init weights",
+        "rccl_world": world if dist.is_initialized() and dist.get_backend() == "nccl" else None,
+        "dist_backend": dist.get_backend() if dist.is_initialized() else None,
         "config": {"workload": WORKLOAD_NAMES[workload][1],
                    "global_batch": world * batch, "seq_len": L, "parallelism": f"ddp{world}",
                    "per_gpu_batch": batch, "optimizer": cfg.optim_type, "loss": cfg.loss_func,
                    "activation_checkpointing": f"first {ckpt} of {len(model_blocks)} encoder blocks" if ckpt
                    else "none",
-                   "hip_graph": bool(graphed)},
+                   "hip_graph": bool(graphed), "eager_ms_per_step": eager_ms},
         "peak_memory_gb": round(peak_mem / 2 ** 30, 1),
         "roofline": roof,
         "kernels": kern,
@@ -354,14 +391,33 @@ def main():
                     help="no per-launch HIP events (rocprofv3 PMC passes); the line then carries no roofline")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N`: start the N ranks (one process per GPU) as a child torch.distributed.run, before
+        # this process makes any GPU call, and exit with its code (never exec from here)
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+        print(f"[bench] launching {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+        sys.exit(subprocess.call(cmd))
+
     if args.batch is None:
         # 2 images per GPU, except the 3-D ViTUNETR / SwinUNETR configs (1 volume); the UperNet heads' BatchNorm needs
         # 2 samples in training (the reference duplicates a batch of 1, trainer_base.py:160-164; run_abct.sh uses 2)
         args.batch = 1 if args.workload in ("swin_p2_128", "vit_mamba_p2_256") else 2
     rank, local, world = init_distributed()
-    device = torch.device("cuda", local % torch.cuda.device_count())   # % : gloo rehearsals on one GPU
-    torch.cuda.set_device(device)
-    tuned = use_tuned_gemms()
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the process group has {world} ranks")
+    if world > 1:
+        assert dist.get_world_size() == args.gpus
+    if args.workload == "rehearsal" or not torch.cuda.is_available():
+        device = torch.device("cpu")
+        tuned = False
+    else:
+        device = torch.device("cuda", local % torch.cuda.device_count())   # % : gloo rehearsals on one GPU
+        torch.cuda.set_device(device)
+        tuned = use_tuned_gemms()
     res = run_workload(args.workload, args.batch, args.steps, args.warmup, rank, world, device,
                        kernel_timer=not args.no_kernel_timer, ckpt_blocks=args.ckpt_blocks)
     if args.workload == "vit_p2_512" and not args.no_secondary:

@@ -10,7 +10,11 @@ Documented deviations from the reference step:
     "A100"/"H100" in the device name and would pick fp16 here); with bf16 no GradScaler is needed;
   * DDP broadcast_buffers=False: the only buffers are constant index tables (relative_position_index,
     Hyena pos-emb t/deltas), so the per-forward broadcast the reference pays moves nothing that changes;
-  * a batch of 1 is not duplicated (trainer_base.py:160-164; that guards BatchNorm, which these models lack).
+  * a batch of 1 is duplicated as the reference does (trainer_base.py:160-164) when the model holds a BatchNorm
+    (the UperNet heads: a PSP bin-1 map has one value per channel and sample, which BatchNorm cannot train on).
+    Without one the duplicate changes nothing — a mean loss over two identical samples has the loss and the
+    gradients of one — so it is skipped there (the 3-D ViTUNETR / SwinUNETR benches at one volume per GPU
+    would otherwise do twice the work for the same update).
 """
 from __future__ import annotations
 
@@ -98,21 +102,33 @@ class TrainStep:
         self.use_amp = bool(config.use_amp)
         self.clip = float(getattr(config, "clip_grad_norm", 0.0) or 0.0)
         self.accum = max(1, int(getattr(config, "iters_to_accumulate", 1) or 1))
+        self.micro = 0   # micro-batches since the last optimizer step (trainer_base.py:172 `idx`)
+        self.dup_batch1 = any(isinstance(m, nn.modules.batchnorm._BatchNorm) for m in model.modules())
         self.optim.zero_grad(set_to_none=True)
 
-    def step(self, inputs, targets, update: bool = True):
-        """trainer_base.py:166-182: autocast forward + loss / iters_to_accumulate, backward, then (when `update`,
-        i.e. at the end of an accumulation window) optional grad-norm clip, optimizer step and zero_grad."""
+    def step(self, inputs, targets, update: bool | None = None):
+        """trainer_base.py:160-182: a batch of 1 is duplicated (BatchNorm), autocast forward + loss /
+        iters_to_accumulate, backward; the optional grad-norm clip, optimizer step and zero_grad run only at the end
+        of an accumulation window, i.e. every `iters_to_accumulate` calls (`update=None`), as the reference's
+        `(idx + 1) % iters_to_accumulate == 0`. `update=True` forces the step (the reference's last iteration of an
+        epoch, `idx + 1 == total_iters`), `update=False` suppresses it."""
+        if inputs.shape[0] == 1 and self.dup_batch1:
+            inputs = torch.cat([inputs] * 2, dim=0)
+            targets = torch.cat([targets] * 2, dim=0)
         dev = "cuda" if self.device.type == "cuda" else "cpu"
         with torch.autocast(device_type=dev, dtype=torch.bfloat16, enabled=self.use_amp):
             out = self.model(inputs)
             loss = self.loss_func(out, targets) / self.accum
         loss.backward()
+        self.micro += 1
+        if update is None:
+            update = self.micro % self.accum == 0
         if update:
             if self.clip > 0:
                 nn.utils.clip_grad_norm_(self.model.parameters(), self.clip)
             self.optim.step()
             self.optim.zero_grad(set_to_none=True)
+            self.micro = 0
         return loss.detach()
 
 
@@ -125,30 +141,46 @@ class GraphedStep:
     kernels are captured as graph nodes; the per-op host work of the Python modules and autograd (~2000 launches
     per Swin-tiny step) is paid once at capture. Single process only (no DDP: its all-reduce hooks are not part
     of the capture here); the optimizer runs with capturable=True (fused Adam / AdamW keep their step on device).
+
+    Constructing it TRAINS: the `warmup` side-stream steps and the captured step are real optimizer steps on the
+    static batch (warmup + 1 updates before the first replay). If the capture fails, the optimizer's `capturable`
+    flags are restored before the error propagates (the weights keep the warm-up updates). Gradient accumulation
+    (iters_to_accumulate > 1) is refused: the graph replays one fixed step, always with the optimizer update.
     """
 
     def __init__(self, trainer: "TrainStep", inputs, targets, warmup: int = 2):
         if not isinstance(trainer.model, nn.Module) or isinstance(trainer.model, nn.parallel.DistributedDataParallel):
             raise ValueError("GraphedStep: single-process TrainStep only")
-        for g in trainer.optim.param_groups:
-            if "capturable" in g:
-                g["capturable"] = True
+        if trainer.accum != 1:
+            raise ValueError("GraphedStep: iters_to_accumulate > 1 is not supported (the graph always updates)")
+        if inputs.shape[0] == 1 and trainer.dup_batch1:   # TrainStep.step's duplication, once on the static buffers
+            inputs, targets = torch.cat([inputs] * 2, dim=0), torch.cat([targets] * 2, dim=0)
+        saved = [(g, g["capturable"]) for g in trainer.optim.param_groups if "capturable" in g]
+        for g, _ in saved:
+            g["capturable"] = True
         self.trainer = trainer
         self.inputs, self.targets = inputs, targets
-        side = torch.cuda.Stream(device=inputs.device)
-        side.wait_stream(torch.cuda.current_stream(inputs.device))
-        with torch.cuda.stream(side):
-            for _ in range(warmup):
-                trainer.step(inputs, targets)
-        torch.cuda.current_stream(inputs.device).wait_stream(side)
-        torch.cuda.synchronize(inputs.device)
-        self.graph = torch.cuda.CUDAGraph()
-        # relaxed: the kernels' one-time launch attributes (hipFuncSetAttribute) are legal during the capture
-        with torch.cuda.graph(self.graph, capture_error_mode="relaxed"):
-            self.loss = trainer.step(inputs, targets)
+        try:
+            side = torch.cuda.Stream(device=inputs.device)
+            side.wait_stream(torch.cuda.current_stream(inputs.device))
+            with torch.cuda.stream(side):
+                for _ in range(warmup):
+                    trainer.step(inputs, targets, update=True)
+            torch.cuda.current_stream(inputs.device).wait_stream(side)
+            torch.cuda.synchronize(inputs.device)
+            self.graph = torch.cuda.CUDAGraph()
+            # relaxed: the kernels' one-time launch attributes (hipFuncSetAttribute) are legal during the capture
+            with torch.cuda.graph(self.graph, capture_error_mode="relaxed"):
+                self.loss = trainer.step(inputs, targets, update=True)
+        except Exception:
+            for g, c in saved:
+                g["capturable"] = c
+            raise
 
     def step(self, inputs=None, targets=None):
         if inputs is not None and inputs is not self.inputs:
+            if inputs.shape[0] == 1 and self.inputs.shape[0] == 2:
+                inputs, targets = torch.cat([inputs] * 2, dim=0), torch.cat([targets] * 2, dim=0)
             self.inputs.copy_(inputs)
         if targets is not None and targets is not self.targets:
             self.targets.copy_(targets)

@@ -218,3 +218,23 @@ def test_ddp_rccl_backend_gpu():
     assert ok_ar and loss == loss and elapsed > 0
     for a, b in zip(w_ddp, w_ref):
         np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-7)
+
+
+def test_bench_gpus2_launch_cpu():
+    """`python bench.py --gpus 2` outside torchrun starts the two ranks itself (torch.distributed.run child, 127.0.0.1
+    rendezvous) and the rank-0 line reports both: the N-rank launch path end to end, on the torch-only rehearsal
+    workload over gloo (no GPU here)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, LCI_DIST_BACKEND="gloo", OMP_NUM_THREADS="2")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--workload", "rehearsal",
+                        "--steps", "3", "--warmup", "1", "--batch", "2"], capture_output=True, text=True, env=env,
+                       timeout=300, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["dist_backend"] == "gloo"
+    assert line["config"]["global_batch"] == 4 and line["config"]["parallelism"] == "ddp2"
+    assert line["value"] > 0 and line["steps"] == 3

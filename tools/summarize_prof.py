@@ -100,7 +100,7 @@ def main():
             w = counters.get("write", {}).get(n)
             if f and w:
                 out[n] = {"read_bytes": 2.0 * sum(f) / len(f) * 1024, "write_bytes": sum(w) / len(w) * 1024,
-                          "avg_ms": sum(dur[n]) / len(dur[n])}
+                          "avg_ms": sum(dur[n]) / len(dur[n]), "launches": len(dur[n])}
         json.dump({"source": d, "note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB -> bytes, per launch",
                    "kernels": out}, open(sys.argv[3], "w"), indent=1)
     print(f"# rocprofv3 summary: {d}\n")
