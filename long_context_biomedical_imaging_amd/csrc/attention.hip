@@ -84,7 +84,7 @@ struct AttnArgs {
   bf16* out;                                       // fwd: O ; bwd dq kernel: dQ
   bf16* dk; bf16* dv;                              // bwd dkdv kernel
   float* lse2;                                     // (B, H, L)
-  float* delta;                                    // (B, H, L)
+  float* delta;                                    // bwd: (B, H, 2, L) negated row constants [-lse2 | -delta]
   long long bs_q, bs_k, bs_v, bs_o, bs_do, bs_out, bs_dk, bs_dv;   // batch strides (elements)
   int rs_q, rs_k, rs_v, rs_o, rs_do, rs_out, rs_dk, rs_dv;         // token (row) strides (elements)
   int hs;                                          // head stride (elements) in every tensor (= 64)
@@ -415,7 +415,9 @@ __global__ __launch_bounds__(FW_NW * 64, 1) void attn_fwd2_kernel(AttnArgs a, co
 }
 
 // --------------------------------------------------------------------------- backward: delta
-// delta[b,h,q] = sum_d dO[b,q,h,d] * O[b,q,h,d]; 8 threads per (q, h) row, 16 B each.
+// delta[b,h,q] = sum_d dO[b,q,h,d] * O[b,q,h,d]; 8 threads per (q, h) row, 16 B each. Written negated, next to the
+// negated lse2, as the backward kernels' row constants: ws[b][h][0][q] = -lse2, ws[b][h][1][q] = -delta (the chains'
+// initial accumulators; the dK/dV kernel stages a tile's 64 + 64 of them with two contiguous loads).
 __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnArgs a) {
   const int tid = threadIdx.x;
   const int row = blockIdx.x * 32 + (tid >> 3), ch = tid & 7;
@@ -430,7 +432,11 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnArgs a) {
   acc += __shfl_xor(acc, 1);
   acc += __shfl_xor(acc, 2);
   acc += __shfl_xor(acc, 4);
-  if (ch == 0 && row < a.L) a.delta[((long long)b * a.H + hh) * a.L + row] = acc;
+  if (ch == 0 && row < a.L) {
+    float* ws = a.delta + ((long long)b * a.H + hh) * 2 * a.L;
+    ws[row] = -a.lse2[((long long)b * a.H + hh) * a.L + row];
+    ws[a.L + row] = -acc;
+  }
 }
 
 // ---------------------------------------------------------------------- backward: dK, dV kernel
@@ -450,8 +456,8 @@ __global__ __launch_bounds__(NW * 64, (KB == 1 ? 8 / NW : 4 / NW)) void attn_bwd
 
   const bf16* qp = a.q + b * a.bs_q + hh * a.hs;
   const bf16* dop = a.dout + b * a.bs_do + hh * a.hs;
-  const float* lsep = a.lse2 + ((long long)b * a.H + hh) * L;
-  const float* dlp = a.delta + ((long long)b * a.H + hh) * L;
+  const float* lsep = a.delta + ((long long)b * a.H + hh) * 2 * L;   // -lse2
+  const float* dlp = lsep + L;                                        // -delta
 
   // K^T and V^T as B operands: lane (key r, half h) holds K[key][16ks+8h..], V[key][16ks+8h..]
   bf16x8 kf[KB][4], vf[KB][4];
@@ -487,15 +493,15 @@ __global__ __launch_bounds__(NW * 64, (KB == 1 ? 8 / NW : 4 / NW)) void attn_bwd
     if constexpr (LCI_DKDV_ROWC_VALU) {
       if (tid < 2 * KT) {
         const int which = tid / KT, qi = tid % KT, q = qt * KT + qi;
-        rowc[buf][which][qi] = which == 0 ? ((q < L) ? lsep[q] : 1.0e30f) : ((q < L) ? dlp[q] : 0.f);
+        rowc[buf][which][qi] = which == 0 ? ((q < L) ? -lsep[q] : 1.0e30f) : ((q < L) ? -dlp[q] : 0.f);
       }
       return;
     }
     if (tid < 2 * KT) {
       const int which = tid / KT, qi = tid % KT, q = qt * KT + qi;
       float v;
-      if (which == 0) v = (q < L) ? -lsep[q] : -1.0e30f;  // invalid rows: P = exp2(-huge) = 0
-      else v = (q < L) ? -dlp[q] : 0.f;
+      if (which == 0) v = (q < L) ? lsep[q] : -1.0e30f;  // invalid rows: P = exp2(-huge) = 0
+      else v = (q < L) ? dlp[q] : 0.f;
       const bf16 hi = to_bf16(v), mid = to_bf16(v - to_f32(hi)), lo = to_bf16(v - to_f32(hi) - to_f32(mid));
       bf16x8 e{};
       e[0] = hi; e[1] = mid; e[2] = lo;
@@ -663,8 +669,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv16_kernel(AttnAr
 
   const bf16* qp = a.q + b * a.bs_q + hh * a.hs;
   const bf16* dop = a.dout + b * a.bs_do + hh * a.hs;
-  const float* lsep = a.lse2 + ((long long)b * a.H + hh) * L;
-  const float* dlp = a.delta + ((long long)b * a.H + hh) * L;
+  const float* lsep = a.delta + ((long long)b * a.H + hh) * 2 * L;   // -lse2
+  const float* dlp = lsep + L;                                        // -delta
 
   // K^T / V^T as B operands: lane holds K[kw0 + 16kb + c16][32ks + 8g + j] (K prescaled into the exp2 domain)
   bf16x8 kf[2][2], vf[2][2];
@@ -703,7 +709,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv16_kernel(AttnAr
   auto stage_rowc = [&](int buf, int qt, float v) __attribute__((always_inline)) {
     if (tid < 2 * KT) {
       const bool ok = qt * KT + tid % KT < L;
-      rowc[buf][tid / KT][tid % KT] = ok ? -v : (tid < KT ? -1.0e30f : 0.f);   // invalid rows: P = 0
+      rowc[buf][tid / KT][tid % KT] = ok ? v : (tid < KT ? -1.0e30f : 0.f);   // invalid rows: P = 0
     }
   };
   qr.load(qp, a.rs_q, 0, L, tid);
@@ -816,6 +822,476 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv16_kernel(AttnAr
   }
 }
 
+// ------------------------------------- backward: dK, dV kernel, one wave per SIMD, placed MFMA / VALU / LDS stream
+// VERDICT r03 item 1. A workgroup = 4 waves (one per SIMD, the whole register file each), a wave owns 64 keys (two
+// key blocks of 32, key on the MFMA lane), so every Q / dO fragment read from LDS feeds two key blocks: half the LDS
+// bytes per MFMA of the 32-key kernels. Per 32-query half-tile and wave: 32 v_mfma_f32_32x32x16_bf16 (S and dP
+// chains 8 + 8, dV^T 8, dK^T 8) against 32 exp2 + 32 multiplies + 32 conversions (P = exp2(S~ - lse2) and dS =
+// P (dP - delta) need no subtract: -lse2 / -delta are the chains' initial accumulators, read as f32x4 from the tile's
+// row-constant rows) and 40 LDS reads: one MFMA gap holds 1 exp2, 1 multiply, 0-2 conversions and 0-2 LDS reads
+// (MI355X_MICROARCH.md "one wave per SIMD": <= 5 fillers, <= 1 transcendental per 32x32x16 gap).
+// Software pipeline: key block 1 runs half a period behind key block 0, so each block's S / dP registers are
+// produced, consumed and refilled in turn and every gap pairs one block's MFMAs with the other block's VALU.
+// Per half-tile p, four segments of 8 MFMA gaps:
+//   seg A: S chain, dP chain kb0 (half p)     || VALU kb1 (half p-1), elements 8-15
+//   seg B: dV^T / dK^T kb1 (half p-1)        || VALU kb0 (half p), elements 0-7  | LDS: dO^T / Q^T of half p
+//   seg C: S chain, dP chain kb1 (half p)     || VALU kb0 (half p), elements 8-15 | LDS: dO^T / Q^T, Q rows of p+1
+//   seg D: dV^T / dK^T kb0 (half p)          || VALU kb1 (half p), elements 0-7  | LDS: row constants, dO rows of p+1
+// Every MFMA and every exp2 / multiply / conversion of the loop is its own `asm volatile` statement, so the stream
+// is issued exactly in the order written (the compiler only allocates registers and inserts the LDS waits); the
+// dV / dK accumulators (128) and the K / V fragments (64) are "a" operands (the AGPR half of the file), the VALU
+// working set (~220) stays in the arch VGPRs. Hazards the compiler cannot see into asm are covered by the placement
+// (gfx950 wait states, measured from the compiler's own insertions: MFMA -> VALU read 12, VALU -> MFMA A/B read 2,
+// exp -> dependent VALU 1, MFMA C read -> overwrite 7): a chain's last S MFMA is 4 gaps before the first exp of it,
+// its last dP MFMA 3 gaps before the first multiply, a pack 2+ gaps before its MFMA, a fragment reloaded 2 gaps after
+// its last MFMA read.
+// Q / dO tiles of 64 queries arrive in a 3-slot LDS ring (128-B rows, 16-B chunk XOR ((r >> 2) & 3 | ((r >> 1) & 1)
+// << 2): conflict-free for the 32x32 row reads and the transposed reads), staged through registers one tile ahead;
+// one barrier per tile, between its two halves (half 1's seg C / D read the next tile).
+constexpr int HS_NW = 4;
+#ifndef LCI_HS_STG
+#define LCI_HS_STG 0   // tile staging: 0 = LDS-DMA into a 4-slot ring; 1 = registers (AGPRs; needs the 2-tile unroll,
+                       // which spills 140 VGPRs): both two tiles ahead
+#endif
+#ifndef LCI_HS_PROBE
+#define LCI_HS_PROBE 0   // timing probes (wrong results): 1 = no barrier, 2 = no tile staging after the prologue,
+                         // 3 = no LDS traffic, staging or barrier in the loop, 4 = no VALU in the loop
+#endif
+#ifndef LCI_HS_V
+#define LCI_HS_V 2   // 1: first placement (conversions in pairs, single fragment set, LDS reads in segs B-D), for A/B
+#endif
+__device__ __forceinline__ int sw128(int row, int col) {
+  const int g = ((row >> 2) & 3) | (((row >> 1) & 1) << 2);
+  return row * DH + ((((col >> 3) ^ g) << 3) | (col & 7));
+}
+// LDS-DMA from a buffer resource: every lane's 16 (4) bytes at voff + soff land at LDS byte address lds + 16 (4) * lane;
+// rows past the resource's range read as zero. Issued from asm so that the compiler neither tracks it as an LDS write
+// nor counts it in its vmcnt waits (completion is waited for explicitly before the barrier that publishes the tile).
+__device__ __forceinline__ void hs_dma16(rsrc_t r, int voff, int soff, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(r), "s"(lds), "s"(soff) : "memory");
+}
+__device__ __forceinline__ void hs_dma4(rsrc_t r, int voff, int soff, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(r), "s"(lds), "s"(soff) : "memory");
+}
+// 16-byte (4-byte) buffer load into AGPRs, issued from asm: the compiler does not count it in its vmcnt waits (it would
+// wait for every load in flight before the first use of any), so the use must be preceded by an explicit hs_vmcnt
+__device__ __forceinline__ u32x4 hs_ld16(rsrc_t r, int voff, int soff) {
+  u32x4 v;
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=a"(v) : "v"(voff), "s"(r), "s"(soff) : "memory");
+  return v;
+}
+__device__ __forceinline__ uint32_t hs_ld4(rsrc_t r, int voff, int soff) {
+  uint32_t v;
+  asm volatile("buffer_load_dword %0, %1, %2, %3 offen" : "=a"(v) : "v"(voff), "s"(r), "s"(soff) : "memory");
+  return v;
+}
+template <int N>
+__device__ __forceinline__ void hs_vmcnt() {   // s_waitcnt vmcnt(N), lgkmcnt / expcnt untouched
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+#define HS_EXP(x) asm volatile("v_exp_f32 %0, %0" : "+v"(x))
+#define HS_MUL(p, e) asm volatile("v_mul_f32 %0, %1, %0" : "+v"(p) : "v"(e))
+#define HS_CVT(w, x0, x1) asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(w) : "v"(x0), "v"(x1))
+// accumulate into AGPRs (dV^T / dK^T), A and B from VGPRs
+#define HS_MFMA_G(acc, A, B) \
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(A), "v"(B))
+// S / dP chains: B = the K / V fragment in AGPRs; the first step reads the row constants as C (separate registers)
+#define HS_MFMA_C0(d, A, B, C) \
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3" : "=&v"(d) : "v"(A), "a"(B), "v"(C))
+#define HS_MFMA_C(d, A, B) \
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(A), "a"(B))
+
+__global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArgs a) {
+  constexpr int TILE_B = KT * DH * 2;               // bytes of a Q or dO tile (128-B rows)
+  constexpr int SLOT_B = 2 * TILE_B;                // Q | dO of one tile
+  constexpr int RC_B = 2 * KT * 4;                  // -lse2[64] | -delta[64] of one tile
+  constexpr int NSLOT = 4;                          // ring: tile t, t+1 (published), t+2, t+3 (in flight)
+  static_assert((NSLOT & (NSLOT - 1)) == 0, "ring slot of tile t is t & (NSLOT - 1)");
+  // the Q / dO ring fills exactly 64 KB, so every fragment read of every slot is one lane register + a 16-bit
+  // immediate (slot, dO and row offsets); the row-constant rows follow in their own 2 KB
+  static_assert(NSLOT * SLOT_B == 65536, "Q / dO ring reachable by DS immediates");
+  __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT_B + NSLOT * RC_B];
+  char* const rcs = smem + NSLOT * SLOT_B;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hh = blockIdx.y, b = blockIdx.z;
+  const int L = a.L;
+  const int h = lane >> 5, r32 = lane & 31;
+  const int kw0 = blockIdx.x * (HS_NW * 64) + wave * 64;
+  const int nqt = (L + KT - 1) / KT;
+
+  // K^T / V^T as B operands: lane holds K[kw0 + 32kb + r32][16ks + 8h + j] (K prescaled into the exp2 domain)
+  bf16x8 kf[2][4], vf[2][4];
+  {
+    const bf16* kp = a.k + b * a.bs_k + hh * a.hs;
+    const bf16* vp = a.v + b * a.bs_v + hh * a.hs;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const int key = kw0 + 32 * kb + r32;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        if (key < L) {
+          kf[kb][ks] = *(const bf16x8*)(kp + (long long)key * a.rs_k + 16 * ks + 8 * h);
+          vf[kb][ks] = *(const bf16x8*)(vp + (long long)key * a.rs_v + 16 * ks + 8 * h);
+        } else {
+          kf[kb][ks] = bf16x8{};
+          vf[kb][ks] = bf16x8{};
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) kf[kb][ks][j] = to_bf16(to_f32(kf[kb][ks][j]) * a.c);
+      }
+    }
+  }
+  // the K / V loads complete here: otherwise the compiler waits for them (vmcnt(0)) at their first use inside the
+  // loop, where that wait would also drain every tile's in-flight staging loads (which it does not track)
+  hs_vmcnt<0>();
+
+  // ---- staging by LDS-DMA, two tiles ahead: wave w copies rows 16w .. 16w+15 of the Q and dO tiles as 1-KB pieces
+  // (8 rows x 128 B, lane l -> row l >> 3 of the piece, physical 16-B chunk l & 7, fetched from the logical chunk
+  // (l & 7) ^ g(row) of the sw128 swizzle), and one row of row constants (waves 0 / 2: -lse2, 1 / 3: -delta; the
+  // pairs write the same bytes). Rows >= L read as zero: they add nothing to dV or dK whatever P is.
+  const int rs2q = a.rs_q * 2, rs2d = a.rs_do * 2;
+  const rsrc_t rq = make_rsrc(a.q + b * a.bs_q + hh * a.hs, (uint32_t)(L - 1) * (uint32_t)rs2q + DH * 2);
+  const rsrc_t rd = make_rsrc(a.dout + b * a.bs_do + hh * a.hs, (uint32_t)(L - 1) * (uint32_t)rs2d + DH * 2);
+  const rsrc_t rr = make_rsrc(a.delta + ((long long)b * a.H + hh) * 2 * L + (wave & 1) * L, (uint32_t)L * 4);
+  // row = 16 wave + 8 j + prow (piece j = 0, 1): g(row) = ((row >> 2) & 3) | ((row >> 1) & 1) << 2 = (2j + (prow >> 2))
+  // | ((prow >> 1) & 1) << 2
+  const int prow = lane >> 3;
+  const int pch0 = (lane & 7) ^ ((prow >> 2) | ((prow >> 1) & 1) << 2);
+  const int pch1 = (lane & 7) ^ ((2 + (prow >> 2)) | ((prow >> 1) & 1) << 2);
+  const int dq0 = (16 * wave + prow) * rs2q + 16 * pch0, dq1 = (16 * wave + 8 + prow) * rs2q + 16 * pch1;
+  const int dd0 = (16 * wave + prow) * rs2d + 16 * pch0, dd1 = (16 * wave + 8 + prow) * rs2d + 16 * pch1;
+  const unsigned lds0 = (unsigned)(uintptr_t)(LCI_LDS char*)smem;
+  auto dma_op = [&](int t, int i) __attribute__((always_inline)) {   // operation i (0-4) of tile t
+    const unsigned sb = lds0 + (unsigned)((t & (NSLOT - 1)) * SLOT_B);
+    if (i == 0) hs_dma16(rq, dq0, t * KT * rs2q, sb + 2048 * wave);
+    if (i == 1) hs_dma16(rq, dq1, t * KT * rs2q, sb + 2048 * wave + 1024);
+    if (i == 2) hs_dma16(rd, dd0, t * KT * rs2d, sb + TILE_B + 2048 * wave);
+    if (i == 3) hs_dma16(rd, dd1, t * KT * rs2d, sb + TILE_B + 2048 * wave + 1024);
+    if (i == 4) hs_dma4(rr, lane * 4, t * KT * 4, lds0 + (unsigned)(NSLOT * SLOT_B + (t & (NSLOT - 1)) * RC_B +
+                                                                     (wave & 1) * KT * 4));
+  };
+  auto dma_tile = [&](int t) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) dma_op(t, i);
+  };
+  // register staging (LCI_HS_STG 1): thread -> rows (srow, srow + 32), chunk sch of the Q and dO tiles, plus one row
+  // constant per lane in waves 0 / 1; two sets, a tile's loads issued two tiles before its LDS store
+  const int srow = tid >> 3, sch = tid & 7;
+  const int vq0 = srow * rs2q + sch * 16, vq1 = vq0 + 32 * rs2q;
+  const int vd0 = srow * rs2d + sch * 16, vd1 = vd0 + 32 * rs2d;
+  const int st0 = 2 * sw128(srow, sch * 8), st1 = st0 + 32 * 128;
+  struct Stage { u32x4 q0, q1, d0, d1; uint32_t rc; };
+  Stage stg[2];
+  auto load_tile = [&](Stage& g, int t) __attribute__((always_inline)) {   // 5 loads in every wave
+    g.q0 = hs_ld16(rq, vq0, t * KT * rs2q);
+    g.q1 = hs_ld16(rq, vq1, t * KT * rs2q);
+    g.d0 = hs_ld16(rd, vd0, t * KT * rs2d);
+    g.d1 = hs_ld16(rd, vd1, t * KT * rs2d);
+    g.rc = hs_ld4(rr, lane * 4, t * KT * 4);
+  };
+  auto store_tile = [&](const Stage& g, char* slot) __attribute__((always_inline)) {
+    *(u32x4*)(slot + st0) = g.q0;
+    *(u32x4*)(slot + st1) = g.q1;
+    *(u32x4*)(slot + TILE_B + st0) = g.d0;
+    *(u32x4*)(slot + TILE_B + st1) = g.d1;
+    if (wave < 2) *(uint32_t*)(rcs + wave * KT * 4 + lane * 4) = g.rc;   // (register staging: ring slot 0 only)
+  };
+
+  // ---- fragment readers (byte offsets; r0 = the half's first query row in the tile)
+  auto qrow = [&](const char* tile, int r0, int ks) __attribute__((always_inline)) {
+    return *(const bf16x8*)(tile + 2 * sw128(r0 + r32, 16 * ks + 8 * h));
+  };
+  auto trf = [&](const char* tile, int r0, int S, int c0) __attribute__((always_inline)) {
+    const int row = r0 + 16 * S + 4 * h + ((lane & 15) >> 2);
+    const int col = c0 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+    return cat44(lds_tr4((const bf16*)(tile + 2 * sw128(row, col))),
+                 lds_tr4((const bf16*)(tile + 2 * sw128(row + 8, col))));
+  };
+  // initial accumulator of a chain: register i <-> query r0 + (i & 3) + 8 (i >> 2) + 4h
+  auto rcblk = [&](const char* rcslot, int which, int r0) __attribute__((always_inline)) {
+    const float* rc = (const float*)(rcslot + which * KT * 4) + r0 + 4 * h;
+    f32x16 r;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 v = *(const f32x4*)(rc + 8 * g);
+      r[4 * g] = v[0]; r[4 * g + 1] = v[1]; r[4 * g + 2] = v[2]; r[4 * g + 3] = v[3];
+    }
+    return r;
+  };
+
+  f32x16 dv[2][2], dk[2][2];   // [d block][key block]: dV^T / dK^T, lane = key, rows d = 32db + (i&3) + 8(i>>2) + 4h
+  f32x16 S[2], P[2];           // [key block]: S~ - lse2 and dP - delta of the block's current half
+  f32x16 NL, ND;               // row constants (-lse2, -delta) of the chains' half
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    S[i] = P[i] = f32x16{};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) dv[i][j] = dk[i][j] = f32x16{};
+  }
+  u32x4 pk[2][2] = {}, dd[2][2] = {};    // [key block][k-step] bf16 P / dS packs (dword j = elements 2j, 2j+1)
+  bf16x8 tdo[2][2][2] = {}, tq[2][2][2] = {};  // [set][d block][k-step] transposed dO / Q fragments: half p uses
+                                              // set p & 1 (its kb1 products run in half p+1, beside p+1's reads)
+  bf16x8 qa[4], da[4];                   // Q / dO row fragments of the chains' half
+
+  // VALU of gap g of a segment over elements 8e..8e+7 of key block kb: one exp2, one multiply, one conversion per
+  // gap (8 + 4 + 4 issue cycles beside the MFMA's 8 of 32); gaps 0-2 finish the previous segment's block
+  // (pkb, pe): its last two multiplies and three conversions
+  auto valu_gap = [&](int g, int kb, int e, int pkb, int pe) __attribute__((always_inline)) {
+    if (LCI_HS_PROBE == 4) return;
+    f32x16& s = S[kb];
+    f32x16& p = P[kb];
+    const int o = 8 * e, po = 8 * pe;
+    HS_EXP(s[o + g]);
+    if (g >= 2) HS_MUL(p[o + g - 2], s[o + g - 2]);
+    if (g == 0) HS_MUL(P[pkb][po + 6], S[pkb][po + 6]);
+    if (g == 1) HS_MUL(P[pkb][po + 7], S[pkb][po + 7]);
+    if (LCI_HS_V == 1) {
+      if (g == 0) HS_CVT(pk[pkb][pe][3], S[pkb][po + 6], S[pkb][po + 7]);
+      if (g == 0) HS_CVT(dd[pkb][pe][2], P[pkb][po + 4], P[pkb][po + 5]);
+      if (g == 2) HS_CVT(dd[pkb][pe][3], P[pkb][po + 6], P[pkb][po + 7]);
+      if (g == 2 || g == 4 || g == 6) HS_CVT(pk[kb][e][g / 2 - 1], s[o + g - 2], s[o + g - 1]);
+      if (g == 4 || g == 6) HS_CVT(dd[kb][e][g / 2 - 2], p[o + g - 4], p[o + g - 3]);
+      return;
+    }
+    switch (g) {
+      case 0: HS_CVT(pk[pkb][pe][3], S[pkb][po + 6], S[pkb][po + 7]); break;
+      case 1: HS_CVT(dd[pkb][pe][2], P[pkb][po + 4], P[pkb][po + 5]); break;
+      case 2: HS_CVT(dd[pkb][pe][3], P[pkb][po + 6], P[pkb][po + 7]); break;
+      case 3: HS_CVT(pk[kb][e][0], s[o], s[o + 1]); break;
+      case 4: HS_CVT(pk[kb][e][1], s[o + 2], s[o + 3]); break;
+      case 5: HS_CVT(dd[kb][e][0], p[o], p[o + 1]); break;
+      case 6: HS_CVT(pk[kb][e][2], s[o + 4], s[o + 5]); break;
+      default: HS_CVT(dd[kb][e][1], p[o + 2], p[o + 3]); break;
+    }
+  };
+  // MFMA of gap g of a chain segment (S chain at gaps 0-3, dP chain at gaps 4-7) for key block kb
+  auto chain_gap = [&](int g, int kb) __attribute__((always_inline)) {
+    if (g == 0) HS_MFMA_C0(S[kb], qa[0], kf[kb][0], NL);
+    else if (g < 4) HS_MFMA_C(S[kb], qa[g], kf[kb][g]);
+    else if (g == 4) HS_MFMA_C0(P[kb], da[0], vf[kb][0], ND);
+    else HS_MFMA_C(P[kb], da[g - 4], vf[kb][g - 4]);
+  };
+  // MFMA of gap g of a gradient segment for key block kb with fragment set st: (k-step s2, d block db, dV | dK)
+  auto grad_gap = [&](int g, int kb, int st) __attribute__((always_inline)) {
+    const int s2 = g >> 2, db = (g >> 1) & 1;
+    const bf16x8 pb = __builtin_bit_cast(bf16x8, pk[kb][s2]);
+    const bf16x8 db8 = __builtin_bit_cast(bf16x8, dd[kb][s2]);
+    if (g & 1) HS_MFMA_G(dk[db][kb], tq[st][db][s2], db8);
+    else HS_MFMA_G(dv[db][kb], tdo[st][db][s2], pb);
+  };
+  // transposed fragment f (gradient order: k-step f >> 2, d block (f >> 1) & 1, dO^T | Q^T) of rows r0 into set st
+  bool probe_noread = false;
+  auto tr_load = [&](int f, int st, const char* slot, int r0) __attribute__((always_inline)) {
+    if (LCI_HS_PROBE == 3 && probe_noread) return;
+    const int s2 = f >> 2, db = (f >> 1) & 1;
+    if (f & 1) tq[st][db][s2] = s2 ? trf(slot, r0, 1, 32 * db) : trf(slot, r0, 0, 32 * db);
+    else tdo[st][db][s2] = s2 ? trf(slot + TILE_B, r0, 1, 32 * db) : trf(slot + TILE_B, r0, 0, 32 * db);
+  };
+  // one f32x4 piece (queries 8g + 4h .. + 3 of the half) of a chain's row-constant block
+  auto rc_load = [&](f32x16& r, const char* rcslot, int which, int r0, int g) __attribute__((always_inline)) {
+    if (LCI_HS_PROBE == 3 && probe_noread) return;
+    const f32x4 v = *(const f32x4*)((const float*)(rcslot + which * KT * 4) + r0 + 4 * h + 8 * g);
+    r[4 * g] = v[0]; r[4 * g + 1] = v[1]; r[4 * g + 2] = v[2]; r[4 * g + 3] = v[3];
+  };
+
+  // One half-tile p = rows r0 of `slot` (fragment set C = p & 1); segs C / D read half p+1 = rows nr0 of `nslot`.
+  // LDS reads, one per gap, each placed at least two gaps after the last MFMA read of the registers it refills
+  // (seven wait states for a row-constant block read as an MFMA C operand):
+  //   seg A, B: this half's transposed fragments into set C (set C^1 is still read by seg B's kb1 products)
+  //   seg C: Q rows of half p+1 (gaps 2-5), -lse2 pieces 0-1 and dO rows 0-1 (gaps 6-7)
+  //   seg D: -lse2 pieces 2-3, -delta pieces 0-3, dO rows 2-3
+  auto half = [&](auto CUR, const char* slot, int r0, const char* nslot, const char* nrc, int nr0, auto mid, auto bgap)
+      __attribute__((always_inline)) {
+    constexpr int C = decltype(CUR)::value;
+    // seg A: chains kb0 || VALU kb1 (p-1) elements 8-15 (finishing its elements 0-7)
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      chain_gap(g, 0);
+      valu_gap(g, 1, 1, 1, 0);
+      if (!(g & 1)) tr_load(g >> 1, C, slot, r0);
+    }
+    mid();
+    // seg B: dV / dK kb1 (p-1, set C^1) || VALU kb0 elements 0-7 (finishing kb1 8-15)
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      grad_gap(g, 1, C ^ 1);
+      valu_gap(g, 0, 0, 1, 1);
+      if (!(g & 1)) tr_load(4 + (g >> 1), C, slot, r0);
+      bgap(g);
+    }
+    // seg C: chains kb1 || VALU kb0 elements 8-15
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      chain_gap(g, 1);
+      valu_gap(g, 0, 1, 0, 0);
+      if (g >= 2 && g < 6 && LCI_HS_PROBE != 3) qa[g - 2] = qrow(nslot, nr0, g - 2);
+      if (g >= 6) {
+        rc_load(NL, nrc, 0, nr0, g - 6);
+        if (LCI_HS_PROBE != 3) da[g - 6] = qrow(nslot + TILE_B, nr0, g - 6);
+      }
+    }
+    // seg D: dV / dK kb0 (set C) || VALU kb1 elements 0-7 (finishing kb0 8-15)
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      grad_gap(g, 0, C);
+      valu_gap(g, 1, 0, 0, 1);
+      if (g < 2) rc_load(NL, nrc, 0, nr0, g + 2);
+      else if (g < 6) rc_load(ND, nrc, 1, nr0, g - 2);
+      else if (LCI_HS_PROBE != 3) da[g - 4] = qrow(nslot + TILE_B, nr0, g - 4);
+    }
+  };
+
+  auto half_v1 = [&](auto CUR, const char* slot, int r0, const char* nslot, const char* nrc, int nr0, auto mid,
+                     auto bgap)
+      __attribute__((always_inline)) {
+    constexpr int C = 0;   // one fragment set, each fragment reloaded two gaps after its last read
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      chain_gap(g, 0);
+      valu_gap(g, 1, 1, 1, 0);
+    }
+    mid();
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      grad_gap(g, 1, C);
+      valu_gap(g, 0, 0, 1, 1);
+      if (g >= 2) tr_load(g - 2, C, slot, r0);
+      bgap(g);
+    }
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      chain_gap(g, 1);
+      valu_gap(g, 0, 1, 0, 0);
+      if (g < 2) tr_load(6 + g, C, slot, r0);
+      if (g >= 4) qa[g - 4] = qrow(nslot, nr0, g - 4);
+    }
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      grad_gap(g, 0, C);
+      valu_gap(g, 1, 0, 0, 1);
+      if (g == 0) NL = rcblk(nrc, 0, nr0);
+      if (g == 1) ND = rcblk(nrc, 1, nr0);
+      if (g >= 4) da[g - 4] = qrow(nslot + TILE_B, nr0, g - 4);
+    }
+  };
+
+  // prologue: tiles 0, 1, 2 in flight (5 memory operations per wave and tile); wait for tile 0, publish it
+  if constexpr (LCI_HS_STG == 0) {
+    dma_tile(0);
+    if (nqt > 1) dma_tile(1);
+    if (nqt > 2) dma_tile(2);
+    if (LCI_HS_PROBE == 2 && nqt > 3) dma_tile(3);   // probe: every ring slot holds real data
+    if (LCI_HS_PROBE == 2) hs_vmcnt<0>();
+    if (nqt > 2) hs_vmcnt<10>(); else if (nqt > 1) hs_vmcnt<5>(); else hs_vmcnt<0>();
+  } else {
+    load_tile(stg[0], 0);
+    hs_vmcnt<0>();
+    store_tile(stg[0], smem);
+    if (nqt > 1) load_tile(stg[1], 1);
+    if (nqt > 2) load_tile(stg[0], 2);
+  }
+  __syncthreads();
+  NL = rcblk(rcs, 0, 0);
+  ND = rcblk(rcs, 1, 0);
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    qa[ks] = qrow(smem, 0, ks);
+    da[ks] = qrow(smem + TILE_B, 0, ks);
+  }
+  if (LCI_HS_PROBE == 3) {   // probe: real data in every fragment, then no LDS reads in the loop
+#pragma unroll
+    for (int f = 0; f < 8; ++f) { tr_load(f, 0, smem, 0); tr_load(f, 1, smem, 32); }
+    probe_noread = true;
+  }
+  // one tile in ring slot t & 3 (a 4-tile unroll that made the slots compile-time spilled 32 VGPRs);
+  // register staging: tile t+1 is in set PAR ^ 1, which then takes tile t+3
+  auto tile = [&](auto PAR, int t) __attribute__((always_inline)) {
+    constexpr int P1 = decltype(PAR)::value ^ 1;
+    const int sl = t & (NSLOT - 1), nsl = (t + 1) & (NSLOT - 1);
+    char* slot = smem + sl * SLOT_B;
+    char* nslot = smem + nsl * SLOT_B;
+    char* rc = rcs + sl * RC_B;
+    char* nrc = rcs + nsl * RC_B;
+    // tile t+1 is published after seg A of half 1 (seg C of half 1 is its first reader): each wave waits for its
+    // own copy of tile t+1 (tile t+2's may stay in flight), then one barrier; tile t+3 goes into the slot of tile
+    // t-1, which every wave finished before this barrier
+    auto stage = [&]() __attribute__((always_inline)) {
+      if (t + 1 < nqt) {
+        if (t + 2 < nqt) hs_vmcnt<5>(); else hs_vmcnt<0>();
+        if constexpr (LCI_HS_STG == 1) store_tile(stg[P1], nslot);
+        if (LCI_HS_PROBE != 1 && LCI_HS_PROBE != 3) __syncthreads();
+        if constexpr (LCI_HS_STG == 1)
+          if (t + 3 < nqt && LCI_HS_PROBE != 2) load_tile(stg[P1], t + 3);
+      }
+    };
+    // LDS-DMA of tile t+3: one operation per MFMA gap of seg B after the barrier (a burst of five stalled the
+    // wave's issue for their whole issue cost)
+    auto dmas = [&](int g) __attribute__((always_inline)) {
+      if (LCI_HS_STG == 0 && LCI_HS_PROBE != 2 && LCI_HS_PROBE != 3 && g < 5)
+        if (t + 3 < nqt) dma_op(t + 3, g);
+    };
+    auto none = []() __attribute__((always_inline)) {};
+    auto none_g = [](int) __attribute__((always_inline)) {};
+    if constexpr (LCI_HS_V == 1) {
+      half_v1(std::integral_constant<int, 0>{}, slot, 0, slot, rc, 32, none, none_g);   // segs C / D: rows 32-63
+      half_v1(std::integral_constant<int, 1>{}, slot, 32, nslot, nrc, 0, stage, dmas);  // ... tile t+1's rows 0-31
+    } else {
+      half(std::integral_constant<int, 0>{}, slot, 0, slot, rc, 32, none, none_g);
+      half(std::integral_constant<int, 1>{}, slot, 32, nslot, nrc, 0, stage, dmas);
+    }
+  };
+  if constexpr (LCI_HS_STG == 0) {
+    for (int t = 0; t < nqt; ++t) tile(std::integral_constant<int, 0>{}, t);
+  } else {
+    for (int t = 0; t < nqt; t += 2) {
+      tile(std::integral_constant<int, 0>{}, t);
+      if (t + 1 < nqt) tile(std::integral_constant<int, 1>{}, t + 1);
+    }
+  }
+  // key block 1 of the last half: elements 8-15 (finishing 0-7), then its dV / dK
+#pragma unroll
+  for (int g = 0; g < 8; ++g) valu_gap(g, 1, 1, 1, 0);
+  HS_MUL(P[1][14], S[1][14]);
+  HS_MUL(P[1][15], S[1][15]);
+  asm volatile("s_nop 0" ::: "memory");
+  HS_CVT(pk[1][1][3], S[1][14], S[1][15]);
+  HS_CVT(dd[1][1][2], P[1][12], P[1][13]);
+  HS_CVT(dd[1][1][3], P[1][14], P[1][15]);
+  asm volatile("s_nop 1" ::: "memory");
+#pragma unroll
+  for (int g = 0; g < 8; ++g) grad_gap(g, 1, LCI_HS_V == 1 ? 0 : 1);   // the last half is a half 1 (set 1)
+  // the accumulators are read by VALU next: let the last MFMAs retire (the compiler cannot see their latency)
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+
+  const float sc = a.scale;
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+    const int key = kw0 + 32 * kb + r32;
+    if (key < L) {
+      bf16* dkp = a.dk + b * a.bs_dk + (long long)key * a.rs_dk + hh * a.hs;
+      bf16* dvp = a.dv + b * a.bs_dv + (long long)key * a.rs_dv + hh * a.hs;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          bf16x4 k4, v4;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            k4[j] = to_bf16(dk[db][kb][4 * g + j] * sc);
+            v4[j] = to_bf16(dv[db][kb][4 * g + j]);
+          }
+          *(bf16x4*)(dkp + 32 * db + 8 * g + 4 * h) = k4;
+          *(bf16x4*)(dvp + 32 * db + 8 * g + 4 * h) = v4;
+        }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------- backward: dQ kernel, v2
 // Work split of attn_bwd_dq_kernel (8 waves x 32 queries on the lane, key tiles of 64), restructured like the
 // v2 forward: buffer-load staging into a 3-slot LDS ring (K tile swizzled: read by rows for S^T and transposed
@@ -854,8 +1330,9 @@ __global__ __launch_bounds__(FW_NW * 64, 1) void attn_bwd_dq2_kernel(AttnArgs a)
       for (int j = 0; j < 8; ++j) qf[ks][j] = to_bf16(to_f32(qf[ks][j]) * a.c);  // scores in the exp2 domain
     }
     if (qrow < L) {
-      lse2 = a.lse2[((long long)b * a.H + hh) * L + qrow];
-      dlt = a.delta[((long long)b * a.H + hh) * L + qrow];
+      const float* ws = a.delta + ((long long)b * a.H + hh) * 2 * L;
+      lse2 = -ws[qrow];
+      dlt = -ws[L + qrow];
     }
   }
   f32x16 neg_lse, neg_dlt;
@@ -999,8 +1476,9 @@ __global__ __launch_bounds__(FW_NW * 64, 1) void attn_bwd_dq16_kernel(AttnArgs a
         for (int j = 0; j < 8; ++j) qf[qb][ks][j] = to_bf16(to_f32(qf[qb][ks][j]) * a.c);
       }
       if (q < L) {
-        lse2 = a.lse2[((long long)b * a.H + hh) * L + q];
-        dlt = a.delta[((long long)b * a.H + hh) * L + q];
+        const float* ws = a.delta + ((long long)b * a.H + hh) * 2 * L;
+        lse2 = -ws[q];
+        dlt = -ws[L + q];
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) { neg_lse[qb][i] = -lse2; neg_dlt[qb][i] = -dlt; }
@@ -1386,7 +1864,13 @@ extern "C" int lci_attn_bwd_stage(int stage, const void* qkv, const void* out, c
 #ifndef LCI_DKDV16
 #define LCI_DKDV16 1   // 16x16x32 dK/dV (default): 22.1 vs 22.6-22.8 ms for the 32x32x16 kernel, three same-box A/Bs
 #endif
-  if (stage < 0 || stage == 1) {
+#ifndef LCI_DKDV_HS
+#define LCI_DKDV_HS 1  // one-wave-per-SIMD placed-stream dK/dV kernel (attn_bwd_dkdv_hs_kernel)
+#endif
+  if ((stage < 0 || stage == 1) && LCI_DKDV_HS) {
+    hipLaunchKernelGGL(attn_bwd_dkdv_hs_kernel, dim3((L + HS_NW * 64 - 1) / (HS_NW * 64), H, B), dim3(HS_NW * 64), 0, s, a);
+    LCI_LAUNCH_CHECK();
+  } else if (stage < 0 || stage == 1) {
     if (LCI_DKDV16 && KB == 1)
       hipLaunchKernelGGL((attn_bwd_dkdv16_kernel<NW>), grid, dim3(NW * 64), 0, s, a);
     else
