@@ -53,8 +53,8 @@ extern "C" {
  * lci_resample1d_adj and the round-3 entry points below; 13: lci_conv3_fwd_split, lci_conv3_pack_weight,
  * lci_inorm_apply_res, lci_convup_interleave, lci_window_bias with either table optional; 14: lci_window_attn_fwd
  * takes the transposed table biasT, lci_window_attn_bwd's plain table only for windows of N > 384; 15:
- * lci_window_attn_bwd pad_ws; 16: lci_attn_bwd delta_ws is (B, H, 2, L): the negated row constants -lse2 | -delta). */
-#define LCI_ABI_VERSION 16
+ * lci_window_attn_bwd pad_ws; 16: lci_attn_bwd delta_ws is (B, H, 2, L): the negated row constants -lse2 | -delta; 17: lci_window_bwd_needs_plain). */
+#define LCI_ABI_VERSION 17
 const char* lci_last_error(void);
 int lci_abi_version(void);
 /* sha256 prefix of the sources the library was built from (build_lib.source_hash); the Python binding refuses a
@@ -108,6 +108,9 @@ int lci_window_attn_bwd(const void* qkv, const float* qkv_bias, const void* bias
                         float* pad_ws, void* dS, float* drpb, const int* geo, float scale, void* stream);
 long long lci_window_dS_elems(const int* geo);
 long long lci_window_pad_ws_elems(const int* geo);
+/* 1 if lci_window_attn_bwd needs the plain `bias` table for geo (the two-phase kernel: windows of more than 12 key
+ * blocks of 32 tokens), 0 if biasT alone suffices; -1 for an invalid geo. */
+int lci_window_bwd_needs_plain(const int* geo);
 /* Index maps of the grid mode (test/inspection entry; same device functions as the kernels), per window w < Bw and
  * window token n < N, int32 (Bw, N): src_row = token row (b, s0, s1[, s2]) flattened that the window token reads
  * and the output scatters to, -1 for a padded voxel (F.pad + roll(-shift) + window_partition, and their inverse);

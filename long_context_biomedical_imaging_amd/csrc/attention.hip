@@ -857,6 +857,10 @@ constexpr int HS_NW = 4;
 #define LCI_HS_PROBE 0   // timing probes (wrong results): 1 = no barrier, 2 = no tile staging after the prologue,
                          // 3 = no LDS traffic, staging or barrier in the loop, 4 = no VALU in the loop
 #endif
+#ifndef LCI_HS_STAMP
+#define LCI_HS_STAMP 0   // diagnostic build: s_memtime at every segment start of tiles 64-95 of workgroups 0-7 (dK/dV),
+                         // written to the dQ part of dqkv, which only the (not launched) dQ stage writes
+#endif
 #ifndef LCI_HS_V
 #define LCI_HS_V 2   // 1: first placement (conversions in pairs, single fragment set, LDS reads in segs B-D), for A/B
 #endif
@@ -893,6 +897,15 @@ template <int N>
 __device__ __forceinline__ void hs_vmcnt() {   // s_waitcnt vmcnt(N), lgkmcnt / expcnt untouched
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
+// Give a value an AGPR home (one copy, here): every later use is an asm "a" operand, so the allocator needs no copy
+// next to a (hazard-blind) asm MFMA that reads it
+#define HS_TO_AGPR(x) asm volatile("" : "=a"(x) : "0"(x))
+// the compiler loses track of x's value (an asm output): zero-initialised fragments and accumulators must not become
+// constants it rematerialises with a VALU move right next to the asm MFMA that reads them (it cannot see the hazard)
+#define HS_OPAQUE(x) asm volatile("" : "+v"(x))
+// keep x's registers allocated up to here: a chain's row-constant initial accumulator is read by the MFMA pipeline
+// after issue, so nothing may reuse those registers within the next seven wait states
+#define HS_KEEP(x) asm volatile("" ::"v"(x))
 #define HS_EXP(x) asm volatile("v_exp_f32 %0, %0" : "+v"(x))
 #define HS_MUL(p, e) asm volatile("v_mul_f32 %0, %1, %0" : "+v"(p) : "v"(e))
 #define HS_CVT(w, x0, x1) asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(w) : "v"(x0), "v"(x1))
@@ -905,6 +918,12 @@ __device__ __forceinline__ void hs_vmcnt() {   // s_waitcnt vmcnt(N), lgkmcnt / 
 #define HS_MFMA_C(d, A, B) \
   asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(A), "a"(B))
 
+#ifndef LCI_HS_AHOME
+#define LCI_HS_AHOME 1       // K / V fragments homed in AGPRs before the loop (0: compiler's choice; unsafe)
+#endif
+#ifndef LCI_HS_DMASPREAD
+#define LCI_HS_DMASPREAD 1   // one LDS-DMA issue per segment (0: tile t+3's five in seg B of half 1)
+#endif
 __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArgs a) {
   constexpr int TILE_B = KT * DH * 2;               // bytes of a Q or dO tile (128-B rows)
   constexpr int SLOT_B = 2 * TILE_B;                // Q | dO of one tile
@@ -923,6 +942,15 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
   const int h = lane >> 5, r32 = lane & 31;
   const int kw0 = blockIdx.x * (HS_NW * 64) + wave * 64;
   const int nqt = (L + KT - 1) / KT;
+  // diagnostic stamps: [workgroup][wave][tile - 64][stamp 0..9] (8 segment starts + before / after the barrier)
+  unsigned long long* stamps = (unsigned long long*)a.out;
+  int stamp_tile = -1;
+  auto stamp = [&](int k) __attribute__((always_inline)) {
+    if (LCI_HS_STAMP && stamp_tile >= 0) {
+      const unsigned long long tm = __builtin_amdgcn_s_memtime();
+      if (lane == 0) stamps[((blockIdx.x * 4 + wave) * 32 + stamp_tile) * 10 + k] = tm;
+    }
+  };
 
   // K^T / V^T as B operands: lane holds K[kw0 + 32kb + r32][16ks + 8h + j] (K prescaled into the exp2 domain)
   bf16x8 kf[2][4], vf[2][4];
@@ -949,6 +977,11 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
   // the K / V loads complete here: otherwise the compiler waits for them (vmcnt(0)) at their first use inside the
   // loop, where that wait would also drain every tile's in-flight staging loads (which it does not track)
   hs_vmcnt<0>();
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (LCI_HS_AHOME) { HS_TO_AGPR(kf[i][j]); HS_TO_AGPR(vf[i][j]); }
 
   // ---- staging by LDS-DMA, two tiles ahead: wave w copies rows 16w .. 16w+15 of the Q and dO tiles as 1-KB pieces
   // (8 rows x 128 B, lane l -> row l >> 3 of the piece, physical 16-B chunk l & 7, fetched from the logical chunk
@@ -1036,6 +1069,20 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
   u32x4 pk[2][2] = {}, dd[2][2] = {};    // [key block][k-step] bf16 P / dS packs (dword j = elements 2j, 2j+1)
   bf16x8 tdo[2][2][2] = {}, tq[2][2][2] = {};  // [set][d block][k-step] transposed dO / Q fragments: half p uses
                                               // set p & 1 (its kb1 products run in half p+1, beside p+1's reads)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    HS_OPAQUE(S[i]);
+    HS_OPAQUE(P[i]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      HS_TO_AGPR(dv[i][j]);
+      HS_TO_AGPR(dk[i][j]);
+      HS_OPAQUE(pk[i][j]);
+      HS_OPAQUE(dd[i][j]);
+#pragma unroll
+      for (int k = 0; k < 2; ++k) { HS_OPAQUE(tdo[i][j][k]); HS_OPAQUE(tq[i][j][k]); }
+    }
+  }
   bf16x8 qa[4], da[4];                   // Q / dO row fragments of the chains' half
 
   // VALU of gap g of a segment over elements 8e..8e+7 of key block kb: one exp2, one multiply, one conversion per
@@ -1105,37 +1152,45 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
   //   seg A, B: this half's transposed fragments into set C (set C^1 is still read by seg B's kb1 products)
   //   seg C: Q rows of half p+1 (gaps 2-5), -lse2 pieces 0-1 and dO rows 0-1 (gaps 6-7)
   //   seg D: -lse2 pieces 2-3, -delta pieces 0-3, dO rows 2-3
-  auto half = [&](auto CUR, const char* slot, int r0, const char* nslot, const char* nrc, int nr0, auto mid, auto bgap)
+  auto half = [&](auto CUR, const char* slot, int r0, const char* nslot, const char* nrc, int nr0, auto mid, auto sgap)
       __attribute__((always_inline)) {
     constexpr int C = decltype(CUR)::value;
     // seg A: chains kb0 || VALU kb1 (p-1) elements 8-15 (finishing its elements 0-7)
+    stamp(4 * C + 0);
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
       chain_gap(g, 0);
       valu_gap(g, 1, 1, 1, 0);
       if (!(g & 1)) tr_load(g >> 1, C, slot, r0);
+      sgap(0, g);
     }
     mid();
     // seg B: dV / dK kb1 (p-1, set C^1) || VALU kb0 elements 0-7 (finishing kb1 8-15)
+    stamp(4 * C + 1);
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
       grad_gap(g, 1, C ^ 1);
       valu_gap(g, 0, 0, 1, 1);
       if (!(g & 1)) tr_load(4 + (g >> 1), C, slot, r0);
-      bgap(g);
+      sgap(1, g);
     }
     // seg C: chains kb1 || VALU kb0 elements 8-15
+    stamp(4 * C + 2);
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
       chain_gap(g, 1);
       valu_gap(g, 0, 1, 0, 0);
+      if (g == 2) HS_KEEP(NL);
+      if (g == 6) HS_KEEP(ND);
       if (g >= 2 && g < 6 && LCI_HS_PROBE != 3) qa[g - 2] = qrow(nslot, nr0, g - 2);
       if (g >= 6) {
         rc_load(NL, nrc, 0, nr0, g - 6);
         if (LCI_HS_PROBE != 3) da[g - 6] = qrow(nslot + TILE_B, nr0, g - 6);
       }
+      sgap(2, g);
     }
     // seg D: dV / dK kb0 (set C) || VALU kb1 elements 0-7 (finishing kb0 8-15)
+    stamp(4 * C + 3);
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
       grad_gap(g, 0, C);
@@ -1143,11 +1198,12 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
       if (g < 2) rc_load(NL, nrc, 0, nr0, g + 2);
       else if (g < 6) rc_load(ND, nrc, 1, nr0, g - 2);
       else if (LCI_HS_PROBE != 3) da[g - 4] = qrow(nslot + TILE_B, nr0, g - 4);
+      sgap(3, g);
     }
   };
 
   auto half_v1 = [&](auto CUR, const char* slot, int r0, const char* nslot, const char* nrc, int nr0, auto mid,
-                     auto bgap)
+                     auto sgap)
       __attribute__((always_inline)) {
     constexpr int C = 0;   // one fragment set, each fragment reloaded two gaps after its last read
 #pragma unroll
@@ -1161,7 +1217,7 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
       grad_gap(g, 1, C);
       valu_gap(g, 0, 0, 1, 1);
       if (g >= 2) tr_load(g - 2, C, slot, r0);
-      bgap(g);
+      sgap(1, g);
     }
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
@@ -1184,10 +1240,17 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
   if constexpr (LCI_HS_STG == 0) {
     dma_tile(0);
     if (nqt > 1) dma_tile(1);
-    if (nqt > 2) dma_tile(2);
+    // tile 2's operations 3-4 come at segs A / B of tile 0 (the loop has no first-tile special case: a peeled copy
+    // would let the compiler fold the zero-initialised state into moves beside the asm MFMAs)
+    constexpr bool SPREAD = LCI_HS_DMASPREAD && LCI_HS_PROBE != 2 && LCI_HS_PROBE != 3;
+    if (nqt > 2) {
+      dma_op(2, 0); dma_op(2, 1); dma_op(2, 2);
+      if (!SPREAD) { dma_op(2, 3); dma_op(2, 4); }
+    }
     if (LCI_HS_PROBE == 2 && nqt > 3) dma_tile(3);   // probe: every ring slot holds real data
     if (LCI_HS_PROBE == 2) hs_vmcnt<0>();
-    if (nqt > 2) hs_vmcnt<10>(); else if (nqt > 1) hs_vmcnt<5>(); else hs_vmcnt<0>();
+    if (nqt > 2) { if (SPREAD) hs_vmcnt<8>(); else hs_vmcnt<10>(); }
+    else if (nqt > 1) hs_vmcnt<5>(); else hs_vmcnt<0>();
   } else {
     load_tile(stg[0], 0);
     hs_vmcnt<0>();
@@ -1213,6 +1276,7 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
   auto tile = [&](auto PAR, int t) __attribute__((always_inline)) {
     constexpr int P1 = decltype(PAR)::value ^ 1;
     const int sl = t & (NSLOT - 1), nsl = (t + 1) & (NSLOT - 1);
+    stamp_tile = (LCI_HS_STAMP && blockIdx.x < 8 && blockIdx.y == 0 && blockIdx.z == 0 && t >= 64 && t < 96) ? t - 64 : -1;
     char* slot = smem + sl * SLOT_B;
     char* nslot = smem + nsl * SLOT_B;
     char* rc = rcs + sl * RC_B;
@@ -1224,25 +1288,35 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
       if (t + 1 < nqt) {
         if (t + 2 < nqt) hs_vmcnt<5>(); else hs_vmcnt<0>();
         if constexpr (LCI_HS_STG == 1) store_tile(stg[P1], nslot);
+        stamp(8);
         if (LCI_HS_PROBE != 1 && LCI_HS_PROBE != 3) __syncthreads();
+        stamp(9);
         if constexpr (LCI_HS_STG == 1)
           if (t + 3 < nqt && LCI_HS_PROBE != 2) load_tile(stg[P1], t + 3);
       }
     };
-    // LDS-DMA of tile t+3: one operation per MFMA gap of seg B after the barrier (a burst of five stalled the
-    // wave's issue for their whole issue cost)
-    auto dmas = [&](int g) __attribute__((always_inline)) {
-      if (LCI_HS_STG == 0 && LCI_HS_PROBE != 2 && LCI_HS_PROBE != 3 && g < 5)
-        if (t + 3 < nqt) dma_op(t + 3, g);
+    // LDS-DMA: one operation per segment, at gap 3 (a DMA issue stalls the wave ~60-80 cycles; five in one
+    // segment doubled it): tile t+3's operations 0-2 in segments B, C, D of half 1 (after this tile's barrier),
+    // operations 3-4 in segments A, B of the next tile's half 0 (still before the next barrier, whose vmcnt(5)
+    // then leaves exactly them in flight; tile 2's come at tile 0, the prologue issued only its operations 0-2)
+    constexpr bool DMA_ON = LCI_HS_STG == 0 && LCI_HS_PROBE != 2 && LCI_HS_PROBE != 3;
+    auto dmas1 = [&](int seg, int g) __attribute__((always_inline)) {
+      if (LCI_HS_DMASPREAD) {
+        if (DMA_ON && g == 3 && seg >= 1 && t + 3 < nqt) dma_op(t + 3, seg - 1);
+      } else if (DMA_ON && seg == 1 && g < 5 && t + 3 < nqt) {
+        dma_op(t + 3, g);
+      }
+    };
+    auto dmas0 = [&](int seg, int g) __attribute__((always_inline)) {
+      if (LCI_HS_DMASPREAD && DMA_ON && g == 3 && seg < 2 && t + 2 < nqt) dma_op(t + 2, 3 + seg);
     };
     auto none = []() __attribute__((always_inline)) {};
-    auto none_g = [](int) __attribute__((always_inline)) {};
     if constexpr (LCI_HS_V == 1) {
-      half_v1(std::integral_constant<int, 0>{}, slot, 0, slot, rc, 32, none, none_g);   // segs C / D: rows 32-63
-      half_v1(std::integral_constant<int, 1>{}, slot, 32, nslot, nrc, 0, stage, dmas);  // ... tile t+1's rows 0-31
+      half_v1(std::integral_constant<int, 0>{}, slot, 0, slot, rc, 32, none, dmas0);    // segs C / D: rows 32-63
+      half_v1(std::integral_constant<int, 1>{}, slot, 32, nslot, nrc, 0, stage, dmas1); // ... tile t+1's rows 0-31
     } else {
-      half(std::integral_constant<int, 0>{}, slot, 0, slot, rc, 32, none, none_g);
-      half(std::integral_constant<int, 1>{}, slot, 32, nslot, nrc, 0, stage, dmas);
+      half(std::integral_constant<int, 0>{}, slot, 0, slot, rc, 32, none, dmas0);
+      half(std::integral_constant<int, 1>{}, slot, 32, nslot, nrc, 0, stage, dmas1);
     }
   };
   if constexpr (LCI_HS_STG == 0) {
@@ -1287,6 +1361,293 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
           }
           *(bf16x4*)(dkp + 32 * db + 8 * g + 4 * h) = k4;
           *(bf16x4*)(dvp + 32 * db + 8 * g + 4 * h) = v4;
+        }
+    }
+  }
+}
+
+// --------------------------------------- backward: dQ kernel, one wave per SIMD, placed MFMA / VALU / LDS stream
+// The dK/dV kernel's structure for dQ (query on the MFMA lane): a workgroup = 4 waves, a wave owns 64 queries (two
+// query blocks of 32, Q~ / dO fragments in AGPRs, -lse2 / -delta splats as the chains' initial accumulators, dQ^T in
+// AGPRs), key tiles of 64 keys (K, V; 128-B sw128 rows) arrive by LDS-DMA into a 4-slot ring two tiles ahead.
+// Per 32-key half-tile and wave: 24 MFMAs (S^T = K Q~^T and dP^T = V dO^T chains, 4 + 4 per query block;
+// dQ^T += K^T dS^T, 4 per block) against 32 exp2 + 32 multiplies + 16 conversions. MFMA order per half:
+//   gaps 0-7: chains of block 0 | 8-11: dQ^T of block 1 (previous half) | 12-19: chains of block 1 |
+//   20-23: dQ^T of block 0,
+// the VALU of each gap from DQ_SCHED (tools/gen_dq_sched.py: <= 2 exp2 and <= 4 VALU per gap, every dependency
+// distance and pack deadline checked); LDS reads one per gap: V rows of this half at gaps 0-3, the transposed K
+// fragments (dQ^T's A operand, shared by both blocks) at 12-19, K rows of the next half at 20-23.
+// Keys past L read as zero rows (dS^T there multiplies zero K); no masking.
+// gap  0: E1.8 E1.9
+// gap  1: M1.8 M1.9 C1.4 E1.10
+// gap  2: M1.10 E1.11 E1.12
+// gap  3: M1.11 M1.12 C1.5 E1.13
+// gap  4: M1.13 C1.6 E1.14 E1.15
+// gap  5: M1.14 M1.15 C1.7 E0.0
+// gap  6: E0.1 E0.2
+// gap  7: E0.3 E0.4
+// gap  8: E0.5 E0.6
+// gap  9: M0.0 M0.1 M0.2 M0.3
+// gap 10: C0.0 C0.1 M0.4 M0.5
+// gap 11: C0.2 M0.6 E0.7 E0.8
+// gap 12: M0.7 M0.8 C0.3 E0.9
+// gap 13: M0.9 C0.4 E0.10 E0.11
+// gap 14: M0.10 M0.11 C0.5 E0.12
+// gap 15: M0.12 E0.13 E0.14
+// gap 16: M0.13 M0.14 C0.6 E0.15
+// gap 17: E1.0 E1.1 M0.15 C0.7
+// gap 18: E1.2 E1.3
+// gap 19: E1.4 E1.5
+// gap 20: E1.6 E1.7
+// gap 21: M1.0 M1.1 M1.2 M1.3
+// gap 22: C1.0 C1.1 M1.4 M1.5
+// gap 23: C1.2 M1.6 M1.7 C1.3
+constexpr unsigned char DQ_SCHED[24][4] = {
+    {0x28, 0x29, 0xff, 0xff},
+    {0x68, 0x69, 0xa4, 0x2a},
+    {0x6a, 0x2b, 0x2c, 0xff},
+    {0x6b, 0x6c, 0xa5, 0x2d},
+    {0x6d, 0xa6, 0x2e, 0x2f},
+    {0x6e, 0x6f, 0xa7, 0x00},
+    {0x01, 0x02, 0xff, 0xff},
+    {0x03, 0x04, 0xff, 0xff},
+    {0x05, 0x06, 0xff, 0xff},
+    {0x40, 0x41, 0x42, 0x43},
+    {0x80, 0x81, 0x44, 0x45},
+    {0x82, 0x46, 0x07, 0x08},
+    {0x47, 0x48, 0x83, 0x09},
+    {0x49, 0x84, 0x0a, 0x0b},
+    {0x4a, 0x4b, 0x85, 0x0c},
+    {0x4c, 0x0d, 0x0e, 0xff},
+    {0x4d, 0x4e, 0x86, 0x0f},
+    {0x20, 0x21, 0x4f, 0x87},
+    {0x22, 0x23, 0xff, 0xff},
+    {0x24, 0x25, 0xff, 0xff},
+    {0x26, 0x27, 0xff, 0xff},
+    {0x60, 0x61, 0x62, 0x63},
+    {0xa0, 0xa1, 0x64, 0x65},
+    {0xa2, 0x66, 0x67, 0xa3}};
+
+#ifndef LCI_DQ_AHOME
+#define LCI_DQ_AHOME 1       // Q~ / dO fragments homed in AGPRs before the loop
+#endif
+#ifndef LCI_DQ_DMASPREAD
+#define LCI_DQ_DMASPREAD 1   // DMA issues at gaps 8 / 20 (half 1) and 6 / 18 (half 0); 0: gaps 6-8, 15 of half 1
+#endif
+__global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs a) {
+  constexpr int TILE_B = KT * DH * 2;               // bytes of a K or V tile (128-B rows)
+  constexpr int SLOT_B = 2 * TILE_B;                // K | V
+  constexpr int NSLOT = 4;
+  static_assert(NSLOT * SLOT_B == 65536, "ring reachable by DS immediates");
+  __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT_B];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hh = blockIdx.y, b = blockIdx.z;
+  const int L = a.L;
+  const int h = lane >> 5, r32 = lane & 31;
+  const int qw0 = blockIdx.x * (HS_NW * 64) + wave * 64;
+  const int nkt = (L + KT - 1) / KT;
+
+  // Q~ / dO as B operands: lane holds X[qw0 + 32qb + r32][16ks + 8h + j] (Q prescaled into the exp2 domain);
+  // -lse2 / -delta of the lane's query splatted over a chain's 16 accumulator registers
+  bf16x8 qf[2][4], df[2][4];
+  f32x16 NL[2], ND[2];
+  {
+    const bf16* qp = a.q + b * a.bs_q + hh * a.hs;
+    const bf16* dop = a.dout + b * a.bs_do + hh * a.hs;
+    const float* ws = a.delta + ((long long)b * a.H + hh) * 2 * L;
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const int q = qw0 + 32 * qb + r32;
+      float nl = 0.f, nd = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        if (q < L) {
+          qf[qb][ks] = *(const bf16x8*)(qp + (long long)q * a.rs_q + 16 * ks + 8 * h);
+          df[qb][ks] = *(const bf16x8*)(dop + (long long)q * a.rs_do + 16 * ks + 8 * h);
+        } else {
+          qf[qb][ks] = bf16x8{};
+          df[qb][ks] = bf16x8{};
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[qb][ks][j] = to_bf16(to_f32(qf[qb][ks][j]) * a.c);
+      }
+      if (q < L) { nl = ws[q]; nd = ws[L + q]; }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { NL[qb][i] = nl; ND[qb][i] = nd; }
+    }
+  }
+  hs_vmcnt<0>();   // (see the dK/dV kernel: no compiler vmcnt wait inside the loop)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (LCI_DQ_AHOME) { HS_TO_AGPR(qf[i][j]); HS_TO_AGPR(df[i][j]); }
+
+  // ---- K / V tiles by LDS-DMA, two tiles ahead (wave w: rows 16w .. 16w+15 of each, 1-KB pieces of 8 rows)
+  const int rs2k = a.rs_k * 2, rs2v = a.rs_v * 2;
+  const rsrc_t rk = make_rsrc(a.k + b * a.bs_k + hh * a.hs, (uint32_t)(L - 1) * (uint32_t)rs2k + DH * 2);
+  const rsrc_t rv = make_rsrc(a.v + b * a.bs_v + hh * a.hs, (uint32_t)(L - 1) * (uint32_t)rs2v + DH * 2);
+  const int prow = lane >> 3;
+  const int pch0 = (lane & 7) ^ ((prow >> 2) | ((prow >> 1) & 1) << 2);
+  const int pch1 = (lane & 7) ^ ((2 + (prow >> 2)) | ((prow >> 1) & 1) << 2);
+  const int dk0 = (16 * wave + prow) * rs2k + 16 * pch0, dk1 = (16 * wave + 8 + prow) * rs2k + 16 * pch1;
+  const int dv0 = (16 * wave + prow) * rs2v + 16 * pch0, dv1 = (16 * wave + 8 + prow) * rs2v + 16 * pch1;
+  const unsigned lds0 = (unsigned)(uintptr_t)(LCI_LDS char*)smem;
+  auto dma_op = [&](int t, int i) __attribute__((always_inline)) {   // operation i (0-3) of tile t
+    const unsigned sb = lds0 + (unsigned)((t & (NSLOT - 1)) * SLOT_B);
+    if (i == 0) hs_dma16(rk, dk0, t * KT * rs2k, sb + 2048 * wave);
+    if (i == 1) hs_dma16(rk, dk1, t * KT * rs2k, sb + 2048 * wave + 1024);
+    if (i == 2) hs_dma16(rv, dv0, t * KT * rs2v, sb + TILE_B + 2048 * wave);
+    if (i == 3) hs_dma16(rv, dv1, t * KT * rs2v, sb + TILE_B + 2048 * wave + 1024);
+  };
+
+  auto row = [&](const char* tile, int r0, int ks) __attribute__((always_inline)) {
+    return *(const bf16x8*)(tile + 2 * sw128(r0 + r32, 16 * ks + 8 * h));
+  };
+  auto trh = [&](const char* tile, int r0, int S, int c0, int part) __attribute__((always_inline)) {
+    const int rw = r0 + 16 * S + 4 * h + ((lane & 15) >> 2) + 8 * part;
+    const int col = c0 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+    return lds_tr4((const bf16*)(tile + 2 * sw128(rw, col)));
+  };
+
+  f32x16 dq[2][2];             // [d block][query block]: dQ^T, lane = query, rows d = 32db + (i&3) + 8(i>>2) + 4h
+  f32x16 S[2], P[2];           // [query block]: S~^T - lse2, dP^T - delta (rows = the half's 32 keys)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    S[i] = P[i] = f32x16{};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) dq[i][j] = f32x16{};
+  }
+  u32x4 dsp[2][2] = {};        // [query block][k-step] bf16 dS^T packs
+  bf16x4 ktr[2][2][2] = {};    // [d block][k-step][half of the fragment] transposed K (keys as the k index)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    HS_OPAQUE(S[i]);
+    HS_OPAQUE(P[i]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      HS_TO_AGPR(dq[i][j]);
+      HS_OPAQUE(dsp[i][j]);
+      HS_OPAQUE(ktr[i][j][0]);
+      HS_OPAQUE(ktr[i][j][1]);
+    }
+  }
+  bf16x8 kr[4], vr[4];         // K / V row fragments (A operands of the chains)
+
+  auto valu_op = [&](unsigned char c, int only_qb) __attribute__((always_inline)) {
+    if (c == 0xFF) return;
+    const int kind = c >> 6, qb = (c >> 5) & 1, i = c & 31;
+    if (only_qb >= 0 && qb != only_qb) return;
+    if (kind == 0) HS_EXP(S[qb][i]);
+    else if (kind == 1) HS_MUL(P[qb][i], S[qb][i]);
+    else HS_CVT(dsp[qb][i >> 2][i & 3], P[qb][2 * i], P[qb][2 * i + 1]);
+  };
+  auto dq_mfma = [&](int k, int qb) __attribute__((always_inline)) {   // k = 0..3: (d block k & 1, k-step k >> 1)
+    const int db = k & 1, s2 = k >> 1;
+    HS_MFMA_G(dq[db][qb], cat44(ktr[db][s2][0], ktr[db][s2][1]), __builtin_bit_cast(bf16x8, dsp[qb][s2]));
+  };
+  auto mfma_gap = [&](int g) __attribute__((always_inline)) {
+    if (g < 4) {
+      if (g == 0) HS_MFMA_C0(S[0], kr[0], qf[0][0], NL[0]); else HS_MFMA_C(S[0], kr[g], qf[0][g]);
+    } else if (g < 8) {
+      if (g == 4) HS_MFMA_C0(P[0], vr[0], df[0][0], ND[0]); else HS_MFMA_C(P[0], vr[g - 4], df[0][g - 4]);
+    } else if (g < 12) {
+      dq_mfma(g - 8, 1);
+    } else if (g < 16) {
+      if (g == 12) HS_MFMA_C0(S[1], kr[0], qf[1][0], NL[1]); else HS_MFMA_C(S[1], kr[g - 12], qf[1][g - 12]);
+    } else if (g < 20) {
+      if (g == 16) HS_MFMA_C0(P[1], vr[0], df[1][0], ND[1]); else HS_MFMA_C(P[1], vr[g - 16], df[1][g - 16]);
+    } else {
+      dq_mfma(g - 20, 0);
+    }
+  };
+
+  // One 32-key half (rows r0 of `slot`); gaps 20-23 read the K rows of the next half (rows nr0 of `nslot`).
+  auto half = [&](const char* slot, int r0, const char* nslot, int nr0, auto hook) __attribute__((always_inline)) {
+#pragma unroll
+    for (int g = 0; g < 24; ++g) {
+      mfma_gap(g);
+      // gap 9's multiplies read the dP^T chain of block 0 (last MFMA at gap 7): 12 wait states by instruction count
+      if (g == 9) asm volatile("s_nop 4" ::: "memory");
+#pragma unroll
+      for (int o = 0; o < 4; ++o) valu_op(DQ_SCHED[g][o], -1);
+      if (g < 4) vr[g] = row(slot + TILE_B, r0, g);
+      else if (g >= 12 && g < 20) {
+        const int f = (g - 12) >> 1, part = (g - 12) & 1;   // fragment f = (d block f & 1, k-step f >> 1)
+        ktr[f & 1][f >> 1][part] = trh(slot, r0, f >> 1, 32 * (f & 1), part);
+      } else if (g >= 20) kr[g - 20] = row(nslot, nr0, g - 20);
+      hook(g);
+    }
+  };
+
+  // prologue: tiles 0, 1, 2 in flight; wait for tile 0, publish it; K rows of half 0
+  dma_op(0, 0); dma_op(0, 1); dma_op(0, 2); dma_op(0, 3);
+  if (nkt > 1) { dma_op(1, 0); dma_op(1, 1); dma_op(1, 2); dma_op(1, 3); }
+  if (nkt > 2) {   // (spread: tile 2's operations 2-3 at gaps 6 / 18 of tile 0, as for every later tile)
+    dma_op(2, 0); dma_op(2, 1);
+    if (!LCI_DQ_DMASPREAD) { dma_op(2, 2); dma_op(2, 3); }
+  }
+  if (nkt > 2) { if (LCI_DQ_DMASPREAD) hs_vmcnt<6>(); else hs_vmcnt<8>(); }
+  else if (nkt > 1) hs_vmcnt<4>(); else hs_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) kr[ks] = row(smem, 0, ks);
+
+  for (int t = 0; t < nkt; ++t) {
+    char* slot = smem + (t & (NSLOT - 1)) * SLOT_B;
+    char* nslot = smem + ((t + 1) & (NSLOT - 1)) * SLOT_B;
+    // tile t+1 is published at gap 6 of half 1 (its first reader: the K rows at gaps 20-23); tile t+3's DMA goes
+    // into the slot of tile t-1 (last read by half 1 of tile t-1, before this barrier), one operation per gap
+    auto stage = [&](int g) __attribute__((always_inline)) {
+      if (t + 1 < nkt && g == 6) {
+        if (t + 2 < nkt) hs_vmcnt<4>(); else hs_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+      }
+      // tile t+3's operations 0-1 at gaps 8 / 20 of half 1 (after this barrier), 2-3 at gaps 6 / 18 of the next
+      // tile's half 0 (before its barrier, whose vmcnt(4) then leaves exactly them in flight): one DMA issue per
+      // 12 gaps (each stalls the wave's issue ~60-80 cycles)
+      if (LCI_DQ_DMASPREAD) {
+        if (t + 3 < nkt && (g == 8 || g == 20)) dma_op(t + 3, g == 8 ? 0 : 1);
+      } else if (t + 3 < nkt && t + 1 < nkt) {
+        if (g == 6) dma_op(t + 3, 0);
+        if (g == 7) dma_op(t + 3, 1);
+        if (g == 8) dma_op(t + 3, 2);
+        if (g == 15) dma_op(t + 3, 3);
+      }
+    };
+    auto stage0 = [&](int g) __attribute__((always_inline)) {
+      if (LCI_DQ_DMASPREAD && t + 2 < nkt && (g == 6 || g == 18)) dma_op(t + 2, g == 6 ? 2 : 3);
+    };
+    half(slot, 0, slot, 32, stage0);
+    half(slot, 32, nslot, 0, stage);
+  }
+  // query block 1 of the last half: its remaining VALU (wrapped into gaps 0-5) and its dQ^T
+#pragma unroll
+  for (int g = 0; g < 12; ++g) {
+#pragma unroll
+    for (int o = 0; o < 4; ++o) valu_op(DQ_SCHED[g][o], 1);
+    if (g >= 8) {
+      asm volatile("s_nop 1" ::: "memory");
+      dq_mfma(g - 8, 1);
+    }
+  }
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+
+  const float sc = a.scale;
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int q = qw0 + 32 * qb + r32;
+    if (q < L) {
+      bf16* dqp = a.out + b * a.bs_out + (long long)q * a.rs_out + hh * a.hs;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          bf16x4 w;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) w[j] = to_bf16(dq[db][qb][4 * g + j] * sc);
+          *(bf16x4*)(dqp + 32 * db + 8 * g + 4 * h) = w;
         }
     }
   }
@@ -1880,7 +2241,13 @@ extern "C" int lci_attn_bwd_stage(int stage, const void* qkv, const void* out, c
 #ifndef LCI_DQ16
 #define LCI_DQ16 0     // 16x16x32 dQ: parity-green, 16.7-17.0 vs 16.7-17.0 ms (within noise), not adopted
 #endif
-  if (stage < 0 || stage == 2) {
+#ifndef LCI_DQ_HS
+#define LCI_DQ_HS 1    // one-wave-per-SIMD placed-stream dQ kernel (attn_bwd_dq_hs_kernel)
+#endif
+  if ((stage < 0 || stage == 2) && LCI_DQ_HS) {
+    hipLaunchKernelGGL(attn_bwd_dq_hs_kernel, dim3((L + HS_NW * 64 - 1) / (HS_NW * 64), H, B), dim3(HS_NW * 64), 0, s, a);
+    LCI_LAUNCH_CHECK();
+  } else if (stage < 0 || stage == 2) {
     const dim3 gq((L + FW_NW * 32 - 1) / (FW_NW * 32), H, B);
     if (LCI_DQ16)
       hipLaunchKernelGGL(attn_bwd_dq16_kernel, gq, dim3(FW_NW * 64), 0, s, a);

@@ -1073,6 +1073,16 @@ extern "C" int lci_window_attn_bwd(const void* qkv, const float* qkv_bias, const
   return 0;
 }
 
+// 1 when lci_window_attn_bwd runs the two-phase kernel for this geometry (windows of more than WBWD1_MAXW key blocks,
+// or LCI_WIN_BWD1=0), which needs the plain query-major table beside biasT; 0 for the single-phase kernel; -1 bad geo
+extern "C" int lci_window_bwd_needs_plain(const int* geo) {
+  WinArgs a{};
+  if (win_fill(a, geo, 1.f)) return -1;
+  const char* e = getenv("LCI_WIN_BWD1");
+  const int bwd1_env = e ? atoi(e) : 1;
+  return (bwd1_env && a.nkt <= WBWD1_MAXW) ? 0 : 1;
+}
+
 extern "C" long long lci_window_pad_ws_elems(const int* geo) {
   WinArgs a{};
   if (win_fill(a, geo, 1.f)) return -1;

@@ -296,7 +296,9 @@ def dwconv_silu_pair(xz, wx, bx, wz, bz):
     _lib.require_gpu(xz)
     if xz.dtype not in _DT:
         xz = xz.float()
-    return _DWConvSiLUPair.apply(xz, wx, bx, wz, bz)
+    xs, yz = _DWConvSiLUPair.apply(xz, wx, bx, wz, bz)
+    yz._lci_z_half_only = True   # its backward reads only the z half of yz's gradient (see selective_scan_cl)
+    return xs, yz
 
 
 class _SelectiveScanCL(torch.autograd.Function):
@@ -331,6 +333,7 @@ class _SelectiveScanCL(torch.autograd.Function):
         if need_grad:
             ctx.save_for_backward(u, delta, Af, Bm, Cm, Dv, bv, sdt, ckpt)
         ctx.tc, ctx.softplus = tc, softplus
+        ctx.z_half_only = getattr(yz, "_lci_z_half_only", False)
         ctx.has_D, ctx.has_b = D is not None, delta_bias is not None
         # final state x_L = exp(A sum(dt) over the last chunk) xinit_last + xend_last (return_last_state)
         last = torch.exp(Af[None] * sdt[:, -1, :, None]) * xinit[:, -1] + xend[:, -1]
@@ -365,9 +368,12 @@ class _SelectiveScanCL(torch.autograd.Function):
             dBC.data_ptr(), dA.data_ptr(), dD.data_ptr(), db.data_ptr(), strides, B, L, Dx, N, tc,
             int(ctx.softplus), sdt.data_ptr(), ckpt.data_ptr(), gl.data_ptr(), gin.data_ptr(), _lib.stream_of(u)))
         # grad of yz: its first half was overwritten by y (zero gradient there), its second half is the SiLU(conv z)
-        # operand of the out_proj input. yz's only producer / consumer pair is dwconv_silu_pair -> this op, and
-        # _DWConvSiLUPair.backward reads only the z half (column offset C): pass gyz through as is instead of a
-        # clone + zero of the x half (a full (B, L, 2 Dx) copy, 0.6 ms per C5 layer).
+        # operand of the out_proj input. When yz came from dwconv_silu_pair (tagged there), whose backward reads
+        # only the z half (column offset C), gyz passes through as is instead of a clone + zero of the x half (a
+        # full (B, L, 2 Dx) copy, 0.6 ms per C5 layer); any other producer gets the exact gradient.
+        if not ctx.z_half_only:
+            gyz = gyz.clone()
+            gyz[..., :Dx] = 0
         if ctx.bc_joint:   # autograd casts the f32 sums to the input's bf16 (what .to(Bm.dtype) did)
             return du, dd, dA, dBC, None, dD if ctx.has_D else None, db if ctx.has_b else None, gyz, None
         return (du, dd, dA, dBC[..., :N].to(Bm.dtype), dBC[..., N:].to(Cm.dtype), dD if ctx.has_D else None,
@@ -571,9 +577,9 @@ class _WindowAttention(torch.autograd.Function):
             n_el = _lib.load().lci_window_dS_elems(g)
             dS = torch.empty(int(n_el), device=qkv.device, dtype=torch.bfloat16)
             drpb = torch.empty(H, N, N, **f32)
-        # the plain (query-major) table only for the two-phase kernel: windows of more than 12 key blocks
+        # the plain (query-major) table only for the two-phase kernel (the library says which kernel runs)
         tab = None
-        if -(-N // 32) > 12 or os.environ.get("LCI_WIN_BWD1", "1") == "0":
+        if _lib.load().lci_window_bwd_needs_plain(g):
             tab, _ = _window_bias(rp, mk, geo)
         KernelTimer.run("window_attn_bwd", 8.0 * Bw * H * N * N * 32, qkv, lambda: _lib.call(
             "lci_window_attn_bwd", qkv.data_ptr(), _lib.ptr(bf), _lib.ptr(tab), tabT.data_ptr(), int(mk is not None),

@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""Generate the VALU placement of the one-wave-per-SIMD dQ kernel (csrc/attention.hip, attn_bwd_dq_hs_kernel).
+
+Per 32-key half-tile a wave issues 24 v_mfma_f32_32x32x16_bf16 in the order
+  gaps 0-7: S^T (0-3) / dP^T (4-7) chains of query block 0 | 8-11: dQ^T of block 1 (previous half) |
+  12-19: chains of block 1 | 20-23: dQ^T of block 0,
+and per query block 40 VALU ops: 16 exp2 (E), 16 multiplies dS = P dP (M), 8 bf16 pair conversions (C). The
+schedule is periodic (24 gaps); block 1's ops wrap into the next half. Rules: E one gap after the S chain's last
+MFMA, M two gaps after the dP chain's last MFMA and in a later gap than its E, C after both M of its pair; at most
+2 exps and 4 VALU ops per gap; a block's pack of elements 0-7 (C 0-3) is complete one gap before its first dQ^T
+MFMA, elements 8-15 (C 4-7) one gap before its third. Output (stdout): the C++ table DQ_SCHED[24][4] of op codes
+(kind << 6 | block << 5 | index; 0xff = none); the placement is listed on stderr.
+"""
+import sys
+
+NG = 24
+START_E = {0: 5, 1: 17}      # S chains at gaps 0-3 / 12-15
+START_M = {0: 9, 1: 21}      # dP chains at gaps 4-7 / 16-19
+DQ = {0: 20, 1: 8 + NG}      # first dQ^T gap that reads the block's packs
+
+
+def main():
+    cap_e = [0] * NG
+    slots = [[] for _ in range(NG)]
+    placed = {}
+    for qb in (1, 0):        # block 1 wraps into the next half: place it first
+        tE, tM, tC = {}, {}, {}
+        g = START_E[qb]
+        while len(tC) < 8:
+            gi = g % NG
+            s = slots[gi]
+            for j in range(8):                       # conversions first: they free the pipeline tail
+                if j not in tC and 2 * j + 1 in tM and len(s) < 4:
+                    tC[j] = g
+                    s.append(("C", qb, j))
+            for e in range(16):
+                if e in tE and e not in tM and tE[e] < g and g >= START_M[qb] and len(s) < 4:
+                    tM[e] = g
+                    s.append(("M", qb, e))
+            for j in range(8):
+                if j not in tC and 2 * j + 1 in tM and len(s) < 4:
+                    tC[j] = g
+                    s.append(("C", qb, j))
+            for e in range(16):
+                if e not in tE and cap_e[gi] < 2 and len(s) < 4:
+                    tE[e] = g
+                    cap_e[gi] += 1
+                    s.append(("E", qb, e))
+            g += 1
+            assert g < START_E[qb] + 2 * NG, "does not fit"
+        assert max(tC[j] for j in range(4)) < DQ[qb], (qb, tC)
+        assert max(tC[j] for j in range(4, 8)) < DQ[qb] + 2, (qb, tC)
+        placed[qb] = (tE, tM, tC)
+    code = {"E": 0, "M": 1, "C": 2}
+    rows = []
+    for g, s in enumerate(slots):
+        print(f"// gap {g:2d}: " + " ".join(f"{k}{qb}.{i}" for k, qb, i in s), file=sys.stderr)
+        ops = [(code[k] << 6) | (qb << 5) | i for k, qb, i in s] + [0xFF] * (4 - len(s))
+        rows.append("{" + ", ".join(f"0x{o:02x}" for o in ops) + "}")
+    print("constexpr unsigned char DQ_SCHED[24][4] = {\n    " + ",\n    ".join(rows) + "};")
+
+
+if __name__ == "__main__":
+    main()
