@@ -922,8 +922,8 @@ __device__ __forceinline__ void hs_vmcnt() {   // s_waitcnt vmcnt(N), lgkmcnt / 
 #define LCI_HS_AHOME 1       // K / V fragments homed in AGPRs before the loop (0: compiler's choice; unsafe)
 #endif
 #ifndef LCI_HS_DMASPREAD
-#define LCI_HS_DMASPREAD 1   // one LDS-DMA issue per segment (0: tile t+3's five in seg B of half 1)
-#endif
+#define LCI_HS_DMASPREAD 0   // 1: one LDS-DMA issue per segment (21.3 ms vs 20.7 ms for tile t+3's five in seg B
+#endif                       // of half 1, same box)
 __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArgs a) {
   constexpr int TILE_B = KT * DH * 2;               // bytes of a Q or dO tile (128-B rows)
   constexpr int SLOT_B = 2 * TILE_B;                // Q | dO of one tile

@@ -31,11 +31,17 @@ HIP_CONV_2D = os.environ.get("LCI_HIP_CONV_2D", "1") != "0"
 HIP_CONV_3D = os.environ.get("LCI_HIP_CONV_3D", "1") != "0"
 
 
+def _hip(x, flag):
+    """The HIP conv / instance-norm path computes bf16 operands with f32 accumulation and returns bf16: it is the
+    autocast (use_amp) path. An f32 model run without autocast keeps the reference's f32 convolutions (torch)."""
+    return flag and x.is_cuda and (x.dtype == torch.bfloat16 or torch.is_autocast_enabled("cuda"))
+
+
 class Conv3x3(nn.Conv3d):
     """nn.Conv3d(cin, cout, 3, 1, padding=1, bias=False) computed by the HIP conv3 kernel."""
 
     def forward(self, x):
-        if not HIP_CONV_3D:
+        if not _hip(x, HIP_CONV_3D):
             return super().forward(x)
         return kernels.conv3(x, self.weight)
 
@@ -44,7 +50,7 @@ class Conv3x3_2d(nn.Conv2d):
     """nn.Conv2d(cin, cout, 3, 1, padding=1, bias=False) computed by the HIP conv3 kernel (D = 1)."""
 
     def forward(self, x):
-        if not HIP_CONV_2D:
+        if not _hip(x, HIP_CONV_2D):
             return super().forward(x)
         return kernels.conv3(x, self.weight)
 
@@ -123,8 +129,25 @@ class ConvUp_2d(nn.ConvTranspose2d):
         return _up_gemm(x, self.weight, self.bias, self.kernel_size, skip)
 
 
+class Convolution(nn.Module):
+    """MONAI 1.3 Convolution without act / norm / dropout: the conv layer under `.conv`, so the parameters carry the
+    reference's state_dict keys (`<block>.conv1.conv.weight`, `<up>.transp_conv.conv.weight`, ...)."""
+
+    def __init__(self, conv):
+        super().__init__()
+        self.conv = conv
+
+    def forward(self, *args):
+        return self.conv(*args)
+
+
 def _conv(nd, cin, cout, k, s, transposed=False, bias=False):
-    """MONAI get_conv_layer(conv_only=True): padding (k - s + 1) // 2, output_padding 2p + s - k (per axis)."""
+    """MONAI get_conv_layer(conv_only=True): padding (k - s + 1) // 2, output_padding 2p + s - k (per axis), the
+    layer wrapped as MONAI's Convolution."""
+    return Convolution(_conv_layer(nd, cin, cout, k, s, transposed, bias))
+
+
+def _conv_layer(nd, cin, cout, k, s, transposed=False, bias=False):
     if isinstance(k, (tuple, list)) or isinstance(s, (tuple, list)):
         k = tuple(k) if isinstance(k, (tuple, list)) else (k,) * nd
         s = tuple(s) if isinstance(s, (tuple, list)) else (s,) * nd
@@ -169,10 +192,10 @@ class UnetResBlock(nn.Module):
 
         # channels-last HIP path: the convs are the HIP conv3 / GEMM forms and the instance norms (+ LeakyReLU)
         # the lci_inorm kernels, so the block never round-trips through NCDHW (2-D: only with HIP_CONV_2D)
-        self.fused = isinstance(self.conv1, (Conv3x3, Conv3x3_2d)) and cout % 8 == 0
+        self.fused = isinstance(self.conv1.conv, (Conv3x3, Conv3x3_2d)) and cout % 8 == 0
 
     def forward(self, inp):
-        if self.fused and inp.is_cuda and (HIP_CONV_3D if inp.dim() == 5 else HIP_CONV_2D):
+        if self.fused and _hip(inp, HIP_CONV_3D if inp.dim() == 5 else HIP_CONV_2D):
             out = kernels.instance_norm_act(self.conv1(inp), True)
             c2 = self.conv2(out)
             r = self.conv3(inp) if self.downsample else inp
@@ -209,8 +232,8 @@ class UnetrUpBlock(nn.Module):
         self.conv_block = UnetResBlock(nd, cout + cout, cout, k, 1)
 
     def forward(self, inp, skip):
-        if isinstance(self.transp_conv, (ConvUp, ConvUp_2d)):
-            return self.conv_block(self.transp_conv(inp, skip))   # up-sampling + cat in one pass
+        if isinstance(self.transp_conv.conv, (ConvUp, ConvUp_2d)):
+            return self.conv_block(self.transp_conv.conv(inp, skip))   # up-sampling + cat in one pass
         return self.conv_block(torch.cat((self.transp_conv(inp), skip), dim=1))
 
 
@@ -311,7 +334,7 @@ class ViTUNETR(nn.Module):
         if p3[1] != p3[2] or p3[1] not in table:
             raise ValueError(f"ViT UNETR patch size {p3} not yet supported")
         (n2, n3, n4), (d1, d2, d3, d4) = table[p3[1]]
-        self.encoder1 = UnetResBlock(nd, cin, fs, 3, 1)
+        self.encoder1 = UnetrBasicBlock(nd, cin, fs, 3, 1)
         self.encoder2 = UnetrPrUpBlock(nd, hidden, fs * 2, n2, 3, 2)
         self.encoder3 = UnetrPrUpBlock(nd, hidden, fs * 4, n3, 3, 2)
         self.encoder4 = UnetrPrUpBlock(nd, hidden, fs * 8, n4, 3, 2)
@@ -387,14 +410,14 @@ class ConvK3(nn.Conv3d):
     """nn.Conv3d(cin, cout, 3, padding=1[, bias]) on the HIP conv3 kernel (any cout, optional bias)."""
 
     def forward(self, x):
-        if not HIP_CONV_3D:
+        if not _hip(x, HIP_CONV_3D):
             return super().forward(x)
         return kernels.conv3(x, self.weight, self.bias).contiguous()
 
 
 class ConvK3_2d(nn.Conv2d):
     def forward(self, x):
-        if not HIP_CONV_2D:
+        if not _hip(x, HIP_CONV_2D):
             return super().forward(x)
         y = kernels.conv3(x, self.weight, self.bias)
         return y if _is_cl(x) else y.contiguous()   # channels-last in -> channels-last out (UPERNET_CL)

@@ -87,3 +87,84 @@ def test_product_train_step_vs_reference():
         assert e < 5e-2, f"{k}: update rel err {e:.3e}"
         checked += 1
     assert checked >= 20
+
+
+@pytest.mark.parametrize("amp", [False, True])
+def test_product_adam_step_vs_reference(amp):
+    """The recipes' step: TrainStep with Adam (betas 0.9 / 0.95, lr 1e-4; optim_base.py:86-87, projects/run_*.sh:36-37)
+    against two reference Adam steps (tools/gen_golden.py:train_step_adam, fp32 on CPU). Here in fp32 and under the
+    product's bf16 autocast (use_amp; no GradScaler with bf16). Adam's first updates are close to lr * sign(g) per
+    element, so where the reference gradient is tiny the update direction is decided by rounding noise: the update
+    (post - pre) is compared element by element on the elements whose reference gradients at both steps exceed 10 %
+    of the tensor's RMS (rel-L2 <= 3e-2 fp32 / 6e-2 autocast), and its sign agrees on >= 97 % (fp32) / 95 %
+    (autocast) of the elements whose gradients exceed 1 % of the RMS. Losses within 5e-3 / 2e-2 relative."""
+    from long_context_biomedical_imaging_amd import config, model_base, trainer
+    g = Golden("train_step_adam")
+    args = ["--encoder_name", "ViT", "--ViT.size", "custom", "--ViT.hidden_size", "128", "--ViT.mlp_dim", "256",
+            "--ViT.num_layers", "2", "--ViT.num_heads", "2", "--ViT.patch_size", "2", "--height", "16", "--width", "16",
+            "--task_type", "class", "--decoder_name", "ViTLinear", "--no_out_channel", "3", "--optim_type", "adam",
+            "--optim.lr", "1e-4", "--optim.beta1", "0.9", "--optim.beta2", "0.95", "--loss_func", "CrossEntropy"]
+    cfg = config.parse_config(args + (["--use_amp"] if amp else []))
+    m = model_base.EncoderDecoderModel(cfg, "ViT", "ViTLinear", 1, 3)
+    m.load_state_dict(g.sd())
+    dev = torch.device("cuda", 0)
+    m = m.to(dev).train()
+    pre = {k: v.detach().double().cpu().clone() for k, v in m.state_dict().items()}
+    step = trainer.TrainStep(m, cfg, dev, ddp=False)
+    assert isinstance(step.optim, torch.optim.Adam)
+    for i in range(2):
+        loss = step.step(g.t(f"in/x{i}").to(dev), g.t(f"in/y{i}").to(dev)).item()
+        ref = g.scalar(f"out/loss{i}")
+        assert abs(loss - ref) <= (2e-2 if amp else 5e-3) * abs(ref), (i, loss, ref)
+    names = dict(m.named_parameters())
+    checked = 0
+    for k in names:
+        d_ours = m.state_dict()[k].detach().double().cpu() - pre[k]
+        d_ref = torch.from_numpy(np.array(g.z[f"post/{k}"], dtype=np.float64)) - pre[k]
+        g0 = torch.from_numpy(np.array(g.z[f"grad0/{k}"], dtype=np.float64)).abs()
+        g1 = torch.from_numpy(np.array(g.z[f"grad1/{k}"], dtype=np.float64)).abs()
+        rms0, rms1 = g0.pow(2).mean().sqrt(), g1.pow(2).mean().sqrt()
+        if rms0 == 0 or rms1 == 0:
+            continue
+        strong = (g0 > 0.1 * rms0) & (g1 > 0.1 * rms1)
+        e = ((d_ours - d_ref)[strong].norm() / d_ref[strong].norm()).item()
+        assert e <= (6e-2 if amp else 3e-2), f"{k}: update rel err {e:.3e} on {int(strong.sum())} elements"
+        live = (g0 > 0.01 * rms0) & (g1 > 0.01 * rms1)
+        agree = (torch.sign(d_ours[live]) == torch.sign(d_ref[live])).double().mean().item()
+        assert agree >= (0.95 if amp else 0.97), f"{k}: update sign agrees on {agree:.4f}"
+        checked += 1
+    assert checked >= 20
+
+
+def test_batch1_upernet_step_trains():
+    """A recipe at --batch_size 1 with a BatchNorm head (ViT + UperNet2D, enhance, MSE, Adam under autocast): the
+    step duplicates the batch of 1 as trainer_base.py:160-164 does (training-mode BatchNorm needs two values per
+    channel), so two steps train: finite losses, the BatchNorm running stats and the head weights updated. (The
+    pyramid's bin-1 conv feeds a BatchNorm over two identical 1x1 samples: zero variance, so its gradient is
+    exactly zero in the reference too and Adam leaves it.)"""
+    from long_context_biomedical_imaging_amd import config, model_base, trainer
+    args = ["--encoder_name", "ViT", "--ViT.size", "custom", "--ViT.hidden_size", "128", "--ViT.mlp_dim", "256",
+            "--ViT.num_layers", "12", "--ViT.num_heads", "2", "--ViT.patch_size", "4", "--height", "64", "--width",
+            "64", "--task_type", "enhance", "--decoder_name", "UperNet2D", "--no_out_channel", "1", "--optim_type",
+            "adam", "--optim.lr", "1e-3", "--loss_func", "MSE", "--batch_size", "1", "--use_amp"]
+    cfg = config.parse_config(args)
+    torch.manual_seed(3)
+    dev = torch.device("cuda", 0)
+    m = model_base.EncoderDecoderModel(cfg, "ViT", "UperNet2D", 1, 1).to(dev).train()
+    bns = [mod for mod in m.modules() if isinstance(mod, torch.nn.modules.batchnorm._BatchNorm)]
+    assert bns, "UperNet2D has BatchNorm"
+    pre = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    step = trainer.TrainStep(m, cfg, dev, ddp=False)
+    assert step.dup_batch1
+    gen = torch.Generator().manual_seed(4)
+    for _ in range(2):
+        x = torch.rand(1, 1, 1, 64, 64, generator=gen).to(dev)
+        loss = step.step(x, x * 0.5).item()
+        assert np.isfinite(loss)
+    post = m.state_dict()
+    moved = [k for k in pre if k.startswith("decoder") and pre[k].is_floating_point() and
+             not torch.equal(pre[k], post[k])]
+    assert any("running_mean" in k for k in moved) and any(k.endswith("weight") for k in moved)
+    dec = [k for k, _ in m.named_parameters() if k.startswith("decoder")]
+    still = [k for k in dec if torch.equal(pre[k], post[k])]
+    assert all(k.startswith("decoder.PPN.stages.0.") for k in still), still

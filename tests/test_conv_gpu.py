@@ -112,9 +112,9 @@ def _ref_resblock(blk, x):
     conv = F.conv3d if nd == 3 else F.conv2d
     dev = x.device
     w = lambda m: m.weight if m.weight.device == dev else m.weight.detach().float().to(dev)   # noqa: E731
-    out = F.leaky_relu(F.instance_norm(conv(x, w(blk.conv1), padding=1), eps=1e-5), 0.01)
-    out = F.instance_norm(conv(out, w(blk.conv2), padding=1), eps=1e-5)
-    res = F.instance_norm(conv(x, w(blk.conv3)), eps=1e-5) if blk.downsample else x
+    out = F.leaky_relu(F.instance_norm(conv(x, w(blk.conv1.conv), padding=1), eps=1e-5), 0.01)
+    out = F.instance_norm(conv(out, w(blk.conv2.conv), padding=1), eps=1e-5)
+    res = F.instance_norm(conv(x, w(blk.conv3.conv)), eps=1e-5) if blk.downsample else x
     return F.leaky_relu(out + res, 0.01)
 
 
@@ -136,7 +136,7 @@ def test_unet_resblock_fused_vs_torch(nd, S, cin, cout):
     with torch.autocast("cuda", dtype=torch.bfloat16):
         yt = _ref_resblock(blk, xt)
     yt.float().backward(dy.cuda())
-    gt = blk.conv1.weight.grad.float().cpu()
+    gt = blk.conv1.conv.weight.grad.float().cpu()
     blk.zero_grad(set_to_none=True)
     xc = x.cuda().requires_grad_(True)                # this repo's fused HIP path
     with torch.autocast("cuda", dtype=torch.bfloat16):
@@ -148,9 +148,9 @@ def test_unet_resblock_fused_vs_torch(nd, S, cin, cout):
     assert e_y < 3e-2 and e_y <= max(1.5 * e_yt, 1e-2), (e_y, e_yt)
     assert e_dx <= max(1.5 * e_dxt, 1e-2), (e_dx, e_dxt)
     # conv1 weight gradient against an fp32 CPU replay with conv1.weight as the leaf (same relative bound)
-    g = blk.conv1.weight.grad.float().cpu()
-    wr = torch.nn.Parameter(blk.conv1.weight.detach().float().cpu())
-    blk.conv1.weight = wr
+    g = blk.conv1.conv.weight.grad.float().cpu()
+    wr = torch.nn.Parameter(blk.conv1.conv.weight.detach().float().cpu())
+    blk.conv1.conv.weight = wr
     _ref_resblock(blk, x.clone()).backward(dy)
     e_g, e_gt = rel_err(g, wr.grad), rel_err(gt, wr.grad)
     assert e_g <= max(1.5 * e_gt, 1e-2), (e_g, e_gt)
@@ -192,6 +192,6 @@ def test_unet_resblock_fused_tail_bit_exact(nd, S, cin, cout, monkeypatch):
         with torch.autocast("cuda", dtype=torch.bfloat16):
             y = blk(xi)
         y.backward(dy)
-        outs.append((y.detach(), xi.grad, blk.conv1.weight.grad, blk.conv2.weight.grad))
+        outs.append((y.detach(), xi.grad, blk.conv1.conv.weight.grad, blk.conv2.conv.weight.grad))
     for name, a, b in zip(("y", "dx", "dW1", "dW2"), outs[0], outs[1]):
         assert torch.equal(a, b), name

@@ -134,10 +134,10 @@ def test_swin_unetr_head_construction():
     cfg = lconfig.parse_config(["--encoder_name", "Swin", "--decoder_name", "SwinUNETR", "--height", "64",
                                 "--width", "64", "--time", "64", "--Swin.patch_size", "2", "2", "2"])
     h = SwinUNETR(cfg, [96, 192, 384, 768, 1536], 2)
-    assert h.encoder10.layer.conv1.weight.shape == (1536, 1536, 3, 3, 3)
-    assert h.decoder5.transp_conv.weight.shape == (1536, 768, 2, 2, 2)
-    assert h.decoder1.transp_conv.weight.shape == (96, 96, 2, 2, 2)
-    assert h.out.conv.weight.shape == (2, 96, 1, 1, 1)
+    assert h.encoder10.layer.conv1.conv.weight.shape == (1536, 1536, 3, 3, 3)
+    assert h.decoder5.transp_conv.conv.weight.shape == (1536, 768, 2, 2, 2)
+    assert h.decoder1.transp_conv.conv.weight.shape == (96, 96, 2, 2, 2)
+    assert h.out.conv.conv.weight.shape == (2, 96, 1, 1, 1)
     with pytest.raises(ValueError):
         SwinUNETR(cfg, [100, 192, 384, 768, 1536], 2)
     cfg.encoder_name = "ViT"

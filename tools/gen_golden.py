@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import hashlib
 import os
+import types
 import sys
 
 import numpy as np
@@ -32,6 +33,7 @@ sys.path.insert(0, REF)
 import backbone_swin as rswin  # noqa: E402
 import backbone_vit as rvit  # noqa: E402
 import class_heads as rcls  # noqa: E402
+import enhance_heads as renh  # noqa: E402
 import hyena as rhyena  # noqa: E402
 import mamba as rmamba  # noqa: E402
 import seg_heads as rseg  # noqa: E402
@@ -303,6 +305,115 @@ def train_step_product(seed):
     dump("train_step_product", None, **arr)
 
 
+def train_step_adam(seed):
+    """Two steps of the reference's loop (trainer_base.py:166-182) with the recipes' optimizer: Adam
+    (optim_base.py:86-87, betas (beta1, beta2) = (0.9, 0.95) config defaults, lr 1e-4 as projects/run_abct.sh:36-37,
+    weight decay 0), CrossEntropy, same small ViT + ViTLinear as train_step_product. Run on CPU, where the
+    reference's torch.autocast(device_type='cuda') is inactive and GradScaler(enabled=True) disables itself (no CUDA):
+    the fp32 step. Each step's gradients are stored too (the test weighs Adam's sign-like first updates by them)."""
+    torch.manual_seed(seed)
+    m = _vit_cls_model("custom", (16, 16), (2, 2, 2), 3, hidden_size=128, mlp_dim=256, num_layers=2, num_heads=2)
+    m.train()
+    g = torch.Generator().manual_seed(seed + 1)
+    xs = [torch.rand(2, 1, 1, 16, 16, generator=g) for _ in range(2)]
+    ys = [torch.randint(0, 3, (2,), generator=g) for _ in range(2)]
+    arr = {f"sd/{k}": v.clone() for k, v in m.state_dict().items()}
+    opt = torch.optim.Adam([{"params": list(m.parameters()), "lr": 1e-4, "weight_decay": 0.0}], lr=1e-4,
+                           betas=(0.9, 0.95), weight_decay=0.0)
+    loss_f = torch.nn.CrossEntropyLoss()
+    for i, (x, y) in enumerate(zip(xs, ys)):
+        loss = loss_f(m(x), y)
+        loss.backward()
+        for k, v in m.named_parameters():
+            arr[f"grad{i}/{k}"] = v.grad.clone()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        arr[f"in/x{i}"], arr[f"in/y{i}"], arr[f"out/loss{i}"] = x, y, loss.detach()
+    for k, v in m.state_dict().items():
+        arr[f"post/{k}"] = v
+    dump("train_step_adam", None, **arr)
+
+
+def _sub(t, n=8192):
+    """A deterministic strided subsample of t (at most ~n elements) and its stride: the fixture keeps big
+    activations and gradients as samples (tests/test_unetr.py compares the same positions)."""
+    flat = t.detach().reshape(-1)
+    step = max(1, flat.numel() // n)
+    return flat[::step].clone(), np.array(step)
+
+
+def _unetr_run(m, ins, grad_idx, seed, small_params):
+    """Forward on the input list, backward of sum(out * seeded cotangent); -> dict of outputs / gradients."""
+    ins = [x.clone().requires_grad_(i in grad_idx) for i, x in enumerate(ins)]
+    out = m(list(ins))
+    cot = torch.randn(out.shape, generator=torch.Generator().manual_seed(123))
+    m.zero_grad(set_to_none=True)
+    (out * cot).sum().backward()
+    arr = {}
+    arr["out/0"], arr["stride/out"] = _sub(out)
+    for i in grad_idx:
+        arr[f"grad/in{i}"], arr[f"stride/in{i}"] = _sub(ins[i].grad)
+    params = dict(m.named_parameters())
+    for k, v in m.state_dict().items():
+        arr[f"chk/{k}"] = np.array([v.double().sum().item(), v.double().abs().sum().item(), float(v.numel())])
+    for k, v in params.items():
+        arr[f"gsum/{k}"] = np.array([v.grad.double().sum().item(), v.grad.double().abs().sum().item()])
+    for k in small_params:
+        arr[f"grad/{k}"] = params[k].grad
+    for i, x in enumerate(ins):
+        arr[f"inchk/{i}"] = np.array([x.double().sum().item(), x.double().abs().sum().item()])
+    return arr
+
+
+def unetr_vit(name, nd, patch, S, hidden, seed):
+    """The reference ViTUNETR (enhance_heads.py:187-356) on the restated MONAI-1.3 blocks, fp32 CPU, fed the input
+    image, 12 hidden-state taps (3, 6, 9 read, enhance_heads.py:338-345; the others zero) and the last tokens.
+    Weights come from torch.manual_seed(seed) (stored as checksums: the product module is seed-identical); inputs
+    from torch.Generator().manual_seed(seed + 1), in list order (stored as checksums); out and input gradients as
+    strided samples, a few small weight gradients whole, every weight gradient's sum and L1 mass."""
+    torch.manual_seed(seed)
+    ns = types.SimpleNamespace
+    cfg = ns(no_in_channel=1, encoder_name="ViT", time=S[0], height=S[1], width=S[2],
+             ViT=ns(hidden_size=hidden, patch_size=tuple(patch)))
+    m = renh.ViTUNETR(cfg, None, 2).train()
+    g = torch.Generator().manual_seed(seed + 1)
+    L = 1
+    for a, b in zip(S, patch):
+        L *= a // b
+    B = 2
+    ins = [torch.randn(B, 1, *S, generator=g)]
+    ins += [torch.randn(B, L, hidden, generator=g) if i in (3, 6, 9) else torch.zeros(B, L, hidden) for i in range(12)]
+    ins.append(torch.randn(B, L, hidden, generator=g))
+    arr = _unetr_run(m, ins, (0, 4, 7, 10, 13), 123,
+                     ("encoder1.layer.conv1.conv.weight", "out.conv.conv.weight", "out.conv.conv.bias",
+                      "encoder2.transp_conv_init.conv.weight", "decoder2.transp_conv.conv.weight"))
+    arr["cfg/shape"] = np.array([nd, *patch, *S, hidden, seed])
+    dump(name, None, **arr)
+
+
+def unetr_swin(name, S, f0, seed):
+    """The reference SwinUNETR (enhance_heads.py:30-184), 3-D, patch 2, Swin-tiny channels [f0 .. 16 f0], fed the
+    input image and the five stage taps (S/2 .. S/32), fp32 CPU; stored as unetr_vit."""
+    torch.manual_seed(seed)
+    ns = types.SimpleNamespace
+    cfg = ns(no_in_channel=1, encoder_name="Swin", time=S[0], height=S[1], width=S[2], Swin=ns(patch_size=(2, 2, 2)))
+    chans = [f0 * 2 ** i for i in range(5)]
+    m = renh.SwinUNETR(cfg, chans, 2).train()
+    g = torch.Generator().manual_seed(seed + 1)
+    B = 1
+    ins = [torch.randn(B, 1, *S, generator=g)]
+    ins += [torch.randn(B, c, *(s // 2 ** (i + 1) for s in S), generator=g) for i, c in enumerate(chans)]
+    arr = _unetr_run(m, ins, (0, 1, 4, 5), 123,
+                     ("encoder1.layer.conv1.conv.weight", "out.conv.conv.weight", "out.conv.conv.bias",
+                      "decoder1.transp_conv.conv.weight"))
+    arr["cfg/shape"] = np.array([3, *S, f0, seed])
+    dump(name, None, **arr)
+
+
+UNETR = [("unetr_vit2d_p2", 2, (1, 2, 2), (1, 32, 32), 96, 40), ("unetr_vit2d_p4", 2, (1, 4, 4), (1, 32, 32), 96, 41),
+         ("unetr_vit3d_p2", 3, (2, 2, 2), (8, 16, 16), 96, 42)]
+
+
 def swin_index():
     arr = {}
     ws, ss = (7, 7, 7), (3, 3, 3)
@@ -420,6 +531,12 @@ def main(only=None):
                 vit_cls_c1(15)
             elif name == "train_step_product":
                 train_step_product(16)
+            elif name == "train_step_adam":
+                train_step_adam(16)
+            elif name == "unetr":
+                for cfg in UNETR:
+                    unetr_vit(*cfg)
+                unetr_swin("unetr_swin3d_p2", (64, 64, 64), 96, 43)
             else:
                 raise SystemExit(f"unknown fixture group {name}")
         return
@@ -437,7 +554,11 @@ def main(only=None):
     swin_index()
     train_step(10)
     train_step_product(16)
+    train_step_adam(16)
     vit_cls_c1(15)
+    for cfg in UNETR:
+        unetr_vit(*cfg)
+    unetr_swin("unetr_swin3d_p2", (64, 64, 64), 96, 43)
     for i, cfg in enumerate(SWIN_ALT):
         swin_alt_layer(*cfg, seed=20 + i)
     upernet("upernet2d_swin", 2, "Swin", 11)

@@ -5,7 +5,9 @@ TEST INFRASTRUCTURE ONLY (used by tools/gen_golden.py to import the reference mo
 
 Each class restates the *published behaviour* of the pinned dependency version:
   - monai==1.3.0  (requirements.txt:5)   PatchEmbeddingBlock, PatchEmbed, MLPBlock, trunc_normal_,
-                                          ensure_tuple_rep, look_up_option, optional_import
+                                          ensure_tuple_rep, look_up_option, optional_import, and the UNETR
+                                          blocks UnetrBasicBlock / UnetrPrUpBlock / UnetrUpBlock / UnetOutBlock
+                                          (dynunet_block.py UnetResBlock / UnetBasicBlock, get_conv_layer)
   - timm==0.9.2   (requirements.txt:13)  only names imported by mamba.py:22-23 (unused in forward)
   - torchvision==0.16.1 (README.md:12)  imported by seg_heads.py, unused: an empty module
   - mamba-ssm==1.2.0.post1 (README.md:15) selective_scan_fn -> selective_scan_ref semantics
@@ -159,9 +161,177 @@ class PatchEmbed(nn.Module):
         return x
 
 
-class _Unavailable(nn.Module):
-    def __init__(self, *a, **k):
-        raise RuntimeError("MONAI UNETR blocks are not available in this image")
+# monai 1.3 networks/blocks/dynunet_block.py + unetr_block.py + networks/blocks/convolutions.py (conv-only form):
+# the UNETR decoder blocks enhance_heads.py:24 imports. Conv layers default to bias=False (get_conv_layer), norms are
+# InstanceNorm without affine parameters, activations LeakyReLU(0.01); every conv sits under a Convolution
+# container's `.conv` (state_dict keys `<block>.conv1.conv.weight`).
+def get_padding(kernel_size, stride):
+    pad = (np.atleast_1d(kernel_size) - np.atleast_1d(stride) + 1) / 2
+    if np.min(pad) < 0:
+        raise AssertionError("padding value should not be negative")
+    pad = tuple(int(p) for p in pad)
+    return pad if len(pad) > 1 else pad[0]
+
+
+def get_output_padding(kernel_size, stride, padding):
+    out = 2 * np.atleast_1d(padding) + np.atleast_1d(stride) - np.atleast_1d(kernel_size)
+    if np.min(out) < 0:
+        raise AssertionError("out_padding value should not be negative")
+    out = tuple(int(p) for p in out)
+    return out if len(out) > 1 else out[0]
+
+
+class Convolution(nn.Sequential):
+    """monai 1.3 Convolution with act = norm = dropout = None: only the `conv` submodule."""
+
+    def __init__(self, spatial_dims, in_channels, out_channels, strides=1, kernel_size=3, bias=True,
+                 is_transposed=False, padding=None, output_padding=None):
+        super().__init__()
+        if is_transposed:
+            conv_t = nn.ConvTranspose2d if spatial_dims == 2 else nn.ConvTranspose3d
+            conv = conv_t(in_channels, out_channels, kernel_size=kernel_size, stride=strides, padding=padding,
+                          output_padding=output_padding, groups=1, bias=bias, dilation=1)
+        else:
+            conv_t = nn.Conv2d if spatial_dims == 2 else nn.Conv3d
+            conv = conv_t(in_channels, out_channels, kernel_size=kernel_size, stride=strides, padding=padding,
+                          dilation=1, groups=1, bias=bias)
+        self.add_module("conv", conv)
+
+
+def get_conv_layer(spatial_dims, in_channels, out_channels, kernel_size=3, stride=1, bias=False,
+                   is_transposed=False):
+    padding = get_padding(kernel_size, stride)
+    output_padding = get_output_padding(kernel_size, stride, padding) if is_transposed else None
+    return Convolution(spatial_dims, in_channels, out_channels, strides=stride, kernel_size=kernel_size, bias=bias,
+                       is_transposed=is_transposed, padding=padding, output_padding=output_padding)
+
+
+def _instance_norm(spatial_dims, channels):
+    return (nn.InstanceNorm2d if spatial_dims == 2 else nn.InstanceNorm3d)(channels)
+
+
+def _check_norm(norm_name):
+    if norm_name != "instance":
+        raise NotImplementedError(f"norm {norm_name!r}: the reference uses 'instance' only (enhance_heads.py)")
+
+
+class UnetResBlock(nn.Module):
+    """monai 1.3 UnetResBlock: conv1 -> norm1 -> lrelu -> conv2 -> norm2, + residual (1x1 conv3 + norm3 when the
+    channel count or stride changes), -> lrelu."""
+
+    def __init__(self, spatial_dims, in_channels, out_channels, kernel_size, stride, norm_name, dropout=None):
+        super().__init__()
+        _check_norm(norm_name)
+        self.conv1 = get_conv_layer(spatial_dims, in_channels, out_channels, kernel_size=kernel_size, stride=stride)
+        self.conv2 = get_conv_layer(spatial_dims, out_channels, out_channels, kernel_size=kernel_size, stride=1)
+        self.lrelu = nn.LeakyReLU(negative_slope=0.01, inplace=True)
+        self.norm1 = _instance_norm(spatial_dims, out_channels)
+        self.norm2 = _instance_norm(spatial_dims, out_channels)
+        self.downsample = in_channels != out_channels
+        if not np.all(np.atleast_1d(stride) == 1):
+            self.downsample = True
+        if self.downsample:
+            self.conv3 = get_conv_layer(spatial_dims, in_channels, out_channels, kernel_size=1, stride=stride)
+            self.norm3 = _instance_norm(spatial_dims, out_channels)
+
+    def forward(self, inp):
+        residual = inp
+        out = self.lrelu(self.norm1(self.conv1(inp)))
+        out = self.norm2(self.conv2(out))
+        if hasattr(self, "conv3"):
+            residual = self.conv3(residual)
+        if hasattr(self, "norm3"):
+            residual = self.norm3(residual)
+        out += residual
+        return self.lrelu(out)
+
+
+class UnetBasicBlock(nn.Module):
+    """monai 1.3 UnetBasicBlock: conv1 -> norm1 -> lrelu -> conv2 -> norm2 -> lrelu."""
+
+    def __init__(self, spatial_dims, in_channels, out_channels, kernel_size, stride, norm_name, dropout=None):
+        super().__init__()
+        _check_norm(norm_name)
+        self.conv1 = get_conv_layer(spatial_dims, in_channels, out_channels, kernel_size=kernel_size, stride=stride)
+        self.conv2 = get_conv_layer(spatial_dims, out_channels, out_channels, kernel_size=kernel_size, stride=1)
+        self.lrelu = nn.LeakyReLU(negative_slope=0.01, inplace=True)
+        self.norm1 = _instance_norm(spatial_dims, out_channels)
+        self.norm2 = _instance_norm(spatial_dims, out_channels)
+
+    def forward(self, inp):
+        out = self.lrelu(self.norm1(self.conv1(inp)))
+        return self.lrelu(self.norm2(self.conv2(out)))
+
+
+class UnetrBasicBlock(nn.Module):
+    """monai 1.3 UnetrBasicBlock: one UnetResBlock (res_block) or UnetBasicBlock under `.layer`."""
+
+    def __init__(self, spatial_dims, in_channels, out_channels, kernel_size, stride, norm_name, res_block=False):
+        super().__init__()
+        blk = UnetResBlock if res_block else UnetBasicBlock
+        self.layer = blk(spatial_dims=spatial_dims, in_channels=in_channels, out_channels=out_channels,
+                         kernel_size=kernel_size, stride=stride, norm_name=norm_name)
+
+    def forward(self, inp):
+        return self.layer(inp)
+
+
+class UnetrPrUpBlock(nn.Module):
+    """monai 1.3 UnetrPrUpBlock: transposed conv (kernel = stride = upsample_kernel_size), then num_layer x
+    [transposed conv, conv block]."""
+
+    def __init__(self, spatial_dims, in_channels, out_channels, num_layer, kernel_size, stride, upsample_kernel_size,
+                 norm_name, conv_block=False, res_block=False):
+        super().__init__()
+        up = upsample_kernel_size
+        self.transp_conv_init = get_conv_layer(spatial_dims, in_channels, out_channels, kernel_size=up, stride=up,
+                                               is_transposed=True)
+        if conv_block:
+            blk = UnetResBlock if res_block else UnetBasicBlock
+            self.blocks = nn.ModuleList([nn.Sequential(
+                get_conv_layer(spatial_dims, out_channels, out_channels, kernel_size=up, stride=up,
+                               is_transposed=True),
+                blk(spatial_dims=spatial_dims, in_channels=out_channels, out_channels=out_channels,
+                    kernel_size=kernel_size, stride=stride, norm_name=norm_name)) for _ in range(num_layer)])
+        else:
+            self.blocks = nn.ModuleList([get_conv_layer(spatial_dims, out_channels, out_channels, kernel_size=up,
+                                                        stride=up, is_transposed=True) for _ in range(num_layer)])
+
+    def forward(self, x):
+        x = self.transp_conv_init(x)
+        for blk in self.blocks:
+            x = blk(x)
+        return x
+
+
+class UnetrUpBlock(nn.Module):
+    """monai 1.3 UnetrUpBlock: transposed conv up-sampling, cat with the skip on channels, conv block on 2C."""
+
+    def __init__(self, spatial_dims, in_channels, out_channels, kernel_size, upsample_kernel_size, norm_name,
+                 res_block=False):
+        super().__init__()
+        up = upsample_kernel_size
+        self.transp_conv = get_conv_layer(spatial_dims, in_channels, out_channels, kernel_size=up, stride=up,
+                                          is_transposed=True)
+        blk = UnetResBlock if res_block else UnetBasicBlock
+        self.conv_block = blk(spatial_dims, out_channels + out_channels, out_channels, kernel_size=kernel_size,
+                              stride=1, norm_name=norm_name)
+
+    def forward(self, inp, skip):
+        out = self.transp_conv(inp)
+        out = torch.cat((out, skip), dim=1)
+        return self.conv_block(out)
+
+
+class UnetOutBlock(nn.Module):
+    """monai 1.3 UnetOutBlock: 1x1 conv with bias."""
+
+    def __init__(self, spatial_dims, in_channels, out_channels, dropout=None):
+        super().__init__()
+        self.conv = get_conv_layer(spatial_dims, in_channels, out_channels, kernel_size=1, stride=1, bias=True)
+
+    def forward(self, inp):
+        return self.conv(inp)
 
 
 # ---------------------------------------------------------------- mamba_ssm selective_scan_ref
@@ -212,8 +382,8 @@ def install():
 
     utils = dict(ensure_tuple_rep=ensure_tuple_rep, look_up_option=look_up_option,
                  optional_import=optional_import, deprecated_arg=deprecated_arg)
-    blocks = dict(PatchEmbed=PatchEmbed, MLPBlock=MLPBlock, UnetOutBlock=_Unavailable,
-                  UnetrBasicBlock=_Unavailable, UnetrUpBlock=_Unavailable, UnetrPrUpBlock=_Unavailable)
+    blocks = dict(PatchEmbed=PatchEmbed, MLPBlock=MLPBlock, UnetOutBlock=UnetOutBlock,
+                  UnetrBasicBlock=UnetrBasicBlock, UnetrUpBlock=UnetrUpBlock, UnetrPrUpBlock=UnetrPrUpBlock)
     mod("monai")
     mod("monai.utils", **utils)
     mod("monai.utils.deprecate_utils", deprecated_arg=deprecated_arg)
@@ -221,7 +391,8 @@ def install():
     mod("monai.networks.blocks", **blocks)
     mod("monai.networks.blocks.patchembedding", PatchEmbeddingBlock=PatchEmbeddingBlock)
     mod("monai.networks.blocks.mlp", MLPBlock=MLPBlock)
-    mod("monai.networks.blocks.dynunet_block", UnetOutBlock=_Unavailable)
+    mod("monai.networks.blocks.dynunet_block", UnetOutBlock=UnetOutBlock, UnetResBlock=UnetResBlock,
+        UnetBasicBlock=UnetBasicBlock, get_conv_layer=get_conv_layer)
     mod("monai.networks.layers", DropPath=DropPath, trunc_normal_=trunc_normal_)
     mod("timm")
     mod("timm.models")
