@@ -33,8 +33,9 @@ HIP_CONV_3D = os.environ.get("LCI_HIP_CONV_3D", "1") != "0"
 
 def _hip(x, flag):
     """The HIP conv / instance-norm path computes bf16 operands with f32 accumulation and returns bf16: it is the
-    autocast (use_amp) path. An f32 model run without autocast keeps the reference's f32 convolutions (torch)."""
-    return flag and x.is_cuda and (x.dtype == torch.bfloat16 or torch.is_autocast_enabled("cuda"))
+    autocast (use_amp) path. An f32 model run on the GPU without autocast keeps the reference's f32 convolutions
+    (torch); CPU tensors go to the HIP path too, which refuses them (no CPU path)."""
+    return flag and (not x.is_cuda or x.dtype == torch.bfloat16 or torch.is_autocast_enabled("cuda"))
 
 
 class Conv3x3(nn.Conv3d):

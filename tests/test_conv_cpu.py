@@ -39,14 +39,16 @@ def test_gemm_forms_match_torch_convs():
 def test_decoder_conv_selection_keeps_parameters():
     """Same parameter names/shapes/seeded init as the nn.Conv layers they replace (state_dict drop-in)."""
     torch.manual_seed(3)
-    a = decoders._conv(3, 96, 96, 3, 1)
+    w = decoders._conv(3, 96, 96, 3, 1)                                 # MONAI Convolution: the layer under .conv
+    assert isinstance(w, decoders.Convolution) and list(w.state_dict().keys()) == ["conv.weight"]
+    a = w.conv
     torch.manual_seed(3)
     b = torch.nn.Conv3d(96, 96, 3, 1, padding=1, bias=False)
     assert isinstance(a, decoders.Conv3x3) and a.state_dict().keys() == b.state_dict().keys()
     assert torch.equal(a.weight, b.weight)
-    assert isinstance(decoders._conv(3, 192, 96, 1, 1), decoders.Conv1x1)
-    assert isinstance(decoders._conv(3, 96, 96, (2, 2, 2), (2, 2, 2), transposed=True), decoders.ConvUp)
-    assert isinstance(decoders._conv(2, 64, 32, 3, 1), decoders.Conv3x3_2d)
-    assert type(decoders._conv(3, 4, 2, 3, 1)) is torch.nn.Conv3d      # Cout % 32 != 0: torch conv
+    assert isinstance(decoders._conv_layer(3, 192, 96, 1, 1), decoders.Conv1x1)
+    assert isinstance(decoders._conv_layer(3, 96, 96, (2, 2, 2), (2, 2, 2), transposed=True), decoders.ConvUp)
+    assert isinstance(decoders._conv_layer(2, 64, 32, 3, 1), decoders.Conv3x3_2d)
+    assert type(decoders._conv_layer(3, 4, 2, 3, 1)) is torch.nn.Conv3d      # Cout % 32 != 0: torch conv
     with pytest.raises(RuntimeError):
         a(torch.randn(1, 96, 4, 4, 4))                                  # no CPU path for the HIP conv

@@ -64,6 +64,11 @@ def _chk(t):
     return t.double().sum().item(), t.double().abs().sum().item()
 
 
+def _same(a, b):
+    """Checksums of identical tensors (f64 sums: the reduction order follows the thread count, so 1e-12)."""
+    return all(abs(x - y) <= 1e-12 * max(1.0, abs(y)) for x, y in zip(a, b))
+
+
 @pytest.mark.parametrize("name", ALL)
 def test_unetr_structure_init_and_inputs(name):
     g = Golden(name)
@@ -74,9 +79,9 @@ def test_unetr_structure_init_and_inputs(name):
     for k, v in sd.items():
         s, a, n = (float(x) for x in g.z[f"chk/{k}"])
         assert v.numel() == n, k
-        assert _chk(v) == (s, a), f"{k}: init differs from the reference's seeded init"
+        assert _same(_chk(v), (s, a)), f"{k}: init differs from the reference's seeded init"
     for i, x in enumerate(ins):
-        assert _chk(x) == tuple(float(v) for v in g.z[f"inchk/{i}"]), f"input {i} not regenerated"
+        assert _same(_chk(x), [float(v) for v in g.z[f"inchk/{i}"]]), f"input {i} not regenerated"
 
 
 def _sample(t, stride):
