@@ -921,6 +921,15 @@ __device__ __forceinline__ void hs_vmcnt() {   // s_waitcnt vmcnt(N), lgkmcnt / 
 #ifndef LCI_HS_AHOME
 #define LCI_HS_AHOME 1       // K / V fragments homed in AGPRs before the loop (0: compiler's choice; unsafe)
 #endif
+#ifndef LCI_HS_LGKM0
+#define LCI_HS_LGKM0 1       // drain the prologue's LDS reads before the loop (see the loop header)
+#endif
+#ifndef LCI_HS_NOFENCE
+#define LCI_HS_NOFENCE 1     // tile barrier without the LDS fence of __syncthreads
+#endif
+// s_waitcnt lgkmcnt(0) with vmcnt / expcnt left at their maxima (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] |
+// lgkmcnt[11:8] | vmcnt[15:14])
+constexpr unsigned LGKM0_WAIT = 0xC07F;
 #ifndef LCI_HS_DMASPREAD
 #define LCI_HS_DMASPREAD 0   // 1: one LDS-DMA issue per segment (21.3 ms vs 20.7 ms for tile t+3's five in seg B
 #endif                       // of half 1, same box)
@@ -1271,6 +1280,9 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
     for (int f = 0; f < 8; ++f) { tr_load(f, 0, smem, 0); tr_load(f, 1, smem, 32); }
     probe_noread = true;
   }
+  // the prologue's reads complete here (a waitcnt the compiler's pass sees): otherwise its wait for them, merged
+  // into the loop header with the back edge's, makes every tile start with lgkmcnt(1)
+  if (LCI_HS_LGKM0) __builtin_amdgcn_s_waitcnt(LGKM0_WAIT);
   // one tile in ring slot t & 3 (a 4-tile unroll that made the slots compile-time spilled 32 VGPRs);
   // register staging: tile t+1 is in set PAR ^ 1, which then takes tile t+3
   auto tile = [&](auto PAR, int t) __attribute__((always_inline)) {
@@ -1289,7 +1301,12 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
         if (t + 2 < nqt) hs_vmcnt<5>(); else hs_vmcnt<0>();
         if constexpr (LCI_HS_STG == 1) store_tile(stg[P1], nslot);
         stamp(8);
-        if (LCI_HS_PROBE != 1 && LCI_HS_PROBE != 3) __syncthreads();
+        // no LDS fence: this wave's reads of the slot tile t+3 overwrites were consumed before now, and the new
+        // tile's bytes are ordered by the vmcnt above (register staging stores to LDS: that one needs the fence)
+        if (LCI_HS_PROBE != 1 && LCI_HS_PROBE != 3) {
+          if (LCI_HS_STG == 1 || !LCI_HS_NOFENCE) __syncthreads();
+          else __builtin_amdgcn_s_barrier();
+        }
         stamp(9);
         if constexpr (LCI_HS_STG == 1)
           if (t + 3 < nqt && LCI_HS_PROBE != 2) load_tile(stg[P1], t + 3);
@@ -1379,60 +1396,63 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
 // fragments (dQ^T's A operand, shared by both blocks) at 12-19, K rows of the next half at 20-23.
 // Keys past L read as zero rows (dS^T there multiplies zero K); no masking.
 // gap  0: E1.8 E1.9
-// gap  1: M1.8 M1.9 C1.4 E1.10
+// gap  1: M1.8 M1.9 E1.10 C1.4
 // gap  2: M1.10 E1.11 E1.12
 // gap  3: M1.11 M1.12 C1.5 E1.13
-// gap  4: M1.13 C1.6 E1.14 E1.15
-// gap  5: M1.14 M1.15 C1.7 E0.0
+// gap  4: E1.14 M1.13 E1.15 C1.6
+// gap  5: M1.14 M1.15 E0.0 C1.7
 // gap  6: E0.1 E0.2
 // gap  7: E0.3 E0.4
 // gap  8: E0.5 E0.6
 // gap  9: M0.0 M0.1 M0.2 M0.3
 // gap 10: C0.0 C0.1 M0.4 M0.5
-// gap 11: C0.2 M0.6 E0.7 E0.8
+// gap 11: M0.6 C0.2 E0.7 E0.8
 // gap 12: M0.7 M0.8 C0.3 E0.9
-// gap 13: M0.9 C0.4 E0.10 E0.11
-// gap 14: M0.10 M0.11 C0.5 E0.12
+// gap 13: E0.10 M0.9 E0.11 C0.4
+// gap 14: M0.10 M0.11 E0.12 C0.5
 // gap 15: M0.12 E0.13 E0.14
 // gap 16: M0.13 M0.14 C0.6 E0.15
-// gap 17: E1.0 E1.1 M0.15 C0.7
+// gap 17: E1.0 M0.15 E1.1 C0.7
 // gap 18: E1.2 E1.3
 // gap 19: E1.4 E1.5
 // gap 20: E1.6 E1.7
 // gap 21: M1.0 M1.1 M1.2 M1.3
 // gap 22: C1.0 C1.1 M1.4 M1.5
-// gap 23: C1.2 M1.6 M1.7 C1.3
+// gap 23: M1.6 M1.7 C1.2 C1.3
 constexpr unsigned char DQ_SCHED[24][4] = {
     {0x28, 0x29, 0xff, 0xff},
-    {0x68, 0x69, 0xa4, 0x2a},
+    {0x68, 0x69, 0x2a, 0xa4},
     {0x6a, 0x2b, 0x2c, 0xff},
     {0x6b, 0x6c, 0xa5, 0x2d},
-    {0x6d, 0xa6, 0x2e, 0x2f},
-    {0x6e, 0x6f, 0xa7, 0x00},
+    {0x2e, 0x6d, 0x2f, 0xa6},
+    {0x6e, 0x6f, 0x00, 0xa7},
     {0x01, 0x02, 0xff, 0xff},
     {0x03, 0x04, 0xff, 0xff},
     {0x05, 0x06, 0xff, 0xff},
     {0x40, 0x41, 0x42, 0x43},
     {0x80, 0x81, 0x44, 0x45},
-    {0x82, 0x46, 0x07, 0x08},
+    {0x46, 0x82, 0x07, 0x08},
     {0x47, 0x48, 0x83, 0x09},
-    {0x49, 0x84, 0x0a, 0x0b},
-    {0x4a, 0x4b, 0x85, 0x0c},
+    {0x0a, 0x49, 0x0b, 0x84},
+    {0x4a, 0x4b, 0x0c, 0x85},
     {0x4c, 0x0d, 0x0e, 0xff},
     {0x4d, 0x4e, 0x86, 0x0f},
-    {0x20, 0x21, 0x4f, 0x87},
+    {0x20, 0x4f, 0x21, 0x87},
     {0x22, 0x23, 0xff, 0xff},
     {0x24, 0x25, 0xff, 0xff},
     {0x26, 0x27, 0xff, 0xff},
     {0x60, 0x61, 0x62, 0x63},
     {0xa0, 0xa1, 0x64, 0x65},
-    {0xa2, 0x66, 0x67, 0xa3}};
+    {0x66, 0x67, 0xa2, 0xa3}};
 
 #ifndef LCI_DQ_AHOME
 #define LCI_DQ_AHOME 1       // Q~ / dO fragments homed in AGPRs before the loop
 #endif
 #ifndef LCI_DQ_DMASPREAD
 #define LCI_DQ_DMASPREAD 1   // DMA issues at gaps 8 / 20 (half 1) and 6 / 18 (half 0); 0: gaps 6-8, 15 of half 1
+#endif
+#ifndef LCI_DQ_V2
+#define LCI_DQ_V2 0          // 1: LDS reads >= 8 gaps ahead of their MFMAs (16.6 vs 15.9 ms same box: slower)
 #endif
 __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs a) {
   constexpr int TILE_B = KT * DH * 2;               // bytes of a K or V tile (128-B rows)
@@ -1520,7 +1540,9 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
     for (int j = 0; j < 2; ++j) dq[i][j] = f32x16{};
   }
   u32x4 dsp[2][2] = {};        // [query block][k-step] bf16 dS^T packs
-  bf16x4 ktr[2][2][2] = {};    // [d block][k-step][half of the fragment] transposed K (keys as the k index)
+  // [set][d block][k-step][half of the fragment] transposed K (keys as the k index); LCI_DQ_V2: half p's in set
+  // p & 1 (read at its gaps 0-7, while dQ^T of block 1 still uses half p-1's set), else one set
+  bf16x4 ktr[2][2][2][2] = {};
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     HS_OPAQUE(S[i]);
@@ -1529,8 +1551,8 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
     for (int j = 0; j < 2; ++j) {
       HS_TO_AGPR(dq[i][j]);
       HS_OPAQUE(dsp[i][j]);
-      HS_OPAQUE(ktr[i][j][0]);
-      HS_OPAQUE(ktr[i][j][1]);
+#pragma unroll
+      for (int k = 0; k < 2; ++k) { HS_OPAQUE(ktr[k][i][j][0]); HS_OPAQUE(ktr[k][i][j][1]); }
     }
   }
   bf16x8 kr[4], vr[4];         // K / V row fragments (A operands of the chains)
@@ -1543,39 +1565,52 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
     else if (kind == 1) HS_MUL(P[qb][i], S[qb][i]);
     else HS_CVT(dsp[qb][i >> 2][i & 3], P[qb][2 * i], P[qb][2 * i + 1]);
   };
-  auto dq_mfma = [&](int k, int qb) __attribute__((always_inline)) {   // k = 0..3: (d block k & 1, k-step k >> 1)
+  // k = 0..3: (d block k & 1, k-step k >> 1) with transposed-K set st
+  auto dq_mfma = [&](int k, int qb, int st) __attribute__((always_inline)) {
     const int db = k & 1, s2 = k >> 1;
-    HS_MFMA_G(dq[db][qb], cat44(ktr[db][s2][0], ktr[db][s2][1]), __builtin_bit_cast(bf16x8, dsp[qb][s2]));
+    HS_MFMA_G(dq[db][qb], cat44(ktr[st][db][s2][0], ktr[st][db][s2][1]), __builtin_bit_cast(bf16x8, dsp[qb][s2]));
   };
-  auto mfma_gap = [&](int g) __attribute__((always_inline)) {
+  auto mfma_gap = [&](int g, int C) __attribute__((always_inline)) {   // C: this half's transposed-K set
     if (g < 4) {
       if (g == 0) HS_MFMA_C0(S[0], kr[0], qf[0][0], NL[0]); else HS_MFMA_C(S[0], kr[g], qf[0][g]);
     } else if (g < 8) {
       if (g == 4) HS_MFMA_C0(P[0], vr[0], df[0][0], ND[0]); else HS_MFMA_C(P[0], vr[g - 4], df[0][g - 4]);
     } else if (g < 12) {
-      dq_mfma(g - 8, 1);
+      dq_mfma(g - 8, 1, C ^ 1);
     } else if (g < 16) {
       if (g == 12) HS_MFMA_C0(S[1], kr[0], qf[1][0], NL[1]); else HS_MFMA_C(S[1], kr[g - 12], qf[1][g - 12]);
     } else if (g < 20) {
       if (g == 16) HS_MFMA_C0(P[1], vr[0], df[1][0], ND[1]); else HS_MFMA_C(P[1], vr[g - 16], df[1][g - 16]);
     } else {
-      dq_mfma(g - 20, 0);
+      dq_mfma(g - 20, 0, C);
     }
   };
 
-  // One 32-key half (rows r0 of `slot`); gaps 20-23 read the K rows of the next half (rows nr0 of `nslot`).
-  auto half = [&](const char* slot, int r0, const char* nslot, int nr0, auto hook) __attribute__((always_inline)) {
+  // One 32-key half (rows r0 of `slot`, transposed-K set SET); the next half's rows are rows nr0 of `nslot`.
+  // LCI_DQ_V2 reads: this half's transposed K at gaps 0-7 (used at 20-23), the next half's K rows at 16-19 (after
+  // their last use by the chains at 12-15; used at its gaps 0-3 and 12-15) and V rows at 20-23 (after 16-19; used
+  // at its 4-7, 16-19): every read >= 8 gaps ahead. Else: V rows at 0-3, transposed K at 12-19, K rows at 20-23.
+  auto half = [&](auto SET, const char* slot, int r0, const char* nslot, int nr0, auto hook)
+      __attribute__((always_inline)) {
+    constexpr int C = LCI_DQ_V2 ? decltype(SET)::value : 0;
 #pragma unroll
     for (int g = 0; g < 24; ++g) {
-      mfma_gap(g);
-      // gap 9's multiplies read the dP^T chain of block 0 (last MFMA at gap 7): 12 wait states by instruction count
-      if (g == 9) asm volatile("s_nop 4" ::: "memory");
+      mfma_gap(g, C);
+      // gaps 9 / 21 multiply the dP^T chain of block 0 / 1 (last MFMA at gap 7 / 19): 12 wait states by
+      // instruction count
+      if (g == 9 || g == 21) asm volatile("s_nop 5" ::: "memory");
 #pragma unroll
       for (int o = 0; o < 4; ++o) valu_op(DQ_SCHED[g][o], -1);
-      if (g < 4) vr[g] = row(slot + TILE_B, r0, g);
+      if (LCI_DQ_V2) {
+        if (g < 8) {
+          const int f = g >> 1, part = g & 1;   // fragment f = (d block f & 1, k-step f >> 1)
+          ktr[C][f & 1][f >> 1][part] = trh(slot, r0, f >> 1, 32 * (f & 1), part);
+        } else if (g >= 16 && g < 20) kr[g - 16] = row(nslot, nr0, g - 16);
+        else if (g >= 20) vr[g - 20] = row(nslot + TILE_B, nr0, g - 20);
+      } else if (g < 4) vr[g] = row(slot + TILE_B, r0, g);
       else if (g >= 12 && g < 20) {
-        const int f = (g - 12) >> 1, part = (g - 12) & 1;   // fragment f = (d block f & 1, k-step f >> 1)
-        ktr[f & 1][f >> 1][part] = trh(slot, r0, f >> 1, 32 * (f & 1), part);
+        const int f = (g - 12) >> 1, part = (g - 12) & 1;
+        ktr[0][f & 1][f >> 1][part] = trh(slot, r0, f >> 1, 32 * (f & 1), part);
       } else if (g >= 20) kr[g - 20] = row(nslot, nr0, g - 20);
       hook(g);
     }
@@ -1592,12 +1627,16 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
   else if (nkt > 1) hs_vmcnt<4>(); else hs_vmcnt<0>();
   __builtin_amdgcn_s_barrier();
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) kr[ks] = row(smem, 0, ks);
+  for (int ks = 0; ks < 4; ++ks) {
+    kr[ks] = row(smem, 0, ks);
+    if (LCI_DQ_V2) vr[ks] = row(smem + TILE_B, 0, ks);
+  }
+  if (LCI_HS_LGKM0) __builtin_amdgcn_s_waitcnt(LGKM0_WAIT);   // (see the dK/dV kernel's loop header)
 
   for (int t = 0; t < nkt; ++t) {
     char* slot = smem + (t & (NSLOT - 1)) * SLOT_B;
     char* nslot = smem + ((t + 1) & (NSLOT - 1)) * SLOT_B;
-    // tile t+1 is published at gap 6 of half 1 (its first reader: the K rows at gaps 20-23); tile t+3's DMA goes
+    // tile t+1 is published at gap 6 of half 1 (its first reader: the K rows at gaps 16-19, V2, or 20-23); tile t+3's DMA goes
     // into the slot of tile t-1 (last read by half 1 of tile t-1, before this barrier), one operation per gap
     auto stage = [&](int g) __attribute__((always_inline)) {
       if (t + 1 < nkt && g == 6) {
@@ -1619,8 +1658,8 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
     auto stage0 = [&](int g) __attribute__((always_inline)) {
       if (LCI_DQ_DMASPREAD && t + 2 < nkt && (g == 6 || g == 18)) dma_op(t + 2, g == 6 ? 2 : 3);
     };
-    half(slot, 0, slot, 32, stage0);
-    half(slot, 32, nslot, 0, stage);
+    half(std::integral_constant<int, 0>{}, slot, 0, slot, 32, stage0);
+    half(std::integral_constant<int, 1>{}, slot, 32, nslot, 0, stage);
   }
   // query block 1 of the last half: its remaining VALU (wrapped into gaps 0-5) and its dQ^T
 #pragma unroll
@@ -1629,7 +1668,7 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
     for (int o = 0; o < 4; ++o) valu_op(DQ_SCHED[g][o], 1);
     if (g >= 8) {
       asm volatile("s_nop 1" ::: "memory");
-      dq_mfma(g - 8, 1);
+      dq_mfma(g - 8, 1, LCI_DQ_V2 ? 1 : 0);   // the last half is a half 1
     }
   }
   asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");

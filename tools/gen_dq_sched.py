@@ -52,6 +52,36 @@ def main():
         assert max(tC[j] for j in range(4, 8)) < DQ[qb] + 2, (qb, tC)
         placed[qb] = (tE, tM, tC)
     code = {"E": 0, "M": 1, "C": 2}
+    # Order within each gap (the periodic stream, gap 23 before gap 0): a conversion after the multiplies of its
+    # pair, and no op directly after the op whose result it reads when that op is an exp (trans use) or a
+    # multiply read by a conversion: the compiler pads both with an s_nop 0 and does not count the asm MFMA
+    # between gaps. Each gap takes the first permutation without such a pair, given the previous gap's last op.
+    import itertools
+
+    def reads(a, b):   # does op b read op a's result?
+        if a[1] != b[1]:
+            return False
+        return (a[0] == "E" and b[0] == "M" and a[2] == b[2]) or \
+            (a[0] == "M" and b[0] == "C" and a[2] in (2 * b[2], 2 * b[2] + 1))
+
+    def padded(prev, nxt):
+        return prev is not None and reads(prev, nxt) and prev[0] in ("E", "M")
+
+    for _ in range(2):   # second pass: gap 0 sees gap 23's final order
+        for g in range(NG):
+            prev = slots[g - 1][-1] if slots[g - 1] else None
+            best = None
+            for perm in itertools.permutations(slots[g]):
+                if any(reads(perm[j], perm[i]) for i in range(len(perm)) for j in range(i + 1, len(perm))):
+                    continue                       # a consumer before its producer
+                chain = [prev] + list(perm)
+                pads = sum(padded(chain[i], chain[i + 1]) for i in range(len(perm)))
+                if best is None or pads < best[0]:
+                    best = (pads, list(perm))
+            slots[g] = best[1]
+    pads = sum(padded(slots[g - 1][-1] if slots[g - 1] else None, slots[g][0]) for g in range(NG) if slots[g]) + \
+        sum(padded(slots[g][i], slots[g][i + 1]) for g in range(NG) for i in range(len(slots[g]) - 1))
+    print(f"// hazard pads left: {pads}", file=sys.stderr)
     rows = []
     for g, s in enumerate(slots):
         print(f"// gap {g:2d}: " + " ".join(f"{k}{qb}.{i}" for k, qb, i in s), file=sys.stderr)
