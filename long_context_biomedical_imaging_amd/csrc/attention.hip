@@ -855,7 +855,8 @@ constexpr int HS_NW = 4;
 #endif
 #ifndef LCI_HS_PROBE
 #define LCI_HS_PROBE 0   // timing probes (wrong results): 1 = no barrier, 2 = no tile staging after the prologue,
-                         // 3 = no LDS traffic, staging or barrier in the loop, 4 = no VALU in the loop
+                         // 3 = no LDS traffic, staging or barrier in the loop, 4 = no VALU in the loop, 5 / 6 / 7 = no
+                         // transposed-fragment / row-constant / Q-dO row reads
 #endif
 #ifndef LCI_HS_STAMP
 #define LCI_HS_STAMP 0   // diagnostic build: s_memtime at every segment start of tiles 64-95 of workgroups 0-7 (dK/dV),
@@ -1051,6 +1052,8 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
   auto trf = [&](const char* tile, int r0, int S, int c0) __attribute__((always_inline)) {
     const int row = r0 + 16 * S + 4 * h + ((lane & 15) >> 2);
     const int col = c0 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+    if (LCI_HS_PROBE == 8)   // probe: plain b64 reads of the same addresses (wrong operands)
+      return cat44(*(const bf16x4*)(tile + 2 * sw128(row, col)), *(const bf16x4*)(tile + 2 * sw128(row + 8, col)));
     return cat44(lds_tr4((const bf16*)(tile + 2 * sw128(row, col))),
                  lds_tr4((const bf16*)(tile + 2 * sw128(row + 8, col))));
   };
@@ -1143,14 +1146,14 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
   // transposed fragment f (gradient order: k-step f >> 2, d block (f >> 1) & 1, dO^T | Q^T) of rows r0 into set st
   bool probe_noread = false;
   auto tr_load = [&](int f, int st, const char* slot, int r0) __attribute__((always_inline)) {
-    if (LCI_HS_PROBE == 3 && probe_noread) return;
+    if ((LCI_HS_PROBE == 3 && probe_noread) || LCI_HS_PROBE == 5) return;
     const int s2 = f >> 2, db = (f >> 1) & 1;
     if (f & 1) tq[st][db][s2] = s2 ? trf(slot, r0, 1, 32 * db) : trf(slot, r0, 0, 32 * db);
     else tdo[st][db][s2] = s2 ? trf(slot + TILE_B, r0, 1, 32 * db) : trf(slot + TILE_B, r0, 0, 32 * db);
   };
   // one f32x4 piece (queries 8g + 4h .. + 3 of the half) of a chain's row-constant block
   auto rc_load = [&](f32x16& r, const char* rcslot, int which, int r0, int g) __attribute__((always_inline)) {
-    if (LCI_HS_PROBE == 3 && probe_noread) return;
+    if ((LCI_HS_PROBE == 3 && probe_noread) || LCI_HS_PROBE == 6) return;
     const f32x4 v = *(const f32x4*)((const float*)(rcslot + which * KT * 4) + r0 + 4 * h + 8 * g);
     r[4 * g] = v[0]; r[4 * g + 1] = v[1]; r[4 * g + 2] = v[2]; r[4 * g + 3] = v[3];
   };
@@ -1191,10 +1194,10 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
       valu_gap(g, 0, 1, 0, 0);
       if (g == 2) HS_KEEP(NL);
       if (g == 6) HS_KEEP(ND);
-      if (g >= 2 && g < 6 && LCI_HS_PROBE != 3) qa[g - 2] = qrow(nslot, nr0, g - 2);
+      if (g >= 2 && g < 6 && LCI_HS_PROBE != 3 && LCI_HS_PROBE != 7) qa[g - 2] = qrow(nslot, nr0, g - 2);
       if (g >= 6) {
         rc_load(NL, nrc, 0, nr0, g - 6);
-        if (LCI_HS_PROBE != 3) da[g - 6] = qrow(nslot + TILE_B, nr0, g - 6);
+        if (LCI_HS_PROBE != 3 && LCI_HS_PROBE != 7) da[g - 6] = qrow(nslot + TILE_B, nr0, g - 6);
       }
       sgap(2, g);
     }
@@ -1206,7 +1209,7 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
       valu_gap(g, 1, 0, 0, 1);
       if (g < 2) rc_load(NL, nrc, 0, nr0, g + 2);
       else if (g < 6) rc_load(ND, nrc, 1, nr0, g - 2);
-      else if (LCI_HS_PROBE != 3) da[g - 4] = qrow(nslot + TILE_B, nr0, g - 4);
+      else if (LCI_HS_PROBE != 3 && LCI_HS_PROBE != 7) da[g - 4] = qrow(nslot + TILE_B, nr0, g - 4);
       sgap(3, g);
     }
   };
@@ -1576,7 +1579,7 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
     } else if (g < 8) {
       if (g == 4) HS_MFMA_C0(P[0], vr[0], df[0][0], ND[0]); else HS_MFMA_C(P[0], vr[g - 4], df[0][g - 4]);
     } else if (g < 12) {
-      dq_mfma(g - 8, 1, C ^ 1);
+      dq_mfma(g - 8, 1, LCI_DQ_V2 ? C ^ 1 : 0);   // (one transposed-K set without LCI_DQ_V2)
     } else if (g < 16) {
       if (g == 12) HS_MFMA_C0(S[1], kr[0], qf[1][0], NL[1]); else HS_MFMA_C(S[1], kr[g - 12], qf[1][g - 12]);
     } else if (g < 20) {
