@@ -53,8 +53,9 @@ extern "C" {
  * lci_resample1d_adj and the round-3 entry points below; 13: lci_conv3_fwd_split, lci_conv3_pack_weight,
  * lci_inorm_apply_res, lci_convup_interleave, lci_window_bias with either table optional; 14: lci_window_attn_fwd
  * takes the transposed table biasT, lci_window_attn_bwd's plain table only for windows of N > 384; 15:
- * lci_window_attn_bwd pad_ws; 16: lci_attn_bwd delta_ws is (B, H, 2, L): the negated row constants -lse2 | -delta; 17: lci_window_bwd_needs_plain). */
-#define LCI_ABI_VERSION 17
+ * lci_window_attn_bwd pad_ws; 16: lci_attn_bwd delta_ws is (B, H, 2, L): the negated row constants -lse2 | -delta; 17: lci_window_bwd_needs_plain;
+ * 18: lci_attn_bwd delta_ws is lci_attn_bwd_ws_bytes(B, H, L) bytes). */
+#define LCI_ABI_VERSION 18
 const char* lci_last_error(void);
 int lci_abi_version(void);
 /* sha256 prefix of the sources the library was built from (build_lib.source_hash); the Python binding refuses a
@@ -73,11 +74,14 @@ int lci_attn_fwd(const void* qkv, void* out, float* lse2, float* knorm_ws, int B
                  float scale, void* stream);
 long long lci_attn_fwd_ws_bytes(int B, int L, int H);
 /* dqkv (B, L, 3*H*64) bf16 <- dQ, dK, dV in the packed layout; dout (B, L, H*64) bf16;
- * delta_ws (B, H, 2, L) f32 workspace (written by the call: -lse2 and -delta per query row). No atomics: bitwise
+ * delta_ws: 16-byte aligned workspace of lci_attn_bwd_ws_bytes(B, H, L) bytes, written by the call: the (B, H, 2, L)
+ * f32 rows -lse2 | -delta, then d-major bf16 copies of Q and dO that the dK/dV kernel stages. No atomics: bitwise
  * reproducible. */
 int lci_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse2, void* dqkv,
                  float* delta_ws, int B, int L, int H, int head_dim, float scale, void* stream);
-/* Same as lci_attn_bwd, one launch at a time (stage 0 = delta, 1 = dK/dV, 2 = dQ; -1 = all) for timing. */
+long long lci_attn_bwd_ws_bytes(int B, int H, int L);
+/* Same as lci_attn_bwd, one launch at a time (stage 0 = delta + the Q / dO copies, 1 = dK/dV, 2 = dQ; -1 = all)
+ * for timing. */
 int lci_attn_bwd_stage(int stage, const void* qkv, const void* out, const void* dout, const float* lse2,
                        void* dqkv, float* delta_ws, int B, int L, int H, int head_dim, float scale, void* stream);
 

@@ -85,6 +85,8 @@ struct AttnArgs {
   bf16* dk; bf16* dv;                              // bwd dkdv kernel
   float* lse2;                                     // (B, H, L)
   float* delta;                                    // bwd: (B, H, 2, L) negated row constants [-lse2 | -delta]
+  bf16* qdoT;                                      // bwd: (B, H, 2, 64, Lp) d-major Q | dO, P-pack query order
+  int Lp;                                          // bwd: L rounded up to 64
   long long bs_q, bs_k, bs_v, bs_o, bs_do, bs_out, bs_dk, bs_dv;   // batch strides (elements)
   int rs_q, rs_k, rs_v, rs_o, rs_do, rs_out, rs_dk, rs_dv;         // token (row) strides (elements)
   int hs;                                          // head stride (elements) in every tensor (= 64)
@@ -436,6 +438,44 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnArgs a) {
     float* ws = a.delta + ((long long)b * a.H + hh) * 2 * a.L;
     ws[row] = -a.lse2[((long long)b * a.H + hh) * a.L + row];
     ws[a.L + row] = -acc;
+  }
+}
+
+// d-major copies of Q and dO for the placed-stream dK/dV kernel (LCI_HS_TQ): row d of a 64-query tile holds the
+// tile's 64 queries, each 16-query group in the order of the bf16 P / dS packs' k index (position 8h + j holds
+// query (j & 3) + 8 (j >> 2) + 4h), so the dV / dK products read their Q^T / dO^T operand fragment (8 queries at one
+// d) with one ds_read_b128 instead of two transposed reads. Queries past L are zero. Workgroup = one 64-query tile of
+// one (b, h); a 64 x 64 tile of each tensor goes through LDS.
+__global__ __launch_bounds__(256) void attn_bwd_qdoT_kernel(AttnArgs a) {
+  __shared__ bf16 tl[2][64][72];   // [Q | dO][query][d], rows padded to 144 B
+  const int tid = threadIdx.x, t0 = blockIdx.x * 64, hh = blockIdx.y, b = blockIdx.z;
+#pragma unroll
+  for (int w = 0; w < 2; ++w) {
+    const bf16* src = w ? a.dout + b * a.bs_do + hh * a.hs : a.q + b * a.bs_q + hh * a.hs;
+    const int rs = w ? a.rs_do : a.rs_q;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      const int q = pass * 32 + (tid >> 3), c = tid & 7;
+      bf16x8 v = bf16x8{};
+      if (t0 + q < a.L) v = *(const bf16x8*)(src + (long long)(t0 + q) * rs + 8 * c);
+      *(bf16x8*)&tl[w][q][8 * c] = v;
+    }
+  }
+  __syncthreads();
+  // thread -> (tensor w, d, 16-query group g): 2 x 64 x 4 = 512 items, 2 per thread
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int item = it * 256 + tid, w = item >> 8, d = (item >> 2) & 63, g = item & 3;
+    bf16x8 lo, hi;
+#pragma unroll
+    for (int p = 0; p < 16; ++p) {
+      const int hp = p >> 3, j = p & 7;
+      const bf16 v = tl[w][16 * g + (j & 3) + 8 * (j >> 2) + 4 * hp][d];
+      if (p < 8) lo[p] = v; else hi[p - 8] = v;
+    }
+    bf16* dst = a.qdoT + ((((long long)b * a.H + hh) * 2 + w) * 64 + d) * a.Lp + t0 + 16 * g;
+    *(bf16x8*)dst = lo;
+    *(bf16x8*)(dst + 8) = hi;
   }
 }
 
@@ -922,6 +962,9 @@ __device__ __forceinline__ void hs_vmcnt() {   // s_waitcnt vmcnt(N), lgkmcnt / 
 #ifndef LCI_HS_AHOME
 #define LCI_HS_AHOME 1       // K / V fragments homed in AGPRs before the loop (0: compiler's choice; unsafe)
 #endif
+#ifndef LCI_HS_TQ
+#define LCI_HS_TQ 0          // 1: dV / dK operands from d-major Q^T / dO^T tiles (attn_bwd_qdoT_kernel), one b128
+#endif                       // each instead of two transposed reads: 21.5 vs 20.85 ms same box (slower)
 #ifndef LCI_HS_LGKM0
 #define LCI_HS_LGKM0 1       // drain the prologue's LDS reads before the loop (see the loop header)
 #endif
@@ -936,13 +979,15 @@ constexpr unsigned LGKM0_WAIT = 0xC07F;
 #endif                       // of half 1, same box)
 __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArgs a) {
   constexpr int TILE_B = KT * DH * 2;               // bytes of a Q or dO tile (128-B rows)
-  constexpr int SLOT_B = 2 * TILE_B;                // Q | dO of one tile
+  // Q | dO of one tile (LCI_HS_TQ: + the d-major Q^T | dO^T tiles, rows = d, read by the dV / dK products)
+  constexpr int SLOT_B = (LCI_HS_TQ ? 4 : 2) * TILE_B;
   constexpr int RC_B = 2 * KT * 4;                  // -lse2[64] | -delta[64] of one tile
   constexpr int NSLOT = 4;                          // ring: tile t, t+1 (published), t+2, t+3 (in flight)
+  constexpr int NOPS = LCI_HS_TQ ? 9 : 5;           // LDS-DMA operations per wave and tile
   static_assert((NSLOT & (NSLOT - 1)) == 0, "ring slot of tile t is t & (NSLOT - 1)");
-  // the Q / dO ring fills exactly 64 KB, so every fragment read of every slot is one lane register + a 16-bit
-  // immediate (slot, dO and row offsets); the row-constant rows follow in their own 2 KB
-  static_assert(NSLOT * SLOT_B == 65536, "Q / dO ring reachable by DS immediates");
+  // without LCI_HS_TQ the Q / dO ring fills exactly 64 KB, so every fragment read of every slot is one lane register
+  // + a 16-bit immediate (slot, dO and row offsets); the row-constant rows follow in their own 2 KB
+  static_assert(LCI_HS_TQ || NSLOT * SLOT_B == 65536, "Q / dO ring reachable by DS immediates");
   __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT_B + NSLOT * RC_B];
   char* const rcs = smem + NSLOT * SLOT_B;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1001,6 +1046,10 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
   const rsrc_t rq = make_rsrc(a.q + b * a.bs_q + hh * a.hs, (uint32_t)(L - 1) * (uint32_t)rs2q + DH * 2);
   const rsrc_t rd = make_rsrc(a.dout + b * a.bs_do + hh * a.hs, (uint32_t)(L - 1) * (uint32_t)rs2d + DH * 2);
   const rsrc_t rr = make_rsrc(a.delta + ((long long)b * a.H + hh) * 2 * L + (wave & 1) * L, (uint32_t)L * 4);
+  // d-major Q^T / dO^T rows (LCI_HS_TQ): row d of (b, hh, which) is Lp bf16; a tile is 128 B at column 64 t
+  const int rs2t = a.Lp * 2;
+  const rsrc_t rqt = make_rsrc(a.qdoT + ((long long)b * a.H + hh) * 2 * 64 * a.Lp, (uint32_t)(64 * rs2t));
+  const rsrc_t rdt = make_rsrc(a.qdoT + (((long long)b * a.H + hh) * 2 + 1) * 64 * a.Lp, (uint32_t)(64 * rs2t));
   // row = 16 wave + 8 j + prow (piece j = 0, 1): g(row) = ((row >> 2) & 3) | ((row >> 1) & 1) << 2 = (2j + (prow >> 2))
   // | ((prow >> 1) & 1) << 2
   const int prow = lane >> 3;
@@ -1008,6 +1057,7 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
   const int pch1 = (lane & 7) ^ ((2 + (prow >> 2)) | ((prow >> 1) & 1) << 2);
   const int dq0 = (16 * wave + prow) * rs2q + 16 * pch0, dq1 = (16 * wave + 8 + prow) * rs2q + 16 * pch1;
   const int dd0 = (16 * wave + prow) * rs2d + 16 * pch0, dd1 = (16 * wave + 8 + prow) * rs2d + 16 * pch1;
+  const int dt0 = (16 * wave + prow) * rs2t + 16 * pch0, dt1 = (16 * wave + 8 + prow) * rs2t + 16 * pch1;
   const unsigned lds0 = (unsigned)(uintptr_t)(LCI_LDS char*)smem;
   auto dma_op = [&](int t, int i) __attribute__((always_inline)) {   // operation i (0-4) of tile t
     const unsigned sb = lds0 + (unsigned)((t & (NSLOT - 1)) * SLOT_B);
@@ -1017,10 +1067,16 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
     if (i == 3) hs_dma16(rd, dd1, t * KT * rs2d, sb + TILE_B + 2048 * wave + 1024);
     if (i == 4) hs_dma4(rr, lane * 4, t * KT * 4, lds0 + (unsigned)(NSLOT * SLOT_B + (t & (NSLOT - 1)) * RC_B +
                                                                      (wave & 1) * KT * 4));
+    if (LCI_HS_TQ) {   // the d-major tiles: rows = d, the tile's 128 B at byte column 128 t
+      if (i == 5) hs_dma16(rqt, dt0, t * 128, sb + 2 * TILE_B + 2048 * wave);
+      if (i == 6) hs_dma16(rqt, dt1, t * 128, sb + 2 * TILE_B + 2048 * wave + 1024);
+      if (i == 7) hs_dma16(rdt, dt0, t * 128, sb + 3 * TILE_B + 2048 * wave);
+      if (i == 8) hs_dma16(rdt, dt1, t * 128, sb + 3 * TILE_B + 2048 * wave + 1024);
+    }
   };
   auto dma_tile = [&](int t) __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < 5; ++i) dma_op(t, i);
+    for (int i = 0; i < NOPS; ++i) dma_op(t, i);
   };
   // register staging (LCI_HS_STG 1): thread -> rows (srow, srow + 32), chunk sch of the Q and dO tiles, plus one row
   // constant per lane in waves 0 / 1; two sets, a tile's loads issued two tiles before its LDS store
@@ -1148,6 +1204,12 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
   auto tr_load = [&](int f, int st, const char* slot, int r0) __attribute__((always_inline)) {
     if ((LCI_HS_PROBE == 3 && probe_noread) || LCI_HS_PROBE == 5) return;
     const int s2 = f >> 2, db = (f >> 1) & 1;
+    if (LCI_HS_TQ) {   // d-major tile: lane (h, r32) reads d = 32 db + r32, queries r0 + 16 s2 + 8h .. +7 (pack order)
+      const char* tt = slot + (f & 1 ? 2 : 3) * TILE_B;
+      const bf16x8 v = *(const bf16x8*)(tt + 2 * sw128(32 * db + r32, r0 + 16 * s2 + 8 * h));
+      if (f & 1) tq[st][db][s2] = v; else tdo[st][db][s2] = v;
+      return;
+    }
     if (f & 1) tq[st][db][s2] = s2 ? trf(slot, r0, 1, 32 * db) : trf(slot, r0, 0, 32 * db);
     else tdo[st][db][s2] = s2 ? trf(slot + TILE_B, r0, 1, 32 * db) : trf(slot + TILE_B, r0, 0, 32 * db);
   };
@@ -1254,15 +1316,14 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
     if (nqt > 1) dma_tile(1);
     // tile 2's operations 3-4 come at segs A / B of tile 0 (the loop has no first-tile special case: a peeled copy
     // would let the compiler fold the zero-initialised state into moves beside the asm MFMAs)
-    constexpr bool SPREAD = LCI_HS_DMASPREAD && LCI_HS_PROBE != 2 && LCI_HS_PROBE != 3;
+    constexpr bool SPREAD = LCI_HS_DMASPREAD && !LCI_HS_TQ && LCI_HS_PROBE != 2 && LCI_HS_PROBE != 3;
     if (nqt > 2) {
-      dma_op(2, 0); dma_op(2, 1); dma_op(2, 2);
-      if (!SPREAD) { dma_op(2, 3); dma_op(2, 4); }
+      if (SPREAD) { dma_op(2, 0); dma_op(2, 1); dma_op(2, 2); } else dma_tile(2);
     }
     if (LCI_HS_PROBE == 2 && nqt > 3) dma_tile(3);   // probe: every ring slot holds real data
     if (LCI_HS_PROBE == 2) hs_vmcnt<0>();
-    if (nqt > 2) { if (SPREAD) hs_vmcnt<8>(); else hs_vmcnt<10>(); }
-    else if (nqt > 1) hs_vmcnt<5>(); else hs_vmcnt<0>();
+    if (nqt > 2) { if (SPREAD) hs_vmcnt<8>(); else hs_vmcnt<2 * NOPS>(); }
+    else if (nqt > 1) hs_vmcnt<NOPS>(); else hs_vmcnt<0>();
   } else {
     load_tile(stg[0], 0);
     hs_vmcnt<0>();
@@ -1301,7 +1362,7 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
     // t-1, which every wave finished before this barrier
     auto stage = [&]() __attribute__((always_inline)) {
       if (t + 1 < nqt) {
-        if (t + 2 < nqt) hs_vmcnt<5>(); else hs_vmcnt<0>();
+        if (t + 2 < nqt) hs_vmcnt<NOPS>(); else hs_vmcnt<0>();
         if constexpr (LCI_HS_STG == 1) store_tile(stg[P1], nslot);
         stamp(8);
         // no LDS fence: this wave's reads of the slot tile t+3 overwrites were consumed before now, and the new
@@ -1321,14 +1382,16 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
     // then leaves exactly them in flight; tile 2's come at tile 0, the prologue issued only its operations 0-2)
     constexpr bool DMA_ON = LCI_HS_STG == 0 && LCI_HS_PROBE != 2 && LCI_HS_PROBE != 3;
     auto dmas1 = [&](int seg, int g) __attribute__((always_inline)) {
-      if (LCI_HS_DMASPREAD) {
+      if (LCI_HS_DMASPREAD && !LCI_HS_TQ) {
         if (DMA_ON && g == 3 && seg >= 1 && t + 3 < nqt) dma_op(t + 3, seg - 1);
       } else if (DMA_ON && seg == 1 && g < 5 && t + 3 < nqt) {
         dma_op(t + 3, g);
+      } else if (DMA_ON && LCI_HS_TQ && seg == 2 && g < 4 && t + 3 < nqt) {   // the d-major pieces in seg C
+        dma_op(t + 3, 5 + g);
       }
     };
     auto dmas0 = [&](int seg, int g) __attribute__((always_inline)) {
-      if (LCI_HS_DMASPREAD && DMA_ON && g == 3 && seg < 2 && t + 2 < nqt) dma_op(t + 2, 3 + seg);
+      if (LCI_HS_DMASPREAD && !LCI_HS_TQ && DMA_ON && g == 3 && seg < 2 && t + 2 < nqt) dma_op(t + 2, 3 + seg);
     };
     auto none = []() __attribute__((always_inline)) {};
     if constexpr (LCI_HS_V == 1) {
@@ -2227,6 +2290,14 @@ extern "C" int lci_attn_fwd(const void* qkv, void* out, float* lse2, float* knor
 }
 
 // stage: -1 = all three launches; 0 = delta, 1 = dK/dV, 2 = dQ (for per-kernel timing)
+// backward workspace: (B, H, 2, L) f32 negated row constants, then (256-B aligned) the (B, H, 2, 64, Lp) bf16
+// d-major Q | dO copies of LCI_HS_TQ
+static long long attn_bwd_rc_bytes(int B, int H, int L) { return ((long long)B * H * 2 * L * 4 + 255) / 256 * 256; }
+extern "C" long long lci_attn_bwd_ws_bytes(int B, int H, int L) {
+  const long long Lp = (L + 63) / 64 * 64;
+  return attn_bwd_rc_bytes(B, H, L) + (LCI_HS_TQ ? (long long)B * H * 2 * 64 * Lp * 2 : 0);
+}
+
 extern "C" int lci_attn_bwd_stage(int stage, const void* qkv, const void* out, const void* dout, const float* lse2,
                                   void* dqkv, float* delta_ws, int B, int L, int H, int head_dim, float scale,
                                   void* stream) {
@@ -2241,6 +2312,8 @@ extern "C" int lci_attn_bwd_stage(int stage, const void* qkv, const void* out, c
   a.q = base; a.k = base + H * DH; a.v = base + 2 * H * DH;
   a.o = (const bf16*)out; a.dout = (const bf16*)dout;
   a.lse2 = (float*)lse2; a.delta = delta_ws;
+  a.Lp = (L + 63) / 64 * 64;   // the d-major Q | dO copies follow the row constants (lci_attn_bwd_ws_bytes)
+  a.qdoT = (bf16*)((char*)delta_ws + attn_bwd_rc_bytes(B, H, L));
   a.bs_q = a.bs_k = a.bs_v = (long long)L * rs;
   a.rs_q = a.rs_k = a.rs_v = rs;
   a.bs_o = a.bs_do = (long long)L * H * DH;
@@ -2263,6 +2336,10 @@ extern "C" int lci_attn_bwd_stage(int stage, const void* qkv, const void* out, c
   if (stage < 0 || stage == 0) {
     hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((L + 31) / 32, H, B), dim3(256), 0, s, a);
     LCI_LAUNCH_CHECK();
+    if (LCI_HS_TQ) {
+      hipLaunchKernelGGL(attn_bwd_qdoT_kernel, dim3(a.Lp / 64, H, B), dim3(256), 0, s, a);
+      LCI_LAUNCH_CHECK();
+    }
   }
 #ifndef LCI_DKDV16
 #define LCI_DKDV16 1   // 16x16x32 dK/dV (default): 22.1 vs 22.6-22.8 ms for the 32x32x16 kernel, three same-box A/Bs

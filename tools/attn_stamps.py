@@ -16,7 +16,7 @@ qkv = torch.randn(B, L, 3 * H * 64, device="cuda").to(torch.bfloat16)
 dout = torch.randn(B, L, H * 64, device="cuda").to(torch.bfloat16)
 out, lse = kernels.attn_fwd(qkv, H, 0.125)
 dqkv = torch.zeros_like(qkv)
-ws = torch.empty(B, H, 2, L, device="cuda", dtype=torch.float32)
+ws = torch.empty(int(_lib.load().lci_attn_bwd_ws_bytes(B, H, L)), device="cuda", dtype=torch.uint8)
 args = (qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(), dqkv.data_ptr(), ws.data_ptr(),
         B, L, H, 64, 0.125, _lib.stream_of(qkv))
 _lib.call("lci_attn_bwd_stage", 0, *args)
