@@ -54,8 +54,9 @@ extern "C" {
  * lci_inorm_apply_res, lci_convup_interleave, lci_window_bias with either table optional; 14: lci_window_attn_fwd
  * takes the transposed table biasT, lci_window_attn_bwd's plain table only for windows of N > 384; 15:
  * lci_window_attn_bwd pad_ws; 16: lci_attn_bwd delta_ws is (B, H, 2, L): the negated row constants -lse2 | -delta; 17: lci_window_bwd_needs_plain;
- * 18: lci_attn_bwd delta_ws is lci_attn_bwd_ws_bytes(B, H, L) bytes). */
-#define LCI_ABI_VERSION 18
+ * 18: lci_attn_bwd delta_ws is lci_attn_bwd_ws_bytes(B, H, L) bytes; 19: selective-scan checkpoints in the I/O
+ * dtype). */
+#define LCI_ABI_VERSION 19
 const char* lci_last_error(void);
 int lci_abi_version(void);
 /* sha256 prefix of the sources the library was built from (build_lib.source_hash); the Python binding refuses a
@@ -186,19 +187,19 @@ int lci_inorm_apply_res(const void* x, const float* stats, const void* y, const 
  * strides[16] (elements) = {bu,tu, bd,td, bB,tB, bC,tC, by,ty, bdy,tdy, bdu,tdu, bdd,tdd} (batch, token).
  * A (Dx, 8), D (Dx), delta_bias (Dx) f32 (D, delta_bias may be null). delta' = softplus(delta + delta_bias)
  * when delta_softplus, else delta + delta_bias.
- * chunk: multiple of 16. Workspaces f32: xend, xinit (B*nch*Dx*8), sdt (B*nch*Dx), nch = ceil(L/chunk);
- * ckpt (B*ceil(L/16)*Dx*8) or null (needed by the backward). */
+ * chunk: multiple of 8. Workspaces f32: xend, xinit (B*nch*Dx*8), sdt (B*nch*Dx), nch = ceil(L/chunk);
+ * ckpt (B*ceil(L/8)*Dx*8) elements of the I/O dtype (bf16 I/O: bf16 states) or null (needed by the backward). */
 int lci_selective_scan_fwd(int dtype, const void* u, const void* delta, const float* A, const void* Bm,
                            const void* Cm, const float* D, const float* delta_bias, void* y,
                            const long long* strides, int B, int L, int Dx, int N, int chunk, int delta_softplus,
-                           float* xend, float* xinit, float* sdt, float* ckpt, void* stream);
+                           float* xend, float* xinit, float* sdt, void* ckpt, void* stream);
 /* du, ddelta (B, L, Dx) written; dBC (B, L, 16) f32 = [dB | dC], dA (Dx, 8), dD, ddelta_bias accumulated.
  * sdt / ckpt from the forward with the same chunk; gl, gin: (B*nch*Dx*8) f32 workspaces. */
 int lci_selective_scan_bwd(int dtype, const void* u, const void* delta, const float* A, const void* Bm,
                            const void* Cm, const float* D, const float* delta_bias, const void* dy, void* du,
                            void* ddelta, float* dBC, float* dA, float* dD, float* ddelta_bias,
                            const long long* strides, int B, int L, int Dx, int N, int chunk, int delta_softplus,
-                           const float* sdt, const float* ckpt, float* gl, float* gin, void* stream);
+                           const float* sdt, const void* ckpt, float* gl, float* gin, void* stream);
 
 /* SiLU(depthwise conv1d(k = 3, 'same')) of both channel halves of in (B, L, 2C) (token stride in_ts):
  * ox (B, L, C) (token stride ox_ts) and oz at column offset zoff of a (B, L, oz_ts) buffer. */

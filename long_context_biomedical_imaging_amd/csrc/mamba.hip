@@ -26,7 +26,8 @@ struct ScanArgs {
   const void* u; const void* delta; const void* Bm; const void* Cm; const void* dy;
   const float* A; const float* D; const float* dbias;
   void* y; void* du; void* ddelta;
-  float* xend; float* sdt; float* xinit; float* ckpt;   // (B,nch,Dx,N) (B,nch,Dx) (B,nch,Dx,N) (B,nck,Dx,N)
+  float* xend; float* sdt; float* xinit;                // (B,nch,Dx,N) (B,nch,Dx) (B,nch,Dx,N)
+  void* ckpt;                                           // (B,nck,Dx,N) states every CKPT steps, in the I/O dtype
   float* gl; float* gin;                                // (B,nch,Dx,N) x2
   float* dBC;                                           // (B, L, 2N) f32
   float* dA; float* dD; float* ddbias;                  // (Dx,N) (Dx) (Dx), accumulated
@@ -169,11 +170,18 @@ __device__ __forceinline__ void lds_row8(const float* p, float (&v)[SCAN_N]) {
 template <typename T, int MODE>
 __device__ __forceinline__ void scan_fwd_step(const ScanArgs& a, float (&x)[SCAN_N], const float (&A2)[SCAN_N],
                                               float bias, float Dd, float uv, float drv, const float* row, int t,
-                                              bool valid, int d, float* ckb, const Col<T>& ycol, float& sumdt) {
+                                              bool valid, int d, T* ckb, const Col<T>& ycol, float& sumdt) {
   if (MODE == 1 && a.write_ckpt && ((t & (CKPT - 1)) == 0) && valid) {
-    float* cp = (ckb + (long long)(t / CKPT) * a.Dx * SCAN_N) + d * SCAN_N;
-    *(f32x4*)cp = f32x4{x[0], x[1], x[2], x[3]};
-    *(f32x4*)(cp + 4) = f32x4{x[4], x[5], x[6], x[7]};
+    T* cp = (ckb + (long long)(t / CKPT) * a.Dx * SCAN_N) + d * SCAN_N;
+    if constexpr (sizeof(T) == 2) {   // bf16 I/O: bf16 checkpoints (one 16-B store; the backward recomputes from them)
+      bf16x8 v;
+#pragma unroll
+      for (int n = 0; n < SCAN_N; ++n) v[n] = to_bf16(x[n]);
+      *(bf16x8*)cp = v;
+    } else {
+      *(f32x4*)cp = f32x4{x[0], x[1], x[2], x[3]};
+      *(f32x4*)(cp + 4) = f32x4{x[4], x[5], x[6], x[7]};
+    }
   }
   float Bv[SCAN_N];
   lds_row8(row, Bv);
@@ -223,7 +231,7 @@ __global__ __launch_bounds__(256) void scan_fwd_kernel(ScanArgs a) {
   const Col<T> ycol((T*)a.y + b * a.by, a.L, a.ty, a.Dx, d, valid);
   const T* Bp = (const T*)a.Bm + b * a.bB;
   const T* Cp = (const T*)a.Cm + b * a.bC;
-  float* ckb = a.ckpt + (long long)b * a.nck * a.Dx * SCAN_N;
+  T* ckb = (T*)a.ckpt + (long long)b * a.nck * a.Dx * SCAN_N;
   float* bc = bcl[wv];
   const int t0 = chunk * a.Tc, t1 = min(a.L, t0 + a.Tc);
   float sumdt = 0.f;
@@ -501,16 +509,14 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(ScanArgs a) {
   const T* Cp = (const T*)a.Cm + b * a.bC;
   T* dub = (T*)a.du + b * a.bdu;
   T* ddb = (T*)a.ddelta + b * a.bdd;
-  const float* ckb = a.ckpt + (long long)b * a.nck * a.Dx * SCAN_N;
+  const T* ckb = (const T*)a.ckpt + (long long)b * a.nck * a.Dx * SCAN_N;
   const int t0 = chunk * a.Tc, t1 = min(a.L, t0 + a.Tc);
   const int nsb = (t1 - t0 + CKPT - 1) / CKPT;
   // per-lane operands of one sub-block, loaded a sub-block ahead
   float nck[SCAN_N], nu[CKPT], nd[CKPT], ng[CKPT];
   auto load_lane = [&](int s0) {
-    const float* cp = (ckb + (long long)(s0 / CKPT) * a.Dx * SCAN_N) + dd * SCAN_N;
-    const f32x4 c0 = *(const f32x4*)cp, c1 = *(const f32x4*)(cp + 4);
-#pragma unroll
-    for (int n = 0; n < 4; ++n) { nck[n] = c0[n]; nck[n + 4] = c1[n]; }
+    const T* cp = (ckb + (long long)(s0 / CKPT) * a.Dx * SCAN_N) + dd * SCAN_N;
+    ld8(cp, nck);
 #pragma unroll
     for (int i = 0; i < CKPT; ++i) {
       const long long t = min(s0 + i, t1 - 1);
@@ -940,11 +946,11 @@ static int scan_strides(ScanArgs& a, const long long* s, int dtype) {
   return 0;
 }
 
-// Workspace (f32): xend, xinit (B*nch*Dx*N each), sdt (B*nch*Dx), ckpt (B*nck*Dx*N) if ckpt != null.
+// Workspace (f32): xend, xinit (B*nch*Dx*N each), sdt (B*nch*Dx); ckpt (B*nck*Dx*N, the I/O dtype) if not null.
 extern "C" int lci_selective_scan_fwd(int dtype, const void* u, const void* delta, const float* A, const void* Bm,
                                       const void* Cm, const float* D, const float* delta_bias, void* y,
                                       const long long* strides, int B, int L, int Dx, int N, int chunk,
-                                      int delta_softplus, float* xend, float* xinit, float* sdt, float* ckpt,
+                                      int delta_softplus, float* xend, float* xinit, float* sdt, void* ckpt,
                                       void* stream) {
   ScanArgs a{};
   if (scan_fill(a, B, L, Dx, N, chunk)) return 1;
@@ -982,7 +988,7 @@ extern "C" int lci_selective_scan_bwd(int dtype, const void* u, const void* delt
                                       const void* Cm, const float* D, const float* delta_bias, const void* dy,
                                       void* du, void* ddelta, float* dBC, float* dA, float* dD, float* ddelta_bias,
                                       const long long* strides, int B, int L, int Dx, int N, int chunk,
-                                      int delta_softplus, const float* sdt, const float* ckpt, float* gl, float* gin,
+                                      int delta_softplus, const float* sdt, const void* ckpt, float* gl, float* gin,
                                       void* stream) {
   ScanArgs a{};
   if (scan_fill(a, B, L, Dx, N, chunk)) return 1;
@@ -991,7 +997,7 @@ extern "C" int lci_selective_scan_bwd(int dtype, const void* u, const void* delt
   if (scan_check_bc(Bm, Cm, strides[5], strides[7], dtype)) return 1;
   a.u = u; a.delta = delta; a.A = A; a.Bm = Bm; a.Cm = Cm; a.D = D; a.dbias = delta_bias; a.dy = dy;
   a.du = du; a.ddelta = ddelta; a.dBC = dBC; a.dA = dA; a.dD = dD; a.ddbias = ddelta_bias;
-  a.sdt = (float*)sdt; a.ckpt = (float*)ckpt; a.gl = gl; a.gin = gin;
+  a.sdt = (float*)sdt; a.ckpt = const_cast<void*>(ckpt); a.gl = gl; a.gin = gin;
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((a.nch + 3) / 4, (Dx + 63) / 64, B);
   if (dtype == 1) hipLaunchKernelGGL((scan_bwd_agg_kernel<bf16>), grid, dim3(256), 0, s, a);

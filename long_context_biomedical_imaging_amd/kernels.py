@@ -319,7 +319,8 @@ class _SelectiveScanCL(torch.autograd.Function):
         xinit = torch.empty(B, nch, Dx, N, **f32)
         sdt = torch.empty(B, nch, Dx, **f32)
         need_grad = any(ctx.needs_input_grad)
-        ckpt = torch.empty(B, nck, Dx, N, **f32) if need_grad else None
+        # states every CKPT steps for the backward's recompute, in the I/O dtype (bf16 I/O: bf16 states, half the bytes)
+        ckpt = torch.empty(B, nck, Dx, N, device=u.device, dtype=dt) if need_grad else None
         Af = A.float().contiguous()
         Dv = D.float().contiguous() if D is not None else torch.zeros(Dx, **f32)
         bv = delta_bias.float().contiguous() if delta_bias is not None else torch.zeros(Dx, **f32)
