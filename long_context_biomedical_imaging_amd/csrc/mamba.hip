@@ -20,6 +20,9 @@ namespace lci {
 
 constexpr int SCAN_N = 8;     // d_state (the reference always uses 8: backbone_vit.py:184, backbone_swin.py:329)
 constexpr int CKPT = 8;       // backward checkpoint spacing (steps); sub-block states live in registers
+#ifndef LCI_SCAN_GXA
+#define LCI_SCAN_GXA 1        // backward g a x_{t-1} as (g a) x_{t-1} from the recomputed states (0: g (x_t - dt u B))
+#endif
 constexpr float LOG2E = 1.4426950408889634f;
 
 struct ScanArgs {
@@ -595,10 +598,12 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(ScanArgs a) {
           v[SCAN_N + n] = gy * xs[i][n];                   // dC_t partial
           v[n] = gt * dtuv;                                // dB_t partial
           sgB = fmaf(gt, Bv[n], sgB);
-          const float gxa = gt * fmaf(-dtu, Bv[n], xs[i][n]);   // g * a * x_{t-1} = g (x_t - dt u B)
+          h[n] = at[i][n] * gt;                            // the adjoint carried to step t-1 (= g a)
+          // g * a * x_{t-1}: (g a) x_{t-1} from the sub-block's recomputed states (one multiply, no cancellation);
+          // at the sub-block's first step x_{t-1} is the checkpoint, no longer live: g (x_t - dt u B)
+          const float gxa = LCI_SCAN_GXA && i > 0 ? h[n] * xs[i - 1][n] : gt * fmaf(-dtu, Bv[n], xs[i][n]);
           sA = fmaf(gxa, A2[n], sA);
           dA[n] = fmaf(gxa, dt, dA[n]);
-          h[n] = at[i][n] * gt;
         }
         const float du = fmaf(dt, sgB, Dd * gy);
         const float ddt = fmaf(uf[i], sgB, sA * LN2);
