@@ -1758,6 +1758,439 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
   }
 }
 
+// ------------------------------------------------ forward: one wave per SIMD, placed MFMA / VALU / LDS stream
+// The placed-stream structure of the backward kernels for O = softmax(Q K^T) V (backbone_vit.py:191-201): a workgroup =
+// 4 waves x 64 queries (two query blocks of 32 on the MFMA lane), Q~ = c q fragments and the O^T accumulators in
+// AGPRs, K | V tiles of 64 keys by LDS-DMA into a 4-slot ring two tiles ahead. Per 32-key half and wave: 16 MFMAs
+//   gaps 0-3: S^T = K Q~^T chain of block 0 | 4-7: O^T += V^T P^T of block 1 (previous half) |
+//   8-11: S^T chain of block 1 | 12-15: O^T += V^T P^T of block 0,
+// against 32 exp2, 32 row-sum adds and 16 bf16 packs, placed by FW_SCHED (tools/gen_fwd_sched.py: every gap 2 exp2 +
+// 2 adds + 1 pack beside its MFMA). LDS reads: this half's transposed V fragments at gaps 0-7 (set p & 1: block 1 reads
+// the previous half's set at gaps 4-7), the next half's K rows at gaps 12-15.
+// Max-free softmax with one reference per query: m = the exact row max over the first key tile, which every chain
+// starts from (-m as the initial accumulator), valid while ||q~|| max||k|| - m <= 64 over the whole key range (then
+// p <= 2^64, exact in f32 sums and bf16 P: the attn_fwd2_kernel criterion, checked once per workgroup from the
+// per-tile key norms); a workgroup outside it takes the exact online-softmax loop below (rescaled per 32 keys).
+// gap  0: A1.4 C1.2 A1.5 E1.6 E1.7
+// gap  1: A1.6 C1.3 A1.7 E1.8 E1.9
+// gap  2: A1.8 C1.4 A1.9 E1.10 E1.11
+// gap  3: A1.10 C1.5 A1.11 E1.12 E1.13
+// gap  4: A1.12 C1.6 A1.13 E1.14 E1.15
+// gap  5: A1.14 C1.7 A1.15 E0.0 E0.1
+// gap  6: A0.0 C0.0 A0.1 E0.2 E0.3
+// gap  7: A0.2 C0.1 A0.3 E0.4 E0.5
+// gap  8: A0.4 C0.2 A0.5 E0.6 E0.7
+// gap  9: A0.6 C0.3 A0.7 E0.8 E0.9
+// gap 10: A0.8 C0.4 A0.9 E0.10 E0.11
+// gap 11: A0.10 C0.5 A0.11 E0.12 E0.13
+// gap 12: A0.12 C0.6 A0.13 E0.14 E0.15
+// gap 13: E1.0 E1.1 C0.7 A0.14 A0.15
+// gap 14: C1.0 A1.0 A1.1 E1.2 E1.3
+// gap 15: A1.2 C1.1 A1.3 E1.4 E1.5
+constexpr unsigned char FW_SCHED[16][5] = {
+    {0x64, 0xa2, 0x65, 0x26, 0x27},
+    {0x66, 0xa3, 0x67, 0x28, 0x29},
+    {0x68, 0xa4, 0x69, 0x2a, 0x2b},
+    {0x6a, 0xa5, 0x6b, 0x2c, 0x2d},
+    {0x6c, 0xa6, 0x6d, 0x2e, 0x2f},
+    {0x6e, 0xa7, 0x6f, 0x00, 0x01},
+    {0x40, 0x80, 0x41, 0x02, 0x03},
+    {0x42, 0x81, 0x43, 0x04, 0x05},
+    {0x44, 0x82, 0x45, 0x06, 0x07},
+    {0x46, 0x83, 0x47, 0x08, 0x09},
+    {0x48, 0x84, 0x49, 0x0a, 0x0b},
+    {0x4a, 0x85, 0x4b, 0x0c, 0x0d},
+    {0x4c, 0x86, 0x4d, 0x0e, 0x0f},
+    {0x20, 0x21, 0x87, 0x4e, 0x4f},
+    {0xa0, 0x60, 0x61, 0x22, 0x23},
+    {0x62, 0xa1, 0x63, 0x24, 0x25}};
+#ifndef LCI_FWD_HS
+#define LCI_FWD_HS 1
+#endif
+#ifndef LCI_FWD_PROBE
+#define LCI_FWD_PROBE 0   // timing probes (wrong results): 1 = no LDS reads in the loop, 2 = the reads without waits
+#endif
+
+// initial S^T of query block 1 before the first half: the exps of block 1 that FW_SCHED wraps into the next half
+// (E1.i in gaps before START_E = 13) see NEG_BIG (exp2 -> 0); the elements exponentiated in the previous half's gaps
+// 13-15 are already "exponentiated": 0. Either way the first half adds and packs zeros for the missing half -1.
+__host__ __device__ constexpr bool fw_wrapped_exp(int i) {
+  for (int g = 0; g < 13; ++g)
+    for (int o = 0; o < 5; ++o)
+      if (FW_SCHED[g][o] == (0x20 | i)) return true;
+  return false;
+}
+
+__global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, const float* knorm) {
+  constexpr int TILE_B = KT * DH * 2;               // bytes of a K or V tile (128-B rows)
+  constexpr int SLOT_B = 2 * TILE_B;                // K | V
+  constexpr int NSLOT = 4;
+  static_assert(NSLOT * SLOT_B == 65536, "ring reachable by DS immediates");
+  __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT_B];
+  __shared__ int unsafe_wg;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hh = blockIdx.y, b = blockIdx.z;
+  const int L = a.L;
+  const int h = lane >> 5, r32 = lane & 31;
+  const int qw0 = blockIdx.x * (HS_NW * 64) + wave * 64;
+  const int nkt = (L + KT - 1) / KT;
+  if (tid == 0) unsafe_wg = 0;
+
+  // Q~ = c q as B operands: lane holds q~[qw0 + 32 qb + r32][16 ks + 8h + j]; qn = ||q~|| of the lane's query
+  bf16x8 qf[2][4];
+  float qn[2];
+  {
+    const bf16* qp = a.q + b * a.bs_q + hh * a.hs;
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const int q = qw0 + 32 * qb + r32;
+      float ss = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        bf16x8 t{};
+        if (q < L) t = *(const bf16x8*)(qp + (long long)q * a.rs_q + 16 * ks + 8 * h);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          t[j] = to_bf16(to_f32(t[j]) * a.c);
+          ss += to_f32(t[j]) * to_f32(t[j]);
+        }
+        qf[qb][ks] = t;
+      }
+      qn[qb] = sqrtf(wave_sum_xor32(ss));
+    }
+  }
+  // the key-norm bound over the whole key range, and the exact row max of the first key tile
+  const float* kn = knorm + ((long long)b * a.H + hh) * nkt;
+  float kmax = 0.f;
+  for (int t = lane; t < nkt; t += 64) kmax = fmaxf(kmax, kn[t]);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) kmax = fmaxf(kmax, __shfl_xor(kmax, o));
+  const bf16* kp = a.k + b * a.bs_k + hh * a.hs;
+  const bf16* vp = a.v + b * a.bs_v + hh * a.hs;
+  float m[2];
+  {
+    bf16x8 k0[2][4];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int key = 32 * kb + r32;
+        k0[kb][ks] = key < L ? *(const bf16x8*)(kp + (long long)key * a.rs_k + 16 * ks + 8 * h) : bf16x8{};
+      }
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      float mx = NEG_BIG;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        f32x16 sc = {};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) sc = mfma32(k0[kb][ks], qf[qb][ks], sc);
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (32 * kb + (i & 3) + 8 * (i >> 2) + 4 * h < L) mx = fmaxf(mx, sc[i]);
+      }
+      m[qb] = wave_max_xor32(mx);
+    }
+  }
+  __syncthreads();
+  if (!__all(qn[0] * kmax - m[0] <= SAFE_EXP2 && qn[1] * kmax - m[1] <= SAFE_EXP2) && lane == 0) unsafe_wg = 1;
+  __syncthreads();
+  const int unsafe = __builtin_amdgcn_readfirstlane(unsafe_wg);
+
+  if (unsafe) {
+    // exact online softmax, 32 keys at a time (operands straight from global memory: the rare path)
+    f32x16 o[2][2];
+    float mr[2] = {m[0], m[1]}, lr[2] = {0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) o[i][j] = f32x16{};
+    for (int k0 = 0; k0 < L; k0 += 32) {
+      bf16x8 kr[4], vt[2][2];
+      const int key = k0 + r32;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+        kr[ks] = key < L ? *(const bf16x8*)(kp + (long long)key * a.rs_k + 16 * ks + 8 * h) : bf16x8{};
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {   // V^T: lane (h, d) holds V[key k(8h + j)][d], k-order of the P packs
+            const int kk = k0 + 16 * s2 + (j & 3) + 8 * (j >> 2) + 4 * h;
+            vt[db][s2][j] = kk < L ? vp[(long long)kk * a.rs_v + 32 * db + r32] : to_bf16(0.f);
+          }
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        f32x16 sc = {};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) sc = mfma32(kr[ks], qf[qb][ks], sc);
+        float mx = NEG_BIG;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          if (k0 + (i & 3) + 8 * (i >> 2) + 4 * h >= L) sc[i] = NEG_BIG;
+          mx = fmaxf(mx, sc[i]);
+        }
+        const float mn = fmaxf(mr[qb], wave_max_xor32(mx));
+        const float alpha = exp2_fast(mr[qb] - mn);
+        mr[qb] = mn;
+        lr[qb] *= alpha;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { o[qb][0][i] *= alpha; o[qb][1][i] *= alpha; }
+        bf16x8 pk[2];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float p = exp2_fast(sc[i] - mn);
+          lr[qb] += p;
+          pk[i >> 3][i & 7] = to_bf16(p);
+        }
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) o[qb][db] = mfma32(vt[db][s2], pk[s2], o[qb][db]);
+      }
+    }
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const int q = qw0 + 32 * qb + r32;
+      const float lt = wave_sum_xor32(lr[qb]);
+      if (q < L) {
+        const float inv = 1.f / lt;
+        bf16* op = a.out + b * a.bs_out + (long long)q * a.rs_out + hh * a.hs;
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            bf16x4 w;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) w[j] = to_bf16(o[qb][db][4 * g + j] * inv);
+            *(bf16x4*)(op + 32 * db + 8 * g + 4 * h) = w;
+          }
+        if (h == 0) a.lse2[((long long)b * a.H + hh) * L + q] = mr[qb] + __log2f(lt);
+      }
+    }
+    return;
+  }
+
+  // ---- the placed stream
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) HS_TO_AGPR(qf[i][j]);
+  const rsrc_t rk = make_rsrc(kp, (uint32_t)(L - 1) * (uint32_t)(a.rs_k * 2) + DH * 2);
+  const rsrc_t rv = make_rsrc(vp, (uint32_t)(L - 1) * (uint32_t)(a.rs_v * 2) + DH * 2);
+  const int rs2k = a.rs_k * 2, rs2v = a.rs_v * 2;
+  const int prow = lane >> 3;
+  const int pch0 = (lane & 7) ^ ((prow >> 2) | ((prow >> 1) & 1) << 2);
+  const int pch1 = (lane & 7) ^ ((2 + (prow >> 2)) | ((prow >> 1) & 1) << 2);
+  const int dk0 = (16 * wave + prow) * rs2k + 16 * pch0, dk1 = (16 * wave + 8 + prow) * rs2k + 16 * pch1;
+  const int dv0 = (16 * wave + prow) * rs2v + 16 * pch0, dv1 = (16 * wave + 8 + prow) * rs2v + 16 * pch1;
+  const unsigned lds0 = (unsigned)(uintptr_t)(LCI_LDS char*)smem;
+  auto dma_op = [&](int t, int i) __attribute__((always_inline)) {   // operation i (0-3) of tile t
+    const unsigned sb = lds0 + (unsigned)((t & (NSLOT - 1)) * SLOT_B);
+    if (i == 0) hs_dma16(rk, dk0, t * KT * rs2k, sb + 2048 * wave);
+    if (i == 1) hs_dma16(rk, dk1, t * KT * rs2k, sb + 2048 * wave + 1024);
+    if (i == 2) hs_dma16(rv, dv0, t * KT * rs2v, sb + TILE_B + 2048 * wave);
+    if (i == 3) hs_dma16(rv, dv1, t * KT * rs2v, sb + TILE_B + 2048 * wave + 1024);
+  };
+  // LDS byte offsets of every distinct fragment read within a ring slot, computed once (the swizzle XOR per row
+  // included) and kept opaque: with the slot a compile-time constant (the 4-tile unroll below) each read is then one
+  // ds_read with a lane register and an immediate, no address VALU in the loop
+  unsigned row_off[2][4], tr_off[2][4][2];   // [rows 0-31 | 32-63][k-step | fragment][part]
+#pragma unroll
+  for (int r0i = 0; r0i < 2; ++r0i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      row_off[r0i][k] = 2 * sw128(32 * r0i + r32, 16 * k + 8 * h);
+      HS_OPAQUE(row_off[r0i][k]);
+#pragma unroll
+      for (int part = 0; part < 2; ++part) {   // fragment k = (d block k & 1, k-step k >> 1)
+        const int rw = 32 * r0i + 16 * (k >> 1) + 4 * h + ((lane & 15) >> 2) + 8 * part;
+        const int col = 32 * (k & 1) + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+        tr_off[r0i][k][part] = TILE_B + 2 * sw128(rw, col);
+        HS_OPAQUE(tr_off[r0i][k][part]);
+      }
+    }
+  auto row = [&](int soff, int r0i, int ks) __attribute__((always_inline)) {
+    return *(const bf16x8*)(smem + row_off[r0i][ks] + soff);
+  };
+  auto trh = [&](int soff, int r0i, int f, int part) __attribute__((always_inline)) {
+    return lds_tr4((const bf16*)(smem + tr_off[r0i][f][part] + soff));
+  };
+
+  f32x16 o[2][2];     // [query block][d block] O^T, lane = query, rows d = 32 db + (i & 3) + 8 (i >> 2) + 4h
+  f32x16 S[2];        // [query block] S~^T - m, then P (rows = the half's 32 keys)
+  f32x16 NM[2];       // -m splat: the chains' initial accumulator
+  u32x4 pp[2][2];     // [query block][k-step] bf16 P^T packs
+  bf16x4 vt[2][2][2][2];   // [set][d block][k-step][half of the fragment] transposed V (keys as the k index)
+  bf16x8 kr[4];       // K row fragments (A operands of the chains)
+  float lp[2][4];     // row-sum partials
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      NM[i][e] = -m[i];
+      S[i][e] = (i == 1 && fw_wrapped_exp(e)) ? NEG_BIG : 0.f;
+    }
+    HS_OPAQUE(NM[i]);
+    HS_OPAQUE(S[i]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      o[i][j] = f32x16{};
+      HS_TO_AGPR(o[i][j]);
+      pp[i][j] = u32x4{};
+      HS_OPAQUE(pp[i][j]);
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        vt[0][i][j][k] = vt[1][i][j][k] = bf16x4{};
+        HS_OPAQUE(vt[0][i][j][k]);
+        HS_OPAQUE(vt[1][i][j][k]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) lp[i][j] = 0.f;
+  }
+
+  auto valu_op = [&](unsigned char cd, int only_qb) __attribute__((always_inline)) {
+    if (cd == 0xFF) return;
+    const int kind = cd >> 6, qb = (cd >> 5) & 1, i = cd & 31;
+    if (only_qb >= 0 && qb != only_qb) return;
+    if (kind == 0) HS_EXP(S[qb][i]);
+    else if (kind == 1) asm volatile("v_add_f32 %0, %0, %1" : "+v"(lp[qb][i & 3]) : "v"(S[qb][i]));
+    else HS_CVT(pp[qb][i >> 2][i & 3], S[qb][2 * i], S[qb][2 * i + 1]);
+  };
+  auto pv_mfma = [&](int k, int qb, int st) __attribute__((always_inline)) {   // k: (d block k & 1, k-step k >> 1)
+    const int db = k & 1, s2 = k >> 1;
+    HS_MFMA_G(o[qb][db], cat44(vt[st][db][s2][0], vt[st][db][s2][1]), __builtin_bit_cast(bf16x8, pp[qb][s2]));
+  };
+  auto mfma_gap = [&](int g, int C, const f32x16& i0, const f32x16& i1) __attribute__((always_inline)) {
+    if (g < 4) {
+      if (g == 0) HS_MFMA_C0(S[0], kr[0], qf[0][0], i0); else HS_MFMA_C(S[0], kr[g], qf[0][g]);
+    } else if (g < 8) {
+      pv_mfma(g - 4, 1, C ^ 1);
+    } else if (g < 12) {
+      if (g == 8) HS_MFMA_C0(S[1], kr[0], qf[1][0], i1); else HS_MFMA_C(S[1], kr[g - 8], qf[1][g - 8]);
+    } else {
+      pv_mfma(g - 12, 0, C);
+    }
+  };
+  // one 32-key half (rows 32 r0i of the slot at byte offset soff, V^T set SET); gaps 12-15 read the next half's K rows
+  // (rows 32 nr0i of the slot at nsoff), 4 gaps before their use (two K-row sets read 5-8 gaps ahead measured slower:
+  // 13.74 vs 13.27 ms)
+  auto half = [&](auto SET, int soff, int r0i, int nsoff, int nr0i, const f32x16& i0, const f32x16& i1, auto hook)
+      __attribute__((always_inline)) {
+    constexpr int C = decltype(SET)::value;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      mfma_gap(g, C, i0, i1);
+      if (g == 2) HS_KEEP(i0);    // the chain-start MFMAs read their initial accumulators as SrcC after issue
+      if (g == 10) HS_KEEP(i1);
+#pragma unroll
+      for (int op = 0; op < 5; ++op) valu_op(FW_SCHED[g][op], -1);
+      if (LCI_FWD_PROBE == 1) {   // timing probe (wrong results): no LDS reads in the loop
+      } else if (g < 8) {
+        const int f = g >> 1, part = g & 1;   // fragment f = (d block f & 1, k-step f >> 1)
+        vt[C][f & 1][f >> 1][part] = trh(soff, r0i, f, part);
+      } else if (g >= 12) {
+        kr[g - 12] = row(nsoff, nr0i, g - 12);
+      }
+      hook(g);
+    }
+  };
+
+  // prologue: tiles 0, 1, 2 in flight; wait for tile 0; K rows of its first half
+  dma_op(0, 0); dma_op(0, 1); dma_op(0, 2); dma_op(0, 3);
+  if (nkt > 1) { dma_op(1, 0); dma_op(1, 1); dma_op(1, 2); dma_op(1, 3); }
+  if (nkt > 2) { dma_op(2, 0); dma_op(2, 1); dma_op(2, 2); dma_op(2, 3); }
+  if (nkt > 2) hs_vmcnt<8>(); else if (nkt > 1) hs_vmcnt<4>(); else hs_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) kr[ks] = row(0, 0, ks);
+  if (LCI_HS_LGKM0) __builtin_amdgcn_s_waitcnt(LGKM0_WAIT);
+
+  // SL >= 0: tile t sits in ring slot SL (compile-time: immediates); SL < 0: slot t & 3 at run time
+  auto tile = [&](auto SL, int t, const f32x16& a0, const f32x16& a1, const f32x16& b0, const f32x16& b1)
+      __attribute__((always_inline)) {
+    constexpr int sl = decltype(SL)::value;
+    const int soff = sl >= 0 ? sl * SLOT_B : (t & (NSLOT - 1)) * SLOT_B;
+    const int nsoff = sl >= 0 ? ((sl + 1) & (NSLOT - 1)) * SLOT_B : ((t + 1) & (NSLOT - 1)) * SLOT_B;
+    // tile t+1 is published at gap 6 of half 1 (first reader: the K rows at gaps 12-15); tile t+3's DMA goes into the
+    // slot of tile t-1 (last read by half 1 of tile t-1, before this barrier), one operation per two gaps
+    auto stage = [&](int g) __attribute__((always_inline)) {
+      if (t + 1 < nkt && g == 6) {
+        if (t + 2 < nkt) hs_vmcnt<4>(); else hs_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+      }
+      if (t + 3 < nkt && g >= 8 && !(g & 1)) dma_op(t + 3, (g - 8) >> 1);
+    };
+    auto none = [](int) __attribute__((always_inline)) {};
+    half(std::integral_constant<int, 0>{}, soff, 0, soff, 1, a0, a1, none);
+    half(std::integral_constant<int, 1>{}, soff, 1, nsoff, 0, b0, b1, stage);
+  };
+  const bool ragged = (L & (KT - 1)) != 0;
+  const int nfast = ragged ? nkt - 1 : nkt;
+  using IC0 = std::integral_constant<int, 0>;
+  using IC1 = std::integral_constant<int, 1>;
+  using IC2 = std::integral_constant<int, 2>;
+  using IC3 = std::integral_constant<int, 3>;
+  using ICR = std::integral_constant<int, -1>;
+  int t = 0;
+  for (; t + 4 <= nfast; t += 4) {   // t & 3 == 0 here
+    tile(IC0{}, t, NM[0], NM[1], NM[0], NM[1]);
+    tile(IC1{}, t + 1, NM[0], NM[1], NM[0], NM[1]);
+    tile(IC2{}, t + 2, NM[0], NM[1], NM[0], NM[1]);
+    tile(IC3{}, t + 3, NM[0], NM[1], NM[0], NM[1]);
+  }
+  for (; t < nfast; ++t) tile(ICR{}, t, NM[0], NM[1], NM[0], NM[1]);
+  if (ragged) {   // the last tile: keys past L start from NEG_BIG (their K rows read as zero), so exp2 gives 0
+    const int tl = nkt - 1;
+    f32x16 M[2][2];
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+          M[hf][qb][e] = tl * KT + 32 * hf + (e & 3) + 8 * (e >> 2) + 4 * h < L ? -m[qb] : NEG_BIG;
+        HS_OPAQUE(M[hf][qb]);
+      }
+    asm volatile("s_nop 4" ::: "memory");
+    tile(ICR{}, tl, M[0][0], M[0][1], M[1][0], M[1][1]);
+  }
+  // query block 1 of the last half: its wrapped VALU (gaps 0-5) and its PV MFMAs
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+#pragma unroll
+    for (int op = 0; op < 5; ++op) valu_op(FW_SCHED[g][op], 1);
+    if (g >= 4) {
+      asm volatile("s_nop 1" ::: "memory");
+      pv_mfma(g - 4, 1, 1);   // the last half is a half 1
+    }
+  }
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int q = qw0 + 32 * qb + r32;
+    const float lt = wave_sum_xor32((lp[qb][0] + lp[qb][1]) + (lp[qb][2] + lp[qb][3]));
+    if (q < L) {
+      const float inv = 1.f / lt;
+      bf16* op = a.out + b * a.bs_out + (long long)q * a.rs_out + hh * a.hs;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          bf16x4 w;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) w[j] = to_bf16(o[qb][db][4 * g + j] * inv);
+          *(bf16x4*)(op + 32 * db + 8 * g + 4 * h) = w;
+        }
+      if (h == 0) a.lse2[((long long)b * a.H + hh) * L + q] = m[qb] + __log2f(lt);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------- backward: dQ kernel, v2
 // Work split of attn_bwd_dq_kernel (8 waves x 32 queries on the lane, key tiles of 64), restructured like the
 // v2 forward: buffer-load staging into a 3-slot LDS ring (K tile swizzled: read by rows for S^T and transposed
@@ -2281,7 +2714,10 @@ extern "C" int lci_attn_fwd(const void* qkv, void* out, float* lse2, float* knor
 #ifndef LCI_FWD16
 #define LCI_FWD16 0    // 16x16x32 forward: parity-green, 12.97 vs 12.37 ms (slower: the VALU-bound body loses issue
 #endif                 // slots, a 16x16x32 MFMA holds vector issue for 8 of its 16 cycles), not adopted
-  if (LCI_FWD16)
+  if (LCI_FWD_HS)
+    hipLaunchKernelGGL(attn_fwd_hs_kernel, dim3((L + HS_NW * 64 - 1) / (HS_NW * 64), H, B), dim3(HS_NW * 64), 0, s, a,
+                       (const float*)knorm_ws);
+  else if (LCI_FWD16)
     hipLaunchKernelGGL(attn_fwd16_kernel, grid, dim3(FW_NW * 64), 0, s, a, (const float*)knorm_ws);
   else
     hipLaunchKernelGGL(attn_fwd2_kernel, grid, dim3(FW_NW * 64), 0, s, a, (const float*)knorm_ws);

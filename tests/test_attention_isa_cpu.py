@@ -15,7 +15,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "long_context_biomedical_imaging_amd", "csrc", "attention.hip")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-KERNELS = ("attn_bwd_dkdv_hs_kernel", "attn_bwd_dq_hs_kernel")
+KERNELS = ("attn_bwd_dkdv_hs_kernel", "attn_bwd_dq_hs_kernel", "attn_fwd_hs_kernel")
 
 
 @pytest.fixture(scope="module")
@@ -43,11 +43,9 @@ def _loops(body):
     out = []
     for m in re.finditer(r"^(\.LBB\d+_\d+):.*Loop Header", body, re.M):
         lab = m.group(1)
-        end = body.find("s_cbranch_scc0 " + lab, m.end())
-        end2 = body.find("s_branch " + lab, m.end())
-        ends = [e for e in (end, end2) if e >= 0]
+        ends = [b.start() for b in re.finditer(r"s_c?branch\w*\s+" + re.escape(lab) + r"\b", body[m.end():])]
         assert ends, f"no back edge for {lab}"
-        out.append(body[m.end():max(ends)])
+        out.append(body[m.end():m.end() + max(ends)])
     return out
 
 
