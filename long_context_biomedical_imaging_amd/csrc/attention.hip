@@ -1588,13 +1588,28 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
     if (i == 3) hs_dma16(rv, dv1, t * KT * rs2v, sb + TILE_B + 2048 * wave + 1024);
   };
 
-  auto row = [&](const char* tile, int r0, int ks) __attribute__((always_inline)) {
-    return *(const bf16x8*)(tile + 2 * sw128(r0 + r32, 16 * ks + 8 * h));
+  // LDS byte offsets of every distinct fragment read within a ring slot, computed once and kept opaque (see the
+  // forward kernel): with a compile-time ring slot every read is a lane register + an immediate
+  unsigned row_off[2][4], tr_off[2][4][2];   // [rows 0-31 | 32-63][k-step | fragment][part]
+#pragma unroll
+  for (int r0i = 0; r0i < 2; ++r0i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      row_off[r0i][k] = 2 * sw128(32 * r0i + r32, 16 * k + 8 * h);
+      HS_OPAQUE(row_off[r0i][k]);
+#pragma unroll
+      for (int part = 0; part < 2; ++part) {   // fragment k = (d block k & 1, k-step k >> 1)
+        const int rw = 32 * r0i + 16 * (k >> 1) + 4 * h + ((lane & 15) >> 2) + 8 * part;
+        const int col = 32 * (k & 1) + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+        tr_off[r0i][k][part] = 2 * sw128(rw, col);
+        HS_OPAQUE(tr_off[r0i][k][part]);
+      }
+    }
+  auto row = [&](int soff, int r0i, int ks) __attribute__((always_inline)) {   // soff: slot (+ TILE_B for V) bytes
+    return *(const bf16x8*)(smem + row_off[r0i][ks] + soff);
   };
-  auto trh = [&](const char* tile, int r0, int S, int c0, int part) __attribute__((always_inline)) {
-    const int rw = r0 + 16 * S + 4 * h + ((lane & 15) >> 2) + 8 * part;
-    const int col = c0 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-    return lds_tr4((const bf16*)(tile + 2 * sw128(rw, col)));
+  auto trh = [&](int soff, int r0i, int f, int part) __attribute__((always_inline)) {
+    return lds_tr4((const bf16*)(smem + tr_off[r0i][f][part] + soff));
   };
 
   f32x16 dq[2][2];             // [d block][query block]: dQ^T, lane = query, rows d = 32db + (i&3) + 8(i>>2) + 4h
@@ -1656,8 +1671,7 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
   // LCI_DQ_V2 reads: this half's transposed K at gaps 0-7 (used at 20-23), the next half's K rows at 16-19 (after
   // their last use by the chains at 12-15; used at its gaps 0-3 and 12-15) and V rows at 20-23 (after 16-19; used
   // at its 4-7, 16-19): every read >= 8 gaps ahead. Else: V rows at 0-3, transposed K at 12-19, K rows at 20-23.
-  auto half = [&](auto SET, const char* slot, int r0, const char* nslot, int nr0, auto hook)
-      __attribute__((always_inline)) {
+  auto half = [&](auto SET, int soff, int r0i, int nsoff, int nr0i, auto hook) __attribute__((always_inline)) {
     constexpr int C = LCI_DQ_V2 ? decltype(SET)::value : 0;
 #pragma unroll
     for (int g = 0; g < 24; ++g) {
@@ -1670,14 +1684,14 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
       if (LCI_DQ_V2) {
         if (g < 8) {
           const int f = g >> 1, part = g & 1;   // fragment f = (d block f & 1, k-step f >> 1)
-          ktr[C][f & 1][f >> 1][part] = trh(slot, r0, f >> 1, 32 * (f & 1), part);
-        } else if (g >= 16 && g < 20) kr[g - 16] = row(nslot, nr0, g - 16);
-        else if (g >= 20) vr[g - 20] = row(nslot + TILE_B, nr0, g - 20);
-      } else if (g < 4) vr[g] = row(slot + TILE_B, r0, g);
+          ktr[C][f & 1][f >> 1][part] = trh(soff, r0i, f, part);
+        } else if (g >= 16 && g < 20) kr[g - 16] = row(nsoff, nr0i, g - 16);
+        else if (g >= 20) vr[g - 20] = row(nsoff + TILE_B, nr0i, g - 20);
+      } else if (g < 4) vr[g] = row(soff + TILE_B, r0i, g);
       else if (g >= 12 && g < 20) {
         const int f = (g - 12) >> 1, part = (g - 12) & 1;
-        ktr[0][f & 1][f >> 1][part] = trh(slot, r0, f >> 1, 32 * (f & 1), part);
-      } else if (g >= 20) kr[g - 20] = row(nslot, nr0, g - 20);
+        ktr[0][f & 1][f >> 1][part] = trh(soff, r0i, f, part);
+      } else if (g >= 20) kr[g - 20] = row(nsoff, nr0i, g - 20);
       hook(g);
     }
   };
@@ -1694,14 +1708,16 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
   __builtin_amdgcn_s_barrier();
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
-    kr[ks] = row(smem, 0, ks);
-    if (LCI_DQ_V2) vr[ks] = row(smem + TILE_B, 0, ks);
+    kr[ks] = row(0, 0, ks);
+    if (LCI_DQ_V2) vr[ks] = row(TILE_B, 0, ks);
   }
   if (LCI_HS_LGKM0) __builtin_amdgcn_s_waitcnt(LGKM0_WAIT);   // (see the dK/dV kernel's loop header)
 
-  for (int t = 0; t < nkt; ++t) {
-    char* slot = smem + (t & (NSLOT - 1)) * SLOT_B;
-    char* nslot = smem + ((t + 1) & (NSLOT - 1)) * SLOT_B;
+  // SL >= 0: tile t sits in ring slot SL (compile-time: DS immediates); SL < 0: slot t & 3 at run time
+  auto tile = [&](auto SL, int t) __attribute__((always_inline)) {
+    constexpr int sl = decltype(SL)::value;
+    const int soff = sl >= 0 ? sl * SLOT_B : (t & (NSLOT - 1)) * SLOT_B;
+    const int nsoff = sl >= 0 ? ((sl + 1) & (NSLOT - 1)) * SLOT_B : ((t + 1) & (NSLOT - 1)) * SLOT_B;
     // tile t+1 is published at gap 6 of half 1 (its first reader: the K rows at gaps 16-19, V2, or 20-23); tile t+3's DMA goes
     // into the slot of tile t-1 (last read by half 1 of tile t-1, before this barrier), one operation per gap
     auto stage = [&](int g) __attribute__((always_inline)) {
@@ -1724,8 +1740,18 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
     auto stage0 = [&](int g) __attribute__((always_inline)) {
       if (LCI_DQ_DMASPREAD && t + 2 < nkt && (g == 6 || g == 18)) dma_op(t + 2, g == 6 ? 2 : 3);
     };
-    half(std::integral_constant<int, 0>{}, slot, 0, slot, 32, stage0);
-    half(std::integral_constant<int, 1>{}, slot, 32, nslot, 0, stage);
+    half(std::integral_constant<int, 0>{}, soff, 0, soff, 1, stage0);
+    half(std::integral_constant<int, 1>{}, soff, 1, nsoff, 0, stage);
+  };
+  {
+    int t = 0;
+    for (; t + 4 <= nkt; t += 4) {   // t & 3 == 0 here
+      tile(std::integral_constant<int, 0>{}, t);
+      tile(std::integral_constant<int, 1>{}, t + 1);
+      tile(std::integral_constant<int, 2>{}, t + 2);
+      tile(std::integral_constant<int, 3>{}, t + 3);
+    }
+    for (; t < nkt; ++t) tile(std::integral_constant<int, -1>{}, t);
   }
   // query block 1 of the last half: its remaining VALU (wrapped into gaps 0-5) and its dQ^T
 #pragma unroll
