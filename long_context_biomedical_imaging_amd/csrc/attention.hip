@@ -902,6 +902,9 @@ constexpr int HS_NW = 4;
 #define LCI_HS_STAMP 0   // diagnostic build: s_memtime at every segment start of tiles 64-95 of workgroups 0-7 (dK/dV),
                          // written to the dQ part of dqkv, which only the (not launched) dQ stage writes
 #endif
+#ifndef LCI_HS_UNROLL
+#define LCI_HS_UNROLL 1   // dK/dV: 4-tile unroll with compile-time ring slots (0: one runtime-slot loop, for A/B)
+#endif
 #ifndef LCI_HS_V
 #define LCI_HS_V 2   // 1: first placement (conversions in pairs, single fragment set, LDS reads in segs B-D), for A/B
 #endif
@@ -1101,17 +1104,33 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
     if (wave < 2) *(uint32_t*)(rcs + wave * KT * 4 + lane * 4) = g.rc;   // (register staging: ring slot 0 only)
   };
 
-  // ---- fragment readers (byte offsets; r0 = the half's first query row in the tile)
-  auto qrow = [&](const char* tile, int r0, int ks) __attribute__((always_inline)) {
-    return *(const bf16x8*)(tile + 2 * sw128(r0 + r32, 16 * ks + 8 * h));
+  // ---- fragment readers. sw128's swizzle depends on row bits 1-3 only, so a row offset that is a multiple of 16
+  // (r0, 16 S) is a plain byte offset: the lane part of every read address is one of 9 registers computed here and
+  // kept opaque, and slot (compile-time in the unrolled loop), dO, row and row-constant offsets are DS immediates
+  unsigned q_off[4], t_off[2][2], rc_off;   // [k-step] | [d block][part] | row constants: + 16 h
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    q_off[ks] = 2 * sw128(r32, 16 * ks + 8 * h);
+    HS_OPAQUE(q_off[ks]);
+  }
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int part = 0; part < 2; ++part) {
+      t_off[db][part] = 2 * sw128(4 * h + ((lane & 15) >> 2) + 8 * part, 32 * db + 16 * ((lane >> 4) & 1) + 4 * (lane & 3));
+      HS_OPAQUE(t_off[db][part]);
+    }
+  rc_off = NSLOT * SLOT_B + 16 * h;   // (past the 64-KB ring: in the register, the rest is an immediate)
+  HS_OPAQUE(rc_off);
+  // soff: byte offset of the tile in the ring (slot, + TILE_B for dO); r0: the half's first query row in the tile
+  auto qrow = [&](int soff, int r0, int ks) __attribute__((always_inline)) {
+    return *(const bf16x8*)(smem + q_off[ks] + (soff + 2 * DH * r0));
   };
-  auto trf = [&](const char* tile, int r0, int S, int c0) __attribute__((always_inline)) {
-    const int row = r0 + 16 * S + 4 * h + ((lane & 15) >> 2);
-    const int col = c0 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+  auto trf = [&](int soff, int r0, int S, int db) __attribute__((always_inline)) {
+    const int imm = soff + 2 * DH * (r0 + 16 * S);
     if (LCI_HS_PROBE == 8)   // probe: plain b64 reads of the same addresses (wrong operands)
-      return cat44(*(const bf16x4*)(tile + 2 * sw128(row, col)), *(const bf16x4*)(tile + 2 * sw128(row + 8, col)));
-    return cat44(lds_tr4((const bf16*)(tile + 2 * sw128(row, col))),
-                 lds_tr4((const bf16*)(tile + 2 * sw128(row + 8, col))));
+      return cat44(*(const bf16x4*)(smem + t_off[db][0] + imm), *(const bf16x4*)(smem + t_off[db][1] + imm));
+    return cat44(lds_tr4((const bf16*)(smem + t_off[db][0] + imm)), lds_tr4((const bf16*)(smem + t_off[db][1] + imm)));
   };
   // initial accumulator of a chain: register i <-> query r0 + (i & 3) + 8 (i >> 2) + 4h
   auto rcblk = [&](const char* rcslot, int which, int r0) __attribute__((always_inline)) {
@@ -1201,22 +1220,23 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
   };
   // transposed fragment f (gradient order: k-step f >> 2, d block (f >> 1) & 1, dO^T | Q^T) of rows r0 into set st
   bool probe_noread = false;
-  auto tr_load = [&](int f, int st, const char* slot, int r0) __attribute__((always_inline)) {
+  auto tr_load = [&](int f, int st, int soff, int r0) __attribute__((always_inline)) {
     if ((LCI_HS_PROBE == 3 && probe_noread) || LCI_HS_PROBE == 5) return;
     const int s2 = f >> 2, db = (f >> 1) & 1;
     if (LCI_HS_TQ) {   // d-major tile: lane (h, r32) reads d = 32 db + r32, queries r0 + 16 s2 + 8h .. +7 (pack order)
-      const char* tt = slot + (f & 1 ? 2 : 3) * TILE_B;
+      const char* tt = smem + soff + (f & 1 ? 2 : 3) * TILE_B;
       const bf16x8 v = *(const bf16x8*)(tt + 2 * sw128(32 * db + r32, r0 + 16 * s2 + 8 * h));
       if (f & 1) tq[st][db][s2] = v; else tdo[st][db][s2] = v;
       return;
     }
-    if (f & 1) tq[st][db][s2] = s2 ? trf(slot, r0, 1, 32 * db) : trf(slot, r0, 0, 32 * db);
-    else tdo[st][db][s2] = s2 ? trf(slot + TILE_B, r0, 1, 32 * db) : trf(slot + TILE_B, r0, 0, 32 * db);
+    if (f & 1) tq[st][db][s2] = trf(soff, r0, s2, db);
+    else tdo[st][db][s2] = trf(soff + TILE_B, r0, s2, db);
   };
-  // one f32x4 piece (queries 8g + 4h .. + 3 of the half) of a chain's row-constant block
-  auto rc_load = [&](f32x16& r, const char* rcslot, int which, int r0, int g) __attribute__((always_inline)) {
+  // one f32x4 piece (queries 8g + 4h .. + 3 of the half) of a chain's row-constant block; rcoff: the tile's
+  // row-constant slot, bytes from the end of the ring
+  auto rc_load = [&](f32x16& r, int rcoff, int which, int r0, int g) __attribute__((always_inline)) {
     if ((LCI_HS_PROBE == 3 && probe_noread) || LCI_HS_PROBE == 6) return;
-    const f32x4 v = *(const f32x4*)((const float*)(rcslot + which * KT * 4) + r0 + 4 * h + 8 * g);
+    const f32x4 v = *(const f32x4*)(smem + rc_off + (rcoff + which * KT * 4 + 4 * (r0 + 8 * g)));
     r[4 * g] = v[0]; r[4 * g + 1] = v[1]; r[4 * g + 2] = v[2]; r[4 * g + 3] = v[3];
   };
 
@@ -1226,7 +1246,7 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
   //   seg A, B: this half's transposed fragments into set C (set C^1 is still read by seg B's kb1 products)
   //   seg C: Q rows of half p+1 (gaps 2-5), -lse2 pieces 0-1 and dO rows 0-1 (gaps 6-7)
   //   seg D: -lse2 pieces 2-3, -delta pieces 0-3, dO rows 2-3
-  auto half = [&](auto CUR, const char* slot, int r0, const char* nslot, const char* nrc, int nr0, auto mid, auto sgap)
+  auto half = [&](auto CUR, int slot, int r0, int nslot, int nrc, int nr0, auto mid, auto sgap)
       __attribute__((always_inline)) {
     constexpr int C = decltype(CUR)::value;
     // seg A: chains kb0 || VALU kb1 (p-1) elements 8-15 (finishing its elements 0-7)
@@ -1276,8 +1296,7 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
     }
   };
 
-  auto half_v1 = [&](auto CUR, const char* slot, int r0, const char* nslot, const char* nrc, int nr0, auto mid,
-                     auto sgap)
+  auto half_v1 = [&](auto CUR, int slot, int r0, int nslot, int nrc, int nr0, auto mid, auto sgap)
       __attribute__((always_inline)) {
     constexpr int C = 0;   // one fragment set, each fragment reloaded two gaps after its last read
 #pragma unroll
@@ -1304,8 +1323,8 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
     for (int g = 0; g < 8; ++g) {
       grad_gap(g, 0, C);
       valu_gap(g, 1, 0, 0, 1);
-      if (g == 0) NL = rcblk(nrc, 0, nr0);
-      if (g == 1) ND = rcblk(nrc, 1, nr0);
+      if (g == 0) NL = rcblk(rcs + nrc, 0, nr0);
+      if (g == 1) ND = rcblk(rcs + nrc, 1, nr0);
       if (g >= 4) da[g - 4] = qrow(nslot + TILE_B, nr0, g - 4);
     }
   };
@@ -1336,34 +1355,33 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
   ND = rcblk(rcs, 1, 0);
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
-    qa[ks] = qrow(smem, 0, ks);
-    da[ks] = qrow(smem + TILE_B, 0, ks);
+    qa[ks] = qrow(0, 0, ks);
+    da[ks] = qrow(TILE_B, 0, ks);
   }
   if (LCI_HS_PROBE == 3) {   // probe: real data in every fragment, then no LDS reads in the loop
 #pragma unroll
-    for (int f = 0; f < 8; ++f) { tr_load(f, 0, smem, 0); tr_load(f, 1, smem, 32); }
+    for (int f = 0; f < 8; ++f) { tr_load(f, 0, 0, 0); tr_load(f, 1, 0, 32); }
     probe_noread = true;
   }
   // the prologue's reads complete here (a waitcnt the compiler's pass sees): otherwise its wait for them, merged
   // into the loop header with the back edge's, makes every tile start with lgkmcnt(1)
   if (LCI_HS_LGKM0) __builtin_amdgcn_s_waitcnt(LGKM0_WAIT);
-  // one tile in ring slot t & 3 (a 4-tile unroll that made the slots compile-time spilled 32 VGPRs);
-  // register staging: tile t+1 is in set PAR ^ 1, which then takes tile t+3
-  auto tile = [&](auto PAR, int t) __attribute__((always_inline)) {
+  // one tile in ring slot SL (compile-time in the 4-tile unroll: every fragment read is a DS immediate off one of
+  // the lane registers above) or, SL < 0, t & 3 at run time; register staging: tile t+1 is in set PAR ^ 1, which
+  // then takes tile t+3
+  auto tile = [&](auto PAR, auto SL, int t) __attribute__((always_inline)) {
     constexpr int P1 = decltype(PAR)::value ^ 1;
-    const int sl = t & (NSLOT - 1), nsl = (t + 1) & (NSLOT - 1);
+    constexpr int SLC = decltype(SL)::value;
+    const int sl = SLC >= 0 ? SLC : t & (NSLOT - 1), nsl = SLC >= 0 ? (SLC + 1) & (NSLOT - 1) : (t + 1) & (NSLOT - 1);
     stamp_tile = (LCI_HS_STAMP && blockIdx.x < 8 && blockIdx.y == 0 && blockIdx.z == 0 && t >= 64 && t < 96) ? t - 64 : -1;
-    char* slot = smem + sl * SLOT_B;
-    char* nslot = smem + nsl * SLOT_B;
-    char* rc = rcs + sl * RC_B;
-    char* nrc = rcs + nsl * RC_B;
+    const int slot = sl * SLOT_B, nslot = nsl * SLOT_B, rc = sl * RC_B, nrc = nsl * RC_B;
     // tile t+1 is published after seg A of half 1 (seg C of half 1 is its first reader): each wave waits for its
     // own copy of tile t+1 (tile t+2's may stay in flight), then one barrier; tile t+3 goes into the slot of tile
     // t-1, which every wave finished before this barrier
     auto stage = [&]() __attribute__((always_inline)) {
       if (t + 1 < nqt) {
         if (t + 2 < nqt) hs_vmcnt<NOPS>(); else hs_vmcnt<0>();
-        if constexpr (LCI_HS_STG == 1) store_tile(stg[P1], nslot);
+        if constexpr (LCI_HS_STG == 1) store_tile(stg[P1], smem + nslot);
         stamp(8);
         // no LDS fence: this wave's reads of the slot tile t+3 overwrites were consumed before now, and the new
         // tile's bytes are ordered by the vmcnt above (register staging stores to LDS: that one needs the fence)
@@ -1402,12 +1420,21 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
       half(std::integral_constant<int, 1>{}, slot, 32, nslot, nrc, 0, stage, dmas1);
     }
   };
+  using IZ = std::integral_constant<int, 0>;
   if constexpr (LCI_HS_STG == 0) {
-    for (int t = 0; t < nqt; ++t) tile(std::integral_constant<int, 0>{}, t);
+    int t = 0;
+    if (LCI_HS_UNROLL)
+      for (; t + 4 <= nqt; t += 4) {   // t & 3 == 0 here
+        tile(IZ{}, IZ{}, t);
+        tile(IZ{}, std::integral_constant<int, 1>{}, t + 1);
+        tile(IZ{}, std::integral_constant<int, 2>{}, t + 2);
+        tile(IZ{}, std::integral_constant<int, 3>{}, t + 3);
+      }
+    for (; t < nqt; ++t) tile(IZ{}, std::integral_constant<int, -1>{}, t);
   } else {
     for (int t = 0; t < nqt; t += 2) {
-      tile(std::integral_constant<int, 0>{}, t);
-      if (t + 1 < nqt) tile(std::integral_constant<int, 1>{}, t + 1);
+      tile(IZ{}, std::integral_constant<int, -1>{}, t);
+      if (t + 1 < nqt) tile(std::integral_constant<int, 1>{}, std::integral_constant<int, -1>{}, t + 1);
     }
   }
   // key block 1 of the last half: elements 8-15 (finishing 0-7), then its dV / dK
