@@ -1177,30 +1177,39 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
   // (pkb, pe): its last two multiplies and three conversions
   auto valu_gap = [&](int g, int kb, int e, int pkb, int pe) __attribute__((always_inline)) {
     if (LCI_HS_PROBE == 4) return;
+#if LCI_HS_PROBE >= 9 && LCI_HS_PROBE <= 11   // probes: 9 no exps, 10 no multiplies, 11 no conversions
+#define HS_P9(x) if (LCI_HS_PROBE != 9) x
+#define HS_P10(x) if (LCI_HS_PROBE != 10) x
+#define HS_P11(x) if (LCI_HS_PROBE != 11) x
+#else
+#define HS_P9(x) x
+#define HS_P10(x) x
+#define HS_P11(x) x
+#endif
     f32x16& s = S[kb];
     f32x16& p = P[kb];
     const int o = 8 * e, po = 8 * pe;
-    HS_EXP(s[o + g]);
-    if (g >= 2) HS_MUL(p[o + g - 2], s[o + g - 2]);
-    if (g == 0) HS_MUL(P[pkb][po + 6], S[pkb][po + 6]);
-    if (g == 1) HS_MUL(P[pkb][po + 7], S[pkb][po + 7]);
+    HS_P9(HS_EXP(s[o + g]));
+    if (g >= 2) HS_P10(HS_MUL(p[o + g - 2], s[o + g - 2]));
+    if (g == 0) HS_P10(HS_MUL(P[pkb][po + 6], S[pkb][po + 6]));
+    if (g == 1) HS_P10(HS_MUL(P[pkb][po + 7], S[pkb][po + 7]));
     if (LCI_HS_V == 1) {
-      if (g == 0) HS_CVT(pk[pkb][pe][3], S[pkb][po + 6], S[pkb][po + 7]);
-      if (g == 0) HS_CVT(dd[pkb][pe][2], P[pkb][po + 4], P[pkb][po + 5]);
-      if (g == 2) HS_CVT(dd[pkb][pe][3], P[pkb][po + 6], P[pkb][po + 7]);
-      if (g == 2 || g == 4 || g == 6) HS_CVT(pk[kb][e][g / 2 - 1], s[o + g - 2], s[o + g - 1]);
-      if (g == 4 || g == 6) HS_CVT(dd[kb][e][g / 2 - 2], p[o + g - 4], p[o + g - 3]);
+      if (g == 0) HS_P11(HS_CVT(pk[pkb][pe][3], S[pkb][po + 6], S[pkb][po + 7]));
+      if (g == 0) HS_P11(HS_CVT(dd[pkb][pe][2], P[pkb][po + 4], P[pkb][po + 5]));
+      if (g == 2) HS_P11(HS_CVT(dd[pkb][pe][3], P[pkb][po + 6], P[pkb][po + 7]));
+      if (g == 2 || g == 4 || g == 6) HS_P11(HS_CVT(pk[kb][e][g / 2 - 1], s[o + g - 2], s[o + g - 1]));
+      if (g == 4 || g == 6) HS_P11(HS_CVT(dd[kb][e][g / 2 - 2], p[o + g - 4], p[o + g - 3]));
       return;
     }
     switch (g) {
-      case 0: HS_CVT(pk[pkb][pe][3], S[pkb][po + 6], S[pkb][po + 7]); break;
-      case 1: HS_CVT(dd[pkb][pe][2], P[pkb][po + 4], P[pkb][po + 5]); break;
-      case 2: HS_CVT(dd[pkb][pe][3], P[pkb][po + 6], P[pkb][po + 7]); break;
-      case 3: HS_CVT(pk[kb][e][0], s[o], s[o + 1]); break;
-      case 4: HS_CVT(pk[kb][e][1], s[o + 2], s[o + 3]); break;
-      case 5: HS_CVT(dd[kb][e][0], p[o], p[o + 1]); break;
-      case 6: HS_CVT(pk[kb][e][2], s[o + 4], s[o + 5]); break;
-      default: HS_CVT(dd[kb][e][1], p[o + 2], p[o + 3]); break;
+      case 0: HS_P11(HS_CVT(pk[pkb][pe][3], S[pkb][po + 6], S[pkb][po + 7])); break;
+      case 1: HS_P11(HS_CVT(dd[pkb][pe][2], P[pkb][po + 4], P[pkb][po + 5])); break;
+      case 2: HS_P11(HS_CVT(dd[pkb][pe][3], P[pkb][po + 6], P[pkb][po + 7])); break;
+      case 3: HS_P11(HS_CVT(pk[kb][e][0], s[o], s[o + 1])); break;
+      case 4: HS_P11(HS_CVT(pk[kb][e][1], s[o + 2], s[o + 3])); break;
+      case 5: HS_P11(HS_CVT(dd[kb][e][0], p[o], p[o + 1])); break;
+      case 6: HS_P11(HS_CVT(pk[kb][e][2], s[o + 4], s[o + 5])); break;
+      default: HS_P11(HS_CVT(dd[kb][e][1], p[o + 2], p[o + 3])); break;
     }
   };
   // MFMA of gap g of a chain segment (S chain at gaps 0-3, dP chain at gaps 4-7) for key block kb
@@ -1861,7 +1870,8 @@ constexpr unsigned char FW_SCHED[16][5] = {
 #define LCI_FWD_HS 1
 #endif
 #ifndef LCI_FWD_PROBE
-#define LCI_FWD_PROBE 0   // timing probes (wrong results): 1 = no LDS reads in the loop, 2 = the reads without waits
+#define LCI_FWD_PROBE 0   // timing probes (wrong results): 1 = no LDS reads in the loop, 2 = the reads without waits,
+                          // 3 / 4 / 5 = no exps / row-sum adds / conversions, 6 = no LDS-DMA in the loop
 #endif
 
 // initial S^T of query block 1 before the first half: the exps of block 1 that FW_SCHED wraps into the next half
@@ -2109,6 +2119,7 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
     if (cd == 0xFF) return;
     const int kind = cd >> 6, qb = (cd >> 5) & 1, i = cd & 31;
     if (only_qb >= 0 && qb != only_qb) return;
+    if (LCI_FWD_PROBE >= 3 && LCI_FWD_PROBE <= 5 && kind == LCI_FWD_PROBE - 3) return;
     if (kind == 0) HS_EXP(S[qb][i]);
     else if (kind == 1) asm volatile("v_add_f32 %0, %0, %1" : "+v"(lp[qb][i & 3]) : "v"(S[qb][i]));
     else HS_CVT(pp[qb][i >> 2][i & 3], S[qb][2 * i], S[qb][2 * i + 1]);
@@ -2175,7 +2186,7 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
         if (t + 2 < nkt) hs_vmcnt<4>(); else hs_vmcnt<0>();
         __builtin_amdgcn_s_barrier();
       }
-      if (t + 3 < nkt && g >= 8 && !(g & 1)) dma_op(t + 3, (g - 8) >> 1);
+      if (LCI_FWD_PROBE != 6 && t + 3 < nkt && g >= 8 && !(g & 1)) dma_op(t + 3, (g - 8) >> 1);
     };
     auto none = [](int) __attribute__((always_inline)) {};
     half(std::integral_constant<int, 0>{}, soff, 0, soff, 1, a0, a1, none);
