@@ -277,6 +277,31 @@ def test_gelu_kernel_exhaustive_bf16():
     assert (xc.grad != xr.grad).float().mean().item() < 5e-3
 
 
+def test_gelu_epilogue_exhaustive_bf16():
+    """Every finite bf16 value (|x| < 1e4) through the GEMM epilogues (csrc/linear.hip erf_epi): rows of 32 values
+    times 4 stacked 32 x 32 identities (N = 128), so pre = x exactly; LF_GELU's activation and LF_DGELU's GELU' (unit
+    upstream gradient) within one bf16 ulp of torch's gelu / gelu_backward and bitwise equal for > 99.5 %."""
+    from long_context_biomedical_imaging_amd import kernels
+    bits = torch.arange(0, 65536, dtype=torch.int32).to(torch.int16)
+    v = bits.view(torch.bfloat16).cuda()
+    v = v[torch.isfinite(v.float()) & (v.float().abs() < 1e4)]
+    v = v[: v.numel() // 32 * 32].contiguous()
+    x = v.view(-1, 32)
+    w = torch.eye(32, device="cuda").repeat(4, 1).to(torch.bfloat16).contiguous()
+    act, pre = kernels.linear_fwd(x, w, None, kernels.LF_GELU)
+    assert torch.equal(pre, x.repeat(1, 4))
+    ref = torch.nn.functional.gelu(pre)
+    d = (act.float() - ref.float()).abs()
+    assert bool((d <= ref.float().abs() * 2.0 ** -7 + 1e-37).all())
+    assert (act != ref).float().mean().item() < 5e-3
+    ones = torch.ones_like(x)
+    g = kernels.linear_fwd(ones, w, None, kernels.LF_DGELU, aux=pre)
+    gref = torch.ops.aten.gelu_backward(torch.ones_like(pre), pre)
+    d = (g.float() - gref.float()).abs()
+    assert bool((d <= gref.float().abs() * 2.0 ** -7 + 1e-37).all())
+    assert (g != gref).float().mean().item() < 5e-3
+
+
 @pytest.mark.parametrize("nd,Cin,Cout,Cs,k", [(3, 64, 32, 32, (2, 2, 2)), (2, 48, 16, 24, (2, 2)), (3, 16, 8, 0, (2, 2, 2))])
 def test_conv_up_interleave_and_cat_bit_exact(nd, Cin, Cout, Cs, k, monkeypatch):
     """lci_convup_interleave (the up-sampling GEMM's rows moved to the channels-last grid, optionally straight into

@@ -254,7 +254,21 @@ def bench_mlp():
         w1t = w1.t().contiguous()
         emit("hip fc1 dgrad", timeit(lambda: kernels.linear_fwd(dp, w1t, None)), f, "TFLOP/s", cfg)
         emit("torch fc1 dgrad", timeit(lambda: dp @ w1), f, "TFLOP/s", cfg)
-        del x, act, pre, dy, dp
+        # the whole MLPBlock (forward + backward under bf16 autocast): fused path vs the TokenLinear + GELU path
+        from long_context_biomedical_imaging_amd import blocks
+        mb = blocks.MLPBlock(D, H).cuda()
+        xm = torch.randn(M, D, device="cuda", requires_grad=True)
+        gy = torch.randn(M, D, device="cuda").to(torch.bfloat16)
+
+        def step():
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = mb(xm)
+            y.backward(gy)
+        for fused in (False, True, False, True):
+            blocks.FUSED_MLP = fused
+            emit(f"MLPBlock fwd+bwd {'fused' if fused else 'unfused'}", timeit(step, 10), 6 * f, "TFLOP/s", cfg)
+        blocks.FUSED_MLP = False
+        del x, act, pre, dy, dp, xm, gy, mb
         torch.cuda.empty_cache()
 
 
