@@ -1874,6 +1874,16 @@ constexpr unsigned char FW_SCHED[16][5] = {
                           // 3 / 4 / 5 = no exps / row-sum adds / conversions, 6 = no LDS-DMA in the loop
 #endif
 
+#ifndef LCI_FWD_RSTG
+#define LCI_FWD_RSTG 1    // K / V staging in the loop: 1 = buffer loads into AGPRs + ds_write_b128, 0 = LDS-DMA
+#endif
+// 16-byte LDS store of an AGPR quad at a lane address + immediate (asm: the compiler neither reorders it nor needs a
+// VGPR copy of the data; completion is implied by the compiler's in-order lgkmcnt waits for later reads)
+template <int OFF>
+__device__ __forceinline__ void hs_st16(unsigned addr, const u32x4& v) {
+  asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(addr), "a"(v), "i"(OFF) : "memory");
+}
+
 // initial S^T of query block 1 before the first half: the exps of block 1 that FW_SCHED wraps into the next half
 // (E1.i in gaps before START_E = 13) see NEG_BIG (exp2 -> 0); the elements exponentiated in the previous half's gaps
 // 13-15 are already "exponentiated": 0. Either way the first half adds and packs zeros for the missing half -1.
@@ -2163,11 +2173,29 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
     }
   };
 
-  // prologue: tiles 0, 1, 2 in flight; wait for tile 0; K rows of its first half
+  // register staging (LCI_FWD_RSTG): tile t+1's pieces (loaded into AGPRs during tile t-1) are stored to ring slot
+  // (t+1) & 3 at gaps 1-7 of tile t's half 0 and tile t+2's loaded at gaps 9-15; the barrier of tile t's half 1
+  // publishes tile t+1. A piece costs a buffer load + a ds_write_b128 instead of an LDS-DMA issue (~56 cycles each,
+  // LCI_FWD_PROBE 6). Pieces past the last tile read as zero (buffer range) into slots nobody reads.
+  u32x4 stg[4];
+  const unsigned wst = lds0 + 2048 * wave + 16 * lane;
+  auto ld_piece = [&](int t, int i) __attribute__((always_inline)) {
+    if (i == 0) stg[0] = hs_ld16(rk, dk0, t * KT * rs2k);
+    if (i == 1) stg[1] = hs_ld16(rk, dk1, t * KT * rs2k);
+    if (i == 2) stg[2] = hs_ld16(rv, dv0, t * KT * rs2v);
+    if (i == 3) stg[3] = hs_ld16(rv, dv1, t * KT * rs2v);
+  };
+  // prologue: tiles 0, 1, 2 in flight (DMA: 0-2; register staging: tile 0 by DMA, tile 1 into the AGPRs); wait for
+  // tile 0; K rows of its first half
   dma_op(0, 0); dma_op(0, 1); dma_op(0, 2); dma_op(0, 3);
-  if (nkt > 1) { dma_op(1, 0); dma_op(1, 1); dma_op(1, 2); dma_op(1, 3); }
-  if (nkt > 2) { dma_op(2, 0); dma_op(2, 1); dma_op(2, 2); dma_op(2, 3); }
-  if (nkt > 2) hs_vmcnt<8>(); else if (nkt > 1) hs_vmcnt<4>(); else hs_vmcnt<0>();
+  if (LCI_FWD_RSTG) {
+    ld_piece(1, 0); ld_piece(1, 1); ld_piece(1, 2); ld_piece(1, 3);
+    hs_vmcnt<0>();
+  } else {
+    if (nkt > 1) { dma_op(1, 0); dma_op(1, 1); dma_op(1, 2); dma_op(1, 3); }
+    if (nkt > 2) { dma_op(2, 0); dma_op(2, 1); dma_op(2, 2); dma_op(2, 3); }
+    if (nkt > 2) hs_vmcnt<8>(); else if (nkt > 1) hs_vmcnt<4>(); else hs_vmcnt<0>();
+  }
   __builtin_amdgcn_s_barrier();
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) kr[ks] = row(0, 0, ks);
@@ -2183,13 +2211,28 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
     // slot of tile t-1 (last read by half 1 of tile t-1, before this barrier), one operation per two gaps
     auto stage = [&](int g) __attribute__((always_inline)) {
       if (t + 1 < nkt && g == 6) {
-        if (t + 2 < nkt) hs_vmcnt<4>(); else hs_vmcnt<0>();
+        if (!LCI_FWD_RSTG) { if (t + 2 < nkt) hs_vmcnt<4>(); else hs_vmcnt<0>(); }
         __builtin_amdgcn_s_barrier();
       }
-      if (LCI_FWD_PROBE != 6 && t + 3 < nkt && g >= 8 && !(g & 1)) dma_op(t + 3, (g - 8) >> 1);
+      if (!LCI_FWD_RSTG && LCI_FWD_PROBE != 6 && t + 3 < nkt && g >= 8 && !(g & 1)) dma_op(t + 3, (g - 8) >> 1);
     };
-    auto none = [](int) __attribute__((always_inline)) {};
-    half(std::integral_constant<int, 0>{}, soff, 0, soff, 1, a0, a1, none);
+    auto rstg = [&](int g) __attribute__((always_inline)) {
+      if (!LCI_FWD_RSTG || LCI_FWD_PROBE == 6) return;
+      if (g == 1) hs_vmcnt<0>();   // tile t+1's pieces (loaded a tile ago)
+      if (g < 8 && (g & 1)) {
+        constexpr int S1 = sl >= 0 ? ((sl + 1) & (NSLOT - 1)) * SLOT_B : 0;
+        const unsigned base = sl >= 0 ? wst : wst + (unsigned)(((t + 1) & (NSLOT - 1)) * SLOT_B);
+        switch (g) {
+          case 1: hs_st16<S1>(base, stg[0]); break;
+          case 3: hs_st16<S1 + 1024>(base, stg[1]); break;
+          case 5: hs_st16<S1 + TILE_B>(base, stg[2]); break;
+          default: hs_st16<S1 + TILE_B + 1024>(base, stg[3]); break;
+        }
+      } else if (g >= 9 && (g & 1)) {
+        ld_piece(t + 2, (g - 9) >> 1);
+      }
+    };
+    half(std::integral_constant<int, 0>{}, soff, 0, soff, 1, a0, a1, rstg);
     half(std::integral_constant<int, 1>{}, soff, 1, nsoff, 0, b0, b1, stage);
   };
   const bool ragged = (L & (KT - 1)) != 0;
@@ -2222,6 +2265,7 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
     asm volatile("s_nop 4" ::: "memory");
     tile(ICR{}, tl, M[0][0], M[0][1], M[1][0], M[1][1]);
   }
+  if (LCI_FWD_RSTG) hs_vmcnt<0>();   // the last tiles' staging loads (past the end: zeros) retire before the exit
   // query block 1 of the last half: its wrapped VALU (gaps 0-5) and its PV MFMAs
 #pragma unroll
   for (int g = 0; g < 8; ++g) {

@@ -39,13 +39,17 @@ def _kernel_body(isa, name):
 
 
 def _loops(body):
-    """Instruction text of every loop (from a loop header label to the branch back to it)."""
+    """Instruction text of every loop: its header block and every block the compiler annotates as in that loop
+    ("in Loop: Header=BBx_y"), wherever they are laid out (a rotated loop's latch may come before its header)."""
+    blocks = re.split(r"^(?=\.LBB\d+_\d+:)", body, flags=re.M)
     out = []
-    for m in re.finditer(r"^(\.LBB\d+_\d+):.*Loop Header", body, re.M):
-        lab = m.group(1)
-        ends = [b.start() for b in re.finditer(r"s_c?branch\w*\s+" + re.escape(lab) + r"\b", body[m.end():])]
-        assert ends, f"no back edge for {lab}"
-        out.append(body[m.end():m.end() + max(ends)])
+    for blk in blocks:
+        m = re.match(r"\.L(BB\d+_\d+):.*Loop Header", blk)
+        if not m:
+            continue
+        hid = m.group(1)
+        members = [b for b in blocks if b is blk or re.match(r"\.LBB\d+_\d+:.*in Loop: Header=" + hid + r"\b", b)]
+        out.append("\n".join(members))
     return out
 
 
