@@ -551,6 +551,99 @@ __device__ __forceinline__ f32x2 tw3(const Tw3& w, long long e) {
   return cmul(cmul(w.t[e0], w.t[(1 << w.l0) + e1]), w.t[(1 << w.l0) + (1 << w.l1) + e2]);
 }
 
+// ------------------------------------------------ column FFTs of n1 = 1024 in registers, one column per wave at a time
+// (LCI_FFT_WAVE): lane L holds x[L + 64 r], r < 16; a 16-point DFT over r (4 x 4 in registers), twiddle
+// W_1024^(L k), then for each half k = 8h + k' of the 16 frequencies the 64-point DFT over the lanes as 8 x 8 with two
+// wave-local LDS transposes (the second and third stages of fft512_wave) -- X[k + 16 m], m = m1 + 8 m2, lands in
+// lane k' + 8 m1. The column's own LDS region (its values are in registers by then) is the transpose buffer, so the
+// only workgroup barriers are the ones around the load and store loops (the in-place Stockham passes take two per
+// radix pass, 8 at n1 = 1024).
+#ifndef LCI_FFT_WAVE
+#define LCI_FFT_WAVE 1
+#endif
+template <bool INV>
+__device__ __forceinline__ f32x2 w16(int t) {   // W_16^t (forward e^{-2 pi i t / 16}), t < 16
+  constexpr float C1 = 0.92387953251128674f, S1 = 0.38268343236508977f, H = 0.70710678118654752f;
+  const float c[16] = {1.f, C1, H, S1, 0.f, -S1, -H, -C1, -1.f, -C1, -H, -S1, 0.f, S1, H, C1};
+  const float sn[16] = {0.f, S1, H, C1, 1.f, C1, H, S1, 0.f, -S1, -H, -C1, -1.f, -C1, -H, -S1};
+  return f32x2{c[t], INV ? sn[t] : -sn[t]};
+}
+template <bool INV>
+__device__ __forceinline__ void dft16(f32x2 (&v)[16]) {   // v[c + 4 d] = sum_r v[r] W_16^(r (c + 4 d)), r = 4 a + b
+  f32x2 t[4][4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    f32x2 q[4] = {v[b], v[4 + b], v[8 + b], v[12 + b]};
+    dft<4, INV>(q);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) t[b][c] = (b * c == 0) ? q[c] : cmul(q[c], w16<INV>(b * c));
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    f32x2 q[4] = {t[0][c], t[1][c], t[2][c], t[3][c]};
+    dft<4, INV>(q);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) v[c + 4 * d] = q[d];
+  }
+}
+// 64-point DFTs over the lanes of 8 sequences: in, lane L holds v[k] = Y[k][L]; out, lane k + 8 m1 holds
+// v[m2] = sum_l Y[k][l] W_64^(l (m1 + 8 m2)). twl: W_N^t (N = 64 TS entries). buf: 8 * R5_S1 complex.
+template <bool INV, int TS>
+__device__ __forceinline__ void dft64_lanes(f32x2 (&v)[8], f32x2* buf, const f32x2* twl, int L) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) buf[k * R5_S1 + L] = v[k];
+  wave_lds_sync();
+  const int la = L & 7, kk = L >> 3;
+#pragma unroll
+  for (int lb = 0; lb < 8; ++lb) v[lb] = buf[kk * R5_S1 + la + 8 * lb];
+  wave_lds_sync();
+  dft<8, INV>(v);
+#pragma unroll
+  for (int m = 1; m < 8; ++m) {
+    f32x2 w = twl[(TS * la * m) & (64 * TS - 1)];
+    if (INV) w.y = -w.y;
+    v[m] = cmul(v[m], w);
+  }
+#pragma unroll
+  for (int m = 0; m < 8; ++m) buf[(kk + 8 * m) * R5_S2 + la] = v[m];
+  wave_lds_sync();
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v[q] = buf[L * R5_S2 + q];
+  wave_lds_sync();
+  dft<8, INV>(v);
+}
+// the columns g = wave, wave + 4, ... of x (ld apart), in place; twl: W_1024^t
+template <bool INV, int GW>
+__device__ __forceinline__ void col_fft1024_waves(f32x2* x, int ld, const f32x2* twl) {
+  const int L = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int g = wave; g < GW; g += 4) {
+    f32x2* col = x + g * ld;
+    f32x2 v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = col[L + 64 * r];
+    wave_lds_sync();   // every lane's reads of the column are done before it becomes the transpose buffer
+    dft16<INV>(v);
+#pragma unroll
+    for (int k = 1; k < 16; ++k) {
+      f32x2 w = twl[(L * k) & 1023];
+      if (INV) w.y = -w.y;
+      v[k] = cmul(v[k], w);
+    }
+    f32x2 lo[8], hi[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { lo[k] = v[k]; hi[k] = v[8 + k]; }
+    dft64_lanes<INV, 16>(lo, col, twl, L);
+    dft64_lanes<INV, 16>(hi, col, twl, L);
+    const int base = (L & 7) + 16 * (L >> 3);   // X[8h + k' + 16 m1 + 128 m2]
+#pragma unroll
+    for (int m2 = 0; m2 < 8; ++m2) {
+      col[base + 128 * m2] = lo[m2];
+      col[base + 8 + 128 * m2] = hi[m2];
+    }
+    wave_lds_sync();
+  }
+}
+
 // grid (n2 / GW, npairs_total or C); block 256. Same math as fft_col_fwd_kernel.
 template <int GW, int CW>
 __global__ __launch_bounds__(256) void fft_colw_fwd_kernel(FftArgs a) {
@@ -618,7 +711,12 @@ __global__ __launch_bounds__(256) void fft_colw_fwd_kernel(FftArgs a) {
     }
   }
   __syncthreads();
-  lds_fft_inplace<false, CW>(x, a.n1, a.ln1, twl, ld);
+  if constexpr (LCI_FFT_WAVE && CW / GW == 1024) {
+    col_fft1024_waves<false, GW>(x, ld, twl);
+    __syncthreads();
+  } else {
+    lds_fft_inplace<false, CW>(x, a.n1, a.ln1, twl, ld);
+  }
   f32x2* S = (a.single ? a.SK : a.S) + (long long)pid * a.n;
   for (int idx = threadIdx.x; idx < CW / 2; idx += 256) {   // 16-byte stores of 2 adjacent columns
     const int g = (idx % (GW / 2)) * 2, k1 = idx / (GW / 2);
@@ -663,7 +761,12 @@ __global__ __launch_bounds__(256) void fft_colw_inv_kernel(FftArgs a) {
     }
   }
   __syncthreads();
-  lds_fft_inplace<true, CW>(x, a.n1, a.ln1, twl, ld);
+  if constexpr (LCI_FFT_WAVE && CW / GW == 1024) {
+    col_fft1024_waves<true, GW>(x, ld, twl);
+    __syncthreads();
+  } else {
+    lds_fft_inplace<true, CW>(x, a.n1, a.ln1, twl, ld);
+  }
   // only a < ceil(L / n2) rows of the column carry outputs (m < L); the rest is the discarded wrap half
   const int na = (a.L - c0 + a.n2 - 1) / a.n2;
   if (a.single) {

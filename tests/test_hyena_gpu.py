@@ -137,7 +137,7 @@ def test_compat_fftconv_ref_signature():
 
 
 def test_fftconv_c4_length_subset():
-    """configs[3] length: L = 262144 (1024^2 patch 2), FFT n = 2^19 (n1 = 512 column FFTs, n2 = 1024 rows).
+    """configs[3] length: L = 262144 (1024^2 patch 2), FFT n = 2^19 (n1 = 1024 column FFTs, in registers, n2 = 512 rows).
     Whole rows vs an fp64 torch.fft evaluation of the same causal convolution, plus 64 output positions of each
     row against the direct sum y[t] = sum_{s<=t} k[t-s] u[s] + D u[t]; gradients through the same path
     (adjoint rows vs fp64 FFT correlation). Tolerance rel-L2 2e-5 (as at L <= 65536)."""

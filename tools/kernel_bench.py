@@ -163,17 +163,19 @@ def bench_dwconv(L=1 << 21, B=1, C=192):
 
 
 def bench_fftconv():
-    B, H, hd, L = 2, 6, 64, 65536
-    u = torch.randn(B * H, hd, L, device="cuda").requires_grad_(True)
-    k = (torch.randn(hd, L, device="cuda") * torch.exp(-torch.linspace(0, 8, L, device="cuda"))).requires_grad_(True)
-    D = torch.randn(hd, device="cuda").requires_grad_(True)
-    rows = B * H * hd
-    emit("fftconv_fwd", timeit(lambda: kernels.fftconv(u, k, D)), 8.0 * rows * L, "GB/s",
-         f"rows {rows} L{L} f32 (ViT-hyena 512^2 p2)")
-    y = kernels.fftconv(u, k, D)
-    g = torch.randn_like(y)
-    emit("fftconv_fwd+bwd", timeit(lambda: torch.autograd.grad(kernels.fftconv(u, k, D), [u, k, D], g)),
-         24.0 * rows * L, "GB/s", "same, fwd+bwd (u, k, D grads)")
+    for L, tag in ((65536, "ViT-hyena 512^2 p2"), (262144, "C4: ViT-hyena 1024^2 p2, n = 2^19")):
+        B, H, hd = 2, 6, 64
+        u = torch.randn(B * H, hd, L, device="cuda").requires_grad_(True)
+        k = (torch.randn(hd, L, device="cuda") * torch.exp(-torch.linspace(0, 8, L, device="cuda"))).requires_grad_(True)
+        D = torch.randn(hd, device="cuda").requires_grad_(True)
+        rows = B * H * hd
+        emit("fftconv_fwd", timeit(lambda: kernels.fftconv(u, k, D)), 8.0 * rows * L, "GB/s", f"rows {rows} L{L} f32 ({tag})")
+        y = kernels.fftconv(u, k, D)
+        g = torch.randn_like(y)
+        emit("fftconv_fwd+bwd", timeit(lambda: torch.autograd.grad(kernels.fftconv(u, k, D), [u, k, D], g)),
+             24.0 * rows * L, "GB/s", f"L{L}, fwd+bwd (u, k, D grads)")
+        del u, k, D, y, g
+        torch.cuda.empty_cache()
 
 
 def bench_direct_conv():
