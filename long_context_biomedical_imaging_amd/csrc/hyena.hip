@@ -644,6 +644,69 @@ __device__ __forceinline__ void col_fft1024_waves(f32x2* x, int ld, const f32x2*
   }
 }
 
+// n1 = 512: fft512_wave per column; n1 = 256: two columns per call (4 points each: a 4-point DFT over r, twiddle
+// W_256^(L k), and the 8 sequences (column, k) through one dft64_lanes). Both use a per-wave scratch of
+// 8 R5_S1 complex after the twiddle tables (the column regions are too short for the transpose strides).
+template <bool INV, int GW, int N1>
+__device__ __forceinline__ void col_fft_small_waves(f32x2* x, int ld, const f32x2* twl, f32x2* scr) {
+  const int L = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  f32x2* buf = scr + wave * 8 * R5_S1;
+  if constexpr (N1 == 512) {
+    for (int g = wave; g < GW; g += 4) {
+      f32x2* col = x + g * ld;
+      f32x2 v[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = col[L + 64 * r];
+      fft512_wave<INV>(v, buf, twl, L);
+#pragma unroll
+      for (int m = 0; m < 8; ++m) col[L + 64 * m] = v[m];
+    }
+  } else {
+    static_assert(N1 == 256 && GW % 8 == 0, "two columns per wave and call");
+    for (int g = wave; g < GW; g += 8) {   // columns g and g + 4
+      f32x2* c0 = x + g * ld;
+      f32x2* c1 = x + (g + 4) * ld;
+      f32x2 p[4], q[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { p[r] = c0[L + 64 * r]; q[r] = c1[L + 64 * r]; }
+      dft<4, INV>(p);
+      dft<4, INV>(q);
+      f32x2 w[8];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        f32x2 t = twl[(L * k) & 255];
+        if (INV) t.y = -t.y;
+        w[k] = k ? cmul(p[k], t) : p[k];
+        w[4 + k] = k ? cmul(q[k], t) : q[k];
+      }
+      dft64_lanes<INV, 4>(w, buf, twl, L);
+      // lane k'' + 8 m1 holds X[k + 4 (m1 + 8 m2)] of column k'' < 4 ? g : g + 4, k = k'' & 3
+      f32x2* col = (L & 7) < 4 ? c0 : c1;
+      const int base = (L & 3) + 4 * (L >> 3);
+#pragma unroll
+      for (int m2 = 0; m2 < 8; ++m2) col[base + 32 * m2] = w[m2];
+    }
+  }
+}
+template <bool INV, int GW, int CW>
+__device__ __forceinline__ bool col_fft_waves(f32x2* x, int ld, const f32x2* twl, f32x2* scr) {
+  constexpr int N1 = CW / GW;
+  if constexpr (!LCI_FFT_WAVE) {
+    return false;
+  } else if constexpr (N1 == 1024) {
+    col_fft1024_waves<INV, GW>(x, ld, twl);
+    return true;
+  } else if constexpr (N1 == 512 || (N1 == 256 && GW % 8 == 0)) {
+    col_fft_small_waves<INV, GW, N1>(x, ld, twl, scr);
+    return true;
+  } else {
+    return false;
+  }
+}
+__host__ __device__ constexpr bool col_wave_scratch(int n1, int gw) {
+  return LCI_FFT_WAVE && (n1 == 512 || (n1 == 256 && gw % 8 == 0));
+}
+
 // grid (n2 / GW, npairs_total or C); block 256. Same math as fft_col_fwd_kernel.
 template <int GW, int CW>
 __global__ __launch_bounds__(256) void fft_colw_fwd_kernel(FftArgs a) {
@@ -711,12 +774,8 @@ __global__ __launch_bounds__(256) void fft_colw_fwd_kernel(FftArgs a) {
     }
   }
   __syncthreads();
-  if constexpr (LCI_FFT_WAVE && CW / GW == 1024) {
-    col_fft1024_waves<false, GW>(x, ld, twl);
-    __syncthreads();
-  } else {
-    lds_fft_inplace<false, CW>(x, a.n1, a.ln1, twl, ld);
-  }
+  if (col_fft_waves<false, GW, CW>(x, ld, twl, twl + a.n1 + tw3_entries(a.ln1 + a.ln2))) __syncthreads();
+  else lds_fft_inplace<false, CW>(x, a.n1, a.ln1, twl, ld);
   f32x2* S = (a.single ? a.SK : a.S) + (long long)pid * a.n;
   for (int idx = threadIdx.x; idx < CW / 2; idx += 256) {   // 16-byte stores of 2 adjacent columns
     const int g = (idx % (GW / 2)) * 2, k1 = idx / (GW / 2);
@@ -761,12 +820,8 @@ __global__ __launch_bounds__(256) void fft_colw_inv_kernel(FftArgs a) {
     }
   }
   __syncthreads();
-  if constexpr (LCI_FFT_WAVE && CW / GW == 1024) {
-    col_fft1024_waves<true, GW>(x, ld, twl);
-    __syncthreads();
-  } else {
-    lds_fft_inplace<true, CW>(x, a.n1, a.ln1, twl, ld);
-  }
+  if (col_fft_waves<true, GW, CW>(x, ld, twl, twl + a.n1 + tw3_entries(a.ln1 + a.ln2))) __syncthreads();
+  else lds_fft_inplace<true, CW>(x, a.n1, a.ln1, twl, ld);
   // only a < ceil(L / n2) rows of the column carry outputs (m < L); the rest is the discarded wrap half
   const int na = (a.L - c0 + a.n2 - 1) / a.n2;
   if (a.single) {
@@ -1623,7 +1678,8 @@ static int launch_col(FftArgs& a, bool inv, int nblk_y, hipStream_t s) {
   const int gw = cw / a.n1;
   if ((cw == 8192 || cw == 4096) && (gw == 4 || gw == 8 || gw == 16 || gw == 32) && a.n2 % gw == 0 &&
       !getenv("LCI_FFT_COL_V1")) {
-    const size_t sh = ((size_t)gw * (a.n1 + 1) + a.n1 + tw3_entries(a.ln1 + a.ln2)) * sizeof(f32x2);
+    const size_t sh = ((size_t)gw * (a.n1 + 1) + a.n1 + tw3_entries(a.ln1 + a.ln2) +
+                       (col_wave_scratch(a.n1, gw) ? 4 * 8 * R5_S1 : 0)) * sizeof(f32x2);
     dim3 grid(a.n2 / gw, nblk_y);
 #define LCI_COLW(GW, CW)                                                                                           \
     (void)hipFuncSetAttribute((const void*)(inv ? fft_colw_inv_kernel<GW, CW> : fft_colw_fwd_kernel<GW, CW>),      \

@@ -30,9 +30,10 @@ def test_fftconv_vs_reference_vectors(L):
     assert rel_err(Dc.grad, Dr.grad) < 1e-4
 
 
-@pytest.mark.parametrize("R,C,L", [(3, 32, 343), (2, 8, 4096), (1, 4, 65536), (5, 3, 777)])
+@pytest.mark.parametrize("R,C,L", [(3, 32, 343), (2, 8, 4096), (1, 4, 65536), (5, 3, 777), (3, 2, 100000)])
 def test_fftconv_shapes(R, C, L):
-    """Odd row counts (a half-empty pair), non-power-of-two L (Swin windows 7^3 = 343), and the metric L."""
+    """Odd row counts (a half-empty pair), non-power-of-two L (Swin windows 7^3 = 343), the metric L, and n = 2^18
+    (n1 = 512 column FFTs)."""
     from long_context_biomedical_imaging_amd import kernels
     torch.manual_seed(R * 1000 + L)
     u = torch.randn(R, C, L)
