@@ -613,10 +613,10 @@ __device__ __forceinline__ void dft64_lanes(f32x2 (&v)[8], f32x2* buf, const f32
   dft<8, INV>(v);
 }
 // the columns g = wave, wave + 4, ... of x (ld apart), in place; twl: W_1024^t
-template <bool INV, int GW>
+template <bool INV, int GW, int NW>
 __device__ __forceinline__ void col_fft1024_waves(f32x2* x, int ld, const f32x2* twl) {
   const int L = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int g = wave; g < GW; g += 4) {
+  for (int g = wave; g < GW; g += NW) {
     f32x2* col = x + g * ld;
     f32x2 v[16];
 #pragma unroll
@@ -688,28 +688,24 @@ __device__ __forceinline__ void col_fft_small_waves(f32x2* x, int ld, const f32x
     }
   }
 }
-template <bool INV, int GW, int CW>
-__device__ __forceinline__ bool col_fft_waves(f32x2* x, int ld, const f32x2* twl, f32x2* scr) {
-  constexpr int N1 = CW / GW;
-  if constexpr (!LCI_FFT_WAVE) {
-    return false;
-  } else if constexpr (N1 == 1024) {
-    col_fft1024_waves<INV, GW>(x, ld, twl);
-    return true;
-  } else if constexpr (N1 == 512 || (N1 == 256 && GW % 8 == 0)) {
-    col_fft_small_waves<INV, GW, N1>(x, ld, twl, scr);
-    return true;
-  } else {
-    return false;
-  }
-}
 __host__ __device__ constexpr bool col_wave_scratch(int n1, int gw) {
   return LCI_FFT_WAVE && (n1 == 512 || (n1 == 256 && gw % 8 == 0));
 }
+__host__ __device__ constexpr bool col_wave_path(int n1, int gw) { return (LCI_FFT_WAVE && n1 == 1024) || col_wave_scratch(n1, gw); }
+template <bool INV, int GW, int CW, int NT>
+__device__ __forceinline__ void col_fft_waves(f32x2* x, int ld, const f32x2* twl, f32x2* scr) {
+  constexpr int N1 = CW / GW;
+  if constexpr (N1 == 1024) {
+    col_fft1024_waves<INV, GW, NT / 64>(x, ld, twl);
+  } else {
+    static_assert(NT == 256, "small column FFTs: 4 waves");
+    col_fft_small_waves<INV, GW, N1>(x, ld, twl, scr);
+  }
+}
 
-// grid (n2 / GW, npairs_total or C); block 256. Same math as fft_col_fwd_kernel.
-template <int GW, int CW>
-__global__ __launch_bounds__(256) void fft_colw_fwd_kernel(FftArgs a) {
+// grid (n2 / GW, npairs_total or C); block NT. Same math as fft_col_fwd_kernel.
+template <int GW, int CW, int NT>
+__global__ __launch_bounds__(NT) void fft_colw_fwd_kernel(FftArgs a) {
   extern __shared__ __attribute__((aligned(16))) f32x2 lds[];
   const int ld = a.n1 + 1;
   f32x2* x = lds;
@@ -729,11 +725,11 @@ __global__ __launch_bounds__(256) void fft_colw_fwd_kernel(FftArgs a) {
   const float* s1 = r1 >= 0 ? a.src + (long long)r1 * a.L : nullptr;
   if ((a.L & 3) == 0) {   // 16-byte loads of 4 adjacent columns (rows are 16-B aligned, chunks all in or out)
     constexpr int NQ = CW / 4;
-    for (int base = 0; base < NQ; base += UB * 256) {
+    for (int base = 0; base < NQ; base += UB * NT) {
       f32x4 v0[UB], v1[UB];
 #pragma unroll
       for (int u = 0; u < UB; ++u) {
-        const int idx = base + u * 256 + threadIdx.x;
+        const int idx = base + u * NT + threadIdx.x;
         const int g = (idx % (GW / 4)) * 4, ai = idx / (GW / 4);
         const int m = ai * a.n2 + c0 + g;
         v0[u] = v1[u] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -744,7 +740,7 @@ __global__ __launch_bounds__(256) void fft_colw_fwd_kernel(FftArgs a) {
       }
 #pragma unroll
       for (int u = 0; u < UB; ++u) {
-        const int idx = base + u * 256 + threadIdx.x;
+        const int idx = base + u * NT + threadIdx.x;
         const int g = (idx % (GW / 4)) * 4, ai = idx / (GW / 4);
         if (idx < NQ) {
 #pragma unroll
@@ -753,11 +749,11 @@ __global__ __launch_bounds__(256) void fft_colw_fwd_kernel(FftArgs a) {
       }
     }
   } else {
-    for (int base = 0; base < CW; base += UB * 256) {
+    for (int base = 0; base < CW; base += UB * NT) {
       f32x2 v[UB];
 #pragma unroll
       for (int u = 0; u < UB; ++u) {
-        const int idx = base + u * 256 + threadIdx.x;
+        const int idx = base + u * NT + threadIdx.x;
         const int g = idx % GW, ai = idx / GW;
         const int m = ai * a.n2 + c0 + g;
         v[u] = f32x2{0.f, 0.f};
@@ -768,16 +764,21 @@ __global__ __launch_bounds__(256) void fft_colw_fwd_kernel(FftArgs a) {
       }
 #pragma unroll
       for (int u = 0; u < UB; ++u) {
-        const int idx = base + u * 256 + threadIdx.x;
+        const int idx = base + u * NT + threadIdx.x;
         x[(idx % GW) * ld + idx / GW] = v[u];
       }
     }
   }
   __syncthreads();
-  if (col_fft_waves<false, GW, CW>(x, ld, twl, twl + a.n1 + tw3_entries(a.ln1 + a.ln2))) __syncthreads();
-  else lds_fft_inplace<false, CW>(x, a.n1, a.ln1, twl, ld);
+  if constexpr (col_wave_path(CW / GW, GW)) {
+    col_fft_waves<false, GW, CW, NT>(x, ld, twl, twl + a.n1 + tw3_entries(a.ln1 + a.ln2));
+    __syncthreads();
+  } else {
+    static_assert(NT == 256, "the LDS Stockham passes assume 256 threads");
+    lds_fft_inplace<false, CW>(x, a.n1, a.ln1, twl, ld);
+  }
   f32x2* S = (a.single ? a.SK : a.S) + (long long)pid * a.n;
-  for (int idx = threadIdx.x; idx < CW / 2; idx += 256) {   // 16-byte stores of 2 adjacent columns
+  for (int idx = threadIdx.x; idx < CW / 2; idx += NT) {   // 16-byte stores of 2 adjacent columns
     const int g = (idx % (GW / 2)) * 2, k1 = idx / (GW / 2);
     const long long e = (long long)(c0 + g) * k1;
     const f32x2 p0 = cmul(x[g * ld + k1], tw3(tw3t, e & (a.n - 1)));
@@ -787,8 +788,8 @@ __global__ __launch_bounds__(256) void fft_colw_fwd_kernel(FftArgs a) {
 }
 
 // grid (n2 / GW, npairs_total or C); same math as fft_col_inv_kernel.
-template <int GW, int CW>
-__global__ __launch_bounds__(256) void fft_colw_inv_kernel(FftArgs a) {
+template <int GW, int CW, int NT>
+__global__ __launch_bounds__(NT) void fft_colw_inv_kernel(FftArgs a) {
   extern __shared__ __attribute__((aligned(16))) f32x2 lds[];
   const int ld = a.n1 + 1;
   f32x2* x = lds;
@@ -800,17 +801,17 @@ __global__ __launch_bounds__(256) void fft_colw_inv_kernel(FftArgs a) {
   const f32x2* S = (a.single ? a.SK : a.S) + (long long)pid * a.n;
   __syncthreads();   // the twiddle tables are read below
   constexpr int NH = CW / 2;   // 16-byte loads of 2 adjacent columns
-  for (int base = 0; base < NH; base += UB * 256) {
+  for (int base = 0; base < NH; base += UB * NT) {
     f32x4 v[UB];
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
-      const int idx = base + u * 256 + threadIdx.x;
+      const int idx = base + u * NT + threadIdx.x;
       const int g = (idx % (GW / 2)) * 2, k1 = idx / (GW / 2);
       if (idx < NH) v[u] = *(const f32x4*)(S + (long long)k1 * a.n2 + c0 + g);
     }
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
-      const int idx = base + u * 256 + threadIdx.x;
+      const int idx = base + u * NT + threadIdx.x;
       const int g = (idx % (GW / 2)) * 2, k1 = idx / (GW / 2);
       if (idx < NH) {
         const long long e = (long long)(c0 + g) * k1;
@@ -820,12 +821,17 @@ __global__ __launch_bounds__(256) void fft_colw_inv_kernel(FftArgs a) {
     }
   }
   __syncthreads();
-  if (col_fft_waves<true, GW, CW>(x, ld, twl, twl + a.n1 + tw3_entries(a.ln1 + a.ln2))) __syncthreads();
-  else lds_fft_inplace<true, CW>(x, a.n1, a.ln1, twl, ld);
+  if constexpr (col_wave_path(CW / GW, GW)) {
+    col_fft_waves<true, GW, CW, NT>(x, ld, twl, twl + a.n1 + tw3_entries(a.ln1 + a.ln2));
+    __syncthreads();
+  } else {
+    static_assert(NT == 256, "the LDS Stockham passes assume 256 threads");
+    lds_fft_inplace<true, CW>(x, a.n1, a.ln1, twl, ld);
+  }
   // only a < ceil(L / n2) rows of the column carry outputs (m < L); the rest is the discarded wrap half
   const int na = (a.L - c0 + a.n2 - 1) / a.n2;
   if (a.single) {
-    for (int idx = threadIdx.x; idx < GW * na; idx += 256) {
+    for (int idx = threadIdx.x; idx < GW * na; idx += NT) {
       const int g = idx % GW, ai = idx / GW;
       const int m = ai * a.n2 + c0 + g;
       if (m < a.L) a.dk[(long long)pid * a.L + m] = x[g * ld + ai].x;
@@ -841,11 +847,11 @@ __global__ __launch_bounds__(256) void fft_colw_inv_kernel(FftArgs a) {
   float* d1 = r1 >= 0 ? a.dst + (long long)r1 * a.L : nullptr;
   if ((a.L & 3) == 0) {   // 16-byte loads / stores of 4 adjacent columns
     const int totq = (GW / 4) * na;
-    for (int base = 0; base < totq; base += UB * 256) {
+    for (int base = 0; base < totq; base += UB * NT) {
       f32x4 u0[UB], u1[UB];
 #pragma unroll
       for (int u = 0; u < UB; ++u) {
-        const int idx = base + u * 256 + threadIdx.x;
+        const int idx = base + u * NT + threadIdx.x;
         const int m = (idx / (GW / 4)) * a.n2 + c0 + (idx % (GW / 4)) * 4;
         u0[u] = u1[u] = f32x4{0.f, 0.f, 0.f, 0.f};
         if (idx < totq && m < a.L && a.Dv) {
@@ -855,7 +861,7 @@ __global__ __launch_bounds__(256) void fft_colw_inv_kernel(FftArgs a) {
       }
 #pragma unroll
       for (int u = 0; u < UB; ++u) {
-        const int idx = base + u * 256 + threadIdx.x;
+        const int idx = base + u * NT + threadIdx.x;
         const int g = (idx % (GW / 4)) * 4, ai = idx / (GW / 4);
         const int m = ai * a.n2 + c0 + g;
         if (idx < totq && m < a.L) {
@@ -874,11 +880,11 @@ __global__ __launch_bounds__(256) void fft_colw_inv_kernel(FftArgs a) {
     return;
   }
   const int total = GW * na;
-  for (int base = 0; base < total; base += UB * 256) {
+  for (int base = 0; base < total; base += UB * NT) {
     float u0[UB], u1[UB];
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
-      const int idx = base + u * 256 + threadIdx.x;
+      const int idx = base + u * NT + threadIdx.x;
       const int m = (idx / GW) * a.n2 + c0 + idx % GW;
       u0[u] = u1[u] = 0.f;
       if (idx < total && m < a.L) {
@@ -888,7 +894,7 @@ __global__ __launch_bounds__(256) void fft_colw_inv_kernel(FftArgs a) {
     }
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
-      const int idx = base + u * 256 + threadIdx.x;
+      const int idx = base + u * NT + threadIdx.x;
       const int g = idx % GW, ai = idx / GW;
       const int m = ai * a.n2 + c0 + g;
       if (idx < total && m < a.L) {
@@ -1674,24 +1680,30 @@ static int launch_col(FftArgs& a, bool inv, int nblk_y, hipStream_t s) {
   // >= 8 columns (32-B row segments); 8192 for n1 = 1024 (C4: 4096 would load 16-B row segments, measured 24 ms/step
   // slower)
   static const int env_cw = getenv("LCI_FFT_CW") ? atoi(getenv("LCI_FFT_CW")) : 0;
-  const int cw = env_cw ? env_cw : (a.n1 <= 512 ? CW_ELEMS / 2 : CW_ELEMS);
+  // n1 = 1024 with the register column FFTs (LCI_FFT_WIDE): 16 columns (64-B row segments) per 512-thread workgroup
+  static const int wide = getenv("LCI_FFT_WIDE") ? atoi(getenv("LCI_FFT_WIDE")) : 1;
+  const int cw = env_cw ? env_cw
+                        : (a.n1 <= 512 ? CW_ELEMS / 2 : (wide && LCI_FFT_WAVE && a.n1 == 1024 ? 2 * CW_ELEMS : CW_ELEMS));
   const int gw = cw / a.n1;
-  if ((cw == 8192 || cw == 4096) && (gw == 4 || gw == 8 || gw == 16 || gw == 32) && a.n2 % gw == 0 &&
+  if ((cw == 16384 ? a.n1 == 1024 && gw == 16 : (cw == 8192 || cw == 4096)) &&
+      (gw == 4 || gw == 8 || gw == 16 || gw == 32) && a.n2 % gw == 0 &&
       !getenv("LCI_FFT_COL_V1")) {
     const size_t sh = ((size_t)gw * (a.n1 + 1) + a.n1 + tw3_entries(a.ln1 + a.ln2) +
                        (col_wave_scratch(a.n1, gw) ? 4 * 8 * R5_S1 : 0)) * sizeof(f32x2);
     dim3 grid(a.n2 / gw, nblk_y);
-#define LCI_COLW(GW, CW)                                                                                           \
-    (void)hipFuncSetAttribute((const void*)(inv ? fft_colw_inv_kernel<GW, CW> : fft_colw_fwd_kernel<GW, CW>),      \
+#define LCI_COLW(GW, CW, NT)                                                                                       \
+    (void)hipFuncSetAttribute((const void*)(inv ? fft_colw_inv_kernel<GW, CW, NT> : fft_colw_fwd_kernel<GW, CW, NT>), \
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                           \
-    if (inv) hipLaunchKernelGGL((fft_colw_inv_kernel<GW, CW>), grid, dim3(256), sh, s, a);                       \
-    else hipLaunchKernelGGL((fft_colw_fwd_kernel<GW, CW>), grid, dim3(256), sh, s, a);
-    if (cw == 8192) {
-      if (gw == 32) { LCI_COLW(32, 8192) } else if (gw == 16) { LCI_COLW(16, 8192) } else if (gw == 8) { LCI_COLW(8, 8192) }
-      else return 1;
+    if (inv) hipLaunchKernelGGL((fft_colw_inv_kernel<GW, CW, NT>), grid, dim3(NT), sh, s, a);                    \
+    else hipLaunchKernelGGL((fft_colw_fwd_kernel<GW, CW, NT>), grid, dim3(NT), sh, s, a);
+    if (cw == 16384) {
+      if (gw == 16) { LCI_COLW(16, 16384, 512) } else return 1;
+    } else if (cw == 8192) {
+      if (gw == 32) { LCI_COLW(32, 8192, 256) } else if (gw == 16) { LCI_COLW(16, 8192, 256) }
+      else if (gw == 8) { LCI_COLW(8, 8192, 256) } else return 1;
     } else {
-      if (gw == 16) { LCI_COLW(16, 4096) } else if (gw == 8) { LCI_COLW(8, 4096) } else if (gw == 4) { LCI_COLW(4, 4096) }
-      else return 1;
+      if (gw == 16) { LCI_COLW(16, 4096, 256) } else if (gw == 8) { LCI_COLW(8, 4096, 256) }
+      else if (gw == 4) { LCI_COLW(4, 4096, 256) } else return 1;
     }
 #undef LCI_COLW
     LCI_LAUNCH_CHECK();
