@@ -647,12 +647,12 @@ __device__ __forceinline__ void col_fft1024_waves(f32x2* x, int ld, const f32x2*
 // n1 = 512: fft512_wave per column; n1 = 256: two columns per call (4 points each: a 4-point DFT over r, twiddle
 // W_256^(L k), and the 8 sequences (column, k) through one dft64_lanes). Both use a per-wave scratch of
 // 8 R5_S1 complex after the twiddle tables (the column regions are too short for the transpose strides).
-template <bool INV, int GW, int N1>
+template <bool INV, int GW, int N1, int NW>
 __device__ __forceinline__ void col_fft_small_waves(f32x2* x, int ld, const f32x2* twl, f32x2* scr) {
   const int L = threadIdx.x & 63, wave = threadIdx.x >> 6;
   f32x2* buf = scr + wave * 8 * R5_S1;
   if constexpr (N1 == 512) {
-    for (int g = wave; g < GW; g += 4) {
+    for (int g = wave; g < GW; g += NW) {
       f32x2* col = x + g * ld;
       f32x2 v[8];
 #pragma unroll
@@ -662,10 +662,10 @@ __device__ __forceinline__ void col_fft_small_waves(f32x2* x, int ld, const f32x
       for (int m = 0; m < 8; ++m) col[L + 64 * m] = v[m];
     }
   } else {
-    static_assert(N1 == 256 && GW % 8 == 0, "two columns per wave and call");
-    for (int g = wave; g < GW; g += 8) {   // columns g and g + 4
+    static_assert(N1 == 256 && GW % (2 * NW) == 0, "two columns per wave and call");
+    for (int g = wave; g < GW; g += 2 * NW) {   // columns g and g + NW
       f32x2* c0 = x + g * ld;
-      f32x2* c1 = x + (g + 4) * ld;
+      f32x2* c1 = x + (g + NW) * ld;
       f32x2 p[4], q[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) { p[r] = c0[L + 64 * r]; q[r] = c1[L + 64 * r]; }
@@ -680,7 +680,7 @@ __device__ __forceinline__ void col_fft_small_waves(f32x2* x, int ld, const f32x
         w[4 + k] = k ? cmul(q[k], t) : q[k];
       }
       dft64_lanes<INV, 4>(w, buf, twl, L);
-      // lane k'' + 8 m1 holds X[k + 4 (m1 + 8 m2)] of column k'' < 4 ? g : g + 4, k = k'' & 3
+      // lane k'' + 8 m1 holds X[k + 4 (m1 + 8 m2)] of column k'' < 4 ? g : g + NW, k = k'' & 3
       f32x2* col = (L & 7) < 4 ? c0 : c1;
       const int base = (L & 3) + 4 * (L >> 3);
 #pragma unroll
@@ -698,8 +698,7 @@ __device__ __forceinline__ void col_fft_waves(f32x2* x, int ld, const f32x2* twl
   if constexpr (N1 == 1024) {
     col_fft1024_waves<INV, GW, NT / 64>(x, ld, twl);
   } else {
-    static_assert(NT == 256, "small column FFTs: 4 waves");
-    col_fft_small_waves<INV, GW, N1>(x, ld, twl, scr);
+    col_fft_small_waves<INV, GW, N1, NT / 64>(x, ld, twl, scr);
   }
 }
 
@@ -1683,13 +1682,15 @@ static int launch_col(FftArgs& a, bool inv, int nblk_y, hipStream_t s) {
   // n1 = 1024 with the register column FFTs (LCI_FFT_WIDE): 16 columns (64-B row segments) per 512-thread workgroup
   static const int wide = getenv("LCI_FFT_WIDE") ? atoi(getenv("LCI_FFT_WIDE")) : 1;
   const int cw = env_cw ? env_cw
-                        : (a.n1 <= 512 ? CW_ELEMS / 2 : (wide && LCI_FFT_WAVE && a.n1 == 1024 ? 2 * CW_ELEMS : CW_ELEMS));
+                        : (a.n1 <= 512 ? (wide > 1 && LCI_FFT_WAVE && a.n1 == 256 ? CW_ELEMS : CW_ELEMS / 2)
+                                       : (wide && LCI_FFT_WAVE && a.n1 == 1024 ? 2 * CW_ELEMS : CW_ELEMS));
   const int gw = cw / a.n1;
   if ((cw == 16384 ? a.n1 == 1024 && gw == 16 : (cw == 8192 || cw == 4096)) &&
       (gw == 4 || gw == 8 || gw == 16 || gw == 32) && a.n2 % gw == 0 &&
       !getenv("LCI_FFT_COL_V1")) {
     const size_t sh = ((size_t)gw * (a.n1 + 1) + a.n1 + tw3_entries(a.ln1 + a.ln2) +
-                       (col_wave_scratch(a.n1, gw) ? 4 * 8 * R5_S1 : 0)) * sizeof(f32x2);
+                       (col_wave_scratch(a.n1, gw) ? (cw == 8192 && a.n1 == 256 ? 8 : 4) * 8 * R5_S1 : 0)) *
+                      sizeof(f32x2);
     dim3 grid(a.n2 / gw, nblk_y);
 #define LCI_COLW(GW, CW, NT)                                                                                       \
     (void)hipFuncSetAttribute((const void*)(inv ? fft_colw_inv_kernel<GW, CW, NT> : fft_colw_fwd_kernel<GW, CW, NT>), \
@@ -1699,7 +1700,8 @@ static int launch_col(FftArgs& a, bool inv, int nblk_y, hipStream_t s) {
     if (cw == 16384) {
       if (gw == 16) { LCI_COLW(16, 16384, 512) } else return 1;
     } else if (cw == 8192) {
-      if (gw == 32) { LCI_COLW(32, 8192, 256) } else if (gw == 16) { LCI_COLW(16, 8192, 256) }
+      if (gw == 32 && a.n1 == 256 && LCI_FFT_WAVE) { LCI_COLW(32, 8192, 512) }
+      else if (gw == 32) { LCI_COLW(32, 8192, 256) } else if (gw == 16) { LCI_COLW(16, 8192, 256) }
       else if (gw == 8) { LCI_COLW(8, 8192, 256) } else return 1;
     } else {
       if (gw == 16) { LCI_COLW(16, 4096, 256) } else if (gw == 8) { LCI_COLW(8, 4096, 256) }
