@@ -1866,6 +1866,54 @@ constexpr unsigned char FW_SCHED[16][5] = {
     {0x20, 0x21, 0x87, 0x4e, 0x4f},
     {0xa0, 0x60, 0x61, 0x22, 0x23},
     {0x62, 0xa1, 0x63, 0x24, 0x25}};
+// LCI_FWD_MSUM: the row sums as MFMAs (ones . P^T per k-step, 4 per half) instead of 32 VALU adds; 20 gaps per half
+//   0-3 S^T chain block 0 | 4-7 O^T block 1 (previous half) | 8-9 sums block 1 | 10-13 S^T chain block 1 |
+//   14-17 O^T block 0 | 18-19 sums block 0, against 32 exp2 + 16 packs (tools/gen_fwd_sched_ms.py):
+// gap  0: E1.10 C1.4 E1.11
+// gap  1: E1.12 C1.5 E1.13
+// gap  2: E1.14 C1.6 E1.15
+// gap  3: C1.7
+// gap  4: 
+// gap  5: E0.0 E0.1
+// gap  6: E0.2 C0.0 E0.3
+// gap  7: E0.4 C0.1 E0.5
+// gap  8: E0.6 C0.2 E0.7
+// gap  9: E0.8 C0.3 E0.9
+// gap 10: E0.10 C0.4 E0.11
+// gap 11: E0.12 C0.5 E0.13
+// gap 12: E0.14 C0.6 E0.15
+// gap 13: C0.7
+// gap 14: 
+// gap 15: E1.0 E1.1
+// gap 16: E1.2 C1.0 E1.3
+// gap 17: E1.4 C1.1 E1.5
+// gap 18: E1.6 C1.2 E1.7
+// gap 19: E1.8 C1.3 E1.9
+constexpr int FW_MS_START_E1 = 15;
+constexpr unsigned char FW_SCHED_MS[20][3] = {
+    {0x2a, 0xa4, 0x2b},
+    {0x2c, 0xa5, 0x2d},
+    {0x2e, 0xa6, 0x2f},
+    {0xa7, 0xff, 0xff},
+    {0xff, 0xff, 0xff},
+    {0x00, 0x01, 0xff},
+    {0x02, 0x80, 0x03},
+    {0x04, 0x81, 0x05},
+    {0x06, 0x82, 0x07},
+    {0x08, 0x83, 0x09},
+    {0x0a, 0x84, 0x0b},
+    {0x0c, 0x85, 0x0d},
+    {0x0e, 0x86, 0x0f},
+    {0x87, 0xff, 0xff},
+    {0xff, 0xff, 0xff},
+    {0x20, 0x21, 0xff},
+    {0x22, 0xa0, 0x23},
+    {0x24, 0xa1, 0x25},
+    {0x26, 0xa2, 0x27},
+    {0x28, 0xa3, 0x29}};
+#ifndef LCI_FWD_MSUM
+#define LCI_FWD_MSUM 0   // measured slower (12.27 vs 11.81 ms): the 4 extra MFMAs per half cost more than the 32 adds
+#endif
 #ifndef LCI_FWD_HS
 #define LCI_FWD_HS 1
 #endif
@@ -1888,6 +1936,12 @@ __device__ __forceinline__ void hs_st16(unsigned addr, const u32x4& v) {
 // (E1.i in gaps before START_E = 13) see NEG_BIG (exp2 -> 0); the elements exponentiated in the previous half's gaps
 // 13-15 are already "exponentiated": 0. Either way the first half adds and packs zeros for the missing half -1.
 __host__ __device__ constexpr bool fw_wrapped_exp(int i) {
+  if (LCI_FWD_MSUM) {
+    for (int g = 0; g < FW_MS_START_E1; ++g)
+      for (int o = 0; o < 3; ++o)
+        if (FW_SCHED_MS[g][o] == (0x20 | i)) return true;
+    return false;
+  }
   for (int g = 0; g < 13; ++g)
     for (int o = 0; o < 5; ++o)
       if (FW_SCHED[g][o] == (0x20 | i)) return true;
@@ -2098,7 +2152,17 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
   u32x4 pp[2][2];     // [query block][k-step] bf16 P^T packs
   bf16x4 vt[2][2][2][2];   // [set][d block][k-step][half of the fragment] transposed V (keys as the k index)
   bf16x8 kr[4];       // K row fragments (A operands of the chains)
-  float lp[2][4];     // row-sum partials
+  float lp[2][4];     // row-sum partials (VALU adds)
+  f32x16 lsum[2];     // [query block] row sums as MFMA accumulators (LCI_FWD_MSUM): every register = the lane's sum
+  bf16x8 ones8;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones8[j] = to_bf16(1.f);
+  HS_OPAQUE(ones8);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    lsum[i] = f32x16{};
+    if (LCI_FWD_MSUM) HS_TO_AGPR(lsum[i]);
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -2138,7 +2202,26 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
     const int db = k & 1, s2 = k >> 1;
     HS_MFMA_G(o[qb][db], cat44(vt[st][db][s2][0], vt[st][db][s2][1]), __builtin_bit_cast(bf16x8, pp[qb][s2]));
   };
+  auto sum_mfma = [&](int qb, int s2) __attribute__((always_inline)) {
+    HS_MFMA_G(lsum[qb], ones8, __builtin_bit_cast(bf16x8, pp[qb][s2]));
+  };
   auto mfma_gap = [&](int g, int C, const f32x16& i0, const f32x16& i1) __attribute__((always_inline)) {
+    if (LCI_FWD_MSUM) {
+      if (g < 4) {
+        if (g == 0) HS_MFMA_C0(S[0], kr[0], qf[0][0], i0); else HS_MFMA_C(S[0], kr[g], qf[0][g]);
+      } else if (g < 8) {
+        pv_mfma(g - 4, 1, C ^ 1);
+      } else if (g < 10) {
+        sum_mfma(1, g - 8);
+      } else if (g < 14) {
+        if (g == 10) HS_MFMA_C0(S[1], kr[0], qf[1][0], i1); else HS_MFMA_C(S[1], kr[g - 10], qf[1][g - 10]);
+      } else if (g < 18) {
+        pv_mfma(g - 14, 0, C);
+      } else {
+        sum_mfma(0, g - 18);
+      }
+      return;
+    }
     if (g < 4) {
       if (g == 0) HS_MFMA_C0(S[0], kr[0], qf[0][0], i0); else HS_MFMA_C(S[0], kr[g], qf[0][g]);
     } else if (g < 8) {
@@ -2155,19 +2238,28 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
   auto half = [&](auto SET, int soff, int r0i, int nsoff, int nr0i, const f32x16& i0, const f32x16& i1, auto hook)
       __attribute__((always_inline)) {
     constexpr int C = decltype(SET)::value;
+    constexpr int NG = LCI_FWD_MSUM ? 20 : 16;
 #pragma unroll
-    for (int g = 0; g < 16; ++g) {
+    for (int g = 0; g < NG; ++g) {
       mfma_gap(g, C, i0, i1);
       if (g == 2) HS_KEEP(i0);    // the chain-start MFMAs read their initial accumulators as SrcC after issue
-      if (g == 10) HS_KEEP(i1);
+      if (g == (LCI_FWD_MSUM ? 12 : 10)) HS_KEEP(i1);
+      // the gaps after a chain's last MFMA carry no VALU in FW_SCHED_MS: pad them so the chain's result is written
+      // back before the first exp two gaps later (MFMA -> VALU read, 12 wait states, tools/isa_hazards.py)
+      if (LCI_FWD_MSUM && (g == 4 || g == 14)) asm volatile("s_nop 7" ::: "memory");
+      if (LCI_FWD_MSUM) {
 #pragma unroll
-      for (int op = 0; op < 5; ++op) valu_op(FW_SCHED[g][op], -1);
+        for (int op = 0; op < 3; ++op) valu_op(FW_SCHED_MS[g][op], -1);
+      } else {
+#pragma unroll
+        for (int op = 0; op < 5; ++op) valu_op(FW_SCHED[g][op], -1);
+      }
       if (LCI_FWD_PROBE == 1) {   // timing probe (wrong results): no LDS reads in the loop
       } else if (g < 8) {
         const int f = g >> 1, part = g & 1;   // fragment f = (d block f & 1, k-step f >> 1)
         vt[C][f & 1][f >> 1][part] = trh(soff, r0i, f, part);
-      } else if (g >= 12) {
-        kr[g - 12] = row(nsoff, nr0i, g - 12);
+      } else if (g >= NG - 4) {   // the next half's K rows (the block-1 chain reads this half's until gap NG - 7)
+        kr[g - (NG - 4)] = row(nsoff, nr0i, g - (NG - 4));
       }
       hook(g);
     }
@@ -2207,7 +2299,7 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
     constexpr int sl = decltype(SL)::value;
     const int soff = sl >= 0 ? sl * SLOT_B : (t & (NSLOT - 1)) * SLOT_B;
     const int nsoff = sl >= 0 ? ((sl + 1) & (NSLOT - 1)) * SLOT_B : ((t + 1) & (NSLOT - 1)) * SLOT_B;
-    // tile t+1 is published at gap 6 of half 1 (first reader: the K rows at gaps 12-15); tile t+3's DMA goes into the
+    // tile t+1 is published at gap 6 of half 1 (first reader: the K rows at gaps 12-15, 16-19 with MSUM); tile t+3's DMA goes into the
     // slot of tile t-1 (last read by half 1 of tile t-1, before this barrier), one operation per two gaps
     auto stage = [&](int g) __attribute__((always_inline)) {
       if (t + 1 < nkt && g == 6) {
@@ -2266,14 +2358,27 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
     tile(ICR{}, tl, M[0][0], M[0][1], M[1][0], M[1][1]);
   }
   if (LCI_FWD_RSTG) hs_vmcnt<0>();   // the last tiles' staging loads (past the end: zeros) retire before the exit
-  // query block 1 of the last half: its wrapped VALU (gaps 0-5) and its PV MFMAs
+  // query block 1 of the last half: its wrapped VALU and its PV (+ row-sum) MFMAs
+  if (LCI_FWD_MSUM) {
 #pragma unroll
-  for (int g = 0; g < 8; ++g) {
+    for (int g = 0; g < 10; ++g) {
 #pragma unroll
-    for (int op = 0; op < 5; ++op) valu_op(FW_SCHED[g][op], 1);
-    if (g >= 4) {
-      asm volatile("s_nop 1" ::: "memory");
-      pv_mfma(g - 4, 1, 1);   // the last half is a half 1
+      for (int op = 0; op < 3; ++op) valu_op(FW_SCHED_MS[g][op], 1);
+      if (g >= 4) {
+        asm volatile("s_nop 1" ::: "memory");
+        if (g < 8) pv_mfma(g - 4, 1, 1);   // the last half is a half 1
+        else sum_mfma(1, g - 8);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+#pragma unroll
+      for (int op = 0; op < 5; ++op) valu_op(FW_SCHED[g][op], 1);
+      if (g >= 4) {
+        asm volatile("s_nop 1" ::: "memory");
+        pv_mfma(g - 4, 1, 1);   // the last half is a half 1
+      }
     }
   }
   asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
@@ -2281,7 +2386,7 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
     const int q = qw0 + 32 * qb + r32;
-    const float lt = wave_sum_xor32((lp[qb][0] + lp[qb][1]) + (lp[qb][2] + lp[qb][3]));
+    const float lt = LCI_FWD_MSUM ? lsum[qb][0] : wave_sum_xor32((lp[qb][0] + lp[qb][1]) + (lp[qb][2] + lp[qb][3]));
     if (q < L) {
       const float inv = 1.f / lt;
       bf16* op = a.out + b * a.bs_out + (long long)q * a.rs_out + hh * a.hs;
