@@ -702,8 +702,10 @@ __device__ __forceinline__ void col_fft_waves(f32x2* x, int ld, const f32x2* twl
   }
 }
 
-// grid (n2 / GW, npairs_total or C); block NT. Same math as fft_col_fwd_kernel.
-template <int GW, int CW, int NT>
+// grid (n2 / GW / GP, npairs_total or C); block NT. Same math as fft_col_fwd_kernel. GP > 1 (wave FFT path, 16-B
+// rows): the workgroup takes GP consecutive column groups and loads group i+1's rows into registers while group i's
+// FFT and stores run (the load, FFT and store phases otherwise serialise: one 141-KB workgroup per CU at n1 = 1024).
+template <int GW, int CW, int NT, int GP = 1>
 __global__ __launch_bounds__(NT) void fft_colw_fwd_kernel(FftArgs a) {
   extern __shared__ __attribute__((aligned(16))) f32x2 lds[];
   const int ld = a.n1 + 1;
@@ -722,6 +724,48 @@ __global__ __launch_bounds__(NT) void fft_colw_fwd_kernel(FftArgs a) {
   }
   const float* s0 = a.src + (long long)r0 * a.L;
   const float* s1 = r1 >= 0 ? a.src + (long long)r1 * a.L : nullptr;
+  if constexpr (GP > 1) {
+    static_assert(col_wave_path(CW / GW, GW) && (CW / 4) % NT == 0, "prefetching column groups: wave FFT path");
+    constexpr int PERT = CW / 4 / NT;   // 16-B chunks per thread and group
+    f32x4 v0[PERT], v1[PERT];
+    auto gload = [&](int cg) __attribute__((always_inline)) {
+#pragma unroll
+      for (int u = 0; u < PERT; ++u) {
+        const int idx = u * NT + threadIdx.x;
+        const int m = (idx / (GW / 4)) * a.n2 + cg + (idx % (GW / 4)) * 4;
+        v0[u] = v1[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (m < a.L) {
+          v0[u] = *(const f32x4*)(s0 + m);
+          if (s1) v1[u] = *(const f32x4*)(s1 + m);
+        }
+      }
+    };
+    f32x2* S = (a.single ? a.SK : a.S) + (long long)pid * a.n;
+    gload(blockIdx.x * GP * GW);
+    for (int it = 0; it < GP; ++it) {
+      const int cg = (blockIdx.x * GP + it) * GW;
+#pragma unroll
+      for (int u = 0; u < PERT; ++u) {
+        const int idx = u * NT + threadIdx.x;
+        const int g = (idx % (GW / 4)) * 4, ai = idx / (GW / 4);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[(g + q) * ld + ai] = f32x2{v0[u][q], v1[u][q]};
+      }
+      if (it + 1 < GP) gload(cg + GW);   // in flight during this group's FFT and stores
+      __syncthreads();
+      col_fft_waves<false, GW, CW, NT>(x, ld, twl, twl + a.n1 + tw3_entries(a.ln1 + a.ln2));
+      __syncthreads();
+      for (int idx = threadIdx.x; idx < CW / 2; idx += NT) {
+        const int g = (idx % (GW / 2)) * 2, k1 = idx / (GW / 2);
+        const long long e = (long long)(cg + g) * k1;
+        const f32x2 p0 = cmul(x[g * ld + k1], tw3(tw3t, e & (a.n - 1)));
+        const f32x2 p1 = cmul(x[(g + 1) * ld + k1], tw3(tw3t, (e + k1) & (a.n - 1)));
+        *(f32x4*)(S + (long long)k1 * a.n2 + cg + g) = f32x4{p0.x, p0.y, p1.x, p1.y};
+      }
+      if (it + 1 < GP) __syncthreads();   // the store loop's LDS reads precede the next group's writes
+    }
+    return;
+  }
   if ((a.L & 3) == 0) {   // 16-byte loads of 4 adjacent columns (rows are 16-B aligned, chunks all in or out)
     constexpr int NQ = CW / 4;
     for (int base = 0; base < NQ; base += UB * NT) {
@@ -786,8 +830,9 @@ __global__ __launch_bounds__(NT) void fft_colw_fwd_kernel(FftArgs a) {
   }
 }
 
-// grid (n2 / GW, npairs_total or C); same math as fft_col_inv_kernel.
-template <int GW, int CW, int NT>
+// grid (n2 / GW / GP, npairs_total or C); same math as fft_col_inv_kernel. GP > 1: as fft_colw_fwd_kernel, the next
+// column group's spectrum rows are loaded into registers during this group's FFT and output pass.
+template <int GW, int CW, int NT, int GP = 1>
 __global__ __launch_bounds__(NT) void fft_colw_inv_kernel(FftArgs a) {
   extern __shared__ __attribute__((aligned(16))) f32x2 lds[];
   const int ld = a.n1 + 1;
@@ -795,11 +840,121 @@ __global__ __launch_bounds__(NT) void fft_colw_inv_kernel(FftArgs a) {
   f32x2* twl = x + GW * ld;
   load_twl(twl, a.tw, a.n1, a.n);
   const Tw3 tw3t = load_tw3(twl + a.n1, a.tw, a.ln1 + a.ln2);
-  const int c0 = blockIdx.x * GW;
   const int pid = a.pid0 + blockIdx.y;
   const f32x2* S = (a.single ? a.SK : a.S) + (long long)pid * a.n;
   __syncthreads();   // the twiddle tables are read below
   constexpr int NH = CW / 2;   // 16-byte loads of 2 adjacent columns
+  // output of column group c0 (after its inverse column FFTs): rows (+ D * src) or the filter gradient
+  auto emit = [&](int c0) __attribute__((always_inline)) {
+    // only a < ceil(L / n2) rows of the column carry outputs (m < L); the rest is the discarded wrap half
+    const int na = (a.L - c0 + a.n2 - 1) / a.n2;
+    if (a.single) {
+      for (int idx = threadIdx.x; idx < GW * na; idx += NT) {
+        const int g = idx % GW, ai = idx / GW;
+        const int m = ai * a.n2 + c0 + g;
+        if (m < a.L) a.dk[(long long)pid * a.L + m] = x[g * ld + ai].x;
+      }
+      return;
+    }
+    const int j = pid / a.P, p = pid % a.P;
+    const int r0 = pair_row(a, j, p, 0), r1 = pair_row(a, j, p, 1);
+    const float Dj = a.Dv ? a.Dv[j] : 0.f;
+    const float* s0 = a.src + (long long)r0 * a.L;
+    const float* s1 = r1 >= 0 ? a.src + (long long)r1 * a.L : nullptr;
+    float* d0 = a.dst + (long long)r0 * a.L;
+    float* d1 = r1 >= 0 ? a.dst + (long long)r1 * a.L : nullptr;
+    if ((a.L & 3) == 0) {   // 16-byte loads / stores of 4 adjacent columns
+      const int totq = (GW / 4) * na;
+      for (int base = 0; base < totq; base += UB * NT) {
+        f32x4 u0[UB], u1[UB];
+  #pragma unroll
+        for (int u = 0; u < UB; ++u) {
+          const int idx = base + u * NT + threadIdx.x;
+          const int m = (idx / (GW / 4)) * a.n2 + c0 + (idx % (GW / 4)) * 4;
+          u0[u] = u1[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (idx < totq && m < a.L && a.Dv) {
+            u0[u] = *(const f32x4*)(s0 + m);
+            if (s1) u1[u] = *(const f32x4*)(s1 + m);
+          }
+        }
+  #pragma unroll
+        for (int u = 0; u < UB; ++u) {
+          const int idx = base + u * NT + threadIdx.x;
+          const int g = (idx % (GW / 4)) * 4, ai = idx / (GW / 4);
+          const int m = ai * a.n2 + c0 + g;
+          if (idx < totq && m < a.L) {
+            f32x4 o0, o1;
+  #pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const f32x2 v = x[(g + q) * ld + ai];
+              o0[q] = fmaf(Dj, u0[u][q], v.x);
+              o1[q] = fmaf(Dj, u1[u][q], v.y);
+            }
+            *(f32x4*)(d0 + m) = o0;
+            if (d1) *(f32x4*)(d1 + m) = o1;
+          }
+        }
+      }
+      return;
+    }
+    const int total = GW * na;
+    for (int base = 0; base < total; base += UB * NT) {
+      float u0[UB], u1[UB];
+  #pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const int idx = base + u * NT + threadIdx.x;
+        const int m = (idx / GW) * a.n2 + c0 + idx % GW;
+        u0[u] = u1[u] = 0.f;
+        if (idx < total && m < a.L) {
+          u0[u] = s0[m];
+          if (s1) u1[u] = s1[m];
+        }
+      }
+  #pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const int idx = base + u * NT + threadIdx.x;
+        const int g = idx % GW, ai = idx / GW;
+        const int m = ai * a.n2 + c0 + g;
+        if (idx < total && m < a.L) {
+          const f32x2 v = x[g * ld + ai];
+          d0[m] = fmaf(Dj, u0[u], v.x);
+          if (d1) d1[m] = fmaf(Dj, u1[u], v.y);
+        }
+      }
+    }
+  };
+  if constexpr (GP > 1) {
+    static_assert(col_wave_path(CW / GW, GW) && NH % NT == 0, "prefetching column groups: wave FFT path");
+    constexpr int PERT = NH / NT;
+    f32x4 v[PERT];
+    auto sload = [&](int cg) __attribute__((always_inline)) {
+#pragma unroll
+      for (int u = 0; u < PERT; ++u) {
+        const int idx = u * NT + threadIdx.x;
+        v[u] = *(const f32x4*)(S + (long long)(idx / (GW / 2)) * a.n2 + cg + (idx % (GW / 2)) * 2);
+      }
+    };
+    sload(blockIdx.x * GP * GW);
+    for (int it = 0; it < GP; ++it) {
+      const int cg = (blockIdx.x * GP + it) * GW;
+#pragma unroll
+      for (int u = 0; u < PERT; ++u) {
+        const int idx = u * NT + threadIdx.x;
+        const int g = (idx % (GW / 2)) * 2, k1 = idx / (GW / 2);
+        const long long e = (long long)(cg + g) * k1;
+        x[g * ld + k1] = cmulc(f32x2{v[u][0], v[u][1]}, tw3(tw3t, e & (a.n - 1)));
+        x[(g + 1) * ld + k1] = cmulc(f32x2{v[u][2], v[u][3]}, tw3(tw3t, (e + k1) & (a.n - 1)));
+      }
+      if (it + 1 < GP) sload(cg + GW);   // in flight during this group's FFT and output pass
+      __syncthreads();
+      col_fft_waves<true, GW, CW, NT>(x, ld, twl, twl + a.n1 + tw3_entries(a.ln1 + a.ln2));
+      __syncthreads();
+      emit(cg);
+      if (it + 1 < GP) __syncthreads();
+    }
+    return;
+  }
+  const int c0 = blockIdx.x * GW;
   for (int base = 0; base < NH; base += UB * NT) {
     f32x4 v[UB];
 #pragma unroll
@@ -827,82 +982,7 @@ __global__ __launch_bounds__(NT) void fft_colw_inv_kernel(FftArgs a) {
     static_assert(NT == 256, "the LDS Stockham passes assume 256 threads");
     lds_fft_inplace<true, CW>(x, a.n1, a.ln1, twl, ld);
   }
-  // only a < ceil(L / n2) rows of the column carry outputs (m < L); the rest is the discarded wrap half
-  const int na = (a.L - c0 + a.n2 - 1) / a.n2;
-  if (a.single) {
-    for (int idx = threadIdx.x; idx < GW * na; idx += NT) {
-      const int g = idx % GW, ai = idx / GW;
-      const int m = ai * a.n2 + c0 + g;
-      if (m < a.L) a.dk[(long long)pid * a.L + m] = x[g * ld + ai].x;
-    }
-    return;
-  }
-  const int j = pid / a.P, p = pid % a.P;
-  const int r0 = pair_row(a, j, p, 0), r1 = pair_row(a, j, p, 1);
-  const float Dj = a.Dv ? a.Dv[j] : 0.f;
-  const float* s0 = a.src + (long long)r0 * a.L;
-  const float* s1 = r1 >= 0 ? a.src + (long long)r1 * a.L : nullptr;
-  float* d0 = a.dst + (long long)r0 * a.L;
-  float* d1 = r1 >= 0 ? a.dst + (long long)r1 * a.L : nullptr;
-  if ((a.L & 3) == 0) {   // 16-byte loads / stores of 4 adjacent columns
-    const int totq = (GW / 4) * na;
-    for (int base = 0; base < totq; base += UB * NT) {
-      f32x4 u0[UB], u1[UB];
-#pragma unroll
-      for (int u = 0; u < UB; ++u) {
-        const int idx = base + u * NT + threadIdx.x;
-        const int m = (idx / (GW / 4)) * a.n2 + c0 + (idx % (GW / 4)) * 4;
-        u0[u] = u1[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (idx < totq && m < a.L && a.Dv) {
-          u0[u] = *(const f32x4*)(s0 + m);
-          if (s1) u1[u] = *(const f32x4*)(s1 + m);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < UB; ++u) {
-        const int idx = base + u * NT + threadIdx.x;
-        const int g = (idx % (GW / 4)) * 4, ai = idx / (GW / 4);
-        const int m = ai * a.n2 + c0 + g;
-        if (idx < totq && m < a.L) {
-          f32x4 o0, o1;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const f32x2 v = x[(g + q) * ld + ai];
-            o0[q] = fmaf(Dj, u0[u][q], v.x);
-            o1[q] = fmaf(Dj, u1[u][q], v.y);
-          }
-          *(f32x4*)(d0 + m) = o0;
-          if (d1) *(f32x4*)(d1 + m) = o1;
-        }
-      }
-    }
-    return;
-  }
-  const int total = GW * na;
-  for (int base = 0; base < total; base += UB * NT) {
-    float u0[UB], u1[UB];
-#pragma unroll
-    for (int u = 0; u < UB; ++u) {
-      const int idx = base + u * NT + threadIdx.x;
-      const int m = (idx / GW) * a.n2 + c0 + idx % GW;
-      u0[u] = u1[u] = 0.f;
-      if (idx < total && m < a.L) {
-        u0[u] = s0[m];
-        if (s1) u1[u] = s1[m];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < UB; ++u) {
-      const int idx = base + u * NT + threadIdx.x;
-      const int g = idx % GW, ai = idx / GW;
-      const int m = ai * a.n2 + c0 + g;
-      if (idx < total && m < a.L) {
-        const f32x2 v = x[g * ld + ai];
-        d0[m] = fmaf(Dj, u0[u], v.x);
-        if (d1) d1[m] = fmaf(Dj, u1[u], v.y);
-      }
-    }
-  }
+  emit(c0);
 }
 
 // dD[j] += sum_rows sum_t a[row][t] * b[row][t] over rows of filter j (block partial + one atomic per block).
@@ -1698,7 +1778,19 @@ static int launch_col(FftArgs& a, bool inv, int nblk_y, hipStream_t s) {
     if (inv) hipLaunchKernelGGL((fft_colw_inv_kernel<GW, CW, NT>), grid, dim3(NT), sh, s, a);                    \
     else hipLaunchKernelGGL((fft_colw_fwd_kernel<GW, CW, NT>), grid, dim3(NT), sh, s, a);
     if (cw == 16384) {
-      if (gw == 16) { LCI_COLW(16, 16384, 512) } else return 1;
+      static const int gp_env = getenv("LCI_FFT_GP") ? atoi(getenv("LCI_FFT_GP")) : 4;
+      if (gw != 16) return 1;
+      if (!inv && gp_env == 4 && (a.L & 3) == 0 && (a.n2 / gw) % 4 == 0) {
+        (void)hipFuncSetAttribute((const void*)fft_colw_fwd_kernel<16, 16384, 512, 4>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipLaunchKernelGGL((fft_colw_fwd_kernel<16, 16384, 512, 4>), dim3(a.n2 / gw / 4, nblk_y), dim3(512), sh, s, a);
+      } else if (inv && getenv("LCI_FFT_GP_INV") && (a.n2 / gw) % 4 == 0) {   // measured slower (7.2 vs 6.6 ms)
+        (void)hipFuncSetAttribute((const void*)fft_colw_inv_kernel<16, 16384, 512, 4>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipLaunchKernelGGL((fft_colw_inv_kernel<16, 16384, 512, 4>), dim3(a.n2 / gw / 4, nblk_y), dim3(512), sh, s, a);
+      } else {
+        LCI_COLW(16, 16384, 512)
+      }
     } else if (cw == 8192) {
       if (gw == 32 && a.n1 == 256 && LCI_FFT_WAVE) { LCI_COLW(32, 8192, 512) }
       else if (gw == 32) { LCI_COLW(32, 8192, 256) } else if (gw == 16) { LCI_COLW(16, 8192, 256) }
