@@ -336,6 +336,9 @@ __device__ __forceinline__ void fft512_wave(f32x2 (&v)[8], f32x2* buf, const f32
 }
 
 // grid (n1, filters of the chunk); block 64 * nw (waves split the filter's pairs). Same math as fft_row_kernel.
+#ifndef LCI_FFT_ROW_PF
+#define LCI_FFT_ROW_PF 0   // next-pair prefetch in the row pass: measured neutral (profiles/r04_fft_ab.txt r4row)
+#endif
 __global__ __launch_bounds__(256) void fft_row512_kernel(FftArgs a) {
   __shared__ f32x2 twl[512];
   __shared__ f32x2 wbuf[4][8 * R5_S1];
@@ -364,13 +367,30 @@ __global__ __launch_bounds__(256) void fft_row512_kernel(FftArgs a) {
   f32x2 acc[8];
 #pragma unroll
   for (int r = 0; r < 8; ++r) acc[r] = f32x2{0.f, 0.f};
+  // the wave's next pair is loaded while this one is transformed (LCI_FFT_ROW_PF)
+  f32x2 nv[8], nv2[8];
+  auto ldp = [&](int p) __attribute__((always_inline)) {
+    const long long off = ((long long)j * a.P + p) * a.n + row;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      nv[r] = a.S[off + 64 * r];
+      if (two) nv2[r] = a.S2[off + 64 * r];
+    }
+  };
+  if (LCI_FFT_ROW_PF && w < a.P) ldp(w);
   for (int p = w; p < a.P; p += nw) {
     const long long off = ((long long)j * a.P + p) * a.n + row;
     f32x2 v[8], v2[8];
+    if (LCI_FFT_ROW_PF) {
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      v[r] = a.S[off + 64 * r];
-      if (two) v2[r] = a.S2[off + 64 * r];
+      for (int r = 0; r < 8; ++r) { v[r] = nv[r]; v2[r] = nv2[r]; }
+      if (p + nw < a.P) ldp(p + nw);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        v[r] = a.S[off + 64 * r];
+        if (two) v2[r] = a.S2[off + 64 * r];
+      }
     }
     fft512_wave<false>(v, buf, twl, L);
     if (two) {
@@ -1815,8 +1835,9 @@ static int launch_col(FftArgs& a, bool inv, int nblk_y, hipStream_t s) {
 
 static int launch_row(FftArgs& a, int nfilt, hipStream_t s) {
   if (a.n2 == 512 && !getenv("LCI_FFT_ROW_V1")) {
-    int nw = 1;   // waves per workgroup: the largest divisor of the pair count up to 4 (balanced waves)
-    for (int q = 4; q >= 1; --q)
+    static const int nw_max = getenv("LCI_FFT_ROW_NW") ? std::max(1, std::min(4, atoi(getenv("LCI_FFT_ROW_NW")))) : 4;
+    int nw = 1;   // waves per workgroup: the largest divisor of the pair count up to nw_max (balanced waves)
+    for (int q = nw_max; q >= 1; --q)
       if (a.P % q == 0) { nw = q; break; }
     if (a.mode == 0) nw = 1;
     hipLaunchKernelGGL(fft_row512_kernel, dim3(a.n1, nfilt), dim3(64 * nw), 0, s, a);
