@@ -1547,6 +1547,19 @@ constexpr unsigned char DQ_SCHED[24][4] = {
     {0xa0, 0xa1, 0x64, 0x65},
     {0x66, 0x67, 0xa2, 0xa3}};
 
+#ifndef LCI_DQ_RSTG
+#define LCI_DQ_RSTG 1     // dQ K / V staging: buffer loads into AGPRs + ds_write_b128 (0: LDS-DMA)
+#endif
+#ifndef LCI_FWD_RSTG
+#define LCI_FWD_RSTG 1    // K / V staging in the loop: 1 = buffer loads into AGPRs + ds_write_b128, 0 = LDS-DMA
+#endif
+// 16-byte LDS store of an AGPR quad at a lane address + immediate (asm: the compiler neither reorders it nor needs a
+// VGPR copy of the data; completion is implied by the compiler's in-order lgkmcnt waits for later reads)
+template <int OFF>
+__device__ __forceinline__ void hs_st16(unsigned addr, const u32x4& v) {
+  asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(addr), "a"(v), "i"(OFF) : "memory");
+}
+
 #ifndef LCI_DQ_AHOME
 #define LCI_DQ_AHOME 1       // Q~ / dO fragments homed in AGPRs before the loop
 #endif
@@ -1732,15 +1745,30 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
     }
   };
 
+  // register staging (LCI_DQ_RSTG, as the forward's LCI_FWD_RSTG): tile t+1's pieces (loaded into AGPRs during tile
+  // t-1) are stored at gaps 1-7 of tile t's half 0, tile t+2's loaded at gaps 9-15; half 1's barrier publishes t+1
+  u32x4 stg[4];
+  const unsigned wst = lds0 + 2048 * wave + 16 * lane;
+  auto ld_piece = [&](int t, int i) __attribute__((always_inline)) {
+    if (i == 0) stg[0] = hs_ld16(rk, dk0, t * KT * rs2k);
+    if (i == 1) stg[1] = hs_ld16(rk, dk1, t * KT * rs2k);
+    if (i == 2) stg[2] = hs_ld16(rv, dv0, t * KT * rs2v);
+    if (i == 3) stg[3] = hs_ld16(rv, dv1, t * KT * rs2v);
+  };
   // prologue: tiles 0, 1, 2 in flight; wait for tile 0, publish it; K rows of half 0
   dma_op(0, 0); dma_op(0, 1); dma_op(0, 2); dma_op(0, 3);
-  if (nkt > 1) { dma_op(1, 0); dma_op(1, 1); dma_op(1, 2); dma_op(1, 3); }
-  if (nkt > 2) {   // (spread: tile 2's operations 2-3 at gaps 6 / 18 of tile 0, as for every later tile)
-    dma_op(2, 0); dma_op(2, 1);
-    if (!LCI_DQ_DMASPREAD) { dma_op(2, 2); dma_op(2, 3); }
+  if (LCI_DQ_RSTG) {
+    ld_piece(1, 0); ld_piece(1, 1); ld_piece(1, 2); ld_piece(1, 3);
+    hs_vmcnt<0>();
+  } else {
+    if (nkt > 1) { dma_op(1, 0); dma_op(1, 1); dma_op(1, 2); dma_op(1, 3); }
+    if (nkt > 2) {   // (spread: tile 2's operations 2-3 at gaps 6 / 18 of tile 0, as for every later tile)
+      dma_op(2, 0); dma_op(2, 1);
+      if (!LCI_DQ_DMASPREAD) { dma_op(2, 2); dma_op(2, 3); }
+    }
+    if (nkt > 2) { if (LCI_DQ_DMASPREAD) hs_vmcnt<6>(); else hs_vmcnt<8>(); }
+    else if (nkt > 1) hs_vmcnt<4>(); else hs_vmcnt<0>();
   }
-  if (nkt > 2) { if (LCI_DQ_DMASPREAD) hs_vmcnt<6>(); else hs_vmcnt<8>(); }
-  else if (nkt > 1) hs_vmcnt<4>(); else hs_vmcnt<0>();
   __builtin_amdgcn_s_barrier();
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
@@ -1758,9 +1786,10 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
     // into the slot of tile t-1 (last read by half 1 of tile t-1, before this barrier), one operation per gap
     auto stage = [&](int g) __attribute__((always_inline)) {
       if (t + 1 < nkt && g == 6) {
-        if (t + 2 < nkt) hs_vmcnt<4>(); else hs_vmcnt<0>();
+        if (!LCI_DQ_RSTG) { if (t + 2 < nkt) hs_vmcnt<4>(); else hs_vmcnt<0>(); }
         __builtin_amdgcn_s_barrier();
       }
+      if (LCI_DQ_RSTG) return;
       // tile t+3's operations 0-1 at gaps 8 / 20 of half 1 (after this barrier), 2-3 at gaps 6 / 18 of the next
       // tile's half 0 (before its barrier, whose vmcnt(4) then leaves exactly them in flight): one DMA issue per
       // 12 gaps (each stalls the wave's issue ~60-80 cycles)
@@ -1774,6 +1803,22 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
       }
     };
     auto stage0 = [&](int g) __attribute__((always_inline)) {
+      if (LCI_DQ_RSTG) {
+        if (g == 1) hs_vmcnt<0>();   // tile t+1's pieces (loaded a tile ago)
+        if (g < 8 && (g & 1)) {
+          constexpr int S1 = sl >= 0 ? ((sl + 1) & (NSLOT - 1)) * SLOT_B : 0;
+          const unsigned base = sl >= 0 ? wst : wst + (unsigned)(((t + 1) & (NSLOT - 1)) * SLOT_B);
+          switch (g) {
+            case 1: hs_st16<S1>(base, stg[0]); break;
+            case 3: hs_st16<S1 + 1024>(base, stg[1]); break;
+            case 5: hs_st16<S1 + TILE_B>(base, stg[2]); break;
+            default: hs_st16<S1 + TILE_B + 1024>(base, stg[3]); break;
+          }
+        } else if (g >= 9 && g < 16 && (g & 1)) {
+          ld_piece(t + 2, (g - 9) >> 1);
+        }
+        return;
+      }
       if (LCI_DQ_DMASPREAD && t + 2 < nkt && (g == 6 || g == 18)) dma_op(t + 2, g == 6 ? 2 : 3);
     };
     half(std::integral_constant<int, 0>{}, soff, 0, soff, 1, stage0);
@@ -1789,6 +1834,7 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
     }
     for (; t < nkt; ++t) tile(std::integral_constant<int, -1>{}, t);
   }
+  if (LCI_DQ_RSTG) hs_vmcnt<0>();   // the last tiles' staging loads (past the end: zeros) retire
   // query block 1 of the last half: its remaining VALU (wrapped into gaps 0-5) and its dQ^T
 #pragma unroll
   for (int g = 0; g < 12; ++g) {
@@ -1922,15 +1968,6 @@ constexpr unsigned char FW_SCHED_MS[20][3] = {
                           // 3 / 4 / 5 = no exps / row-sum adds / conversions, 6 = no LDS-DMA in the loop
 #endif
 
-#ifndef LCI_FWD_RSTG
-#define LCI_FWD_RSTG 1    // K / V staging in the loop: 1 = buffer loads into AGPRs + ds_write_b128, 0 = LDS-DMA
-#endif
-// 16-byte LDS store of an AGPR quad at a lane address + immediate (asm: the compiler neither reorders it nor needs a
-// VGPR copy of the data; completion is implied by the compiler's in-order lgkmcnt waits for later reads)
-template <int OFF>
-__device__ __forceinline__ void hs_st16(unsigned addr, const u32x4& v) {
-  asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(addr), "a"(v), "i"(OFF) : "memory");
-}
 
 // initial S^T of query block 1 before the first half: the exps of block 1 that FW_SCHED wraps into the next half
 // (E1.i in gaps before START_E = 13) see NEG_BIG (exp2 -> 0); the elements exponentiated in the previous half's gaps
