@@ -980,6 +980,19 @@ constexpr unsigned LGKM0_WAIT = 0xC07F;
 #ifndef LCI_HS_DMASPREAD
 #define LCI_HS_DMASPREAD 0   // 1: one LDS-DMA issue per segment (21.3 ms vs 20.7 ms for tile t+3's five in seg B
 #endif                       // of half 1, same box)
+#ifndef LCI_HS_RSTG
+#define LCI_HS_RSTG 1     // dK/dV Q / dO / row-constant staging: buffer loads into AGPRs + ds_write (0: LDS-DMA)
+#endif
+// 16- / 4-byte LDS stores of AGPR data at a lane address + immediate (asm: no VGPR copy; completion is implied by the
+// compiler's in-order lgkmcnt waits for later reads)
+template <int OFF>
+__device__ __forceinline__ void hs_st16(unsigned addr, const u32x4& v) {
+  asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(addr), "a"(v), "i"(OFF) : "memory");
+}
+template <int OFF>
+__device__ __forceinline__ void hs_st4(unsigned addr, uint32_t v) {
+  asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(addr), "a"(v), "i"(OFF) : "memory");
+}
 __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArgs a) {
   constexpr int TILE_B = KT * DH * 2;               // bytes of a Q or dO tile (128-B rows)
   // Q | dO of one tile (LCI_HS_TQ: + the d-major Q^T | dO^T tiles, rows = d, read by the dV / dK products)
@@ -1338,8 +1351,27 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
     }
   };
 
+  // register staging (LCI_HS_RSTG, as the forward / dQ): tile t+1's Q / dO pieces and row constants (loaded into
+  // AGPRs during tile t-1) are stored at seg A gaps 1-7 / seg B gap 1 of tile t's half 0, tile t+2's loaded at seg C
+  // gaps 1-7 / seg D gap 1; half 1's barrier publishes tile t+1
+  u32x4 rsq[4];
+  uint32_t rsr = 0;
+  const unsigned wst = lds0 + 2048 * wave + 16 * lane;
+  const unsigned wrc = lds0 + NSLOT * SLOT_B + (wave & 1) * KT * 4 + 4 * lane;   // (past the ring: in the register)
+  auto ld_piece = [&](int t, int i) __attribute__((always_inline)) {
+    if (i == 0) rsq[0] = hs_ld16(rq, dq0, t * KT * rs2q);
+    if (i == 1) rsq[1] = hs_ld16(rq, dq1, t * KT * rs2q);
+    if (i == 2) rsq[2] = hs_ld16(rd, dd0, t * KT * rs2d);
+    if (i == 3) rsq[3] = hs_ld16(rd, dd1, t * KT * rs2d);
+    if (i == 4) rsr = hs_ld4(rr, lane * 4, t * KT * 4);
+  };
+  constexpr bool RSTG = LCI_HS_RSTG && LCI_HS_STG == 0 && !LCI_HS_TQ && LCI_HS_PROBE == 0;
   // prologue: tiles 0, 1, 2 in flight (5 memory operations per wave and tile); wait for tile 0, publish it
-  if constexpr (LCI_HS_STG == 0) {
+  if constexpr (RSTG) {
+    dma_tile(0);
+    ld_piece(1, 0); ld_piece(1, 1); ld_piece(1, 2); ld_piece(1, 3); ld_piece(1, 4);
+    hs_vmcnt<0>();
+  } else if constexpr (LCI_HS_STG == 0) {
     dma_tile(0);
     if (nqt > 1) dma_tile(1);
     // tile 2's operations 3-4 come at segs A / B of tile 0 (the loop has no first-tile special case: a peeled copy
@@ -1389,7 +1421,7 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
     // t-1, which every wave finished before this barrier
     auto stage = [&]() __attribute__((always_inline)) {
       if (t + 1 < nqt) {
-        if (t + 2 < nqt) hs_vmcnt<NOPS>(); else hs_vmcnt<0>();
+        if (!RSTG) { if (t + 2 < nqt) hs_vmcnt<NOPS>(); else hs_vmcnt<0>(); }
         if constexpr (LCI_HS_STG == 1) store_tile(stg[P1], smem + nslot);
         stamp(8);
         // no LDS fence: this wave's reads of the slot tile t+3 overwrites were consumed before now, and the new
@@ -1407,7 +1439,7 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
     // segment doubled it): tile t+3's operations 0-2 in segments B, C, D of half 1 (after this tile's barrier),
     // operations 3-4 in segments A, B of the next tile's half 0 (still before the next barrier, whose vmcnt(5)
     // then leaves exactly them in flight; tile 2's come at tile 0, the prologue issued only its operations 0-2)
-    constexpr bool DMA_ON = LCI_HS_STG == 0 && LCI_HS_PROBE != 2 && LCI_HS_PROBE != 3;
+    constexpr bool DMA_ON = LCI_HS_STG == 0 && LCI_HS_PROBE != 2 && LCI_HS_PROBE != 3 && !RSTG;
     auto dmas1 = [&](int seg, int g) __attribute__((always_inline)) {
       if (LCI_HS_DMASPREAD && !LCI_HS_TQ) {
         if (DMA_ON && g == 3 && seg >= 1 && t + 3 < nqt) dma_op(t + 3, seg - 1);
@@ -1415,6 +1447,28 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
         dma_op(t + 3, g);
       } else if (DMA_ON && LCI_HS_TQ && seg == 2 && g < 4 && t + 3 < nqt) {   // the d-major pieces in seg C
         dma_op(t + 3, 5 + g);
+      }
+    };
+    auto rstg0 = [&](int seg, int g) __attribute__((always_inline)) {
+      if (!(g & 1)) return;
+      if (seg == 0 && g == 1) hs_vmcnt<0>();   // tile t+1's pieces (loaded a tile ago)
+      constexpr int S1 = SLC >= 0 ? ((SLC + 1) & (NSLOT - 1)) * SLOT_B : 0;
+      constexpr int R1 = SLC >= 0 ? ((SLC + 1) & (NSLOT - 1)) * RC_B : 0;
+      const unsigned base = SLC >= 0 ? wst : wst + (unsigned)nslot;
+      const unsigned rbase = SLC >= 0 ? wrc : wrc + (unsigned)nrc;
+      if (seg == 0) {
+        switch (g) {
+          case 1: hs_st16<S1>(base, rsq[0]); break;
+          case 3: hs_st16<S1 + 1024>(base, rsq[1]); break;
+          case 5: hs_st16<S1 + TILE_B>(base, rsq[2]); break;
+          default: hs_st16<S1 + TILE_B + 1024>(base, rsq[3]); break;
+        }
+      } else if (seg == 1 && g == 1) {
+        hs_st4<R1>(rbase, rsr);
+      } else if (seg == 2) {
+        ld_piece(t + 2, g >> 1);
+      } else if (seg == 3 && g == 1) {
+        ld_piece(t + 2, 4);
       }
     };
     auto dmas0 = [&](int seg, int g) __attribute__((always_inline)) {
@@ -1425,7 +1479,8 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
       half_v1(std::integral_constant<int, 0>{}, slot, 0, slot, rc, 32, none, dmas0);    // segs C / D: rows 32-63
       half_v1(std::integral_constant<int, 1>{}, slot, 32, nslot, nrc, 0, stage, dmas1); // ... tile t+1's rows 0-31
     } else {
-      half(std::integral_constant<int, 0>{}, slot, 0, slot, rc, 32, none, dmas0);
+      if constexpr (RSTG) half(std::integral_constant<int, 0>{}, slot, 0, slot, rc, 32, none, rstg0);
+      else half(std::integral_constant<int, 0>{}, slot, 0, slot, rc, 32, none, dmas0);
       half(std::integral_constant<int, 1>{}, slot, 32, nslot, nrc, 0, stage, dmas1);
     }
   };
@@ -1446,6 +1501,7 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
       if (t + 1 < nqt) tile(std::integral_constant<int, 1>{}, std::integral_constant<int, -1>{}, t + 1);
     }
   }
+  if (RSTG) hs_vmcnt<0>();   // the last tiles' staging loads (past the end: zeros) retire
   // key block 1 of the last half: elements 8-15 (finishing 0-7), then its dV / dK
 #pragma unroll
   for (int g = 0; g < 8; ++g) valu_gap(g, 1, 1, 1, 0);
@@ -1553,12 +1609,6 @@ constexpr unsigned char DQ_SCHED[24][4] = {
 #ifndef LCI_FWD_RSTG
 #define LCI_FWD_RSTG 1    // K / V staging in the loop: 1 = buffer loads into AGPRs + ds_write_b128, 0 = LDS-DMA
 #endif
-// 16-byte LDS store of an AGPR quad at a lane address + immediate (asm: the compiler neither reorders it nor needs a
-// VGPR copy of the data; completion is implied by the compiler's in-order lgkmcnt waits for later reads)
-template <int OFF>
-__device__ __forceinline__ void hs_st16(unsigned addr, const u32x4& v) {
-  asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(addr), "a"(v), "i"(OFF) : "memory");
-}
 
 #ifndef LCI_DQ_AHOME
 #define LCI_DQ_AHOME 1       // Q~ / dO fragments homed in AGPRs before the loop
