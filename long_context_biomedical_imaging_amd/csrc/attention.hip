@@ -983,6 +983,9 @@ constexpr unsigned LGKM0_WAIT = 0xC07F;
 #ifndef LCI_HS_RSTG
 #define LCI_HS_RSTG 1     // dK/dV Q / dO / row-constant staging: buffer loads into AGPRs + ds_write (0: LDS-DMA)
 #endif
+#ifndef LCI_HS_RSTG_SEGS
+#define LCI_HS_RSTG_SEGS 2   // half-0 segments of the staging stores (tens) and loads (units)
+#endif
 // 16- / 4-byte LDS stores of AGPR data at a lane address + immediate (asm: no VGPR copy; completion is implied by the
 // compiler's in-order lgkmcnt waits for later reads)
 template <int OFF>
@@ -1451,24 +1454,23 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
     };
     auto rstg0 = [&](int seg, int g) __attribute__((always_inline)) {
       if (!(g & 1)) return;
-      if (seg == 0 && g == 1) hs_vmcnt<0>();   // tile t+1's pieces (loaded a tile ago)
+      constexpr int SS = LCI_HS_RSTG_SEGS / 10, LS = LCI_HS_RSTG_SEGS % 10;   // store / load segments of half 0
+      if (seg == SS && g == 1) hs_vmcnt<0>();   // tile t+1's pieces (loaded a tile ago)
       constexpr int S1 = SLC >= 0 ? ((SLC + 1) & (NSLOT - 1)) * SLOT_B : 0;
       constexpr int R1 = SLC >= 0 ? ((SLC + 1) & (NSLOT - 1)) * RC_B : 0;
       const unsigned base = SLC >= 0 ? wst : wst + (unsigned)nslot;
       const unsigned rbase = SLC >= 0 ? wrc : wrc + (unsigned)nrc;
-      if (seg == 0) {
+      if (seg == SS) {
         switch (g) {
           case 1: hs_st16<S1>(base, rsq[0]); break;
           case 3: hs_st16<S1 + 1024>(base, rsq[1]); break;
           case 5: hs_st16<S1 + TILE_B>(base, rsq[2]); break;
-          default: hs_st16<S1 + TILE_B + 1024>(base, rsq[3]); break;
+          default: hs_st16<S1 + TILE_B + 1024>(base, rsq[3]); hs_st4<R1>(rbase, rsr); break;
         }
-      } else if (seg == 1 && g == 1) {
-        hs_st4<R1>(rbase, rsr);
-      } else if (seg == 2) {
+      }
+      if (seg == LS) {
         ld_piece(t + 2, g >> 1);
-      } else if (seg == 3 && g == 1) {
-        ld_piece(t + 2, 4);
+        if (g == 7) ld_piece(t + 2, 4);
       }
     };
     auto dmas0 = [&](int seg, int g) __attribute__((always_inline)) {
