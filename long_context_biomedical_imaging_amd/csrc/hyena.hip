@@ -865,6 +865,8 @@ __global__ __launch_bounds__(NT) void fft_colw_inv_kernel(FftArgs a) {
   __syncthreads();   // the twiddle tables are read below
   constexpr int NH = CW / 2;   // 16-byte loads of 2 adjacent columns
   // output of column group c0 (after its inverse column FFTs): rows (+ D * src) or the filter gradient
+  // (with a prefetched group in registers, the output pass keeps fewer of its own loads in flight: no spills)
+  constexpr int UBE = GP > 1 ? 2 : UB;
   auto emit = [&](int c0) __attribute__((always_inline)) {
     // only a < ceil(L / n2) rows of the column carry outputs (m < L); the rest is the discarded wrap half
     const int na = (a.L - c0 + a.n2 - 1) / a.n2;
@@ -885,10 +887,10 @@ __global__ __launch_bounds__(NT) void fft_colw_inv_kernel(FftArgs a) {
     float* d1 = r1 >= 0 ? a.dst + (long long)r1 * a.L : nullptr;
     if ((a.L & 3) == 0) {   // 16-byte loads / stores of 4 adjacent columns
       const int totq = (GW / 4) * na;
-      for (int base = 0; base < totq; base += UB * NT) {
-        f32x4 u0[UB], u1[UB];
+      for (int base = 0; base < totq; base += UBE * NT) {
+        f32x4 u0[UBE], u1[UBE];
   #pragma unroll
-        for (int u = 0; u < UB; ++u) {
+        for (int u = 0; u < UBE; ++u) {
           const int idx = base + u * NT + threadIdx.x;
           const int m = (idx / (GW / 4)) * a.n2 + c0 + (idx % (GW / 4)) * 4;
           u0[u] = u1[u] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -898,7 +900,7 @@ __global__ __launch_bounds__(NT) void fft_colw_inv_kernel(FftArgs a) {
           }
         }
   #pragma unroll
-        for (int u = 0; u < UB; ++u) {
+        for (int u = 0; u < UBE; ++u) {
           const int idx = base + u * NT + threadIdx.x;
           const int g = (idx % (GW / 4)) * 4, ai = idx / (GW / 4);
           const int m = ai * a.n2 + c0 + g;
@@ -918,10 +920,10 @@ __global__ __launch_bounds__(NT) void fft_colw_inv_kernel(FftArgs a) {
       return;
     }
     const int total = GW * na;
-    for (int base = 0; base < total; base += UB * NT) {
-      float u0[UB], u1[UB];
+    for (int base = 0; base < total; base += UBE * NT) {
+      float u0[UBE], u1[UBE];
   #pragma unroll
-      for (int u = 0; u < UB; ++u) {
+      for (int u = 0; u < UBE; ++u) {
         const int idx = base + u * NT + threadIdx.x;
         const int m = (idx / GW) * a.n2 + c0 + idx % GW;
         u0[u] = u1[u] = 0.f;
@@ -931,7 +933,7 @@ __global__ __launch_bounds__(NT) void fft_colw_inv_kernel(FftArgs a) {
         }
       }
   #pragma unroll
-      for (int u = 0; u < UB; ++u) {
+      for (int u = 0; u < UBE; ++u) {
         const int idx = base + u * NT + threadIdx.x;
         const int g = idx % GW, ai = idx / GW;
         const int m = ai * a.n2 + c0 + g;
@@ -1804,7 +1806,8 @@ static int launch_col(FftArgs& a, bool inv, int nblk_y, hipStream_t s) {
         (void)hipFuncSetAttribute((const void*)fft_colw_fwd_kernel<16, 16384, 512, 4>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         hipLaunchKernelGGL((fft_colw_fwd_kernel<16, 16384, 512, 4>), dim3(a.n2 / gw / 4, nblk_y), dim3(512), sh, s, a);
-      } else if (inv && getenv("LCI_FFT_GP_INV") && (a.n2 / gw) % 4 == 0) {   // measured slower (7.2 vs 6.6 ms)
+      } else if (inv && gp_env == 4 && !(getenv("LCI_FFT_GP_INV") && atoi(getenv("LCI_FFT_GP_INV")) == 0) &&
+                 (a.n2 / gw) % 4 == 0) {
         (void)hipFuncSetAttribute((const void*)fft_colw_inv_kernel<16, 16384, 512, 4>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         hipLaunchKernelGGL((fft_colw_inv_kernel<16, 16384, 512, 4>), dim3(a.n2 / gw / 4, nblk_y), dim3(512), sh, s, a);
