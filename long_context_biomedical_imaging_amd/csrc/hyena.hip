@@ -1819,7 +1819,19 @@ static int launch_col(FftArgs& a, bool inv, int nblk_y, hipStream_t s) {
       else if (gw == 32) { LCI_COLW(32, 8192, 256) } else if (gw == 16) { LCI_COLW(16, 8192, 256) }
       else if (gw == 8) { LCI_COLW(8, 8192, 256) } else return 1;
     } else {
-      if (gw == 16) { LCI_COLW(16, 4096, 256) } else if (gw == 8) { LCI_COLW(8, 4096, 256) }
+      static const int gp4 = getenv("LCI_FFT_GP") ? atoi(getenv("LCI_FFT_GP")) : 4;
+      if (gw == 16 && gp4 == 4 && LCI_FFT_WAVE && a.n1 == 256 && (a.n2 / gw) % 4 == 0 && (inv || (a.L & 3) == 0)) {
+        // the column-group prefetch at n1 = 256 as well (LCI_FFT_GP)
+        if (inv) {
+          (void)hipFuncSetAttribute((const void*)fft_colw_inv_kernel<16, 4096, 256, 4>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+          hipLaunchKernelGGL((fft_colw_inv_kernel<16, 4096, 256, 4>), dim3(a.n2 / gw / 4, nblk_y), dim3(256), sh, s, a);
+        } else {
+          (void)hipFuncSetAttribute((const void*)fft_colw_fwd_kernel<16, 4096, 256, 4>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+          hipLaunchKernelGGL((fft_colw_fwd_kernel<16, 4096, 256, 4>), dim3(a.n2 / gw / 4, nblk_y), dim3(256), sh, s, a);
+        }
+      } else if (gw == 16) { LCI_COLW(16, 4096, 256) } else if (gw == 8) { LCI_COLW(8, 4096, 256) }
       else if (gw == 4) { LCI_COLW(4, 4096, 256) } else return 1;
     }
 #undef LCI_COLW
