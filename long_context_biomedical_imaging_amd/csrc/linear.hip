@@ -60,6 +60,18 @@ __device__ __forceinline__ void wait_vmcnt() {   // s_waitcnt vmcnt(N), expcnt /
   __builtin_amdgcn_sched_barrier(0);
 }
 
+#ifndef LCI_LW_RSTG
+#define LCI_LW_RSTG 0   // slab staging: 1 = global loads into AGPRs + ds_write_b128 one slab ahead, 0 = LDS-DMA ring
+#endif
+// 16-B global load into an AGPR quad / LDS store from one (asm: no VGPR copies, no compiler vmcnt waits)
+__device__ __forceinline__ u32x4 lw_gld16(const void* p) {
+  u32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=a"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ void lw_dsw16(unsigned addr, const u32x4& v) {
+  asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "a"(v) : "memory");
+}
 // Slabs of R token rows arrive by LDS-DMA (global_load_lds_dwordx4: lane l of a wave-instruction writes bytes
 // 16 l .. 16 l + 15 of a 1-KB unit = 16 rows x 64 B of one 32-column block) into a ring of NBUF LDS buffers,
 // NBUF - 1 slabs ahead: no staging registers, no ds_write pass; each wave waits (counted vmcnt) only for its own
@@ -159,14 +171,48 @@ __global__ __launch_bounds__(64 * WN * WC, 1) void linear_wgrad_kernel(LinWgradA
 #pragma unroll
   for (int j = 0; j < 8; ++j) bsum[j] = 0.f;
 
+  // register staging (RSTG): slab s+2's units are loaded into AGPRs during slab s and stored to its ring slot
+  // after slab s+1's barrier (the DMA issue stalls a wave ~60 cycles per 1-KB unit, 8 units per wave and slab here)
+  // (the 6-wave 64 x 128 tile spills with the staging registers: it keeps the DMA ring)
+  constexpr bool RSTG = LCI_LW_RSTG && !(MB == 2 && CB == 4 && WN == 2 && WC == 3);
+  u32x4 st[UPW];
+  auto gload = [&](int slab) __attribute__((always_inline)) {
+    const long long m0 = ms + (long long)slab * R;
+    const bool full = m0 + R <= me;
 #pragma unroll
-  for (int p = 0; p < NBUF - 1; ++p)
-    if (p < nslab) issue(p);
+    for (int t = 0; t < UPW; ++t) {
+      if (t < nunits) st[t] = lw_gld16(full || m0 + urow[t] < me ? (const void*)uptr[t] : (const void*)(kLwZero + 8 * lc));
+      uptr[t] += ustep[t];
+    }
+  };
+  auto lwrite = [&](int slab) __attribute__((always_inline)) {
+    const unsigned lds0 = lds_base + (unsigned)(2 * (slab % NBUF) * BUF) + 16 * lane;
+#pragma unroll
+    for (int t = 0; t < UPW; ++t)
+      if (t < nunits) lw_dsw16(lds0 + ulds[t], st[t]);
+  };
+  if constexpr (RSTG) {
+    gload(0);
+    wait_vmcnt<0>();
+    lwrite(0);
+    if (nslab > 1) gload(1);
+  } else {
+#pragma unroll
+    for (int p = 0; p < NBUF - 1; ++p)
+      if (p < nslab) issue(p);
+  }
   for (int sl = 0; sl < nslab; ++sl) {
-    wait_for(min(NBUF - 2, nslab - 1 - sl));
+    if (!RSTG) wait_for(min(NBUF - 2, nslab - 1 - sl));
     __builtin_amdgcn_s_waitcnt(15 | (3 << 14) | (7 << 4));   // lgkmcnt(0): this wave's LDS reads are done
     __builtin_amdgcn_s_barrier();
-    if (sl + NBUF - 1 < nslab) issue(sl + NBUF - 1);
+    if (RSTG) {
+      if (sl + 1 < nslab) {   // slab sl+1 (loaded during slab sl-1) into its slot: slab sl-1's, retired by this barrier
+        wait_vmcnt<0>();
+        lwrite(sl + 1);
+      }
+    } else if (sl + NBUF - 1 < nslab) {
+      issue(sl + NBUF - 1);
+    }
     const bf16* base = lsm + (sl % NBUF) * BUF;
     const bf16* ty = base + (MB * wn) * BLK;
     const bf16* tx = base + NBY * BLK + (CB * wc) * BLK;
@@ -185,6 +231,8 @@ __global__ __launch_bounds__(64 * WN * WC, 1) void linear_wgrad_kernel(LinWgradA
         for (int i = 0; i < MB; ++i)
 #pragma unroll
           for (int j = 0; j < CB; ++j) acc[i][j] = mfma32(fa[i], fb[j], acc[i][j]);
+        // the next-but-one slab's loads, a k-step after the stores that read the same AGPRs
+        if (RSTG && r0 == 0 && s == 0 && sl + 2 < nslab) gload(sl + 2);
       }
     }
     if (do_bias) {   // column sums of the staged dY block rows (zero rows past M contribute nothing)
