@@ -1802,7 +1802,17 @@ static int launch_col(FftArgs& a, bool inv, int nblk_y, hipStream_t s) {
     if (cw == 16384) {
       static const int gp_env = getenv("LCI_FFT_GP") ? atoi(getenv("LCI_FFT_GP")) : 4;
       if (gw != 16) return 1;
-      if (!inv && gp_env == 4 && (a.L & 3) == 0 && (a.n2 / gw) % 4 == 0) {
+      if (gp_env == 8 && (inv || (a.L & 3) == 0) && (a.n2 / gw) % 8 == 0) {   // (A/B: 8 groups per workgroup)
+        if (inv) {
+          (void)hipFuncSetAttribute((const void*)fft_colw_inv_kernel<16, 16384, 512, 8>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+          hipLaunchKernelGGL((fft_colw_inv_kernel<16, 16384, 512, 8>), dim3(a.n2 / gw / 8, nblk_y), dim3(512), sh, s, a);
+        } else {
+          (void)hipFuncSetAttribute((const void*)fft_colw_fwd_kernel<16, 16384, 512, 8>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+          hipLaunchKernelGGL((fft_colw_fwd_kernel<16, 16384, 512, 8>), dim3(a.n2 / gw / 8, nblk_y), dim3(512), sh, s, a);
+        }
+      } else if (!inv && gp_env == 4 && (a.L & 3) == 0 && (a.n2 / gw) % 4 == 0) {
         (void)hipFuncSetAttribute((const void*)fft_colw_fwd_kernel<16, 16384, 512, 4>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         hipLaunchKernelGGL((fft_colw_fwd_kernel<16, 16384, 512, 4>), dim3(a.n2 / gw / 4, nblk_y), dim3(512), sh, s, a);
