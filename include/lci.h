@@ -76,12 +76,11 @@ int lci_attn_fwd(const void* qkv, void* out, float* lse2, float* knorm_ws, int B
 long long lci_attn_fwd_ws_bytes(int B, int L, int H);
 /* dqkv (B, L, 3*H*64) bf16 <- dQ, dK, dV in the packed layout; dout (B, L, H*64) bf16;
  * delta_ws: 16-byte aligned workspace of lci_attn_bwd_ws_bytes(B, H, L) bytes, written by the call: the (B, H, 2, L)
- * f32 rows -lse2 | -delta, then d-major bf16 copies of Q and dO that the dK/dV kernel stages. No atomics: bitwise
- * reproducible. */
+ * f32 rows -lse2 | -delta (the backward kernels' row constants). No atomics: bitwise reproducible. */
 int lci_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse2, void* dqkv,
                  float* delta_ws, int B, int L, int H, int head_dim, float scale, void* stream);
 long long lci_attn_bwd_ws_bytes(int B, int H, int L);
-/* Same as lci_attn_bwd, one launch at a time (stage 0 = delta + the Q / dO copies, 1 = dK/dV, 2 = dQ; -1 = all)
+/* Same as lci_attn_bwd, one launch at a time (stage 0 = delta, 1 = dK/dV, 2 = dQ; -1 = all)
  * for timing. */
 int lci_attn_bwd_stage(int stage, const void* qkv, const void* out, const void* dout, const float* lse2,
                        void* dqkv, float* delta_ws, int B, int L, int H, int head_dim, float scale, void* stream);

@@ -5,17 +5,17 @@
 //            order (qkv, head, d) (backbone_vit.py:168); O is written as (B, L, H*64) = out_rearrange.
 //            The L x L score matrix is never materialised; the forward keeps lse2 = log2(sum exp) per row.
 //
-// Forward:   attn_key_norm_kernel (per-64-key-tile max ||k||) + attn_fwd2_kernel: one workgroup = 8 waves x 32
-//            query rows; K/V tiles of 64 keys by buffer loads into a 3-slot LDS ring. Per wave and tile:
-//            S^T = K.Q~^T with the query on the MFMA lane (v_mfma_f32_32x32x16_bf16, 8 MFMAs), lane-local
-//            max-free softmax on tiles the key-norm bound proves safe (exact row max otherwise), O^T += V^T.P^T
-//            with P taken straight from the S accumulators (8 MFMAs, V^T via ds_read_b64_tr_b16); the next
-//            tile's scores are computed in place while this tile's exp2 runs.
-// Backward:  (1) delta = rowsum(dO*O); (2) dK/dV kernel: a workgroup owns NW*32 keys (key on the lane),
-//            sweeps query tiles: S, dP recomputed, dV^T += dO^T.P, dK^T += Q^T.dS (default: attn_bwd_dkdv16_kernel
-//            on v_mfma_f32_16x16x32_bf16, row constants as initial accumulators);
-//            (3) dQ kernel (v2, pipelined like the forward): a workgroup owns 256 queries, sweeps key tiles:
+// Three kernels, each one wave per SIMD (4-wave workgroups, the whole register file per wave) running a hand-placed
+// stream of v_mfma_f32_32x32x16_bf16 and softmax VALU (inline asm, fixed order):
+// Forward:   attn_key_norm_kernel (per-64-key-tile max ||k||) + attn_fwd_hs_kernel: 64 queries per wave on the MFMA
+//            lane, S^T = K.Q~^T, lane-local max-free softmax on tiles the key-norm bound proves safe (exact online
+//            softmax otherwise), O^T += V^T.P^T with P straight from the S accumulators.
+// Backward:  (1) attn_bwd_delta_kernel: delta = rowsum(dO*O), written with -lse2 as the chains' row constants;
+//            (2) attn_bwd_dkdv_hs_kernel: 64 keys per wave on the lane, sweeps query tiles: S, dP recomputed,
+//            dV^T += dO^T.P, dK^T += Q^T.dS; (3) attn_bwd_dq_hs_kernel: 64 queries per wave, sweeps key tiles:
 //            S^T, dP^T, dQ^T += K^T.dS^T. No atomics: results are bitwise reproducible.
+// Superseded variants (2 waves per SIMD, 16x16x32 shapes, d-major Q/dO staging, MFMA row sums, timing probes) were
+// removed in round 5; their same-box A/B records are kept in profiles/r0[1-4]_attn_*.
 #include "common.hpp"
 
 #include <type_traits>
@@ -24,59 +24,7 @@ namespace lci {
 
 constexpr int DH = 64;        // head dim (ViT-small/base: 384/6, 768/12)
 constexpr int KT = 64;        // keys (or queries) per LDS tile
-constexpr int LD_ROW = 72;    // LDS row stride (elements) for tiles read by rows: 144 B, b128 conflict-free
-constexpr int LD_TR = 96;     // LDS row stride for tiles read only transposed: 192 B, tr_b16 conflict-free
-// Tiles read BOTH by rows (ds_read_b128) and transposed (ds_read_b64_tr_b16): no plain stride is conflict-free
-// for both (144 B: 2-way on tr; 192 B: 4-way on b128). 192-B rows with the 16-B chunk index XORed by
-// (row >> 2) & 3 are conflict-free for both (exhaustive check over the lane groups of MI355X_MICROARCH.md).
-constexpr int LD_SW = 96;
-__device__ __forceinline__ int swz(int row, int col) {   // col: element index; 8-element chunks stay whole
-  return row * LD_SW + ((((col >> 3) ^ ((row >> 2) & 3)) << 3) | (col & 7));
-}
-// The dK/dV kernel on v_mfma_f32_16x16x32_bf16 reads its Q / dO tiles with the 16x16x32 lane maps (b128 rows: row =
-// lane & 15, chunk = lane >> 4; transposed: 4 rows x 16 columns per 16 lanes), for which the swizzle above leaves
-// 2-way conflicts (PMC: 2.2 extra LDS cycles per LDS instruction, 13 % of the wave cycles stalled on LDS issue).
-// 128-byte rows with the chunk XORed by 2 * ((row >> 1) & 3) are conflict-free for both reads and for the 16-byte
-// staging writes (exhaustive check over the MI355X_MICROARCH.md lane groups), and need no padding.
-constexpr int LD_D16 = 64;
-__device__ __forceinline__ int swz16(int row, int col) {
-  return row * LD_D16 + ((((col >> 3) ^ (((row >> 1) & 3) << 1)) << 3) | (col & 7));
-}
-__device__ __forceinline__ bf16x8 frag_row_sw(const bf16* tile, int r0, int c0, int lane) {
-  return *(const bf16x8*)(tile + swz(r0 + (lane & 31), c0 + 8 * (lane >> 5)));
-}
-template <int S>
-__device__ __forceinline__ bf16x8 frag_tr_sw(const bf16* tile, int r0, int c0, int lane) {
-  const int row = r0 + 16 * S + 4 * (lane >> 5) + ((lane & 15) >> 2);
-  const int col = c0 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-  return cat44(lds_tr4(tile + swz(row, col)), lds_tr4(tile + swz(row + 8, col)));
-}
 constexpr float NEG_BIG = -1.0e30f;
-
-// dK/dV loop scheduling strategy: iglp_opt(3) (MFMA / exp interleave) measured 23.66 -> 23.11 ms on one box
-// (profiles/r01_attn_dkdv_iglp_ab.jsonl); 0-2 were slower. -DLCI_IGLP=-1 builds without the hint.
-#ifndef LCI_IGLP
-#define LCI_IGLP 3
-#endif
-#if LCI_IGLP >= 0
-#define LCI_SCHED_HINT() __builtin_amdgcn_iglp_opt(LCI_IGLP)
-#else
-#define LCI_SCHED_HINT()
-#endif
-
-// Static priority for waves 4-7 (the arbitration losers of an 8-wave workgroup; MI355X_MICROARCH.md "Two waves
-// per SIMD" item 4): -DLCI_PRIO_YOUNG=1 sets s_setprio 1 on them once, before the main loop.
-#ifndef LCI_PRIO_YOUNG
-#define LCI_PRIO_YOUNG 0
-#endif
-__device__ __forceinline__ void prio_young(int wave) {
-  if (LCI_PRIO_YOUNG && wave >= 4) __builtin_amdgcn_s_setprio(1);
-}
-// dK/dV row constants: 0 = extra MFMA k-step on bf16 hi/mid/lo splits staged in the Q/dO rows (default);
-// 1 = f32 -lse2 / -delta staged in a side LDS array, subtracted on the VALU (2 fewer MFMAs of 18 per half-tile)
-#ifndef LCI_DKDV_ROWC_VALU
-#define LCI_DKDV_ROWC_VALU 0
-#endif
 
 struct AttnArgs {
   const bf16* q; const bf16* k; const bf16* v;    // base pointers of head 0, batch 0
@@ -85,8 +33,6 @@ struct AttnArgs {
   bf16* dk; bf16* dv;                              // bwd dkdv kernel
   float* lse2;                                     // (B, H, L)
   float* delta;                                    // bwd: (B, H, 2, L) negated row constants [-lse2 | -delta]
-  bf16* qdoT;                                      // bwd: (B, H, 2, 64, Lp) d-major Q | dO, P-pack query order
-  int Lp;                                          // bwd: L rounded up to 64
   long long bs_q, bs_k, bs_v, bs_o, bs_do, bs_out, bs_dk, bs_dv;   // batch strides (elements)
   int rs_q, rs_k, rs_v, rs_o, rs_do, rs_out, rs_dk, rs_dv;         // token (row) strides (elements)
   int hs;                                          // head stride (elements) in every tensor (= 64)
@@ -95,50 +41,6 @@ struct AttnArgs {
   float scale;
 };
 
-// Stage a 64 x 64 bf16 tile (rows row0.., 128 B per row) into registers: NT threads, 16 B per thread-pass.
-template <int NT>
-struct TileRegs {
-  static constexpr int PASSES = (KT * DH * 2) / (NT * 16);
-  u32x4 r[PASSES];
-  // GUARD=false: the caller knows rows row0..row0+63 are all < L (full tiles: no exec-masked branches).
-  template <bool GUARD = true>
-  __device__ __forceinline__ void load(const bf16* base, int rs, int row0, int L, int tid) {
-#pragma unroll
-    for (int p = 0; p < PASSES; ++p) {
-      const int idx = p * NT + tid;
-      const int row = idx >> 3, ch = idx & 7;
-      const int g = row0 + row;
-      if (!GUARD || g < L) r[p] = *(const u32x4*)(base + (long long)g * rs + ch * 8);
-      else r[p] = u32x4{0u, 0u, 0u, 0u};
-    }
-  }
-  __device__ __forceinline__ void store_sw(bf16* lds, int tid) const {   // swizzled LD_SW layout
-#pragma unroll
-    for (int p = 0; p < PASSES; ++p) {
-      const int idx = p * NT + tid;
-      const int row = idx >> 3, ch = idx & 7;
-      *(u32x4*)(lds + swz(row, ch * 8)) = r[p];
-    }
-  }
-  __device__ __forceinline__ void store_sw16(bf16* lds, int tid) const {   // swz16 layout (dK/dV16 tiles)
-#pragma unroll
-    for (int p = 0; p < PASSES; ++p) {
-      const int idx = p * NT + tid;
-      const int row = idx >> 3, ch = idx & 7;
-      *(u32x4*)(lds + swz16(row, ch * 8)) = r[p];
-    }
-  }
-  __device__ __forceinline__ void store(bf16* lds, int ld, int tid) const {
-#pragma unroll
-    for (int p = 0; p < PASSES; ++p) {
-      const int idx = p * NT + tid;
-      const int row = idx >> 3, ch = idx & 7;
-      *(u32x4*)(lds + row * ld + ch * 8) = r[p];
-    }
-  }
-};
-
-// ------------------------------------------------------------------------------ forward, v2
 // Per-64-key-tile bound on |k|: knorm[b][h][t] = max_{key in tile t} ||k_key||_2 (f32 of the bf16 keys).
 // One wave per tile, lane = key. Used by the forward's max-free fast path (below).
 __global__ __launch_bounds__(256) void attn_key_norm_kernel(AttnArgs a, float* knorm, int nkt) {
@@ -161,261 +63,12 @@ __global__ __launch_bounds__(256) void attn_key_norm_kernel(AttnArgs a, float* k
   if (lane == 0) knorm[((long long)b * a.H + hh) * nkt + t] = sqrtf(ss);
 }
 
-// Forward v2: one workgroup = 8 waves x 32 query rows (256 queries share every staged K/V tile: half the LDS
-// write traffic per MFMA of a 4-wave group), 2 waves per SIMD.
-//  * K/V tiles arrive by buffer loads (scalar tile offset, no per-tile address VALU; rows >= L read as zero)
-//    two tiles ahead into alternating register sets, and are written into a 3-slot LDS ring one tile ahead:
-//    one barrier per tile.
-//  * Software pipeline per wave: while the exp2/pack/row-sum of tile j runs on the VALU, the MFMAs of tile j+1's
-//    scores S_{j+1} = K_{j+1} Q~^T are in flight; then O^T += V_j^T P_j^T.
-//  * Max-free softmax: p = exp2(s~ - m) against a reference m that is only moved when it must be. A tile is
-//    "safe" when every row's bound ||q~|| * max||k|| - m <= 64 (q~ = c q, bf16; knorm per tile from
-//    attn_key_norm_kernel): then p <= 2^64, which f32 sums and bf16 P carry exactly as well as p <= 1, and
-//    the tile needs no row max at all. Unsafe tiles (and the first) take the exact path: row max, lazy
-//    re-base of m (alpha = exp2(-d) on O and l). The result is the same softmax; only the reference point
-//    of the exponent differs.
-#ifndef LCI_SB
-#if defined(LCI_SB_OFF) && LCI_SB_OFF
-#define LCI_SB()
-#else
-#define LCI_SB() __builtin_amdgcn_sched_barrier(0)
-#endif
-#endif
-constexpr int FW_NW = 8;
-constexpr int FSLOT = KT * LD_ROW + KT * LD_TR;   // one ring slot: K tile (rows) + V tile (transposed reads)
+// Max-free softmax (forward): p = exp2(s~ - m) against a reference m that is only moved when it must be. A tile is
+// "safe" when every row's bound ||q~|| * max||k|| - m <= 64 (q~ = c q, bf16; knorm per tile from
+// attn_key_norm_kernel): then p <= 2^64, which f32 sums and bf16 P carry exactly as well as p <= 1, and the tile
+// needs no row max at all. Unsafe tiles (and the first) take the exact path: row max, lazy re-base of m
+// (alpha = exp2(-d) on O and l). The result is the same softmax; only the reference point of the exponent differs.
 constexpr float SAFE_EXP2 = 64.f;
-
-
-__global__ __launch_bounds__(FW_NW * 64, 1) void attn_fwd2_kernel(AttnArgs a, const float* knorm) {
-  __shared__ __attribute__((aligned(16))) bf16 smem[3 * FSLOT];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int hh = blockIdx.y, b = blockIdx.z;
-  const int L = a.L;
-  const int qrow = blockIdx.x * (FW_NW * 32) + wave * 32 + (lane & 31);
-  const int half = lane >> 5;
-  const int nkt = (L + KT - 1) / KT, nfull = L / KT;
-
-  // staging: thread -> (row, 16-B chunk) of a 64 x 128 B tile; one K and one V chunk per thread per tile
-  const int srow = tid >> 3, sch = tid & 7;
-  const int rs2 = a.rs_k * 2;
-  const uint32_t nbytes = (uint32_t)(L - 1) * (uint32_t)rs2 + DH * 2;
-  const rsrc_t rk = make_rsrc(a.k + b * a.bs_k + hh * a.hs, nbytes);
-  const rsrc_t rv = make_rsrc(a.v + b * a.bs_v + hh * a.hs, nbytes);
-  const int voff = srow * rs2 + sch * 16;
-  const int st_k = srow * LD_ROW + sch * 8, st_v = KT * LD_ROW + srow * LD_TR + sch * 8;
-  const float* kn = knorm + ((long long)b * a.H + hh) * nkt;
-
-  const float c = a.c;
-  bf16x8 qf[4];
-  float qss = 0.f;
-  {
-    const bf16* qp = a.q + b * a.bs_q + hh * a.hs;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      bf16x8 t{};
-      if (qrow < L) t = *(const bf16x8*)(qp + (long long)qrow * a.rs_q + ks * 16 + 8 * half);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        t[j] = to_bf16(to_f32(t[j]) * c);
-        qss += to_f32(t[j]) * to_f32(t[j]);
-      }
-      qf[ks] = t;
-    }
-  }
-  const float qn = sqrtf(wave_sum_xor32(qss));   // ||q~|| of this lane's row
-
-  // per-lane LDS fragment bases; a ring slot adds a wave-uniform element offset, fragments add immediates
-  const bf16* kfrag = smem + (lane & 31) * LD_ROW + 8 * half;
-  const bf16* vfrag = smem + KT * LD_ROW + (4 * half + ((lane & 15) >> 2)) * LD_TR + 16 * ((lane >> 4) & 1) +
-                      4 * (lane & 3);
-  auto kf = [&](int slot, int r0, int c0) __attribute__((always_inline)) { return *(const bf16x8*)(kfrag + slot + r0 * LD_ROW + c0); };
-  auto vf = [&](int slot, int r0, int s, int c0) __attribute__((always_inline)) {
-    const bf16* p = vfrag + slot + (r0 + 16 * s) * LD_TR + c0;
-    return cat44(lds_tr4(p), lds_tr4(p + 8 * LD_TR));
-  };
-
-  // prologue: tiles 0 and 1 into ring slots 0 and 1
-  {
-    const u32x4 k0 = bload16(rk, voff, 0), v0 = bload16(rv, voff, 0);
-    const u32x4 k1 = bload16(rk, voff, KT * rs2), v1 = bload16(rv, voff, KT * rs2);
-    *(u32x4*)(smem + st_k) = k0;
-    *(u32x4*)(smem + st_v) = v0;
-    *(u32x4*)(smem + FSLOT + st_k) = k1;   // beyond L: zeros, never read
-    *(u32x4*)(smem + FSLOT + st_v) = v1;
-  }
-  __syncthreads();
-
-  f32x16 o0 = {}, o1 = {}, negm = {};
-  float m_run = 0.f, l_run = 0.f;
-  prio_young(wave);
-
-  auto mask_ragged = [&](int kt, f32x16& t0, f32x16& t1) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int key = kt * KT + (i & 3) + 8 * (i >> 2) + 4 * half;
-      if (key >= L) t0[i] = NEG_BIG;
-      if (key + 32 >= L) t1[i] = NEG_BIG;
-    }
-  };
-  // exact path: row max of the tile (relative to m), lazy re-base when it grew (always on the first tile)
-  auto exact = [&](f32x16& t0, f32x16& t1, bool first) __attribute__((always_inline)) {
-    float mq[4] = {fmaxf(t0[0], t0[1]), fmaxf(t0[2], t0[3]), fmaxf(t1[0], t1[1]), fmaxf(t1[2], t1[3])};
-#pragma unroll
-    for (int i = 4; i < 16; i += 4) {
-      mq[0] = fmaxf(mq[0], fmaxf(t0[i], t0[i + 1]));
-      mq[1] = fmaxf(mq[1], fmaxf(t0[i + 2], t0[i + 3]));
-      mq[2] = fmaxf(mq[2], fmaxf(t1[i], t1[i + 1]));
-      mq[3] = fmaxf(mq[3], fmaxf(t1[i + 2], t1[i + 3]));
-    }
-    const float mx = wave_max_xor32(fmaxf(fmaxf(mq[0], mq[1]), fmaxf(mq[2], mq[3])));
-    if (first || __any(mx > 0.f)) {
-      const float d = first ? mx : fmaxf(mx, 0.f);
-      m_run += d;
-      if (!first) {
-        const float alpha = exp2_fast(-d);
-        l_run *= alpha;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) { o0[i] *= alpha; o1[i] *= alpha; }
-      }
-#pragma unroll
-      for (int i = 0; i < 16; ++i) { t0[i] -= d; t1[i] -= d; negm[i] = -m_run; }
-    }
-  };
-
-  // S_0
-  f32x16 x0, x1;
-  x0 = mfma32(kf(0, 0, 0), qf[0], negm);
-  x1 = mfma32(kf(0, 32, 0), qf[0], negm);
-#pragma unroll
-  for (int ks = 1; ks < 4; ++ks) {
-    x0 = mfma32(kf(0, 0, ks * 16), qf[ks], x0);
-    x1 = mfma32(kf(0, 32, ks * 16), qf[ks], x1);
-  }
-  if (nfull == 0) mask_ragged(0, x0, x1);
-  exact(x0, x1, true);
-
-  // Ring slots (element offsets) of tiles j, j+1, j+2; rotated every tile.
-  int slA = 0, slB = FSLOT, slC = 2 * FSLOT;
-  // One tile j. Entry: S_j in (x0, x1). Exit (NEXT): S_{j+1} in (x0, x1) - the score MFMAs of the next tile
-  // write the registers of this tile's scores once these have been exponentiated, packed and summed.
-  auto iter = [&](const int j, auto next) __attribute__((always_inline)) -> bool {
-    constexpr bool NEXT = decltype(next)::value;
-    // tile j+2 -> registers now, -> LDS slot C at the end (beyond the last tile the range check gives zeros)
-    const u32x4 kw = bload16(rk, voff, (j + 2) * KT * rs2);
-    const u32x4 vw = bload16(rv, voff, (j + 2) * KT * rs2);
-    const float knext = NEXT ? kn[j + 1] : 0.f;
-    float lq[4];
-    bf16x8 vq[8], kq[8];
-    // (1) exp2 of keys 0-31 half 0, pack p00; V fragments for the first PV MFMAs
-    vq[0] = vf(slA, 0, 0, 0);
-    vq[1] = vf(slA, 0, 0, 32);
-    vq[2] = vf(slA, 0, 1, 0);
-    vq[3] = vf(slA, 0, 1, 32);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) x0[i] = exp2_fast(x0[i]);
-    const bf16x8 p00 = pack8<0>(x0);
-    lq[0] = (x0[0] + x0[1]) + (x0[2] + x0[3]);
-    lq[1] = (x0[4] + x0[5]) + (x0[6] + x0[7]);
-    LCI_SB();
-    // (2) PV with p00, exp2 of x0[8..15]
-    o0 = mfma32(vq[0], p00, o0);
-    o1 = mfma32(vq[1], p00, o1);
-    vq[4] = vf(slA, 32, 0, 0);
-    vq[5] = vf(slA, 32, 0, 32);
-#pragma unroll
-    for (int i = 8; i < 16; ++i) x0[i] = exp2_fast(x0[i]);
-    const bf16x8 p01 = pack8<1>(x0);
-    lq[0] += (x0[8] + x0[9]) + (x0[10] + x0[11]);
-    lq[1] += (x0[12] + x0[13]) + (x0[14] + x0[15]);
-    if constexpr (NEXT) {
-      kq[0] = kf(slB, 0, 0);
-      kq[1] = kf(slB, 0, 16);
-    }
-    LCI_SB();
-    // (3) PV with p01, exp2 of x1[0..7]
-    o0 = mfma32(vq[2], p01, o0);
-    o1 = mfma32(vq[3], p01, o1);
-    vq[6] = vf(slA, 32, 1, 0);
-    vq[7] = vf(slA, 32, 1, 32);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) x1[i] = exp2_fast(x1[i]);
-    const bf16x8 p10 = pack8<0>(x1);
-    lq[2] = (x1[0] + x1[1]) + (x1[2] + x1[3]);
-    lq[3] = (x1[4] + x1[5]) + (x1[6] + x1[7]);
-    if constexpr (NEXT) {
-      kq[2] = kf(slB, 0, 32);
-      kq[3] = kf(slB, 0, 48);
-    }
-    LCI_SB();
-    // (4) scores S_{j+1} keys 0..31 into x0, exp2 of x1[8..15]
-    if constexpr (NEXT) {
-      x0 = mfma32(kq[0], qf[0], negm);
-      x0 = mfma32(kq[1], qf[1], x0);
-      kq[4] = kf(slB, 32, 0);
-      kq[5] = kf(slB, 32, 16);
-    }
-#pragma unroll
-    for (int i = 8; i < 16; ++i) x1[i] = exp2_fast(x1[i]);
-    const bf16x8 p11 = pack8<1>(x1);
-    lq[2] += (x1[8] + x1[9]) + (x1[10] + x1[11]);
-    lq[3] += (x1[12] + x1[13]) + (x1[14] + x1[15]);
-    l_run += (lq[0] + lq[1]) + (lq[2] + lq[3]);
-    LCI_SB();
-    // (5) rest of the PV MFMAs and of the scores
-    if constexpr (NEXT) {
-      x0 = mfma32(kq[2], qf[2], x0);
-      kq[6] = kf(slB, 32, 32);
-      kq[7] = kf(slB, 32, 48);
-    }
-    o0 = mfma32(vq[4], p10, o0);
-    o1 = mfma32(vq[5], p10, o1);
-    if constexpr (NEXT) x0 = mfma32(kq[3], qf[3], x0);
-    o0 = mfma32(vq[6], p11, o0);
-    o1 = mfma32(vq[7], p11, o1);
-    if constexpr (NEXT) {
-      x1 = mfma32(kq[4], qf[0], negm);
-      x1 = mfma32(kq[5], qf[1], x1);
-      x1 = mfma32(kq[6], qf[2], x1);
-      x1 = mfma32(kq[7], qf[3], x1);
-    }
-    *(u32x4*)(smem + slC + st_k) = kw;
-    *(u32x4*)(smem + slC + st_v) = vw;
-    __syncthreads();
-    const int t = slA; slA = slB; slB = slC; slC = t;
-    if constexpr (NEXT) return (j + 1 == nfull) | !__all(qn * knext - m_run <= SAFE_EXP2);
-    return false;
-  };
-  using T = std::true_type;
-  using F = std::false_type;
-  // a ragged or unsafe next tile takes the exact path (in place)
-  int j = 0;
-  for (; j + 1 < nkt; ++j) {
-    if (iter(j, T{})) [[unlikely]] {
-      if (j + 1 == nfull) mask_ragged(j + 1, x0, x1);
-      exact(x0, x1, false);
-    }
-  }
-  iter(j, F{});
-
-  const float l_tot = wave_sum_xor32(l_run);
-  const float inv = 1.f / l_tot;
-  if (qrow < L) {
-    bf16* op = a.out + b * a.bs_out + (long long)qrow * a.rs_out + hh * a.hs;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      bf16x4 w0, w1;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        w0[j] = to_bf16(o0[4 * g + j] * inv);
-        w1[j] = to_bf16(o1[4 * g + j] * inv);
-      }
-      *(bf16x4*)(op + 8 * g + 4 * half) = w0;
-      *(bf16x4*)(op + 32 + 8 * g + 4 * half) = w1;
-    }
-    if (half == 0) a.lse2[((long long)b * a.H + hh) * L + qrow] = m_run + __log2f(l_tot);
-  }
-}
-
 // --------------------------------------------------------------------------- backward: delta
 // delta[b,h,q] = sum_d dO[b,q,h,d] * O[b,q,h,d]; 8 threads per (q, h) row, 16 B each. Written negated, next to the
 // negated lse2, as the backward kernels' row constants: ws[b][h][0][q] = -lse2, ws[b][h][1][q] = -delta (the chains'
@@ -438,427 +91,6 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnArgs a) {
     float* ws = a.delta + ((long long)b * a.H + hh) * 2 * a.L;
     ws[row] = -a.lse2[((long long)b * a.H + hh) * a.L + row];
     ws[a.L + row] = -acc;
-  }
-}
-
-// d-major copies of Q and dO for the placed-stream dK/dV kernel (LCI_HS_TQ): row d of a 64-query tile holds the
-// tile's 64 queries, each 16-query group in the order of the bf16 P / dS packs' k index (position 8h + j holds
-// query (j & 3) + 8 (j >> 2) + 4h), so the dV / dK products read their Q^T / dO^T operand fragment (8 queries at one
-// d) with one ds_read_b128 instead of two transposed reads. Queries past L are zero. Workgroup = one 64-query tile of
-// one (b, h); a 64 x 64 tile of each tensor goes through LDS.
-__global__ __launch_bounds__(256) void attn_bwd_qdoT_kernel(AttnArgs a) {
-  __shared__ bf16 tl[2][64][72];   // [Q | dO][query][d], rows padded to 144 B
-  const int tid = threadIdx.x, t0 = blockIdx.x * 64, hh = blockIdx.y, b = blockIdx.z;
-#pragma unroll
-  for (int w = 0; w < 2; ++w) {
-    const bf16* src = w ? a.dout + b * a.bs_do + hh * a.hs : a.q + b * a.bs_q + hh * a.hs;
-    const int rs = w ? a.rs_do : a.rs_q;
-#pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-      const int q = pass * 32 + (tid >> 3), c = tid & 7;
-      bf16x8 v = bf16x8{};
-      if (t0 + q < a.L) v = *(const bf16x8*)(src + (long long)(t0 + q) * rs + 8 * c);
-      *(bf16x8*)&tl[w][q][8 * c] = v;
-    }
-  }
-  __syncthreads();
-  // thread -> (tensor w, d, 16-query group g): 2 x 64 x 4 = 512 items, 2 per thread
-#pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    const int item = it * 256 + tid, w = item >> 8, d = (item >> 2) & 63, g = item & 3;
-    bf16x8 lo, hi;
-#pragma unroll
-    for (int p = 0; p < 16; ++p) {
-      const int hp = p >> 3, j = p & 7;
-      const bf16 v = tl[w][16 * g + (j & 3) + 8 * (j >> 2) + 4 * hp][d];
-      if (p < 8) lo[p] = v; else hi[p - 8] = v;
-    }
-    bf16* dst = a.qdoT + ((((long long)b * a.H + hh) * 2 + w) * 64 + d) * a.Lp + t0 + 16 * g;
-    *(bf16x8*)dst = lo;
-    *(bf16x8*)(dst + 8) = hi;
-  }
-}
-
-// ---------------------------------------------------------------------- backward: dK, dV kernel
-// KB key blocks of 32 per wave (key on the MFMA lane). With KB = 2 every Q / dO fragment read from LDS (row
-// fragments of the S and dP chains, transposed fragments of the dV / dK products) feeds two key blocks: half the
-// LDS read cycles per MFMA, at one wave per SIMD (the second key block's chains are the in-wave ILP).
-template <int NW, int KB>
-__global__ __launch_bounds__(NW * 64, (KB == 1 ? 8 / NW : 4 / NW)) void attn_bwd_dkdv_kernel(AttnArgs a) {
-  constexpr int NT = NW * 64;
-  constexpr int TILE = 2 * KT * LD_SW;                  // Q tile + dO tile (both read by rows and transposed)
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * TILE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int hh = blockIdx.y, b = blockIdx.z;
-  const int L = a.L;
-  const int half = lane >> 5;
-  const int key0 = blockIdx.x * (NW * 32 * KB) + wave * (32 * KB) + (lane & 31);
-
-  const bf16* qp = a.q + b * a.bs_q + hh * a.hs;
-  const bf16* dop = a.dout + b * a.bs_do + hh * a.hs;
-  const float* lsep = a.delta + ((long long)b * a.H + hh) * 2 * L;   // -lse2
-  const float* dlp = lsep + L;                                        // -delta
-
-  // K^T and V^T as B operands: lane (key r, half h) holds K[key][16ks+8h..], V[key][16ks+8h..]
-  bf16x8 kf[KB][4], vf[KB][4];
-  {
-    const bf16* kp = a.k + b * a.bs_k + hh * a.hs;
-    const bf16* vp = a.v + b * a.bs_v + hh * a.hs;
-#pragma unroll
-    for (int kb = 0; kb < KB; ++kb) {
-      const int key = key0 + 32 * kb;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        if (key < L) {
-          kf[kb][ks] = *(const bf16x8*)(kp + (long long)key * a.rs_k + ks * 16 + 8 * half);
-          vf[kb][ks] = *(const bf16x8*)(vp + (long long)key * a.rs_v + ks * 16 + 8 * half);
-        } else {
-          kf[kb][ks] = bf16x8{};
-          vf[kb][ks] = bf16x8{};
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) kf[kb][ks][j] = to_bf16(to_f32(kf[kb][ks][j]) * a.c);  // exp2-domain scores
-      }
-    }
-  }
-
-  TileRegs<NT> qr, dr;
-  const int nqt = (L + KT - 1) / KT;
-  // Row constants as an extra k-step of the S and dP chains: columns 64..79 of each staged Q (dO) row hold
-  // -lse2 (-delta) split into three bf16 terms (hi + mid + lo carries ~24 bits), and the matching B fragment is
-  // 1 in rows 0..2. The chains then yield S c - lse2 and dP - delta with no per-lane row-constant loads
-  // (those were a third of this kernel's LDS read cycles) and no accumulator initialisation moves.
-  __shared__ __attribute__((aligned(16))) float rowc[2][2][KT];   // ROWC_VALU: [buf][lse2 | delta][query]
-  auto stage_rowc = [&](int buf, int qt) __attribute__((always_inline)) {
-    if constexpr (LCI_DKDV_ROWC_VALU) {
-      if (tid < 2 * KT) {
-        const int which = tid / KT, qi = tid % KT, q = qt * KT + qi;
-        rowc[buf][which][qi] = which == 0 ? ((q < L) ? -lsep[q] : 1.0e30f) : ((q < L) ? -dlp[q] : 0.f);
-      }
-      return;
-    }
-    if (tid < 2 * KT) {
-      const int which = tid / KT, qi = tid % KT, q = qt * KT + qi;
-      float v;
-      if (which == 0) v = (q < L) ? lsep[q] : -1.0e30f;  // invalid rows: P = exp2(-huge) = 0
-      else v = (q < L) ? dlp[q] : 0.f;
-      const bf16 hi = to_bf16(v), mid = to_bf16(v - to_f32(hi)), lo = to_bf16(v - to_f32(hi) - to_f32(mid));
-      bf16x8 e{};
-      e[0] = hi; e[1] = mid; e[2] = lo;
-      bf16* row = smem + buf * TILE + which * KT * LD_SW;
-      *(bf16x8*)(row + swz(qi, 64)) = e;
-      *(bf16x8*)(row + swz(qi, 72)) = bf16x8{};
-    }
-  };
-  bf16x8 onef{};
-  if (half == 0) { onef[0] = to_bf16(1.f); onef[1] = onef[0]; onef[2] = onef[0]; }
-  qr.load(qp, a.rs_q, 0, L, tid);
-  dr.load(dop, a.rs_do, 0, L, tid);
-  qr.store_sw(smem, tid);
-  dr.store_sw(smem + KT * LD_SW, tid);
-  stage_rowc(0, 0);
-  __syncthreads();
-
-  f32x16 dv0[KB], dv1[KB], dk0[KB], dk1[KB];
-#pragma unroll
-  for (int kb = 0; kb < KB; ++kb) dv0[kb] = dv1[kb] = dk0[kb] = dk1[kb] = f32x16{};
-  prio_young(wave);
-  for (int qt = 0; qt < nqt; ++qt) {
-    const int buf = qt & 1;
-    const bf16* ql = smem + buf * TILE;
-    const bf16* dl = ql + KT * LD_SW;
-    if (qt + 1 < nqt) {
-      qr.load(qp, a.rs_q, (qt + 1) * KT, L, tid);
-      dr.load(dop, a.rs_do, (qt + 1) * KT, L, tid);
-    }
-    LCI_SCHED_HINT();
-    // Two 32-query halves per 64-query tile (halves the live S/dP/P/dS registers); key on the lane.
-#pragma unroll
-    for (int qs = 0; qs < 2; ++qs) {
-      // Row constants enter as the extra k-step: the chains give S c - lse2[q] and dP - delta[q] directly;
-      // then P = exp2(.), dS = P (dP - delta).
-      bf16x8 qa[5], da[5];
-      if constexpr (!LCI_DKDV_ROWC_VALU) {
-        qa[4] = frag_row_sw(ql, qs * 32, 64, lane);
-        da[4] = frag_row_sw(dl, qs * 32, 64, lane);
-      }
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        qa[ks] = frag_row_sw(ql, qs * 32, ks * 16, lane);
-        da[ks] = frag_row_sw(dl, qs * 32, ks * 16, lane);
-      }
-      f32x16 s[KB], p[KB];
-#pragma unroll
-      for (int kb = 0; kb < KB; ++kb) {
-        if constexpr (LCI_DKDV_ROWC_VALU) {
-          s[kb] = mfma32(qa[0], kf[kb][0], f32x16{});
-          p[kb] = mfma32(da[0], vf[kb][0], f32x16{});
-        } else {
-          s[kb] = mfma32(qa[4], onef, f32x16{});
-          p[kb] = mfma32(da[4], onef, f32x16{});
-          s[kb] = mfma32(qa[0], kf[kb][0], s[kb]);
-          p[kb] = mfma32(da[0], vf[kb][0], p[kb]);
-        }
-#pragma unroll
-        for (int ks = 1; ks < 4; ++ks) {
-          s[kb] = mfma32(qa[ks], kf[kb][ks], s[kb]);
-          p[kb] = mfma32(da[ks], vf[kb][ks], p[kb]);
-        }
-      }
-      if constexpr (LCI_DKDV_ROWC_VALU) {
-        // query of accumulator register i of this lane: qs*32 + 8(i>>2) + 4*half + (i&3): 4 contiguous per group
-        const float* rl = &rowc[buf][0][qs * 32 + 4 * half];
-        const float* rd = &rowc[buf][1][qs * 32 + 4 * half];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 l4 = *(const f32x4*)(rl + 8 * g), d4 = *(const f32x4*)(rd + 8 * g);
-#pragma unroll
-          for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-              s[kb][4 * g + jj] -= l4[jj];
-              p[kb][4 * g + jj] -= d4[jj];
-            }
-        }
-      }
-      const bf16x8 tdo00 = frag_tr_sw<0>(dl, qs * 32, 0, lane), tdo10 = frag_tr_sw<1>(dl, qs * 32, 0, lane);
-      const bf16x8 tdo01 = frag_tr_sw<0>(dl, qs * 32, 32, lane), tdo11 = frag_tr_sw<1>(dl, qs * 32, 32, lane);
-      const bf16x8 tq00 = frag_tr_sw<0>(ql, qs * 32, 0, lane), tq10 = frag_tr_sw<1>(ql, qs * 32, 0, lane);
-      const bf16x8 tq01 = frag_tr_sw<0>(ql, qs * 32, 32, lane), tq11 = frag_tr_sw<1>(ql, qs * 32, 32, lane);
-#pragma unroll
-      for (int kb = 0; kb < KB; ++kb) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          s[kb][i] = exp2_fast(s[kb][i]);
-          p[kb][i] = s[kb][i] * p[kb][i];
-        }
-        const bf16x8 P0 = pack8<0>(s[kb]), P1 = pack8<1>(s[kb]), D0 = pack8<0>(p[kb]), D1 = pack8<1>(p[kb]);
-        // dV^T[d][key] += dO^T[d][q] P[q][key] ; dK^T[d][key] += Q^T[d][q] dS[q][key]
-        dv0[kb] = mfma32(tdo00, P0, dv0[kb]);
-        dv0[kb] = mfma32(tdo10, P1, dv0[kb]);
-        dv1[kb] = mfma32(tdo01, P0, dv1[kb]);
-        dv1[kb] = mfma32(tdo11, P1, dv1[kb]);
-        dk0[kb] = mfma32(tq00, D0, dk0[kb]);
-        dk0[kb] = mfma32(tq10, D1, dk0[kb]);
-        dk1[kb] = mfma32(tq01, D0, dk1[kb]);
-        dk1[kb] = mfma32(tq11, D1, dk1[kb]);
-      }
-    }
-    if (qt + 1 < nqt) {
-      bf16* nb = smem + (buf ^ 1) * TILE;
-      qr.store_sw(nb, tid);
-      dr.store_sw(nb + KT * LD_SW, tid);
-      stage_rowc(buf ^ 1, qt + 1);
-    }
-    __syncthreads();
-  }
-
-  const float sc = a.scale;
-#pragma unroll
-  for (int kb = 0; kb < KB; ++kb) {
-    const int key = key0 + 32 * kb;
-    if (key < L) {
-      bf16* dkp = a.dk + b * a.bs_dk + (long long)key * a.rs_dk + hh * a.hs;
-      bf16* dvp = a.dv + b * a.bs_dv + (long long)key * a.rs_dv + hh * a.hs;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        bf16x4 k0, k1, v0, v1;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          k0[j] = to_bf16(dk0[kb][4 * g + j] * sc);
-          k1[j] = to_bf16(dk1[kb][4 * g + j] * sc);
-          v0[j] = to_bf16(dv0[kb][4 * g + j]);
-          v1[j] = to_bf16(dv1[kb][4 * g + j]);
-        }
-        *(bf16x4*)(dkp + 8 * g + 4 * half) = k0;
-        *(bf16x4*)(dkp + 32 + 8 * g + 4 * half) = k1;
-        *(bf16x4*)(dvp + 8 * g + 4 * half) = v0;
-        *(bf16x4*)(dvp + 32 + 8 * g + 4 * half) = v1;
-      }
-    }
-  }
-}
-
-// ------------------------------------------------- backward: dK, dV kernel on v_mfma_f32_16x16x32_bf16
-// Same work split as attn_bwd_dkdv_kernel<NW, 1> (a wave owns 32 keys, key on the lane; 64-query tiles in two
-// 32-query halves), on the 16x16x32 MFMA shape: under sustained matrix load the chip holds a higher clock on this
-// shape at equal cycles per FLOP (MI355X_MICROARCH.md "DVFS give-back" item 7). Per half: 2 key blocks x 2 query
-// blocks of 16. The row constants need no MFMA k-step here: a lane's 4 accumulator rows of an S / dP block are 4
-// consecutive queries, so -lse2 / -delta of those queries is ONE f32x4 LDS read, used as the chains' initial
-// accumulator for both key blocks (32 MFMAs of 16 cycles per half: 512 MFMA cycles against the 32x32 form's
-// 18 x 32 = 576 with its row-constant k-step). P / dS feed dV^T / dK^T as B operands in the permuted k-order
-// {q 4g..4g+3 of block 0, q 4g..4g+3 of block 1} (g = lane >> 4), matched by the transposed dO / Q reads.
-__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-#ifndef LCI_D16_IGLP
-#define LCI_D16_IGLP 1   // iglp_opt(1) 22.01 / 22.11 ms vs (3) 22.78 / 22.11 ms in two same-box A/Bs
-#endif
-
-template <int NW>
-__global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv16_kernel(AttnArgs a) {
-  constexpr int NT = NW * 64;
-  constexpr int TILE = 2 * KT * LD_D16;                 // Q tile + dO tile (read by rows and transposed)
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * TILE];
-  __shared__ __attribute__((aligned(16))) float rowc[2][2][KT];   // [buf][-lse2 | -delta][query]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int hh = blockIdx.y, b = blockIdx.z;
-  const int L = a.L;
-  const int g = lane >> 4, c16 = lane & 15;
-  const int kw0 = blockIdx.x * (NW * 32) + wave * 32;   // first key of this wave
-
-  const bf16* qp = a.q + b * a.bs_q + hh * a.hs;
-  const bf16* dop = a.dout + b * a.bs_do + hh * a.hs;
-  const float* lsep = a.delta + ((long long)b * a.H + hh) * 2 * L;   // -lse2
-  const float* dlp = lsep + L;                                        // -delta
-
-  // K^T / V^T as B operands: lane holds K[kw0 + 16kb + c16][32ks + 8g + j] (K prescaled into the exp2 domain)
-  bf16x8 kf[2][2], vf[2][2];
-  {
-    const bf16* kp = a.k + b * a.bs_k + hh * a.hs;
-    const bf16* vp = a.v + b * a.bs_v + hh * a.hs;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      const int key = kw0 + 16 * kb + c16;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        if (key < L) {
-          kf[kb][ks] = *(const bf16x8*)(kp + (long long)key * a.rs_k + 32 * ks + 8 * g);
-          vf[kb][ks] = *(const bf16x8*)(vp + (long long)key * a.rs_v + 32 * ks + 8 * g);
-        } else {
-          kf[kb][ks] = bf16x8{};
-          vf[kb][ks] = bf16x8{};
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) kf[kb][ks][j] = to_bf16(to_f32(kf[kb][ks][j]) * a.c);
-      }
-    }
-  }
-
-  TileRegs<NT> qr, dr;
-  const int nqt = (L + KT - 1) / KT;
-  // Row constants of a query tile: thread tid < 128 owns one (-lse2 | -delta, query) entry. Loaded into a register
-  // at the top of the previous tile's iteration with the Q / dO tiles, written to LDS at its end: a load issued at
-  // the end would put a full memory latency in front of every tile's barrier.
-  // The load is unconditional (clamped index) so no exec-masked join makes the compiler wait for it early; the
-  // out-of-range substitutions happen at the LDS write.
-  const float* rcp = (tid / KT) == 1 ? dlp : lsep;
-  auto load_rowc = [&](int qt) __attribute__((always_inline)) -> float {
-    return rcp[min(qt * KT + tid % KT, L - 1)];
-  };
-  auto stage_rowc = [&](int buf, int qt, float v) __attribute__((always_inline)) {
-    if (tid < 2 * KT) {
-      const bool ok = qt * KT + tid % KT < L;
-      rowc[buf][tid / KT][tid % KT] = ok ? v : (tid < KT ? -1.0e30f : 0.f);   // invalid rows: P = 0
-    }
-  };
-  qr.load(qp, a.rs_q, 0, L, tid);
-  dr.load(dop, a.rs_do, 0, L, tid);
-  qr.store_sw16(smem, tid);
-  dr.store_sw16(smem + KT * LD_D16, tid);
-  stage_rowc(0, 0, load_rowc(0));
-  __syncthreads();
-
-  f32x4 dv[4][2], dk[4][2];   // [d block][key block]: lane holds rows d = 16db + 4g + i, column key c16
-#pragma unroll
-  for (int db = 0; db < 4; ++db)
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) dv[db][kb] = dk[db][kb] = f32x4{};
-  for (int qt = 0; qt < nqt; ++qt) {
-    const int buf = qt & 1;
-    const bf16* ql = smem + buf * TILE;
-    const bf16* dl = ql + KT * LD_D16;
-    float rc_next = 0.f;
-    if (qt + 1 < nqt) {
-      qr.load(qp, a.rs_q, (qt + 1) * KT, L, tid);
-      dr.load(dop, a.rs_do, (qt + 1) * KT, L, tid);
-      rc_next = load_rowc(qt + 1);
-    }
-#if LCI_D16_IGLP >= 0
-    __builtin_amdgcn_iglp_opt(LCI_D16_IGLP);
-#endif
-#pragma unroll
-    for (int qs = 0; qs < 2; ++qs) {
-      const int q0 = qs * 32;
-      f32x4 nl[2], nd[2];
-      bf16x8 qa[2][2], da[2][2];
-#pragma unroll
-      for (int qb = 0; qb < 2; ++qb) {
-        nl[qb] = *(const f32x4*)&rowc[buf][0][q0 + 16 * qb + 4 * g];
-        nd[qb] = *(const f32x4*)&rowc[buf][1][q0 + 16 * qb + 4 * g];
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          qa[qb][ks] = *(const bf16x8*)(ql + swz16(q0 + 16 * qb + c16, 32 * ks + 8 * g));
-          da[qb][ks] = *(const bf16x8*)(dl + swz16(q0 + 16 * qb + c16, 32 * ks + 8 * g));
-        }
-      }
-      f32x4 s[2][2], p[2][2];   // [query block][key block]
-#pragma unroll
-      for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
-          s[qb][kb] = mfma16(qa[qb][0], kf[kb][0], nl[qb]);
-          p[qb][kb] = mfma16(da[qb][0], vf[kb][0], nd[qb]);
-          s[qb][kb] = mfma16(qa[qb][1], kf[kb][1], s[qb][kb]);
-          p[qb][kb] = mfma16(da[qb][1], vf[kb][1], p[qb][kb]);
-        }
-      // transposed fragments (A operands): lane holds X^T[d = 16db + c16][q0 + 4g + (j & 3) + 16 (j >> 2)]
-      bf16x8 tdo[4], tq[4];
-      {
-        const int r = q0 + 4 * g + ((lane & 15) >> 2);
-#pragma unroll
-        for (int db = 0; db < 4; ++db) {
-          const int col = 16 * db + 4 * (lane & 3);
-          tdo[db] = cat44(lds_tr4(dl + swz16(r, col)), lds_tr4(dl + swz16(r + 16, col)));
-          tq[db] = cat44(lds_tr4(ql + swz16(r, col)), lds_tr4(ql + swz16(r + 16, col)));
-        }
-      }
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-        bf16x8 P, D;
-#pragma unroll
-        for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float e = exp2_fast(s[qb][kb][i]);
-            P[4 * qb + i] = to_bf16(e);
-            D[4 * qb + i] = to_bf16(e * p[qb][kb][i]);
-          }
-#pragma unroll
-        for (int db = 0; db < 4; ++db) {
-          dv[db][kb] = mfma16(tdo[db], P, dv[db][kb]);
-          dk[db][kb] = mfma16(tq[db], D, dk[db][kb]);
-        }
-      }
-    }
-    if (qt + 1 < nqt) {
-      bf16* nb = smem + (buf ^ 1) * TILE;
-      qr.store_sw16(nb, tid);
-      dr.store_sw16(nb + KT * LD_D16, tid);
-      stage_rowc(buf ^ 1, qt + 1, rc_next);
-    }
-    __syncthreads();
-  }
-
-  const float sc = a.scale;
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb) {
-    const int key = kw0 + 16 * kb + c16;
-    if (key < L) {
-      bf16* dkp = a.dk + b * a.bs_dk + (long long)key * a.rs_dk + hh * a.hs;
-      bf16* dvp = a.dv + b * a.bs_dv + (long long)key * a.rs_dv + hh * a.hs;
-#pragma unroll
-      for (int db = 0; db < 4; ++db) {
-        bf16x4 k4, v4;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          k4[i] = to_bf16(dk[db][kb][i] * sc);
-          v4[i] = to_bf16(dv[db][kb][i]);
-        }
-        *(bf16x4*)(dkp + 16 * db + 4 * g) = k4;
-        *(bf16x4*)(dvp + 16 * db + 4 * g) = v4;
-      }
-    }
   }
 }
 
@@ -889,25 +121,6 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkdv16_kernel(AttnAr
 // << 2): conflict-free for the 32x32 row reads and the transposed reads), staged through registers one tile ahead;
 // one barrier per tile, between its two halves (half 1's seg C / D read the next tile).
 constexpr int HS_NW = 4;
-#ifndef LCI_HS_STG
-#define LCI_HS_STG 0   // tile staging: 0 = LDS-DMA into a 4-slot ring; 1 = registers (AGPRs; needs the 2-tile unroll,
-                       // which spills 140 VGPRs): both two tiles ahead
-#endif
-#ifndef LCI_HS_PROBE
-#define LCI_HS_PROBE 0   // timing probes (wrong results): 1 = no barrier, 2 = no tile staging after the prologue,
-                         // 3 = no LDS traffic, staging or barrier in the loop, 4 = no VALU in the loop, 5 / 6 / 7 = no
-                         // transposed-fragment / row-constant / Q-dO row reads
-#endif
-#ifndef LCI_HS_STAMP
-#define LCI_HS_STAMP 0   // diagnostic build: s_memtime at every segment start of tiles 64-95 of workgroups 0-7 (dK/dV),
-                         // written to the dQ part of dqkv, which only the (not launched) dQ stage writes
-#endif
-#ifndef LCI_HS_UNROLL
-#define LCI_HS_UNROLL 1   // dK/dV: 4-tile unroll with compile-time ring slots (0: one runtime-slot loop, for A/B)
-#endif
-#ifndef LCI_HS_V
-#define LCI_HS_V 2   // 1: first placement (conversions in pairs, single fragment set, LDS reads in segs B-D), for A/B
-#endif
 __device__ __forceinline__ int sw128(int row, int col) {
   const int g = ((row >> 2) & 3) | (((row >> 1) & 1) << 2);
   return row * DH + ((((col >> 3) ^ g) << 3) | (col & 7));
@@ -962,30 +175,9 @@ __device__ __forceinline__ void hs_vmcnt() {   // s_waitcnt vmcnt(N), lgkmcnt / 
 #define HS_MFMA_C(d, A, B) \
   asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(A), "a"(B))
 
-#ifndef LCI_HS_AHOME
-#define LCI_HS_AHOME 1       // K / V fragments homed in AGPRs before the loop (0: compiler's choice; unsafe)
-#endif
-#ifndef LCI_HS_TQ
-#define LCI_HS_TQ 0          // 1: dV / dK operands from d-major Q^T / dO^T tiles (attn_bwd_qdoT_kernel), one b128
-#endif                       // each instead of two transposed reads: 21.5 vs 20.85 ms same box (slower)
-#ifndef LCI_HS_LGKM0
-#define LCI_HS_LGKM0 1       // drain the prologue's LDS reads before the loop (see the loop header)
-#endif
-#ifndef LCI_HS_NOFENCE
-#define LCI_HS_NOFENCE 1     // tile barrier without the LDS fence of __syncthreads
-#endif
 // s_waitcnt lgkmcnt(0) with vmcnt / expcnt left at their maxima (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] |
 // lgkmcnt[11:8] | vmcnt[15:14])
 constexpr unsigned LGKM0_WAIT = 0xC07F;
-#ifndef LCI_HS_DMASPREAD
-#define LCI_HS_DMASPREAD 0   // 1: one LDS-DMA issue per segment (21.3 ms vs 20.7 ms for tile t+3's five in seg B
-#endif                       // of half 1, same box)
-#ifndef LCI_HS_RSTG
-#define LCI_HS_RSTG 1     // dK/dV Q / dO / row-constant staging: buffer loads into AGPRs + ds_write (0: LDS-DMA)
-#endif
-#ifndef LCI_HS_RSTG_SEGS
-#define LCI_HS_RSTG_SEGS 2   // half-0 segments of the staging stores (tens) and loads (units)
-#endif
 // 16- / 4-byte LDS stores of AGPR data at a lane address + immediate (asm: no VGPR copy; completion is implied by the
 // compiler's in-order lgkmcnt waits for later reads)
 template <int OFF>
@@ -998,15 +190,14 @@ __device__ __forceinline__ void hs_st4(unsigned addr, uint32_t v) {
 }
 __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArgs a) {
   constexpr int TILE_B = KT * DH * 2;               // bytes of a Q or dO tile (128-B rows)
-  // Q | dO of one tile (LCI_HS_TQ: + the d-major Q^T | dO^T tiles, rows = d, read by the dV / dK products)
-  constexpr int SLOT_B = (LCI_HS_TQ ? 4 : 2) * TILE_B;
+  constexpr int SLOT_B = 2 * TILE_B;                // Q | dO of one tile
   constexpr int RC_B = 2 * KT * 4;                  // -lse2[64] | -delta[64] of one tile
   constexpr int NSLOT = 4;                          // ring: tile t, t+1 (published), t+2, t+3 (in flight)
-  constexpr int NOPS = LCI_HS_TQ ? 9 : 5;           // LDS-DMA operations per wave and tile
+  constexpr int NOPS = 5;                           // LDS-DMA operations per wave and tile (prologue)
   static_assert((NSLOT & (NSLOT - 1)) == 0, "ring slot of tile t is t & (NSLOT - 1)");
-  // without LCI_HS_TQ the Q / dO ring fills exactly 64 KB, so every fragment read of every slot is one lane register
-  // + a 16-bit immediate (slot, dO and row offsets); the row-constant rows follow in their own 2 KB
-  static_assert(LCI_HS_TQ || NSLOT * SLOT_B == 65536, "Q / dO ring reachable by DS immediates");
+  // the Q / dO ring fills exactly 64 KB, so every fragment read of every slot is one lane register + a 16-bit
+  // immediate (slot, dO and row offsets); the row-constant rows follow in their own 2 KB
+  static_assert(NSLOT * SLOT_B == 65536, "Q / dO ring reachable by DS immediates");
   __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT_B + NSLOT * RC_B];
   char* const rcs = smem + NSLOT * SLOT_B;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1016,15 +207,6 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
   const int h = lane >> 5, r32 = lane & 31;
   const int kw0 = blockIdx.x * (HS_NW * 64) + wave * 64;
   const int nqt = (L + KT - 1) / KT;
-  // diagnostic stamps: [workgroup][wave][tile - 64][stamp 0..9] (8 segment starts + before / after the barrier)
-  unsigned long long* stamps = (unsigned long long*)a.out;
-  int stamp_tile = -1;
-  auto stamp = [&](int k) __attribute__((always_inline)) {
-    if (LCI_HS_STAMP && stamp_tile >= 0) {
-      const unsigned long long tm = __builtin_amdgcn_s_memtime();
-      if (lane == 0) stamps[((blockIdx.x * 4 + wave) * 32 + stamp_tile) * 10 + k] = tm;
-    }
-  };
 
   // K^T / V^T as B operands: lane holds K[kw0 + 32kb + r32][16ks + 8h + j] (K prescaled into the exp2 domain)
   bf16x8 kf[2][4], vf[2][4];
@@ -1055,9 +237,9 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      if (LCI_HS_AHOME) { HS_TO_AGPR(kf[i][j]); HS_TO_AGPR(vf[i][j]); }
+      { HS_TO_AGPR(kf[i][j]); HS_TO_AGPR(vf[i][j]); }
 
-  // ---- staging by LDS-DMA, two tiles ahead: wave w copies rows 16w .. 16w+15 of the Q and dO tiles as 1-KB pieces
+  // ---- prologue staging by LDS-DMA: wave w copies rows 16w .. 16w+15 of the Q and dO tiles as 1-KB pieces
   // (8 rows x 128 B, lane l -> row l >> 3 of the piece, physical 16-B chunk l & 7, fetched from the logical chunk
   // (l & 7) ^ g(row) of the sw128 swizzle), and one row of row constants (waves 0 / 2: -lse2, 1 / 3: -delta; the
   // pairs write the same bytes). Rows >= L read as zero: they add nothing to dV or dK whatever P is.
@@ -1065,10 +247,6 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
   const rsrc_t rq = make_rsrc(a.q + b * a.bs_q + hh * a.hs, (uint32_t)(L - 1) * (uint32_t)rs2q + DH * 2);
   const rsrc_t rd = make_rsrc(a.dout + b * a.bs_do + hh * a.hs, (uint32_t)(L - 1) * (uint32_t)rs2d + DH * 2);
   const rsrc_t rr = make_rsrc(a.delta + ((long long)b * a.H + hh) * 2 * L + (wave & 1) * L, (uint32_t)L * 4);
-  // d-major Q^T / dO^T rows (LCI_HS_TQ): row d of (b, hh, which) is Lp bf16; a tile is 128 B at column 64 t
-  const int rs2t = a.Lp * 2;
-  const rsrc_t rqt = make_rsrc(a.qdoT + ((long long)b * a.H + hh) * 2 * 64 * a.Lp, (uint32_t)(64 * rs2t));
-  const rsrc_t rdt = make_rsrc(a.qdoT + (((long long)b * a.H + hh) * 2 + 1) * 64 * a.Lp, (uint32_t)(64 * rs2t));
   // row = 16 wave + 8 j + prow (piece j = 0, 1): g(row) = ((row >> 2) & 3) | ((row >> 1) & 1) << 2 = (2j + (prow >> 2))
   // | ((prow >> 1) & 1) << 2
   const int prow = lane >> 3;
@@ -1076,7 +254,6 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
   const int pch1 = (lane & 7) ^ ((2 + (prow >> 2)) | ((prow >> 1) & 1) << 2);
   const int dq0 = (16 * wave + prow) * rs2q + 16 * pch0, dq1 = (16 * wave + 8 + prow) * rs2q + 16 * pch1;
   const int dd0 = (16 * wave + prow) * rs2d + 16 * pch0, dd1 = (16 * wave + 8 + prow) * rs2d + 16 * pch1;
-  const int dt0 = (16 * wave + prow) * rs2t + 16 * pch0, dt1 = (16 * wave + 8 + prow) * rs2t + 16 * pch1;
   const unsigned lds0 = (unsigned)(uintptr_t)(LCI_LDS char*)smem;
   auto dma_op = [&](int t, int i) __attribute__((always_inline)) {   // operation i (0-4) of tile t
     const unsigned sb = lds0 + (unsigned)((t & (NSLOT - 1)) * SLOT_B);
@@ -1086,40 +263,11 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
     if (i == 3) hs_dma16(rd, dd1, t * KT * rs2d, sb + TILE_B + 2048 * wave + 1024);
     if (i == 4) hs_dma4(rr, lane * 4, t * KT * 4, lds0 + (unsigned)(NSLOT * SLOT_B + (t & (NSLOT - 1)) * RC_B +
                                                                      (wave & 1) * KT * 4));
-    if (LCI_HS_TQ) {   // the d-major tiles: rows = d, the tile's 128 B at byte column 128 t
-      if (i == 5) hs_dma16(rqt, dt0, t * 128, sb + 2 * TILE_B + 2048 * wave);
-      if (i == 6) hs_dma16(rqt, dt1, t * 128, sb + 2 * TILE_B + 2048 * wave + 1024);
-      if (i == 7) hs_dma16(rdt, dt0, t * 128, sb + 3 * TILE_B + 2048 * wave);
-      if (i == 8) hs_dma16(rdt, dt1, t * 128, sb + 3 * TILE_B + 2048 * wave + 1024);
-    }
   };
   auto dma_tile = [&](int t) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < NOPS; ++i) dma_op(t, i);
   };
-  // register staging (LCI_HS_STG 1): thread -> rows (srow, srow + 32), chunk sch of the Q and dO tiles, plus one row
-  // constant per lane in waves 0 / 1; two sets, a tile's loads issued two tiles before its LDS store
-  const int srow = tid >> 3, sch = tid & 7;
-  const int vq0 = srow * rs2q + sch * 16, vq1 = vq0 + 32 * rs2q;
-  const int vd0 = srow * rs2d + sch * 16, vd1 = vd0 + 32 * rs2d;
-  const int st0 = 2 * sw128(srow, sch * 8), st1 = st0 + 32 * 128;
-  struct Stage { u32x4 q0, q1, d0, d1; uint32_t rc; };
-  Stage stg[2];
-  auto load_tile = [&](Stage& g, int t) __attribute__((always_inline)) {   // 5 loads in every wave
-    g.q0 = hs_ld16(rq, vq0, t * KT * rs2q);
-    g.q1 = hs_ld16(rq, vq1, t * KT * rs2q);
-    g.d0 = hs_ld16(rd, vd0, t * KT * rs2d);
-    g.d1 = hs_ld16(rd, vd1, t * KT * rs2d);
-    g.rc = hs_ld4(rr, lane * 4, t * KT * 4);
-  };
-  auto store_tile = [&](const Stage& g, char* slot) __attribute__((always_inline)) {
-    *(u32x4*)(slot + st0) = g.q0;
-    *(u32x4*)(slot + st1) = g.q1;
-    *(u32x4*)(slot + TILE_B + st0) = g.d0;
-    *(u32x4*)(slot + TILE_B + st1) = g.d1;
-    if (wave < 2) *(uint32_t*)(rcs + wave * KT * 4 + lane * 4) = g.rc;   // (register staging: ring slot 0 only)
-  };
-
   // ---- fragment readers. sw128's swizzle depends on row bits 1-3 only, so a row offset that is a multiple of 16
   // (r0, 16 S) is a plain byte offset: the lane part of every read address is one of 9 registers computed here and
   // kept opaque, and slot (compile-time in the unrolled loop), dO, row and row-constant offsets are DS immediates
@@ -1144,8 +292,6 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
   };
   auto trf = [&](int soff, int r0, int S, int db) __attribute__((always_inline)) {
     const int imm = soff + 2 * DH * (r0 + 16 * S);
-    if (LCI_HS_PROBE == 8)   // probe: plain b64 reads of the same addresses (wrong operands)
-      return cat44(*(const bf16x4*)(smem + t_off[db][0] + imm), *(const bf16x4*)(smem + t_off[db][1] + imm));
     return cat44(lds_tr4((const bf16*)(smem + t_off[db][0] + imm)), lds_tr4((const bf16*)(smem + t_off[db][1] + imm)));
   };
   // initial accumulator of a chain: register i <-> query r0 + (i & 3) + 8 (i >> 2) + 4h
@@ -1192,40 +338,22 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
   // gap (8 + 4 + 4 issue cycles beside the MFMA's 8 of 32); gaps 0-2 finish the previous segment's block
   // (pkb, pe): its last two multiplies and three conversions
   auto valu_gap = [&](int g, int kb, int e, int pkb, int pe) __attribute__((always_inline)) {
-    if (LCI_HS_PROBE == 4) return;
-#if LCI_HS_PROBE >= 9 && LCI_HS_PROBE <= 11   // probes: 9 no exps, 10 no multiplies, 11 no conversions
-#define HS_P9(x) if (LCI_HS_PROBE != 9) x
-#define HS_P10(x) if (LCI_HS_PROBE != 10) x
-#define HS_P11(x) if (LCI_HS_PROBE != 11) x
-#else
-#define HS_P9(x) x
-#define HS_P10(x) x
-#define HS_P11(x) x
-#endif
     f32x16& s = S[kb];
     f32x16& p = P[kb];
     const int o = 8 * e, po = 8 * pe;
-    HS_P9(HS_EXP(s[o + g]));
-    if (g >= 2) HS_P10(HS_MUL(p[o + g - 2], s[o + g - 2]));
-    if (g == 0) HS_P10(HS_MUL(P[pkb][po + 6], S[pkb][po + 6]));
-    if (g == 1) HS_P10(HS_MUL(P[pkb][po + 7], S[pkb][po + 7]));
-    if (LCI_HS_V == 1) {
-      if (g == 0) HS_P11(HS_CVT(pk[pkb][pe][3], S[pkb][po + 6], S[pkb][po + 7]));
-      if (g == 0) HS_P11(HS_CVT(dd[pkb][pe][2], P[pkb][po + 4], P[pkb][po + 5]));
-      if (g == 2) HS_P11(HS_CVT(dd[pkb][pe][3], P[pkb][po + 6], P[pkb][po + 7]));
-      if (g == 2 || g == 4 || g == 6) HS_P11(HS_CVT(pk[kb][e][g / 2 - 1], s[o + g - 2], s[o + g - 1]));
-      if (g == 4 || g == 6) HS_P11(HS_CVT(dd[kb][e][g / 2 - 2], p[o + g - 4], p[o + g - 3]));
-      return;
-    }
+    HS_EXP(s[o + g]);
+    if (g >= 2) HS_MUL(p[o + g - 2], s[o + g - 2]);
+    if (g == 0) HS_MUL(P[pkb][po + 6], S[pkb][po + 6]);
+    if (g == 1) HS_MUL(P[pkb][po + 7], S[pkb][po + 7]);
     switch (g) {
-      case 0: HS_P11(HS_CVT(pk[pkb][pe][3], S[pkb][po + 6], S[pkb][po + 7])); break;
-      case 1: HS_P11(HS_CVT(dd[pkb][pe][2], P[pkb][po + 4], P[pkb][po + 5])); break;
-      case 2: HS_P11(HS_CVT(dd[pkb][pe][3], P[pkb][po + 6], P[pkb][po + 7])); break;
-      case 3: HS_P11(HS_CVT(pk[kb][e][0], s[o], s[o + 1])); break;
-      case 4: HS_P11(HS_CVT(pk[kb][e][1], s[o + 2], s[o + 3])); break;
-      case 5: HS_P11(HS_CVT(dd[kb][e][0], p[o], p[o + 1])); break;
-      case 6: HS_P11(HS_CVT(pk[kb][e][2], s[o + 4], s[o + 5])); break;
-      default: HS_P11(HS_CVT(dd[kb][e][1], p[o + 2], p[o + 3])); break;
+      case 0: HS_CVT(pk[pkb][pe][3], S[pkb][po + 6], S[pkb][po + 7]); break;
+      case 1: HS_CVT(dd[pkb][pe][2], P[pkb][po + 4], P[pkb][po + 5]); break;
+      case 2: HS_CVT(dd[pkb][pe][3], P[pkb][po + 6], P[pkb][po + 7]); break;
+      case 3: HS_CVT(pk[kb][e][0], s[o], s[o + 1]); break;
+      case 4: HS_CVT(pk[kb][e][1], s[o + 2], s[o + 3]); break;
+      case 5: HS_CVT(dd[kb][e][0], p[o], p[o + 1]); break;
+      case 6: HS_CVT(pk[kb][e][2], s[o + 4], s[o + 5]); break;
+      default: HS_CVT(dd[kb][e][1], p[o + 2], p[o + 3]); break;
     }
   };
   // MFMA of gap g of a chain segment (S chain at gaps 0-3, dP chain at gaps 4-7) for key block kb
@@ -1244,23 +372,14 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
     else HS_MFMA_G(dv[db][kb], tdo[st][db][s2], pb);
   };
   // transposed fragment f (gradient order: k-step f >> 2, d block (f >> 1) & 1, dO^T | Q^T) of rows r0 into set st
-  bool probe_noread = false;
   auto tr_load = [&](int f, int st, int soff, int r0) __attribute__((always_inline)) {
-    if ((LCI_HS_PROBE == 3 && probe_noread) || LCI_HS_PROBE == 5) return;
     const int s2 = f >> 2, db = (f >> 1) & 1;
-    if (LCI_HS_TQ) {   // d-major tile: lane (h, r32) reads d = 32 db + r32, queries r0 + 16 s2 + 8h .. +7 (pack order)
-      const char* tt = smem + soff + (f & 1 ? 2 : 3) * TILE_B;
-      const bf16x8 v = *(const bf16x8*)(tt + 2 * sw128(32 * db + r32, r0 + 16 * s2 + 8 * h));
-      if (f & 1) tq[st][db][s2] = v; else tdo[st][db][s2] = v;
-      return;
-    }
     if (f & 1) tq[st][db][s2] = trf(soff, r0, s2, db);
     else tdo[st][db][s2] = trf(soff + TILE_B, r0, s2, db);
   };
   // one f32x4 piece (queries 8g + 4h .. + 3 of the half) of a chain's row-constant block; rcoff: the tile's
   // row-constant slot, bytes from the end of the ring
   auto rc_load = [&](f32x16& r, int rcoff, int which, int r0, int g) __attribute__((always_inline)) {
-    if ((LCI_HS_PROBE == 3 && probe_noread) || LCI_HS_PROBE == 6) return;
     const f32x4 v = *(const f32x4*)(smem + rc_off + (rcoff + which * KT * 4 + 4 * (r0 + 8 * g)));
     r[4 * g] = v[0]; r[4 * g + 1] = v[1]; r[4 * g + 2] = v[2]; r[4 * g + 3] = v[3];
   };
@@ -1275,7 +394,6 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
       __attribute__((always_inline)) {
     constexpr int C = decltype(CUR)::value;
     // seg A: chains kb0 || VALU kb1 (p-1) elements 8-15 (finishing its elements 0-7)
-    stamp(4 * C + 0);
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
       chain_gap(g, 0);
@@ -1285,7 +403,6 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
     }
     mid();
     // seg B: dV / dK kb1 (p-1, set C^1) || VALU kb0 elements 0-7 (finishing kb1 8-15)
-    stamp(4 * C + 1);
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
       grad_gap(g, 1, C ^ 1);
@@ -1294,67 +411,32 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
       sgap(1, g);
     }
     // seg C: chains kb1 || VALU kb0 elements 8-15
-    stamp(4 * C + 2);
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
       chain_gap(g, 1);
       valu_gap(g, 0, 1, 0, 0);
       if (g == 2) HS_KEEP(NL);
       if (g == 6) HS_KEEP(ND);
-      if (g >= 2 && g < 6 && LCI_HS_PROBE != 3 && LCI_HS_PROBE != 7) qa[g - 2] = qrow(nslot, nr0, g - 2);
+      if (g >= 2 && g < 6) qa[g - 2] = qrow(nslot, nr0, g - 2);
       if (g >= 6) {
         rc_load(NL, nrc, 0, nr0, g - 6);
-        if (LCI_HS_PROBE != 3 && LCI_HS_PROBE != 7) da[g - 6] = qrow(nslot + TILE_B, nr0, g - 6);
+        da[g - 6] = qrow(nslot + TILE_B, nr0, g - 6);
       }
       sgap(2, g);
     }
     // seg D: dV / dK kb0 (set C) || VALU kb1 elements 0-7 (finishing kb0 8-15)
-    stamp(4 * C + 3);
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
       grad_gap(g, 0, C);
       valu_gap(g, 1, 0, 0, 1);
       if (g < 2) rc_load(NL, nrc, 0, nr0, g + 2);
       else if (g < 6) rc_load(ND, nrc, 1, nr0, g - 2);
-      else if (LCI_HS_PROBE != 3 && LCI_HS_PROBE != 7) da[g - 4] = qrow(nslot + TILE_B, nr0, g - 4);
+      else da[g - 4] = qrow(nslot + TILE_B, nr0, g - 4);
       sgap(3, g);
     }
   };
 
-  auto half_v1 = [&](auto CUR, int slot, int r0, int nslot, int nrc, int nr0, auto mid, auto sgap)
-      __attribute__((always_inline)) {
-    constexpr int C = 0;   // one fragment set, each fragment reloaded two gaps after its last read
-#pragma unroll
-    for (int g = 0; g < 8; ++g) {
-      chain_gap(g, 0);
-      valu_gap(g, 1, 1, 1, 0);
-    }
-    mid();
-#pragma unroll
-    for (int g = 0; g < 8; ++g) {
-      grad_gap(g, 1, C);
-      valu_gap(g, 0, 0, 1, 1);
-      if (g >= 2) tr_load(g - 2, C, slot, r0);
-      sgap(1, g);
-    }
-#pragma unroll
-    for (int g = 0; g < 8; ++g) {
-      chain_gap(g, 1);
-      valu_gap(g, 0, 1, 0, 0);
-      if (g < 2) tr_load(6 + g, C, slot, r0);
-      if (g >= 4) qa[g - 4] = qrow(nslot, nr0, g - 4);
-    }
-#pragma unroll
-    for (int g = 0; g < 8; ++g) {
-      grad_gap(g, 0, C);
-      valu_gap(g, 1, 0, 0, 1);
-      if (g == 0) NL = rcblk(rcs + nrc, 0, nr0);
-      if (g == 1) ND = rcblk(rcs + nrc, 1, nr0);
-      if (g >= 4) da[g - 4] = qrow(nslot + TILE_B, nr0, g - 4);
-    }
-  };
-
-  // register staging (LCI_HS_RSTG, as the forward / dQ): tile t+1's Q / dO pieces and row constants (loaded into
+  // register staging (as the forward / dQ): tile t+1's Q / dO pieces and row constants (loaded into
   // AGPRs during tile t-1) are stored at seg A gaps 1-7 / seg B gap 1 of tile t's half 0, tile t+2's loaded at seg C
   // gaps 1-7 / seg D gap 1; half 1's barrier publishes tile t+1
   u32x4 rsq[4];
@@ -1368,32 +450,10 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
     if (i == 3) rsq[3] = hs_ld16(rd, dd1, t * KT * rs2d);
     if (i == 4) rsr = hs_ld4(rr, lane * 4, t * KT * 4);
   };
-  constexpr bool RSTG = LCI_HS_RSTG && LCI_HS_STG == 0 && !LCI_HS_TQ && LCI_HS_PROBE == 0;
-  // prologue: tiles 0, 1, 2 in flight (5 memory operations per wave and tile); wait for tile 0, publish it
-  if constexpr (RSTG) {
-    dma_tile(0);
-    ld_piece(1, 0); ld_piece(1, 1); ld_piece(1, 2); ld_piece(1, 3); ld_piece(1, 4);
-    hs_vmcnt<0>();
-  } else if constexpr (LCI_HS_STG == 0) {
-    dma_tile(0);
-    if (nqt > 1) dma_tile(1);
-    // tile 2's operations 3-4 come at segs A / B of tile 0 (the loop has no first-tile special case: a peeled copy
-    // would let the compiler fold the zero-initialised state into moves beside the asm MFMAs)
-    constexpr bool SPREAD = LCI_HS_DMASPREAD && !LCI_HS_TQ && LCI_HS_PROBE != 2 && LCI_HS_PROBE != 3;
-    if (nqt > 2) {
-      if (SPREAD) { dma_op(2, 0); dma_op(2, 1); dma_op(2, 2); } else dma_tile(2);
-    }
-    if (LCI_HS_PROBE == 2 && nqt > 3) dma_tile(3);   // probe: every ring slot holds real data
-    if (LCI_HS_PROBE == 2) hs_vmcnt<0>();
-    if (nqt > 2) { if (SPREAD) hs_vmcnt<8>(); else hs_vmcnt<2 * NOPS>(); }
-    else if (nqt > 1) hs_vmcnt<NOPS>(); else hs_vmcnt<0>();
-  } else {
-    load_tile(stg[0], 0);
-    hs_vmcnt<0>();
-    store_tile(stg[0], smem);
-    if (nqt > 1) load_tile(stg[1], 1);
-    if (nqt > 2) load_tile(stg[0], 2);
-  }
+  // prologue: tile 0 by LDS-DMA, tile 1 into the staging registers (5 memory operations per wave and tile)
+  dma_tile(0);
+  ld_piece(1, 0); ld_piece(1, 1); ld_piece(1, 2); ld_piece(1, 3); ld_piece(1, 4);
+  hs_vmcnt<0>();
   __syncthreads();
   NL = rcblk(rcs, 0, 0);
   ND = rcblk(rcs, 1, 0);
@@ -1402,59 +462,25 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
     qa[ks] = qrow(0, 0, ks);
     da[ks] = qrow(TILE_B, 0, ks);
   }
-  if (LCI_HS_PROBE == 3) {   // probe: real data in every fragment, then no LDS reads in the loop
-#pragma unroll
-    for (int f = 0; f < 8; ++f) { tr_load(f, 0, 0, 0); tr_load(f, 1, 0, 32); }
-    probe_noread = true;
-  }
   // the prologue's reads complete here (a waitcnt the compiler's pass sees): otherwise its wait for them, merged
   // into the loop header with the back edge's, makes every tile start with lgkmcnt(1)
-  if (LCI_HS_LGKM0) __builtin_amdgcn_s_waitcnt(LGKM0_WAIT);
+  __builtin_amdgcn_s_waitcnt(LGKM0_WAIT);
   // one tile in ring slot SL (compile-time in the 4-tile unroll: every fragment read is a DS immediate off one of
-  // the lane registers above) or, SL < 0, t & 3 at run time; register staging: tile t+1 is in set PAR ^ 1, which
-  // then takes tile t+3
-  auto tile = [&](auto PAR, auto SL, int t) __attribute__((always_inline)) {
-    constexpr int P1 = decltype(PAR)::value ^ 1;
+  // the lane registers above) or, SL < 0, t & 3 at run time
+  auto tile = [&](auto SL, int t) __attribute__((always_inline)) {
     constexpr int SLC = decltype(SL)::value;
     const int sl = SLC >= 0 ? SLC : t & (NSLOT - 1), nsl = SLC >= 0 ? (SLC + 1) & (NSLOT - 1) : (t + 1) & (NSLOT - 1);
-    stamp_tile = (LCI_HS_STAMP && blockIdx.x < 8 && blockIdx.y == 0 && blockIdx.z == 0 && t >= 64 && t < 96) ? t - 64 : -1;
     const int slot = sl * SLOT_B, nslot = nsl * SLOT_B, rc = sl * RC_B, nrc = nsl * RC_B;
-    // tile t+1 is published after seg A of half 1 (seg C of half 1 is its first reader): each wave waits for its
-    // own copy of tile t+1 (tile t+2's may stay in flight), then one barrier; tile t+3 goes into the slot of tile
-    // t-1, which every wave finished before this barrier
+    // tile t+1 (stored from registers in half 0) is published after seg A of half 1 (seg C of half 1 is its first
+    // reader): one barrier; no LDS fence: the stores were ordered by the waits of this wave's own later reads
     auto stage = [&]() __attribute__((always_inline)) {
-      if (t + 1 < nqt) {
-        if (!RSTG) { if (t + 2 < nqt) hs_vmcnt<NOPS>(); else hs_vmcnt<0>(); }
-        if constexpr (LCI_HS_STG == 1) store_tile(stg[P1], smem + nslot);
-        stamp(8);
-        // no LDS fence: this wave's reads of the slot tile t+3 overwrites were consumed before now, and the new
-        // tile's bytes are ordered by the vmcnt above (register staging stores to LDS: that one needs the fence)
-        if (LCI_HS_PROBE != 1 && LCI_HS_PROBE != 3) {
-          if (LCI_HS_STG == 1 || !LCI_HS_NOFENCE) __syncthreads();
-          else __builtin_amdgcn_s_barrier();
-        }
-        stamp(9);
-        if constexpr (LCI_HS_STG == 1)
-          if (t + 3 < nqt && LCI_HS_PROBE != 2) load_tile(stg[P1], t + 3);
-      }
+      if (t + 1 < nqt) __builtin_amdgcn_s_barrier();
     };
-    // LDS-DMA: one operation per segment, at gap 3 (a DMA issue stalls the wave ~60-80 cycles; five in one
-    // segment doubled it): tile t+3's operations 0-2 in segments B, C, D of half 1 (after this tile's barrier),
-    // operations 3-4 in segments A, B of the next tile's half 0 (still before the next barrier, whose vmcnt(5)
-    // then leaves exactly them in flight; tile 2's come at tile 0, the prologue issued only its operations 0-2)
-    constexpr bool DMA_ON = LCI_HS_STG == 0 && LCI_HS_PROBE != 2 && LCI_HS_PROBE != 3 && !RSTG;
-    auto dmas1 = [&](int seg, int g) __attribute__((always_inline)) {
-      if (LCI_HS_DMASPREAD && !LCI_HS_TQ) {
-        if (DMA_ON && g == 3 && seg >= 1 && t + 3 < nqt) dma_op(t + 3, seg - 1);
-      } else if (DMA_ON && seg == 1 && g < 5 && t + 3 < nqt) {
-        dma_op(t + 3, g);
-      } else if (DMA_ON && LCI_HS_TQ && seg == 2 && g < 4 && t + 3 < nqt) {   // the d-major pieces in seg C
-        dma_op(t + 3, 5 + g);
-      }
-    };
+    // half 0: tile t+1's pieces (loaded a tile ago) stored at seg A gaps 1-7 and seg B gap 1... (SS = 0), tile t+2's
+    // loaded at seg C gaps 1-7 (LS = 2)
     auto rstg0 = [&](int seg, int g) __attribute__((always_inline)) {
       if (!(g & 1)) return;
-      constexpr int SS = LCI_HS_RSTG_SEGS / 10, LS = LCI_HS_RSTG_SEGS % 10;   // store / load segments of half 0
+      constexpr int SS = 0, LS = 2;   // store / load segments of half 0
       if (seg == SS && g == 1) hs_vmcnt<0>();   // tile t+1's pieces (loaded a tile ago)
       constexpr int S1 = SLC >= 0 ? ((SLC + 1) & (NSLOT - 1)) * SLOT_B : 0;
       constexpr int R1 = SLC >= 0 ? ((SLC + 1) & (NSLOT - 1)) * RC_B : 0;
@@ -1473,37 +499,20 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
         if (g == 7) ld_piece(t + 2, 4);
       }
     };
-    auto dmas0 = [&](int seg, int g) __attribute__((always_inline)) {
-      if (LCI_HS_DMASPREAD && !LCI_HS_TQ && DMA_ON && g == 3 && seg < 2 && t + 2 < nqt) dma_op(t + 2, 3 + seg);
-    };
     auto none = []() __attribute__((always_inline)) {};
-    if constexpr (LCI_HS_V == 1) {
-      half_v1(std::integral_constant<int, 0>{}, slot, 0, slot, rc, 32, none, dmas0);    // segs C / D: rows 32-63
-      half_v1(std::integral_constant<int, 1>{}, slot, 32, nslot, nrc, 0, stage, dmas1); // ... tile t+1's rows 0-31
-    } else {
-      if constexpr (RSTG) half(std::integral_constant<int, 0>{}, slot, 0, slot, rc, 32, none, rstg0);
-      else half(std::integral_constant<int, 0>{}, slot, 0, slot, rc, 32, none, dmas0);
-      half(std::integral_constant<int, 1>{}, slot, 32, nslot, nrc, 0, stage, dmas1);
-    }
+    auto nogap = [](int, int) __attribute__((always_inline)) {};
+    half(std::integral_constant<int, 0>{}, slot, 0, slot, rc, 32, none, rstg0);    // segs C / D: rows 32-63
+    half(std::integral_constant<int, 1>{}, slot, 32, nslot, nrc, 0, stage, nogap); // ... tile t+1's rows 0-31
   };
-  using IZ = std::integral_constant<int, 0>;
-  if constexpr (LCI_HS_STG == 0) {
-    int t = 0;
-    if (LCI_HS_UNROLL)
-      for (; t + 4 <= nqt; t += 4) {   // t & 3 == 0 here
-        tile(IZ{}, IZ{}, t);
-        tile(IZ{}, std::integral_constant<int, 1>{}, t + 1);
-        tile(IZ{}, std::integral_constant<int, 2>{}, t + 2);
-        tile(IZ{}, std::integral_constant<int, 3>{}, t + 3);
-      }
-    for (; t < nqt; ++t) tile(IZ{}, std::integral_constant<int, -1>{}, t);
-  } else {
-    for (int t = 0; t < nqt; t += 2) {
-      tile(IZ{}, std::integral_constant<int, -1>{}, t);
-      if (t + 1 < nqt) tile(std::integral_constant<int, 1>{}, std::integral_constant<int, -1>{}, t + 1);
-    }
+  int t = 0;
+  for (; t + 4 <= nqt; t += 4) {   // t & 3 == 0 here
+    tile(std::integral_constant<int, 0>{}, t);
+    tile(std::integral_constant<int, 1>{}, t + 1);
+    tile(std::integral_constant<int, 2>{}, t + 2);
+    tile(std::integral_constant<int, 3>{}, t + 3);
   }
-  if (RSTG) hs_vmcnt<0>();   // the last tiles' staging loads (past the end: zeros) retire
+  for (; t < nqt; ++t) tile(std::integral_constant<int, -1>{}, t);
+  hs_vmcnt<0>();   // the last tiles' staging loads (past the end: zeros) retire
   // key block 1 of the last half: elements 8-15 (finishing 0-7), then its dV / dK
 #pragma unroll
   for (int g = 0; g < 8; ++g) valu_gap(g, 1, 1, 1, 0);
@@ -1515,7 +524,7 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
   HS_CVT(dd[1][1][3], P[1][14], P[1][15]);
   asm volatile("s_nop 1" ::: "memory");
 #pragma unroll
-  for (int g = 0; g < 8; ++g) grad_gap(g, 1, LCI_HS_V == 1 ? 0 : 1);   // the last half is a half 1 (set 1)
+  for (int g = 0; g < 8; ++g) grad_gap(g, 1, 1);   // the last half is a half 1 (set 1)
   // the accumulators are read by VALU next: let the last MFMAs retire (the compiler cannot see their latency)
   asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
 
@@ -1546,7 +555,8 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
 // --------------------------------------- backward: dQ kernel, one wave per SIMD, placed MFMA / VALU / LDS stream
 // The dK/dV kernel's structure for dQ (query on the MFMA lane): a workgroup = 4 waves, a wave owns 64 queries (two
 // query blocks of 32, Q~ / dO fragments in AGPRs, -lse2 / -delta splats as the chains' initial accumulators, dQ^T in
-// AGPRs), key tiles of 64 keys (K, V; 128-B sw128 rows) arrive by LDS-DMA into a 4-slot ring two tiles ahead.
+// AGPRs), key tiles of 64 keys (K, V; 128-B sw128 rows) arrive in a 4-slot ring, staged through AGPRs one tile
+// ahead (buffer loads during tile t-1, ds_write during tile t's half 0).
 // Per 32-key half-tile and wave: 24 MFMAs (S^T = K Q~^T and dP^T = V dO^T chains, 4 + 4 per query block;
 // dQ^T += K^T dS^T, 4 per block) against 32 exp2 + 32 multiplies + 16 conversions. MFMA order per half:
 //   gaps 0-7: chains of block 0 | 8-11: dQ^T of block 1 (previous half) | 12-19: chains of block 1 |
@@ -1605,22 +615,7 @@ constexpr unsigned char DQ_SCHED[24][4] = {
     {0xa0, 0xa1, 0x64, 0x65},
     {0x66, 0x67, 0xa2, 0xa3}};
 
-#ifndef LCI_DQ_RSTG
-#define LCI_DQ_RSTG 1     // dQ K / V staging: buffer loads into AGPRs + ds_write_b128 (0: LDS-DMA)
-#endif
-#ifndef LCI_FWD_RSTG
-#define LCI_FWD_RSTG 1    // K / V staging in the loop: 1 = buffer loads into AGPRs + ds_write_b128, 0 = LDS-DMA
-#endif
 
-#ifndef LCI_DQ_AHOME
-#define LCI_DQ_AHOME 1       // Q~ / dO fragments homed in AGPRs before the loop
-#endif
-#ifndef LCI_DQ_DMASPREAD
-#define LCI_DQ_DMASPREAD 1   // DMA issues at gaps 8 / 20 (half 1) and 6 / 18 (half 0); 0: gaps 6-8, 15 of half 1
-#endif
-#ifndef LCI_DQ_V2
-#define LCI_DQ_V2 0          // 1: LDS reads >= 8 gaps ahead of their MFMAs (16.6 vs 15.9 ms same box: slower)
-#endif
 __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs a) {
   constexpr int TILE_B = KT * DH * 2;               // bytes of a K or V tile (128-B rows)
   constexpr int SLOT_B = 2 * TILE_B;                // K | V
@@ -1669,9 +664,9 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      if (LCI_DQ_AHOME) { HS_TO_AGPR(qf[i][j]); HS_TO_AGPR(df[i][j]); }
+      { HS_TO_AGPR(qf[i][j]); HS_TO_AGPR(df[i][j]); }
 
-  // ---- K / V tiles by LDS-DMA, two tiles ahead (wave w: rows 16w .. 16w+15 of each, 1-KB pieces of 8 rows)
+  // ---- K / V tile pieces (wave w: rows 16w .. 16w+15 of each, 1-KB pieces of 8 rows): tile 0 by LDS-DMA
   const int rs2k = a.rs_k * 2, rs2v = a.rs_v * 2;
   const rsrc_t rk = make_rsrc(a.k + b * a.bs_k + hh * a.hs, (uint32_t)(L - 1) * (uint32_t)rs2k + DH * 2);
   const rsrc_t rv = make_rsrc(a.v + b * a.bs_v + hh * a.hs, (uint32_t)(L - 1) * (uint32_t)rs2v + DH * 2);
@@ -1722,8 +717,8 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
     for (int j = 0; j < 2; ++j) dq[i][j] = f32x16{};
   }
   u32x4 dsp[2][2] = {};        // [query block][k-step] bf16 dS^T packs
-  // [set][d block][k-step][half of the fragment] transposed K (keys as the k index); LCI_DQ_V2: half p's in set
-  // p & 1 (read at its gaps 0-7, while dQ^T of block 1 still uses half p-1's set), else one set
+  // [set][d block][k-step][half of the fragment] transposed K (keys as the k index). Only set 0 is read; set 1 is
+  // an opaque dead copy that keeps the register allocation (and so the placed stream) of the measured build
   bf16x4 ktr[2][2][2][2] = {};
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -1747,48 +742,39 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
     else if (kind == 1) HS_MUL(P[qb][i], S[qb][i]);
     else HS_CVT(dsp[qb][i >> 2][i & 3], P[qb][2 * i], P[qb][2 * i + 1]);
   };
-  // k = 0..3: (d block k & 1, k-step k >> 1) with transposed-K set st
-  auto dq_mfma = [&](int k, int qb, int st) __attribute__((always_inline)) {
+  // k = 0..3: (d block k & 1, k-step k >> 1)
+  auto dq_mfma = [&](int k, int qb) __attribute__((always_inline)) {
     const int db = k & 1, s2 = k >> 1;
-    HS_MFMA_G(dq[db][qb], cat44(ktr[st][db][s2][0], ktr[st][db][s2][1]), __builtin_bit_cast(bf16x8, dsp[qb][s2]));
+    HS_MFMA_G(dq[db][qb], cat44(ktr[0][db][s2][0], ktr[0][db][s2][1]), __builtin_bit_cast(bf16x8, dsp[qb][s2]));
   };
-  auto mfma_gap = [&](int g, int C) __attribute__((always_inline)) {   // C: this half's transposed-K set
+  auto mfma_gap = [&](int g) __attribute__((always_inline)) {
     if (g < 4) {
       if (g == 0) HS_MFMA_C0(S[0], kr[0], qf[0][0], NL[0]); else HS_MFMA_C(S[0], kr[g], qf[0][g]);
     } else if (g < 8) {
       if (g == 4) HS_MFMA_C0(P[0], vr[0], df[0][0], ND[0]); else HS_MFMA_C(P[0], vr[g - 4], df[0][g - 4]);
     } else if (g < 12) {
-      dq_mfma(g - 8, 1, LCI_DQ_V2 ? C ^ 1 : 0);   // (one transposed-K set without LCI_DQ_V2)
+      dq_mfma(g - 8, 1);
     } else if (g < 16) {
       if (g == 12) HS_MFMA_C0(S[1], kr[0], qf[1][0], NL[1]); else HS_MFMA_C(S[1], kr[g - 12], qf[1][g - 12]);
     } else if (g < 20) {
       if (g == 16) HS_MFMA_C0(P[1], vr[0], df[1][0], ND[1]); else HS_MFMA_C(P[1], vr[g - 16], df[1][g - 16]);
     } else {
-      dq_mfma(g - 20, 0, C);
+      dq_mfma(g - 20, 0);
     }
   };
 
-  // One 32-key half (rows r0 of `slot`, transposed-K set SET); the next half's rows are rows nr0 of `nslot`.
-  // LCI_DQ_V2 reads: this half's transposed K at gaps 0-7 (used at 20-23), the next half's K rows at 16-19 (after
-  // their last use by the chains at 12-15; used at its gaps 0-3 and 12-15) and V rows at 20-23 (after 16-19; used
-  // at its 4-7, 16-19): every read >= 8 gaps ahead. Else: V rows at 0-3, transposed K at 12-19, K rows at 20-23.
-  auto half = [&](auto SET, int soff, int r0i, int nsoff, int nr0i, auto hook) __attribute__((always_inline)) {
-    constexpr int C = LCI_DQ_V2 ? decltype(SET)::value : 0;
+  // One 32-key half (rows r0i of slot soff); the next half's rows are rows nr0i of slot nsoff. LDS reads: V rows at
+  // gaps 0-3, transposed K at 12-19, the next half's K rows at 20-23.
+  auto half = [&](int soff, int r0i, int nsoff, int nr0i, auto hook) __attribute__((always_inline)) {
 #pragma unroll
     for (int g = 0; g < 24; ++g) {
-      mfma_gap(g, C);
+      mfma_gap(g);
       // gaps 9 / 21 multiply the dP^T chain of block 0 / 1 (last MFMA at gap 7 / 19): 12 wait states by
       // instruction count
       if (g == 9 || g == 21) asm volatile("s_nop 5" ::: "memory");
 #pragma unroll
       for (int o = 0; o < 4; ++o) valu_op(DQ_SCHED[g][o], -1);
-      if (LCI_DQ_V2) {
-        if (g < 8) {
-          const int f = g >> 1, part = g & 1;   // fragment f = (d block f & 1, k-step f >> 1)
-          ktr[C][f & 1][f >> 1][part] = trh(soff, r0i, f, part);
-        } else if (g >= 16 && g < 20) kr[g - 16] = row(nsoff, nr0i, g - 16);
-        else if (g >= 20) vr[g - 20] = row(nsoff + TILE_B, nr0i, g - 20);
-      } else if (g < 4) vr[g] = row(soff + TILE_B, r0i, g);
+      if (g < 4) vr[g] = row(soff + TILE_B, r0i, g);
       else if (g >= 12 && g < 20) {
         const int f = (g - 12) >> 1, part = (g - 12) & 1;
         ktr[0][f & 1][f >> 1][part] = trh(soff, r0i, f, part);
@@ -1797,7 +783,7 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
     }
   };
 
-  // register staging (LCI_DQ_RSTG, as the forward's LCI_FWD_RSTG): tile t+1's pieces (loaded into AGPRs during tile
+  // register staging (as the forward's): tile t+1's pieces (loaded into AGPRs during tile
   // t-1) are stored at gaps 1-7 of tile t's half 0, tile t+2's loaded at gaps 9-15; half 1's barrier publishes t+1
   u32x4 stg[4];
   const unsigned wst = lds0 + 2048 * wave + 16 * lane;
@@ -1807,74 +793,41 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
     if (i == 2) stg[2] = hs_ld16(rv, dv0, t * KT * rs2v);
     if (i == 3) stg[3] = hs_ld16(rv, dv1, t * KT * rs2v);
   };
-  // prologue: tiles 0, 1, 2 in flight; wait for tile 0, publish it; K rows of half 0
+  // prologue: tile 0 by LDS-DMA, tile 1 into the staging registers; wait, publish tile 0; K rows of half 0
   dma_op(0, 0); dma_op(0, 1); dma_op(0, 2); dma_op(0, 3);
-  if (LCI_DQ_RSTG) {
-    ld_piece(1, 0); ld_piece(1, 1); ld_piece(1, 2); ld_piece(1, 3);
-    hs_vmcnt<0>();
-  } else {
-    if (nkt > 1) { dma_op(1, 0); dma_op(1, 1); dma_op(1, 2); dma_op(1, 3); }
-    if (nkt > 2) {   // (spread: tile 2's operations 2-3 at gaps 6 / 18 of tile 0, as for every later tile)
-      dma_op(2, 0); dma_op(2, 1);
-      if (!LCI_DQ_DMASPREAD) { dma_op(2, 2); dma_op(2, 3); }
-    }
-    if (nkt > 2) { if (LCI_DQ_DMASPREAD) hs_vmcnt<6>(); else hs_vmcnt<8>(); }
-    else if (nkt > 1) hs_vmcnt<4>(); else hs_vmcnt<0>();
-  }
+  ld_piece(1, 0); ld_piece(1, 1); ld_piece(1, 2); ld_piece(1, 3);
+  hs_vmcnt<0>();
   __builtin_amdgcn_s_barrier();
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    kr[ks] = row(0, 0, ks);
-    if (LCI_DQ_V2) vr[ks] = row(TILE_B, 0, ks);
-  }
-  if (LCI_HS_LGKM0) __builtin_amdgcn_s_waitcnt(LGKM0_WAIT);   // (see the dK/dV kernel's loop header)
+  for (int ks = 0; ks < 4; ++ks) kr[ks] = row(0, 0, ks);
+  __builtin_amdgcn_s_waitcnt(LGKM0_WAIT);   // (see the dK/dV kernel's loop header)
 
   // SL >= 0: tile t sits in ring slot SL (compile-time: DS immediates); SL < 0: slot t & 3 at run time
   auto tile = [&](auto SL, int t) __attribute__((always_inline)) {
     constexpr int sl = decltype(SL)::value;
     const int soff = sl >= 0 ? sl * SLOT_B : (t & (NSLOT - 1)) * SLOT_B;
     const int nsoff = sl >= 0 ? ((sl + 1) & (NSLOT - 1)) * SLOT_B : ((t + 1) & (NSLOT - 1)) * SLOT_B;
-    // tile t+1 is published at gap 6 of half 1 (its first reader: the K rows at gaps 16-19, V2, or 20-23); tile t+3's DMA goes
-    // into the slot of tile t-1 (last read by half 1 of tile t-1, before this barrier), one operation per gap
+    // tile t+1 is published at gap 6 of half 1 (its first reader: the K rows at gaps 20-23)
     auto stage = [&](int g) __attribute__((always_inline)) {
-      if (t + 1 < nkt && g == 6) {
-        if (!LCI_DQ_RSTG) { if (t + 2 < nkt) hs_vmcnt<4>(); else hs_vmcnt<0>(); }
-        __builtin_amdgcn_s_barrier();
-      }
-      if (LCI_DQ_RSTG) return;
-      // tile t+3's operations 0-1 at gaps 8 / 20 of half 1 (after this barrier), 2-3 at gaps 6 / 18 of the next
-      // tile's half 0 (before its barrier, whose vmcnt(4) then leaves exactly them in flight): one DMA issue per
-      // 12 gaps (each stalls the wave's issue ~60-80 cycles)
-      if (LCI_DQ_DMASPREAD) {
-        if (t + 3 < nkt && (g == 8 || g == 20)) dma_op(t + 3, g == 8 ? 0 : 1);
-      } else if (t + 3 < nkt && t + 1 < nkt) {
-        if (g == 6) dma_op(t + 3, 0);
-        if (g == 7) dma_op(t + 3, 1);
-        if (g == 8) dma_op(t + 3, 2);
-        if (g == 15) dma_op(t + 3, 3);
-      }
+      if (t + 1 < nkt && g == 6) __builtin_amdgcn_s_barrier();
     };
     auto stage0 = [&](int g) __attribute__((always_inline)) {
-      if (LCI_DQ_RSTG) {
-        if (g == 1) hs_vmcnt<0>();   // tile t+1's pieces (loaded a tile ago)
-        if (g < 8 && (g & 1)) {
-          constexpr int S1 = sl >= 0 ? ((sl + 1) & (NSLOT - 1)) * SLOT_B : 0;
-          const unsigned base = sl >= 0 ? wst : wst + (unsigned)(((t + 1) & (NSLOT - 1)) * SLOT_B);
-          switch (g) {
-            case 1: hs_st16<S1>(base, stg[0]); break;
-            case 3: hs_st16<S1 + 1024>(base, stg[1]); break;
-            case 5: hs_st16<S1 + TILE_B>(base, stg[2]); break;
-            default: hs_st16<S1 + TILE_B + 1024>(base, stg[3]); break;
-          }
-        } else if (g >= 9 && g < 16 && (g & 1)) {
-          ld_piece(t + 2, (g - 9) >> 1);
+      if (g == 1) hs_vmcnt<0>();   // tile t+1's pieces (loaded a tile ago)
+      if (g < 8 && (g & 1)) {
+        constexpr int S1 = sl >= 0 ? ((sl + 1) & (NSLOT - 1)) * SLOT_B : 0;
+        const unsigned base = sl >= 0 ? wst : wst + (unsigned)(((t + 1) & (NSLOT - 1)) * SLOT_B);
+        switch (g) {
+          case 1: hs_st16<S1>(base, stg[0]); break;
+          case 3: hs_st16<S1 + 1024>(base, stg[1]); break;
+          case 5: hs_st16<S1 + TILE_B>(base, stg[2]); break;
+          default: hs_st16<S1 + TILE_B + 1024>(base, stg[3]); break;
         }
-        return;
+      } else if (g >= 9 && g < 16 && (g & 1)) {
+        ld_piece(t + 2, (g - 9) >> 1);
       }
-      if (LCI_DQ_DMASPREAD && t + 2 < nkt && (g == 6 || g == 18)) dma_op(t + 2, g == 6 ? 2 : 3);
     };
-    half(std::integral_constant<int, 0>{}, soff, 0, soff, 1, stage0);
-    half(std::integral_constant<int, 1>{}, soff, 1, nsoff, 0, stage);
+    half(soff, 0, soff, 1, stage0);
+    half(soff, 1, nsoff, 0, stage);
   };
   {
     int t = 0;
@@ -1886,7 +839,7 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
     }
     for (; t < nkt; ++t) tile(std::integral_constant<int, -1>{}, t);
   }
-  if (LCI_DQ_RSTG) hs_vmcnt<0>();   // the last tiles' staging loads (past the end: zeros) retire
+  hs_vmcnt<0>();   // the last tiles' staging loads (past the end: zeros) retire
   // query block 1 of the last half: its remaining VALU (wrapped into gaps 0-5) and its dQ^T
 #pragma unroll
   for (int g = 0; g < 12; ++g) {
@@ -1894,7 +847,7 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
     for (int o = 0; o < 4; ++o) valu_op(DQ_SCHED[g][o], 1);
     if (g >= 8) {
       asm volatile("s_nop 1" ::: "memory");
-      dq_mfma(g - 8, 1, LCI_DQ_V2 ? 1 : 0);   // the last half is a half 1
+      dq_mfma(g - 8, 1);   // the last half is a half 1
     }
   }
   asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
@@ -1964,73 +917,11 @@ constexpr unsigned char FW_SCHED[16][5] = {
     {0x20, 0x21, 0x87, 0x4e, 0x4f},
     {0xa0, 0x60, 0x61, 0x22, 0x23},
     {0x62, 0xa1, 0x63, 0x24, 0x25}};
-// LCI_FWD_MSUM: the row sums as MFMAs (ones . P^T per k-step, 4 per half) instead of 32 VALU adds; 20 gaps per half
-//   0-3 S^T chain block 0 | 4-7 O^T block 1 (previous half) | 8-9 sums block 1 | 10-13 S^T chain block 1 |
-//   14-17 O^T block 0 | 18-19 sums block 0, against 32 exp2 + 16 packs (tools/gen_fwd_sched_ms.py):
-// gap  0: E1.10 C1.4 E1.11
-// gap  1: E1.12 C1.5 E1.13
-// gap  2: E1.14 C1.6 E1.15
-// gap  3: C1.7
-// gap  4: 
-// gap  5: E0.0 E0.1
-// gap  6: E0.2 C0.0 E0.3
-// gap  7: E0.4 C0.1 E0.5
-// gap  8: E0.6 C0.2 E0.7
-// gap  9: E0.8 C0.3 E0.9
-// gap 10: E0.10 C0.4 E0.11
-// gap 11: E0.12 C0.5 E0.13
-// gap 12: E0.14 C0.6 E0.15
-// gap 13: C0.7
-// gap 14: 
-// gap 15: E1.0 E1.1
-// gap 16: E1.2 C1.0 E1.3
-// gap 17: E1.4 C1.1 E1.5
-// gap 18: E1.6 C1.2 E1.7
-// gap 19: E1.8 C1.3 E1.9
-constexpr int FW_MS_START_E1 = 15;
-constexpr unsigned char FW_SCHED_MS[20][3] = {
-    {0x2a, 0xa4, 0x2b},
-    {0x2c, 0xa5, 0x2d},
-    {0x2e, 0xa6, 0x2f},
-    {0xa7, 0xff, 0xff},
-    {0xff, 0xff, 0xff},
-    {0x00, 0x01, 0xff},
-    {0x02, 0x80, 0x03},
-    {0x04, 0x81, 0x05},
-    {0x06, 0x82, 0x07},
-    {0x08, 0x83, 0x09},
-    {0x0a, 0x84, 0x0b},
-    {0x0c, 0x85, 0x0d},
-    {0x0e, 0x86, 0x0f},
-    {0x87, 0xff, 0xff},
-    {0xff, 0xff, 0xff},
-    {0x20, 0x21, 0xff},
-    {0x22, 0xa0, 0x23},
-    {0x24, 0xa1, 0x25},
-    {0x26, 0xa2, 0x27},
-    {0x28, 0xa3, 0x29}};
-#ifndef LCI_FWD_MSUM
-#define LCI_FWD_MSUM 0   // measured slower (12.27 vs 11.81 ms): the 4 extra MFMAs per half cost more than the 32 adds
-#endif
-#ifndef LCI_FWD_HS
-#define LCI_FWD_HS 1
-#endif
-#ifndef LCI_FWD_PROBE
-#define LCI_FWD_PROBE 0   // timing probes (wrong results): 1 = no LDS reads in the loop, 2 = the reads without waits,
-                          // 3 / 4 / 5 = no exps / row-sum adds / conversions, 6 = no LDS-DMA in the loop
-#endif
-
 
 // initial S^T of query block 1 before the first half: the exps of block 1 that FW_SCHED wraps into the next half
 // (E1.i in gaps before START_E = 13) see NEG_BIG (exp2 -> 0); the elements exponentiated in the previous half's gaps
 // 13-15 are already "exponentiated": 0. Either way the first half adds and packs zeros for the missing half -1.
 __host__ __device__ constexpr bool fw_wrapped_exp(int i) {
-  if (LCI_FWD_MSUM) {
-    for (int g = 0; g < FW_MS_START_E1; ++g)
-      for (int o = 0; o < 3; ++o)
-        if (FW_SCHED_MS[g][o] == (0x20 | i)) return true;
-    return false;
-  }
   for (int g = 0; g < 13; ++g)
     for (int o = 0; o < 5; ++o)
       if (FW_SCHED[g][o] == (0x20 | i)) return true;
@@ -2242,16 +1133,6 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
   bf16x4 vt[2][2][2][2];   // [set][d block][k-step][half of the fragment] transposed V (keys as the k index)
   bf16x8 kr[4];       // K row fragments (A operands of the chains)
   float lp[2][4];     // row-sum partials (VALU adds)
-  f32x16 lsum[2];     // [query block] row sums as MFMA accumulators (LCI_FWD_MSUM): every register = the lane's sum
-  bf16x8 ones8;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ones8[j] = to_bf16(1.f);
-  HS_OPAQUE(ones8);
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    lsum[i] = f32x16{};
-    if (LCI_FWD_MSUM) HS_TO_AGPR(lsum[i]);
-  }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -2282,7 +1163,6 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
     if (cd == 0xFF) return;
     const int kind = cd >> 6, qb = (cd >> 5) & 1, i = cd & 31;
     if (only_qb >= 0 && qb != only_qb) return;
-    if (LCI_FWD_PROBE >= 3 && LCI_FWD_PROBE <= 5 && kind == LCI_FWD_PROBE - 3) return;
     if (kind == 0) HS_EXP(S[qb][i]);
     else if (kind == 1) asm volatile("v_add_f32 %0, %0, %1" : "+v"(lp[qb][i & 3]) : "v"(S[qb][i]));
     else HS_CVT(pp[qb][i >> 2][i & 3], S[qb][2 * i], S[qb][2 * i + 1]);
@@ -2291,26 +1171,7 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
     const int db = k & 1, s2 = k >> 1;
     HS_MFMA_G(o[qb][db], cat44(vt[st][db][s2][0], vt[st][db][s2][1]), __builtin_bit_cast(bf16x8, pp[qb][s2]));
   };
-  auto sum_mfma = [&](int qb, int s2) __attribute__((always_inline)) {
-    HS_MFMA_G(lsum[qb], ones8, __builtin_bit_cast(bf16x8, pp[qb][s2]));
-  };
   auto mfma_gap = [&](int g, int C, const f32x16& i0, const f32x16& i1) __attribute__((always_inline)) {
-    if (LCI_FWD_MSUM) {
-      if (g < 4) {
-        if (g == 0) HS_MFMA_C0(S[0], kr[0], qf[0][0], i0); else HS_MFMA_C(S[0], kr[g], qf[0][g]);
-      } else if (g < 8) {
-        pv_mfma(g - 4, 1, C ^ 1);
-      } else if (g < 10) {
-        sum_mfma(1, g - 8);
-      } else if (g < 14) {
-        if (g == 10) HS_MFMA_C0(S[1], kr[0], qf[1][0], i1); else HS_MFMA_C(S[1], kr[g - 10], qf[1][g - 10]);
-      } else if (g < 18) {
-        pv_mfma(g - 14, 0, C);
-      } else {
-        sum_mfma(0, g - 18);
-      }
-      return;
-    }
     if (g < 4) {
       if (g == 0) HS_MFMA_C0(S[0], kr[0], qf[0][0], i0); else HS_MFMA_C(S[0], kr[g], qf[0][g]);
     } else if (g < 8) {
@@ -2327,24 +1188,15 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
   auto half = [&](auto SET, int soff, int r0i, int nsoff, int nr0i, const f32x16& i0, const f32x16& i1, auto hook)
       __attribute__((always_inline)) {
     constexpr int C = decltype(SET)::value;
-    constexpr int NG = LCI_FWD_MSUM ? 20 : 16;
+    constexpr int NG = 16;
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       mfma_gap(g, C, i0, i1);
       if (g == 2) HS_KEEP(i0);    // the chain-start MFMAs read their initial accumulators as SrcC after issue
-      if (g == (LCI_FWD_MSUM ? 12 : 10)) HS_KEEP(i1);
-      // the gaps after a chain's last MFMA carry no VALU in FW_SCHED_MS: pad them so the chain's result is written
-      // back before the first exp two gaps later (MFMA -> VALU read, 12 wait states, tools/isa_hazards.py)
-      if (LCI_FWD_MSUM && (g == 4 || g == 14)) asm volatile("s_nop 7" ::: "memory");
-      if (LCI_FWD_MSUM) {
+      if (g == 10) HS_KEEP(i1);
 #pragma unroll
-        for (int op = 0; op < 3; ++op) valu_op(FW_SCHED_MS[g][op], -1);
-      } else {
-#pragma unroll
-        for (int op = 0; op < 5; ++op) valu_op(FW_SCHED[g][op], -1);
-      }
-      if (LCI_FWD_PROBE == 1) {   // timing probe (wrong results): no LDS reads in the loop
-      } else if (g < 8) {
+      for (int op = 0; op < 5; ++op) valu_op(FW_SCHED[g][op], -1);
+      if (g < 8) {
         const int f = g >> 1, part = g & 1;   // fragment f = (d block f & 1, k-step f >> 1)
         vt[C][f & 1][f >> 1][part] = trh(soff, r0i, f, part);
       } else if (g >= NG - 4) {   // the next half's K rows (the block-1 chain reads this half's until gap NG - 7)
@@ -2354,10 +1206,10 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
     }
   };
 
-  // register staging (LCI_FWD_RSTG): tile t+1's pieces (loaded into AGPRs during tile t-1) are stored to ring slot
-  // (t+1) & 3 at gaps 1-7 of tile t's half 0 and tile t+2's loaded at gaps 9-15; the barrier of tile t's half 1
-  // publishes tile t+1. A piece costs a buffer load + a ds_write_b128 instead of an LDS-DMA issue (~56 cycles each,
-  // LCI_FWD_PROBE 6). Pieces past the last tile read as zero (buffer range) into slots nobody reads.
+  // register staging: tile t+1's pieces (loaded into AGPRs during tile t-1) are stored to ring slot (t+1) & 3 at
+  // gaps 1-7 of tile t's half 0 and tile t+2's loaded at gaps 9-15; the barrier of tile t's half 1 publishes tile
+  // t+1. A piece costs a buffer load + a ds_write_b128 instead of an LDS-DMA issue (~56 cycles each, measured).
+  // Pieces past the last tile read as zero (buffer range) into slots nobody reads.
   u32x4 stg[4];
   const unsigned wst = lds0 + 2048 * wave + 16 * lane;
   auto ld_piece = [&](int t, int i) __attribute__((always_inline)) {
@@ -2366,21 +1218,14 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
     if (i == 2) stg[2] = hs_ld16(rv, dv0, t * KT * rs2v);
     if (i == 3) stg[3] = hs_ld16(rv, dv1, t * KT * rs2v);
   };
-  // prologue: tiles 0, 1, 2 in flight (DMA: 0-2; register staging: tile 0 by DMA, tile 1 into the AGPRs); wait for
-  // tile 0; K rows of its first half
+  // prologue: tile 0 by LDS-DMA, tile 1 into the staging AGPRs; wait for tile 0; K rows of its first half
   dma_op(0, 0); dma_op(0, 1); dma_op(0, 2); dma_op(0, 3);
-  if (LCI_FWD_RSTG) {
-    ld_piece(1, 0); ld_piece(1, 1); ld_piece(1, 2); ld_piece(1, 3);
-    hs_vmcnt<0>();
-  } else {
-    if (nkt > 1) { dma_op(1, 0); dma_op(1, 1); dma_op(1, 2); dma_op(1, 3); }
-    if (nkt > 2) { dma_op(2, 0); dma_op(2, 1); dma_op(2, 2); dma_op(2, 3); }
-    if (nkt > 2) hs_vmcnt<8>(); else if (nkt > 1) hs_vmcnt<4>(); else hs_vmcnt<0>();
-  }
+  ld_piece(1, 0); ld_piece(1, 1); ld_piece(1, 2); ld_piece(1, 3);
+  hs_vmcnt<0>();
   __builtin_amdgcn_s_barrier();
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) kr[ks] = row(0, 0, ks);
-  if (LCI_HS_LGKM0) __builtin_amdgcn_s_waitcnt(LGKM0_WAIT);
+  __builtin_amdgcn_s_waitcnt(LGKM0_WAIT);
 
   // SL >= 0: tile t sits in ring slot SL (compile-time: immediates); SL < 0: slot t & 3 at run time
   auto tile = [&](auto SL, int t, const f32x16& a0, const f32x16& a1, const f32x16& b0, const f32x16& b1)
@@ -2388,17 +1233,11 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
     constexpr int sl = decltype(SL)::value;
     const int soff = sl >= 0 ? sl * SLOT_B : (t & (NSLOT - 1)) * SLOT_B;
     const int nsoff = sl >= 0 ? ((sl + 1) & (NSLOT - 1)) * SLOT_B : ((t + 1) & (NSLOT - 1)) * SLOT_B;
-    // tile t+1 is published at gap 6 of half 1 (first reader: the K rows at gaps 12-15, 16-19 with MSUM); tile t+3's DMA goes into the
-    // slot of tile t-1 (last read by half 1 of tile t-1, before this barrier), one operation per two gaps
+    // tile t+1 is published at gap 6 of half 1 (first reader: the K rows at gaps 12-15)
     auto stage = [&](int g) __attribute__((always_inline)) {
-      if (t + 1 < nkt && g == 6) {
-        if (!LCI_FWD_RSTG) { if (t + 2 < nkt) hs_vmcnt<4>(); else hs_vmcnt<0>(); }
-        __builtin_amdgcn_s_barrier();
-      }
-      if (!LCI_FWD_RSTG && LCI_FWD_PROBE != 6 && t + 3 < nkt && g >= 8 && !(g & 1)) dma_op(t + 3, (g - 8) >> 1);
+      if (t + 1 < nkt && g == 6) __builtin_amdgcn_s_barrier();
     };
     auto rstg = [&](int g) __attribute__((always_inline)) {
-      if (!LCI_FWD_RSTG || LCI_FWD_PROBE == 6) return;
       if (g == 1) hs_vmcnt<0>();   // tile t+1's pieces (loaded a tile ago)
       if (g < 8 && (g & 1)) {
         constexpr int S1 = sl >= 0 ? ((sl + 1) & (NSLOT - 1)) * SLOT_B : 0;
@@ -2446,28 +1285,15 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
     asm volatile("s_nop 4" ::: "memory");
     tile(ICR{}, tl, M[0][0], M[0][1], M[1][0], M[1][1]);
   }
-  if (LCI_FWD_RSTG) hs_vmcnt<0>();   // the last tiles' staging loads (past the end: zeros) retire before the exit
-  // query block 1 of the last half: its wrapped VALU and its PV (+ row-sum) MFMAs
-  if (LCI_FWD_MSUM) {
+  hs_vmcnt<0>();   // the last tiles' staging loads (past the end: zeros) retire before the exit
+  // query block 1 of the last half: its wrapped VALU and its PV MFMAs
 #pragma unroll
-    for (int g = 0; g < 10; ++g) {
+  for (int g = 0; g < 8; ++g) {
 #pragma unroll
-      for (int op = 0; op < 3; ++op) valu_op(FW_SCHED_MS[g][op], 1);
-      if (g >= 4) {
-        asm volatile("s_nop 1" ::: "memory");
-        if (g < 8) pv_mfma(g - 4, 1, 1);   // the last half is a half 1
-        else sum_mfma(1, g - 8);
-      }
-    }
-  } else {
-#pragma unroll
-    for (int g = 0; g < 8; ++g) {
-#pragma unroll
-      for (int op = 0; op < 5; ++op) valu_op(FW_SCHED[g][op], 1);
-      if (g >= 4) {
-        asm volatile("s_nop 1" ::: "memory");
-        pv_mfma(g - 4, 1, 1);   // the last half is a half 1
-      }
+    for (int op = 0; op < 5; ++op) valu_op(FW_SCHED[g][op], 1);
+    if (g >= 4) {
+      asm volatile("s_nop 1" ::: "memory");
+      pv_mfma(g - 4, 1, 1);   // the last half is a half 1
     }
   }
   asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
@@ -2475,7 +1301,7 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
     const int q = qw0 + 32 * qb + r32;
-    const float lt = LCI_FWD_MSUM ? lsum[qb][0] : wave_sum_xor32((lp[qb][0] + lp[qb][1]) + (lp[qb][2] + lp[qb][3]));
+    const float lt = wave_sum_xor32((lp[qb][0] + lp[qb][1]) + (lp[qb][2] + lp[qb][3]));
     if (q < L) {
       const float inv = 1.f / lt;
       bf16* op = a.out + b * a.bs_out + (long long)q * a.rs_out + hh * a.hs;
@@ -2489,491 +1315,6 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
           *(bf16x4*)(op + 32 * db + 8 * g + 4 * h) = w;
         }
       if (h == 0) a.lse2[((long long)b * a.H + hh) * L + q] = m[qb] + __log2f(lt);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------- backward: dQ kernel, v2
-// Work split of attn_bwd_dq_kernel (8 waves x 32 queries on the lane, key tiles of 64), restructured like the
-// v2 forward: buffer-load staging into a 3-slot LDS ring (K tile swizzled: read by rows for S^T and transposed
-// for dQ), one barrier per tile, and the next tile's S^T / dP^T chains written in place into the accumulators
-// of the current tile as soon as its exp2 / dS / packing has consumed them:
-//   A: VALU on keys 0-31 of tile j (s0, p0) -> dS packs
-//   B: S^T, dP^T chains of keys 0-31 of tile j+1 + dQ MFMAs of keys 0-31 of tile j  ||  VALU on keys 32-63
-//   C: chains of keys 32-63 of tile j+1 + dQ MFMAs of keys 32-63 of tile j
-// Key rows >= L read as zero and are masked (P = 0) on the ragged last tile only.
-constexpr int QSLOT = KT * LD_SW + KT * LD_ROW;   // K tile (swizzled rows) + V tile (rows)
-
-__global__ __launch_bounds__(FW_NW * 64, 1) void attn_bwd_dq2_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16 smem[3 * QSLOT];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int hh = blockIdx.y, b = blockIdx.z;
-  const int L = a.L;
-  const int half = lane >> 5;
-  const int qrow = blockIdx.x * (FW_NW * 32) + wave * 32 + (lane & 31);
-  const int nkt = (L + KT - 1) / KT, nfull = L / KT;
-
-  bf16x8 qf[4], df[4];
-  float lse2 = 1.0e30f, dlt = 0.f;
-  {
-    const bf16* qp = a.q + b * a.bs_q + hh * a.hs;
-    const bf16* dop = a.dout + b * a.bs_do + hh * a.hs;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      if (qrow < L) {
-        qf[ks] = *(const bf16x8*)(qp + (long long)qrow * a.rs_q + ks * 16 + 8 * half);
-        df[ks] = *(const bf16x8*)(dop + (long long)qrow * a.rs_do + ks * 16 + 8 * half);
-      } else {
-        qf[ks] = bf16x8{};
-        df[ks] = bf16x8{};
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[ks][j] = to_bf16(to_f32(qf[ks][j]) * a.c);  // scores in the exp2 domain
-    }
-    if (qrow < L) {
-      const float* ws = a.delta + ((long long)b * a.H + hh) * 2 * L;
-      lse2 = -ws[qrow];
-      dlt = -ws[L + qrow];
-    }
-  }
-  f32x16 neg_lse, neg_dlt;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) { neg_lse[i] = -lse2; neg_dlt[i] = -dlt; }
-
-  const int srow = tid >> 3, sch = tid & 7;
-  const int rs2 = a.rs_k * 2;
-  const uint32_t nbytes = (uint32_t)(L - 1) * (uint32_t)rs2 + DH * 2;
-  const rsrc_t rk = make_rsrc(a.k + b * a.bs_k + hh * a.hs, nbytes);
-  const rsrc_t rv = make_rsrc(a.v + b * a.bs_v + hh * a.hs, nbytes);
-  const int voff = srow * rs2 + sch * 16;
-  const int st_k = swz(srow, sch * 8), st_v = KT * LD_SW + srow * LD_ROW + sch * 8;
-
-  {
-    const u32x4 k0 = bload16(rk, voff, 0), v0 = bload16(rv, voff, 0);
-    const u32x4 k1 = bload16(rk, voff, KT * rs2), v1 = bload16(rv, voff, KT * rs2);
-    *(u32x4*)(smem + st_k) = k0;
-    *(u32x4*)(smem + st_v) = v0;
-    *(u32x4*)(smem + QSLOT + st_k) = k1;
-    *(u32x4*)(smem + QSLOT + st_v) = v1;
-  }
-  __syncthreads();
-
-  f32x16 s0, s1, p0, p1, dq0 = {}, dq1 = {};
-  prio_young(wave);
-  // chains of keys kb*32..+31 of the tile in `slot`
-  auto chains = [&](int slot, int kb, f32x16& sx, f32x16& px) __attribute__((always_inline)) {
-    const bf16* kl = smem + slot * QSLOT;
-    const bf16* vl = kl + KT * LD_SW;
-    sx = mfma32(frag_row_sw(kl, kb * 32, 0, lane), qf[0], neg_lse);
-    px = mfma32(frag_row(vl, LD_ROW, kb * 32, 0, lane), df[0], neg_dlt);
-#pragma unroll
-    for (int ks = 1; ks < 4; ++ks) {
-      sx = mfma32(frag_row_sw(kl, kb * 32, ks * 16, lane), qf[ks], sx);
-      px = mfma32(frag_row(vl, LD_ROW, kb * 32, ks * 16, lane), df[ks], px);
-    }
-  };
-  auto mask_ragged = [&](int kt, f32x16& sx, int kb) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
-      if (kt * KT + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * half >= L) sx[i] = -1.0e30f;
-  };
-  // dS^T = P^T (dP^T - delta), packed as the B operands of dQ^T += K^T dS^T
-  auto grad = [&](f32x16& sx, f32x16& px, bf16x8& d0, bf16x8& d1) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) sx[i] = exp2_fast(sx[i]) * px[i];
-    d0 = pack8<0>(sx);
-    d1 = pack8<1>(sx);
-  };
-  auto dq_mfma = [&](int slot, int kb, const bf16x8& d0, const bf16x8& d1) __attribute__((always_inline)) {
-    const bf16* kl = smem + slot * QSLOT;
-    dq0 = mfma32(frag_tr_sw<0>(kl, kb * 32, 0, lane), d0, dq0);
-    dq1 = mfma32(frag_tr_sw<0>(kl, kb * 32, 32, lane), d0, dq1);
-    dq0 = mfma32(frag_tr_sw<1>(kl, kb * 32, 0, lane), d1, dq0);
-    dq1 = mfma32(frag_tr_sw<1>(kl, kb * 32, 32, lane), d1, dq1);
-  };
-
-  chains(0, 0, s0, p0);
-  chains(0, 1, s1, p1);
-  if (nfull == 0) { mask_ragged(0, s0, 0); mask_ragged(0, s1, 1); }
-  int slA = 0, slB = 1, slC = 2;   // ring slots of tiles j, j+1, j+2
-  auto iter = [&](const int j, auto next) __attribute__((always_inline)) {
-    constexpr bool NEXT = decltype(next)::value;
-#ifdef LCI_DQ_IGLP
-    __builtin_amdgcn_iglp_opt(LCI_DQ_IGLP);
-#endif
-    const u32x4 kw = bload16(rk, voff, (j + 2) * KT * rs2);
-    const u32x4 vw = bload16(rv, voff, (j + 2) * KT * rs2);
-    bf16x8 a0, a1, c0, c1;
-    grad(s0, p0, a0, a1);                              // A
-    LCI_SB();
-    if constexpr (NEXT) chains(slB, 0, s0, p0);       // B
-    dq_mfma(slA, 0, a0, a1);
-    grad(s1, p1, c0, c1);
-    LCI_SB();
-    if constexpr (NEXT) chains(slB, 1, s1, p1);       // C
-    dq_mfma(slA, 1, c0, c1);
-    LCI_SB();
-    *(u32x4*)(smem + slC * QSLOT + st_k) = kw;
-    *(u32x4*)(smem + slC * QSLOT + st_v) = vw;
-    __syncthreads();
-    const int t = slA; slA = slB; slB = slC; slC = t;
-    if constexpr (NEXT) {
-      if (j + 1 == nfull) [[unlikely]] { mask_ragged(j + 1, s0, 0); mask_ragged(j + 1, s1, 1); }
-    }
-  };
-  int j = 0;
-  for (; j + 1 < nkt; ++j) iter(j, std::true_type{});
-  iter(j, std::false_type{});
-
-  if (qrow < L) {
-    bf16* dqp = a.out + b * a.bs_out + (long long)qrow * a.rs_out + hh * a.hs;
-    const float sc = a.scale;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      bf16x4 w0, w1;
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        w0[jj] = to_bf16(dq0[4 * g + jj] * sc);
-        w1[jj] = to_bf16(dq1[4 * g + jj] * sc);
-      }
-      *(bf16x4*)(dqp + 8 * g + 4 * half) = w0;
-      *(bf16x4*)(dqp + 32 + 8 * g + 4 * half) = w1;
-    }
-  }
-}
-
-// dQ kernel on v_mfma_f32_16x16x32_bf16: the work split, ring and software pipeline of attn_bwd_dq2_kernel; per
-// 32-key half of a tile 2 key blocks x 2 query blocks of 16. The query is the accumulator column, so the row
-// constants are per-lane splats (initial accumulators, as in v2); dS^T feeds dQ^T += K^T dS^T as the B operand in
-// the permuted key order {4g..4g+3 of key block 0, 4g..4g+3 of key block 1}, matched by the transposed K reads.
-__global__ __launch_bounds__(FW_NW * 64, 1) void attn_bwd_dq16_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16 smem[3 * QSLOT];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int hh = blockIdx.y, b = blockIdx.z;
-  const int L = a.L;
-  const int g = lane >> 4, c16 = lane & 15;
-  const int qw0 = blockIdx.x * (FW_NW * 32) + wave * 32;   // first query of this wave
-  const int nkt = (L + KT - 1) / KT, nfull = L / KT;
-
-  bf16x8 qf[2][2], df[2][2];   // [query block][k-step]: lane holds Q[qw0 + 16qb + c16][32ks + 8g + j]
-  f32x4 neg_lse[2], neg_dlt[2];
-  {
-    const bf16* qp = a.q + b * a.bs_q + hh * a.hs;
-    const bf16* dop = a.dout + b * a.bs_do + hh * a.hs;
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
-      const int q = qw0 + 16 * qb + c16;
-      float lse2 = 1.0e30f, dlt = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        if (q < L) {
-          qf[qb][ks] = *(const bf16x8*)(qp + (long long)q * a.rs_q + 32 * ks + 8 * g);
-          df[qb][ks] = *(const bf16x8*)(dop + (long long)q * a.rs_do + 32 * ks + 8 * g);
-        } else {
-          qf[qb][ks] = bf16x8{};
-          df[qb][ks] = bf16x8{};
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) qf[qb][ks][j] = to_bf16(to_f32(qf[qb][ks][j]) * a.c);
-      }
-      if (q < L) {
-        const float* ws = a.delta + ((long long)b * a.H + hh) * 2 * L;
-        lse2 = -ws[q];
-        dlt = -ws[L + q];
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) { neg_lse[qb][i] = -lse2; neg_dlt[qb][i] = -dlt; }
-    }
-  }
-
-  const int srow = tid >> 3, sch = tid & 7;
-  const int rs2 = a.rs_k * 2;
-  const uint32_t nbytes = (uint32_t)(L - 1) * (uint32_t)rs2 + DH * 2;
-  const rsrc_t rk = make_rsrc(a.k + b * a.bs_k + hh * a.hs, nbytes);
-  const rsrc_t rv = make_rsrc(a.v + b * a.bs_v + hh * a.hs, nbytes);
-  const int voff = srow * rs2 + sch * 16;
-  const int st_k = swz(srow, sch * 8), st_v = KT * LD_SW + srow * LD_ROW + sch * 8;
-  {
-    const u32x4 k0 = bload16(rk, voff, 0), v0 = bload16(rv, voff, 0);
-    const u32x4 k1 = bload16(rk, voff, KT * rs2), v1 = bload16(rv, voff, KT * rs2);
-    *(u32x4*)(smem + st_k) = k0;
-    *(u32x4*)(smem + st_v) = v0;
-    *(u32x4*)(smem + QSLOT + st_k) = k1;
-    *(u32x4*)(smem + QSLOT + st_v) = v1;
-  }
-  __syncthreads();
-
-  typedef f32x4 Blk[2][2];   // [key block of the half][query block]
-  Blk s0, p0, s1, p1;
-  f32x4 dq[4][2];            // [d block][query block]: lane holds dQ^T[16db + 4g + i][16qb + c16]
-#pragma unroll
-  for (int db = 0; db < 4; ++db) dq[db][0] = dq[db][1] = f32x4{};
-  // S^T / dP^T chains of keys 32h .. 32h + 31 of the tile in `slot`
-  auto chains = [&](int slot, int h, Blk& sx, Blk& px) __attribute__((always_inline)) {
-    const bf16* kl = smem + slot * QSLOT;
-    const bf16* vl = kl + KT * LD_SW;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      const int r = 32 * h + 16 * kb + c16;
-      const bf16x8 k0 = *(const bf16x8*)(kl + swz(r, 8 * g)), k1 = *(const bf16x8*)(kl + swz(r, 32 + 8 * g));
-      const bf16x8 v0 = *(const bf16x8*)(vl + r * LD_ROW + 8 * g), v1 = *(const bf16x8*)(vl + r * LD_ROW + 32 + 8 * g);
-#pragma unroll
-      for (int qb = 0; qb < 2; ++qb) {
-        sx[kb][qb] = mfma16(k1, qf[qb][1], mfma16(k0, qf[qb][0], neg_lse[qb]));
-        px[kb][qb] = mfma16(v1, df[qb][1], mfma16(v0, df[qb][0], neg_dlt[qb]));
-      }
-    }
-  };
-  auto mask_ragged = [&](int kt, int h, Blk& sx) __attribute__((always_inline)) {
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (kt * KT + 32 * h + 16 * kb + 4 * g + i >= L) { sx[kb][0][i] = -1.0e30f; sx[kb][1][i] = -1.0e30f; }
-  };
-  // dS^T = P^T (dP^T - delta), packed per query block as the B operand (k = the half's 32 keys, permuted)
-  auto grad = [&](Blk& sx, Blk& px, bf16x8* d) __attribute__((always_inline)) {
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) d[qb][4 * kb + i] = to_bf16(exp2_fast(sx[kb][qb][i]) * px[kb][qb][i]);
-  };
-  auto dq_mfma = [&](int slot, int h, const bf16x8* d) __attribute__((always_inline)) {
-    const bf16* kl = smem + slot * QSLOT;
-    const int r = 32 * h + 4 * g + ((lane & 15) >> 2);
-#pragma unroll
-    for (int db = 0; db < 4; ++db) {
-      const int col = 16 * db + 4 * (lane & 3);
-      const bf16x8 kt = cat44(lds_tr4(kl + swz(r, col)), lds_tr4(kl + swz(r + 16, col)));
-      dq[db][0] = mfma16(kt, d[0], dq[db][0]);
-      dq[db][1] = mfma16(kt, d[1], dq[db][1]);
-    }
-  };
-
-  chains(0, 0, s0, p0);
-  chains(0, 1, s1, p1);
-  if (nfull == 0) { mask_ragged(0, 0, s0); mask_ragged(0, 1, s1); }
-  int slA = 0, slB = 1, slC = 2;
-  auto iter = [&](const int j, auto next) __attribute__((always_inline)) {
-    constexpr bool NEXT = decltype(next)::value;
-    const u32x4 kw = bload16(rk, voff, (j + 2) * KT * rs2);
-    const u32x4 vw = bload16(rv, voff, (j + 2) * KT * rs2);
-    bf16x8 d0[2], d1[2];
-    grad(s0, p0, d0);
-    LCI_SB();
-    if constexpr (NEXT) chains(slB, 0, s0, p0);
-    dq_mfma(slA, 0, d0);
-    grad(s1, p1, d1);
-    LCI_SB();
-    if constexpr (NEXT) chains(slB, 1, s1, p1);
-    dq_mfma(slA, 1, d1);
-    LCI_SB();
-    *(u32x4*)(smem + slC * QSLOT + st_k) = kw;
-    *(u32x4*)(smem + slC * QSLOT + st_v) = vw;
-    __syncthreads();
-    const int t = slA; slA = slB; slB = slC; slC = t;
-    if constexpr (NEXT) {
-      if (j + 1 == nfull) [[unlikely]] { mask_ragged(j + 1, 0, s0); mask_ragged(j + 1, 1, s1); }
-    }
-  };
-  int j = 0;
-  for (; j + 1 < nkt; ++j) iter(j, std::true_type{});
-  iter(j, std::false_type{});
-
-  const float sc = a.scale;
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
-    const int q = qw0 + 16 * qb + c16;
-    if (q < L) {
-      bf16* dqp = a.out + b * a.bs_out + (long long)q * a.rs_out + hh * a.hs;
-#pragma unroll
-      for (int db = 0; db < 4; ++db) {
-        bf16x4 w;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) w[i] = to_bf16(dq[db][qb][i] * sc);
-        *(bf16x4*)(dqp + 16 * db + 4 * g) = w;
-      }
-    }
-  }
-}
-
-// Forward on v_mfma_f32_16x16x32_bf16: the ring, max-free softmax and pipeline of attn_fwd2_kernel. Per wave 32
-// queries = 2 query blocks of 16 (the accumulator column); a 64-key tile = 4 key blocks of 16 (rows 4g + i of a
-// lane). The running row sum stays a per-lane partial over the lane's keys, summed over the 4 lane groups once at
-// the end; the exact path's row max reduces over the groups with two xor shuffles. P^T feeds O^T += V^T P^T as the
-// B operand in the permuted key order of two key blocks, matched by the transposed V reads.
-__global__ __launch_bounds__(FW_NW * 64, 1) void attn_fwd16_kernel(AttnArgs a, const float* knorm) {
-  __shared__ __attribute__((aligned(16))) bf16 smem[3 * FSLOT];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int hh = blockIdx.y, b = blockIdx.z;
-  const int L = a.L;
-  const int g = lane >> 4, c16 = lane & 15;
-  const int qw0 = blockIdx.x * (FW_NW * 32) + wave * 32;
-  const int nkt = (L + KT - 1) / KT, nfull = L / KT;
-
-  const int srow = tid >> 3, sch = tid & 7;
-  const int rs2 = a.rs_k * 2;
-  const uint32_t nbytes = (uint32_t)(L - 1) * (uint32_t)rs2 + DH * 2;
-  const rsrc_t rk = make_rsrc(a.k + b * a.bs_k + hh * a.hs, nbytes);
-  const rsrc_t rv = make_rsrc(a.v + b * a.bs_v + hh * a.hs, nbytes);
-  const int voff = srow * rs2 + sch * 16;
-  const int st_k = srow * LD_ROW + sch * 8, st_v = KT * LD_ROW + srow * LD_TR + sch * 8;
-  const float* kn = knorm + ((long long)b * a.H + hh) * nkt;
-
-  const float c = a.c;
-  bf16x8 qf[2][2];
-  float qn[2];
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
-    const int q = qw0 + 16 * qb + c16;
-    const bf16* qp = a.q + b * a.bs_q + hh * a.hs + (long long)q * a.rs_q;
-    float qss = 0.f;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 t{};
-      if (q < L) t = *(const bf16x8*)(qp + 32 * ks + 8 * g);
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        t[jj] = to_bf16(to_f32(t[jj]) * c);
-        qss += to_f32(t[jj]) * to_f32(t[jj]);
-      }
-      qf[qb][ks] = t;
-    }
-    qss += __shfl_xor(qss, 16);
-    qss += __shfl_xor(qss, 32);
-    qn[qb] = sqrtf(qss);
-  }
-
-  {
-    const u32x4 k0 = bload16(rk, voff, 0), v0 = bload16(rv, voff, 0);
-    const u32x4 k1 = bload16(rk, voff, KT * rs2), v1 = bload16(rv, voff, KT * rs2);
-    *(u32x4*)(smem + st_k) = k0;
-    *(u32x4*)(smem + st_v) = v0;
-    *(u32x4*)(smem + FSLOT + st_k) = k1;
-    *(u32x4*)(smem + FSLOT + st_v) = v1;
-  }
-  __syncthreads();
-
-  f32x4 o[4][2], negm[2];   // o[d block][query block]: lane holds O^T[16db + 4g + i][16qb + c16]
-#pragma unroll
-  for (int db = 0; db < 4; ++db) o[db][0] = o[db][1] = f32x4{};
-  negm[0] = negm[1] = f32x4{};
-  float m_run[2] = {0.f, 0.f}, l_run[2] = {0.f, 0.f};
-  f32x4 x[4][2];            // scores of the current tile: [key block][query block], rows = keys 16kb + 4g + i
-
-  auto scores = [&](int slot, int kb) __attribute__((always_inline)) {
-    const bf16* kl = smem + slot + (16 * kb + c16) * LD_ROW + 8 * g;
-    const bf16x8 k0 = *(const bf16x8*)kl, k1 = *(const bf16x8*)(kl + 32);
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb) x[kb][qb] = mfma16(k1, qf[qb][1], mfma16(k0, qf[qb][0], negm[qb]));
-  };
-  auto mask_ragged = [&](int kt) __attribute__((always_inline)) {
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (kt * KT + 16 * kb + 4 * g + i >= L) { x[kb][0][i] = NEG_BIG; x[kb][1][i] = NEG_BIG; }
-  };
-  auto exact = [&](bool first) __attribute__((always_inline)) {
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
-      float mx = fmaxf(fmaxf(x[0][qb][0], x[0][qb][1]), fmaxf(x[0][qb][2], x[0][qb][3]));
-#pragma unroll
-      for (int kb = 1; kb < 4; ++kb)
-        mx = fmaxf(mx, fmaxf(fmaxf(x[kb][qb][0], x[kb][qb][1]), fmaxf(x[kb][qb][2], x[kb][qb][3])));
-      mx = fmaxf(mx, __shfl_xor(mx, 16));
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
-      if (first || __any(mx > 0.f)) {
-        const float d = first ? mx : fmaxf(mx, 0.f);
-        m_run[qb] += d;
-        if (!first) {
-          const float alpha = exp2_fast(-d);
-          l_run[qb] *= alpha;
-#pragma unroll
-          for (int db = 0; db < 4; ++db) o[db][qb] *= alpha;
-        }
-#pragma unroll
-        for (int kb = 0; kb < 4; ++kb) x[kb][qb] -= d;
-        negm[qb] = f32x4{-m_run[qb], -m_run[qb], -m_run[qb], -m_run[qb]};
-      }
-    }
-  };
-
-#pragma unroll
-  for (int kb = 0; kb < 4; ++kb) scores(0, kb);
-  if (nfull == 0) mask_ragged(0);
-  exact(true);
-
-  int slA = 0, slB = FSLOT, slC = 2 * FSLOT;
-  auto iter = [&](const int j, auto next) __attribute__((always_inline)) -> bool {
-    constexpr bool NEXT = decltype(next)::value;
-    const u32x4 kw = bload16(rk, voff, (j + 2) * KT * rs2);
-    const u32x4 vw = bload16(rv, voff, (j + 2) * KT * rs2);
-    const float knext = NEXT ? kn[j + 1] : 0.f;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      // exp2 of key blocks 2h, 2h+1 -> P^T fragments (k = the half's 32 keys, permuted), row-sum partials
-      bf16x8 pf[2];
-#pragma unroll
-      for (int qb = 0; qb < 2; ++qb) {
-        float ls = 0.f;
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float e = exp2_fast(x[2 * h + kk][qb][i]);
-            pf[qb][4 * kk + i] = to_bf16(e);
-            ls += e;
-          }
-        l_run[qb] += ls;
-      }
-      LCI_SB();
-      if constexpr (NEXT) { scores(slB, 2 * h); scores(slB, 2 * h + 1); }
-      const bf16* vl = smem + slA + KT * LD_ROW + (32 * h + 4 * g + ((lane & 15) >> 2)) * LD_TR + 4 * (lane & 3);
-#pragma unroll
-      for (int db = 0; db < 4; ++db) {
-        const bf16x8 vt = cat44(lds_tr4(vl + 16 * db), lds_tr4(vl + 16 * db + 16 * LD_TR));
-        o[db][0] = mfma16(vt, pf[0], o[db][0]);
-        o[db][1] = mfma16(vt, pf[1], o[db][1]);
-      }
-      LCI_SB();
-    }
-    *(u32x4*)(smem + slC + st_k) = kw;
-    *(u32x4*)(smem + slC + st_v) = vw;
-    __syncthreads();
-    const int t = slA; slA = slB; slB = slC; slC = t;
-    if constexpr (NEXT)
-      return (j + 1 == nfull) | !__all((qn[0] * knext - m_run[0] <= SAFE_EXP2) & (qn[1] * knext - m_run[1] <= SAFE_EXP2));
-    return false;
-  };
-  int j = 0;
-  for (; j + 1 < nkt; ++j) {
-    if (iter(j, std::true_type{})) [[unlikely]] {
-      if (j + 1 == nfull) mask_ragged(j + 1);
-      exact(false);
-    }
-  }
-  iter(j, std::false_type{});
-
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
-    float l_tot = l_run[qb];
-    l_tot += __shfl_xor(l_tot, 16);
-    l_tot += __shfl_xor(l_tot, 32);
-    const float inv = 1.f / l_tot;
-    const int q = qw0 + 16 * qb + c16;
-    if (q < L) {
-      bf16* op = a.out + b * a.bs_out + (long long)q * a.rs_out + hh * a.hs;
-#pragma unroll
-      for (int db = 0; db < 4; ++db) {
-        bf16x4 w;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) w[i] = to_bf16(o[db][qb][i] * inv);
-        *(bf16x4*)(op + 16 * db + 4 * g) = w;
-      }
-      if (g == 0) a.lse2[((long long)b * a.H + hh) * L + q] = m_run[qb] + __log2f(l_tot);
     }
   }
 }
@@ -2998,6 +1339,7 @@ extern "C" int lci_attn_fwd(const void* qkv, void* out, float* lse2, float* knor
   const int rs = 3 * H * DH;
   LCI_CHECK(check_packed(qkv, rs) && check_packed(out, H * DH), "lci_attn_fwd: misaligned pointers");
   LCI_CHECK((long long)(L + 4 * KT) * rs * 2 < (1ll << 31), "lci_attn_fwd: L=%d too long for 32-bit buffer offsets", L);
+  LCI_CHECK(knorm_ws != nullptr, "lci_attn_fwd: knorm_ws (lci_attn_fwd_ws_bytes) is required");
   AttnArgs a{};
   const bf16* base = (const bf16*)qkv;
   a.q = base; a.k = base + H * DH; a.v = base + 2 * H * DH;
@@ -3008,34 +1350,21 @@ extern "C" int lci_attn_fwd(const void* qkv, void* out, float* lse2, float* knor
   a.hs = DH; a.H = H; a.L = L;
   a.scale = scale; a.c = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
-  LCI_CHECK(knorm_ws != nullptr, "lci_attn_fwd: knorm_ws (lci_attn_fwd_ws_bytes) is required");
   const int nkt = (L + KT - 1) / KT;
   hipLaunchKernelGGL(attn_key_norm_kernel, dim3((nkt + 3) / 4, H, B), dim3(256), 0, s, a, knorm_ws, nkt);
   LCI_LAUNCH_CHECK();
-  dim3 grid((L + FW_NW * 32 - 1) / (FW_NW * 32), H, B);
-#ifndef LCI_FWD16
-#define LCI_FWD16 0    // 16x16x32 forward: parity-green, 12.97 vs 12.37 ms (slower: the VALU-bound body loses issue
-#endif                 // slots, a 16x16x32 MFMA holds vector issue for 8 of its 16 cycles), not adopted
-  if (LCI_FWD_HS)
-    hipLaunchKernelGGL(attn_fwd_hs_kernel, dim3((L + HS_NW * 64 - 1) / (HS_NW * 64), H, B), dim3(HS_NW * 64), 0, s, a,
-                       (const float*)knorm_ws);
-  else if (LCI_FWD16)
-    hipLaunchKernelGGL(attn_fwd16_kernel, grid, dim3(FW_NW * 64), 0, s, a, (const float*)knorm_ws);
-  else
-    hipLaunchKernelGGL(attn_fwd2_kernel, grid, dim3(FW_NW * 64), 0, s, a, (const float*)knorm_ws);
+  hipLaunchKernelGGL(attn_fwd_hs_kernel, dim3((L + HS_NW * 64 - 1) / (HS_NW * 64), H, B), dim3(HS_NW * 64), 0, s, a,
+                     (const float*)knorm_ws);
   LCI_LAUNCH_CHECK();
   return 0;
 }
 
-// stage: -1 = all three launches; 0 = delta, 1 = dK/dV, 2 = dQ (for per-kernel timing)
-// backward workspace: (B, H, 2, L) f32 negated row constants, then (256-B aligned) the (B, H, 2, 64, Lp) bf16
-// d-major Q | dO copies of LCI_HS_TQ
-static long long attn_bwd_rc_bytes(int B, int H, int L) { return ((long long)B * H * 2 * L * 4 + 255) / 256 * 256; }
+// backward workspace: (B, H, 2, L) f32 negated row constants [-lse2 | -delta], 256-B aligned
 extern "C" long long lci_attn_bwd_ws_bytes(int B, int H, int L) {
-  const long long Lp = (L + 63) / 64 * 64;
-  return attn_bwd_rc_bytes(B, H, L) + (LCI_HS_TQ ? (long long)B * H * 2 * 64 * Lp * 2 : 0);
+  return ((long long)B * H * 2 * L * 4 + 255) / 256 * 256;
 }
 
+// stage: -1 = all three launches; 0 = delta, 1 = dK/dV, 2 = dQ (for per-kernel timing)
 extern "C" int lci_attn_bwd_stage(int stage, const void* qkv, const void* out, const void* dout, const float* lse2,
                                   void* dqkv, float* delta_ws, int B, int L, int H, int head_dim, float scale,
                                   void* stream) {
@@ -3044,14 +1373,15 @@ extern "C" int lci_attn_bwd_stage(int stage, const void* qkv, const void* out, c
   const int rs = 3 * H * DH;
   LCI_CHECK(check_packed(qkv, rs) && check_packed(dqkv, rs) && check_packed(out, H * DH) &&
                 check_packed(dout, H * DH), "lci_attn_bwd: misaligned pointers");
+  // the placed kernels address q / k / v / dO rows through buffer resources with 32-bit sizes
+  LCI_CHECK((long long)(L + 4 * KT) * rs * 2 < (1ll << 31), "lci_attn_bwd: L=%d too long for 32-bit buffer offsets", L);
+  LCI_CHECK(delta_ws != nullptr, "lci_attn_bwd: delta_ws (lci_attn_bwd_ws_bytes) is required");
   AttnArgs a{};
   const bf16* base = (const bf16*)qkv;
   bf16* dbase = (bf16*)dqkv;
   a.q = base; a.k = base + H * DH; a.v = base + 2 * H * DH;
   a.o = (const bf16*)out; a.dout = (const bf16*)dout;
   a.lse2 = (float*)lse2; a.delta = delta_ws;
-  a.Lp = (L + 63) / 64 * 64;   // the d-major Q | dO copies follow the row constants (lci_attn_bwd_ws_bytes)
-  a.qdoT = (bf16*)((char*)delta_ws + attn_bwd_rc_bytes(B, H, L));
   a.bs_q = a.bs_k = a.bs_v = (long long)L * rs;
   a.rs_q = a.rs_k = a.rs_v = rs;
   a.bs_o = a.bs_do = (long long)L * H * DH;
@@ -3062,54 +1392,17 @@ extern "C" int lci_attn_bwd_stage(int stage, const void* qkv, const void* out, c
   a.hs = DH; a.H = H; a.L = L;
   a.scale = scale; a.c = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
-#ifndef LCI_BWD_NW
-#define LCI_BWD_NW 8   // 8 waves share each staged Q/dO (K/V) tile: -4% dK/dV, -8% dQ vs 4
-#endif
-#ifndef LCI_DKDV_KB
-#define LCI_DKDV_KB 1
-#endif
-  constexpr int KB = LCI_DKDV_KB;
-  constexpr int NW = KB == 1 ? LCI_BWD_NW : 4;   // KB = 2: one wave per SIMD
-  dim3 grid((L + NW * 32 * KB - 1) / (NW * 32 * KB), H, B);
+  const dim3 grid((L + HS_NW * 64 - 1) / (HS_NW * 64), H, B);
   if (stage < 0 || stage == 0) {
     hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((L + 31) / 32, H, B), dim3(256), 0, s, a);
     LCI_LAUNCH_CHECK();
-    if (LCI_HS_TQ) {
-      hipLaunchKernelGGL(attn_bwd_qdoT_kernel, dim3(a.Lp / 64, H, B), dim3(256), 0, s, a);
-      LCI_LAUNCH_CHECK();
-    }
   }
-#ifndef LCI_DKDV16
-#define LCI_DKDV16 1   // 16x16x32 dK/dV (default): 22.1 vs 22.6-22.8 ms for the 32x32x16 kernel, three same-box A/Bs
-#endif
-#ifndef LCI_DKDV_HS
-#define LCI_DKDV_HS 1  // one-wave-per-SIMD placed-stream dK/dV kernel (attn_bwd_dkdv_hs_kernel)
-#endif
-  if ((stage < 0 || stage == 1) && LCI_DKDV_HS) {
-    hipLaunchKernelGGL(attn_bwd_dkdv_hs_kernel, dim3((L + HS_NW * 64 - 1) / (HS_NW * 64), H, B), dim3(HS_NW * 64), 0, s, a);
-    LCI_LAUNCH_CHECK();
-  } else if (stage < 0 || stage == 1) {
-    if (LCI_DKDV16 && KB == 1)
-      hipLaunchKernelGGL((attn_bwd_dkdv16_kernel<NW>), grid, dim3(NW * 64), 0, s, a);
-    else
-      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<NW, KB>), grid, dim3(NW * 64), 0, s, a);
+  if (stage < 0 || stage == 1) {
+    hipLaunchKernelGGL(attn_bwd_dkdv_hs_kernel, grid, dim3(HS_NW * 64), 0, s, a);
     LCI_LAUNCH_CHECK();
   }
-#ifndef LCI_DQ16
-#define LCI_DQ16 0     // 16x16x32 dQ: parity-green, 16.7-17.0 vs 16.7-17.0 ms (within noise), not adopted
-#endif
-#ifndef LCI_DQ_HS
-#define LCI_DQ_HS 1    // one-wave-per-SIMD placed-stream dQ kernel (attn_bwd_dq_hs_kernel)
-#endif
-  if ((stage < 0 || stage == 2) && LCI_DQ_HS) {
-    hipLaunchKernelGGL(attn_bwd_dq_hs_kernel, dim3((L + HS_NW * 64 - 1) / (HS_NW * 64), H, B), dim3(HS_NW * 64), 0, s, a);
-    LCI_LAUNCH_CHECK();
-  } else if (stage < 0 || stage == 2) {
-    const dim3 gq((L + FW_NW * 32 - 1) / (FW_NW * 32), H, B);
-    if (LCI_DQ16)
-      hipLaunchKernelGGL(attn_bwd_dq16_kernel, gq, dim3(FW_NW * 64), 0, s, a);
-    else
-      hipLaunchKernelGGL(attn_bwd_dq2_kernel, gq, dim3(FW_NW * 64), 0, s, a);
+  if (stage < 0 || stage == 2) {
+    hipLaunchKernelGGL(attn_bwd_dq_hs_kernel, grid, dim3(HS_NW * 64), 0, s, a);
     LCI_LAUNCH_CHECK();
   }
   return 0;

@@ -73,7 +73,7 @@ def attn_bwd(qkv, out, dout, lse2, num_heads: int, scale: float):
     B, L, C = qkv.shape
     dh = C // (3 * num_heads)
     dqkv = torch.empty_like(qkv)
-    # -lse2 | -delta rows, then the d-major Q / dO copies (include/lci.h lci_attn_bwd_ws_bytes)
+    # -lse2 | -delta rows (include/lci.h lci_attn_bwd_ws_bytes)
     delta = torch.empty(int(_lib.load().lci_attn_bwd_ws_bytes(B, num_heads, L)), device=qkv.device, dtype=torch.uint8)
     args = (qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse2.data_ptr(), dqkv.data_ptr(), delta.data_ptr(),
             B, L, num_heads, dh, float(scale), _lib.stream_of(qkv))
