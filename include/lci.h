@@ -55,8 +55,8 @@ extern "C" {
  * takes the transposed table biasT, lci_window_attn_bwd's plain table only for windows of N > 384; 15:
  * lci_window_attn_bwd pad_ws; 16: lci_attn_bwd delta_ws is (B, H, 2, L): the negated row constants -lse2 | -delta; 17: lci_window_bwd_needs_plain;
  * 18: lci_attn_bwd delta_ws is lci_attn_bwd_ws_bytes(B, H, L) bytes; 19: selective-scan checkpoints in the I/O
- * dtype). */
-#define LCI_ABI_VERSION 19
+ * dtype; 20: lci_attn_gen_fwd / lci_attn_gen_bwd). */
+#define LCI_ABI_VERSION 20
 const char* lci_last_error(void);
 int lci_abi_version(void);
 /* sha256 prefix of the sources the library was built from (build_lib.source_hash); the Python binding refuses a
@@ -84,6 +84,17 @@ long long lci_attn_bwd_ws_bytes(int B, int H, int L);
  * for timing. */
 int lci_attn_bwd_stage(int stage, const void* qkv, const void* out, const void* dout, const float* lse2,
                        void* dqkv, float* delta_ws, int B, int L, int H, int head_dim, float scale, void* stream);
+
+/* ViT attention in exact f32 products (csrc/attention_gen.hip): the reference's fp32 (non-AMP) SABlock path
+ * (backbone_vit.py:191-201: fp32 einsums + softmax) and head dims 65..256 (the `custom` preset,
+ * backbone_vit.py:78-86) in either dtype. dtype 0 = f32, 1 = bf16 (I/O; f32 arithmetic on v_mfma_f32_16x16x4_f32).
+ * qkv (B, L, 3*H*D), out (B, L, H*D), dqkv like qkv, dout like out, all in the I/O dtype; D = head_dim <= 256,
+ * any L. lse: (B, H, L) f32, NATURAL-log row logsumexp of scale q.k. delta_ws: (B, H, L) f32 workspace.
+ * Deterministic (no atomics). Replaces the same reference lines as lci_attn_fwd / lci_attn_bwd. */
+int lci_attn_gen_fwd(int dtype, const void* qkv, void* out, float* lse, int B, int L, int H, int head_dim,
+                     float scale, void* stream);
+int lci_attn_gen_bwd(int dtype, const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
+                     float* delta_ws, int B, int L, int H, int head_dim, float scale, void* stream);
 
 /* ------------------------------------------------------------------ Swin window attention (head_dim 32)
  * geo[16] = {mode, nd, S0, S1, S2, ws0, ws1, ws2, sh0, sh1, sh2, B_or_Bw, nW, N, C, H}

@@ -14,7 +14,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_LIB = os.path.join(HERE, "liblci.so")
 LIB_PATH = os.environ.get("LCI_LIB_PATH", DEFAULT_LIB)   # override: kernel-variant A/B runs (no staleness check)
-ABI_VERSION = 19   # include/lci.h LCI_ABI_VERSION
+ABI_VERSION = 20   # include/lci.h LCI_ABI_VERSION
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -26,6 +26,8 @@ SIGNATURES = {
     "lci_attn_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _F, _P],
     "lci_attn_bwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P],
     "lci_attn_bwd_stage": [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P],
+    "lci_attn_gen_fwd": [_I, _P, _P, _P, _I, _I, _I, _I, _F, _P],
+    "lci_attn_gen_bwd": [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P],
     "lci_patch_embed_fwd": [_P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P],
     "lci_patch_embed_bwd": [_P, _I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P, _P, _I, _P],
     "lci_selective_scan_fwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],

@@ -58,7 +58,6 @@ def custom_ViT(config, input_feature_channels):
 HYENA_L_MAX = 66000
 
 
-ATTN_HEAD_DIM = 64   # csrc/attention.hip DH
 
 
 class SABlock(nn.Module):
@@ -79,13 +78,13 @@ class SABlock(nn.Module):
             self.drop_output = nn.Dropout(dropout_rate)
             self.drop_weights = nn.Dropout(dropout_rate)
             self.head_dim = hidden_size // num_heads
-            if self.head_dim > ATTN_HEAD_DIM:
-                # the flash-attention kernels are built for head_dim 64 (every reference preset: small 384/6, base
-                # 768/12); the reference's `custom` preset (backbone_vit.py:78-86) accepts any split: smaller head
-                # dims run zero-padded to 64 (kernels.pad_heads, exact), larger ones fail here, not mid-step
+            if self.head_dim > kernels.ATTN_GEN_MAX_HEAD_DIM:
+                # head_dim <= 64 (every reference preset: small 384/6, base 768/12) runs on the placed bf16 kernels
+                # (smaller dims zero-padded, exact), 65..256 on csrc/attention_gen.hip; larger `custom` splits
+                # (backbone_vit.py:78-86) fail here, not mid-step
                 raise ValueError(f"attention head_dim {self.head_dim} (hidden_size {hidden_size} / num_heads "
-                                 f"{num_heads}) is not supported: the HIP flash-attention kernels take head_dim "
-                                 f"<= {ATTN_HEAD_DIM} (DESIGN.md §7)")
+                                 f"{num_heads}) is not supported: the HIP attention kernels take head_dim "
+                                 f"<= {kernels.ATTN_GEN_MAX_HEAD_DIM} (DESIGN.md §7)")
             self.scale = self.head_dim ** -0.5
             self.save_attn = save_attn
             self.att_mat = torch.Tensor()

@@ -1018,6 +1018,13 @@ extern "C" int lci_window_attn_fwd(const void* qkv, const float* qkv_bias, const
   return 0;
 }
 
+// LCI_WIN_BWD1 (A/B hook, default 1: the single-phase backward) read once per process, in one place: the launch and
+// lci_window_bwd_needs_plain must agree even if the environment changes later
+static int win_bwd1_enabled() {
+  static const int v = getenv("LCI_WIN_BWD1") ? atoi(getenv("LCI_WIN_BWD1")) : 1;
+  return v;
+}
+
 // dbias_pad (3C) accumulated (caller zeroes); pad_ws (lci_window_pad_ws_elems f32) required with dbias_pad;
 // dS tiles (Bw*H*nqb*nkt*1024 bf16) optional workspace;
 // drpb (H, N, N) f32 written when dS and drpb are given.
@@ -1036,7 +1043,7 @@ extern "C" int lci_window_attn_bwd(const void* qkv, const float* qkv_bias, const
   hipStream_t s = (hipStream_t)stream;
   // single-phase kernel for windows of <= 12 key blocks (every 7^3 / 7^2 / 4^3 window; LCI_WIN_BWD1=0: the
   // two-phase kernel, A/B hook); waves per (window, head) workgroup of the two-phase kernel: LCI_WIN_BWD_WAVES
-  static const int bwd1_env = getenv("LCI_WIN_BWD1") ? atoi(getenv("LCI_WIN_BWD1")) : 1;
+  const int bwd1_env = win_bwd1_enabled();
   static const int nw_env = getenv("LCI_WIN_BWD_WAVES") ? atoi(getenv("LCI_WIN_BWD_WAVES")) : 4;
   LCI_CHECK(biasT && ((uintptr_t)biasT & 15) == 0, "window_attn_bwd: biasT must be a 16-byte aligned table");
   if (bwd1_env && a.nkt <= WBWD1_MAXW) {
@@ -1078,9 +1085,7 @@ extern "C" int lci_window_attn_bwd(const void* qkv, const float* qkv_bias, const
 extern "C" int lci_window_bwd_needs_plain(const int* geo) {
   WinArgs a{};
   if (win_fill(a, geo, 1.f)) return -1;
-  const char* e = getenv("LCI_WIN_BWD1");
-  const int bwd1_env = e ? atoi(e) : 1;
-  return (bwd1_env && a.nkt <= WBWD1_MAXW) ? 0 : 1;
+  return (win_bwd1_enabled() && a.nkt <= WBWD1_MAXW) ? 0 : 1;
 }
 
 extern "C" long long lci_window_pad_ws_elems(const int* geo) {

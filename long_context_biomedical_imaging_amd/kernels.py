@@ -103,8 +103,51 @@ class _FlashAttention(torch.autograd.Function):
         return attn_bwd(qkv, out, dout, lse2, ctx.num_heads, ctx.scale), None, None
 
 
-ATTN_HEAD_DIM = 64   # csrc/attention.hip DH
+ATTN_HEAD_DIM = 64        # csrc/attention.hip DH (the placed bf16 kernels)
+ATTN_GEN_MAX_HEAD_DIM = 256   # csrc/attention_gen.hip (f32 products: fp32 mode, and head dims above 64)
 WIN_HEAD_DIM = 32    # csrc/window.hip WHD
+
+
+def attn_gen_fwd(qkv: torch.Tensor, num_heads: int, scale: float):
+    """qkv (B, L, 3*H*D) f32 or bf16, any D <= 256 -> out (B, L, H*D) same dtype, lse (B, H, L) f32 (natural log).
+
+    csrc/attention_gen.hip: every product on the f32-input MFMA (exact f32), f32 softmax."""
+    _lib.require_gpu(qkv)
+    B, L, C = qkv.shape
+    dh = C // (3 * num_heads)
+    out = torch.empty(B, L, num_heads * dh, device=qkv.device, dtype=qkv.dtype)
+    lse = torch.empty(B, num_heads, L, device=qkv.device, dtype=torch.float32)
+    KernelTimer.run("attn_gen_fwd", 4.0 * B * num_heads * L * L * dh, qkv, lambda: _lib.call(
+        "lci_attn_gen_fwd", _DT[qkv.dtype], qkv.data_ptr(), out.data_ptr(), lse.data_ptr(), B, L, num_heads, dh,
+        float(scale), _lib.stream_of(qkv)))
+    return out, lse
+
+
+def attn_gen_bwd(qkv, out, dout, lse, num_heads: int, scale: float):
+    _lib.require_gpu(qkv, out, dout, lse)
+    B, L, C = qkv.shape
+    dh = C // (3 * num_heads)
+    dqkv = torch.empty_like(qkv)
+    delta = torch.empty(B, num_heads, L, device=qkv.device, dtype=torch.float32)
+    KernelTimer.run("attn_gen_bwd", 8.0 * B * num_heads * L * L * dh, qkv, lambda: _lib.call(
+        "lci_attn_gen_bwd", _DT[qkv.dtype], qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(),
+        dqkv.data_ptr(), delta.data_ptr(), B, L, num_heads, dh, float(scale), _lib.stream_of(qkv)))
+    return dqkv
+
+
+class _GenAttention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, num_heads, scale):
+        out, lse = attn_gen_fwd(qkv, num_heads, scale)
+        ctx.save_for_backward(qkv, out, lse)
+        ctx.num_heads, ctx.scale = num_heads, scale
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse = ctx.saved_tensors
+        dout = dout.to(qkv.dtype).contiguous()
+        return attn_gen_bwd(qkv, out, dout, lse, ctx.num_heads, ctx.scale), None, None
 
 
 def pad_heads(x: torch.Tensor, parts: int, num_heads: int, to: int) -> torch.Tensor:
@@ -135,19 +178,25 @@ def _check_head_dim(hd: int, limit: int, what: str) -> None:
 def flash_attention(qkv: torch.Tensor, num_heads: int, scale: float) -> torch.Tensor:
     """softmax(q k^T * scale) v for the packed qkv projection (B, L, 3*H*dh) -> (B, L, H*dh).
 
-    Computes in bf16 MFMA with f32 accumulation and f32 softmax. A non-bf16 qkv (no autocast) is cast to
-    bf16 for the kernel and the result cast back. dh < 64 runs zero-padded to the kernels' 64 (pad_heads).
+    bf16 qkv (the trainer's autocast) with dh <= 64: the placed bf16-MFMA kernels (csrc/attention.hip), f32
+    accumulation and softmax; dh < 64 runs zero-padded to 64 (pad_heads). f32 qkv (a model run without autocast,
+    whose reference einsums run in fp32, backbone_vit.py:193,200) and head dims 65..256 (the `custom` splits):
+    csrc/attention_gen.hip, every product in exact f32 (bf16 I/O rounded once on the way out).
     """
     hd = qkv.shape[-1] // (3 * num_heads)
-    _check_head_dim(hd, ATTN_HEAD_DIM, "attention")
+    _check_head_dim(hd, ATTN_GEN_MAX_HEAD_DIM, "attention")
     dt = qkv.dtype
-    q = qkv if dt == torch.bfloat16 else qkv.to(torch.bfloat16)
+    if dt != torch.bfloat16 or hd > ATTN_HEAD_DIM:
+        q = qkv if dt in (torch.float32, torch.bfloat16) else qkv.float()
+        o = _GenAttention.apply(q.contiguous(), num_heads, scale)
+        return o if o.dtype == dt else o.to(dt)
+    q = qkv
     if hd < ATTN_HEAD_DIM:
         q = pad_heads(q, 3, num_heads, ATTN_HEAD_DIM)
     o = _FlashAttention.apply(q.contiguous(), num_heads, scale)
     if hd < ATTN_HEAD_DIM:
         o = unpad_heads(o, num_heads, hd)
-    return o if dt == torch.bfloat16 else o.to(dt)
+    return o
 
 
 # ------------------------------------------------------------------------------------- patch embed

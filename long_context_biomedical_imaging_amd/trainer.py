@@ -153,8 +153,11 @@ class GraphedStep:
             raise ValueError("GraphedStep: single-process TrainStep only")
         if trainer.accum != 1:
             raise ValueError("GraphedStep: iters_to_accumulate > 1 is not supported (the graph always updates)")
-        if inputs.shape[0] == 1 and trainer.dup_batch1:   # TrainStep.step's duplication, once on the static buffers
-            inputs, targets = torch.cat([inputs] * 2, dim=0), torch.cat([targets] * 2, dim=0)
+        # TrainStep.step's duplication of a batch of 1, once on the static buffers; replays duplicate exactly when
+        # the capture did (a BatchNorm model captured at batch 1), never a genuine batch of 2
+        self.dup = inputs.shape[0] == 1 and trainer.dup_batch1
+        if self.dup:
+            inputs, targets = self._dup(inputs), self._dup(targets)
         saved = [(g, g["capturable"]) for g in trainer.optim.param_groups if "capturable" in g]
         for g, _ in saved:
             g["capturable"] = True
@@ -177,12 +180,18 @@ class GraphedStep:
                 g["capturable"] = c
             raise
 
+    @staticmethod
+    def _dup(t):
+        return None if t is None else torch.cat([t] * 2, dim=0)
+
     def step(self, inputs=None, targets=None):
         if inputs is not None and inputs is not self.inputs:
-            if inputs.shape[0] == 1 and self.inputs.shape[0] == 2:
-                inputs, targets = torch.cat([inputs] * 2, dim=0), torch.cat([targets] * 2, dim=0)
+            if self.dup and inputs.shape[0] == 1:
+                inputs = self._dup(inputs)
             self.inputs.copy_(inputs)
         if targets is not None and targets is not self.targets:
+            if self.dup and targets.shape[0] == 1:
+                targets = self._dup(targets)
             self.targets.copy_(targets)
         self.graph.replay()
         return self.loss

@@ -110,8 +110,9 @@ def test_flag_surface_and_factories():
     with pytest.raises(ValueError):
         backbone_vit.SABlock(False, False, 100, 3)
     backbone_vit.SABlock(False, False, 192, 6)                # custom head_dim 32: zero-padded to the kernels' 64
-    with pytest.raises(ValueError, match="head_dim 128"):     # custom split above the kernels' head dim
-        backbone_vit.SABlock(False, False, 1024, 8)
+    backbone_vit.SABlock(False, False, 1024, 8)               # custom head_dim 128: csrc/attention_gen.hip
+    with pytest.raises(ValueError, match="head_dim 512"):     # custom split above the kernels' largest head dim
+        backbone_vit.SABlock(False, False, 1024, 2)
     backbone_swin.WindowAttention(False, False, 48, 3, (7, 7, 7))   # head_dim 16: zero-padded to 32
     with pytest.raises(ValueError, match="head_dim 64"):
         backbone_swin.WindowAttention(False, False, 128, 2, (7, 7, 7))

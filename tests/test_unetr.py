@@ -1,6 +1,10 @@
 """ViTUNETR / SwinUNETR heads (enhance_heads.py:187-356 / 30-184) against golden vectors the reference produced on
 CPU (tools/gen_golden.py:unetr_vit / unetr_swin: the reference's head classes on MONAI-1.3 UNETR blocks restated in
 tools/ref_standins.py, whose internals stay parity-unpinned: MONAI is absent from this image).
+PARITY UNPINNED against real MONAI for the UNETR blocks themselves: decoders.py and the stand-ins were written from
+the same reading of MONAI 1.3, so a misreading of a block (down-sampling rule, padding, norm affine, nesting) would
+appear in both and still pass. What these goldens pin is the reference's head code on top of those blocks (taps,
+proj_feat, up-sampling table, skip order) and the product path's numerics against it.
 
 Cases: ViTUNETR 2-D patch 2 and 4 (the up-sampling table of enhance_heads.py:220-242 at two rows), 3-D patch 2,
 and SwinUNETR 3-D patch 2 with Swin-tiny channels 96 .. 1536 at 64^3. Inputs (image + hidden-state taps / stage
