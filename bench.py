@@ -25,7 +25,6 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import re
 import socket
 import subprocess
 import sys
@@ -181,27 +180,20 @@ def cpu_baseline(budget_s: float = 20.0):
                       f"x12 layers; {ncores} threads (affinity mask capped by OMP_NUM_THREADS)"}
 
 
-# KernelTimer name -> the liblci kernel(s) it launches (rocprofv3 names carry variant suffixes / template args)
-TRAFFIC_KERNELS = {"conv3": r"conv3_fwd\w*_kernel", "conv3_wgrad": r"conv3_wgrad\w*_kernel",
-                   "attn_bwd_dkdv": r"attn_bwd_dkdv\w*_kernel", "attn_bwd_dq": r"attn_bwd_dq\w*_kernel",
-                   "attn_fwd": r"attn_fwd\w*_kernel"}
-
-
-def profiled_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the committed PMC profile of this bench (profiles/traffic.json, written
-    by tools/summarize_prof.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes), or None. A timer name
-    that covers several kernel variants (the conv3 shapes) gets the launch-weighted mean over them."""
+def profiled_traffic(timer: str, workload: str):
+    """HBM bytes per launch of KernelTimer `timer` in `workload`, from that workload's committed PMC profile
+    (profiles/traffic.json `workloads`, written by tools/summarize_prof.py from separate rocprofv3 --pmc FETCH_SIZE /
+    WRITE_SIZE passes of that workload, or by tools/fft_traffic.py for the FFT-conv timers, which launch several
+    kernels per call), or None when the workload has no such profile. Returns (bytes, source)."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     if not os.path.exists(path):
-        return None
+        return None, None
     with open(path) as f:
         prof = json.load(f)
-    pat = TRAFFIC_KERNELS.get(kernel, re.escape(kernel) + r"\w*_kernel")
-    hits = [d for name, d in prof.get("kernels", {}).items() if re.search(pat, name) or name.endswith(kernel)]
-    if not hits:
-        return None
-    n = [d.get("launches", 1) for d in hits]
-    return int(sum(k * (d["read_bytes"] + d["write_bytes"]) for k, d in zip(n, hits)) / sum(n))
+    wl = prof.get("workloads", {}).get(workload)
+    if not wl or timer not in wl.get("timers", {}):
+        return None, None
+    return int(wl["timers"][timer]["bytes_per_call"]), f"profiles/traffic.json workloads.{workload} ({wl['source']})"
 
 
 def _sync(device):
@@ -350,9 +342,10 @@ def run_workload(workload, batch, steps, warmup, rank, world, device, kernel_tim
             bound = "mfma"
         else:
             ach, peak, unit = work / (dd["avg_ms"] * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s"
+        traffic, tsrc = profiled_traffic(dom, workload)
         roof = {"kernel": dom, "bound": bound, "achieved": round(ach, 1), "peak": peak,
                 "unit": unit, "frac": round(ach / peak, 4),
-                "traffic": profiled_traffic(dom), "traffic_source": "profiles/traffic.json",
+                "traffic": traffic, "traffic_source": tsrc,
                 "work_per_launch": work, "avg_launch_ms": round(dd["avg_ms"], 3)}
     return {
         "metric": WORKLOAD_NAMES[workload][0],

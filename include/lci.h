@@ -55,8 +55,8 @@ extern "C" {
  * takes the transposed table biasT, lci_window_attn_bwd's plain table only for windows of N > 384; 15:
  * lci_window_attn_bwd pad_ws; 16: lci_attn_bwd delta_ws is (B, H, 2, L): the negated row constants -lse2 | -delta; 17: lci_window_bwd_needs_plain;
  * 18: lci_attn_bwd delta_ws is lci_attn_bwd_ws_bytes(B, H, L) bytes; 19: selective-scan checkpoints in the I/O
- * dtype; 20: lci_attn_gen_fwd / lci_attn_gen_bwd). */
-#define LCI_ABI_VERSION 20
+ * dtype; 20: lci_attn_gen_fwd / lci_attn_gen_bwd; 21: lci_gemm_bt). */
+#define LCI_ABI_VERSION 21
 const char* lci_last_error(void);
 int lci_abi_version(void);
 /* sha256 prefix of the sources the library was built from (build_lib.source_hash); the Python binding refuses a
@@ -388,6 +388,15 @@ int lci_gelu_fwd(const void* x, void* y, long long n, void* stream);
 int lci_gelu_bwd(const void* x, const void* dy, void* dx, long long n, void* stream);
 int lci_linear_fwd(int epilogue, const void* x, long long ldx, const void* w, const void* bias, void* y,
                    long long ldy, void* aux, long long ldaux, long long M, int N, int K, void* stream);
+/* Projection GEMM (csrc/gemm.hip): y (M, ldy) bf16 = x (M, ldx) . w^T + bias, w (N, K) bf16 contiguous, bias (N) bf16
+ * or null; f32 accumulation, bias added in f32 and the sum rounded once (the autocast nn.Linear's arithmetic). The
+ * forward and data-gradient GEMMs of the token-wise Linear layers: SABlock qkv / out_proj (backbone_vit.py:166-167),
+ * MLPBlock (:249), Hyena in/out_proj (hyena.py:278-279), Mamba in/out_proj (mamba.py:60-64,90); the data gradient
+ * is the call with the transposed weight. Supported when lci_gemm_bt_supported(N, K): N % 384 == 0, N <= 4096,
+ * K % 32 == 0; ldx, ldy % 8 == 0; x / w / y 16-byte aligned; any M (per-tile 32-bit offsets). */
+int lci_gemm_bt_supported(int N, int K);
+int lci_gemm_bt(const void* x, long long ldx, const void* w, const void* bias, void* y, long long ldy, long long M,
+                int N, int K, void* stream);
 
 #ifdef __cplusplus
 }

@@ -20,9 +20,6 @@ namespace lci {
 
 constexpr int SCAN_N = 8;     // d_state (the reference always uses 8: backbone_vit.py:184, backbone_swin.py:329)
 constexpr int CKPT = 8;       // backward checkpoint spacing (steps); sub-block states live in registers
-#ifndef LCI_SCAN_GXA
-#define LCI_SCAN_GXA 1        // backward g a x_{t-1} as (g a) x_{t-1} from the recomputed states (0: g (x_t - dt u B))
-#endif
 constexpr float LOG2E = 1.4426950408889634f;
 
 struct ScanArgs {
@@ -451,30 +448,34 @@ __device__ __forceinline__ float sel_bits(unsigned m, float x, float y) {   // m
 }
 
 // Reduce 16 values over the 64 lanes of a wave (reduce-scatter butterfly); afterwards lane l holds the total of
-// value index (l >> 2) & 15. Levels: lanes l / l^32 by v_permlane32_swap and l / l^16 by v_permlane16_swap on
-// value pairs (the swap itself routes each half its kept index: one add per pair, no select), then l / l^8
-// (DPP row_ror:8) and the half-row mirror (DPP), then the quad (DPP quad_perm) -- no LDS round trips.
-__device__ __forceinline__ float wave_reduce16(float (&v)[16], int lane) {
+// value index (l >> 2) & 15 (vb: the 8 dB values, vc: the 8 dC values, as 4 pairs each: dB 0-7, then dC 8-15).
+// Levels: lanes l / l^32 by v_permlane32_swap and l / l^16 by v_permlane16_swap (the swap routes each half its kept
+// index: one v_pk_add_f32 per value pair, no select), then l / l^8 (DPP row_ror:8) and the half-row mirror (DPP),
+// then the quad (DPP quad_perm) -- no LDS round trips.
+__device__ __forceinline__ float wave_reduce16p(const f32x2 (&vb)[4], const f32x2 (&vc)[4], int lane) {
+  f32x2 w[4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 8]), false, false);
-    v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  for (int k = 0; k < 4; ++k) {   // lanes l / l^32: keep dB (lower half) or dC (upper half) of pair k
+    const auto rx = __builtin_amdgcn_permlane32_swap(__float_as_uint(vb[k].x), __float_as_uint(vc[k].x), false, false);
+    const auto ry = __builtin_amdgcn_permlane32_swap(__float_as_uint(vb[k].y), __float_as_uint(vc[k].y), false, false);
+    w[k] = f32x2{__uint_as_float(rx[0]), __uint_as_float(ry[0])} + f32x2{__uint_as_float(rx[1]), __uint_as_float(ry[1])};
   }
+  f32x2 q[2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 4]), false, false);
-    v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  for (int k = 0; k < 2; ++k) {   // lanes l / l^16: pairs k and k + 2
+    const auto rx = __builtin_amdgcn_permlane16_swap(__float_as_uint(w[k].x), __float_as_uint(w[k + 2].x), false, false);
+    const auto ry = __builtin_amdgcn_permlane16_swap(__float_as_uint(w[k].y), __float_as_uint(w[k + 2].y), false, false);
+    q[k] = f32x2{__uint_as_float(rx[0]), __uint_as_float(ry[0])} + f32x2{__uint_as_float(rx[1]), __uint_as_float(ry[1])};
   }
+  // q[0] = values 0, 1 (of this lane's quarter), q[1] = values 2, 3: the rest as wave_reduce16's last levels
   const unsigned up8 = (lane & 8) ? 0xffffffffu : 0u, up4 = (lane & 4) ? 0xffffffffu : 0u;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const float lo = v[i] + dpp<0x128>(v[i]), hi = v[i + 2] + dpp<0x128>(v[i + 2]);   // row_ror:8 = lane ^ 8
-    v[i] = sel_bits(up8, hi, lo);
-  }
-  const float lo = v[0] + dpp<0x141>(v[0]), hi = v[1] + dpp<0x141>(v[1]);             // row_half_mirror
+  const float lo0 = q[0].x + dpp<0x128>(q[0].x), hi0 = q[1].x + dpp<0x128>(q[1].x);
+  const float lo1 = q[0].y + dpp<0x128>(q[0].y), hi1 = q[1].y + dpp<0x128>(q[1].y);
+  const float v0 = sel_bits(up8, hi0, lo0), v1 = sel_bits(up8, hi1, lo1);
+  const float lo = v0 + dpp<0x141>(v0), hi = v1 + dpp<0x141>(v1);
   float r = sel_bits(up4, hi, lo);
-  r += dpp<0xB1>(r);   // quad_perm [1,0,3,2]
-  r += dpp<0x4E>(r);   // quad_perm [2,3,0,1]
+  r += dpp<0xB1>(r);
+  r += dpp<0x4E>(r);
   return r;
 }
 
@@ -483,10 +484,19 @@ __device__ __forceinline__ float wave_reduce16(float (&v)[16], int lane) {
 // sub-block's states x and decays exp(dt A) are recomputed from its checkpoint into registers, then swept back.
 // B_t / C_t rows and the per-token dB/dC partial sums go through LDS in blocks of SB steps (two workgroup
 // barriers per SB steps); each lane's u / dt / dy / checkpoint loads are issued one sub-block ahead.
+// The per-state arithmetic runs on packed pairs of states (f32x2: v_pk_fma_f32 / v_pk_mul_f32, four instructions
+// per 8 states and operation; the B_t / C_t rows read from LDS as b128 pairs), the per-step column loads and du /
+// d(delta) stores go through buffer resources (wave-uniform token offsets in SGPRs: no 64-bit address VALU), and the
+// kernel is held to 256 registers so two waves share each SIMD (round 5: L = 2^21 backward 8.9 -> 6.5 ms,
+// profiles/r05_scan_ab.txt).
 // PARTIALS: per-(b, chunk) dA / dD / d(delta_bias) partials into the lane's own gin entry (read at the start) and
 // its dead gl entry, summed by scan_param_reduce_kernel, instead of B * nch float atomics per address.
+__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f32x2 splat2(float v) { return f32x2{v, v}; }
+
 template <typename T, bool PARTIALS>
-__global__ __launch_bounds__(256) void scan_bwd_kernel(ScanArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void scan_bwd_kernel(ScanArgs a) {
+  constexpr int NP = SCAN_N / 2;   // state pairs
   __shared__ float red[SB][2 * SCAN_N];
   __shared__ __attribute__((aligned(16))) float bcs[SB][BCS];
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -494,38 +504,41 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(ScanArgs a) {
   const int d = blockIdx.y * blockDim.x + wv * 64 + lane;
   const bool valid = d < a.Dx;
   const int dd = valid ? d : a.Dx - 1;
+  const bool single = blockDim.x == 64;
   for (int i = tid; i < SB * 2 * SCAN_N; i += blockDim.x) (&red[0][0])[i] = 0.f;
-  float A2[SCAN_N], h[SCAN_N], dA[SCAN_N];
+  f32x2 A2[NP], h[NP], dA[NP];
+  {
+    const float* gi = a.gin + (((long long)b * a.nch + chunk) * a.Dx + dd) * SCAN_N;
 #pragma unroll
-  for (int n = 0; n < SCAN_N; ++n) {
-    A2[n] = a.A[dd * SCAN_N + n] * LOG2E;
-    h[n] = valid ? a.gin[(((long long)b * a.nch + chunk) * a.Dx + d) * SCAN_N + n] : 0.f;
-    dA[n] = 0.f;
+    for (int k = 0; k < NP; ++k) {
+      A2[k] = f32x2{a.A[dd * SCAN_N + 2 * k], a.A[dd * SCAN_N + 2 * k + 1]} * LOG2E;
+      h[k] = valid ? f32x2{gi[2 * k], gi[2 * k + 1]} : f32x2{0.f, 0.f};
+      dA[k] = f32x2{0.f, 0.f};
+    }
   }
   const float bias = a.dbias ? a.dbias[dd] : 0.f;
   const float Dd = a.D ? a.D[dd] : 0.f;
   float dDacc = 0.f, dbacc = 0.f;
-  const T* ub = (const T*)a.u + b * a.bu;
-  const T* db = (const T*)a.delta + b * a.bd;
-  const T* gb = (const T*)a.dy + b * a.bdy;
+  const Col<T> ucol((const T*)a.u + b * a.bu, a.L, a.tu, a.Dx, d, valid);
+  const Col<T> dcol((const T*)a.delta + b * a.bd, a.L, a.td, a.Dx, d, valid);
+  const Col<T> gcol((const T*)a.dy + b * a.bdy, a.L, a.tdy, a.Dx, d, valid);
+  const Col<T> ducol((T*)a.du + b * a.bdu, a.L, a.tdu, a.Dx, d, valid);
+  const Col<T> ddcol((T*)a.ddelta + b * a.bdd, a.L, a.tdd, a.Dx, d, valid);
   const T* Bp = (const T*)a.Bm + b * a.bB;
   const T* Cp = (const T*)a.Cm + b * a.bC;
-  T* dub = (T*)a.du + b * a.bdu;
-  T* ddb = (T*)a.ddelta + b * a.bdd;
   const T* ckb = (const T*)a.ckpt + (long long)b * a.nck * a.Dx * SCAN_N;
   const int t0 = chunk * a.Tc, t1 = min(a.L, t0 + a.Tc);
   const int nsb = (t1 - t0 + CKPT - 1) / CKPT;
-  // per-lane operands of one sub-block, loaded a sub-block ahead
+  // per-lane operands of one sub-block, loaded a sub-block ahead (invalid lanes read zeros)
   float nck[SCAN_N], nu[CKPT], nd[CKPT], ng[CKPT];
   auto load_lane = [&](int s0) {
-    const T* cp = (ckb + (long long)(s0 / CKPT) * a.Dx * SCAN_N) + dd * SCAN_N;
-    ld8(cp, nck);
+    ld8((ckb + (long long)(s0 / CKPT) * a.Dx * SCAN_N) + dd * SCAN_N, nck);
 #pragma unroll
     for (int i = 0; i < CKPT; ++i) {
-      const long long t = min(s0 + i, t1 - 1);
-      nu[i] = ldf((ub + t * a.tu) + dd);
-      nd[i] = ldf((db + t * a.td) + dd);
-      ng[i] = ldf((gb + t * a.tdy) + dd);
+      const int t = min(s0 + i, t1 - 1);
+      nu[i] = ucol.ld(t);
+      nd[i] = dcol.ld(t);
+      ng[i] = gcol.ld(t);
     }
   };
   load_lane(t0 + (nsb - 1) * CKPT);
@@ -555,28 +568,30 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(ScanArgs a) {
       }
       __syncthreads();
     }
-    float xck[SCAN_N], uf[CKPT], gyv[CKPT], dts[CKPT];
+    f32x2 xck[NP];
+    float uf[CKPT], gyv[CKPT], dts[CKPT];
 #pragma unroll
-    for (int n = 0; n < SCAN_N; ++n) xck[n] = nck[n];
+    for (int k = 0; k < NP; ++k) xck[k] = f32x2{nck[2 * k], nck[2 * k + 1]};
 #pragma unroll
     for (int i = 0; i < CKPT; ++i) {
       uf[i] = nu[i];
-      gyv[i] = valid ? ng[i] : 0.f;
+      gyv[i] = ng[i];   // 0 on padding lanes (range-checked loads): their dC partials vanish
       dts[i] = softplus(nd[i] + bias);
     }
     if (sb > 0) load_lane(s0 - CKPT);
     const float* rows = &bcs[s0 - blk0][0];
+    auto brow = [&](int i, int k) { return *(const f32x2*)(rows + i * BCS + 2 * k); };
+    auto crow = [&](int i, int k) { return *(const f32x2*)(rows + i * BCS + SCAN_N + 2 * k); };
     // forward recompute from the checkpoint: xs[i] = x after step s0 + i, at[i] = exp(dt A)
-    float xs[CKPT][SCAN_N], at[CKPT][SCAN_N];
+    f32x2 xs[CKPT][NP], at[CKPT][NP];
 #pragma unroll
     for (int i = 0; i < CKPT; ++i) {
-      float Bv[SCAN_N];
-      lds_row8(rows + i * BCS, Bv);
-      const float dtu = dts[i] * uf[i];
-      decay8(dts[i], A2, at[i]);
+      const f32x2 dt2 = splat2(dts[i]), dtu2 = splat2(dts[i] * uf[i]);
 #pragma unroll
-      for (int n = 0; n < SCAN_N; ++n) {
-        xs[i][n] = fmaf(at[i][n], (i == 0) ? xck[n] : xs[i - 1][n], dtu * Bv[n]);
+      for (int k = 0; k < NP; ++k) {
+        const f32x2 arg = dt2 * A2[k];
+        at[i][k] = f32x2{exp2_fast(arg.x), exp2_fast(arg.y)};
+        xs[i][k] = fma2(at[i][k], i == 0 ? xck[k] : xs[i - 1][k], dtu2 * brow(i, k));
       }
     }
     // reverse sweep
@@ -584,40 +599,38 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(ScanArgs a) {
     for (int i = CKPT - 1; i >= 0; --i) {
       const int t = s0 + i;
       if (t < t1) {
-        float Bv[SCAN_N], Cv[SCAN_N];
-        lds_row8(rows + i * BCS, Bv);
-        lds_row8(rows + i * BCS + SCAN_N, Cv);
-        const float dt = dts[i], gy = gyv[i];   // gy = 0 on padding lanes: their dC partials vanish
-        const float dtu = dt * uf[i];
-        const float dtuv = valid ? dtu : 0.f;    // ... and dB partials
-        float v[16];
-        float sgB = 0.f, sA = 0.f;   // sum_n g_n B_n, sum_n g_n (a_n x_{t-1,n}) A2_n
+        const float dt = dts[i], gy = gyv[i], u = uf[i];
+        const f32x2 dt2 = splat2(dt), gy2 = splat2(gy), dtu2 = splat2(dt * u);   // u = 0 on padding lanes
+        f32x2 sgB2 = {0.f, 0.f}, sA2 = {0.f, 0.f};   // sum_n g_n B_n, sum_n g_n (a_n x_{t-1,n}) A2_n (pairs)
+        f32x2 vb[NP], vc[NP];
 #pragma unroll
-        for (int n = 0; n < SCAN_N; ++n) {
-          const float gt = fmaf(Cv[n], gy, h[n]);
-          v[SCAN_N + n] = gy * xs[i][n];                   // dC_t partial
-          v[n] = gt * dtuv;                                // dB_t partial
-          sgB = fmaf(gt, Bv[n], sgB);
-          h[n] = at[i][n] * gt;                            // the adjoint carried to step t-1 (= g a)
-          // g * a * x_{t-1}: (g a) x_{t-1} from the sub-block's recomputed states (one multiply, no cancellation);
-          // at the sub-block's first step x_{t-1} is the checkpoint, no longer live: g (x_t - dt u B)
-          const float gxa = LCI_SCAN_GXA && i > 0 ? h[n] * xs[i - 1][n] : gt * fmaf(-dtu, Bv[n], xs[i][n]);
-          sA = fmaf(gxa, A2[n], sA);
-          dA[n] = fmaf(gxa, dt, dA[n]);
+        for (int k = 0; k < NP; ++k) {
+          const f32x2 gt = fma2(crow(i, k), gy2, h[k]);
+          vc[k] = gy2 * xs[i][k];                   // dC_t partial
+          vb[k] = gt * dtu2;                        // dB_t partial
+          sgB2 = fma2(gt, brow(i, k), sgB2);
+          h[k] = at[i][k] * gt;                     // the adjoint carried to step t-1 (= g a)
+          // g a x_{t-1}: (g a) x_{t-1} from the recomputed states; at the sub-block's first step x_{t-1} is the
+          // checkpoint, no longer live: g (x_t - dt u B)
+          const f32x2 gxa = i > 0 ? h[k] * xs[i - 1][k] : gt * fma2(-dtu2, brow(i, k), xs[i][k]);
+          sA2 = fma2(gxa, A2[k], sA2);
+          dA[k] = fma2(gxa, dt2, dA[k]);
         }
+        const float sgB = sgB2.x + sgB2.y, sA = sA2.x + sA2.y;
         const float du = fmaf(dt, sgB, Dd * gy);
-        const float ddt = fmaf(uf[i], sgB, sA * LN2);
+        const float ddt = fmaf(u, sgB, sA * LN2);
         // d softplus / dx = sigmoid(x) = 1 - exp(-softplus(x))  (1 above the threshold 20)
         const float sg = a.softplus ? 1.f - exp2_fast(-dt * LOG2E) : 1.f;
         const float ddl = ddt * sg;
-        dDacc = fmaf(gy, uf[i], dDacc);
+        dDacc = fmaf(gy, u, dDacc);
         dbacc += ddl;
-        if (valid) {
-          (dub + (long long)t * a.tdu)[dd] = (T)du;
-          (ddb + (long long)t * a.tdd)[dd] = (T)ddl;
+        ducol.st(t, du);
+        ddcol.st(t, ddl);
+        const float r = wave_reduce16p(vb, vc, lane);
+        if ((lane & 3) == 0) {   // one wave per workgroup: the only writer of its (t, j) entry
+          if (single) red[t - blk0][lane >> 2] = r;
+          else atomicAdd(&red[t - blk0][lane >> 2], r);
         }
-        const float r = wave_reduce16(v, lane);
-        if ((lane & 3) == 0) atomicAdd(&red[t - blk0][lane >> 2], r);
       }
     }
   }
@@ -630,13 +643,16 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(ScanArgs a) {
   if constexpr (PARTIALS) {
     if (!valid) return;
     const long long o = (((long long)b * a.nch + chunk) * a.Dx + d) * SCAN_N;
-    *(f32x4*)(a.gin + o) = f32x4{dA[0], dA[1], dA[2], dA[3]};
-    *(f32x4*)(a.gin + o + 4) = f32x4{dA[4], dA[5], dA[6], dA[7]};
+    *(f32x4*)(a.gin + o) = f32x4{dA[0].x, dA[0].y, dA[1].x, dA[1].y};
+    *(f32x4*)(a.gin + o + 4) = f32x4{dA[2].x, dA[2].y, dA[3].x, dA[3].y};
     a.gl[o] = dDacc;
     a.gl[o + 1] = dbacc;
   } else if (valid) {
 #pragma unroll
-    for (int n = 0; n < SCAN_N; ++n) atomicAdd(a.dA + d * SCAN_N + n, dA[n]);
+    for (int k = 0; k < NP; ++k) {
+      atomicAdd(a.dA + d * SCAN_N + 2 * k, dA[k].x);
+      atomicAdd(a.dA + d * SCAN_N + 2 * k + 1, dA[k].y);
+    }
     atomicAdd(a.dD + d, dDacc);
     atomicAdd(a.ddbias + d, dbacc);
   }

@@ -1772,10 +1772,38 @@ def _wgrad_tiny_k(dy2: torch.Tensor, x2: torch.Tensor, bias: bool):
     return dw, (dy2.float().sum(0) if bias else None)
 
 
+# csrc/gemm.hip for the bf16 projection GEMMs whose output width it takes (N % 384 == 0: every ViT-small / Mamba /
+# Hyena projection and data gradient); LCI_HIP_GEMM=0 routes them to torch's hipBLASLt GEMM (A/B hook)
+HIP_GEMM = os.environ.get("LCI_HIP_GEMM", "1") != "0"
+
+
+def gemm_bt_supported(x2: torch.Tensor, N: int, K: int) -> bool:
+    """Whether lci_gemm_bt takes x2 (M, K) bf16 rows (unit column stride, 8-element row stride, 16-B aligned)."""
+    return (HIP_GEMM and x2.is_cuda and x2.dtype == torch.bfloat16 and x2.dim() == 2 and x2.stride(1) == 1
+            and x2.stride(0) % 8 == 0 and x2.data_ptr() % 16 == 0 and x2.shape[0] > 0
+            and bool(_lib.load().lci_gemm_bt_supported(N, K)))
+
+
+def gemm_bt(x2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
+    """y (M, N) bf16 = x2 (M, K) . w^T + bias on csrc/gemm.hip (w (N, K) bf16, made contiguous; bias bf16 or None)."""
+    M, K = x2.shape
+    N = w.shape[0]
+    w = w.contiguous()
+    if bias is not None:
+        bias = bias.contiguous()
+    _lib.require_gpu(w, bias)
+    y = torch.empty(M, N, device=x2.device, dtype=torch.bfloat16)
+    KernelTimer.run("gemm_bt", 2.0 * M * N * K, x2, lambda: _lib.call(
+        "lci_gemm_bt", x2.data_ptr(), x2.stride(0), w.data_ptr(), _lib.ptr(bias), y.data_ptr(), N, M, N, K,
+        _lib.stream_of(x2)))
+    return y
+
+
 class _Linear(torch.autograd.Function):
     """y = x W^T + b with autocast's casts done here (x, W, b -> the autocast dtype, exactly what F.linear under
-    autocast computes: hipBLASLt forward and data gradient); the weight / bias gradient runs on lci_linear_wgrad
-    (f32 result, returned to the f32 parameters without the bf16 rounding the autocast GEMM would apply)."""
+    autocast computes); the bf16 forward and data-gradient GEMMs on csrc/gemm.hip where it takes the shape (hipBLASLt
+    otherwise), the weight / bias gradient on lci_linear_wgrad (f32 result, returned to the f32 parameters without
+    the bf16 rounding the autocast GEMM would apply)."""
 
     @staticmethod
     def forward(ctx, x, weight, bias):
@@ -1785,8 +1813,13 @@ class _Linear(torch.autograd.Function):
             bc = bias.to(dt) if bias is not None else None
         else:
             xc, wc, bc = x, weight, bias
-        with torch.autocast("cuda", enabled=False):
-            y = torch.nn.functional.linear(xc, wc, bc)
+        N, K = wc.shape
+        x2 = xc.reshape(-1, K) if xc.dim() != 2 else xc
+        if x2.dim() == 2 and gemm_bt_supported(x2, N, K):
+            y = gemm_bt(x2, wc, bc).view(*xc.shape[:-1], N)
+        else:
+            with torch.autocast("cuda", enabled=False):
+                y = torch.nn.functional.linear(xc, wc, bc)
         ctx.save_for_backward(xc, wc)
         ctx.has_bias = bias is not None
         return y
@@ -1800,7 +1833,10 @@ class _Linear(torch.autograd.Function):
             dy2 = dy2.contiguous()
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = (dy2 @ wc).view(*dy.shape[:-1], K)
+            if dy2.dtype == wc.dtype and gemm_bt_supported(dy2, K, N):
+                dx = gemm_bt(dy2, wc.t()).view(*dy.shape[:-1], K)   # dX = dY . W = dY . (W^T)^T
+            else:
+                dx = (dy2 @ wc).view(*dy.shape[:-1], K)
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             x2 = xc.reshape(-1, K)
             if K <= 4 and x2.dtype == torch.bfloat16 and pointwise_small_supported(dy2, K):

@@ -3,13 +3,14 @@
 1. BASELINE configs[0] (C1): EncoderDecoderModel(ViT small, 64x64 2-D, patch 16, ViTLinear, 4 classes) —
    reference custom_ViT + class_heads.ViTLinear (backbone_vit.py:45-116, class_heads.py:13-49) run fp32 on CPU by
    tools/gen_golden.py:vit_cls_c1. The fixture pins the seeded init by per-tensor checksums (checked bit-exact on
-   CPU in tests/test_modules_cpu.py), so the model here is rebuilt from the same seed. Tolerances: the attention
-   core computes in bf16 MFMA operands even in an fp32 model, so output rel-L2 <= 2e-2 and
-   gradients <= 5e-2, as for the other attention goldens; under bf16 autocast the same bounds.
+   CPU in tests/test_modules_cpu.py), so the model here is rebuilt from the same seed. Tolerances: without
+   autocast the model is the reference's fp32 path end to end (attention on the exact-f32 kernels of
+   csrc/attention_gen.hip): logits rel-L2 <= 1e-4 and gradients <= 1e-4; under bf16 autocast (the reference's
+   use_amp) logits <= 2e-2 and gradients <= 5e-2, as for the other attention goldens.
 2. The product TrainStep (trainer.py; trainer_base.py:166-182 with optim_base.py:90-91 SGD momentum 0.9,
    CrossEntropy, use_amp off) takes two steps on a small ViT + ViTLinear classifier; the reference took the same
-   two steps (tools/gen_golden.py:train_step_product). Losses within 5e-3 relative; every weight tensor's
-   two-step update (post - pre) within rel-L2 5e-2 of the reference's, element by element.
+   two steps (tools/gen_golden.py:train_step_product). Losses within 1e-5 relative; every weight tensor's
+   two-step update (post - pre) within rel-L2 1e-4 of the reference's, element by element (fp32 end to end).
 """
 import numpy as np
 import pytest
@@ -42,20 +43,25 @@ def test_c1_vit_linear_classification_vs_reference(amp):
         out = m(x)
     ref = g.t("out/0")
     assert out.shape == ref.shape == (2, 4)
+    tol_o, tol_g = (2e-2, 5e-2) if amp else (1e-4, 1e-4)
     e = rel_err(out, ref)
-    assert e < 2e-2, f"logits rel err {e:.3e}"
+    print(f"C1 amp={amp}: logits {e:.2e}")
+    assert e < tol_o, f"logits rel err {e:.3e}"
     out.float().backward(cotangents([ref])[0].cuda())
     params = dict(m.named_parameters())
+    worst = 0.0
     for k in g.z.files:
         if k.startswith("grad/"):
             p = k[5:]
             e = rel_err(params[p].grad, g.t(k))
-            assert e < 5e-2, f"{p}: rel err {e:.3e}"
-    # every parameter's gradient L1 mass (sum |g|) within 5e-2 of the reference's
+            worst = max(worst, e)
+            assert e < tol_g, f"{p}: rel err {e:.3e}"
+    # every parameter's gradient L1 mass (sum |g|) within tol_g of the reference's
     for p, v in params.items():
         ref_abs = float(g.z[f"gsum/{p}"][1])
         got = v.grad.double().abs().sum().item()
-        assert abs(got - ref_abs) <= 5e-2 * ref_abs + 1e-9, f"{p}: sum|g| {got:.6g} vs {ref_abs:.6g}"
+        assert abs(got - ref_abs) <= tol_g * ref_abs + 1e-9, f"{p}: sum|g| {got:.6g} vs {ref_abs:.6g}"
+    print(f"C1 amp={amp}: worst gradient {worst:.2e}")
 
 
 def test_product_train_step_vs_reference():
@@ -75,8 +81,8 @@ def test_product_train_step_vs_reference():
     for i in range(2):
         loss = step.step(g.t(f"in/x{i}").to(dev), g.t(f"in/y{i}").to(dev)).item()
         ref = g.scalar(f"out/loss{i}")
-        assert abs(loss - ref) <= 5e-3 * abs(ref), (i, loss, ref)
-    checked = 0
+        assert abs(loss - ref) <= 1e-5 * abs(ref), (i, loss, ref)
+    checked, worst = 0, 0.0
     for k, v in m.state_dict().items():
         d_ours = v.detach().double().cpu() - pre[k]
         d_ref = torch.from_numpy(np.array(g.z[f"post/{k}"], dtype=np.float64)) - pre[k]
@@ -84,8 +90,10 @@ def test_product_train_step_vs_reference():
             assert d_ours.abs().max() == 0, f"{k}: updated, the reference's is not"
             continue
         e = ((d_ours - d_ref).norm() / d_ref.norm()).item()
-        assert e < 5e-2, f"{k}: update rel err {e:.3e}"
+        worst = max(worst, e)
+        assert e < 1e-4, f"{k}: update rel err {e:.3e}"
         checked += 1
+    print(f"SGD two-step update: worst rel err {worst:.2e}")
     assert checked >= 20
 
 
@@ -96,8 +104,8 @@ def test_product_adam_step_vs_reference(amp):
     product's bf16 autocast (use_amp; no GradScaler with bf16). Adam's first updates are close to lr * sign(g) per
     element, so where the reference gradient is tiny the update direction is decided by rounding noise: the update
     (post - pre) is compared element by element on the elements whose reference gradients at both steps exceed 10 %
-    of the tensor's RMS (rel-L2 <= 3e-2 fp32 / 6e-2 autocast), and its sign agrees on >= 97 % (fp32) / 95 %
-    (autocast) of the elements whose gradients exceed 1 % of the RMS. Losses within 5e-3 / 2e-2 relative."""
+    of the tensor's RMS (rel-L2 <= 1e-3 fp32 / 6e-2 autocast), and its sign agrees on >= 99.5 % (fp32) / 95 %
+    (autocast) of the elements whose gradients exceed 1 % of the RMS. Losses within 1e-5 / 2e-2 relative."""
     from long_context_biomedical_imaging_amd import config, model_base, trainer
     g = Golden("train_step_adam")
     args = ["--encoder_name", "ViT", "--ViT.size", "custom", "--ViT.hidden_size", "128", "--ViT.mlp_dim", "256",
@@ -115,9 +123,9 @@ def test_product_adam_step_vs_reference(amp):
     for i in range(2):
         loss = step.step(g.t(f"in/x{i}").to(dev), g.t(f"in/y{i}").to(dev)).item()
         ref = g.scalar(f"out/loss{i}")
-        assert abs(loss - ref) <= (2e-2 if amp else 5e-3) * abs(ref), (i, loss, ref)
+        assert abs(loss - ref) <= (2e-2 if amp else 1e-5) * abs(ref), (i, loss, ref)
     names = dict(m.named_parameters())
-    checked = 0
+    checked, worst, worst_sign = 0, 0.0, 1.0
     for k in names:
         d_ours = m.state_dict()[k].detach().double().cpu() - pre[k]
         d_ref = torch.from_numpy(np.array(g.z[f"post/{k}"], dtype=np.float64)) - pre[k]
@@ -128,11 +136,13 @@ def test_product_adam_step_vs_reference(amp):
             continue
         strong = (g0 > 0.1 * rms0) & (g1 > 0.1 * rms1)
         e = ((d_ours - d_ref)[strong].norm() / d_ref[strong].norm()).item()
-        assert e <= (6e-2 if amp else 3e-2), f"{k}: update rel err {e:.3e} on {int(strong.sum())} elements"
+        assert e <= (6e-2 if amp else 1e-3), f"{k}: update rel err {e:.3e} on {int(strong.sum())} elements"
         live = (g0 > 0.01 * rms0) & (g1 > 0.01 * rms1)
         agree = (torch.sign(d_ours[live]) == torch.sign(d_ref[live])).double().mean().item()
-        assert agree >= (0.95 if amp else 0.97), f"{k}: update sign agrees on {agree:.4f}"
+        assert agree >= (0.95 if amp else 0.995), f"{k}: update sign agrees on {agree:.4f}"
+        worst, worst_sign = max(worst, e), min(worst_sign, agree)
         checked += 1
+    print(f"Adam amp={amp}: worst strong-element update rel err {worst:.2e}, worst sign agreement {worst_sign:.4f}")
     assert checked >= 20
 
 

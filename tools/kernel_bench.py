@@ -274,6 +274,25 @@ def bench_mlp():
         torch.cuda.empty_cache()
 
 
+def bench_gemm():
+    """Projection GEMMs y = x w^T (+ b), bf16: lci_gemm_bt vs torch's (hipBLASLt, TunableOp table if present) at the
+    ViT-small shapes (qkv 384->1152, out_proj 384->384, fc1 384->1536, fc2 1536->384 and its data gradient) for the
+    metric's M = 131072 tokens and C5's 2^21."""
+    from long_context_biomedical_imaging_amd import trainer
+    trainer.use_tuned_gemms()
+    for M in (131072, 1 << 21):
+        for K, N, nm in ((384, 1152, "qkv"), (384, 384, "out_proj"), (384, 1536, "fc1"), (1536, 384, "fc2")):
+            x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+            w = (torch.randn(N, K, device="cuda") * K ** -0.5).to(torch.bfloat16)
+            b = torch.randn(N, device="cuda").to(torch.bfloat16)
+            f = 2.0 * M * N * K
+            emit(f"gemm_bt {nm}", timeit(lambda: kernels.gemm_bt(x, w, b), iters=10), f, "TFLOP/s", f"M{M} K{K} N{N} bf16")
+            emit(f"torch linear {nm}", timeit(lambda: torch.nn.functional.linear(x, w, b), iters=10), f, "TFLOP/s",
+                 f"M{M} K{K} N{N} bf16 (hipBLASLt)")
+            del x, w, b
+            torch.cuda.empty_cache()
+
+
 def main():
     which = sys.argv[1:] or ["attention", "window", "scan", "fftconv", "patch", "linear", "mlp"]
     if "attention" in which:
@@ -297,6 +316,8 @@ def main():
         bench_linear()
     if "mlp" in which:
         bench_mlp()
+    if "gemm" in which:
+        bench_gemm()
 
 
 if __name__ == "__main__":

@@ -7,7 +7,7 @@ FETCH_SIZE reports half the bytes of a wide (16 B/lane) coalesced streaming read
 Only dispatches after the first `skip_frac` of the run are counted (warm-up includes MIOpen's find phase).
 
     python tools/summarize_prof.py gpurun_out/prof_r01 > profiles/r01_rocprof_summary.md
-    python tools/summarize_prof.py gpurun_out/prof_r01 0.5 profiles/traffic.json   # + per-kernel HBM bytes
+    python tools/summarize_prof.py gpurun_out/prof_r01 0.5 profiles/traffic.json [workload]   # + HBM bytes
 
 Directory layouts: tools/profile_bench.sh (trace/, fetch/, write/) or tools/gpu_round.sh (trace/, pmc_FETCH_SIZE/,
 pmc_WRITE_SIZE/, pmc_SQ_WAVES/). The SQ pass gives, per kernel (MI355X_MICROARCH.md §rocprofv3 PMC slots,
@@ -22,9 +22,18 @@ import sys
 from collections import defaultdict
 
 
+# KernelTimer name (bench.py) -> the liblci kernels it launches (rocprofv3 names carry template arguments)
+TIMER_KERNELS = {"conv3": r"conv3_fwd\w*_kernel", "conv3_wgrad": r"conv3_wgrad\w*_kernel",
+                 "attn_bwd_dkdv": r"attn_bwd_dkdv\w*_kernel", "attn_bwd_dq": r"attn_bwd_dq\w*_kernel",
+                 "attn_fwd": r"attn_fwd\w*_kernel", "gemm_bt": r"gemm_bt_kernel", "window_attn_bwd": r"win_attn_bwd\w*_kernel",
+                 "window_attn_fwd": r"win_attn_fwd\w*_kernel", "selective_scan_bwd": r"scan_bwd\w*_kernel",
+                 "linear_wgrad": r"linear_wgrad\w*_kernel"}
+
+
 def short(name):
     for key in ("attn_fwd", "attn_bwd_dkdv", "attn_bwd_dq", "attn_bwd_delta", "patch_embed", "scan", "window", "fft_",
-                "fftconv", "hyena", "dwconv", "conv3", "inorm", "ln_fwd", "ln_bwd", "linear_", "gelu_", "upsample2x", "hf_"):
+                "fftconv", "hyena", "dwconv", "conv3", "inorm", "ln_fwd", "ln_bwd", "linear_", "gelu_", "upsample2x", "hf_",
+                "gemm_bt", "win_", "longconv", "row_dot"):
         if key in name:
             return name.split("(")[0].replace("void ", "")
     return None
@@ -94,6 +103,7 @@ def main():
         counters[c] = acc
     if len(sys.argv) > 3:   # per-kernel HBM bytes per launch as JSON (bench.py's roofline.traffic)
         import json
+        import re
         out = {}
         for n in dur:
             f = counters.get("fetch", {}).get(n)
@@ -101,8 +111,22 @@ def main():
             if f and w:
                 out[n] = {"read_bytes": 2.0 * sum(f) / len(f) * 1024, "write_bytes": sum(w) / len(w) * 1024,
                           "avg_ms": sum(dur[n]) / len(dur[n]), "launches": len(dur[n])}
-        json.dump({"source": d, "note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB -> bytes, per launch",
-                   "kernels": out}, open(sys.argv[3], "w"), indent=1)
+        # per KernelTimer name (bench.py's roofline kernel): the launch-weighted mean over the kernels it launches
+        timers = {}
+        for t, pat in TIMER_KERNELS.items():
+            hits = [v for k, v in out.items() if re.search(pat, k)]
+            if hits:
+                nl = sum(v["launches"] for v in hits)
+                timers[t] = {"bytes_per_call": sum(v["launches"] * (v["read_bytes"] + v["write_bytes"]) for v in hits) / nl,
+                             "kernels": sorted(k for k, v in out.items() if re.search(pat, k)), "launches": nl}
+        path, wl = sys.argv[3], (sys.argv[4] if len(sys.argv) > 4 else "vit_p2_512")
+        doc = json.load(open(path)) if os.path.exists(path) else {}
+        doc.pop("kernels", None); doc.pop("source", None)
+        doc["note"] = ("per workload: HBM bytes per launch from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of "
+                       "that workload (FETCH_SIZE x2, the gfx950 correction; KiB -> bytes); `timers` = per KernelTimer "
+                       "name, launch-weighted over the kernels it launches")
+        doc.setdefault("workloads", {})[wl] = {"source": d, "kernels": out, "timers": timers}
+        json.dump(doc, open(path, "w"), indent=1)
     print(f"# rocprofv3 summary: {d}\n")
     print(f"Kernel-trace dispatches counted: the last {100 * (1 - skip_frac):.0f}% of the run "
           f"({len(tr) - start} of {len(tr)} dispatches).\n")
