@@ -17,6 +17,8 @@
 // are conflict-free; one raw s_barrier per slab after a counted vmcnt (vmcnt counts the epilogue's stores too, in
 // issue order). The epilogue stores each lane's 4 consecutive features as 8-B pieces straight from the registers
 // (buffer stores range-checked at the token tile's end: M need not be a multiple of 256), bias from LDS.
+#include <stdlib.h>
+
 #include <algorithm>
 #include <type_traits>
 
@@ -40,6 +42,7 @@ struct GemmArgs {
   int ntn;                        // feature tiles
   long long ntiles;
   int G8, dmt, dnt;               // workgroups per XCD; G8 tiles = dmt token tiles + dnt feature tiles
+  int probe;                      // timing probe (LCI_GEMM_PROBE, wrong results): 1 = no epilogue stores
 };
 
 // LDS-DMA of one 1-KB unit: lane l's 16 bytes at (voff + soff) of resource r land at LDS byte lds + 16 l
@@ -205,7 +208,7 @@ __global__ __launch_bounds__(GM_WAVES * 64, 1) void gemm_bt_kernel(GemmArgs a) {
             bf16x4 o;
 #pragma unroll
             for (int q = 0; q < 4; ++q) o[q] = to_bf16(acc[i][j][4 * g + q] + b4[q]);
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), ry, vbase,
+            if (!a.probe) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), ry, vbase,
                                                   (128 * wm + 32 * j) * ldy2 + fs * 2, 0);
           }
         }
@@ -247,6 +250,8 @@ extern "C" int lci_gemm_bt(const void* x, long long ldx, const void* w, const vo
   a.G8 = (int)(grid / 8);
   a.dmt = a.G8 / a.ntn;
   a.dnt = a.G8 % a.ntn;
+  static const int probe = getenv("LCI_GEMM_PROBE") ? atoi(getenv("LCI_GEMM_PROBE")) : 0;
+  a.probe = probe;
   constexpr int TN = 384;
   const size_t sh = (size_t)GM_NSLOT * (GM_TM + TN) * 64 + GM_MAXN * 2;
   (void)hipFuncSetAttribute((const void*)gemm_bt_kernel<TN>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);

@@ -1773,13 +1773,14 @@ def _wgrad_tiny_k(dy2: torch.Tensor, x2: torch.Tensor, bias: bool):
 
 
 # csrc/gemm.hip for the bf16 projection GEMMs whose output width it takes (N % 384 == 0: every ViT-small / Mamba /
-# Hyena projection and data gradient); LCI_HIP_GEMM=0 routes them to torch's hipBLASLt GEMM (A/B hook)
-HIP_GEMM = os.environ.get("LCI_HIP_GEMM", "1") != "0"
+# Hyena projection and data gradient): opt-in (LCI_HIP_GEMM=1) while it is slower than the TunableOp-tuned hipBLASLt
+# GEMM on the metric shapes (profiles/r05_gemm_ab.txt)
+HIP_GEMM = os.environ.get("LCI_HIP_GEMM", "0") == "1"
 
 
 def gemm_bt_supported(x2: torch.Tensor, N: int, K: int) -> bool:
     """Whether lci_gemm_bt takes x2 (M, K) bf16 rows (unit column stride, 8-element row stride, 16-B aligned)."""
-    return (HIP_GEMM and x2.is_cuda and x2.dtype == torch.bfloat16 and x2.dim() == 2 and x2.stride(1) == 1
+    return (x2.is_cuda and x2.dtype == torch.bfloat16 and x2.dim() == 2 and x2.stride(1) == 1
             and x2.stride(0) % 8 == 0 and x2.data_ptr() % 16 == 0 and x2.shape[0] > 0
             and bool(_lib.load().lci_gemm_bt_supported(N, K)))
 
@@ -1815,7 +1816,7 @@ class _Linear(torch.autograd.Function):
             xc, wc, bc = x, weight, bias
         N, K = wc.shape
         x2 = xc.reshape(-1, K) if xc.dim() != 2 else xc
-        if x2.dim() == 2 and gemm_bt_supported(x2, N, K):
+        if HIP_GEMM and x2.dim() == 2 and gemm_bt_supported(x2, N, K):
             y = gemm_bt(x2, wc, bc).view(*xc.shape[:-1], N)
         else:
             with torch.autocast("cuda", enabled=False):
@@ -1833,7 +1834,7 @@ class _Linear(torch.autograd.Function):
             dy2 = dy2.contiguous()
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            if dy2.dtype == wc.dtype and gemm_bt_supported(dy2, K, N):
+            if HIP_GEMM and dy2.dtype == wc.dtype and gemm_bt_supported(dy2, K, N):
                 dx = gemm_bt(dy2, wc.t()).view(*dy.shape[:-1], K)   # dX = dY . W = dY . (W^T)^T
             else:
                 dx = (dy2 @ wc).view(*dy.shape[:-1], K)

@@ -43,9 +43,10 @@ def test_gemm_bt_vs_fp64(M, N, K, bias, pad):
 
 
 @pytest.mark.parametrize("D,H,M", [(384, 1152, 3000), (1536, 384, 2048), (384, 384, 513)])
-def test_token_linear_autocast_fwd_bwd(D, H, M):
-    """TokenLinear (kernels.linear) under bf16 autocast vs torch's autocast nn.Linear on the same weights."""
+def test_token_linear_autocast_fwd_bwd(D, H, M, monkeypatch):
+    """TokenLinear (kernels.linear) on lci_gemm_bt under bf16 autocast vs torch's autocast nn.Linear, same weights."""
     from long_context_biomedical_imaging_amd import blocks, kernels
+    monkeypatch.setattr(kernels, "HIP_GEMM", True)
     torch.manual_seed(D + H)
     lin = blocks.TokenLinear(D, H).cuda()
     ref = torch.nn.Linear(D, H).cuda()
