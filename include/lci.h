@@ -55,8 +55,9 @@ extern "C" {
  * takes the transposed table biasT, lci_window_attn_bwd's plain table only for windows of N > 384; 15:
  * lci_window_attn_bwd pad_ws; 16: lci_attn_bwd delta_ws is (B, H, 2, L): the negated row constants -lse2 | -delta; 17: lci_window_bwd_needs_plain;
  * 18: lci_attn_bwd delta_ws is lci_attn_bwd_ws_bytes(B, H, L) bytes; 19: selective-scan checkpoints in the I/O
- * dtype; 20: lci_attn_gen_fwd / lci_attn_gen_bwd; 21: lci_gemm_bt). */
-#define LCI_ABI_VERSION 21
+ * dtype; 20: lci_attn_gen_fwd / lci_attn_gen_bwd; 21: lci_gemm_bt; 22: lci_linear_fwd removed, superseded by
+ * lci_gemm_bt). */
+#define LCI_ABI_VERSION 22
 const char* lci_last_error(void);
 int lci_abi_version(void);
 /* sha256 prefix of the sources the library was built from (build_lib.source_hash); the Python binding refuses a
@@ -366,14 +367,6 @@ int lci_layernorm_bwd(const float* x, const void* dy, int bf16_dy, const float* 
 long long lci_linear_wgrad_splits(long long M, int N, int K);
 int lci_linear_wgrad(const void* dy, long long ldy, const void* x, long long ldx, long long M, int N, int K,
                      float* part, float* dbpart, void* stream);
-/* y (M, ldy) bf16 = epilogue(x (M, ldx) bf16 . w^T), w (N, K) bf16 contiguous, f32 accumulation:
- *   epilogue 0: y = bf16(acc + bias)            (bias (N) bf16 or null; nn.Linear under autocast)
- *   epilogue 1: aux = pre = bf16(acc + bias), y = bf16(gelu(pre))    (MLPBlock linear1 + GELU, exact erf)
- *   epilogue 2: y = bf16(bf16(acc) * gelu'(aux))  (linear2's data gradient through GELU; aux = saved pre)
- * The data gradient of a Linear is the same call with the transposed weight. Supported when
- * lci_linear_fwd_supported(N, K): N % 128 == 0 or N % 96 == 0, K % 8 == 0; row strides % 8 == 0,
- * x / w / y / aux 16-byte aligned, bias 8-byte aligned. */
-int lci_linear_fwd_supported(int N, int K);
 /* Narrow outputs (the UNETR heads' 1x1 conv to 1-8 channels, over channels-last voxel rows): y (M, N) bf16 =
  * x (M, ldx) . w^T + bias, w (N, K) bf16, bias (N) bf16 or null; N <= 8, K <= 256, K % 8 == 0.
  * bwd (N <= 4): dx (M, K) bf16 = dy . w (optional); part ((N K + N), lci_linear_small_threads()) f32 <- per-thread
@@ -386,8 +379,6 @@ int lci_linear_small_bwd(const void* x, long long ldx, const void* w, const void
 /* GELU (erf) of n bf16 elements (n % 8 == 0, 16-B aligned): y = gelu(x); dx = dy * gelu'(x). */
 int lci_gelu_fwd(const void* x, void* y, long long n, void* stream);
 int lci_gelu_bwd(const void* x, const void* dy, void* dx, long long n, void* stream);
-int lci_linear_fwd(int epilogue, const void* x, long long ldx, const void* w, const void* bias, void* y,
-                   long long ldy, void* aux, long long ldaux, long long M, int N, int K, void* stream);
 /* Projection GEMM (csrc/gemm.hip): y (M, ldy) bf16 = x (M, ldx) . w^T + bias, w (N, K) bf16 contiguous, bias (N) bf16
  * or null; f32 accumulation, bias added in f32 and the sum rounded once (the autocast nn.Linear's arithmetic). The
  * forward and data-gradient GEMMs of the token-wise Linear layers: SABlock qkv / out_proj (backbone_vit.py:166-167),

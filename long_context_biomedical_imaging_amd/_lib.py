@@ -14,7 +14,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_LIB = os.path.join(HERE, "liblci.so")
 LIB_PATH = os.environ.get("LCI_LIB_PATH", DEFAULT_LIB)   # override: kernel-variant A/B runs (no staleness check)
-ABI_VERSION = 21   # include/lci.h LCI_ABI_VERSION
+ABI_VERSION = 22   # include/lci.h LCI_ABI_VERSION
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -59,7 +59,6 @@ SIGNATURES = {
     "lci_layernorm_bwd": [_P, _P, _I, _P, _P, _P, _P, _P, _P, _L, _I, _P],
     "lci_dwconv_silu_bwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "lci_linear_wgrad": [_P, _L, _P, _L, _L, _I, _I, _P, _P, _P],
-    "lci_linear_fwd": [_I, _P, _L, _P, _P, _P, _L, _P, _L, _L, _I, _I, _P],
     "lci_gemm_bt": [_P, _L, _P, _P, _P, _L, _L, _I, _I, _P],
     "lci_linear_small_fwd": [_P, _L, _P, _P, _P, _L, _I, _I, _P],
     "lci_linear_small_bwd": [_P, _L, _P, _P, _P, _P, _L, _I, _I, _P],
@@ -128,8 +127,6 @@ def load(path: str = LIB_PATH):
     lib.lci_conv3_wgrad_splits.argtypes = [ctypes.c_longlong, _I, _I, _I]
     lib.lci_linear_wgrad_splits.restype = ctypes.c_longlong
     lib.lci_linear_wgrad_splits.argtypes = [ctypes.c_longlong, _I, _I]
-    lib.lci_linear_fwd_supported.restype = ctypes.c_int
-    lib.lci_linear_fwd_supported.argtypes = [_I, _I]
     lib.lci_gemm_bt_supported.restype = ctypes.c_int
     lib.lci_gemm_bt_supported.argtypes = [_I, _I]
     lib.lci_linear_small_threads.restype = ctypes.c_int

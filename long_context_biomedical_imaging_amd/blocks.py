@@ -59,20 +59,14 @@ class TokenLayerNorm(nn.LayerNorm):
 
 
 class TokenLinear(nn.Linear):
-    """nn.Linear (same parameters, state_dict keys and seeded init) for the token-wise projections. On the GPU the
-    forward and data gradient are the autocast GEMMs torch would run (hipBLASLt); the weight and bias gradients,
-    a reduction over all B*L tokens into a small N x K output, run on lci_linear_wgrad (kernels.linear)."""
+    """nn.Linear (same parameters, state_dict keys and seeded init) for the token-wise projections. On the GPU
+    (kernels.linear) the forward and data gradient run on lci_gemm_bt where it takes the shape (hipBLASLt otherwise),
+    the weight and bias gradients, a reduction over all B*L tokens into a small N x K output, on lci_linear_wgrad."""
 
     def forward(self, x):
         if x.is_cuda:
             return kernels.linear(x, self.weight, self.bias)
         return super().forward(x)
-
-
-# MLPBlock on the fused-epilogue HIP GEMMs (lci_linear_fwd): opt-in (LCI_FUSED_MLP=1). Parity-tested, but measured
-# slower than hipBLASLt + torch's GELU kernels on MI355X today (DESIGN.md §4, tools/kernel_bench.py mlp), so the
-# default keeps the TokenLinear path (hipBLASLt forward / data gradient, HIP weight gradient).
-FUSED_MLP = os.environ.get("LCI_FUSED_MLP", "0") == "1"
 
 
 class MLPBlock(nn.Module):
@@ -96,11 +90,6 @@ class MLPBlock(nn.Module):
             raise ValueError(f"dropout_mode {dropout_mode}")
 
     def forward(self, x):
-        D, H = self.linear1.in_features, self.linear1.out_features
-        if (FUSED_MLP and self.drop1.p == 0 and self.drop2.p == 0 and self.linear1.bias is not None
-                and kernels.mlp_supported(x, D, H)):
-            # fused HIP path (kernels.mlp): GEMM epilogues carry bias + GELU forward and GELU' backward
-            return kernels.mlp(x, self.linear1.weight, self.linear1.bias, self.linear2.weight, self.linear2.bias)
         h = self.linear1(x)
         h = kernels.gelu(h) if kernels.gelu_supported(h) else self.fn(h)
         return self.drop2(self.linear2(self.drop1(h)))

@@ -10,15 +10,21 @@
 // no per-tile prologue. Tiles are dealt out XCD-contiguously (blocks b and b + 8 share an XCD): the feature tiles of
 // one token tile run on one XCD at the same time and read its X rows from that XCD's L2.
 //
-// Per workgroup: 8 waves = 2 (tokens, 128 each) x 4 (features, 96 each); a wave holds 4 x 3 accumulator blocks of
+// Per workgroup: 8 waves = 4 (tokens, 64 each) x 2 (features, 192 each); a wave holds 6 x 2 accumulator blocks of
 // v_mfma_f32_32x32x16_bf16 (W the A operand: features on the accumulator registers, tokens on the lanes). K slabs of
 // 32 arrive by LDS-DMA (buffer_load_dwordx4 ... lds, 1-KB units = 16 rows x 64 B) into a 3-slot ring two slabs ahead,
 // 16-B chunks XOR-swizzled by (row >> 2) & 3 through the per-lane source offset so the ds_read_b128 fragment reads
 // are conflict-free; one raw s_barrier per slab after a counted vmcnt (vmcnt counts the epilogue's stores too, in
-// issue order). The epilogue stores each lane's 4 consecutive features as 8-B pieces straight from the registers
-// (buffer stores range-checked at the token tile's end: M need not be a multiple of 256), bias from LDS.
-#include <stdlib.h>
-
+// issue order). A slab's 5 DMA units per wave are issued one per MFMA group of its first k-substep (an LDS-DMA
+// instruction holds its wave's issue for tens of cycles), and the second k-substep's W fragments are read as the
+// first substep's MFMAs release their registers.
+//
+// Epilogue: each wave turns 32 tokens x 64 features at a time into bf16 (+ bias) rows of 128 B in its own 4-KB LDS
+// buffer (v_permlane32_swap pairs the two half-waves' 8-B pieces into 16-B chunks; chunks XOR-swizzled by row & 7,
+// conflict-free both ways) and stores them back as whole 128-B lines, 8 rows per buffer_store_dwordx4. Stored
+// straight from the MFMA layout instead (each instruction touching 32 rows x 16 B), the tile's stores cost as much
+// as its MFMAs (profiles/r05_gemm_ab.txt). Buffer stores are range-checked at the token tile's end (M need not be a
+// multiple of 256).
 #include <algorithm>
 #include <type_traits>
 
@@ -31,6 +37,7 @@ constexpr int GM_WAVES = 8;
 constexpr int GM_BK = 32;         // K per slab
 constexpr int GM_NSLOT = 3;
 constexpr int GM_MAXN = 4096;     // bias staged in LDS
+constexpr int GM_EPI = 4096;      // per-wave epilogue buffer (32 tokens x 64 features bf16)
 
 struct GemmArgs {
   const bf16* x; long long ldx;   // (M, ldx), columns [0, K)
@@ -42,7 +49,6 @@ struct GemmArgs {
   int ntn;                        // feature tiles
   long long ntiles;
   int G8, dmt, dnt;               // workgroups per XCD; G8 tiles = dmt token tiles + dnt feature tiles
-  int probe;                      // timing probe (LCI_GEMM_PROBE, wrong results): 1 = no epilogue stores
 };
 
 // LDS-DMA of one 1-KB unit: lane l's 16 bytes at (voff + soff) of resource r land at LDS byte lds + 16 l
@@ -60,16 +66,18 @@ __device__ __forceinline__ void gm_vmcnt() {   // s_waitcnt vmcnt(N), lgkmcnt / 
 
 template <int TN>
 __global__ __launch_bounds__(GM_WAVES * 64, 1) void gemm_bt_kernel(GemmArgs a) {
-  constexpr int WN = 4, WM = 2;
+  constexpr int WN = 2, WM = 4;
   constexpr int NB = TN / WN / 32, MB = GM_TM / WM / 32;           // 32x32 blocks per wave (features, tokens)
   constexpr int ROWS = GM_TM + TN;                                 // LDS rows per slab (64 B each)
   constexpr int SLOT_B = ROWS * 64;
   constexpr int UNITS = ROWS / 16, UX = GM_TM / 16;                // 1-KB DMA units per slab; X units first
   constexpr int UPW = UNITS / GM_WAVES;
   static_assert(UNITS % GM_WAVES == 0 && UX % GM_WAVES == 0, "units per wave");
-  static_assert(GM_NSLOT * SLOT_B + GM_MAXN * 2 <= 160 * 1024, "LDS");
+  static_assert(GM_NSLOT * SLOT_B + GM_WAVES * GM_EPI + GM_MAXN * 2 <= 160 * 1024, "LDS");
+  static_assert(NB % 2 == 0, "epilogue chunks are 64 features");
   extern __shared__ __attribute__((aligned(16))) char gsm[];
-  bf16* sbias = (bf16*)(gsm + GM_NSLOT * SLOT_B);
+  char* sepi = gsm + GM_NSLOT * SLOT_B;
+  bf16* sbias = (bf16*)(sepi + GM_WAVES * GM_EPI);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
@@ -117,22 +125,20 @@ __global__ __launch_bounds__(GM_WAVES * 64, 1) void gemm_bt_kernel(GemmArgs a) {
   Cursor ic = c0;
   rsrc_t irx = x_rsrc(ic);
   int ik = 0, ij = 0, islot = 0;   // issue stream: slab ik of tile ij, into ring slot islot
-  auto issue = [&]() {
-    const unsigned sb = lds0 + (unsigned)(islot * SLOT_B);
+  // One slab's DMA: issue_begin() takes the next slab of the stream (its LDS slot, K offset, lane source offsets)
+  // and advances the stream; piece(d, q) issues its unit q (X units first). The pieces are spread between the first
+  // k-substep's MFMA groups (an LDS-DMA instruction holds its wave's issue for tens of cycles).
+  struct Dma { unsigned sb; int ko, xo, wo; rsrc_t rx; };
+  auto issue_begin = [&]() {
+    Dma d{lds0 + (unsigned)(islot * SLOT_B), ik * GM_BK * 2, 0, 0, irx};
     islot = islot == GM_NSLOT - 1 ? 0 : islot + 1;
-    const int ko = ik * GM_BK * 2;
     // lane source offsets, recomputed per issue (a few VALU) rather than held across the loop in registers: the
     // lane index made opaque so the compiler does not hoist them
     int l = lane;
     asm volatile("" : "+v"(l));
     const int drow = l >> 2, dchunk = (l & 3) ^ ((l >> 4) & 3);
-    const int xo = (16 * wave + drow) * ldx2 + 16 * dchunk;
-    const int wo = (16 * (wave + GM_WAVES * (UX / GM_WAVES) - UX) + drow + ic.n0()) * K2 + 16 * dchunk;
-#pragma unroll
-    for (int q = 0; q < UX / GM_WAVES; ++q) gm_dma16(irx, xo + 16 * GM_WAVES * q * ldx2, ko, sb + 1024 * (wave + GM_WAVES * q));
-#pragma unroll
-    for (int q = 0; q < UPW - UX / GM_WAVES; ++q)
-      gm_dma16(rw, wo + 16 * GM_WAVES * q * K2, ko, sb + 1024 * (wave + GM_WAVES * (q + UX / GM_WAVES)));
+    d.xo = (16 * wave + drow) * ldx2 + 16 * dchunk;
+    d.wo = (16 * (wave + GM_WAVES * (UX / GM_WAVES) - UX) + drow + ic.n0()) * K2 + 16 * dchunk;
     if (++ik == nslab) {   // next tile
       ik = 0;
       ++ij;
@@ -141,75 +147,125 @@ __global__ __launch_bounds__(GM_WAVES * 64, 1) void gemm_bt_kernel(GemmArgs a) {
         irx = x_rsrc(ic);
       }
     }
+    return d;
   };
+  auto piece = [&](const Dma& d, int q) __attribute__((always_inline)) {
+    constexpr int QX = UX / GM_WAVES;
+    if (q < QX) gm_dma16(d.rx, d.xo + 16 * GM_WAVES * q * ldx2, d.ko, d.sb + 1024 * (wave + GM_WAVES * q));
+    else gm_dma16(rw, d.wo + 16 * GM_WAVES * (q - QX) * K2, d.ko, d.sb + 1024 * (wave + GM_WAVES * q));
+  };
+
 
   f32x16 acc[NB][MB];
-  // fragment offsets within a slot: the swizzle depends on the lane's row bits 2-3 only (block rows are multiples
-  // of 32), so the two k-substeps' chunk offsets are lane constants
-  const int sw = (r >> 2) & 3;
-  const int coff0 = 16 * ((0 + h) ^ sw), coff1 = 16 * ((2 + h) ^ sw);
-  const int xrow0 = (128 * wm + r) * 64, wrow0 = (GM_TM + 96 * wn + r) * 64;
+  constexpr int WT = GM_TM / WM, WF = TN / WN;                     // tokens, features per wave
 
-  // one slab's MFMAs (FIRST: the tile's first slab starts its accumulators from zero, no zeroing pass)
-  auto compute = [&](const char* slot, auto FIRST) __attribute__((always_inline)) {
+  // one slab's MFMAs (FIRST: the tile's first slab starts its accumulators from zero, no zeroing pass). Fragment
+  // offsets within a slot: the swizzle depends on the lane's row bits 2-3 only (block rows are multiples of 32), so
+  // the two k-substeps' chunk offsets are lane constants -- recomputed per slab from an opaque lane index (a few VALU)
+  // rather than held across the loop for every slot
+  auto compute = [&](const char* slot, auto FIRST, bool iss, const Dma& d) __attribute__((always_inline)) {
+    int l = lane;
+    asm volatile("" : "+v"(l));
+    const int fr = l & 31, fh = l >> 5, sw = (fr >> 2) & 3;
+    const char* xb = slot + (WT * wm + fr) * 64;
+    const char* wb = slot + (GM_TM + WF * wn + fr) * 64;
+    // reads and MFMAs of the two k-substeps interleaved: substep 1's W fragment i is read into fragment i's
+    // registers as soon as substep 0's two MFMAs on it have issued (LDS returns in order; the waitcnt pass counts)
+    const int co0 = 16 * (fh ^ sw), co1 = 16 * ((2 + fh) ^ sw);
+    bf16x8 fw[NB], fx0[MB], fx1[MB];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int co = ks ? coff1 : coff0;
-      bf16x8 fw[NB], fx[MB];
+    for (int j = 0; j < MB; ++j) fx0[j] = *(const bf16x8*)(xb + 32 * 64 * j + co0);
 #pragma unroll
-      for (int i = 0; i < NB; ++i) fw[i] = *(const bf16x8*)(slot + wrow0 + 32 * 64 * i + co);
+    for (int i = 0; i < NB; ++i) fw[i] = *(const bf16x8*)(wb + 32 * 64 * i + co0);
 #pragma unroll
-      for (int j = 0; j < MB; ++j) fx[j] = *(const bf16x8*)(slot + xrow0 + 32 * 64 * j + co);
+    for (int j = 0; j < MB; ++j) fx1[j] = *(const bf16x8*)(xb + 32 * 64 * j + co1);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int i = 0; i < NB; ++i)
+    for (int i = 0; i < NB; ++i) {
 #pragma unroll
-        for (int j = 0; j < MB; ++j)
-          acc[i][j] = mfma32(fw[i], fx[j], (decltype(FIRST)::value && ks == 0) ? f32x16{} : acc[i][j]);
+      for (int j = 0; j < MB; ++j) acc[i][j] = mfma32(fw[i], fx0[j], decltype(FIRST)::value ? f32x16{} : acc[i][j]);
+      __builtin_amdgcn_sched_barrier(0);
+      fw[i] = *(const bf16x8*)(wb + 32 * 64 * i + co1);
+      if (iss && i < UPW) piece(d, i);
+      __builtin_amdgcn_sched_barrier(0);
     }
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+#pragma unroll
+      for (int j = 0; j < MB; ++j) acc[i][j] = mfma32(fw[i], fx1[j], acc[i][j]);
   };
 
-  issue();
-  if (S > 1) issue();
+  static_assert(UPW <= NB, "one DMA piece per MFMA group");
+  for (int t = 0; t < 2 && t < S; ++t) {
+    const Dma d = issue_begin();
+#pragma unroll
+    for (int q = 0; q < UPW; ++q) piece(d, q);
+  }
   Cursor cc = c0;             // the tile being computed
   int ck = 0, cj = 0, cslot = 0;
   int since_epi = 8;          // slabs since the last epilogue
   for (int s = 0; s < S; ++s) {
     ++since_epi;
     // slab s landed: the next slab's UPW units may still be in flight, and, in the two slabs after an epilogue, its
-    // 4 NB MB stores too (they were issued between two slabs' units; vmcnt retires in issue order)
+    // 2 NB MB stores too (they were issued between two slabs' units; vmcnt retires in issue order)
     if (s + 1 >= S) gm_vmcnt<0>();
-    else if (since_epi <= 2) gm_vmcnt<UPW + 4 * NB * MB>();
+    else if (since_epi <= 2) gm_vmcnt<UPW + 2 * NB * MB>();
     else gm_vmcnt<UPW>();
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's reads of the slot being refilled are done
     __builtin_amdgcn_s_barrier();
-    if (s + 2 < S) issue();               // into slot (s + 2) % 3 = (s - 1) % 3, free after this barrier
+    const bool iss = s + 2 < S;           // slab s + 2 into slot (s + 2) % 3 = (s - 1) % 3, free after this barrier
+    Dma d{0u, 0, 0, 0, irx};
+    if (iss) d = issue_begin();
     const char* slot = gsm + cslot * SLOT_B;
     cslot = cslot == GM_NSLOT - 1 ? 0 : cslot + 1;
-    if (ck == 0) compute(slot, std::integral_constant<bool, true>{});
-    else compute(slot, std::integral_constant<bool, false>{});
-    if (++ck == nslab) {   // the tile's last slab: epilogue straight from the registers
+    if (ck == 0) compute(slot, std::integral_constant<bool, true>{}, iss, d);
+    else compute(slot, std::integral_constant<bool, false>{}, iss, d);
+    if (++ck == nslab) {   // the tile's last slab: epilogue through the wave's LDS buffer
       const long long rows = min((long long)GM_TM, a.M - cc.m0());
       const rsrc_t ry = make_rsrc(a.y + cc.m0() * a.ldy, (uint32_t)(rows * a.ldy * 2));
       const int ldy2 = (int)a.ldy * 2;
-      const int vbase = r * ldy2 + 8 * h;   // the lane's part of every store offset; the rest is wave-uniform
+      char* eb = sepi + wave * GM_EPI;
+      // lane-derived offsets recomputed here from an opaque lane index (not hoisted into registers held across the
+      // main loop)
+      int l = lane;
+      asm volatile("" : "+v"(l));
+      const int er = l & 31, eh = l >> 5;
+      const int erow = l >> 3, echk = l & 7;   // read-back: row erow + 8k, 16-B chunk echk of the 128-B row
 #pragma unroll
-      for (int i = 0; i < NB; ++i)
+      for (int j = 0; j < MB; ++j)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int fs = cc.n0() + 96 * wn + 32 * i + 8 * g;   // acc reg 4g + q <-> feature fs + 4h + q
-          float b4[4] = {0.f, 0.f, 0.f, 0.f};
-          if (a.bias) {
-            const bf16x4 bb = *(const bf16x4*)(sbias + fs + 4 * h);
+        for (int ip = 0; ip < NB / 2; ++ip) {
+          // blocks 2ip, 2ip + 1 = the wave's features 64 ip .. + 63 of tokens 32 j .. + 31, as bf16 rows of 128 B
 #pragma unroll
-            for (int q = 0; q < 4; ++q) b4[q] = to_f32(bb[q]);
-          }
+          for (int b = 0; b < 2; ++b)
 #pragma unroll
-          for (int j = 0; j < MB; ++j) {
-            bf16x4 o;
+            for (int p = 0; p < 2; ++p) {
+              const int i = 2 * ip + b;
+              const int fs = cc.n0() + WF * wn + 32 * i + 16 * p + 4 * eh;   // regs 8p + q / 8p + 4 + q: fs + q / fs + 8 + q
+              float b0[4] = {0.f, 0.f, 0.f, 0.f}, b1[4] = {0.f, 0.f, 0.f, 0.f};
+              if (a.bias) {
+                const bf16x4 bb0 = *(const bf16x4*)(sbias + fs), bb1 = *(const bf16x4*)(sbias + fs + 8);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) o[q] = to_bf16(acc[i][j][4 * g + q] + b4[q]);
-            if (!a.probe) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), ry, vbase,
-                                                  (128 * wm + 32 * j) * ldy2 + fs * 2, 0);
+                for (int q = 0; q < 4; ++q) { b0[q] = to_f32(bb0[q]); b1[q] = to_f32(bb1[q]); }
+              }
+              bf16x4 lo, hi;
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                lo[q] = to_bf16(acc[i][j][8 * p + q] + b0[q]);
+                hi[q] = to_bf16(acc[i][j][8 * p + 4 + q] + b1[q]);
+              }
+              // lane h gets features 16p + 8h .. + 7 of block i: 16-B chunk 4b + 2p + h of the row
+              const u32x2 ul = __builtin_bit_cast(u32x2, lo), uh = __builtin_bit_cast(u32x2, hi);
+              const auto s0 = __builtin_amdgcn_permlane32_swap(ul[0], uh[0], false, false);
+              const auto s1 = __builtin_amdgcn_permlane32_swap(ul[1], uh[1], false, false);
+              *(u32x4*)(eb + er * 128 + 16 * ((4 * b + 2 * p + eh) ^ (er & 7))) = u32x4{s0[0], s1[0], s0[1], s1[1]};
+            }
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int row = 8 * k + erow;
+            const u32x4 v = *(const u32x4*)(eb + row * 128 + 16 * (echk ^ (row & 7)));
+            __builtin_amdgcn_raw_buffer_store_b128(v, ry, erow * ldy2 + 16 * echk,
+                                                   (WT * wm + 32 * j + 8 * k) * ldy2 + (cc.n0() + WF * wn + 64 * ip) * 2, 0);
           }
         }
       since_epi = 0;
@@ -250,10 +306,8 @@ extern "C" int lci_gemm_bt(const void* x, long long ldx, const void* w, const vo
   a.G8 = (int)(grid / 8);
   a.dmt = a.G8 / a.ntn;
   a.dnt = a.G8 % a.ntn;
-  static const int probe = getenv("LCI_GEMM_PROBE") ? atoi(getenv("LCI_GEMM_PROBE")) : 0;
-  a.probe = probe;
   constexpr int TN = 384;
-  const size_t sh = (size_t)GM_NSLOT * (GM_TM + TN) * 64 + GM_MAXN * 2;
+  const size_t sh = (size_t)GM_NSLOT * (GM_TM + TN) * 64 + GM_WAVES * GM_EPI + GM_MAXN * 2;
   (void)hipFuncSetAttribute((const void*)gemm_bt_kernel<TN>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
   hipLaunchKernelGGL(gemm_bt_kernel<TN>, dim3((unsigned)grid), dim3(GM_WAVES * 64), sh, (hipStream_t)stream, a);
   LCI_LAUNCH_CHECK();

@@ -321,254 +321,6 @@ static int launch_lw(LinWgradArgs a, hipStream_t st) {
 }
 
 
-// ---------------------------------------------------------------------------------------- forward / data gradient
-// Y (M x N) = X (M x K) . W^T (W: N x K, both K-contiguous) with a fused epilogue, for the token-wise Linear layers:
-//   LF_PLAIN: y = bf16(acc + b)                              (nn.Linear under autocast; b rounded to bf16 first)
-//   LF_GELU:  aux = pre = bf16(acc + b), y = bf16(gelu(pre))  (MONAI MLPBlock linear1 -> nn.GELU(), exact erf)
-//   LF_DGELU: y = bf16(bf16(acc) * gelu'(aux))               (the data gradient of linear2 feeding GELU's
-//             backward: aux = the saved pre-activation; torch rounds the GEMM output to bf16 first)
-// The data gradient dX = dY . W is the same GEMM with the transposed weight (the caller transposes W, N x K small).
-// W is the MFMA A operand (output features on the accumulator registers, tokens on the lanes), so a lane's
-// accumulators hold 4 consecutive features per register quad and leave as 8-B stores. K slabs of 32 arrive by
-// LDS-DMA into a ring of LDS buffers, 64-B rows whose 16-B chunks are XOR-swizzled by (row >> 2) & 3 through the
-// per-lane source address, so the ds_read_b128 fragment rows are bank-conflict-free.
-enum { LF_PLAIN = 0, LF_GELU = 1, LF_DGELU = 2 };
-#ifndef LCI_LF_PROBE
-#define LCI_LF_PROBE 0   // timing probe (wrong results): 1 = the GELU epilogue writes pre-activation twice (no erf)
-#endif
-
-struct LinFwdArgs {
-  const bf16* x;      // (M, ldx), columns [0, K)
-  const bf16* w;      // (N, K) contiguous
-  const bf16* bias;   // (N) or null
-  bf16* y;            // (M, ldy)
-  bf16* aux;          // (M, ldaux): LF_GELU writes pre, LF_DGELU reads it
-  long long M, ldx, ldy, ldaux;
-  int N, K, ntn, nb;
-};
-
-// erff for the GEMM epilogues: the two polynomials of the device library's erff (ocml __ocml_erf_f32: |x| < 1 ->
-// x + x P(x^2), else 1 - exp(-(x + x Q(x)))) with the same coefficients and operation order, both evaluated and
-// selected (no divergent branches; the library's version branches per element), and the exp as one v_exp_f32 of
-// the log2e-scaled argument instead of the library's extended-precision range reduction. The |x| < 1 result is
-// bitwise the library's; the other side differs by <= 3e-7 absolute (exhaustive bf16 check in
-// tests/test_linear_gpu.py). The GELU epilogue ran 0.135 ms of its 0.505 ms in the library erff at M = 131072.
-#ifndef LCI_LF_FASTERF
-#define LCI_LF_FASTERF 1
-#endif
-__device__ __forceinline__ float erf_epi(float x) {
-  if (!LCI_LF_FASTERF) return erff(x);
-  const float ax = fabsf(x), s = x * x;
-  float p = fmaf(s, -0x1.268bc2p-11f, 0x1.420828p-8f);
-  p = fmaf(s, p, -0x1.b59370p-6f);
-  p = fmaf(s, p, 0x1.ce077cp-4f);
-  p = fmaf(s, p, -0x1.81266p-2f);
-  p = fmaf(s, p, 0x1.06eba0p-3f);
-  const float lo = fmaf(ax, p, ax);
-  float q = fmaf(ax, 0x1.1d3156p-16f, -0x1.8d129p-12f);
-  q = fmaf(ax, q, 0x1.f9a6d2p-9f);
-  q = fmaf(ax, q, -0x1.8c3164p-6f);
-  q = fmaf(ax, q, 0x1.b4e9c8p-4f);
-  q = fmaf(ax, q, 0x1.4515fap-1f);
-  q = fmaf(ax, q, 0x1.078e5p-3f);
-  const float hi = 1.f - __builtin_amdgcn_exp2f(-fmaf(ax, q, ax) * 1.44269504088896341f);
-  return copysignf(ax < 1.f ? lo : hi, x);
-}
-__device__ __forceinline__ float gelu_erf(float v) { return 0.5f * v * (1.f + erf_epi(v * 0.70710678118654752f)); }
-__device__ __forceinline__ float gelu_erf_grad(float v) {   // torch GeluBackward (approximate = 'none')
-  const float cdf = 0.5f * (1.f + erf_epi(v * 0.70710678118654752f));
-  const float pdf = (LCI_LF_FASTERF ? __builtin_amdgcn_exp2f(-0.5f * v * v * 1.44269504088896341f)
-                                    : expf(-0.5f * v * v)) * 0.39894228040143268f;
-  return cdf + v * pdf;
-}
-
-template <int MB, int NB, int WM, int WN, int NBUF, int EPI>
-__global__ __launch_bounds__(64 * WM * WN, 1) void linear_fwd_kernel(LinFwdArgs a) {
-  constexpr int NW = WM * WN;
-  constexpr int TM = 32 * MB * WM, TN = 32 * NB * WN;          // tokens x features per workgroup
-  constexpr int SLOT = (TM + TN) * 32;                          // elements per ring slot (K slab of 32)
-  constexpr int U = (TM + TN) / 16;                             // DMA units per slab
-  constexpr int UPW = (U + NW - 1) / NW, ULO = U / NW;
-  extern __shared__ __attribute__((aligned(16))) bf16 lsm[];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave / WN, wn = wave % WN;
-  long long w = blockIdx.x;
-  {
-    const long long per = ((long long)a.nb + 7) / 8;   // XCD-contiguous: the N tiles of an M tile share X rows
-    w = (long long)(blockIdx.x % 8) * per + blockIdx.x / 8;
-  }
-  if (w >= a.nb) return;   // grid padding, uniform per workgroup, before any barrier
-  const int nt = (int)(w % a.ntn);
-  const long long m0 = (w / a.ntn) * TM;
-  const int n0 = nt * TN;
-  const int nslab = (a.K + 31) / 32;
-  const int nunits = wave < U % NW ? UPW : ULO;
-
-  f32x16 acc[NB][MB];
-#pragma unroll
-  for (int i = 0; i < NB; ++i)
-#pragma unroll
-    for (int j = 0; j < MB; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-
-  // DMA unit u < TM / 16: X rows m0 + 16u .. +15; else W rows n0 + 16 (u - TM / 16) ..; lane (lr, lc) writes
-  // physical chunk lc of row lr, i.e. source chunk lc ^ ((lr >> 2) & 3) of the slab
-  const int lr = lane >> 2, lc = lane & 3, sc = lc ^ ((lr >> 2) & 3);
-  const unsigned lds_base = (unsigned)(uintptr_t)(LCI_LDS bf16*)lsm;
-  const bf16* uptr[UPW];
-  bool uok[UPW];
-  int ulds[UPW];
-#pragma unroll
-  for (int t = 0; t < UPW; ++t) {
-    const int u = min(wave + NW * t, U - 1);
-    ulds[t] = 2 * 512 * u;   // unit u = rows 16u .. 16u + 15 of the slot
-    if (u < TM / 16) {
-      const long long row = m0 + 16 * u + lr;
-      uok[t] = row < a.M;
-      uptr[t] = a.x + (uok[t] ? row : 0) * a.ldx + 8 * sc;
-    } else {
-      const int row = n0 + 16 * (u - TM / 16) + lr;
-      uok[t] = row < a.N;
-      uptr[t] = a.w + (long long)(uok[t] ? row : 0) * a.K + 8 * sc;
-    }
-  }
-  auto issue = [&](int slab) {
-    const unsigned lds0 = lds_base + (unsigned)(2 * (slab % NBUF) * SLOT);
-    const int k0 = 32 * slab;
-    const bool kfull = k0 + 32 <= a.K;
-#pragma unroll
-    for (int t = 0; t < UPW; ++t) {
-      if (t < nunits) {
-        const bool ok = uok[t] && (kfull || k0 + 8 * sc < a.K);
-        glds16(ok ? (const void*)(uptr[t] + k0) : (const void*)(kLwZero + 8 * lc), lds0 + ulds[t]);
-      }
-    }
-  };
-  auto wait_for = [&](int later) {
-    if (later >= NBUF - 2) {
-      if (nunits == UPW) wait_vmcnt<UPW * (NBUF - 2)>(); else wait_vmcnt<ULO * (NBUF - 2)>();
-    } else if (NBUF > 3 && later == 1) {
-      if (nunits == UPW) wait_vmcnt<UPW>(); else wait_vmcnt<ULO>();
-    } else {
-      wait_vmcnt<0>();
-    }
-  };
-  // fragment row r (within the slot), logical 16-B chunk c -> element offset
-  auto frag = [&](const bf16* slot, int r, int c) {
-    return *(const bf16x8*)(slot + r * 32 + 8 * (c ^ ((r >> 2) & 3)));
-  };
-
-#pragma unroll
-  for (int p = 0; p < NBUF - 1; ++p)
-    if (p < nslab) issue(p);
-  const int h = lane >> 5, r = lane & 31;
-  for (int sl = 0; sl < nslab; ++sl) {
-    wait_for(min(NBUF - 2, nslab - 1 - sl));
-    __builtin_amdgcn_s_waitcnt(15 | (3 << 14) | (7 << 4));   // lgkmcnt(0)
-    __builtin_amdgcn_s_barrier();
-    if (sl + NBUF - 1 < nslab) issue(sl + NBUF - 1);
-    const bf16* slot = lsm + (sl % NBUF) * SLOT;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 fw[NB], fx[MB];
-#pragma unroll
-      for (int i = 0; i < NB; ++i) fw[i] = frag(slot, TM + 32 * (NB * wn + i) + r, 2 * s + h);
-#pragma unroll
-      for (int j = 0; j < MB; ++j) fx[j] = frag(slot, 32 * (MB * wm + j) + r, 2 * s + h);
-#pragma unroll
-      for (int i = 0; i < NB; ++i)
-#pragma unroll
-        for (int j = 0; j < MB; ++j) acc[i][j] = mfma32(fw[i], fx[j], acc[i][j]);
-    }
-  }
-  // Epilogue through LDS: the accumulators (+ bias, rounded to bf16: the pre-activation for LF_GELU, the bf16 GEMM
-  // output for LF_DGELU) go to a [TM][TN + 8] tile in the freed ring, then the workgroup streams whole rows: every
-  // global access (y, and aux for the GELU forms) is a 16-B piece of a contiguous 2 TN-byte row segment.
-  // acc[i][j] reg e: feature 32 (NB wn + i) + (e&3) + 8(e>>2) + 4h, token 32 (MB wm + j) + (lane & 31) of the tile
-  constexpr int TLD = TN + 8;
-  static_assert(TM * TLD <= NBUF * SLOT, "epilogue tile must fit the ring");
-  __syncthreads();   // every wave is done reading the ring
-  bf16* tile = lsm;
-#pragma unroll
-  for (int j = 0; j < MB; ++j)
-#pragma unroll
-    for (int i = 0; i < NB; ++i)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int nl = 32 * (NB * wn + i) + 8 * g + 4 * h;
-        float v[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = acc[i][j][4 * g + q];
-        if (EPI != LF_DGELU && a.bias && n0 + nl < a.N) {
-          const bf16x4 bb = *(const bf16x4*)(a.bias + n0 + nl);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] += to_f32(bb[q]);
-        }
-        bf16x4 o;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) o[q] = to_bf16(v[q]);
-        *(bf16x4*)(tile + (32 * (MB * wm + j) + r) * TLD + nl) = o;
-      }
-  __syncthreads();
-  constexpr int CPR = TN / 8;                       // 16-B chunks per tile row
-  for (int c = threadIdx.x; c < TM * CPR; c += 64 * NW) {
-    const int row = c / CPR, col = 8 * (c - row * CPR);
-    const long long m = m0 + row;
-    const int n = n0 + col;
-    if (m >= a.M || n >= a.N) continue;
-    const bf16x8 t = *(const bf16x8*)(tile + row * TLD + col);
-    bf16x8 o;
-    if constexpr (EPI == LF_PLAIN) {
-      o = t;
-    } else if constexpr (EPI == LF_GELU) {
-      *(bf16x8*)(a.aux + m * a.ldaux + n) = t;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) o[q] = LCI_LF_PROBE == 1 ? t[q] : to_bf16(gelu_erf(to_f32(t[q])));
-    } else {
-      const bf16x8 p = *(const bf16x8*)(a.aux + m * a.ldaux + n);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) o[q] = to_bf16(to_f32(t[q]) * gelu_erf_grad(to_f32(p[q])));
-    }
-    *(bf16x8*)(a.y + m * a.ldy + n) = o;
-  }
-}
-
-#ifndef LCI_LF_NBUF
-#define LCI_LF_NBUF 3
-#endif
-
-template <int MB, int NB, int WM, int WN, int EPI>
-static int launch_lf(LinFwdArgs a, hipStream_t st) {
-  constexpr int TM = 32 * MB * WM, TN = 32 * NB * WN, NBUF = LCI_LF_NBUF;
-  const size_t sh = (size_t)NBUF * (TM + TN) * 32 * sizeof(bf16);
-  a.ntn = (a.N + TN - 1) / TN;
-  const long long nb = (a.M + TM - 1) / TM * a.ntn;
-  LCI_CHECK(nb < (1LL << 30), "linear_fwd: too many workgroups");
-  a.nb = (int)nb;
-  (void)hipFuncSetAttribute((const void*)linear_fwd_kernel<MB, NB, WM, WN, NBUF, EPI>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipLaunchKernelGGL((linear_fwd_kernel<MB, NB, WM, WN, NBUF, EPI>), dim3((unsigned)((nb + 7) / 8 * 8)),
-                     dim3(64 * WM * WN), sh, st, a);
-  LCI_LAUNCH_CHECK();
-  return 0;
-}
-
-// Feature tile: 128 (N % 128 == 0: the ViT / Mamba / Hyena widths) or 96 (the Swin widths); 0 = unsupported.
-static int lf_tile(int N) { return N % 128 == 0 ? 128 : (N % 96 == 0 ? 96 : 0); }
-
-template <int EPI>
-static int lf_dispatch(const LinFwdArgs& a, hipStream_t st) {
-  static const int wide = getenv("LCI_LF_WIDE") ? atoi(getenv("LCI_LF_WIDE")) : 0;
-  if (lf_tile(a.N) == 128) {
-    if (wide) return launch_lf<4, 4, 2, 1, EPI>(a, st);   // 2 waves of 128 x 128 (one per SIMD, 2 WGs per CU)
-    return launch_lf<4, 2, 2, 2, EPI>(a, st);             // 4 waves of 128 tokens x 64 features
-  }
-  return launch_lf<4, 3, 2, 1, EPI>(a, st);               // 2 waves of 128 tokens x 96 features
-}
-
-
 // ------------------------------------------------------------------------- narrow outputs (the heads' 1x1 convs)
 // y (M, N) = x (M, K) . w^T + b for N <= 8: UnetOutBlock's 1x1 conv to the class / output channels (MONAI-1.3
 // get_conv_layer(kernel_size=1, bias=True), enhance_heads.py:30-356) over every voxel, as channels-last rows.
@@ -654,6 +406,37 @@ __global__ __launch_bounds__(256) void linear_small_bwd_kernel(const bf16* __res
       for (int o = 0; o < N; ++o) part[(long long)(N * K + o) * LS_THREADS + t] = gb[o];
     }
   }
+}
+
+
+// erff for the GELU kernels: the two polynomials of the device library's erff (ocml __ocml_erf_f32: |x| < 1 ->
+// x + x P(x^2), else 1 - exp(-(x + x Q(x)))) with the same coefficients and operation order, both evaluated and
+// selected (no divergent branches; the library's version branches per element), and the exp as one v_exp_f32 of
+// the log2e-scaled argument instead of the library's extended-precision range reduction. The |x| < 1 result is
+// bitwise the library's; the other side differs by <= 3e-7 absolute (exhaustive bf16 check in
+// tests/test_linear_gpu.py; after the bf16 rounding the GELU results are bitwise torch's).
+__device__ __forceinline__ float erf_epi(float x) {
+  const float ax = fabsf(x), s = x * x;
+  float p = fmaf(s, -0x1.268bc2p-11f, 0x1.420828p-8f);
+  p = fmaf(s, p, -0x1.b59370p-6f);
+  p = fmaf(s, p, 0x1.ce077cp-4f);
+  p = fmaf(s, p, -0x1.81266p-2f);
+  p = fmaf(s, p, 0x1.06eba0p-3f);
+  const float lo = fmaf(ax, p, ax);
+  float q = fmaf(ax, 0x1.1d3156p-16f, -0x1.8d129p-12f);
+  q = fmaf(ax, q, 0x1.f9a6d2p-9f);
+  q = fmaf(ax, q, -0x1.8c3164p-6f);
+  q = fmaf(ax, q, 0x1.b4e9c8p-4f);
+  q = fmaf(ax, q, 0x1.4515fap-1f);
+  q = fmaf(ax, q, 0x1.078e5p-3f);
+  const float hi = 1.f - __builtin_amdgcn_exp2f(-fmaf(ax, q, ax) * 1.44269504088896341f);
+  return copysignf(ax < 1.f ? lo : hi, x);
+}
+__device__ __forceinline__ float gelu_erf(float v) { return 0.5f * v * (1.f + erf_epi(v * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_erf_grad(float v) {   // torch GeluBackward (approximate = 'none')
+  const float cdf = 0.5f * (1.f + erf_epi(v * 0.70710678118654752f));
+  const float pdf = __builtin_amdgcn_exp2f(-0.5f * v * v * 1.44269504088896341f) * 0.39894228040143268f;
+  return cdf + v * pdf;
 }
 
 
@@ -744,25 +527,6 @@ extern "C" int lci_linear_wgrad(const void* dy, long long ldy, const void* x, lo
 #undef LCI_LW
   LCI_CHECK(false, "linear_wgrad: tile not instantiated");
   return 1;
-}
-
-extern "C" int lci_linear_fwd_supported(int N, int K) { return lf_tile(N) > 0 && K % 8 == 0 && K > 0 ? 1 : 0; }
-
-extern "C" int lci_linear_fwd(int epilogue, const void* x, long long ldx, const void* w, const void* bias, void* y,
-                              long long ldy, void* aux, long long ldaux, long long M, int N, int K, void* stream) {
-  LCI_CHECK(M > 0 && lci_linear_fwd_supported(N, K), "linear_fwd: unsupported shape N = %d, K = %d", N, K);
-  LCI_CHECK(epilogue >= LF_PLAIN && epilogue <= LF_DGELU, "linear_fwd: bad epilogue %d", epilogue);
-  LCI_CHECK(ldx % 8 == 0 && ldy % 8 == 0 && ldx >= K && ldy >= N && (epilogue == LF_PLAIN || (aux && ldaux % 8 == 0)),
-            "linear_fwd: bad row strides");
-  LCI_CHECK(((uintptr_t)x & 15) == 0 && ((uintptr_t)w & 15) == 0 && ((uintptr_t)y & 15) == 0 &&
-            ((uintptr_t)aux & 15) == 0 && ((uintptr_t)bias & 7) == 0, "linear_fwd: misaligned pointers");
-  LinFwdArgs a{};
-  a.x = (const bf16*)x; a.w = (const bf16*)w; a.bias = (const bf16*)bias; a.y = (bf16*)y; a.aux = (bf16*)aux;
-  a.M = M; a.ldx = ldx; a.ldy = ldy; a.ldaux = ldaux; a.N = N; a.K = K;
-  hipStream_t st = (hipStream_t)stream;
-  if (epilogue == LF_GELU) return lf_dispatch<LF_GELU>(a, st);
-  if (epilogue == LF_DGELU) return lf_dispatch<LF_DGELU>(a, st);
-  return lf_dispatch<LF_PLAIN>(a, st);
 }
 
 extern "C" int lci_linear_small_threads(void) { return LS_THREADS; }

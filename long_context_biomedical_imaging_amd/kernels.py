@@ -1773,9 +1773,8 @@ def _wgrad_tiny_k(dy2: torch.Tensor, x2: torch.Tensor, bias: bool):
 
 
 # csrc/gemm.hip for the bf16 projection GEMMs whose output width it takes (N % 384 == 0: every ViT-small / Mamba /
-# Hyena projection and data gradient): opt-in (LCI_HIP_GEMM=1) while it is slower than the TunableOp-tuned hipBLASLt
-# GEMM on the metric shapes (profiles/r05_gemm_ab.txt)
-HIP_GEMM = os.environ.get("LCI_HIP_GEMM", "0") == "1"
+# Hyena projection and data gradient); LCI_HIP_GEMM=0 routes them to hipBLASLt (A/B: profiles/r05_gemm_ab.txt)
+HIP_GEMM = os.environ.get("LCI_HIP_GEMM", "1") == "1"
 
 
 def gemm_bt_supported(x2: torch.Tensor, N: int, K: int) -> bool:
@@ -1857,79 +1856,6 @@ class _Linear(torch.autograd.Function):
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None) -> torch.Tensor:
     return _Linear.apply(x, weight, bias)
-
-
-LF_PLAIN, LF_GELU, LF_DGELU = 0, 1, 2
-
-
-def linear_fwd_supported(x2: torch.Tensor, N: int, K: int) -> bool:
-    """Whether lci_linear_fwd takes x2 (M, K): bf16 CUDA rows with unit column stride, 16-byte aligned."""
-    return (x2.is_cuda and x2.dtype == torch.bfloat16 and x2.stride(1) == 1 and x2.stride(0) % 8 == 0
-            and x2.data_ptr() % 16 == 0 and x2.shape[0] > 0 and bool(_lib.load().lci_linear_fwd_supported(N, K)))
-
-
-def linear_fwd(x2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, epilogue: int = LF_PLAIN,
-               aux: torch.Tensor | None = None):
-    """y (M, N) bf16 = epilogue(x2 (M, K) . w^T) on the HIP GEMM (w (N, K) bf16 contiguous, bias (N) bf16).
-    LF_GELU returns (y, pre) with pre = the pre-activation; LF_DGELU reads aux = the saved pre-activation."""
-    M, K = x2.shape
-    N = w.shape[0]
-    _lib.require_gpu(w, bias)
-    y = torch.empty(M, N, device=x2.device, dtype=torch.bfloat16)
-    if epilogue == LF_GELU:
-        aux = torch.empty(M, N, device=x2.device, dtype=torch.bfloat16)
-    elif epilogue == LF_DGELU:
-        _lib.require_gpu(aux)
-    names = {LF_PLAIN: "linear_fwd", LF_GELU: "linear_fwd_gelu", LF_DGELU: "linear_dgrad_dgelu"}
-    KernelTimer.run(names[epilogue], 2.0 * M * N * K, x2, lambda: _lib.call(
-        "lci_linear_fwd", epilogue, x2.data_ptr(), x2.stride(0), w.data_ptr(), _lib.ptr(bias), y.data_ptr(), N,
-        _lib.ptr(aux), N if aux is not None else 0, M, N, K, _lib.stream_of(x2)))
-    return (y, aux) if epilogue == LF_GELU else y
-
-
-class _MLP(torch.autograd.Function):
-    """MONAI MLPBlock (linear1 -> GELU(erf) -> linear2, dropout 0) under bf16 autocast: linear1 on the HIP GEMM whose
-    epilogue adds the bias and applies GELU (writing the pre-activation for the backward), linear2 on hipBLASLt;
-    backward: linear2's data gradient on the HIP GEMM with GELU' in its epilogue, linear1's data gradient a plain
-    hipBLASLt GEMM, both weight / bias gradients on lci_linear_wgrad. Same roundings as the reference's autocast
-    path."""
-
-    @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2):
-        dt = torch.bfloat16
-        D, H = x.shape[-1], w1.shape[0]
-        x2 = x.to(dt).reshape(-1, D)
-        w1c, w2c = w1.to(dt).contiguous(), w2.to(dt).contiguous()
-        act, pre = linear_fwd(x2, w1c, b1.to(dt), LF_GELU)
-        # the plain GEMMs (no epilogue to fuse) stay on hipBLASLt: 0.18 vs 0.26 ms (linear2) and 0.19 vs 0.24 ms
-        # (linear1's data gradient) at M = 131072 (tools/kernel_bench.py mlp)
-        y = torch.nn.functional.linear(act, w2c, b2.to(dt))
-        ctx.save_for_backward(x2, w1c, w2c, pre, act)
-        ctx.shape = x.shape
-        return y.view(*x.shape[:-1], D)
-
-    @staticmethod
-    def backward(ctx, dy):
-        x2, w1c, w2c, pre, act = ctx.saved_tensors
-        D = x2.shape[1]
-        dy2 = dy.to(torch.bfloat16).reshape(-1, D)
-        if dy2.stride(1) != 1 or dy2.stride(0) % 8 or dy2.data_ptr() % 16:
-            dy2 = dy2.contiguous()
-        d_pre = linear_fwd(dy2, w2c.t().contiguous(), None, LF_DGELU, aux=pre)
-        dw2, db2 = linear_wgrad(dy2, act, True)
-        dx = d_pre @ w1c
-        dw1, db1 = linear_wgrad(d_pre, x2, True)
-        return dx.view(ctx.shape), dw1, db1, dw2, db2
-
-
-def mlp_supported(x: torch.Tensor, D: int, H: int) -> bool:
-    return (x.is_cuda and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
-            and D % 32 == 0 and H % 32 == 0 and bool(_lib.load().lci_linear_fwd_supported(H, D))
-            and bool(_lib.load().lci_linear_fwd_supported(D, H)))
-
-
-def mlp(x, w1, b1, w2, b2):
-    return _MLP.apply(x, w1, b1, w2, b2)
 
 
 def pointwise_small_supported(x2: torch.Tensor, N: int) -> bool:

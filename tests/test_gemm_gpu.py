@@ -25,7 +25,8 @@ def _check(y, x, w, b):
 
 @pytest.mark.parametrize("M,N,K,bias,pad", [(1, 384, 384, True, 0), (255, 384, 384, False, 0), (256, 1152, 384, True, 0),
                                             (1000, 1536, 384, True, 64), (4173, 384, 1536, False, 0),
-                                            (777, 768, 96, True, 8), (131072, 1152, 384, True, 0)])
+                                            (777, 768, 96, True, 8), (3001, 384, 320, True, 0),
+                                            (2500, 384, 1152, True, 0), (131072, 1152, 384, True, 0)])
 def test_gemm_bt_vs_fp64(M, N, K, bias, pad):
     from long_context_biomedical_imaging_amd import kernels
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
@@ -74,3 +75,10 @@ def test_gemm_bt_deterministic():
     x = torch.randn(5000, 384, device="cuda", generator=g).to(torch.bfloat16)
     w = torch.randn(1536, 384, device="cuda", generator=g).to(torch.bfloat16)
     assert torch.equal(kernels.gemm_bt(x, w), kernels.gemm_bt(x, w))
+
+
+def test_gemm_bt_supported_shapes():
+    from long_context_biomedical_imaging_amd import _lib
+    lib = _lib.load()
+    assert lib.lci_gemm_bt_supported(384, 192) and not lib.lci_gemm_bt_supported(4224, 1536)
+    assert not lib.lci_gemm_bt_supported(384, 48) and not lib.lci_gemm_bt_supported(400, 384)

@@ -6,9 +6,10 @@
   reads x_proj's output columns [0, 24) of a 40-wide row). Bound: |err| <= 1e-5 * (|dY|^T |X|) + 1e-6 elementwise
   (f32 accumulation of exact bf16 products).
 - At the C5 token count (M = 2^21, 384 x 384) the same bound.
-- TokenLinear under bf16 autocast vs nn.Linear under autocast (the reference path, backbone_vit.py:166-167):
-  identical output and input gradient (the same hipBLASLt GEMMs), weight / bias gradients within the bf16 rounding
-  the autocast GEMM applies to its dW (ours stay f32).
+- TokenLinear under bf16 autocast vs nn.Linear under autocast (the reference path, backbone_vit.py:166-167), with
+  the forward / data-gradient GEMMs on hipBLASLt (LCI_HIP_GEMM=0; lci_gemm_bt's own parity is tests/test_gemm_gpu.py):
+  identical output and input gradient, weight / bias gradients within the bf16 rounding the autocast GEMM applies to
+  its dW (ours stay f32).
 """
 import pytest
 import torch
@@ -58,8 +59,10 @@ def test_linear_wgrad_c5_tokens():
 
 
 @pytest.mark.parametrize("N,K,bias", [(1152, 384, False), (384, 384, True), (1536, 384, True), (40, 192, False)])
-def test_token_linear_matches_autocast_linear(N, K, bias):
+def test_token_linear_matches_autocast_linear(N, K, bias, monkeypatch):
+    from long_context_biomedical_imaging_amd import kernels
     from long_context_biomedical_imaging_amd.blocks import TokenLinear
+    monkeypatch.setattr(kernels, "HIP_GEMM", False)   # hipBLASLt forward / dX: bitwise torch's (lci_gemm_bt: test_gemm_gpu)
     torch.manual_seed(0)
     ref = torch.nn.Linear(K, N, bias=bias).cuda()
     mine = TokenLinear(K, N, bias=bias).cuda()
@@ -89,64 +92,6 @@ def _ulp_close(a, b, ulps=1):
     a, b = a.double(), b.double()
     tol = ulps * 2.0 ** -7 * torch.maximum(a.abs(), b.abs()) + 1e-30
     return ((a - b).abs() <= tol)
-
-
-@pytest.mark.parametrize("M,N,K", [(1000, 1536, 384), (4099, 384, 1536), (333, 1152, 384), (2500, 288, 96),
-                                   (1234, 96, 384), (65, 384, 384)])
-def test_linear_fwd_epilogues_vs_reference(M, N, K):
-    from long_context_biomedical_imaging_amd import kernels
-    g = torch.Generator(device="cuda").manual_seed(M * 7 + N)
-    x = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
-    w = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).to(torch.bfloat16)
-    b = torch.randn(N, device="cuda", generator=g).to(torch.bfloat16)
-    acc = x.double() @ w.double().t()
-    bound = x.double().abs() @ w.double().abs().t()
-    # plain: bf16(acc + b) -- within half an ulp of the exact value plus f32 reassociation
-    y = kernels.linear_fwd(x, w, b, kernels.LF_PLAIN)
-    exact = acc + b.double()
-    assert ((y.double() - exact).abs() <= 2.0 ** -8 * exact.abs() + 1e-5 * bound + 1e-6).all()
-    # GELU: pre as plain; act = bf16(gelu(pre)) exactly as torch's GELU of the same bf16 pre-activation
-    act, pre = kernels.linear_fwd(x, w, b, kernels.LF_GELU)
-    assert torch.equal(pre, y)
-    ref_act = torch.nn.functional.gelu(pre.float()).to(torch.bfloat16)
-    assert _ulp_close(act, ref_act).all()
-    # dGELU (linear2's data gradient through GELU): x = dY (M, K), w = W2^T (N, K), aux = pre (M, N);
-    # reference = torch's gelu_backward of bf16(dY . W2) and the same bf16 pre-activation
-    dy = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
-    w2t = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).to(torch.bfloat16)
-    d_pre = kernels.linear_fwd(dy, w2t, None, kernels.LF_DGELU, aux=pre)
-    d_act = (dy.double() @ w2t.double().t()).to(torch.bfloat16)
-    ref = torch.ops.aten.gelu_backward(d_act, pre)
-    close = _ulp_close(d_pre, ref, ulps=2) | ((d_pre.double() - ref.double()).abs() <= 1e-5 * (
-        dy.double().abs() @ w2t.double().abs().t()))
-    assert close.all(), f"{(~close).sum().item()} mismatches"
-
-
-@pytest.mark.parametrize("D,H,M", [(384, 1536, 3000), (96, 384, 4099), (192, 768, 65)])
-def test_mlp_block_fused_matches_module_path(D, H, M):
-    """blocks.MLPBlock under bf16 autocast: the fused HIP path vs the same module run op by op (torch GEMMs +
-    nn.GELU), same weights: outputs and all five gradients."""
-    from long_context_biomedical_imaging_amd import blocks, kernels
-    torch.manual_seed(D + H)
-    mod = blocks.MLPBlock(D, H).cuda()
-    x = torch.randn(2, M, D, device="cuda")
-    gy = torch.randn(2, M, D, device="cuda").to(torch.bfloat16)
-    res = []
-    for fused in (True, False):
-        mod.zero_grad()
-        xi = x.clone().requires_grad_(True)
-        with torch.autocast("cuda", dtype=torch.bfloat16):
-            if fused:
-                assert kernels.mlp_supported(xi, D, H)
-                y = kernels.mlp(xi, mod.linear1.weight, mod.linear1.bias, mod.linear2.weight, mod.linear2.bias)
-            else:
-                y = mod.linear2(mod.fn(torch.nn.functional.linear(xi, mod.linear1.weight, mod.linear1.bias)))
-        y.backward(gy)
-        res.append([y.detach().float(), xi.grad] + [p.grad.clone() for p in mod.parameters()])
-    names = ["y", "dx", "dW1", "db1", "dW2", "db2"]
-    for n, a, b in zip(names, res[0], res[1]):
-        e = ((a.double() - b.double()).norm() / b.double().norm()).item()
-        assert e < 1e-2, f"{n}: rel-L2 {e:.3e}"
 
 
 @pytest.mark.parametrize("M,N,K", [(2 * 64 ** 3, 2, 48), (524288, 2, 16), (1000, 1, 24), (777, 4, 256), (99, 3, 64)])
@@ -275,31 +220,6 @@ def test_gelu_kernel_exhaustive_bf16():
     d = (xc.grad.float() - xr.grad.float()).abs()
     assert bool((d <= xr.grad.float().abs() * 2.0 ** -7 + 1e-37).all())
     assert (xc.grad != xr.grad).float().mean().item() < 5e-3
-
-
-def test_gelu_epilogue_exhaustive_bf16():
-    """Every finite bf16 value (|x| < 1e4) through the GEMM epilogues (csrc/linear.hip erf_epi): rows of 32 values
-    times 4 stacked 32 x 32 identities (N = 128), so pre = x exactly; LF_GELU's activation and LF_DGELU's GELU' (unit
-    upstream gradient) within one bf16 ulp of torch's gelu / gelu_backward and bitwise equal for > 99.5 %."""
-    from long_context_biomedical_imaging_amd import kernels
-    bits = torch.arange(0, 65536, dtype=torch.int32).to(torch.int16)
-    v = bits.view(torch.bfloat16).cuda()
-    v = v[torch.isfinite(v.float()) & (v.float().abs() < 1e4)]
-    v = v[: v.numel() // 32 * 32].contiguous()
-    x = v.view(-1, 32)
-    w = torch.eye(32, device="cuda").repeat(4, 1).to(torch.bfloat16).contiguous()
-    act, pre = kernels.linear_fwd(x, w, None, kernels.LF_GELU)
-    assert torch.equal(pre, x.repeat(1, 4))
-    ref = torch.nn.functional.gelu(pre)
-    d = (act.float() - ref.float()).abs()
-    assert bool((d <= ref.float().abs() * 2.0 ** -7 + 1e-37).all())
-    assert (act != ref).float().mean().item() < 5e-3
-    ones = torch.ones_like(x)
-    g = kernels.linear_fwd(ones, w, None, kernels.LF_DGELU, aux=pre)
-    gref = torch.ops.aten.gelu_backward(torch.ones_like(pre), pre)
-    d = (g.float() - gref.float()).abs()
-    assert bool((d <= gref.float().abs() * 2.0 ** -7 + 1e-37).all())
-    assert (g != gref).float().mean().item() < 5e-3
 
 
 @pytest.mark.parametrize("nd,Cin,Cout,Cs,k", [(3, 64, 32, 32, (2, 2, 2)), (2, 48, 16, 24, (2, 2)), (3, 16, 8, 0, (2, 2, 2))])

@@ -229,35 +229,14 @@ def bench_linear():
 
 
 def bench_mlp():
-    """MLPBlock GEMMs at the ViT (M = 131072) and C5 (M = 2^21) token counts: HIP fused-epilogue GEMMs vs torch
-    (hipBLASLt addmm + GELU / matmul + gelu_backward) on the same bf16 operands."""
+    """The MLPBlock (linear1 -> GELU -> linear2, backbone_vit.py:249) forward + backward under bf16 autocast at the
+    ViT (M = 131072) and C5 (M = 2^21) token counts: forward / data-gradient GEMMs on lci_gemm_bt (the default) vs
+    hipBLASLt (LCI_HIP_GEMM=0), the GELU and weight gradients on the HIP kernels either way."""
+    from long_context_biomedical_imaging_amd import blocks, trainer
+    trainer.use_tuned_gemms()
     D, H = 384, 1536
     for M in (131072, 1 << 21):
-        x = torch.randn(M, D, device="cuda").to(torch.bfloat16)
-        w1 = (torch.randn(H, D, device="cuda") * 0.05).to(torch.bfloat16)
-        b1 = torch.randn(H, device="cuda").to(torch.bfloat16)
-        w2 = (torch.randn(D, H, device="cuda") * 0.05).to(torch.bfloat16)
-        b2 = torch.randn(D, device="cuda").to(torch.bfloat16)
         f = 2.0 * M * D * H
-        cfg = f"M{M} D{D} H{H}"
-        act, pre = kernels.linear_fwd(x, w1, b1, kernels.LF_GELU)
-        emit("hip fc1+bias+gelu", timeit(lambda: kernels.linear_fwd(x, w1, b1, kernels.LF_GELU)), f, "TFLOP/s", cfg)
-        emit("torch fc1 addmm+gelu", timeit(lambda: torch.nn.functional.gelu(torch.nn.functional.linear(x, w1, b1))),
-             f, "TFLOP/s", cfg)
-        emit("hip fc2+bias", timeit(lambda: kernels.linear_fwd(act, w2, b2)), f, "TFLOP/s", cfg)
-        emit("torch fc2 addmm", timeit(lambda: torch.nn.functional.linear(act, w2, b2)), f, "TFLOP/s", cfg)
-        dy = torch.randn(M, D, device="cuda").to(torch.bfloat16)
-        w2t = w2.t().contiguous()
-        emit("hip fc2 dgrad+gelu'", timeit(lambda: kernels.linear_fwd(dy, w2t, None, kernels.LF_DGELU, aux=pre)), f,
-             "TFLOP/s", cfg)
-        emit("torch fc2 dgrad+gelu_backward", timeit(lambda: torch.ops.aten.gelu_backward(dy @ w2, pre)), f,
-             "TFLOP/s", cfg)
-        dp = torch.randn(M, H, device="cuda").to(torch.bfloat16)
-        w1t = w1.t().contiguous()
-        emit("hip fc1 dgrad", timeit(lambda: kernels.linear_fwd(dp, w1t, None)), f, "TFLOP/s", cfg)
-        emit("torch fc1 dgrad", timeit(lambda: dp @ w1), f, "TFLOP/s", cfg)
-        # the whole MLPBlock (forward + backward under bf16 autocast): fused path vs the TokenLinear + GELU path
-        from long_context_biomedical_imaging_amd import blocks
         mb = blocks.MLPBlock(D, H).cuda()
         xm = torch.randn(M, D, device="cuda", requires_grad=True)
         gy = torch.randn(M, D, device="cuda").to(torch.bfloat16)
@@ -266,11 +245,12 @@ def bench_mlp():
             with torch.autocast("cuda", dtype=torch.bfloat16):
                 y = mb(xm)
             y.backward(gy)
-        for fused in (False, True, False, True):
-            blocks.FUSED_MLP = fused
-            emit(f"MLPBlock fwd+bwd {'fused' if fused else 'unfused'}", timeit(step, 10), 6 * f, "TFLOP/s", cfg)
-        blocks.FUSED_MLP = False
-        del x, act, pre, dy, dp, xm, gy, mb
+        for hip in (True, False, True, False):
+            kernels.HIP_GEMM = hip
+            emit(f"MLPBlock fwd+bwd {'gemm_bt' if hip else 'hipBLASLt'}", timeit(step, 10), 6 * f, "TFLOP/s",
+                 f"M{M} D{D} H{H}")
+        kernels.HIP_GEMM = True
+        del xm, gy, mb
         torch.cuda.empty_cache()
 
 
