@@ -56,8 +56,8 @@ extern "C" {
  * lci_window_attn_bwd pad_ws; 16: lci_attn_bwd delta_ws is (B, H, 2, L): the negated row constants -lse2 | -delta; 17: lci_window_bwd_needs_plain;
  * 18: lci_attn_bwd delta_ws is lci_attn_bwd_ws_bytes(B, H, L) bytes; 19: selective-scan checkpoints in the I/O
  * dtype; 20: lci_attn_gen_fwd / lci_attn_gen_bwd; 21: lci_gemm_bt; 22: lci_linear_fwd removed, superseded by
- * lci_gemm_bt). */
-#define LCI_ABI_VERSION 22
+ * lci_gemm_bt; 23: lci_fftconv_spectrum Dv). */
+#define LCI_ABI_VERSION 23
 const char* lci_last_error(void);
 int lci_abi_version(void);
 /* sha256 prefix of the sources the library was built from (build_lib.source_hash); the Python binding refuses a
@@ -248,14 +248,18 @@ int lci_mamba_proj_bwd(const void* ddt, long long ts_ddt, const void* dbc, const
  * Rows are channel-major f32 (R, C, L); the filter of row r is r % C; k (C, L). */
 long long lci_fft_size(int L);
 int lci_fft_twiddles(void* tw, int n, void* stream);
-/* K (C, n) complex f32 = filter spectra (scaled by 1/n); SK (C, n) complex scratch. */
-int lci_fftconv_spectrum(const float* k, void* K, void* SK, const void* tw, int C, int L, void* stream);
+/* K (C, n) complex f32 = filter spectra (scaled by 1/n); SK (C, n) complex scratch. Dv (C) or null: folded into the
+ * spectra (K += D / n, the spectrum of D delta), so the convolution with K carries the + D u term (ABI 23). */
+int lci_fftconv_spectrum(const float* k, const float* Dv, void* K, void* SK, const void* tw, int C, int L,
+                         void* stream);
 /* y = causal_conv(u, k) + D u; S: (C*ceil(R/2), n) complex scratch. Su (optional, same shape): receives the
- * column spectra of u, left intact for lci_fftconv_bwd (ABI 11). */
+ * column spectra of u, left intact for lci_fftconv_bwd (ABI 11). Dv (C) or null: D u added in the time domain (null
+ * when K already carries D, lci_fftconv_spectrum with Dv). */
 int lci_fftconv_fwd(const float* u, const void* K, const float* Dv, float* y, void* S, void* Su, const void* tw,
                     int R, int C, int L, void* stream);
-/* du = corr(dy, k) + D dy (written); dk (C, L) = sum_rows corr(dy, u) (written, optional); dD accumulated
- * (optional). S, S2: (C*ceil(R/2), n) complex scratch (S2 only with dk and no Su); Su: the forward's kept
+/* du = corr(dy, k) + D dy (written; Dv (C) or null as in lci_fftconv_fwd); dk (C, L) = sum_rows corr(dy, u)
+ * (written, optional); dD accumulated (optional): dk[:, 0] (the lag-0 correlation sum_rows sum_t dy u) when dk is
+ * computed, else a row dot product. S, S2: (C*ceil(R/2), n) complex scratch (S2 only with dk and no Su); Su: the forward's kept
  * column spectra of u (optional: skips their recomputation); SK: (C, n) complex scratch. */
 int lci_fftconv_bwd(const float* dy, const float* u, const void* K, const float* Dv, float* du, float* dk,
                     float* dD, void* S, void* S2, const void* Su, void* SK, const void* tw, int R, int C, int L,

@@ -14,7 +14,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_LIB = os.path.join(HERE, "liblci.so")
 LIB_PATH = os.environ.get("LCI_LIB_PATH", DEFAULT_LIB)   # override: kernel-variant A/B runs (no staleness check)
-ABI_VERSION = 22   # include/lci.h LCI_ABI_VERSION
+ABI_VERSION = 23   # include/lci.h LCI_ABI_VERSION
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -38,7 +38,7 @@ SIGNATURES = {
     "lci_window_attn_bwd": [_P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P],
     "lci_window_index_map": [_P, _P, _P, _P, _P, _P],
     "lci_fft_twiddles": [_P, _I, _P],
-    "lci_fftconv_spectrum": [_P, _P, _P, _P, _I, _I, _P],
+    "lci_fftconv_spectrum": [_P, _P, _P, _P, _P, _I, _I, _P],
     "lci_fftconv_fwd": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
     "lci_fftconv_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
     "lci_hyena_pre_fwd": [_I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],

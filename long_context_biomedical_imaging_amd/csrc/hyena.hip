@@ -355,8 +355,9 @@ __global__ __launch_bounds__(256) void fft_row512_kernel(FftArgs a) {
 #pragma unroll
     for (int r = 0; r < 8; ++r) v[r] = a.SK[(long long)j * a.n + row + 64 * r];
     fft512_wave<false>(v, buf, twl, L);
+    const float dn = a.Dv ? a.Dv[j] * invn : 0.f;   // + D / n: the spectrum of D delta (the D u term)
 #pragma unroll
-    for (int r = 0; r < 8; ++r) a.K[(long long)j * a.n + row + 64 * r] = v[r] * invn;
+    for (int r = 0; r < 8; ++r) a.K[(long long)j * a.n + row + 64 * r] = v[r] * invn + f32x2{dn, 0.f};
     return;
   }
   f32x2 kr[8];
@@ -1005,6 +1006,12 @@ __global__ __launch_bounds__(NT) void fft_colw_inv_kernel(FftArgs a) {
     lds_fft_inplace<true, CW>(x, a.n1, a.ln1, twl, ld);
   }
   emit(c0);
+}
+
+// dD[j] += dk[j][0]: sum_rows sum_t dy u is the lag-0 entry of the filter gradient sum_rows corr(dy, u)
+__global__ __launch_bounds__(256) void dd_from_dk_kernel(const float* dk, float* dD, int C, int L) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j < C) dD[j] += dk[(long long)j * L];
 }
 
 // dD[j] += sum_rows sum_t a[row][t] * b[row][t] over rows of filter j (block partial + one atomic per block).
@@ -1889,11 +1896,13 @@ static int fft_chunk(int C, long long bytes_per_filter) {
   return (int)std::max(1LL, std::min((long long)C, jc));
 }
 
-// Filter spectra: k (C, L) f32 -> K (C, n) complex in [k1][k2] layout, scaled by 1/n. SK: (C, n) scratch.
-extern "C" int lci_fftconv_spectrum(const float* k, void* K, void* SK, const void* tw, int C, int L, void* stream) {
+// Filter spectra: k (C, L) f32 -> K (C, n) complex in [k1][k2] layout, scaled by 1/n, + D / n when Dv is given
+// (the conv with K then carries + D u, forward and adjoint: D is real). SK: (C, n) scratch.
+extern "C" int lci_fftconv_spectrum(const float* k, const float* Dv, void* K, void* SK, const void* tw, int C, int L,
+                                    void* stream) {
   FftArgs a{};
   if (fft_plan(a, L)) return 1;
-  a.src = k; a.K = (f32x2*)K; a.SK = (f32x2*)SK; a.tw = (const f32x2*)tw; a.C = C; a.single = 1; a.mode = 0;
+  a.src = k; a.Dv = Dv; a.K = (f32x2*)K; a.SK = (f32x2*)SK; a.tw = (const f32x2*)tw; a.C = C; a.single = 1; a.mode = 0;
   hipStream_t s = (hipStream_t)stream;
   const int jc = fft_chunk(C, (long long)a.n * 8);
   for (int j0 = 0; j0 < C; j0 += jc) {
@@ -1970,7 +1979,10 @@ extern "C" int lci_fftconv_bwd(const float* dy, const float* u, const void* K, c
       if (launch_col(b, true, nj, s)) return 3;              // dk[j] = Re IFFT(SK_j)
     }
   }
-  if (dD) {
+  if (dD && dk) {   // the lag-0 filter-gradient entry is the dD sum
+    hipLaunchKernelGGL(dd_from_dk_kernel, dim3((C + 255) / 256), dim3(256), 0, s, dk, dD, C, L);
+    LCI_LAUNCH_CHECK();
+  } else if (dD) {
     const int vec = (L % 4 == 0) && ((uintptr_t)dy & 15) == 0 && ((uintptr_t)u & 15) == 0;
     hipLaunchKernelGGL(row_dot_kernel, dim3(R * C, (L + RD_SPAN - 1) / RD_SPAN), dim3(256), 0, s, dy, u, dD, L, C,
                        vec);

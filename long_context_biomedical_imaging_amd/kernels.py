@@ -798,14 +798,16 @@ def _fft_n(L):
     return int(_lib.load().lci_fft_size(int(L)))
 
 
-def _spectrum(k):
+def _spectrum(k, Dv=None):
+    """Filter spectra K = FFT_n(k) / n (+ D / n: the + D u term of fftconv_ref folded into the convolution)."""
     C, L = k.shape
     n = _fft_n(L)
     tw = _twiddles(n, k.device)
     K = torch.empty(C, n, 2, device=k.device, dtype=torch.float32)
     SK = torch.empty(C, n, 2, device=k.device, dtype=torch.float32)
     KernelTimer.run("fftconv_spectrum", 0.0, k, lambda: _lib.call(
-        "lci_fftconv_spectrum", k.data_ptr(), K.data_ptr(), SK.data_ptr(), tw.data_ptr(), C, L, _lib.stream_of(k)))
+        "lci_fftconv_spectrum", k.data_ptr(), _lib.ptr(Dv), K.data_ptr(), SK.data_ptr(), tw.data_ptr(), C, L,
+        _lib.stream_of(k)))
     return K
 
 
@@ -813,14 +815,15 @@ _KEEP_U_SPECTRUM = os.environ.get("LCI_FFT_KEEP_SPECTRUM", "1") != "0"
 
 
 class _FFTConv(torch.autograd.Function):
-    """y = causal_conv(u, k) + D u along L for rows (R, C, L) f32; filter = channel index."""
+    """y = causal_conv(u, k) + D u along L for rows (R, C, L) f32; filter = channel index. D rides in the filter
+    spectra (K + D / n), so neither pass reads u / dy again for the D term, and dD is the lag-0 entry of dk."""
 
     @staticmethod
     def forward(ctx, u, k, D):
         R, C, L = u.shape
         kf = k.float().contiguous()
         Dv = D.float().contiguous()
-        K = _spectrum(kf)
+        K = _spectrum(kf, Dv)
         n = K.shape[1]
         tw = _twiddles(n, u.device)
         y = torch.empty_like(u)
@@ -828,16 +831,16 @@ class _FFTConv(torch.autograd.Function):
         # column spectra of u kept for the filter gradient (one column pass fewer in the backward), when k needs one
         Su = torch.empty_like(S) if (ctx.needs_input_grad[1] and _KEEP_U_SPECTRUM) else None
         KernelTimer.run("fftconv_fwd", float(R * C * L), u, lambda: _lib.call(
-            "lci_fftconv_fwd", u.data_ptr(), K.data_ptr(), Dv.data_ptr(), y.data_ptr(), S.data_ptr(), _lib.ptr(Su),
+            "lci_fftconv_fwd", u.data_ptr(), K.data_ptr(), None, y.data_ptr(), S.data_ptr(), _lib.ptr(Su),
             tw.data_ptr(), R, C, L, _lib.stream_of(u)))
         del S
-        ctx.save_for_backward(u, K, Dv, Su)
+        ctx.save_for_backward(u, K, Su)
         ctx.kdtype = k.dtype
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        u, K, Dv, Su = ctx.saved_tensors
+        u, K, Su = ctx.saved_tensors
         R, C, L = u.shape
         n = K.shape[1]
         tw = _twiddles(n, u.device)
@@ -852,7 +855,7 @@ class _FFTConv(torch.autograd.Function):
         S2 = torch.empty(C * P, n, 2, device=u.device, dtype=torch.float32) if (want_k and Su is None) else None
         SK = torch.empty(C, n, 2, device=u.device, dtype=torch.float32) if want_k else None
         KernelTimer.run("fftconv_bwd", float(R * C * L), u, lambda: _lib.call(
-            "lci_fftconv_bwd", dy.data_ptr(), u.data_ptr(), K.data_ptr(), Dv.data_ptr(), du.data_ptr(),
+            "lci_fftconv_bwd", dy.data_ptr(), u.data_ptr(), K.data_ptr(), None, du.data_ptr(),
             _lib.ptr(dk), _lib.ptr(dD), S.data_ptr(), _lib.ptr(S2), _lib.ptr(Su if want_k else None), _lib.ptr(SK),
             tw.data_ptr(), R, C, L, _lib.stream_of(u)))
         return du, (dk.to(ctx.kdtype) if dk is not None else None), dD
