@@ -223,7 +223,8 @@ __global__ __launch_bounds__(512) void fft_row_kernel(FftArgs a) {
     __syncthreads();
     f32x2* r = lds_fft<false>(x, y, N, a.ln2, 1, twl, N);
     f32x2* K = a.K + (long long)j * a.n + (long long)k1 * N;
-    for (int i = threadIdx.x; i < N; i += blockDim.x) K[i] = r[i] * invn;
+    const float dn = a.Dv ? a.Dv[j] * invn : 0.f;   // + D / n: the spectrum of D delta (the D u term)
+    for (int i = threadIdx.x; i < N; i += blockDim.x) K[i] = r[i] * invn + f32x2{dn, 0.f};
     return;
   }
   const f32x2* K = a.K + (long long)j * a.n + (long long)k1 * N;

@@ -1,7 +1,7 @@
 export TMPDIR=/tmp
 OUT=gpurun_out/r5e
 mkdir -p $OUT
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/gputest.log 2>&1 || { echo "STOP gputest"; tail -30 $OUT/gputest.log; exit 1; }
+timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $OUT/gputest.log 2>&1 || { echo "STOP gputest"; tail -30 $OUT/gputest.log; exit 1; }
 tail -2 $OUT/gputest.log
 timeout -k 10 300 python -u tools/kernel_bench.py gemm mlp > $OUT/kb.jsonl 2> $OUT/kb.err || { echo "STOP kb"; tail $OUT/kb.err; exit 1; }
 python3 - <<'PY'
