@@ -20,7 +20,6 @@
 
 #include <algorithm>
 #include <initializer_list>
-#include <cstdlib>
 
 namespace lci {
 
@@ -47,7 +46,7 @@ struct FftArgs {
   int mode;                             // row pass: 0 = spectrum of filters, 1 = fwd conv, 2 = bwd (conj + dk)
   int single;                           // col passes: 1 = the source is the filter (C rows, no pairing)
   int pid0;                             // first pair (col passes) / filter (row pass) of this launch's chunk
-  int pb;                               // row pass: sequences per LDS batch (ROW_PB, LCI_FFT_ROW_PB)
+  int pb;                               // row pass: sequences per LDS batch (ROW_PB)
 };
 
 // ------------------------------------------------------------------- sub-FFTs: radix-8/4/2 Stockham in LDS
@@ -336,22 +335,20 @@ __device__ __forceinline__ void fft512_wave(f32x2 (&v)[8], f32x2* buf, const f32
   dft<8, INV>(v);                                        // over la -> m2: X[k + 8 m1 + 64 m2] = X[L + 64 m2]
 }
 
-// grid (n1, filters of the chunk); block 64 * nw (waves split the filter's pairs). Same math as fft_row_kernel.
-#ifndef LCI_FFT_ROW_PF
-#define LCI_FFT_ROW_PF 0   // next-pair prefetch in the row pass: measured neutral (profiles/r04_fft_ab.txt r4row)
-#endif
+// grid (n1, filters); block 64 * nw (waves split the filter's pairs). Same math as fft_row_kernel. (A next-pair
+// prefetch measured neutral, profiles/r04_fft_ab.txt r4row.)
 __global__ __launch_bounds__(256) void fft_row512_kernel(FftArgs a) {
   __shared__ f32x2 twl[512];
   __shared__ f32x2 wbuf[4][8 * R5_S1];
   const int L = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int k1 = blockIdx.x, j = a.pid0 + blockIdx.y;
+  // filter spectra (mode 0): the workgroup's waves take nw consecutive rows k1; else one row k1, waves split pairs
+  const int k1 = a.mode == 0 ? blockIdx.x * nw + w : blockIdx.x, j = a.pid0 + blockIdx.y;
   const float invn = 1.f / (float)a.n;
   load_twl(twl, a.tw, 512, a.n);
   __syncthreads();
   f32x2* buf = wbuf[w];
   const long long row = (long long)k1 * 512 + L;
-  if (a.mode == 0) {   // filter spectrum: K_j[k1][:] = FFT_512(T[k1][:]) / n  (one wave)
-    if (w != 0) return;
+  if (a.mode == 0) {   // filter spectrum: K_j[k1][:] = FFT_512(T[k1][:]) / n  (one wave per row)
     f32x2 v[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) v[r] = a.SK[(long long)j * a.n + row + 64 * r];
@@ -369,30 +366,13 @@ __global__ __launch_bounds__(256) void fft_row512_kernel(FftArgs a) {
   f32x2 acc[8];
 #pragma unroll
   for (int r = 0; r < 8; ++r) acc[r] = f32x2{0.f, 0.f};
-  // the wave's next pair is loaded while this one is transformed (LCI_FFT_ROW_PF)
-  f32x2 nv[8], nv2[8];
-  auto ldp = [&](int p) __attribute__((always_inline)) {
-    const long long off = ((long long)j * a.P + p) * a.n + row;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      nv[r] = a.S[off + 64 * r];
-      if (two) nv2[r] = a.S2[off + 64 * r];
-    }
-  };
-  if (LCI_FFT_ROW_PF && w < a.P) ldp(w);
   for (int p = w; p < a.P; p += nw) {
     const long long off = ((long long)j * a.P + p) * a.n + row;
     f32x2 v[8], v2[8];
-    if (LCI_FFT_ROW_PF) {
 #pragma unroll
-      for (int r = 0; r < 8; ++r) { v[r] = nv[r]; v2[r] = nv2[r]; }
-      if (p + nw < a.P) ldp(p + nw);
-    } else {
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        v[r] = a.S[off + 64 * r];
-        if (two) v2[r] = a.S2[off + 64 * r];
-      }
+    for (int r = 0; r < 8; ++r) {
+      v[r] = a.S[off + 64 * r];
+      if (two) v2[r] = a.S2[off + 64 * r];
     }
     fft512_wave<false>(v, buf, twl, L);
     if (two) {
@@ -573,16 +553,13 @@ __device__ __forceinline__ f32x2 tw3(const Tw3& w, long long e) {
   return cmul(cmul(w.t[e0], w.t[(1 << w.l0) + e1]), w.t[(1 << w.l0) + (1 << w.l1) + e2]);
 }
 
-// ------------------------------------------------ column FFTs of n1 = 1024 in registers, one column per wave at a time
-// (LCI_FFT_WAVE): lane L holds x[L + 64 r], r < 16; a 16-point DFT over r (4 x 4 in registers), twiddle
+// ------------------------------------------------ column FFTs of n1 = 1024 in registers, one column per wave at a time:
+// lane L holds x[L + 64 r], r < 16; a 16-point DFT over r (4 x 4 in registers), twiddle
 // W_1024^(L k), then for each half k = 8h + k' of the 16 frequencies the 64-point DFT over the lanes as 8 x 8 with two
 // wave-local LDS transposes (the second and third stages of fft512_wave) -- X[k + 16 m], m = m1 + 8 m2, lands in
 // lane k' + 8 m1. The column's own LDS region (its values are in registers by then) is the transpose buffer, so the
 // only workgroup barriers are the ones around the load and store loops (the in-place Stockham passes take two per
 // radix pass, 8 at n1 = 1024).
-#ifndef LCI_FFT_WAVE
-#define LCI_FFT_WAVE 1
-#endif
 template <bool INV>
 __device__ __forceinline__ f32x2 w16(int t) {   // W_16^t (forward e^{-2 pi i t / 16}), t < 16
   constexpr float C1 = 0.92387953251128674f, S1 = 0.38268343236508977f, H = 0.70710678118654752f;
@@ -711,9 +688,9 @@ __device__ __forceinline__ void col_fft_small_waves(f32x2* x, int ld, const f32x
   }
 }
 __host__ __device__ constexpr bool col_wave_scratch(int n1, int gw) {
-  return LCI_FFT_WAVE && (n1 == 512 || (n1 == 256 && gw % 8 == 0));
+  return n1 == 512 || (n1 == 256 && gw % 8 == 0);
 }
-__host__ __device__ constexpr bool col_wave_path(int n1, int gw) { return (LCI_FFT_WAVE && n1 == 1024) || col_wave_scratch(n1, gw); }
+__host__ __device__ constexpr bool col_wave_path(int n1, int gw) { return n1 == 1024 || col_wave_scratch(n1, gw); }
 template <bool INV, int GW, int CW, int NT>
 __device__ __forceinline__ void col_fft_waves(f32x2* x, int ld, const f32x2* twl, f32x2* scr) {
   constexpr int N1 = CW / GW;
@@ -1079,45 +1056,6 @@ struct GateArgs {
   int BB, L, D, H, hd, K;
 };
 
-template <typename T>
-__device__ __forceinline__ float conv_at(const GateArgs& a, const T* zb, int t, int c) {
-  float acc = a.bias ? a.bias[c] : 0.f;
-  for (int i = 0; i < a.K; ++i) {
-    const int s = t + i - (a.K - 1);
-    if (s >= 0) acc = fmaf(a.w[c * a.K + i], (float)zb[(long long)s * 3 * a.D + c], acc);
-  }
-  return acc;
-}
-
-// tile: 64 tokens x 64 output channels; grid (ceil(L/64), ceil(D/64), BB); block 256
-template <typename T>
-__global__ __launch_bounds__(256) void hyena_pre_fwd_kernel(GateArgs a) {
-  __shared__ float tile[64][65];
-  const int t0 = blockIdx.x * 64, ch0 = blockIdx.y * 64, bb = blockIdx.z;
-  const T* zb = (const T*)a.z + (long long)bb * a.L * 3 * a.D;
-  for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
-    const int cl = idx & 63, tl = idx >> 6;
-    const int t = t0 + tl, ch = ch0 + cl;
-    float vg = 0.f;
-    if (t < a.L && ch < a.D) {
-      const int h = ch / a.hd, jj = ch % a.hd;
-      const int base = h * 3 * a.hd + jj;
-      const float x1 = conv_at(a, zb, t, base);
-      const float x2 = conv_at(a, zb, t, base + a.hd);
-      const float v = conv_at(a, zb, t, base + 2 * a.hd);
-      vg = v * x1;
-      ((T*)a.x2)[((long long)bb * a.L + t) * a.D + ch] = (T)x2;
-    }
-    tile[cl][tl] = vg;
-  }
-  __syncthreads();
-  for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
-    const int tl = idx & 63, cl = idx >> 6;
-    const int t = t0 + tl, ch = ch0 + cl;
-    if (t < a.L && ch < a.D) a.vg[((long long)bb * a.D + ch) * a.L + t] = tile[cl][tl];
-  }
-}
-
 // out[bb, t, ch] = y[bb, ch, t] * x2[bb, t, ch]
 template <typename T>
 __global__ __launch_bounds__(256) void hyena_post_fwd_kernel(GateArgs a) {
@@ -1169,127 +1107,6 @@ __global__ __launch_bounds__(256) void hyena_post_bwd_kernel(GateArgs a) {
     const int t = t0 + tl, ch = ch0 + cl;
     if (t < a.L && ch < a.D) a.dy[((long long)bb * a.D + ch) * a.L + t] = tg[cl][tl];
   }
-}
-
-// pre bwd: per (token tile, channel tile): dconv for the 3 groups, then the causal conv transpose.
-// dconv_x1 = dvg * v, dconv_v = dvg * x1, dconv_x2 = gx2. dz[s][c] = sum_i w[c][i] dconv_c[s - i + K - 1].
-// One thread per (channel of 3D, token run of 64): sliding window, register partials for dw/db.
-template <typename T>
-__global__ __launch_bounds__(256) void hyena_pre_bwd_kernel(GateArgs a) {
-  const int c = blockIdx.y * 256 + threadIdx.x;   // channel of 3D
-  const int bb = blockIdx.z, t0 = blockIdx.x * 64, t1 = min(a.L, t0 + 64);
-  const int h = c / (3 * a.hd), rem = c % (3 * a.hd), part = rem / a.hd, jj = rem % a.hd;
-  const int ch = h * a.hd + jj;                   // output channel of D
-  const int base = h * 3 * a.hd + jj;
-  const T* zb = (const T*)a.z + (long long)bb * a.L * 3 * a.D;
-  // dvg is channel-major (BB, D, L): a thread per channel reading it directly strides by L across the wave
-  // (uncoalesced, ~9x slower overall), so the workgroup first stages the rows of its heads' channels for
-  // tokens [t0, t0 + 64 + K - 1) through LDS with token-contiguous loads.
-  extern __shared__ float sdvg[];                 // [256 threads][64 + K - 1] (row of the thread's channel)
-  __shared__ int chrow[256];
-  const int tw = 64 + a.K - 1;
-  chrow[threadIdx.x] = (c < 3 * a.D && part != 1) ? ch : -1;   // the x2 part (1) does not read dvg
-  __syncthreads();
-  for (int idx = threadIdx.x; idx < 256 * tw; idx += 256) {
-    const int rr = idx / tw, tt = idx - rr * tw, t = t0 + tt, cr = chrow[rr];
-    sdvg[idx] = (cr >= 0 && t < a.L) ? a.dvg[((long long)bb * a.D + cr) * a.L + t] : 0.f;
-  }
-  __syncthreads();
-  if (c >= 3 * a.D) return;
-  const float* dvl = sdvg + threadIdx.x * tw - t0;
-  auto dconv = [&](int t) -> float {
-    if (t < 0 || t >= a.L) return 0.f;
-    if (part == 1) return (float)((const float*)a.gx2)[((long long)bb * a.L + t) * a.D + ch];
-    const float other = conv_at(a, zb, t, part == 0 ? base + 2 * a.hd : base);
-    return dvl[t] * other;
-  };
-  float dwl[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  float dbl = 0.f;
-  const int K = a.K;
-  for (int s = t0; s < t1; ++s) {
-    // dz[s] = sum_i w[i] dconv[s - i + K - 1]
-    float acc = 0.f;
-    for (int i = 0; i < K; ++i) acc = fmaf(a.w[c * K + i], dconv(s - i + K - 1), acc);
-    ((T*)a.dz)[((long long)bb * a.L + s) * 3 * a.D + c] = (T)acc;
-    // dw[i] += dconv[s] * z[s + i - (K-1)]
-    const float g = dconv(s);
-    dbl += g;
-    for (int i = 0; i < K && i < 8; ++i) {
-      const int q = s + i - (K - 1);
-      if (q >= 0) dwl[i] = fmaf(g, (float)zb[(long long)q * 3 * a.D + c], dwl[i]);
-    }
-  }
-  for (int i = 0; i < K && i < 8; ++i) atomicAdd(a.dw + c * K + i, dwl[i]);
-  if (a.db) atomicAdd(a.db + c, dbl);
-}
-
-// Same result as hyena_pre_bwd_kernel for a compile-time filter order KC: each dconv(t), each short-conv value
-// and each z element is produced once per thread and kept in register rings (the generic kernel recomputes
-// dconv K + 1 times per token, each with a K-tap conv: ~16 loads per token-channel instead of 2).
-template <typename T, int KC>
-__global__ __launch_bounds__(256) void hyena_pre_bwd_ring_kernel(GateArgs a) {
-  const int c = blockIdx.y * 256 + threadIdx.x;   // channel of 3D
-  const int bb = blockIdx.z, t0 = blockIdx.x * 64, t1 = min(a.L, t0 + 64);
-  const int h = c / (3 * a.hd), rem = c % (3 * a.hd), part = rem / a.hd, jj = rem % a.hd;
-  const int ch = h * a.hd + jj;
-  const int base = h * 3 * a.hd + jj;
-  const T* zb = (const T*)a.z + (long long)bb * a.L * 3 * a.D;
-  constexpr int TW = 64 + KC;
-  extern __shared__ float sdvg[];                 // [256 threads][TW]: dvg row of the thread's channel
-  __shared__ int chrow[256];
-  chrow[threadIdx.x] = (c < 3 * a.D && part != 1) ? ch : -1;
-  __syncthreads();
-  for (int idx = threadIdx.x; idx < 256 * TW; idx += 256) {
-    const int rr = idx / TW, tt = idx - rr * TW, t = t0 + tt, cr = chrow[rr];
-    sdvg[idx] = (cr >= 0 && t < a.L) ? a.dvg[((long long)bb * a.D + cr) * a.L + t] : 0.f;
-  }
-  __syncthreads();
-  if (c >= 3 * a.D) return;
-  const float* dvl = sdvg + threadIdx.x * TW - t0;
-  const int oc = part == 0 ? base + 2 * a.hd : base;   // the other gate factor's channel (parts 0, 2)
-  float wc[KC], wo[KC];
-#pragma unroll
-  for (int i = 0; i < KC; ++i) { wc[i] = a.w[c * KC + i]; wo[i] = a.w[oc * KC + i]; }
-  const float bo = a.bias ? a.bias[oc] : 0.f;
-  auto zl = [&](int t, int cc) -> float { return (t >= 0 && t < a.L) ? (float)zb[(long long)t * 3 * a.D + cc] : 0.f; };
-  float zo[KC];   // z[t - KC + 1 .. t][oc] for the newest dconv position t
-  float zs[KC];   // z[s - KC + 1 .. s][c]
-  float dcw[KC];  // dconv(s .. s + KC - 1)
-#pragma unroll
-  for (int i = 0; i < KC; ++i) { zo[i] = zl(t0 - KC + i, oc); zs[i] = zl(t0 - KC + 1 + i, c); }
-  auto dconv_push = [&](int t) -> float {   // advance zo to position t, return dconv(t)
-#pragma unroll
-    for (int i = 0; i < KC - 1; ++i) zo[i] = zo[i + 1];
-    zo[KC - 1] = zl(t, oc);
-    if (t < 0 || t >= a.L) return 0.f;
-    if (part == 1) return (float)((const float*)a.gx2)[((long long)bb * a.L + t) * a.D + ch];
-    float conv = bo;
-#pragma unroll
-    for (int i = 0; i < KC; ++i) conv = fmaf(wo[i], zo[i], conv);
-    return dvl[t] * conv;
-  };
-#pragma unroll
-  for (int j = 0; j < KC; ++j) dcw[j] = dconv_push(t0 + j);
-  float dwl[KC], dbl = 0.f;
-#pragma unroll
-  for (int i = 0; i < KC; ++i) dwl[i] = 0.f;
-  for (int s = t0; s < t1; ++s) {
-    float acc = 0.f;
-#pragma unroll
-    for (int i = 0; i < KC; ++i) acc = fmaf(wc[i], dcw[KC - 1 - i], acc);
-    ((T*)a.dz)[((long long)bb * a.L + s) * 3 * a.D + c] = (T)acc;
-    const float g = dcw[0];
-    dbl += g;
-#pragma unroll
-    for (int i = 0; i < KC; ++i) dwl[i] = fmaf(g, zs[i], dwl[i]);
-#pragma unroll
-    for (int i = 0; i < KC - 1; ++i) { dcw[i] = dcw[i + 1]; zs[i] = zs[i + 1]; }
-    zs[KC - 1] = zl(s + 1, c);
-    dcw[KC - 1] = (s + KC < t0 + TW) ? dconv_push(s + KC) : 0.f;
-  }
-#pragma unroll
-  for (int i = 0; i < KC; ++i) atomicAdd(a.dw + c * KC + i, dwl[i]);
-  if (a.db) atomicAdd(a.db + c, dbl);
 }
 
 // ------------------------------------------------------------- short conv + gating, register-ring kernels
@@ -1485,19 +1302,15 @@ static int fft_plan(FftArgs& a, int L) {
   a.n = 1 << e;
   // n1 = 256-point column FFTs over G = 8 adjacent columns, n2 = n / 256 row FFTs (512 at L = 65536): the best
   // of the (n1, G) sweep in tools/fft_sweep.sh (wider column groups cost more in LDS occupancy than they save)
-  // tuning knobs for A/B runs: LCI_FFT_LN1 (log2 n1), LCI_FFT_G (columns per column-pass workgroup)
-  static const int env_ln1 = getenv("LCI_FFT_LN1") ? atoi(getenv("LCI_FFT_LN1")) : 8;
-  static const int env_g = getenv("LCI_FFT_G") ? atoi(getenv("LCI_FFT_G")) : 8;
-  a.ln1 = e < env_ln1 ? e : env_ln1;
+  a.ln1 = e < 8 ? e : 8;
   // the row pass keeps ~11 n2-point complex rows in LDS: n2 <= 1024 (n = 2^19 at L = 262144: n1 = 512, n2 = 1024)
   if (e - a.ln1 > 10) a.ln1 = e - 10;
   a.ln2 = e - a.ln1;
   if (a.ln2 == 0) { a.ln1 = e - 1; a.ln2 = 1; }
   // n = 2^17 .. 2^19: 512-point rows on fft_row512_kernel, n1 = 256 .. 1024 columns on the wide column kernel
-  static const bool row512 = !getenv("LCI_FFT_ROW_V1") && !getenv("LCI_FFT_LN1");
-  if (row512 && e >= 17 && e <= 19) { a.ln2 = 9; a.ln1 = e - 9; }
+  if (e >= 17 && e <= 19) { a.ln2 = 9; a.ln1 = e - 9; }
   a.n1 = 1 << a.ln1; a.n2 = 1 << a.ln2;
-  a.G = a.n2 < env_g ? a.n2 : env_g;
+  a.G = a.n2 < 8 ? a.n2 : 8;
   a.L = L;
   return 0;
 }
@@ -1759,10 +1572,9 @@ __global__ __launch_bounds__(256) void hyena_pre_bwd3_kernel(GateArgs a) {
   }
 }
 
-// Whether the v3 kernels take this call (LCI_HYENA_GLUE_V2=1 forces the v2 kernels).
+// Whether the v3 kernels take this call (else the v2 register-ring kernels run).
 static bool hg_v3_ok(const GateArgs& a, int dtype, std::initializer_list<const void*> ptrs) {
-  static const bool off = getenv("LCI_HYENA_GLUE_V2") != nullptr;
-  if (off || dtype != 1 || a.hd % 8 || a.D % 8 || a.L % 4) return false;
+  if (dtype != 1 || a.hd % 8 || a.D % 8 || a.L % 4) return false;
   for (const void* p : ptrs)
     if (p && ((uintptr_t)p & 15)) return false;
   return true;
@@ -1785,72 +1597,29 @@ extern "C" int lci_fft_twiddles(void* tw, int n, void* stream) {
 }
 
 static int launch_col(FftArgs& a, bool inv, int nblk_y, hipStream_t s) {
-  // complex elements per workgroup: 4096 (~130 instead of ~245 VGPRs, 4 workgroups per CU) while that still gives
-  // >= 8 columns (32-B row segments); 8192 for n1 = 1024 (C4: 4096 would load 16-B row segments, measured 24 ms/step
-  // slower)
-  static const int env_cw = getenv("LCI_FFT_CW") ? atoi(getenv("LCI_FFT_CW")) : 0;
-  // n1 = 1024 with the register column FFTs (LCI_FFT_WIDE): 16 columns (64-B row segments) per 512-thread workgroup
-  static const int wide = getenv("LCI_FFT_WIDE") ? atoi(getenv("LCI_FFT_WIDE")) : 1;
-  const int cw = env_cw ? env_cw
-                        : (a.n1 <= 512 ? (wide > 1 && LCI_FFT_WAVE && a.n1 == 256 ? CW_ELEMS : CW_ELEMS / 2)
-                                       : (wide && LCI_FFT_WAVE && a.n1 == 1024 ? 2 * CW_ELEMS : CW_ELEMS));
+  // wide column kernels: complex elements per workgroup 4096 at n1 <= 512 (~130 instead of ~245 VGPRs, 4 workgroups
+  // per CU; >= 8 columns = 32-B row segments), 16384 at n1 = 1024 (16 columns, 64-B row segments, 512 threads, the
+  // register column FFTs); the LDS kernels below for short columns / few columns (n2 < GW)
+  const int cw = a.n1 == 1024 ? 2 * CW_ELEMS : CW_ELEMS / 2;
   const int gw = cw / a.n1;
-  if ((cw == 16384 ? a.n1 == 1024 && gw == 16 : (cw == 8192 || cw == 4096)) &&
-      (gw == 4 || gw == 8 || gw == 16 || gw == 32) && a.n2 % gw == 0 &&
-      !getenv("LCI_FFT_COL_V1")) {
+  if ((a.n1 == 1024 || a.n1 <= 512) && (gw == 8 || gw == 16) && a.n2 % gw == 0) {
     const size_t sh = ((size_t)gw * (a.n1 + 1) + a.n1 + tw3_entries(a.ln1 + a.ln2) +
-                       (col_wave_scratch(a.n1, gw) ? (cw == 8192 && a.n1 == 256 ? 8 : 4) * 8 * R5_S1 : 0)) *
-                      sizeof(f32x2);
-    dim3 grid(a.n2 / gw, nblk_y);
-#define LCI_COLW(GW, CW, NT)                                                                                       \
-    (void)hipFuncSetAttribute((const void*)(inv ? fft_colw_inv_kernel<GW, CW, NT> : fft_colw_fwd_kernel<GW, CW, NT>), \
+                       (col_wave_scratch(a.n1, gw) ? 4 * 8 * R5_S1 : 0)) * sizeof(f32x2);
+    // GP = 4 column groups per workgroup, the next group's rows loaded during this group's FFT (wave FFT path;
+    // the forward's 16-B loads need L % 4 == 0)
+    const bool gp = gw == 16 && (a.n2 / gw) % 4 == 0 && (inv || (a.L & 3) == 0);
+    const dim3 grid(gp ? a.n2 / gw / 4 : a.n2 / gw, nblk_y);
+#define LCI_COLW(GW, CW, NT, GP)                                                                                   \
+    (void)hipFuncSetAttribute((const void*)(inv ? fft_colw_inv_kernel<GW, CW, NT, GP> : fft_colw_fwd_kernel<GW, CW, NT, GP>), \
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                           \
-    if (inv) hipLaunchKernelGGL((fft_colw_inv_kernel<GW, CW, NT>), grid, dim3(NT), sh, s, a);                    \
-    else hipLaunchKernelGGL((fft_colw_fwd_kernel<GW, CW, NT>), grid, dim3(NT), sh, s, a);
-    if (cw == 16384) {
-      static const int gp_env = getenv("LCI_FFT_GP") ? atoi(getenv("LCI_FFT_GP")) : 4;
-      if (gw != 16) return 1;
-      if (gp_env == 8 && (inv || (a.L & 3) == 0) && (a.n2 / gw) % 8 == 0) {   // (A/B: 8 groups per workgroup)
-        if (inv) {
-          (void)hipFuncSetAttribute((const void*)fft_colw_inv_kernel<16, 16384, 512, 8>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-          hipLaunchKernelGGL((fft_colw_inv_kernel<16, 16384, 512, 8>), dim3(a.n2 / gw / 8, nblk_y), dim3(512), sh, s, a);
-        } else {
-          (void)hipFuncSetAttribute((const void*)fft_colw_fwd_kernel<16, 16384, 512, 8>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-          hipLaunchKernelGGL((fft_colw_fwd_kernel<16, 16384, 512, 8>), dim3(a.n2 / gw / 8, nblk_y), dim3(512), sh, s, a);
-        }
-      } else if (!inv && gp_env == 4 && (a.L & 3) == 0 && (a.n2 / gw) % 4 == 0) {
-        (void)hipFuncSetAttribute((const void*)fft_colw_fwd_kernel<16, 16384, 512, 4>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        hipLaunchKernelGGL((fft_colw_fwd_kernel<16, 16384, 512, 4>), dim3(a.n2 / gw / 4, nblk_y), dim3(512), sh, s, a);
-      } else if (inv && gp_env == 4 && !(getenv("LCI_FFT_GP_INV") && atoi(getenv("LCI_FFT_GP_INV")) == 0) &&
-                 (a.n2 / gw) % 4 == 0) {
-        (void)hipFuncSetAttribute((const void*)fft_colw_inv_kernel<16, 16384, 512, 4>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        hipLaunchKernelGGL((fft_colw_inv_kernel<16, 16384, 512, 4>), dim3(a.n2 / gw / 4, nblk_y), dim3(512), sh, s, a);
-      } else {
-        LCI_COLW(16, 16384, 512)
-      }
-    } else if (cw == 8192) {
-      if (gw == 32 && a.n1 == 256 && LCI_FFT_WAVE) { LCI_COLW(32, 8192, 512) }
-      else if (gw == 32) { LCI_COLW(32, 8192, 256) } else if (gw == 16) { LCI_COLW(16, 8192, 256) }
-      else if (gw == 8) { LCI_COLW(8, 8192, 256) } else return 1;
+    if (inv) hipLaunchKernelGGL((fft_colw_inv_kernel<GW, CW, NT, GP>), grid, dim3(NT), sh, s, a);                \
+    else hipLaunchKernelGGL((fft_colw_fwd_kernel<GW, CW, NT, GP>), grid, dim3(NT), sh, s, a);
+    if (a.n1 == 1024) {
+      if (gp) { LCI_COLW(16, 16384, 512, 4) } else { LCI_COLW(16, 16384, 512, 1) }
+    } else if (gw == 16) {
+      if (gp && a.n1 == 256) { LCI_COLW(16, 4096, 256, 4) } else { LCI_COLW(16, 4096, 256, 1) }
     } else {
-      static const int gp4 = getenv("LCI_FFT_GP") ? atoi(getenv("LCI_FFT_GP")) : 4;
-      if (gw == 16 && gp4 == 4 && LCI_FFT_WAVE && a.n1 == 256 && (a.n2 / gw) % 4 == 0 && (inv || (a.L & 3) == 0)) {
-        // the column-group prefetch at n1 = 256 as well (LCI_FFT_GP)
-        if (inv) {
-          (void)hipFuncSetAttribute((const void*)fft_colw_inv_kernel<16, 4096, 256, 4>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-          hipLaunchKernelGGL((fft_colw_inv_kernel<16, 4096, 256, 4>), dim3(a.n2 / gw / 4, nblk_y), dim3(256), sh, s, a);
-        } else {
-          (void)hipFuncSetAttribute((const void*)fft_colw_fwd_kernel<16, 4096, 256, 4>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-          hipLaunchKernelGGL((fft_colw_fwd_kernel<16, 4096, 256, 4>), dim3(a.n2 / gw / 4, nblk_y), dim3(256), sh, s, a);
-        }
-      } else if (gw == 16) { LCI_COLW(16, 4096, 256) } else if (gw == 8) { LCI_COLW(8, 4096, 256) }
-      else if (gw == 4) { LCI_COLW(4, 4096, 256) } else return 1;
+      LCI_COLW(8, 4096, 256, 1)
     }
 #undef LCI_COLW
     LCI_LAUNCH_CHECK();
@@ -1867,18 +1636,20 @@ static int launch_col(FftArgs& a, bool inv, int nblk_y, hipStream_t s) {
 }
 
 static int launch_row(FftArgs& a, int nfilt, hipStream_t s) {
-  if (a.n2 == 512 && !getenv("LCI_FFT_ROW_V1")) {
-    static const int nw_max = getenv("LCI_FFT_ROW_NW") ? std::max(1, std::min(4, atoi(getenv("LCI_FFT_ROW_NW")))) : 4;
-    int nw = 1;   // waves per workgroup: the largest divisor of the pair count up to nw_max (balanced waves)
-    for (int q = nw_max; q >= 1; --q)
+  if (a.n2 == 512) {
+    int nw = 1;   // waves per workgroup: the largest divisor of the pair count up to 4 (balanced waves)
+    for (int q = 4; q >= 1; --q)
       if (a.P % q == 0) { nw = q; break; }
-    if (a.mode == 0) nw = 1;
+    if (a.mode == 0) {   // filter spectra: 4 rows k1 per workgroup (one-wave workgroups were latency-bound)
+      hipLaunchKernelGGL(fft_row512_kernel, dim3(a.n1 / 4, nfilt), dim3(256), 0, s, a);
+      LCI_LAUNCH_CHECK();
+      return 0;
+    }
     hipLaunchKernelGGL(fft_row512_kernel, dim3(a.n1, nfilt), dim3(64 * nw), 0, s, a);
     LCI_LAUNCH_CHECK();
     return 0;
   }
-  static const int env_pb = getenv("LCI_FFT_ROW_PB") ? atoi(getenv("LCI_FFT_ROW_PB")) : ROW_PB;
-  a.pb = std::max(2, std::min(16, env_pb)) & ~1;
+  a.pb = ROW_PB;
   const size_t sh = ((size_t)2 * a.pb + 3) * a.n2 * sizeof(f32x2);   // x, y (+ x2, y2 at PB/2) + kr, acc, twl
   LCI_CHECK(sh <= 160 * 1024, "fft row pass: %zu bytes of LDS", sh);
   (void)hipFuncSetAttribute((const void*)fft_row_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -1886,15 +1657,6 @@ static int launch_row(FftArgs& a, int nfilt, hipStream_t s) {
   hipLaunchKernelGGL(fft_row_kernel, dim3(a.n1, nfilt), dim3(thr), sh, s, a);
   LCI_LAUNCH_CHECK();
   return 0;
-}
-
-// Filters per launch chunk: the passes of one chunk run back to back so its spectra scratch (bytes_per_filter
-// each) stays resident in the Infinity Cache between the column and row passes (LCI_FFT_CHUNK_MB, 0 = one chunk).
-static int fft_chunk(int C, long long bytes_per_filter) {
-  static const long long mb = getenv("LCI_FFT_CHUNK_MB") ? atoll(getenv("LCI_FFT_CHUNK_MB")) : 0;
-  if (mb <= 0) return C;
-  const long long jc = (mb << 20) / std::max(1LL, bytes_per_filter);
-  return (int)std::max(1LL, std::min((long long)C, jc));
 }
 
 // Filter spectra: k (C, L) f32 -> K (C, n) complex in [k1][k2] layout, scaled by 1/n, + D / n when Dv is given
@@ -1905,13 +1667,9 @@ extern "C" int lci_fftconv_spectrum(const float* k, const float* Dv, void* K, vo
   if (fft_plan(a, L)) return 1;
   a.src = k; a.Dv = Dv; a.K = (f32x2*)K; a.SK = (f32x2*)SK; a.tw = (const f32x2*)tw; a.C = C; a.single = 1; a.mode = 0;
   hipStream_t s = (hipStream_t)stream;
-  const int jc = fft_chunk(C, (long long)a.n * 8);
-  for (int j0 = 0; j0 < C; j0 += jc) {
-    const int nj = std::min(jc, C - j0);
-    a.pid0 = j0;
-    if (launch_col(a, false, nj, s)) return 3;
-    if (launch_row(a, nj, s)) return 3;
-  }
+  a.pid0 = 0;
+  if (launch_col(a, false, C, s)) return 3;
+  if (launch_row(a, C, s)) return 3;
   return 0;
 }
 
@@ -1925,20 +1683,14 @@ extern "C" int lci_fftconv_fwd(const float* u, const void* K, const float* Dv, f
   a.src = u; a.dst = y; a.K = (f32x2*)K; a.tw = (const f32x2*)tw; a.Dv = Dv;
   a.R = R; a.C = C; a.P = (R + 1) / 2; a.single = 0; a.mode = 1;
   hipStream_t s = (hipStream_t)stream;
-  const int jc = fft_chunk(C, (long long)a.P * a.n * 8);
-  for (int j0 = 0; j0 < C; j0 += jc) {
-    const int nj = std::min(jc, C - j0);
-    a.pid0 = j0 * a.P;
-    a.S = (f32x2*)(Su ? Su : S);
-    if (launch_col(a, false, nj * a.P, s)) return 3;
-    a.pid0 = j0;
-    a.So = Su ? (f32x2*)S : nullptr;
-    if (launch_row(a, nj, s)) return 3;
-    a.So = nullptr;
-    a.S = (f32x2*)S;
-    a.pid0 = j0 * a.P;
-    if (launch_col(a, true, nj * a.P, s)) return 3;
-  }
+  a.pid0 = 0;
+  a.S = (f32x2*)(Su ? Su : S);
+  if (launch_col(a, false, C * a.P, s)) return 3;
+  a.So = Su ? (f32x2*)S : nullptr;
+  if (launch_row(a, C, s)) return 3;
+  a.So = nullptr;
+  a.S = (f32x2*)S;
+  if (launch_col(a, true, C * a.P, s)) return 3;
   return 0;
 }
 
@@ -1954,31 +1706,24 @@ extern "C" int lci_fftconv_bwd(const float* dy, const float* u, const void* K, c
   a.SK = dk ? (f32x2*)SK : nullptr;
   a.R = R; a.C = C; a.P = (R + 1) / 2; a.Dv = Dv; a.dk = dk;
   hipStream_t s = (hipStream_t)stream;
-  const int jc = fft_chunk(C, (long long)a.P * a.n * 8 * (dk ? 2 : 1));
-  for (int j0 = 0; j0 < C; j0 += jc) {
-    const int nj = std::min(jc, C - j0);
-    FftArgs c = a;
-    c.single = 0;
-    c.src = dy;
-    c.pid0 = j0 * a.P;
-    if (launch_col(c, false, nj * a.P, s)) return 3;         // S <- col FFT of dy pairs
-    if (dk && !Su) {
-      FftArgs b = c;
-      b.S = (f32x2*)S2; b.src = u;
-      if (launch_col(b, false, nj * a.P, s)) return 3;       // S2 <- col FFT of u pairs
-    }
-    c.mode = 2;
-    c.pid0 = j0;
-    if (launch_row(c, nj, s)) return 3;                      // S <- conj(K) products, SK <- dk rows
-    c.src = dy; c.dst = du;
-    c.pid0 = j0 * a.P;
-    if (launch_col(c, true, nj * a.P, s)) return 3;          // du = IFFT + D dy
-    if (dk) {
-      FftArgs b = c;
-      b.single = 1;
-      b.pid0 = j0;
-      if (launch_col(b, true, nj, s)) return 3;              // dk[j] = Re IFFT(SK_j)
-    }
+  FftArgs c = a;
+  c.single = 0;
+  c.src = dy;
+  c.pid0 = 0;
+  if (launch_col(c, false, C * a.P, s)) return 3;            // S <- col FFT of dy pairs
+  if (dk && !Su) {
+    FftArgs b = c;
+    b.S = (f32x2*)S2; b.src = u;
+    if (launch_col(b, false, C * a.P, s)) return 3;          // S2 <- col FFT of u pairs
+  }
+  c.mode = 2;
+  if (launch_row(c, C, s)) return 3;                         // S <- conj(K) products, SK <- dk rows
+  c.src = dy; c.dst = du;
+  if (launch_col(c, true, C * a.P, s)) return 3;             // du = IFFT (+ D dy)
+  if (dk) {
+    FftArgs b = c;
+    b.single = 1;
+    if (launch_col(b, true, C, s)) return 3;                 // dk[j] = Re IFFT(SK_j)
   }
   if (dD && dk) {   // the lag-0 filter-gradient entry is the dD sum
     hipLaunchKernelGGL(dd_from_dk_kernel, dim3((C + 255) / 256), dim3(256), 0, s, dk, dD, C, L);
@@ -2008,28 +1753,21 @@ extern "C" int lci_hyena_pre_fwd(int dtype, const void* z, const float* w, const
     }
 #undef LCI_PRE_FWD3
   }
-  {   // register-ring kernels (every order the C-ABI accepts)
-    dim3 grid2((L + HY_TT - 1) / HY_TT, (a.D + 63) / 64, BB);
+  // register-ring kernels (every order the C-ABI accepts)
+  dim3 grid2((L + HY_TT - 1) / HY_TT, (a.D + 63) / 64, BB);
 #define LCI_PRE_FWD(KK)                                                                                         \
   case KK:                                                                                                    \
     if (dtype == 1)                                                                                           \
       hipLaunchKernelGGL((hyena_pre_fwd2_kernel<bf16, KK>), grid2, dim3(256), 0, (hipStream_t)stream, a);     \
     else                                                                                                      \
       hipLaunchKernelGGL((hyena_pre_fwd2_kernel<float, KK>), grid2, dim3(256), 0, (hipStream_t)stream, a);    \
-    LCI_LAUNCH_CHECK();                                                                                       \
-    return 0;
-    if (!getenv("LCI_HYENA_PRE_V1")) {
-      switch (K) {
-        LCI_PRE_FWD(1) LCI_PRE_FWD(2) LCI_PRE_FWD(3) LCI_PRE_FWD(4) LCI_PRE_FWD(5) LCI_PRE_FWD(6) LCI_PRE_FWD(7)
-        LCI_PRE_FWD(8)
-        default: break;
-      }
-    }
-#undef LCI_PRE_FWD
+    break;
+  switch (K) {
+    LCI_PRE_FWD(1) LCI_PRE_FWD(2) LCI_PRE_FWD(3) LCI_PRE_FWD(4) LCI_PRE_FWD(5) LCI_PRE_FWD(6) LCI_PRE_FWD(7)
+    LCI_PRE_FWD(8)
+    default: break;
   }
-  dim3 grid((L + 63) / 64, (a.D + 63) / 64, BB);
-  if (dtype == 1) hipLaunchKernelGGL(hyena_pre_fwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, a);
-  else hipLaunchKernelGGL(hyena_pre_fwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, a);
+#undef LCI_PRE_FWD
   LCI_LAUNCH_CHECK();
   return 0;
 }
@@ -2087,46 +1825,23 @@ extern "C" int lci_hyena_pre_bwd(int dtype, const void* z, const float* w, const
     }
 #undef LCI_PRE_BWD3
   }
-  if (!getenv("LCI_HYENA_PRE_V1")) {   // one lane per output channel, token tiles strided over ~8 workgroups/CU
-    const int ntiles = (L + HY_TT - 1) / HY_TT, ncy = (a.D + 63) / 64;
-    const int gx = std::max(1, std::min(ntiles, 2048 / std::max(1, ncy * BB)));
-    dim3 grid2(gx, ncy, BB);
+  // one lane per output channel, token tiles strided over ~8 workgroups/CU (every order the C-ABI accepts)
+  const int ntiles = (L + HY_TT - 1) / HY_TT, ncy = (a.D + 63) / 64;
+  const int gx = std::max(1, std::min(ntiles, 2048 / std::max(1, ncy * BB)));
+  dim3 grid2(gx, ncy, BB);
 #define LCI_PRE_BWD2(KK)                                                                                        \
   case KK:                                                                                                    \
     if (dtype == 1)                                                                                           \
       hipLaunchKernelGGL((hyena_pre_bwd2_kernel<bf16, KK>), grid2, dim3(256), 0, (hipStream_t)stream, a);     \
     else                                                                                                      \
       hipLaunchKernelGGL((hyena_pre_bwd2_kernel<float, KK>), grid2, dim3(256), 0, (hipStream_t)stream, a);    \
-    LCI_LAUNCH_CHECK();                                                                                       \
-    return 0;
-    switch (K) {
-      LCI_PRE_BWD2(1) LCI_PRE_BWD2(2) LCI_PRE_BWD2(3) LCI_PRE_BWD2(4) LCI_PRE_BWD2(5) LCI_PRE_BWD2(6)
-      LCI_PRE_BWD2(7) LCI_PRE_BWD2(8)
-      default: break;
-    }
+    break;
+  switch (K) {
+    LCI_PRE_BWD2(1) LCI_PRE_BWD2(2) LCI_PRE_BWD2(3) LCI_PRE_BWD2(4) LCI_PRE_BWD2(5) LCI_PRE_BWD2(6)
+    LCI_PRE_BWD2(7) LCI_PRE_BWD2(8)
+    default: break;
+  }
 #undef LCI_PRE_BWD2
-  }
-  dim3 grid((L + 63) / 64, (3 * a.D + 255) / 256, BB);
-  {   // register-ring kernel for every supported order (the reference's models use short_filter_order = 5)
-    const size_t lds = (size_t)256 * (64 + K) * sizeof(float);
-#define LCI_PRE_BWD(KK)                                                                                          \
-  case KK:                                                                                                     \
-    if (dtype == 1)                                                                                            \
-      hipLaunchKernelGGL((hyena_pre_bwd_ring_kernel<bf16, KK>), grid, dim3(256), lds, (hipStream_t)stream, a); \
-    else                                                                                                       \
-      hipLaunchKernelGGL((hyena_pre_bwd_ring_kernel<float, KK>), grid, dim3(256), lds, (hipStream_t)stream, a); \
-    LCI_LAUNCH_CHECK();                                                                                        \
-    return 0;
-    switch (K) {
-      LCI_PRE_BWD(1) LCI_PRE_BWD(2) LCI_PRE_BWD(3) LCI_PRE_BWD(4) LCI_PRE_BWD(5) LCI_PRE_BWD(6) LCI_PRE_BWD(7)
-      LCI_PRE_BWD(8)
-      default: break;
-    }
-#undef LCI_PRE_BWD
-  }
-  const size_t lds = (size_t)256 * (64 + K - 1) * sizeof(float);
-  if (dtype == 1) hipLaunchKernelGGL(hyena_pre_bwd_kernel<bf16>, grid, dim3(256), lds, (hipStream_t)stream, a);
-  else hipLaunchKernelGGL(hyena_pre_bwd_kernel<float>, grid, dim3(256), lds, (hipStream_t)stream, a);
   LCI_LAUNCH_CHECK();
   return 0;
 }

@@ -87,7 +87,14 @@ def parse(out_dir, traffic_path=None):
             kern = sorted({fs[i][0].split("(")[0] for i in lib})
         rows = B * H * HD
         alg = (8.0 if which == "fftconv_fwd" else 16.0) * rows * L
-        res[which] = {"bytes_per_call": sum(tot) / len(tot), "algorithmic_bytes": alg,
+        per = {}   # per-kernel bytes of the first call (read = 2 x FETCH_SIZE, write)
+        fs, ws = fetch[sl][0], write[sl][0]
+        for i, (nm, _) in enumerate(fs):
+            if "lci::" in nm:
+                key = f"{i}:{nm.split('(')[0]}"
+                per[key] = {"read": 2.0 * fs[i][1] * 1024, "write": ws[i][1] * 1024}
+                print(f"  {which} {key:60s} read {per[key]['read'] / 1e9:7.3f} GB  write {per[key]['write'] / 1e9:7.3f} GB")
+        res[which] = {"bytes_per_call": sum(tot) / len(tot), "algorithmic_bytes": alg, "per_kernel": per,
                       "ratio_to_algorithmic": sum(tot) / len(tot) / alg, "kernels": kern, "calls": len(tot)}
         print(f"{which}: {res[which]['bytes_per_call'] / 1e9:.3f} GB per call, algorithmic {alg / 1e9:.3f} GB "
               f"({res[which]['ratio_to_algorithmic']:.2f}x); kernels {kern}")
