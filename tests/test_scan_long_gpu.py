@@ -4,7 +4,10 @@ The GPU scan runs the whole sequence in thousands of chunks with the two-level c
 reference is oracle/scan_ref.c, an fp64 per-step restatement of mamba-ssm's `selective_scan_ref` (cross-checked
 against the fixture-pinned Python restatement in tests/test_oracle_golden.py), run on the host cores.
 - bf16 I/O (the C5 autocast dtype) at L = 2^21, forward + all seven gradients, on the same bf16-rounded inputs:
-  rel-L2 <= 2e-2 on y and 3e-2 on the gradients (bf16 outputs; dB/dC sum 192 channels of bf16-rounded terms).
+  rel-L2 <= 5e-3 on y and on every gradient. The backward recomputes its 8-step sub-blocks from bf16 checkpoints
+  (half the bytes of f32 states); measured errors (profiles/r05_pmc.txt) are 1.7e-3 on y / du / ddelta / dB / dC
+  (the bf16 rounding of the outputs themselves, 2^-9 / sqrt(3)), 8.5e-4 on dA: the checkpoint rounding adds nothing
+  visible at this bound.
 - f32 I/O at L = 2^20 (the f32 y/z buffer of 2^21 tokens exceeds the kernel's 32-bit buffer offsets, which it
   reports as an error), forward + all seven gradients: rel-L2 <= 2e-4 (f32 arithmetic over 2^20 steps vs f64).
 """
@@ -65,9 +68,10 @@ def _run(dtype, Lr, seed):
     return y, yr, grads, ref
 
 
-@pytest.mark.parametrize("dtype,Lr,tol_y,tol_g", [(torch.bfloat16, L, 2e-2, 3e-2), (torch.float32, L // 2, 2e-4, 2e-4)])
+@pytest.mark.parametrize("dtype,Lr,tol_y,tol_g", [(torch.bfloat16, L, 5e-3, 5e-3), (torch.float32, L // 2, 2e-4, 2e-4)])
 def test_scan_full_length_fwd_bwd(dtype, Lr, tol_y, tol_g):
     y, yr, grads, ref = _run(dtype, Lr, 0 if dtype == torch.float32 else 2)
+    print(f"{dtype} L={Lr}: y {_rel(y, yr):.2e} " + " ".join(f"d{k} {_rel(grads[k], r):.2e}" for k, r in ref.items()))
     assert _rel(y, yr) < tol_y, f"y rel {_rel(y, yr):.3e}"
     assert _rel(y[-4096:], yr[-4096:]) < tol_y, "y over the last 4096 tokens (after ~L steps of carries)"
     for name, r in ref.items():
