@@ -1787,6 +1787,17 @@ def gemm_bt_supported(x2: torch.Tensor, N: int, K: int) -> bool:
             and bool(_lib.load().lci_gemm_bt_supported(N, K)))
 
 
+GEMM_BT_MIN_TILES = 256   # one 256 x 384 output tile per CU at least
+
+
+def gemm_bt_preferred(M: int, N: int) -> bool:
+    """The product routing: lci_gemm_bt when its persistent grid has a tile for every CU. Below that (the Swin
+    stage-3 / 4 projections: 4096 / 512 tokens, 16-48 tiles) its one-tile-per-CU walk leaves most of the chip idle
+    and hipBLASLt's smaller / split-K tiles win (M = 4096 fc2: 0.056 vs 0.020 ms; C3 step 57.0 vs 54.2 ms with every
+    supported shape on lci_gemm_bt; profiles/r05_gemm_ab.txt)."""
+    return -(-M // 256) * (N // 384) >= GEMM_BT_MIN_TILES
+
+
 def gemm_bt(x2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
     """y (M, N) bf16 = x2 (M, K) . w^T + bias on csrc/gemm.hip (w (N, K) bf16, made contiguous; bias bf16 or None)."""
     M, K = x2.shape
@@ -1818,7 +1829,7 @@ class _Linear(torch.autograd.Function):
             xc, wc, bc = x, weight, bias
         N, K = wc.shape
         x2 = xc.reshape(-1, K) if xc.dim() != 2 else xc
-        if HIP_GEMM and x2.dim() == 2 and gemm_bt_supported(x2, N, K):
+        if HIP_GEMM and x2.dim() == 2 and gemm_bt_preferred(x2.shape[0], N) and gemm_bt_supported(x2, N, K):
             y = gemm_bt(x2, wc, bc).view(*xc.shape[:-1], N)
         else:
             with torch.autocast("cuda", enabled=False):
@@ -1836,7 +1847,7 @@ class _Linear(torch.autograd.Function):
             dy2 = dy2.contiguous()
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            if HIP_GEMM and dy2.dtype == wc.dtype and gemm_bt_supported(dy2, K, N):
+            if HIP_GEMM and dy2.dtype == wc.dtype and gemm_bt_preferred(dy2.shape[0], K) and gemm_bt_supported(dy2, K, N):
                 dx = gemm_bt(dy2, wc.t()).view(*dy.shape[:-1], K)   # dX = dY . W = dY . (W^T)^T
             else:
                 dx = (dy2 @ wc).view(*dy.shape[:-1], K)

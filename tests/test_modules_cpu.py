@@ -217,3 +217,11 @@ def test_head_padding_is_exact():
     (gr,) = torch.autograd.grad(ref, qkv, g)
     (gp,) = torch.autograd.grad(op, qkv, g)
     assert torch.allclose(gp, gr, rtol=0, atol=1e-12)
+
+
+def test_gemm_bt_routing():
+    """lci_gemm_bt is preferred only when its persistent grid has a 256 x 384 tile per CU (kernels.gemm_bt_preferred)."""
+    from long_context_biomedical_imaging_amd import kernels
+    assert kernels.gemm_bt_preferred(131072, 384) and kernels.gemm_bt_preferred(262144, 384)
+    assert kernels.gemm_bt_preferred(32768, 768)                    # 128 x 2 tiles
+    assert not kernels.gemm_bt_preferred(4096, 1536) and not kernels.gemm_bt_preferred(512, 3072)

@@ -273,6 +273,24 @@ def bench_gemm():
             torch.cuda.empty_cache()
 
 
+def bench_gemm_swin():
+    """lci_gemm_bt vs torch at the Swin-tiny projection shapes of C3 (128^3 p2, B = 1: 64^3 / 32^3 / 16^3 / 8^3 tokens;
+    widths 96 / 192 / 384 / 768) that the HIP GEMM takes (N % 384 == 0), forward and data gradient."""
+    from long_context_biomedical_imaging_amd import trainer
+    trainer.use_tuned_gemms()
+    for M, K, N, nm in ((262144, 96, 384, "s1 fc1"), (262144, 96, 384, "s1 fc2 dX"), (32768, 192, 768, "s2 fc1"),
+                        (32768, 192, 384, "s2 qkv dX? (192->576 no) fc2 dX"), (4096, 384, 1152, "s3 qkv"),
+                        (4096, 384, 1536, "s3 fc1"), (4096, 1536, 384, "s3 fc2"), (512, 768, 3072 - 3072 % 384, "s4 fc1"),
+                        (131072, 96, 384, "K96 M131072"), (131072, 192, 384, "K192"), (131072, 288, 384, "K288")):
+        x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+        w = (torch.randn(N, K, device="cuda") * K ** -0.5).to(torch.bfloat16)
+        b = torch.randn(N, device="cuda").to(torch.bfloat16)
+        f = 2.0 * M * N * K
+        emit(f"gemm_bt {nm}", timeit(lambda: kernels.gemm_bt(x, w, b), iters=20), f, "TFLOP/s", f"M{M} K{K} N{N} bf16")
+        emit(f"torch linear {nm}", timeit(lambda: torch.nn.functional.linear(x, w, b), iters=20), f, "TFLOP/s",
+             f"M{M} K{K} N{N} bf16 (hipBLASLt)")
+
+
 def main():
     which = sys.argv[1:] or ["attention", "window", "scan", "fftconv", "patch", "linear", "mlp"]
     if "attention" in which:
@@ -298,6 +316,8 @@ def main():
         bench_mlp()
     if "gemm" in which:
         bench_gemm()
+    if "gemm_swin" in which:
+        bench_gemm_swin()
 
 
 if __name__ == "__main__":
