@@ -76,6 +76,21 @@ __device__ __forceinline__ u32x4 bload16(rsrc_t r, int voff, int soff) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
 }
 
+// LDS-DMA of one 1-KB unit (buffer_load_dwordx4 ... lds): lane l's 16 bytes at (voff + soff) of resource r land at
+// LDS byte lds + 16 l (m0 holds the wave-uniform LDS base; saved and restored around the load). Range-checked like
+// bload16: out-of-range lanes write zeros.
+__device__ __forceinline__ void dma16_lds(rsrc_t r, int voff, int soff, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(r), "s"(lds), "s"(soff) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {   // s_waitcnt vmcnt(N), lgkmcnt / expcnt untouched (gfx9 encoding)
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 // Combine lane l with lane l^32 (the two halves of a 32x32 MFMA column): one v_permlane32_swap, no LDS.
 __device__ __forceinline__ float wave_max_xor32(float v) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);

@@ -13,27 +13,9 @@
 // fragments, and issues 2*NT v_mfma_f32_32x32x16_bf16. With W as the A operand, a lane's accumulators hold 4
 // consecutive output channels per register quad, so the bf16 results go out as 8-byte stores.
 // Neighbour reuse (27 taps read the same voxels) is served by L1/L2: the volume is swept in voxel order.
-#include <stdlib.h>
-
 #include <algorithm>
 
 #include "common.hpp"
-
-#ifndef LCI_CONV_MV_WIDE
-#define LCI_CONV_MV_WIDE 4   // 32-voxel blocks per wave for NT >= 3 (A/B: tools/conv_variants.sh)
-#endif
-
-// scheduling-strategy hooks for A/B runs (tools/conv_variants.sh): iglp_opt(N) on the fwd / wgrad main loops
-#ifdef LCI_CONV_IGLP
-#define LCI_CONV_SCHED() __builtin_amdgcn_iglp_opt(LCI_CONV_IGLP)
-#else
-#define LCI_CONV_SCHED()
-#endif
-#ifdef LCI_WGRAD_IGLP
-#define LCI_WGRAD_SCHED() __builtin_amdgcn_iglp_opt(LCI_WGRAD_IGLP)
-#else
-#define LCI_WGRAD_SCHED()
-#endif
 
 namespace lci {
 
@@ -162,127 +144,17 @@ __global__ __launch_bounds__(256) void conv3_fwd_kernel(ConvArgs a) {
   }
 }
 
-// LDS-staged variant (Cin % 32 == 0): a workgroup owns 4*32*MV consecutive voxels. For each (dz, dy) tap
-// group and 32-channel chunk it stages the contiguous source rows [v0 + off(dz,dy) - 1, ... + 4*32*MV + 1) of x
-// (so the three dx taps read the same LDS rows at offsets 0, 1, 2) and the three taps' weight slabs, with
-// coalesced 16-B loads; fragments then come from LDS (80-B rows). Replaces 3 global fragment loads per voxel
-// block and tap by one staged row set, and shares the weight fragments across the 4 waves.
-constexpr int CLD = 40;   // LDS row stride (elements): 32 channels + 8 pad = 80 B
 // v2 kernel rows: 64 B (no pad) with the 16-byte chunk XORed by (row >> 2) & 3 -- conflict-free for the MFMA fragment
 // reads (b128, lane = row, chunk = 2 ks + h) AND for the 16-byte staging writes, which the 80-B rows left at 8 extra
 // LDS cycles per write (exhaustive bank check, tools/lds_swizzle_check.py patterns)
 constexpr int CLD2 = 32;
 __device__ __forceinline__ int cpos2(int row, int chunk) { return row * CLD2 + ((chunk ^ ((row >> 2) & 3)) << 3); }
 
-template <int NT, int MV>
-__global__ __launch_bounds__(256) void conv3_fwd_lds_kernel(ConvArgs a) {
-  constexpr int WV = 4 * 32 * MV;                 // voxels per workgroup
-  constexpr int XR = WV + 2;                      // staged rows (dx halo)
-  __shared__ __attribute__((aligned(16))) bf16 sX[XR * CLD];
-  __shared__ __attribute__((aligned(16))) bf16 sW[3 * 32 * NT * CLD];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
-  const int r = lane & 31, h = lane >> 5;
-  long long vblk;
-  int ntl;
-  if (!conv_work(a, vblk, ntl)) return;   // 1-D grid padding (uniform per workgroup, before any barrier)
-  const long long vg0 = vblk * WV;
-  const int n0 = ntl * 32 * NT;
-  const int T = a.KD * 9;
-  const int HW = a.H * a.W;
-  int zc[MV], yc[MV], xc[MV];
-  bool inb[MV];
-#pragma unroll
-  for (int m = 0; m < MV; ++m) {
-    const long long v = vg0 + wave * 32 * MV + 32 * m + r;
-    inb[m] = v < a.V;
-    const long long vv = inb[m] ? v : 0;
-    const long long s = vv / ((long long)a.D * HW);
-    int rem = (int)(vv - s * (long long)a.D * HW);
-    zc[m] = rem / HW; rem -= zc[m] * HW;
-    yc[m] = rem / a.W; xc[m] = rem - yc[m] * a.W;
-  }
-  f32x16 acc[MV][NT];
-#pragma unroll
-  for (int m = 0; m < MV; ++m)
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[m][t][i] = 0.f;
-
-  const int ngroups = a.KD * 3;
-  for (int grp = 0; grp < ngroups; ++grp) {
-    const int dz = (a.KD == 3 ? grp / 3 : 1) - 1, dy = grp % 3 - 1;
-    const long long src0 = vg0 + (long long)dz * HW + (long long)dy * a.W - 1;   // source row of LDS row 0
-    bool okzy[MV];
-#pragma unroll
-    for (int m = 0; m < MV; ++m)
-      okzy[m] = inb[m] && (unsigned)(zc[m] + dz) < (unsigned)a.D && (unsigned)(yc[m] + dy) < (unsigned)a.H;
-    for (int c0 = 0; c0 < a.Cin; c0 += 32) {
-      __syncthreads();
-      for (int q = tid; q < XR * 4; q += 256) {
-        const int row = q >> 2, ch = q & 3;
-        const long long u = src0 + row;
-        u32x4 val = {0u, 0u, 0u, 0u};
-        if (u >= 0 && u < a.V) val = *(const u32x4*)(a.x + u * a.Cin + c0 + 8 * ch);
-        *(u32x4*)(sX + row * CLD + 8 * ch) = val;
-      }
-      for (int q = tid; q < 3 * 32 * NT * 4; q += 256) {
-        const int row = q >> 2, ch = q & 3;                 // row = dx * 32NT + n
-        const int dxi = row / (32 * NT), n = row - dxi * 32 * NT;
-        const int tap = grp * 3 + dxi;
-        *(u32x4*)(sW + row * CLD + 8 * ch) =
-            *(const u32x4*)(a.w + ((long long)(n0 + n) * T + tap) * a.Cin + c0 + 8 * ch);
-      }
-      __syncthreads();
-      LCI_CONV_SCHED();
-#pragma unroll
-      for (int dxi = 0; dxi < 3; ++dxi) {
-        bool ok[MV];
-#pragma unroll
-        for (int m = 0; m < MV; ++m) ok[m] = okzy[m] && (unsigned)(xc[m] + dxi - 1) < (unsigned)a.W;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          bf16x8 wa[NT], xb[MV];
-#pragma unroll
-          for (int t = 0; t < NT; ++t)
-            wa[t] = *(const bf16x8*)(sW + (dxi * 32 * NT + 32 * t + r) * CLD + 16 * ks + 8 * h);
-#pragma unroll
-          for (int m = 0; m < MV; ++m) {
-            xb[m] = *(const bf16x8*)(sX + (wave * 32 * MV + 32 * m + r + dxi) * CLD + 16 * ks + 8 * h);
-            if (!ok[m]) xb[m] = zero8();
-          }
-#pragma unroll
-          for (int t = 0; t < NT; ++t)
-#pragma unroll
-            for (int m = 0; m < MV; ++m) acc[m][t] = mfma32(wa[t], xb[m], acc[m][t]);
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int m = 0; m < MV; ++m) {
-    if (!inb[m]) continue;
-    const long long v = vg0 + wave * 32 * MV + 32 * m + r;
-    bf16* yp = a.y + v * a.Cout + n0 + 4 * h;
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        bf16x4 o;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = to_bf16(acc[m][t][4 * q + j]);
-        *(bf16x4*)(yp + 32 * t + 8 * q) = o;
-      }
-  }
-}
-
-// LDS-staged forward v2 (Cin % 32 == 0): 8 waves x 64 voxels = 512 voxels x 32*NT output channels per workgroup
-// (the staged weight slab is shared by twice the voxels of v1), and the staging is double-buffered: the next
-// (tap group, 32-channel chunk) slab is loaded into registers while this one's 48 MFMAs per wave run, then written
-// to the other LDS buffer -- one barrier per slab instead of two around an exposed global-load wait.
-// PF2 = true: the slab loads are issued two slabs ahead into alternating register sets (A / B, the loop unrolled by
-// two), so each load has two slabs of MFMAs (~6k cycles per SIMD) to land before its LDS store instead of one.
-template <int NT, bool SPLIT, bool PF2 = false>
+// LDS-staged forward v2 (Cin % 32 == 0; run at Cout = 32, the DMA kernel below elsewhere): 8 waves x 64 voxels = 512
+// voxels x 32*NT output channels per workgroup, and the staging is double-buffered: the next (tap group, 32-channel
+// chunk) slab is loaded into registers while this one's MFMAs run, then written to the other LDS buffer -- one
+// barrier per slab.
+template <int NT>
 __global__ __launch_bounds__(512) void conv3_fwd_lds2_kernel(ConvArgs a) {
   constexpr int ML = 2, NWV = 8;
   constexpr int WV = NWV * 32 * ML;            // 512 voxels
@@ -293,8 +165,8 @@ __global__ __launch_bounds__(512) void conv3_fwd_lds2_kernel(ConvArgs a) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
   const int r = lane & 31, h = lane >> 5;
   long long vblk;
-  int ntl, split = 0;
-  if (!conv_work(a, vblk, ntl, SPLIT ? &split : nullptr)) return;   // grid padding (uniform, before any barrier)
+  int ntl;
+  if (!conv_work(a, vblk, ntl)) return;   // grid padding (uniform, before any barrier)
   const long long vg0 = vblk * WV;
   const int n0 = ntl * 32 * NT;
   const int T = a.KD * 9;
@@ -321,11 +193,8 @@ __global__ __launch_bounds__(512) void conv3_fwd_lds2_kernel(ConvArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[m][t][i] = 0.f;
 
-  const int nchunk = a.Cin / 32, nslab_all = a.KD * 3 * nchunk;
-  // this workgroup's slab range (split-K: contiguous ranges of the (tap group, channel chunk) slabs)
-  const int sl0 = SPLIT ? (int)((long long)nslab_all * split / a.nsplit) : 0;
-  const int sl1 = SPLIT ? (int)((long long)nslab_all * (split + 1) / a.nsplit) : nslab_all;
-  u32x4 vxA[NXS], vwA[NWS], vxB[NXS], vwB[NWS];
+  const int nchunk = a.Cin / 32, sl0 = 0, sl1 = a.KD * 3 * nchunk;
+  u32x4 vxA[NXS], vwA[NWS];
   // x rows through a buffer resource based at the slab's first in-range row (wave-uniform 64-bit arithmetic on the
   // scalar unit): per-lane offsets are 32-bit, rows before the volume give a negative offset and rows past it one
   // beyond num_records, both of which the range check reads as zero (no 64-bit address VALU, no branch per load)
@@ -372,7 +241,6 @@ __global__ __launch_bounds__(512) void conv3_fwd_lds2_kernel(ConvArgs a) {
     }
   };
   auto compute = [&](int sl, int buf) __attribute__((always_inline)) {
-    LCI_CONV_SCHED();
     const int grp = sl / nchunk;
     const int dz = (a.KD == 3 ? grp / 3 : 1) - 1, dy = grp % 3 - 1;
     bool okzy[ML];
@@ -407,32 +275,157 @@ __global__ __launch_bounds__(512) void conv3_fwd_lds2_kernel(ConvArgs a) {
   load(sl0, vxA, vwA);
   store(0, vxA, vwA);
   int buf = 0;
-  if constexpr (PF2) {
-    if (sl0 + 1 < sl1) load(sl0 + 1, vxA, vwA);
+  __syncthreads();
+  for (int sl = sl0; sl < sl1; ++sl) {
+    const bool more = sl + 1 < sl1;
+    if (more) load(sl + 1, vxA, vwA);
+    compute(sl, buf);
+    if (more) store(buf ^ 1, vxA, vwA);
     __syncthreads();
-    for (int sl = sl0; sl < sl1; sl += 2) {   // entry: set A holds slab sl + 1 (in flight)
-      if (sl + 2 < sl1) load(sl + 2, vxB, vwB);
-      compute(sl, buf);
-      if (sl + 1 < sl1) store(buf ^ 1, vxA, vwA);
-      __syncthreads();
-      buf ^= 1;
-      if (sl + 1 >= sl1) break;               // uniform over the workgroup
-      if (sl + 3 < sl1) load(sl + 3, vxA, vwA);
-      compute(sl + 1, buf);
-      if (sl + 2 < sl1) store(buf ^ 1, vxB, vwB);
-      __syncthreads();
-      buf ^= 1;
+    buf ^= 1;
+  }
+#pragma unroll
+  for (int m = 0; m < ML; ++m) {
+    if (!inb[m]) continue;
+    const long long v = vg0 + wave * 32 * ML + 32 * m + r;
+    bf16* yp = a.y + v * a.Cout + n0 + 4 * h;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        bf16x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = to_bf16(acc[m][t][4 * q + j]);
+        *(bf16x4*)(yp + 32 * t + 8 * q) = o;
+      }
+  }
+}
+
+// LDS-DMA staged forward v3 (Cin % 32 == 0; 512 voxels x 32 NT output channels per workgroup, as v2): the (tap
+// group, 32-channel chunk) slabs arrive by LDS-DMA (1-KB units of 16 rows x 64 B, the rows' 16-B chunks swizzled by
+// (row >> 2) & 3 through the per-lane source offset) into two LDS slots, slab s + 1 issued right after the barrier
+// that frees its slot and landing during slab s's MFMAs -- no staging registers (v2 held one or two slabs in VGPRs
+// and stored them itself). The freed registers hold a second fragment set: the six (dx tap, k-substep) groups of a
+// slab read group g + 1's fragments while group g's MFMAs run.
+template <int NT, bool SPLIT>
+__global__ __launch_bounds__(512) void conv3_fwd_dma_kernel(ConvArgs a) {
+  constexpr int ML = 2, NWV = 8;
+  constexpr int WV = NWV * 32 * ML;            // 512 voxels
+  constexpr int XU = (WV + 2 + 15) / 16;       // X units (dx halo rows included): 33
+  constexpr int WU = 3 * 32 * NT / 16;         // weight units: 3 taps x 32 NT rows
+  constexpr int U = XU + WU, UPW = (U + NWV - 1) / NWV;
+  constexpr int XB = XU * 16 * 64, SLOT = XB + WU * 16 * 64;   // bytes
+  extern __shared__ __attribute__((aligned(16))) char smem3[];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  long long vblk;
+  int ntl, split = 0;
+  if (!conv_work(a, vblk, ntl, SPLIT ? &split : nullptr)) return;   // grid padding (uniform, before any barrier)
+  const long long vg0 = vblk * WV;
+  const int n0 = ntl * 32 * NT;
+  const int T = a.KD * 9;
+  const int HW = a.H * a.W;
+  const bool live = vg0 + wave * 32 * ML < a.V;
+  int zc[ML], yc[ML], xc[ML];
+  bool inb[ML];
+#pragma unroll
+  for (int m = 0; m < ML; ++m) {
+    const long long v = vg0 + wave * 32 * ML + 32 * m + r;
+    inb[m] = v < a.V;
+    const long long vv = inb[m] ? v : 0;
+    const long long s = vv / ((long long)a.D * HW);
+    int rem = (int)(vv - s * (long long)a.D * HW);
+    zc[m] = rem / HW; rem -= zc[m] * HW;
+    yc[m] = rem / a.W; xc[m] = rem - yc[m] * a.W;
+  }
+  f32x16 acc[ML][NT];
+#pragma unroll
+  for (int m = 0; m < ML; ++m)
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[m][t][i] = 0.f;
+
+  const int nchunk = a.Cin / 32, nslab_all = a.KD * 3 * nchunk;
+  const int sl0 = SPLIT ? (int)((long long)nslab_all * split / a.nsplit) : 0;
+  const int sl1 = SPLIT ? (int)((long long)nslab_all * (split + 1) / a.nsplit) : nslab_all;
+  const int rowb = a.Cin * 2;
+  const unsigned lds0 = (unsigned)(uintptr_t)(LCI_LDS char*)smem3;
+  const rsrc_t rw = make_rsrc(a.w, (uint32_t)((long long)a.Cout * T * rowb));
+  // DMA lane mapping inside a unit: row (lane >> 2) of 16, physical chunk lane & 3 <- logical (lane & 3) ^ row bits 2-3
+  int lx, lw;
+  {
+    int l = lane;
+    asm volatile("" : "+v"(l));   // opaque: the two lane offsets stay two registers
+    const int drow = l >> 2, dch = (l & 3) ^ ((l >> 4) & 3);
+    lx = drow * rowb + 16 * dch;
+    lw = drow * T * rowb + 16 * dch;
+  }
+  // slab sl into slot p: X rows [src0, src0 + 16 XU) of channels [c0, c0 + 32) (a resource based at the first
+  // in-volume row: rows before it give negative offsets, rows past V offsets beyond num_records -- both read zeros),
+  // then the three dx taps' weight rows (n0 + n, tap 3 grp + dx) of the same channels
+  auto issue = [&](int sl, int p) __attribute__((always_inline)) {
+    const int grp = sl / nchunk, c0 = (sl - grp * nchunk) * 32;
+    const int dz = (a.KD == 3 ? grp / 3 : 1) - 1, dy = grp % 3 - 1;
+    const long long src0 = vg0 + (long long)dz * HW + (long long)dy * a.W - 1;
+    const long long b0 = src0 < 0 ? 0 : src0;
+    const long long left = (a.V - b0) * rowb;
+    const rsrc_t rx = make_rsrc(a.x + b0 * a.Cin + c0, left <= 0 ? 0u : (left > 0x7fffffffLL ? 0x7fffffffu : (uint32_t)left));
+    const int sh = (int)(src0 - b0) * rowb;   // <= 0
+    const int wg = (grp * 3 * a.Cin + c0) * 2;
+    const unsigned sb = lds0 + (unsigned)(p * SLOT);
+#pragma unroll
+    for (int i = 0; i < UPW; ++i) {
+      const int q = wave + NWV * i;            // wave-uniform
+      if (q < XU) {
+        dma16_lds(rx, lx + 16 * q * rowb + sh, 0, sb + 1024 * q);
+      } else if (q < U) {
+        const int q2 = q - XU, dxi = q2 / (2 * NT), nb = 16 * (q2 - dxi * 2 * NT);
+        dma16_lds(rw, lw + ((n0 + nb) * T + dxi) * rowb + wg, 0, sb + XB + 1024 * q2);
+      }
     }
-  } else {
-    __syncthreads();
-    for (int sl = sl0; sl < sl1; ++sl) {
-      const bool more = sl + 1 < sl1;
-      if (more) load(sl + 1, vxA, vwA);
-      compute(sl, buf);
-      if (more) store(buf ^ 1, vxA, vwA);
-      __syncthreads();
-      buf ^= 1;
+  };
+  auto compute = [&](int sl, int p) __attribute__((always_inline)) {
+    const int grp = sl / nchunk;
+    const int dz = (a.KD == 3 ? grp / 3 : 1) - 1, dy = grp % 3 - 1;
+    bool okzy[ML];
+#pragma unroll
+    for (int m = 0; m < ML; ++m)
+      okzy[m] = inb[m] && (unsigned)(zc[m] + dz) < (unsigned)a.D && (unsigned)(yc[m] + dy) < (unsigned)a.H;
+    const bf16* sX = (const bf16*)(smem3 + p * SLOT);
+    const bf16* sW = (const bf16*)(smem3 + p * SLOT + XB);
+    bf16x8 wa[2][NT], xb[2][ML];
+    auto rd = [&](int g, int s) __attribute__((always_inline)) {
+      const int dxi = g >> 1, ks = g & 1;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) wa[s][t] = *(const bf16x8*)(sW + cpos2(dxi * 32 * NT + 32 * t + r, 2 * ks + h));
+#pragma unroll
+      for (int m = 0; m < ML; ++m) {
+        xb[s][m] = *(const bf16x8*)(sX + cpos2(wave * 32 * ML + 32 * m + r + dxi, 2 * ks + h));
+        if (!(okzy[m] && (unsigned)(xc[m] + dxi - 1) < (unsigned)a.W)) xb[s][m] = zero8();
+      }
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int g = 0; g < 6; ++g) {
+      if (g + 1 < 6) rd(g + 1, (g + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int m = 0; m < ML; ++m) acc[m][t] = mfma32(wa[g & 1][t], xb[g & 1][m], acc[m][t]);
+      __builtin_amdgcn_sched_barrier(0);
     }
+  };
+  issue(sl0, 0);
+  int p = 0;
+  for (int sl = sl0; sl < sl1; ++sl) {
+    wait_vmcnt<0>();                          // this wave's units of slab sl landed
+    __builtin_amdgcn_s_waitcnt(0xC07F);       // lgkmcnt(0): this wave's reads of the other slot are done
+    __builtin_amdgcn_s_barrier();             // every wave's units landed; the other slot is free
+    if (sl + 1 < sl1) issue(sl + 1, p ^ 1);
+    if (live) compute(sl, p);
+    p ^= 1;
   }
   if (SPLIT) {   // f32 partial of this slab range: 16-B stores of 4 consecutive output channels
 #pragma unroll
@@ -778,7 +771,6 @@ __global__ __launch_bounds__(256) void conv3_wgrad4_kernel(WgradArgs a) {
   for (long long g0 = gs; g0 < ge; g0 += WG_ROWS) {
     const bool more = g0 + WG_ROWS < ge;
     if (more) load(g0 + WG_ROWS);
-    LCI_WGRAD_SCHED();
     const bf16* tdy = sdy[buf];
     const bf16* tx = sx[buf];
 #pragma unroll
@@ -923,7 +915,6 @@ __global__ __launch_bounds__(64 * WN * WC) void conv3_wgrad5_kernel(WgradArgs a)
   for (long long g0 = gs; g0 < ge; g0 += WG_ROWS) {
     const bool more = g0 + WG_ROWS < ge;
     if (more) load(g0 + WG_ROWS);
-    LCI_WGRAD_SCHED();
     const bf16* tdy0 = wsm + buf * BUF + (MB * wn) * DYBLK;
     const bf16* tx = wsm + buf * BUF + NB_DY * DYBLK + wc * XBLK;
 #pragma unroll
@@ -995,61 +986,45 @@ static void wgrad5_tile(int Cin, int Cout, int& mb, int& wn, int& wc) {
   if (wc == 0) mb = wn = 0;
 }
 
-static bool lci_conv_lds() {   // LCI_CONV_LDS=0: the direct-load kernel (A/B)
-  static const bool on = !getenv("LCI_CONV_LDS") || atoi(getenv("LCI_CONV_LDS")) != 0;
-  return on;
-}
-
 template <int NT>
 static int launch(const ConvArgs& a, hipStream_t st) {
-  constexpr int MV = NT <= 2 ? 4 : LCI_CONV_MV_WIDE;   // narrow outputs: more voxels per wave
-  static const int v2_env = getenv("LCI_CONV_V2") ? atoi(getenv("LCI_CONV_V2")) : 1;
-  if (a.Cin % 32 == 0 && lci_conv_lds() && v2_env) {
-    static const int order_env = getenv("LCI_CONV_ORDER") ? atoi(getenv("LCI_CONV_ORDER")) : -1;
+  if (a.Cin % 32 == 0) {
     ConvArgs b = a;
     b.nvb = (int)((a.V + 511) / 512);
     b.ntile = a.Cout / (32 * NT);
-    b.order = order_env >= 0 ? order_env : (a.Cout >= 96 ? 1 : 0);
+    // measured (tools/conv_bench.py, C3/C5 shapes): order 1 gains up to 12 % from Cout >= 96 (512->256 at 256^3:
+    // 164 -> 146 ms) and loses up to 15 % on the 1-2 tile Cout = 32 / 64 convs, which keep order 0
+    b.order = a.Cout >= 96 ? 1 : 0;
     const long long nb = (long long)b.nvb * b.ntile;
-    const size_t sh = (size_t)2 * (514 * CLD2 + 3 * 32 * NT * CLD2) * sizeof(bf16);
+    constexpr int XU = (512 + 2 + 15) / 16, WU = 3 * 32 * NT / 16;
+    const size_t shd = (size_t)2 * (XU + WU) * 1024;
     if (a.nsplit > 1) {
       LCI_CHECK(a.part != nullptr, "conv3: split-K needs the partial workspace");
       LCI_CHECK(nb * a.nsplit < (1LL << 31), "conv3: too many workgroups");
-      (void)hipFuncSetAttribute((const void*)conv3_fwd_lds2_kernel<NT, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      hipLaunchKernelGGL((conv3_fwd_lds2_kernel<NT, true>), dim3((unsigned)(nb * a.nsplit)), dim3(512), sh, st, b);
+      (void)hipFuncSetAttribute((const void*)conv3_fwd_dma_kernel<NT, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024);
+      hipLaunchKernelGGL((conv3_fwd_dma_kernel<NT, true>), dim3((unsigned)(nb * a.nsplit)), dim3(512), shd, st, b);
       LCI_LAUNCH_CHECK();
       const long long n8 = a.V * a.Cout / 8;
       hipLaunchKernelGGL(conv3_sum_kernel, dim3((unsigned)std::min<long long>((n8 + 255) / 256, 8192)), dim3(256), 0,
                          st, (const float*)a.part, a.y, n8, a.nsplit);
     } else {
-      // two-slab-ahead prefetch for the wide tiles (NT >= 3: 1-6 % at the C3 / C5 shapes); NT <= 2 keeps one slab
-      // (PF2 there: 15-20 % slower at Cout = 32, profiles/r03_conv_pf2_ab.txt). LCI_CONV_PF2=0/1 forces it (A/B).
-      static const int pf2_env = getenv("LCI_CONV_PF2") ? atoi(getenv("LCI_CONV_PF2")) : -1;
-      dim3 grid((unsigned)(b.order ? (nb + 7) / 8 * 8 : nb));
-      if (pf2_env > 0 || (pf2_env < 0 && NT >= 3)) {
-        (void)hipFuncSetAttribute((const void*)conv3_fwd_lds2_kernel<NT, false, true>,
+      const dim3 grid((unsigned)(b.order ? (nb + 7) / 8 * 8 : nb));
+      if constexpr (NT >= 2) {
+        // LDS-DMA staging: equal to v2 at the 256- / 512-channel C5 shapes, 2-8 % faster at 64 / 96 channels
+        // (profiles/r05_conv_dma_ab.txt)
+        (void)hipFuncSetAttribute((const void*)conv3_fwd_dma_kernel<NT, false>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        hipLaunchKernelGGL((conv3_fwd_lds2_kernel<NT, false, true>), grid, dim3(512), sh, st, b);
-      } else {
-        (void)hipFuncSetAttribute((const void*)conv3_fwd_lds2_kernel<NT, false>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        hipLaunchKernelGGL((conv3_fwd_lds2_kernel<NT, false>), grid, dim3(512), sh, st, b);
+        hipLaunchKernelGGL((conv3_fwd_dma_kernel<NT, false>), grid, dim3(512), shd, st, b);
+      } else {   // Cout = 32: the register-staged v2 kernel (2-5 % ahead of the DMA one there)
+        const size_t sh = (size_t)2 * (514 * CLD2 + 3 * 32 * NT * CLD2) * sizeof(bf16);
+        (void)hipFuncSetAttribute((const void*)conv3_fwd_lds2_kernel<NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        hipLaunchKernelGGL((conv3_fwd_lds2_kernel<NT>), grid, dim3(512), sh, st, b);
       }
     }
-  } else if (a.Cin % 32 == 0 && lci_conv_lds()) {
-    constexpr int ML = NT == 4 ? 2 : 4;
-    // measured (tools/conv_bench.py, C3/C5 shapes): order 1 gains up to 12 % from Cout >= 96 (512->256 at 256^3:
-    // 164 -> 146 ms) and loses up to 15 % on the 1-2 tile Cout = 32 / 64 convs, which keep order 0
-    static const int order_env = getenv("LCI_CONV_ORDER") ? atoi(getenv("LCI_CONV_ORDER")) : -1;
-    ConvArgs b = a;
-    b.nvb = (int)((a.V + 128 * ML - 1) / (128 * ML));
-    b.ntile = a.Cout / (32 * NT);
-    b.order = order_env >= 0 ? order_env : (a.Cout >= 96 ? 1 : 0);
-    const long long nb = (long long)b.nvb * b.ntile;
-    dim3 grid((unsigned)(b.order ? (nb + 7) / 8 * 8 : nb));
-    hipLaunchKernelGGL((conv3_fwd_lds_kernel<NT, ML>), grid, dim3(256), 0, st, b);
   } else if (a.Cin % 16 == 0) {
+    constexpr int MV = 4;
     dim3 grid((unsigned)((a.V + 128 * MV - 1) / (128 * MV)), a.Cout / (32 * NT));
     hipLaunchKernelGGL((conv3_fwd_kernel<NT, MV>), grid, dim3(256), 0, st, a);
   } else {
@@ -1103,7 +1078,6 @@ extern "C" int lci_conv3_fwd(const void* x, const void* w, void* y, int B, int D
 // partials a second pass sums: ~512 workgroups, at most 100 MB of partials, at least 2 slabs per range.
 extern "C" int lci_conv3_fwd_splits(long long V, int Cin, int Cout, int KD) {
   if (V <= 0 || Cin % 32 || Cout % 32 || (KD != 1 && KD != 3)) return 1;
-  if (getenv("LCI_CONV_SPLITK") && atoi(getenv("LCI_CONV_SPLITK")) == 0) return 1;
   const long long nb = (V + 511) / 512 * (Cout / (32 * conv3_nt(Cout)));
   if (nb >= 256) return 1;
   const long long nslab = (long long)KD * 3 * (Cin / 32);
@@ -1175,27 +1149,23 @@ extern "C" int lci_conv3_wgrad(const void* x, const void* dy, float* part, int B
   a.Lv = (a.Lv + WG_ROWS - 1) / WG_ROWS * WG_ROWS;   // splits start on a step boundary
   hipStream_t st = (hipStream_t)stream;
   a.ns = (int)ns;
-  static const int v5_env = getenv("LCI_WGRAD_V5") ? atoi(getenv("LCI_WGRAD_V5")) : 1;
   int mb, wn, wc;
   wgrad5_tile(Cin, Cout, mb, wn, wc);
-  if (v5_env && mb) {
+  if (mb) {
 #define LCI_W5(M, N, C) if (mb == M && wn == N && wc == C) return launch_wgrad5<M, N, C>(a, st);
     LCI_W5(2, 2, 4) LCI_W5(2, 2, 2) LCI_W5(1, 3, 3) LCI_W5(1, 3, 2)
 #undef LCI_W5
   }
   // 32*MT output channels per workgroup: 2 where Cout allows (2 waves per SIMD), else 1. MT = 3 (256 registers, one
-  // wave per SIMD) measured 1.2-1.4x slower than MT = 1 on the Cout = 96 / 192 C3 shapes. LCI_WGRAD3_MT: A/B override
-  static const int mt_env = getenv("LCI_WGRAD3_MT") ? atoi(getenv("LCI_WGRAD3_MT")) : 0;
-  const int mt = (mt_env > 0 && (Cout / 32) % mt_env == 0) ? mt_env : ((Cout / 32) % 2 == 0 ? 2 : 1);
+  // wave per SIMD) measured 1.2-1.4x slower than MT = 1 on the Cout = 96 / 192 C3 shapes
+  const int mt = (Cout / 32) % 2 == 0 ? 2 : 1;
   a.ns = (int)ns;
   const long long nb = (long long)KD * 3 * ns * (Cout / (32 * mt)) * (Cin / 32);
   LCI_CHECK(nb < (1LL << 30), "conv3_wgrad: too many workgroups");
   a.nb = (int)nb;
-  static const int order_env = getenv("LCI_WGRAD_ORDER") ? atoi(getenv("LCI_WGRAD_ORDER")) : 1;
-  a.order = order_env;
+  a.order = 1;
   dim3 grid((unsigned)(a.order ? (nb + 7) / 8 * 8 : nb));
-  if (mt == 3) hipLaunchKernelGGL(conv3_wgrad4_kernel<3>, grid, dim3(256), 0, st, a);
-  else if (mt == 2) hipLaunchKernelGGL(conv3_wgrad4_kernel<2>, grid, dim3(256), 0, st, a);
+  if (mt == 2) hipLaunchKernelGGL(conv3_wgrad4_kernel<2>, grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL(conv3_wgrad4_kernel<1>, grid, dim3(256), 0, st, a);
   LCI_LAUNCH_CHECK();
   return 0;

@@ -51,19 +51,6 @@ struct GemmArgs {
   int G8, dmt, dnt;               // workgroups per XCD; G8 tiles = dmt token tiles + dnt feature tiles
 };
 
-// LDS-DMA of one 1-KB unit: lane l's 16 bytes at (voff + soff) of resource r land at LDS byte lds + 16 l
-__device__ __forceinline__ void gm_dma16(rsrc_t r, int voff, int soff, unsigned lds) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(voff), "s"(r), "s"(lds), "s"(soff) : "memory");
-}
-template <int N>
-__device__ __forceinline__ void gm_vmcnt() {   // s_waitcnt vmcnt(N), lgkmcnt / expcnt untouched (gfx9 encoding)
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
-  __builtin_amdgcn_sched_barrier(0);
-}
-
 template <int TN>
 __global__ __launch_bounds__(GM_WAVES * 64, 1) void gemm_bt_kernel(GemmArgs a) {
   constexpr int WN = 2, WM = 4;
@@ -151,8 +138,8 @@ __global__ __launch_bounds__(GM_WAVES * 64, 1) void gemm_bt_kernel(GemmArgs a) {
   };
   auto piece = [&](const Dma& d, int q) __attribute__((always_inline)) {
     constexpr int QX = UX / GM_WAVES;
-    if (q < QX) gm_dma16(d.rx, d.xo + 16 * GM_WAVES * q * ldx2, d.ko, d.sb + 1024 * (wave + GM_WAVES * q));
-    else gm_dma16(rw, d.wo + 16 * GM_WAVES * (q - QX) * K2, d.ko, d.sb + 1024 * (wave + GM_WAVES * q));
+    if (q < QX) dma16_lds(d.rx, d.xo + 16 * GM_WAVES * q * ldx2, d.ko, d.sb + 1024 * (wave + GM_WAVES * q));
+    else dma16_lds(rw, d.wo + 16 * GM_WAVES * (q - QX) * K2, d.ko, d.sb + 1024 * (wave + GM_WAVES * q));
   };
 
 
@@ -208,9 +195,9 @@ __global__ __launch_bounds__(GM_WAVES * 64, 1) void gemm_bt_kernel(GemmArgs a) {
     ++since_epi;
     // slab s landed: the next slab's UPW units may still be in flight, and, in the two slabs after an epilogue, its
     // 2 NB MB stores too (they were issued between two slabs' units; vmcnt retires in issue order)
-    if (s + 1 >= S) gm_vmcnt<0>();
-    else if (since_epi <= 2) gm_vmcnt<UPW + 2 * NB * MB>();
-    else gm_vmcnt<UPW>();
+    if (s + 1 >= S) wait_vmcnt<0>();
+    else if (since_epi <= 2) wait_vmcnt<UPW + 2 * NB * MB>();
+    else wait_vmcnt<UPW>();
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's reads of the slot being refilled are done
     __builtin_amdgcn_s_barrier();
     const bool iss = s + 2 < S;           // slab s + 2 into slot (s + 2) % 3 = (s - 1) % 3, free after this barrier

@@ -53,13 +53,6 @@ __device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_dst) {
                : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
 }
 
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {   // s_waitcnt vmcnt(N), expcnt / lgkmcnt untouched (gfx9 encoding)
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
-  __builtin_amdgcn_sched_barrier(0);
-}
-
 #ifndef LCI_LW_RSTG
 #define LCI_LW_RSTG 0   // slab staging: 1 = global loads into AGPRs + ds_write_b128 one slab ahead, 0 = LDS-DMA ring
 #endif
