@@ -196,6 +196,24 @@ def profiled_traffic(timer: str, workload: str):
     return int(wl["timers"][timer]["bytes_per_call"]), f"profiles/traffic.json workloads.{workload} ({wl['source']})"
 
 
+def profiled_launch_ms(timer: str, workload: str):
+    """Average launch time of KernelTimer `timer` in `workload`'s committed rocprofv3 kernel trace (the same
+    profiles/traffic.json entry: sum over the timer's kernels of avg_ms x launches / the timer's launches), or None.
+    Reported beside the live HIP-event figure: the two come from different boxes and runs (box-to-box spread)."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        wl = json.load(f).get("workloads", {}).get(workload)
+    if not wl or timer not in wl.get("timers", {}):
+        return None
+    t = wl["timers"][timer]
+    tot = sum(wl["kernels"][k]["avg_ms"] * wl["kernels"][k]["launches"] for k in t.get("kernels", [])
+              if k in wl.get("kernels", {}) and "avg_ms" in wl["kernels"][k])
+    n = t.get("launches") or 0
+    return tot / n if tot > 0 and n > 0 else None
+
+
 def _sync(device):
     if device.type == "cuda":
         torch.cuda.synchronize(device)
@@ -347,6 +365,10 @@ def run_workload(workload, batch, steps, warmup, rank, world, device, kernel_tim
                 "unit": unit, "frac": round(ach / peak, 4),
                 "traffic": traffic, "traffic_source": tsrc,
                 "work_per_launch": work, "avg_launch_ms": round(dd["avg_ms"], 3)}
+        pms = profiled_launch_ms(dom, workload)
+        if pms:   # the committed rocprofv3 trace's figure for the same kernel: the frac spread across boxes / runs
+            roof["profile_avg_launch_ms"] = round(pms, 3)
+            roof["profile_frac"] = round(work / (pms * 1e-3) / (1e12 if unit == "TFLOP/s" else 1e9) / peak, 4)
     return {
         "metric": WORKLOAD_NAMES[workload][0],
         "value": round(tokens / elapsed, 1), "unit": "image-tokens/s", "n_gpus": world, "steps": steps,

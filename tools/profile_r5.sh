@@ -4,7 +4,7 @@
 #   2. C3 (swin_p2_128) eager (LCI_GRAPH=0: rocprofv3 --pmc aborts on graph replays, tools/graph_pmc_repro.py):
 #      FETCH_SIZE / WRITE_SIZE                                                          -> traffic.json swin_p2_128
 #   3. C4 FFT conv calls (tools/fft_traffic.py): FETCH_SIZE / WRITE_SIZE per call      -> traffic.json vit_hyena_p2_1024
-# Usage (GPU box): bash tools/profile_r5.sh <tag> [stages...]  (stages: metric c3 fft; default all)
+# Usage (GPU box): bash tools/profile_r5.sh <tag> [stages...]  (stages: metric c3 c4 c5 fft; default metric c3 fft)
 TAG=$1; shift
 STAGES=${*:-metric c3 fft}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -42,6 +42,16 @@ for st in $STAGES; do
       pmc $OUT/c3/fetch FETCH_SIZE python3 $ROOT/bench.py --workload swin_p2_128 --no-kernel-timer --steps 3 --warmup 1
       pmc $OUT/c3/write WRITE_SIZE python3 $ROOT/bench.py --workload swin_p2_128 --no-kernel-timer --steps 3 --warmup 1
       unset LCI_GRAPH
+      ;;
+    c4|c5)   # vit_hyena_p2_1024 / vit_mamba_p2_256: trace + FETCH / WRITE passes of the workload (eager steps)
+      WL=$([ $st = c4 ] && echo vit_hyena_p2_1024 || echo vit_mamba_p2_256)
+      mkdir -p $OUT/$st
+      timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$st/trace -o run -- \
+        python3 $ROOT/bench.py --workload $WL --steps 3 --warmup 1 > $OUT/${st}_trace.log 2>&1 \
+        || { echo "STOP $st trace"; tail -5 $OUT/${st}_trace.log; exit 1; }
+      echo "$st trace done"
+      pmc $OUT/$st/fetch FETCH_SIZE python3 $ROOT/bench.py --workload $WL --no-kernel-timer --steps 2 --warmup 1
+      pmc $OUT/$st/write WRITE_SIZE python3 $ROOT/bench.py --workload $WL --no-kernel-timer --steps 2 --warmup 1
       ;;
     fft)
       mkdir -p $OUT/fft

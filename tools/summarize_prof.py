@@ -125,7 +125,13 @@ def main():
         doc["note"] = ("per workload: HBM bytes per launch from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of "
                        "that workload (FETCH_SIZE x2, the gfx950 correction; KiB -> bytes); `timers` = per KernelTimer "
                        "name, launch-weighted over the kernels it launches")
-        doc.setdefault("workloads", {})[wl] = {"source": d, "kernels": out, "timers": timers}
+        prev = doc.setdefault("workloads", {}).get(wl, {})
+        # timers this run did not produce (tools/fft_traffic.py's fftconv_fwd / _bwd entries) are kept
+        kept = {k: v for k, v in prev.get("timers", {}).items() if k not in timers}
+        entry = {"source": d, "kernels": out, "timers": {**kept, **timers}}
+        if "fft_source" in prev:
+            entry["fft_source"] = prev["fft_source"]
+        doc["workloads"][wl] = entry
         json.dump(doc, open(path, "w"), indent=1)
     print(f"# rocprofv3 summary: {d}\n")
     print(f"Kernel-trace dispatches counted: the last {100 * (1 - skip_frac):.0f}% of the run "
