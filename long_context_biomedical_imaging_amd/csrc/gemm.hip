@@ -51,7 +51,7 @@ struct GemmArgs {
   int G8, dmt, dnt;               // workgroups per XCD; G8 tiles = dmt token tiles + dnt feature tiles
 };
 
-template <int TN>
+template <int TN, bool HAS_BIAS>
 __global__ __launch_bounds__(GM_WAVES * 64, 1) void gemm_bt_kernel(GemmArgs a) {
   constexpr int WN = 2, WM = 4;
   constexpr int NB = TN / WN / 32, MB = GM_TM / WM / 32;           // 32x32 blocks per wave (features, tokens)
@@ -79,7 +79,7 @@ __global__ __launch_bounds__(GM_WAVES * 64, 1) void gemm_bt_kernel(GemmArgs a) {
   const int nslab = a.K / GM_BK;
   const int S = my_tiles * nslab;
 
-  if (a.bias) {
+  if (HAS_BIAS) {
     for (int i = tid; i < a.N; i += GM_WAVES * 64) sbias[i] = a.bias[i];
   }
   __syncthreads();
@@ -229,17 +229,20 @@ __global__ __launch_bounds__(GM_WAVES * 64, 1) void gemm_bt_kernel(GemmArgs a) {
             for (int p = 0; p < 2; ++p) {
               const int i = 2 * ip + b;
               const int fs = cc.n0() + WF * wn + 32 * i + 16 * p + 4 * eh;   // regs 8p + q / 8p + 4 + q: fs + q / fs + 8 + q
-              float b0[4] = {0.f, 0.f, 0.f, 0.f}, b1[4] = {0.f, 0.f, 0.f, 0.f};
-              if (a.bias) {
+              bf16x4 lo, hi;   // (+ bias: the autocast Linear's f32 sum, rounded once)
+              if constexpr (HAS_BIAS) {
                 const bf16x4 bb0 = *(const bf16x4*)(sbias + fs), bb1 = *(const bf16x4*)(sbias + fs + 8);
 #pragma unroll
-                for (int q = 0; q < 4; ++q) { b0[q] = to_f32(bb0[q]); b1[q] = to_f32(bb1[q]); }
-              }
-              bf16x4 lo, hi;
+                for (int q = 0; q < 4; ++q) {
+                  lo[q] = to_bf16(acc[i][j][8 * p + q] + to_f32(bb0[q]));
+                  hi[q] = to_bf16(acc[i][j][8 * p + 4 + q] + to_f32(bb1[q]));
+                }
+              } else {
 #pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                lo[q] = to_bf16(acc[i][j][8 * p + q] + b0[q]);
-                hi[q] = to_bf16(acc[i][j][8 * p + 4 + q] + b1[q]);
+                for (int q = 0; q < 4; ++q) {
+                  lo[q] = to_bf16(acc[i][j][8 * p + q]);
+                  hi[q] = to_bf16(acc[i][j][8 * p + 4 + q]);
+                }
               }
               // lane h gets features 16p + 8h .. + 7 of block i: 16-B chunk 4b + 2p + h of the row
               const u32x2 ul = __builtin_bit_cast(u32x2, lo), uh = __builtin_bit_cast(u32x2, hi);
@@ -295,8 +298,13 @@ extern "C" int lci_gemm_bt(const void* x, long long ldx, const void* w, const vo
   a.dnt = a.G8 % a.ntn;
   constexpr int TN = 384;
   const size_t sh = (size_t)GM_NSLOT * (GM_TM + TN) * 64 + GM_WAVES * GM_EPI + GM_MAXN * 2;
-  (void)hipFuncSetAttribute((const void*)gemm_bt_kernel<TN>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
-  hipLaunchKernelGGL(gemm_bt_kernel<TN>, dim3((unsigned)grid), dim3(GM_WAVES * 64), sh, (hipStream_t)stream, a);
+  if (bias) {
+    (void)hipFuncSetAttribute((const void*)gemm_bt_kernel<TN, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
+    hipLaunchKernelGGL((gemm_bt_kernel<TN, true>), dim3((unsigned)grid), dim3(GM_WAVES * 64), sh, (hipStream_t)stream, a);
+  } else {
+    (void)hipFuncSetAttribute((const void*)gemm_bt_kernel<TN, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
+    hipLaunchKernelGGL((gemm_bt_kernel<TN, false>), dim3((unsigned)grid), dim3(GM_WAVES * 64), sh, (hipStream_t)stream, a);
+  }
   LCI_LAUNCH_CHECK();
   return 0;
 }
