@@ -583,40 +583,44 @@ __global__ __launch_bounds__(WBWD1_MAXW * 64) void win_attn_bwd1_kernel(WinArgs 
   bf16* scr = (bf16*)(dq_l + a.Npad * DQLD) + wave * 32 * WLD;   // this wave's 32 x 32 transpose tile
   const float c = a.c;
 
-  // Q -> t0, dO -> t1 (padded / cropped queries: dO = 0): Npad * 4 16-byte chunks = exactly 2 per thread,
-  // all four loads in flight before the LDS writes
-  {
-    bf16x8 r0[2], r1[2];
-#pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int idx = it * NT + threadIdx.x, n = idx >> 2, ch = idx & 3;
-      r0[it] = win_load8(a, L.row[n], hh * WHD + ch * 8, n < a.N);
-      r1[it] = win_stage_src1(a, L, n, ch, hh * WHD, true, a.dout, w);
-    }
-#pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int idx = it * NT + threadIdx.x, n = idx >> 2, ch = idx & 3;
-      *(bf16x8*)(L.t0 + n * WLD + ch * 8) = r0[it];
-      *(bf16x8*)(L.t1 + n * WLD + ch * 8) = r1[it];
-    }
-    __syncthreads();
-  }
-  // row constants: lse2 and -delta = -rowsum(dO * O), 4 threads per query row (8 channels each); dQ zeroed
+  // Prologue: every global read of the window issued at once, then consumed -- Q and dO rows (-> t0, t1), the O rows
+  // and lse2 of the row constants, this wave's K / V rows -- so the workgroup pays one memory round trip before its
+  // loop instead of three in sequence. Npad * 4 16-byte chunks = exactly 2 per thread; the row-constant items are the
+  // same (n, ch) chunks, so delta = rowsum(dO * O) uses the dO values in registers.
+  const int kb = wave;
+  const int key = kb * 32 + (lane & 31);
+  const bool kv = key < a.N;
+  const int krow = kv ? L.row[key] : -2;
   const float* lseg = a.lse2 + ((long long)w * a.H + hh) * a.N;
-  for (int it = threadIdx.x; it < a.Npad * 4; it += NT) {   // Npad * 4 is a multiple of 64: whole waves
-    const int n = it >> 2, ch = it & 3;
-    const int row = L.row[n];
-    float dsum = 0.f;
-    if (n < a.N && row != -1) {
-      const bf16x8 ov = *(const bf16x8*)(out_row_ptr(a, a.o, w, n, row) + hh * WHD + ch * 8);
-      const bf16x8 dv8 = *(const bf16x8*)(L.t1 + n * WLD + ch * 8);
+  bf16x8 r0[2], r1[2], ov[2], kr[2], vr[2];
+  float lsv[2];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) dsum = fmaf(to_f32(dv8[j]), to_f32(ov[j]), dsum);
-    }
+  for (int it = 0; it < 2; ++it) {
+    const int idx = it * NT + threadIdx.x, n = idx >> 2, ch = idx & 3;
+    r0[it] = win_load8(a, L.row[n], hh * WHD + ch * 8, n < a.N);
+    r1[it] = win_stage_src1(a, L, n, ch, hh * WHD, true, a.dout, w);
+    const int row = L.row[n];
+    ov[it] = (n < a.N && row != -1) ? *(const bf16x8*)(out_row_ptr(a, a.o, w, n, row) + hh * WHD + ch * 8) : bf16x8{};
+    lsv[it] = (ch == 0 && n < a.N) ? lseg[n] : 0.f;
+  }
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    kr[ks] = win_load8(a, krow, a.C + hh * WHD + ks * 16 + 8 * half, kv);
+    vr[ks] = win_load8(a, krow, 2 * a.C + hh * WHD + ks * 16 + 8 * half, kv);
+  }
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int idx = it * NT + threadIdx.x, n = idx >> 2, ch = idx & 3;
+    *(bf16x8*)(L.t0 + n * WLD + ch * 8) = r0[it];
+    *(bf16x8*)(L.t1 + n * WLD + ch * 8) = r1[it];
+    // row constants: lse2 and -delta = -rowsum(dO * O), 4 threads per query row (8 channels each)
+    float dsum = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dsum = fmaf(to_f32(r1[it][j]), to_f32(ov[it][j]), dsum);
     dsum += __shfl_xor(dsum, 1);
     dsum += __shfl_xor(dsum, 2);
     if (ch == 0) {
-      lse_l[n] = n < a.N ? -lseg[n] : -1.0e30f;   // -lse2 (the S chain's initial accumulator); padded rows: P = 0
+      lse_l[n] = n < a.N ? -lsv[it] : -1.0e30f;   // -lse2 (the S chain's initial accumulator); padded rows: P = 0
       ndl_l[n] = -dsum;
     }
   }
@@ -625,17 +629,12 @@ __global__ __launch_bounds__(WBWD1_MAXW * 64) void win_attn_bwd1_kernel(WinArgs 
   if (threadIdx.x < nkb) cnt[threadIdx.x] = 0;
 
   // this wave's key block: K (prescaled into the exp2 domain) / V as B operands, raw K^T as the dQ A operand
-  const int kb = wave;
-  const int key = kb * 32 + (lane & 31);
-  const bool kv = key < a.N;
-  const int krow = kv ? L.row[key] : -2;
   bf16x8 kf[2], vf[2];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
-    const bf16x8 kr = win_load8(a, krow, a.C + hh * WHD + ks * 16 + 8 * half, kv);
-    *(bf16x8*)(scr + (lane & 31) * WLD + ks * 16 + 8 * half) = kr;
-    kf[ks] = scaled8(kr, c);
-    vf[ks] = win_load8(a, krow, 2 * a.C + hh * WHD + ks * 16 + 8 * half, kv);
+    *(bf16x8*)(scr + (lane & 31) * WLD + ks * 16 + 8 * half) = kr[ks];
+    kf[ks] = scaled8(kr[ks], c);
+    vf[ks] = vr[ks];
   }
   __syncthreads();   // staging, row constants, dQ zero, K scratch
   const bf16x8 kt0 = frag_tr<0>(scr, WLD, 0, 0, lane), kt1 = frag_tr<1>(scr, WLD, 0, 0, lane);
