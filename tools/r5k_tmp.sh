@@ -7,3 +7,4 @@ timeout -k 10 300 python -u tools/kernel_bench.py window > $OUT/kb.jsonl 2> $OUT
 cat $OUT/kb.jsonl | cut -c1-200
 timeout -k 10 600 python -u bench.py --workload swin_p2_128 --steps 10 --warmup 3 > $OUT/c3.json 2> $OUT/c3.err || { echo "STOP c3"; tail -3 $OUT/c3.err; exit 1; }
 python3 -c "import json; d=json.loads(open('$OUT/c3.json').read().strip().splitlines()[-1]); print('C3', d['ms_per_step'], d['roofline']['frac'], {k: v for k, v in d['kernels'].items() if 'window' in k})"
+bash tools/pmc_r5.sh pmc_r5w2 window || exit 1
