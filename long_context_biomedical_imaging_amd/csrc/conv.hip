@@ -314,6 +314,7 @@ __global__ __launch_bounds__(512) void conv3_fwd_dma_kernel(ConvArgs a) {
   constexpr int XU = (WV + 2 + 15) / 16;       // X units (dx halo rows included): 33
   constexpr int WU = 3 * 32 * NT / 16;         // weight units: 3 taps x 32 NT rows
   constexpr int U = XU + WU, UPW = (U + NWV - 1) / NWV;
+  constexpr bool SPREAD = NT >= 4;   // next slab's DMA spread over this slab's MFMA groups (see Dma below)
   constexpr int XB = XU * 16 * 64, SLOT = XB + WU * 16 * 64;   // bytes
   extern __shared__ __attribute__((aligned(16))) char smem3[];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -364,28 +365,37 @@ __global__ __launch_bounds__(512) void conv3_fwd_dma_kernel(ConvArgs a) {
   // slab sl into slot p: X rows [src0, src0 + 16 XU) of channels [c0, c0 + 32) (a resource based at the first
   // in-volume row: rows before it give negative offsets, rows past V offsets beyond num_records -- both read zeros),
   // then the three dx taps' weight rows (n0 + n, tap 3 grp + dx) of the same channels
-  auto issue = [&](int sl, int p) __attribute__((always_inline)) {
+  // slab sl into slot p: issue_begin() sets up the slab (resources, offsets), piece(d, i) issues this wave's unit i
+  // (i < UPW). At NT = 4 the pieces are spread over the six MFMA groups of the slab being computed (an LDS-DMA
+  // instruction holds its wave's issue for tens of cycles); the narrower tiles' slabs are too short for that (the
+  // late pieces land after the slab ends) and issue them all before their MFMAs.
+  struct Dma { rsrc_t rx; int sh, wg; unsigned sb; };
+  auto issue_begin = [&](int sl, int p) __attribute__((always_inline)) {
     const int grp = sl / nchunk, c0 = (sl - grp * nchunk) * 32;
     const int dz = (a.KD == 3 ? grp / 3 : 1) - 1, dy = grp % 3 - 1;
     const long long src0 = vg0 + (long long)dz * HW + (long long)dy * a.W - 1;
     const long long b0 = src0 < 0 ? 0 : src0;
     const long long left = (a.V - b0) * rowb;
-    const rsrc_t rx = make_rsrc(a.x + b0 * a.Cin + c0, left <= 0 ? 0u : (left > 0x7fffffffLL ? 0x7fffffffu : (uint32_t)left));
-    const int sh = (int)(src0 - b0) * rowb;   // <= 0
-    const int wg = (grp * 3 * a.Cin + c0) * 2;
-    const unsigned sb = lds0 + (unsigned)(p * SLOT);
-#pragma unroll
-    for (int i = 0; i < UPW; ++i) {
-      const int q = wave + NWV * i;            // wave-uniform
-      if (q < XU) {
-        dma16_lds(rx, lx + 16 * q * rowb + sh, 0, sb + 1024 * q);
-      } else if (q < U) {
-        const int q2 = q - XU, dxi = q2 / (2 * NT), nb = 16 * (q2 - dxi * 2 * NT);
-        dma16_lds(rw, lw + ((n0 + nb) * T + dxi) * rowb + wg, 0, sb + XB + 1024 * q2);
-      }
+    Dma d{make_rsrc(a.x + b0 * a.Cin + c0, left <= 0 ? 0u : (left > 0x7fffffffLL ? 0x7fffffffu : (uint32_t)left)),
+          (int)(src0 - b0) * rowb,   // <= 0
+          (grp * 3 * a.Cin + c0) * 2, lds0 + (unsigned)(p * SLOT)};
+    return d;
+  };
+  auto piece = [&](const Dma& d, int i) __attribute__((always_inline)) {
+    const int q = wave + NWV * i;            // wave-uniform
+    if (q < XU) {
+      dma16_lds(d.rx, lx + 16 * q * rowb + d.sh, 0, d.sb + 1024 * q);
+    } else if (q < U) {
+      const int q2 = q - XU, dxi = q2 / (2 * NT), nb = 16 * (q2 - dxi * 2 * NT);
+      dma16_lds(rw, lw + ((n0 + nb) * T + dxi) * rowb + d.wg, 0, d.sb + XB + 1024 * q2);
     }
   };
-  auto compute = [&](int sl, int p) __attribute__((always_inline)) {
+  auto issue = [&](int sl, int p) __attribute__((always_inline)) {
+    const Dma d = issue_begin(sl, p);
+#pragma unroll
+    for (int i = 0; i < UPW; ++i) piece(d, i);
+  };
+  auto compute = [&](int sl, int p, bool iss, const Dma& nd) __attribute__((always_inline)) {
     const int grp = sl / nchunk;
     const int dz = (a.KD == 3 ? grp / 3 : 1) - 1, dy = grp % 3 - 1;
     bool okzy[ML];
@@ -415,6 +425,11 @@ __global__ __launch_bounds__(512) void conv3_fwd_dma_kernel(ConvArgs a) {
 #pragma unroll
         for (int m = 0; m < ML; ++m) acc[m][t] = mfma32(wa[g & 1][t], xb[g & 1][m], acc[m][t]);
       __builtin_amdgcn_sched_barrier(0);
+      if (SPREAD && iss) {   // the next slab's units i = g, g + 6, ... of this wave
+#pragma unroll
+        for (int i = g; i < UPW; i += 6) piece(nd, i);
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
   issue(sl0, 0);
@@ -423,8 +438,13 @@ __global__ __launch_bounds__(512) void conv3_fwd_dma_kernel(ConvArgs a) {
     wait_vmcnt<0>();                          // this wave's units of slab sl landed
     __builtin_amdgcn_s_waitcnt(0xC07F);       // lgkmcnt(0): this wave's reads of the other slot are done
     __builtin_amdgcn_s_barrier();             // every wave's units landed; the other slot is free
-    if (sl + 1 < sl1) issue(sl + 1, p ^ 1);
-    if (live) compute(sl, p);
+    const bool iss = sl + 1 < sl1;
+    const Dma nd = issue_begin(iss ? sl + 1 : sl, p ^ 1);
+    if ((!SPREAD || !live) && iss) {   // the next slab's units all at once, before this slab's MFMAs
+#pragma unroll
+      for (int i = 0; i < UPW; ++i) piece(nd, i);
+    }
+    if (live) compute(sl, p, iss, nd);
     p ^= 1;
   }
   if (SPLIT) {   // f32 partial of this slab range: 16-B stores of 4 consecutive output channels
