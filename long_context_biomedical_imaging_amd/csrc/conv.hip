@@ -1137,13 +1137,47 @@ extern "C" int lci_convup_interleave(const void* src, void* dst, int B, int D, i
   return 0;
 }
 
-// Voxel (gapped-row) splits: up to 2^17 rows per workgroup, fewer (>= 1024) when that leaves under ~2048 workgroups
-// (small 2-D volumes, few channel tiles), so the grid still fills the 256 CUs.
+template <int MB, int WN, int WC>
+static int wgrad5_slots_of() {   // co-resident workgroups of this tile on the whole device
+  constexpr int XR = WG_ROWS + 2;
+  const size_t sh = (size_t)2 * (MB * WN * WG_ROWS * 32 + WC * (XR + 6) * 32) * sizeof(bf16);
+  int dev = 0, ncu = 0, per = 0;
+  LCI_HIP(hipGetDevice(&dev));
+  LCI_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  (void)hipFuncSetAttribute((const void*)conv3_wgrad5_kernel<MB, WN, WC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024);
+  LCI_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)conv3_wgrad5_kernel<MB, WN, WC>,
+                                                       64 * WN * WC, sh));
+  return std::max(1, ncu * std::max(1, per));
+}
+
+static int wgrad5_slots(int mb, int wn, int wc) {
+  static int cache[4] = {};
+  const int i = mb == 2 ? (wc == 4 ? 0 : 1) : (wc == 3 ? 2 : 3);
+  if (!cache[i]) {
+#define LCI_W5(M, N, C) if (mb == M && wn == N && wc == C) cache[i] = wgrad5_slots_of<M, N, C>();
+    LCI_W5(2, 2, 4) LCI_W5(2, 2, 2) LCI_W5(1, 3, 3) LCI_W5(1, 3, 2)
+#undef LCI_W5
+  }
+  return cache[i];
+}
+
+// Voxel (gapped-row) splits. v5 tiles: at most 2^17 rows per workgroup, then as many splits as fill the last round of
+// co-resident workgroups (a grid of r full rounds, not r rounds and a sliver: the C3 96-channel gradient went from
+// 2304 workgroups of 8192 rows to 1 round), at least 1024 rows each. v4: up to 2^17 rows, fewer (>= 1024) when that
+// leaves under ~2048 workgroups (small 2-D volumes, few channel tiles).
 extern "C" long long lci_conv3_wgrad_splits(long long V, int Cin, int Cout, int KD) {
   int mb, wn, wc;
   wgrad5_tile(Cin, Cout, mb, wn, wc);
-  const long long tiles = mb ? (long long)KD * 3 * (Cout / (32 * mb * wn)) * (Cin / (32 * wc))
-                             : (long long)KD * 3 * (Cout / (32 * ((Cout / 32) % 2 == 0 ? 2 : 1))) * (Cin / 32);
+  if (mb) {
+    const long long tiles = (long long)KD * 3 * (Cout / (32 * mb * wn)) * (Cin / (32 * wc));
+    const long long slots = wgrad5_slots(mb, wn, wc);
+    const long long ns_min = (V + (1 << 17) - 1) >> 17;
+    const long long rounds = std::max(1LL, (tiles * ns_min + slots - 1) / slots);
+    const long long ns = std::max(ns_min, rounds * slots / tiles);
+    return std::max(1LL, std::min(ns, (V + 1023) / 1024));
+  }
+  const long long tiles = (long long)KD * 3 * (Cout / (32 * ((Cout / 32) % 2 == 0 ? 2 : 1))) * (Cin / 32);
   long long lv = 1 << 17;
   while (lv > 1024 && ((V + lv - 1) / lv) * tiles < 2048) lv >>= 1;
   return (V + lv - 1) / lv;

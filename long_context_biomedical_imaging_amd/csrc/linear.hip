@@ -23,13 +23,8 @@
 
 namespace lci {
 
-#ifndef LCI_LW_R
-#define LCI_LW_R 32      // token rows per staged slab
-#endif
-#ifndef LCI_LW_NBUF
-#define LCI_LW_NBUF 4    // LDS ring depth (slabs in flight: NBUF - 1)
-#endif
-constexpr int LW_R = LCI_LW_R, LW_NBUF = LCI_LW_NBUF;
+constexpr int LW_R = 32;     // token rows per staged slab
+constexpr int LW_NBUF = 4;   // LDS ring depth (slabs in flight: NBUF - 1)
 
 struct LinWgradArgs {
   const bf16* dy;     // (M, ldy) row-major, columns [0, N)
@@ -53,18 +48,6 @@ __device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_dst) {
                : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
 }
 
-#ifndef LCI_LW_RSTG
-#define LCI_LW_RSTG 0   // slab staging: 1 = global loads into AGPRs + ds_write_b128 one slab ahead, 0 = LDS-DMA ring
-#endif
-// 16-B global load into an AGPR quad / LDS store from one (asm: no VGPR copies, no compiler vmcnt waits)
-__device__ __forceinline__ u32x4 lw_gld16(const void* p) {
-  u32x4 v;
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=a"(v) : "v"(p) : "memory");
-  return v;
-}
-__device__ __forceinline__ void lw_dsw16(unsigned addr, const u32x4& v) {
-  asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "a"(v) : "memory");
-}
 // Slabs of R token rows arrive by LDS-DMA (global_load_lds_dwordx4: lane l of a wave-instruction writes bytes
 // 16 l .. 16 l + 15 of a 1-KB unit = 16 rows x 64 B of one 32-column block) into a ring of NBUF LDS buffers,
 // NBUF - 1 slabs ahead: no staging registers, no ds_write pass; each wave waits (counted vmcnt) only for its own
@@ -164,48 +147,14 @@ __global__ __launch_bounds__(64 * WN * WC, 1) void linear_wgrad_kernel(LinWgradA
 #pragma unroll
   for (int j = 0; j < 8; ++j) bsum[j] = 0.f;
 
-  // register staging (RSTG): slab s+2's units are loaded into AGPRs during slab s and stored to its ring slot
-  // after slab s+1's barrier (the DMA issue stalls a wave ~60 cycles per 1-KB unit, 8 units per wave and slab here)
-  // (the 6-wave 64 x 128 tile spills with the staging registers: it keeps the DMA ring)
-  constexpr bool RSTG = LCI_LW_RSTG && !(MB == 2 && CB == 4 && WN == 2 && WC == 3);
-  u32x4 st[UPW];
-  auto gload = [&](int slab) __attribute__((always_inline)) {
-    const long long m0 = ms + (long long)slab * R;
-    const bool full = m0 + R <= me;
 #pragma unroll
-    for (int t = 0; t < UPW; ++t) {
-      if (t < nunits) st[t] = lw_gld16(full || m0 + urow[t] < me ? (const void*)uptr[t] : (const void*)(kLwZero + 8 * lc));
-      uptr[t] += ustep[t];
-    }
-  };
-  auto lwrite = [&](int slab) __attribute__((always_inline)) {
-    const unsigned lds0 = lds_base + (unsigned)(2 * (slab % NBUF) * BUF) + 16 * lane;
-#pragma unroll
-    for (int t = 0; t < UPW; ++t)
-      if (t < nunits) lw_dsw16(lds0 + ulds[t], st[t]);
-  };
-  if constexpr (RSTG) {
-    gload(0);
-    wait_vmcnt<0>();
-    lwrite(0);
-    if (nslab > 1) gload(1);
-  } else {
-#pragma unroll
-    for (int p = 0; p < NBUF - 1; ++p)
-      if (p < nslab) issue(p);
-  }
+  for (int p = 0; p < NBUF - 1; ++p)
+    if (p < nslab) issue(p);
   for (int sl = 0; sl < nslab; ++sl) {
-    if (!RSTG) wait_for(min(NBUF - 2, nslab - 1 - sl));
+    wait_for(min(NBUF - 2, nslab - 1 - sl));
     __builtin_amdgcn_s_waitcnt(15 | (3 << 14) | (7 << 4));   // lgkmcnt(0): this wave's LDS reads are done
     __builtin_amdgcn_s_barrier();
-    if (RSTG) {
-      if (sl + 1 < nslab) {   // slab sl+1 (loaded during slab sl-1) into its slot: slab sl-1's, retired by this barrier
-        wait_vmcnt<0>();
-        lwrite(sl + 1);
-      }
-    } else if (sl + NBUF - 1 < nslab) {
-      issue(sl + NBUF - 1);
-    }
+    if (sl + NBUF - 1 < nslab) issue(sl + NBUF - 1);
     const bf16* base = lsm + (sl % NBUF) * BUF;
     const bf16* ty = base + (MB * wn) * BLK;
     const bf16* tx = base + NBY * BLK + (CB * wc) * BLK;
@@ -224,8 +173,6 @@ __global__ __launch_bounds__(64 * WN * WC, 1) void linear_wgrad_kernel(LinWgradA
         for (int i = 0; i < MB; ++i)
 #pragma unroll
           for (int j = 0; j < CB; ++j) acc[i][j] = mfma32(fa[i], fb[j], acc[i][j]);
-        // the next-but-one slab's loads, a k-step after the stores that read the same AGPRs
-        if (RSTG && r0 == 0 && s == 0 && sl + 2 < nslab) gload(sl + 2);
       }
     }
     if (do_bias) {   // column sums of the staged dY block rows (zero rows past M contribute nothing)
@@ -277,10 +224,8 @@ static const LwTile kLwTiles[] = {{4, 3, 1, 4}, {2, 4, 2, 3}, {2, 2, 2, 3}, {2, 
                                   {2, 2, 1, 3}, {2, 1, 3, 1}, {1, 3, 3, 1}, {1, 1, 2, 2}};
 constexpr int kLwNTiles = (int)(sizeof(kLwTiles) / sizeof(kLwTiles[0]));
 
-// The first tile with the least padded work (LCI_LW_TILE=i forces tile i for A/B runs); -1 if every tile more than
-// doubles the work.
+// The first tile with the least padded work; -1 if every tile more than doubles the work.
 static int lw_pick(int N, int K) {
-  static const int force = getenv("LCI_LW_TILE") ? atoi(getenv("LCI_LW_TILE")) : -1;
   int best = -1;
   double bw = 0.0;
   for (int t = 0; t < kLwNTiles; ++t) {
@@ -288,7 +233,6 @@ static int lw_pick(int N, int K) {
     const int tn = 32 * c.mb * c.wn, tk = 32 * c.cb * c.wc;
     const double padded = (double)((N + tn - 1) / tn * tn) * ((K + tk - 1) / tk * tk);
     const double waste = padded / ((double)N * K);
-    if (t == force && waste <= 2.0) return t;
     if (t == kLwNTiles - 1 && best >= 0) break;
     if (waste <= 2.0 && (best < 0 || waste < bw - 1e-9)) { best = t; bw = waste; }
   }
@@ -467,32 +411,45 @@ static unsigned gelu_grid(long long n8) { return (unsigned)std::max(1LL, (n8 + 2
 
 using namespace lci;
 
-// Token splits for the weight gradient of an (N x K) Linear over M tokens: about LCI_LW_WGS (default 4096)
-// workgroups in all, splits of >= 2048 rows. Fewer, longer splits cut the f32 partial traffic (ns N K 4 bytes
-// written + read, against M (N + K) 2 bytes of operands); 0 if the shape is not supported.
+template <int MB, int CB, int WN, int WC>
+static int lw_slots_of() {   // co-resident workgroups of this tile on the whole device
+  constexpr int NBY = MB * WN, NBX = CB * WC;
+  const size_t sh = (size_t)LW_NBUF * (NBY + NBX) * LW_R * 32 * sizeof(bf16);
+  int dev = 0, ncu = 0, per = 0;
+  LCI_HIP(hipGetDevice(&dev));
+  LCI_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  (void)hipFuncSetAttribute((const void*)linear_wgrad_kernel<MB, CB, WN, WC, LW_R, LW_NBUF>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  LCI_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &per, (const void*)linear_wgrad_kernel<MB, CB, WN, WC, LW_R, LW_NBUF>, 64 * WN * WC, sh));
+  return std::max(1, ncu * std::max(1, per));
+}
+
+static int lw_slots(int t) {
+  static int cache[kLwNTiles] = {};
+  if (!cache[t]) {
+    const LwTile& c = kLwTiles[t];
+#define LCI_LW(A, B, C, D) \
+    if (c.mb == A && c.cb == B && c.wn == C && c.wc == D) cache[t] = lw_slots_of<A, B, C, D>();
+    LCI_LW(4, 3, 1, 4) LCI_LW(2, 4, 2, 3) LCI_LW(2, 2, 2, 3) LCI_LW(2, 2, 2, 2) LCI_LW(2, 2, 1, 3) LCI_LW(2, 1, 3, 1)
+    LCI_LW(1, 3, 3, 1) LCI_LW(1, 1, 2, 2)
+#undef LCI_LW
+  }
+  return cache[t];
+}
+
+// Token splits for the weight gradient of an (N x K) Linear over M tokens (at least 256 rows each).
 extern "C" long long lci_linear_wgrad_splits(long long M, int N, int K) {
   const int t = lw_pick(N, K);
   if (t < 0 || M <= 0) return 0;
-  static const long long target = getenv("LCI_LW_WGS") ? atoll(getenv("LCI_LW_WGS")) : 4096;
   const LwTile& c = kLwTiles[t];
   const long long tiles = (long long)((N + 32 * c.mb * c.wn - 1) / (32 * c.mb * c.wn)) *
                           ((K + 32 * c.cb * c.wc - 1) / (32 * c.cb * c.wc));
-  long long ns = (target + tiles - 1) / tiles;
-  // rows per split: at least 2048, or down to 512 while the f32 partials (ns N K 4 B, summed by the caller) stay
-  // within 32 MiB or a quarter of the operand bytes read (M (N + K) 2 B) -- the narrow Swin-width gradients (N x K =
-  // 96 x 288 over 2^18 tokens: 3 tiles, 128 splits at 2048 rows; 576 x 192 over 2^15) were short of workgroups (C3
-  // linear_wgrad 3.54 -> 2.45 ms per step at 512 rows, profiles/r03_lw_minrows_ab.txt); the wide ViT / Mamba shapes
-  // keep their split counts. LCI_LW_MINROWS=n: a fixed minimum (A/B).
-  static const long long minrows = getenv("LCI_LW_MINROWS") ? atoll(getenv("LCI_LW_MINROWS")) : 0;
-  long long cap;
-  if (minrows > 0) {
-    cap = (M + minrows - 1) / minrows;
-  } else {
-    const long long budget = std::max(32LL << 20, M * (N + K) / 2);   // partial bytes
-    cap = std::max((M + 2047) / 2048, std::min((M + 511) / 512, budget / (4LL * N * K)));
-  }
-  ns = std::min(ns, cap);
-  return std::max(ns, 1LL);
+  // one round of co-resident workgroups: every split's rows in one workgroup, the grid = the device's slots (a grid
+  // of r rounds and a sliver ran the sliver as a whole extra round; fewer splits also cut the f32 partials the
+  // caller sums: C4 fc1 256 -> 21 splits, 0.98 -> 0.81 ms with the sum, profiles/r05_split_ab.txt)
+  const long long ns = std::max(1LL, lw_slots(t) / tiles);
+  return std::max(1LL, std::min(ns, (M + 255) / 256));
 }
 
 extern "C" int lci_linear_wgrad(const void* dy, long long ldy, const void* x, long long ldx, long long M, int N,

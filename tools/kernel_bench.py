@@ -228,6 +228,22 @@ def bench_linear():
             torch.cuda.empty_cache()
 
 
+def bench_lw_split():
+    """lci_linear_wgrad + the caller's partial sums (the product path) at the metric / C4 / C5 token counts; run under
+    different LCI_LW_WGS / LCI_LW_MINROWS to price the split count."""
+    shapes = {"qkv": (1152, 384), "proj": (384, 384), "fc1": (1536, 384), "fc2": (384, 1536), "m_in": (768, 384),
+              "m_x": (40, 192), "m_dt": (192, 24)}
+    for M in (131072, 524288, 1 << 21):
+        for name, (N, K) in shapes.items():
+            dy = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+            x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+            ns = kernels._lib.load().lci_linear_wgrad_splits(M, N, K)
+            emit(f"linear_wgrad {name}", timeit(lambda: kernels.linear_wgrad(dy, x, True), iters=10), 2.0 * M * N * K,
+                 "TFLOP/s", f"M{M} N{N} K{K} ns{ns}")
+            del dy, x
+        torch.cuda.empty_cache()
+
+
 def bench_mlp():
     """The MLPBlock (linear1 -> GELU -> linear2, backbone_vit.py:249) forward + backward under bf16 autocast at the
     ViT (M = 131072) and C5 (M = 2^21) token counts: forward / data-gradient GEMMs on lci_gemm_bt (the default) vs
@@ -314,6 +330,8 @@ def main():
         bench_linear()
     if "mlp" in which:
         bench_mlp()
+    if "lwsplit" in which:
+        bench_lw_split()
     if "gemm" in which:
         bench_gemm()
     if "gemm_swin" in which:
