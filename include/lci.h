@@ -56,8 +56,8 @@ extern "C" {
  * lci_window_attn_bwd pad_ws; 16: lci_attn_bwd delta_ws is (B, H, 2, L): the negated row constants -lse2 | -delta; 17: lci_window_bwd_needs_plain;
  * 18: lci_attn_bwd delta_ws is lci_attn_bwd_ws_bytes(B, H, L) bytes; 19: selective-scan checkpoints in the I/O
  * dtype; 20: lci_attn_gen_fwd / lci_attn_gen_bwd; 21: lci_gemm_bt; 22: lci_linear_fwd removed, superseded by
- * lci_gemm_bt; 23: lci_fftconv_spectrum Dv). */
-#define LCI_ABI_VERSION 23
+ * lci_gemm_bt; 23: lci_fftconv_spectrum Dv; 24: lci_inorm_finalize). */
+#define LCI_ABI_VERSION 24
 const char* lci_last_error(void);
 int lci_abi_version(void);
 /* sha256 prefix of the sources the library was built from (build_lib.source_hash); the Python binding refuses a
@@ -178,13 +178,16 @@ int lci_conv3_wgrad(const void* x, const void* dy, float* part, int B, int D, in
 /* ------------------------------------------------------------------ decoder-head instance norm (+ LeakyReLU)
  * Replaces MONAI-1.3 UnetResBlock norm1+lrelu / norm2 / norm3 (InstanceNorm, affine=False, eps 1e-5) in the UNETR
  * heads (enhance_heads.py:30-356), channels-last. x, dz, out: (B, V, C) bf16, C % 8 == 0, C <= 2048.
- * reduce: part (B, lci_inorm_chunks(V, B), 2, C) f32 <- per-chunk sums of (x, x^2) when dz is null, else of
+ * reduce: part (B, 2, C, lci_inorm_chunks(V, B)) f32 <- per-chunk sums of (x, x^2) when dz is null, else of
  *   (dn, dn*n) with n = (x - mean) * rstd, dn = dz * (act && n < 0 ? slope : 1); stats (B, 2, C) = mean, rstd.
  * apply: dz null -> out = act ? lrelu(n) : n;  else out = dx = rstd * (dn - coef0 - n * coef1), coef (B, 2, C)
- *   = voxel means of (dn, dn*n). The caller combines the partial sums (in f64) between the two calls. */
+ *   = voxel means of (dn, dn*n).
+ * finalize: the partial sums (in f64, fixed order) -> out (B, 2, C): mode 0 the stats (mean, rstd with eps), mode 1
+ *   the coefficients (the voxel means of both sums). */
 int lci_inorm_chunks(long long V, int B);
 int lci_inorm_reduce(const void* x, const void* dz, const float* stats, float* part, long long V, int B, int C,
                      int act, float slope, void* stream);
+int lci_inorm_finalize(const float* part, float* out, long long V, int B, int C, int mode, float eps, void* stream);
 int lci_inorm_apply(const void* x, const void* dz, const float* stats, const float* coef, void* out, long long V,
                     int B, int C, int act, float slope, void* stream);
 /* UnetResBlock's tail, lrelu(norm2(x) + r), in one pass with the unfused bf16 roundings: out (B, V, C) bf16 =

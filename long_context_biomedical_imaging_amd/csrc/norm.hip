@@ -6,8 +6,9 @@
 // view): x stays (B, V, C) bf16 channels-last between the HIP convolutions.
 //   forward : n = (x - mean[b,c]) * rstd[b,c];  z = act ? lrelu(n) : n
 //   backward: dn = dz * (act && n < 0 ? slope : 1);  dx = rstd * (dn - mean_V(dn) - n * mean_V(dn * n))
-// Two passes each way: a reduction (per-(b, c) partial sums over voxel chunks, combined in f64 by the caller)
-// and an elementwise pass. All HBM-bound: a thread moves 8 channels (16 B) per voxel.
+// Two passes each way: a reduction (per-(b, c) partial sums over voxel chunks, combined in f64 by
+// inorm_finalize_kernel into the stats / coefficients) and an elementwise pass. All HBM-bound: a thread moves 8
+// channels (16 B) per voxel.
 #include "common.hpp"
 
 namespace lci {
@@ -18,7 +19,7 @@ struct NormArgs {
   bf16* out;           // fwd: z; bwd: dx
   const float* stats;  // (B, 2, C): mean, rstd
   const float* coef;   // bwd: (B, 2, C): mean_V(dn), mean_V(dn * n)
-  float* part;         // (B, nchunk, 2, C) partial sums
+  float* part;         // (B, 2, C, nchunk) partial sums (chunk fastest: one contiguous row per (b, sum, c))
   long long V, chunk;
   int C, nchunk, act;
   float slope;
@@ -88,9 +89,9 @@ __global__ __launch_bounds__(256) void inorm_reduce_kernel(NormArgs a) {
   for (int c = tid; c < a.C; c += 256) {
     float t1 = 0.f, t2 = 0.f;
     for (int q = 0; q < rows; ++q) { t1 += red[0][q * a.C + c]; t2 += red[1][q * a.C + c]; }
-    float* p = a.part + ((long long)b * a.nchunk + chunk) * 2 * a.C;
-    p[c] = t1;
-    p[a.C + c] = t2;
+    float* p = a.part + ((long long)b * 2 * a.C + c) * a.nchunk + chunk;
+    p[0] = t1;
+    p[(long long)a.C * a.nchunk] = t2;
   }
 }
 
@@ -156,9 +157,64 @@ __global__ __launch_bounds__(256) void inorm_res_kernel(NormArgs a, const bf16* 
   *(bf16x8*)(a.out + off) = o;
 }
 
+// part (B, 2, C, nchunk) -> out (B, 2, C): one wave per (b, c) sums both rows in f64 (lane-strided, 8 loads in
+// flight per lane, then a fixed xor-shuffle tree: deterministic), divided by V; mode 0: (mean, rstd = 1 / sqrt(
+// max(E[x^2] - mean^2, 0) + eps)), the f64 arithmetic of the unfused torch code; mode 1: the voxel means themselves
+// (the backward's coefficients).
+__global__ __launch_bounds__(256) void inorm_finalize_kernel(const float* __restrict__ part, float* __restrict__ out,
+                                                             long long V, int B, int C, int nchunk, int mode,
+                                                             float eps) {
+  const int lane = threadIdx.x & 63;
+  const long long wv = blockIdx.x * 4LL + (threadIdx.x >> 6);   // (b, c)
+  if (wv >= (long long)B * C) return;
+  const int b = (int)(wv / C), c = (int)(wv % C);
+  const float* p1 = part + ((long long)b * 2 * C + c) * nchunk;
+  const float* p2 = p1 + (long long)C * nchunk;
+  double s1 = 0.0, s2 = 0.0;
+  for (int k0 = 0; k0 < nchunk; k0 += 64 * 8) {
+    float v1[8], v2[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = k0 + 64 * u + lane;
+      v1[u] = k < nchunk ? p1[k] : 0.f;
+      v2[u] = k < nchunk ? p2[k] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { s1 += (double)v1[u]; s2 += (double)v2[u]; }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    s1 += __shfl_xor(s1, o);
+    s2 += __shfl_xor(s2, o);
+  }
+  if (lane == 0) {
+    const double m1 = s1 / (double)V, m2 = s2 / (double)V;
+    float* o = out + (long long)b * 2 * C;
+    if (mode == 0) {
+      o[c] = (float)m1;
+      o[C + c] = (float)(1.0 / sqrt(fmax(m2 - m1 * m1, 0.0) + (double)eps));
+    } else {
+      o[c] = (float)m1;
+      o[C + c] = (float)m2;
+    }
+  }
+}
+
 }  // namespace lci
 
 using namespace lci;
+
+extern "C" int lci_inorm_chunks(long long V, int B);
+
+extern "C" int lci_inorm_finalize(const float* part, float* out, long long V, int B, int C, int mode, float eps,
+                                  void* stream) {
+  LCI_CHECK(V > 0 && B > 0 && C > 0 && (mode == 0 || mode == 1), "inorm_finalize: bad arguments");
+  const int nchunk = lci_inorm_chunks(V, B);
+  hipLaunchKernelGGL(inorm_finalize_kernel, dim3((unsigned)(((long long)B * C + 3) / 4)), dim3(256), 0,
+                     (hipStream_t)stream, part, out, V, B, C, nchunk, mode, eps);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
 
 // Voxel chunks per sample for the reduction: ~2048 workgroups in total, at least 256 voxels per chunk.
 extern "C" int lci_inorm_chunks(long long V, int B) {

@@ -1453,31 +1453,31 @@ INORM_EPS = 1e-5
 LRELU_SLOPE = 0.01
 
 
-def _inorm_sums(x_cl, dz_cl, stats, act):
-    """(B, 2, C) f64 sums over voxels: (x, x^2) forward, (dn, dn * n) backward."""
+def _inorm_sums(x_cl, dz_cl, stats, act, mode):
+    """(B, 2, C) f32 from the voxel sums (lci_inorm_reduce partials, combined in f64 by lci_inorm_finalize):
+    mode 0 the stats (mean, rstd) of x; mode 1 the voxel means of (dn, dn * n) for the backward."""
     B, V, C = x_cl.shape
     lib = _lib.load()
     nch = lib.lci_inorm_chunks(V, B)
-    part = torch.empty(B, nch, 2, C, device=x_cl.device, dtype=torch.float32)
+    part = torch.empty(B, 2, C, nch, device=x_cl.device, dtype=torch.float32)
+    out = torch.empty(B, 2, C, device=x_cl.device, dtype=torch.float32)
+    st = _lib.stream_of(x_cl)
     _lib.call("lci_inorm_reduce", x_cl.data_ptr(), _lib.ptr(dz_cl), _lib.ptr(stats), part.data_ptr(), V, B, C,
-              int(act), LRELU_SLOPE, _lib.stream_of(x_cl))
-    return part.double().sum(1)
+              int(act), LRELU_SLOPE, st)
+    _lib.call("lci_inorm_finalize", part.data_ptr(), out.data_ptr(), V, B, C, mode, INORM_EPS, st)
+    return out
 
 
 def _inorm_stats(x_cl, act):
     """(B, 2, C) f32 mean, rstd of a (B, V, C) bf16 tensor over its voxels."""
-    V = x_cl.shape[1]
-    s = _inorm_sums(x_cl, None, None, act) / V
-    mean = s[:, 0]
-    rstd = torch.rsqrt((s[:, 1] - mean * mean).clamp_min(0.0) + INORM_EPS)
-    return torch.stack([mean, rstd], 1).float().contiguous()
+    return _inorm_sums(x_cl, None, None, act, 0)
 
 
 def _inorm_bwd(x_cl, stats, dz, act):
     """dx of z = [lrelu](norm(x)) for the upstream gradient dz (B, V, C)."""
     B, V, C = x_cl.shape
     dz = dz.to(torch.bfloat16).contiguous()
-    coef = (_inorm_sums(x_cl, dz, stats, act) / V).float().contiguous()
+    coef = _inorm_sums(x_cl, dz, stats, act, 1)
     dx = torch.empty_like(x_cl)
     KernelTimer.run("inorm_bwd", 0.0, x_cl, lambda: _lib.call(
         "lci_inorm_apply", x_cl.data_ptr(), dz.data_ptr(), stats.data_ptr(), coef.data_ptr(), dx.data_ptr(),
