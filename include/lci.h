@@ -390,7 +390,7 @@ int lci_gelu_bwd(const void* x, const void* dy, void* dx, long long n, void* str
  * or null; f32 accumulation, bias added in f32 and the sum rounded once (the autocast nn.Linear's arithmetic). The
  * forward and data-gradient GEMMs of the token-wise Linear layers: SABlock qkv / out_proj (backbone_vit.py:166-167),
  * MLPBlock (:249), Hyena in/out_proj (hyena.py:278-279), Mamba in/out_proj (mamba.py:60-64,90); the data gradient
- * is the call with the transposed weight. Supported when lci_gemm_bt_supported(N, K): N % 384 == 0, N <= 4096,
+ * is the call with the transposed weight. Supported when lci_gemm_bt_supported(N, K): N % 384 == 0 or N % 256 == 0, N <= 4096,
  * K % 32 == 0; ldx, ldy % 8 == 0; x / w / y 16-byte aligned; any M (per-tile 32-bit offsets). */
 int lci_gemm_bt_supported(int N, int K);
 int lci_gemm_bt(const void* x, long long ldx, const void* w, const void* bias, void* y, long long ldy, long long M,

@@ -269,14 +269,32 @@ __global__ __launch_bounds__(GM_WAVES * 64, 1) void gemm_bt_kernel(GemmArgs a) {
 
 using namespace lci;
 
-// 1 when lci_gemm_bt takes (N, K): N a multiple of the 384-feature tile, K of the 32-deep slab
-extern "C" int lci_gemm_bt_supported(int N, int K) { return N > 0 && N % 384 == 0 && N <= GM_MAXN && K > 0 && K % GM_BK == 0; }
+// feature tile of an output width: 384 where it divides N, else 256 (the ConvTranspose-as-GEMM widths 8 Cout:
+// 512 .. 4096), 0 if neither does
+static int gm_tn(int N) { return N % 384 == 0 ? 384 : (N % 256 == 0 ? 256 : 0); }
+
+// 1 when lci_gemm_bt takes (N, K): N a multiple of a 384- or 256-feature tile, K of the 32-deep slab
+extern "C" int lci_gemm_bt_supported(int N, int K) {
+  return N > 0 && gm_tn(N) && N <= GM_MAXN && K > 0 && K % GM_BK == 0;
+}
+
+template <int TN>
+static void gm_launch(const GemmArgs& a, long long grid, bool bias, hipStream_t st) {
+  const size_t sh = (size_t)GM_NSLOT * (GM_TM + TN) * 64 + GM_WAVES * GM_EPI + GM_MAXN * 2;
+  if (bias) {
+    (void)hipFuncSetAttribute((const void*)gemm_bt_kernel<TN, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
+    hipLaunchKernelGGL((gemm_bt_kernel<TN, true>), dim3((unsigned)grid), dim3(GM_WAVES * 64), sh, st, a);
+  } else {
+    (void)hipFuncSetAttribute((const void*)gemm_bt_kernel<TN, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
+    hipLaunchKernelGGL((gemm_bt_kernel<TN, false>), dim3((unsigned)grid), dim3(GM_WAVES * 64), sh, st, a);
+  }
+}
 
 // Y (M x N, row stride ldy) = X (M x K, row stride ldx) . W^T (W: N x K contiguous) + bias (N, bf16, or null); bf16.
 // x, w, y 16-byte aligned; ldx, ldy multiples of 8; M * ldx and M * ldy any size (per-tile 32-bit offsets).
 extern "C" int lci_gemm_bt(const void* x, long long ldx, const void* w, const void* bias, void* y, long long ldy,
                            long long M, int N, int K, void* stream) {
-  LCI_CHECK(lci_gemm_bt_supported(N, K), "gemm_bt: N=%d K=%d unsupported (N %% 384, K %% 32)", N, K);
+  LCI_CHECK(lci_gemm_bt_supported(N, K), "gemm_bt: N=%d K=%d unsupported (N %% 384 or %% 256, K %% 32)", N, K);
   LCI_CHECK(M > 0 && ldx >= K && ldy >= N && ldx % 8 == 0 && ldy % 8 == 0, "gemm_bt: bad M / strides");
   LCI_CHECK(((uintptr_t)x | (uintptr_t)w | (uintptr_t)y) % 16 == 0, "gemm_bt: pointers must be 16-byte aligned");
   LCI_CHECK((long long)GM_TM * ldx * 2 < (1ll << 31) && (long long)GM_TM * ldy * 2 < (1ll << 31) &&
@@ -284,7 +302,8 @@ extern "C" int lci_gemm_bt(const void* x, long long ldx, const void* w, const vo
   GemmArgs a{};
   a.x = (const bf16*)x; a.ldx = ldx; a.w = (const bf16*)w; a.bias = (const bf16*)bias; a.y = (bf16*)y; a.ldy = ldy;
   a.M = M; a.N = N; a.K = K;
-  a.ntn = N / 384;
+  const int tn = gm_tn(N);
+  a.ntn = N / tn;
   a.ntiles = (M + GM_TM - 1) / GM_TM * a.ntn;
   static int ncu = 0;
   if (!ncu) {
@@ -296,15 +315,8 @@ extern "C" int lci_gemm_bt(const void* x, long long ldx, const void* w, const vo
   a.G8 = (int)(grid / 8);
   a.dmt = a.G8 / a.ntn;
   a.dnt = a.G8 % a.ntn;
-  constexpr int TN = 384;
-  const size_t sh = (size_t)GM_NSLOT * (GM_TM + TN) * 64 + GM_WAVES * GM_EPI + GM_MAXN * 2;
-  if (bias) {
-    (void)hipFuncSetAttribute((const void*)gemm_bt_kernel<TN, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
-    hipLaunchKernelGGL((gemm_bt_kernel<TN, true>), dim3((unsigned)grid), dim3(GM_WAVES * 64), sh, (hipStream_t)stream, a);
-  } else {
-    (void)hipFuncSetAttribute((const void*)gemm_bt_kernel<TN, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
-    hipLaunchKernelGGL((gemm_bt_kernel<TN, false>), dim3((unsigned)grid), dim3(GM_WAVES * 64), sh, (hipStream_t)stream, a);
-  }
+  if (tn == 384) gm_launch<384>(a, grid, bias != nullptr, (hipStream_t)stream);
+  else gm_launch<256>(a, grid, bias != nullptr, (hipStream_t)stream);
   LCI_LAUNCH_CHECK();
   return 0;
 }

@@ -1776,7 +1776,8 @@ def _wgrad_tiny_k(dy2: torch.Tensor, x2: torch.Tensor, bias: bool):
 
 
 # csrc/gemm.hip for the bf16 projection GEMMs whose output width it takes (N % 384 == 0: every ViT-small / Mamba /
-# Hyena projection and data gradient); LCI_HIP_GEMM=0 routes them to hipBLASLt (A/B: profiles/r05_gemm_ab.txt)
+# Hyena projection and data gradient; N % 256 == 0: the decoders' ConvTranspose GEMMs); LCI_HIP_GEMM=0 routes them to
+# hipBLASLt (A/B: profiles/r05_gemm_ab.txt)
 HIP_GEMM = os.environ.get("LCI_HIP_GEMM", "1") == "1"
 
 
@@ -1795,7 +1796,7 @@ def gemm_bt_preferred(M: int, N: int) -> bool:
     stage-3 / 4 projections: 4096 / 512 tokens, 16-48 tiles) its one-tile-per-CU walk leaves most of the chip idle
     and hipBLASLt's smaller / split-K tiles win (M = 4096 fc2: 0.056 vs 0.020 ms; C3 step 57.0 vs 54.2 ms with every
     supported shape on lci_gemm_bt; profiles/r05_gemm_ab.txt)."""
-    return -(-M // 256) * (N // 384) >= GEMM_BT_MIN_TILES
+    return -(-M // 256) * (N // (384 if N % 384 == 0 else 256)) >= GEMM_BT_MIN_TILES
 
 
 def gemm_bt(x2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:

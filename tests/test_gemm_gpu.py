@@ -26,7 +26,10 @@ def _check(y, x, w, b):
 @pytest.mark.parametrize("M,N,K,bias,pad", [(1, 384, 384, True, 0), (255, 384, 384, False, 0), (256, 1152, 384, True, 0),
                                             (1000, 1536, 384, True, 64), (4173, 384, 1536, False, 0),
                                             (777, 768, 96, True, 8), (3001, 384, 320, True, 0),
-                                            (2500, 384, 1152, True, 0), (131072, 1152, 384, True, 0)])
+                                            (2500, 384, 1152, True, 0), (131072, 1152, 384, True, 0),
+                                            # 256-feature tiles (N % 384 != 0: ConvTranspose-as-GEMM widths 8 Cout)
+                                            (3001, 512, 384, True, 0), (700, 1024, 256, False, 8),
+                                            (20000, 2048, 384, True, 0), (513, 4096, 512, True, 0)])
 def test_gemm_bt_vs_fp64(M, N, K, bias, pad):
     from long_context_biomedical_imaging_amd import kernels
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
@@ -83,3 +86,5 @@ def test_gemm_bt_supported_shapes():
     lib = _lib.load()
     assert lib.lci_gemm_bt_supported(384, 192) and not lib.lci_gemm_bt_supported(4224, 1536)
     assert not lib.lci_gemm_bt_supported(384, 48) and not lib.lci_gemm_bt_supported(400, 384)
+    assert lib.lci_gemm_bt_supported(2048, 384) and lib.lci_gemm_bt_supported(512, 64)
+    assert not lib.lci_gemm_bt_supported(640, 384) and not lib.lci_gemm_bt_supported(4352, 384)

@@ -5,9 +5,11 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/bench_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 900 python -u $ROOT/bench.py > $OUT/metric.json 2> $OUT/metric.err || { echo "STOP metric"; tail -5 $OUT/metric.err; exit 1; }
-echo "metric done"
-for wl in vit_p4_512 vit_hyena_p2_1024 vit_hyena_p2_512 swin_mamba_p2_128 swin_hyena_p2_128 vit_mamba_p2_256; do
+if [ -z "$SKIP_METRIC" ]; then
+  timeout -k 10 900 python -u $ROOT/bench.py > $OUT/metric.json 2> $OUT/metric.err || { echo "STOP metric"; tail -5 $OUT/metric.err; exit 1; }
+  echo "metric done"
+fi
+for wl in ${WORKLOADS:-vit_p4_512 vit_hyena_p2_1024 vit_hyena_p2_512 swin_mamba_p2_128 swin_hyena_p2_128 vit_mamba_p2_256}; do
   timeout -k 10 900 python -u $ROOT/bench.py --workload $wl --steps 5 --warmup 2 > $OUT/$wl.json 2> $OUT/$wl.err || { echo "STOP $wl"; tail -5 $OUT/$wl.err; exit 1; }
   echo "$wl done"
 done

@@ -277,7 +277,8 @@ def bench_gemm():
     from long_context_biomedical_imaging_amd import trainer
     trainer.use_tuned_gemms()
     for M in (131072, 1 << 21):
-        for K, N, nm in ((384, 1152, "qkv"), (384, 384, "out_proj"), (384, 1536, "fc1"), (1536, 384, "fc2")):
+        for K, N, nm in ((384, 1152, "qkv"), (384, 384, "out_proj"), (384, 1536, "fc1"), (1536, 384, "fc2"),
+                         (384, 2048, "convup 384->8x256"), (256, 1024, "convup 256->8x128"), (512, 2048, "convup K512")):
             x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
             w = (torch.randn(N, K, device="cuda") * K ** -0.5).to(torch.bfloat16)
             b = torch.randn(N, device="cuda").to(torch.bfloat16)
