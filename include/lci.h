@@ -56,8 +56,8 @@ extern "C" {
  * lci_window_attn_bwd pad_ws; 16: lci_attn_bwd delta_ws is (B, H, 2, L): the negated row constants -lse2 | -delta; 17: lci_window_bwd_needs_plain;
  * 18: lci_attn_bwd delta_ws is lci_attn_bwd_ws_bytes(B, H, L) bytes; 19: selective-scan checkpoints in the I/O
  * dtype; 20: lci_attn_gen_fwd / lci_attn_gen_bwd; 21: lci_gemm_bt; 22: lci_linear_fwd removed, superseded by
- * lci_gemm_bt; 23: lci_fftconv_spectrum Dv; 24: lci_inorm_finalize). */
-#define LCI_ABI_VERSION 24
+ * lci_gemm_bt; 23: lci_fftconv_spectrum Dv; 24: lci_inorm_finalize; 25: lci_adam_step). */
+#define LCI_ABI_VERSION 25
 const char* lci_last_error(void);
 int lci_abi_version(void);
 /* sha256 prefix of the sources the library was built from (build_lib.source_hash); the Python binding refuses a
@@ -395,6 +395,18 @@ int lci_gelu_bwd(const void* x, const void* dy, void* dx, long long n, void* str
 int lci_gemm_bt_supported(int N, int K);
 int lci_gemm_bt(const void* x, long long ldx, const void* w, const void* bias, void* y, long long ldy, long long M,
                 int N, int K, void* stream);
+
+/* ------------------------------------------------------------------ optimizer step (csrc/optim.hip)
+ * Adam / AdamW update of nt <= lci_adam_max_tensors() f32 tensors in one launch (trainer_base.py:171-177 ->
+ * torch.optim.Adam / AdamW, optim_base.py:87-89): p[i], g[i], m[i] (exp_avg), v[i]
+ * (exp_avg_sq) of n[i] elements each; step[i] -> the tensor's device step count, already incremented for this update
+ * (bias corrections 1 - beta^step evaluated on the device, so the call can sit in a captured graph). adamw = 1:
+ * decoupled weight decay, 0: L2 (added to the gradient); maximize negates the gradient. The arithmetic is torch's
+ * fused Adam's (f64 moment updates, f32 step size / denominator / update). The pointer arrays are host memory. */
+int lci_adam_max_tensors(void);
+int lci_adam_step(float* const* p, const float* const* g, float* const* m, float* const* v, const float* const* step,
+                  const long long* n, int nt, double lr, double beta1, double beta2, double weight_decay, double eps,
+                  int adamw, int maximize, void* stream);
 
 #ifdef __cplusplus
 }

@@ -14,12 +14,13 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_LIB = os.path.join(HERE, "liblci.so")
 LIB_PATH = os.environ.get("LCI_LIB_PATH", DEFAULT_LIB)   # override: kernel-variant A/B runs (no staleness check)
-ABI_VERSION = 24   # include/lci.h LCI_ABI_VERSION
+ABI_VERSION = 25   # include/lci.h LCI_ABI_VERSION
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 _F = ctypes.c_float
 _L = ctypes.c_longlong
+_D = ctypes.c_double
 
 # name -> argtypes (all return int status)
 SIGNATURES = {
@@ -79,6 +80,7 @@ SIGNATURES = {
     "lci_direct_conv_dk": [_P, _P, _P, _I, _I, _I, _P],
     "lci_hyena_filter_prep": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P],
     "lci_hyena_filter_fwd": [_P, _P, _P, _P, _I, _I, _F, _P, _P],
+    "lci_adam_step": [_P, _P, _P, _P, _P, _P, _I, _D, _D, _D, _D, _D, _I, _I, _P],
     "lci_hyena_filter_bwd": [_P, _P, _P, _P, _I, _I, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
 }
 
@@ -144,6 +146,8 @@ def load(path: str = LIB_PATH):
     lib.lci_fft_size.argtypes = [_I]
     lib.lci_dwconv_silu_bwd_part_rows.restype = ctypes.c_longlong
     lib.lci_dwconv_silu_bwd_part_rows.argtypes = [_I, _I]
+    lib.lci_adam_max_tensors.restype = ctypes.c_int
+    lib.lci_adam_max_tensors.argtypes = []
     lib.lci_direct_conv_max_len.restype = ctypes.c_int
     lib.lci_direct_conv_max_len.argtypes = []
     lib.lci_direct_conv_dk_splits.restype = ctypes.c_int

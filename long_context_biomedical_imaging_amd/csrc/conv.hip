@@ -844,7 +844,9 @@ __global__ __launch_bounds__(64 * WN * WC) void conv3_wgrad5_kernel(WgradArgs a)
   constexpr int NTH = 64 * WN * WC;
   constexpr int XR = WG_ROWS + 2;
   constexpr int NB_DY = MB * WN, NB_X = WC;                     // 32-channel blocks staged per step
-  constexpr int DYBLK = WG_ROWS * 32, XBLK = (XR + 6) * 32;     // elements per LDS block
+  // elements per LDS block, each padded by 64 B: the 16-B staging stores of one 8-lane group hit two adjacent blocks,
+  // which would otherwise start on the same bank (4 KB / 8.5 KB multiples)
+  constexpr int DYBLK = WG_ROWS * 32 + 32, XBLK = (XR + 6) * 32 + 32;
   constexpr int BUF = NB_DY * DYBLK + NB_X * XBLK;
   constexpr int NDY = (WG_ROWS * NB_DY * 4 + NTH - 1) / NTH;    // 16-B chunks per thread per step
   constexpr int NXS = (XR * NB_X * 4 + NTH - 1) / NTH;
@@ -981,9 +983,13 @@ __global__ __launch_bounds__(64 * WN * WC) void conv3_wgrad5_kernel(WgradArgs a)
 }
 
 template <int MB, int WN, int WC>
+constexpr size_t wgrad5_lds() {   // two buffers of the kernel's padded dy / x blocks
+  return (size_t)2 * (MB * WN * (WG_ROWS * 32 + 32) + WC * ((WG_ROWS + 8) * 32 + 32)) * sizeof(bf16);
+}
+
+template <int MB, int WN, int WC>
 static int launch_wgrad5(WgradArgs a, hipStream_t st) {
-  constexpr int XR = WG_ROWS + 2;
-  const size_t sh = (size_t)2 * (MB * WN * WG_ROWS * 32 + WC * (XR + 6) * 32) * sizeof(bf16);
+  const size_t sh = wgrad5_lds<MB, WN, WC>();
   const long long nb = (long long)a.KD * 3 * a.ns * (a.Cout / (32 * MB * WN)) * (a.Cin / (32 * WC));
   LCI_CHECK(nb < (1LL << 30), "conv3_wgrad: too many workgroups");
   a.nb = (int)nb;
@@ -1139,8 +1145,7 @@ extern "C" int lci_convup_interleave(const void* src, void* dst, int B, int D, i
 
 template <int MB, int WN, int WC>
 static int wgrad5_slots_of() {   // co-resident workgroups of this tile on the whole device
-  constexpr int XR = WG_ROWS + 2;
-  const size_t sh = (size_t)2 * (MB * WN * WG_ROWS * 32 + WC * (XR + 6) * 32) * sizeof(bf16);
+  const size_t sh = wgrad5_lds<MB, WN, WC>();
   int dev = 0, ncu = 0, per = 0;
   LCI_HIP(hipGetDevice(&dev));
   LCI_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));

@@ -1,6 +1,7 @@
 """torch.autograd wrappers over the liblci C-ABI. Each op runs the HIP kernels; none has a CPU path."""
 from __future__ import annotations
 
+import ctypes
 import os
 
 import torch
@@ -1917,3 +1918,27 @@ class _PointwiseSmall(torch.autograd.Function):
 
 def pointwise_small(x2: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None) -> torch.Tensor:
     return _PointwiseSmall.apply(x2, weight, bias)
+
+
+# ------------------------------------------------------------------------------------------- optimizer step
+def adam_step(params, grads, exp_avgs, exp_avg_sqs, steps, lr: float, beta1: float, beta2: float,
+              weight_decay: float, eps: float, decoupled: bool, maximize: bool) -> None:
+    """One Adam / AdamW update of f32 CUDA tensors in place by csrc/optim.hip (lci_adam_step, up to
+    lci_adam_max_tensors() tensors per launch); `steps` are the per-tensor device step counts, already incremented
+    (trainer_base.py:171-177 -> torch.optim.Adam / AdamW with optim_base.py:87-89's hyper-parameters)."""
+    if not params:
+        return
+    lib = _lib.load()
+    per = lib.lci_adam_max_tensors()
+    for t in (*params, *grads, *exp_avgs, *exp_avg_sqs):
+        if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()):
+            raise _lib.LciError("adam_step: f32 contiguous CUDA tensors only")
+    st = _lib.stream_of(params[0])
+    for i0 in range(0, len(params), per):
+        sl = slice(i0, i0 + per)
+        n = len(params[sl])
+        arr = lambda ts: (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])   # noqa: E731
+        sizes = (ctypes.c_longlong * n)(*[t.numel() for t in params[sl]])
+        _lib.call("lci_adam_step", arr(params[sl]), arr(grads[sl]), arr(exp_avgs[sl]), arr(exp_avg_sqs[sl]),
+                  arr(steps[sl]), sizes, n, float(lr), float(beta1), float(beta2), float(weight_decay), float(eps),
+                  int(decoupled), int(maximize), st)

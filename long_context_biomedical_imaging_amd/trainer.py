@@ -61,17 +61,72 @@ def use_tuned_gemms(path: str = TUNED_GEMMS) -> bool:
     return bool(tunable.read_file(path))
 
 
+class _LciAdamStep:
+    """Adam / AdamW whose update runs on csrc/optim.hip (kernels.adam_step). A subclass of torch's optimizer built
+    with fused=True, so its state (per-parameter device `step`, `exp_avg`, `exp_avg_sq`), param_groups and
+    state_dict are torch's own and checkpoints move between the two; only the arithmetic kernel differs (the same
+    formulas: csrc/optim.hip). torch's fused kernel gave each 64-K-element chunk one workgroup (~1000 over a
+    SwinUNETR step at ~1 TB/s); this one streams at the HBM rate. Groups with options the reference never sets
+    (amsgrad, complex or non-f32 parameters, a tensor lr, differentiable) take torch's fused update."""
+
+    _decoupled = False
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for group in self.param_groups:
+            params, grads, exp_avgs, exp_avg_sqs, max_sqs, steps = [], [], [], [], [], []
+            has_complex = self._init_group(group, params, grads, exp_avgs, exp_avg_sqs, max_sqs, steps)
+            if not params:
+                continue
+            beta1, beta2 = group["betas"]
+            if (has_complex or group["amsgrad"] or group.get("differentiable") or isinstance(group["lr"], torch.Tensor)
+                    or any(p.dtype != torch.float32 or not p.is_cuda for p in params)
+                    or any(g.is_sparse or not g.is_contiguous() for g in grads)):
+                torch.optim.adam._fused_adam(params, grads, exp_avgs, exp_avg_sqs, max_sqs, steps, None, None,
+                                             amsgrad=group["amsgrad"], has_complex=has_complex, beta1=beta1,
+                                             beta2=beta2, lr=group["lr"], weight_decay=group["weight_decay"],
+                                             eps=group["eps"], maximize=group["maximize"], capturable=True,
+                                             differentiable=False, decoupled_weight_decay=self._decoupled)
+                continue
+            torch._foreach_add_(steps, 1)
+            from . import kernels
+            kernels.adam_step(params, grads, exp_avgs, exp_avg_sqs, steps, group["lr"], beta1, beta2,
+                              group["weight_decay"], group["eps"], self._decoupled, group["maximize"])
+        return loss
+
+
+class LciAdam(_LciAdamStep, torch.optim.Adam):
+    def __init__(self, params, **kw):
+        torch.optim.Adam.__init__(self, params, fused=True, **kw)
+
+
+class LciAdamW(_LciAdamStep, torch.optim.AdamW):
+    _decoupled = True
+
+    def __init__(self, params, **kw):
+        torch.optim.AdamW.__init__(self, params, fused=True, **kw)
+
+
 def build_optimizer(params, config):
-    """The reference's optimizers (trainer_base.py; same hyper-parameters). On the GPU Adam / AdamW use torch's
-    fused single-kernel implementation (same update rule; the default multi-tensor version launched ~150 kernels per
-    step for the SwinUNETR parameter list, 6.4 ms per C3 step)."""
+    """The reference's optimizers (optim_base.py:87-93; same hyper-parameters). On the GPU Adam / AdamW update on
+    csrc/optim.hip (LciAdam / LciAdamW, torch-compatible state); LCI_HIP_ADAM=0 uses torch's fused kernel,
+    LCI_FUSED_ADAM=0 torch's multi-tensor one (~150 launches per SwinUNETR step, 6.4 ms per C3 step)."""
     o = config.optim
     params = list(params)
     fused = all(p.is_cuda for p in params) and os.environ.get("LCI_FUSED_ADAM", "1") != "0"
+    hip = fused and os.environ.get("LCI_HIP_ADAM", "1") != "0"
     if config.optim_type == "adam":
+        if hip:
+            return LciAdam(params, lr=o.lr, betas=(o.beta1, o.beta2), weight_decay=o.weight_decay)
         return torch.optim.Adam(params, lr=o.lr, betas=(o.beta1, o.beta2), weight_decay=o.weight_decay,
                                 fused=fused or None)
     if config.optim_type == "adamw":
+        if hip:
+            return LciAdamW(params, lr=o.lr, betas=(o.beta1, o.beta2), weight_decay=o.weight_decay)
         return torch.optim.AdamW(params, lr=o.lr, betas=(o.beta1, o.beta2), weight_decay=o.weight_decay,
                                  fused=fused or None)
     if config.optim_type == "nadam":
@@ -210,4 +265,4 @@ def synthetic_batch(config, batch, device, seed):
     return x.to(device), y.to(device)
 
 
-__all__ = ["init_distributed", "TrainStep", "synthetic_batch", "F"]
+__all__ = ["init_distributed", "TrainStep", "synthetic_batch", "LciAdam", "LciAdamW", "F"]
