@@ -25,7 +25,7 @@ from collections import defaultdict
 # KernelTimer name (bench.py) -> the liblci kernels it launches (rocprofv3 names carry template arguments)
 TIMER_KERNELS = {"conv3": r"conv3_fwd\w*_kernel", "conv3_wgrad": r"conv3_wgrad\w*_kernel",
                  "attn_bwd_dkdv": r"attn_bwd_dkdv\w*_kernel", "attn_bwd_dq": r"attn_bwd_dq\w*_kernel",
-                 "attn_fwd": r"attn_fwd\w*_kernel", "gemm_bt": r"gemm_bt_kernel", "window_attn_bwd": r"win_attn_bwd\w*_kernel",
+                 "attn_fwd": r"(?<!win_)attn_fwd\w*_kernel", "gemm_bt": r"gemm_bt_kernel", "window_attn_bwd": r"win_attn_bwd\w*_kernel",
                  "window_attn_fwd": r"win_attn_fwd\w*_kernel", "selective_scan_bwd": r"scan_bwd\w*_kernel",
                  "linear_wgrad": r"linear_wgrad\w*_kernel"}
 
