@@ -261,10 +261,9 @@ __global__ __launch_bounds__(512) void conv3_fwd_lds2_kernel(ConvArgs a) {
         for (int t = 0; t < NT; ++t)
           wa[t] = *(const bf16x8*)(sW + cpos2(dxi * 32 * NT + 32 * t + r, 2 * ks + h));
 #pragma unroll
-        for (int m = 0; m < ML; ++m) {
-          xb[m] = *(const bf16x8*)(sX + cpos2(wave * 32 * ML + 32 * m + r + dxi, 2 * ks + h));
-          if (!ok[m]) xb[m] = zero8();
-        }
+        for (int m = 0; m < ML; ++m)   // outside the volume: the zero chunk past the buffers (address select)
+          xb[m] = *(const bf16x8*)(ok[m] ? sX + cpos2(wave * 32 * ML + 32 * m + r + dxi, 2 * ks + h)
+                                         : smem2 + 2 * (XBUF + WBUF));
 #pragma unroll
         for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -274,6 +273,7 @@ __global__ __launch_bounds__(512) void conv3_fwd_lds2_kernel(ConvArgs a) {
   };
   load(sl0, vxA, vwA);
   store(0, vxA, vwA);
+  if (threadIdx.x == 0) *(u32x4*)(smem2 + 2 * (XBUF + WBUF)) = u32x4{0u, 0u, 0u, 0u};
   int buf = 0;
   __syncthreads();
   for (int sl = sl0; sl < sl1; ++sl) {
@@ -318,6 +318,7 @@ __global__ __launch_bounds__(512) void conv3_fwd_dma_kernel(ConvArgs a) {
   constexpr int XB = XU * 16 * 64, SLOT = XB + WU * 16 * 64;   // bytes
   extern __shared__ __attribute__((aligned(16))) char smem3[];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  __builtin_assume(wave >= 0 && wave < NWV);   // readfirstlane drops the range: lets each DMA piece's kind fold
   const int r = lane & 31, h = lane >> 5;
   long long vblk;
   int ntl, split = 0;
@@ -404,6 +405,7 @@ __global__ __launch_bounds__(512) void conv3_fwd_dma_kernel(ConvArgs a) {
       okzy[m] = inb[m] && (unsigned)(zc[m] + dz) < (unsigned)a.D && (unsigned)(yc[m] + dy) < (unsigned)a.H;
     const bf16* sX = (const bf16*)(smem3 + p * SLOT);
     const bf16* sW = (const bf16*)(smem3 + p * SLOT + XB);
+    const bf16* szero = (const bf16*)(smem3 + 2 * SLOT);
     bf16x8 wa[2][NT], xb[2][ML];
     auto rd = [&](int g, int s) __attribute__((always_inline)) {
       const int dxi = g >> 1, ks = g & 1;
@@ -411,8 +413,10 @@ __global__ __launch_bounds__(512) void conv3_fwd_dma_kernel(ConvArgs a) {
       for (int t = 0; t < NT; ++t) wa[s][t] = *(const bf16x8*)(sW + cpos2(dxi * 32 * NT + 32 * t + r, 2 * ks + h));
 #pragma unroll
       for (int m = 0; m < ML; ++m) {
-        xb[s][m] = *(const bf16x8*)(sX + cpos2(wave * 32 * ML + 32 * m + r + dxi, 2 * ks + h));
-        if (!(okzy[m] && (unsigned)(xc[m] + dxi - 1) < (unsigned)a.W)) xb[s][m] = zero8();
+        // a voxel whose tap falls outside the volume reads the 16 zero bytes past the slots (an address select, not
+        // a read then a conditional overwrite, which made the compiler drain every pending LDS read first)
+        const bool ok = okzy[m] && (unsigned)(xc[m] + dxi - 1) < (unsigned)a.W;
+        xb[s][m] = *(const bf16x8*)(ok ? sX + cpos2(wave * 32 * ML + 32 * m + r + dxi, 2 * ks + h) : szero);
       }
     };
     rd(0, 0);
@@ -432,6 +436,7 @@ __global__ __launch_bounds__(512) void conv3_fwd_dma_kernel(ConvArgs a) {
       __builtin_amdgcn_sched_barrier(0);
     }
   };
+  if (threadIdx.x == 0) *(u32x4*)(smem3 + 2 * SLOT) = u32x4{0u, 0u, 0u, 0u};   // published by the loop's barrier
   issue(sl0, 0);
   int p = 0;
   for (int sl = sl0; sl < sl1; ++sl) {
@@ -1023,7 +1028,7 @@ static int launch(const ConvArgs& a, hipStream_t st) {
     b.order = a.Cout >= 96 ? 1 : 0;
     const long long nb = (long long)b.nvb * b.ntile;
     constexpr int XU = (512 + 2 + 15) / 16, WU = 3 * 32 * NT / 16;
-    const size_t shd = (size_t)2 * (XU + WU) * 1024;
+    const size_t shd = (size_t)2 * (XU + WU) * 1024 + 16;   // two slots + the zero chunk
     if (a.nsplit > 1) {
       LCI_CHECK(a.part != nullptr, "conv3: split-K needs the partial workspace");
       LCI_CHECK(nb * a.nsplit < (1LL << 31), "conv3: too many workgroups");
@@ -1043,7 +1048,7 @@ static int launch(const ConvArgs& a, hipStream_t st) {
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         hipLaunchKernelGGL((conv3_fwd_dma_kernel<NT, false>), grid, dim3(512), shd, st, b);
       } else {   // Cout = 32: the register-staged v2 kernel (2-5 % ahead of the DMA one there)
-        const size_t sh = (size_t)2 * (514 * CLD2 + 3 * 32 * NT * CLD2) * sizeof(bf16);
+        const size_t sh = (size_t)2 * (514 * CLD2 + 3 * 32 * NT * CLD2) * sizeof(bf16) + 16;   // + the zero chunk
         (void)hipFuncSetAttribute((const void*)conv3_fwd_lds2_kernel<NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
         hipLaunchKernelGGL((conv3_fwd_lds2_kernel<NT>), grid, dim3(512), sh, st, b);
