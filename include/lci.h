@@ -56,8 +56,9 @@ extern "C" {
  * lci_window_attn_bwd pad_ws; 16: lci_attn_bwd delta_ws is (B, H, 2, L): the negated row constants -lse2 | -delta; 17: lci_window_bwd_needs_plain;
  * 18: lci_attn_bwd delta_ws is lci_attn_bwd_ws_bytes(B, H, L) bytes; 19: selective-scan checkpoints in the I/O
  * dtype; 20: lci_attn_gen_fwd / lci_attn_gen_bwd; 21: lci_gemm_bt; 22: lci_linear_fwd removed, superseded by
- * lci_gemm_bt; 23: lci_fftconv_spectrum Dv; 24: lci_inorm_finalize; 25: lci_adam_step). */
-#define LCI_ABI_VERSION 25
+ * lci_gemm_bt; 23: lci_fftconv_spectrum Dv; 24: lci_inorm_finalize; 25: lci_adam_step; 26: Hyena gate dx2 / gx2
+ * in the activation dtype). */
+#define LCI_ABI_VERSION 26
 const char* lci_last_error(void);
 int lci_abi_version(void);
 /* sha256 prefix of the sources the library was built from (build_lib.source_hash); the Python binding refuses a
@@ -287,12 +288,14 @@ int lci_hyena_pre_fwd(int dtype, const void* z, const float* w, const float* bia
                       int L, int H, int hd, int K, void* stream);
 /* out (BB, L, D) = y (BB, D, L) f32 * x2, channels-last. */
 int lci_hyena_post_fwd(int dtype, const float* y, const void* x2, void* out, int BB, int L, int D, void* stream);
-/* dy (BB, D, L) f32 = dout * x2; dx2 (BB, L, D) f32 = dout * y. */
-int lci_hyena_post_bwd(int dtype, const float* y, const void* x2, const void* dout, float* dy, float* dx2, int BB,
+/* dy (BB, D, L) f32 = dout * x2; dx2 (BB, L, D) = dout * y in the activation dtype (x2's). */
+int lci_hyena_post_bwd(int dtype, const float* y, const void* x2, const void* dout, float* dy, void* dx2, int BB,
                        int L, int D, void* stream);
-/* dz (BB, L, 3D) written; dw (3D, K), db (3D) accumulated. gx2: (BB, L, D) f32. */
+/* dz (BB, L, 3D) written; dw (3D, K), db (3D) accumulated. gx2: (BB, L, D) in the activation dtype, i.e. the
+ * post backward's dx2 as it is (ABI 26: dx2 / gx2 were f32, so the autograd engine cast dx2 to x2's bf16 and the
+ * caller cast it back). */
 int lci_hyena_pre_bwd(int dtype, const void* z, const float* w, const float* bias, const float* dvg,
-                      const float* gx2, void* dz, float* dw, float* db, int BB, int L, int H, int hd, int K,
+                      const void* gx2, void* dz, float* dw, float* db, int BB, int L, int H, int hd, int K,
                       void* stream);
 
 /* ------------------------------------------------------------------ Hyena implicit filter (order = D = 64)

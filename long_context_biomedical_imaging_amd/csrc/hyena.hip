@@ -1048,9 +1048,9 @@ struct GateArgs {
   void* out;            // (BB, L, D) channels-last (z dtype) = y * x2 (post)
   const void* dout;     // post bwd: (BB, L, D)
   float* dy;            // post bwd: (BB, D, L) f32 = dout * x2
-  void* dx2;            // post bwd: (BB, L, D) f32 = dout * y
+  void* dx2;            // post bwd: (BB, L, D) z dtype = dout * y (the dtype of x2, so no cast follows)
   const float* dvg;     // pre bwd: (BB, D, L)
-  const void* gx2;      // pre bwd: dL/dx2 (BB, L, D) (f32)
+  const void* gx2;      // pre bwd: dL/dx2 (BB, L, D) (z dtype)
   void* dz;             // pre bwd: (BB, L, 3D)
   float* dw; float* db; // pre bwd: (3D, K), (3D) accumulated
   int BB, L, D, H, hd, K;
@@ -1097,7 +1097,7 @@ __global__ __launch_bounds__(256) void hyena_post_bwd_kernel(GateArgs a) {
       const long long o = ((long long)bb * a.L + t) * a.D + ch;
       const float go = (float)((const T*)a.dout)[o];
       g = go * (float)((const T*)a.x2)[o];
-      ((float*)a.dx2)[o] = go * ty[cl][tl];
+      ((T*)a.dx2)[o] = (T)(go * ty[cl][tl]);
     }
     tg[cl][tl] = g;
   }
@@ -1201,7 +1201,7 @@ __global__ __launch_bounds__(256) void hyena_pre_bwd2_kernel(GateArgs a) {
   const int h = chc / a.hd, jj = chc - h * a.hd;
   const int c1 = h * 3 * a.hd + jj, c2 = c1 + a.hd, c3 = c1 + 2 * a.hd;
   const T* zb = (const T*)a.z + (long long)bb * L * D3;
-  const float* gx2 = (const float*)a.gx2 + (long long)bb * L * a.D + chc;
+  const T* gx2 = (const T*)a.gx2 + (long long)bb * L * a.D + chc;
   T* dzb = (T*)a.dz + (long long)bb * L * D3;
   float w1[KC], w2[KC], w3[KC];
 #pragma unroll
@@ -1238,7 +1238,7 @@ __global__ __launch_bounds__(256) void hyena_pre_bwd2_kernel(GateArgs a) {
         n1[u] = zld(zb, tn, L, D3, c1);
         n2[u] = zld(zb, tn, L, D3, c2);
         n3[u] = zld(zb, tn, L, D3, c3);
-        ng[u] = (tn < L && g + u < NIT) ? gx2[(long long)tn * a.D] : 0.f;
+        ng[u] = (tn < L && g + u < NIT) ? (float)gx2[(long long)tn * a.D] : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < HY_PF; ++u) {
@@ -1382,16 +1382,14 @@ __global__ __launch_bounds__(256) void hyena_post_bwd3_kernel(GateArgs a) {
     const long long o = ((long long)bb * L + t) * D + ch;
     const bf16x8 gv = *(const bf16x8*)((const bf16*)a.dout + o);
     const bf16x8 xv = *(const bf16x8*)((const bf16*)a.x2 + o);
-    f32x4 d0, d1;
+    bf16x8 dv;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float go = (float)gv[j];
       tg[(8 * q + j) * HG_S + tl] = go * (float)xv[j];
-      const float dx = go * ty[(8 * q + j) * HG_S + tl];
-      if (j < 4) d0[j] = dx; else d1[j - 4] = dx;
+      dv[j] = (bf16)(go * ty[(8 * q + j) * HG_S + tl]);
     }
-    *(f32x4*)((float*)a.dx2 + o) = d0;
-    *(f32x4*)((float*)a.dx2 + o + 4) = d1;
+    *(bf16x8*)((bf16*)a.dx2 + o) = dv;
   }
   __syncthreads();
   hg_store_cm(a.dy, tg, bb, ch0, t0, D, L);
@@ -1471,7 +1469,7 @@ __global__ __launch_bounds__(256) void hyena_pre_bwd3_kernel(GateArgs a) {
   const int ch = ch0 + lane, chc = min(ch, D - 1);
   const int c1 = hg_zcol(chc, 0, a.hd), c2 = c1 + a.hd, c3 = c1 + 2 * a.hd;
   const bf16* zb = (const bf16*)a.z + (long long)bb * L * D3;
-  const float* gx2 = (const float*)a.gx2 + (long long)bb * L * D;
+  const bf16* gx2 = (const bf16*)a.gx2 + (long long)bb * L * D;
   bf16* dzb = (bf16*)a.dz + (long long)bb * L * D3;
   float w1[KC], w2[KC], w3[KC];
 #pragma unroll
@@ -1492,11 +1490,15 @@ __global__ __launch_bounds__(256) void hyena_pre_bwd3_kernel(GateArgs a) {
       for (int j = 0; j < 4; ++j)
         if (c4 + j < W) dvt[r * WS + c4 + j] = v[j];
     }
-    for (int i = threadIdx.x; i < W4 * 4 * 16; i += 256) {      // gx2 rows (tokens), 64 channels
-      const int r = i >> 4, c4 = (i & 15) * 4, t = t0 + r, c = ch0 + c4;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (t < L && c < D) v = *(const f32x4*)(gx2 + (long long)t * D + c);
-      *(f32x4*)(gxt + r * 64 + c4) = v;
+    for (int i = threadIdx.x; i < W4 * 4 * 8; i += 256) {       // gx2 rows (tokens), 64 channels, bf16 -> f32
+      const int r = i >> 3, c8 = (i & 7) * 8, t = t0 + r, c = ch0 + c8;
+      bf16x8 v = {};
+      if (t < L && c < D) v = *(const bf16x8*)(gx2 + (long long)t * D + c);
+      f32x4 lo, hi;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { lo[j] = (float)v[j]; hi[j] = (float)v[4 + j]; }
+      *(f32x4*)(gxt + r * 64 + c8) = lo;
+      *(f32x4*)(gxt + r * 64 + c8 + 4) = hi;
     }
     __syncthreads();
     const int sl0 = wave * TW, s0 = t0 + sl0;
@@ -1788,7 +1790,7 @@ extern "C" int lci_hyena_post_fwd(int dtype, const float* y, const void* x2, voi
   return 0;
 }
 
-extern "C" int lci_hyena_post_bwd(int dtype, const float* y, const void* x2, const void* dout, float* dy, float* dx2,
+extern "C" int lci_hyena_post_bwd(int dtype, const float* y, const void* x2, const void* dout, float* dy, void* dx2,
                                   int BB, int L, int D, void* stream) {
   GateArgs a{};
   a.y = y; a.x2 = (void*)x2; a.dout = dout; a.dy = dy; a.dx2 = dx2; a.BB = BB; a.L = L; a.D = D; a.hd = 8;
@@ -1804,9 +1806,9 @@ extern "C" int lci_hyena_post_bwd(int dtype, const float* y, const void* x2, con
   return 0;
 }
 
-// dw (3D, K), db (3D) accumulated (caller zeroes). gx2 is f32 (BB, L, D).
+// dw (3D, K), db (3D) accumulated (caller zeroes). gx2 (BB, L, D) in z's dtype.
 extern "C" int lci_hyena_pre_bwd(int dtype, const void* z, const float* w, const float* bias, const float* dvg,
-                                 const float* gx2, void* dz, float* dw, float* db, int BB, int L, int H, int hd, int K,
+                                 const void* gx2, void* dz, float* dw, float* db, int BB, int L, int H, int hd, int K,
                                  void* stream) {
   LCI_CHECK(K >= 1 && K <= 8, "hyena_pre: short filter order %d unsupported (<= 8)", K);
   GateArgs a{};

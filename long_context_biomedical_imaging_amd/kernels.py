@@ -964,7 +964,9 @@ class _HyenaPre(torch.autograd.Function):
         K = wf.shape[1]
         f32 = dict(device=z.device, dtype=torch.float32)
         dvg = torch.zeros(BB, D, L, **f32) if dvg is None else dvg.float().contiguous()
-        dx2 = torch.zeros(BB, L, D, **f32) if dx2 is None else dx2.float().contiguous()
+        # dx2 in z's dtype (lci_hyena_post_bwd writes it in x2's = z's dtype: no cast either side, ABI 26)
+        dx2 = (torch.zeros(BB, L, D, device=z.device, dtype=z.dtype) if dx2 is None
+               else dx2.to(z.dtype).contiguous())
         dz = torch.empty_like(z)
         dw = torch.zeros(C3, K, **f32)
         db = torch.zeros(C3, **f32) if has_b else None
@@ -991,7 +993,7 @@ class _HyenaPost(torch.autograd.Function):
         BB, D, L = y.shape
         dout = dout.to(x2.dtype).contiguous()
         dy = torch.empty(BB, D, L, device=y.device, dtype=torch.float32)
-        dx2 = torch.empty(BB, L, D, device=y.device, dtype=torch.float32)
+        dx2 = torch.empty(BB, L, D, device=y.device, dtype=x2.dtype)   # x2's dtype: the engine casts nothing
         KernelTimer.run("hyena_post_bwd", 0.0, y, lambda: _lib.call(
             "lci_hyena_post_bwd", _DT[x2.dtype], y.data_ptr(), x2.data_ptr(), dout.data_ptr(), dy.data_ptr(),
             dx2.data_ptr(), BB, L, D, _lib.stream_of(y)))

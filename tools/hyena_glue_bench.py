@@ -38,7 +38,7 @@ def main():
     vg = torch.empty(B, D, L, device=dev, dtype=f32)
     x2 = torch.empty(B, L, D, device=dev, dtype=bf)
     dvg = torch.randn(B, D, L, device=dev, dtype=f32)
-    gx2 = torch.randn(B, L, D, device=dev, dtype=f32)
+    gx2 = torch.randn(B, L, D, device=dev, dtype=bf)   # ABI 26: the activation dtype
     dz = torch.empty_like(z)
     dw = torch.zeros(3 * D, K, device=dev, dtype=f32)
     db = torch.zeros(3 * D, device=dev, dtype=f32)
@@ -46,7 +46,7 @@ def main():
     out = torch.empty(B, L, D, device=dev, dtype=bf)
     dout = torch.randn(B, L, D, device=dev, dtype=bf)
     dy = torch.empty(B, D, L, device=dev, dtype=f32)
-    dx2 = torch.empty(B, L, D, device=dev, dtype=f32)
+    dx2 = torch.empty(B, L, D, device=dev, dtype=bf)
     st = _lib.stream_of(z)
     n = B * L * D
     cases = {
@@ -54,11 +54,11 @@ def main():
                                       x2.data_ptr(), B, L, H, hd, K, st), n * (3 * 2 + 4 + 2)),
         "pre_bwd": (lambda: _lib.call("lci_hyena_pre_bwd", 1, z.data_ptr(), w.data_ptr(), b.data_ptr(),
                                       dvg.data_ptr(), gx2.data_ptr(), dz.data_ptr(), dw.data_ptr(), db.data_ptr(),
-                                      B, L, H, hd, K, st), n * (3 * 2 + 4 + 4 + 3 * 2)),
+                                      B, L, H, hd, K, st), n * (3 * 2 + 4 + 2 + 3 * 2)),
         "post_fwd": (lambda: _lib.call("lci_hyena_post_fwd", 1, y.data_ptr(), x2.data_ptr(), out.data_ptr(), B, L, D,
                                        st), n * (4 + 2 + 2)),
         "post_bwd": (lambda: _lib.call("lci_hyena_post_bwd", 1, y.data_ptr(), x2.data_ptr(), dout.data_ptr(),
-                                       dy.data_ptr(), dx2.data_ptr(), B, L, D, st), n * (4 + 2 + 2 + 4 + 4)),
+                                       dy.data_ptr(), dx2.data_ptr(), B, L, D, st), n * (4 + 2 + 2 + 4 + 2)),
     }
     only = os.environ.get("GLUE_ONLY")
     for name, (fn, nbytes) in cases.items():
