@@ -138,12 +138,21 @@ class TransformerBlock(nn.Module):
         self.norm2 = TokenLayerNorm(hidden_size)
 
     def forward(self, x):
-        # x + attn(norm1(x)); x + mlp(norm2(x)) (backbone_vit.py:261-262), the residual gradient of each added
-        # inside the LayerNorm backward kernel
-        h, y = self.norm1.forward_residual(x)
-        h, y = self.norm2.forward_residual_add(h, self.attn(y))   # x + attn(.) summed inside the norm2 kernel
-        x = h + self.mlp(y)
-        return x
+        # x + attn(norm1(x)); x + mlp(norm2(x)) (backbone_vit.py:261-262)
+        _, h, m = self.forward_pair(x, None)
+        return h + m
+
+    def forward_pair(self, h, m):
+        """The block on the residual stream held as a pair: its input is h + m (m = the previous block's MLP output,
+        bf16, or None), summed inside the norm1 LayerNorm kernel instead of by a separate add; returns (h + m, the
+        stream after the attention residual, this block's MLP output). The residual gradient of each add is summed
+        inside the LayerNorm backward kernels, which also write m's bf16 gradient (no cast passes)."""
+        if m is None:
+            x, y = self.norm1.forward_residual(h)
+        else:
+            x, y = self.norm1.forward_residual_add(h, m)
+        h, y = self.norm2.forward_residual_add(x, self.attn(y))   # x + attn(.) summed inside the norm2 kernel
+        return x, h, self.mlp(y)
 
 
 class ViT_with_alt_ops(nn.Module):
@@ -188,12 +197,25 @@ class ViT_with_alt_ops(nn.Module):
             cls_token = self.cls_token.expand(x.shape[0], -1, -1)
             x = torch.cat((cls_token, x), dim=1)
         nck = len(self.blocks) if self.checkpoint_blocks is True else int(self.checkpoint_blocks or 0)
+        # the stream between un-checkpointed blocks as (h, m): block i + 1's norm1 kernel forms block i's output
+        # h + m, which is also what hidden_states_out records (the same tensor); only the last block's output is a
+        # separate add. Checkpointed blocks keep the stream as one tensor, so each checkpoint saves one input, not
+        # two (at 2^21 tokens the pair would add ~3 GB per block to the peak).
+        h, m = x, None
         for i, blk in enumerate(self.blocks):
             if i < nck and self.training and torch.is_grad_enabled():
-                x = torch.utils.checkpoint.checkpoint(blk, x, use_reentrant=False)
+                h = torch.utils.checkpoint.checkpoint(blk, h, use_reentrant=False)
+                hidden_states_out.append(h)
             else:
-                x = blk(x)
+                fused = m is not None
+                xin, h, m = blk.forward_pair(h, m)
+                if fused:
+                    hidden_states_out.append(xin)
+        if m is not None:
+            x = h + m
             hidden_states_out.append(x)
+        else:               # every block checkpointed (or none at all: the embedding, not recorded)
+            x = h
         x = self.norm(x)
         hidden_states_out.append(x)
         return hidden_states_out

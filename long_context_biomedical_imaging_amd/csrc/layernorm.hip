@@ -27,6 +27,7 @@ struct LnArgs {
   void* y;              // fwd: (rows, C) bf16 or f32
   const void* dy;       // bwd: (rows, C) bf16 or f32
   float* dx;            // bwd: (rows, C) f32
+  void* dxb;            // bwd: (rows, C) bf16 copy of dx, or null (the gradient of a bf16 branch output)
   const float* dres;    // bwd: (rows, C) f32 residual-path gradient added into dx, or null
   float* mean;          // (rows)
   float* rstd;          // (rows)
@@ -161,6 +162,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] += rstd * (g[k][j] - m1 - n[k][j] * m2);
         *(f32x4*)(a.dx + row * C + c) = o;
+        if (a.dxb) {   // the same value rounded for a bf16 branch output (no separate cast pass over dx)
+          bf16x4 hb;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) hb[j] = to_bf16(o[j]);
+          *(bf16x4*)((bf16*)a.dxb + row * C + c) = hb;
+        }
       }
     }
   }
@@ -251,16 +258,16 @@ extern "C" int lci_layernorm_add_fwd(const float* h, const void* add, int add_bf
 }
 
 extern "C" int lci_layernorm_bwd(const float* x, const void* dy, int bf16_dy, const float* gamma, const float* mean,
-                                 const float* rstd, const float* dres, float* dx, float* part, long long rows, int C,
-                                 void* stream) {
+                                 const float* rstd, const float* dres, float* dx, void* dxb, float* part, long long rows,
+                                 int C, void* stream) {
   if (ln_check(rows, C, x)) return 1;
   LCI_CHECK(!dres || ((uintptr_t)dres & 15) == 0, "layernorm: misaligned residual gradient");
   LCI_CHECK(((uintptr_t)dy & (bf16_dy ? 7 : 15)) == 0 && ((uintptr_t)gamma & 15) == 0 &&
-            ((uintptr_t)dx & 15) == 0, "layernorm: misaligned dy/gamma/dx");
+            ((uintptr_t)dx & 15) == 0 && ((uintptr_t)dxb & 7) == 0, "layernorm: misaligned dy/gamma/dx");
   LnArgs a = {};
   a.dres = dres;
   a.x = x; a.dy = dy; a.gamma = gamma; a.mean = const_cast<float*>(mean); a.rstd = const_cast<float*>(rstd);
-  a.dx = dx; a.part = part;
+  a.dx = dx; a.dxb = dxb; a.part = part;
   a.rows = rows; a.C = C; a.bf16_io = bf16_dy;
   const int nb = lci_layernorm_bwd_blocks(rows);
   const int NV = (C + 255) / 256;

@@ -1584,7 +1584,8 @@ def _ln_fwd(x, weight, bias, eps, bf16_out):
     return y, x2, mean, rstd
 
 
-def _ln_bwd(x2, weight, mean, rstd, dy, dres, shape):
+def _ln_bwd(x2, weight, mean, rstd, dy, dres, shape, want_bf16=False):
+    """dx (f32, `shape`), dgamma, dbeta [, dx rounded to bf16 in the same kernel pass when want_bf16]."""
     rows, C = x2.shape
     bf = dy.dtype == torch.bfloat16
     dy = (dy if bf else dy.float()).contiguous()
@@ -1595,13 +1596,16 @@ def _ln_bwd(x2, weight, mean, rstd, dy, dres, shape):
         if dres.data_ptr() % 16:
             dres = dres.clone()
     dx = torch.empty(rows, C, device=x2.device, dtype=torch.float32)
+    dxb = torch.empty(rows, C, device=x2.device, dtype=torch.bfloat16) if want_bf16 else None
     nblk = _lib.load().lci_layernorm_bwd_blocks(rows)
     part = torch.empty(nblk, 2, C, device=x2.device, dtype=torch.float32)
-    KernelTimer.run("ln_bwd", rows * C * (8 + dy.element_size() + (4 if dres is not None else 0)), x2,
-                    lambda: _lib.call("lci_layernorm_bwd", x2.data_ptr(), dy.data_ptr(), int(bf), weight.data_ptr(),
-                                      mean.data_ptr(), rstd.data_ptr(), _lib.ptr(dres), dx.data_ptr(),
-                                      part.data_ptr(), rows, C, _lib.stream_of(x2)))
+    KernelTimer.run("ln_bwd", rows * C * (8 + dy.element_size() + (4 if dres is not None else 0) + (2 if want_bf16 else 0)),
+                    x2, lambda: _lib.call("lci_layernorm_bwd", x2.data_ptr(), dy.data_ptr(), int(bf), weight.data_ptr(),
+                                          mean.data_ptr(), rstd.data_ptr(), _lib.ptr(dres), dx.data_ptr(),
+                                          _lib.ptr(dxb), part.data_ptr(), rows, C, _lib.stream_of(x2)))
     s = part.sum(0)
+    if want_bf16:
+        return dx.view(shape), s[0], s[1], dxb.view(shape)
     return dx.view(shape), s[0], s[1]
 
 
@@ -1671,6 +1675,9 @@ class _AddResidualLayerNorm(torch.autograd.Function):
         xsum, weight, mean, rstd = ctx.saved_tensors
         if dy is None:
             dx, dw, db = dx_out, None, None
+        elif ctx.adtype == torch.bfloat16:   # the bf16 branch gradient written by the same kernel pass
+            dx, dw, db, da = _ln_bwd(xsum, weight, mean, rstd, dy, dx_out, ctx.shape, want_bf16=True)
+            return dx, da, dw, db, None, None
         else:
             dx, dw, db = _ln_bwd(xsum, weight, mean, rstd, dy, dx_out, ctx.shape)
         if dx is None:

@@ -152,6 +152,8 @@ def test_add_residual_layernorm(adtype):
     assert rel_err(y, F.layer_norm(h + a, (C,), w, b, 1e-5)) < 1e-6
     (((x + y @ P) * cot).sum()).backward()
     assert ac.grad.dtype == adtype
+    # the bf16 branch gradient is written by the LN backward kernel: h's f32 gradient rounded once
+    assert torch.equal(ac.grad, hc.grad.to(adtype))
     assert rel_err(hc.grad, hr.grad) < 1e-5
     assert rel_err(ac.grad, ar.grad) < (1e-5 if adtype == torch.float32 else 1e-2)
     assert rel_err(wc.grad, wr.grad) < 1e-5
