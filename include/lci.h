@@ -57,8 +57,8 @@ extern "C" {
  * 18: lci_attn_bwd delta_ws is lci_attn_bwd_ws_bytes(B, H, L) bytes; 19: selective-scan checkpoints in the I/O
  * dtype; 20: lci_attn_gen_fwd / lci_attn_gen_bwd; 21: lci_gemm_bt; 22: lci_linear_fwd removed, superseded by
  * lci_gemm_bt; 23: lci_fftconv_spectrum Dv; 24: lci_inorm_finalize; 25: lci_adam_step; 26: Hyena gate dx2 / gx2
- * in the activation dtype; 27: lci_layernorm_bwd dxb). */
-#define LCI_ABI_VERSION 27
+ * in the activation dtype; 27: lci_layernorm_bwd dxb; 28: lci_resample_cl_fwd, lci_resample1d_adj_ac). */
+#define LCI_ABI_VERSION 28
 const char* lci_last_error(void);
 int lci_abi_version(void);
 /* sha256 prefix of the sources the library was built from (build_lib.source_hash); the Python binding refuses a
@@ -324,6 +324,17 @@ int lci_upsample3d_cl_fwd(const float* x, void* y, int B, int C, int D, int H, i
                           void* stream);
 int lci_resample1d_adj(const void* dy, int dy_bf16, float* dx, long long outer, int n_out, int n_in, long long inner,
                        void* stream);
+/* ------------------------------------------------ linear re-sampling to any size, align_corners either way (ABI 28)
+ * FPN_fuse's resize (seg_heads.py:49-50, :74 / :181-182, :206, F.interpolate(x, size, mode=(bi|tri)linear, align_corners=True))
+ * and PSPModule's up-sampling of the pooled bins (seg_heads.py:44 / :176): x (B, D, H, W, C) channels-last (f32, or
+ * bf16 when x_bf16) -> y (B, OD, OH, OW, C) f32 [+ add of y's shape (f32, or bf16 when add_bf16), summed in the same
+ * pass]; bilinear when D = OD = 1. torch's scale and source-index arithmetic (area_pixel_compute_scale /
+ * _source_index). lci_resample1d_adj_ac is the one-axis adjoint with the same align_corners choice (deterministic
+ * gathers in place of torch's atomic upsample backward). C % 8 == 0, inner % 8 == 0, 16-byte aligned. */
+int lci_resample_cl_fwd(const void* x, int x_bf16, const void* add, int add_bf16, float* y, int B, int C, int D, int H,
+                        int W, int OD, int OH, int OW, int align_corners, void* stream);
+int lci_resample1d_adj_ac(const void* dy, int dy_bf16, float* dx, long long outer, int n_out, int n_in,
+                          long long inner, int align_corners, void* stream);
 
 long long lci_hyena_filter_img_elems(void);
 long long lci_hyena_filter_partials(int L, int E);

@@ -14,7 +14,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_LIB = os.path.join(HERE, "liblci.so")
 LIB_PATH = os.environ.get("LCI_LIB_PATH", DEFAULT_LIB)   # override: kernel-variant A/B runs (no staleness check)
-ABI_VERSION = 27   # include/lci.h LCI_ABI_VERSION
+ABI_VERSION = 28   # include/lci.h LCI_ABI_VERSION
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -72,6 +72,8 @@ SIGNATURES = {
     "lci_upsample2x_nhwc_bwd": [_P, _P, _I, _I, _I, _I, _P],
     "lci_upsample3d_cl_fwd": [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "lci_resample1d_adj": [_P, _I, _P, _L, _I, _I, _L, _P],
+    "lci_resample1d_adj_ac": [_P, _I, _P, _L, _I, _I, _L, _I, _P],
+    "lci_resample_cl_fwd": [_P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "lci_direct_conv_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _P],
     "lci_window_gather": [_P, _P, _I, _P, _I, _P],
     "lci_mamba_proj_dims": [_I, _I, _I, _P],

@@ -224,7 +224,10 @@ static const LwTile kLwTiles[] = {{4, 3, 1, 4}, {2, 4, 2, 3}, {2, 2, 2, 3}, {2, 
                                   {2, 2, 1, 3}, {2, 1, 3, 1}, {1, 3, 3, 1}, {1, 1, 2, 2}};
 constexpr int kLwNTiles = (int)(sizeof(kLwTiles) / sizeof(kLwTiles[0]));
 
-// The first tile with the least padded work; -1 if every tile more than doubles the work.
+// The first tile with the least padded work; -1 if every tile more than doubles the work. Narrow outputs (N x K <=
+// 8192: the Mamba x_proj / dt_proj gradients of the Swin recipes, 24 x 48, 48 x 8, 32 x 96, 96 x 16) take the tile
+// with the least padding whatever it is: their cost is streaming the M token rows, not the padded MFMAs (hipBLASLt
+// ran 24 x 48 over 2^19 tokens in 0.27 ms, 15x the rows' read time).
 static int lw_pick(int N, int K) {
   int best = -1;
   double bw = 0.0;
@@ -235,6 +238,14 @@ static int lw_pick(int N, int K) {
     const double waste = padded / ((double)N * K);
     if (t == kLwNTiles - 1 && best >= 0) break;
     if (waste <= 2.0 && (best < 0 || waste < bw - 1e-9)) { best = t; bw = waste; }
+  }
+  if (best < 0 && (long long)N * K <= 8192) {
+    for (int t = 0; t < kLwNTiles; ++t) {
+      const LwTile& c = kLwTiles[t];
+      const int tn = 32 * c.mb * c.wn, tk = 32 * c.cb * c.wc;
+      const double padded = (double)((N + tn - 1) / tn * tn) * ((K + tk - 1) / tk * tk);
+      if (best < 0 || padded < bw - 1e-9) { best = t; bw = padded; }
+    }
   }
   return best;
 }

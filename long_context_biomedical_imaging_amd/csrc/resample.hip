@@ -255,47 +255,190 @@ __global__ __launch_bounds__(256) void upsample3d_cl_fwd_kernel(Up3Args a) {
 struct Adj1Args {
   const void* dy; float* dx;
   long long outer, inner;
-  int n_out, n_in, dy_bf16;
+  int n_out, n_in, dy_bf16, ac;
   float scale;
 };
+
+// align_corners=True taps (torch: scale = (in - 1) / (out - 1), 0 for one output; src = scale * o)
+__device__ __forceinline__ void lin_taps_ac(int o, int n, float scale, int& i0, int& i1, float& l0, float& l1) {
+  const float src = __fmul_rn(scale, (float)o);
+  i0 = (int)src;
+  i1 = i0 + (i0 < n - 1 ? 1 : 0);
+  l1 = __fsub_rn(src, (float)i0);
+  l0 = __fsub_rn(1.f, l1);
+}
+
+// Outputs [lo, hi] whose source coordinate lies in (i - 1, i + 1] (one extra on each side covers the f32 rounding),
+// and the weight of input i in output o (the sum of both taps: they coincide at the borders).
+__device__ __forceinline__ void adj_range(const Adj1Args& a, int i, int& lo, int& hi) {
+  const float r = 1.f / a.scale;    // outputs per input sample
+  if (a.ac) {
+    lo = a.scale > 0.f ? max(0, (int)floorf(((float)i - 1.f) * r) - 1) : 0;
+    hi = a.scale > 0.f ? min(a.n_out - 1, (int)ceilf(((float)i + 1.f) * r) + 1) : a.n_out - 1;
+  } else {
+    lo = max(0, (int)floorf(((float)i - 1.f + 0.5f) * r - 0.5f) - 1);
+    hi = min(a.n_out - 1, (int)ceilf(((float)i + 1.f + 0.5f) * r - 0.5f) + 1);
+  }
+}
+
+__device__ __forceinline__ float adj_weight(const Adj1Args& a, int o, int i) {
+  int i0, i1;
+  float l0, l1;
+  if (a.ac) lin_taps_ac(o, a.n_in, a.scale, i0, i1, l0, l1);
+  else lin_taps(o, a.n_in, a.scale, i0, i1, l0, l1);
+  return (i0 == i ? l0 : 0.f) + (i1 == i ? l1 : 0.f);
+}
+
+__device__ __forceinline__ void adj_acc(const Adj1Args& a, long long off, float w, float (&acc)[8]) {
+  if (a.dy_bf16) {
+    const bf16x8 g = *(const bf16x8*)((const bf16*)a.dy + off);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = fmaf(w, (float)g[k], acc[k]);
+  } else {
+    const f32x4 g0 = *(const f32x4*)((const float*)a.dy + off), g1 = *(const f32x4*)((const float*)a.dy + off + 4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      acc[k] = fmaf(w, g0[k], acc[k]);
+      acc[4 + k] = fmaf(w, g1[k], acc[4 + k]);
+    }
+  }
+}
 
 __global__ __launch_bounds__(256) void resample1d_adj_kernel(Adj1Args a) {
   const long long I8 = a.inner / 8;
   const long long total = a.outer * a.n_in * I8;
-  const float r = 1.f / a.scale;    // outputs per input sample
   for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
     const long long q = t % I8;
     long long p = t / I8;
     const int i = (int)(p % a.n_in);
     const long long ou = p / a.n_in;
-    // outputs whose source coordinate lies in (i - 1, i + 1]; one extra on each side covers the f32 rounding
-    const int lo = max(0, (int)floorf(((float)i - 1.f + 0.5f) * r - 0.5f) - 1);
-    const int hi = min(a.n_out - 1, (int)ceilf(((float)i + 1.f + 0.5f) * r - 0.5f) + 1);
+    int lo, hi;
+    adj_range(a, i, lo, hi);
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int o = lo; o <= hi; ++o) {
-      int i0, i1;
-      float l0, l1;
-      lin_taps(o, a.n_in, a.scale, i0, i1, l0, l1);
-      const float w = (i0 == i ? l0 : 0.f) + (i1 == i ? l1 : 0.f);
+      const float w = adj_weight(a, o, i);
       if (w == 0.f) continue;
-      const long long off = (ou * a.n_out + o) * a.inner + 8 * q;
-      if (a.dy_bf16) {
-        const bf16x8 g = *(const bf16x8*)((const bf16*)a.dy + off);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) acc[k] = fmaf(w, (float)g[k], acc[k]);
-      } else {
-        const f32x4 g0 = *(const f32x4*)((const float*)a.dy + off), g1 = *(const f32x4*)((const float*)a.dy + off + 4);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          acc[k] = fmaf(w, g0[k], acc[k]);
-          acc[4 + k] = fmaf(w, g1[k], acc[4 + k]);
-        }
-      }
+      adj_acc(a, (ou * a.n_out + o) * a.inner + 8 * q, w, acc);
     }
     float* o = a.dx + (ou * a.n_in + i) * a.inner + 8 * q;
     *(f32x4*)o = f32x4{acc[0], acc[1], acc[2], acc[3]};
     *(f32x4*)(o + 4) = f32x4{acc[4], acc[5], acc[6], acc[7]};
   }
+}
+
+// The same adjoint where each input sample gathers many outputs (the PSP's 1-6 pooled bins up-sampled to the
+// feature grid: up to n_out per input): one thread per output there was ~1 wave per CU, each looping over hundreds of
+// dependent-address loads. Here a workgroup takes (outer, i, 8 consecutive 8-element chunks of inner): 32 lanes
+// per chunk split the output range (o = lo + s, lo + s + 32, ...), and the 32 partials are summed in LDS in a fixed
+// order (deterministic).
+constexpr int ADJ_WIDE_S = 32;
+__global__ __launch_bounds__(256) void resample1d_adj_wide_kernel(Adj1Args a) {
+  __shared__ float red[ADJ_WIDE_S][8][9];
+  const long long I8 = a.inner / 8, QB = (I8 + 7) / 8;
+  const int c = threadIdx.x & 7, s = threadIdx.x >> 3;
+  const long long blk = blockIdx.x;
+  const long long qb = blk % QB;
+  const long long p = blk / QB;
+  const int i = (int)(p % a.n_in);
+  const long long ou = p / a.n_in;
+  const long long q = qb * 8 + c;
+  int lo, hi;
+  adj_range(a, i, lo, hi);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (q < I8) {
+    for (int o = lo + s; o <= hi; o += ADJ_WIDE_S) {
+      const float w = adj_weight(a, o, i);
+      if (w == 0.f) continue;
+      adj_acc(a, (ou * a.n_out + o) * a.inner + 8 * q, w, acc);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[s][c][k] = acc[k];
+  __syncthreads();
+  if (threadIdx.x < 64) {   // (chunk c2, element k2): the 32 partials in order s = 0 .. 31
+    const int c2 = threadIdx.x >> 3, k2 = threadIdx.x & 7;
+    float v = 0.f;
+#pragma unroll 8
+    for (int ss = 0; ss < ADJ_WIDE_S; ++ss) v += red[ss][c2][k2];
+    const long long q2 = qb * 8 + c2;
+    if (q2 < I8) a.dx[(ou * a.n_in + i) * a.inner + 8 * q2 + k2] = v;
+  }
+}
+
+// ------------------------------------------------ linear re-sampling to any size, f32 out (align_corners either way)
+// FPN_fuse's resize (seg_heads.py:49-50, :74 / :181-182, :206: F.interpolate(x, size, mode=(bi|tri)linear, align_corners=True),
+// f32 under autocast) and PSPModule's up-sampling of the pooled bins (seg_heads.py:44 / :176), on channels-last maps
+// (2-D as D = OD = 1): one thread per (output voxel, 8-channel chunk), torch's upsample_{bilinear2d,trilinear3d}
+// expression in f32 (products unfused), plus an optional addend of the output's shape summed in the same pass (the
+// FPN's `resize(f) + lateral`, an f32 add as torch's). Input and addend f32 or bf16 (read as f32: the cast autocast
+// would apply is exact). The adjoint is resample1d_adj per axis (deterministic gathers, no atomic scatter).
+struct RsArgs {
+  const void* x; const void* add; float* y;
+  int B, C, D, H, W, OD, OH, OW;
+  float sd, sh, sw;
+  int x_bf16, add_bf16, ac;
+};
+
+__device__ __forceinline__ void rs_taps(int ac, int o, int n, float scale, int& i0, int& i1, float& l0, float& l1) {
+  if (ac) lin_taps_ac(o, n, scale, i0, i1, l0, l1);
+  else lin_taps(o, n, scale, i0, i1, l0, l1);
+}
+
+__device__ __forceinline__ void ld8f(const void* p, long long off, bool bf, float (&v)[8]) {
+  if (bf) {
+    const bf16x8 g = *(const bf16x8*)((const bf16*)p + off);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = (float)g[k];
+  } else {
+    const f32x4 g0 = *(const f32x4*)((const float*)p + off), g1 = *(const f32x4*)((const float*)p + off + 4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { v[k] = g0[k]; v[4 + k] = g1[k]; }
+  }
+}
+
+// grid (ceil(OW * C/8 / 256), OH, B * OD)
+__global__ __launch_bounds__(256) void resample_cl_fwd_kernel(RsArgs a) {
+  const int C8 = a.C / 8;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.OW * C8) return;
+  const int ox = i / C8, q = i - ox * C8;
+  const int oy = blockIdx.y, oz = blockIdx.z % a.OD, b = blockIdx.z / a.OD;
+  int d0, d1, h0, h1, w0, w1;
+  float dl0, dl1, hl0, hl1, wl0, wl1;
+  rs_taps(a.ac, oz, a.D, a.sd, d0, d1, dl0, dl1);
+  rs_taps(a.ac, oy, a.H, a.sh, h0, h1, hl0, hl1);
+  rs_taps(a.ac, ox, a.W, a.sw, w0, w1, wl0, wl1);
+  const bool bf = a.x_bf16 != 0;
+  const long long base = (long long)b * a.D * a.H * a.W * a.C + 8 * q;
+  auto at = [&](int d, int h, int w) { return base + (((long long)d * a.H + h) * a.W + w) * a.C; };
+  float x000[8], x001[8], x010[8], x011[8];
+  ld8f(a.x, at(d0, h0, w0), bf, x000); ld8f(a.x, at(d0, h0, w1), bf, x001);
+  ld8f(a.x, at(d0, h1, w0), bf, x010); ld8f(a.x, at(d0, h1, w1), bf, x011);
+  float v[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    v[k] = __fadd_rn(__fmul_rn(hl0, __fadd_rn(__fmul_rn(wl0, x000[k]), __fmul_rn(wl1, x001[k]))),
+                     __fmul_rn(hl1, __fadd_rn(__fmul_rn(wl0, x010[k]), __fmul_rn(wl1, x011[k]))));
+  if (a.D > 1 || a.OD > 1) {   // trilinear: t0 * (plane d0) + t1 * (plane d1)
+    float x100[8], x101[8], x110[8], x111[8];
+    ld8f(a.x, at(d1, h0, w0), bf, x100); ld8f(a.x, at(d1, h0, w1), bf, x101);
+    ld8f(a.x, at(d1, h1, w0), bf, x110); ld8f(a.x, at(d1, h1, w1), bf, x111);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float p1 = __fadd_rn(__fmul_rn(hl0, __fadd_rn(__fmul_rn(wl0, x100[k]), __fmul_rn(wl1, x101[k]))),
+                                 __fmul_rn(hl1, __fadd_rn(__fmul_rn(wl0, x110[k]), __fmul_rn(wl1, x111[k]))));
+      v[k] = __fadd_rn(__fmul_rn(dl0, v[k]), __fmul_rn(dl1, p1));
+    }
+  }
+  const long long oo = ((((long long)b * a.OD + oz) * a.OH + oy) * a.OW + ox) * a.C + 8 * q;
+  if (a.add != nullptr) {
+    float r[8];
+    ld8f(a.add, oo, a.add_bf16 != 0, r);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = __fadd_rn(v[k], r[k]);
+  }
+  *(f32x4*)(a.y + oo) = f32x4{v[0], v[1], v[2], v[3]};
+  *(f32x4*)(a.y + oo + 4) = f32x4{v[4], v[5], v[6], v[7]};
 }
 
 static unsigned up_grid(long long items) {
@@ -368,17 +511,56 @@ extern "C" int lci_upsample3d_cl_fwd(const float* x, void* y, int B, int C, int 
   return 0;
 }
 
+// torch's area_pixel_compute_scale for linear modes without a scale factor
+static float rs_scale(int n_in, int n_out, int ac) {
+  if (ac) return n_out > 1 ? (float)(n_in - 1) / (float)(n_out - 1) : 0.f;
+  return (float)n_in / (float)n_out;
+}
+
 // Adjoint of linear interpolation along one axis: dy (outer, n_out, inner) (bf16 if dy_bf16 else f32) ->
-// dx (outer, n_in, inner) f32, scale = n_in / n_out (align_corners=False). inner % 8 == 0, 16-byte aligned.
-extern "C" int lci_resample1d_adj(const void* dy, int dy_bf16, float* dx, long long outer, int n_out, int n_in,
-                                  long long inner, void* stream) {
+// dx (outer, n_in, inner) f32, align_corners as given. inner % 8 == 0, 16-byte aligned.
+extern "C" int lci_resample1d_adj_ac(const void* dy, int dy_bf16, float* dx, long long outer, int n_out, int n_in,
+                                     long long inner, int align_corners, void* stream) {
   LCI_CHECK(outer > 0 && n_out > 0 && n_in > 0 && inner > 0 && inner % 8 == 0,
             "resample1d_adj: bad shape outer=%lld n_out=%d n_in=%d inner=%lld", outer, n_out, n_in, inner);
   LCI_CHECK(((uintptr_t)dy & 15) == 0 && ((uintptr_t)dx & 15) == 0, "resample1d_adj: pointers must be 16-byte aligned");
   Adj1Args a{};
   a.dy = dy; a.dx = dx; a.outer = outer; a.inner = inner; a.n_out = n_out; a.n_in = n_in; a.dy_bf16 = dy_bf16;
-  a.scale = (float)n_in / (float)n_out;
-  hipLaunchKernelGGL(resample1d_adj_kernel, dim3(up_grid(outer * n_in * (inner / 8))), dim3(256), 0,
+  a.ac = align_corners ? 1 : 0;
+  a.scale = rs_scale(n_in, n_out, a.ac);
+  if (n_out >= 16 * n_in) {   // >= ~32 outputs per input: the split-range kernel
+    const long long nblk = outer * n_in * ((inner / 8 + 7) / 8);
+    LCI_CHECK(nblk < (1LL << 31), "resample1d_adj: grid too large");
+    hipLaunchKernelGGL(resample1d_adj_wide_kernel, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, a);
+  } else {
+    hipLaunchKernelGGL(resample1d_adj_kernel, dim3(up_grid(outer * n_in * (inner / 8))), dim3(256), 0,
+                       (hipStream_t)stream, a);
+  }
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+
+// The align_corners=False adjoint (UperNet3D's final re-sampling).
+extern "C" int lci_resample1d_adj(const void* dy, int dy_bf16, float* dx, long long outer, int n_out, int n_in,
+                                  long long inner, void* stream) {
+  return lci_resample1d_adj_ac(dy, dy_bf16, dx, outer, n_out, n_in, inner, 0, stream);
+}
+
+// Linear re-sampling (bilinear for D = OD = 1, else trilinear) of x (B, D, H, W, C) channels-last (f32, or bf16 when
+// x_bf16) to y (B, OD, OH, OW, C) f32 [+ add (B, OD, OH, OW, C), f32 or bf16 when add_bf16], align_corners as given.
+// C % 8 == 0; pointers 16-byte aligned.
+extern "C" int lci_resample_cl_fwd(const void* x, int x_bf16, const void* add, int add_bf16, float* y, int B, int C,
+                                   int D, int H, int W, int OD, int OH, int OW, int align_corners, void* stream) {
+  LCI_CHECK(B > 0 && C > 0 && D > 0 && H > 0 && W > 0 && OD > 0 && OH > 0 && OW > 0 && C % 8 == 0,
+            "resample: bad shape B=%d C=%d in %dx%dx%d out %dx%dx%d", B, C, D, H, W, OD, OH, OW);
+  LCI_CHECK((((uintptr_t)x | (uintptr_t)add | (uintptr_t)y) & 15) == 0, "resample: pointers must be 16-byte aligned");
+  LCI_CHECK((long long)B * OD <= 65535 && OH <= 65535, "resample: output too large for the grid");
+  RsArgs a{};
+  a.x = x; a.add = add; a.y = y; a.B = B; a.C = C; a.D = D; a.H = H; a.W = W; a.OD = OD; a.OH = OH; a.OW = OW;
+  a.ac = align_corners ? 1 : 0;
+  a.sd = rs_scale(D, OD, a.ac); a.sh = rs_scale(H, OH, a.ac); a.sw = rs_scale(W, OW, a.ac);
+  a.x_bf16 = x_bf16; a.add_bf16 = add_bf16;
+  hipLaunchKernelGGL(resample_cl_fwd_kernel, dim3((OW * (C / 8) + 255) / 256, OH, B * OD), dim3(256), 0,
                      (hipStream_t)stream, a);
   LCI_LAUNCH_CHECK();
   return 0;

@@ -489,6 +489,13 @@ _SEP_CACHE = {}
 # channels-last views of 1x1 maps).
 UPERNET_CL = os.environ.get("LCI_UPERNET_CL", "1") != "0"
 
+# The FPN's align_corners re-sampling (up_and_add and the final resize to the finest level) and the PSP's
+# up-sampling of the pooled bins on lci_resample_cl_fwd (one pass, the FPN's lateral add summed in it) with a
+# deterministic one-axis-at-a-time adjoint (kernels.resample_cl): torch's upsample_bilinear2d_backward is an atomic
+# scatter (3.2 ms per 514^2 -> 512^2 x 384 call at C4) and the separable GEMMs run as batched hipBLASLt calls on
+# 4-36 element matrices at the 3-D shapes (~0.1-0.5 ms each, ~5 ms per Swin-recipe step).
+HIP_RESAMPLE = os.environ.get("LCI_HIP_RESAMPLE", "1") != "0"
+
 
 def _is_cl(x):
     """A 4-D map in channels-last memory that is not also plain-contiguous (and big enough to matter)."""
@@ -608,7 +615,10 @@ class PSPModule(nn.Module):
                 y = _pool_cl(features, stage[0].output_size)
                 for m in list(stage)[1:]:
                     y = m(y)
-                up = _up_cl(y, size)
+                if HIP_RESAMPLE and kernels.resample_cl_supported(y, size):
+                    up = kernels.resample_cl(y, size, True)
+                else:
+                    up = _up_cl(y, size)
                 pyramids.append(up if up.dtype == y.dtype else up.to(y.dtype))
             return self.bottleneck(_cat_channels(pyramids))
         if SEPARABLE_PSP and features.is_cuda:
@@ -617,7 +627,10 @@ class PSPModule(nn.Module):
                 y = adaptive_avg_pool(features, stage[0].output_size)
                 for m in list(stage)[1:]:
                     y = m(y)
-                up = upsample_align_corners(y, size)
+                if HIP_RESAMPLE and kernels.resample_cl_supported(y, size):
+                    up = kernels.resample_cl(y, size, True)
+                else:
+                    up = upsample_align_corners(y, size)
                 pyramids.append(up if up.dtype == y.dtype else up.to(y.dtype))
         else:
             pyramids = [features] + [F.interpolate(stage(features), size=size, mode=mode, align_corners=True)
@@ -663,12 +676,21 @@ class FPN_fuse(nn.Module):
         def resize(x, size):
             if tuple(x.shape[2:]) == tuple(size):
                 return x.to(_interp_dtype(x, mode))
+            if HIP_RESAMPLE and kernels.resample_cl_supported(x, size):
+                return kernels.resample_cl(x, size, True).to(_interp_dtype(x, mode))
             if SEPARABLE_PSP and x.is_cuda and not _is_cl(x):
                 # separable GEMMs (f32, as torch's kernel) whose backward is a GEMM, not an atomic scatter
                 return upsample_align_corners(x, size).to(_interp_dtype(x, mode))
             return F.interpolate(x, size=size, mode=mode, align_corners=True)
 
-        P = [resize(features[i], features[i - 1].shape[2:]) + features[i - 1] for i in reversed(range(1, len(features)))]
+        def up_and_add(x, y):   # seg_heads.py:49-50 / :181-182
+            size = y.shape[2:]
+            if (tuple(x.shape[2:]) != tuple(size) and HIP_RESAMPLE and _interp_dtype(x, mode) == torch.float32
+                    and kernels.resample_cl_supported(x, size, y)):
+                return kernels.resample_cl(x, size, True, add=y)   # the f32 sum, in the re-sampling pass
+            return resize(x, size) + y
+
+        P = [up_and_add(features[i], features[i - 1]) for i in reversed(range(1, len(features)))]
         P = [sc(x) for sc, x in zip(self.smooth_conv, P)]
         P = list(reversed(P))
         P.append(features[-1])

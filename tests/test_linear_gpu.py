@@ -33,7 +33,9 @@ def _check(dy, x, bias):
 
 @pytest.mark.parametrize("M,N,K", [(1000, 384, 384), (4099, 1536, 384), (3001, 384, 1536), (2500, 1152, 384),
                                    (777, 40, 192), (70001, 384, 384), (300, 288, 96), (1234, 96, 96),
-                                   (2049, 192, 768), (65, 768, 384), (1, 384, 384)])
+                                   (2049, 192, 768), (65, 768, 384), (1, 384, 384),
+                                   # narrow outputs (any padding): Swin-recipe Mamba x_proj / dt_proj gradients
+                                   (5003, 24, 48), (4000, 48, 8), (3333, 32, 96), (2999, 96, 16), (1 << 19, 24, 48)])
 def test_linear_wgrad_vs_fp64(M, N, K):
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     dy = torch.randn(M, N, device="cuda", generator=g).to(torch.bfloat16)
