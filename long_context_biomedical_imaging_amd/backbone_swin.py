@@ -16,7 +16,6 @@ WindowAttention.forward(x, mask) keeps the reference signature (pre-partitioned 
 """
 from __future__ import annotations
 
-import itertools
 from collections.abc import Sequence
 
 import numpy as np
@@ -26,7 +25,7 @@ import torch.nn.functional as F
 
 from . import kernels
 from .blocks import MLPBlock as Mlp
-from .blocks import PatchEmbed, TokenLayerNorm, TokenLinear, trunc_normal_
+from .blocks import PatchEmbed, TokenLayerNorm, TokenLinear, layer_norm_no_affine, trunc_normal_
 from .hyena import HyenaOperator
 from .mamba import MambaVisionMixer
 
@@ -283,6 +282,8 @@ class PatchMergingV2(nn.Module):
     def __init__(self, dim: int, norm_layer: type[nn.LayerNorm] = nn.LayerNorm, spatial_dims: int = 3) -> None:
         super().__init__()
         self.dim = dim
+        if norm_layer is nn.LayerNorm:   # same parameters and init; its output is the reduction's bf16 operand
+            norm_layer = TokenLayerNorm
         if spatial_dims == 3:
             self.reduction = TokenLinear(8 * dim, 2 * dim, bias=False)
             self.norm = norm_layer(8 * dim)
@@ -296,12 +297,19 @@ class PatchMergingV2(nn.Module):
             b, d, h, w, c = x_shape
             if (h % 2 == 1) or (w % 2 == 1) or (d % 2 == 1):
                 x = F.pad(x, (0, 0, 0, w % 2, 0, h % 2, 0, d % 2))
-            x = torch.cat([x[:, i::2, j::2, k::2, :] for i, j, k in itertools.product(range(2), range(2), range(2))], -1)
+            # = torch.cat([x[:, i::2, j::2, k::2, :] for i, j, k in product(range(2), repeat=3)], -1) as one
+            # permuted copy: the eight strided slices' backward accumulated eight full-size gradients (seven adds)
+            b, d, h, w, c = x.shape
+            x = (x.view(b, d // 2, 2, h // 2, 2, w // 2, 2, c).permute(0, 1, 3, 5, 2, 4, 6, 7)
+                 .reshape(b, d // 2, h // 2, w // 2, 8 * c))
         elif len(x_shape) == 4:
             b, h, w, c = x_shape
             if (h % 2 == 1) or (w % 2 == 1):
                 x = F.pad(x, (0, 0, 0, w % 2, 0, h % 2))
-            x = torch.cat([x[:, j::2, i::2, :] for i, j in itertools.product(range(2), range(2))], -1)
+            # = torch.cat([x[:, j::2, i::2, :] for i, j in product(range(2), range(2))], -1) (block = 2 (w parity)
+            # + h parity) as one permuted copy
+            b, h, w, c = x.shape
+            x = x.view(b, h // 2, 2, w // 2, 2, c).permute(0, 1, 3, 4, 2, 5).reshape(b, h // 2, w // 2, 4 * c)
         return self.reduction(self.norm(x))
 
 
@@ -415,7 +423,7 @@ class SwinTransformer_with_alt_ops(nn.Module):
             nd = x.dim() - 2
             ch = x.shape[1]
             x = x.permute(0, *range(2, 2 + nd), 1)
-            x = F.layer_norm(x, [ch])
+            x = layer_norm_no_affine(x)
             x = x.permute(0, nd + 1, *range(1, nd + 1))
         return x
 

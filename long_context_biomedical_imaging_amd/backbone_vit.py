@@ -16,7 +16,7 @@ import torch.nn as nn
 import torch.utils.checkpoint
 
 from . import kernels
-from .blocks import MLPBlock, PatchEmbeddingBlock, TokenLayerNorm, TokenLinear
+from .blocks import MLPBlock, OutLayerNorm, PatchEmbeddingBlock, TokenLayerNorm, TokenLinear
 from .hyena import HyenaOperator
 from .mamba import MambaVisionMixer
 
@@ -179,7 +179,7 @@ class ViT_with_alt_ops(nn.Module):
         self.blocks = nn.ModuleList([
             TransformerBlock(use_hyena, use_mamba, hidden_size, mlp_dim, num_heads, dropout_rate, qkv_bias,
                              save_attn, hyena_l_max=hyena_l_max) for _ in range(num_layers)])
-        self.norm = nn.LayerNorm(hidden_size)
+        self.norm = OutLayerNorm(hidden_size)
         # Not a reference option: per-block activation checkpointing (recompute each block's forward in the
         # backward) for token counts whose saved activations exceed one GPU (256^3 p2: ~35 GB per block).
         # True = every block; an int k = the first k blocks only (the rest keep their activations: less recompute

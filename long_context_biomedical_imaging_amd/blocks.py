@@ -58,6 +58,33 @@ class TokenLayerNorm(nn.LayerNorm):
         return kernels.residual_layer_norm(x, self.weight, self.bias, self.eps, self._bf16_out())
 
 
+class OutLayerNorm(nn.LayerNorm):
+    """nn.LayerNorm (same parameters, keys, init) whose f32 result is a model output rather than a Linear operand:
+    ViT_with_alt_ops.norm (backbone_vit.py:368, :390), run on the HIP LayerNorm kernels with f32 out (what nn.LayerNorm
+    returns under autocast); torch's layer_norm on the CPU."""
+
+    def forward(self, x):
+        if x.is_cuda:
+            return kernels.layer_norm(x, self.weight, self.bias, self.eps, False)
+        return super().forward(x)
+
+
+_UNIT_AFFINE = {}
+
+
+def layer_norm_no_affine(x: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
+    """F.layer_norm(x, [C]) without affine parameters (SwinTransformer.proj_out, backbone_swin.py:866-873), f32 out,
+    on the HIP LayerNorm kernels (unit gamma / zero beta) on the GPU."""
+    if not x.is_cuda:
+        return torch.nn.functional.layer_norm(x, [x.shape[-1]], eps=eps)
+    key = (x.shape[-1], x.device)
+    wb = _UNIT_AFFINE.get(key)
+    if wb is None:
+        wb = (torch.ones(x.shape[-1], device=x.device), torch.zeros(x.shape[-1], device=x.device))
+        _UNIT_AFFINE[key] = wb
+    return kernels.layer_norm(x, wb[0], wb[1], eps, False)
+
+
 class TokenLinear(nn.Linear):
     """nn.Linear (same parameters, state_dict keys and seeded init) for the token-wise projections. On the GPU
     (kernels.linear) the forward and data gradient run on lci_gemm_bt where it takes the shape (hipBLASLt otherwise),

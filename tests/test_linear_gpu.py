@@ -14,6 +14,8 @@
 import pytest
 import torch
 
+from golden_util import rel_err
+
 pytestmark = pytest.mark.gpu
 
 
@@ -251,3 +253,28 @@ def test_conv_up_interleave_and_cat_bit_exact(nd, Cin, Cout, Cs, k, monkeypatch)
         res.append((y.detach(), xi.grad, ct.weight.grad.clone(), ct.bias.grad.clone(), si.grad if Cs else None))
     for name, a, b in zip(("y", "dx", "dW", "db", "dskip"), res[0], res[1]):
         assert (a is None and b is None) or torch.equal(a, b), name
+
+
+@pytest.mark.parametrize("bias", [True, False])
+def test_linear_one_input_channel_outer_product(bias):
+    """K = 1 (the 1-channel image into encoder1's 1x1 residual conv) runs as an outer product: bitwise the autocast
+    F.linear result (the bf16 x bf16 product is exact in f32, both round the same f32 value once), weight / bias
+    gradients within the bf16 rounding the autocast GEMM applies to its dW."""
+    from long_context_biomedical_imaging_amd import kernels
+    torch.manual_seed(4)
+    x = torch.randn(70001, 1, device="cuda")
+    w = torch.randn(96, 1, device="cuda", requires_grad=True)
+    b = torch.randn(96, device="cuda", requires_grad=True) if bias else None
+    w2 = w.detach().clone().requires_grad_(True)
+    b2 = b.detach().clone().requires_grad_(True) if bias else None
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        ref = torch.nn.functional.linear(x, w, b)
+        y = kernels.linear(x, w2, b2)
+    assert y.dtype == ref.dtype == torch.bfloat16
+    assert torch.equal(y, ref)
+    g = torch.randn_like(ref)
+    ref.float().backward(g.float())
+    y.float().backward(g.float())
+    assert rel_err(w2.grad, w.grad) < 1e-2
+    if bias:
+        assert rel_err(b2.grad, b.grad) < 1e-2

@@ -225,3 +225,24 @@ def test_gemm_bt_routing():
     assert kernels.gemm_bt_preferred(131072, 384) and kernels.gemm_bt_preferred(262144, 384)
     assert kernels.gemm_bt_preferred(32768, 768)                    # 128 x 2 tiles
     assert not kernels.gemm_bt_preferred(4096, 1536) and not kernels.gemm_bt_preferred(512, 3072)
+
+
+def test_patch_merging_permute_equals_cat_of_slices():
+    """PatchMergingV2's merge as one permuted copy equals the reference's cat of the 8 (3-D) / 4 (2-D) strided slices
+    (backbone_swin.py PatchMergingV2.forward), odd sizes padded first."""
+    import itertools
+
+    import torch.nn.functional as F
+    from long_context_biomedical_imaging_amd import backbone_swin
+    torch.manual_seed(0)
+    for shape in ((2, 6, 4, 8, 5), (1, 3, 5, 7, 2), (2, 6, 4, 5), (1, 5, 7, 3)):
+        m = backbone_swin.PatchMergingV2(shape[-1], spatial_dims=len(shape) - 2)
+        m.norm, m.reduction = torch.nn.Identity(), torch.nn.Identity()
+        x = torch.randn(*shape)
+        if len(shape) == 5:
+            xp = F.pad(x, (0, 0, 0, shape[3] % 2, 0, shape[2] % 2, 0, shape[1] % 2))
+            ref = torch.cat([xp[:, i::2, j::2, k::2, :] for i, j, k in itertools.product(range(2), repeat=3)], -1)
+        else:
+            xp = F.pad(x, (0, 0, 0, shape[2] % 2, 0, shape[1] % 2))
+            ref = torch.cat([xp[:, j::2, i::2, :] for i, j in itertools.product(range(2), range(2))], -1)
+        assert torch.equal(m(x), ref)
