@@ -185,6 +185,8 @@ class ViT_with_alt_ops(nn.Module):
         # True = every block; an int k = the first k blocks only (the rest keep their activations: less recompute
         # where the memory allows it).
         self.checkpoint_blocks = False
+        # hidden_states_out indices some consumer reads (None: all); the others are returned as None
+        self.keep_hidden = None
         if self.classification and not use_hyena and not use_mamba:
             self.cls_token = nn.Parameter(torch.zeros(1, 1, hidden_size))
 
@@ -197,25 +199,33 @@ class ViT_with_alt_ops(nn.Module):
             cls_token = self.cls_token.expand(x.shape[0], -1, -1)
             x = torch.cat((cls_token, x), dim=1)
         nck = len(self.blocks) if self.checkpoint_blocks is True else int(self.checkpoint_blocks or 0)
-        # the stream between un-checkpointed blocks as (h, m): block i + 1's norm1 kernel forms block i's output
+        # The residual stream between blocks is the pair (h, m): block i + 1's norm1 kernel forms block i's output
         # h + m, which is also what hidden_states_out records (the same tensor); only the last block's output is a
-        # separate add. Checkpointed blocks keep the stream as one tensor, so each checkpoint saves one input, not
-        # two (at 2^21 tokens the pair would add ~3 GB per block to the peak).
+        # separate add. A checkpointed block saves its inputs, so where its input is also a recorded hidden state
+        # the stream is materialised as one tensor there (the add; the checkpoint and the list share it) -- the pair
+        # would hold h, m and the sum. keep_hidden (set by EncoderDecoderModel from the decoder's taps) leaves the
+        # block outputs no decoder reads as None, so untapped checkpoint boundaries keep the pair (+1 bf16 tensor per
+        # boundary, 1.6 GB at 2^21 tokens) and skip the add, its recompute and its backward cast.
+        def keep(idx):
+            return self.keep_hidden is None or idx in self.keep_hidden
+
+        train = self.training and torch.is_grad_enabled()
         h, m = x, None
         for i, blk in enumerate(self.blocks):
-            if i < nck and self.training and torch.is_grad_enabled():
-                h = torch.utils.checkpoint.checkpoint(blk, h, use_reentrant=False)
-                hidden_states_out.append(h)
+            if i < nck and train:
+                xin, h, m = torch.utils.checkpoint.checkpoint(blk.forward_pair, h, m, use_reentrant=False)
             else:
-                fused = m is not None
                 xin, h, m = blk.forward_pair(h, m)
-                if fused:
-                    hidden_states_out.append(xin)
+            if i > 0:   # xin = block i - 1's output, hidden_states_out[i]
+                hidden_states_out.append(xin if keep(i) else None)
+            if i + 1 < min(nck, len(self.blocks)) and train and keep(i + 1):
+                h, m = h + m, None   # a recorded input of a checkpointed block: one tensor
         if m is not None:
             x = h + m
-            hidden_states_out.append(x)
-        else:               # every block checkpointed (or none at all: the embedding, not recorded)
+        else:               # no blocks (the embedding, not recorded) or a materialised last output
             x = h
+        if len(self.blocks):
+            hidden_states_out.append(x)
         x = self.norm(x)
         hidden_states_out.append(x)
         return hidden_states_out

@@ -311,6 +311,8 @@ class SwinUNETR(nn.Module):
 class ViTUNETR(nn.Module):
     """enhance_heads.py:187-356 (feature_size 32, taps h3/h6/h9 + final LN)."""
 
+    hidden_taps = (4, 7, 10)   # hidden_states_out indices read besides [0] and [-1] (hs[3], hs[6], hs[9])
+
     def __init__(self, config, input_feature_channels, output_feature_channels):
         super().__init__()
         fs = 32
@@ -624,7 +626,12 @@ class PSPModule(nn.Module):
         if SEPARABLE_PSP and features.is_cuda:
             pyramids = [features]
             for stage in self.stages:
-                y = adaptive_avg_pool(features, stage[0].output_size)
+                if features.numel() <= (1 << 21):
+                    # a small map (Swin's last stage, 4^3 x 768 at 128^3): torch's own pooling kernel; the separable
+                    # form runs as batched hipBLASLt calls on 4-36 element matrices (~0.15 ms each)
+                    y = stage[0](features)
+                else:
+                    y = adaptive_avg_pool(features, stage[0].output_size)
                 for m in list(stage)[1:]:
                     y = m(y)
                 if HIP_RESAMPLE and kernels.resample_cl_supported(y, size):
@@ -706,6 +713,7 @@ class _UperNet(nn.Module):
             self.upernet_feature_channels = [-4, -3, -2, -1]
         elif config.encoder_name == "ViT":
             self.upernet_feature_channels = [4, 7, 10, -1]
+            self.hidden_taps = (4, 7, 10)   # the encoder's other block outputs are not read (keep_hidden)
         else:
             raise ValueError(f"encoder_name {config.encoder_name} not recognized or comaptible with UperNet3D")
         chans = [input_feature_channels[c] for c in self.upernet_feature_channels]

@@ -44,6 +44,11 @@ class EncoderDecoderModel(nn.Module):
             self.decoder = UperNet3D(config, self.encoder_feature_channels, output_feature_channels)
         else:
             raise NotImplementedError(f"Decoder not implemented: {decoder_name}")
+        # the encoder's hidden states this decoder reads (besides the input and the final output); the encoder may
+        # return the others as None (ViT_with_alt_ops.keep_hidden: no sum kept alive only for the list)
+        taps = getattr(self.decoder, "hidden_taps", None)
+        if taps is not None and hasattr(self.encoder, "keep_hidden"):
+            self.encoder.keep_hidden = frozenset(taps)
 
     @property
     def device(self):

@@ -59,12 +59,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("workload")
     ap.add_argument("--rows", type=int, default=50)
+    ap.add_argument("--ckpt", type=int, default=None, help="checkpointed encoder blocks (default: bench.py's)")
     a = ap.parse_args()
     batch = 1 if a.workload in ("swin_p2_128", "vit_mamba_p2_256") else 2
     cfg = lconfig.parse_config(list(bench.WORKLOADS[a.workload]) + ["--batch_size", str(batch)])
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
     model = EncoderDecoderModel(cfg, cfg.encoder_name, cfg.decoder_name, cfg.no_in_channel, cfg.no_out_channel).to(dev)
+    ckpt = a.ckpt if a.ckpt is not None else (10 if a.workload == "vit_mamba_p2_256" else 0)
+    if ckpt:
+        model.encoder.checkpoint_blocks = ckpt
     tr = TrainStep(model, cfg, dev, ddp=False)
     x, y = synthetic_batch(cfg, batch, dev, seed=1234)
     for _ in range(2):
