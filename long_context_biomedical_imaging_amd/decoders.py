@@ -197,9 +197,17 @@ class UnetResBlock(nn.Module):
 
     def forward(self, inp):
         if self.fused and _hip(inp, HIP_CONV_3D if inp.dim() == 5 else HIP_CONV_2D):
-            out = kernels.instance_norm_act(self.conv1(inp), True)
+            if (self.downsample and isinstance(self.conv3.conv, (Conv1x1, Conv1x1_2d)) and self.conv3.conv.bias is None
+                    and self.conv3.conv.stride == (1,) * (inp.dim() - 2)
+                    and kernels.res_convs_supported(inp, self.conv1.conv.weight, self.conv3.conv.weight)):
+                # conv1 and the 1x1 residual conv read the same input: one backward node sums their input
+                # gradients inside the GEMM
+                c1, r = kernels.res_convs(inp, self.conv1.conv.weight, self.conv3.conv.weight)
+                out = kernels.instance_norm_act(c1, True)
+            else:
+                out = kernels.instance_norm_act(self.conv1(inp), True)
+                r = self.conv3(inp) if self.downsample else inp
             c2 = self.conv2(out)
-            r = self.conv3(inp) if self.downsample else inp
             # norm2 (+ norm3) + residual add + LeakyReLU in one pass where the operands are bf16 channels-last
             z = kernels.inorm_add_lrelu(c2, r, self.downsample)
             if z is not None:

@@ -526,10 +526,12 @@ class _MambaProj(torch.autograd.Function):
             bc.data_ptr(), dtl.data_ptr(), ldl, M, Dx, R, N2, _lib.stream_of(xs)))
         ctx.save_for_backward(xs, dtl, w2t, w1t)
         ctx.meta = (R, N2, Wx.shape, Wdt.shape)
-        return dt, bc
+        # xs again as an output: the scan reads this alias, so its input gradient du arrives here and is added to
+        # dxs inside lci_mamba_proj_bwd instead of by an autograd add of two (B, L, Dx) gradients
+        return dt, bc, xs.view_as(xs)
 
     @staticmethod
-    def backward(ctx, gdt, gbc):
+    def backward(ctx, gdt, gbc, gu):
         xs, dtl, w2t, w1t = ctx.saved_tensors
         R, N2, wxs, wds = ctx.meta
         Bb, L, Dx = xs.shape
@@ -540,9 +542,14 @@ class _MambaProj(torch.autograd.Function):
         ldx = -(-(R + N2) // 8) * 8
         dxs = torch.empty(Bb, L, Dx, **b16)
         dxdbl = torch.empty(Bb, L, ldx, **b16)
+        if gu is not None:
+            gu = gu.to(torch.bfloat16).contiguous()
+            if gu.data_ptr() % 16:
+                gu = gu.clone()
         KernelTimer.run("mamba_proj_bwd", 0.0, xs, lambda: _lib.call(
-            "lci_mamba_proj_bwd", gdt.data_ptr(), Dx, gbc.data_ptr(), w2t.data_ptr(), w1t.data_ptr(), None, 0,
-            dxs.data_ptr(), Dx, dxdbl.data_ptr(), ldx, M, Dx, R, N2, _lib.stream_of(xs)))
+            "lci_mamba_proj_bwd", gdt.data_ptr(), Dx, gbc.data_ptr(), w2t.data_ptr(), w1t.data_ptr(), _lib.ptr(gu),
+            Dx if gu is not None else 0, dxs.data_ptr(), Dx, dxdbl.data_ptr(), ldx, M, Dx, R, N2,
+            _lib.stream_of(xs)))
         dW, _ = _wgrad_any(dxdbl.view(M, ldx), xs.reshape(M, Dx), False)
         dWd, db = _wgrad_any(gdt.view(M, Dx), dtl.view(M, -1), True)
         return dxs, dW[:R + N2].reshape(wxs), dWd[:, :R].reshape(wds), db, None, None
@@ -566,9 +573,11 @@ def mamba_proj_supported(xs: torch.Tensor, Dx: int, R: int, N2: int) -> bool:
     return not (Dx % 16 or N2 % 8 or R + N2 > 64 or Dx > 1024)
 
 
-def mamba_proj(xs, Wx, Wdt, bias, R, N2):
-    """(dt (B, L, Dx) bf16, bc (B, L, 2N) bf16 = [B | C]) of MambaVisionMixer's x_proj / dt_proj (mamba.py:120-124)."""
-    return _MambaProj.apply(xs, Wx, Wdt, bias, R, N2)
+def mamba_proj(xs, Wx, Wdt, bias, R, N2, with_u=False):
+    """(dt (B, L, Dx) bf16, bc (B, L, 2N) bf16 = [B | C]) of MambaVisionMixer's x_proj / dt_proj (mamba.py:120-124);
+    with_u: also xs itself for the scan to read, whose gradient is then summed inside the projection's backward."""
+    dt, bc, u = _MambaProj.apply(xs, Wx, Wdt, bias, R, N2)
+    return (dt, bc, u) if with_u else (dt, bc)
 
 
 # ------------------------------------------------------------------------------------ window attention
@@ -1535,6 +1544,72 @@ def conv3(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = Non
     if bias is not None:
         y = y + bias.to(y.dtype).view(1, -1, *([1] * (y.dim() - 2)))
     return y
+
+
+class _ResConvs(torch.autograd.Function):
+    """UnetResBlock's conv1 (3x3[x3], stride 1, no bias) and conv3 (1x1 residual projection, no bias) of the same
+    input (MONAI-1.3 UnetResBlock via enhance_heads.py:30-356) as one node: the forward is conv3_cl and the 1x1 GEMM
+    as before; the backward computes conv1's data gradient and adds conv3's (dr . W3) into it with the GEMM itself
+    (addmm_, beta = 1) instead of autograd summing two full-resolution gradients (C5's 512-channel 256^3 input: 8.6 GB
+    per pass). That sum is rounded once (the unfused path rounds dr . W3 to bf16 first: <= 1 bf16 ulp apart)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, w3, nd):
+        kd = 3 if nd == 3 else 1
+        Cin = w1.shape[1]
+        x_cl = _to_cl(x, nd)
+        c1 = conv3_cl(x_cl, _conv3_pack(w1, kd, 0, Cin), kd)
+        x2 = x_cl.view(-1, Cin)
+        w3b = w3.reshape(w3.shape[0], Cin).to(torch.bfloat16)
+        N3 = w3b.shape[0]
+        if HIP_GEMM and gemm_bt_preferred(x2.shape[0], N3) and gemm_bt_supported(x2, N3, Cin):
+            r2 = gemm_bt(x2, w3b)
+        else:
+            with torch.autocast("cuda", enabled=False):
+                r2 = torch.nn.functional.linear(x2, w3b)
+        ctx.save_for_backward(x_cl, w1, w3b)
+        ctx.nd, ctx.w3shape, ctx.w3dtype = nd, w3.shape, w3.dtype
+        return _from_cl(c1, nd), _from_cl(r2.view(*x_cl.shape[:-1], N3), nd)
+
+    @staticmethod
+    def backward(ctx, dc1, dr):
+        x_cl, w1, w3b = ctx.saved_tensors
+        nd = ctx.nd
+        kd = 3 if nd == 3 else 1
+        Cin = w1.shape[1]
+        N3 = w3b.shape[0]
+        dy_cl = _to_cl(dc1, nd) if dc1 is not None else None
+        dr2 = _to_cl(dr, nd).view(-1, N3) if dr is not None else None
+        dx = dw1 = dw3 = None
+        if ctx.needs_input_grad[0] and (dy_cl is not None or dr2 is not None):
+            if dy_cl is not None:
+                dx = conv3_cl(dy_cl, _conv3_pack(w1, kd, 1, Cin), kd)      # (B, D, H, W, Cin) bf16
+                if dr2 is not None:
+                    dx.view(-1, Cin).addmm_(dr2, w3b)                        # += dr . W3 in the GEMM
+            else:
+                dx = (dr2 @ w3b).view(*x_cl.shape)
+            dx = _from_cl(dx, nd)
+        if ctx.needs_input_grad[1] and dy_cl is not None:
+            dw1 = conv3_wgrad_cl(x_cl, dy_cl, kd).to(w1.dtype)
+        if ctx.needs_input_grad[2] and dr2 is not None:
+            x2 = x_cl.view(-1, Cin)
+            if linear_wgrad_supported(dr2, x2):
+                dw3, _ = linear_wgrad(dr2, x2, False)
+            else:
+                dw3 = (dr2.t() @ x2).float()
+            dw3 = dw3.reshape(ctx.w3shape).to(ctx.w3dtype)
+        return dx, dw1, dw3, None
+
+
+def res_convs_supported(x: torch.Tensor, w1: torch.Tensor, w3: torch.Tensor) -> bool:
+    """_ResConvs takes GPU maps whose conv channel counts are multiples of 32 (the UNETR decoder blocks)."""
+    return (x.is_cuda and w1.shape[0] % 32 == 0 and w1.shape[1] % 32 == 0 and w3.shape[0] == w1.shape[0]
+            and w3.shape[1] == w1.shape[1] and all(k == 1 for k in w3.shape[2:]) and x.shape[1] == w1.shape[1])
+
+
+def res_convs(x: torch.Tensor, w1: torch.Tensor, w3: torch.Tensor):
+    """(conv3x3(x, w1), conv1x1(x, w3)) in bf16, channels-last strides; one backward node (see _ResConvs)."""
+    return _ResConvs.apply(x, w1, w3, w1.dim() - 2)
 
 
 # ------------------------------------------------------- decoder-head instance norm (+ LeakyReLU), channels-last

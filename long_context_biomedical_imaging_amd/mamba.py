@@ -81,9 +81,11 @@ class MambaVisionMixer(nn.Module):
         Dx = self.d_inner // 2
         if kernels.mamba_proj_supported(xs, Dx, R, 2 * N) and self.dt_proj.bias is not None:
             # bf16 autocast: x_proj -> split -> dt_proj in one HIP pass (lci_mamba_proj_fwd); [B | C] as one aligned
-            # (B, L, 2N) tensor the scan reads in place
-            dt, bc = kernels.mamba_proj(xs, self.x_proj.weight, self.dt_proj.weight, self.dt_proj.bias, R, 2 * N)
-            y = kernels.selective_scan_cl(xs, dt, A, bc, None, self.D.float(), self.dt_proj.bias.float(), yz)
+            # (B, L, 2N) tensor the scan reads in place; the scan's u is the projection's alias of xs, so its
+            # gradient is added inside the projection's backward kernel
+            dt, bc, u = kernels.mamba_proj(xs, self.x_proj.weight, self.dt_proj.weight, self.dt_proj.bias, R, 2 * N,
+                                           with_u=True)
+            y = kernels.selective_scan_cl(u, dt, A, bc, None, self.D.float(), self.dt_proj.bias.float(), yz)
             return self.out_proj(y)
         if (R * es) % 16 or ((R + 2 * N) * es) % 16 or (N * es) % 16:
             # the scan reads B / C rows with 16-byte vectors: when dt_rank breaks their alignment (Swin stages,
