@@ -57,8 +57,8 @@ extern "C" {
  * 18: lci_attn_bwd delta_ws is lci_attn_bwd_ws_bytes(B, H, L) bytes; 19: selective-scan checkpoints in the I/O
  * dtype; 20: lci_attn_gen_fwd / lci_attn_gen_bwd; 21: lci_gemm_bt; 22: lci_linear_fwd removed, superseded by
  * lci_gemm_bt; 23: lci_fftconv_spectrum Dv; 24: lci_inorm_finalize; 25: lci_adam_step; 26: Hyena gate dx2 / gx2
- * in the activation dtype; 27: lci_layernorm_bwd dxb; 28: lci_resample_cl_fwd, lci_resample1d_adj_ac). */
-#define LCI_ABI_VERSION 28
+ * in the activation dtype; 27: lci_layernorm_bwd dxb; 28: lci_resample_cl_fwd, lci_resample1d_adj_ac; 29: lci_bn_relu_*). */
+#define LCI_ABI_VERSION 29
 const char* lci_last_error(void);
 int lci_abi_version(void);
 /* sha256 prefix of the sources the library was built from (build_lib.source_hash); the Python binding refuses a
@@ -189,6 +189,18 @@ int lci_inorm_chunks(long long V, int B);
 int lci_inorm_reduce(const void* x, const void* dz, const float* stats, float* part, long long V, int B, int C,
                      int act, float slope, void* stream);
 int lci_inorm_finalize(const float* part, float* out, long long V, int B, int C, int mode, float eps, void* stream);
+/* Training BatchNorm + ReLU (UperNet PSPModule.bottleneck / FPN_fuse.conv_fusion, seg_heads.py:26-31, :60-63,
+ * :158-163, :192-195) over x (V, C) bf16 channels-last = every voxel of the batch; stats (2, C) = (mean, rstd) from
+ * lci_inorm_reduce / lci_inorm_finalize with B = 1. Forward y (V, C) f32 = relu((x - mean) rstd w + b). Backward:
+ * part (2, C, lci_inorm_chunks(V, 1)) sums of g = dy [y > 0] and g xhat (dy f32 when dy_f32, else bf16), then
+ * lci_inorm_finalize mode 1 -> coef (2, C) means, then dx (V, C) bf16 = (g - coef0 - xhat coef1) rstd w.
+ * C % 8 == 0, C <= 2048, 16-byte aligned. */
+int lci_bn_relu_fwd(const void* x, const float* stats, const float* w, const float* b, float* y, long long V, int C,
+                    void* stream);
+int lci_bn_relu_bwd_reduce(const void* x, const void* dy, int dy_f32, const float* stats, const float* w,
+                           const float* b, float* part, long long V, int C, void* stream);
+int lci_bn_relu_bwd_apply(const void* x, const void* dy, int dy_f32, const float* stats, const float* coef,
+                          const float* w, const float* b, void* dx, long long V, int C, void* stream);
 int lci_inorm_apply(const void* x, const void* dz, const float* stats, const float* coef, void* out, long long V,
                     int B, int C, int act, float slope, void* stream);
 /* UnetResBlock's tail, lrelu(norm2(x) + r), in one pass with the unfused bf16 roundings: out (B, V, C) bf16 =

@@ -14,7 +14,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_LIB = os.path.join(HERE, "liblci.so")
 LIB_PATH = os.environ.get("LCI_LIB_PATH", DEFAULT_LIB)   # override: kernel-variant A/B runs (no staleness check)
-ABI_VERSION = 28   # include/lci.h LCI_ABI_VERSION
+ABI_VERSION = 29   # include/lci.h LCI_ABI_VERSION
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -54,6 +54,9 @@ SIGNATURES = {
     "lci_conv3_wgrad": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "lci_inorm_reduce": [_P, _P, _P, _P, _L, _I, _I, _I, _F, _P],
     "lci_inorm_finalize": [_P, _P, _L, _I, _I, _I, _F, _P],
+    "lci_bn_relu_fwd": [_P, _P, _P, _P, _P, _L, _I, _P],
+    "lci_bn_relu_bwd_reduce": [_P, _P, _I, _P, _P, _P, _P, _L, _I, _P],
+    "lci_bn_relu_bwd_apply": [_P, _P, _I, _P, _P, _P, _P, _P, _L, _I, _P],
     "lci_inorm_apply": [_P, _P, _P, _P, _P, _L, _I, _I, _I, _F, _P],
     "lci_inorm_apply_res": [_P, _P, _P, _P, _P, _L, _I, _I, _F, _P],
     "lci_layernorm_fwd": [_P, _P, _P, _P, _I, _P, _P, _L, _I, _F, _P],

@@ -200,11 +200,171 @@ __global__ __launch_bounds__(256) void inorm_finalize_kernel(const float* __rest
   }
 }
 
+// ------------------------------------------------------------------ BatchNorm (training) + ReLU, channels-last
+// UperNet's conv -> BatchNorm -> ReLU (seg_heads.py PSPModule bottleneck :23-27 / FPN conv_fusion :59-62, the 2-D
+// and 3-D heads) on the conv's bf16 channels-last output: the batch statistics are the instance-norm reduction over
+// all B * V voxels as one sample (lci_inorm_reduce / _finalize with B = 1); these kernels apply the affine map and the
+// ReLU (f32 out, what autocast's fp32 batch_norm returns) and run the backward: g = dy * [y > 0], the channel sums of
+// g and g * xhat (partials, then lci_inorm_finalize mode 1), dx = (g - mean(g) - xhat mean(g xhat)) rstd w in x's
+// dtype. Per element torch's expression order: xhat = (x - mean) * rstd, y = xhat * w + b.
+struct BnArgs {
+  const bf16* x;          // (V, C)
+  const void* dy;         // bwd: (V, C) f32 or bf16
+  const float* stats;     // (2, C): mean, rstd
+  const float* coef;      // bwd apply: (2, C): mean(g), mean(g xhat)
+  const float* w; const float* b;
+  void* out;              // fwd: y f32; bwd: dx bf16
+  float* part;            // bwd reduce: (2, C, nchunk)
+  long long V, chunk;
+  int C, nchunk, dy_f32;
+};
+
+__device__ __forceinline__ void load8f(const void* p, long long off, bool f32, float* v) {
+  if (f32) {
+    const f32x4 a = *(const f32x4*)((const float*)p + off), c = *(const f32x4*)((const float*)p + off + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[4 + j] = c[j]; }
+  } else {
+    load8((const bf16*)p + off, v);
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_relu_fwd_kernel(BnArgs a) {
+  const int G = a.C >> 3;
+  const long long e = blockIdx.x * 256LL + threadIdx.x;
+  if (e >= a.V * G) return;
+  const int g = (int)(e % G);
+  float x[8], mu[8], rs[8];
+  load8(a.x + e * 8, x);
+  load_stats(a.stats + 8 * g, a.C, mu, rs);
+  float* y = (float*)a.out + e * 8;
+  float o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float v = __fadd_rn(__fmul_rn(__fmul_rn(__fsub_rn(x[j], mu[j]), rs[j]), a.w[8 * g + j]), a.b[8 * g + j]);
+    o[j] = v > 0.f ? v : 0.f;
+  }
+  *(f32x4*)y = f32x4{o[0], o[1], o[2], o[3]};
+  *(f32x4*)(y + 4) = f32x4{o[4], o[5], o[6], o[7]};
+}
+
+// partial sums of g and g * xhat per (channel, voxel chunk); part (2, C, nchunk)
+__global__ __launch_bounds__(256) void bn_relu_bwd_reduce_kernel(BnArgs a) {
+  __shared__ float red[2][2048];
+  const int G = a.C >> 3, rows = 256 / G;
+  const int tid = threadIdx.x, g = tid % G, r = tid / G;
+  const int chunk = blockIdx.x;
+  const long long v0 = chunk * a.chunk, v1 = min(a.V, v0 + a.chunk);
+  float s1[8], s2[8], mu[8], rs[8], w[8], bb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+  if (r < rows) {
+    load_stats(a.stats + 8 * g, a.C, mu, rs);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { w[j] = a.w[8 * g + j]; bb[j] = a.b[8 * g + j]; }
+    for (long long v = v0 + r; v < v1; v += rows) {
+      float x[8], d[8];
+      load8(a.x + v * a.C + 8 * g, x);
+      load8f(a.dy, v * a.C + 8 * g, a.dy_f32 != 0, d);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float n = __fmul_rn(__fsub_rn(x[j], mu[j]), rs[j]);
+        const float gg = __fadd_rn(__fmul_rn(n, w[j]), bb[j]) > 0.f ? d[j] : 0.f;
+        s1[j] += gg;
+        s2[j] += gg * n;
+      }
+    }
+  }
+  for (int c = tid; c < rows * a.C; c += 256) { red[0][c] = 0.f; red[1][c] = 0.f; }
+  __syncthreads();
+  if (r < rows) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { red[0][r * a.C + 8 * g + j] = s1[j]; red[1][r * a.C + 8 * g + j] = s2[j]; }
+  }
+  __syncthreads();
+  for (int c = tid; c < a.C; c += 256) {
+    float t1 = 0.f, t2 = 0.f;
+    for (int q = 0; q < rows; ++q) { t1 += red[0][q * a.C + c]; t2 += red[1][q * a.C + c]; }
+    float* p = a.part + (long long)c * a.nchunk + chunk;
+    p[0] = t1;
+    p[(long long)a.C * a.nchunk] = t2;
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_relu_bwd_apply_kernel(BnArgs a) {
+  const int G = a.C >> 3;
+  const long long e = blockIdx.x * 256LL + threadIdx.x;
+  if (e >= a.V * G) return;
+  const int g = (int)(e % G);
+  float x[8], d[8], mu[8], rs[8], m1[8], m2[8];
+  load8(a.x + e * 8, x);
+  load8f(a.dy, e * 8, a.dy_f32 != 0, d);
+  load_stats(a.stats + 8 * g, a.C, mu, rs);
+  load_stats(a.coef + 8 * g, a.C, m1, m2);
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float w = a.w[8 * g + j];
+    const float n = __fmul_rn(__fsub_rn(x[j], mu[j]), rs[j]);
+    const float gg = __fadd_rn(__fmul_rn(n, w), a.b[8 * g + j]) > 0.f ? d[j] : 0.f;
+    o[j] = to_bf16((gg - m1[j] - n * m2[j]) * (rs[j] * w));
+  }
+  *(bf16x8*)((bf16*)a.out + e * 8) = o;
+}
+
 }  // namespace lci
 
 using namespace lci;
 
 extern "C" int lci_inorm_chunks(long long V, int B);
+
+// Training BatchNorm + ReLU over x (V, C) bf16 channels-last (all B * V voxels), stats (2, C) from lci_inorm_reduce /
+// lci_inorm_finalize (B = 1): y (V, C) f32 = relu((x - mean) rstd w + b).
+extern "C" int lci_bn_relu_fwd(const void* x, const float* stats, const float* w, const float* b, float* y,
+                               long long V, int C, void* stream) {
+  LCI_CHECK(V > 0 && C > 0 && C % 8 == 0 && C <= 2048, "bn_relu: bad shape");
+  LCI_CHECK((((uintptr_t)x | (uintptr_t)y | (uintptr_t)stats) & 15) == 0, "bn_relu: misaligned buffers");
+  BnArgs a = {};
+  a.x = (const bf16*)x; a.stats = stats; a.w = w; a.b = b; a.out = y; a.V = V; a.C = C;
+  const long long groups = V * (C / 8);
+  LCI_CHECK((groups + 255) / 256 < (1LL << 31), "bn_relu: volume too large");
+  hipLaunchKernelGGL(bn_relu_fwd_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+
+// Backward partial sums: part (2, C, lci_inorm_chunks(V, 1)) of g = dy [y > 0] and g xhat; dy (V, C) f32 or bf16.
+extern "C" int lci_bn_relu_bwd_reduce(const void* x, const void* dy, int dy_f32, const float* stats, const float* w,
+                                      const float* b, float* part, long long V, int C, void* stream) {
+  LCI_CHECK(V > 0 && C > 0 && C % 8 == 0 && C <= 2048, "bn_relu: bad shape");
+  LCI_CHECK((((uintptr_t)x | (uintptr_t)dy | (uintptr_t)stats) & 15) == 0, "bn_relu: misaligned buffers");
+  BnArgs a = {};
+  a.x = (const bf16*)x; a.dy = dy; a.dy_f32 = dy_f32; a.stats = stats; a.w = w; a.b = b; a.part = part;
+  a.V = V; a.C = C;
+  a.nchunk = lci_inorm_chunks(V, 1);
+  a.chunk = (V + a.nchunk - 1) / a.nchunk;
+  hipLaunchKernelGGL(bn_relu_bwd_reduce_kernel, dim3(a.nchunk), dim3(256), 0, (hipStream_t)stream, a);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+
+// dx (V, C) bf16 = (g - coef[0]) - xhat coef[1]) rstd w; coef (2, C) = (mean(g), mean(g xhat)) from lci_inorm_finalize
+// mode 1 over the reduce partials.
+extern "C" int lci_bn_relu_bwd_apply(const void* x, const void* dy, int dy_f32, const float* stats, const float* coef,
+                                     const float* w, const float* b, void* dx, long long V, int C, void* stream) {
+  LCI_CHECK(V > 0 && C > 0 && C % 8 == 0 && C <= 2048, "bn_relu: bad shape");
+  LCI_CHECK((((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx | (uintptr_t)stats | (uintptr_t)coef) & 15) == 0,
+            "bn_relu: misaligned buffers");
+  BnArgs a = {};
+  a.x = (const bf16*)x; a.dy = dy; a.dy_f32 = dy_f32; a.stats = stats; a.coef = coef; a.w = w; a.b = b; a.out = dx;
+  a.V = V; a.C = C;
+  const long long groups = V * (C / 8);
+  LCI_CHECK((groups + 255) / 256 < (1LL << 31), "bn_relu: volume too large");
+  hipLaunchKernelGGL(bn_relu_bwd_apply_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, a);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
 
 extern "C" int lci_inorm_finalize(const float* part, float* out, long long V, int B, int C, int mode, float eps,
                                   void* stream) {

@@ -1632,6 +1632,77 @@ def _inorm_sums(x_cl, dz_cl, stats, act, mode):
     return out
 
 
+class _BatchNormReLU(torch.autograd.Function):
+    """relu(batch_norm(x)) in training mode over x_cl (V, C) bf16 = every voxel of the batch, f32 out (autocast's
+    fp32 batch_norm): statistics by the instance-norm reduction with the batch as one sample, the affine map + ReLU
+    and the backward by lci_bn_relu_*. Returns (y, stats) -- stats (1, 2, C) = (mean, rstd) for the running-stat
+    update."""
+
+    @staticmethod
+    def forward(ctx, x_cl, w, b):
+        V, C = x_cl.shape
+        stats = _inorm_stats(x_cl.view(1, V, C), False)
+        y = torch.empty(V, C, device=x_cl.device, dtype=torch.float32)
+        KernelTimer.run("bn_relu_fwd", 0.0, x_cl, lambda: _lib.call(
+            "lci_bn_relu_fwd", x_cl.data_ptr(), stats.data_ptr(), w.data_ptr(), b.data_ptr(), y.data_ptr(), V, C,
+            _lib.stream_of(x_cl)))
+        ctx.save_for_backward(x_cl, stats, w, b)
+        ctx.mark_non_differentiable(stats)
+        return y, stats
+
+    @staticmethod
+    def backward(ctx, dy, _dstats):
+        x_cl, stats, w, b = ctx.saved_tensors
+        V, C = x_cl.shape
+        g = dy if dy.dtype in (torch.float32, torch.bfloat16) else dy.float()
+        g = g.contiguous()
+        if g.data_ptr() % 16:
+            g = g.clone()
+        f32 = int(g.dtype == torch.float32)
+        lib = _lib.load()
+        st = _lib.stream_of(x_cl)
+        part = torch.empty(2, C, lib.lci_inorm_chunks(V, 1), device=x_cl.device, dtype=torch.float32)
+        coef = torch.empty(1, 2, C, device=x_cl.device, dtype=torch.float32)
+        dx = torch.empty_like(x_cl)
+        KernelTimer.run("bn_relu_bwd", 0.0, x_cl, lambda: (
+            _lib.call("lci_bn_relu_bwd_reduce", x_cl.data_ptr(), g.data_ptr(), f32, stats.data_ptr(), w.data_ptr(),
+                      b.data_ptr(), part.data_ptr(), V, C, st),
+            _lib.call("lci_inorm_finalize", part.data_ptr(), coef.data_ptr(), V, 1, C, 1, INORM_EPS, st),
+            _lib.call("lci_bn_relu_bwd_apply", x_cl.data_ptr(), g.data_ptr(), f32, stats.data_ptr(), coef.data_ptr(),
+                      w.data_ptr(), b.data_ptr(), dx.data_ptr(), V, C, st)))
+        dw = coef[0, 1] * V if ctx.needs_input_grad[1] else None
+        db = coef[0, 0] * V if ctx.needs_input_grad[2] else None
+        return dx, dw, db
+
+
+def batch_norm_relu_supported(x: torch.Tensor, bn) -> bool:
+    """The fused training BatchNorm + ReLU takes a bf16 map with dense channels-last strides, 8 | C <= 2048, an
+    affine BN with eps 1e-5 and a momentum, in training mode."""
+    C = x.shape[1]
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and bn.training and bn.affine and bn.track_running_stats
+            and bn.momentum is not None and bn.eps == INORM_EPS and C % 8 == 0 and C <= 2048):
+        return False
+    x_cl = x.movedim(1, -1)
+    return x_cl.is_contiguous() and x_cl.data_ptr() % 16 == 0 and x.numel() // C > 1
+
+
+def batch_norm_relu(x: torch.Tensor, bn) -> torch.Tensor:
+    """relu(bn(x)) for a training-mode nn.BatchNorm{2,3}d `bn` (running statistics updated as torch does: momentum,
+    unbiased variance), x (B, C, *S) bf16 channels-last -> f32 with channels-last strides."""
+    B, C = x.shape[:2]
+    x_cl = x.movedim(1, -1).reshape(-1, C)
+    V = x_cl.shape[0]
+    y, stats = _BatchNormReLU.apply(x_cl, bn.weight, bn.bias)
+    with torch.no_grad():
+        m = bn.momentum
+        mean = stats[0, 0]
+        var = (1.0 / stats[0, 1].double() ** 2 - bn.eps).clamp_min(0.0) * (V / max(V - 1, 1))
+        bn.running_mean.mul_(1.0 - m).add_(mean, alpha=m)
+        bn.running_var.mul_(1.0 - m).add_(var.float(), alpha=m)
+        bn.num_batches_tracked.add_(1)
+    return y.view(B, *x.shape[2:], C).movedim(-1, 1)
+
+
 def _inorm_stats(x_cl, act):
     """(B, 2, C) f32 mean, rstd of a (B, V, C) bf16 tensor over its voxels."""
     return _inorm_sums(x_cl, None, None, act, 0)
