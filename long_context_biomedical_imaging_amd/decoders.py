@@ -489,6 +489,15 @@ def _bn(nd, c):
 HIP_BN = os.environ.get("LCI_HIP_BN", "1") != "0"
 
 
+def _bf16_operands(ts):
+    """The maps a following conv concatenates, cast to its autocast operand dtype first: the cast commutes with the
+    cat (the same bf16 values), and the cat then moves 2 bytes per element instead of 4 (the FPN fusion's 1536-channel
+    512^2 cat at C4: 3.2 GB f32) with no separate cast pass."""
+    if ts and ts[0].is_cuda and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16:
+        return [t.to(torch.bfloat16) for t in ts]
+    return ts
+
+
 def _conv_bn_relu(seq, x):
     """seq = Sequential(conv, BatchNorm, ReLU[, Dropout]) (PSPModule.bottleneck seg_heads.py:26-31 / :158-163,
     FPN_fuse.conv_fusion :60-63 / :192-195): in training mode the BatchNorm + ReLU of the conv's bf16 channels-last
@@ -650,7 +659,7 @@ class PSPModule(nn.Module):
                 else:
                     up = _up_cl(y, size)
                 pyramids.append(up if up.dtype == y.dtype else up.to(y.dtype))
-            return _conv_bn_relu(self.bottleneck, _cat_channels(pyramids))
+            return _conv_bn_relu(self.bottleneck, _cat_channels(_bf16_operands(pyramids)))
         if SEPARABLE_PSP and features.is_cuda:
             pyramids = [features]
             for stage in self.stages:
@@ -731,7 +740,7 @@ class FPN_fuse(nn.Module):
         P.append(features[-1])
         size = P[0].shape[2:]
         P[1:] = [resize(f, size) for f in P[1:]]
-        return _conv_bn_relu(self.conv_fusion, _cat_channels(P))
+        return _conv_bn_relu(self.conv_fusion, _cat_channels(_bf16_operands(P)))
 
 
 class _UperNet(nn.Module):
