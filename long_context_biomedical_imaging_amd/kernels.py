@@ -15,11 +15,12 @@ class KernelTimer:
     bench.py enables it for the timed region; each entry is (name, start_event, end_event, algorithmic work).
     """
     enabled = False
+    only = None          # a set of names: time only those launches (None: every launch)
     records: list = []
 
     @classmethod
     def run(cls, name, work, t, fn):
-        if not cls.enabled:
+        if not cls.enabled or (cls.only is not None and name not in cls.only):
             fn()
             return
         st = torch.cuda.current_stream(t.device)
