@@ -57,8 +57,8 @@ extern "C" {
  * 18: lci_attn_bwd delta_ws is lci_attn_bwd_ws_bytes(B, H, L) bytes; 19: selective-scan checkpoints in the I/O
  * dtype; 20: lci_attn_gen_fwd / lci_attn_gen_bwd; 21: lci_gemm_bt; 22: lci_linear_fwd removed, superseded by
  * lci_gemm_bt; 23: lci_fftconv_spectrum Dv; 24: lci_inorm_finalize; 25: lci_adam_step; 26: Hyena gate dx2 / gx2
- * in the activation dtype; 27: lci_layernorm_bwd dxb; 28: lci_resample_cl_fwd, lci_resample1d_adj_ac; 29: lci_bn_relu_*). */
-#define LCI_ABI_VERSION 29
+ * in the activation dtype; 27: lci_layernorm_bwd dxb; 28: lci_resample_cl_fwd, lci_resample1d_adj_ac; 29: lci_bn_relu_*; 30: lci_gemm_bt_acc). */
+#define LCI_ABI_VERSION 30
 const char* lci_last_error(void);
 int lci_abi_version(void);
 /* sha256 prefix of the sources the library was built from (build_lib.source_hash); the Python binding refuses a
@@ -421,6 +421,10 @@ int lci_gelu_bwd(const void* x, const void* dy, void* dx, long long n, void* str
  * is the call with the transposed weight. Supported when lci_gemm_bt_supported(N, K): N % 384 == 0 or N % 256 == 0, N <= 4096,
  * K % 32 == 0; ldx, ldy % 8 == 0; x / w / y 16-byte aligned; any M (per-tile 32-bit offsets). */
 int lci_gemm_bt_supported(int N, int K);
+/* y = bf16(y + bf16(x . w^T)) (no bias): the product added into an existing bf16 matrix in the epilogue -- UnetResBlock's
+ * 1x1 residual data gradient summed into conv1's (the autograd sum, same roundings). Same support as lci_gemm_bt. */
+int lci_gemm_bt_acc(const void* x, long long ldx, const void* w, void* y, long long ldy, long long M, int N, int K,
+                    void* stream);
 int lci_gemm_bt(const void* x, long long ldx, const void* w, const void* bias, void* y, long long ldy, long long M,
                 int N, int K, void* stream);
 

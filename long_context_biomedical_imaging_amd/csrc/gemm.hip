@@ -51,7 +51,7 @@ struct GemmArgs {
   int G8, dmt, dnt;               // workgroups per XCD; G8 tiles = dmt token tiles + dnt feature tiles
 };
 
-template <int TN, bool HAS_BIAS>
+template <int TN, bool HAS_BIAS, bool ACC = false>
 __global__ __launch_bounds__(GM_WAVES * 64, 1) void gemm_bt_kernel(GemmArgs a) {
   constexpr int WN = 2, WM = 4;
   constexpr int NB = TN / WN / 32, MB = GM_TM / WM / 32;           // 32x32 blocks per wave (features, tokens)
@@ -253,9 +253,17 @@ __global__ __launch_bounds__(GM_WAVES * 64, 1) void gemm_bt_kernel(GemmArgs a) {
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
             const int row = 8 * k + erow;
-            const u32x4 v = *(const u32x4*)(eb + row * 128 + 16 * (echk ^ (row & 7)));
-            __builtin_amdgcn_raw_buffer_store_b128(v, ry, erow * ldy2 + 16 * echk,
-                                                   (WT * wm + 32 * j + 8 * k) * ldy2 + (cc.n0() + WF * wn + 64 * ip) * 2, 0);
+            u32x4 v = *(const u32x4*)(eb + row * 128 + 16 * (echk ^ (row & 7)));
+            const int vo = erow * ldy2 + 16 * echk;
+            const int so = (WT * wm + 32 * j + 8 * k) * ldy2 + (cc.n0() + WF * wn + 64 * ip) * 2;
+            if constexpr (ACC) {   // y += the bf16 product: the autograd sum of two bf16 gradients, rounded once more
+              bf16x8 pv = __builtin_bit_cast(bf16x8, v);
+              const bf16x8 ov = __builtin_bit_cast(bf16x8, bload16(ry, vo, so));
+#pragma unroll
+              for (int q = 0; q < 8; ++q) pv[q] = to_bf16(to_f32(ov[q]) + to_f32(pv[q]));
+              v = __builtin_bit_cast(u32x4, pv);
+            }
+            __builtin_amdgcn_raw_buffer_store_b128(v, ry, vo, so, 0);
           }
         }
       since_epi = 0;
@@ -279,9 +287,12 @@ extern "C" int lci_gemm_bt_supported(int N, int K) {
 }
 
 template <int TN>
-static void gm_launch(const GemmArgs& a, long long grid, bool bias, hipStream_t st) {
+static void gm_launch(const GemmArgs& a, long long grid, bool bias, hipStream_t st, bool acc = false) {
   const size_t sh = (size_t)GM_NSLOT * (GM_TM + TN) * 64 + GM_WAVES * GM_EPI + GM_MAXN * 2;
-  if (bias) {
+  if (acc) {
+    (void)hipFuncSetAttribute((const void*)gemm_bt_kernel<TN, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
+    hipLaunchKernelGGL((gemm_bt_kernel<TN, false, true>), dim3((unsigned)grid), dim3(GM_WAVES * 64), sh, st, a);
+  } else if (bias) {
     (void)hipFuncSetAttribute((const void*)gemm_bt_kernel<TN, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
     hipLaunchKernelGGL((gemm_bt_kernel<TN, true>), dim3((unsigned)grid), dim3(GM_WAVES * 64), sh, st, a);
   } else {
@@ -292,8 +303,8 @@ static void gm_launch(const GemmArgs& a, long long grid, bool bias, hipStream_t 
 
 // Y (M x N, row stride ldy) = X (M x K, row stride ldx) . W^T (W: N x K contiguous) + bias (N, bf16, or null); bf16.
 // x, w, y 16-byte aligned; ldx, ldy multiples of 8; M * ldx and M * ldy any size (per-tile 32-bit offsets).
-extern "C" int lci_gemm_bt(const void* x, long long ldx, const void* w, const void* bias, void* y, long long ldy,
-                           long long M, int N, int K, void* stream) {
+static int gemm_bt_run(const void* x, long long ldx, const void* w, const void* bias, void* y, long long ldy,
+                       long long M, int N, int K, void* stream, bool acc) {
   LCI_CHECK(lci_gemm_bt_supported(N, K), "gemm_bt: N=%d K=%d unsupported (N %% 384 or %% 256, K %% 32)", N, K);
   LCI_CHECK(M > 0 && ldx >= K && ldy >= N && ldx % 8 == 0 && ldy % 8 == 0, "gemm_bt: bad M / strides");
   LCI_CHECK(((uintptr_t)x | (uintptr_t)w | (uintptr_t)y) % 16 == 0, "gemm_bt: pointers must be 16-byte aligned");
@@ -315,8 +326,20 @@ extern "C" int lci_gemm_bt(const void* x, long long ldx, const void* w, const vo
   a.G8 = (int)(grid / 8);
   a.dmt = a.G8 / a.ntn;
   a.dnt = a.G8 % a.ntn;
-  if (tn == 384) gm_launch<384>(a, grid, bias != nullptr, (hipStream_t)stream);
-  else gm_launch<256>(a, grid, bias != nullptr, (hipStream_t)stream);
+  if (tn == 384) gm_launch<384>(a, grid, bias != nullptr, (hipStream_t)stream, acc);
+  else gm_launch<256>(a, grid, bias != nullptr, (hipStream_t)stream, acc);
   LCI_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" int lci_gemm_bt(const void* x, long long ldx, const void* w, const void* bias, void* y, long long ldy,
+                           long long M, int N, int K, void* stream) {
+  return gemm_bt_run(x, ldx, w, bias, y, ldy, M, N, K, stream, false);
+}
+
+// y (M x N, bf16) = bf16(y + bf16(X . W^T)): the product added into an existing bf16 gradient in the epilogue
+// (UnetResBlock's 1x1 residual data gradient into conv1's, the sum autograd would form; no bias). Same support.
+extern "C" int lci_gemm_bt_acc(const void* x, long long ldx, const void* w, void* y, long long ldy, long long M, int N,
+                               int K, void* stream) {
+  return gemm_bt_run(x, ldx, w, nullptr, y, ldy, M, N, K, stream, true);
 }

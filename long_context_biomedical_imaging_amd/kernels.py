@@ -1586,7 +1586,15 @@ class _ResConvs(torch.autograd.Function):
             if dy_cl is not None:
                 dx = conv3_cl(dy_cl, _conv3_pack(w1, kd, 1, Cin), kd)      # (B, D, H, W, Cin) bf16
                 if dr2 is not None:
-                    dx.view(-1, Cin).addmm_(dr2, w3b)                        # += dr . W3 in the GEMM
+                    dx2 = dx.view(-1, Cin)
+                    if HIP_GEMM and gemm_bt_preferred(dr2.shape[0], Cin) and gemm_bt_supported(dr2, Cin, N3):
+                        # += bf16(dr . W3) in lci_gemm_bt's epilogue: the autograd sum's own roundings
+                        w3t = w3b.t().contiguous()
+                        KernelTimer.run("gemm_bt", 2.0 * dr2.shape[0] * Cin * N3, dr2, lambda: _lib.call(
+                            "lci_gemm_bt_acc", dr2.data_ptr(), dr2.stride(0), w3t.data_ptr(), dx2.data_ptr(), Cin,
+                            dr2.shape[0], Cin, N3, _lib.stream_of(dr2)))
+                    else:
+                        dx2.addmm_(dr2, w3b)                                 # += dr . W3 in the GEMM (beta = 1)
             else:
                 dx = (dr2 @ w3b).view(*x_cl.shape)
             dx = _from_cl(dx, nd)

@@ -88,3 +88,18 @@ def test_gemm_bt_supported_shapes():
     assert not lib.lci_gemm_bt_supported(384, 48) and not lib.lci_gemm_bt_supported(400, 384)
     assert lib.lci_gemm_bt_supported(2048, 384) and lib.lci_gemm_bt_supported(512, 64)
     assert not lib.lci_gemm_bt_supported(640, 384) and not lib.lci_gemm_bt_supported(4352, 384)
+
+
+@pytest.mark.parametrize("M,N,K", [(70001, 256, 32), (66000, 512, 256), (131072, 384, 384)])
+def test_gemm_bt_acc_is_the_autograd_sum(M, N, K):
+    """lci_gemm_bt_acc: y <- bf16(y + bf16(x . w^T)), bitwise the sum autograd forms of y and lci_gemm_bt's product
+    (UnetResBlock's 1x1 residual data gradient added into conv1's)."""
+    from long_context_biomedical_imaging_amd import _lib, kernels
+    g = torch.Generator(device="cuda").manual_seed(M + N)
+    x = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).to(torch.bfloat16)
+    y0 = torch.randn(M, N, device="cuda", generator=g).to(torch.bfloat16)
+    ref = (y0.float() + kernels.gemm_bt(x, w).float()).to(torch.bfloat16)
+    y = y0.clone()
+    _lib.call("lci_gemm_bt_acc", x.data_ptr(), K, w.data_ptr(), y.data_ptr(), N, M, N, K, _lib.stream_of(x))
+    assert torch.equal(y, ref)
