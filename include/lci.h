@@ -57,8 +57,9 @@ extern "C" {
  * 18: lci_attn_bwd delta_ws is lci_attn_bwd_ws_bytes(B, H, L) bytes; 19: selective-scan checkpoints in the I/O
  * dtype; 20: lci_attn_gen_fwd / lci_attn_gen_bwd; 21: lci_gemm_bt; 22: lci_linear_fwd removed, superseded by
  * lci_gemm_bt; 23: lci_fftconv_spectrum Dv; 24: lci_inorm_finalize; 25: lci_adam_step; 26: Hyena gate dx2 / gx2
- * in the activation dtype; 27: lci_layernorm_bwd dxb; 28: lci_resample_cl_fwd, lci_resample1d_adj_ac; 29: lci_bn_relu_*; 30: lci_gemm_bt_acc). */
-#define LCI_ABI_VERSION 30
+ * in the activation dtype; 27: lci_layernorm_bwd dxb; 28: lci_resample_cl_fwd, lci_resample1d_adj_ac; 29: lci_bn_relu_*; 30: lci_gemm_bt_acc;
+ * 31: lci_layernorm_bwd dres2). */
+#define LCI_ABI_VERSION 31
 const char* lci_last_error(void);
 int lci_abi_version(void);
 /* sha256 prefix of the sources the library was built from (build_lib.source_hash); the Python binding refuses a
@@ -388,10 +389,12 @@ int lci_layernorm_add_fwd(const float* h, const void* add, int add_bf16, float* 
                           const float* beta, void* y, int bf16_out, float* mean, float* rstd, long long rows, int C,
                           float eps, void* stream);
 /* dxb (rows, C) bf16 or null: dx rounded to bf16 in the same pass, the gradient of a bf16 branch output added by
- * lci_layernorm_add_fwd (ABI 27). */
+ * lci_layernorm_add_fwd (ABI 27). dres2 (rows, C) f32 or null (needs dres): a second residual gradient, summed with
+ * dres first -- a recorded hidden state's decoder gradient, which autograd would otherwise add in a separate pass
+ * (ABI 31). */
 int lci_layernorm_bwd(const float* x, const void* dy, int bf16_dy, const float* gamma, const float* mean,
-                      const float* rstd, const float* dres, float* dx, void* dxb, float* part, long long rows, int C,
-                      void* stream);
+                      const float* rstd, const float* dres, const float* dres2, float* dx, void* dxb, float* part,
+                      long long rows, int C, void* stream);
 
 /* ------------------------------------------------------------------ token-wise Linear: weight / bias gradient
  * dy (M, ldy) bf16 row-major (columns [0, N) used), x (M, ldx) bf16 row-major (columns [0, K) used): the layer's

@@ -14,7 +14,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_LIB = os.path.join(HERE, "liblci.so")
 LIB_PATH = os.environ.get("LCI_LIB_PATH", DEFAULT_LIB)   # override: kernel-variant A/B runs (no staleness check)
-ABI_VERSION = 30   # include/lci.h LCI_ABI_VERSION
+ABI_VERSION = 31   # include/lci.h LCI_ABI_VERSION
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -61,7 +61,7 @@ SIGNATURES = {
     "lci_inorm_apply_res": [_P, _P, _P, _P, _P, _L, _I, _I, _F, _P],
     "lci_layernorm_fwd": [_P, _P, _P, _P, _I, _P, _P, _L, _I, _F, _P],
     "lci_layernorm_add_fwd": [_P, _P, _I, _P, _P, _P, _P, _I, _P, _P, _L, _I, _F, _P],
-    "lci_layernorm_bwd": [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P],
+    "lci_layernorm_bwd": [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P],
     "lci_dwconv_silu_bwd": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "lci_linear_wgrad": [_P, _L, _P, _L, _L, _I, _I, _P, _P, _P],
     "lci_gemm_bt": [_P, _L, _P, _P, _P, _L, _L, _I, _I, _P],

@@ -142,17 +142,19 @@ class TransformerBlock(nn.Module):
         _, h, m = self.forward_pair(x, None)
         return h + m
 
-    def forward_pair(self, h, m):
+    def forward_pair(self, h, m, tap=False):
         """The block on the residual stream held as a pair: its input is h + m (m = the previous block's MLP output,
         bf16, or None), summed inside the norm1 LayerNorm kernel instead of by a separate add; returns (h + m, the
         stream after the attention residual, this block's MLP output). The residual gradient of each add is summed
         inside the LayerNorm backward kernels, which also write m's bf16 gradient (no cast passes)."""
         if m is None:
-            x, y = self.norm1.forward_residual(h)
+            x, xt, y = self.norm1.forward_residual(h, tap=True)
         else:
-            x, y = self.norm1.forward_residual_add(h, m)
+            x, xt, y = self.norm1.forward_residual_add(h, m, tap=True)
         h, y = self.norm2.forward_residual_add(x, self.attn(y))   # x + attn(.) summed inside the norm2 kernel
-        return x, h, self.mlp(y)
+        # tap: the returned block input is a separate alias, so a consumer outside the block (a decoder reading the
+        # hidden state) gets its gradient summed inside norm1's backward kernel rather than by an autograd add
+        return (xt if tap else x), h, self.mlp(y)
 
 
 class ViT_with_alt_ops(nn.Module):
@@ -212,10 +214,11 @@ class ViT_with_alt_ops(nn.Module):
         train = self.training and torch.is_grad_enabled()
         h, m = x, None
         for i, blk in enumerate(self.blocks):
+            tap = i > 0 and keep(i)
             if i < nck and train:
-                xin, h, m = torch.utils.checkpoint.checkpoint(blk.forward_pair, h, m, use_reentrant=False)
+                xin, h, m = torch.utils.checkpoint.checkpoint(blk.forward_pair, h, m, tap, use_reentrant=False)
             else:
-                xin, h, m = blk.forward_pair(h, m)
+                xin, h, m = blk.forward_pair(h, m, tap)
             if i > 0:   # xin = block i - 1's output, hidden_states_out[i]
                 hidden_states_out.append(xin if keep(i) else None)
             if i + 1 < min(nck, len(self.blocks)) and train and keep(i + 1):

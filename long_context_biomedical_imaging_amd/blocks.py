@@ -48,14 +48,16 @@ class TokenLayerNorm(nn.LayerNorm):
     def forward(self, x):
         return kernels.layer_norm(x, self.weight, self.bias, self.eps, self._bf16_out())
 
-    def forward_residual_add(self, h, a):
-        """(h + a, self(h + a)) with the residual add inside the LayerNorm forward kernel."""
-        return kernels.add_residual_layer_norm(h, a, self.weight, self.bias, self.eps, self._bf16_out())
+    def forward_residual_add(self, h, a, tap=False):
+        """(h + a, self(h + a)) with the residual add inside the LayerNorm forward kernel; tap: (h + a, an alias of it
+        for a consumer outside the block, self(h + a))."""
+        return kernels.add_residual_layer_norm(h, a, self.weight, self.bias, self.eps, self._bf16_out(), tap)
 
-    def forward_residual(self, x):
+    def forward_residual(self, x, tap=False):
         """(x, self(x)) for a residual block x + f(self(x)); the backward adds the residual gradient inside the
-        LayerNorm kernel (one pass over the residual stream fewer)."""
-        return kernels.residual_layer_norm(x, self.weight, self.bias, self.eps, self._bf16_out())
+        LayerNorm kernel (one pass over the residual stream fewer); tap: (x, an alias of x, self(x)), whose gradient
+        is summed in the same kernel."""
+        return kernels.residual_layer_norm(x, self.weight, self.bias, self.eps, self._bf16_out(), tap)
 
 
 class OutLayerNorm(nn.LayerNorm):

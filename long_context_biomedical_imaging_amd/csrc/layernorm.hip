@@ -29,6 +29,7 @@ struct LnArgs {
   float* dx;            // bwd: (rows, C) f32
   void* dxb;            // bwd: (rows, C) bf16 copy of dx, or null (the gradient of a bf16 branch output)
   const float* dres;    // bwd: (rows, C) f32 residual-path gradient added into dx, or null
+  const float* dres2;   // bwd: a second one (a hidden-state tap's gradient, summed with dres first), or null
   float* mean;          // (rows)
   float* rstd;          // (rows)
   float* part;          // bwd: (gridDim.x, 2, C) partial dgamma, dbeta
@@ -159,6 +160,11 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnArgs a) {
       const int c = 4 * lane + 256 * k;
       if (c < C) {
         f32x4 o = a.dres ? *(const f32x4*)(a.dres + row * C + c) : f32x4{};
+        if (a.dres2) {   // dres + dres2: the sum autograd would form of the two consumers' gradients
+          const f32x4 o2 = *(const f32x4*)(a.dres2 + row * C + c);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] += o2[j];
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] += rstd * (g[k][j] - m1 - n[k][j] * m2);
         *(f32x4*)(a.dx + row * C + c) = o;
@@ -258,14 +264,16 @@ extern "C" int lci_layernorm_add_fwd(const float* h, const void* add, int add_bf
 }
 
 extern "C" int lci_layernorm_bwd(const float* x, const void* dy, int bf16_dy, const float* gamma, const float* mean,
-                                 const float* rstd, const float* dres, float* dx, void* dxb, float* part, long long rows,
-                                 int C, void* stream) {
+                                 const float* rstd, const float* dres, const float* dres2, float* dx, void* dxb,
+                                 float* part, long long rows, int C, void* stream) {
   if (ln_check(rows, C, x)) return 1;
   LCI_CHECK(!dres || ((uintptr_t)dres & 15) == 0, "layernorm: misaligned residual gradient");
+  LCI_CHECK(!dres2 || (dres && ((uintptr_t)dres2 & 15) == 0), "layernorm: dres2 needs dres, 16-byte aligned");
   LCI_CHECK(((uintptr_t)dy & (bf16_dy ? 7 : 15)) == 0 && ((uintptr_t)gamma & 15) == 0 &&
             ((uintptr_t)dx & 15) == 0 && ((uintptr_t)dxb & 7) == 0, "layernorm: misaligned dy/gamma/dx");
   LnArgs a = {};
   a.dres = dres;
+  a.dres2 = dres2;
   a.x = x; a.dy = dy; a.gamma = gamma; a.mean = const_cast<float*>(mean); a.rstd = const_cast<float*>(rstd);
   a.dx = dx; a.dxb = dxb; a.part = part;
   a.rows = rows; a.C = C; a.bf16_io = bf16_dy;

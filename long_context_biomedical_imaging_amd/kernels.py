@@ -1825,8 +1825,9 @@ def _ln_fwd(x, weight, bias, eps, bf16_out):
     return y, x2, mean, rstd
 
 
-def _ln_bwd(x2, weight, mean, rstd, dy, dres, shape, want_bf16=False):
-    """dx (f32, `shape`), dgamma, dbeta [, dx rounded to bf16 in the same kernel pass when want_bf16]."""
+def _ln_bwd(x2, weight, mean, rstd, dy, dres, shape, want_bf16=False, dres2=None):
+    """dx (f32, `shape`), dgamma, dbeta [, dx rounded to bf16 in the same kernel pass when want_bf16]; dres2: a second
+    residual gradient (a recorded hidden state's), summed with dres inside the kernel."""
     rows, C = x2.shape
     bf = dy.dtype == torch.bfloat16
     dy = (dy if bf else dy.float()).contiguous()
@@ -1836,14 +1837,23 @@ def _ln_bwd(x2, weight, mean, rstd, dy, dres, shape, want_bf16=False):
         dres = dres.float().contiguous()
         if dres.data_ptr() % 16:
             dres = dres.clone()
+    if dres2 is not None:
+        if dres is None:
+            dres, dres2 = dres2, None
+        else:
+            dres2 = dres2.float().contiguous()
+            if dres2.data_ptr() % 16:
+                dres2 = dres2.clone()
+    if dres is not None and dres.data_ptr() % 16:
+        dres = dres.clone()
     dx = torch.empty(rows, C, device=x2.device, dtype=torch.float32)
     dxb = torch.empty(rows, C, device=x2.device, dtype=torch.bfloat16) if want_bf16 else None
     nblk = _lib.load().lci_layernorm_bwd_blocks(rows)
     part = torch.empty(nblk, 2, C, device=x2.device, dtype=torch.float32)
     KernelTimer.run("ln_bwd", rows * C * (8 + dy.element_size() + (4 if dres is not None else 0) + (2 if want_bf16 else 0)),
                     x2, lambda: _lib.call("lci_layernorm_bwd", x2.data_ptr(), dy.data_ptr(), int(bf), weight.data_ptr(),
-                                          mean.data_ptr(), rstd.data_ptr(), _lib.ptr(dres), dx.data_ptr(),
-                                          _lib.ptr(dxb), part.data_ptr(), rows, C, _lib.stream_of(x2)))
+                                          mean.data_ptr(), rstd.data_ptr(), _lib.ptr(dres), _lib.ptr(dres2),
+                                          dx.data_ptr(), _lib.ptr(dxb), part.data_ptr(), rows, C, _lib.stream_of(x2)))
     s = part.sum(0)
     if want_bf16:
         return dx.view(shape), s[0], s[1], dxb.view(shape)
@@ -1866,8 +1876,10 @@ class _LayerNorm(torch.autograd.Function):
 
 
 class _ResidualLayerNorm(torch.autograd.Function):
-    """(h, y) = (x, LN(x)) for a block `x + f(LN(x))`: the backward adds the residual path's gradient dh into
-    the LN input gradient inside the HIP kernel, instead of autograd accumulating the two in a separate pass."""
+    """(h, t, y) = (x, x, LN(x)) for a block `x + f(LN(x))`: the backward adds the residual path's gradient dh into
+    the LN input gradient inside the HIP kernel, instead of autograd accumulating the two in a separate pass; t is
+    a second alias of x for a consumer outside the block (a recorded hidden state), whose gradient is summed in the
+    same kernel."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, eps, bf16_out):
@@ -1875,14 +1887,16 @@ class _ResidualLayerNorm(torch.autograd.Function):
         ctx.save_for_backward(x2, weight, mean, rstd)
         ctx.shape = x.shape
         ctx.set_materialize_grads(False)   # an unused output arrives as None, not as a zeros tensor
-        return x.view_as(x), y
+        return x.view_as(x), x.view_as(x), y
 
     @staticmethod
-    def backward(ctx, dh, dy):
+    def backward(ctx, dh, dt, dy):
         x2, weight, mean, rstd = ctx.saved_tensors
-        if dy is None:   # LN output unused: the residual gradient passes straight through
-            return dh, None, None, None, None
-        dx, dw, db = _ln_bwd(x2, weight, mean, rstd, dy, dh, ctx.shape)
+        if dy is None:   # LN output unused: the residual gradients pass straight through
+            if dh is None or dt is None:
+                return (dh if dt is None else dt), None, None, None, None
+            return dh + dt, None, None, None, None
+        dx, dw, db = _ln_bwd(x2, weight, mean, rstd, dy, dh, ctx.shape, dres2=dt)
         return dx, dw, db, None, None
 
 
@@ -1909,25 +1923,27 @@ class _AddResidualLayerNorm(torch.autograd.Function):
         ctx.shape = h.shape
         ctx.adtype = a.dtype
         ctx.set_materialize_grads(False)
-        return xsum.view(h.shape), y
+        return xsum.view(h.shape), xsum.view(h.shape), y   # the stream, and an alias for a hidden-state tap
 
     @staticmethod
-    def backward(ctx, dx_out, dy):
+    def backward(ctx, dx_out, dt, dy):
         xsum, weight, mean, rstd = ctx.saved_tensors
         if dy is None:
-            dx, dw, db = dx_out, None, None
+            dx, dw, db = (dx_out if dt is None else (dt if dx_out is None else dx_out + dt)), None, None
         elif ctx.adtype == torch.bfloat16:   # the bf16 branch gradient written by the same kernel pass
-            dx, dw, db, da = _ln_bwd(xsum, weight, mean, rstd, dy, dx_out, ctx.shape, want_bf16=True)
+            dx, dw, db, da = _ln_bwd(xsum, weight, mean, rstd, dy, dx_out, ctx.shape, want_bf16=True, dres2=dt)
             return dx, da, dw, db, None, None
         else:
-            dx, dw, db = _ln_bwd(xsum, weight, mean, rstd, dy, dx_out, ctx.shape)
+            dx, dw, db = _ln_bwd(xsum, weight, mean, rstd, dy, dx_out, ctx.shape, dres2=dt)
         if dx is None:
             return None, None, None, None, None, None
         return dx, dx.to(ctx.adtype), dw, db, None, None
 
 
-def add_residual_layer_norm(h, a, weight, bias, eps, bf16_out):
-    """(h + a, layer_norm(h + a)) with the add inside the HIP LN forward; h f32, a bf16 / f32 of h's shape."""
+def add_residual_layer_norm(h, a, weight, bias, eps, bf16_out, tap=False):
+    """(h + a, layer_norm(h + a)) with the add inside the HIP LN forward; h f32, a bf16 / f32 of h's shape.
+    tap: (h + a, a second alias of it for a consumer outside the block, layer_norm(h + a)), the alias's gradient
+    summed inside the LN backward kernel."""
     h = _ln_checks(h, weight, bias)
     ok = (ln_kernel_supports(h.shape[-1]) and a.shape == h.shape and a.dtype in (torch.bfloat16, torch.float32)
           and a.is_cuda)
@@ -1936,8 +1952,9 @@ def add_residual_layer_norm(h, a, weight, bias, eps, bf16_out):
         ok = a.data_ptr() % 16 == 0
     if not ok:
         x = h + a
-        return residual_layer_norm(x, weight, bias, eps, bf16_out)
-    return _AddResidualLayerNorm.apply(h, a, weight, bias, eps, bf16_out)
+        return residual_layer_norm(x, weight, bias, eps, bf16_out, tap)
+    x, t, y = _AddResidualLayerNorm.apply(h, a, weight, bias, eps, bf16_out)
+    return (x, t, y) if tap else (x, y)
 
 
 def _ln_checks(x, weight, bias):
@@ -1973,12 +1990,16 @@ def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: f
     return _LayerNorm.apply(x, weight, bias, eps, bf16_out)
 
 
-def residual_layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float, bf16_out: bool):
-    """(x, layer_norm(x)) with the residual gradient fused into the LN backward (see _ResidualLayerNorm)."""
+def residual_layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float, bf16_out: bool,
+                        tap: bool = False):
+    """(x, layer_norm(x)) with the residual gradient fused into the LN backward (see _ResidualLayerNorm); tap: (x, a
+    second alias of x, layer_norm(x)), the alias's gradient summed in the same kernel."""
     x = _ln_checks(x, weight, bias)
     if not ln_kernel_supports(x.shape[-1]):
-        return x, _torch_ln(x, weight, bias, eps, bf16_out)
-    return _ResidualLayerNorm.apply(x, weight, bias, eps, bf16_out)
+        y = _torch_ln(x, weight, bias, eps, bf16_out)
+        return (x, x, y) if tap else (x, y)
+    h, t, y = _ResidualLayerNorm.apply(x, weight, bias, eps, bf16_out)
+    return (h, t, y) if tap else (h, y)
 
 
 # ------------------------------------------------------------------------------------- token-wise Linear

@@ -158,3 +158,33 @@ def test_add_residual_layernorm(adtype):
     assert rel_err(ac.grad, ar.grad) < (1e-5 if adtype == torch.float32 else 1e-2)
     assert rel_err(wc.grad, wr.grad) < 1e-5
     assert rel_err(bc.grad, br.grad) < 1e-5
+
+
+@pytest.mark.parametrize("add", [False, True])
+def test_residual_layernorm_tap_alias(add):
+    """tap=True returns a second alias of the LN input (a recorded hidden state read outside the block): its gradient
+    is summed inside the LN backward kernel (lci_layernorm_bwd dres2), bitwise the autograd sum of the two consumers'
+    gradients that the one-alias form gets."""
+    from long_context_biomedical_imaging_amd import kernels
+    torch.manual_seed(21)
+    rows, C = 3001, 384
+    h0 = (torch.randn(rows, C) * 2).cuda()
+    a0 = torch.randn(rows, C).cuda().to(torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(C)).cuda()
+    b = (0.1 * torch.randn(C)).cuda()
+    P = (torch.randn(C, C) / C ** 0.5).cuda()
+    c1, c2 = torch.randn(rows, C).cuda(), torch.randn(rows, C).cuda()
+    grads = []
+    for tap in (False, True):
+        h = h0.clone().requires_grad_(True)
+        a = a0.clone().requires_grad_(True)
+        if add:
+            out = kernels.add_residual_layer_norm(h, a, w, b, 1e-5, False, tap)
+        else:
+            out = kernels.residual_layer_norm(h, w, b, 1e-5, False, tap)
+        x, t, y = out if tap else (out[0], out[0], out[1])
+        ((x * c1).sum() + (t * t * c2).sum() + (y @ P).square().sum()).backward()
+        grads.append((h.grad.clone(), a.grad.clone() if add else None))
+    assert torch.equal(grads[0][0], grads[1][0])
+    if add:
+        assert torch.equal(grads[0][1], grads[1][1])
