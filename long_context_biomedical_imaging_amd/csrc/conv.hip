@@ -539,24 +539,24 @@ __global__ __launch_bounds__(256) void conv3_pack_kernel(const float* __restrict
 // moved to the channels-last output grid (B, D*kd, H*kh, W*kw) whose rows have `ld` channels (ld = C, or 2C when the
 // result is written straight into the first half of UnetrUpBlock's torch.cat buffer); adjoint: the output-grid rows
 // gathered back to Y's layout. One thread per (input voxel, tap, 16-byte chunk): both sides are whole 2C-byte rows.
+// grid (ceil(W taps C/8 / 256), min(B D H, 65535)): one input row (b, z, y) per block row (a loop over rows beyond the
+// grid), so the per-chunk index math is 32-bit (the grid-stride form's 64-bit divisions cost as much as the copy).
 __global__ __launch_bounds__(256) void convup_interleave_kernel(const bf16* __restrict__ src, bf16* __restrict__ dst,
-                                                                long long n, int D, int H, int W, int kd, int kh,
+                                                                long long nrows, int D, int H, int W, int kd, int kh,
                                                                 int kw, int C, int ld, int adjoint) {
   const int CC = C >> 3;                       // 16-byte chunks per row
   const int taps = kd * kh * kw;
-  const long long stride = (long long)gridDim.x * 256;
-  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n; e += stride) {
-    const int ch = (int)(e % CC);
-    long long q = e / CC;
-    const int t = (int)(q % taps);
-    const long long v = q / taps;              // input voxel (b, z, y, x)
-    const int x = (int)(v % W);
-    long long r = v / W;
-    const int y = (int)(r % H);
-    r /= H;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= W * taps * CC) return;
+  const int ch = e % CC, q = e / CC;
+  const int t = q % taps, x = q / taps;
+  const int a = t / (kh * kw), bb = (t / kw) % kh, c = t % kw;
+  for (long long row = blockIdx.y; row < nrows; row += gridDim.y) {
+    const int y = (int)(row % H);
+    const long long r = row / H;
     const int z = (int)(r % D);
     const long long b = r / D;
-    const int a = t / (kh * kw), bb = (t / kw) % kh, c = t % kw;
+    const long long v = row * W + x;           // input voxel (b, z, y, x)
     const long long o = (((b * D + z) * kd + a) * ((long long)H * kh) + (long long)y * kh + bb) * ((long long)W * kw) +
                         (long long)x * kw + c;    // output voxel
     const long long yoff = (v * taps + t) * C + 8 * ch, ooff = o * ld + 8 * ch;
@@ -1141,9 +1141,11 @@ extern "C" int lci_convup_interleave(const void* src, void* dst, int B, int D, i
   LCI_CHECK(B > 0 && D > 0 && H > 0 && W > 0 && kd > 0 && kh > 0 && kw > 0 && C > 0 && C % 8 == 0 && ld >= C &&
                 ld % 8 == 0, "convup_interleave: bad shape (C, ld multiples of 8)");
   LCI_CHECK(((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0, "convup_interleave: pointers must be 16-byte aligned");
-  const long long n = (long long)B * D * H * W * kd * kh * kw * (C / 8);
-  hipLaunchKernelGGL(convup_interleave_kernel, dim3((unsigned)std::min<long long>((n + 255) / 256, 65536)), dim3(256),
-                     0, (hipStream_t)stream, (const bf16*)src, (bf16*)dst, n, D, H, W, kd, kh, kw, C, ld, adjoint);
+  const long long per_row = (long long)W * kd * kh * kw * (C / 8), nrows = (long long)B * D * H;
+  LCI_CHECK(per_row < (1LL << 31), "convup_interleave: row too wide");
+  hipLaunchKernelGGL(convup_interleave_kernel, dim3((unsigned)((per_row + 255) / 256),
+                     (unsigned)std::min<long long>(nrows, 65535)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16*)src, (bf16*)dst, nrows, D, H, W, kd, kh, kw, C, ld, adjoint);
   LCI_LAUNCH_CHECK();
   return 0;
 }
