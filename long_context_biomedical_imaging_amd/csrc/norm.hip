@@ -59,21 +59,33 @@ __global__ __launch_bounds__(256) void inorm_reduce_kernel(NormArgs a) {
   }
   if (r < rows) {
     const long long base = (long long)b * a.V * a.C + 8 * g;
-    for (long long v = v0 + r; v < v1; v += rows) {
-      float x[8];
-      load8(a.x + base + v * a.C, x);
-      if (!BWD) {
+    // UN voxels per iteration, their loads issued together (one 16-byte load in flight per lane held the pass near
+    // 2-3 TB/s); the sums keep the single-voxel order (voxel v, then v + rows, ...)
+    constexpr int UN = 4;
+    for (long long v = v0 + r; v < v1; v += UN * rows) {
+      float x[UN][8], d[UN][8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { s1[j] += x[j]; s2[j] += x[j] * x[j]; }
-      } else {
-        float d[8];
-        load8(a.dz + base + v * a.C, d);
+      for (int u = 0; u < UN; ++u) {
+        const long long vu = v + (long long)u * rows;
+        if (vu < v1) {
+          load8(a.x + base + vu * a.C, x[u]);
+          if (BWD) load8(a.dz + base + vu * a.C, d[u]);
+        }
+      }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float n = (x[j] - mu[j]) * rs[j];
-          const float dn = (a.act && n < 0.f) ? d[j] * a.slope : d[j];
-          s1[j] += dn;
-          s2[j] += dn * n;
+      for (int u = 0; u < UN; ++u) {
+        if (v + (long long)u * rows >= v1) break;
+        if (!BWD) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { s1[j] += x[u][j]; s2[j] += x[u][j] * x[u][j]; }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float n = (x[u][j] - mu[j]) * rs[j];
+            const float dn = (a.act && n < 0.f) ? d[u][j] * a.slope : d[u][j];
+            s1[j] += dn;
+            s2[j] += dn * n;
+          }
         }
       }
     }
@@ -98,32 +110,33 @@ __global__ __launch_bounds__(256) void inorm_reduce_kernel(NormArgs a) {
 template <bool BWD>
 __global__ __launch_bounds__(256) void inorm_apply_kernel(NormArgs a) {
   const int G = a.C >> 3;
-  const long long e = blockIdx.x * 256LL + threadIdx.x;   // 8-channel group index over (B, V, G)
+  const long long e0 = blockIdx.x * 256LL;                 // 8-channel group index over (B, V, G)
+  const long long e = e0 + threadIdx.x;
   const int b = blockIdx.y;
   if (e >= a.V * G) return;
-  const int g = (int)(e % G);
+  // the block's first group modulo G is workgroup-uniform (scalar); the lane's is then a 32-bit remainder
+  const int g = ((int)(e0 % G) + (int)threadIdx.x) % G;
   const long long off = (long long)b * a.V * a.C + e * 8;
-  const float* st = a.stats + (long long)b * 2 * a.C + 8 * g;
-  float x[8];
+  float x[8], mu[8], rs[8];
   load8(a.x + off, x);
+  load_stats(a.stats + (long long)b * 2 * a.C + 8 * g, a.C, mu, rs);   // f32x4 loads, not 16 scalar ones
   bf16x8 o;
   if (!BWD) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float n = (x[j] - st[j]) * st[a.C + j];
+      float n = (x[j] - mu[j]) * rs[j];
       if (a.act && n < 0.f) n *= a.slope;
       o[j] = to_bf16(n);
     }
   } else {
-    float d[8];
+    float d[8], c1[8], c2[8];
     load8(a.dz + off, d);
-    const float* cf = a.coef + (long long)b * 2 * a.C + 8 * g;
+    load_stats(a.coef + (long long)b * 2 * a.C + 8 * g, a.C, c1, c2);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float rs = st[a.C + j];
-      const float n = (x[j] - st[j]) * rs;
+      const float n = (x[j] - mu[j]) * rs[j];
       const float dn = (a.act && n < 0.f) ? d[j] * a.slope : d[j];
-      o[j] = to_bf16(rs * (dn - cf[j] - n * cf[a.C + j]));
+      o[j] = to_bf16(rs[j] * (dn - c1[j] - n * c2[j]));
     }
   }
   *(bf16x8*)(a.out + off) = o;
@@ -139,7 +152,7 @@ __global__ __launch_bounds__(256) void inorm_res_kernel(NormArgs a, const bf16* 
   const long long e = blockIdx.x * 256LL + threadIdx.x;
   const int b = blockIdx.y;
   if (e >= a.V * G) return;
-  const int g = (int)(e % G);
+  const int g = ((int)((e - threadIdx.x) % G) + (int)threadIdx.x) % G;   // uniform 64-bit part, 32-bit lane part
   const long long off = (long long)b * a.V * a.C + e * 8;
   float x[8], r[8], mu[8], rs[8], muy[8], rsy[8];
   load8(a.x + off, x);
@@ -229,19 +242,28 @@ __device__ __forceinline__ void load8f(const void* p, long long off, bool f32, f
   }
 }
 
+// the affine parameters of 8 consecutive channels as f32x4 loads
+__device__ __forceinline__ void load_wb(const float* w, const float* b, int g, float* wv, float* bv) {
+  const f32x4 w0 = *(const f32x4*)(w + 8 * g), w1 = *(const f32x4*)(w + 8 * g + 4);
+  const f32x4 b0 = *(const f32x4*)(b + 8 * g), b1 = *(const f32x4*)(b + 8 * g + 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { wv[j] = w0[j]; wv[4 + j] = w1[j]; bv[j] = b0[j]; bv[4 + j] = b1[j]; }
+}
+
 __global__ __launch_bounds__(256) void bn_relu_fwd_kernel(BnArgs a) {
   const int G = a.C >> 3;
   const long long e = blockIdx.x * 256LL + threadIdx.x;
   if (e >= a.V * G) return;
-  const int g = (int)(e % G);
-  float x[8], mu[8], rs[8];
+  const int g = ((int)((e - threadIdx.x) % G) + (int)threadIdx.x) % G;   // uniform 64-bit part, 32-bit lane part
+  float x[8], mu[8], rs[8], wv[8], bv[8];
   load8(a.x + e * 8, x);
   load_stats(a.stats + 8 * g, a.C, mu, rs);
+  load_wb(a.w, a.b, g, wv, bv);
   float* y = (float*)a.out + e * 8;
   float o[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const float v = __fadd_rn(__fmul_rn(__fmul_rn(__fsub_rn(x[j], mu[j]), rs[j]), a.w[8 * g + j]), a.b[8 * g + j]);
+    const float v = __fadd_rn(__fmul_rn(__fmul_rn(__fsub_rn(x[j], mu[j]), rs[j]), wv[j]), bv[j]);
     o[j] = v > 0.f ? v : 0.f;
   }
   *(f32x4*)y = f32x4{o[0], o[1], o[2], o[3]};
@@ -295,18 +317,19 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_kernel(BnArgs a) {
   const int G = a.C >> 3;
   const long long e = blockIdx.x * 256LL + threadIdx.x;
   if (e >= a.V * G) return;
-  const int g = (int)(e % G);
-  float x[8], d[8], mu[8], rs[8], m1[8], m2[8];
+  const int g = ((int)((e - threadIdx.x) % G) + (int)threadIdx.x) % G;   // uniform 64-bit part, 32-bit lane part
+  float x[8], d[8], mu[8], rs[8], m1[8], m2[8], wv[8], bv[8];
   load8(a.x + e * 8, x);
   load8f(a.dy, e * 8, a.dy_f32 != 0, d);
   load_stats(a.stats + 8 * g, a.C, mu, rs);
   load_stats(a.coef + 8 * g, a.C, m1, m2);
+  load_wb(a.w, a.b, g, wv, bv);
   bf16x8 o;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const float w = a.w[8 * g + j];
+    const float w = wv[j];
     const float n = __fmul_rn(__fsub_rn(x[j], mu[j]), rs[j]);
-    const float gg = __fadd_rn(__fmul_rn(n, w), a.b[8 * g + j]) > 0.f ? d[j] : 0.f;
+    const float gg = __fadd_rn(__fmul_rn(n, w), bv[j]) > 0.f ? d[j] : 0.f;
     o[j] = to_bf16((gg - m1[j] - n * m2[j]) * (rs[j] * w));
   }
   *(bf16x8*)((bf16*)a.out + e * 8) = o;
