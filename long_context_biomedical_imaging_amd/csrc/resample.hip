@@ -301,16 +301,15 @@ __device__ __forceinline__ void adj_acc(const Adj1Args& a, long long off, float 
   }
 }
 
+// grid (ceil(n_in inner/8 / 256), min(outer, 65535)): 32-bit (input sample, chunk) index math, outer rows by block row
 __global__ __launch_bounds__(256) void resample1d_adj_kernel(Adj1Args a) {
-  const long long I8 = a.inner / 8;
-  const long long total = a.outer * a.n_in * I8;
-  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
-    const long long q = t % I8;
-    long long p = t / I8;
-    const int i = (int)(p % a.n_in);
-    const long long ou = p / a.n_in;
-    int lo, hi;
-    adj_range(a, i, lo, hi);
+  const int I8 = (int)(a.inner / 8);
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= a.n_in * I8) return;
+  const int i = e / I8, q = e - i * I8;
+  int lo, hi;
+  adj_range(a, i, lo, hi);
+  for (long long ou = blockIdx.y; ou < a.outer; ou += gridDim.y) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int o = lo; o <= hi; ++o) {
       const float w = adj_weight(a, o, i);
@@ -533,8 +532,10 @@ extern "C" int lci_resample1d_adj_ac(const void* dy, int dy_bf16, float* dx, lon
     LCI_CHECK(nblk < (1LL << 31), "resample1d_adj: grid too large");
     hipLaunchKernelGGL(resample1d_adj_wide_kernel, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, a);
   } else {
-    hipLaunchKernelGGL(resample1d_adj_kernel, dim3(up_grid(outer * n_in * (inner / 8))), dim3(256), 0,
-                       (hipStream_t)stream, a);
+    LCI_CHECK((long long)n_in * (inner / 8) < (1LL << 31), "resample1d_adj: row too wide");
+    hipLaunchKernelGGL(resample1d_adj_kernel, dim3((unsigned)(((long long)n_in * (inner / 8) + 255) / 256),
+                                                   (unsigned)std::min<long long>(outer, 65535)),
+                       dim3(256), 0, (hipStream_t)stream, a);
   }
   LCI_LAUNCH_CHECK();
   return 0;
