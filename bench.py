@@ -50,7 +50,9 @@ HBM_PEAK_GBS = 8000.0
 ROOF = {"selective_scan_fwd": ("hbm", 1.0), "selective_scan_bwd": ("hbm", 1.0),
         "fftconv_fwd": ("hbm", 8.0), "fftconv_bwd": ("hbm", 16.0),
         # LayerNorm work is counted in bytes already (f32 x in, bf16 y out; bwd + bf16 dy in, f32 dx out)
-        "ln_fwd": ("hbm", 1.0), "ln_bwd": ("hbm", 1.0),
+        "ln_fwd": ("hbm", 1.0), "ln_bwd": ("hbm", 1.0), "ln_add_fwd": ("hbm", 1.0),
+        # GELU work is its bytes too (bf16 x in, y out; bwd + dy in)
+        "gelu_fwd": ("hbm", 1.0), "gelu_bwd": ("hbm", 1.0),
         # direct (Toeplitz) long conv of Swin-window rows: FLOPs on the f32-input MFMA (157.3 TF dense)
         "direct_conv_fwd": ("mfma_f32", 1.0), "direct_conv_bwd": ("mfma_f32", 1.0), "direct_conv_dk": ("mfma_f32", 1.0)}
 MFMA_F32_PEAK_TFLOPS = 157.3     # v_mfma_f32_32x32x2_f32, MI355X_MICROARCH.md chip table

@@ -58,8 +58,9 @@ extern "C" {
  * dtype; 20: lci_attn_gen_fwd / lci_attn_gen_bwd; 21: lci_gemm_bt; 22: lci_linear_fwd removed, superseded by
  * lci_gemm_bt; 23: lci_fftconv_spectrum Dv; 24: lci_inorm_finalize; 25: lci_adam_step; 26: Hyena gate dx2 / gx2
  * in the activation dtype; 27: lci_layernorm_bwd dxb; 28: lci_resample_cl_fwd, lci_resample1d_adj_ac; 29: lci_bn_relu_*; 30: lci_gemm_bt_acc;
- * 31: lci_layernorm_bwd dres2). */
-#define LCI_ABI_VERSION 31
+ * 31: lci_layernorm_bwd dres2; 32: one-chunk selective scan without end-state workspaces (xend / xinit / sdt null),
+ * lci_selective_scan_bwd_plain_dbc). */
+#define LCI_ABI_VERSION 32
 const char* lci_last_error(void);
 int lci_abi_version(void);
 /* sha256 prefix of the sources the library was built from (build_lib.source_hash); the Python binding refuses a
@@ -216,18 +217,23 @@ int lci_inorm_apply_res(const void* x, const float* stats, const void* y, const 
  * A (Dx, 8), D (Dx), delta_bias (Dx) f32 (D, delta_bias may be null). delta' = softplus(delta + delta_bias)
  * when delta_softplus, else delta + delta_bias.
  * chunk: multiple of 8. Workspaces f32: xend, xinit (B*nch*Dx*8), sdt (B*nch*Dx), nch = ceil(L/chunk);
- * ckpt (B*ceil(L/8)*Dx*8) elements of the I/O dtype (bf16 I/O: bf16 states) or null (needed by the backward). */
+ * ckpt (B*ceil(L/8)*Dx*8) elements of the I/O dtype (bf16 I/O: bf16 states) or null (needed by the backward).
+ * With one chunk (L <= chunk, e.g. Swin-window sequences) xend / xinit / sdt may all be null: only the output pass
+ * runs (nothing is carried into the chunk) and the final state is not produced. */
 int lci_selective_scan_fwd(int dtype, const void* u, const void* delta, const float* A, const void* Bm,
                            const void* Cm, const float* D, const float* delta_bias, void* y,
                            const long long* strides, int B, int L, int Dx, int N, int chunk, int delta_softplus,
                            float* xend, float* xinit, float* sdt, void* ckpt, void* stream);
-/* du, ddelta (B, L, Dx) written; dBC (B, L, 16) f32 = [dB | dC], dA (Dx, 8), dD, ddelta_bias accumulated.
- * sdt / ckpt from the forward with the same chunk; gl, gin: (B*nch*Dx*8) f32 workspaces. */
+/* du, ddelta (B, L, Dx) written; dBC (B, L, 16) f32 = [dB | dC], dA (Dx, 8), dD, ddelta_bias accumulated (dBC stored
+ * instead, needing no zero fill, where lci_selective_scan_bwd_plain_dbc(L, Dx, chunk) returns 1).
+ * sdt / ckpt from the forward with the same chunk (sdt null after a one-chunk forward without end states: the
+ * adjoint aggregate and reverse carry are skipped); gl, gin: (B*nch*Dx*8) f32 workspaces. */
 int lci_selective_scan_bwd(int dtype, const void* u, const void* delta, const float* A, const void* Bm,
                            const void* Cm, const float* D, const float* delta_bias, const void* dy, void* du,
                            void* ddelta, float* dBC, float* dA, float* dD, float* ddelta_bias,
                            const long long* strides, int B, int L, int Dx, int N, int chunk, int delta_softplus,
                            const float* sdt, const void* ckpt, float* gl, float* gin, void* stream);
+int lci_selective_scan_bwd_plain_dbc(int L, int Dx, int chunk);
 
 /* SiLU(depthwise conv1d(k = 3, 'same')) of both channel halves of in (B, L, 2C) (token stride in_ts):
  * ox (B, L, C) (token stride ox_ts) and oz at column offset zoff of a (B, L, oz_ts) buffer. */

@@ -14,7 +14,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_LIB = os.path.join(HERE, "liblci.so")
 LIB_PATH = os.environ.get("LCI_LIB_PATH", DEFAULT_LIB)   # override: kernel-variant A/B runs (no staleness check)
-ABI_VERSION = 31   # include/lci.h LCI_ABI_VERSION
+ABI_VERSION = 32   # include/lci.h LCI_ABI_VERSION
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -124,6 +124,8 @@ def load(path: str = LIB_PATH):
     lib.lci_window_pad_ws_elems.argtypes = [_P]
     lib.lci_window_bwd_needs_plain.restype = ctypes.c_int
     lib.lci_window_bwd_needs_plain.argtypes = [_P]
+    lib.lci_selective_scan_bwd_plain_dbc.restype = ctypes.c_int
+    lib.lci_selective_scan_bwd_plain_dbc.argtypes = [_I, _I, _I]
     lib.lci_window_bias_elems.restype = ctypes.c_longlong
     lib.lci_window_bias_elems.argtypes = [_P, _I]
     lib.lci_attn_bwd_ws_bytes.restype = ctypes.c_longlong

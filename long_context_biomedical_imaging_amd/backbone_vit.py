@@ -187,12 +187,14 @@ class ViT_with_alt_ops(nn.Module):
         # True = every block; an int k = the first k blocks only (the rest keep their activations: less recompute
         # where the memory allows it).
         self.checkpoint_blocks = False
-        # hidden_states_out indices some consumer reads (None: all); the others are returned as None
-        self.keep_hidden = None
         if self.classification and not use_hyena and not use_mamba:
             self.cls_token = nn.Parameter(torch.zeros(1, 1, hidden_size))
 
-    def forward(self, x):
+    def forward(self, x, keep_hidden=None):
+        """Returns hidden_states_out as the reference's (backbone_vit.py:379-397): [image, block outputs 1..L,
+        LN(last)]. keep_hidden (not a reference argument; EncoderDecoderModel passes its decoder's `hidden_taps`):
+        the hidden_states_out indices the caller reads; the other block outputs come back as None. The default
+        (None) returns every entry, as the reference does, to any other caller."""
         if self.spatial_dims == 2:
             x = x.squeeze(2)
         hidden_states_out = [x]
@@ -205,11 +207,11 @@ class ViT_with_alt_ops(nn.Module):
         # h + m, which is also what hidden_states_out records (the same tensor); only the last block's output is a
         # separate add. A checkpointed block saves its inputs, so where its input is also a recorded hidden state
         # the stream is materialised as one tensor there (the add; the checkpoint and the list share it) -- the pair
-        # would hold h, m and the sum. keep_hidden (set by EncoderDecoderModel from the decoder's taps) leaves the
-        # block outputs no decoder reads as None, so untapped checkpoint boundaries keep the pair (+1 bf16 tensor per
+        # would hold h, m and the sum. keep_hidden (the decoder's taps, from EncoderDecoderModel) leaves the block
+        # outputs no decoder reads as None, so untapped checkpoint boundaries keep the pair (+1 bf16 tensor per
         # boundary, 1.6 GB at 2^21 tokens) and skip the add, its recompute and its backward cast.
         def keep(idx):
-            return self.keep_hidden is None or idx in self.keep_hidden
+            return keep_hidden is None or idx in keep_hidden
 
         train = self.training and torch.is_grad_enabled()
         h, m = x, None

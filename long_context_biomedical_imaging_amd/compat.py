@@ -30,8 +30,8 @@ def selective_scan_fn(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_
     bc = torch.cat([B.to(dt).transpose(1, 2), C.to(dt).transpose(1, 2)], dim=-1).contiguous()
     yz = torch.empty(b, L, 2 * d, device=u.device, dtype=dt)
     res = kernels.selective_scan_cl(ucl, dcl, A, bc[..., :n], bc[..., n:], D, delta_bias, yz,
-                                    delta_softplus=delta_softplus, return_last_state=True)
-    out, last = res
+                                    delta_softplus=delta_softplus, return_last_state=return_last_state)
+    out, last = res if return_last_state else (res, None)
     y = out[..., :d].transpose(1, 2).to(u.dtype)
     return (y, last) if return_last_state else y
 

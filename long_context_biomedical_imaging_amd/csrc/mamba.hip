@@ -36,6 +36,9 @@ struct ScanArgs {
   int B, L, Dx, Tc, nch, nck;
   int write_ckpt;
   int softplus;                                         // delta_softplus
+  int zero_carry;                                       // one chunk: no carry-in (xinit / gin not read)
+  int dbc_plain;                                        // one workgroup per (b, chunk) covers every channel:
+                                                        // dBC entries stored, not accumulated (no zero fill)
 };
 
 template <typename T> __device__ __forceinline__ float ldf(const T* p) { return (float)(*p); }
@@ -224,7 +227,7 @@ __global__ __launch_bounds__(256) void scan_fwd_kernel(ScanArgs a) {
   const float Dd = a.D ? a.D[dd] : 0.f;
   const long long sidx = (((long long)b * a.nch + chunk) * a.Dx + dd) * SCAN_N;
 #pragma unroll
-  for (int n = 0; n < SCAN_N; ++n) x[n] = MODE ? a.xinit[sidx + n] : 0.f;
+  for (int n = 0; n < SCAN_N; ++n) x[n] = MODE && !a.zero_carry ? a.xinit[sidx + n] : 0.f;
   // per-step addresses = wave-uniform row base (scalar arithmetic) + this lane's channel offset
   const Col<T> ucol((const T*)a.u + b * a.bu, a.L, a.tu, a.Dx, d, valid);
   const Col<T> dcol((const T*)a.delta + b * a.bd, a.L, a.td, a.Dx, d, valid);
@@ -512,7 +515,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
       A2[k] = f32x2{a.A[dd * SCAN_N + 2 * k], a.A[dd * SCAN_N + 2 * k + 1]} * LOG2E;
-      h[k] = valid ? f32x2{gi[2 * k], gi[2 * k + 1]} : f32x2{0.f, 0.f};
+      h[k] = valid && !a.zero_carry ? f32x2{gi[2 * k], gi[2 * k + 1]} : f32x2{0.f, 0.f};
       dA[k] = f32x2{0.f, 0.f};
     }
   }
@@ -551,7 +554,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int k = tid; k < SB * 2 * SCAN_N; k += blockDim.x) {
           const int i = k / (2 * SCAN_N), j = k % (2 * SCAN_N);
           const int t = blk0 + i;
-          if (t < t1) atomicAdd(a.dBC + ((long long)b * a.L + t) * (2 * SCAN_N) + j, red[i][j]);
+          float* dst = a.dBC + ((long long)b * a.L + t) * (2 * SCAN_N) + j;
+          if (t < t1) {
+            if (a.dbc_plain) *dst = red[i][j];
+            else atomicAdd(dst, red[i][j]);
+          }
           red[i][j] = 0.f;
         }
       }
@@ -638,7 +645,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   for (int k = tid; k < SB * 2 * SCAN_N; k += blockDim.x) {
     const int i = k / (2 * SCAN_N), j = k % (2 * SCAN_N);
     const int t = blk0 + i;
-    if (t < t1) atomicAdd(a.dBC + ((long long)b * a.L + t) * (2 * SCAN_N) + j, red[i][j]);
+    float* dst = a.dBC + ((long long)b * a.L + t) * (2 * SCAN_N) + j;
+    if (t < t1) {
+      if (a.dbc_plain) *dst = red[i][j];
+      else atomicAdd(dst, red[i][j]);
+    }
   }
   if constexpr (PARTIALS) {
     if (!valid) return;
@@ -968,6 +979,9 @@ static int scan_strides(ScanArgs& a, const long long* s, int dtype) {
 }
 
 // Workspace (f32): xend, xinit (B*nch*Dx*N each), sdt (B*nch*Dx); ckpt (B*nck*Dx*N, the I/O dtype) if not null.
+// With one chunk (L <= chunk: the Swin recipes' window sequences) xend / xinit / sdt may be null: the zero-init
+// end-state pass and the carry are then skipped (nothing is carried into the only chunk) and only the output
+// pass runs; the final state is not produced.
 extern "C" int lci_selective_scan_fwd(int dtype, const void* u, const void* delta, const float* A, const void* Bm,
                                       const void* Cm, const float* D, const float* delta_bias, void* y,
                                       const long long* strides, int B, int L, int Dx, int N, int chunk,
@@ -980,6 +994,10 @@ extern "C" int lci_selective_scan_fwd(int dtype, const void* u, const void* delt
   if (scan_check_bc(Bm, Cm, strides[5], strides[7], dtype)) return 1;
   a.u = u; a.delta = delta; a.A = A; a.Bm = Bm; a.Cm = Cm; a.D = D; a.dbias = delta_bias; a.y = y;
   a.xend = xend; a.xinit = xinit; a.sdt = sdt; a.ckpt = ckpt; a.write_ckpt = ckpt != nullptr;
+  const bool one = !xend || !xinit || !sdt;
+  LCI_CHECK(!one || (!xend && !xinit && !sdt && a.nch == 1),
+            "selective_scan_fwd: null end-state workspaces only with one chunk (L=%d, chunk %d)", L, chunk);
+  a.zero_carry = one;
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((a.nch + 3) / 4, (Dx + 63) / 64, B);
   // LCI_SCAN_PF=0: the forward passes without the software-pipelined loads (A/B hook)
@@ -994,17 +1012,35 @@ extern "C" int lci_selective_scan_fwd(int dtype, const void* u, const void* delt
       else hipLaunchKernelGGL((scan_fwd_kernel<float, M, false>), grid, dim3(256), 0, s, a);
     }
   };
-  chunk_pass(std::integral_constant<int, 0>{});
-  LCI_LAUNCH_CHECK();
-  hipLaunchKernelGGL(scan_carry_kernel<false>, dim3(Dx, B), dim3(64), 0, s, a);
-  LCI_LAUNCH_CHECK();
+  if (!one) {
+    chunk_pass(std::integral_constant<int, 0>{});
+    LCI_LAUNCH_CHECK();
+    hipLaunchKernelGGL(scan_carry_kernel<false>, dim3(Dx, B), dim3(64), 0, s, a);
+    LCI_LAUNCH_CHECK();
+  }
   chunk_pass(std::integral_constant<int, 1>{});
   LCI_LAUNCH_CHECK();
   return 0;
 }
 
-// dA (Dx*N), dD (Dx), ddelta_bias (Dx) and dBC (B, L, 2N) are accumulated (caller zeroes them).
-// Workspace: gl, gin (B*nch*Dx*N each); sdt and ckpt from the forward (same chunk).
+static int scan_bwd_waves(int Tc, int Dx) {
+  static const int wenv = getenv("LCI_SCAN_BWD_WAVES") ? atoi(getenv("LCI_SCAN_BWD_WAVES")) : 0;
+  const int wmax = wenv > 0 ? wenv : (Tc >= 512 ? 1 : 4);
+  return std::max(1, std::min(std::min(wmax, 4), (Dx + 63) / 64));
+}
+
+// 1: lci_selective_scan_bwd stores every dBC entry exactly once at this shape (one workgroup per (b, chunk) holds
+// all Dx channels), so dBC needs no zero fill; 0: it accumulates into dBC with atomics.
+extern "C" int lci_selective_scan_bwd_plain_dbc(int L, int Dx, int chunk) {
+  (void)L;
+  const int nwv = scan_bwd_waves(chunk, Dx);
+  return (Dx + nwv * 64 - 1) / (nwv * 64) == 1;
+}
+
+// dA (Dx*N), dD (Dx), ddelta_bias (Dx) are accumulated (caller zeroes them); dBC (B, L, 2N) too, except where
+// lci_selective_scan_bwd_plain_dbc says every entry is stored once (no zero fill needed).
+// Workspace: gl, gin (B*nch*Dx*N each); sdt and ckpt from the forward (same chunk). sdt null (one chunk, the
+// forward ran without end states): the adjoint aggregate and the reverse carry are skipped.
 extern "C" int lci_selective_scan_bwd(int dtype, const void* u, const void* delta, const float* A, const void* Bm,
                                       const void* Cm, const float* D, const float* delta_bias, const void* dy,
                                       void* du, void* ddelta, float* dBC, float* dA, float* dD, float* ddelta_bias,
@@ -1019,22 +1055,25 @@ extern "C" int lci_selective_scan_bwd(int dtype, const void* u, const void* delt
   a.u = u; a.delta = delta; a.A = A; a.Bm = Bm; a.Cm = Cm; a.D = D; a.dbias = delta_bias; a.dy = dy;
   a.du = du; a.ddelta = ddelta; a.dBC = dBC; a.dA = dA; a.dD = dD; a.ddbias = ddelta_bias;
   a.sdt = (float*)sdt; a.ckpt = const_cast<void*>(ckpt); a.gl = gl; a.gin = gin;
+  LCI_CHECK(sdt || a.nch == 1, "selective_scan_bwd: sdt is null with %d chunks", a.nch);
+  a.zero_carry = sdt == nullptr;
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((a.nch + 3) / 4, (Dx + 63) / 64, B);
-  if (dtype == 1) hipLaunchKernelGGL((scan_bwd_agg_kernel<bf16>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((scan_bwd_agg_kernel<float>), grid, dim3(256), 0, s, a);
-  LCI_LAUNCH_CHECK();
-  hipLaunchKernelGGL(scan_carry_kernel<true>, dim3(Dx, B), dim3(64), 0, s, a);
-  LCI_LAUNCH_CHECK();
+  if (!a.zero_carry) {
+    if (dtype == 1) hipLaunchKernelGGL((scan_bwd_agg_kernel<bf16>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((scan_bwd_agg_kernel<float>), grid, dim3(256), 0, s, a);
+    LCI_LAUNCH_CHECK();
+    hipLaunchKernelGGL(scan_carry_kernel<true>, dim3(Dx, B), dim3(64), 0, s, a);
+    LCI_LAUNCH_CHECK();
+  }
   // waves per workgroup (channel blocks of 64 sharing one chunk's B/C staging and dB/dC sums): at 254 VGPRs
   // (2 waves per SIMD) 3-wave groups leave 2 of a CU's 8 wave slots empty and two SIMDs with one wave each, so
   // long chunks run one wave per workgroup (L=2^21: 7.8 -> 6.6 ms); short chunks keep the shared staging, whose
   // per-token dB/dC flush (one set of global atomics per workgroup and token) dominates there (L=65536, Tc=64:
   // 0.60 ms at 4 waves vs 0.80 at 1). LCI_SCAN_BWD_WAVES overrides.
-  static const int wenv = getenv("LCI_SCAN_BWD_WAVES") ? atoi(getenv("LCI_SCAN_BWD_WAVES")) : 0;
-  const int wmax = wenv > 0 ? wenv : (a.Tc >= 512 ? 1 : 4);
-  const int nwv = std::max(1, std::min(std::min(wmax, 4), (Dx + 63) / 64));
+  const int nwv = scan_bwd_waves(a.Tc, Dx);
   dim3 gridc(a.nch, (Dx + nwv * 64 - 1) / (nwv * 64), B);
+  a.dbc_plain = gridc.y == 1;
   // parameter gradients: the B * nch float atomics per address from the waves' ends serialise in L2 (the dwconv
   // backward's lesson): short chunks write partials and sum them in one more launch (L=65536: 0.60 -> 0.42 ms).
   // Long chunks keep the atomics: there the partials build of the kernel measured slower (8.6 vs 6.9 ms at L=2^21,

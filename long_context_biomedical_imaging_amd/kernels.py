@@ -355,7 +355,7 @@ def dwconv_silu_pair(xz, wx, bx, wz, bz):
 
 class _SelectiveScanCL(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, u, delta, A, Bm, Cm, D, delta_bias, yz, softplus=True):
+    def forward(ctx, u, delta, A, Bm, Cm, D, delta_bias, yz, softplus=True, want_last=False):
         B, L, Dx = u.shape
         N = A.shape[1]
         ctx.bc_joint = Cm is None            # Bm = [B | C] in one (B, L, 2N) tensor: one gradient for both
@@ -366,9 +366,12 @@ class _SelectiveScanCL(torch.autograd.Function):
         nch = -(-L // tc)
         nck = -(-L // CKPT)
         f32 = dict(device=u.device, dtype=torch.float32)
-        xend = torch.empty(B, nch, Dx, N, **f32)
-        xinit = torch.empty(B, nch, Dx, N, **f32)
-        sdt = torch.empty(B, nch, Dx, **f32)
+        # one chunk (the Swin recipes' window sequences, L <= 512): nothing is carried into it, so without a
+        # requested final state the end-state pass and the carry are skipped (lci.h ABI 32)
+        one = nch == 1 and not want_last
+        xend = None if one else torch.empty(B, nch, Dx, N, **f32)
+        xinit = None if one else torch.empty(B, nch, Dx, N, **f32)
+        sdt = None if one else torch.empty(B, nch, Dx, **f32)
         need_grad = any(ctx.needs_input_grad)
         # states every CKPT steps for the backward's recompute, in the I/O dtype (bf16 I/O: bf16 states, half the bytes)
         ckpt = torch.empty(B, nck, Dx, N, device=u.device, dtype=dt) if need_grad else None
@@ -381,15 +384,17 @@ class _SelectiveScanCL(torch.autograd.Function):
         KernelTimer.run("selective_scan_fwd", float(B * L * (3 * Dx + 2 * N) * es), u, lambda: _lib.call(
             "lci_selective_scan_fwd", _DT[dt], u.data_ptr(), delta.data_ptr(), Af.data_ptr(), Bm.data_ptr(),
             Cm.data_ptr(), Dv.data_ptr(), bv.data_ptr(), y.data_ptr(), strides, B, L, Dx, N, tc, int(softplus),
-            xend.data_ptr(), xinit.data_ptr(), sdt.data_ptr(), _lib.ptr(ckpt), _lib.stream_of(u)))
+            _lib.ptr(xend), _lib.ptr(xinit), _lib.ptr(sdt), _lib.ptr(ckpt), _lib.stream_of(u)))
         ctx.mark_dirty(yz)
         if need_grad:
             ctx.save_for_backward(u, delta, Af, Bm, Cm, Dv, bv, sdt, ckpt)
         ctx.tc, ctx.softplus = tc, softplus
         ctx.z_half_only = getattr(yz, "_lci_z_half_only", False)
         ctx.has_D, ctx.has_b = D is not None, delta_bias is not None
-        # final state x_L = exp(A sum(dt) over the last chunk) xinit_last + xend_last (return_last_state)
-        last = torch.exp(Af[None] * sdt[:, -1, :, None]) * xinit[:, -1] + xend[:, -1]
+        if one:   # no final state requested (an empty placeholder output)
+            last = torch.empty(0, **f32)
+        else:     # final state x_L = exp(A sum(dt) over the last chunk) xinit_last + xend_last (return_last_state)
+            last = torch.exp(Af[None] * sdt[:, -1, :, None]) * xinit[:, -1] + xend[:, -1]
         ctx.mark_non_differentiable(last)
         return yz, last
 
@@ -407,7 +412,8 @@ class _SelectiveScanCL(torch.autograd.Function):
         f32 = dict(device=u.device, dtype=torch.float32)
         du = torch.empty_like(u)
         dd = torch.empty(B, L, Dx, device=u.device, dtype=u.dtype)
-        dBC = torch.zeros(B, L, 2 * N, **f32)
+        plain = _lib.load().lci_selective_scan_bwd_plain_dbc(L, Dx, tc)   # every entry stored once: no zero fill
+        dBC = (torch.empty if plain else torch.zeros)(B, L, 2 * N, **f32)
         dA = torch.zeros(Dx, N, **f32)
         dD = torch.zeros(Dx, **f32)
         db = torch.zeros(Dx, **f32)
@@ -419,7 +425,7 @@ class _SelectiveScanCL(torch.autograd.Function):
             "lci_selective_scan_bwd", _DT[u.dtype], u.data_ptr(), delta.data_ptr(), Af.data_ptr(), Bm.data_ptr(),
             Cm.data_ptr(), Dv.data_ptr(), bv.data_ptr(), dy.data_ptr(), du.data_ptr(), dd.data_ptr(),
             dBC.data_ptr(), dA.data_ptr(), dD.data_ptr(), db.data_ptr(), strides, B, L, Dx, N, tc,
-            int(ctx.softplus), sdt.data_ptr(), ckpt.data_ptr(), gl.data_ptr(), gin.data_ptr(), _lib.stream_of(u)))
+            int(ctx.softplus), _lib.ptr(sdt), ckpt.data_ptr(), gl.data_ptr(), gin.data_ptr(), _lib.stream_of(u)))
         # grad of yz: its first half was overwritten by y (zero gradient there), its second half is the SiLU(conv z)
         # operand of the out_proj input. When yz came from dwconv_silu_pair (tagged there), whose backward reads
         # only the z half (column offset C), gyz passes through as is instead of a clone + zero of the x half (a
@@ -428,9 +434,9 @@ class _SelectiveScanCL(torch.autograd.Function):
             gyz = gyz.clone()
             gyz[..., :Dx] = 0
         if ctx.bc_joint:   # autograd casts the f32 sums to the input's bf16 (what .to(Bm.dtype) did)
-            return du, dd, dA, dBC, None, dD if ctx.has_D else None, db if ctx.has_b else None, gyz, None
+            return du, dd, dA, dBC, None, dD if ctx.has_D else None, db if ctx.has_b else None, gyz, None, None
         return (du, dd, dA, dBC[..., :N].to(Bm.dtype), dBC[..., N:].to(Cm.dtype), dD if ctx.has_D else None,
-                db if ctx.has_b else None, gyz, None)
+                db if ctx.has_b else None, gyz, None, None)
 
 
 def selective_scan_cl(u, delta, A, Bm, Cm, D, delta_bias, yz, delta_softplus=True, return_last_state=False):
@@ -457,7 +463,8 @@ def selective_scan_cl(u, delta, A, Bm, Cm, D, delta_bias, yz, delta_softplus=Tru
         delta = delta.contiguous()
     if yz.dtype != dt:
         raise _lib.LciError("selective_scan: yz dtype must match u")
-    out, last = _SelectiveScanCL.apply(u, delta, A, Bm, Cm, D, delta_bias, yz, bool(delta_softplus))
+    out, last = _SelectiveScanCL.apply(u, delta, A, Bm, Cm, D, delta_bias, yz, bool(delta_softplus),
+                                       bool(return_last_state))
     return (out, last) if return_last_state else out
 
 
@@ -1116,7 +1123,7 @@ class _GELU(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x):
         y = torch.empty_like(x)
-        KernelTimer.run("gelu_fwd", 0.0, x, lambda: _lib.call(
+        KernelTimer.run("gelu_fwd", 2.0 * x.element_size() * x.numel(), x, lambda: _lib.call(
             "lci_gelu_fwd", x.data_ptr(), y.data_ptr(), x.numel(), _lib.stream_of(x)))
         ctx.save_for_backward(x)
         return y
@@ -1128,7 +1135,7 @@ class _GELU(torch.autograd.Function):
         if dy.data_ptr() % 16:          # a contiguous view at a storage offset: the kernel needs 16-byte vectors
             dy = dy.clone()
         dx = torch.empty_like(x)
-        KernelTimer.run("gelu_bwd", 0.0, x, lambda: _lib.call(
+        KernelTimer.run("gelu_bwd", 3.0 * x.element_size() * x.numel(), x, lambda: _lib.call(
             "lci_gelu_bwd", x.data_ptr(), dy.data_ptr(), dx.data_ptr(), x.numel(), _lib.stream_of(x)))
         return dx
 
@@ -1833,19 +1840,15 @@ def _ln_bwd(x2, weight, mean, rstd, dy, dres, shape, want_bf16=False, dres2=None
     dy = (dy if bf else dy.float()).contiguous()
     if dy.data_ptr() % 16:   # a contiguous view at a storage offset: the kernel's vector loads need 8/16-B rows
         dy = dy.clone()
-    if dres is not None:
-        dres = dres.float().contiguous()
-        if dres.data_ptr() % 16:
-            dres = dres.clone()
-    if dres2 is not None:
-        if dres is None:
-            dres, dres2 = dres2, None
-        else:
-            dres2 = dres2.float().contiguous()
-            if dres2.data_ptr() % 16:
-                dres2 = dres2.clone()
-    if dres is not None and dres.data_ptr() % 16:
-        dres = dres.clone()
+    def dense_f32(t):   # the kernel reads residual gradients as dense, 16-B aligned f32 (rows, C) arrays
+        if t is None:
+            return None
+        t = t.float().contiguous()
+        return t.clone() if t.data_ptr() % 16 else t
+
+    dres, dres2 = dense_f32(dres), dense_f32(dres2)
+    if dres is None:   # a lone second residual gradient takes the first slot
+        dres, dres2 = dres2, None
     dx = torch.empty(rows, C, device=x2.device, dtype=torch.float32)
     dxb = torch.empty(rows, C, device=x2.device, dtype=torch.bfloat16) if want_bf16 else None
     nblk = _lib.load().lci_layernorm_bwd_blocks(rows)

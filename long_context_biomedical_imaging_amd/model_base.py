@@ -4,7 +4,7 @@ from __future__ import annotations
 import torch.nn as nn
 
 from .backbone_swin import custom_Swin
-from .backbone_vit import custom_ViT
+from .backbone_vit import ViT_with_alt_ops, custom_ViT
 from .decoders import Identity, SwinLinear, SwinUNETR, UperNet2D, UperNet3D, ViTLinear, ViTUNETR
 
 
@@ -44,15 +44,18 @@ class EncoderDecoderModel(nn.Module):
             self.decoder = UperNet3D(config, self.encoder_feature_channels, output_feature_channels)
         else:
             raise NotImplementedError(f"Decoder not implemented: {decoder_name}")
-        # the encoder's hidden states this decoder reads (besides the input and the final output); the encoder may
-        # return the others as None (ViT_with_alt_ops.keep_hidden: no sum kept alive only for the list)
+        # the encoder's hidden states this decoder reads (besides the input and the final output): the ViT encoder
+        # is asked for those only (forward(x, keep_hidden=...): no sum kept alive only for the list); the argument
+        # is passed per call, so the encoder called on its own still returns every hidden state
         taps = getattr(self.decoder, "hidden_taps", None)
-        if taps is not None and hasattr(self.encoder, "keep_hidden"):
-            self.encoder.keep_hidden = frozenset(taps)
+        self._keep_hidden = frozenset(taps) if taps is not None and isinstance(self.encoder, ViT_with_alt_ops) \
+            else None
 
     @property
     def device(self):
         return next(self.parameters()).device
 
     def forward(self, x):
+        if self._keep_hidden is not None:
+            return self.decoder(self.encoder(x, keep_hidden=self._keep_hidden))
         return self.decoder(self.encoder(x))

@@ -172,3 +172,36 @@ def test_fused_mamba_projection_matches_linear_layers(d_model, B, L, monkeypatch
                       **{n: p.grad.detach().clone() for n, p in m.named_parameters()}}
     for k, ref in res[False].items():
         assert rel_err(res[True][k], ref) < 1e-2, (k, rel_err(res[True][k], ref))
+
+
+@pytest.mark.parametrize("nseq,L,d,dtype", [(300, 64, 48, torch.bfloat16), (40, 343, 96, torch.float32),
+                                           (8, 512, 384, torch.bfloat16), (3, 37, 200, torch.float32)])
+def test_selective_scan_one_chunk_path_bitwise(nseq, L, d, dtype):
+    """Window sequences (one chunk, ABI 32): without a requested final state the forward runs only the output pass
+    and the backward skips the adjoint aggregate / carry, and dB / dC are stored rather than accumulated where one
+    workgroup holds every channel (Dx <= 256). Nothing is carried into a single chunk, so y and all seven
+    gradients must equal the full three-pass path (forced by return_last_state=True) bit for bit."""
+    from long_context_biomedical_imaging_amd import kernels
+    torch.manual_seed(nseq + L)
+    n = 8
+    dev = "cuda"
+    u = torch.randn(nseq, L, d, device=dev).to(dtype)
+    delta = (torch.randn(nseq, L, d, device=dev) * 0.5 - 1.0).to(dtype)
+    A = -torch.exp(torch.randn(d, n, device=dev) * 0.3)
+    bc = torch.randn(nseq, L, 2 * n, device=dev).to(dtype)
+    D, db = torch.randn(d, device=dev), torch.randn(d, device=dev) * 0.1
+    cot = torch.randn(nseq, L, d, device=dev)
+    res = []
+    for want_last in (False, True):
+        leaves = [t.detach().clone().requires_grad_(True) for t in (u, delta, A, bc, D, db)]
+        uc, dc, Ac, bcc, Dc, dbc = leaves
+        yz = torch.zeros(nseq, L, 2 * d, device=dev, dtype=dtype)
+        out = kernels.selective_scan_cl(uc, dc, Ac, bcc[..., :n], bcc[..., n:], Dc, dbc, yz,
+                                        return_last_state=want_last)
+        if want_last:
+            out, last = out
+            assert last.shape == (nseq, d, n) and torch.isfinite(last).all()
+        (out[..., :d].float() * cot).sum().backward()
+        res.append([out[..., :d].detach()] + [t.grad for t in leaves])
+    for a, b in zip(*res):
+        assert torch.equal(a, b)

@@ -7,10 +7,13 @@ another revision's (or compiled with extra flags), linked into build_variants/li
     python tools/build_variant.py new                              # the tree's library as is
 
 The variant keeps the tree's ABI version (lci_abi_version) so _lib.load() accepts it under LCI_LIB_PATH; it is never
-the library the tests or bench.py load by default.
+the library the tests or bench.py load by default. With --rev, the revision's include/lci.h must declare the same
+LCI_ABI_VERSION as the tree's: objects built from sources of another ABI (other argument lists behind the same
+symbols) are refused instead of being linked under the tree's version stamp.
 """
 import argparse
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -28,6 +31,17 @@ def main():
     ap.add_argument("--rev", default=None, help="git revision to take those sources from (default: the tree)")
     ap.add_argument("--define", action="append", default=[], help="extra -D for those sources")
     a = ap.parse_intermixed_args()
+    if a.rev and a.sources:
+        def abi(text):
+            m = re.search(r"^#define LCI_ABI_VERSION (\d+)", text, re.M)
+            return int(m.group(1)) if m else None
+        rev_h = subprocess.run(["git", "-C", ROOT, "show", f"{a.rev}:include/lci.h"], check=True,
+                               capture_output=True, text=True).stdout
+        with open(b.HEADER) as fh:
+            tree = abi(fh.read())
+        if abi(rev_h) != tree:
+            sys.exit(f"build_variant: {a.rev} declares LCI_ABI_VERSION {abi(rev_h)}, the tree {tree}: refusing to link "
+                     "its objects under the tree's ABI stamp")
     b.build(verbose=False)
     out_dir = os.path.join(ROOT, "build_variants")
     os.makedirs(out_dir, exist_ok=True)
