@@ -616,6 +616,10 @@ constexpr unsigned char DQ_SCHED[24][4] = {
     {0x66, 0x67, 0xa2, 0xa3}};
 
 
+#ifndef LCI_DQ_EARLY
+#define LCI_DQ_EARLY 1
+#endif
+constexpr bool DQ_EARLY = LCI_DQ_EARLY != 0;
 __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs a) {
   constexpr int TILE_B = KT * DH * 2;               // bytes of a K or V tile (128-B rows)
   constexpr int SLOT_B = 2 * TILE_B;                // K | V
@@ -629,6 +633,7 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
   const int h = lane >> 5, r32 = lane & 31;
   const int qw0 = blockIdx.x * (HS_NW * 64) + wave * 64;
   const int nkt = (L + KT - 1) / KT;
+  const int nkt4 = (nkt + 3) & ~3;
 
   // Q~ / dO as B operands: lane holds X[qw0 + 32qb + r32][16ks + 8h + j] (Q prescaled into the exp2 domain);
   // -lse2 / -delta of the lane's query splatted over a chain's 16 accumulator registers
@@ -763,8 +768,10 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
     }
   };
 
-  // One 32-key half (rows r0i of slot soff); the next half's rows are rows nr0i of slot nsoff. LDS reads: V rows at
-  // gaps 0-3, transposed K at 12-19, the next half's K rows at 20-23.
+  // One 32-key half (rows r0i of slot soff); the next half's rows are rows nr0i of slot nsoff. LDS reads: transposed
+  // K at 12-19, the next half's K rows at 20-23; DQ_EARLY (round 6): the next half's V rows there too, 8 gaps before
+  // the dP^T chain of block 0 instead of 4 (reloaded 1-4 gaps after their last read by block 1's chain: no extra
+  // registers); else V rows at gaps 0-3.
   auto half = [&](int soff, int r0i, int nsoff, int nr0i, auto hook) __attribute__((always_inline)) {
 #pragma unroll
     for (int g = 0; g < 24; ++g) {
@@ -774,11 +781,19 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
       if (g == 9 || g == 21) asm volatile("s_nop 5" ::: "memory");
 #pragma unroll
       for (int o = 0; o < 4; ++o) valu_op(DQ_SCHED[g][o], -1);
-      if (g < 4) vr[g] = row(soff + TILE_B, r0i, g);
-      else if (g >= 12 && g < 20) {
+      if (g >= 12 && g < 20) {
         const int f = (g - 12) >> 1, part = (g - 12) & 1;
         ktr[0][f & 1][f >> 1][part] = trh(soff, r0i, f, part);
-      } else if (g >= 20) kr[g - 20] = row(nsoff, nr0i, g - 20);
+      }
+      if constexpr (DQ_EARLY) {
+        if (g >= 20) {
+          kr[g - 20] = row(nsoff, nr0i, g - 20);
+          vr[g - 20] = row(nsoff + TILE_B, nr0i, g - 20);
+        }
+      } else {
+        if (g < 4) vr[g] = row(soff + TILE_B, r0i, g);
+        else if (g >= 20) kr[g - 20] = row(nsoff, nr0i, g - 20);
+      }
       hook(g);
     }
   };
@@ -799,7 +814,10 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
   hs_vmcnt<0>();
   __builtin_amdgcn_s_barrier();
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) kr[ks] = row(0, 0, ks);
+  for (int ks = 0; ks < 4; ++ks) {
+    kr[ks] = row(0, 0, ks);
+    if (DQ_EARLY) vr[ks] = row(TILE_B, 0, ks);
+  }
   __builtin_amdgcn_s_waitcnt(LGKM0_WAIT);   // (see the dK/dV kernel's loop header)
 
   // SL >= 0: tile t sits in ring slot SL (compile-time: DS immediates); SL < 0: slot t & 3 at run time
@@ -809,7 +827,7 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
     const int nsoff = sl >= 0 ? ((sl + 1) & (NSLOT - 1)) * SLOT_B : ((t + 1) & (NSLOT - 1)) * SLOT_B;
     // tile t+1 is published at gap 6 of half 1 (its first reader: the K rows at gaps 20-23)
     auto stage = [&](int g) __attribute__((always_inline)) {
-      if (t + 1 < nkt && g == 6) __builtin_amdgcn_s_barrier();
+      if (t + 1 < nkt4 && g == 6) __builtin_amdgcn_s_barrier();
     };
     auto stage0 = [&](int g) __attribute__((always_inline)) {
       if (g == 1) hs_vmcnt<0>();   // tile t+1's pieces (loaded a tile ago)
@@ -829,15 +847,14 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
     half(soff, 0, soff, 1, stage0);
     half(soff, 1, nsoff, 0, stage);
   };
-  {
-    int t = 0;
-    for (; t + 4 <= nkt; t += 4) {   // t & 3 == 0 here
-      tile(std::integral_constant<int, 0>{}, t);
-      tile(std::integral_constant<int, 1>{}, t + 1);
-      tile(std::integral_constant<int, 2>{}, t + 2);
-      tile(std::integral_constant<int, 3>{}, t + 3);
-    }
-    for (; t < nkt; ++t) tile(std::integral_constant<int, -1>{}, t);
+  // the key tiles padded to a multiple of 4 (ring slots as DS immediates, no run-time-slot remainder loop, whose
+  // second copy of the loop state spilled): tiles past L hold zero K / V rows (the staging loads' buffer range), so
+  // their dS meets K^T = 0 and adds nothing to dQ^T
+  for (int t = 0; t < nkt4; t += 4) {   // t & 3 == 0 here
+    tile(std::integral_constant<int, 0>{}, t);
+    tile(std::integral_constant<int, 1>{}, t + 1);
+    tile(std::integral_constant<int, 2>{}, t + 2);
+    tile(std::integral_constant<int, 3>{}, t + 3);
   }
   hs_vmcnt<0>();   // the last tiles' staging loads (past the end: zeros) retire
   // query block 1 of the last half: its remaining VALU (wrapped into gaps 0-5) and its dQ^T
@@ -853,9 +870,14 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
   asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
 
   const float sc = a.scale;
+  // the lane's query re-derived here, not kept from the prologue: hoisted out of the loop, the epilogue's row
+  // pointers were 8 VGPRs the full register file (DQ_EARLY) spills
+  unsigned lane_e;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane_e));
+  const int r32e = (int)lane_e & 31;
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
-    const int q = qw0 + 32 * qb + r32;
+    const int q = qw0 + 32 * qb + r32e;
     if (q < L) {
       bf16* dqp = a.out + b * a.bs_out + (long long)q * a.rs_out + hh * a.hs;
 #pragma unroll
@@ -874,57 +896,78 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dq_hs_kernel(AttnArgs 
 // ------------------------------------------------ forward: one wave per SIMD, placed MFMA / VALU / LDS stream
 // The placed-stream structure of the backward kernels for O = softmax(Q K^T) V (backbone_vit.py:191-201): a workgroup =
 // 4 waves x 64 queries (two query blocks of 32 on the MFMA lane), Q~ = c q fragments and the O^T accumulators in
-// AGPRs, K | V tiles of 64 keys by LDS-DMA into a 4-slot ring two tiles ahead. Per 32-key half and wave: 16 MFMAs
-//   gaps 0-3: S^T = K Q~^T chain of block 0 | 4-7: O^T += V^T P^T of block 1 (previous half) |
-//   8-11: S^T chain of block 1 | 12-15: O^T += V^T P^T of block 0,
-// against 32 exp2, 32 row-sum adds and 16 bf16 packs, placed by FW_SCHED (tools/gen_fwd_sched.py: every gap 2 exp2 +
-// 2 adds + 1 pack beside its MFMA). LDS reads: this half's transposed V fragments at gaps 0-7 (set p & 1: block 1 reads
-// the previous half's set at gaps 4-7), the next half's K rows at gaps 12-15.
+// AGPRs, K | V tiles of 64 keys in a 4-slot LDS ring (tile t+1 stored from staging registers during tile t).
 // Max-free softmax with one reference per query: m = the exact row max over the first key tile, which every chain
 // starts from (-m as the initial accumulator), valid while ||q~|| max||k|| - m <= 64 over the whole key range (then
 // p <= 2^64, exact in f32 sums and bf16 P: the attn_fwd2_kernel criterion, checked once per workgroup from the
 // per-tile key norms); a workgroup outside it takes the exact online-softmax loop below (rescaled per 32 keys).
-// gap  0: A1.4 C1.2 A1.5 E1.6 E1.7
-// gap  1: A1.6 C1.3 A1.7 E1.8 E1.9
-// gap  2: A1.8 C1.4 A1.9 E1.10 E1.11
-// gap  3: A1.10 C1.5 A1.11 E1.12 E1.13
-// gap  4: A1.12 C1.6 A1.13 E1.14 E1.15
-// gap  5: A1.14 C1.7 A1.15 E0.0 E0.1
-// gap  6: A0.0 C0.0 A0.1 E0.2 E0.3
-// gap  7: A0.2 C0.1 A0.3 E0.4 E0.5
-// gap  8: A0.4 C0.2 A0.5 E0.6 E0.7
-// gap  9: A0.6 C0.3 A0.7 E0.8 E0.9
-// gap 10: A0.8 C0.4 A0.9 E0.10 E0.11
-// gap 11: A0.10 C0.5 A0.11 E0.12 E0.13
-// gap 12: A0.12 C0.6 A0.13 E0.14 E0.15
-// gap 13: E1.0 E1.1 C0.7 A0.14 A0.15
-// gap 14: C1.0 A1.0 A1.1 E1.2 E1.3
-// gap 15: A1.2 C1.1 A1.3 E1.4 E1.5
-constexpr unsigned char FW_SCHED[16][5] = {
-    {0x64, 0xa2, 0x65, 0x26, 0x27},
-    {0x66, 0xa3, 0x67, 0x28, 0x29},
-    {0x68, 0xa4, 0x69, 0x2a, 0x2b},
-    {0x6a, 0xa5, 0x6b, 0x2c, 0x2d},
-    {0x6c, 0xa6, 0x6d, 0x2e, 0x2f},
-    {0x6e, 0xa7, 0x6f, 0x00, 0x01},
-    {0x40, 0x80, 0x41, 0x02, 0x03},
-    {0x42, 0x81, 0x43, 0x04, 0x05},
-    {0x44, 0x82, 0x45, 0x06, 0x07},
-    {0x46, 0x83, 0x47, 0x08, 0x09},
-    {0x48, 0x84, 0x49, 0x0a, 0x0b},
-    {0x4a, 0x85, 0x4b, 0x0c, 0x0d},
-    {0x4c, 0x86, 0x4d, 0x0e, 0x0f},
-    {0x20, 0x21, 0x87, 0x4e, 0x4f},
-    {0xa0, 0x60, 0x61, 0x22, 0x23},
-    {0x62, 0xa1, 0x63, 0x24, 0x25}};
 
-// initial S^T of query block 1 before the first half: the exps of block 1 that FW_SCHED wraps into the next half
-// (E1.i in gaps before START_E = 13) see NEG_BIG (exp2 -> 0); the elements exponentiated in the previous half's gaps
-// 13-15 are already "exponentiated": 0. Either way the first half adds and packs zeros for the missing half -1.
+// Row sums on the matrix pipe (round 6): the 32 v_add_f32 per half of the round-4 stream (a quarter of its VALU issue)
+// are replaced by 4 v_mfma_f32_16x16x32_bf16 that sum the bf16 P^T packs the PV MFMAs read anyway: with the pack as
+// the B operand (lane l = 16 g + n holds 8 keys of query 16 (g & 1) + n) and A = a 0/1 selector (row 0 sums the lane
+// groups g = 0, 2: query n; row 1 the groups 1, 3: query 16 + n), D rows 0 / 1 accumulate l of the block's 32 queries.
+// The denominator is then the sum of the same bf16-rounded P the numerator uses. The MFMA's accumulation is not an
+// f32 RNE sum (a running 65536-key row sum on it came out up to 1.3 % low against an exact sum: bits of the new
+// products below the accumulator's ulp are dropped, a bias in one direction when every term is positive), so each
+// half's two row-sum MFMAs start from a zero accumulator and their result is added into an f32 running sum by a
+// v_add_f32 per block and row half (A ops: 4 per half instead of 32). Per half (20 gaps):
+//   0-3 S^T chain of block 0 | 4, 5, 7, 8 O^T += V^T P^T of block 1 (previous half), 6 / 9 its row sums (k-step 0 / 1)
+//   10-13 S^T chain of block 1 | 14, 15, 17, 18 O^T of block 0, 16 / 19 its row sums,
+// against 32 exp2 and 16 packs placed by FW_SCHED_R (tools/gen_fwd_sched.py --rsum: <= 2 exp2 + 1 pack beside a
+// 32x32x16 MFMA, one op beside a 16x16x32; E starts two gaps after its chain, packs before the MFMAs that read them).
+constexpr int FW_NG = 20;          // gaps per half
+constexpr int FW_START_E1 = 15;    // first gap of block 1's exps
+// gap  0 S0: E1.6 E1.7
+// gap  1 S0: E1.8 E1.9 C1.3
+// gap  2 S0: E1.10 E1.11 C1.4 A0.0
+// gap  3 S0: E1.12 E1.13 C1.5 A0.1
+// gap  4 P1: E1.14 E1.15 C1.6
+// gap  5 P1: C1.7 E0.0 E0.1
+// gap  6 R1: C0.0
+// gap  7 P1: E0.2 E0.3
+// gap  8 P1: E0.4 E0.5 C0.1
+// gap  9 R1: C0.2
+// gap 10 S1: E0.6 E0.7
+// gap 11 S1: E0.8 E0.9 C0.3
+// gap 12 S1: E0.10 E0.11 C0.4 A1.0
+// gap 13 S1: E0.12 E0.13 C0.5 A1.1
+// gap 14 P0: E0.14 E0.15 C0.6
+// gap 15 P0: C0.7 E1.0 E1.1
+// gap 16 R0: C1.0
+// gap 17 P0: E1.2 E1.3
+// gap 18 P0: E1.4 E1.5 C1.1
+// gap 19 R0: C1.2
+constexpr unsigned char FW_SCHED_R[20][4] = {
+    {0x26, 0x27, 0xff, 0xff},
+    {0x28, 0x29, 0xa3, 0xff},
+    {0x2a, 0x2b, 0xa4, 0x40},
+    {0x2c, 0x2d, 0xa5, 0x41},
+    {0x2e, 0x2f, 0xa6, 0xff},
+    {0xa7, 0x00, 0x01, 0xff},
+    {0x80, 0xff, 0xff, 0xff},
+    {0x02, 0x03, 0xff, 0xff},
+    {0x04, 0x05, 0x81, 0xff},
+    {0x82, 0xff, 0xff, 0xff},
+    {0x06, 0x07, 0xff, 0xff},
+    {0x08, 0x09, 0x83, 0xff},
+    {0x0a, 0x0b, 0x84, 0x60},
+    {0x0c, 0x0d, 0x85, 0x61},
+    {0x0e, 0x0f, 0x86, 0xff},
+    {0x87, 0x20, 0x21, 0xff},
+    {0xa0, 0xff, 0xff, 0xff},
+    {0x22, 0x23, 0xff, 0xff},
+    {0x24, 0x25, 0xa1, 0xff},
+    {0xa2, 0xff, 0xff, 0xff}};
+constexpr int FW_CAP = 4;
+__host__ __device__ constexpr unsigned char fw_sched(int g, int o) { return FW_SCHED_R[g][o]; }
+
+// initial S^T of query block 1 before the first half: the exps of block 1 that the schedule wraps into the next half
+// (E1.i in gaps before FW_START_E1) see NEG_BIG (exp2 -> 0); the elements exponentiated in the previous half's last
+// gaps are already "exponentiated": 0. Either way the first half sums and packs zeros for the missing half -1.
 __host__ __device__ constexpr bool fw_wrapped_exp(int i) {
-  for (int g = 0; g < 13; ++g)
-    for (int o = 0; o < 5; ++o)
-      if (FW_SCHED[g][o] == (0x20 | i)) return true;
+  for (int g = 0; g < FW_START_E1; ++g)
+    for (int o = 0; o < FW_CAP; ++o)
+      if (fw_sched(g, o) == (0x20 | i)) return true;
   return false;
 }
 
@@ -1132,7 +1175,16 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
   u32x4 pp[2][2];     // [query block][k-step] bf16 P^T packs
   bf16x4 vt[2][2][2][2];   // [set][d block][k-step][half of the fragment] transposed V (keys as the k index)
   bf16x8 kr[4];       // K row fragments (A operands of the chains)
-  float lp[2][4];     // row-sum partials (VALU adds)
+  float lp[2][2];     // [query block][row half] running f32 row sums (lanes 0-15: queries 16 s + lane)
+  f32x4 rs[2];        // [query block] the half's row-sum partial on the matrix pipe: D rows 0 / 1 in lanes 0-15
+  bf16x8 sel;         // 16x16x32 A operand: row 0 selects lane groups 0 / 2, row 1 groups 1 / 3 (all 8 k per lane)
+  {
+    const int m16 = lane & 15, g16 = lane >> 4;
+    const float one = (m16 == 0 && (g16 & 1) == 0) || (m16 == 1 && (g16 & 1) == 1) ? 1.f : 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sel[j] = to_bf16(one);
+    HS_TO_AGPR(sel);
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -1155,8 +1207,9 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
         HS_OPAQUE(vt[1][i][j][k]);
       }
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) lp[i][j] = 0.f;
+    lp[i][0] = lp[i][1] = 0.f;
+    rs[i] = f32x4{};
+    HS_OPAQUE(rs[i]);
   }
 
   auto valu_op = [&](unsigned char cd, int only_qb) __attribute__((always_inline)) {
@@ -1164,44 +1217,69 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
     const int kind = cd >> 6, qb = (cd >> 5) & 1, i = cd & 31;
     if (only_qb >= 0 && qb != only_qb) return;
     if (kind == 0) HS_EXP(S[qb][i]);
-    else if (kind == 1) asm volatile("v_add_f32 %0, %0, %1" : "+v"(lp[qb][i & 3]) : "v"(S[qb][i]));
-    else HS_CVT(pp[qb][i >> 2][i & 3], S[qb][2 * i], S[qb][2 * i + 1]);
+    else if (kind == 1) {
+      asm volatile("v_add_f32 %0, %0, %1" : "+v"(lp[qb][i]) : "v"(rs[qb][i]));
+      // rows 2 / 3 of the accumulator are never read, but the next MFMA writes all four registers: keep them
+      // allocated so that nothing else lives in them inside its hazard window
+      if (i == 1) HS_KEEP(rs[qb]);
+    } else HS_CVT(pp[qb][i >> 2][i & 3], S[qb][2 * i], S[qb][2 * i + 1]);
   };
   auto pv_mfma = [&](int k, int qb, int st) __attribute__((always_inline)) {   // k: (d block k & 1, k-step k >> 1)
     const int db = k & 1, s2 = k >> 1;
     HS_MFMA_G(o[qb][db], cat44(vt[st][db][s2][0], vt[st][db][s2][1]), __builtin_bit_cast(bf16x8, pp[qb][s2]));
   };
+  // the half's row-sum partial of block qb: the column sums of its two P^T packs (k-step 0 starts from zero)
+  auto rs_mfma = [&](int qb, int s2) __attribute__((always_inline)) {
+    if (s2 == 0)
+      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(rs[qb]) : "a"(sel), "v"(pp[qb][0]));
+    else
+      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(rs[qb]) : "a"(sel), "v"(pp[qb][1]));
+  };
   auto mfma_gap = [&](int g, int C, const f32x16& i0, const f32x16& i1) __attribute__((always_inline)) {
+    // 0-3 S0 | 4 5 (6) 7 8 (9) PV / row sums of block 1 | 10-13 S1 | 14 15 (16) 17 18 (19) PV / row sums of block 0
     if (g < 4) {
       if (g == 0) HS_MFMA_C0(S[0], kr[0], qf[0][0], i0); else HS_MFMA_C(S[0], kr[g], qf[0][g]);
-    } else if (g < 8) {
-      pv_mfma(g - 4, 1, C ^ 1);
-    } else if (g < 12) {
-      if (g == 8) HS_MFMA_C0(S[1], kr[0], qf[1][0], i1); else HS_MFMA_C(S[1], kr[g - 8], qf[1][g - 8]);
+    } else if (g < 10) {
+      if (g == 6 || g == 9) rs_mfma(1, g == 9);
+      else pv_mfma(g < 6 ? g - 4 : g - 5, 1, C ^ 1);
+    } else if (g < 14) {
+      if (g == 10) HS_MFMA_C0(S[1], kr[0], qf[1][0], i1); else HS_MFMA_C(S[1], kr[g - 10], qf[1][g - 10]);
     } else {
-      pv_mfma(g - 12, 0, C);
+      if (g == 16 || g == 19) rs_mfma(0, g == 19);
+      else pv_mfma(g < 16 ? g - 14 : g - 15, 0, C);
     }
   };
-  // one 32-key half (rows 32 r0i of the slot at byte offset soff, V^T set SET); gaps 12-15 read the next half's K rows
-  // (rows 32 nr0i of the slot at nsoff), 4 gaps before their use (two K-row sets read 5-8 gaps ahead measured slower:
-  // 13.74 vs 13.27 ms)
-  auto half = [&](auto SET, int soff, int r0i, int nsoff, int nr0i, const f32x16& i0, const f32x16& i1, auto hook)
-      __attribute__((always_inline)) {
+
+  // one 32-key half (rows 32 r0i of the slot at byte offset soff, V^T set SET): the transposed V fragments at gaps 0-7,
+  // the next half's K rows (rows 32 nr0i of the slot at nsoff) at gaps 13-16, right behind the gap's MFMA
+  auto half = [&](auto SET, auto FIXED, int soff, int r0i, int nsoff, int nr0i, const f32x16& i0, const f32x16& i1,
+                  auto hook) __attribute__((always_inline)) {
     constexpr int C = decltype(SET)::value;
-    constexpr int NG = 16;
+    constexpr bool FIXED_SLOT = decltype(FIXED)::value;
+    constexpr int NG = FW_NG;
+    constexpr int KR0 = 13;   // first gap of the next half's K-row reads (each fragment reloaded >= 3 gaps after the S1
+                              // chain's last read of it)
+    auto lds_reads = [&](int g) __attribute__((always_inline)) {
+      if (g < 8) {
+        const int f = g >> 1, part = g & 1;   // fragment f = (d block f & 1, k-step f >> 1)
+        vt[C][f & 1][f >> 1][part] = trh(soff, r0i, f, part);
+      } else if (g >= KR0 && g < KR0 + 4) {   // the next half's K rows
+        kr[g - KR0] = row(nsoff, nr0i, g - KR0);
+      }
+    };
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       mfma_gap(g, C, i0, i1);
       if (g == 2) HS_KEEP(i0);    // the chain-start MFMAs read their initial accumulators as SrcC after issue
-      if (g == 10) HS_KEEP(i1);
+      if (g == 12) HS_KEEP(i1);
+      // the gap's LDS read right behind its MFMA (one more wait state between a chain's last MFMA and the first exp
+      // that reads it, and between an exp and a pack reading it across the gap boundary)
+      lds_reads(g);
+      // run-time-slot tiles (remainder, ragged last tile): the compiler may sink their LDS reads, so the wait states
+      // between a chain's last MFMA and its first exp are padded explicitly
+      if (!FIXED_SLOT && (g == 5 || g == 15)) asm volatile("s_nop 1" ::: "memory");
 #pragma unroll
-      for (int op = 0; op < 5; ++op) valu_op(FW_SCHED[g][op], -1);
-      if (g < 8) {
-        const int f = g >> 1, part = g & 1;   // fragment f = (d block f & 1, k-step f >> 1)
-        vt[C][f & 1][f >> 1][part] = trh(soff, r0i, f, part);
-      } else if (g >= NG - 4) {   // the next half's K rows (the block-1 chain reads this half's until gap NG - 7)
-        kr[g - (NG - 4)] = row(nsoff, nr0i, g - (NG - 4));
-      }
+      for (int op = 0; op < FW_CAP; ++op) valu_op(fw_sched(g, op), -1);
       hook(g);
     }
   };
@@ -1235,8 +1313,9 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
     const int nsoff = sl >= 0 ? ((sl + 1) & (NSLOT - 1)) * SLOT_B : ((t + 1) & (NSLOT - 1)) * SLOT_B;
     // tile t+1 is published at gap 6 of half 1 (first reader: the K rows at gaps 12-15)
     auto stage = [&](int g) __attribute__((always_inline)) {
-      if (t + 1 < nkt && g == 6) __builtin_amdgcn_s_barrier();
+      if (t + 1 < nkt && g == 7) __builtin_amdgcn_s_barrier();
     };
+    constexpr int LD0 = 11;   // tile t+2's loads at gaps 11, 13, 15, 17 (32x32x16 gaps)
     auto rstg = [&](int g) __attribute__((always_inline)) {
       if (g == 1) hs_vmcnt<0>();   // tile t+1's pieces (loaded a tile ago)
       if (g < 8 && (g & 1)) {
@@ -1248,12 +1327,12 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
           case 5: hs_st16<S1 + TILE_B>(base, stg[2]); break;
           default: hs_st16<S1 + TILE_B + 1024>(base, stg[3]); break;
         }
-      } else if (g >= 9 && (g & 1)) {
-        ld_piece(t + 2, (g - 9) >> 1);
+      } else if (g >= LD0 && g < LD0 + 8 && ((g - LD0) & 1) == 0) {
+        ld_piece(t + 2, (g - LD0) >> 1);
       }
     };
-    half(std::integral_constant<int, 0>{}, soff, 0, soff, 1, a0, a1, rstg);
-    half(std::integral_constant<int, 1>{}, soff, 1, nsoff, 0, b0, b1, stage);
+    half(std::integral_constant<int, 0>{}, std::bool_constant<(sl >= 0)>{}, soff, 0, soff, 1, a0, a1, rstg);
+    half(std::integral_constant<int, 1>{}, std::bool_constant<(sl >= 0)>{}, soff, 1, nsoff, 0, b0, b1, stage);
   };
   const bool ragged = (L & (KT - 1)) != 0;
   const int nfast = ragged ? nkt - 1 : nkt;
@@ -1286,22 +1365,28 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
     tile(ICR{}, tl, M[0][0], M[0][1], M[1][0], M[1][1]);
   }
   hs_vmcnt<0>();   // the last tiles' staging loads (past the end: zeros) retire before the exit
-  // query block 1 of the last half: its wrapped VALU and its PV MFMAs
+  // query block 1 of the last half: its wrapped VALU and its PV (and row-sum) MFMAs
 #pragma unroll
-  for (int g = 0; g < 8; ++g) {
+  for (int g = 0; g < 10; ++g) {
 #pragma unroll
-    for (int op = 0; op < 5; ++op) valu_op(FW_SCHED[g][op], 1);
+    for (int op = 0; op < FW_CAP; ++op) valu_op(fw_sched(g, op), 1);
     if (g >= 4) {
       asm volatile("s_nop 1" ::: "memory");
-      pv_mfma(g - 4, 1, 1);   // the last half is a half 1
+      if (g == 6 || g == 9) rs_mfma(1, g == 9);
+      else pv_mfma(g < 6 ? g - 4 : g - 5, 1, 1);   // the last half is a half 1
     }
   }
   asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+  HS_OPAQUE(rs[0]);   // read only after the last MFMAs completed
+  HS_OPAQUE(rs[1]);
 
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
     const int q = qw0 + 32 * qb + r32;
-    const float lt = wave_sum_xor32((lp[qb][0] + lp[qb][1]) + (lp[qb][2] + lp[qb][3]));
+    // l of query 16 s + n sits in lane n, row s of the block's 16x16 accumulator (+ the last half's partials)
+    const float s0 = lp[qb][0] + rs[qb][0], s1 = lp[qb][1] + rs[qb][1];
+    const float l0 = __shfl(s0, r32 & 15), l1 = __shfl(s1, r32 & 15);
+    const float lt = r32 < 16 ? l0 : l1;
     if (q < L) {
       const float inv = 1.f / lt;
       bf16* op = a.out + b * a.bs_out + (long long)q * a.rs_out + hh * a.hs;

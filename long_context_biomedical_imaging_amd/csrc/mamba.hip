@@ -18,6 +18,9 @@
 
 namespace lci {
 
+#ifndef LCI_SCAN_PROBE
+#define LCI_SCAN_PROBE 0   // 1: the transcendental-floor timing probe of the forward passes (build_variant only)
+#endif
 constexpr int SCAN_N = 8;     // d_state (the reference always uses 8: backbone_vit.py:184, backbone_swin.py:329)
 constexpr int CKPT = 8;       // backward checkpoint spacing (steps); sub-block states live in registers
 constexpr float LOG2E = 1.4426950408889634f;
@@ -186,6 +189,21 @@ __device__ __forceinline__ void scan_fwd_step(const ScanArgs& a, float (&x)[SCAN
       *(f32x4*)(cp + 4) = f32x4{x[4], x[5], x[6], x[7]};
     }
   }
+#if LCI_SCAN_PROBE
+  // transcendental-floor probe (timing only, wrong results): the same loads, softplus and 8 decay exps per
+  // channel-step; the state update is one add, the B / C rows, the dtu B product and the C x dot are dropped
+  {
+    const float dt = softplus(drv + bias);
+    float e[SCAN_N];
+    decay8(dt, A2, e);
+#pragma unroll
+    for (int n = 0; n < SCAN_N; ++n) x[n] += e[n];
+    (void)row; (void)uv; (void)Dd;
+    if (MODE == 1) ycol.st(t, x[0]);
+    else sumdt += dt;
+    return;
+  }
+#endif
   float Bv[SCAN_N];
   lds_row8(row, Bv);
   const float dt = softplus(drv + bias);
@@ -1033,8 +1051,9 @@ static int scan_bwd_waves(int Tc, int Dx) {
 // all Dx channels), so dBC needs no zero fill; 0: it accumulates into dBC with atomics.
 extern "C" int lci_selective_scan_bwd_plain_dbc(int L, int Dx, int chunk) {
   (void)L;
+  static const bool off = getenv("LCI_SCAN_PLAIN_DBC") && atoi(getenv("LCI_SCAN_PLAIN_DBC")) == 0;   // A/B hook
   const int nwv = scan_bwd_waves(chunk, Dx);
-  return (Dx + nwv * 64 - 1) / (nwv * 64) == 1;
+  return !off && (Dx + nwv * 64 - 1) / (nwv * 64) == 1;
 }
 
 // dA (Dx*N), dD (Dx), ddelta_bias (Dx) are accumulated (caller zeroes them); dBC (B, L, 2N) too, except where
@@ -1073,7 +1092,7 @@ extern "C" int lci_selective_scan_bwd(int dtype, const void* u, const void* delt
   // 0.60 ms at 4 waves vs 0.80 at 1). LCI_SCAN_BWD_WAVES overrides.
   const int nwv = scan_bwd_waves(a.Tc, Dx);
   dim3 gridc(a.nch, (Dx + nwv * 64 - 1) / (nwv * 64), B);
-  a.dbc_plain = gridc.y == 1;
+  a.dbc_plain = lci_selective_scan_bwd_plain_dbc(L, Dx, a.Tc);
   // parameter gradients: the B * nch float atomics per address from the waves' ends serialise in L2 (the dwconv
   // backward's lesson): short chunks write partials and sum them in one more launch (L=65536: 0.60 -> 0.42 ms).
   // Long chunks keep the atomics: there the partials build of the kernel measured slower (8.6 vs 6.9 ms at L=2^21,

@@ -368,7 +368,7 @@ class _SelectiveScanCL(torch.autograd.Function):
         f32 = dict(device=u.device, dtype=torch.float32)
         # one chunk (the Swin recipes' window sequences, L <= 512): nothing is carried into it, so without a
         # requested final state the end-state pass and the carry are skipped (lci.h ABI 32)
-        one = nch == 1 and not want_last
+        one = nch == 1 and not want_last and os.environ.get("LCI_SCAN_ONE", "1") != "0"   # (=0: A/B hook)
         xend = None if one else torch.empty(B, nch, Dx, N, **f32)
         xinit = None if one else torch.empty(B, nch, Dx, N, **f32)
         sdt = None if one else torch.empty(B, nch, Dx, **f32)

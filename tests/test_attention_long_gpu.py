@@ -10,6 +10,8 @@ Tolerances as tests/test_attention_gpu.py (bf16 I/O, f32 softmax): O rel-L2 <= 1
 1e-2 and the reference's own autocast deviation on the same rows, plus <= 3e-3 from an emulation of the kernel's
 own roundings); grads rel-L2 <= 2e-2, max |err| <= 3e-2 max|ref| + 2e-3.
 """
+import math
+
 import pytest
 import torch
 
@@ -103,7 +105,8 @@ def test_attention_forward_L65536_rows_with_late_outlier_keys():
     qe = (q[:, :, rows] * (SCALE * LOG2E)).to(torch.bfloat16).double()
     se = torch.einsum("bhid,bhjd->bhij", qe, kd)
     pe = torch.exp2(se - se.max(-1, keepdim=True).values)
-    emu = (torch.einsum("bhij,bhjd->bhid", pe.to(torch.bfloat16).double(), vd) / pe.sum(-1, keepdim=True))
+    pb = pe.to(torch.bfloat16).double()   # the kernel's denominator is the sum of the same bf16 P (matrix pipe)
+    emu = (torch.einsum("bhij,bhjd->bhid", pb, vd) / pb.sum(-1, keepdim=True))
     emu = emu.permute(0, 2, 1, 3).reshape(B, len(rows), C)
     # the reference's own autocast GPU path on the same rows (backbone_vit.py:191-201: bf16 einsum output, bf16
     # `* scale`, f32 softmax rounded to bf16 before the AV einsum): with 65536 keys and diffuse attention, rounding
@@ -115,7 +118,14 @@ def test_attention_forward_L65536_rows_with_late_outlier_keys():
     _check(got, ref, "O rows L65536", rel=max(1e-2, rel_err(ac, ref)))
     assert rel_err(got, emu) <= 3e-3, f"kernel vs its own rounding emulation: {rel_err(got, emu):.3e}"
     lse_got = lse2[:, :, rows].double() / LOG2E
-    assert (lse_got - lse).abs().max().item() < 1e-3 * max(1.0, lse.abs().max().item())
+    # the lse the kernel's bf16 q~ rounding implies (se: log2-domain scores of the rounded q~), and the kernel's own
+    # deviation from it: the denominator sums bf16-rounded P, whose rounding a dominant key carries into l in full
+    # (|ln(1 + 2^-8)| = 3.9e-3); against the exact lse the bound is the larger of the old 1e-3 relative one and the
+    # q~ rounding's own lse error plus that
+    lse_emu = torch.logsumexp(se * math.log(2.0), -1)
+    assert (lse_got - lse_emu).abs().max().item() < 4e-3
+    bound = max(1e-3 * max(1.0, lse.abs().max().item()), (lse_emu - lse).abs().max().item() + 4e-3)
+    assert (lse_got - lse).abs().max().item() < bound
 
 
 def _torch_gpu_rows(q, k, v, do, chunk=4096):

@@ -82,20 +82,26 @@ def _run(name, rank, world, dev):
     return grads, weights
 
 
+def _host(res):
+    """(grads, weights) as numpy arrays: a torch CPU tensor crosses the queue as a shared-memory handle that the
+    receiver opens through the sender's resource sharer, gone once the sender exits; arrays are pickled by value."""
+    return tuple({n: t.numpy() for n, t in d.items()} for d in res)
+
+
 def _worker(name, rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0", LCI_DIST_BACKEND="gloo")
     from long_context_biomedical_imaging_amd.trainer import init_distributed
     init_distributed()
     try:
-        q.put((rank, _run(name, rank, world, torch.device("cuda", 0))))
+        q.put((rank, _host(_run(name, rank, world, torch.device("cuda", 0)))))
     finally:
         dist.barrier()
         dist.destroy_process_group()
 
 
 def _ref_worker(name, q):
-    q.put(_run(name, 0, 1, torch.device("cuda", 0)))
+    q.put(_host(_run(name, 0, 1, torch.device("cuda", 0))))
 
 
 def _rel(a, b):
@@ -121,7 +127,10 @@ def test_ddp_two_ranks_real_model(name):
     p.join(timeout=120)
     assert p.exitcode == 0
 
-    (g0, w0), (g1, w1) = res[0], res[1]
+    def tt(d):
+        return {n: torch.from_numpy(a) for n, a in d.items()}
+    g_ref, w_ref = tt(g_ref), tt(w_ref)
+    (g0, w0), (g1, w1) = ((tt(g), tt(w)) for g, w in (res[0], res[1]))
     assert g0.keys() == g1.keys() == g_ref.keys()
     worst = 0.0
     for n in g_ref:

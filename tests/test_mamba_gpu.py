@@ -179,8 +179,10 @@ def test_fused_mamba_projection_matches_linear_layers(d_model, B, L, monkeypatch
 def test_selective_scan_one_chunk_path_bitwise(nseq, L, d, dtype):
     """Window sequences (one chunk, ABI 32): without a requested final state the forward runs only the output pass
     and the backward skips the adjoint aggregate / carry, and dB / dC are stored rather than accumulated where one
-    workgroup holds every channel (Dx <= 256). Nothing is carried into a single chunk, so y and all seven
-    gradients must equal the full three-pass path (forced by return_last_state=True) bit for bit."""
+    workgroup holds every channel (Dx <= 256). Nothing is carried into a single chunk, so y, du and d(delta) must
+    equal the full three-pass path (forced by return_last_state=True) bit for bit. dB / dC are summed over the
+    workgroup's waves with LDS float atomics, and dA / dD / d(delta_bias) over per-(b, chunk) partials with float
+    atomics, in either path: their summation order varies from run to run, so they match to f32 rounding."""
     from long_context_biomedical_imaging_amd import kernels
     torch.manual_seed(nseq + L)
     n = 8
@@ -203,5 +205,10 @@ def test_selective_scan_one_chunk_path_bitwise(nseq, L, d, dtype):
             assert last.shape == (nseq, d, n) and torch.isfinite(last).all()
         (out[..., :d].float() * cot).sum().backward()
         res.append([out[..., :d].detach()] + [t.grad for t in leaves])
-    for a, b in zip(*res):
-        assert torch.equal(a, b)
+    names = ("y", "du", "ddelta", "dA", "dBC", "dD", "ddelta_bias")
+    for name, a, b in zip(names, *res):
+        if name in ("dA", "dBC", "dD", "ddelta_bias"):   # summed by float atomics: the order varies
+            err = (a - b).abs().max().item()
+            assert err <= 1e-4 * b.abs().max().item() + 1e-6, (name, err)
+        else:
+            assert torch.equal(a, b), name

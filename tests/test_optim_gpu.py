@@ -97,6 +97,9 @@ def test_lci_adam_under_grad_scaler_skips_inf_and_unscales():
                 gr[3] = float("inf")                     # an overflowed step: both must skip it
             a.grad, b.grad = gr.clone(), gr.clone()
         before = [b.detach().clone() for b in lci.param_groups[0]["params"]]
+        one = torch.ones((), device="cuda")
+        s_ref.scale(one)                                 # (a scaled loss: initialises the scalers' scale tensors)
+        s_lci.scale(one)
         s_ref.step(ref)
         s_lci.step(lci)
         s_ref.update()

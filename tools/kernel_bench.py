@@ -144,6 +144,34 @@ def bench_scan(L, B=2, Dx=192):
              f"B{B} L{L} Dx{Dx} N8 bf16")
 
 
+def bench_scan_windows():
+    """The Swin-Mamba recipe's scans (projects/run_abct.sh: Swin-tiny p2, 4^3 windows, 128^3 volume, B = 2): every
+    window is an L = 64 sequence; stages 1-4 give (B nW, Dx) = (8192, 48), (1024, 96), (128, 192), (16, 384).
+    Algorithmic bytes per token: fwd 2 (3 Dx + 2 N), bwd 2 (5 Dx + 4 N) (bf16 I/O)."""
+    for B, Dx in ((8192, 48), (1024, 96), (128, 192), (16, 384)):
+        L, N = 64, 8
+        u = torch.randn(B, L, Dx, device="cuda").to(torch.bfloat16).requires_grad_(True)
+        dl = (torch.randn(B, L, Dx, device="cuda") * 0.5 - 3).to(torch.bfloat16).requires_grad_(True)
+        A = -torch.rand(Dx, N, device="cuda") - 0.5
+        bc = torch.randn(B, L, 2 * N, device="cuda").to(torch.bfloat16).requires_grad_(True)
+        D = torch.randn(Dx, device="cuda")
+        db = torch.randn(Dx, device="cuda") * 0.1
+
+        def fwd(grad=False):
+            yz = torch.empty(B, L, 2 * Dx, device="cuda", dtype=torch.bfloat16)
+            with torch.set_grad_enabled(grad):
+                return kernels.selective_scan_cl(u, dl, A, bc[..., :N], bc[..., N:], D, db, yz)
+
+        fb, bb = 2.0 * (3 * Dx + 2 * N) * B * L, 2.0 * (5 * Dx + 4 * N) * B * L
+        cfg = f"B{B} L{L} Dx{Dx} N8 bf16 (window scan)"
+        emit("selective_scan_fwd_win", timeit(lambda: fwd(False), iters=20), fb, "GB/s", cfg)
+        y = fwd(True)
+        gy = torch.randn_like(y)
+        tb = timeit(lambda: torch.autograd.grad(fwd(True), [u, dl, bc], gy), iters=20)
+        tf = timeit(lambda: fwd(True), iters=20)
+        emit("selective_scan_bwd_win", tb - tf, bb, "GB/s", cfg + " (fwd+bwd minus the training fwd)")
+
+
 def bench_dwconv(L=1 << 21, B=1, C=192):
     """Mamba depthwise conv + SiLU pair (mamba.py:118-119) at the C5 shape: in (B, L, 2C) bf16; fwd reads 2C and
     writes 2C values per token (4 B each way per channel at bf16), bwd reads in + dout and writes din."""
@@ -319,6 +347,8 @@ def main():
     if "scan" in which:
         bench_scan(65536)
         bench_scan(1 << 21)
+    if "scanwin" in which:
+        bench_scan_windows()
     if "dwconv" in which:
         bench_dwconv()
     if "fftconv" in which:
