@@ -14,7 +14,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_LIB = os.path.join(HERE, "liblci.so")
 LIB_PATH = os.environ.get("LCI_LIB_PATH", DEFAULT_LIB)   # override: kernel-variant A/B runs (no staleness check)
-ABI_VERSION = 32   # include/lci.h LCI_ABI_VERSION
+ABI_VERSION = 33   # include/lci.h LCI_ABI_VERSION
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -66,6 +66,10 @@ SIGNATURES = {
     "lci_linear_wgrad": [_P, _L, _P, _L, _L, _I, _I, _P, _P, _P],
     "lci_gemm_bt": [_P, _L, _P, _P, _P, _L, _L, _I, _I, _P],
     "lci_gemm_bt_acc": [_P, _L, _P, _P, _L, _L, _I, _I, _P],
+    "lci_gemm_bt_small": [_P, _L, _P, _P, _P, _L, _L, _I, _I, _P],
+    "lci_gemm_bt_small_acc": [_P, _L, _P, _P, _L, _L, _I, _I, _P],
+    "lci_sum_splits": [_P, _P, _L, _I, _P],
+    "lci_conv3_wgrad_sum": [_P, _P, _I, _I, _I, _I, _I, _P],
     "lci_linear_small_fwd": [_P, _L, _P, _P, _P, _L, _I, _I, _P],
     "lci_linear_small_bwd": [_P, _L, _P, _P, _P, _P, _L, _I, _I, _P],
     "lci_gelu_fwd": [_P, _P, _L, _P],
@@ -140,6 +144,8 @@ def load(path: str = LIB_PATH):
     lib.lci_linear_wgrad_splits.argtypes = [ctypes.c_longlong, _I, _I]
     lib.lci_gemm_bt_supported.restype = ctypes.c_int
     lib.lci_gemm_bt_supported.argtypes = [_I, _I]
+    lib.lci_gemm_bt_small_supported.restype = ctypes.c_int
+    lib.lci_gemm_bt_small_supported.argtypes = [_I, _I]
     lib.lci_linear_small_threads.restype = ctypes.c_int
     lib.lci_linear_small_threads.argtypes = []
     lib.lci_inorm_chunks.restype = ctypes.c_int

@@ -273,6 +273,88 @@ __global__ __launch_bounds__(GM_WAVES * 64, 1) void gemm_bt_kernel(GemmArgs a) {
   }
 }
 
+
+// ------------------------------------------------------------------------------ small / narrow GEMM (round 6)
+// The persistent kernel above wants a 256 x 384 (or 256) tile per CU. Two families of projections miss it and ran on
+// hipBLASLt: the Swin stage-3 / 4 projections and their data gradients (4096 / 512 tokens, K and
+// N 384 .. 3072: 16-48 tiles) and the decoder heads' 1x1 convolutions (N = 96 / 192 / 288 at up to 2^21 voxels,
+// UnetResBlock conv3 / UnetOutBlock, enhance_heads.py). Here one wave owns 32 tokens x 32 NBW features and reads its
+// MFMA fragments straight from global memory (no LDS, no barriers). K runs in chunks of CH 16-deep k-steps, two chunks
+// of fragments in registers: chunk c + 1's loads are in flight while chunk c's MFMAs run (a first version with one
+// k-step ahead was latency-bound: 30 us for a 4096 x 384 x 384 product, 1 ms for 2^21 x 192 x 96). Within a chunk
+// the reduction index is permuted so that a lane's loads are contiguous: lane (row r, half h) holds columns
+// c0 + 8 CH h + 8 j + t of its X row and of its W row for k-step j (t < 8) -- 16 CH bytes per row and lane, a whole
+// 32 CH-byte row segment per lane pair -- and the MFMAs of a chunk sum each of its 16 CH columns once. W is the A
+// operand (features on the accumulator registers, tokens on the lanes): a lane stores 4 consecutive features (8 B)
+// of its token row per register group. Workgroups are numbered feature block fastest, so the waves that read the
+// same X rows for other features run at the same time (L2 hits).
+template <int NBW, int CH, bool HAS_BIAS, bool ACC = false>
+__global__ __launch_bounds__(256) void gemm_bt_small_kernel(GemmArgs a) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nfb = a.N / (32 * NBW);
+  const long long tb = blockIdx.x / nfb;
+  const int fb = (int)(blockIdx.x - tb * nfb);
+  const long long m0 = (tb * 4 + wave) * 32;
+  if (m0 >= a.M) return;   // (no barriers in this kernel)
+  const int n0 = fb * 32 * NBW;
+  const int r = lane & 31, h = lane >> 5;
+  const int rows = (int)min(32LL, a.M - m0);
+  // rows past M read as zeros (buffer range check); their outputs are not stored
+  const rsrc_t rx = make_rsrc(a.x + m0 * a.ldx, (uint32_t)((long long)rows * a.ldx * 2));
+  const int xo = r * (int)a.ldx * 2 + 16 * CH * h;
+  const bf16* wp = a.w + (long long)(n0 + r) * a.K + 8 * CH * h;
+  const int nch = a.K / (16 * CH);
+  f32x16 acc[NBW];
+#pragma unroll
+  for (int i = 0; i < NBW; ++i) acc[i] = f32x16{};
+  bf16x8 xa[CH], wa[NBW][CH], xb[CH], wb[NBW][CH];
+  auto load = [&](int c, bf16x8 (&xs)[CH], bf16x8 (&ws)[NBW][CH]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < CH; ++j) xs[j] = __builtin_bit_cast(bf16x8, bload16(rx, xo + 16 * j, 32 * CH * c));
+#pragma unroll
+    for (int i = 0; i < NBW; ++i)
+#pragma unroll
+      for (int j = 0; j < CH; ++j) ws[i][j] = *(const bf16x8*)(wp + (long long)32 * i * a.K + 16 * CH * c + 8 * j);
+  };
+  auto mma = [&](const bf16x8 (&xs)[CH], const bf16x8 (&ws)[NBW][CH]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < CH; ++j)
+#pragma unroll
+      for (int i = 0; i < NBW; ++i) acc[i] = mfma32(ws[i][j], xs[j], acc[i]);
+  };
+  load(0, xa, wa);
+  for (int c = 0; c < nch; c += 2) {
+    if (c + 1 < nch) load(c + 1, xb, wb);
+    mma(xa, wa);
+    if (c + 1 < nch) {
+      if (c + 2 < nch) load(c + 2, xa, wa);
+      mma(xb, wb);
+    }
+  }
+  if (r >= rows) return;
+  bf16* yrow = a.y + (m0 + r) * a.ldy + n0 + 4 * h;
+#pragma unroll
+  for (int i = 0; i < NBW; ++i)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {   // register 4g + q <-> feature 32 i + 8 g + 4 h + q
+      bf16x4 v;
+      if constexpr (HAS_BIAS) {
+        const bf16x4 bb = *(const bf16x4*)(a.bias + n0 + 32 * i + 8 * g + 4 * h);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = to_bf16(acc[i][4 * g + q] + to_f32(bb[q]));
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = to_bf16(acc[i][4 * g + q]);
+      }
+      if constexpr (ACC) {   // y += the bf16 product (lci_gemm_bt_acc's roundings)
+        const bf16x4 o = *(const bf16x4*)(yrow + 32 * i + 8 * g);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = to_bf16(to_f32(o[q]) + to_f32(v[q]));
+      }
+      *(bf16x4*)(yrow + 32 * i + 8 * g) = v;
+    }
+}
+
 }  // namespace lci
 
 using namespace lci;
@@ -342,4 +424,66 @@ extern "C" int lci_gemm_bt(const void* x, long long ldx, const void* w, const vo
 extern "C" int lci_gemm_bt_acc(const void* x, long long ldx, const void* w, void* y, long long ldy, long long M, int N,
                                int K, void* stream) {
   return gemm_bt_run(x, ldx, w, nullptr, y, ldy, M, N, K, stream, true);
+}
+
+// Features per wave of the small kernel (32 NBW, NBW <= 3): the widest that divides N / 32 while the grid still has
+// >= 4096 waves (4 waves per workgroup, 32 tokens each: the 2^17 - 2^21-row 1x1 convolutions, where each wave then
+// reads its X rows once), else 1 (the 512 / 4096-token Swin projections: as many waves as the shape has).
+static int gm_small_nbw(long long M, int N) {
+  if (N % 32) return 0;
+  const long long mb = (M + 31) / 32;
+  for (int nbw : {3, 2}) {
+    if ((N / 32) % nbw == 0 && mb * (N / (32 * nbw)) >= 4096) return nbw;
+  }
+  return 1;
+}
+
+// k-steps per chunk: the largest of 4, 3, 2, 1 dividing K / 16
+static int gm_small_ch(int K) {
+  const int nk = K / 16;
+  return nk % 4 == 0 ? 4 : (nk % 3 == 0 ? 3 : (nk % 2 == 0 ? 2 : 1));
+}
+
+// 1 when lci_gemm_bt_small takes (N, K): N % 32 == 0, K % 16 == 0
+extern "C" int lci_gemm_bt_small_supported(int N, int K) { return N > 0 && N % 32 == 0 && K > 0 && K % 16 == 0; }
+
+static int gemm_bt_small_run(const void* x, long long ldx, const void* w, const void* bias, void* y, long long ldy,
+                             long long M, int N, int K, void* stream, bool acc) {
+  LCI_CHECK(lci_gemm_bt_small_supported(N, K), "gemm_bt_small: N=%d K=%d unsupported (N %% 32, K %% 16)", N, K);
+  LCI_CHECK(M > 0 && ldx >= K && ldy >= N && ldx % 8 == 0 && ldy % 8 == 0, "gemm_bt_small: bad M / strides");
+  LCI_CHECK(((uintptr_t)x | (uintptr_t)w | (uintptr_t)y) % 16 == 0 && ((uintptr_t)bias % 8) == 0,
+            "gemm_bt_small: x, w, y must be 16-byte aligned, bias 8-byte");
+  LCI_CHECK(32LL * ldx * 2 < (1ll << 31) && (long long)N * K < (1ll << 31), "gemm_bt_small: strides too large");
+  GemmArgs a{};
+  a.x = (const bf16*)x; a.ldx = ldx; a.w = (const bf16*)w; a.bias = (const bf16*)bias; a.y = (bf16*)y; a.ldy = ldy;
+  a.M = M; a.N = N; a.K = K;
+  const int nbw = gm_small_nbw(M, N), ch = gm_small_ch(K);
+  const long long nwg = (M + 127) / 128 * (N / (32 * nbw));
+  LCI_CHECK(nwg < (1ll << 31), "gemm_bt_small: M too large");
+  const dim3 grid((unsigned)nwg);
+  hipStream_t st = (hipStream_t)stream;
+#define LCI_GS(NB, C)                                                                                     \
+  if (nbw == NB && ch == C) {                                                                             \
+    if (acc) hipLaunchKernelGGL((gemm_bt_small_kernel<NB, C, false, true>), grid, dim3(256), 0, st, a);   \
+    else if (bias) hipLaunchKernelGGL((gemm_bt_small_kernel<NB, C, true>), grid, dim3(256), 0, st, a);    \
+    else hipLaunchKernelGGL((gemm_bt_small_kernel<NB, C, false>), grid, dim3(256), 0, st, a);             \
+  }
+  LCI_GS(1, 1) LCI_GS(1, 2) LCI_GS(1, 3) LCI_GS(1, 4) LCI_GS(2, 1) LCI_GS(2, 2) LCI_GS(2, 3) LCI_GS(2, 4)
+  LCI_GS(3, 1) LCI_GS(3, 2) LCI_GS(3, 3) LCI_GS(3, 4)
+#undef LCI_GS
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+
+// Y (M x N, row stride ldy) = X (M x K, row stride ldx) . W^T (+ bias), as lci_gemm_bt, for any M and N % 32 == 0,
+// K % 16 == 0 (the small-token / narrow-output projections; see gemm_bt_small_kernel).
+extern "C" int lci_gemm_bt_small(const void* x, long long ldx, const void* w, const void* bias, void* y, long long ldy,
+                                 long long M, int N, int K, void* stream) {
+  return gemm_bt_small_run(x, ldx, w, bias, y, ldy, M, N, K, stream, false);
+}
+
+// y = bf16(y + bf16(X . W^T)), as lci_gemm_bt_acc, with lci_gemm_bt_small's support.
+extern "C" int lci_gemm_bt_small_acc(const void* x, long long ldx, const void* w, void* y, long long ldy, long long M,
+                                     int N, int K, void* stream) {
+  return gemm_bt_small_run(x, ldx, w, nullptr, y, ldy, M, N, K, stream, true);
 }

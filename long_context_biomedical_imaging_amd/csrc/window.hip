@@ -63,6 +63,7 @@ struct WinArgs {
   int Bw, nW, N, Npad, nqb, nkt, C, H, masked, T;
   int dS_kl;                               // dS tiles in the key-on-lane layout (win_attn_bwd1_kernel)
   int bwd1_cnt;                            // win_attn_bwd1_kernel: per-tile dQ order counters instead of a barrier
+  int order;                               // workgroup -> (window, head) order of the attention kernels (win_item)
   float scale, c;
 };
 
@@ -91,38 +92,74 @@ __device__ __forceinline__ int win_row(const WinArgs& a, int w, int n, int& rid)
   return pad ? -1 : (int)row;
 }
 
-// load 8 bf16 (16 B) of token row `row` at channel offset col, or of the bias for padded tokens
-__device__ __forceinline__ bf16x8 win_load8(const WinArgs& a, int row, int col, bool exists) {
-  if (!exists) return bf16x8{};
-  if (row >= 0) return *(const bf16x8*)(a.qkv + (long long)row * 3 * a.C + col);
-  bf16x8 r;
-  if (a.qkv_bias) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = to_bf16(a.qkv_bias[col + j]);
-  } else {
-    r = bf16x8{};
-  }
-  return r;
-}
-
 __device__ __forceinline__ const bf16* out_row_ptr(const WinArgs& a, const bf16* base, int w, int n, int row) {
   return base + (long long)(a.mode == 0 ? w * a.N + n : row) * a.C;
 }
 
+// (window, head) of attention workgroup blockIdx.x (1-D grid of Bw * H). order 1 (default, round 6): in super-blocks of
+// 8 windows x H heads, workgroup b = 8 H g + 8 hh + i is window 8 g + i, head hh -- the dispatcher deals workgroup b
+// to XCD b % 8 (observed round-robin; nothing depends on it for correctness), so the H heads of a window run back to
+// back on one XCD and their 64-byte pieces of the same token rows (q | k | v of 3C-channel qkv rows, the C-channel
+// out / dout rows) meet in that XCD's L2 instead of being fetched from HBM H times, 1000 windows apart. The last,
+// partial super-block (Bw % 8 windows) is head-major. order 0: the round-5 (window, head) grid order.
+__device__ __forceinline__ void win_item(const WinArgs& a, int& w, int& hh) {
+  const int b = blockIdx.x;
+  if (a.order == 0) { w = b % a.Bw; hh = b / a.Bw; return; }
+  const int G = a.Bw / 8, full = G * 8 * a.H;
+  if (b < full) {
+    const int g = b / (8 * a.H), r = b - g * 8 * a.H;
+    w = 8 * g + (r & 7);
+    hh = r >> 3;
+  } else {
+    const int rem = a.Bw - 8 * G, r = b - full;
+    w = 8 * G + r % rem;
+    hh = r / rem;
+  }
+}
+
 struct WinLds {
   bf16* t0; bf16* t1; int* row; int* rid;
+  const bf16* bias;   // the head's q | k | v bias, bf16 (3 x 32): the value of padded voxels' qkv rows
+  int hoff;           // hh * WHD
 };
 
-__device__ __forceinline__ void win_setup(const WinArgs& a, char* smem, WinLds& L, int w) {
-  L.t0 = (bf16*)smem;
+constexpr int WBIAS_B = 256;   // LDS bytes ahead of t0: the head's bf16 qkv bias (192 B)
+
+// 16 zero bytes: the source of the staging loads of rows that do not exist (loads are branch-free pointer selects)
+__device__ __attribute__((aligned(16))) bf16 kWinZero[8];
+
+// load 8 bf16 (16 B) of token row `row` at channel offset col (q | k | v block of the 3C-channel row), or of the bias
+// for padded tokens -- from the LDS copy win_setup made. Branch-free: the global load reads the row or 16 zero bytes,
+// the LDS read the bias, and a select picks. (With the f32 bias loaded and converted inside a padded-voxel branch, and
+// the row loads in exec-masked branches, the compiler placed vmcnt(0) waits inside those branches: every staging load
+// of the prologue waited for the previous ones; round 6.)
+__device__ __forceinline__ bf16x8 win_load8(const WinArgs& a, const WinLds& L, int row, int col, bool exists) {
+  const bf16* src = exists && row >= 0 ? a.qkv + (long long)row * 3 * a.C + col : kWinZero;
+  const bf16x8 g = *(const bf16x8*)src;
+  const int which = col >= 2 * a.C ? 2 : (col >= a.C ? 1 : 0);
+  const bf16x8 b = *(const bf16x8*)(L.bias + which * WHD + (col - which * a.C - L.hoff));
+  return exists && row < 0 ? b : g;
+}
+
+__device__ __forceinline__ void win_setup(const WinArgs& a, char* smem, WinLds& L, int w, int hh) {
+  bf16* bl = (bf16*)smem;
+  L.bias = bl;
+  L.hoff = hh * WHD;
+  L.t0 = (bf16*)(smem + WBIAS_B);
   L.t1 = L.t0 + a.Npad * WLD;
   L.row = (int*)(L.t1 + a.Npad * WLD);
   L.rid = L.row + a.Npad;
+  // the bias values are loaded first (their latency under the row map's integer math), stored after it
+  const int bi = threadIdx.x < 3 * WHD ? threadIdx.x : 0;
+  const float bv = *(a.qkv_bias ? a.qkv_bias + (bi / WHD) * a.C + hh * WHD + bi % WHD : (const float*)kWinZero);
   for (int n = threadIdx.x; n < a.Npad; n += blockDim.x) {
     int rid = 0;
     L.row[n] = n < a.N ? win_row(a, w, n, rid) : -2;
     L.rid[n] = rid;
   }
+  if (threadIdx.x < 3 * WHD) bl[threadIdx.x] = to_bf16(bv);
+  for (int i = threadIdx.x + blockDim.x; i < 3 * WHD; i += blockDim.x)   // (workgroups of fewer than 96 threads)
+    bl[i] = a.qkv_bias ? to_bf16(a.qkv_bias[(i / WHD) * a.C + hh * WHD + i % WHD]) : to_bf16(0.f);
   __syncthreads();
 }
 
@@ -132,8 +169,8 @@ __device__ __forceinline__ bf16x8 win_stage_src1(const WinArgs& a, const WinLds&
   const int row = L.row[n];
   const bool ex = n < a.N;
   if (second_is_out)
-    return (ex && row != -1) ? *(const bf16x8*)(out_row_ptr(a, obase, w, n, row) + c1 + ch * 8) : bf16x8{};
-  return win_load8(a, row, c1 + ch * 8, ex);
+    return *(const bf16x8*)(ex && row != -1 ? out_row_ptr(a, obase, w, n, row) + c1 + ch * 8 : kWinZero);
+  return win_load8(a, L, row, c1 + ch * 8, ex);
 }
 
 template <int NT>
@@ -148,7 +185,7 @@ __device__ __forceinline__ void win_stage(const WinArgs& a, const WinLds& L, int
       const int idx = it * NT + threadIdx.x;
       if (idx < items) {
         const int n = idx >> 2, ch = idx & 3;
-        r0[it] = win_load8(a, L.row[n], c0 + ch * 8, n < a.N);
+        r0[it] = win_load8(a, L, L.row[n], c0 + ch * 8, n < a.N);
         r1[it] = win_stage_src1(a, L, n, ch, c1, second_is_out, obase, w);
       }
     }
@@ -164,7 +201,7 @@ __device__ __forceinline__ void win_stage(const WinArgs& a, const WinLds& L, int
   } else {
     for (int idx = threadIdx.x; idx < items; idx += blockDim.x) {
       const int n = idx >> 2, ch = idx & 3;
-      *(bf16x8*)(L.t0 + n * WLD + ch * 8) = win_load8(a, L.row[n], c0 + ch * 8, n < a.N);
+      *(bf16x8*)(L.t0 + n * WLD + ch * 8) = win_load8(a, L, L.row[n], c0 + ch * 8, n < a.N);
       *(bf16x8*)(L.t1 + n * WLD + ch * 8) = win_stage_src1(a, L, n, ch, c1, second_is_out, obase, w);
     }
   }
@@ -183,7 +220,7 @@ __device__ __forceinline__ void win_stage_rt(const WinArgs& a, const WinLds& L, 
       const int idx = base + it * NT + threadIdx.x;
       if (idx < items) {
         const int n = idx >> 2, ch = idx & 3;
-        r0[it] = win_load8(a, L.row[n], c0 + ch * 8, n < a.N);
+        r0[it] = win_load8(a, L, L.row[n], c0 + ch * 8, n < a.N);
         r1[it] = win_stage_src1(a, L, n, ch, c1, second_is_out, obase, w);
       }
     }
@@ -298,11 +335,12 @@ __device__ __forceinline__ bf16x8 scaled8(bf16x8 v, float c) {
 template <int NW>
 __global__ __launch_bounds__(NW ? NW * 64 : 1024) void win_attn_fwd_kernel(WinArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int w = blockIdx.x, hh = blockIdx.y;
+  int w, hh;
+  win_item(a, w, hh);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5;
   const int nw = NW ? NW : (int)(blockDim.x >> 6);
   WinLds L;
-  win_setup(a, smem, L, w);
+  win_setup(a, smem, L, w, hh);
   if constexpr (NW != 0) win_stage<NW * 64>(a, L, a.C + hh * WHD, 2 * a.C + hh * WHD, false, nullptr, w);   // K, V
   else win_stage_rt(a, L, a.C + hh * WHD, 2 * a.C + hh * WHD, false, nullptr, w);
   const float c = a.c;
@@ -321,7 +359,7 @@ __global__ __launch_bounds__(NW ? NW * 64 : 1024) void win_attn_fwd_kernel(WinAr
     const bool qv = q < a.N;
     const int qrow = qv ? L.row[q] : -2;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) qn[ks] = win_load8(a, qrow, hh * WHD + ks * 16 + 8 * half, qv);
+    for (int ks = 0; ks < 2; ++ks) qn[ks] = win_load8(a, L, qrow, hh * WHD + ks * 16 + 8 * half, qv);
   };
   if (wave < a.nqb) load_q(wave);
   for (int qb = wave; qb < a.nqb; qb += nw) {
@@ -399,10 +437,11 @@ __global__ __launch_bounds__(NW ? NW * 64 : 1024) void win_attn_fwd_kernel(WinAr
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void win_attn_bwd_kernel(WinArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int w = blockIdx.x, hh = blockIdx.y;
+  int w, hh;
+  win_item(a, w, hh);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5;
   WinLds L;
-  win_setup(a, smem, L, w);
+  win_setup(a, smem, L, w, hh);
   float* lse_l = (float*)(L.rid + a.Npad);
   float* ndl_l = lse_l + a.Npad;   // -delta
   const float c = a.c;
@@ -420,7 +459,7 @@ __global__ __launch_bounds__(NW * 64) void win_attn_bwd_kernel(WinArgs a) {
     const bool has_out = qv && qrow != -1;   // padded queries are cropped: dO = 0
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      qf[ks] = scaled8(win_load8(a, qrow, hh * WHD + ks * 16 + 8 * half, qv), c);
+      qf[ks] = scaled8(win_load8(a, L, qrow, hh * WHD + ks * 16 + 8 * half, qv), c);
       if (has_out) {
         df[ks] = *(const bf16x8*)(out_row_ptr(a, a.dout, w, q, qrow) + hh * WHD + ks * 16 + 8 * half);
         const bf16x8 ov = *(const bf16x8*)(out_row_ptr(a, a.o, w, q, qrow) + hh * WHD + ks * 16 + 8 * half);
@@ -486,8 +525,8 @@ __global__ __launch_bounds__(NW * 64) void win_attn_bwd_kernel(WinArgs a) {
     bf16x8 kf[2], vf[2];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      kf[ks] = scaled8(win_load8(a, krow, a.C + hh * WHD + ks * 16 + 8 * half, kv), c);
-      vf[ks] = win_load8(a, krow, 2 * a.C + hh * WHD + ks * 16 + 8 * half, kv);
+      kf[ks] = scaled8(win_load8(a, L, krow, a.C + hh * WHD + ks * 16 + 8 * half, kv), c);
+      vf[ks] = win_load8(a, L, krow, 2 * a.C + hh * WHD + ks * 16 + 8 * half, kv);
     }
     const bf16* brow = a.biasT + tho + (long long)key * a.Npad + 4 * half;
     f32x16 dk = {}, dv = {};
@@ -570,13 +609,33 @@ __global__ __launch_bounds__(NW * 64) void win_attn_bwd_kernel(WinArgs a) {
 // rotation: deterministic). Q / dO are staged once; delta = rowsum(dO * O) is computed at staging.
 constexpr int DQLD = 36;   // f32 row stride of the LDS dQ accumulator: the b128 RMW of 16 query rows is conflict-free
 constexpr int WBWD1_MAXW = 12;
+// Phase timestamps of the single-phase backward (variant builds only, -DLCI_WIN_STAMPS: tools/r6_win_stamps.py):
+// lane 0 of every wave of the first 2048 workgroups (dispatch order) writes s_memrealtime (100 MHz) at slot k of
+// its 20-slot record, slot 19 the CU (__smid)
+#ifdef LCI_WIN_STAMPS
+constexpr int WST_WG = 2048, WST_SLOTS = 20;
+__device__ long long g_win_stamps[WST_WG * WBWD1_MAXW * WST_SLOTS];
+#define WSTAMP(k)                                                                                              \
+  do {                                                                                                         \
+    const int wg_ = blockIdx.x;                                                                                \
+    if ((threadIdx.x & 63) == 0 && wg_ < WST_WG)                                                               \
+      g_win_stamps[((long long)wg_ * WBWD1_MAXW + (threadIdx.x >> 6)) * WST_SLOTS + (k)] =                     \
+          (k) == 19 ? (long long)__smid() : (long long)wall_clock64();                                         \
+  } while (0)
+#else
+#define WSTAMP(k)
+#endif
 __global__ __launch_bounds__(WBWD1_MAXW * 64) void win_attn_bwd1_kernel(WinArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int w = blockIdx.x, hh = blockIdx.y;
+  int w, hh;
+  win_item(a, w, hh);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5;
   const int nkb = a.nkt, NT = blockDim.x;
+  WSTAMP(0);
+  WSTAMP(19);
   WinLds L;
-  win_setup(a, smem, L, w);                                  // t0, t1, row, rid
+  win_setup(a, smem, L, w, hh);                                  // t0, t1, row, rid
+  WSTAMP(1);
   float* lse_l = (float*)(L.rid + a.Npad);                   // -lse2
   float* ndl_l = lse_l + a.Npad;                             // -delta
   float* dq_l = ndl_l + a.Npad;                              // (Npad, DQLD) f32
@@ -597,16 +656,16 @@ __global__ __launch_bounds__(WBWD1_MAXW * 64) void win_attn_bwd1_kernel(WinArgs 
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
     const int idx = it * NT + threadIdx.x, n = idx >> 2, ch = idx & 3;
-    r0[it] = win_load8(a, L.row[n], hh * WHD + ch * 8, n < a.N);
+    r0[it] = win_load8(a, L, L.row[n], hh * WHD + ch * 8, n < a.N);
     r1[it] = win_stage_src1(a, L, n, ch, hh * WHD, true, a.dout, w);
     const int row = L.row[n];
-    ov[it] = (n < a.N && row != -1) ? *(const bf16x8*)(out_row_ptr(a, a.o, w, n, row) + hh * WHD + ch * 8) : bf16x8{};
-    lsv[it] = (ch == 0 && n < a.N) ? lseg[n] : 0.f;
+    ov[it] = *(const bf16x8*)(n < a.N && row != -1 ? out_row_ptr(a, a.o, w, n, row) + hh * WHD + ch * 8 : kWinZero);
+    lsv[it] = *(ch == 0 && n < a.N ? lseg + n : (const float*)kWinZero);
   }
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
-    kr[ks] = win_load8(a, krow, a.C + hh * WHD + ks * 16 + 8 * half, kv);
-    vr[ks] = win_load8(a, krow, 2 * a.C + hh * WHD + ks * 16 + 8 * half, kv);
+    kr[ks] = win_load8(a, L, krow, a.C + hh * WHD + ks * 16 + 8 * half, kv);
+    vr[ks] = win_load8(a, L, krow, 2 * a.C + hh * WHD + ks * 16 + 8 * half, kv);
   }
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
@@ -637,6 +696,7 @@ __global__ __launch_bounds__(WBWD1_MAXW * 64) void win_attn_bwd1_kernel(WinArgs 
     vf[ks] = vr[ks];
   }
   __syncthreads();   // staging, row constants, dQ zero, K scratch
+  WSTAMP(2);
   const bf16x8 kt0 = frag_tr<0>(scr, WLD, 0, 0, lane), kt1 = frag_tr<1>(scr, WLD, 0, 0, lane);
   __builtin_amdgcn_wave_barrier();   // K^T read before the scratch takes dS tiles
 
@@ -718,6 +778,7 @@ __global__ __launch_bounds__(WBWD1_MAXW * 64) void win_attn_bwd1_kernel(WinArgs 
   int qt_prev = -1;
   for (int t = 0; t < nkb; ++t) {
     LCI_WIN_BWD_SCHED();
+    WSTAMP(3 + t);
     const int qn = qt + 1 == nkb ? 0 : qt + 1;
     if (t > 0) {   // the previous step's tile
       if (a.bwd1_cnt) dq_rmw_ordered(qt_prev, t - 1, dq_prev);
@@ -757,9 +818,11 @@ __global__ __launch_bounds__(WBWD1_MAXW * 64) void win_attn_bwd1_kernel(WinArgs 
     }
     if (!a.bwd1_cnt) step_barrier();   // next interval: the RMW of this step's tile
   }
+  WSTAMP(15);
   if (a.bwd1_cnt) dq_rmw_ordered(qt_prev, nkb - 1, dq_prev);
   else dq_rmw(qt_prev, dq_prev);
   __syncthreads();
+  WSTAMP(16);
   if (kv && krow >= 0) {
     bf16* base = a.dqkv + (long long)(a.mode == 0 ? w * a.N + key : krow) * 3 * a.C + hh * WHD;
 #pragma unroll
@@ -818,6 +881,7 @@ __global__ __launch_bounds__(WBWD1_MAXW * 64) void win_attn_bwd1_kernel(WinArgs 
       }
     }
   }
+  WSTAMP(17);
   // dQ rows (the loop's last barrier ordered every RMW): 16-byte chunks of 8 channels, scaled, bf16
   for (int it = threadIdx.x; it < a.N * 4; it += NT) {
     const int n = it >> 2, ch = it & 3;
@@ -829,6 +893,7 @@ __global__ __launch_bounds__(WBWD1_MAXW * 64) void win_attn_bwd1_kernel(WinArgs 
     for (int j = 0; j < 4; ++j) { o8[j] = to_bf16(lo[j] * a.scale); o8[j + 4] = to_bf16(hi[j] * a.scale); }
     *(bf16x8*)(a.dqkv + (long long)(a.mode == 0 ? w * a.N + n : row) * 3 * a.C + hh * WHD + ch * 8) = o8;
   }
+  WSTAMP(18);
 }
 
 // dbias_pad[C | 2C + h*32 + d] += sum_w pad_ws[w][h][k|v, d]: one workgroup per (head, value), windows split over
@@ -956,11 +1021,14 @@ static int win_fill(WinArgs& a, const int* geo, float scale) {
   a.Npad = (a.N + 31) / 32 * 32;
   a.nqb = a.nkt = a.Npad / 32;
   a.scale = scale; a.c = scale * WLOG2E;
+  static const int order_env = getenv("LCI_WIN_ORDER") ? atoi(getenv("LCI_WIN_ORDER")) : 1;   // A/B hook
+  a.order = order_env;
+  LCI_CHECK((long long)a.Bw * a.H < (1LL << 31), "window_attn: too many (window, head) workgroups");
   return 0;
 }
 
 static size_t win_lds(const WinArgs& a, bool bwd) {
-  return (size_t)a.Npad * WLD * 2 * 2 + (size_t)a.Npad * 4 * 2 + (bwd ? (size_t)a.Npad * 4 * 2 : 0);
+  return WBIAS_B + (size_t)a.Npad * WLD * 2 * 2 + (size_t)a.Npad * 4 * 2 + (bwd ? (size_t)a.Npad * 4 * 2 : 0);
 }
 
 }  // namespace lci
@@ -1004,13 +1072,13 @@ extern "C" int lci_window_attn_fwd(const void* qkv, const float* qkv_bias, const
   if (fwd_nw == 0 && a.nqb <= 16) {
     (void)hipFuncSetAttribute((const void*)win_attn_fwd_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
-    hipLaunchKernelGGL(win_attn_fwd_kernel<0>, dim3(a.Bw, a.H), dim3(a.nqb * 64), win_lds(a, false),
+    hipLaunchKernelGGL(win_attn_fwd_kernel<0>, dim3(a.Bw * a.H), dim3(a.nqb * 64), win_lds(a, false),
                        (hipStream_t)stream, a);
   } else {
     constexpr int NW = 8;
     (void)hipFuncSetAttribute((const void*)win_attn_fwd_kernel<NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
-    hipLaunchKernelGGL(win_attn_fwd_kernel<NW>, dim3(a.Bw, a.H), dim3(NW * 64), win_lds(a, false),
+    hipLaunchKernelGGL(win_attn_fwd_kernel<NW>, dim3(a.Bw * a.H), dim3(NW * 64), win_lds(a, false),
                        (hipStream_t)stream, a);
   }
   LCI_LAUNCH_CHECK();
@@ -1049,13 +1117,13 @@ extern "C" int lci_window_attn_bwd(const void* qkv, const float* qkv_bias, const
     a.dS_kl = 1;
     static const int cnt_env = getenv("LCI_WIN_BWD1_CNT") ? atoi(getenv("LCI_WIN_BWD1_CNT")) : 1;
     a.bwd1_cnt = cnt_env;
-    const size_t lds = (size_t)a.Npad * WLD * 2 * 2 + (size_t)a.Npad * 4 * 4 + (size_t)a.Npad * DQLD * 4 +
+    const size_t lds = WBIAS_B + (size_t)a.Npad * WLD * 2 * 2 + (size_t)a.Npad * 4 * 4 + (size_t)a.Npad * DQLD * 4 +
                        (size_t)a.nkt * 32 * WLD * 2 + 64;
     LCI_CHECK(lds <= 160 * 1024, "window_attn_bwd: %zu B of LDS", lds);
     (void)hipFuncSetAttribute((const void*)win_attn_bwd1_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     a.pad_ws = dbias_pad ? pad_ws : nullptr;
-    hipLaunchKernelGGL(win_attn_bwd1_kernel, dim3(a.Bw, a.H), dim3(a.nkt * 64), lds, s, a);
+    hipLaunchKernelGGL(win_attn_bwd1_kernel, dim3(a.Bw * a.H), dim3(a.nkt * 64), lds, s, a);
     LCI_LAUNCH_CHECK();
     if (dbias_pad) hipLaunchKernelGGL(win_pad_reduce_kernel, dim3(a.H * 64), dim3(256), 0, s, a);
   } else if (!bias) {
@@ -1064,11 +1132,11 @@ extern "C" int lci_window_attn_bwd(const void* qkv, const float* qkv_bias, const
   } else if (nw_env == 8) {
     (void)hipFuncSetAttribute((const void*)win_attn_bwd_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
-    hipLaunchKernelGGL(win_attn_bwd_kernel<8>, dim3(a.Bw, a.H), dim3(512), win_lds(a, true), s, a);
+    hipLaunchKernelGGL(win_attn_bwd_kernel<8>, dim3(a.Bw * a.H), dim3(512), win_lds(a, true), s, a);
   } else {
     (void)hipFuncSetAttribute((const void*)win_attn_bwd_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
-    hipLaunchKernelGGL(win_attn_bwd_kernel<4>, dim3(a.Bw, a.H), dim3(256), win_lds(a, true), s, a);
+    hipLaunchKernelGGL(win_attn_bwd_kernel<4>, dim3(a.Bw * a.H), dim3(256), win_lds(a, true), s, a);
   }
   LCI_LAUNCH_CHECK();
   if (dS && drpb) {
@@ -1086,6 +1154,13 @@ extern "C" int lci_window_bwd_needs_plain(const int* geo) {
   if (win_fill(a, geo, 1.f)) return -1;
   return (win_bwd1_enabled() && a.nkt <= WBWD1_MAXW) ? 0 : 1;
 }
+
+#ifdef LCI_WIN_STAMPS
+extern "C" int lci_debug_win_stamps(void* dst, long long n) {   // variant builds only (not in lci.h)
+  n = std::min<long long>(n, (long long)WST_WG * WBWD1_MAXW * WST_SLOTS);
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_win_stamps), n * 8, 0, hipMemcpyDeviceToHost) != hipSuccess;
+}
+#endif
 
 extern "C" long long lci_window_pad_ws_elems(const int* geo) {
   WinArgs a{};

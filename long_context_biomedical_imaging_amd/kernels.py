@@ -1481,8 +1481,10 @@ def conv3_wgrad_cl(x_cl: torch.Tensor, dy_cl: torch.Tensor, kd: int) -> torch.Te
     KernelTimer.run("conv3_wgrad", 2.0 * B * D * H * W * Cout * Cin * kd * 9, x_cl, lambda: _lib.call(
         "lci_conv3_wgrad", xp.data_ptr(), dy_cl.data_ptr(), part.data_ptr(), B, D, H, W, cp, Cout, kd,
         _lib.stream_of(x_cl)))
-    g = (part[0] if ns == 1 else part.sum(0))[..., :Cin]         # (taps, Cout, Cin)
-    return g.permute(1, 2, 0).reshape(Cout, Cin, *((3, 3, 3) if kd == 3 else (3, 3)))
+    # (Cout, Cin, taps): the split sum and the permute to the Conv weight layout in one pass (lci_conv3_wgrad_sum)
+    g = torch.empty(Cout, Cin, kd * 9, device=x_cl.device, dtype=torch.float32)
+    _lib.call("lci_conv3_wgrad_sum", part.data_ptr(), g.data_ptr(), ns, kd * 9, Cout, cp, Cin, _lib.stream_of(x_cl))
+    return g.view(Cout, Cin, *((3, 3, 3) if kd == 3 else (3, 3)))
 
 
 def _conv3_pack(weight: torch.Tensor, kd: int, mode: int, cin_pad: int) -> torch.Tensor:
@@ -1572,6 +1574,8 @@ class _ResConvs(torch.autograd.Function):
         N3 = w3b.shape[0]
         if HIP_GEMM and gemm_bt_preferred(x2.shape[0], N3) and gemm_bt_supported(x2, N3, Cin):
             r2 = gemm_bt(x2, w3b)
+        elif SMALL_GEMM and gemm_small_supported(x2, N3, Cin):
+            r2 = gemm_small(x2, w3b)
         else:
             with torch.autocast("cuda", enabled=False):
                 r2 = torch.nn.functional.linear(x2, w3b)
@@ -1600,8 +1604,12 @@ class _ResConvs(torch.autograd.Function):
                         KernelTimer.run("gemm_bt", 2.0 * dr2.shape[0] * Cin * N3, dr2, lambda: _lib.call(
                             "lci_gemm_bt_acc", dr2.data_ptr(), dr2.stride(0), w3t.data_ptr(), dx2.data_ptr(), Cin,
                             dr2.shape[0], Cin, N3, _lib.stream_of(dr2)))
+                    elif SMALL_GEMM and gemm_small_supported(dr2, Cin, N3):
+                        gemm_small(dr2, w3b.t(), out=dx2)                  # += bf16(dr . W3), as lci_gemm_bt_acc
                     else:
                         dx2.addmm_(dr2, w3b)                                 # += dr . W3 in the GEMM (beta = 1)
+            elif SMALL_GEMM and gemm_small_supported(dr2, Cin, N3):
+                dx = gemm_small(dr2, w3b.t()).view(*x_cl.shape)
             else:
                 dx = (dr2 @ w3b).view(*x_cl.shape)
             dx = _from_cl(dx, nd)
@@ -1857,7 +1865,7 @@ def _ln_bwd(x2, weight, mean, rstd, dy, dres, shape, want_bf16=False, dres2=None
                     x2, lambda: _lib.call("lci_layernorm_bwd", x2.data_ptr(), dy.data_ptr(), int(bf), weight.data_ptr(),
                                           mean.data_ptr(), rstd.data_ptr(), _lib.ptr(dres), _lib.ptr(dres2),
                                           dx.data_ptr(), _lib.ptr(dxb), part.data_ptr(), rows, C, _lib.stream_of(x2)))
-    s = part.sum(0)
+    s = sum_splits(part)
     if want_bf16:
         return dx.view(shape), s[0], s[1], dxb.view(shape)
     return dx.view(shape), s[0], s[1]
@@ -2019,6 +2027,19 @@ def linear_wgrad_supported(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
     return _lib.load().lci_linear_wgrad_splits(M, N, K) > 0
 
 
+def sum_splits(part: torch.Tensor) -> torch.Tensor:
+    """part (ns, ...) f32 contiguous -> the sum over dim 0 in split order (lci_sum_splits); part[0] when ns == 1."""
+    ns = part.shape[0]
+    if ns == 1:
+        return part[0]
+    n = part[0].numel()
+    if n % 4 or part.data_ptr() % 16:
+        return part.sum(0)
+    out = torch.empty(part.shape[1:], device=part.device, dtype=torch.float32)
+    _lib.call("lci_sum_splits", part.data_ptr(), out.data_ptr(), n, ns, _lib.stream_of(part))
+    return out
+
+
 def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor, bias: bool):
     """dW (N, K) f32 = dy2^T x2 and db (N) f32 = column sums of dy2 (or None), by the HIP split-token kernel
     (per-split partials summed here)."""
@@ -2032,7 +2053,7 @@ def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor, bias: bool):
     KernelTimer.run("linear_wgrad", 2.0 * M * N * K, dy2, lambda: _lib.call(
         "lci_linear_wgrad", dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), M, N, K, part.data_ptr(),
         _lib.ptr(dbp), _lib.stream_of(dy2)))
-    return part.sum(0), (dbp.sum(0) if bias else None)
+    return sum_splits(part), (sum_splits(dbp) if bias else None)
 
 
 def _wgrad_tiny_k(dy2: torch.Tensor, x2: torch.Tensor, bias: bool):
@@ -2046,7 +2067,7 @@ def _wgrad_tiny_k(dy2: torch.Tensor, x2: torch.Tensor, bias: bool):
     KernelTimer.run("linear_wgrad_tiny", 2.0 * M * N * K, dy2, lambda: _lib.call(
         "lci_linear_small_bwd", dy2.data_ptr(), dy2.stride(0), w_unused.data_ptr(), x2.data_ptr(), None,
         part.data_ptr(), M, K, N, _lib.stream_of(dy2)))
-    dw = part[:K * N].sum(1).view(K, N).t()
+    dw = part[:K * N].sum(1).view(K, N).t().contiguous()   # (the parameter's strides: DDP's bucket views)
     return dw, (dy2.float().sum(0) if bias else None)
 
 
@@ -2089,6 +2110,45 @@ def gemm_bt(x2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None)
     return y
 
 
+# csrc/gemm.hip's small / narrow kernel (round 6) for the GEMMs lci_gemm_bt does not take or fill: the Swin stage-3 / 4
+# projections (4096 / 512 tokens) and the decoder heads' 96 / 192 / 288-wide 1x1 convolutions. Opt-in
+# (LCI_SMALL_GEMM=1): against hipBLASLt it won on 5 of the 23 C3 shapes and lost up to 3x on the rest (K >= 192 at
+# 2^18 - 2^21 rows, K >= 768 at 512 - 4096; profiles/r06_gemm_small.txt), and the C3 step went 48.8 -> 51.9 ms with
+# it routed to every supported shape, so hipBLASLt keeps them.
+SMALL_GEMM = os.environ.get("LCI_SMALL_GEMM", "0") == "1"
+
+
+def gemm_small_supported(x2: torch.Tensor, N: int, K: int) -> bool:
+    """Whether lci_gemm_bt_small takes x2 (M, K) bf16 rows (unit column stride, 8-element row stride, 16-B aligned)
+    for N outputs: N % 32 == 0, K % 16 == 0."""
+    return (x2.is_cuda and x2.dtype == torch.bfloat16 and x2.dim() == 2 and x2.stride(1) == 1
+            and x2.stride(0) % 8 == 0 and x2.data_ptr() % 16 == 0 and x2.shape[0] > 0
+            and bool(_lib.load().lci_gemm_bt_small_supported(N, K)))
+
+
+def gemm_small(x2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None,
+               out: torch.Tensor | None = None) -> torch.Tensor:
+    """y (M, N) bf16 = x2 (M, K) . w^T + bias on lci_gemm_bt_small (w (N, K) bf16, made contiguous; bias bf16 or
+    None); with `out` (an (M, N) bf16 matrix, unit column stride): out += bf16(x2 . w^T) in place (no bias)."""
+    M, K = x2.shape
+    N = w.shape[0]
+    w = w.contiguous()
+    if bias is not None:
+        bias = bias.contiguous()
+    _lib.require_gpu(w, bias)
+    if out is not None:
+        assert bias is None and out.shape == (M, N) and out.stride(1) == 1 and out.dtype == torch.bfloat16
+        KernelTimer.run("gemm_bt_small", 2.0 * M * N * K, x2, lambda: _lib.call(
+            "lci_gemm_bt_small_acc", x2.data_ptr(), x2.stride(0), w.data_ptr(), out.data_ptr(), out.stride(0), M, N, K,
+            _lib.stream_of(x2)))
+        return out
+    y = torch.empty(M, N, device=x2.device, dtype=torch.bfloat16)
+    KernelTimer.run("gemm_bt_small", 2.0 * M * N * K, x2, lambda: _lib.call(
+        "lci_gemm_bt_small", x2.data_ptr(), x2.stride(0), w.data_ptr(), _lib.ptr(bias), y.data_ptr(), N, M, N, K,
+        _lib.stream_of(x2)))
+    return y
+
+
 class _Linear(torch.autograd.Function):
     """y = x W^T + b with autocast's casts done here (x, W, b -> the autocast dtype, exactly what F.linear under
     autocast computes); the bf16 forward and data-gradient GEMMs on csrc/gemm.hip where it takes the shape (hipBLASLt
@@ -2107,6 +2167,8 @@ class _Linear(torch.autograd.Function):
         x2 = xc.reshape(-1, K) if xc.dim() != 2 else xc
         if HIP_GEMM and x2.dim() == 2 and gemm_bt_preferred(x2.shape[0], N) and gemm_bt_supported(x2, N, K):
             y = gemm_bt(x2, wc, bc).view(*xc.shape[:-1], N)
+        elif SMALL_GEMM and x2.dim() == 2 and gemm_small_supported(x2, N, K):
+            y = gemm_small(x2, wc, bc).view(*xc.shape[:-1], N)
         elif K == 1 and xc.is_cuda:
             # one input channel (the image into encoder1's 1x1 residual conv): an outer product, one stream; the
             # product of two bf16 values is exact in f32, so x w (+ b) rounds the same f32 value the GEMM does
@@ -2131,6 +2193,8 @@ class _Linear(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if HIP_GEMM and dy2.dtype == wc.dtype and gemm_bt_preferred(dy2.shape[0], K) and gemm_bt_supported(dy2, K, N):
                 dx = gemm_bt(dy2, wc.t()).view(*dy.shape[:-1], K)   # dX = dY . W = dY . (W^T)^T
+            elif SMALL_GEMM and dy2.dtype == wc.dtype and gemm_small_supported(dy2, K, N):
+                dx = gemm_small(dy2, wc.t()).view(*dy.shape[:-1], K)
             else:
                 dx = (dy2 @ wc).view(*dy.shape[:-1], K)
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):

@@ -24,6 +24,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 import torch.nn.functional as F
+from torch.optim.adam import _fused_adam
 
 
 def init_distributed():
@@ -94,7 +95,7 @@ class _LciAdamStep:
                     or isinstance(group["lr"], torch.Tensor)
                     or any(p.dtype != torch.float32 or not p.is_cuda for p in params)
                     or any(g.is_sparse or not g.is_contiguous() for g in grads)):
-                torch.optim.adam._fused_adam(params, grads, exp_avgs, exp_avg_sqs, max_sqs, steps, grad_scale, found_inf,
+                _fused_adam(params, grads, exp_avgs, exp_avg_sqs, max_sqs, steps, grad_scale, found_inf,
                                              amsgrad=group["amsgrad"], has_complex=has_complex, beta1=beta1,
                                              beta2=beta2, lr=group["lr"], weight_decay=group["weight_decay"],
                                              eps=group["eps"], maximize=group["maximize"], capturable=True,

@@ -17,6 +17,7 @@ pytestmark = pytest.mark.gpu
     (2, (9, 10, 11), 32, 32),      # ragged volume, NT=1
     (1, (16, 16, 16), 96, 96),     # Swin-tiny stage-1 channels, NT=3
     (1, (7, 12, 5), 192, 96),      # UnetrUpBlock conv1 (2C -> C)
+    (2, (9, 7, 13), 96, 192),      # ragged, two samples: the (3, 1, 3) weight-gradient tile (Cout, Cin % 96)
     (2, (6, 6, 6), 64, 128),       # NT=4
     (1, (8, 9, 10), 1, 96),        # encoder1 on the image: generic (Cin % 16 != 0) path
     (2, (1, 33, 47), 64, 32),      # 2-D (D = 1, 9 taps)
