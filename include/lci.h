@@ -59,7 +59,7 @@ extern "C" {
  * lci_gemm_bt; 23: lci_fftconv_spectrum Dv; 24: lci_inorm_finalize; 25: lci_adam_step; 26: Hyena gate dx2 / gx2
  * in the activation dtype; 27: lci_layernorm_bwd dxb; 28: lci_resample_cl_fwd, lci_resample1d_adj_ac; 29: lci_bn_relu_*; 30: lci_gemm_bt_acc;
  * 31: lci_layernorm_bwd dres2; 32: one-chunk selective scan without end-state workspaces (xend / xinit / sdt null),
- * lci_selective_scan_bwd_plain_dbc); 33: lci_gemm_bt_small (+ _supported, _acc), lci_sum_splits, lci_conv3_wgrad_sum. */
+ * lci_selective_scan_bwd_plain_dbc); 33: lci_gemm_bt_small (+ _supported, _acc). */
 #define LCI_ABI_VERSION 33
 const char* lci_last_error(void);
 int lci_abi_version(void);
@@ -175,9 +175,6 @@ int lci_conv3_fwd_split(const void* x, const void* w, void* y, float* part, int 
  * partial sums of dy[p, n] * x[p + off(tap), c]; dW[n, c, tap] = sum over the first axis (caller). x (.., Cin),
  * dy (.., Cout) bf16 channels-last; Cin, Cout multiples of 32. Deterministic (no atomics). */
 long long lci_conv3_wgrad_splits(long long V, int Cin, int Cout, int KD);
-/* dW (Cout, Cin, T) f32 in PyTorch's Conv weight layout = the sum over splits of lci_conv3_wgrad's partials
- * part (ns, T, Cout, Cp) (Cp >= Cin: the padded input channels are dropped), in split order; T = 27 or 9. */
-int lci_conv3_wgrad_sum(const float* part, float* out, int ns, int T, int Cout, int Cp, int Cin, void* stream);
 int lci_conv3_wgrad(const void* x, const void* dy, float* part, int B, int D, int H, int W, int Cin, int Cout,
                     int KD, void* stream);
 
@@ -412,9 +409,6 @@ int lci_layernorm_bwd(const float* x, const void* dy, int bf16_dy, const float* 
  * (0: shape not supported). dW / db = sums over the first axis (caller). N, K, ldy, ldx multiples of 8, pointers
  * 16-byte aligned. Deterministic (no atomics). */
 long long lci_linear_wgrad_splits(long long M, int N, int K);
-/* out (n) f32 = part[0] + ... + part[ns - 1] (part: ns rows of n f32, summed in split order): the split partials of
- * lci_linear_wgrad (weight and bias) and lci_layernorm_bwd. part / out 16-byte aligned, n % 4 == 0 (or ns == 1). */
-int lci_sum_splits(const float* part, float* out, long long n, int ns, void* stream);
 int lci_linear_wgrad(const void* dy, long long ldy, const void* x, long long ldx, long long M, int N, int K,
                      float* part, float* dbpart, void* stream);
 /* Narrow outputs (the UNETR heads' 1x1 conv to 1-8 channels, over channels-last voxel rows): y (M, N) bf16 =

@@ -68,8 +68,6 @@ SIGNATURES = {
     "lci_gemm_bt_acc": [_P, _L, _P, _P, _L, _L, _I, _I, _P],
     "lci_gemm_bt_small": [_P, _L, _P, _P, _P, _L, _L, _I, _I, _P],
     "lci_gemm_bt_small_acc": [_P, _L, _P, _P, _L, _L, _I, _I, _P],
-    "lci_sum_splits": [_P, _P, _L, _I, _P],
-    "lci_conv3_wgrad_sum": [_P, _P, _I, _I, _I, _I, _I, _P],
     "lci_linear_small_fwd": [_P, _L, _P, _P, _P, _L, _I, _I, _P],
     "lci_linear_small_bwd": [_P, _L, _P, _P, _P, _P, _L, _I, _I, _P],
     "lci_gelu_fwd": [_P, _P, _L, _P],

@@ -1195,42 +1195,6 @@ extern "C" long long lci_conv3_wgrad_splits(long long V, int Cin, int Cout, int 
   return (V + lv - 1) / lv;
 }
 
-// dW in PyTorch's layout from the weight gradient's split partials: out[n][c][t] (Cout, Cin, T) f32 =
-// sum_s part[s][t][n][c] (part: (ns, T, Cout, Cp), Cp >= Cin, summed in split order). Before round 6 torch summed the
-// splits and then copied the (T, Cout, Cin) -> (Cout, Cin, T) permute: two passes and a transpose copy per conv. One
-// workgroup per (output channel n, 64-input-channel block): coalesced 256-B reads of the T partial rows per split, the
-// sums in LDS, and the block's Cin_blk x T outputs written as one contiguous run.
-__global__ __launch_bounds__(256) void conv3_wgrad_sum_kernel(const float* __restrict__ part, float* __restrict__ out,
-                                                              int ns, int T, int Cout, int Cp, int Cin) {
-  __shared__ float tile[27 * 64];
-  const int n = blockIdx.y, c0 = blockIdx.x * 64;
-  const int cw = min(64, Cin - c0);
-  const long long sstride = (long long)T * Cout * Cp;
-  for (int e = threadIdx.x; e < T * 64; e += 256) {
-    const int t = e >> 6, c = e & 63;
-    float acc = 0.f;
-    if (c < cw) {
-      const float* p = part + ((long long)t * Cout + n) * Cp + c0 + c;
-      acc = p[0];
-      for (int s = 1; s < ns; ++s) acc += p[(long long)s * sstride];
-    }
-    tile[t * 64 + c] = acc;
-  }
-  __syncthreads();
-  float* o = out + ((long long)n * Cin + c0) * T;
-  for (int j = threadIdx.x; j < cw * T; j += 256) o[j] = tile[(j % T) * 64 + j / T];
-}
-
-extern "C" int lci_conv3_wgrad_sum(const float* part, float* out, int ns, int T, int Cout, int Cp, int Cin,
-                                   void* stream) {
-  LCI_CHECK(part && out && ns > 0 && (T == 27 || T == 9) && Cout > 0 && Cin > 0 && Cp >= Cin,
-            "conv3_wgrad_sum: bad arguments");
-  hipLaunchKernelGGL(conv3_wgrad_sum_kernel, dim3((unsigned)((Cin + 63) / 64), (unsigned)Cout), dim3(256), 0,
-                     (hipStream_t)stream, part, out, ns, T, Cout, Cp, Cin);
-  LCI_LAUNCH_CHECK();
-  return 0;
-}
-
 extern "C" int lci_conv3_wgrad(const void* x, const void* dy, float* part, int B, int D, int H, int W, int Cin,
                                int Cout, int KD, void* stream) {
   LCI_CHECK(B > 0 && D > 0 && H > 0 && W > 0, "conv3_wgrad: bad shape");

@@ -463,36 +463,6 @@ extern "C" long long lci_linear_wgrad_splits(long long M, int N, int K) {
   return std::max(1LL, std::min(ns, (M + 255) / 256));
 }
 
-// Sum of split partials: out[i] = part[0][i] + part[1][i] + ... + part[ns-1][i] (f32, in split order: deterministic)
-// -- the weight / bias gradients' split-K partials of lci_linear_wgrad and the LayerNorm backward's block partials,
-// summed by torch's reduce kernel before round 6 (1 us of arithmetic, 10-20 us per call at 2-4 TB/s: ~1.4 ms of the C3
-// step). 16-byte loads, eight splits' loads in flight per thread before the in-order adds.
-__global__ __launch_bounds__(256) void sum_splits_kernel(const float* __restrict__ part, float* __restrict__ out,
-                                                         long long n, int ns) {
-  const long long n4 = n >> 2;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
-    f32x4 acc = ((const f32x4*)part)[i];
-#pragma unroll 8
-    for (int s = 1; s < ns; ++s) acc += ((const f32x4*)(part + (long long)s * n))[i];
-    ((f32x4*)out)[i] = acc;
-  }
-  for (long long i = (n4 << 2) + blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-    float acc = part[i];
-    for (int s = 1; s < ns; ++s) acc += part[(long long)s * n + i];
-    out[i] = acc;
-  }
-}
-
-extern "C" int lci_sum_splits(const float* part, float* out, long long n, int ns, void* stream) {
-  LCI_CHECK(n > 0 && ns > 0 && part && out, "sum_splits: bad arguments");
-  LCI_CHECK(((uintptr_t)part & 15) == 0 && ((uintptr_t)out & 15) == 0 && (n % 4 == 0 || ns == 1),
-            "sum_splits: part / out 16-byte aligned and n %% 4 == 0 (split rows 16-byte aligned)");
-  const long long blocks = std::min<long long>((n / 4 + 255) / 256 + 1, 8192);
-  hipLaunchKernelGGL(sum_splits_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, part, out, n, ns);
-  LCI_LAUNCH_CHECK();
-  return 0;
-}
-
 extern "C" int lci_linear_wgrad(const void* dy, long long ldy, const void* x, long long ldx, long long M, int N,
                                 int K, float* part, float* dbpart, void* stream) {
   LCI_CHECK(M > 0 && N > 0 && K > 0, "linear_wgrad: bad shape");

@@ -1481,10 +1481,8 @@ def conv3_wgrad_cl(x_cl: torch.Tensor, dy_cl: torch.Tensor, kd: int) -> torch.Te
     KernelTimer.run("conv3_wgrad", 2.0 * B * D * H * W * Cout * Cin * kd * 9, x_cl, lambda: _lib.call(
         "lci_conv3_wgrad", xp.data_ptr(), dy_cl.data_ptr(), part.data_ptr(), B, D, H, W, cp, Cout, kd,
         _lib.stream_of(x_cl)))
-    # (Cout, Cin, taps): the split sum and the permute to the Conv weight layout in one pass (lci_conv3_wgrad_sum)
-    g = torch.empty(Cout, Cin, kd * 9, device=x_cl.device, dtype=torch.float32)
-    _lib.call("lci_conv3_wgrad_sum", part.data_ptr(), g.data_ptr(), ns, kd * 9, Cout, cp, Cin, _lib.stream_of(x_cl))
-    return g.view(Cout, Cin, *((3, 3, 3) if kd == 3 else (3, 3)))
+    g = (part[0] if ns == 1 else part.sum(0))[..., :Cin]         # (taps, Cout, Cin)
+    return g.permute(1, 2, 0).reshape(Cout, Cin, *((3, 3, 3) if kd == 3 else (3, 3)))
 
 
 def _conv3_pack(weight: torch.Tensor, kd: int, mode: int, cin_pad: int) -> torch.Tensor:
@@ -1865,7 +1863,7 @@ def _ln_bwd(x2, weight, mean, rstd, dy, dres, shape, want_bf16=False, dres2=None
                     x2, lambda: _lib.call("lci_layernorm_bwd", x2.data_ptr(), dy.data_ptr(), int(bf), weight.data_ptr(),
                                           mean.data_ptr(), rstd.data_ptr(), _lib.ptr(dres), _lib.ptr(dres2),
                                           dx.data_ptr(), _lib.ptr(dxb), part.data_ptr(), rows, C, _lib.stream_of(x2)))
-    s = sum_splits(part)
+    s = part.sum(0)
     if want_bf16:
         return dx.view(shape), s[0], s[1], dxb.view(shape)
     return dx.view(shape), s[0], s[1]
@@ -2027,19 +2025,6 @@ def linear_wgrad_supported(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
     return _lib.load().lci_linear_wgrad_splits(M, N, K) > 0
 
 
-def sum_splits(part: torch.Tensor) -> torch.Tensor:
-    """part (ns, ...) f32 contiguous -> the sum over dim 0 in split order (lci_sum_splits); part[0] when ns == 1."""
-    ns = part.shape[0]
-    if ns == 1:
-        return part[0]
-    n = part[0].numel()
-    if n % 4 or part.data_ptr() % 16:
-        return part.sum(0)
-    out = torch.empty(part.shape[1:], device=part.device, dtype=torch.float32)
-    _lib.call("lci_sum_splits", part.data_ptr(), out.data_ptr(), n, ns, _lib.stream_of(part))
-    return out
-
-
 def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor, bias: bool):
     """dW (N, K) f32 = dy2^T x2 and db (N) f32 = column sums of dy2 (or None), by the HIP split-token kernel
     (per-split partials summed here)."""
@@ -2053,7 +2038,7 @@ def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor, bias: bool):
     KernelTimer.run("linear_wgrad", 2.0 * M * N * K, dy2, lambda: _lib.call(
         "lci_linear_wgrad", dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), M, N, K, part.data_ptr(),
         _lib.ptr(dbp), _lib.stream_of(dy2)))
-    return sum_splits(part), (sum_splits(dbp) if bias else None)
+    return part.sum(0), (dbp.sum(0) if bias else None)
 
 
 def _wgrad_tiny_k(dy2: torch.Tensor, x2: torch.Tensor, bias: bool):
