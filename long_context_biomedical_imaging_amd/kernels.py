@@ -2052,7 +2052,8 @@ def _wgrad_tiny_k(dy2: torch.Tensor, x2: torch.Tensor, bias: bool):
     KernelTimer.run("linear_wgrad_tiny", 2.0 * M * N * K, dy2, lambda: _lib.call(
         "lci_linear_small_bwd", dy2.data_ptr(), dy2.stride(0), w_unused.data_ptr(), x2.data_ptr(), None,
         part.data_ptr(), M, K, N, _lib.stream_of(dy2)))
-    dw = part[:K * N].sum(1).view(K, N).t().contiguous()   # (the parameter's strides: DDP's bucket views)
+    # the parameter's strides (DDP's bucket views); .contiguous() keeps (1, N) strides when K == 1, clone does not
+    dw = part[:K * N].sum(1).view(K, N).t().clone(memory_format=torch.contiguous_format)
     return dw, (dy2.float().sum(0) if bias else None)
 
 

@@ -5,7 +5,8 @@ bench.py uses to rehearse N ranks on fewer GPUs). Each rank trains the full Enco
 trainer.TrainStep (DDP with gradient_as_bucket_view, bf16 autocast, the HIP LciAdam update):
   * ViT-small (12 blocks, D 384, 6 heads) with the Mamba mixer, every block activation-checkpointed (C5's setting),
     ViTUNETR head on hidden states 3 / 6 / 9 (the tap aliases summed inside the LN backward kernel), 16^3 volumes;
-  * Swin-tiny + SwinUNETR, 64^3 volumes (C3's model on a smaller grid).
+  * Swin-tiny + SwinUNETR, 64^3 volumes (C3's model on a smaller grid);
+  * ViT-small with full attention + ViTUNETR on 64^2 images (the metric's model on a smaller image).
 Checks, per model:
   1. after a micro-step without update, every rank holds the same all-reduced gradient, and it is the mean of the
      gradients ONE process computes on each rank's batch separately (the all-reduce is the only difference: per
@@ -32,6 +33,10 @@ MODELS = {
                          "--height", "16", "--width", "16", "--time", "16", "--no_in_channel", "1",
                          "--no_out_channel", "2", "--ViT.size", "small", "--ViT.patch_size", "2", "2", "2",
                          "--ViT.use_mamba", "True"], True),
+    # the metric's model (bench.py vit_p2_512: ViT-small, full attention, patch 1x2x2, ViTUNETR) on a 64^2 image
+    "vit_unetr_2d": (["--encoder_name", "ViT", "--decoder_name", "ViTUNETR", "--task_type", "seg",
+                      "--height", "64", "--width", "64", "--time", "1", "--no_in_channel", "1",
+                      "--no_out_channel", "2", "--ViT.size", "small", "--ViT.patch_size", "1", "2", "2"], False),
     "swin_unetr": (["--encoder_name", "Swin", "--decoder_name", "SwinUNETR", "--task_type", "seg",
                     "--height", "64", "--width", "64", "--time", "64", "--no_in_channel", "1",
                     "--no_out_channel", "2", "--Swin.size", "tiny", "--Swin.patch_size", "2", "2", "2",
@@ -196,11 +201,12 @@ def test_ddp_two_ranks_real_model(name):
     num = sum(((g0[n] - g_ref[n]) ** 2).sum().item() for n in g_ref)
     den = sum((g_ref[n] ** 2).sum().item() for n in g_ref)
     glob = (num / den) ** 0.5
-    # bound per model: one process alone, batch of 2 against each sample separately (no DDP), differs by 1.1e-2 (Swin)
-    # and 1.0e-1 (ViT + Mamba) in rel-L2 under bf16 autocast, 5.5e-4 / 2.4e-3 in fp32 (tools/r6_batch_coupling.py,
-    # profiles/r06_batch_coupling.txt): the GEMMs' batch-size-dependent tilings round differently, the forward
-    # outputs differ by ~1 %, and the gradients amplify that; check 1 is the DDP-specific one
-    tol = {"swin_unetr": 2e-2, "vit_mamba_unetr": 0.2}[name]
+    # bound per model: one process alone, batch of 2 against each sample separately (no DDP), differs by 1.1e-2 (Swin),
+    # 1.0e-1 (ViT + Mamba) and 8.0e-2 (ViT) in rel-L2 under bf16 autocast, and by 5.5e-4 / 2.4e-3 / 2.5e-5 in fp32
+    # (tools/r6_batch_coupling.py, profiles/r06_batch_coupling.txt): at these small sizes the projections run on
+    # hipBLASLt, whose kernel choice depends on the row count, the forward outputs then differ by ~1 %, and the
+    # gradients amplify that; check 1 is the DDP-specific one
+    tol = {"swin_unetr": 2e-2, "vit_mamba_unetr": 0.2, "vit_unetr_2d": 0.15}[name]
     assert glob <= tol, f"DDP gradient vs one process on the concatenated batch: rel-L2 {glob:.3e}"
     lr = 1e-4
     for n in w_ref:
