@@ -188,7 +188,32 @@ template <int OFF>
 __device__ __forceinline__ void hs_st4(unsigned addr, uint32_t v) {
   asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(addr), "a"(v), "i"(OFF) : "memory");
 }
+// Row constants of the next half by DPP (LCI_DKDV_DPPRC=1): one ds_read_b32 per constant row set (lane l holds the
+// constant of register l & 15 of its half-wave) and 16 v_mov_b32_dpp row_newbcast:i per set, instead of eight
+// broadcast 16-byte reads per half (a quarter of the kernel's LDS return bytes); the sets alternate with the halves.
+// Measured 0.4 % slower (profiles/r06_dkdv_dpp_ab.txt: LDS return bytes do not limit the kernel, the 32 movs cost
+// VALU issue), so it stays off; parity-tested on the GPU all the same
+#ifndef LCI_DKDV_DPPRC
+#define LCI_DKDV_DPPRC 0
+#endif
+template <int I>
+__device__ __forceinline__ float hs_bcast(float x) {   // lane I of each 16-lane row, to the whole row
+  float d;
+  asm volatile("v_mov_b32_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "=v"(d) : "v"(x), "i"(I));
+  return d;
+}
+__device__ __forceinline__ float hs_bcast_i(float x, int i) {   // (i compile-time after unrolling)
+  switch (i & 15) {
+    case 0: return hs_bcast<0>(x); case 1: return hs_bcast<1>(x); case 2: return hs_bcast<2>(x);
+    case 3: return hs_bcast<3>(x); case 4: return hs_bcast<4>(x); case 5: return hs_bcast<5>(x);
+    case 6: return hs_bcast<6>(x); case 7: return hs_bcast<7>(x); case 8: return hs_bcast<8>(x);
+    case 9: return hs_bcast<9>(x); case 10: return hs_bcast<10>(x); case 11: return hs_bcast<11>(x);
+    case 12: return hs_bcast<12>(x); case 13: return hs_bcast<13>(x); case 14: return hs_bcast<14>(x);
+    default: return hs_bcast<15>(x);
+  }
+}
 __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArgs a) {
+  constexpr bool DPPRC = LCI_DKDV_DPPRC != 0;
   constexpr int TILE_B = KT * DH * 2;               // bytes of a Q or dO tile (128-B rows)
   constexpr int SLOT_B = 2 * TILE_B;                // Q | dO of one tile
   constexpr int RC_B = 2 * KT * 4;                  // -lse2[64] | -delta[64] of one tile
@@ -286,6 +311,9 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
     }
   rc_off = NSLOT * SLOT_B + 16 * h;   // (past the 64-KB ring: in the register, the rest is an immediate)
   HS_OPAQUE(rc_off);
+  // DPPRC: lane l reads the constant of query (l & 3) + 8 ((l >> 2) & 3) + 4h, register l & 15's row
+  unsigned rcx_off = NSLOT * SLOT_B + 4 * ((lane & 3) + 8 * ((lane >> 2) & 3) + 4 * h);
+  HS_OPAQUE(rcx_off);
   // soff: byte offset of the tile in the ring (slot, + TILE_B for dO); r0: the half's first query row in the tile
   auto qrow = [&](int soff, int r0, int ks) __attribute__((always_inline)) {
     return *(const bf16x8*)(smem + q_off[ks] + (soff + 2 * DH * r0));
@@ -308,7 +336,8 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
 
   f32x16 dv[2][2], dk[2][2];   // [d block][key block]: dV^T / dK^T, lane = key, rows d = 32db + (i&3) + 8(i>>2) + 4h
   f32x16 S[2], P[2];           // [key block]: S~ - lse2 and dP - delta of the block's current half
-  f32x16 NL, ND;               // row constants (-lse2, -delta) of the chains' half
+  f32x16 NLs[2], NDs[2];       // row constants (-lse2, -delta) of the chains' half ([half parity] with DPPRC, else [0])
+  float xNL = 0.f, xND = 0.f;  // DPPRC: the next half's constants, one per lane
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     S[i] = P[i] = f32x16{};
@@ -357,10 +386,10 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
     }
   };
   // MFMA of gap g of a chain segment (S chain at gaps 0-3, dP chain at gaps 4-7) for key block kb
-  auto chain_gap = [&](int g, int kb) __attribute__((always_inline)) {
-    if (g == 0) HS_MFMA_C0(S[kb], qa[0], kf[kb][0], NL);
+  auto chain_gap = [&](int g, int kb, int st) __attribute__((always_inline)) {
+    if (g == 0) HS_MFMA_C0(S[kb], qa[0], kf[kb][0], NLs[st]);
     else if (g < 4) HS_MFMA_C(S[kb], qa[g], kf[kb][g]);
-    else if (g == 4) HS_MFMA_C0(P[kb], da[0], vf[kb][0], ND);
+    else if (g == 4) HS_MFMA_C0(P[kb], da[0], vf[kb][0], NDs[st]);
     else HS_MFMA_C(P[kb], da[g - 4], vf[kb][g - 4]);
   };
   // MFMA of gap g of a gradient segment for key block kb with fragment set st: (k-step s2, d block db, dV | dK)
@@ -383,6 +412,20 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
     const f32x4 v = *(const f32x4*)(smem + rc_off + (rcoff + which * KT * 4 + 4 * (r0 + 8 * g)));
     r[4 * g] = v[0]; r[4 * g + 1] = v[1]; r[4 * g + 2] = v[2]; r[4 * g + 3] = v[3];
   };
+  // DPPRC: one lane-mapped constant per lane, and mov k (0-31: -lse2 registers 0-15, then -delta's) of set st
+  auto rcx_load = [&](int rcoff, int which, int r0) __attribute__((always_inline)) {
+    return *(const float*)(smem + rcx_off + (rcoff + which * KT * 4 + 4 * r0));
+  };
+  auto bc_mov = [&](int k, int st) __attribute__((always_inline)) {
+    if (k < 16) NLs[st][k] = hs_bcast_i(xNL, k);
+    else NDs[st][k - 16] = hs_bcast_i(xND, k - 16);
+  };
+  // the 32 movs over the 19 gaps seg B 5-7, seg C 0-7, seg D 0-7 (j = 0-18): two per gap for j < 13, then one
+  // (<= 2 x 4 issue cycles beside the gap's 16 of exp2 / multiply / conversion)
+  auto bc_gap = [&](int j, int st) __attribute__((always_inline)) {
+    if (j < 13) { bc_mov(2 * j, st); bc_mov(2 * j + 1, st); }
+    else bc_mov(13 + j, st);
+  };
 
   // One half-tile p = rows r0 of `slot` (fragment set C = p & 1); segs C / D read half p+1 = rows nr0 of `nslot`.
   // LDS reads, one per gap, each placed at least two gaps after the last MFMA read of the registers it refills
@@ -393,10 +436,11 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
   auto half = [&](auto CUR, int slot, int r0, int nslot, int nrc, int nr0, auto mid, auto sgap)
       __attribute__((always_inline)) {
     constexpr int C = decltype(CUR)::value;
+    constexpr int ST = DPPRC ? C : 0, NST = DPPRC ? C ^ 1 : 0;   // row-constant sets of this / the next half
     // seg A: chains kb0 || VALU kb1 (p-1) elements 8-15 (finishing its elements 0-7)
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
-      chain_gap(g, 0);
+      chain_gap(g, 0, ST);
       valu_gap(g, 1, 1, 1, 0);
       if (!(g & 1)) tr_load(g >> 1, C, slot, r0);
       sgap(0, g);
@@ -408,18 +452,24 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
       grad_gap(g, 1, C ^ 1);
       valu_gap(g, 0, 0, 1, 1);
       if (!(g & 1)) tr_load(4 + (g >> 1), C, slot, r0);
+      if (DPPRC) {   // the next half's rows are readable here (half 1: published by mid()'s barrier)
+        if (g == 1) xNL = rcx_load(nrc, 0, nr0);
+        if (g == 3) xND = rcx_load(nrc, 1, nr0);
+        if (g >= 5) bc_gap(g - 5, NST);
+      }
       sgap(1, g);
     }
     // seg C: chains kb1 || VALU kb0 elements 8-15
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
-      chain_gap(g, 1);
+      chain_gap(g, 1, ST);
       valu_gap(g, 0, 1, 0, 0);
-      if (g == 2) HS_KEEP(NL);
-      if (g == 6) HS_KEEP(ND);
+      if (g == 2) HS_KEEP(NLs[ST]);
+      if (g == 6) HS_KEEP(NDs[ST]);
+      if (DPPRC) bc_gap(3 + g, NST);
       if (g >= 2 && g < 6) qa[g - 2] = qrow(nslot, nr0, g - 2);
       if (g >= 6) {
-        rc_load(NL, nrc, 0, nr0, g - 6);
+        if (!DPPRC) rc_load(NLs[0], nrc, 0, nr0, g - 6);
         da[g - 6] = qrow(nslot + TILE_B, nr0, g - 6);
       }
       sgap(2, g);
@@ -429,8 +479,9 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
     for (int g = 0; g < 8; ++g) {
       grad_gap(g, 0, C);
       valu_gap(g, 1, 0, 0, 1);
-      if (g < 2) rc_load(NL, nrc, 0, nr0, g + 2);
-      else if (g < 6) rc_load(ND, nrc, 1, nr0, g - 2);
+      if (DPPRC) bc_gap(11 + g, NST);
+      if (g < 2) { if (!DPPRC) rc_load(NLs[0], nrc, 0, nr0, g + 2); }
+      else if (g < 6) { if (!DPPRC) rc_load(NDs[0], nrc, 1, nr0, g - 2); }
       else da[g - 4] = qrow(nslot + TILE_B, nr0, g - 4);
       sgap(3, g);
     }
@@ -455,8 +506,8 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
   ld_piece(1, 0); ld_piece(1, 1); ld_piece(1, 2); ld_piece(1, 3); ld_piece(1, 4);
   hs_vmcnt<0>();
   __syncthreads();
-  NL = rcblk(rcs, 0, 0);
-  ND = rcblk(rcs, 1, 0);
+  NLs[0] = rcblk(rcs, 0, 0);
+  NDs[0] = rcblk(rcs, 1, 0);
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
     qa[ks] = qrow(0, 0, ks);
