@@ -14,6 +14,7 @@
 // consecutive output channels per register quad, so the bf16 results go out as 8-byte stores.
 // Neighbour reuse (27 taps read the same voxels) is served by L1/L2: the volume is swept in voxel order.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.hpp"
 
@@ -1006,6 +1007,154 @@ static int launch_wgrad5(WgradArgs a, hipStream_t st) {
   return 0;
 }
 
+// Weight gradient v6 (round 6): v5's (1, 3, WC) tiles (the Swin channel counts: C3) with the staging done by LDS-DMA
+// into three LDS buffers. Step k+2's rows land while step k computes, so two steps of rows are in flight per
+// workgroup where v5 had one (v5 stalls on each step's register-staged loads: MFMA busy 0.31 at C3,
+// profiles/r06_pmc.txt), and no VGPRs hold staged rows. A 1-KB DMA unit is 16 rows x 64 B of one 32-channel block
+// (lane l: row l >> 2, 16-B chunk l & 3); a step is 24 dy units (3 blocks x 128 rows) then 9 WC x units (WC blocks x
+// 144 rows: the 130 a step reads, rounded up to whole units), unit u at LDS byte 1024 u of its buffer. Rows that do not
+// exist (gap rows, taps outside the volume, rows past the split) are lanes with an out-of-range offset: the DMA writes
+// them as zeros. Every wave issues S operations per step (spare slots repeat the last unit: the same bytes to the same
+// place), so one vmcnt immediate waits for exactly the step before the newest.
+// Measured (profiles/r06_wgrad_dma_ab.txt): 1.75 -> 1.655 ms at C3 128^3 96 -> 96, 3.03 -> 2.91 ms at 192 -> 96 (4-6 %).
+constexpr int W6_XR = 144;
+template <int WC>
+constexpr int w6_buf() { return 3 * WG_ROWS * 64 + WC * W6_XR * 64; }
+template <int WC>
+constexpr size_t wgrad6_lds() { return (size_t)3 * w6_buf<WC>(); }
+
+template <int WC>
+__global__ __launch_bounds__(64 * 3 * WC) void conv3_wgrad6_kernel(WgradArgs a) {
+  constexpr int NW = 3 * WC, U = 24 + 9 * WC, S = (U + NW - 1) / NW, BUFB = w6_buf<WC>();
+  extern __shared__ __attribute__((aligned(16))) bf16 wsm[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int wn = wave / WC, wc = wave % WC;
+  // work decode (XCD-contiguous, as v5)
+  const int G = a.KD * 3, NT = a.Cout / 96, NC = a.Cin / (32 * WC);
+  long long w;
+  {
+    const long long per = ((long long)a.nb + 7) / 8;
+    w = (long long)(blockIdx.x % 8) * per + blockIdx.x / 8;
+  }
+  if (w >= a.nb) return;
+  const int ct = (int)(w % NC);
+  long long q = w / NC;
+  const int grp = (int)(q % G);
+  q /= G;
+  const int nt = (int)(q % NT), split = (int)(q / NT);
+  const int n0 = nt * 96, c0 = ct * 32 * WC;
+  const int T = a.KD * 9;
+  const int dz = (a.KD == 3 ? grp / 3 : 1) - 1, dyy = grp % 3 - 1;
+  const int HW = a.H * a.W, W1 = a.W + 1;
+  const long long lines = a.V / a.W, R = lines * W1;
+  const int shift = dz * HW + dyy * a.W;
+  const long long gs = (long long)split * a.Lv, ge = min(R, gs + a.Lv);
+  const int q128 = WG_ROWS / W1, r128 = WG_ROWS % W1;
+  const rsrc_t rdy = make_rsrc(a.dy, (uint32_t)(a.V * a.Cout * 2));
+  const rsrc_t rx = make_rsrc(a.x, (uint32_t)(a.V * a.Cin * 2));
+  const unsigned lds0 = (unsigned)(uintptr_t)(LCI_LDS bf16*)wsm;
+  const int lrow = lane >> 2, lch = lane & 3;
+
+  f32x16 acc[3];
+#pragma unroll
+  for (int d = 0; d < 3; ++d)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[d][i] = 0.f;
+
+  // slot i: unit u (wave-uniform), its row base in the step and the lane's channel byte offset; the lane's row walker
+  GRow gr[S];
+  int urow[S], ucb[S], uu[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    const int u = min(wave + NW * i, U - 1);
+    uu[i] = u;
+    const bool isx = u >= 24;
+    const int b = isx ? (u - 24) / 9 : u / 8;
+    urow[i] = isx ? 16 * ((u - 24) % 9) : 16 * (u % 8);
+    ucb[i] = 2 * ((isx ? c0 : n0) + 32 * b + 8 * lch);
+    gr[i].init(gs + urow[i] + lrow - (isx ? 1 : 0), W1, a.H, a.D);
+  }
+  // this wave's S units of the step whose first gapped row is g0, into buffer p
+  auto issue = [&](long long g0, int p) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      const bool isx = uu[i] >= 24;
+      const GRow& g = gr[i];
+      bool ok;
+      int vox;
+      if (isx) {
+        const long long Gr = g0 - 1 + urow[i] + lrow;
+        ok = Gr >= 0 && Gr < R && g.X < a.W && (unsigned)(g.z + dz) < (unsigned)a.D &&
+             (unsigned)(g.y + dyy) < (unsigned)a.H;
+        vox = g.L * a.W + g.X + shift;
+      } else {
+        ok = g0 + urow[i] + lrow < ge && g.X < a.W;
+        vox = g.L * a.W + g.X;
+      }
+      const int voff = ok ? vox * (isx ? a.Cin : a.Cout) * 2 + ucb[i] : 0x7FFFFFF0;
+      dma16_lds(isx ? rx : rdy, voff, 0, lds0 + (unsigned)(p * BUFB + 1024 * uu[i]));
+      gr[i].advance(q128, r128, W1, a.H, a.D);
+    }
+  };
+  const int nsteps = (int)((ge - gs + WG_ROWS - 1) / WG_ROWS);
+  issue(gs, 0);
+  if (nsteps > 1) issue(gs + WG_ROWS, 1);
+  int p = 0;
+  for (int k = 0; k < nsteps; ++k) {
+    if (k + 1 < nsteps) wait_vmcnt<S>();   // this wave's units of step k landed (step k+1's may be in flight)
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_waitcnt(0xC07F);     // lgkmcnt(0): this wave's reads of step k-1's buffer are done
+    __builtin_amdgcn_s_barrier();           // every wave's units of step k landed; step k-1's buffer is free
+    if (k + 2 < nsteps) issue(gs + (long long)(k + 2) * WG_ROWS, p == 0 ? 2 : p - 1);
+    const bf16* tdy0 = (const bf16*)((const char*)wsm + p * BUFB) + wn * WG_ROWS * 32;
+    const bf16* tx = (const bf16*)((const char*)wsm + p * BUFB) + 3 * WG_ROWS * 32 + wc * W6_XR * 32;
+#pragma unroll
+    for (int r0 = 0; r0 < WG_ROWS; r0 += 32) {
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        const bf16x8 fa0 = sub ? frag_tr<1>(tdy0, 32, r0, 0, lane) : frag_tr<0>(tdy0, 32, r0, 0, lane);
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+          const bf16x8 fb = sub ? frag_tr<1>(tx, 32, r0 + d, 0, lane) : frag_tr<0>(tx, 32, r0 + d, 0, lane);
+          acc[d] = mfma32(fa0, fb, acc[d]);
+        }
+      }
+    }
+    p = p == 2 ? 0 : p + 1;
+  }
+  // acc[d] reg i: n = n0 + 32 wn + (i&3) + 8(i>>2) + 4h, c = c0 + 32 wc + (lane & 31)
+  const int h = lane >> 5;
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    float* out = a.part + ((long long)split * T + grp * 3 + d) * a.Cout * a.Cin;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int row = n0 + 32 * wn + (i & 3) + 8 * (i >> 2) + 4 * h;
+      out[(long long)row * a.Cin + c0 + 32 * wc + (lane & 31)] = acc[d][i];
+    }
+  }
+}
+
+template <int WC>
+static int launch_wgrad6(WgradArgs a, hipStream_t st) {
+  const size_t sh = wgrad6_lds<WC>();
+  const long long nb = (long long)a.KD * 3 * a.ns * (a.Cout / 96) * (a.Cin / (32 * WC));
+  LCI_CHECK(nb < (1LL << 30), "conv3_wgrad: too many workgroups");
+  a.nb = (int)nb;
+  (void)hipFuncSetAttribute((const void*)conv3_wgrad6_kernel<WC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024);
+  hipLaunchKernelGGL((conv3_wgrad6_kernel<WC>), dim3((unsigned)((nb + 7) / 8 * 8)), dim3(64 * 3 * WC), sh, st, a);
+  LCI_LAUNCH_CHECK();
+  return 0;
+}
+// v6 takes v5's (1, 3, WC) shapes whose operands a 32-bit DMA offset reaches; LCI_WGRAD_DMA=0 keeps them on v5 (A/B)
+static bool wgrad6_ok(const WgradArgs& a) {
+  const char* e = getenv("LCI_WGRAD_DMA");   // (read per call: the tests compare v6 with v5 in one process)
+  const bool on = !(e && e[0] == '0');
+  return on && a.V * a.Cin * 2 <= 0x7FFFFF00LL && a.V * a.Cout * 2 <= 0x7FFFFF00LL;
+}
+
 // (MB, WN, WC) of the v5 weight gradient, or MB = 0 when the v4 kernel handles the shape. Measured
 // (tools/conv_bench.py): the 8-wave (2, 2, 4) tile 1.6-1.8x over v4 (C5 512->256: 228 -> 128 ms); a 4-wave
 // (1, 1, 4) tile was 5-10 % slower than v4, so v5 needs >= 6 waves: Cout % 128 -> (2, 2, 4 or 2); the Swin
@@ -1219,6 +1368,7 @@ extern "C" int lci_conv3_wgrad(const void* x, const void* dy, float* part, int B
   wgrad5_tile(Cin, Cout, mb, wn, wc);
   if (mb) {
 #define LCI_W5(M, N, C) if (mb == M && wn == N && wc == C) return launch_wgrad5<M, N, C>(a, st);
+    if (mb == 1 && wgrad6_ok(a)) return wc == 3 ? launch_wgrad6<3>(a, st) : launch_wgrad6<2>(a, st);
     LCI_W5(2, 2, 4) LCI_W5(2, 2, 2) LCI_W5(1, 3, 3) LCI_W5(1, 3, 2)
 #undef LCI_W5
   }

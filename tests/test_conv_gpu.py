@@ -196,3 +196,36 @@ def test_unet_resblock_fused_tail_bit_exact(nd, S, cin, cout, monkeypatch):
         outs.append((y.detach(), xi.grad, blk.conv1.conv.weight.grad, blk.conv2.conv.weight.grad))
     for name, a, b in zip(("y", "dx", "dW1", "dW2"), outs[0], outs[1]):
         assert torch.equal(a, b), name
+
+
+@pytest.mark.parametrize("B,S,Cin,Cout", [
+    (1, (32, 32, 32), 96, 96),     # C3 stage-2 channels, many 128-row steps per split
+    (2, (9, 7, 13), 192, 96),      # ragged lines (gap rows mid-step), two samples, Cin % 96
+    (1, (12, 11, 10), 64, 192),    # the (1, 3, 2) tile (Cin % 64)
+    (1, (1, 70, 50), 96, 96),      # 2-D (9 taps)
+])
+def test_conv3_wgrad_dma_vs_register_staging(B, S, Cin, Cout, monkeypatch):
+    """Weight gradient v6 (LDS-DMA staging, three buffers; the default for the (1, 3, WC) tiles) against v5 (register
+    staging, LCI_WGRAD_DMA=0): the same MFMA sequence over the same staged rows, so bitwise equal; and against the
+    fp64 product over the same bf16 operands (f32 accumulation bound)."""
+    torch.manual_seed(3)
+    kd = 1 if S[0] == 1 else 3
+    x = torch.randn(B, *S, Cin, device="cuda").bfloat16()
+    dy = torch.randn(B, *S, Cout, device="cuda").bfloat16()
+    g6 = kernels.conv3_wgrad_cl(x, dy, kd)
+    monkeypatch.setenv("LCI_WGRAD_DMA", "0")
+    g5 = kernels.conv3_wgrad_cl(x, dy, kd)
+    monkeypatch.delenv("LCI_WGRAD_DMA")
+    assert torch.equal(g6, g5)
+    nd = 2 if kd == 1 else 3
+    xs = x.double().movedim(-1, 1)
+    dys = dy.double().movedim(-1, 1)
+    if nd == 2:
+        xs, dys = xs[:, :, 0], dys[:, :, 0]
+    wr = torch.zeros(Cout, Cin, *(3,) * nd, dtype=torch.float64, device="cuda", requires_grad=True)
+    conv = F.conv3d if nd == 3 else F.conv2d
+    (conv(xs, wr, padding=1) * dys).sum().backward()
+    ref = wr.grad.reshape(g6.shape)
+    err = (g6.double() - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    assert err <= 1e-4 * scale + 1e-6, f"max err {err:.3e} (max |ref| {scale:.3e})"
