@@ -607,6 +607,20 @@ __global__ __launch_bounds__(NW * 64) void win_attn_bwd_kernel(WinArgs a) {
 // dQ, 16 exp2), and dQ^T += K^T dS^T with dS transposed through a per-wave LDS scratch tile, added into an f32 dQ
 // accumulator in LDS that this wave owns for the step (one barrier per step; the summation order is fixed by the
 // rotation: deterministic). Q / dO are staged once; delta = rowsum(dO * O) is computed at staging.
+// The per-wave scratch tile (K^T once, then dS^T every step; 8-byte stores, transposed reads): 64-byte rows, the
+// 8-byte chunk c of row r at c ^ ((r >> 1) & 7) -- conflict-free for both (with 80-byte rows the stores took 4 extra
+// LDS cycles and the reads 2, profiles/r06_pmc.txt). Its rows always start at 0, so the swizzled lane offsets are
+// loop-invariant registers.
+constexpr int SLD = 32;
+__device__ __forceinline__ int ssw(int row, int col) {
+  return row * SLD + ((((col >> 2) ^ (row >> 1)) & 7) << 2) + (col & 3);
+}
+template <int S>
+__device__ __forceinline__ bf16x8 sfrag_tr(const bf16* t, int lane) {   // frag_tr<S>(t, ld, 0, 0, lane) on it
+  const int row = 16 * S + 4 * (lane >> 5) + ((lane & 15) >> 2);
+  const int col = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+  return cat44(lds_tr4(t + ssw(row, col)), lds_tr4(t + ssw(row + 8, col)));
+}
 constexpr int DQLD = 36;   // f32 row stride of the LDS dQ accumulator: the b128 RMW of 16 query rows is conflict-free
 constexpr int WBWD1_MAXW = 12;
 // Phase timestamps of the single-phase backward (variant builds only, -DLCI_WIN_STAMPS: tools/r6_win_stamps.py):
@@ -639,7 +653,7 @@ __global__ __launch_bounds__(WBWD1_MAXW * 64) void win_attn_bwd1_kernel(WinArgs 
   float* lse_l = (float*)(L.rid + a.Npad);                   // -lse2
   float* ndl_l = lse_l + a.Npad;                             // -delta
   float* dq_l = ndl_l + a.Npad;                              // (Npad, DQLD) f32
-  bf16* scr = (bf16*)(dq_l + a.Npad * DQLD) + wave * 32 * WLD;   // this wave's 32 x 32 transpose tile
+  bf16* scr = (bf16*)(dq_l + a.Npad * DQLD) + wave * 32 * SLD;   // this wave's 32 x 32 transpose tile
   const float c = a.c;
 
   // Prologue: every global read of the window issued at once, then consumed -- Q and dO rows (-> t0, t1), the O rows
@@ -684,20 +698,22 @@ __global__ __launch_bounds__(WBWD1_MAXW * 64) void win_attn_bwd1_kernel(WinArgs 
     }
   }
   for (int i = threadIdx.x; i < a.Npad * DQLD / 4; i += NT) ((f32x4*)dq_l)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  int* cnt = (int*)((bf16*)(dq_l + a.Npad * DQLD) + nkb * 32 * WLD);   // dQ contributions added per query tile
+  int* cnt = (int*)((bf16*)(dq_l + a.Npad * DQLD) + nkb * 32 * SLD);   // dQ contributions added per query tile
   if (threadIdx.x < nkb) cnt[threadIdx.x] = 0;
 
   // this wave's key block: K (prescaled into the exp2 domain) / V as B operands, raw K^T as the dQ A operand
   bf16x8 kf[2], vf[2];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
-    *(bf16x8*)(scr + (lane & 31) * WLD + ks * 16 + 8 * half) = kr[ks];
+    const bf16x8 kk = kr[ks];
+    *(bf16x4*)(scr + ssw(lane & 31, ks * 16 + 8 * half)) = bf16x4{kk[0], kk[1], kk[2], kk[3]};
+    *(bf16x4*)(scr + ssw(lane & 31, ks * 16 + 8 * half + 4)) = bf16x4{kk[4], kk[5], kk[6], kk[7]};
     kf[ks] = scaled8(kr[ks], c);
     vf[ks] = vr[ks];
   }
   __syncthreads();   // staging, row constants, dQ zero, K scratch
   WSTAMP(2);
-  const bf16x8 kt0 = frag_tr<0>(scr, WLD, 0, 0, lane), kt1 = frag_tr<1>(scr, WLD, 0, 0, lane);
+  const bf16x8 kt0 = sfrag_tr<0>(scr, lane), kt1 = sfrag_tr<1>(scr, lane);
   __builtin_amdgcn_wave_barrier();   // K^T read before the scratch takes dS tiles
 
   const long long tho = ((long long)win_type(a, w) * a.H + hh) * a.Npad * a.Npad;
@@ -800,16 +816,16 @@ __global__ __launch_bounds__(WBWD1_MAXW * 64) void win_attn_bwd1_kernel(WinArgs 
       *(bf16x8*)(dst + 8) = d1;
     }
     // dS^T through the scratch tile [key][query]: register r of this lane is query (r&3) + 8(r>>2) + 4h
-    bf16* srow = scr + (lane & 31) * WLD + 4 * half;
-    *(bf16x4*)(srow + 0) = bf16x4{d0[0], d0[1], d0[2], d0[3]};
-    *(bf16x4*)(srow + 8) = bf16x4{d0[4], d0[5], d0[6], d0[7]};
-    *(bf16x4*)(srow + 16) = bf16x4{d1[0], d1[1], d1[2], d1[3]};
-    *(bf16x4*)(srow + 24) = bf16x4{d1[4], d1[5], d1[6], d1[7]};
+    const int sr = lane & 31;
+    *(bf16x4*)(scr + ssw(sr, 4 * half)) = bf16x4{d0[0], d0[1], d0[2], d0[3]};
+    *(bf16x4*)(scr + ssw(sr, 4 * half + 8)) = bf16x4{d0[4], d0[5], d0[6], d0[7]};
+    *(bf16x4*)(scr + ssw(sr, 4 * half + 16)) = bf16x4{d1[0], d1[1], d1[2], d1[3]};
+    *(bf16x4*)(scr + ssw(sr, 4 * half + 24)) = bf16x4{d1[4], d1[5], d1[6], d1[7]};
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    dq_prev = mfma32(kt0, frag_tr<0>(scr, WLD, 0, 0, lane), f32x16{});
-    dq_prev = mfma32(kt1, frag_tr<1>(scr, WLD, 0, 0, lane), dq_prev);   // dQ^T[d][query], query on the lane
+    dq_prev = mfma32(kt0, sfrag_tr<0>(scr, lane), f32x16{});
+    dq_prev = mfma32(kt1, sfrag_tr<1>(scr, lane), dq_prev);   // dQ^T[d][query], query on the lane
     qt_prev = qt;
     qt = qn;
     if (t + 1 < nkb) {
@@ -862,7 +878,7 @@ __global__ __launch_bounds__(WBWD1_MAXW * 64) void win_attn_bwd1_kernel(WinArgs 
     __syncthreads();
     if (threadIdx.x < 64) {
       float acc = 0.f;
-      for (int v = 0; v < nkb; ++v) acc += ((const float*)(scr - wave * 32 * WLD + v * 32 * WLD))[threadIdx.x];
+      for (int v = 0; v < nkb; ++v) acc += ((const float*)(scr - wave * 32 * SLD + v * 32 * SLD))[threadIdx.x];
       a.pad_ws[((long long)w * a.H + hh) * 64 + threadIdx.x] = acc;
     }
   } else if (__any(padk)) {
@@ -1118,7 +1134,7 @@ extern "C" int lci_window_attn_bwd(const void* qkv, const float* qkv_bias, const
     static const int cnt_env = getenv("LCI_WIN_BWD1_CNT") ? atoi(getenv("LCI_WIN_BWD1_CNT")) : 1;
     a.bwd1_cnt = cnt_env;
     const size_t lds = WBIAS_B + (size_t)a.Npad * WLD * 2 * 2 + (size_t)a.Npad * 4 * 4 + (size_t)a.Npad * DQLD * 4 +
-                       (size_t)a.nkt * 32 * WLD * 2 + 64;
+                       (size_t)a.nkt * 32 * SLD * 2 + 64;
     LCI_CHECK(lds <= 160 * 1024, "window_attn_bwd: %zu B of LDS", lds);
     (void)hipFuncSetAttribute((const void*)win_attn_bwd1_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
