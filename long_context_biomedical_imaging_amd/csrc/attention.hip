@@ -1022,6 +1022,11 @@ __host__ __device__ constexpr bool fw_wrapped_exp(int i) {
   return false;
 }
 
+// Timing probes (variant builds only; results are wrong): LCI_FWD_PROBE bit 0 drops the per-tile barrier, bit 1 the
+// wait for tile t+1's staging loads -- what the two synchronisation points of the stream cost
+#ifndef LCI_FWD_PROBE
+#define LCI_FWD_PROBE 0
+#endif
 __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, const float* knorm) {
   constexpr int TILE_B = KT * DH * 2;               // bytes of a K or V tile (128-B rows)
   constexpr int SLOT_B = 2 * TILE_B;                // K | V
@@ -1364,11 +1369,11 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_fwd_hs_kernel(AttnArgs a, 
     const int nsoff = sl >= 0 ? ((sl + 1) & (NSLOT - 1)) * SLOT_B : ((t + 1) & (NSLOT - 1)) * SLOT_B;
     // tile t+1 is published at gap 6 of half 1 (first reader: the K rows at gaps 12-15)
     auto stage = [&](int g) __attribute__((always_inline)) {
-      if (t + 1 < nkt && g == 7) __builtin_amdgcn_s_barrier();
+      if (!(LCI_FWD_PROBE & 1) && t + 1 < nkt && g == 7) __builtin_amdgcn_s_barrier();
     };
     constexpr int LD0 = 11;   // tile t+2's loads at gaps 11, 13, 15, 17 (32x32x16 gaps)
     auto rstg = [&](int g) __attribute__((always_inline)) {
-      if (g == 1) hs_vmcnt<0>();   // tile t+1's pieces (loaded a tile ago)
+      if (!(LCI_FWD_PROBE & 2) && g == 1) hs_vmcnt<0>();   // tile t+1's pieces (loaded a tile ago)
       if (g < 8 && (g & 1)) {
         constexpr int S1 = sl >= 0 ? ((sl + 1) & (NSLOT - 1)) * SLOT_B : 0;
         const unsigned base = sl >= 0 ? wst : wst + (unsigned)(((t + 1) & (NSLOT - 1)) * SLOT_B);
