@@ -193,6 +193,11 @@ __device__ __forceinline__ void hs_st4(unsigned addr, uint32_t v) {
 // broadcast 16-byte reads per half (a quarter of the kernel's LDS return bytes); the sets alternate with the halves.
 // Measured 0.4 % slower (profiles/r06_dkdv_dpp_ab.txt: LDS return bytes do not limit the kernel, the 32 movs cost
 // VALU issue), so it stays off; parity-tested on the GPU all the same
+// Timing probes as LCI_FWD_PROBE (variant builds only; results are wrong): bit 0 drops the per-tile barrier, bit 1 the
+// wait for tile t+1's staging loads
+#ifndef LCI_DKDV_PROBE
+#define LCI_DKDV_PROBE 0
+#endif
 #ifndef LCI_DKDV_DPPRC
 #define LCI_DKDV_DPPRC 0
 #endif
@@ -525,14 +530,14 @@ __global__ __launch_bounds__(HS_NW * 64, 1) void attn_bwd_dkdv_hs_kernel(AttnArg
     // tile t+1 (stored from registers in half 0) is published after seg A of half 1 (seg C of half 1 is its first
     // reader): one barrier; no LDS fence: the stores were ordered by the waits of this wave's own later reads
     auto stage = [&]() __attribute__((always_inline)) {
-      if (t + 1 < nqt) __builtin_amdgcn_s_barrier();
+      if (!(LCI_DKDV_PROBE & 1) && t + 1 < nqt) __builtin_amdgcn_s_barrier();
     };
     // half 0: tile t+1's pieces (loaded a tile ago) stored at seg A gaps 1-7 and seg B gap 1... (SS = 0), tile t+2's
     // loaded at seg C gaps 1-7 (LS = 2)
     auto rstg0 = [&](int seg, int g) __attribute__((always_inline)) {
       if (!(g & 1)) return;
       constexpr int SS = 0, LS = 2;   // store / load segments of half 0
-      if (seg == SS && g == 1) hs_vmcnt<0>();   // tile t+1's pieces (loaded a tile ago)
+      if (!(LCI_DKDV_PROBE & 2) && seg == SS && g == 1) hs_vmcnt<0>();   // tile t+1's pieces (loaded a tile ago)
       constexpr int S1 = SLC >= 0 ? ((SLC + 1) & (NSLOT - 1)) * SLOT_B : 0;
       constexpr int R1 = SLC >= 0 ? ((SLC + 1) & (NSLOT - 1)) * RC_B : 0;
       const unsigned base = SLC >= 0 ? wst : wst + (unsigned)nslot;
