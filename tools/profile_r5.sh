@@ -4,7 +4,8 @@
 #   2. C3 (swin_p2_128) eager (LCI_GRAPH=0: rocprofv3 --pmc aborts on graph replays, tools/graph_pmc_repro.py):
 #      FETCH_SIZE / WRITE_SIZE                                                          -> traffic.json swin_p2_128
 #   3. C4 FFT conv calls (tools/fft_traffic.py): FETCH_SIZE / WRITE_SIZE per call      -> traffic.json vit_hyena_p2_1024
-# Usage (GPU box): bash tools/profile_r5.sh <tag> [stages...]  (stages: metric c3 c4 c5 fft; default metric c3 fft)
+# Usage (GPU box): bash tools/profile_r5.sh <tag> [stages...]  (stages: metric c3 c4 c5 fft wl-<workload>; default
+# metric c3 fft)
 TAG=$1; shift
 STAGES=${*:-metric c3 fft}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -52,6 +53,18 @@ for st in $STAGES; do
       echo "$st trace done"
       pmc $OUT/$st/fetch FETCH_SIZE python3 $ROOT/bench.py --workload $WL --no-kernel-timer --steps 2 --warmup 1
       pmc $OUT/$st/write WRITE_SIZE python3 $ROOT/bench.py --workload $WL --no-kernel-timer --steps 2 --warmup 1
+      ;;
+    wl-*)   # any other workload (round 6): trace as it runs, FETCH / WRITE passes eager (LCI_GRAPH=0, as C3)
+      WL=${st#wl-}
+      mkdir -p $OUT/$WL
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$WL/trace -o run -- \
+        python3 $ROOT/bench.py --workload $WL --steps 3 --warmup 2 > $OUT/${WL}_trace.log 2>&1 \
+        || { echo "STOP $WL trace"; tail -5 $OUT/${WL}_trace.log; exit 1; }
+      echo "$WL trace done"
+      export LCI_GRAPH=0
+      pmc $OUT/$WL/fetch FETCH_SIZE python3 $ROOT/bench.py --workload $WL --no-kernel-timer --steps 2 --warmup 1
+      pmc $OUT/$WL/write WRITE_SIZE python3 $ROOT/bench.py --workload $WL --no-kernel-timer --steps 2 --warmup 1
+      unset LCI_GRAPH
       ;;
     fft)
       mkdir -p $OUT/fft
