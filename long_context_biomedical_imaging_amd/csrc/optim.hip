@@ -3,8 +3,9 @@
 // The trainer's optimizer step (trainer_base.py:171-177 -> torch.optim.Adam / AdamW, optim_base.py:87-89): torch's fused
 // kernel deals each launch's tensors out in 64-K-element chunks, one workgroup each, so a 62-M-parameter model
 // (SwinUNETR) runs ~1000 workgroups over 16 launches at ~1 TB/s (1.8 ms of the C3 step). Here every workgroup takes
-// 2048 elements, so the grid covers the chip and the update streams at the HBM rate (28 bytes per parameter: read
-// p, g, m, v, write p, m, v). The arithmetic follows torch's FusedAdamMathFunctor (ATen fused_adam_utils.cuh): the
+// ADAM_CHUNK elements, so the grid covers the chip and the update streams near the HBM rate (28 bytes per parameter:
+// read p, g, m, v, write p, m, v). Round 6: 4096 elements per workgroup as four 1-KB-per-wave groups, all 16 loads of a
+// thread issued before the arithmetic, and the bias corrections (f64 pow) evaluated once per workgroup. The arithmetic follows torch's FusedAdamMathFunctor (ATen fused_adam_utils.cuh): the
 // moment updates in f64 from f32 operands, bias corrections from the device step count (f64 pow, kept in f32),
 // step size and denominator rounded to f32, the final update in f32 -- so results match torch's fused Adam.
 #include "common.hpp"
@@ -12,7 +13,7 @@
 namespace lci {
 
 constexpr int ADAM_MAXT = 40;       // tensors per launch (kernel-argument space)
-constexpr int ADAM_CHUNK = 2048;    // elements per workgroup (256 threads x 8)
+constexpr int ADAM_CHUNK = 4096;    // elements per workgroup (256 threads x 4 groups of 4)
 
 struct AdamTensor {
   float* p;
@@ -50,34 +51,45 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
   while (k + 1 < a.nt && a.blk0[k + 1] <= b) ++k;   // this workgroup's tensor (uniform)
   const AdamTensor& t = a.t[k];
   const long long e0 = (long long)(b - a.blk0[k]) * ADAM_CHUNK;
-  const float stp = *t.step;
-  const float bc1 = (float)(1.0 - pow(a.beta1, (double)stp));
-  const float bc2s = (float)sqrt(1.0 - pow(a.beta2, (double)stp));
-  const float step_size = (float)(a.lr / (double)bc1);
-  const long long i0 = e0 + 8LL * threadIdx.x;
+  __shared__ float coef[2];
+  if (threadIdx.x == 0) {
+    const float stp = *t.step;
+    const float bc1 = (float)(1.0 - pow(a.beta1, (double)stp));
+    coef[0] = (float)(a.lr / (double)bc1);                          // step size
+    coef[1] = (float)sqrt(1.0 - pow(a.beta2, (double)stp));         // sqrt(bias correction 2)
+  }
+  __syncthreads();
+  const float step_size = coef[0], bc2s = coef[1];
   const bool vec = (((uintptr_t)t.p | (uintptr_t)t.g | (uintptr_t)t.m | (uintptr_t)t.v) & 15) == 0;
-  if (vec && i0 + 8 <= t.n) {
+  const long long i0 = e0 + 4LL * threadIdx.x;   // group h: elements i0 + 1024 h .. + 3
+  if (vec && e0 + ADAM_CHUNK <= t.n) {
+    f32x4 p[4], g[4], m[4], v[4];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const long long i = i0 + 4 * h;
-      f32x4 p = *(const f32x4*)(t.p + i), g = *(const f32x4*)(t.g + i);
-      f32x4 m = *(const f32x4*)(t.m + i), v = *(const f32x4*)(t.v + i);
+    for (int h = 0; h < 4; ++h) {
+      const long long i = i0 + 1024 * h;
+      p[h] = *(const f32x4*)(t.p + i); g[h] = *(const f32x4*)(t.g + i);
+      m[h] = *(const f32x4*)(t.m + i); v[h] = *(const f32x4*)(t.v + i);
+    }
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const long long i = i0 + 1024 * h;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        float pj = p[j], mj = m[j], vj = v[j];
-        adam_elem(pj, g[j], mj, vj, a, step_size, bc2s);
-        p[j] = pj; m[j] = mj; v[j] = vj;
+        float pj = p[h][j], mj = m[h][j], vj = v[h][j];
+        adam_elem(pj, g[h][j], mj, vj, a, step_size, bc2s);
+        p[h][j] = pj; m[h][j] = mj; v[h][j] = vj;
       }
-      *(f32x4*)(t.p + i) = p;
-      *(f32x4*)(t.m + i) = m;
-      *(f32x4*)(t.v + i) = v;
+      *(f32x4*)(t.p + i) = p[h];
+      *(f32x4*)(t.m + i) = m[h];
+      *(f32x4*)(t.v + i) = v[h];
     }
   } else {
-    for (long long i = i0; i < i0 + 8 && i < t.n; ++i) {
-      float p = t.p[i], m = t.m[i], v = t.v[i];
-      adam_elem(p, t.g[i], m, v, a, step_size, bc2s);
-      t.p[i] = p; t.m[i] = m; t.v[i] = v;
-    }
+    for (int h = 0; h < 4; ++h)
+      for (long long i = i0 + 1024 * h; i < i0 + 1024 * h + 4 && i < t.n; ++i) {
+        float p = t.p[i], m = t.m[i], v = t.v[i];
+        adam_elem(p, t.g[i], m, v, a, step_size, bc2s);
+        t.p[i] = p; t.m[i] = m; t.v[i] = v;
+      }
   }
 }
 
