@@ -116,6 +116,7 @@ def _ref_worker(name, q):
     try:
         q.put(_host(_run(name, 0, 1, torch.device("cuda", 0))))
         q.put(_host((_grads_per_rank_batch(name, torch.device("cuda", 0)),)))
+        q.put(_host((_grads_per_rank_batch(name, torch.device("cuda", 0)),)))   # run-to-run floor
     except BaseException:
         q.put("error: " + traceback.format_exc())
         os._exit(1)
@@ -182,21 +183,26 @@ def test_ddp_two_ranks_real_model(name):
     p.start()
     g_ref, w_ref = _get(rq, [p], "one-process reference")
     (g_avg,) = _get(rq, [p], "per-rank-batch reference")
+    (g_avg2,) = _get(rq, [p], "per-rank-batch reference, repeated")
     p.join(timeout=120)
     assert p.exitcode == 0
 
     def tt(d):
         return {n: torch.from_numpy(a) for n, a in d.items()}
-    g_ref, w_ref, g_avg = tt(g_ref), tt(w_ref), tt(g_avg)
+    g_ref, w_ref, g_avg, g_avg2 = tt(g_ref), tt(w_ref), tt(g_avg), tt(g_avg2)
     (g0, w0), (g1, w1) = ((tt(g), tt(w)) for g, w in (res[0], res[1]))
     assert g0.keys() == g1.keys() == g_ref.keys() == g_avg.keys()
     for n in g_ref:
         assert torch.equal(g0[n], g1[n]), f"all-reduced gradient differs between ranks: {n}"
-    # 1. the all-reduced gradient is the mean of the per-rank-batch gradients (f32 summation rounding, float-atomic
-    # parameter sums of the scan)
-    bad = [(n, (g0[n] - g_avg[n]).norm().item(), g_avg[n].norm().item()) for n in g_avg
-           if (g0[n] - g_avg[n]).norm() > 1e-4 * g_avg[n].norm() + 1e-9]
-    assert not bad, f"DDP all-reduce vs the mean of per-rank gradients: {bad[:6]}"
+    # 1. the all-reduced gradient is the mean of the per-rank-batch gradients, to f32 summation rounding plus the
+    # run-to-run spread of the same single-process computation: the Mamba scan backward sums its dB / dC through LDS
+    # float atomics (order not fixed), and under bf16 autocast a last-bit difference there can flip later bf16
+    # roundings, so two identical runs of the ViT-Mamba model differ by ~1e-3 in the upstream tensors (round 6: one
+    # full-suite run of this check failed at 1.5e-3 relative with a 1e-4 bound); the repeated reference measures it
+    bad = [(n, (g0[n] - g_avg[n]).norm().item(), (g_avg2[n] - g_avg[n]).norm().item(), g_avg[n].norm().item())
+           for n in g_avg
+           if (g0[n] - g_avg[n]).norm() > 1e-4 * g_avg[n].norm() + 4 * (g_avg2[n] - g_avg[n]).norm() + 1e-9]
+    assert not bad, f"DDP all-reduce vs the mean of per-rank gradients (name, |diff|, run-to-run, |g|): {bad[:6]}"
     # 2. against one process on the concatenated batch, on the whole gradient
     num = sum(((g0[n] - g_ref[n]) ** 2).sum().item() for n in g_ref)
     den = sum((g_ref[n] ** 2).sum().item() for n in g_ref)
